@@ -1,0 +1,143 @@
+"""Flagship benchmark: VGG-11(-BN) on CIFAR-10-shaped synthetic data, top-1 % + 8-bit QSGD
+gradient exchange over RCCL, one process per MI355X.
+
+    python bench.py --gpus 1 --steps 50 --warmup 10
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
+        --master-port 29500 bench.py --gpus 8 --steps 50 --warmup 10
+
+Metric (BASELINE.json): "grad bytes/step on wire + images/sec, VGG-11 CIFAR-10 at 1/2/4/8
+MI355X".  ``value`` = whole-job images/sec (sum over ranks: N x per-GPU batch x K / max-over-ranks
+time of the K timed steps).  Every timed step is a full training step: on-device batch gather +
+augmentation, bf16-autocast forward/backward (fp32 master weights), per-bucket top-k + QSGD encode
+(HIP) overlapped with backward, RCCL all-gather of the packed payloads, fused decode + average +
+SGD (HIP).  Weak scaling: the per-GPU batch is fixed as N grows.  The byte fields report the
+payload per rank, the algorithmic wire bytes, and the reference-equivalent MiB/step.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+# The reference publishes no images/sec; BASELINE.md derives ~104 img/s aggregate for VGG-11 on
+# its 2-worker Colab CPU setup from the end-to-end training-time chart.
+BASELINE_IMG_S = 104.0
+
+
+def parse(argv=None):
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=30)
+    p.add_argument("--warmup", type=int, default=8)
+    p.add_argument("--network", default="VGG11")
+    p.add_argument("--dataset", default="Cifar10")
+    p.add_argument("--batch-size", type=int, default=128, help="per-GPU batch")
+    p.add_argument("--compress", default="topk_qsgd")
+    p.add_argument("--topk-ratio", type=float, default=0.01)
+    p.add_argument("--qsgd-bits", type=int, default=8)
+    p.add_argument("--qsgd-levels", type=int, default=None)
+    p.add_argument("--bucket-mb", type=float, default=16.0)
+    p.add_argument("--amp", default="bf16")
+    p.add_argument("--channels-last", action="store_true")
+    p.add_argument("--no-overlap", action="store_true")
+    p.add_argument("--error-feedback", action="store_true")
+    p.add_argument("--extra", default="", help="extra distributed_nn.py flags")
+    return p.parse_args(argv)
+
+
+def main(argv=None):
+    a = parse(argv)
+    import torch
+    import torch.distributed as dist
+
+    import ewdml
+    from ewdml.runtime.trainer import Trainer
+    from ewdml.utils.metrics import byte_summary
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}; launch with torch.distributed.run")
+    levels = a.qsgd_levels or (127 if a.qsgd_bits == 8 else 7)
+    flags = ["--network", a.network, "--dataset", a.dataset, "--batch-size", str(a.batch_size),
+             "--compress", a.compress, "--topk-ratio", str(a.topk_ratio), "--qsgd-bits",
+             str(a.qsgd_bits), "--qsgd-levels", str(levels), "--momentum", "0.9", "--lr", "0.01",
+             "--bucket-mb", str(a.bucket_mb), "--amp", a.amp, "--synthetic-size", "16384",
+             "--eval-freq", "0", "--log-interval", "1000000", "--quiet",
+             "--max-steps", str(a.steps + a.warmup)]
+    if a.channels_last:
+        flags.append("--channels-last")
+    if a.no_overlap:
+        flags.append("--no-overlap")
+    if a.error_feedback:
+        flags.append("--error-feedback")
+    flags += a.extra.split()
+    cfg = ewdml.parse_args(flags, prog="bench.py")
+    tr = Trainer(cfg)
+    cuda = tr.cuda
+
+    def sync():
+        if cuda:
+            torch.cuda.synchronize()
+
+    for _ in range(a.warmup):
+        tr.train_step()
+    sync()
+    tr.comm.barrier()
+    sync()
+    t0 = time.perf_counter()
+    loss = None
+    for _ in range(a.steps):
+        loss, _ = tr.train_step()
+    sync()
+    t1 = time.perf_counter()
+    tr.comm.barrier()
+    sync()
+    elapsed = t1 - t0
+    elapsed_max = tr.comm.all_reduce_scalars([elapsed], op="max")[0]
+    final_loss = float(loss.detach()) if loss is not None else float("nan")
+    ms = elapsed_max * 1e3 / a.steps
+    img_s = world * a.batch_size * a.steps / elapsed_max
+    bytes_ = byte_summary(tr.exchange.last, world)
+    rec = {
+        "metric": "grad bytes/step on wire + images/sec, VGG-11 CIFAR-10 at 1/2/4/8 MI355X",
+        "value": round(img_s, 2),
+        "unit": "images/sec",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(ms, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": round(img_s / BASELINE_IMG_S, 2),
+        "baseline_note": "reference publishes no img/s; BASELINE.md derives ~104 img/s (VGG-11, "
+                         "2 Colab CPU workers)",
+        "dtype": a.amp if a.amp != "none" else "fp32",
+        "data": "synthetic (CIFAR-10 shape 3x32x32, 10 classes, random-init weights)",
+        "config": {"model": "vgg11_bn" if a.network.lower() in ("vgg11", "vgg11_bn") else
+                   a.network, "global_batch": world * a.batch_size, "per_gpu_batch": a.batch_size,
+                   "seq_len": None, "parallelism": f"dp{world}",
+                   "codec": tr.exchange.codec.describe() if hasattr(tr.exchange, "codec") else
+                   a.compress, "optimizer": "sgd(momentum=0.9)", "overlap": not a.no_overlap,
+                   "buckets": len(tr.flat.buckets)},
+        "grad_bytes_per_step_on_wire": bytes_["wire_bytes_total"],
+        "payload_bytes_per_rank": bytes_["payload_bytes_per_rank"],
+        "dense_fp32_grad_bytes": bytes_["dense_fp32_bytes"],
+        "compression_ratio": bytes_["compression_ratio"],
+        "ref_equiv_MiB_per_step": round(bytes_["ref_equiv_MiB_per_step"], 4),
+        "ref_equiv_reduction": bytes_["ref_equiv_reduction"],
+        "final_loss": final_loss,
+        "hip_ext": ewdml.ops.library_path() if cuda else None,
+    }
+    if tr.rank == 0:
+        print(json.dumps(rec), flush=True)
+    if dist.is_initialized():
+        dist.destroy_process_group()
+    return rec
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,261 @@
+"""Pure-torch reference implementations of every codec (the "oracle").
+
+These define the exact semantics the HIP kernels in ``ops/csrc`` implement; on CPU (Gloo tests,
+``BASELINE.json`` config #1) they are also the execution path.  The HIP kernels reproduce them
+bit-for-bit for the top-k selection, the codes and the decoded sums (the kernel file is compiled
+with ``-ffp-contract=off`` so no FMA changes a rounding); only L2 norms may differ in the last bit
+because the GPU sums squares in a different (but fixed) order.
+
+Reference semantics being reproduced:
+  * QSGD (``Compresssor/qsgd.py:12-40``): level = floor(s*|g|/norm) + Bernoulli(frac), code =
+    sign*level, decode = norm/s*code.  Differences, all deliberate:
+    codes are real int8/int4 (the reference ships fp32 "levels"), s <= 127 so the code fits int8
+    (the reference's s=128 overflows), a zero norm yields zeros instead of NaN, and the uniform
+    variates come from the counter RNG in ``rng.py``.
+  * Top-k (``Compresssor/TopK.py:5-35``): k = max(1, int(numel*ratio)) largest |g| per tensor.  Ties
+    at the threshold are broken by lowest index (torch.topk leaves them unspecified), entries are
+    stored sorted by index.
+"""
+import numpy as np
+import torch
+
+from . import rng
+from .plan import CHUNK, BucketPlan, Layout
+
+
+def _section(buf: torch.Tensor, start: int, count: int, dtype: torch.dtype) -> torch.Tensor:
+    nbytes = count * torch.empty((), dtype=dtype).element_size()
+    return buf[start:start + nbytes].view(dtype)
+
+
+def topk_indices(x: torch.Tensor, k: int) -> torch.Tensor:
+    """Sorted int64 indices of the k largest |x| (ties -> lowest index)."""
+    n = x.numel()
+    if k >= n:
+        return torch.arange(n, dtype=torch.int64, device=x.device)
+    key = x.abs().contiguous().view(torch.int32)
+    kth = torch.topk(key, k, sorted=False).values.min()
+    gt = key > kth
+    need = k - int(gt.sum())
+    sel = gt.clone()
+    if need > 0:
+        sel[(key == kth).nonzero().flatten()[:need]] = True
+    return sel.nonzero().flatten()
+
+
+def inv_scale(levels: int, scale: float) -> float:
+    """fp32 ``levels / scale`` (0 for a zero scale), rounded exactly like the kernels' IEEE divide."""
+    scale = np.float32(scale)
+    if not scale > 0:
+        return 0.0
+    return float(np.float32(levels) / scale)
+
+
+def dequant_step(levels: int, scale: float) -> float:
+    """fp32 ``scale * fp32(1/levels)``: the value of one code unit."""
+    return float(np.float32(scale) * np.float32(1.0 / levels))
+
+
+def quantize(vals: torch.Tensor, scale: float, levels: int, gidx: torch.Tensor,
+             key: int) -> torch.Tensor:
+    """Stochastic QSGD rounding of ``vals`` against ``scale`` -> int32 codes in [-levels, levels]."""
+    lvl = vals.abs() * inv_scale(levels, scale)
+    fl = torch.floor(lvl)
+    u = rng.uniform(gidx, key)
+    q = fl + (u < (lvl - fl)).to(torch.float32)
+    q = torch.clamp(q, max=float(levels))
+    q = torch.where(vals < 0, -q, q)
+    return q.to(torch.int32)
+
+
+def _pack4(codes: torch.Tensor) -> torch.Tensor:
+    c = (codes & 0xF).to(torch.uint8)
+    if c.numel() % 2:
+        c = torch.cat([c, c.new_zeros(1)])
+    return c[0::2] | (c[1::2] << 4)
+
+
+def _unpack4(b: torch.Tensor, n: int) -> torch.Tensor:
+    lo = (b & 0xF).to(torch.int32)
+    hi = (b >> 4).to(torch.int32)
+    c = torch.stack([lo, hi], 1).flatten()[:n]
+    return torch.where(c >= 8, c - 16, c)
+
+
+def _scale_of(vals: torch.Tensor, norm: str) -> float:
+    if vals.numel() == 0:
+        return 0.0
+    if norm == "max":
+        return float(vals.abs().max())
+    if norm == "l2":
+        return float(np.float32(vals.to(torch.float64).norm()))
+    raise ValueError(f"unknown QSGD norm {norm!r}")
+
+
+# ---------------------------------------------------------------------------------------------
+# encode
+# ---------------------------------------------------------------------------------------------
+def encode_topk(g: torch.Tensor, plan: BucketPlan, layout: Layout, levels: int, norm: str,
+                key: int, residual: torch.Tensor = None) -> torch.Tensor:
+    """Top-k (+QSGD when ``layout.kind == 'topk_qsgd'``) of one bucket -> uint8 payload.
+
+    ``g`` is the bucket's flat fp32 gradient (length ``plan.length``).  With ``residual`` (error
+    feedback) the compressed vector is ``g + residual`` and ``residual`` is overwritten with what was
+    not transmitted.
+    """
+    if residual is not None:
+        g = g + residual
+    out = torch.zeros(layout.nbytes, dtype=torch.uint8, device=g.device)
+    T, C, K = plan.num_tensors, plan.num_chunks, plan.total_k
+    scales = _section(out, layout.scales, T, torch.float32)
+    counts = _section(out, layout.counts, C, torch.int16)
+    idx = _section(out, layout.idx, K, torch.int16)
+    codes_all = []
+    sent = torch.zeros_like(g) if residual is not None else None
+    for t in range(T):
+        off, n, k = plan.offsets[t], plan.numels[t], plan.ks[t]
+        x = g[off:off + n]
+        sel = topk_indices(x, k)
+        vals = x[sel]
+        c0, nch, e0 = plan.tensor_chunk0[t], plan.tensor_nchunks[t], plan.tensor_entry0[t]
+        counts[c0:c0 + nch] = torch.bincount(sel // CHUNK, minlength=nch).to(torch.int16)
+        idx[e0:e0 + k] = (sel % CHUNK).to(torch.int16)
+        scale = _scale_of(vals, norm)
+        scales[t] = scale  # plain top-k keeps the scale in the header too (uniform layout)
+        if layout.kind == "topk":
+            codes_all.append(vals.to(torch.float32))
+            if sent is not None:
+                sent[off + sel] = vals
+            continue
+        q = quantize(vals, scale, levels, plan.bucket_offset + off + sel, key)
+        codes_all.append(q)
+        if sent is not None:
+            sent[off + sel] = q.to(torch.float32) * dequant_step(levels, scale)
+    codes = torch.cat(codes_all)
+    if layout.kind == "topk":
+        _section(out, layout.codes, K, torch.float32).copy_(codes)
+    elif layout.bits == 8:
+        _section(out, layout.codes, K, torch.int8).copy_(codes.to(torch.int8))
+    else:
+        p = _pack4(codes)
+        out[layout.codes:layout.codes + p.numel()] = p
+    if residual is not None:
+        residual.copy_(g - sent)
+    return out
+
+
+def encode_qsgd(g: torch.Tensor, plan: BucketPlan, layout: Layout, levels: int, norm: str,
+                key: int, residual: torch.Tensor = None) -> torch.Tensor:
+    """Dense QSGD of every element of the bucket -> uint8 payload (reference Method 4)."""
+    if residual is not None:
+        g = g + residual
+    out = torch.zeros(layout.nbytes, dtype=torch.uint8, device=g.device)
+    T = plan.num_tensors
+    scales = _section(out, layout.scales, T, torch.float32)
+    codes = torch.zeros(plan.total_codes, dtype=torch.int32, device=g.device)
+    sent = torch.zeros_like(g) if residual is not None else None
+    for t in range(T):
+        off, n, d0 = plan.offsets[t], plan.numels[t], plan.tensor_code0[t]
+        x = g[off:off + n]
+        scale = _scale_of(x, norm)
+        scales[t] = scale
+        gidx = plan.bucket_offset + off + torch.arange(n, device=g.device)
+        q = quantize(x, scale, levels, gidx, key)
+        codes[d0:d0 + n] = q
+        if sent is not None:
+            sent[off:off + n] = q.to(torch.float32) * dequant_step(levels, scale)
+    if layout.bits == 8:
+        _section(out, layout.codes, plan.total_codes, torch.int8).copy_(codes.to(torch.int8))
+    else:
+        p = _pack4(codes)
+        out[layout.codes:layout.codes + p.numel()] = p
+    if residual is not None:
+        residual.copy_(g - sent)
+    return out
+
+
+# ---------------------------------------------------------------------------------------------
+# decode: sum over ranks (in rank order) of the dequantised payloads, times ``scale``
+# ---------------------------------------------------------------------------------------------
+def _decoded_entries(pay: torch.Tensor, plan: BucketPlan, layout: Layout, levels: int):
+    T, C, K = plan.num_tensors, plan.num_chunks, plan.total_k
+    scales = _section(pay, layout.scales, T, torch.float32)
+    counts = _section(pay, layout.counts, C, torch.int16).to(torch.int64)
+    idx = _section(pay, layout.idx, K, torch.int16).to(torch.int64) & 0xFFFF
+    if layout.kind == "topk":
+        vals = _section(pay, layout.codes, K, torch.float32)
+    elif layout.bits == 8:
+        vals = _section(pay, layout.codes, K, torch.int8).to(torch.float32)
+    else:
+        vals = _unpack4(pay[layout.codes:layout.codes + (K + 1) // 2], K).to(torch.float32)
+    # chunk id of every entry (entries of a tensor are ordered by chunk)
+    chunk_of_entry = torch.repeat_interleave(torch.arange(C, device=pay.device), counts)
+    start = torch.tensor(plan.chunk_start, dtype=torch.int64, device=pay.device)
+    pos = start[chunk_of_entry] + idx
+    if layout.kind != "topk":
+        tensor_of_entry = torch.repeat_interleave(
+            torch.arange(T, device=pay.device),
+            torch.tensor(plan.ks, dtype=torch.int64, device=pay.device))
+        step = scales * float(np.float32(1.0 / levels))
+        vals = vals * step[tensor_of_entry]
+    return pos, vals
+
+
+def decode_sum(recv: torch.Tensor, plan: BucketPlan, layout: Layout, levels: int,
+               scale: float) -> torch.Tensor:
+    """``recv``: uint8 [N, nbytes].  Returns fp32 [plan.length] = scale * sum_r decode(r)."""
+    acc = torch.zeros(plan.length, dtype=torch.float32, device=recv.device)
+    for r in range(recv.shape[0]):
+        if layout.kind in ("topk", "topk_qsgd"):
+            pos, vals = _decoded_entries(recv[r], plan, layout, levels)
+            acc.index_add_(0, pos, vals)
+        else:
+            acc += _dense_decoded(recv[r], plan, layout, levels)
+    return acc * torch.tensor(scale, dtype=torch.float32)
+
+
+def _dense_decoded(pay, plan, layout, levels):
+    T = plan.num_tensors
+    scales = _section(pay, layout.scales, T, torch.float32)
+    if layout.bits == 8:
+        codes = _section(pay, layout.codes, plan.total_codes, torch.int8).to(torch.float32)
+    else:
+        codes = _unpack4(pay[layout.codes:layout.codes + plan.total_codes // 2],
+                         plan.total_codes).to(torch.float32)
+    out = torch.zeros(plan.length, dtype=torch.float32, device=pay.device)
+    for t in range(T):
+        off, n, d0 = plan.offsets[t], plan.numels[t], plan.tensor_code0[t]
+        out[off:off + n] = codes[d0:d0 + n] * dequant_step(levels, float(scales[t]))
+    return out
+
+
+# ---------------------------------------------------------------------------------------------
+# optimizers with explicit gradients (reference ``optim/sgd.py:59-91``, ``optim/adam.py:38-94``)
+# ---------------------------------------------------------------------------------------------
+def sgd_apply(p, buf, g, lr, momentum, dampening, weight_decay, nesterov, first):
+    d_p = g
+    if weight_decay != 0:
+        d_p = d_p + weight_decay * p
+    if momentum != 0:
+        if first:
+            buf.copy_(d_p)
+        else:
+            buf.mul_(momentum).add_(d_p, alpha=1 - dampening)
+        d_p = d_p + momentum * buf if nesterov else buf
+    p.add_(d_p, alpha=-lr)
+
+
+def adam_apply(p, m, v, vmax, g, lr, beta1, beta2, eps, weight_decay, step, amsgrad):
+    import math
+    if weight_decay != 0:
+        g = g + weight_decay * p
+    m.mul_(beta1).add_(g, alpha=1 - beta1)
+    v.mul_(beta2).addcmul_(g, g, value=1 - beta2)
+    if amsgrad:
+        torch.maximum(vmax, v, out=vmax)
+        denom = vmax.sqrt().add_(eps)
+    else:
+        denom = v.sqrt().add_(eps)
+    bc1 = 1 - beta1 ** step
+    bc2 = 1 - beta2 ** step
+    p.addcdiv_(m, denom, value=-lr * math.sqrt(bc2) / bc1)

@@ -1,0 +1,132 @@
+"""Static description of a gradient bucket and of the packed payloads exchanged for it.
+
+A *bucket* is a contiguous range of the flat gradient buffer holding whole parameter tensors
+(see ``parallel/flat.py``).  Each tensor is cut into *chunks* of ``CHUNK`` = 8192 elements; a chunk
+is the unit of work of every encode/decode kernel and the base of the 16-bit sparse indices.
+
+Top-k semantics follow the reference exactly: per tensor, ``k = max(1, int(numel * ratio))``
+(``Compresssor/TopK.py:7``).  Selected entries are emitted sorted by index, so an entry is stored as
+a chunk-local ``uint16`` offset plus its code, and one ``uint16`` count per chunk says how many
+entries each chunk owns.  That is what gets VGG-11 at top-1 % + 8-bit QSGD to ~132x fewer bytes than
+dense fp32 instead of the 80x that int32 indices would give.
+
+Payload layouts (every section starts 16-byte aligned; all ranks send identical sizes, so the
+exchange is a fixed-size all-gather with no size handshake):
+
+``topk_qsgd``: scales f32[T] | counts u16[C] | idx u16[K] | codes i8[K] (bits=8) or nibbles[K/2]
+``topk``     : scales f32[T] (unused, kept for a uniform header) | counts | idx | values f32[K]
+``qsgd``     : scales f32[T] | codes i8[D'] or nibbles  (dense; D' = numels padded to 16 per tensor)
+"""
+from dataclasses import dataclass, field
+from typing import List
+
+import torch
+
+CHUNK = 8192
+
+
+def _align(n: int, a: int = 16) -> int:
+    return (n + a - 1) // a * a
+
+
+@dataclass
+class BucketPlan:
+    """Tensors of one bucket.  ``offsets`` are element offsets relative to the bucket start."""
+
+    numels: List[int]
+    offsets: List[int]
+    ratio: float = 1.0
+    bucket_offset: int = 0  # element offset of the bucket inside the flat buffer
+    length: int = 0  # bucket length in elements (>= last offset + numel; includes align pad)
+    ks: List[int] = field(default_factory=list)
+    chunk_tensor: List[int] = field(default_factory=list)
+    chunk_start: List[int] = field(default_factory=list)  # relative to bucket start
+    chunk_len: List[int] = field(default_factory=list)
+    tensor_chunk0: List[int] = field(default_factory=list)
+    tensor_nchunks: List[int] = field(default_factory=list)
+    tensor_entry0: List[int] = field(default_factory=list)
+    tensor_code0: List[int] = field(default_factory=list)  # dense code offset (16-aligned)
+
+    def __post_init__(self):
+        assert len(self.numels) == len(self.offsets) and self.numels
+        if not self.length:
+            self.length = self.offsets[-1] + self.numels[-1]
+        self.ks = [max(1, int(n * self.ratio)) for n in self.numels]
+        e = c = 0
+        for t, (n, off) in enumerate(zip(self.numels, self.offsets)):
+            nch = (n + CHUNK - 1) // CHUNK
+            self.tensor_chunk0.append(len(self.chunk_tensor))
+            self.tensor_nchunks.append(nch)
+            for j in range(nch):
+                self.chunk_tensor.append(t)
+                self.chunk_start.append(off + j * CHUNK)
+                self.chunk_len.append(min(CHUNK, n - j * CHUNK))
+            self.tensor_entry0.append(e)
+            e += self.ks[t]
+            self.tensor_code0.append(c)
+            c += _align(n, 16)
+        self.total_k = e
+        self.total_codes = c
+
+    @property
+    def num_tensors(self) -> int:
+        return len(self.numels)
+
+    @property
+    def num_chunks(self) -> int:
+        return len(self.chunk_tensor)
+
+    @property
+    def numel(self) -> int:
+        return sum(self.numels)
+
+    # ---- device tables consumed by the kernels -------------------------------------------
+    def tensor_table(self, device) -> torch.Tensor:
+        """int32 [T, 8]: offset, numel, k, chunk0, nchunks, entry0, code0, 0."""
+        rows = [[o, n, k, c0, nc, e0, d0, 0] for o, n, k, c0, nc, e0, d0 in zip(
+            self.offsets, self.numels, self.ks, self.tensor_chunk0, self.tensor_nchunks,
+            self.tensor_entry0, self.tensor_code0)]
+        return torch.tensor(rows, dtype=torch.int32, device=device)
+
+    def chunk_table(self, device) -> torch.Tensor:
+        """int32 [C, 4]: tensor, start (rel. bucket), len, local chunk index."""
+        rows = []
+        for c, (t, s, ln) in enumerate(zip(self.chunk_tensor, self.chunk_start, self.chunk_len)):
+            rows.append([t, s, ln, c - self.tensor_chunk0[t]])
+        return torch.tensor(rows, dtype=torch.int32, device=device)
+
+
+@dataclass(frozen=True)
+class Layout:
+    """Byte offsets of the payload sections for one bucket and one codec."""
+
+    kind: str
+    bits: int
+    scales: int
+    counts: int
+    idx: int
+    codes: int
+    nbytes: int
+
+    @staticmethod
+    def build(kind: str, plan: BucketPlan, bits: int = 8) -> "Layout":
+        T, C, K = plan.num_tensors, plan.num_chunks, plan.total_k
+        scales = 0
+        off = _align(4 * T)
+        if kind in ("topk_qsgd", "topk"):
+            counts = off
+            off = _align(off + 2 * C)
+            idx = off
+            off = _align(off + 2 * K)
+            codes = off
+            if kind == "topk":
+                off += 4 * K
+            else:
+                off += K if bits == 8 else (K + 1) // 2
+        elif kind == "qsgd":
+            counts = idx = off
+            codes = off
+            off += plan.total_codes if bits == 8 else plan.total_codes // 2
+        else:
+            raise ValueError(kind)
+        return Layout(kind, bits, scales, counts, idx, codes, _align(off))

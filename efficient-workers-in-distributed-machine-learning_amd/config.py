@@ -1,0 +1,203 @@
+"""Run configuration and the ``distributed_nn.py`` command line.
+
+Every flag of the reference CLI (``src/distributed_nn.py:24-72``) is accepted with the same name
+and default; the ones the reference parses but never uses keep their meaning documented below.
+New flags select the exchange method, codec, topology and the MI355X execution options.
+
+Method presets (``--method``; ``Report.zip:main.tex:80-119``):
+  1  vanilla PS: push dense grads to rank 0, server steps, pull dense *weights*
+  2  QSGD push, dense weight pull
+  3  push + pull dense gradients (the reference's live HEAD path) -> dense all-reduce
+  4  QSGD both ways
+  5  top-k -> QSGD both ways (ratio --topk-ratio; the report used 0.4)
+  6  method 5 + communicate every --sync-every (default 20) steps + best-worker selection
+Methods 1 and 2 imply ``--topology ps``; 3-6 default to the all-to-all topology (every GPU is a
+worker, no idle server); ``--topology ps`` reproduces the reference's star for any method.
+"""
+import argparse
+import dataclasses
+from dataclasses import dataclass, field
+from typing import Optional
+
+
+def _str2bool(v) -> bool:
+    if isinstance(v, bool):
+        return v
+    # reference `--enable-gpu` is `type=bool`: any non-empty string is True (distributed_nn.py:68)
+    return str(v).strip().lower() not in ("", "0", "false", "no", "off", "none")
+
+
+@dataclass
+class Config:
+    # ---- reference flags (distributed_nn.py:24-72) -----------------------------------------
+    batch_size: int = 128
+    test_batch_size: int = 500
+    epochs: int = 100
+    max_steps: int = 10000
+    lr: float = 0.01
+    momentum: float = 0.5
+    no_cuda: bool = False
+    seed: int = 1
+    log_interval: int = 10
+    network: str = "LeNet"
+    mode: str = "normal"  # straggler mode; 'kill' enables the --kill-threshold step timeout
+    kill_threshold: float = 7.0  # seconds; comm watchdog timeout in 'kill' mode
+    dataset: str = "MNIST"
+    comm_type: str = "Bcast"  # accepted; the all-to-all exchange needs no choice here
+    num_aggregate: int = 5  # PS k-of-n aggregation (used with --topology ps --mode kill)
+    eval_freq: int = 50  # checkpoint (and evaluation) cadence in steps
+    train_dir: str = "output/models/"
+    compress_grad: str = "compress"  # 'none' forces --compress none (reference switch)
+    gather_type: str = "gather"  # accepted for compatibility
+    enable_gpu: bool = False
+    local_rank: Optional[int] = None
+    # ---- exchange / compression ---------------------------------------------------------------
+    method: Optional[int] = None
+    compress: str = "topk_qsgd"  # none | fp16 | bf16 | qsgd | topk | topk_qsgd
+    topk_ratio: float = 0.01
+    qsgd_levels: int = 127
+    qsgd_bits: int = 8
+    qsgd_norm: str = "max"  # max | l2 (the reference's L2 norm)
+    topology: str = "allgather"  # allgather (all-to-all) | ps (rank-0 parameter server)
+    pull: str = "grad"  # ps topology: pull averaged 'grad' or server 'weights'
+    pull_compress: Optional[str] = None  # ps topology: codec of the pull (default = push codec)
+    sync_every: int = 1  # local SGD: exchange every H steps (method 6)
+    sync_mode: str = "grad"  # grad: compressed gradient on sync steps | model: compressed delta
+    select_best: bool = False  # method 6: adopt the weights of the best-accuracy rank at sync
+    error_feedback: bool = False
+    bucket_mb: float = 16.0
+    overlap: bool = True
+    predivide: float = 1.0  # Horovod gradient_predivide_factor
+    sync_bn: bool = False  # broadcast BN running stats from rank 0 at every checkpoint/eval
+    # ---- optimizer -------------------------------------------------------------------------------
+    optimizer: str = "sgd"
+    weight_decay: float = 0.0
+    dampening: float = 0.0
+    nesterov: bool = False
+    lr_scale_world: bool = False  # Horovod: lr *= world size
+    # ---- execution -------------------------------------------------------------------------------
+    device: str = "auto"  # auto | cuda | cpu
+    amp: str = "bf16"  # bf16 | fp16 | none  (autocast compute dtype; master weights fp32)
+    channels_last: bool = False
+    hip_graph: bool = False
+    data_dir: Optional[str] = None  # None -> synthetic data of the dataset's shape
+    synthetic_size: int = 0
+    augment: bool = True
+    # ---- checkpoint / metrics / faults -----------------------------------------------------------
+    ckpt_dir: Optional[str] = None  # defaults to train_dir
+    resume: bool = False
+    legacy_ckpt: bool = True  # also write <train_dir>/model_step_ (the evaluator's file)
+    eval_on_ckpt: bool = False
+    metrics_file: Optional[str] = None  # per-step JSONL
+    profile: int = 0  # wrap N steps in torch.profiler
+    inject_fault: Optional[str] = None  # "rank:step" -> that rank raises at that step (tests)
+    comm_timeout: float = 600.0
+    quiet: bool = False
+
+    def resolved(self) -> "Config":
+        c = dataclasses.replace(self)
+        if c.method is not None:
+            m = int(c.method)
+            if m not in range(1, 7):
+                raise ValueError("--method must be in 1..6")
+            if m == 1:
+                c.topology, c.pull, c.compress = "ps", "weights", "none"
+            elif m == 2:
+                c.topology, c.pull, c.compress = "ps", "weights", "qsgd"
+            elif m == 3:
+                c.compress = "none"
+            elif m == 4:
+                c.compress = "qsgd"
+            elif m in (5, 6):
+                c.compress = "topk_qsgd"
+            if m == 6:
+                if c.sync_every == 1:
+                    c.sync_every = 20
+                c.select_best = True
+        if c.compress_grad.lower() == "none":
+            c.compress = "none"
+        if c.topology not in ("allgather", "ps"):
+            raise ValueError("--topology must be allgather or ps")
+        if c.ckpt_dir is None:
+            c.ckpt_dir = c.train_dir
+        return c
+
+
+def build_parser(prog="distributed_nn.py") -> argparse.ArgumentParser:
+    d = Config()
+    p = argparse.ArgumentParser(prog=prog, description="MI355X gradient-compressed data-parallel "
+                                "training (parameter-server / all-reduce / top-k + QSGD)")
+    a = p.add_argument
+    # reference flags
+    a("--batch-size", type=int, default=d.batch_size)
+    a("--test-batch-size", type=int, default=d.test_batch_size)
+    a("--epochs", type=int, default=d.epochs)
+    a("--max-steps", type=int, default=d.max_steps)
+    a("--lr", type=float, default=d.lr)
+    a("--momentum", type=float, default=d.momentum)
+    a("--no-cuda", action="store_true", default=False)
+    a("--seed", type=int, default=d.seed)
+    a("--log-interval", type=int, default=d.log_interval)
+    a("--network", type=str, default=d.network)
+    a("--mode", type=str, default=d.mode)
+    a("--kill-threshold", type=float, default=d.kill_threshold)
+    a("--dataset", type=str, default=d.dataset)
+    a("--comm-type", type=str, default=d.comm_type)
+    a("--num-aggregate", type=int, default=d.num_aggregate)
+    a("--eval-freq", type=int, default=d.eval_freq)
+    a("--train-dir", type=str, default=d.train_dir)
+    a("--compress-grad", type=str, default=d.compress_grad)
+    a("--gather-type", type=str, default=d.gather_type)
+    a("--enable-gpu", type=_str2bool, default=d.enable_gpu)
+    a("--local_rank", "--local-rank", dest="local_rank", type=int, default=None)
+    # exchange
+    a("--method", type=int, default=None, choices=range(1, 7))
+    a("--compress", type=str, default=d.compress,
+      choices=["none", "fp16", "bf16", "qsgd", "topk", "topk_qsgd"])
+    a("--topk-ratio", type=float, default=d.topk_ratio)
+    a("--qsgd-levels", type=int, default=d.qsgd_levels)
+    a("--qsgd-bits", type=int, default=d.qsgd_bits, choices=[4, 8])
+    a("--qsgd-norm", type=str, default=d.qsgd_norm, choices=["max", "l2"])
+    a("--topology", type=str, default=d.topology, choices=["allgather", "ps"])
+    a("--pull", type=str, default=d.pull, choices=["grad", "weights"])
+    a("--pull-compress", type=str, default=None,
+      choices=["none", "fp16", "bf16", "qsgd", "topk", "topk_qsgd"])
+    a("--sync-every", type=int, default=d.sync_every)
+    a("--sync-mode", type=str, default=d.sync_mode, choices=["grad", "model"])
+    a("--select-best", action="store_true", default=False)
+    a("--error-feedback", action="store_true", default=False)
+    a("--bucket-mb", type=float, default=d.bucket_mb)
+    a("--no-overlap", dest="overlap", action="store_false", default=True)
+    a("--predivide", type=float, default=d.predivide)
+    a("--sync-bn", action="store_true", default=False)
+    # optimizer
+    a("--optimizer", type=str, default=d.optimizer, choices=["sgd", "adam", "amsgrad"])
+    a("--weight-decay", type=float, default=d.weight_decay)
+    a("--dampening", type=float, default=d.dampening)
+    a("--nesterov", action="store_true", default=False)
+    a("--lr-scale-world", action="store_true", default=False)
+    # execution
+    a("--device", type=str, default=d.device, choices=["auto", "cuda", "cpu"])
+    a("--amp", type=str, default=d.amp, choices=["bf16", "fp16", "none"])
+    a("--channels-last", action="store_true", default=False)
+    a("--hip-graph", action="store_true", default=False)
+    a("--data-dir", type=str, default=None)
+    a("--synthetic-size", type=int, default=0)
+    a("--no-augment", dest="augment", action="store_false", default=True)
+    # checkpoint / metrics / faults
+    a("--ckpt-dir", type=str, default=None)
+    a("--resume", action="store_true", default=False)
+    a("--no-legacy-ckpt", dest="legacy_ckpt", action="store_false", default=True)
+    a("--eval-on-ckpt", action="store_true", default=False)
+    a("--metrics-file", type=str, default=None)
+    a("--profile", type=int, default=0)
+    a("--inject-fault", type=str, default=None)
+    a("--comm-timeout", type=float, default=d.comm_timeout)
+    a("--quiet", action="store_true", default=False)
+    return p
+
+
+def parse_args(argv=None, prog="distributed_nn.py") -> Config:
+    ns = build_parser(prog).parse_args(argv)
+    fields = {f.name for f in dataclasses.fields(Config)}
+    return Config(**{k: v for k, v in vars(ns).items() if k in fields}).resolved()

@@ -1,0 +1,52 @@
+"""LeNet for 1x28x28 inputs.
+
+Parity: ``PyTorch-parameter-server/src/model_ops/lenet.py:15-36`` (conv 1->20 k5, pool, relu,
+conv 20->50 k5, pool, relu, fc 800->500, fc 500->10 -- note the reference has *no* nonlinearity
+between the two fully connected layers).  431,080 parameters in 8 tensors.
+
+``fc_relu=True`` inserts the missing ReLU (off by default so the parameter/compute graph matches
+the reference exactly).
+"""
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+class LeNet(nn.Module):
+    def __init__(self, num_classes: int = 10, fc_relu: bool = False):
+        super().__init__()
+        self.conv1 = nn.Conv2d(1, 20, 5, 1)
+        self.conv2 = nn.Conv2d(20, 50, 5, 1)
+        self.fc1 = nn.Linear(4 * 4 * 50, 500)
+        self.fc2 = nn.Linear(500, num_classes)
+        self.fc_relu = fc_relu
+
+    def forward(self, x):
+        x = F.relu(F.max_pool2d(self.conv1(x), 2, 2))
+        x = F.relu(F.max_pool2d(self.conv2(x), 2, 2))
+        x = self.fc1(x.flatten(1))
+        if self.fc_relu:
+            x = F.relu(x)
+        return self.fc2(x)
+
+    def name(self):
+        return "lenet"
+
+
+class MnistNet(nn.Module):
+    """The Horovod example network (``horvod_pytorch.py:43-59``): conv10-conv20-dropout2d-fc50-fc10
+    with log-softmax output."""
+
+    def __init__(self, num_classes: int = 10):
+        super().__init__()
+        self.conv1 = nn.Conv2d(1, 10, kernel_size=5)
+        self.conv2 = nn.Conv2d(10, 20, kernel_size=5)
+        self.conv2_drop = nn.Dropout2d()
+        self.fc1 = nn.Linear(320, 50)
+        self.fc2 = nn.Linear(50, num_classes)
+
+    def forward(self, x):
+        x = F.relu(F.max_pool2d(self.conv1(x), 2))
+        x = F.relu(F.max_pool2d(self.conv2_drop(self.conv2(x)), 2))
+        x = F.relu(self.fc1(x.flatten(1)))
+        x = F.dropout(x, training=self.training)
+        return F.log_softmax(self.fc2(x), dim=1)

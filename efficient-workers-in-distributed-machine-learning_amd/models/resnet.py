@@ -1,0 +1,116 @@
+"""ResNets: the CIFAR variants of the reference plus an ImageNet-stem variant.
+
+Parity: ``PyTorch-parameter-server/src/model_ops/resnet.py`` -- BasicBlock / Bottleneck with
+projection shortcuts, 3x3 stride-1 stem, 4 stages (64/128/256/512 planes).  ResNet-18 has
+11,173,962 parameters (62 tensors); ResNet-50 with 10 classes has 23,520,842 (161 tensors).
+
+Fixed reference defects:
+  * every factory takes ``num_classes`` (the reference's ResNet34/50 do not);
+  * the CIFAR head uses adaptive average pooling, so it still equals ``avg_pool2d(4)`` on 32x32
+    inputs but no longer crashes on other resolutions;
+  * ``stem="imagenet"`` gives the standard 7x7/2 conv + 3x3/2 max-pool stem used for the
+    224x224 ResNet-50 config (BASELINE.json config #5).
+"""
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+class BasicBlock(nn.Module):
+    expansion = 1
+
+    def __init__(self, in_planes, planes, stride=1):
+        super().__init__()
+        self.conv1 = nn.Conv2d(in_planes, planes, 3, stride, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(planes)
+        self.conv2 = nn.Conv2d(planes, planes, 3, 1, 1, bias=False)
+        self.bn2 = nn.BatchNorm2d(planes)
+        self.shortcut = nn.Sequential()
+        if stride != 1 or in_planes != planes * self.expansion:
+            self.shortcut = nn.Sequential(
+                nn.Conv2d(in_planes, planes * self.expansion, 1, stride, bias=False),
+                nn.BatchNorm2d(planes * self.expansion),
+            )
+
+    def forward(self, x):
+        out = F.relu(self.bn1(self.conv1(x)))
+        out = self.bn2(self.conv2(out))
+        return F.relu(out + self.shortcut(x))
+
+
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, in_planes, planes, stride=1):
+        super().__init__()
+        self.conv1 = nn.Conv2d(in_planes, planes, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(planes)
+        self.conv2 = nn.Conv2d(planes, planes, 3, stride, 1, bias=False)
+        self.bn2 = nn.BatchNorm2d(planes)
+        self.conv3 = nn.Conv2d(planes, planes * self.expansion, 1, bias=False)
+        self.bn3 = nn.BatchNorm2d(planes * self.expansion)
+        self.shortcut = nn.Sequential()
+        if stride != 1 or in_planes != planes * self.expansion:
+            self.shortcut = nn.Sequential(
+                nn.Conv2d(in_planes, planes * self.expansion, 1, stride, bias=False),
+                nn.BatchNorm2d(planes * self.expansion),
+            )
+
+    def forward(self, x):
+        out = F.relu(self.bn1(self.conv1(x)))
+        out = F.relu(self.bn2(self.conv2(out)))
+        out = self.bn3(self.conv3(out))
+        return F.relu(out + self.shortcut(x))
+
+
+class ResNet(nn.Module):
+    def __init__(self, block, num_blocks, num_classes=10, stem="cifar", in_channels=3):
+        super().__init__()
+        self.in_planes = 64
+        self.stem = stem
+        if stem == "cifar":
+            self.conv1 = nn.Conv2d(in_channels, 64, 3, 1, 1, bias=False)
+        elif stem == "imagenet":
+            self.conv1 = nn.Conv2d(in_channels, 64, 7, 2, 3, bias=False)
+        else:
+            raise ValueError(f"unknown stem {stem!r}")
+        self.bn1 = nn.BatchNorm2d(64)
+        self.layer1 = self._make_layer(block, 64, num_blocks[0], 1)
+        self.layer2 = self._make_layer(block, 128, num_blocks[1], 2)
+        self.layer3 = self._make_layer(block, 256, num_blocks[2], 2)
+        self.layer4 = self._make_layer(block, 512, num_blocks[3], 2)
+        self.linear = nn.Linear(512 * block.expansion, num_classes)
+
+    def _make_layer(self, block, planes, n, stride):
+        layers = []
+        for s in [stride] + [1] * (n - 1):
+            layers.append(block(self.in_planes, planes, s))
+            self.in_planes = planes * block.expansion
+        return nn.Sequential(*layers)
+
+    def forward(self, x):
+        out = F.relu(self.bn1(self.conv1(x)))
+        if self.stem == "imagenet":
+            out = F.max_pool2d(out, 3, 2, 1)
+        out = self.layer4(self.layer3(self.layer2(self.layer1(out))))
+        out = F.adaptive_avg_pool2d(out, 1).flatten(1)
+        return self.linear(out)
+
+
+def ResNet18(num_classes=10, stem="cifar"):
+    return ResNet(BasicBlock, [2, 2, 2, 2], num_classes, stem)
+
+
+def ResNet34(num_classes=10, stem="cifar"):
+    return ResNet(BasicBlock, [3, 4, 6, 3], num_classes, stem)
+
+
+def ResNet50(num_classes=10, stem="cifar"):
+    return ResNet(Bottleneck, [3, 4, 6, 3], num_classes, stem)
+
+
+def ResNet101(num_classes=10, stem="cifar"):
+    return ResNet(Bottleneck, [3, 4, 23, 3], num_classes, stem)
+
+
+def ResNet152(num_classes=10, stem="cifar"):
+    return ResNet(Bottleneck, [3, 8, 36, 3], num_classes, stem)

@@ -1,0 +1,221 @@
+"""Python entry points of the hand-written gfx950 kernels (``ops/csrc/*.hip``).
+
+Every wrapper validates shapes/dtypes/alignment on the host (a kernel launched on a bad operand can
+fault the whole GPU node), then launches on torch's *current* HIP stream so calls compose with
+``torch.cuda.stream(...)`` and are captured by ``torch.cuda.graph``.
+
+These wrappers only accept device tensors.  CPU execution (Gloo tests) goes through the torch
+oracle in ``compress/oracle.py``; there is no silent fallback on the GPU: if the extension is not
+built, :func:`require` raises.
+"""
+import importlib
+import os
+
+import torch
+
+_IMPORT_ERROR = None
+try:  # torch is imported first so the extension binds to torch's already-loaded HIP runtime
+    _C = importlib.import_module(__name__ + "._C")
+except ImportError as e:  # pragma: no cover - depends on the build
+    _C = None
+    _IMPORT_ERROR = e
+
+VK_Q8, VK_Q4, VK_F32 = 0, 1, 2
+
+
+def available() -> bool:
+    return _C is not None
+
+
+def require():
+    if _C is None:
+        raise RuntimeError(
+            "ewdml HIP extension is not built or failed to load "
+            f"({_IMPORT_ERROR}); run `python -m ewdml.ops.build` (or __graft_entry__.build())")
+    return _C
+
+
+def library_path():
+    return getattr(_C, "__file__", None)
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _ptr(t) -> int:
+    return 0 if t is None else t.data_ptr()
+
+
+def _check(t, dtype, name, align=16):
+    if not t.is_cuda:
+        raise ValueError(f"{name} must be a device tensor")
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    if t.data_ptr() % align:
+        raise ValueError(f"{name} must be {align}-byte aligned")
+
+
+class DevicePlan:
+    """Device-resident tables + scratch for one bucket (built once, reused every step)."""
+
+    def __init__(self, plan, device):
+        self.plan = plan
+        self.tensors = plan.tensor_table(device)
+        self.chunks = plan.chunk_table(device)
+        C, T = plan.num_chunks, plan.num_tensors
+        nbytes = max(require().topk_scratch_bytes(T, C), require().qsgd_scratch_bytes(T, C))
+        self.scratch = torch.zeros(nbytes, dtype=torch.uint8, device=device)
+
+
+def _check_bucket(dp, grad, name="grad"):
+    _check(grad, torch.float32, name)
+    if grad.numel() < dp.plan.length:
+        raise ValueError(f"{name} has {grad.numel()} elements, bucket needs {dp.plan.length}")
+
+
+def topk_encode(dp: DevicePlan, grad, payload, layout, levels: int, norm: str, key: int,
+                resid=None):
+    C = require()
+    _check_bucket(dp, grad)
+    _check(payload, torch.uint8, "payload")
+    if payload.numel() < layout.nbytes:
+        raise ValueError("payload too small")
+    if resid is not None:
+        _check_bucket(dp, resid, "resid")
+    if layout.kind == "topk":
+        vk = VK_F32
+    elif layout.bits == 8:
+        vk = VK_Q8
+    else:
+        vk = VK_Q4
+    if vk != VK_F32 and not (1 <= levels <= (127 if layout.bits == 8 else 7)):
+        raise ValueError(f"levels={levels} does not fit {layout.bits}-bit codes")
+    C.topk_encode(_ptr(grad), _ptr(resid), _ptr(dp.chunks), _ptr(dp.tensors), _ptr(dp.scratch),
+                  _ptr(payload), layout.nbytes, dp.plan.num_tensors, dp.plan.num_chunks,
+                  layout.scales, layout.counts, layout.idx, layout.codes, vk,
+                  1 if norm == "l2" else 0, float(levels), float(1.0 / levels), key & 0xFFFFFFFF,
+                  dp.plan.bucket_offset & 0xFFFFFFFF, _stream())
+
+
+def topk_decode_apply(dp: DevicePlan, recv, layout, levels: int, param=None, mom=None,
+                      grad_out=None, lr=0.0, momentum=0.0, dampening=0.0, weight_decay=0.0,
+                      grad_scale=1.0, nesterov=False, first=False):
+    C = require()
+    _check(recv, torch.uint8, "recv")
+    if recv.dim() != 2 or recv.shape[1] != layout.nbytes:
+        raise ValueError(f"recv must be [nranks, {layout.nbytes}]")
+    if recv.shape[0] > 64:
+        raise ValueError("at most 64 ranks per decode")
+    apply = param is not None
+    if apply:
+        _check_bucket(dp, param, "param")
+        _check_bucket(dp, mom, "mom")
+    if grad_out is not None:
+        _check_bucket(dp, grad_out, "grad_out")
+    if not apply and grad_out is None:
+        raise ValueError("nothing to do: pass param/mom and/or grad_out")
+    vk = VK_F32 if layout.kind == "topk" else (VK_Q8 if layout.bits == 8 else VK_Q4)
+    C.topk_decode_apply(_ptr(recv), recv.shape[0], layout.nbytes, _ptr(dp.chunks),
+                        _ptr(dp.tensors), dp.plan.num_chunks, layout.scales, layout.counts,
+                        layout.idx, layout.codes, vk, float(1.0 / levels), _ptr(param), _ptr(mom),
+                        _ptr(grad_out), lr, momentum, dampening, weight_decay, grad_scale,
+                        int(nesterov), int(first), int(apply), _stream())
+
+
+def qsgd_encode(dp: DevicePlan, grad, payload, layout, levels: int, norm: str, key: int,
+                resid=None):
+    C = require()
+    _check_bucket(dp, grad)
+    _check(payload, torch.uint8, "payload")
+    if payload.numel() < layout.nbytes:
+        raise ValueError("payload too small")
+    if resid is not None:
+        _check_bucket(dp, resid, "resid")
+    if not (1 <= levels <= (127 if layout.bits == 8 else 7)):
+        raise ValueError(f"levels={levels} does not fit {layout.bits}-bit codes")
+    C.qsgd_encode(_ptr(grad), _ptr(resid), _ptr(dp.chunks), _ptr(dp.tensors), _ptr(dp.scratch),
+                  _ptr(payload), layout.nbytes, dp.plan.num_tensors, dp.plan.num_chunks,
+                  layout.scales, layout.codes, layout.bits, 1 if norm == "l2" else 0,
+                  float(levels), float(1.0 / levels), key & 0xFFFFFFFF,
+                  dp.plan.bucket_offset & 0xFFFFFFFF, _stream())
+
+
+def qsgd_decode_apply(dp: DevicePlan, recv, layout, levels: int, param=None, mom=None,
+                      grad_out=None, lr=0.0, momentum=0.0, dampening=0.0, weight_decay=0.0,
+                      grad_scale=1.0, nesterov=False, first=False):
+    C = require()
+    _check(recv, torch.uint8, "recv")
+    if recv.dim() != 2 or recv.shape[1] != layout.nbytes:
+        raise ValueError(f"recv must be [nranks, {layout.nbytes}]")
+    apply = param is not None
+    if apply:
+        _check_bucket(dp, param, "param")
+        _check_bucket(dp, mom, "mom")
+    if grad_out is not None:
+        _check_bucket(dp, grad_out, "grad_out")
+    if not apply and grad_out is None:
+        raise ValueError("nothing to do: pass param/mom and/or grad_out")
+    C.qsgd_decode_apply(_ptr(recv), recv.shape[0], layout.nbytes, _ptr(dp.chunks),
+                        _ptr(dp.tensors), dp.plan.num_chunks, layout.scales, layout.codes,
+                        layout.bits, float(1.0 / levels), _ptr(param), _ptr(mom), _ptr(grad_out),
+                        lr, momentum, dampening, weight_decay, grad_scale, int(nesterov),
+                        int(first), int(apply), _stream())
+
+
+_GDT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
+
+
+def sgd_flat(param, mom, grad, lr, momentum=0.0, dampening=0.0, weight_decay=0.0,
+             grad_scale=1.0, nesterov=False, first=False):
+    C = require()
+    _check(param, torch.float32, "param")
+    _check(mom, torch.float32, "mom")
+    if grad.dtype not in _GDT:
+        raise TypeError(f"unsupported grad dtype {grad.dtype}")
+    _check(grad, grad.dtype, "grad", align=8)
+    n = param.numel()
+    if mom.numel() != n or grad.numel() != n or n % 4:
+        raise ValueError("param/mom/grad must have equal numel, a multiple of 4")
+    C.sgd_flat(_ptr(param), _ptr(mom), _ptr(grad), n, _GDT[grad.dtype], lr, momentum, dampening,
+               weight_decay, grad_scale, int(nesterov), int(first), _stream())
+
+
+def adam_flat(param, exp_avg, exp_avg_sq, max_exp_avg_sq, grad, lr_step, beta1, beta2, eps,
+              weight_decay=0.0, grad_scale=1.0, amsgrad=False):
+    C = require()
+    for t, nm in ((param, "param"), (exp_avg, "exp_avg"), (exp_avg_sq, "exp_avg_sq")):
+        _check(t, torch.float32, nm)
+    if amsgrad:
+        _check(max_exp_avg_sq, torch.float32, "max_exp_avg_sq")
+    _check(grad, grad.dtype, "grad", align=8)
+    n = param.numel()
+    if n % 4 or grad.numel() != n or exp_avg.numel() != n or exp_avg_sq.numel() != n:
+        raise ValueError("flat buffers must have equal numel, a multiple of 4")
+    C.adam_flat(_ptr(param), _ptr(exp_avg), _ptr(exp_avg_sq), _ptr(max_exp_avg_sq), _ptr(grad),
+                n, _GDT[grad.dtype], lr_step, beta1, beta2, eps, weight_decay, grad_scale,
+                int(amsgrad), _stream())
+
+
+def cast_scale(src, dst, scale=1.0):
+    C = require()
+    _check(src, torch.float32, "src")
+    if dst.dtype not in (torch.bfloat16, torch.float16):
+        raise TypeError("dst must be bf16 or fp16")
+    _check(dst, dst.dtype, "dst", align=8)
+    if src.numel() != dst.numel() or src.numel() % 4:
+        raise ValueError("src/dst must have equal numel, a multiple of 4")
+    C.cast_scale(_ptr(src), _ptr(dst), src.numel(), float(scale),
+                 int(dst.dtype == torch.bfloat16), _stream())
+
+
+def build(force: bool = False) -> str:
+    from .build import build as _b
+    return _b(force=force)
+
+
+def hip_required() -> bool:
+    """True when running on a GPU box where the HIP path must be used (fail loudly otherwise)."""
+    return torch.cuda.is_available() and os.environ.get("EWDML_ALLOW_NO_EXT") != "1"

@@ -1,0 +1,139 @@
+// Shared device helpers for the ewdml CDNA4 (gfx950) kernels.
+//
+// Conventions used by every kernel in this directory:
+//   * a block is 256 threads = 4 wave64s (EW_BLOCK); lane = threadIdx.x & 63;
+//   * a *chunk* is EW_CHUNK = 8192 consecutive elements of one parameter tensor inside the flat
+//     gradient bucket; one block owns one chunk (compress/plan.py builds the tables);
+//   * reductions use a fixed shuffle tree so results are bitwise reproducible run to run;
+//   * the file set is compiled with -ffp-contract=off so results match the torch oracle
+//     (compress/oracle.py) bit for bit.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <stdexcept>
+#include <string>
+
+// Host-side error check: turn a HIP error into a C++ exception (surfaces as a Python RuntimeError).
+#define EW_CHECK(expr)                                                                       \
+  do {                                                                                       \
+    hipError_t _e = (expr);                                                                  \
+    if (_e != hipSuccess)                                                                    \
+      throw std::runtime_error(std::string("ewdml HIP error: ") + hipGetErrorString(_e) +   \
+                               " at " __FILE__ ":" + std::to_string(__LINE__));             \
+  } while (0)
+#define EW_CHECK_LAUNCH() EW_CHECK(hipGetLastError())
+
+#define EW_CHUNK 8192
+#define EW_BLOCK 256
+#define EW_WAVES (EW_BLOCK / 64)
+#define EW_MAX_RANKS 64
+
+struct TensorRow {  // mirrors BucketPlan.tensor_table()
+  int off, numel, k, chunk0, nchunks, entry0, code0, pad;
+};
+struct ChunkRow {  // mirrors BucketPlan.chunk_table()
+  int tensor, start, len, local;
+};
+
+struct SgdArgs {
+  float lr, momentum, dampening, weight_decay, grad_scale;
+  int nesterov, first;
+};
+
+// ---- counter-based RNG (must equal compress/rng.py) -------------------------------------------
+__device__ __forceinline__ uint32_t ew_mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352dU;
+  x ^= x >> 15;
+  x *= 0x846ca68bU;
+  x ^= x >> 16;
+  return x;
+}
+__device__ __forceinline__ float ew_uniform(uint32_t idx, uint32_t key) {
+  return (float)(ew_mix32(idx ^ key) >> 8) * (1.0f / 16777216.0f);
+}
+
+// QSGD stochastic rounding of one value (compress/oracle.py::quantize).
+__device__ __forceinline__ int ew_quantize(float x, float inv, float levels, uint32_t gidx,
+                                           uint32_t key) {
+  float lvl = fabsf(x) * inv;
+  float fl = floorf(lvl);
+  float u = ew_uniform(gidx, key);
+  float q = fl + ((u < (lvl - fl)) ? 1.0f : 0.0f);
+  q = fminf(q, levels);
+  return (int)(x < 0.0f ? -q : q);
+}
+
+__device__ __forceinline__ uint32_t ew_key(float x) { return __float_as_uint(x) & 0x7fffffffu; }
+
+// ---- wave / block scans and reductions ----------------------------------------------------------
+__device__ __forceinline__ uint32_t ew_wave_incl_scan(uint32_t v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t t = __shfl_up(v, d, 64);
+    if (lane >= d) v += t;
+  }
+  return v;
+}
+
+// Exclusive scan over the block in thread order; `ws` is EW_WAVES words of LDS.
+__device__ __forceinline__ uint32_t ew_block_excl_scan(uint32_t v, uint32_t* ws, uint32_t& total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t inc = ew_wave_incl_scan(v);
+  if (lane == 63) ws[w] = inc;
+  __syncthreads();
+  uint32_t base = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < EW_WAVES; ++i) {
+    uint32_t x = ws[i];
+    base += (i < w) ? x : 0u;
+    tot += x;
+  }
+  __syncthreads();
+  total = tot;
+  return base + inc - v;
+}
+
+__device__ __forceinline__ float ew_wave_sum(float v) {
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) v += __shfl_down(v, d, 64);
+  return v;  // valid in lane 0
+}
+__device__ __forceinline__ uint32_t ew_wave_sum_u(uint32_t v) {
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) v += __shfl_down(v, d, 64);
+  return v;
+}
+__device__ __forceinline__ uint32_t ew_wave_max_u(uint32_t v) {
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) v = max(v, (uint32_t)__shfl_down(v, d, 64));
+  return v;
+}
+
+// Block sum in a fixed order (wave trees, then waves 0..3); result valid in thread 0.
+__device__ __forceinline__ float ew_block_sum(float v, float* wsf) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  v = ew_wave_sum(v);
+  if (lane == 0) wsf[w] = v;
+  __syncthreads();
+  float s = 0.0f;
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int i = 0; i < EW_WAVES; ++i) s += wsf[i];
+  }
+  __syncthreads();
+  return s;
+}
+
+// ---- optimizer element updates (reference optim/sgd.py:75-91) ----------------------------------
+__device__ __forceinline__ void ew_sgd(float& p, float& b, float g, const SgdArgs& a) {
+  float d = g;
+  if (a.weight_decay != 0.0f) d = d + a.weight_decay * p;
+  if (a.momentum != 0.0f) {
+    b = a.first ? d : (b * a.momentum + (1.0f - a.dampening) * d);
+    d = a.nesterov ? (d + a.momentum * b) : b;
+  }
+  p = p - a.lr * d;
+}

@@ -1,0 +1,76 @@
+// Host-side entry points of the ewdml HIP kernels (C++ only, no HIP types), bound to Python in
+// bindings.cpp.  Pointers are device addresses passed as integers; `stream` is a hipStream_t.
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+struct TopkEncodeArgs {
+  uintptr_t grad, resid, chunks, tensors, scratch, payload, stream;
+  long long payload_bytes;
+  int num_tensors, num_chunks;
+  int scales_off, counts_off, idx_off, codes_off;
+  int value_kind;  // 0 = int8 QSGD, 1 = int4 QSGD, 2 = fp32 values (plain top-k)
+  int norm_l2;     // 0 = max-norm scale, 1 = L2 norm of the selected values
+  float levels, inv_levels;
+  uint32_t key, bucket_offset;
+};
+
+struct TopkDecodeArgs {
+  uintptr_t recv, chunks, tensors, param, mom, grad_out, stream;
+  long long stride;
+  int nranks, num_chunks;
+  int scales_off, counts_off, idx_off, codes_off;
+  int value_kind;
+  float inv_levels;
+  float lr, momentum, dampening, weight_decay, grad_scale;
+  int nesterov, first, apply;
+};
+
+struct QsgdEncodeArgs {
+  uintptr_t grad, resid, chunks, tensors, scratch, payload, stream;
+  long long payload_bytes;
+  int num_tensors, num_chunks;
+  int scales_off, codes_off, bits, norm_l2;
+  float levels, inv_levels;
+  uint32_t key, bucket_offset;
+};
+
+struct QsgdDecodeArgs {
+  uintptr_t recv, chunks, tensors, param, mom, grad_out, stream;
+  long long stride;
+  int nranks, num_chunks;
+  int scales_off, codes_off, bits;
+  float inv_levels;
+  float lr, momentum, dampening, weight_decay, grad_scale;
+  int nesterov, first, apply;
+};
+
+struct SgdFlatArgs {
+  uintptr_t param, mom, grad, stream;
+  long long n;
+  int grad_dtype;  // 0 = fp32, 1 = bf16, 2 = fp16
+  float lr, momentum, dampening, weight_decay, grad_scale;
+  int nesterov, first;
+};
+
+struct AdamFlatArgs {
+  uintptr_t param, exp_avg, exp_avg_sq, max_exp_avg_sq, grad, stream;
+  long long n;
+  int grad_dtype;
+  float lr_step, beta1, beta2, eps, weight_decay, grad_scale, bc2_sqrt;
+  int amsgrad;
+};
+
+size_t ew_topk_scratch_bytes(int num_tensors, int num_chunks);
+void ew_topk_encode(const TopkEncodeArgs& a);
+void ew_topk_decode_apply(const TopkDecodeArgs& a);
+
+size_t ew_qsgd_scratch_bytes(int num_tensors, int num_chunks);
+void ew_qsgd_encode(const QsgdEncodeArgs& a);
+void ew_qsgd_decode_apply(const QsgdDecodeArgs& a);
+
+void ew_sgd_flat(const SgdFlatArgs& a);
+void ew_adam_flat(const AdamFlatArgs& a);
+// dst (bf16 when to_bf16 else fp16) = src * scale
+void ew_cast_scale(uintptr_t src, uintptr_t dst, long long n, float scale, int to_bf16,
+                   uintptr_t stream);

@@ -1,0 +1,474 @@
+// Top-k sparsification + QSGD quantisation of a flat gradient bucket, and the fused
+// decode -> average -> SGD step on the receive side.  CDNA4 / gfx950, wave64.
+//
+// Replaces the reference's per-tensor torch chains:
+//   TopK.py:5-10   flatten/abs/topk/gather       -> radix select + ordered compaction below
+//   qsgd.py:17-28  norm/abs/floor/uniform/sign   -> fused into the compaction (ew_quantize)
+//   TopK.py:13-17  zeros().scatter_()            -> LDS scatter in k_topk_decode_apply
+//   sync_replicas_master_nn.py:189,216  sum/avg  -> fused (rank-ordered LDS sum * 1/N)
+//   optim/sgd.py:75-91 per-tensor SGD           -> fused into the same kernel (ew_sgd)
+//
+// Exact top-k by a 3-pass MSD radix select over the 31-bit |g| key (11 + 10 + 10 bits).  Per
+// pass: every chunk block builds an LDS histogram of the current digit over the elements that
+// match the prefix selected so far and merges it into a per-tensor global histogram; a one-block-
+// per-tensor kernel then finds the digit holding the k-th largest key.  After 3 passes the exact
+// threshold key and the number of threshold ties to keep are known; ties are kept lowest index
+// first, so every rank emits exactly k entries per tensor (fixed-size all-gather).
+//
+// Encode launches per bucket: hist0, select0, hist1, select1, hist2, select2, count, scan, write.
+// The global state lives in one zero-initialised scratch block (one hipMemsetAsync).
+#include "common.h"
+#include "ewdml_ops.h"
+
+namespace {
+
+constexpr int NB0 = 2048;  // pass-0 digit: key bits [30:20]
+constexpr int NB1 = 1024;  // pass-1 digit: key bits [19:10]
+constexpr int NB2 = 1024;  // pass-2 digit: key bits [9:0]
+
+// state[t] = {prefix, k_rem, max_key, pad}
+template <bool EF>
+__global__ __launch_bounds__(EW_BLOCK) void k_topk_hist0(float* __restrict__ g,
+                                                         float* __restrict__ resid,
+                                                         const ChunkRow* __restrict__ chunks,
+                                                         uint32_t* __restrict__ hist,
+                                                         uint32_t* __restrict__ state) {
+  __shared__ uint32_t h[NB0];
+  for (int i = threadIdx.x; i < NB0; i += EW_BLOCK) h[i] = 0;
+  __syncthreads();
+  const ChunkRow c = chunks[blockIdx.x];
+  float* src = g + c.start;
+  uint32_t kmax = 0;
+  const int n4 = c.len >> 2;
+  for (int i = threadIdx.x; i < n4; i += EW_BLOCK) {
+    float4 v = reinterpret_cast<float4*>(src)[i];
+    if (EF) {  // error feedback: compress g + residual, write it back (later passes reread it)
+      float4 r = reinterpret_cast<const float4*>(resid + c.start)[i];
+      v.x = v.x + r.x; v.y = v.y + r.y; v.z = v.z + r.z; v.w = v.w + r.w;
+      reinterpret_cast<float4*>(src)[i] = v;
+    }
+    const uint32_t k0 = ew_key(v.x), k1 = ew_key(v.y), k2 = ew_key(v.z), k3 = ew_key(v.w);
+    atomicAdd(&h[k0 >> 20], 1u);
+    atomicAdd(&h[k1 >> 20], 1u);
+    atomicAdd(&h[k2 >> 20], 1u);
+    atomicAdd(&h[k3 >> 20], 1u);
+    kmax = max(max(kmax, max(k0, k1)), max(k2, k3));
+  }
+  for (int i = (n4 << 2) + threadIdx.x; i < c.len; i += EW_BLOCK) {
+    float x = src[i];
+    if (EF) {
+      x = x + resid[c.start + i];
+      src[i] = x;
+    }
+    const uint32_t k = ew_key(x);
+    atomicAdd(&h[k >> 20], 1u);
+    kmax = max(kmax, k);
+  }
+  kmax = ew_wave_max_u(kmax);
+  if ((threadIdx.x & 63) == 0) atomicMax(&state[c.tensor * 4 + 2], kmax);
+  __syncthreads();
+  uint32_t* dst = hist + (size_t)c.tensor * NB0;
+  for (int i = threadIdx.x; i < NB0; i += EW_BLOCK)
+    if (h[i]) atomicAdd(&dst[i], h[i]);
+}
+
+// Histogram of key bits [SHIFT+9 : SHIFT] over elements whose bits above MATCH equal the prefix.
+template <int SHIFT, int MATCH>
+__global__ __launch_bounds__(EW_BLOCK) void k_topk_hist(const float* __restrict__ g,
+                                                        const ChunkRow* __restrict__ chunks,
+                                                        const uint32_t* __restrict__ state,
+                                                        uint32_t* __restrict__ hist) {
+  __shared__ uint32_t h[NB1];
+  for (int i = threadIdx.x; i < NB1; i += EW_BLOCK) h[i] = 0;
+  __syncthreads();
+  const ChunkRow c = chunks[blockIdx.x];
+  const float* src = g + c.start;
+  const uint32_t want = state[c.tensor * 4] >> MATCH;
+  const int n4 = c.len >> 2;
+  for (int i = threadIdx.x; i < n4; i += EW_BLOCK) {
+    const float4 v = reinterpret_cast<const float4*>(src)[i];
+    const uint32_t kk[4] = {ew_key(v.x), ew_key(v.y), ew_key(v.z), ew_key(v.w)};
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if ((kk[j] >> MATCH) == want) atomicAdd(&h[(kk[j] >> SHIFT) & (NB1 - 1)], 1u);
+  }
+  for (int i = (n4 << 2) + threadIdx.x; i < c.len; i += EW_BLOCK) {
+    const uint32_t k = ew_key(src[i]);
+    if ((k >> MATCH) == want) atomicAdd(&h[(k >> SHIFT) & (NB1 - 1)], 1u);
+  }
+  __syncthreads();
+  uint32_t* dst = hist + (size_t)c.tensor * NB1;
+  for (int i = threadIdx.x; i < NB1; i += EW_BLOCK)
+    if (h[i]) atomicAdd(&dst[i], h[i]);
+}
+
+// One block per tensor: find the digit (scanning from the top) that holds the k_rem-th largest.
+template <int NB, int SHIFT, bool FIRST>
+__global__ __launch_bounds__(EW_BLOCK) void k_topk_select(const uint32_t* __restrict__ hist,
+                                                          const TensorRow* __restrict__ tensors,
+                                                          uint32_t* __restrict__ state) {
+  constexpr int PER = NB / EW_BLOCK;
+  __shared__ uint32_t ws[EW_WAVES];
+  const int t = blockIdx.x;
+  const uint32_t k_rem = FIRST ? (uint32_t)tensors[t].k : state[t * 4 + 1];
+  const uint32_t* ht = hist + (size_t)t * NB;
+  uint32_t cnt[PER];
+  uint32_t tsum = 0;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    cnt[j] = ht[NB - 1 - (threadIdx.x * PER + j)];
+    tsum += cnt[j];
+  }
+  uint32_t total;
+  const uint32_t excl = ew_block_excl_scan(tsum, ws, total);
+  if (excl < k_rem && k_rem <= excl + tsum) {
+    uint32_t run = excl;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      if (run + cnt[j] >= k_rem) {
+        const uint32_t bin = NB - 1 - (threadIdx.x * PER + j);
+        state[t * 4 + 0] |= bin << SHIFT;
+        state[t * 4 + 1] = k_rem - run;
+        break;
+      }
+      run += cnt[j];
+    }
+  }
+}
+
+// Per chunk: #(key > thr), #(key == thr) and sum of squares of the key > thr values.
+__global__ __launch_bounds__(EW_BLOCK) void k_topk_count(const float* __restrict__ g,
+                                                         const ChunkRow* __restrict__ chunks,
+                                                         const uint32_t* __restrict__ state,
+                                                         uint32_t* __restrict__ cnt_gt,
+                                                         uint32_t* __restrict__ cnt_eq,
+                                                         float* __restrict__ chunk_sq) {
+  __shared__ float wsf[EW_WAVES];
+  const ChunkRow c = chunks[blockIdx.x];
+  const float* src = g + c.start;
+  const uint32_t thr = state[c.tensor * 4];
+  uint32_t gt = 0, eq = 0;
+  float sq = 0.0f;
+  const int n4 = c.len >> 2;
+  for (int i = threadIdx.x; i < n4; i += EW_BLOCK) {
+    const float4 v = reinterpret_cast<const float4*>(src)[i];
+    const float xs[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t k = ew_key(xs[j]);
+      if (k > thr) {
+        ++gt;
+        sq = sq + xs[j] * xs[j];
+      }
+      eq += (k == thr);
+    }
+  }
+  for (int i = (n4 << 2) + threadIdx.x; i < c.len; i += EW_BLOCK) {
+    const float x = src[i];
+    const uint32_t k = ew_key(x);
+    if (k > thr) {
+      ++gt;
+      sq = sq + x * x;
+    }
+    eq += (k == thr);
+  }
+  __shared__ uint32_t wsu[2 * EW_WAVES];
+  gt = ew_wave_sum_u(gt);
+  eq = ew_wave_sum_u(eq);
+  if ((threadIdx.x & 63) == 0) {
+    wsu[threadIdx.x >> 6] = gt;
+    wsu[EW_WAVES + (threadIdx.x >> 6)] = eq;
+  }
+  const float s = ew_block_sum(sq, wsf);  // contains a __syncthreads
+  if (threadIdx.x == 0) {
+    uint32_t a = 0, b = 0;
+    for (int i = 0; i < EW_WAVES; ++i) {
+      a += wsu[i];
+      b += wsu[EW_WAVES + i];
+    }
+    cnt_gt[blockIdx.x] = a;
+    cnt_eq[blockIdx.x] = b;
+    chunk_sq[blockIdx.x] = s;
+  }
+}
+
+// One block per tensor: allocate threshold ties to chunks (lowest index first), chunk entry
+// offsets, the per-chunk uint16 counts of the payload, and the tensor's QSGD scale.
+__global__ __launch_bounds__(EW_BLOCK) void k_topk_scan(
+    const TensorRow* __restrict__ tensors, const uint32_t* __restrict__ state,
+    const uint32_t* __restrict__ cnt_gt, const uint32_t* __restrict__ cnt_eq,
+    const float* __restrict__ chunk_sq, uint32_t* __restrict__ chunk_off,
+    uint32_t* __restrict__ chunk_ties, float* __restrict__ inv_out, uint8_t* __restrict__ payload,
+    int scales_off, int counts_off, float levels, int norm_l2) {
+  __shared__ uint32_t ws[EW_WAVES];
+  __shared__ float wsf[EW_WAVES];
+  const int t = blockIdx.x;
+  const TensorRow tr = tensors[t];
+  const uint32_t need = state[t * 4 + 1];
+  const uint32_t thr = state[t * 4 + 0];
+  uint16_t* counts = reinterpret_cast<uint16_t*>(payload + counts_off);
+  uint32_t carry_eq = 0, carry_cnt = 0;
+  float sq = 0.0f;
+  for (int base = 0; base < tr.nchunks; base += EW_BLOCK) {
+    const int lc = base + threadIdx.x;
+    const bool ok = lc < tr.nchunks;
+    const int c = tr.chunk0 + lc;
+    const uint32_t gt = ok ? cnt_gt[c] : 0u, eq = ok ? cnt_eq[c] : 0u;
+    uint32_t tot_eq, tot_cnt;
+    const uint32_t eq_before = carry_eq + ew_block_excl_scan(eq, ws, tot_eq);
+    const uint32_t ties = need > eq_before ? min(need - eq_before, eq) : 0u;
+    const uint32_t cnt = gt + ties;
+    const uint32_t off = carry_cnt + ew_block_excl_scan(cnt, ws, tot_cnt);
+    if (ok) {
+      counts[c] = (uint16_t)cnt;
+      chunk_off[c] = off;
+      chunk_ties[c] = ties;
+      sq = sq + chunk_sq[c];
+    }
+    carry_eq += tot_eq;
+    carry_cnt += tot_cnt;
+  }
+  const float total_sq = ew_block_sum(sq, wsf);
+  if (threadIdx.x == 0) {
+    const float tv = __uint_as_float(thr);
+    float scale;
+    if (norm_l2) {
+      scale = sqrtf(total_sq + (float)need * (tv * tv));
+    } else {
+      scale = __uint_as_float(state[t * 4 + 2]);
+    }
+    reinterpret_cast<float*>(payload + scales_off)[t] = scale;
+    inv_out[t] = scale > 0.0f ? levels / scale : 0.0f;
+  }
+}
+
+enum ValueKind { VK_Q8 = 0, VK_Q4 = 1, VK_F32 = 2 };
+
+// Ordered stream compaction of the selected entries of one chunk + fused quantisation.
+template <int VK, bool EF>
+__global__ __launch_bounds__(EW_BLOCK) void k_topk_write(
+    const float* __restrict__ g, float* __restrict__ resid, const ChunkRow* __restrict__ chunks,
+    const TensorRow* __restrict__ tensors, const uint32_t* __restrict__ state,
+    const uint32_t* __restrict__ chunk_off, const uint32_t* __restrict__ chunk_ties,
+    const float* __restrict__ inv_arr, uint8_t* __restrict__ payload, int scales_off, int idx_off,
+    int codes_off, float levels, float inv_levels, uint32_t key, uint32_t bucket_offset) {
+  __shared__ uint32_t ws[EW_WAVES];
+  const ChunkRow c = chunks[blockIdx.x];
+  const TensorRow tr = tensors[c.tensor];
+  const float* src = g + c.start;
+  const uint32_t thr = state[c.tensor * 4];
+  const uint32_t ties = chunk_ties[blockIdx.x];
+  const uint32_t ebase = (uint32_t)tr.entry0 + chunk_off[blockIdx.x];
+  const uint32_t eend = (uint32_t)(tr.entry0 + tr.k);  // never write past this tensor's entries
+  const float inv = inv_arr[c.tensor];
+  float step = 0.0f;
+  if (VK != VK_F32) step = reinterpret_cast<const float*>(payload + scales_off)[c.tensor] * inv_levels;
+  uint16_t* idx_out = reinterpret_cast<uint16_t*>(payload + idx_off);
+  const uint32_t gbase = bucket_offset + (uint32_t)c.start;
+  uint32_t carry_gt = 0, carry_eq = 0;
+  for (int it = 0; it < c.len; it += 4 * EW_BLOCK) {
+    const int i0 = it + 4 * threadIdx.x;
+    float xs[4];
+    bool valid[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) valid[j] = (i0 + j) < c.len;
+    if (valid[3]) {
+      const float4 v = *reinterpret_cast<const float4*>(src + i0);
+      xs[0] = v.x; xs[1] = v.y; xs[2] = v.z; xs[3] = v.w;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) xs[j] = valid[j] ? src[i0 + j] : 0.0f;
+    }
+    uint32_t ngt = 0, neq = 0;
+    bool isgt[4], iseq[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t k = ew_key(xs[j]);
+      isgt[j] = valid[j] && k > thr;
+      iseq[j] = valid[j] && k == thr;
+      ngt += isgt[j];
+      neq += iseq[j];
+    }
+    uint32_t tot;
+    const uint32_t ex = ew_block_excl_scan(ngt | (neq << 16), ws, tot);
+    const uint32_t gt_before = carry_gt + (ex & 0xffffu);
+    uint32_t eqr = carry_eq + (ex >> 16);
+    uint32_t pos = ebase + gt_before + min(ties, eqr);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const bool sel = isgt[j] || (iseq[j] && eqr < ties);
+      eqr += iseq[j];
+      float sent = 0.0f;
+      if (sel && pos < eend) {
+        idx_out[pos] = (uint16_t)(i0 + j);
+        if (VK == VK_F32) {
+          reinterpret_cast<float*>(payload + codes_off)[pos] = xs[j];
+          sent = xs[j];
+        } else {
+          const int q = ew_quantize(xs[j], inv, levels, gbase + (uint32_t)(i0 + j), key);
+          if (VK == VK_Q8) {
+            reinterpret_cast<int8_t*>(payload + codes_off)[pos] = (int8_t)q;
+          } else {
+            atomicOr(reinterpret_cast<uint32_t*>(payload + codes_off) + (pos >> 3),
+                     ((uint32_t)q & 0xfu) << ((pos & 7u) * 4u));
+          }
+          sent = (float)q * step;
+        }
+        ++pos;
+      }
+      if (EF && valid[j]) resid[c.start + i0 + j] = xs[j] - sent;
+    }
+    carry_gt += tot & 0xffffu;
+    carry_eq += tot >> 16;
+  }
+}
+
+// Receive side: one block per chunk.  Sum the N ranks' entries for this chunk in rank order in an
+// LDS accumulator (indices are unique within a rank, so no atomics), scale by 1/N, then either
+// write the averaged gradient and/or apply the SGD update to the chunk's parameters.
+template <int VK>
+__global__ __launch_bounds__(EW_BLOCK) void k_topk_decode_apply(
+    const uint8_t* __restrict__ recv, int nranks, long long stride,
+    const ChunkRow* __restrict__ chunks, const TensorRow* __restrict__ tensors, int scales_off,
+    int counts_off, int idx_off, int codes_off, float inv_levels, float* __restrict__ param,
+    float* __restrict__ mom, float* __restrict__ grad_out, SgdArgs sa, int apply) {
+  __shared__ float4 acc4[EW_CHUNK / 4];
+  __shared__ uint32_t s_off[EW_MAX_RANKS];
+  float* acc = reinterpret_cast<float*>(acc4);
+  const ChunkRow c = chunks[blockIdx.x];
+  const TensorRow tr = tensors[c.tensor];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int i = threadIdx.x; i < (c.len + 3) / 4; i += EW_BLOCK) acc4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  // entry offset of this chunk inside each rank's payload: entry0 + sum of earlier chunk counts
+  for (int r = w; r < nranks; r += EW_WAVES) {
+    const uint16_t* cnts = reinterpret_cast<const uint16_t*>(recv + r * stride + counts_off) + tr.chunk0;
+    uint32_t s = 0;
+    for (int j = lane; j < c.local; j += 64) s += cnts[j];
+    s = ew_wave_sum_u(s);
+    if (lane == 0) s_off[r] = (uint32_t)tr.entry0 + s;
+  }
+  __syncthreads();
+  for (int r = 0; r < nranks; ++r) {
+    const uint8_t* pay = recv + r * stride;
+    const uint32_t off = s_off[r];
+    // clamp to the tensor's entry range: a corrupted payload must not read out of bounds
+    const uint32_t eend = (uint32_t)(tr.entry0 + tr.k);
+    uint32_t cnt = reinterpret_cast<const uint16_t*>(pay + counts_off)[blockIdx.x];
+    cnt = off >= eend ? 0u : min(cnt, eend - off);
+    const uint16_t* idx = reinterpret_cast<const uint16_t*>(pay + idx_off) + off;
+    float step = 1.0f;
+    if (VK != VK_F32) step = reinterpret_cast<const float*>(pay + scales_off)[c.tensor] * inv_levels;
+    for (uint32_t e = threadIdx.x; e < cnt; e += EW_BLOCK) {
+      float v;
+      if (VK == VK_F32) {
+        v = reinterpret_cast<const float*>(pay + codes_off)[off + e];
+      } else if (VK == VK_Q8) {
+        v = (float)reinterpret_cast<const int8_t*>(pay + codes_off)[off + e];
+      } else {
+        const uint32_t pe = off + e;
+        const uint32_t b = pay[codes_off + (pe >> 1)];
+        int q = (int)((pe & 1u) ? (b >> 4) : (b & 0xfu));
+        v = (float)(q >= 8 ? q - 16 : q);
+      }
+      const float prod = v * step;
+      const int i = idx[e];
+      if (i < c.len) acc[i] = acc[i] + prod;
+    }
+    __syncthreads();
+  }
+  const float inv_n = sa.grad_scale;
+  float* p = param + c.start;
+  float* b = mom + c.start;
+  float* go = grad_out ? grad_out + c.start : nullptr;
+  for (int i = threadIdx.x; i < c.len; i += EW_BLOCK) {
+    const float gv = acc[i] * inv_n;
+    if (go) go[i] = gv;
+    if (apply) {
+      float pv = p[i], bv = b[i];
+      ew_sgd(pv, bv, gv, sa);
+      p[i] = pv;
+      b[i] = bv;
+    }
+  }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------------
+// host launchers
+// ---------------------------------------------------------------------------------------------
+#define EW_LAUNCH(kern, grid, stream, ...) \
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(EW_BLOCK), 0, (hipStream_t)(stream), __VA_ARGS__)
+
+void ew_topk_encode(const TopkEncodeArgs& a) {
+  auto* chunks = reinterpret_cast<const ChunkRow*>(a.chunks);
+  auto* tensors = reinterpret_cast<const TensorRow*>(a.tensors);
+  auto* scratch = reinterpret_cast<uint8_t*>(a.scratch);
+  const int T = a.num_tensors, C = a.num_chunks;
+  // scratch layout (all zeroed at once): state[T*4] | hist0[T*NB0] | hist1[T*NB1] | hist2[T*NB2]
+  // | cnt_gt[C] | cnt_eq[C] | chunk_off[C] | chunk_ties[C] | chunk_sq[C] | inv[T]
+  uint32_t* state = reinterpret_cast<uint32_t*>(scratch);
+  uint32_t* hist0 = state + 4 * T;
+  uint32_t* hist1 = hist0 + (size_t)T * NB0;
+  uint32_t* hist2 = hist1 + (size_t)T * NB1;
+  uint32_t* cnt_gt = hist2 + (size_t)T * NB2;
+  uint32_t* cnt_eq = cnt_gt + C;
+  uint32_t* chunk_off = cnt_eq + C;
+  uint32_t* chunk_ties = chunk_off + C;
+  float* chunk_sq = reinterpret_cast<float*>(chunk_ties + C);
+  float* inv = chunk_sq + C;
+  hipStream_t s = (hipStream_t)a.stream;
+  EW_CHECK(hipMemsetAsync(scratch, 0, ew_topk_scratch_bytes(T, C), s));
+  EW_CHECK(hipMemsetAsync(reinterpret_cast<void*>(a.payload), 0, a.payload_bytes, s));
+  float* g = reinterpret_cast<float*>(a.grad);
+  float* resid = reinterpret_cast<float*>(a.resid);
+  if (resid)
+    EW_LAUNCH(k_topk_hist0<true>, C, s, g, resid, chunks, hist0, state);
+  else
+    EW_LAUNCH(k_topk_hist0<false>, C, s, g, resid, chunks, hist0, state);
+  EW_LAUNCH((k_topk_select<NB0, 20, true>), T, s, hist0, tensors, state);
+  EW_LAUNCH((k_topk_hist<10, 20>), C, s, g, chunks, state, hist1);
+  EW_LAUNCH((k_topk_select<NB1, 10, false>), T, s, hist1, tensors, state);
+  EW_LAUNCH((k_topk_hist<0, 10>), C, s, g, chunks, state, hist2);
+  EW_LAUNCH((k_topk_select<NB2, 0, false>), T, s, hist2, tensors, state);
+  EW_LAUNCH(k_topk_count, C, s, g, chunks, state, cnt_gt, cnt_eq, chunk_sq);
+  auto* pay = reinterpret_cast<uint8_t*>(a.payload);
+  EW_LAUNCH(k_topk_scan, T, s, tensors, state, cnt_gt, cnt_eq, chunk_sq, chunk_off, chunk_ties, inv,
+            pay, a.scales_off, a.counts_off, a.levels, a.norm_l2);
+#define EW_WRITE(VK, EFV)                                                                          \
+  EW_LAUNCH((k_topk_write<VK, EFV>), C, s, g, resid, chunks, tensors, state, chunk_off, chunk_ties, \
+            inv, pay, a.scales_off, a.idx_off, a.codes_off, a.levels, a.inv_levels, a.key,         \
+            a.bucket_offset)
+  if (a.value_kind == VK_Q8) {
+    if (resid) EW_WRITE(VK_Q8, true); else EW_WRITE(VK_Q8, false);
+  } else if (a.value_kind == VK_Q4) {
+    if (resid) EW_WRITE(VK_Q4, true); else EW_WRITE(VK_Q4, false);
+  } else {
+    if (resid) EW_WRITE(VK_F32, true); else EW_WRITE(VK_F32, false);
+  }
+#undef EW_WRITE
+  EW_CHECK_LAUNCH();
+}
+
+size_t ew_topk_scratch_bytes(int T, int C) {
+  return sizeof(uint32_t) * ((size_t)4 * T + (size_t)T * (NB0 + NB1 + NB2) + 5 * (size_t)C + T);
+}
+
+void ew_topk_decode_apply(const TopkDecodeArgs& a) {
+  auto* chunks = reinterpret_cast<const ChunkRow*>(a.chunks);
+  auto* tensors = reinterpret_cast<const TensorRow*>(a.tensors);
+  SgdArgs sa{a.lr, a.momentum, a.dampening, a.weight_decay, a.grad_scale, a.nesterov, a.first};
+  auto* recv = reinterpret_cast<const uint8_t*>(a.recv);
+  auto* p = reinterpret_cast<float*>(a.param);
+  auto* m = reinterpret_cast<float*>(a.mom);
+  auto* go = reinterpret_cast<float*>(a.grad_out);
+  const int C = a.num_chunks;
+#define EW_DEC(VK)                                                                                   \
+  EW_LAUNCH(k_topk_decode_apply<VK>, C, a.stream, recv, a.nranks, a.stride, chunks, tensors,         \
+            a.scales_off, a.counts_off, a.idx_off, a.codes_off, a.inv_levels, p, m, go, sa, a.apply)
+  if (a.value_kind == VK_Q8) EW_DEC(VK_Q8);
+  else if (a.value_kind == VK_Q4) EW_DEC(VK_Q4);
+  else EW_DEC(VK_F32);
+#undef EW_DEC
+  EW_CHECK_LAUNCH();
+}

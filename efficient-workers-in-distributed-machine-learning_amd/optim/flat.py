@@ -1,0 +1,130 @@
+"""Optimizers over the flat parameter buffer with *explicit* gradients.
+
+Parity: ``optim/sgd.py:11-91`` (SGD whose ``step(grads=...)`` takes the averaged gradient received
+from the server; momentum buffer initialised to the first gradient, dampening, Nesterov, weight
+decay) and ``optim/adam.py:12-94`` (Adam/AMSGrad with explicit gradients).  The reference loops
+over parameter tensors; these run one HIP kernel over a flat range (``ops.sgd_flat`` /
+``ops.adam_flat``), and the top-k / QSGD exchanges fuse the SGD update into their decode kernel
+(``Codec.decode_apply_sgd``) so the averaged gradient never round-trips through HBM.
+"""
+import math
+
+import torch
+
+from .. import ops
+from ..compress import oracle
+
+
+class FlatSGD:
+    fusable = True
+
+    def __init__(self, flat, lr=0.01, momentum=0.0, dampening=0.0, weight_decay=0.0,
+                 nesterov=False):
+        if nesterov and (momentum <= 0 or dampening != 0):
+            raise ValueError("Nesterov momentum requires a momentum and zero dampening")
+        self.flat = flat
+        self.lr, self.momentum, self.dampening = lr, momentum, dampening
+        self.weight_decay, self.nesterov = weight_decay, nesterov
+        self.mom = torch.zeros_like(flat.data)
+        self.steps = 0
+
+    @property
+    def first(self) -> bool:
+        return self.steps == 0
+
+    def hparams(self) -> dict:
+        return dict(lr=self.lr, momentum=self.momentum, dampening=self.dampening,
+                    weight_decay=self.weight_decay, nesterov=self.nesterov)
+
+    def step_range(self, start: int, length: int, grad: torch.Tensor, grad_scale: float = 1.0):
+        """Apply SGD to ``flat.data[start:start+length]`` with ``grad`` (same length) * scale."""
+        p = self.flat.data[start:start + length]
+        m = self.mom[start:start + length]
+        if p.is_cuda:
+            ops.sgd_flat(p, m, grad, self.lr, self.momentum, self.dampening, self.weight_decay,
+                         grad_scale, self.nesterov, self.first)
+            return
+        g = grad.to(torch.float32)
+        if grad_scale != 1.0:
+            g = g * grad_scale
+        oracle.sgd_apply(p, m, g, self.lr, self.momentum, self.dampening, self.weight_decay,
+                         self.nesterov, self.first)
+
+    def step(self, grad: torch.Tensor = None, grad_scale: float = 1.0):
+        """Whole-model step (``grad`` defaults to the flat gradient buffer)."""
+        self.step_range(0, self.flat.numel, self.flat.grad if grad is None else grad, grad_scale)
+        self.end_step()
+
+    def end_step(self):
+        self.steps += 1
+
+    def state_dict(self):
+        return {"kind": "sgd", "mom": self.mom, "steps": self.steps, **self.hparams()}
+
+    def load_state_dict(self, sd):
+        self.mom.copy_(sd["mom"])
+        self.steps = int(sd["steps"])
+        for k in ("lr", "momentum", "dampening", "weight_decay", "nesterov"):
+            if k in sd:
+                setattr(self, k, sd[k])
+
+
+class FlatAdam:
+    fusable = False
+
+    def __init__(self, flat, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0,
+                 amsgrad=False):
+        self.flat = flat
+        self.lr, self.betas, self.eps = lr, betas, eps
+        self.weight_decay, self.amsgrad = weight_decay, amsgrad
+        self.exp_avg = torch.zeros_like(flat.data)
+        self.exp_avg_sq = torch.zeros_like(flat.data)
+        self.max_exp_avg_sq = torch.zeros_like(flat.data) if amsgrad else None
+        self.steps = 0
+
+    def step_range(self, start, length, grad, grad_scale=1.0):
+        t = self.steps + 1
+        b1, b2 = self.betas
+        sl = slice(start, start + length)
+        p = self.flat.data[sl]
+        vmax = self.max_exp_avg_sq[sl] if self.amsgrad else None
+        if p.is_cuda:
+            lr_step = self.lr * math.sqrt(1 - b2 ** t) / (1 - b1 ** t)
+            ops.adam_flat(p, self.exp_avg[sl], self.exp_avg_sq[sl], vmax, grad, lr_step, b1, b2,
+                          self.eps, self.weight_decay, grad_scale, self.amsgrad)
+            return
+        g = grad.to(torch.float32) * grad_scale
+        oracle.adam_apply(p, self.exp_avg[sl], self.exp_avg_sq[sl],
+                          vmax if vmax is not None else torch.empty(0), g, self.lr, b1, b2,
+                          self.eps, self.weight_decay, t, self.amsgrad)
+
+    def step(self, grad=None, grad_scale=1.0):
+        self.step_range(0, self.flat.numel, self.flat.grad if grad is None else grad, grad_scale)
+        self.end_step()
+
+    def end_step(self):
+        self.steps += 1
+
+    def state_dict(self):
+        return {"kind": "adam", "exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq,
+                "max_exp_avg_sq": self.max_exp_avg_sq, "steps": self.steps, "lr": self.lr}
+
+    def load_state_dict(self, sd):
+        self.exp_avg.copy_(sd["exp_avg"])
+        self.exp_avg_sq.copy_(sd["exp_avg_sq"])
+        if self.amsgrad and sd.get("max_exp_avg_sq") is not None:
+            self.max_exp_avg_sq.copy_(sd["max_exp_avg_sq"])
+        self.steps = int(sd["steps"])
+        self.lr = sd.get("lr", self.lr)
+
+
+def make_optimizer(name, flat, **kw):
+    name = name.lower()
+    if name == "sgd":
+        return FlatSGD(flat, **{k: v for k, v in kw.items()
+                                if k in ("lr", "momentum", "dampening", "weight_decay",
+                                         "nesterov")})
+    if name in ("adam", "amsgrad"):
+        return FlatAdam(flat, lr=kw.get("lr", 1e-3), weight_decay=kw.get("weight_decay", 0.0),
+                        amsgrad=(name == "amsgrad") or kw.get("amsgrad", False))
+    raise ValueError(f"unknown optimizer {name!r}")

@@ -1,0 +1,119 @@
+"""Thin communicator over ``torch.distributed``.
+
+On the GPU the process group is ``nccl``, which on ROCm *is* RCCL: every collective runs on RCCL's
+internal HIP stream over xGMI peer links, ordered after the work already queued on the caller's
+current stream.  On the CPU it is ``gloo`` (tests, ``BASELINE.json`` config #1).  A world of one
+process needs no process group at all: collectives degenerate to local copies.
+
+Parity: replaces the reference's per-layer ``dist.gather`` / ``dist.broadcast`` call sites
+(``distributed_worker.py:256,278,350``, ``sync_replicas_master_nn.py:212,223``) and Horovod's
+``hvd.allreduce`` / ``broadcast_parameters`` (``horvod_pytorch.py:84-87,187-188``).
+"""
+import datetime
+import os
+
+import torch
+import torch.distributed as dist
+
+
+def init_distributed(backend: str = None, timeout_s: float = None, device=None) -> "Comm":
+    """env:// rendezvous (RANK/WORLD_SIZE/MASTER_ADDR/MASTER_PORT as set by torchrun)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1 and not dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        kw = {}
+        if timeout_s:
+            kw["timeout"] = datetime.timedelta(seconds=float(timeout_s))
+        if backend == "nccl" and device is not None:
+            kw["device_id"] = torch.device(device)
+        dist.init_process_group(backend=backend, **kw)
+    return Comm()
+
+
+class Comm:
+    def __init__(self, group=None):
+        self.group = group
+        if dist.is_available() and dist.is_initialized():
+            self.rank = dist.get_rank(group)
+            self.world = dist.get_world_size(group)
+            self.backend = dist.get_backend(group)
+        else:
+            self.rank, self.world, self.backend = 0, 1, "local"
+        self._gloo_ag = self.backend == "gloo"
+
+    @property
+    def distributed(self) -> bool:
+        return self.world > 1
+
+    # -- collectives (return a Work handle or None when already complete) --------------------
+    def all_gather(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = False):
+        """``out`` [world * n] <- concat of every rank's ``inp`` [n]."""
+        if self.world == 1:
+            out[:inp.numel()].copy_(inp)
+            return None
+        if self._gloo_ag:
+            chunks = list(out.view(self.world, -1).unbind(0))
+            return dist.all_gather(chunks, inp, group=self.group, async_op=async_op)
+        return dist.all_gather_into_tensor(out, inp, group=self.group, async_op=async_op)
+
+    def all_reduce(self, t: torch.Tensor, op=dist.ReduceOp.SUM, async_op: bool = False):
+        if self.world == 1:
+            return None
+        return dist.all_reduce(t, op=op, group=self.group, async_op=async_op)
+
+    def broadcast(self, t: torch.Tensor, src: int = 0, async_op: bool = False):
+        if self.world == 1:
+            return None
+        return dist.broadcast(t, src=src, group=self.group, async_op=async_op)
+
+    def gather(self, t: torch.Tensor, out: torch.Tensor = None, dst: int = 0):
+        """Rank ``dst`` receives every rank's ``t`` into ``out`` [world, *t.shape]."""
+        if self.world == 1:
+            out[0].copy_(t)
+            return
+        if self.rank == dst:
+            dist.gather(t, list(out.unbind(0)), dst=dst, group=self.group)
+        else:
+            dist.gather(t, None, dst=dst, group=self.group)
+
+    def all_to_all(self, out: torch.Tensor, inp: torch.Tensor):
+        if self.world == 1:
+            out.copy_(inp)
+            return
+        dist.all_to_all_single(out, inp, group=self.group)
+
+    def barrier(self):
+        if self.world > 1:
+            if self.backend == "nccl":
+                dist.barrier(group=self.group, device_ids=[torch.cuda.current_device()])
+            else:
+                dist.barrier(group=self.group)
+
+    def all_reduce_scalars(self, values, op="sum", device="cpu"):
+        """All-reduce a short list of Python floats (metrics averaging, ``horvod_pytorch.py:84``)."""
+        t = torch.tensor(values, dtype=torch.float64, device=device)
+        if self.world > 1:
+            rop = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX,
+                   "min": dist.ReduceOp.MIN}[op]
+            dist.all_reduce(t, op=rop, group=self.group)
+        return t.tolist()
+
+    def all_gather_object(self, obj):
+        if self.world == 1:
+            return [obj]
+        out = [None] * self.world
+        dist.all_gather_object(out, obj, group=self.group)
+        return out
+
+    def broadcast_object(self, obj, src=0):
+        if self.world == 1:
+            return obj
+        lst = [obj]
+        dist.broadcast_object_list(lst, src=src, group=self.group)
+        return lst[0]
+
+
+def shutdown():
+    if dist.is_available() and dist.is_initialized():
+        dist.destroy_process_group()

@@ -1,0 +1,243 @@
+"""Gradient exchange engine: buckets, comm/backward overlap, fused apply.
+
+Per step (``begin`` -> ``loss.backward()`` -> ``finish``):
+
+1. As autograd finishes accumulating the last gradient of a bucket, a post-accumulate hook
+   records an event on the compute stream and, on a side HIP stream that waits on it, runs the
+   codec's encode kernels and issues the bucket's collective (RCCL all-gather of the packed
+   payloads, or all-reduce for dense codecs).  Backward of the earlier layers keeps running on the
+   compute stream meanwhile -- the overlap that the reference only prototyped with per-layer MPI
+   ``Isend`` in ``LeNetSplit.backward_normal`` (``model_ops/lenet.py:111-186``).
+2. ``finish`` makes the compute stream wait for every collective, then per bucket runs ONE fused
+   kernel: decode all N payloads in rank order -> scale 1/N -> SGD update of that bucket's
+   parameters (``Codec.decode_apply_sgd``).  Dense codecs get one flat SGD kernel.
+
+Every rank decodes the same bytes in the same order, so replicas stay bitwise identical without
+re-broadcasting weights.  That is the all-to-all counterpart of the reference's star
+(``sync_replicas_master_nn.py:158-232``: gather -> sum -> /(N-1) -> broadcast) with no idle server.
+"""
+import contextlib
+import time
+
+import torch
+
+from .. import ops
+
+
+class StepStats:
+    __slots__ = ("payload_bytes", "wire_bytes_sent", "wire_bytes_recv", "dense_bytes",
+                 "collectives")
+
+    def __init__(self):
+        self.payload_bytes = 0
+        self.wire_bytes_sent = 0
+        self.wire_bytes_recv = 0
+        self.dense_bytes = 0
+        self.collectives = 0
+
+
+class GradientExchange:
+    """All-to-all exchange: all-reduce for dense codecs, all-gather of payloads otherwise."""
+
+    def __init__(self, flat, comm, codec, optimizer, overlap: bool = True,
+                 error_feedback: bool = False, predivide: float = 1.0, seed_offset: int = 0):
+        self.flat, self.comm, self.codec, self.opt = flat, comm, codec, optimizer
+        self.device = flat.data.device
+        self.cuda = self.device.type == "cuda"
+        self.codec.bind([b.plan for b in flat.buckets], self.device)
+        self.nb = len(flat.buckets)
+        self.N = comm.world
+        self.predivide = predivide
+        self.seed_offset = seed_offset
+        self.payload, self.recv, self.send = [], [], []
+        for b in flat.buckets:
+            if codec.allreduce:
+                self.payload.append(None)
+                self.recv.append(None)
+                self.send.append(None if codec.wire_dtype == torch.float32 else torch.zeros(
+                    b.length, dtype=codec.wire_dtype, device=self.device))
+            else:
+                P = codec.payload_bytes(b.index)
+                self.payload.append(torch.zeros(P, dtype=torch.uint8, device=self.device))
+                self.recv.append(torch.zeros(self.N * P, dtype=torch.uint8, device=self.device))
+                self.send.append(None)
+        self.resid = torch.zeros_like(flat.grad) if (error_feedback and not codec.allreduce) else None
+        self.overlap = overlap
+        self.side = torch.cuda.Stream(device=self.device) if (self.cuda and overlap) else None
+        self._bucket_of = flat.bucket_of()
+        self._sizes = [len(b.params) for b in flat.buckets]
+        self._count = [0] * self.nb
+        self._launched = [False] * self.nb
+        self._works = [None] * self.nb
+        self._active = False
+        self.step_idx = 0
+        self._hooks = []
+        if overlap:
+            for p in flat.params:
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+        self.last = StepStats()
+
+    # -- accounting ---------------------------------------------------------------------------
+    def bytes_per_step(self) -> StepStats:
+        """Algorithmic bytes of one exchange (what RCCL moves per rank, ring/direct algorithms)."""
+        s = StepStats()
+        N = self.N
+        for b in self.flat.buckets:
+            P = self.codec.payload_bytes(b.index)
+            s.payload_bytes += P
+            s.dense_bytes += self.codec.dense_bytes(b.index)
+            if N > 1:
+                if self.codec.allreduce:
+                    s.wire_bytes_sent += 2 * (N - 1) * P // N
+                    s.wire_bytes_recv += 2 * (N - 1) * P // N
+                else:
+                    s.wire_bytes_sent += (N - 1) * P
+                    s.wire_bytes_recv += (N - 1) * P
+                s.collectives += 1
+        return s
+
+    # -- step protocol ------------------------------------------------------------------------
+    def begin(self):
+        """Call before ``loss.backward()``; gradients must be zero (``flat.zero_grad()``)."""
+        self._count = [0] * self.nb
+        self._launched = [False] * self.nb
+        self._works = [None] * self.nb
+        self._active = True
+
+    def _on_grad(self, p):
+        if not self._active:
+            return
+        b = self._bucket_of[id(p)]
+        self._count[b] += 1
+        if self._count[b] == self._sizes[b] and not self._launched[b]:
+            self._launch(b)
+
+    def _stream_ctx(self):
+        if self.side is None:
+            return contextlib.nullcontext()
+        ev = torch.cuda.Event()
+        ev.record()
+        self.side.wait_event(ev)
+        return torch.cuda.stream(self.side)
+
+    def _launch(self, bi: int):
+        self._launched[bi] = True
+        b = self.flat.buckets[bi]
+        g = self.flat.grad_view(b)
+        with self._stream_ctx():
+            if self.codec.allreduce:
+                if self.send[bi] is None:
+                    if self.predivide != 1.0:
+                        g.mul_(1.0 / self.predivide)
+                    work = self.comm.all_reduce(g, async_op=True)
+                else:
+                    if self.cuda:
+                        ops.cast_scale(g, self.send[bi], 1.0 / self.predivide)
+                    else:
+                        self.send[bi].copy_(g * (1.0 / self.predivide))
+                    work = self.comm.all_reduce(self.send[bi], async_op=True)
+            else:
+                resid = None if self.resid is None else self.resid[b.start:b.start + b.length]
+                self.codec.encode(bi, g, self.payload[bi], self.step_idx + self.seed_offset,
+                                  self.comm.rank, resid)
+                work = self.comm.all_gather(self.recv[bi], self.payload[bi], async_op=True)
+        self._works[bi] = work
+
+    def finish(self, apply: bool = True):
+        """Complete every bucket's exchange and (by default) apply the optimizer step."""
+        for bi in range(self.nb):
+            if not self._launched[bi]:
+                self._launch(bi)
+        for w in self._works:
+            if w is not None:
+                w.wait()
+        if self.side is not None:
+            torch.cuda.current_stream().wait_stream(self.side)
+        self._active = False
+        if apply:
+            self.apply()
+        self.last = self.bytes_per_step()
+        self.step_idx += 1
+
+    def apply(self):
+        scale = self.predivide / self.N
+        opt = self.opt
+        if self.codec.allreduce:
+            if self.codec.wire_dtype == torch.float32:
+                opt.step_range(0, self.flat.numel, self.flat.grad, scale)
+            else:
+                for b in self.flat.buckets:
+                    opt.step_range(b.start, b.length, self.send[b.index], scale)
+        else:
+            for b in self.flat.buckets:
+                recv = self.recv[b.index].view(self.N, -1)
+                if getattr(opt, "fusable", False):
+                    self.codec.decode_apply_sgd(b.index, recv, scale, self.flat.data_view(b),
+                                                opt.mom[b.start:b.start + b.length],
+                                                opt.hparams(), opt.first)
+                else:
+                    gv = self.flat.grad_view(b)
+                    self.codec.decode(b.index, recv, gv, scale)
+                    opt.step_range(b.start, b.length, gv, 1.0)
+        opt.end_step()
+
+    def decode_average(self):
+        """Write the averaged exchanged gradient into ``flat.grad`` (no optimizer step)."""
+        scale = self.predivide / self.N
+        if self.codec.allreduce:
+            if self.codec.wire_dtype == torch.float32:
+                self.flat.grad.mul_(scale)
+            else:
+                for b in self.flat.buckets:
+                    self.flat.grad_view(b).copy_(self.send[b.index].float() * scale)
+            return
+        for b in self.flat.buckets:
+            self.codec.decode(b.index, self.recv[b.index].view(self.N, -1),
+                              self.flat.grad_view(b), scale)
+
+    def close(self):
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+
+
+def sync_params(flat, comm, src: int = 0):
+    """Broadcast the flat parameters from ``src`` (fixes the reference's independent random init,
+    SURVEY Appendix B #1; Horovod's ``broadcast_parameters``, ``horvod_pytorch.py:187``)."""
+    comm.broadcast(flat.data, src=src)
+
+
+def sync_buffers(model, comm, src: int = 0):
+    for buf in model.buffers():
+        if buf.dtype.is_floating_point or buf.dtype in (torch.int64, torch.int32):
+            comm.broadcast(buf.data, src=src)
+
+
+class Stopwatch:
+    """HIP-event (GPU) or wall-clock (CPU) phase timer."""
+
+    def __init__(self, cuda: bool):
+        self.cuda = cuda
+        self.marks = []
+
+    def mark(self, name: str):
+        if self.cuda:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            self.marks.append((name, e))
+        else:
+            self.marks.append((name, time.perf_counter()))
+
+    def phases(self):
+        """{phase: ms} between consecutive marks (synchronises on GPU)."""
+        out = {}
+        if len(self.marks) < 2:
+            return out
+        if self.cuda:
+            self.marks[-1][1].synchronize()
+        for (n0, a), (n1, b) in zip(self.marks, self.marks[1:]):
+            out[n1] = a.elapsed_time(b) if self.cuda else (b - a) * 1e3
+        return out
+
+    def reset(self):
+        self.marks = []

@@ -1,0 +1,117 @@
+"""Flat, bucketed parameter and gradient storage.
+
+All trainable parameters become views of ONE contiguous fp32 buffer and their ``.grad`` views of a
+second one, laid out in *reverse* registration order (the order backward produces gradients) with
+every tensor 64-element (256 B) aligned.  Consequences:
+
+* autograd accumulates straight into the flat gradient buffer (``AccumulateGrad`` adds in place
+  into an existing ``.grad``), so a bucket is a contiguous range ready for a collective with no
+  copy -- what Horovod's fusion buffer (``--fusion-threshold-mb 32``, ``Horovod all reduce.ipynb``)
+  emulates by copying;
+* the optimizer is one multi-tensor kernel over the buffer instead of the reference's per-tensor
+  loop (``optim/sgd.py:75``);
+* a checkpoint/broadcast of the model is one tensor.
+
+Parity: the per-layer gather buffers of ``sync_replicas_master_nn.py:49-86`` (GradientAccumulator)
+and ``distributed_worker.py:41-59`` (ModelBuffer) are replaced by these views.
+"""
+from dataclasses import dataclass
+from typing import List
+
+import torch
+
+from ..compress.plan import BucketPlan
+
+ALIGN = 64
+
+
+def _align(n, a=ALIGN):
+    return (n + a - 1) // a * a
+
+
+@dataclass
+class Bucket:
+    index: int
+    start: int  # element offset in the flat buffer
+    length: int
+    params: List[torch.nn.Parameter]
+    plan: BucketPlan
+
+
+class FlatModel:
+    def __init__(self, model, bucket_bytes: int = 8 << 20, reverse: bool = True):
+        """``model``: an ``nn.Module`` or an iterable of parameters."""
+        seen = set()
+        params = []
+        plist = model.parameters() if isinstance(model, torch.nn.Module) else model
+        if not isinstance(model, torch.nn.Module):
+            model = None
+        for p in plist:
+            if p.requires_grad and id(p) not in seen:
+                seen.add(id(p))
+                params.append(p)
+        if reverse:
+            params = params[::-1]
+        self.model = model
+        self.params = params
+        dev = params[0].device
+        offs = []
+        total = 0
+        for p in params:
+            offs.append(total)
+            total += _align(p.numel())
+        self.offsets = offs
+        self.numel = total
+        self.param_numel = sum(p.numel() for p in params)
+        self.data = torch.zeros(total, dtype=torch.float32, device=dev)
+        self.grad = torch.zeros(total, dtype=torch.float32, device=dev)
+        for p, o in zip(params, offs):
+            if p.dtype != torch.float32:
+                raise TypeError("flat buffers hold fp32 master weights; keep params fp32 "
+                                "(compute in bf16 via autocast)")
+            n = p.numel()
+            dv = self.data[o:o + n].as_strided(p.shape, p.stride())
+            dv.copy_(p.data)
+            p.data = dv
+            p.grad = self.grad[o:o + n].as_strided(p.shape, p.stride())
+        self.buckets = self._make_buckets(bucket_bytes)
+
+    def _make_buckets(self, bucket_bytes):
+        cap = max(1, bucket_bytes // 4)
+        groups, cur = [], []
+        for i, p in enumerate(self.params):
+            cur.append(i)
+            end = self.offsets[i] + _align(p.numel())
+            if end - self.offsets[cur[0]] >= cap:
+                groups.append(cur)
+                cur = []
+        if cur:
+            groups.append(cur)
+        buckets = []
+        for bi, g in enumerate(groups):
+            start = self.offsets[g[0]]
+            end = self.offsets[g[-1]] + _align(self.params[g[-1]].numel())
+            plan = BucketPlan(numels=[self.params[i].numel() for i in g],
+                              offsets=[self.offsets[i] - start for i in g],
+                              ratio=1.0, bucket_offset=start, length=end - start)
+            buckets.append(Bucket(bi, start, end - start, [self.params[i] for i in g], plan))
+        return buckets
+
+    def bucket_of(self):
+        """param id -> bucket index."""
+        return {id(p): b.index for b in self.buckets for p in b.params}
+
+    def grad_view(self, b: Bucket) -> torch.Tensor:
+        return self.grad[b.start:b.start + b.length]
+
+    def data_view(self, b: Bucket) -> torch.Tensor:
+        return self.data[b.start:b.start + b.length]
+
+    def zero_grad(self):
+        self.grad.zero_()
+
+    def reattach_grads(self):
+        """Restore the ``.grad`` views (e.g. after user code set them to None)."""
+        for p, o in zip(self.params, self.offsets):
+            if p.grad is None or p.grad.data_ptr() != self.grad[o:o + 1].data_ptr():
+                p.grad = self.grad[o:o + p.numel()].as_strided(p.shape, p.stride())

@@ -1,0 +1,126 @@
+"""Parameter-server topology: rank 0 is the server, ranks 1..N-1 are workers.
+
+Reproduces the reference's star (``sync_replicas_master_nn.py`` + ``distributed_worker.py``) for
+every method, with the codecs applied for real:
+
+* push: each worker encodes its gradient (push codec) and ``gather``s it to rank 0
+  (``distributed_worker.py:317-351`` / ``sync_replicas_master_nn.py:218-232``);
+* the server decodes the N-1 worker payloads (its own slot is a dummy, as in the reference's
+  ``aggregate_gradient`` summing ``gradient[1:]``, ``:215-216``) and averages them (``:187-190``);
+* pull ``grad`` (Methods 3-5): the server encodes the *averaged* gradient with the pull codec and
+  broadcasts it (``:193-212``); every process decodes it and applies the same SGD step, so the
+  server's replica tracks the workers' (the server's replica is what gets checkpointed);
+* pull ``weights`` (Methods 1-2): the server steps its optimizer with the averaged gradient and
+  broadcasts the flat weights (the reference's intended ``_bcast_weight``, which at HEAD
+  broadcasts the wrong buffer -- SURVEY Appendix B #14).
+
+Collectives are per bucket: one gather + one broadcast per bucket instead of 2 x #tensors
+blocking Gloo round trips per step.  The server runs no forward/backward.
+"""
+import torch
+
+from .engine import StepStats
+
+
+class PSExchange:
+    server_rank = 0
+
+    def __init__(self, flat, comm, push_codec, pull_codec, optimizer, pull: str = "grad"):
+        if comm.world < 2:
+            raise ValueError("the ps topology needs at least 2 processes (1 server + workers)")
+        self.flat, self.comm, self.opt, self.pull = flat, comm, optimizer, pull
+        self.device = flat.data.device
+        self.push = push_codec.bind([b.plan for b in flat.buckets], self.device)
+        self.pullc = pull_codec.bind([b.plan for b in flat.buckets], self.device)
+        self.N = comm.world
+        self.is_server = comm.rank == self.server_rank
+        self.nb = len(flat.buckets)
+        self.step_idx = 0
+        self.payload, self.gathered, self.pull_buf = [], [], []
+        for b in flat.buckets:
+            P = self._nbytes(self.push, b)
+            self.payload.append(torch.zeros(P, dtype=torch.uint8, device=self.device))
+            self.gathered.append(torch.zeros((self.N, P), dtype=torch.uint8, device=self.device)
+                                 if self.is_server else None)
+            Q = self._nbytes(self.pullc, b)
+            self.pull_buf.append(torch.zeros((1, Q), dtype=torch.uint8, device=self.device))
+        self.avg = torch.zeros_like(flat.grad)
+        self.last = StepStats()
+
+    @staticmethod
+    def _nbytes(codec, b):
+        if codec.allreduce:  # dense payload = raw gradient bytes in the codec's wire dtype
+            return b.length * codec.wire_dtype.itemsize
+        return codec.payload_bytes(b.index)
+
+    # dense codecs ship the gradient bytes themselves
+    def _encode(self, codec, bi, src, out, rank):
+        if codec.allreduce:
+            out.view(codec.wire_dtype).copy_(src.to(codec.wire_dtype))
+        else:
+            codec.encode(bi, src, out, self.step_idx, rank)
+
+    def _decode(self, codec, bi, recv, out, scale):
+        if codec.allreduce:
+            n = recv.shape[0]
+            vals = recv.view(codec.wire_dtype).view(n, -1).to(torch.float32)
+            out.copy_(vals.sum(0) * scale)
+        else:
+            codec.decode(bi, recv, out, scale)
+
+    def begin(self):
+        pass
+
+    def finish(self):
+        W = self.N - 1
+        rank = self.comm.rank
+        for b in self.flat.buckets:
+            bi = b.index
+            g = self.flat.grad_view(b)
+            if not self.is_server:
+                self._encode(self.push, bi, g, self.payload[bi], rank)
+            self.comm.gather(self.payload[bi], self.gathered[bi], dst=self.server_rank)
+            av = self.avg[b.start:b.start + b.length]
+            if self.is_server:
+                self._decode(self.push, bi, self.gathered[bi][1:], av, 1.0 / W)
+            if self.pull == "grad":
+                if self.is_server:
+                    self._encode(self.pullc, bi, av, self.pull_buf[bi][0], rank)
+                self.comm.broadcast(self.pull_buf[bi], src=self.server_rank)
+                self._decode(self.pullc, bi, self.pull_buf[bi], av, 1.0)
+        if self.pull == "grad":
+            self.opt.step(grad=self.avg)
+        else:
+            if self.is_server:
+                self.opt.step(grad=self.avg)
+            else:
+                self.opt.end_step()
+            self.comm.broadcast(self.flat.data, src=self.server_rank)
+        self.last = self.bytes_per_step()
+        self.step_idx += 1
+
+    def bytes_per_step(self):
+        s = StepStats()
+        for b in self.flat.buckets:
+            push = self._nbytes(self.push, b)
+            pull = self.flat.numel * 4 // self.nb if self.pull == "weights" else \
+                self._nbytes(self.pullc, b)
+            if self.pull == "weights":
+                pull = b.length * 4
+            s.payload_bytes += push
+            s.dense_bytes += b.plan.numel * 4
+            if self.is_server:
+                s.wire_bytes_recv += push * (self.N - 1)
+                s.wire_bytes_sent += pull * (self.N - 1)
+            else:
+                s.wire_bytes_sent += push
+                s.wire_bytes_recv += pull
+            s.collectives += 2
+        return s
+
+    def pull_bytes(self):
+        return sum(b.length * 4 if self.pull == "weights" else self._nbytes(self.pullc, b)
+                   for b in self.flat.buckets)
+
+    def close(self):
+        pass

@@ -1,0 +1,4 @@
+"""Roles and drivers: the trainer (workers / PS server) and the standalone evaluator."""
+from .trainer import FaultInjected, Trainer, resolve_device, run
+
+__all__ = ["Trainer", "run", "resolve_device", "FaultInjected"]

@@ -1,0 +1,299 @@
+"""Training driver: one process per GPU, every rank a worker (or rank 0 a server with
+``--topology ps``).
+
+Parity: the roles of ``distributed_nn.py:123-146`` (rank dispatch), ``DistributedWorker.train_updated``
+(``distributed_worker.py:162-239``: forward, backward, send grads, fetch grads, SGD step, accuracy,
+log, periodic ``model_step_`` save) and ``SyncReplicasMaster_NN.start_updated``
+(``sync_replicas_master_nn.py:158-177``).  Fixed defects: replicas start from rank 0's weights,
+data is sharded with equal step counts on every rank, the loop ends on ``--max-steps`` *or*
+``--epochs`` identically everywhere (no deadlock), only rank 0 checkpoints.
+"""
+import contextlib
+import math
+import os
+import time
+
+import torch
+import torch.nn.functional as F
+
+from ..compress.codecs import make_codec
+from ..config import Config
+from ..data import DeviceLoader, load_dataset
+from ..models import build_model, canonical_name, input_shape
+from ..optim.flat import make_optimizer
+from ..parallel.comm import Comm, init_distributed
+from ..parallel.engine import GradientExchange, Stopwatch, sync_buffers, sync_params
+from ..parallel.flat import FlatModel
+from ..parallel.local_sgd import LocalSGDExchange
+from ..parallel.ps import PSExchange
+from ..utils import checkpoint as ckpt
+from ..utils.metrics import MetricsLogger, accuracy, byte_summary
+
+
+def resolve_device(cfg: Config) -> torch.device:
+    want = cfg.device
+    if cfg.no_cuda:
+        want = "cpu"
+    if want == "auto":
+        want = "cuda" if torch.cuda.is_available() else "cpu"
+    if want == "cuda":
+        local = int(os.environ.get("LOCAL_RANK", cfg.local_rank or 0))
+        torch.cuda.set_device(local)
+        return torch.device("cuda", local)
+    return torch.device("cpu")
+
+
+class FaultInjected(RuntimeError):
+    pass
+
+
+class Trainer:
+    def __init__(self, cfg: Config, comm: Comm = None):
+        self.cfg = cfg = cfg.resolved()
+        self.device = resolve_device(cfg)
+        self.comm = comm or init_distributed(timeout_s=cfg.comm_timeout,
+                                             device=self.device if self.device.type == "cuda"
+                                             else None)
+        self.rank, self.world = self.comm.rank, self.comm.world
+        self.cuda = self.device.type == "cuda"
+        torch.manual_seed(cfg.seed)
+        if self.cuda:
+            torch.backends.cudnn.benchmark = True
+        self.log = MetricsLogger(cfg.metrics_file, self.rank, cfg.quiet)
+        self.is_server = cfg.topology == "ps" and self.rank == 0
+
+        # data -------------------------------------------------------------------------------
+        net = canonical_name(cfg.network)
+        x, y, info = load_dataset(cfg.dataset, cfg.data_dir, train=True,
+                                  synthetic_size=cfg.synthetic_size, seed=cfg.seed,
+                                  device=self.device)
+        if tuple(info["shape"]) != tuple(input_shape(net)):
+            raise ValueError(f"{cfg.network} expects inputs {input_shape(net)}, dataset "
+                             f"{cfg.dataset} has {info['shape']}")
+        self.info = info
+        n_workers = self.world - 1 if cfg.topology == "ps" else self.world
+        w_rank = self.rank - 1 if cfg.topology == "ps" else self.rank
+        self.loader = None
+        if not self.is_server:
+            self.loader = DeviceLoader(x, y, info, cfg.batch_size, rank=w_rank,
+                                       world=n_workers, shuffle=True,
+                                       augment=cfg.augment and info["shape"][0] == 3,
+                                       seed=cfg.seed, device=self.device,
+                                       channels_last=cfg.channels_last)
+        tx, ty, _ = load_dataset(cfg.dataset, cfg.data_dir, train=False,
+                                 synthetic_size=(cfg.synthetic_size // 5) if cfg.synthetic_size else 0,
+                                 seed=cfg.seed, device=self.device)
+        self.test_loader = DeviceLoader(tx, ty, info, min(cfg.test_batch_size, tx.shape[0]),
+                                        shuffle=False, augment=False, seed=cfg.seed,
+                                        device=self.device, channels_last=cfg.channels_last,
+                                        drop_last=False)
+
+        # model / flat buffers / optimizer ------------------------------------------------------
+        model = build_model(net, info["classes"]).to(self.device)
+        if cfg.channels_last:
+            model = model.to(memory_format=torch.channels_last)
+        self.model = model
+        self.flat = FlatModel(model, bucket_bytes=int(cfg.bucket_mb * (1 << 20)))
+        sync_params(self.flat, self.comm)
+        sync_buffers(model, self.comm)
+        lr = cfg.lr * (n_workers if cfg.lr_scale_world else 1)
+        self.opt = make_optimizer(cfg.optimizer, self.flat, lr=lr, momentum=cfg.momentum,
+                                  dampening=cfg.dampening, weight_decay=cfg.weight_decay,
+                                  nesterov=cfg.nesterov)
+
+        # exchange ---------------------------------------------------------------------------------
+        ckw = dict(ratio=cfg.topk_ratio, levels=cfg.qsgd_levels, bits=cfg.qsgd_bits,
+                   norm=cfg.qsgd_norm, seed=cfg.seed)
+        if cfg.topology == "ps":
+            self.exchange = PSExchange(self.flat, self.comm, make_codec(cfg.compress, **ckw),
+                                       make_codec(cfg.pull_compress or cfg.compress, **ckw),
+                                       self.opt, pull=cfg.pull)
+        else:
+            self.exchange = GradientExchange(self.flat, self.comm,
+                                             make_codec(cfg.compress, **ckw), self.opt,
+                                             overlap=cfg.overlap,
+                                             error_feedback=cfg.error_feedback,
+                                             predivide=cfg.predivide)
+            if cfg.sync_every > 1 or cfg.select_best:
+                self.exchange = LocalSGDExchange(self.exchange, cfg.sync_every, cfg.sync_mode,
+                                                 cfg.select_best, score_fn=self._holdout_score)
+        self.amp_dtype = {"bf16": torch.bfloat16, "fp16": torch.float16}.get(cfg.amp)
+        self.step = 0
+        self.epoch = 0
+        self.fault = None
+        if cfg.inject_fault:
+            r, s = cfg.inject_fault.split(":")
+            self.fault = (int(r), int(s))
+        if cfg.resume:
+            self._resume()
+
+    # --------------------------------------------------------------------------------------------
+    def autocast(self):
+        if self.amp_dtype is None:
+            return contextlib.nullcontext()
+        return torch.autocast(device_type=self.device.type, dtype=self.amp_dtype,
+                              enabled=self.cuda or self.amp_dtype == torch.bfloat16)
+
+    def forward_backward(self, x, y):
+        self.flat.zero_grad()
+        self.exchange.begin()
+        with self.autocast():
+            out = self.model(x)
+        loss = F.cross_entropy(out.float(), y)
+        loss.backward()
+        return loss, out
+
+    def train_step(self, x=None, y=None):
+        """One synchronous step.  Returns (loss tensor, logits) (server: (None, None))."""
+        if self.fault is not None and self.fault == (self.rank, self.step):
+            raise FaultInjected(f"injected fault on rank {self.rank} at step {self.step}")
+        if self.is_server:
+            self.model.train()
+            self.exchange.finish()
+            self.step += 1
+            return None, None
+        if x is None:
+            x, y = self.loader.next()
+        self.model.train()
+        loss, out = self.forward_backward(x, y)
+        self.exchange.finish()
+        self.step += 1
+        return loss, (out, y)
+
+    @torch.no_grad()
+    def evaluate(self, max_batches=None):
+        """Test loss / top-1 / top-5 of this rank's replica (the reference evaluator's output,
+        with a correct cross-entropy instead of NLL on raw logits)."""
+        self.model.eval()
+        n = 0
+        loss = torch.zeros((), device=self.device, dtype=torch.float64)
+        c1 = torch.zeros((), device=self.device, dtype=torch.float64)
+        c5 = torch.zeros((), device=self.device, dtype=torch.float64)
+        self.test_loader.set_epoch(0)
+        for i, (x, y) in enumerate(self.test_loader):
+            if max_batches is not None and i >= max_batches:
+                break
+            with self.autocast():
+                out = self.model(x)
+            out = out.float()
+            loss += F.cross_entropy(out, y, reduction="sum")
+            a1, a5 = accuracy(out, y, (1, 5))
+            c1 += a1 * y.shape[0] / 100.0
+            c5 += a5 * y.shape[0] / 100.0
+            n += y.shape[0]
+        self.model.train()
+        n = max(n, 1)
+        return {"test_loss": float(loss) / n, "top1": 100.0 * float(c1) / n,
+                "top5": 100.0 * float(c5) / n, "samples": n}
+
+    def _holdout_score(self):
+        return self.evaluate(max_batches=1)["top1"]
+
+    # --------------------------------------------------------------------------------------------
+    def state_extra(self):
+        ex = self.exchange
+        inner = getattr(ex, "inner", ex)
+        extra = {"config": {k: v for k, v in vars(self.cfg).items()
+                            if isinstance(v, (int, float, str, bool)) or v is None},
+                 "world": self.world}
+        if getattr(inner, "resid", None) is not None:
+            extra["ef_residual"] = inner.resid
+        return extra
+
+    def save_checkpoint(self):
+        if self.rank != 0:
+            return None
+        return ckpt.save(self.cfg.ckpt_dir, self.step, self.model, self.opt, self.epoch,
+                         extra=self.state_extra(),
+                         legacy_dir=self.cfg.train_dir if self.cfg.legacy_ckpt else None)
+
+    def _resume(self):
+        path = ckpt.latest(self.cfg.ckpt_dir)
+        path = self.comm.broadcast_object(path, src=0)
+        if not path:
+            self.log.info("resume: no checkpoint found, starting fresh")
+            return
+        st = ckpt.load(path)
+        self.model.load_state_dict(st["model"])
+        # the params are views of the flat buffer; load_state_dict copies in place
+        self.opt.load_state_dict({k: (v.to(self.device) if torch.is_tensor(v) else v)
+                                  for k, v in st["optimizer"].items()})
+        self.step = int(st["step"])
+        self.epoch = int(st["epoch"])
+        inner = getattr(self.exchange, "inner", self.exchange)
+        r = st["extra"].get("ef_residual")
+        if r is not None and getattr(inner, "resid", None) is not None:
+            inner.resid.copy_(r.to(self.device))
+        if hasattr(self.exchange, "step_idx"):
+            self.exchange.step_idx = self.step
+        if self.loader is not None:
+            self.loader.set_epoch(self.epoch)
+            self.loader._pos = self.step % len(self.loader)
+        self.log.info(f"resumed from {path} at step {self.step}")
+
+    # --------------------------------------------------------------------------------------------
+    def fit(self):
+        cfg = self.cfg
+        total = cfg.max_steps  # the ps server has no loader: the min over ranks decides
+        if self.loader is not None:
+            total = min(cfg.max_steps, cfg.epochs * len(self.loader))
+        total = int(self.comm.all_reduce_scalars([total], op="min")[0])
+        sw = Stopwatch(self.cuda)
+        t_start = time.time()
+        summary = None
+        prof = None
+        if cfg.profile and self.rank == 0:
+            prof = torch.profiler.profile(
+                activities=[torch.profiler.ProfilerActivity.CPU] +
+                ([torch.profiler.ProfilerActivity.CUDA] if self.cuda else []))
+            prof.__enter__()
+        while self.step < total:
+            if self.loader is not None:
+                self.epoch = self.loader.epoch
+            sw.reset()
+            sw.mark("start")
+            loss, outy = self.train_step()
+            sw.mark("step")
+            if prof is not None and self.step == cfg.profile:
+                prof.__exit__(None, None, None)
+                prof.export_chrome_trace(os.path.join(cfg.train_dir, "trace.json"))
+                prof = None
+            if self.step % cfg.log_interval == 0 or self.step == total:
+                rec = {"step": self.step, "epoch": self.epoch, "rank": self.rank,
+                       "time_s": time.time() - t_start}
+                if loss is not None:
+                    out, y = outy
+                    a1, a5 = accuracy(out.float(), y, (1, 5))
+                    rec.update(loss=float(loss), acc1=float(a1), acc5=float(a5))
+                rec["step_ms"] = sw.phases().get("step")
+                rec.update(byte_summary(self.exchange.last, self.world))
+                rec["images_per_sec_rank"] = (cfg.batch_size * 1e3 / rec["step_ms"]
+                                              if rec["step_ms"] else None)
+                self.log.record(rec)
+                if loss is not None:
+                    self.log.info(
+                        f"Worker {self.rank} Step {self.step}/{total} loss {rec['loss']:.4f} "
+                        f"acc@1 {rec['acc1']:.1f} acc@5 {rec['acc5']:.1f} "
+                        f"payload {rec['payload_bytes_per_rank'] / 1024:.1f} KiB "
+                        f"(x{(rec['compression_ratio'] or 0):.0f}) step {rec['step_ms'] or 0:.2f} ms")
+                summary = rec
+            if cfg.eval_freq and self.step % cfg.eval_freq == 0:
+                if cfg.sync_bn:
+                    sync_buffers(self.model, self.comm, src=0 if not self.is_server else 0)
+                self.save_checkpoint()
+                if cfg.eval_on_ckpt and self.rank == (1 if cfg.topology == "ps" else 0):
+                    ev = self.evaluate()
+                    self.log.info(f"Test step {self.step}: loss {ev['test_loss']:.4f} "
+                                  f"top1 {ev['top1']:.2f}% top5 {ev['top5']:.2f}%")
+                    self.log.record({"step": self.step, "eval": ev})
+        self.comm.barrier()
+        wall = time.time() - t_start
+        self.log.info(f"total time {wall:.1f}s for {total} steps")
+        self.exchange.close()
+        self.log.close()
+        return {"steps": total, "wall_s": wall, "last": summary}
+
+
+def run(cfg: Config):
+    tr = Trainer(cfg)
+    return tr.fit()

@@ -1,0 +1,240 @@
+"""HIP kernels vs the torch oracle (compress/oracle.py), on one MI355X.
+
+Exactness contract: top-k selection, int8/int4/fp32 payload bytes and decoded sums are bitwise
+equal to the oracle (max-norm scales are exact; the kernels are built with -ffp-contract=off).
+L2-norm scales and the optimizer updates are compared with tight tolerances.
+"""
+import pytest
+import torch
+
+from ewdml import ops
+from ewdml.compress import oracle
+from ewdml.compress.plan import BucketPlan, Layout
+from ewdml.compress.rng import stream_key
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _plan(numels, ratio, bucket_offset=0):
+    offs, o = [], 0
+    for n in numels:
+        offs.append(o)
+        o += (n + 63) // 64 * 64
+    return BucketPlan(numels, offs, ratio, bucket_offset, o)
+
+
+def _grad(plan, seed=0, ties=False):
+    g = torch.zeros(plan.length)
+    gen = torch.Generator().manual_seed(seed)
+    for off, n in zip(plan.offsets, plan.numels):
+        x = torch.randn(n, generator=gen) * (0.1 + torch.rand(1, generator=gen))
+        if ties:  # quantised values -> many exact ties at the threshold
+            x = torch.round(x * 4) / 4
+        g[off:off + n] = x
+    return g
+
+
+SHAPES = [
+    [10], [500, 10], [20 * 25, 20, 50 * 500, 50], [8192 * 3 + 5, 7, 64, 100003],
+    [2359296], [1, 2, 3, 4, 5],
+]
+
+
+@pytest.mark.parametrize("numels", SHAPES)
+@pytest.mark.parametrize("ratio", [0.01, 0.4, 1.0])
+@pytest.mark.parametrize("kind,bits", [("topk_qsgd", 8), ("topk_qsgd", 4), ("topk", 8)])
+def test_topk_encode_matches_oracle(numels, ratio, kind, bits):
+    ops.require()
+    plan = _plan(numels, ratio, bucket_offset=4096)
+    lay = Layout.build(kind, plan, bits)
+    levels = 127 if bits == 8 else 7
+    g = _grad(plan, seed=len(numels))
+    key = stream_key(3, 11, 1)
+    ref = oracle.encode_topk(g.clone(), plan, lay, levels, "max", key)
+    dp = ops.DevicePlan(plan, DEV)
+    pay = torch.zeros(lay.nbytes, dtype=torch.uint8, device=DEV)
+    ops.topk_encode(dp, g.to(DEV), pay, lay, levels, "max", key)
+    got = pay.cpu()
+    assert torch.equal(got, ref), f"payload mismatch at {(got != ref).nonzero()[:10].flatten()}"
+
+
+def test_topk_ties_exact_count():
+    ops.require()
+    plan = _plan([8192 * 4 + 17, 333], 0.05)
+    lay = Layout.build("topk_qsgd", plan, 8)
+    g = _grad(plan, seed=5, ties=True)
+    key = stream_key(0, 0, 0)
+    ref = oracle.encode_topk(g.clone(), plan, lay, 127, "max", key)
+    dp = ops.DevicePlan(plan, DEV)
+    pay = torch.zeros(lay.nbytes, dtype=torch.uint8, device=DEV)
+    ops.topk_encode(dp, g.to(DEV), pay, lay, 127, "max", key)
+    assert torch.equal(pay.cpu(), ref)
+
+
+def test_topk_l2_norm_close():
+    ops.require()
+    plan = _plan([100003, 4097], 0.02)
+    lay = Layout.build("topk_qsgd", plan, 8)
+    g = _grad(plan, seed=9)
+    key = stream_key(1, 2, 0)
+    ref = oracle.encode_topk(g.clone(), plan, lay, 127, "l2", key)
+    dp = ops.DevicePlan(plan, DEV)
+    pay = torch.zeros(lay.nbytes, dtype=torch.uint8, device=DEV)
+    ops.topk_encode(dp, g.to(DEV), pay, lay, 127, "l2", key)
+    got = pay.cpu()
+    T = plan.num_tensors
+    s_ref = ref[:4 * T].view(torch.float32)
+    s_got = got[:4 * T].view(torch.float32)
+    torch.testing.assert_close(s_got, s_ref, rtol=1e-5, atol=0)
+    # indices and counts identical; codes may differ by at most 1 where the scale's last bit moved
+    assert torch.equal(got[lay.counts:lay.codes], ref[lay.counts:lay.codes])
+    c_ref = ref[lay.codes:lay.codes + plan.total_k].view(torch.int8).int()
+    c_got = got[lay.codes:lay.codes + plan.total_k].view(torch.int8).int()
+    assert (c_ref - c_got).abs().max() <= 1
+
+
+@pytest.mark.parametrize("kind,bits", [("topk_qsgd", 8), ("topk_qsgd", 4), ("topk", 8)])
+def test_topk_decode_matches_oracle(kind, bits):
+    ops.require()
+    plan = _plan([20 * 25, 20, 8192 * 5 + 3, 50, 70001], 0.03, bucket_offset=128)
+    lay = Layout.build(kind, plan, bits)
+    levels = 127 if bits == 8 else 7
+    N = 5
+    pays = []
+    for r in range(N):
+        g = _grad(plan, seed=100 + r)
+        pays.append(oracle.encode_topk(g, plan, lay, levels, "max", stream_key(0, 4, r)))
+    recv = torch.stack(pays)
+    ref = oracle.decode_sum(recv, plan, lay, levels, 1.0 / N)
+    dp = ops.DevicePlan(plan, DEV)
+    out = torch.full((plan.length,), float("nan"), device=DEV)
+    ops.topk_decode_apply(dp, recv.to(DEV), lay, levels, grad_out=out, grad_scale=1.0 / N)
+    got = out.cpu()
+    for off, n in zip(plan.offsets, plan.numels):
+        assert torch.equal(got[off:off + n], ref[off:off + n])
+
+
+def test_topk_decode_fused_sgd():
+    ops.require()
+    plan = _plan([9000, 64, 33333], 0.05)
+    lay = Layout.build("topk_qsgd", plan, 8)
+    N = 3
+    recv = torch.stack([oracle.encode_topk(_grad(plan, seed=r), plan, lay, 127, "max",
+                                           stream_key(0, 0, r)) for r in range(N)])
+    p0 = torch.randn(plan.length)
+    m0 = torch.randn(plan.length)
+    hp = dict(lr=0.05, momentum=0.9, dampening=0.1, weight_decay=1e-4, nesterov=False)
+    for first in (True, False):
+        p, m = p0.clone(), m0.clone()
+        g = oracle.decode_sum(recv, plan, lay, 127, 1.0 / N)
+        for off, n in zip(plan.offsets, plan.numels):
+            oracle.sgd_apply(p[off:off + n], m[off:off + n], g[off:off + n], first=first, **hp)
+        dp = ops.DevicePlan(plan, DEV)
+        pd, md = p0.to(DEV), m0.to(DEV)
+        ops.topk_decode_apply(dp, recv.to(DEV), lay, 127, param=pd, mom=md,
+                              grad_scale=1.0 / N, first=first, **hp)
+        torch.testing.assert_close(pd.cpu(), p, rtol=1e-6, atol=1e-7)
+        torch.testing.assert_close(md.cpu(), m, rtol=1e-6, atol=1e-7)
+
+
+def test_topk_error_feedback_matches_oracle():
+    ops.require()
+    plan = _plan([40000, 1000], 0.01)
+    lay = Layout.build("topk_qsgd", plan, 8)
+    g = _grad(plan, seed=1)
+    r0 = _grad(plan, seed=2) * 0.1
+    key = stream_key(0, 1, 0)
+    r_ref = r0.clone()
+    ref = oracle.encode_topk(g.clone(), plan, lay, 127, "max", key, residual=r_ref)
+    dp = ops.DevicePlan(plan, DEV)
+    pay = torch.zeros(lay.nbytes, dtype=torch.uint8, device=DEV)
+    r_dev = r0.to(DEV)
+    ops.topk_encode(dp, g.to(DEV), pay, lay, 127, "max", key, resid=r_dev)
+    assert torch.equal(pay.cpu(), ref)
+    for off, n in zip(plan.offsets, plan.numels):
+        assert torch.equal(r_dev.cpu()[off:off + n], r_ref[off:off + n])
+
+
+@pytest.mark.parametrize("bits,norm", [(8, "max"), (4, "max"), (8, "l2")])
+def test_qsgd_dense_roundtrip(bits, norm):
+    ops.require()
+    plan = _plan([8192 * 2 + 13, 10, 5000], 1.0, bucket_offset=64)
+    lay = Layout.build("qsgd", plan, bits)
+    levels = 127 if bits == 8 else 7
+    N = 4
+    dp = ops.DevicePlan(plan, DEV)
+    pays_ref, pays_dev = [], []
+    for r in range(N):
+        g = _grad(plan, seed=20 + r)
+        key = stream_key(7, 3, r)
+        ref = oracle.encode_qsgd(g.clone(), plan, lay, levels, norm, key)
+        pay = torch.zeros(lay.nbytes, dtype=torch.uint8, device=DEV)
+        ops.qsgd_encode(dp, g.to(DEV), pay, lay, levels, norm, key)
+        pays_ref.append(ref)
+        pays_dev.append(pay)
+        if norm == "max":
+            assert torch.equal(pay.cpu(), ref)
+    recv = torch.stack(pays_ref)
+    out = torch.zeros(plan.length, device=DEV)
+    ops.qsgd_decode_apply(dp, recv.to(DEV), lay, levels, grad_out=out, grad_scale=1.0 / N)
+    ref_dec = oracle.decode_sum(recv, plan, lay, levels, 1.0 / N)
+    for off, n in zip(plan.offsets, plan.numels):
+        assert torch.equal(out.cpu()[off:off + n], ref_dec[off:off + n])
+
+
+def test_sgd_and_adam_flat():
+    ops.require()
+    n = 100000
+    p0, m0, g = torch.randn(n), torch.randn(n), torch.randn(n)
+    hp = dict(lr=0.1, momentum=0.9, dampening=0.0, weight_decay=1e-3, nesterov=True)
+    p, m = p0.clone(), m0.clone()
+    oracle.sgd_apply(p, m, g * 0.5, first=False, **hp)
+    pd, md = p0.cuda(), m0.cuda()
+    ops.sgd_flat(pd, md, g.cuda(), grad_scale=0.5, first=False, **hp)
+    torch.testing.assert_close(pd.cpu(), p, rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(md.cpu(), m, rtol=1e-6, atol=1e-7)
+    # bf16 gradient input
+    gb = g.to(torch.bfloat16)
+    p, m = p0.clone(), m0.clone()
+    oracle.sgd_apply(p, m, gb.float(), first=True, **hp)
+    pd, md = p0.cuda(), m0.cuda()
+    ops.sgd_flat(pd, md, gb.cuda(), first=True, **hp)
+    torch.testing.assert_close(pd.cpu(), p, rtol=1e-6, atol=1e-7)
+    # adam / amsgrad
+    for ams in (False, True):
+        p = p0.clone()
+        mm, vv, vx = torch.zeros(n), torch.zeros(n), torch.zeros(n)
+        for t in (1, 2, 3):
+            oracle.adam_apply(p, mm, vv, vx, g * t, 1e-3, 0.9, 0.999, 1e-8, 1e-2, t, ams)
+        pd = p0.cuda()
+        mmd, vvd, vxd = torch.zeros(n, device=DEV), torch.zeros(n, device=DEV), \
+            torch.zeros(n, device=DEV)
+        import math
+        for t in (1, 2, 3):
+            ls = 1e-3 * math.sqrt(1 - 0.999 ** t) / (1 - 0.9 ** t)
+            ops.adam_flat(pd, mmd, vvd, vxd, (g * t).cuda(), ls, 0.9, 0.999, 1e-8, 1e-2, 1.0, ams)
+        torch.testing.assert_close(pd.cpu(), p, rtol=1e-5, atol=1e-6)
+
+
+def test_cast_scale_bf16_fp16():
+    ops.require()
+    x = torch.randn(4096 * 3, device=DEV) * 100
+    for dt in (torch.bfloat16, torch.float16):
+        out = torch.empty(x.numel(), dtype=dt, device=DEV)
+        ops.cast_scale(x, out, 0.25)
+        assert torch.equal(out, (x * 0.25).to(dt))
+
+
+def test_bad_operands_rejected():
+    ops.require()
+    plan = _plan([1000], 0.1)
+    lay = Layout.build("topk_qsgd", plan, 8)
+    dp = ops.DevicePlan(plan, DEV)
+    with pytest.raises(ValueError):
+        ops.topk_encode(dp, torch.zeros(10, device=DEV), torch.zeros(lay.nbytes,
+                        dtype=torch.uint8, device=DEV), lay, 127, "max", 0)
+    with pytest.raises(ValueError):
+        ops.topk_encode(dp, torch.zeros(plan.length, device=DEV), torch.zeros(
+            lay.nbytes, dtype=torch.uint8, device=DEV), lay, 200, "max", 0)
