@@ -1,0 +1,126 @@
+"""Multi-process exchange tests on CPU/Gloo (BASELINE.json config #1: LeNet, world_size=2,
+top-k 1 % + QSGD, plumbing without a GPU)."""
+import os
+
+import pytest
+import torch
+
+from .helpers import run_world
+
+pytestmark = pytest.mark.slow
+
+BASE = ["--network", "LeNet", "--dataset", "MNIST", "--batch-size", "16", "--synthetic-size",
+        "512", "--momentum", "0.9", "--lr", "0.05", "--eval-freq", "0", "--quiet",
+        "--device", "cpu", "--log-interval", "1000"]
+
+
+def _train(rank, world, flags, steps):
+    import ewdml
+    from ewdml.runtime import Trainer
+
+    cfg = ewdml.parse_args(BASE + flags + ["--max-steps", str(steps)])
+    tr = Trainer(cfg)
+    losses = []
+    for _ in range(steps):
+        loss, _ = tr.train_step()
+        losses.append(None if loss is None else float(loss))
+    return {"params": tr.flat.data.clone(), "losses": losses,
+            "bytes": tr.exchange.last.payload_bytes, "rank": rank}
+
+
+def _same_params(results, ranks=None):
+    ranks = ranks if ranks is not None else range(len(results))
+    ps = [results[r]["params"] for r in ranks]
+    for p in ps[1:]:
+        assert torch.equal(p, ps[0])
+
+
+@pytest.mark.parametrize("flags", [
+    ["--compress", "topk_qsgd"],
+    ["--compress", "topk_qsgd", "--qsgd-bits", "4", "--qsgd-levels", "7"],
+    ["--compress", "topk", "--topk-ratio", "0.05"],
+    ["--compress", "qsgd", "--qsgd-norm", "l2"],
+    ["--compress", "none"],
+    ["--compress", "bf16"],
+    ["--compress", "topk_qsgd", "--error-feedback"],
+    ["--compress", "topk_qsgd", "--no-overlap", "--bucket-mb", "0.5"],
+])
+def test_allgather_replicas_identical(tmp_path, flags):
+    res = run_world(_train, 2, tmp_path, args=(flags, 4))
+    _same_params(res)
+    assert all(res[0]["losses"])
+
+
+def test_world3_topk_qsgd_identical(tmp_path):
+    res = run_world(_train, 3, tmp_path, args=(["--compress", "topk_qsgd"], 3))
+    _same_params(res)
+
+
+def test_dense_allreduce_equals_average(tmp_path):
+    res = run_world(_worker_dense, 2, tmp_path)
+    # single-process reference: average grads of both batches
+    import torch.nn.functional as F
+    from ewdml.models import build_model
+    from ewdml.parallel.flat import FlatModel
+
+    m = build_model("LeNet")
+    flat = FlatModel(m, bucket_bytes=16 << 20)
+    flat.data.copy_(res[0]["p0"])
+    g = torch.zeros_like(flat.grad)
+    for r in res:
+        flat.zero_grad()
+        F.cross_entropy(m(r["x"]), r["y"]).backward()
+        g += flat.grad
+    g /= 2
+    lr = 0.05
+    expected = res[0]["p0"] - lr * g  # first step: momentum buffer = g
+    torch.testing.assert_close(res[0]["p1"], expected, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(res[1]["p1"], res[0]["p1"], rtol=0, atol=0)
+
+
+def _worker_dense(rank, world):
+    import ewdml
+    from ewdml.runtime import Trainer
+
+    cfg = ewdml.parse_args(BASE + ["--compress", "none", "--max-steps", "1", "--amp", "none"])
+    tr = Trainer(cfg)
+    x, y = tr.loader.next()
+    p0 = tr.flat.data.clone()
+    tr.train_step(x, y)
+    return {"p0": p0, "p1": tr.flat.data.clone(), "x": x, "y": y}
+
+
+@pytest.mark.parametrize("method", [1, 2, 3, 4, 5])
+def test_ps_topology_methods(tmp_path, method):
+    flags = ["--method", str(method), "--topology", "ps"]
+    res = run_world(_train, 3, tmp_path, args=(flags, 3))
+    _same_params(res, [1, 2])  # workers identical
+    if method >= 3:  # pull-grad: the server's replica tracks the workers'
+        _same_params(res)
+    assert res[0]["losses"] == [None, None, None]
+
+
+def test_ps_matches_allreduce_dense(tmp_path):
+    ps = run_world(_train, 3, tmp_path / "ps",
+                   args=(["--topology", "ps", "--compress", "none", "--amp", "none"], 3))
+    ar = run_world(_train, 2, tmp_path / "ar",
+                   args=(["--compress", "none", "--amp", "none"], 3))
+    torch.testing.assert_close(ps[1]["params"], ar[0]["params"], rtol=1e-5, atol=1e-6)
+
+
+def test_method6_local_sgd_select_best(tmp_path):
+    res = run_world(_train, 2, tmp_path, args=(["--method", "6", "--sync-every", "3"], 6))
+    _same_params(res)  # after the step-6 sync everyone holds the best rank's weights
+
+
+def test_local_sgd_model_mode(tmp_path):
+    res = run_world(_train, 2, tmp_path,
+                    args=(["--compress", "topk_qsgd", "--topk-ratio", "0.2", "--sync-every", "2",
+                           "--sync-mode", "model"], 4))
+    _same_params(res)
+
+
+def test_payload_bytes_lenet(tmp_path):
+    res = run_world(_train, 2, tmp_path, args=(["--compress", "topk_qsgd"], 1))
+    assert res[0]["bytes"] == res[1]["bytes"]
+    assert 431080 * 4 / res[0]["bytes"] > 125

@@ -1,0 +1,52 @@
+"""CLI parity with the reference's distributed_nn.py flags and the method presets."""
+import pytest
+
+import ewdml
+from ewdml.config import Config, build_parser
+
+REFERENCE_FLAGS = ["--batch-size", "--test-batch-size", "--epochs", "--max-steps", "--lr",
+                   "--momentum", "--no-cuda", "--seed", "--log-interval", "--network", "--mode",
+                   "--kill-threshold", "--dataset", "--comm-type", "--num-aggregate",
+                   "--eval-freq", "--train-dir", "--compress-grad", "--gather-type",
+                   "--enable-gpu", "--local_rank"]
+
+
+def test_every_reference_flag_accepted():
+    opts = {o for a in build_parser()._actions for o in a.option_strings}
+    for f in REFERENCE_FLAGS:
+        assert f in opts, f
+
+
+def test_reference_defaults():
+    c = ewdml.parse_args([])
+    assert (c.batch_size, c.test_batch_size, c.epochs, c.max_steps, c.lr, c.momentum) == \
+        (128, 500, 100, 10000, 0.01, 0.5)
+    assert c.network == "LeNet" and c.dataset == "MNIST" and c.train_dir == "output/models/"
+
+
+def test_reference_script_invocation():
+    # src/run_pytorch_single.sh:4-18
+    c = ewdml.parse_args("--lr=0.01 --momentum=0.9 --network=LeNet --dataset=MNIST "
+                         "--batch-size=64 --comm-type=Bcast --mode=normal --num-aggregate=2 "
+                         "--eval-freq=20 --epochs=10 --max-steps=10000 --train-dir=/tmp/x/ "
+                         "--compress-grad=compress --gather-type=gather --enable-gpu= "
+                         "--local_rank=0".split())
+    assert c.batch_size == 64 and c.enable_gpu is False and c.local_rank == 0
+
+
+@pytest.mark.parametrize("m,topo,comp,pull,every", [
+    (1, "ps", "none", "weights", 1), (2, "ps", "qsgd", "weights", 1),
+    (3, "allgather", "none", "grad", 1), (4, "allgather", "qsgd", "grad", 1),
+    (5, "allgather", "topk_qsgd", "grad", 1), (6, "allgather", "topk_qsgd", "grad", 20)])
+def test_method_presets(m, topo, comp, pull, every):
+    c = ewdml.parse_args(["--method", str(m)])
+    assert (c.topology, c.compress, c.pull, c.sync_every) == (topo, comp, pull, every)
+    assert c.select_best == (m == 6)
+
+
+def test_compress_grad_none_switch():
+    assert ewdml.parse_args(["--compress-grad", "none"]).compress == "none"
+
+
+def test_ckpt_dir_defaults_to_train_dir():
+    assert Config(train_dir="/a/").resolved().ckpt_dir == "/a/"
