@@ -45,6 +45,7 @@ def parse(argv=None):
     p.add_argument("--channels-last", action="store_true")
     p.add_argument("--no-overlap", action="store_true")
     p.add_argument("--error-feedback", action="store_true")
+    p.add_argument("--hip-graph", default="off", choices=["off", "split", "full"])
     p.add_argument("--extra", default="", help="extra distributed_nn.py flags")
     return p.parse_args(argv)
 
@@ -74,6 +75,9 @@ def main(argv=None):
         flags.append("--no-overlap")
     if a.error_feedback:
         flags.append("--error-feedback")
+    # graph capture happens inside the untimed warmup: eager steps, then the capturing step
+    gw = max(1, min(3, a.warmup - 1))
+    flags += ["--hip-graph", a.hip_graph, "--graph-warmup", str(gw)]
     flags += a.extra.split()
     cfg = ewdml.parse_args(flags, prog="bench.py")
     tr = Trainer(cfg)
@@ -83,7 +87,8 @@ def main(argv=None):
         if cuda:
             torch.cuda.synchronize()
 
-    for _ in range(a.warmup):
+    warm = a.warmup if a.hip_graph == "off" else max(a.warmup, gw + 1)
+    for _ in range(warm):
         tr.train_step()
     sync()
     tr.comm.barrier()
@@ -122,7 +127,7 @@ def main(argv=None):
                    "seq_len": None, "parallelism": f"dp{world}",
                    "codec": tr.exchange.codec.describe() if hasattr(tr.exchange, "codec") else
                    a.compress, "optimizer": "sgd(momentum=0.9)", "overlap": not a.no_overlap,
-                   "buckets": len(tr.flat.buckets)},
+                   "buckets": len(tr.flat.buckets), "hip_graph": a.hip_graph},
         "grad_bytes_per_step_on_wire": bytes_["wire_bytes_total"],
         "payload_bytes_per_rank": bytes_["payload_bytes_per_rank"],
         "dense_fp32_grad_bytes": bytes_["dense_fp32_bytes"],

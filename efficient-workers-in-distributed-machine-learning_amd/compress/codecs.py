@@ -93,17 +93,17 @@ class Codec:
 
     # -- encode / decode ----------------------------------------------------------------------
     def encode(self, b: int, grad: torch.Tensor, payload: torch.Tensor, step: int, rank: int,
-               resid: torch.Tensor = None):
+               resid: torch.Tensor = None, key_tensor: torch.Tensor = None):
         """Compress bucket ``b`` of the flat gradient (``grad`` = that bucket's view)."""
         plan, lay = self.plans[b], self.layouts[b]
         key = self.key(step, rank)
         if grad.is_cuda:
             if self.kind == "qsgd":
                 ops.qsgd_encode(self.dplans[b], grad, payload, lay, self.levels, self.norm, key,
-                                resid)
+                                resid, key_tensor)
             else:
                 ops.topk_encode(self.dplans[b], grad, payload, lay, self.levels, self.norm, key,
-                                resid)
+                                resid, key_tensor)
             return
         if self.kind == "qsgd":
             out = oracle.encode_qsgd(grad, plan, lay, self.levels, self.norm, key, resid)

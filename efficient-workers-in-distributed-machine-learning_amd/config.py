@@ -79,7 +79,8 @@ class Config:
     device: str = "auto"  # auto | cuda | cpu
     amp: str = "bf16"  # bf16 | fp16 | none  (autocast compute dtype; master weights fp32)
     channels_last: bool = False
-    hip_graph: bool = False
+    hip_graph: str = "off"  # off | split (graphs around eager RCCL calls) | full (one graph)
+    graph_warmup: int = 3  # eager steps before capture (MIOpen find, momentum init)
     data_dir: Optional[str] = None  # None -> synthetic data of the dataset's shape
     synthetic_size: int = 0
     augment: bool = True
@@ -180,7 +181,8 @@ def build_parser(prog="distributed_nn.py") -> argparse.ArgumentParser:
     a("--device", type=str, default=d.device, choices=["auto", "cuda", "cpu"])
     a("--amp", type=str, default=d.amp, choices=["bf16", "fp16", "none"])
     a("--channels-last", action="store_true", default=False)
-    a("--hip-graph", action="store_true", default=False)
+    a("--hip-graph", type=str, default=d.hip_graph, choices=["off", "split", "full"])
+    a("--graph-warmup", type=int, default=d.graph_warmup)
     a("--data-dir", type=str, default=None)
     a("--synthetic-size", type=int, default=0)
     a("--no-augment", dest="augment", action="store_false", default=True)

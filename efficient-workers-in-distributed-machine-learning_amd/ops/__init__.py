@@ -76,8 +76,16 @@ def _check_bucket(dp, grad, name="grad"):
         raise ValueError(f"{name} has {grad.numel()} elements, bucket needs {dp.plan.length}")
 
 
+def _keyp(key_tensor):
+    if key_tensor is None:
+        return 0
+    if not key_tensor.is_cuda or key_tensor.dtype != torch.int32 or key_tensor.numel() < 1:
+        raise ValueError("key_tensor must be a device int32 tensor")
+    return key_tensor.data_ptr()
+
+
 def topk_encode(dp: DevicePlan, grad, payload, layout, levels: int, norm: str, key: int,
-                resid=None):
+                resid=None, key_tensor=None):
     C = require()
     _check_bucket(dp, grad)
     _check(payload, torch.uint8, "payload")
@@ -97,7 +105,7 @@ def topk_encode(dp: DevicePlan, grad, payload, layout, levels: int, norm: str, k
                   _ptr(payload), layout.nbytes, dp.plan.num_tensors, dp.plan.num_chunks,
                   layout.scales, layout.counts, layout.idx, layout.codes, vk,
                   1 if norm == "l2" else 0, float(levels), float(1.0 / levels), key & 0xFFFFFFFF,
-                  dp.plan.bucket_offset & 0xFFFFFFFF, _stream())
+                  dp.plan.bucket_offset & 0xFFFFFFFF, _keyp(key_tensor), _stream())
 
 
 def topk_decode_apply(dp: DevicePlan, recv, layout, levels: int, param=None, mom=None,
@@ -126,7 +134,7 @@ def topk_decode_apply(dp: DevicePlan, recv, layout, levels: int, param=None, mom
 
 
 def qsgd_encode(dp: DevicePlan, grad, payload, layout, levels: int, norm: str, key: int,
-                resid=None):
+                resid=None, key_tensor=None):
     C = require()
     _check_bucket(dp, grad)
     _check(payload, torch.uint8, "payload")
@@ -140,7 +148,7 @@ def qsgd_encode(dp: DevicePlan, grad, payload, layout, levels: int, norm: str, k
                   _ptr(payload), layout.nbytes, dp.plan.num_tensors, dp.plan.num_chunks,
                   layout.scales, layout.codes, layout.bits, 1 if norm == "l2" else 0,
                   float(levels), float(1.0 / levels), key & 0xFFFFFFFF,
-                  dp.plan.bucket_offset & 0xFFFFFFFF, _stream())
+                  dp.plan.bucket_offset & 0xFFFFFFFF, _keyp(key_tensor), _stream())
 
 
 def qsgd_decode_apply(dp: DevicePlan, recv, layout, levels: int, param=None, mom=None,

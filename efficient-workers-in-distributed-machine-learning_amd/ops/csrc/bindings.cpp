@@ -20,11 +20,12 @@ PYBIND11_MODULE(_C, m) {
         [](uintptr_t grad, uintptr_t resid, uintptr_t chunks, uintptr_t tensors, uintptr_t scratch,
            uintptr_t payload, long long payload_bytes, int T, int C, int scales_off,
            int counts_off, int idx_off, int codes_off, int value_kind, int norm_l2, float levels,
-           float inv_levels, uint32_t key, uint32_t bucket_offset, uintptr_t stream) {
+           float inv_levels, uint32_t key, uint32_t bucket_offset, uintptr_t key_ptr,
+           uintptr_t stream) {
           TopkEncodeArgs a{grad,         resid,      chunks,     tensors,  scratch,   payload,
                            stream,       payload_bytes, T,       C,        scales_off, counts_off,
                            idx_off,      codes_off,  value_kind, norm_l2,  levels,    inv_levels,
-                           key,          bucket_offset};
+                           key,          bucket_offset, key_ptr};
           ew_topk_encode(a);
         });
 
@@ -46,10 +47,10 @@ PYBIND11_MODULE(_C, m) {
         [](uintptr_t grad, uintptr_t resid, uintptr_t chunks, uintptr_t tensors, uintptr_t scratch,
            uintptr_t payload, long long payload_bytes, int T, int C, int scales_off, int codes_off,
            int bits, int norm_l2, float levels, float inv_levels, uint32_t key,
-           uint32_t bucket_offset, uintptr_t stream) {
+           uint32_t bucket_offset, uintptr_t key_ptr, uintptr_t stream) {
           QsgdEncodeArgs a{grad,      resid,   chunks,        tensors,   scratch, payload, stream,
                            payload_bytes, T,   C,             scales_off, codes_off, bits, norm_l2,
-                           levels,    inv_levels, key,        bucket_offset};
+                           levels,    inv_levels, key,        bucket_offset, key_ptr};
           ew_qsgd_encode(a);
         });
 

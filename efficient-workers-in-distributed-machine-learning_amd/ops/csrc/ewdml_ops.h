@@ -13,6 +13,7 @@ struct TopkEncodeArgs {
   int norm_l2;     // 0 = max-norm scale, 1 = L2 norm of the selected values
   float levels, inv_levels;
   uint32_t key, bucket_offset;
+  uintptr_t key_ptr;  // optional device uint32 overriding `key` (graph replay)
 };
 
 struct TopkDecodeArgs {
@@ -33,6 +34,7 @@ struct QsgdEncodeArgs {
   int scales_off, codes_off, bits, norm_l2;
   float levels, inv_levels;
   uint32_t key, bucket_offset;
+  uintptr_t key_ptr;
 };
 
 struct QsgdDecodeArgs {

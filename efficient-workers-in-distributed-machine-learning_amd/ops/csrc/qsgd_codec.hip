@@ -65,7 +65,8 @@ __global__ __launch_bounds__(EW_BLOCK) void k_qsgd_quant(
     const float* __restrict__ g, float* __restrict__ resid, const ChunkRow* __restrict__ chunks,
     const TensorRow* __restrict__ tensors, const float* __restrict__ inv_arr,
     uint8_t* __restrict__ payload, int scales_off, int codes_off, float levels, float inv_levels,
-    uint32_t key, uint32_t bucket_offset) {
+    uint32_t key_arg, const uint32_t* __restrict__ keyp, uint32_t bucket_offset) {
+  const uint32_t key = keyp ? *keyp : key_arg;
   const ChunkRow c = chunks[blockIdx.x];
   const TensorRow tr = tensors[c.tensor];
   const float* src = g + c.start;
@@ -184,7 +185,8 @@ void ew_qsgd_encode(const QsgdEncodeArgs& a) {
             a.norm_l2);
 #define EW_Q(B, EFV)                                                                             \
   EW_LAUNCH((k_qsgd_quant<B, EFV>), C, s, g, resid, chunks, tensors, inv, pay, a.scales_off,      \
-            a.codes_off, a.levels, a.inv_levels, a.key, a.bucket_offset)
+            a.codes_off, a.levels, a.inv_levels, a.key,                                          \
+            reinterpret_cast<const uint32_t*>(a.key_ptr), a.bucket_offset)
   if (a.bits == 8) {
     if (resid) EW_Q(8, true); else EW_Q(8, false);
   } else {

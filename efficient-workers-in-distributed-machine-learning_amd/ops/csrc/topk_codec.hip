@@ -251,8 +251,10 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_write(
     const TensorRow* __restrict__ tensors, const uint32_t* __restrict__ state,
     const uint32_t* __restrict__ chunk_off, const uint32_t* __restrict__ chunk_ties,
     const float* __restrict__ inv_arr, uint8_t* __restrict__ payload, int scales_off, int idx_off,
-    int codes_off, float levels, float inv_levels, uint32_t key, uint32_t bucket_offset) {
+    int codes_off, float levels, float inv_levels, uint32_t key_arg, const uint32_t* __restrict__ keyp,
+    uint32_t bucket_offset) {
   __shared__ uint32_t ws[EW_WAVES];
+  const uint32_t key = keyp ? *keyp : key_arg;  // device key: fresh per replay of a captured graph
   const ChunkRow c = chunks[blockIdx.x];
   const TensorRow tr = tensors[c.tensor];
   const float* src = g + c.start;
@@ -438,7 +440,7 @@ void ew_topk_encode(const TopkEncodeArgs& a) {
 #define EW_WRITE(VK, EFV)                                                                          \
   EW_LAUNCH((k_topk_write<VK, EFV>), C, s, g, resid, chunks, tensors, state, chunk_off, chunk_ties, \
             inv, pay, a.scales_off, a.idx_off, a.codes_off, a.levels, a.inv_levels, a.key,         \
-            a.bucket_offset)
+            reinterpret_cast<const uint32_t*>(a.key_ptr), a.bucket_offset)
   if (a.value_kind == VK_Q8) {
     if (resid) EW_WRITE(VK_Q8, true); else EW_WRITE(VK_Q8, false);
   } else if (a.value_kind == VK_Q4) {

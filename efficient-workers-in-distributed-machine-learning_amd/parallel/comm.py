@@ -19,7 +19,12 @@ import torch.distributed as dist
 def init_distributed(backend: str = None, timeout_s: float = None, device=None) -> "Comm":
     """env:// rendezvous (RANK/WORLD_SIZE/MASTER_ADDR/MASTER_PORT as set by torchrun)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world > 1 and not dist.is_initialized():
+    force = os.environ.get("EWDML_FORCE_PG") == "1"  # real process group even for one rank
+    if (world > 1 or force) and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29511")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
         kw = {}
@@ -41,6 +46,10 @@ class Comm:
         else:
             self.rank, self.world, self.backend = 0, 1, "local"
         self._gloo_ag = self.backend == "gloo"
+        # EWDML_FORCE_PG=1: issue real collectives even in a world of one (exercises RCCL and
+        # graph capture of collectives on a single-GPU box)
+        self._local = self.world == 1 and not (os.environ.get("EWDML_FORCE_PG") == "1"
+                                               and self.backend != "local")
 
     @property
     def distributed(self) -> bool:
@@ -49,7 +58,7 @@ class Comm:
     # -- collectives (return a Work handle or None when already complete) --------------------
     def all_gather(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = False):
         """``out`` [world * n] <- concat of every rank's ``inp`` [n]."""
-        if self.world == 1:
+        if self._local:
             out[:inp.numel()].copy_(inp)
             return None
         if self._gloo_ag:
@@ -58,7 +67,7 @@ class Comm:
         return dist.all_gather_into_tensor(out, inp, group=self.group, async_op=async_op)
 
     def all_reduce(self, t: torch.Tensor, op=dist.ReduceOp.SUM, async_op: bool = False):
-        if self.world == 1:
+        if self._local:
             return None
         return dist.all_reduce(t, op=op, group=self.group, async_op=async_op)
 
@@ -90,8 +99,10 @@ class Comm:
             else:
                 dist.barrier(group=self.group)
 
-    def all_reduce_scalars(self, values, op="sum", device="cpu"):
+    def all_reduce_scalars(self, values, op="sum", device=None):
         """All-reduce a short list of Python floats (metrics averaging, ``horvod_pytorch.py:84``)."""
+        if device is None:  # RCCL only reduces device tensors
+            device = torch.cuda.current_device() if self.backend == "nccl" else "cpu"
         t = torch.tensor(values, dtype=torch.float64, device=device)
         if self.world > 1:
             rop = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX,

@@ -69,8 +69,12 @@ class GradientExchange:
         self._count = [0] * self.nb
         self._launched = [False] * self.nb
         self._works = [None] * self.nb
+        self._next = 0
         self._active = False
         self.step_idx = 0
+        self.defer_comm = False
+        self.use_dev_key = False
+        self.key_dev = torch.zeros(1, dtype=torch.int32, device=self.device)
         self._hooks = []
         if overlap:
             for p in flat.params:
@@ -102,6 +106,7 @@ class GradientExchange:
         self._count = [0] * self.nb
         self._launched = [False] * self.nb
         self._works = [None] * self.nb
+        self._next = 0
         self._active = True
 
     def _on_grad(self, p):
@@ -109,8 +114,12 @@ class GradientExchange:
             return
         b = self._bucket_of[id(p)]
         self._count[b] += 1
-        if self._count[b] == self._sizes[b] and not self._launched[b]:
-            self._launch(b)
+        # Launch strictly in bucket order so every rank issues its collectives in the same
+        # sequence, whatever order autograd finishes the buckets in (a mismatch would deadlock).
+        while self._next < self.nb and self._count[self._next] >= self._sizes[self._next]:
+            if not self._launched[self._next]:
+                self._launch(self._next)
+            self._next += 1
 
     def _stream_ctx(self):
         if self.side is None:
@@ -121,38 +130,73 @@ class GradientExchange:
         return torch.cuda.stream(self.side)
 
     def _launch(self, bi: int):
+        """Encode bucket ``bi`` on the side stream and (unless deferred) issue its collective."""
         self._launched[bi] = True
+        with self._stream_ctx():
+            self._encode(bi)
+            if not self.defer_comm:
+                self._works[bi] = self._collective(bi)
+
+    def _encode(self, bi: int):
         b = self.flat.buckets[bi]
         g = self.flat.grad_view(b)
-        with self._stream_ctx():
-            if self.codec.allreduce:
-                if self.send[bi] is None:
-                    if self.predivide != 1.0:
-                        g.mul_(1.0 / self.predivide)
-                    work = self.comm.all_reduce(g, async_op=True)
-                else:
-                    if self.cuda:
-                        ops.cast_scale(g, self.send[bi], 1.0 / self.predivide)
-                    else:
-                        self.send[bi].copy_(g * (1.0 / self.predivide))
-                    work = self.comm.all_reduce(self.send[bi], async_op=True)
+        if self.codec.allreduce:
+            if self.send[bi] is None:
+                if self.predivide != 1.0:
+                    g.mul_(1.0 / self.predivide)
+            elif self.cuda:
+                ops.cast_scale(g, self.send[bi], 1.0 / self.predivide)
             else:
-                resid = None if self.resid is None else self.resid[b.start:b.start + b.length]
-                self.codec.encode(bi, g, self.payload[bi], self.step_idx + self.seed_offset,
-                                  self.comm.rank, resid)
-                work = self.comm.all_gather(self.recv[bi], self.payload[bi], async_op=True)
-        self._works[bi] = work
+                self.send[bi].copy_(g * (1.0 / self.predivide))
+            return
+        resid = None if self.resid is None else self.resid[b.start:b.start + b.length]
+        self.codec.encode(bi, g, self.payload[bi], self.step_idx + self.seed_offset,
+                          self.comm.rank, resid,
+                          key_tensor=self.key_dev if self.use_dev_key else None)
 
-    def finish(self, apply: bool = True):
-        """Complete every bucket's exchange and (by default) apply the optimizer step."""
+    def _collective(self, bi: int):
+        if self.codec.allreduce:
+            t = self.flat.grad_view(self.flat.buckets[bi]) if self.send[bi] is None \
+                else self.send[bi]
+            return self.comm.all_reduce(t, async_op=True)
+        return self.comm.all_gather(self.recv[bi], self.payload[bi], async_op=True)
+
+    def launch_pending(self):
         for bi in range(self.nb):
             if not self._launched[bi]:
                 self._launch(bi)
+
+    def join_side(self):
+        if self.side is not None:
+            torch.cuda.current_stream().wait_stream(self.side)
+
+    def communicate(self):
+        """Issue the deferred collectives (split-graph mode: outside any captured graph)."""
+        for bi in range(self.nb):
+            self._works[bi] = self._collective(bi)
+
+    def wait(self):
         for w in self._works:
             if w is not None:
                 w.wait()
-        if self.side is not None:
-            torch.cuda.current_stream().wait_stream(self.side)
+        self._works = [None] * self.nb
+
+    def set_device_key(self, step: int = None):
+        """Upload this step's RNG key (graph replay reads it from device memory)."""
+        key = self.codec.key((self.step_idx if step is None else step) + self.seed_offset,
+                             self.comm.rank)
+        if key >= 1 << 31:
+            key -= 1 << 32
+        self.key_dev.copy_(torch.tensor([key], dtype=torch.int32))
+
+    def finish(self, apply: bool = True):
+        """Complete every bucket's exchange and (by default) apply the optimizer step."""
+        self.launch_pending()
+        if self.defer_comm:
+            self.join_side()
+            self.communicate()
+        self.wait()
+        self.join_side()
         self._active = False
         if apply:
             self.apply()

@@ -118,6 +118,10 @@ class Trainer:
                 self.exchange = LocalSGDExchange(self.exchange, cfg.sync_every, cfg.sync_mode,
                                                  cfg.select_best, score_fn=self._holdout_score)
         self.amp_dtype = {"bf16": torch.bfloat16, "fp16": torch.float16}.get(cfg.amp)
+        self.graph_mode = cfg.hip_graph if self.cuda else "off"
+        if self.graph_mode != "off" and not isinstance(self.exchange, GradientExchange):
+            raise ValueError("--hip-graph needs the all-to-all topology without local SGD")
+        self._graphs = None
         self.step = 0
         self.epoch = 0
         self.fault = None
@@ -132,7 +136,8 @@ class Trainer:
         if self.amp_dtype is None:
             return contextlib.nullcontext()
         return torch.autocast(device_type=self.device.type, dtype=self.amp_dtype,
-                              enabled=self.cuda or self.amp_dtype == torch.bfloat16)
+                              enabled=self.cuda or self.amp_dtype == torch.bfloat16,
+                              cache_enabled=self.graph_mode == "off")
 
     def forward_backward(self, x, y):
         self.flat.zero_grad()
@@ -155,10 +160,70 @@ class Trainer:
         if x is None:
             x, y = self.loader.next()
         self.model.train()
+        if self.graph_mode != "off" and self.step >= self.cfg.graph_warmup:
+            if self._graphs is None:
+                self._capture(x, y)
+            return self._graph_step(x, y)
         loss, out = self.forward_backward(x, y)
         self.exchange.finish()
         self.step += 1
         return loss, (out, y)
+
+    # -- HIP graph execution ----------------------------------------------------------------------
+    def _capture(self, x, y):
+        """Capture the whole training step into HIP graph(s) (static input buffers; the QSGD RNG key
+        and the batch are refreshed in device memory before every replay).
+
+        ``full``: one graph = zero grads, fwd, bwd, hook-driven encode on the side stream, RCCL
+        collectives, fused decode+SGD.  ``split``: graph A (through encode) -> eager RCCL calls ->
+        graph B (decode+SGD), for process groups whose collectives cannot be captured."""
+        ex = self.exchange
+        self._gx = x.clone()
+        self._gy = y.clone()
+        ex.use_dev_key = True
+        saved = (ex.step_idx, self.opt.steps)
+        mode = os.environ.get("EWDML_GRAPH_CAPTURE_MODE", "global")
+        torch.cuda.synchronize()
+        if self.graph_mode == "full":
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, capture_error_mode=mode):
+                loss, out = self.forward_backward(self._gx, self._gy)
+                ex.finish()
+            self._graphs = (g,)
+        else:
+            ex.defer_comm = True
+            ga = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(ga, capture_error_mode=mode):
+                loss, out = self.forward_backward(self._gx, self._gy)
+                ex.launch_pending()
+                ex.join_side()
+            ex._active = False
+            gb = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gb, pool=ga.pool(), capture_error_mode=mode):
+                ex.apply()
+            self._graphs = (ga, gb)
+        ex.step_idx, self.opt.steps = saved
+        self._gloss, self._gout = loss, out
+        self._gbytes = ex.bytes_per_step()
+
+    def _graph_step(self, x, y):
+        ex = self.exchange
+        if x is not self._gx:
+            self._gx.copy_(x)
+            self._gy.copy_(y)
+        ex.set_device_key()
+        if len(self._graphs) == 1:
+            self._graphs[0].replay()
+        else:
+            self._graphs[0].replay()
+            ex.communicate()
+            ex.wait()
+            self._graphs[1].replay()
+        ex.step_idx += 1
+        self.opt.steps += 1
+        ex.last = self._gbytes
+        self.step += 1
+        return self._gloss, (self._gout, self._gy)
 
     @torch.no_grad()
     def evaluate(self, max_batches=None):
@@ -197,14 +262,20 @@ class Trainer:
                             if isinstance(v, (int, float, str, bool)) or v is None},
                  "world": self.world}
         if getattr(inner, "resid", None) is not None:
-            extra["ef_residual"] = inner.resid
+            # the error-feedback residual is per-rank state: keep every rank's row
+            r = inner.resid
+            allr = torch.zeros((self.world, r.numel()), dtype=r.dtype, device=r.device)
+            self.comm.all_gather(allr.view(-1), r)
+            extra["ef_residual"] = allr
         return extra
 
     def save_checkpoint(self):
+        """Collective (every rank calls it); rank 0 writes."""
+        extra = self.state_extra()
         if self.rank != 0:
             return None
         return ckpt.save(self.cfg.ckpt_dir, self.step, self.model, self.opt, self.epoch,
-                         extra=self.state_extra(),
+                         extra=extra,
                          legacy_dir=self.cfg.train_dir if self.cfg.legacy_ckpt else None)
 
     def _resume(self):
@@ -223,7 +294,10 @@ class Trainer:
         inner = getattr(self.exchange, "inner", self.exchange)
         r = st["extra"].get("ef_residual")
         if r is not None and getattr(inner, "resid", None) is not None:
-            inner.resid.copy_(r.to(self.device))
+            if r.dim() == 2 and r.shape[0] == self.world:
+                inner.resid.copy_(r[self.rank].to(self.device))
+            else:
+                self.log.info("resume: world size changed, error-feedback residual reset")
         if hasattr(self.exchange, "step_idx"):
             self.exchange.step_idx = self.step
         if self.loader is not None:
@@ -264,7 +338,7 @@ class Trainer:
                 if loss is not None:
                     out, y = outy
                     a1, a5 = accuracy(out.float(), y, (1, 5))
-                    rec.update(loss=float(loss), acc1=float(a1), acc5=float(a5))
+                    rec.update(loss=float(loss.detach()), acc1=float(a1), acc5=float(a5))
                 rec["step_ms"] = sw.phases().get("step")
                 rec.update(byte_summary(self.exchange.last, self.world))
                 rec["images_per_sec_rank"] = (cfg.batch_size * 1e3 / rec["step_ms"]

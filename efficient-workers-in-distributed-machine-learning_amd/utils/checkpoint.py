@@ -17,7 +17,7 @@ import torch
 def _atomic_save(obj, path):
     d = os.path.dirname(os.path.abspath(path))
     os.makedirs(d, exist_ok=True)
-    fd, tmp = tempfile.mkstemp(dir=d, prefix=".tmp_ckpt_")
+    fd, tmp = tempfile.mkstemp(dir=d, prefix="tmp_ckpt_", suffix=".part")
     os.close(fd)
     try:
         torch.save(obj, tmp)

@@ -1,0 +1,75 @@
+"""Summarise a rocprofv3 ``--kernel-trace --output-format csv`` run into a small text report.
+
+Usage: python tools/prof_summarize.py <dir containing *kernel_trace.csv> <out.txt> [--steps K]
+       [--delete]
+
+Reports per-kernel totals over the last K-step window (the timed region of bench.py: the final
+``steps`` iterations), GPU busy fraction (union of kernel intervals / wall span), and kernels per
+step.  ``--delete`` removes the raw trace CSVs afterwards (gpurun copies back <= 64 MiB).
+"""
+import csv
+import glob
+import os
+import sys
+from collections import defaultdict
+
+
+def load(d):
+    rows = []
+    for f in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]),
+                             r.get("Kernel_Name", "?")))
+    rows.sort()
+    return rows
+
+
+def short(name):
+    n = name.split("(")[0]
+    for pre in ("void ", "__omp"):
+        n = n.replace(pre, "")
+    return n[:110]
+
+
+def summarize(rows, frac=0.5):
+    if not rows:
+        return "no kernels\n"
+    t0, t1 = rows[0][0], max(r[1] for r in rows)
+    cut = t0 + (t1 - t0) * (1 - frac)
+    win = [r for r in rows if r[0] >= cut]
+    span = max(r[1] for r in win) - win[0][0]
+    busy = 0
+    cur_s, cur_e = win[0][0], win[0][1]
+    for s, e, _ in win[1:]:
+        if s > cur_e:
+            busy += cur_e - cur_s
+            cur_s, cur_e = s, e
+        else:
+            cur_e = max(cur_e, e)
+    busy += cur_e - cur_s
+    agg = defaultdict(lambda: [0, 0])
+    for s, e, n in win:
+        agg[short(n)][0] += 1
+        agg[short(n)][1] += e - s
+    out = [f"window: last {frac:.0%} of trace, {len(win)} kernels, span {span / 1e6:.3f} ms, "
+           f"GPU busy {busy / 1e6:.3f} ms ({100 * busy / span:.1f}%)",
+           f"{'calls':>7} {'total_ms':>10} {'avg_us':>9}  kernel"]
+    for n, (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:60]:
+        out.append(f"{c:>7} {t / 1e6:>10.3f} {t / c / 1e3:>9.2f}  {n}")
+    return "\n".join(out) + "\n"
+
+
+if __name__ == "__main__":
+    d, out = sys.argv[1], sys.argv[2]
+    rows = load(d)
+    txt = summarize(rows)
+    with open(out, "w") as f:
+        f.write(txt)
+    print(txt[:3000])
+    if "--delete" in sys.argv:
+        for f in glob.glob(os.path.join(d, "**", "*.csv"), recursive=True):
+            if "stats" not in os.path.basename(f):
+                os.remove(f)
+        for f in glob.glob(os.path.join(d, "**", "*.db"), recursive=True):
+            os.remove(f)
