@@ -45,7 +45,7 @@ def parse(argv=None):
     p.add_argument("--channels-last", action="store_true")
     p.add_argument("--no-overlap", action="store_true")
     p.add_argument("--error-feedback", action="store_true")
-    p.add_argument("--hip-graph", default="off", choices=["off", "split", "full"])
+    p.add_argument("--hip-graph", default="full", choices=["off", "split", "full"])
     p.add_argument("--extra", default="", help="extra distributed_nn.py flags")
     return p.parse_args(argv)
 
@@ -93,6 +93,8 @@ def main(argv=None):
     sync()
     tr.comm.barrier()
     sync()
+    if os.environ.get("EWDML_PROF_GAP") == "1":  # idle gap marking the timed region in traces
+        time.sleep(0.25)
     t0 = time.perf_counter()
     loss = None
     for _ in range(a.steps):
@@ -127,7 +129,7 @@ def main(argv=None):
                    "seq_len": None, "parallelism": f"dp{world}",
                    "codec": tr.exchange.codec.describe() if hasattr(tr.exchange, "codec") else
                    a.compress, "optimizer": "sgd(momentum=0.9)", "overlap": not a.no_overlap,
-                   "buckets": len(tr.flat.buckets), "hip_graph": a.hip_graph},
+                   "buckets": len(tr.flat.buckets), "hip_graph": tr.graph_mode},
         "grad_bytes_per_step_on_wire": bytes_["wire_bytes_total"],
         "payload_bytes_per_rank": bytes_["payload_bytes_per_rank"],
         "dense_fp32_grad_bytes": bytes_["dense_fp32_bytes"],

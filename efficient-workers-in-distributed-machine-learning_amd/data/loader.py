@@ -90,6 +90,8 @@ class DeviceLoader:
         return self._make(self._idx[s:s + self.batch_size])
 
     def __iter__(self):
-        """One epoch of batches."""
+        """The rest of the current epoch (a fresh epoch if the current one is exhausted)."""
+        if self._pos >= self.batches_per_epoch:
+            self._start_epoch(self.epoch + 1)
         for _ in range(self.batches_per_epoch - self._pos):
             yield self.next()

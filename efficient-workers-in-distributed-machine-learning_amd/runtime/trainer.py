@@ -57,8 +57,8 @@ class Trainer:
         self.rank, self.world = self.comm.rank, self.comm.world
         self.cuda = self.device.type == "cuda"
         torch.manual_seed(cfg.seed)
-        if self.cuda:
-            torch.backends.cudnn.benchmark = True
+        if self.cuda:  # MIOpen find once per shape during warmup (EWDML_CUDNN_BENCHMARK=0: heuristics)
+            torch.backends.cudnn.benchmark = os.environ.get("EWDML_CUDNN_BENCHMARK", "1") == "1"
         self.log = MetricsLogger(cfg.metrics_file, self.rank, cfg.quiet)
         self.is_server = cfg.topology == "ps" and self.rank == 0
 
@@ -161,8 +161,8 @@ class Trainer:
             x, y = self.loader.next()
         self.model.train()
         if self.graph_mode != "off" and self.step >= self.cfg.graph_warmup:
-            if self._graphs is None:
-                self._capture(x, y)
+            if self._graphs is None and not self._try_capture(x, y):
+                return self.train_step(x, y)  # capture failed on some rank: all run eager
             return self._graph_step(x, y)
         loss, out = self.forward_backward(x, y)
         self.exchange.finish()
@@ -170,6 +170,26 @@ class Trainer:
         return loss, (out, y)
 
     # -- HIP graph execution ----------------------------------------------------------------------
+    def _try_capture(self, x, y) -> bool:
+        """Capture on every rank, then agree (eager all-reduce) whether all succeeded; otherwise
+        every rank drops its graphs and continues eagerly, so no rank replays collectives that a
+        peer would not match."""
+        err = None
+        try:
+            self._capture(x, y)
+        except Exception as e:  # noqa: BLE001 - any capture failure falls back to eager
+            err = e
+        bad = self.comm.all_reduce_scalars([0.0 if err is None else 1.0], op="max")[0]
+        if bad:
+            ex = self.exchange
+            self._graphs = None
+            self.graph_mode = "off"
+            ex.use_dev_key = ex.defer_comm = ex._active = False
+            torch.cuda.synchronize()
+            self.log.info(f"HIP graph capture failed ({err!r} on this rank); running eagerly")
+            return False
+        return True
+
     def _capture(self, x, y):
         """Capture the whole training step into HIP graph(s) (static input buffers; the QSGD RNG key
         and the batch are refreshed in device memory before every replay).

@@ -32,11 +32,22 @@ def short(name):
     return n[:110]
 
 
-def summarize(rows, frac=0.5):
+def summarize(rows, frac=0.5, gap_ns=150_000_000, steps=None):
+    """Window = kernels after the last idle gap >= gap_ns (bench.py EWDML_PROF_GAP=1 sleeps before
+    the timed loop); falls back to the last ``frac`` of the trace."""
     if not rows:
         return "no kernels\n"
     t0, t1 = rows[0][0], max(r[1] for r in rows)
-    cut = t0 + (t1 - t0) * (1 - frac)
+    cut = None
+    end = rows[0][1]
+    for s, e, _ in rows[1:]:
+        if s - end >= gap_ns:
+            cut = s
+        end = max(end, e)
+    how = "after last idle gap"
+    if cut is None:
+        cut = t0 + (t1 - t0) * (1 - frac)
+        how = f"last {frac:.0%} of trace"
     win = [r for r in rows if r[0] >= cut]
     span = max(r[1] for r in win) - win[0][0]
     busy = 0
@@ -52,18 +63,24 @@ def summarize(rows, frac=0.5):
     for s, e, n in win:
         agg[short(n)][0] += 1
         agg[short(n)][1] += e - s
-    out = [f"window: last {frac:.0%} of trace, {len(win)} kernels, span {span / 1e6:.3f} ms, "
+    per = f", per step {span / 1e6 / steps:.3f} ms" if steps else ""
+    out = [f"window: {how}, {len(win)} kernels, span {span / 1e6:.3f} ms{per}, "
            f"GPU busy {busy / 1e6:.3f} ms ({100 * busy / span:.1f}%)",
-           f"{'calls':>7} {'total_ms':>10} {'avg_us':>9}  kernel"]
+           f"{'calls':>7} {'total_ms':>10} {'avg_us':>9}" + (" us/step " if steps else "") +
+           "  kernel"]
     for n, (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:60]:
-        out.append(f"{c:>7} {t / 1e6:>10.3f} {t / c / 1e3:>9.2f}  {n}")
+        ps = f" {t / 1e3 / steps:>9.2f}" if steps else ""
+        out.append(f"{c:>7} {t / 1e6:>10.3f} {t / c / 1e3:>9.2f}{ps}  {n}")
     return "\n".join(out) + "\n"
 
 
 if __name__ == "__main__":
     d, out = sys.argv[1], sys.argv[2]
     rows = load(d)
-    txt = summarize(rows)
+    steps = None
+    if "--steps" in sys.argv:
+        steps = int(sys.argv[sys.argv.index("--steps") + 1])
+    txt = summarize(rows, steps=steps)
     with open(out, "w") as f:
         f.write(txt)
     print(txt[:3000])
