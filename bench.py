@@ -28,26 +28,44 @@ if ROOT not in sys.path:
 BASELINE_IMG_S = 104.0
 
 
+# BASELINE.json configs (the default is the headline VGG-11 one)
+PRESETS = {
+    "vgg11": dict(network="VGG11", dataset="Cifar10", topk_ratio=0.01, qsgd_bits=8),
+    "lenet": dict(network="LeNet", dataset="MNIST", topk_ratio=0.01, qsgd_bits=8,
+                  batch_size=64),
+    "resnet50_cifar": dict(network="ResNet50", dataset="Cifar10", topk_ratio=0.01, qsgd_bits=8),
+    "resnet50_imagenet": dict(network="resnet50_imagenet", dataset="imagenet", topk_ratio=0.001,
+                              qsgd_bits=4, batch_size=64),
+}
+
+
 def parse(argv=None):
     p = argparse.ArgumentParser()
+    p.add_argument("--preset", default="vgg11", choices=sorted(PRESETS),
+                   help="BASELINE.json config (explicit flags override it)")
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=30)
     p.add_argument("--warmup", type=int, default=8)
-    p.add_argument("--network", default="VGG11")
-    p.add_argument("--dataset", default="Cifar10")
-    p.add_argument("--batch-size", type=int, default=128, help="per-GPU batch")
+    p.add_argument("--network", default=None)
+    p.add_argument("--dataset", default=None)
+    p.add_argument("--batch-size", type=int, default=None, help="per-GPU batch (default 128)")
     p.add_argument("--compress", default="topk_qsgd")
-    p.add_argument("--topk-ratio", type=float, default=0.01)
-    p.add_argument("--qsgd-bits", type=int, default=8)
+    p.add_argument("--topk-ratio", type=float, default=None)
+    p.add_argument("--qsgd-bits", type=int, default=None)
     p.add_argument("--qsgd-levels", type=int, default=None)
-    p.add_argument("--bucket-mb", type=float, default=16.0)
+    p.add_argument("--bucket-mb", type=float, default=64.0)
     p.add_argument("--amp", default="bf16")
     p.add_argument("--channels-last", action="store_true")
     p.add_argument("--no-overlap", action="store_true")
     p.add_argument("--error-feedback", action="store_true")
     p.add_argument("--hip-graph", default="full", choices=["off", "split", "full"])
     p.add_argument("--extra", default="", help="extra distributed_nn.py flags")
-    return p.parse_args(argv)
+    a = p.parse_args(argv)
+    pre = {"batch_size": 128, **PRESETS[a.preset]}
+    for k, v in pre.items():
+        if getattr(a, k) is None:
+            setattr(a, k, v)
+    return a
 
 
 def main(argv=None):
@@ -66,7 +84,8 @@ def main(argv=None):
     flags = ["--network", a.network, "--dataset", a.dataset, "--batch-size", str(a.batch_size),
              "--compress", a.compress, "--topk-ratio", str(a.topk_ratio), "--qsgd-bits",
              str(a.qsgd_bits), "--qsgd-levels", str(levels), "--momentum", "0.9", "--lr", "0.01",
-             "--bucket-mb", str(a.bucket_mb), "--amp", a.amp, "--synthetic-size", "16384",
+             "--bucket-mb", str(a.bucket_mb), "--amp", a.amp, "--synthetic-size",
+             str(max(2048, 4 * a.batch_size * world)),
              "--eval-freq", "0", "--log-interval", "1000000", "--quiet",
              "--max-steps", str(a.steps + a.warmup)]
     if a.channels_last:
@@ -109,8 +128,11 @@ def main(argv=None):
     ms = elapsed_max * 1e3 / a.steps
     img_s = world * a.batch_size * a.steps / elapsed_max
     bytes_ = byte_summary(tr.exchange.last, world)
+    metric = "grad bytes/step on wire + images/sec, VGG-11 CIFAR-10 at 1/2/4/8 MI355X"
+    if a.preset != "vgg11":
+        metric = f"grad bytes/step on wire + images/sec, {a.network} {a.dataset}"
     rec = {
-        "metric": "grad bytes/step on wire + images/sec, VGG-11 CIFAR-10 at 1/2/4/8 MI355X",
+        "metric": metric,
         "value": round(img_s, 2),
         "unit": "images/sec",
         "n_gpus": world,
@@ -119,11 +141,12 @@ def main(argv=None):
         "ms_per_step": round(ms, 4),
         "higher_is_better": True,
         "scaling": "weak",
-        "vs_baseline": round(img_s / BASELINE_IMG_S, 2),
+        "vs_baseline": round(img_s / BASELINE_IMG_S, 2) if a.preset == "vgg11" else None,
         "baseline_note": "reference publishes no img/s; BASELINE.md derives ~104 img/s (VGG-11, "
                          "2 Colab CPU workers)",
         "dtype": a.amp if a.amp != "none" else "fp32",
-        "data": "synthetic (CIFAR-10 shape 3x32x32, 10 classes, random-init weights)",
+        "data": f"synthetic ({a.dataset} shape {'x'.join(map(str, tr.info['shape']))}, "
+                f"{tr.info['classes']} classes, random-init weights)",
         "config": {"model": "vgg11_bn" if a.network.lower() in ("vgg11", "vgg11_bn") else
                    a.network, "global_batch": world * a.batch_size, "per_gpu_batch": a.batch_size,
                    "seq_len": None, "parallelism": f"dp{world}",

@@ -97,7 +97,8 @@ class Codec:
         """Compress bucket ``b`` of the flat gradient (``grad`` = that bucket's view)."""
         plan, lay = self.plans[b], self.layouts[b]
         key = self.key(step, rank)
-        if grad.is_cuda:
+        on_dev = (grad[0] if isinstance(grad, (list, tuple)) else grad).is_cuda
+        if on_dev:
             if self.kind == "qsgd":
                 ops.qsgd_encode(self.dplans[b], grad, payload, lay, self.levels, self.norm, key,
                                 resid, key_tensor)
@@ -105,6 +106,8 @@ class Codec:
                 ops.topk_encode(self.dplans[b], grad, payload, lay, self.levels, self.norm, key,
                                 resid, key_tensor)
             return
+        if isinstance(grad, (list, tuple)):
+            raise TypeError("CPU encode takes the bucket's flat gradient view")
         if self.kind == "qsgd":
             out = oracle.encode_qsgd(grad, plan, lay, self.levels, self.norm, key, resid)
         else:

@@ -80,7 +80,8 @@ class Config:
     amp: str = "bf16"  # bf16 | fp16 | none  (autocast compute dtype; master weights fp32)
     channels_last: bool = False
     hip_graph: str = "off"  # off | split (graphs around eager RCCL calls) | full (one graph)
-    graph_warmup: int = 3  # eager steps before capture (MIOpen find, momentum init)
+    graph_warmup: int = 3  # eager steps (>= 1) before capture: MIOpen find, handles, momentum
+
     data_dir: Optional[str] = None  # None -> synthetic data of the dataset's shape
     synthetic_size: int = 0
     augment: bool = True
@@ -93,6 +94,7 @@ class Config:
     profile: int = 0  # wrap N steps in torch.profiler
     inject_fault: Optional[str] = None  # "rank:step" -> that rank raises at that step (tests)
     comm_timeout: float = 600.0
+    sync_debug: bool = False  # synchronise after every custom kernel (race / fault localisation)
     quiet: bool = False
 
     def resolved(self) -> "Config":
@@ -119,6 +121,8 @@ class Config:
             c.compress = "none"
         if c.topology not in ("allgather", "ps"):
             raise ValueError("--topology must be allgather or ps")
+        if c.graph_warmup < 1:
+            raise ValueError("--graph-warmup must be >= 1 (one eager step initialises the stream)")
         if c.ckpt_dir is None:
             c.ckpt_dir = c.train_dir
         return c
@@ -195,6 +199,7 @@ def build_parser(prog="distributed_nn.py") -> argparse.ArgumentParser:
     a("--profile", type=int, default=0)
     a("--inject-fault", type=str, default=None)
     a("--comm-timeout", type=float, default=d.comm_timeout)
+    a("--sync-debug", action="store_true", default=False)
     a("--quiet", action="store_true", default=False)
     return p
 

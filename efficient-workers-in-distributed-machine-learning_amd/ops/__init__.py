@@ -22,6 +22,33 @@ except ImportError as e:  # pragma: no cover - depends on the build
 
 VK_Q8, VK_Q4, VK_F32 = 0, 1, 2
 
+_SYNC_DEBUG = os.environ.get("EWDML_SYNC_DEBUG") == "1"
+
+
+class _SyncDebug:
+    """``--sync-debug`` / EWDML_SYNC_DEBUG=1: synchronise the device after every custom kernel
+    launch so a fault, race or bad operand is reported at the launch that caused it."""
+
+    def __init__(self, mod):
+        self._m = mod
+
+    def __getattr__(self, name):
+        f = getattr(self._m, name)
+        if not callable(f):
+            return f
+
+        def call(*a, **k):
+            r = f(*a, **k)
+            if _SYNC_DEBUG:
+                torch.cuda.synchronize()
+            return r
+        return call
+
+
+def set_sync_debug(on: bool = True):
+    global _SYNC_DEBUG
+    _SYNC_DEBUG = bool(on)
+
 
 def available() -> bool:
     return _C is not None
@@ -32,7 +59,7 @@ def require():
         raise RuntimeError(
             "ewdml HIP extension is not built or failed to load "
             f"({_IMPORT_ERROR}); run `python -m ewdml.ops.build` (or __graft_entry__.build())")
-    return _C
+    return _SyncDebug(_C) if _SYNC_DEBUG else _C
 
 
 def library_path():
@@ -76,6 +103,31 @@ def _check_bucket(dp, grad, name="grad"):
         raise ValueError(f"{name} has {grad.numel()} elements, bucket needs {dp.plan.length}")
 
 
+MAX_TENSORS_PER_BUCKET = 128  # EW_MAX_T in csrc/common.h
+
+
+def grad_pointers(dp, grad):
+    """Per-tensor gradient base pointers of a bucket.  ``grad`` is either the bucket's flat fp32
+    view (tensors at the plan offsets) or a list with one fp32 tensor per plan tensor (autograd's
+    own ``p.grad`` tensors, read in place)."""
+    plan = dp.plan
+    if plan.num_tensors > MAX_TENSORS_PER_BUCKET:
+        raise ValueError(f"bucket has {plan.num_tensors} tensors (max {MAX_TENSORS_PER_BUCKET})")
+    if torch.is_tensor(grad):
+        _check_bucket(dp, grad)
+        base = grad.data_ptr()
+        return [base + 4 * o for o in plan.offsets]
+    if len(grad) != plan.num_tensors:
+        raise ValueError(f"{len(grad)} gradients for a bucket of {plan.num_tensors} tensors")
+    ptrs = []
+    for t, n in zip(grad, plan.numels):
+        _check(t, torch.float32, "grad tensor")
+        if t.numel() != n:
+            raise ValueError(f"gradient has {t.numel()} elements, plan expects {n}")
+        ptrs.append(t.data_ptr())
+    return ptrs
+
+
 def _keyp(key_tensor):
     if key_tensor is None:
         return 0
@@ -87,7 +139,7 @@ def _keyp(key_tensor):
 def topk_encode(dp: DevicePlan, grad, payload, layout, levels: int, norm: str, key: int,
                 resid=None, key_tensor=None):
     C = require()
-    _check_bucket(dp, grad)
+    ptrs = grad_pointers(dp, grad)
     _check(payload, torch.uint8, "payload")
     if payload.numel() < layout.nbytes:
         raise ValueError("payload too small")
@@ -101,7 +153,7 @@ def topk_encode(dp: DevicePlan, grad, payload, layout, levels: int, norm: str, k
         vk = VK_Q4
     if vk != VK_F32 and not (1 <= levels <= (127 if layout.bits == 8 else 7)):
         raise ValueError(f"levels={levels} does not fit {layout.bits}-bit codes")
-    C.topk_encode(_ptr(grad), _ptr(resid), _ptr(dp.chunks), _ptr(dp.tensors), _ptr(dp.scratch),
+    C.topk_encode(ptrs, _ptr(resid), _ptr(dp.chunks), _ptr(dp.tensors), _ptr(dp.scratch),
                   _ptr(payload), layout.nbytes, dp.plan.num_tensors, dp.plan.num_chunks,
                   layout.scales, layout.counts, layout.idx, layout.codes, vk,
                   1 if norm == "l2" else 0, float(levels), float(1.0 / levels), key & 0xFFFFFFFF,
@@ -136,7 +188,7 @@ def topk_decode_apply(dp: DevicePlan, recv, layout, levels: int, param=None, mom
 def qsgd_encode(dp: DevicePlan, grad, payload, layout, levels: int, norm: str, key: int,
                 resid=None, key_tensor=None):
     C = require()
-    _check_bucket(dp, grad)
+    ptrs = grad_pointers(dp, grad)
     _check(payload, torch.uint8, "payload")
     if payload.numel() < layout.nbytes:
         raise ValueError("payload too small")
@@ -144,7 +196,7 @@ def qsgd_encode(dp: DevicePlan, grad, payload, layout, levels: int, norm: str, k
         _check_bucket(dp, resid, "resid")
     if not (1 <= levels <= (127 if layout.bits == 8 else 7)):
         raise ValueError(f"levels={levels} does not fit {layout.bits}-bit codes")
-    C.qsgd_encode(_ptr(grad), _ptr(resid), _ptr(dp.chunks), _ptr(dp.tensors), _ptr(dp.scratch),
+    C.qsgd_encode(ptrs, _ptr(resid), _ptr(dp.chunks), _ptr(dp.tensors), _ptr(dp.scratch),
                   _ptr(payload), layout.nbytes, dp.plan.num_tensors, dp.plan.num_chunks,
                   layout.scales, layout.codes, layout.bits, 1 if norm == "l2" else 0,
                   float(levels), float(1.0 / levels), key & 0xFFFFFFFF,
@@ -205,6 +257,22 @@ def adam_flat(param, exp_avg, exp_avg_sq, max_exp_avg_sq, grad, lr_step, beta1, 
     C.adam_flat(_ptr(param), _ptr(exp_avg), _ptr(exp_avg_sq), _ptr(max_exp_avg_sq), _ptr(grad),
                 n, _GDT[grad.dtype], lr_step, beta1, beta2, eps, weight_decay, grad_scale,
                 int(amsgrad), _stream())
+
+
+_DDT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
+
+
+def pack_grads(dp, grads, dst, scale=1.0):
+    """Gather the bucket's per-tensor gradients into the flat ``dst`` (fp32/bf16/fp16), * scale."""
+    C = require()
+    ptrs = grad_pointers(dp, grads)
+    if dst.dtype not in _DDT:
+        raise TypeError("dst must be fp32, bf16 or fp16")
+    _check(dst, dst.dtype, "dst", align=8)
+    if dst.numel() < dp.plan.length:
+        raise ValueError("dst too small for the bucket")
+    C.pack_grads(ptrs, dp.plan.num_tensors, _ptr(dp.chunks), dp.plan.num_chunks, _ptr(dst),
+                 _DDT[dst.dtype], float(scale), _stream())
 
 
 def cast_scale(src, dst, scale=1.0):

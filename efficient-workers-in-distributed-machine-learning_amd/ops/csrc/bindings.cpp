@@ -4,6 +4,9 @@
 // current hipStream_t of torch (so every launch is ordered on, and graph-capturable from, the
 // caller's stream).
 #include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <vector>
 
 #include "ewdml_ops.h"
 
@@ -17,12 +20,14 @@ PYBIND11_MODULE(_C, m) {
   m.def("qsgd_scratch_bytes", &ew_qsgd_scratch_bytes);
 
   m.def("topk_encode",
-        [](uintptr_t grad, uintptr_t resid, uintptr_t chunks, uintptr_t tensors, uintptr_t scratch,
+        [](const std::vector<uintptr_t>& grads, uintptr_t resid, uintptr_t chunks,
+           uintptr_t tensors, uintptr_t scratch,
            uintptr_t payload, long long payload_bytes, int T, int C, int scales_off,
            int counts_off, int idx_off, int codes_off, int value_kind, int norm_l2, float levels,
            float inv_levels, uint32_t key, uint32_t bucket_offset, uintptr_t key_ptr,
            uintptr_t stream) {
-          TopkEncodeArgs a{grad,         resid,      chunks,     tensors,  scratch,   payload,
+          TopkEncodeArgs a{grads.data(), (int)grads.size(),
+                           resid,      chunks,     tensors,  scratch,   payload,
                            stream,       payload_bytes, T,       C,        scales_off, counts_off,
                            idx_off,      codes_off,  value_kind, norm_l2,  levels,    inv_levels,
                            key,          bucket_offset, key_ptr};
@@ -44,11 +49,13 @@ PYBIND11_MODULE(_C, m) {
         });
 
   m.def("qsgd_encode",
-        [](uintptr_t grad, uintptr_t resid, uintptr_t chunks, uintptr_t tensors, uintptr_t scratch,
+        [](const std::vector<uintptr_t>& grads, uintptr_t resid, uintptr_t chunks,
+           uintptr_t tensors, uintptr_t scratch,
            uintptr_t payload, long long payload_bytes, int T, int C, int scales_off, int codes_off,
            int bits, int norm_l2, float levels, float inv_levels, uint32_t key,
            uint32_t bucket_offset, uintptr_t key_ptr, uintptr_t stream) {
-          QsgdEncodeArgs a{grad,      resid,   chunks,        tensors,   scratch, payload, stream,
+          QsgdEncodeArgs a{grads.data(), (int)grads.size(),
+                           resid,   chunks,        tensors,   scratch, payload, stream,
                            payload_bytes, T,   C,             scales_off, codes_off, bits, norm_l2,
                            levels,    inv_levels, key,        bucket_offset, key_ptr};
           ew_qsgd_encode(a);
@@ -87,4 +94,10 @@ PYBIND11_MODULE(_C, m) {
         });
 
   m.def("cast_scale", &ew_cast_scale);
+  m.def("pack_grads",
+        [](const std::vector<uintptr_t>& grads, int T, uintptr_t chunks, int C, uintptr_t dst,
+           int dst_dtype, float scale, uintptr_t stream) {
+          ew_pack_grads(grads.data(), (int)grads.size(), T, chunks, C, dst, dst_dtype, scale,
+                        stream);
+        });
 }

@@ -36,6 +36,24 @@ struct ChunkRow {  // mirrors BucketPlan.chunk_table()
   int tensor, start, len, local;
 };
 
+// Per-tensor gradient base pointers of one bucket, passed by value as a kernel argument so a
+// captured HIP graph keeps them (autograd's own gradient tensors are read in place: no copy into
+// a flat buffer, no accumulate-add).  Buckets hold at most EW_MAX_T tensors.
+#define EW_MAX_T 128
+struct GradPtrs {
+  float* p[EW_MAX_T];
+};
+__device__ __forceinline__ float* ew_chunk_src(const GradPtrs& gp, const ChunkRow& c) {
+  return gp.p[c.tensor] + (size_t)c.local * EW_CHUNK;
+}
+inline void ew_fill_ptrs(GradPtrs& g, const uintptr_t* ptrs, int n, int T) {
+  if (n != T || T > EW_MAX_T)
+    throw std::runtime_error("ewdml: gradient pointer table has " + std::to_string(n) +
+                             " entries, bucket has " + std::to_string(T) + " tensors (max " +
+                             std::to_string(EW_MAX_T) + ")");
+  for (int i = 0; i < EW_MAX_T; ++i) g.p[i] = i < T ? reinterpret_cast<float*>(ptrs[i]) : nullptr;
+}
+
 struct SgdArgs {
   float lr, momentum, dampening, weight_decay, grad_scale;
   int nesterov, first;

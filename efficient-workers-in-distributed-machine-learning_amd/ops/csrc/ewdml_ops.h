@@ -5,7 +5,9 @@
 #include <stdint.h>
 
 struct TopkEncodeArgs {
-  uintptr_t grad, resid, chunks, tensors, scratch, payload, stream;
+  const uintptr_t* grad_ptrs;  // per-tensor gradient base pointers (host array, n_grad_ptrs)
+  int n_grad_ptrs;
+  uintptr_t resid, chunks, tensors, scratch, payload, stream;
   long long payload_bytes;
   int num_tensors, num_chunks;
   int scales_off, counts_off, idx_off, codes_off;
@@ -28,7 +30,9 @@ struct TopkDecodeArgs {
 };
 
 struct QsgdEncodeArgs {
-  uintptr_t grad, resid, chunks, tensors, scratch, payload, stream;
+  const uintptr_t* grad_ptrs;
+  int n_grad_ptrs;
+  uintptr_t resid, chunks, tensors, scratch, payload, stream;
   long long payload_bytes;
   int num_tensors, num_chunks;
   int scales_off, codes_off, bits, norm_l2;
@@ -73,6 +77,8 @@ void ew_qsgd_decode_apply(const QsgdDecodeArgs& a);
 
 void ew_sgd_flat(const SgdFlatArgs& a);
 void ew_adam_flat(const AdamFlatArgs& a);
+void ew_pack_grads(const uintptr_t* grad_ptrs, int n_ptrs, int num_tensors, uintptr_t chunks,
+                   int num_chunks, uintptr_t dst, int dst_dtype, float scale, uintptr_t stream);
 // dst (bf16 when to_bf16 else fp16) = src * scale
 void ew_cast_scale(uintptr_t src, uintptr_t dst, long long n, float scale, int to_bf16,
                    uintptr_t stream);

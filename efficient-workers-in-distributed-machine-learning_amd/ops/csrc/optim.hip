@@ -118,6 +118,38 @@ __global__ __launch_bounds__(EW_BLOCK) void k_cast_scale(const float* __restrict
   }
 }
 
+// Gather a bucket's per-tensor gradients into the flat (fp32 / bf16 / fp16) all-reduce buffer,
+// scaled -- one launch per bucket replaces per-parameter copies (dense codecs).
+__global__ __launch_bounds__(EW_BLOCK) void k_pack_grads(GradPtrs gp,
+                                                         const ChunkRow* __restrict__ chunks,
+                                                         void* __restrict__ dst, int dst_dtype,
+                                                         float scale) {
+  const ChunkRow c = chunks[blockIdx.x];
+  const float* src = ew_chunk_src(gp, c);
+  for (int i = 4 * threadIdx.x; i < c.len; i += 4 * EW_BLOCK) {
+    float y[4];
+    if (i + 3 < c.len) {
+      const float4 v = *reinterpret_cast<const float4*>(src + i);
+      y[0] = v.x * scale; y[1] = v.y * scale; y[2] = v.z * scale; y[3] = v.w * scale;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) y[j] = (i + j < c.len) ? src[i + j] * scale : 0.0f;
+    }
+    const long long o = (long long)c.start + i;
+    if (dst_dtype == 0) {
+      float* d = reinterpret_cast<float*>(dst) + o;
+      if (i + 3 < c.len) *reinterpret_cast<float4*>(d) = make_float4(y[0], y[1], y[2], y[3]);
+      else for (int j = 0; j < 4 && i + j < c.len; ++j) d[j] = y[j];
+    } else if (dst_dtype == 1) {
+      uint16_t* d = reinterpret_cast<uint16_t*>(dst) + o;
+      for (int j = 0; j < 4 && i + j < c.len; ++j) d[j] = ew_f32_to_bf16(y[j]);
+    } else {
+      __half* d = reinterpret_cast<__half*>(dst) + o;
+      for (int j = 0; j < 4 && i + j < c.len; ++j) d[j] = __float2half(y[j]);
+    }
+  }
+}
+
 inline int ew_grid(long long n4) {
   long long b = (n4 + EW_BLOCK - 1) / EW_BLOCK;
   return (int)(b < 2048 ? (b > 0 ? b : 1) : 2048);  // 8 blocks per CU, grid-stride the rest
@@ -156,6 +188,16 @@ void ew_adam_flat(const AdamFlatArgs& a) {
     hipLaunchKernelGGL(k_adam_flat<1>, dim3(ew_grid(n4)), dim3(EW_BLOCK), 0, s, p, m, v, vm, g, n4, aa);
   else
     hipLaunchKernelGGL(k_adam_flat<2>, dim3(ew_grid(n4)), dim3(EW_BLOCK), 0, s, p, m, v, vm, g, n4, aa);
+  EW_CHECK_LAUNCH();
+}
+
+void ew_pack_grads(const uintptr_t* grad_ptrs, int n_ptrs, int num_tensors, uintptr_t chunks,
+                   int num_chunks, uintptr_t dst, int dst_dtype, float scale, uintptr_t stream) {
+  GradPtrs g;
+  ew_fill_ptrs(g, grad_ptrs, n_ptrs, num_tensors);
+  hipLaunchKernelGGL(k_pack_grads, dim3(num_chunks), dim3(EW_BLOCK), 0, (hipStream_t)stream, g,
+                     reinterpret_cast<const ChunkRow*>(chunks), reinterpret_cast<void*>(dst),
+                     dst_dtype, scale);
   EW_CHECK_LAUNCH();
 }
 

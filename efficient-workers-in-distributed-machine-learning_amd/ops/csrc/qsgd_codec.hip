@@ -11,14 +11,14 @@
 namespace {
 
 template <bool EF>
-__global__ __launch_bounds__(EW_BLOCK) void k_qsgd_stats(float* __restrict__ g,
+__global__ __launch_bounds__(EW_BLOCK) void k_qsgd_stats(GradPtrs gp,
                                                          const float* __restrict__ resid,
                                                          const ChunkRow* __restrict__ chunks,
                                                          float* __restrict__ chunk_sq,
                                                          uint32_t* __restrict__ maxkey) {
   __shared__ float wsf[EW_WAVES];
   const ChunkRow c = chunks[blockIdx.x];
-  float* src = g + c.start;
+  float* src = ew_chunk_src(gp, c);
   float sq = 0.0f;
   uint32_t km = 0;
   for (int i = 4 * threadIdx.x; i < c.len; i += 4 * EW_BLOCK) {
@@ -62,14 +62,14 @@ __global__ __launch_bounds__(EW_BLOCK) void k_qsgd_scale(const TensorRow* __rest
 
 template <int BITS, bool EF>
 __global__ __launch_bounds__(EW_BLOCK) void k_qsgd_quant(
-    const float* __restrict__ g, float* __restrict__ resid, const ChunkRow* __restrict__ chunks,
+    GradPtrs gp, float* __restrict__ resid, const ChunkRow* __restrict__ chunks,
     const TensorRow* __restrict__ tensors, const float* __restrict__ inv_arr,
     uint8_t* __restrict__ payload, int scales_off, int codes_off, float levels, float inv_levels,
     uint32_t key_arg, const uint32_t* __restrict__ keyp, uint32_t bucket_offset) {
   const uint32_t key = keyp ? *keyp : key_arg;
   const ChunkRow c = chunks[blockIdx.x];
   const TensorRow tr = tensors[c.tensor];
-  const float* src = g + c.start;
+  const float* src = ew_chunk_src(gp, c);
   const float inv = inv_arr[c.tensor];
   const float step = reinterpret_cast<const float*>(payload + scales_off)[c.tensor] * inv_levels;
   const uint32_t gbase = bucket_offset + (uint32_t)c.start;
@@ -174,7 +174,8 @@ void ew_qsgd_encode(const QsgdEncodeArgs& a) {
   float* inv = chunk_sq + C;
   hipStream_t s = (hipStream_t)a.stream;
   EW_CHECK(hipMemsetAsync(reinterpret_cast<void*>(a.scratch), 0, ew_qsgd_scratch_bytes(T, C), s));
-  float* g = reinterpret_cast<float*>(a.grad);
+  GradPtrs g;
+  ew_fill_ptrs(g, a.grad_ptrs, a.n_grad_ptrs, T);
   float* resid = reinterpret_cast<float*>(a.resid);
   auto* pay = reinterpret_cast<uint8_t*>(a.payload);
   if (resid)

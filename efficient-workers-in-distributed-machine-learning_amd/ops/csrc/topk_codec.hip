@@ -28,16 +28,19 @@ constexpr int NB2 = 1024;  // pass-2 digit: key bits [9:0]
 
 // state[t] = {prefix, k_rem, max_key, pad}
 template <bool EF>
-__global__ __launch_bounds__(EW_BLOCK) void k_topk_hist0(float* __restrict__ g,
+__global__ __launch_bounds__(EW_BLOCK) void k_topk_hist0(GradPtrs gp,
                                                          float* __restrict__ resid,
                                                          const ChunkRow* __restrict__ chunks,
                                                          uint32_t* __restrict__ hist,
                                                          uint32_t* __restrict__ state) {
-  __shared__ uint32_t h[NB0];
-  for (int i = threadIdx.x; i < NB0; i += EW_BLOCK) h[i] = 0;
+  // one private histogram per wave: gradients cluster in a few exponent bins, and four waves
+  // hammering the same LDS words serialise; the waves' copies are summed at the flush
+  __shared__ uint32_t hw[EW_WAVES][NB0];
+  for (int i = threadIdx.x; i < EW_WAVES * NB0; i += EW_BLOCK) (&hw[0][0])[i] = 0;
   __syncthreads();
+  uint32_t* h = hw[threadIdx.x >> 6];
   const ChunkRow c = chunks[blockIdx.x];
-  float* src = g + c.start;
+  float* src = ew_chunk_src(gp, c);
   uint32_t kmax = 0;
   const int n4 = c.len >> 2;
   for (int i = threadIdx.x; i < n4; i += EW_BLOCK) {
@@ -68,13 +71,17 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_hist0(float* __restrict__ g,
   if ((threadIdx.x & 63) == 0) atomicMax(&state[c.tensor * 4 + 2], kmax);
   __syncthreads();
   uint32_t* dst = hist + (size_t)c.tensor * NB0;
-  for (int i = threadIdx.x; i < NB0; i += EW_BLOCK)
-    if (h[i]) atomicAdd(&dst[i], h[i]);
+  for (int i = threadIdx.x; i < NB0; i += EW_BLOCK) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int w = 0; w < EW_WAVES; ++w) v += hw[w][i];
+    if (v) atomicAdd(&dst[i], v);
+  }
 }
 
 // Histogram of key bits [SHIFT+9 : SHIFT] over elements whose bits above MATCH equal the prefix.
 template <int SHIFT, int MATCH>
-__global__ __launch_bounds__(EW_BLOCK) void k_topk_hist(const float* __restrict__ g,
+__global__ __launch_bounds__(EW_BLOCK) void k_topk_hist(GradPtrs gp,
                                                         const ChunkRow* __restrict__ chunks,
                                                         const uint32_t* __restrict__ state,
                                                         uint32_t* __restrict__ hist) {
@@ -82,7 +89,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_hist(const float* __restrict_
   for (int i = threadIdx.x; i < NB1; i += EW_BLOCK) h[i] = 0;
   __syncthreads();
   const ChunkRow c = chunks[blockIdx.x];
-  const float* src = g + c.start;
+  const float* src = ew_chunk_src(gp, c);
   const uint32_t want = state[c.tensor * 4] >> MATCH;
   const int n4 = c.len >> 2;
   for (int i = threadIdx.x; i < n4; i += EW_BLOCK) {
@@ -137,7 +144,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_select(const uint32_t* __rest
 }
 
 // Per chunk: #(key > thr), #(key == thr) and sum of squares of the key > thr values.
-__global__ __launch_bounds__(EW_BLOCK) void k_topk_count(const float* __restrict__ g,
+__global__ __launch_bounds__(EW_BLOCK) void k_topk_count(GradPtrs gp,
                                                          const ChunkRow* __restrict__ chunks,
                                                          const uint32_t* __restrict__ state,
                                                          uint32_t* __restrict__ cnt_gt,
@@ -145,7 +152,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_count(const float* __restrict
                                                          float* __restrict__ chunk_sq) {
   __shared__ float wsf[EW_WAVES];
   const ChunkRow c = chunks[blockIdx.x];
-  const float* src = g + c.start;
+  const float* src = ew_chunk_src(gp, c);
   const uint32_t thr = state[c.tensor * 4];
   uint32_t gt = 0, eq = 0;
   float sq = 0.0f;
@@ -247,7 +254,7 @@ enum ValueKind { VK_Q8 = 0, VK_Q4 = 1, VK_F32 = 2 };
 // Ordered stream compaction of the selected entries of one chunk + fused quantisation.
 template <int VK, bool EF>
 __global__ __launch_bounds__(EW_BLOCK) void k_topk_write(
-    const float* __restrict__ g, float* __restrict__ resid, const ChunkRow* __restrict__ chunks,
+    GradPtrs gp, float* __restrict__ resid, const ChunkRow* __restrict__ chunks,
     const TensorRow* __restrict__ tensors, const uint32_t* __restrict__ state,
     const uint32_t* __restrict__ chunk_off, const uint32_t* __restrict__ chunk_ties,
     const float* __restrict__ inv_arr, uint8_t* __restrict__ payload, int scales_off, int idx_off,
@@ -257,7 +264,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_write(
   const uint32_t key = keyp ? *keyp : key_arg;  // device key: fresh per replay of a captured graph
   const ChunkRow c = chunks[blockIdx.x];
   const TensorRow tr = tensors[c.tensor];
-  const float* src = g + c.start;
+  const float* src = ew_chunk_src(gp, c);
   const uint32_t thr = state[c.tensor * 4];
   const uint32_t ties = chunk_ties[blockIdx.x];
   const uint32_t ebase = (uint32_t)tr.entry0 + chunk_off[blockIdx.x];
@@ -382,7 +389,24 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_decode_apply(
   float* p = param + c.start;
   float* b = mom + c.start;
   float* go = grad_out ? grad_out + c.start : nullptr;
-  for (int i = threadIdx.x; i < c.len; i += EW_BLOCK) {
+  // chunk starts are 64-element aligned: float4 body + scalar tail
+  const int n4 = c.len >> 2;
+  for (int i = threadIdx.x; i < n4; i += EW_BLOCK) {
+    const float4 a = acc4[i];
+    const float4 gv = make_float4(a.x * inv_n, a.y * inv_n, a.z * inv_n, a.w * inv_n);
+    if (go) reinterpret_cast<float4*>(go)[i] = gv;
+    if (apply) {
+      float4 pv = reinterpret_cast<float4*>(p)[i];
+      float4 bv = reinterpret_cast<float4*>(b)[i];
+      ew_sgd(pv.x, bv.x, gv.x, sa);
+      ew_sgd(pv.y, bv.y, gv.y, sa);
+      ew_sgd(pv.z, bv.z, gv.z, sa);
+      ew_sgd(pv.w, bv.w, gv.w, sa);
+      reinterpret_cast<float4*>(p)[i] = pv;
+      reinterpret_cast<float4*>(b)[i] = bv;
+    }
+  }
+  for (int i = (n4 << 2) + threadIdx.x; i < c.len; i += EW_BLOCK) {
     const float gv = acc[i] * inv_n;
     if (go) go[i] = gv;
     if (apply) {
@@ -422,7 +446,8 @@ void ew_topk_encode(const TopkEncodeArgs& a) {
   hipStream_t s = (hipStream_t)a.stream;
   EW_CHECK(hipMemsetAsync(scratch, 0, ew_topk_scratch_bytes(T, C), s));
   EW_CHECK(hipMemsetAsync(reinterpret_cast<void*>(a.payload), 0, a.payload_bytes, s));
-  float* g = reinterpret_cast<float*>(a.grad);
+  GradPtrs g;
+  ew_fill_ptrs(g, a.grad_ptrs, a.n_grad_ptrs, T);
   float* resid = reinterpret_cast<float*>(a.resid);
   if (resid)
     EW_LAUNCH(k_topk_hist0<true>, C, s, g, resid, chunks, hist0, state);

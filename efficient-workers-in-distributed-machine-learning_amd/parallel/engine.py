@@ -62,6 +62,10 @@ class GradientExchange:
                 self.recv.append(torch.zeros(self.N * P, dtype=torch.uint8, device=self.device))
                 self.send.append(None)
         self.resid = torch.zeros_like(flat.grad) if (error_feedback and not codec.allreduce) else None
+        if not flat.attach_grads and not self.cuda:
+            raise ValueError("pointer-mode gradients need the HIP kernels (device tensors)")
+        self._pack_plans = [ops.DevicePlan(b.plan, self.device) for b in flat.buckets] \
+            if (codec.allreduce and not flat.attach_grads) else None
         self.overlap = overlap
         self.side = torch.cuda.Stream(device=self.device) if (self.cuda and overlap) else None
         self._bucket_of = flat.bucket_of()
@@ -139,9 +143,12 @@ class GradientExchange:
 
     def _encode(self, bi: int):
         b = self.flat.buckets[bi]
-        g = self.flat.grad_view(b)
+        g = self.flat.bucket_grads(b)
         if self.codec.allreduce:
-            if self.send[bi] is None:
+            dst = self.flat.grad_view(b) if self.send[bi] is None else self.send[bi]
+            if not self.flat.attach_grads:  # one gather(+cast) kernel from autograd's tensors
+                ops.pack_grads(self._pack_plans[bi], g, dst, 1.0 / self.predivide)
+            elif self.send[bi] is None:
                 if self.predivide != 1.0:
                     g.mul_(1.0 / self.predivide)
             elif self.cuda:

@@ -38,9 +38,18 @@ class Bucket:
     plan: BucketPlan
 
 
+MAX_TENSORS_PER_BUCKET = 128  # kernel pointer-table capacity (ops.MAX_TENSORS_PER_BUCKET)
+
+
 class FlatModel:
-    def __init__(self, model, bucket_bytes: int = 8 << 20, reverse: bool = True):
-        """``model``: an ``nn.Module`` or an iterable of parameters."""
+    def __init__(self, model, bucket_bytes: int = 8 << 20, reverse: bool = True,
+                 attach_grads: bool = True):
+        """``model``: an ``nn.Module`` or an iterable of parameters.
+
+        ``attach_grads=True``: every ``p.grad`` is a view of ``self.grad`` and autograd accumulates
+        into it.  ``False``: ``p.grad`` is left to autograd (``zero_grad`` sets it to None, so the
+        incoming gradient is stolen, not added) and the exchange reads each tensor in place
+        through a pointer table -- no per-parameter accumulate kernels, no buffer fill."""
         seen = set()
         params = []
         plist = model.parameters() if isinstance(model, torch.nn.Module) else model
@@ -63,6 +72,7 @@ class FlatModel:
         self.offsets = offs
         self.numel = total
         self.param_numel = sum(p.numel() for p in params)
+        self.attach_grads = attach_grads
         self.data = torch.zeros(total, dtype=torch.float32, device=dev)
         self.grad = torch.zeros(total, dtype=torch.float32, device=dev)
         for p, o in zip(params, offs):
@@ -73,7 +83,7 @@ class FlatModel:
             dv = self.data[o:o + n].as_strided(p.shape, p.stride())
             dv.copy_(p.data)
             p.data = dv
-            p.grad = self.grad[o:o + n].as_strided(p.shape, p.stride())
+            p.grad = self.grad[o:o + n].as_strided(p.shape, p.stride()) if attach_grads else None
         self.buckets = self._make_buckets(bucket_bytes)
 
     def _make_buckets(self, bucket_bytes):
@@ -82,7 +92,7 @@ class FlatModel:
         for i, p in enumerate(self.params):
             cur.append(i)
             end = self.offsets[i] + _align(p.numel())
-            if end - self.offsets[cur[0]] >= cap:
+            if end - self.offsets[cur[0]] >= cap or len(cur) >= MAX_TENSORS_PER_BUCKET:
                 groups.append(cur)
                 cur = []
         if cur:
@@ -108,7 +118,28 @@ class FlatModel:
         return self.data[b.start:b.start + b.length]
 
     def zero_grad(self):
-        self.grad.zero_()
+        if self.attach_grads:
+            self.grad.zero_()
+        else:
+            for p in self.params:
+                p.grad = None
+
+    def bucket_grads(self, b: Bucket):
+        """The bucket's gradients: the flat view, or (pointer mode) autograd's tensors in plan
+        order (unused parameters contribute zeros)."""
+        if self.attach_grads:
+            return self.grad_view(b)
+        out = []
+        for p in b.params:
+            g = p.grad
+            if g is None:
+                g = torch.zeros_like(p, memory_format=torch.contiguous_format)
+                p.grad = g
+            elif not g.is_contiguous() or g.dtype != torch.float32:
+                g = g.to(torch.float32).contiguous()
+                p.grad = g
+            out.append(g)
+        return out
 
     def reattach_grads(self):
         """Restore the ``.grad`` views (e.g. after user code set them to None)."""

@@ -51,11 +51,19 @@ class Trainer:
     def __init__(self, cfg: Config, comm: Comm = None):
         self.cfg = cfg = cfg.resolved()
         self.device = resolve_device(cfg)
-        self.comm = comm or init_distributed(timeout_s=cfg.comm_timeout,
+        # straggler mode 'kill' (distributed_nn.py:50-53): a rank that stalls longer than
+        # --kill-threshold seconds in a collective aborts the job instead of hanging it
+        timeout = cfg.kill_threshold if cfg.mode == "kill" else cfg.comm_timeout
+        self.comm = comm or init_distributed(timeout_s=timeout,
                                              device=self.device if self.device.type == "cuda"
                                              else None)
         self.rank, self.world = self.comm.rank, self.comm.world
         self.cuda = self.device.type == "cuda"
+        if cfg.sync_debug:
+            from .. import ops
+            ops.set_sync_debug(True)
+            if cfg.hip_graph != "off":
+                raise ValueError("--sync-debug synchronises after each launch: use --hip-graph off")
         torch.manual_seed(cfg.seed)
         if self.cuda:  # MIOpen find once per shape during warmup (EWDML_CUDNN_BENCHMARK=0: heuristics)
             torch.backends.cudnn.benchmark = os.environ.get("EWDML_CUDNN_BENCHMARK", "1") == "1"
@@ -93,7 +101,12 @@ class Trainer:
         if cfg.channels_last:
             model = model.to(memory_format=torch.channels_last)
         self.model = model
-        self.flat = FlatModel(model, bucket_bytes=int(cfg.bucket_mb * (1 << 20)))
+        # pointer-mode gradients (read in place by the HIP kernels) when the exchange is the plain
+        # all-to-all one; PS / local SGD keep flat gradient views (they step on the local grad)
+        ptr_grads = (self.cuda and cfg.topology == "allgather" and cfg.sync_every == 1
+                     and not cfg.select_best and os.environ.get("EWDML_GRAD_VIEWS") != "1")
+        self.flat = FlatModel(model, bucket_bytes=int(cfg.bucket_mb * (1 << 20)),
+                              attach_grads=not ptr_grads)
         sync_params(self.flat, self.comm)
         sync_buffers(model, self.comm)
         lr = cfg.lr * (n_workers if cfg.lr_scale_world else 1)
@@ -122,6 +135,10 @@ class Trainer:
         if self.graph_mode != "off" and not isinstance(self.exchange, GradientExchange):
             raise ValueError("--hip-graph needs the all-to-all topology without local SGD")
         self._graphs = None
+        # Graph mode: warmup, capture and replay all run on ONE dedicated stream, so MIOpen /
+        # hipBLASLt create their per-stream handles and workspaces during the eager warmup and not
+        # inside the capture (lazy per-stream init inside a capture crashes capture_end).
+        self.gstream = torch.cuda.Stream(device=self.device) if self.graph_mode != "off" else None
         self.step = 0
         self.epoch = 0
         self.fault = None
@@ -148,8 +165,23 @@ class Trainer:
         loss.backward()
         return loss, out
 
+    def stream_ctx(self):
+        """Context of the stream the training step runs on (the graph stream in graph mode)."""
+        if self.gstream is None:
+            return contextlib.nullcontext()
+        return torch.cuda.stream(self.gstream)
+
     def train_step(self, x=None, y=None):
         """One synchronous step.  Returns (loss tensor, logits) (server: (None, None))."""
+        if self.gstream is None:
+            return self._train_step(x, y)
+        self.gstream.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(self.gstream):
+            out = self._train_step(x, y)
+        torch.cuda.current_stream().wait_stream(self.gstream)
+        return out
+
+    def _train_step(self, x=None, y=None):
         if self.fault is not None and self.fault == (self.rank, self.step):
             raise FaultInjected(f"injected fault on rank {self.rank} at step {self.step}")
         if self.is_server:
@@ -162,7 +194,7 @@ class Trainer:
         self.model.train()
         if self.graph_mode != "off" and self.step >= self.cfg.graph_warmup:
             if self._graphs is None and not self._try_capture(x, y):
-                return self.train_step(x, y)  # capture failed on some rank: all run eager
+                return self._train_step(x, y)  # capture failed on some rank: all run eager
             return self._graph_step(x, y)
         loss, out = self.forward_backward(x, y)
         self.exchange.finish()
@@ -206,20 +238,21 @@ class Trainer:
         torch.cuda.synchronize()
         if self.graph_mode == "full":
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, capture_error_mode=mode):
+            with torch.cuda.graph(g, stream=self.gstream, capture_error_mode=mode):
                 loss, out = self.forward_backward(self._gx, self._gy)
                 ex.finish()
             self._graphs = (g,)
         else:
             ex.defer_comm = True
             ga = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(ga, capture_error_mode=mode):
+            with torch.cuda.graph(ga, stream=self.gstream, capture_error_mode=mode):
                 loss, out = self.forward_backward(self._gx, self._gy)
                 ex.launch_pending()
                 ex.join_side()
             ex._active = False
             gb = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(gb, pool=ga.pool(), capture_error_mode=mode):
+            with torch.cuda.graph(gb, pool=ga.pool(), stream=self.gstream,
+                                  capture_error_mode=mode):
                 ex.apply()
             self._graphs = (ga, gb)
         ex.step_idx, self.opt.steps = saved
@@ -360,6 +393,10 @@ class Trainer:
                     a1, a5 = accuracy(out.float(), y, (1, 5))
                     rec.update(loss=float(loss.detach()), acc1=float(a1), acc5=float(a5))
                 rec["step_ms"] = sw.phases().get("step")
+                if self.world > 1:  # straggler report: slowest / fastest rank's step time
+                    mx, mn = self.comm.all_reduce_scalars([rec["step_ms"] or 0.0], op="max")[0], \
+                        -self.comm.all_reduce_scalars([-(rec["step_ms"] or 0.0)], op="max")[0]
+                    rec["step_ms_max"], rec["step_ms_min"] = mx, mn
                 rec.update(byte_summary(self.exchange.last, self.world))
                 rec["images_per_sec_rank"] = (cfg.batch_size * 1e3 / rec["step_ms"]
                                               if rec["step_ms"] else None)

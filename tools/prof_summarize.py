@@ -26,10 +26,18 @@ def load(d):
 
 
 def short(name):
-    n = name.split("(")[0]
-    for pre in ("void ", "__omp"):
-        n = n.replace(pre, "")
-    return n[:110]
+    n = name.replace("(anonymous namespace)::", "").replace("void ", "")
+    # drop the argument list (first "(" not inside a template) but keep template args
+    depth, cut = 0, len(n)
+    for i, ch in enumerate(n):
+        if ch == "<":
+            depth += 1
+        elif ch == ">":
+            depth -= 1
+        elif ch == "(" and depth == 0 and i > 0:
+            cut = i
+            break
+    return n[:cut][:110] or name[:110]
 
 
 def summarize(rows, frac=0.5, gap_ns=150_000_000, steps=None):
