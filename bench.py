@@ -59,6 +59,7 @@ def parse(argv=None):
     p.add_argument("--no-overlap", action="store_true")
     p.add_argument("--error-feedback", action="store_true")
     p.add_argument("--hip-graph", default="full", choices=["off", "split", "full"])
+    p.add_argument("--param-dtype", default="auto", choices=["auto", "fp32"])
     p.add_argument("--extra", default="", help="extra distributed_nn.py flags")
     a = p.parse_args(argv)
     pre = {"batch_size": 128, **PRESETS[a.preset]}
@@ -96,7 +97,8 @@ def main(argv=None):
         flags.append("--error-feedback")
     # graph capture happens inside the untimed warmup: eager steps, then the capturing step
     gw = max(1, min(3, a.warmup - 1))
-    flags += ["--hip-graph", a.hip_graph, "--graph-warmup", str(gw)]
+    flags += ["--hip-graph", a.hip_graph, "--graph-warmup", str(gw), "--param-dtype",
+              a.param_dtype]
     flags += a.extra.split()
     cfg = ewdml.parse_args(flags, prog="bench.py")
     tr = Trainer(cfg)
@@ -152,7 +154,9 @@ def main(argv=None):
                    "seq_len": None, "parallelism": f"dp{world}",
                    "codec": tr.exchange.codec.describe() if hasattr(tr.exchange, "codec") else
                    a.compress, "optimizer": "sgd(momentum=0.9)", "overlap": not a.no_overlap,
-                   "buckets": len(tr.flat.buckets), "hip_graph": tr.graph_mode},
+                   "buckets": len(tr.flat.buckets), "hip_graph": tr.graph_mode,
+                   "bf16_params": tr.flat.shadow is not None,
+                   "grad_mode": "views" if tr.flat.attach_grads else "pointers"},
         "grad_bytes_per_step_on_wire": bytes_["wire_bytes_total"],
         "payload_bytes_per_rank": bytes_["payload_bytes_per_rank"],
         "dense_fp32_grad_bytes": bytes_["dense_fp32_bytes"],

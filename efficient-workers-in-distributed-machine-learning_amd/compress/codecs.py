@@ -124,7 +124,7 @@ class Codec:
         out[:plan.length].copy_(oracle.decode_sum(recv, plan, lay, self.levels, scale))
 
     def decode_apply_sgd(self, b: int, recv: torch.Tensor, scale: float, param: torch.Tensor,
-                         mom: torch.Tensor, hp: dict, first: bool, grad_out=None):
+                         mom: torch.Tensor, hp: dict, first: bool, grad_out=None, shadow=None):
         """Fused decode -> average -> SGD step of bucket ``b`` (one kernel on the GPU)."""
         plan, lay = self.plans[b], self.layouts[b]
         if recv.is_cuda:
@@ -132,7 +132,7 @@ class Codec:
             fn(self.dplans[b], recv, lay, self.levels, param=param, mom=mom, grad_out=grad_out,
                lr=hp["lr"], momentum=hp["momentum"], dampening=hp["dampening"],
                weight_decay=hp["weight_decay"], grad_scale=scale, nesterov=hp["nesterov"],
-               first=first)
+               first=first, shadow=shadow)
             return
         g = oracle.decode_sum(recv, plan, lay, self.levels, scale)
         if grad_out is not None:

@@ -75,9 +75,14 @@ class Config:
     dampening: float = 0.0
     nesterov: bool = False
     lr_scale_world: bool = False  # Horovod: lr *= world size
+    lr_warmup_epochs: float = 0.0  # Horovod LearningRateWarmupCallback: lr/W -> lr linearly
+    lr_decay_epochs: str = ""  # e.g. "30,60,90": multiply lr by --lr-decay at these epochs
+    lr_decay: float = 0.1
     # ---- execution -------------------------------------------------------------------------------
     device: str = "auto"  # auto | cuda | cpu
     amp: str = "bf16"  # bf16 | fp16 | none  (autocast compute dtype; master weights fp32)
+    param_dtype: str = "auto"  # auto: conv/linear weights kept in bf16 (fp32 master) under bf16
+    #                            autocast on the GPU all-to-all path | fp32
     channels_last: bool = False
     hip_graph: str = "off"  # off | split (graphs around eager RCCL calls) | full (one graph)
     graph_warmup: int = 3  # eager steps (>= 1) before capture: MIOpen find, handles, momentum
@@ -92,6 +97,7 @@ class Config:
     eval_on_ckpt: bool = False
     metrics_file: Optional[str] = None  # per-step JSONL
     profile: int = 0  # wrap N steps in torch.profiler
+    roctx: bool = False  # roctx ranges per phase (rocprofv3 --marker-trace)
     inject_fault: Optional[str] = None  # "rank:step" -> that rank raises at that step (tests)
     comm_timeout: float = 600.0
     sync_debug: bool = False  # synchronise after every custom kernel (race / fault localisation)
@@ -181,9 +187,13 @@ def build_parser(prog="distributed_nn.py") -> argparse.ArgumentParser:
     a("--dampening", type=float, default=d.dampening)
     a("--nesterov", action="store_true", default=False)
     a("--lr-scale-world", action="store_true", default=False)
+    a("--lr-warmup-epochs", type=float, default=d.lr_warmup_epochs)
+    a("--lr-decay-epochs", type=str, default=d.lr_decay_epochs)
+    a("--lr-decay", type=float, default=d.lr_decay)
     # execution
     a("--device", type=str, default=d.device, choices=["auto", "cuda", "cpu"])
     a("--amp", type=str, default=d.amp, choices=["bf16", "fp16", "none"])
+    a("--param-dtype", type=str, default=d.param_dtype, choices=["auto", "fp32"])
     a("--channels-last", action="store_true", default=False)
     a("--hip-graph", type=str, default=d.hip_graph, choices=["off", "split", "full"])
     a("--graph-warmup", type=int, default=d.graph_warmup)
@@ -197,6 +207,7 @@ def build_parser(prog="distributed_nn.py") -> argparse.ArgumentParser:
     a("--eval-on-ckpt", action="store_true", default=False)
     a("--metrics-file", type=str, default=None)
     a("--profile", type=int, default=0)
+    a("--roctx", action="store_true", default=False)
     a("--inject-fault", type=str, default=None)
     a("--comm-timeout", type=float, default=d.comm_timeout)
     a("--sync-debug", action="store_true", default=False)

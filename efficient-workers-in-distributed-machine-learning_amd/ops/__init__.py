@@ -107,25 +107,37 @@ MAX_TENSORS_PER_BUCKET = 128  # EW_MAX_T in csrc/common.h
 
 
 def grad_pointers(dp, grad):
-    """Per-tensor gradient base pointers of a bucket.  ``grad`` is either the bucket's flat fp32
-    view (tensors at the plan offsets) or a list with one fp32 tensor per plan tensor (autograd's
-    own ``p.grad`` tensors, read in place)."""
+    """(pointers, bf16 bit mask) of a bucket's per-tensor gradients.  ``grad`` is the bucket's
+    flat fp32 view (tensors at the plan offsets) or a list with one fp32/bf16 tensor per plan
+    tensor (autograd's own ``p.grad`` tensors, read in place)."""
     plan = dp.plan
     if plan.num_tensors > MAX_TENSORS_PER_BUCKET:
         raise ValueError(f"bucket has {plan.num_tensors} tensors (max {MAX_TENSORS_PER_BUCKET})")
+    mask = [0] * (MAX_TENSORS_PER_BUCKET // 32)
     if torch.is_tensor(grad):
         _check_bucket(dp, grad)
         base = grad.data_ptr()
-        return [base + 4 * o for o in plan.offsets]
+        return [base + 4 * o for o in plan.offsets], mask
     if len(grad) != plan.num_tensors:
         raise ValueError(f"{len(grad)} gradients for a bucket of {plan.num_tensors} tensors")
     ptrs = []
-    for t, n in zip(grad, plan.numels):
-        _check(t, torch.float32, "grad tensor")
+    for i, (t, n) in enumerate(zip(grad, plan.numels)):
+        if t.dtype == torch.bfloat16:
+            _check(t, torch.bfloat16, "grad tensor", align=8)
+            mask[i >> 5] |= 1 << (i & 31)
+        else:
+            _check(t, torch.float32, "grad tensor")
         if t.numel() != n:
             raise ValueError(f"gradient has {t.numel()} elements, plan expects {n}")
         ptrs.append(t.data_ptr())
-    return ptrs
+    return ptrs, mask
+
+
+def _check_shadow(dp, shadow):
+    if shadow is not None:
+        _check(shadow, torch.bfloat16, "shadow", align=8)
+        if shadow.numel() < dp.plan.length:
+            raise ValueError("shadow too small for the bucket")
 
 
 def _keyp(key_tensor):
@@ -139,7 +151,7 @@ def _keyp(key_tensor):
 def topk_encode(dp: DevicePlan, grad, payload, layout, levels: int, norm: str, key: int,
                 resid=None, key_tensor=None):
     C = require()
-    ptrs = grad_pointers(dp, grad)
+    ptrs, mask = grad_pointers(dp, grad)
     _check(payload, torch.uint8, "payload")
     if payload.numel() < layout.nbytes:
         raise ValueError("payload too small")
@@ -153,7 +165,7 @@ def topk_encode(dp: DevicePlan, grad, payload, layout, levels: int, norm: str, k
         vk = VK_Q4
     if vk != VK_F32 and not (1 <= levels <= (127 if layout.bits == 8 else 7)):
         raise ValueError(f"levels={levels} does not fit {layout.bits}-bit codes")
-    C.topk_encode(ptrs, _ptr(resid), _ptr(dp.chunks), _ptr(dp.tensors), _ptr(dp.scratch),
+    C.topk_encode(ptrs, mask, _ptr(resid), _ptr(dp.chunks), _ptr(dp.tensors), _ptr(dp.scratch),
                   _ptr(payload), layout.nbytes, dp.plan.num_tensors, dp.plan.num_chunks,
                   layout.scales, layout.counts, layout.idx, layout.codes, vk,
                   1 if norm == "l2" else 0, float(levels), float(1.0 / levels), key & 0xFFFFFFFF,
@@ -162,7 +174,7 @@ def topk_encode(dp: DevicePlan, grad, payload, layout, levels: int, norm: str, k
 
 def topk_decode_apply(dp: DevicePlan, recv, layout, levels: int, param=None, mom=None,
                       grad_out=None, lr=0.0, momentum=0.0, dampening=0.0, weight_decay=0.0,
-                      grad_scale=1.0, nesterov=False, first=False):
+                      grad_scale=1.0, nesterov=False, first=False, shadow=None):
     C = require()
     _check(recv, torch.uint8, "recv")
     if recv.dim() != 2 or recv.shape[1] != layout.nbytes:
@@ -177,18 +189,19 @@ def topk_decode_apply(dp: DevicePlan, recv, layout, levels: int, param=None, mom
         _check_bucket(dp, grad_out, "grad_out")
     if not apply and grad_out is None:
         raise ValueError("nothing to do: pass param/mom and/or grad_out")
+    _check_shadow(dp, shadow)
     vk = VK_F32 if layout.kind == "topk" else (VK_Q8 if layout.bits == 8 else VK_Q4)
     C.topk_decode_apply(_ptr(recv), recv.shape[0], layout.nbytes, _ptr(dp.chunks),
                         _ptr(dp.tensors), dp.plan.num_chunks, layout.scales, layout.counts,
                         layout.idx, layout.codes, vk, float(1.0 / levels), _ptr(param), _ptr(mom),
-                        _ptr(grad_out), lr, momentum, dampening, weight_decay, grad_scale,
-                        int(nesterov), int(first), int(apply), _stream())
+                        _ptr(grad_out), _ptr(shadow), lr, momentum, dampening, weight_decay,
+                        grad_scale, int(nesterov), int(first), int(apply), _stream())
 
 
 def qsgd_encode(dp: DevicePlan, grad, payload, layout, levels: int, norm: str, key: int,
                 resid=None, key_tensor=None):
     C = require()
-    ptrs = grad_pointers(dp, grad)
+    ptrs, mask = grad_pointers(dp, grad)
     _check(payload, torch.uint8, "payload")
     if payload.numel() < layout.nbytes:
         raise ValueError("payload too small")
@@ -196,7 +209,7 @@ def qsgd_encode(dp: DevicePlan, grad, payload, layout, levels: int, norm: str, k
         _check_bucket(dp, resid, "resid")
     if not (1 <= levels <= (127 if layout.bits == 8 else 7)):
         raise ValueError(f"levels={levels} does not fit {layout.bits}-bit codes")
-    C.qsgd_encode(ptrs, _ptr(resid), _ptr(dp.chunks), _ptr(dp.tensors), _ptr(dp.scratch),
+    C.qsgd_encode(ptrs, mask, _ptr(resid), _ptr(dp.chunks), _ptr(dp.tensors), _ptr(dp.scratch),
                   _ptr(payload), layout.nbytes, dp.plan.num_tensors, dp.plan.num_chunks,
                   layout.scales, layout.codes, layout.bits, 1 if norm == "l2" else 0,
                   float(levels), float(1.0 / levels), key & 0xFFFFFFFF,
@@ -205,7 +218,7 @@ def qsgd_encode(dp: DevicePlan, grad, payload, layout, levels: int, norm: str, k
 
 def qsgd_decode_apply(dp: DevicePlan, recv, layout, levels: int, param=None, mom=None,
                       grad_out=None, lr=0.0, momentum=0.0, dampening=0.0, weight_decay=0.0,
-                      grad_scale=1.0, nesterov=False, first=False):
+                      grad_scale=1.0, nesterov=False, first=False, shadow=None):
     C = require()
     _check(recv, torch.uint8, "recv")
     if recv.dim() != 2 or recv.shape[1] != layout.nbytes:
@@ -218,18 +231,19 @@ def qsgd_decode_apply(dp: DevicePlan, recv, layout, levels: int, param=None, mom
         _check_bucket(dp, grad_out, "grad_out")
     if not apply and grad_out is None:
         raise ValueError("nothing to do: pass param/mom and/or grad_out")
+    _check_shadow(dp, shadow)
     C.qsgd_decode_apply(_ptr(recv), recv.shape[0], layout.nbytes, _ptr(dp.chunks),
                         _ptr(dp.tensors), dp.plan.num_chunks, layout.scales, layout.codes,
                         layout.bits, float(1.0 / levels), _ptr(param), _ptr(mom), _ptr(grad_out),
-                        lr, momentum, dampening, weight_decay, grad_scale, int(nesterov),
-                        int(first), int(apply), _stream())
+                        _ptr(shadow), lr, momentum, dampening, weight_decay, grad_scale,
+                        int(nesterov), int(first), int(apply), _stream())
 
 
 _GDT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
 
 
 def sgd_flat(param, mom, grad, lr, momentum=0.0, dampening=0.0, weight_decay=0.0,
-             grad_scale=1.0, nesterov=False, first=False):
+             grad_scale=1.0, nesterov=False, first=False, shadow=None):
     C = require()
     _check(param, torch.float32, "param")
     _check(mom, torch.float32, "mom")
@@ -239,12 +253,17 @@ def sgd_flat(param, mom, grad, lr, momentum=0.0, dampening=0.0, weight_decay=0.0
     n = param.numel()
     if mom.numel() != n or grad.numel() != n or n % 4:
         raise ValueError("param/mom/grad must have equal numel, a multiple of 4")
-    C.sgd_flat(_ptr(param), _ptr(mom), _ptr(grad), n, _GDT[grad.dtype], lr, momentum, dampening,
-               weight_decay, grad_scale, int(nesterov), int(first), _stream())
+    if shadow is not None:
+        _check(shadow, torch.bfloat16, "shadow", align=8)
+        if shadow.numel() != n:
+            raise ValueError("shadow must match param")
+    C.sgd_flat(_ptr(param), _ptr(mom), _ptr(grad), _ptr(shadow), n, _GDT[grad.dtype], lr,
+               momentum, dampening, weight_decay, grad_scale, int(nesterov), int(first),
+               _stream())
 
 
 def adam_flat(param, exp_avg, exp_avg_sq, max_exp_avg_sq, grad, lr_step, beta1, beta2, eps,
-              weight_decay=0.0, grad_scale=1.0, amsgrad=False):
+              weight_decay=0.0, grad_scale=1.0, amsgrad=False, shadow=None):
     C = require()
     for t, nm in ((param, "param"), (exp_avg, "exp_avg"), (exp_avg_sq, "exp_avg_sq")):
         _check(t, torch.float32, nm)
@@ -254,9 +273,13 @@ def adam_flat(param, exp_avg, exp_avg_sq, max_exp_avg_sq, grad, lr_step, beta1, 
     n = param.numel()
     if n % 4 or grad.numel() != n or exp_avg.numel() != n or exp_avg_sq.numel() != n:
         raise ValueError("flat buffers must have equal numel, a multiple of 4")
+    if shadow is not None:
+        _check(shadow, torch.bfloat16, "shadow", align=8)
+        if shadow.numel() != n:
+            raise ValueError("shadow must match param")
     C.adam_flat(_ptr(param), _ptr(exp_avg), _ptr(exp_avg_sq), _ptr(max_exp_avg_sq), _ptr(grad),
-                n, _GDT[grad.dtype], lr_step, beta1, beta2, eps, weight_decay, grad_scale,
-                int(amsgrad), _stream())
+                _ptr(shadow), n, _GDT[grad.dtype], lr_step, beta1, beta2, eps, weight_decay,
+                grad_scale, int(amsgrad), _stream())
 
 
 _DDT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
@@ -265,13 +288,13 @@ _DDT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
 def pack_grads(dp, grads, dst, scale=1.0):
     """Gather the bucket's per-tensor gradients into the flat ``dst`` (fp32/bf16/fp16), * scale."""
     C = require()
-    ptrs = grad_pointers(dp, grads)
+    ptrs, mask = grad_pointers(dp, grads)
     if dst.dtype not in _DDT:
         raise TypeError("dst must be fp32, bf16 or fp16")
     _check(dst, dst.dtype, "dst", align=8)
     if dst.numel() < dp.plan.length:
         raise ValueError("dst too small for the bucket")
-    C.pack_grads(ptrs, dp.plan.num_tensors, _ptr(dp.chunks), dp.plan.num_chunks, _ptr(dst),
+    C.pack_grads(ptrs, mask, dp.plan.num_tensors, _ptr(dp.chunks), dp.plan.num_chunks, _ptr(dst),
                  _DDT[dst.dtype], float(scale), _stream())
 
 

@@ -11,6 +11,8 @@
 #include "ewdml_ops.h"
 
 namespace py = pybind11;
+using Ptrs = std::vector<uintptr_t>;
+using Mask = std::vector<uint32_t>;
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "ewdml CDNA4 (gfx950) kernels";
@@ -20,84 +22,192 @@ PYBIND11_MODULE(_C, m) {
   m.def("qsgd_scratch_bytes", &ew_qsgd_scratch_bytes);
 
   m.def("topk_encode",
-        [](const std::vector<uintptr_t>& grads, uintptr_t resid, uintptr_t chunks,
-           uintptr_t tensors, uintptr_t scratch,
-           uintptr_t payload, long long payload_bytes, int T, int C, int scales_off,
-           int counts_off, int idx_off, int codes_off, int value_kind, int norm_l2, float levels,
-           float inv_levels, uint32_t key, uint32_t bucket_offset, uintptr_t key_ptr,
-           uintptr_t stream) {
-          TopkEncodeArgs a{grads.data(), (int)grads.size(),
-                           resid,      chunks,     tensors,  scratch,   payload,
-                           stream,       payload_bytes, T,       C,        scales_off, counts_off,
-                           idx_off,      codes_off,  value_kind, norm_l2,  levels,    inv_levels,
-                           key,          bucket_offset, key_ptr};
+        [](const Ptrs& grads, const Mask& mask, uintptr_t resid, uintptr_t chunks,
+           uintptr_t tensors, uintptr_t scratch, uintptr_t payload, long long payload_bytes,
+           int T, int C, int scales_off, int counts_off, int idx_off, int codes_off,
+           int value_kind, int norm_l2, float levels, float inv_levels, uint32_t key,
+           uint32_t bucket_offset, uintptr_t key_ptr, uintptr_t stream) {
+          TopkEncodeArgs a{};
+          a.grad_ptrs = grads.data();
+          a.n_grad_ptrs = (int)grads.size();
+          a.bf16_mask = mask.data();
+          a.n_bf16_mask = (int)mask.size();
+          a.resid = resid;
+          a.chunks = chunks;
+          a.tensors = tensors;
+          a.scratch = scratch;
+          a.payload = payload;
+          a.stream = stream;
+          a.payload_bytes = payload_bytes;
+          a.num_tensors = T;
+          a.num_chunks = C;
+          a.scales_off = scales_off;
+          a.counts_off = counts_off;
+          a.idx_off = idx_off;
+          a.codes_off = codes_off;
+          a.value_kind = value_kind;
+          a.norm_l2 = norm_l2;
+          a.levels = levels;
+          a.inv_levels = inv_levels;
+          a.key = key;
+          a.bucket_offset = bucket_offset;
+          a.key_ptr = key_ptr;
           ew_topk_encode(a);
         });
 
   m.def("topk_decode_apply",
         [](uintptr_t recv, int nranks, long long stride, uintptr_t chunks, uintptr_t tensors,
            int C, int scales_off, int counts_off, int idx_off, int codes_off, int value_kind,
-           float inv_levels, uintptr_t param, uintptr_t mom, uintptr_t grad_out, float lr,
-           float momentum, float dampening, float weight_decay, float grad_scale, int nesterov,
-           int first, int apply, uintptr_t stream) {
-          TopkDecodeArgs a{recv,       chunks,     tensors,    param,       mom,
-                           grad_out,   stream,     stride,     nranks,      C,
-                           scales_off, counts_off, idx_off,    codes_off,   value_kind,
-                           inv_levels, lr,         momentum,   dampening,   weight_decay,
-                           grad_scale, nesterov,   first,      apply};
+           float inv_levels, uintptr_t param, uintptr_t mom, uintptr_t grad_out, uintptr_t shadow,
+           float lr, float momentum, float dampening, float weight_decay, float grad_scale,
+           int nesterov, int first, int apply, uintptr_t stream) {
+          TopkDecodeArgs a{};
+          a.recv = recv;
+          a.chunks = chunks;
+          a.tensors = tensors;
+          a.param = param;
+          a.mom = mom;
+          a.grad_out = grad_out;
+          a.shadow = shadow;
+          a.stream = stream;
+          a.stride = stride;
+          a.nranks = nranks;
+          a.num_chunks = C;
+          a.scales_off = scales_off;
+          a.counts_off = counts_off;
+          a.idx_off = idx_off;
+          a.codes_off = codes_off;
+          a.value_kind = value_kind;
+          a.inv_levels = inv_levels;
+          a.lr = lr;
+          a.momentum = momentum;
+          a.dampening = dampening;
+          a.weight_decay = weight_decay;
+          a.grad_scale = grad_scale;
+          a.nesterov = nesterov;
+          a.first = first;
+          a.apply = apply;
           ew_topk_decode_apply(a);
         });
 
   m.def("qsgd_encode",
-        [](const std::vector<uintptr_t>& grads, uintptr_t resid, uintptr_t chunks,
-           uintptr_t tensors, uintptr_t scratch,
-           uintptr_t payload, long long payload_bytes, int T, int C, int scales_off, int codes_off,
-           int bits, int norm_l2, float levels, float inv_levels, uint32_t key,
-           uint32_t bucket_offset, uintptr_t key_ptr, uintptr_t stream) {
-          QsgdEncodeArgs a{grads.data(), (int)grads.size(),
-                           resid,   chunks,        tensors,   scratch, payload, stream,
-                           payload_bytes, T,   C,             scales_off, codes_off, bits, norm_l2,
-                           levels,    inv_levels, key,        bucket_offset, key_ptr};
+        [](const Ptrs& grads, const Mask& mask, uintptr_t resid, uintptr_t chunks,
+           uintptr_t tensors, uintptr_t scratch, uintptr_t payload, long long payload_bytes,
+           int T, int C, int scales_off, int codes_off, int bits, int norm_l2, float levels,
+           float inv_levels, uint32_t key, uint32_t bucket_offset, uintptr_t key_ptr,
+           uintptr_t stream) {
+          QsgdEncodeArgs a{};
+          a.grad_ptrs = grads.data();
+          a.n_grad_ptrs = (int)grads.size();
+          a.bf16_mask = mask.data();
+          a.n_bf16_mask = (int)mask.size();
+          a.resid = resid;
+          a.chunks = chunks;
+          a.tensors = tensors;
+          a.scratch = scratch;
+          a.payload = payload;
+          a.stream = stream;
+          a.payload_bytes = payload_bytes;
+          a.num_tensors = T;
+          a.num_chunks = C;
+          a.scales_off = scales_off;
+          a.codes_off = codes_off;
+          a.bits = bits;
+          a.norm_l2 = norm_l2;
+          a.levels = levels;
+          a.inv_levels = inv_levels;
+          a.key = key;
+          a.bucket_offset = bucket_offset;
+          a.key_ptr = key_ptr;
           ew_qsgd_encode(a);
         });
 
   m.def("qsgd_decode_apply",
         [](uintptr_t recv, int nranks, long long stride, uintptr_t chunks, uintptr_t tensors,
            int C, int scales_off, int codes_off, int bits, float inv_levels, uintptr_t param,
-           uintptr_t mom, uintptr_t grad_out, float lr, float momentum, float dampening,
-           float weight_decay, float grad_scale, int nesterov, int first, int apply,
-           uintptr_t stream) {
-          QsgdDecodeArgs a{recv,   chunks,    tensors,   param,        mom,        grad_out,
-                           stream, stride,    nranks,    C,            scales_off, codes_off,
-                           bits,   inv_levels, lr,       momentum,     dampening,  weight_decay,
-                           grad_scale, nesterov, first,  apply};
+           uintptr_t mom, uintptr_t grad_out, uintptr_t shadow, float lr, float momentum,
+           float dampening, float weight_decay, float grad_scale, int nesterov, int first,
+           int apply, uintptr_t stream) {
+          QsgdDecodeArgs a{};
+          a.recv = recv;
+          a.chunks = chunks;
+          a.tensors = tensors;
+          a.param = param;
+          a.mom = mom;
+          a.grad_out = grad_out;
+          a.shadow = shadow;
+          a.stream = stream;
+          a.stride = stride;
+          a.nranks = nranks;
+          a.num_chunks = C;
+          a.scales_off = scales_off;
+          a.codes_off = codes_off;
+          a.bits = bits;
+          a.inv_levels = inv_levels;
+          a.lr = lr;
+          a.momentum = momentum;
+          a.dampening = dampening;
+          a.weight_decay = weight_decay;
+          a.grad_scale = grad_scale;
+          a.nesterov = nesterov;
+          a.first = first;
+          a.apply = apply;
           ew_qsgd_decode_apply(a);
         });
 
   m.def("sgd_flat",
-        [](uintptr_t param, uintptr_t mom, uintptr_t grad, long long n, int grad_dtype, float lr,
-           float momentum, float dampening, float weight_decay, float grad_scale, int nesterov,
-           int first, uintptr_t stream) {
-          SgdFlatArgs a{param, mom,      grad,      stream,       n,          grad_dtype,
-                        lr,    momentum, dampening, weight_decay, grad_scale, nesterov,  first};
+        [](uintptr_t param, uintptr_t mom, uintptr_t grad, uintptr_t shadow, long long n,
+           int grad_dtype, float lr, float momentum, float dampening, float weight_decay,
+           float grad_scale, int nesterov, int first, uintptr_t stream) {
+          SgdFlatArgs a{};
+          a.param = param;
+          a.mom = mom;
+          a.grad = grad;
+          a.shadow = shadow;
+          a.stream = stream;
+          a.n = n;
+          a.grad_dtype = grad_dtype;
+          a.lr = lr;
+          a.momentum = momentum;
+          a.dampening = dampening;
+          a.weight_decay = weight_decay;
+          a.grad_scale = grad_scale;
+          a.nesterov = nesterov;
+          a.first = first;
           ew_sgd_flat(a);
         });
 
   m.def("adam_flat",
-        [](uintptr_t param, uintptr_t m1, uintptr_t m2, uintptr_t vmax, uintptr_t grad, long long n,
-           int grad_dtype, float lr_step, float beta1, float beta2, float eps, float weight_decay,
-           float grad_scale, int amsgrad, uintptr_t stream) {
-          AdamFlatArgs a{param, m1,    m2,  vmax,  grad,         stream,     n,
-                         grad_dtype, lr_step, beta1, beta2, eps, weight_decay, grad_scale,
-                         1.0f,  amsgrad};
+        [](uintptr_t param, uintptr_t m1, uintptr_t m2, uintptr_t vmax, uintptr_t grad,
+           uintptr_t shadow, long long n, int grad_dtype, float lr_step, float beta1, float beta2,
+           float eps, float weight_decay, float grad_scale, int amsgrad, uintptr_t stream) {
+          AdamFlatArgs a{};
+          a.param = param;
+          a.exp_avg = m1;
+          a.exp_avg_sq = m2;
+          a.max_exp_avg_sq = vmax;
+          a.grad = grad;
+          a.shadow = shadow;
+          a.stream = stream;
+          a.n = n;
+          a.grad_dtype = grad_dtype;
+          a.lr_step = lr_step;
+          a.beta1 = beta1;
+          a.beta2 = beta2;
+          a.eps = eps;
+          a.weight_decay = weight_decay;
+          a.grad_scale = grad_scale;
+          a.bc2_sqrt = 1.0f;
+          a.amsgrad = amsgrad;
           ew_adam_flat(a);
         });
 
   m.def("cast_scale", &ew_cast_scale);
+
   m.def("pack_grads",
-        [](const std::vector<uintptr_t>& grads, int T, uintptr_t chunks, int C, uintptr_t dst,
+        [](const Ptrs& grads, const Mask& mask, int T, uintptr_t chunks, int C, uintptr_t dst,
            int dst_dtype, float scale, uintptr_t stream) {
-          ew_pack_grads(grads.data(), (int)grads.size(), T, chunks, C, dst, dst_dtype, scale,
-                        stream);
+          ew_pack_grads(grads.data(), (int)grads.size(), mask.data(), (int)mask.size(), T, chunks,
+                        C, dst, dst_dtype, scale, stream);
         });
 }

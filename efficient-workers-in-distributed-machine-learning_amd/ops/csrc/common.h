@@ -41,17 +41,69 @@ struct ChunkRow {  // mirrors BucketPlan.chunk_table()
 // a flat buffer, no accumulate-add).  Buckets hold at most EW_MAX_T tensors.
 #define EW_MAX_T 128
 struct GradPtrs {
-  float* p[EW_MAX_T];
+  const void* p[EW_MAX_T];         // gradient base pointer of each tensor of the bucket
+  uint32_t bf16[EW_MAX_T / 32];    // bit t set: tensor t's gradient is bf16 (else fp32)
 };
-__device__ __forceinline__ float* ew_chunk_src(const GradPtrs& gp, const ChunkRow& c) {
-  return gp.p[c.tensor] + (size_t)c.local * EW_CHUNK;
-}
-inline void ew_fill_ptrs(GradPtrs& g, const uintptr_t* ptrs, int n, int T) {
+inline void ew_fill_ptrs(GradPtrs& g, const uintptr_t* ptrs, int n, int T, const uint32_t* mask,
+                         int nmask) {
   if (n != T || T > EW_MAX_T)
     throw std::runtime_error("ewdml: gradient pointer table has " + std::to_string(n) +
                              " entries, bucket has " + std::to_string(T) + " tensors (max " +
                              std::to_string(EW_MAX_T) + ")");
-  for (int i = 0; i < EW_MAX_T; ++i) g.p[i] = i < T ? reinterpret_cast<float*>(ptrs[i]) : nullptr;
+  for (int i = 0; i < EW_MAX_T; ++i) g.p[i] = i < T ? reinterpret_cast<const void*>(ptrs[i]) : nullptr;
+  for (int i = 0; i < EW_MAX_T / 32; ++i) g.bf16[i] = (mask && i < nmask) ? mask[i] : 0u;
+}
+
+__device__ __forceinline__ float ew_bf16f(uint32_t v) { return __uint_as_float((v & 0xffffu) << 16); }
+__device__ __forceinline__ uint16_t ew_f2bf(float x) {  // round-to-nearest-even, quiet NaN
+  uint32_t u = __float_as_uint(x);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40u);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+// Gradient source of a chunk: the per-tensor table (fp32 or bf16 per tensor), or -- when `flat`
+// is set -- a flat fp32 buffer indexed by the chunk's bucket offset (error-feedback passes read
+// the staged g + residual from there).  The branch is uniform per block.
+__device__ __forceinline__ float4 ew_ld4(const GradPtrs& gp, const float* flat, const ChunkRow& c,
+                                         int i) {
+  if (flat) return *reinterpret_cast<const float4*>(flat + c.start + i);
+  const size_t off = (size_t)c.local * EW_CHUNK + i;
+  if ((gp.bf16[c.tensor >> 5] >> (c.tensor & 31)) & 1u) {
+    const uint2 v = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(gp.p[c.tensor]) + off);
+    return make_float4(ew_bf16f(v.x), ew_bf16f(v.x >> 16), ew_bf16f(v.y), ew_bf16f(v.y >> 16));
+  }
+  return *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(gp.p[c.tensor]) + off);
+}
+__device__ __forceinline__ float ew_ld1(const GradPtrs& gp, const float* flat, const ChunkRow& c,
+                                       int i) {
+  if (flat) return flat[c.start + i];
+  const size_t off = (size_t)c.local * EW_CHUNK + i;
+  if ((gp.bf16[c.tensor >> 5] >> (c.tensor & 31)) & 1u)
+    return ew_bf16f(reinterpret_cast<const uint16_t*>(gp.p[c.tensor])[off]);
+  return reinterpret_cast<const float*>(gp.p[c.tensor])[off];
+}
+// 4 consecutive elements (i % 4 == 0) with tail handling
+__device__ __forceinline__ void ew_ld4t(const GradPtrs& gp, const float* flat, const ChunkRow& c,
+                                       int i, float xs[4]) {
+  if (i + 3 < c.len) {
+    const float4 v = ew_ld4(gp, flat, c, i);
+    xs[0] = v.x; xs[1] = v.y; xs[2] = v.z; xs[3] = v.w;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) xs[j] = (i + j < c.len) ? ew_ld1(gp, flat, c, i + j) : 0.0f;
+  }
+}
+// store 4 fp32 values as bf16 (8-byte store when whole)
+__device__ __forceinline__ void ew_st4_bf16(uint16_t* dst, int n, const float v[4]) {
+  if (n >= 4) {
+    uint2 o;
+    o.x = (uint32_t)ew_f2bf(v[0]) | ((uint32_t)ew_f2bf(v[1]) << 16);
+    o.y = (uint32_t)ew_f2bf(v[2]) | ((uint32_t)ew_f2bf(v[3]) << 16);
+    *reinterpret_cast<uint2*>(dst) = o;
+  } else {
+    for (int j = 0; j < n; ++j) dst[j] = ew_f2bf(v[j]);
+  }
 }
 
 struct SgdArgs {

@@ -7,6 +7,8 @@
 struct TopkEncodeArgs {
   const uintptr_t* grad_ptrs;  // per-tensor gradient base pointers (host array, n_grad_ptrs)
   int n_grad_ptrs;
+  const uint32_t* bf16_mask;   // bit t: tensor t's gradient is bf16
+  int n_bf16_mask;
   uintptr_t resid, chunks, tensors, scratch, payload, stream;
   long long payload_bytes;
   int num_tensors, num_chunks;
@@ -19,7 +21,7 @@ struct TopkEncodeArgs {
 };
 
 struct TopkDecodeArgs {
-  uintptr_t recv, chunks, tensors, param, mom, grad_out, stream;
+  uintptr_t recv, chunks, tensors, param, mom, grad_out, shadow, stream;
   long long stride;
   int nranks, num_chunks;
   int scales_off, counts_off, idx_off, codes_off;
@@ -32,6 +34,8 @@ struct TopkDecodeArgs {
 struct QsgdEncodeArgs {
   const uintptr_t* grad_ptrs;
   int n_grad_ptrs;
+  const uint32_t* bf16_mask;
+  int n_bf16_mask;
   uintptr_t resid, chunks, tensors, scratch, payload, stream;
   long long payload_bytes;
   int num_tensors, num_chunks;
@@ -42,7 +46,7 @@ struct QsgdEncodeArgs {
 };
 
 struct QsgdDecodeArgs {
-  uintptr_t recv, chunks, tensors, param, mom, grad_out, stream;
+  uintptr_t recv, chunks, tensors, param, mom, grad_out, shadow, stream;
   long long stride;
   int nranks, num_chunks;
   int scales_off, codes_off, bits;
@@ -52,7 +56,7 @@ struct QsgdDecodeArgs {
 };
 
 struct SgdFlatArgs {
-  uintptr_t param, mom, grad, stream;
+  uintptr_t param, mom, grad, shadow, stream;
   long long n;
   int grad_dtype;  // 0 = fp32, 1 = bf16, 2 = fp16
   float lr, momentum, dampening, weight_decay, grad_scale;
@@ -60,7 +64,7 @@ struct SgdFlatArgs {
 };
 
 struct AdamFlatArgs {
-  uintptr_t param, exp_avg, exp_avg_sq, max_exp_avg_sq, grad, stream;
+  uintptr_t param, exp_avg, exp_avg_sq, max_exp_avg_sq, grad, shadow, stream;
   long long n;
   int grad_dtype;
   float lr_step, beta1, beta2, eps, weight_decay, grad_scale, bc2_sqrt;
@@ -77,8 +81,9 @@ void ew_qsgd_decode_apply(const QsgdDecodeArgs& a);
 
 void ew_sgd_flat(const SgdFlatArgs& a);
 void ew_adam_flat(const AdamFlatArgs& a);
-void ew_pack_grads(const uintptr_t* grad_ptrs, int n_ptrs, int num_tensors, uintptr_t chunks,
-                   int num_chunks, uintptr_t dst, int dst_dtype, float scale, uintptr_t stream);
+void ew_pack_grads(const uintptr_t* grad_ptrs, int n_ptrs, const uint32_t* bf16_mask, int n_mask,
+                   int num_tensors, uintptr_t chunks, int num_chunks, uintptr_t dst,
+                   int dst_dtype, float scale, uintptr_t stream);
 // dst (bf16 when to_bf16 else fp16) = src * scale
 void ew_cast_scale(uintptr_t src, uintptr_t dst, long long n, float scale, int to_bf16,
                    uintptr_t stream);

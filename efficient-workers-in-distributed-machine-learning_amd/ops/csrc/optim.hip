@@ -12,12 +12,7 @@
 namespace {
 
 __device__ __forceinline__ float ew_bf16_to_f32(uint16_t v) { return __uint_as_float((uint32_t)v << 16); }
-__device__ __forceinline__ uint16_t ew_f32_to_bf16(float x) {
-  uint32_t u = __float_as_uint(x);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40u);  // quiet NaN
-  u += 0x7fffu + ((u >> 16) & 1u);                                               // RNE
-  return (uint16_t)(u >> 16);
-}
+__device__ __forceinline__ uint16_t ew_f32_to_bf16(float x) { return ew_f2bf(x); }
 
 template <int GT>
 __device__ __forceinline__ void ew_load_grad4(const void* g, long long i, float out[4]) {
@@ -38,7 +33,7 @@ __device__ __forceinline__ void ew_load_grad4(const void* g, long long i, float 
 template <int GT>
 __global__ __launch_bounds__(EW_BLOCK) void k_sgd_flat(float* __restrict__ p, float* __restrict__ mom,
                                                        const void* __restrict__ g, long long n4,
-                                                       SgdArgs sa) {
+                                                       uint16_t* __restrict__ shadow, SgdArgs sa) {
   for (long long v = blockIdx.x * (long long)EW_BLOCK + threadIdx.x; v < n4;
        v += (long long)gridDim.x * EW_BLOCK) {
     float gv[4];
@@ -51,6 +46,10 @@ __global__ __launch_bounds__(EW_BLOCK) void k_sgd_flat(float* __restrict__ p, fl
     ew_sgd(pv.w, bv.w, gv[3] * sa.grad_scale, sa);
     reinterpret_cast<float4*>(p)[v] = pv;
     reinterpret_cast<float4*>(mom)[v] = bv;
+    if (shadow) {
+      const float w[4] = {pv.x, pv.y, pv.z, pv.w};
+      ew_st4_bf16(shadow + 4 * v, 4, w);
+    }
   }
 }
 
@@ -78,7 +77,7 @@ template <int GT>
 __global__ __launch_bounds__(EW_BLOCK) void k_adam_flat(float* __restrict__ p, float* __restrict__ m,
                                                         float* __restrict__ v, float* __restrict__ vm,
                                                         const void* __restrict__ g, long long n4,
-                                                        AdamArgs a) {
+                                                        uint16_t* __restrict__ shadow, AdamArgs a) {
   for (long long i = blockIdx.x * (long long)EW_BLOCK + threadIdx.x; i < n4;
        i += (long long)gridDim.x * EW_BLOCK) {
     float gv[4];
@@ -95,6 +94,10 @@ __global__ __launch_bounds__(EW_BLOCK) void k_adam_flat(float* __restrict__ p, f
     reinterpret_cast<float4*>(m)[i] = mv;
     reinterpret_cast<float4*>(v)[i] = vv;
     if (a.amsgrad) reinterpret_cast<float4*>(vm)[i] = xv;
+    if (shadow) {
+      const float w[4] = {pv.x, pv.y, pv.z, pv.w};
+      ew_st4_bf16(shadow + 4 * i, 4, w);
+    }
   }
 }
 
@@ -125,16 +128,11 @@ __global__ __launch_bounds__(EW_BLOCK) void k_pack_grads(GradPtrs gp,
                                                          void* __restrict__ dst, int dst_dtype,
                                                          float scale) {
   const ChunkRow c = chunks[blockIdx.x];
-  const float* src = ew_chunk_src(gp, c);
   for (int i = 4 * threadIdx.x; i < c.len; i += 4 * EW_BLOCK) {
     float y[4];
-    if (i + 3 < c.len) {
-      const float4 v = *reinterpret_cast<const float4*>(src + i);
-      y[0] = v.x * scale; y[1] = v.y * scale; y[2] = v.z * scale; y[3] = v.w * scale;
-    } else {
+    ew_ld4t(gp, nullptr, c, i, y);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) y[j] = (i + j < c.len) ? src[i + j] * scale : 0.0f;
-    }
+    for (int j = 0; j < 4; ++j) y[j] = y[j] * scale;
     const long long o = (long long)c.start + i;
     if (dst_dtype == 0) {
       float* d = reinterpret_cast<float*>(dst) + o;
@@ -163,13 +161,14 @@ void ew_sgd_flat(const SgdFlatArgs& a) {
   auto* p = reinterpret_cast<float*>(a.param);
   auto* m = reinterpret_cast<float*>(a.mom);
   auto* g = reinterpret_cast<const void*>(a.grad);
+  auto* sh = reinterpret_cast<uint16_t*>(a.shadow);
   hipStream_t s = (hipStream_t)a.stream;
   if (a.grad_dtype == 0)
-    hipLaunchKernelGGL(k_sgd_flat<0>, dim3(ew_grid(n4)), dim3(EW_BLOCK), 0, s, p, m, g, n4, sa);
+    hipLaunchKernelGGL(k_sgd_flat<0>, dim3(ew_grid(n4)), dim3(EW_BLOCK), 0, s, p, m, g, n4, sh, sa);
   else if (a.grad_dtype == 1)
-    hipLaunchKernelGGL(k_sgd_flat<1>, dim3(ew_grid(n4)), dim3(EW_BLOCK), 0, s, p, m, g, n4, sa);
+    hipLaunchKernelGGL(k_sgd_flat<1>, dim3(ew_grid(n4)), dim3(EW_BLOCK), 0, s, p, m, g, n4, sh, sa);
   else
-    hipLaunchKernelGGL(k_sgd_flat<2>, dim3(ew_grid(n4)), dim3(EW_BLOCK), 0, s, p, m, g, n4, sa);
+    hipLaunchKernelGGL(k_sgd_flat<2>, dim3(ew_grid(n4)), dim3(EW_BLOCK), 0, s, p, m, g, n4, sh, sa);
   EW_CHECK_LAUNCH();
 }
 
@@ -181,20 +180,22 @@ void ew_adam_flat(const AdamFlatArgs& a) {
   auto* v = reinterpret_cast<float*>(a.exp_avg_sq);
   auto* vm = reinterpret_cast<float*>(a.max_exp_avg_sq);
   auto* g = reinterpret_cast<const void*>(a.grad);
+  auto* sh = reinterpret_cast<uint16_t*>(a.shadow);
   hipStream_t s = (hipStream_t)a.stream;
   if (a.grad_dtype == 0)
-    hipLaunchKernelGGL(k_adam_flat<0>, dim3(ew_grid(n4)), dim3(EW_BLOCK), 0, s, p, m, v, vm, g, n4, aa);
+    hipLaunchKernelGGL(k_adam_flat<0>, dim3(ew_grid(n4)), dim3(EW_BLOCK), 0, s, p, m, v, vm, g, n4, sh, aa);
   else if (a.grad_dtype == 1)
-    hipLaunchKernelGGL(k_adam_flat<1>, dim3(ew_grid(n4)), dim3(EW_BLOCK), 0, s, p, m, v, vm, g, n4, aa);
+    hipLaunchKernelGGL(k_adam_flat<1>, dim3(ew_grid(n4)), dim3(EW_BLOCK), 0, s, p, m, v, vm, g, n4, sh, aa);
   else
-    hipLaunchKernelGGL(k_adam_flat<2>, dim3(ew_grid(n4)), dim3(EW_BLOCK), 0, s, p, m, v, vm, g, n4, aa);
+    hipLaunchKernelGGL(k_adam_flat<2>, dim3(ew_grid(n4)), dim3(EW_BLOCK), 0, s, p, m, v, vm, g, n4, sh, aa);
   EW_CHECK_LAUNCH();
 }
 
-void ew_pack_grads(const uintptr_t* grad_ptrs, int n_ptrs, int num_tensors, uintptr_t chunks,
-                   int num_chunks, uintptr_t dst, int dst_dtype, float scale, uintptr_t stream) {
+void ew_pack_grads(const uintptr_t* grad_ptrs, int n_ptrs, const uint32_t* bf16_mask, int n_mask,
+                   int num_tensors, uintptr_t chunks, int num_chunks, uintptr_t dst,
+                   int dst_dtype, float scale, uintptr_t stream) {
   GradPtrs g;
-  ew_fill_ptrs(g, grad_ptrs, n_ptrs, num_tensors);
+  ew_fill_ptrs(g, grad_ptrs, n_ptrs, num_tensors, bf16_mask, n_mask);
   hipLaunchKernelGGL(k_pack_grads, dim3(num_chunks), dim3(EW_BLOCK), 0, (hipStream_t)stream, g,
                      reinterpret_cast<const ChunkRow*>(chunks), reinterpret_cast<void*>(dst),
                      dst_dtype, scale);

@@ -12,23 +12,24 @@ namespace {
 
 template <bool EF>
 __global__ __launch_bounds__(EW_BLOCK) void k_qsgd_stats(GradPtrs gp,
-                                                         const float* __restrict__ resid,
+                                                         float* __restrict__ resid,
                                                          const ChunkRow* __restrict__ chunks,
                                                          float* __restrict__ chunk_sq,
                                                          uint32_t* __restrict__ maxkey) {
   __shared__ float wsf[EW_WAVES];
   const ChunkRow c = chunks[blockIdx.x];
-  float* src = ew_chunk_src(gp, c);
   float sq = 0.0f;
   uint32_t km = 0;
   for (int i = 4 * threadIdx.x; i < c.len; i += 4 * EW_BLOCK) {
+    float xs[4];
+    ew_ld4t(gp, nullptr, c, i, xs);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       if (i + j < c.len) {
-        float x = src[i + j];
-        if (EF) {
+        float x = xs[j];
+        if (EF) {  // stage e = g + residual in the residual buffer
           x = x + resid[c.start + i + j];
-          src[i + j] = x;
+          resid[c.start + i + j] = x;
         }
         sq = sq + x * x;
         km = max(km, ew_key(x));
@@ -69,20 +70,14 @@ __global__ __launch_bounds__(EW_BLOCK) void k_qsgd_quant(
   const uint32_t key = keyp ? *keyp : key_arg;
   const ChunkRow c = chunks[blockIdx.x];
   const TensorRow tr = tensors[c.tensor];
-  const float* src = ew_chunk_src(gp, c);
+  const float* flat = EF ? resid : nullptr;
   const float inv = inv_arr[c.tensor];
   const float step = reinterpret_cast<const float*>(payload + scales_off)[c.tensor] * inv_levels;
   const uint32_t gbase = bucket_offset + (uint32_t)c.start;
   const long long cbase = (long long)tr.code0 + (long long)c.local * EW_CHUNK;
   for (int i = 4 * threadIdx.x; i < c.len; i += 4 * EW_BLOCK) {
     float xs[4];
-    if (i + 3 < c.len) {
-      const float4 v = *reinterpret_cast<const float4*>(src + i);
-      xs[0] = v.x; xs[1] = v.y; xs[2] = v.z; xs[3] = v.w;
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) xs[j] = (i + j < c.len) ? src[i + j] : 0.0f;
-    }
+    ew_ld4t(gp, flat, c, i, xs);
     int q[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -111,7 +106,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_qsgd_decode_apply(
     const uint8_t* __restrict__ recv, int nranks, long long stride,
     const ChunkRow* __restrict__ chunks, const TensorRow* __restrict__ tensors, int scales_off,
     int codes_off, float inv_levels, float* __restrict__ param, float* __restrict__ mom,
-    float* __restrict__ grad_out, SgdArgs sa, int apply) {
+    float* __restrict__ grad_out, uint16_t* __restrict__ shadow, SgdArgs sa, int apply) {
   const ChunkRow c = chunks[blockIdx.x];
   const TensorRow tr = tensors[c.tensor];
   const long long cbase = (long long)tr.code0 + (long long)c.local * EW_CHUNK;
@@ -149,6 +144,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_qsgd_decode_apply(
           ew_sgd(pv, bv, gv, sa);
           p[i + j] = pv;
           b[i + j] = bv;
+          if (shadow) shadow[c.start + i + j] = ew_f2bf(pv);
         }
       }
     }
@@ -175,7 +171,7 @@ void ew_qsgd_encode(const QsgdEncodeArgs& a) {
   hipStream_t s = (hipStream_t)a.stream;
   EW_CHECK(hipMemsetAsync(reinterpret_cast<void*>(a.scratch), 0, ew_qsgd_scratch_bytes(T, C), s));
   GradPtrs g;
-  ew_fill_ptrs(g, a.grad_ptrs, a.n_grad_ptrs, T);
+  ew_fill_ptrs(g, a.grad_ptrs, a.n_grad_ptrs, T, a.bf16_mask, a.n_bf16_mask);
   float* resid = reinterpret_cast<float*>(a.resid);
   auto* pay = reinterpret_cast<uint8_t*>(a.payload);
   if (resid)
@@ -205,11 +201,12 @@ void ew_qsgd_decode_apply(const QsgdDecodeArgs& a) {
   auto* p = reinterpret_cast<float*>(a.param);
   auto* m = reinterpret_cast<float*>(a.mom);
   auto* go = reinterpret_cast<float*>(a.grad_out);
+  auto* sh = reinterpret_cast<uint16_t*>(a.shadow);
   if (a.bits == 8)
     EW_LAUNCH(k_qsgd_decode_apply<8>, a.num_chunks, a.stream, recv, a.nranks, a.stride, chunks,
-              tensors, a.scales_off, a.codes_off, a.inv_levels, p, m, go, sa, a.apply);
+              tensors, a.scales_off, a.codes_off, a.inv_levels, p, m, go, sh, sa, a.apply);
   else
     EW_LAUNCH(k_qsgd_decode_apply<4>, a.num_chunks, a.stream, recv, a.nranks, a.stride, chunks,
-              tensors, a.scales_off, a.codes_off, a.inv_levels, p, m, go, sa, a.apply);
+              tensors, a.scales_off, a.codes_off, a.inv_levels, p, m, go, sh, sa, a.apply);
   EW_CHECK_LAUNCH();
 }

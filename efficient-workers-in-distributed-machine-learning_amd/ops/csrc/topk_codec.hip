@@ -40,32 +40,31 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_hist0(GradPtrs gp,
   __syncthreads();
   uint32_t* h = hw[threadIdx.x >> 6];
   const ChunkRow c = chunks[blockIdx.x];
-  float* src = ew_chunk_src(gp, c);
   uint32_t kmax = 0;
-  const int n4 = c.len >> 2;
-  for (int i = threadIdx.x; i < n4; i += EW_BLOCK) {
-    float4 v = reinterpret_cast<float4*>(src)[i];
-    if (EF) {  // error feedback: compress g + residual, write it back (later passes reread it)
-      float4 r = reinterpret_cast<const float4*>(resid + c.start)[i];
-      v.x = v.x + r.x; v.y = v.y + r.y; v.z = v.z + r.z; v.w = v.w + r.w;
-      reinterpret_cast<float4*>(src)[i] = v;
+  for (int i = 4 * threadIdx.x; i < c.len; i += 4 * EW_BLOCK) {
+    float xs[4];
+    ew_ld4t(gp, nullptr, c, i, xs);
+    if (EF) {  // error feedback: compress e = g + residual, staged in the residual buffer
+      float* r = resid + c.start + i;
+      if (i + 3 < c.len) {
+        float4 rv = *reinterpret_cast<float4*>(r);
+        xs[0] = xs[0] + rv.x; xs[1] = xs[1] + rv.y; xs[2] = xs[2] + rv.z; xs[3] = xs[3] + rv.w;
+        *reinterpret_cast<float4*>(r) = make_float4(xs[0], xs[1], xs[2], xs[3]);
+      } else {
+        for (int j = 0; j < 4 && i + j < c.len; ++j) {
+          xs[j] = xs[j] + r[j];
+          r[j] = xs[j];
+        }
+      }
     }
-    const uint32_t k0 = ew_key(v.x), k1 = ew_key(v.y), k2 = ew_key(v.z), k3 = ew_key(v.w);
-    atomicAdd(&h[k0 >> 20], 1u);
-    atomicAdd(&h[k1 >> 20], 1u);
-    atomicAdd(&h[k2 >> 20], 1u);
-    atomicAdd(&h[k3 >> 20], 1u);
-    kmax = max(max(kmax, max(k0, k1)), max(k2, k3));
-  }
-  for (int i = (n4 << 2) + threadIdx.x; i < c.len; i += EW_BLOCK) {
-    float x = src[i];
-    if (EF) {
-      x = x + resid[c.start + i];
-      src[i] = x;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (i + j < c.len) {
+        const uint32_t k = ew_key(xs[j]);
+        atomicAdd(&h[k >> 20], 1u);
+        kmax = max(kmax, k);
+      }
     }
-    const uint32_t k = ew_key(x);
-    atomicAdd(&h[k >> 20], 1u);
-    kmax = max(kmax, k);
   }
   kmax = ew_wave_max_u(kmax);
   if ((threadIdx.x & 63) == 0) atomicMax(&state[c.tensor * 4 + 2], kmax);
@@ -81,7 +80,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_hist0(GradPtrs gp,
 
 // Histogram of key bits [SHIFT+9 : SHIFT] over elements whose bits above MATCH equal the prefix.
 template <int SHIFT, int MATCH>
-__global__ __launch_bounds__(EW_BLOCK) void k_topk_hist(GradPtrs gp,
+__global__ __launch_bounds__(EW_BLOCK) void k_topk_hist(GradPtrs gp, const float* __restrict__ flat,
                                                         const ChunkRow* __restrict__ chunks,
                                                         const uint32_t* __restrict__ state,
                                                         uint32_t* __restrict__ hist) {
@@ -89,19 +88,15 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_hist(GradPtrs gp,
   for (int i = threadIdx.x; i < NB1; i += EW_BLOCK) h[i] = 0;
   __syncthreads();
   const ChunkRow c = chunks[blockIdx.x];
-  const float* src = ew_chunk_src(gp, c);
   const uint32_t want = state[c.tensor * 4] >> MATCH;
-  const int n4 = c.len >> 2;
-  for (int i = threadIdx.x; i < n4; i += EW_BLOCK) {
-    const float4 v = reinterpret_cast<const float4*>(src)[i];
-    const uint32_t kk[4] = {ew_key(v.x), ew_key(v.y), ew_key(v.z), ew_key(v.w)};
+  for (int i = 4 * threadIdx.x; i < c.len; i += 4 * EW_BLOCK) {
+    float xs[4];
+    ew_ld4t(gp, flat, c, i, xs);
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      if ((kk[j] >> MATCH) == want) atomicAdd(&h[(kk[j] >> SHIFT) & (NB1 - 1)], 1u);
-  }
-  for (int i = (n4 << 2) + threadIdx.x; i < c.len; i += EW_BLOCK) {
-    const uint32_t k = ew_key(src[i]);
-    if ((k >> MATCH) == want) atomicAdd(&h[(k >> SHIFT) & (NB1 - 1)], 1u);
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t k = ew_key(xs[j]);
+      if (i + j < c.len && (k >> MATCH) == want) atomicAdd(&h[(k >> SHIFT) & (NB1 - 1)], 1u);
+    }
   }
   __syncthreads();
   uint32_t* dst = hist + (size_t)c.tensor * NB1;
@@ -144,42 +139,33 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_select(const uint32_t* __rest
 }
 
 // Per chunk: #(key > thr), #(key == thr) and sum of squares of the key > thr values.
-__global__ __launch_bounds__(EW_BLOCK) void k_topk_count(GradPtrs gp,
+__global__ __launch_bounds__(EW_BLOCK) void k_topk_count(GradPtrs gp, const float* __restrict__ flat,
                                                          const ChunkRow* __restrict__ chunks,
                                                          const uint32_t* __restrict__ state,
                                                          uint32_t* __restrict__ cnt_gt,
                                                          uint32_t* __restrict__ cnt_eq,
                                                          float* __restrict__ chunk_sq) {
   __shared__ float wsf[EW_WAVES];
+  __shared__ uint32_t wsu[2 * EW_WAVES];
   const ChunkRow c = chunks[blockIdx.x];
-  const float* src = ew_chunk_src(gp, c);
   const uint32_t thr = state[c.tensor * 4];
   uint32_t gt = 0, eq = 0;
   float sq = 0.0f;
-  const int n4 = c.len >> 2;
-  for (int i = threadIdx.x; i < n4; i += EW_BLOCK) {
-    const float4 v = reinterpret_cast<const float4*>(src)[i];
-    const float xs[4] = {v.x, v.y, v.z, v.w};
+  for (int i = 4 * threadIdx.x; i < c.len; i += 4 * EW_BLOCK) {
+    float xs[4];
+    ew_ld4t(gp, flat, c, i, xs);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const uint32_t k = ew_key(xs[j]);
-      if (k > thr) {
-        ++gt;
-        sq = sq + xs[j] * xs[j];
+      if (i + j < c.len) {
+        const uint32_t k = ew_key(xs[j]);
+        if (k > thr) {
+          ++gt;
+          sq = sq + xs[j] * xs[j];
+        }
+        eq += (k == thr);
       }
-      eq += (k == thr);
     }
   }
-  for (int i = (n4 << 2) + threadIdx.x; i < c.len; i += EW_BLOCK) {
-    const float x = src[i];
-    const uint32_t k = ew_key(x);
-    if (k > thr) {
-      ++gt;
-      sq = sq + x * x;
-    }
-    eq += (k == thr);
-  }
-  __shared__ uint32_t wsu[2 * EW_WAVES];
   gt = ew_wave_sum_u(gt);
   eq = ew_wave_sum_u(eq);
   if ((threadIdx.x & 63) == 0) {
@@ -264,7 +250,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_write(
   const uint32_t key = keyp ? *keyp : key_arg;  // device key: fresh per replay of a captured graph
   const ChunkRow c = chunks[blockIdx.x];
   const TensorRow tr = tensors[c.tensor];
-  const float* src = ew_chunk_src(gp, c);
+  const float* flat = EF ? resid : nullptr;  // EF: hist0 staged e = g + r in the residual
   const uint32_t thr = state[c.tensor * 4];
   const uint32_t ties = chunk_ties[blockIdx.x];
   const uint32_t ebase = (uint32_t)tr.entry0 + chunk_off[blockIdx.x];
@@ -281,13 +267,8 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_write(
     bool valid[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) valid[j] = (i0 + j) < c.len;
-    if (valid[3]) {
-      const float4 v = *reinterpret_cast<const float4*>(src + i0);
-      xs[0] = v.x; xs[1] = v.y; xs[2] = v.z; xs[3] = v.w;
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) xs[j] = valid[j] ? src[i0 + j] : 0.0f;
-    }
+    if (i0 < c.len) ew_ld4t(gp, flat, c, i0, xs);
+    else xs[0] = xs[1] = xs[2] = xs[3] = 0.0f;
     uint32_t ngt = 0, neq = 0;
     bool isgt[4], iseq[4];
 #pragma unroll
@@ -340,7 +321,8 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_decode_apply(
     const uint8_t* __restrict__ recv, int nranks, long long stride,
     const ChunkRow* __restrict__ chunks, const TensorRow* __restrict__ tensors, int scales_off,
     int counts_off, int idx_off, int codes_off, float inv_levels, float* __restrict__ param,
-    float* __restrict__ mom, float* __restrict__ grad_out, SgdArgs sa, int apply) {
+    float* __restrict__ mom, float* __restrict__ grad_out, uint16_t* __restrict__ shadow,
+    SgdArgs sa, int apply) {
   __shared__ float4 acc4[EW_CHUNK / 4];
   __shared__ uint32_t s_off[EW_MAX_RANKS];
   float* acc = reinterpret_cast<float*>(acc4);
@@ -404,6 +386,10 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_decode_apply(
       ew_sgd(pv.w, bv.w, gv.w, sa);
       reinterpret_cast<float4*>(p)[i] = pv;
       reinterpret_cast<float4*>(b)[i] = bv;
+      if (shadow) {  // bf16 compute copy of the updated master weights
+        const float v4[4] = {pv.x, pv.y, pv.z, pv.w};
+        ew_st4_bf16(shadow + c.start + 4 * i, 4, v4);
+      }
     }
   }
   for (int i = (n4 << 2) + threadIdx.x; i < c.len; i += EW_BLOCK) {
@@ -414,6 +400,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_decode_apply(
       ew_sgd(pv, bv, gv, sa);
       p[i] = pv;
       b[i] = bv;
+      if (shadow) shadow[c.start + i] = ew_f2bf(pv);
     }
   }
 }
@@ -445,20 +432,22 @@ void ew_topk_encode(const TopkEncodeArgs& a) {
   float* inv = chunk_sq + C;
   hipStream_t s = (hipStream_t)a.stream;
   EW_CHECK(hipMemsetAsync(scratch, 0, ew_topk_scratch_bytes(T, C), s));
-  EW_CHECK(hipMemsetAsync(reinterpret_cast<void*>(a.payload), 0, a.payload_bytes, s));
+  if (a.value_kind == VK_Q4)  // nibbles are OR-ed in; every other section is fully overwritten
+    EW_CHECK(hipMemsetAsync(reinterpret_cast<void*>(a.payload), 0, a.payload_bytes, s));
   GradPtrs g;
-  ew_fill_ptrs(g, a.grad_ptrs, a.n_grad_ptrs, T);
+  ew_fill_ptrs(g, a.grad_ptrs, a.n_grad_ptrs, T, a.bf16_mask, a.n_bf16_mask);
   float* resid = reinterpret_cast<float*>(a.resid);
+  const float* src_flat = resid;  // passes after hist0 read the staged e = g + r under EF
   if (resid)
     EW_LAUNCH(k_topk_hist0<true>, C, s, g, resid, chunks, hist0, state);
   else
     EW_LAUNCH(k_topk_hist0<false>, C, s, g, resid, chunks, hist0, state);
   EW_LAUNCH((k_topk_select<NB0, 20, true>), T, s, hist0, tensors, state);
-  EW_LAUNCH((k_topk_hist<10, 20>), C, s, g, chunks, state, hist1);
+  EW_LAUNCH((k_topk_hist<10, 20>), C, s, g, src_flat, chunks, state, hist1);
   EW_LAUNCH((k_topk_select<NB1, 10, false>), T, s, hist1, tensors, state);
-  EW_LAUNCH((k_topk_hist<0, 10>), C, s, g, chunks, state, hist2);
+  EW_LAUNCH((k_topk_hist<0, 10>), C, s, g, src_flat, chunks, state, hist2);
   EW_LAUNCH((k_topk_select<NB2, 0, false>), T, s, hist2, tensors, state);
-  EW_LAUNCH(k_topk_count, C, s, g, chunks, state, cnt_gt, cnt_eq, chunk_sq);
+  EW_LAUNCH(k_topk_count, C, s, g, src_flat, chunks, state, cnt_gt, cnt_eq, chunk_sq);
   auto* pay = reinterpret_cast<uint8_t*>(a.payload);
   EW_LAUNCH(k_topk_scan, T, s, tensors, state, cnt_gt, cnt_eq, chunk_sq, chunk_off, chunk_ties, inv,
             pay, a.scales_off, a.counts_off, a.levels, a.norm_l2);
@@ -489,10 +478,12 @@ void ew_topk_decode_apply(const TopkDecodeArgs& a) {
   auto* p = reinterpret_cast<float*>(a.param);
   auto* m = reinterpret_cast<float*>(a.mom);
   auto* go = reinterpret_cast<float*>(a.grad_out);
+  auto* sh = reinterpret_cast<uint16_t*>(a.shadow);
   const int C = a.num_chunks;
 #define EW_DEC(VK)                                                                                   \
   EW_LAUNCH(k_topk_decode_apply<VK>, C, a.stream, recv, a.nranks, a.stride, chunks, tensors,         \
-            a.scales_off, a.counts_off, a.idx_off, a.codes_off, a.inv_levels, p, m, go, sa, a.apply)
+            a.scales_off, a.counts_off, a.idx_off, a.codes_off, a.inv_levels, p, m, go, sh, sa,      \
+            a.apply)
   if (a.value_kind == VK_Q8) EW_DEC(VK_Q8);
   else if (a.value_kind == VK_Q4) EW_DEC(VK_Q4);
   else EW_DEC(VK_F32);

@@ -41,8 +41,9 @@ class FlatSGD:
         p = self.flat.data[start:start + length]
         m = self.mom[start:start + length]
         if p.is_cuda:
+            sh = self.flat.shadow[start:start + length] if self.flat.shadow is not None else None
             ops.sgd_flat(p, m, grad, self.lr, self.momentum, self.dampening, self.weight_decay,
-                         grad_scale, self.nesterov, self.first)
+                         grad_scale, self.nesterov, self.first, shadow=sh)
             return
         g = grad.to(torch.float32)
         if grad_scale != 1.0:
@@ -90,8 +91,9 @@ class FlatAdam:
         vmax = self.max_exp_avg_sq[sl] if self.amsgrad else None
         if p.is_cuda:
             lr_step = self.lr * math.sqrt(1 - b2 ** t) / (1 - b1 ** t)
+            sh = self.flat.shadow[sl] if self.flat.shadow is not None else None
             ops.adam_flat(p, self.exp_avg[sl], self.exp_avg_sq[sl], vmax, grad, lr_step, b1, b2,
-                          self.eps, self.weight_decay, grad_scale, self.amsgrad)
+                          self.eps, self.weight_decay, grad_scale, self.amsgrad, shadow=sh)
             return
         g = grad.to(torch.float32) * grad_scale
         oracle.adam_apply(p, self.exp_avg[sl], self.exp_avg_sq[sl],

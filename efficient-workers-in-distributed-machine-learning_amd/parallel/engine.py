@@ -225,7 +225,8 @@ class GradientExchange:
                 if getattr(opt, "fusable", False):
                     self.codec.decode_apply_sgd(b.index, recv, scale, self.flat.data_view(b),
                                                 opt.mom[b.start:b.start + b.length],
-                                                opt.hparams(), opt.first)
+                                                opt.hparams(), opt.first,
+                                                shadow=self.flat.shadow_view(b))
                 else:
                     gv = self.flat.grad_view(b)
                     self.codec.decode(b.index, recv, gv, scale)
@@ -256,6 +257,7 @@ def sync_params(flat, comm, src: int = 0):
     """Broadcast the flat parameters from ``src`` (fixes the reference's independent random init,
     SURVEY Appendix B #1; Horovod's ``broadcast_parameters``, ``horvod_pytorch.py:187``)."""
     comm.broadcast(flat.data, src=src)
+    flat.sync_shadow()
 
 
 def sync_buffers(model, comm, src: int = 0):

@@ -43,13 +43,20 @@ MAX_TENSORS_PER_BUCKET = 128  # kernel pointer-table capacity (ops.MAX_TENSORS_P
 
 class FlatModel:
     def __init__(self, model, bucket_bytes: int = 8 << 20, reverse: bool = True,
-                 attach_grads: bool = True):
+                 attach_grads: bool = True, bf16_params: bool = False):
         """``model``: an ``nn.Module`` or an iterable of parameters.
 
         ``attach_grads=True``: every ``p.grad`` is a view of ``self.grad`` and autograd accumulates
         into it.  ``False``: ``p.grad`` is left to autograd (``zero_grad`` sets it to None, so the
         incoming gradient is stolen, not added) and the exchange reads each tensor in place
-        through a pointer table -- no per-parameter accumulate kernels, no buffer fill."""
+        through a pointer table -- no per-parameter accumulate kernels, no buffer fill.
+
+        ``bf16_params=True`` (needs ``attach_grads=False``): the weights and biases of conv and
+        linear layers become bf16 views of ``self.shadow``, a bf16 copy of the fp32 master
+        ``self.data`` that the optimizer kernels rewrite (round-to-nearest-even) after every
+        update.  Under bf16 autocast this computes exactly what autocast computes (it would cast
+        the same fp32 master to the same bf16 values every forward), without the per-step weight
+        casts and without casting the bf16 weight gradients back to fp32."""
         seen = set()
         params = []
         plist = model.parameters() if isinstance(model, torch.nn.Module) else model
@@ -73,8 +80,18 @@ class FlatModel:
         self.numel = total
         self.param_numel = sum(p.numel() for p in params)
         self.attach_grads = attach_grads
+        if bf16_params and attach_grads:
+            raise ValueError("bf16 compute parameters need attach_grads=False")
+        lowp = set()
+        if bf16_params and model is not None:
+            for m in model.modules():
+                if isinstance(m, (torch.nn.Conv1d, torch.nn.Conv2d, torch.nn.Conv3d,
+                                  torch.nn.Linear)):
+                    lowp.update(id(q) for q in m.parameters(recurse=False))
+        self.bf16_ids = lowp
         self.data = torch.zeros(total, dtype=torch.float32, device=dev)
         self.grad = torch.zeros(total, dtype=torch.float32, device=dev)
+        self.shadow = torch.zeros(total, dtype=torch.bfloat16, device=dev) if lowp else None
         for p, o in zip(params, offs):
             if p.dtype != torch.float32:
                 raise TypeError("flat buffers hold fp32 master weights; keep params fp32 "
@@ -82,6 +99,10 @@ class FlatModel:
             n = p.numel()
             dv = self.data[o:o + n].as_strided(p.shape, p.stride())
             dv.copy_(p.data)
+            if id(p) in lowp:
+                sv = self.shadow[o:o + n].as_strided(p.shape, p.stride())
+                sv.copy_(dv)
+                dv = sv
             p.data = dv
             p.grad = self.grad[o:o + n].as_strided(p.shape, p.stride()) if attach_grads else None
         self.buckets = self._make_buckets(bucket_bytes)
@@ -117,6 +138,40 @@ class FlatModel:
     def data_view(self, b: Bucket) -> torch.Tensor:
         return self.data[b.start:b.start + b.length]
 
+    def sync_shadow(self):
+        """Refresh the bf16 compute copy from the fp32 master (after a non-kernel update)."""
+        if self.shadow is not None:
+            self.shadow.copy_(self.data)
+
+    def shadow_view(self, b: "Bucket" = None):
+        if self.shadow is None:
+            return None
+        return self.shadow if b is None else self.shadow[b.start:b.start + b.length]
+
+    def master_view(self, p):
+        i = next(k for k, q in enumerate(self.params) if q is p)
+        o = self.offsets[i]
+        return self.data[o:o + p.numel()].as_strided(p.shape, p.stride())
+
+    def master_state_dict(self, model):
+        """``model.state_dict()`` with every parameter taken from the fp32 master."""
+        sd = model.state_dict()
+        if self.shadow is None:
+            return sd
+        for name, p in model.named_parameters():
+            if id(p) in self.bf16_ids:
+                sd[name] = self.master_view(p)
+        return sd
+
+    def load_state_dict(self, model, sd):
+        """Load parameters into the fp32 master (and refresh the bf16 copy) plus buffers."""
+        model.load_state_dict(sd)
+        if self.shadow is not None:
+            for name, p in model.named_parameters():
+                if id(p) in self.bf16_ids:
+                    self.master_view(p).copy_(sd[name])
+            self.sync_shadow()
+
     def zero_grad(self):
         if self.attach_grads:
             self.grad.zero_()
@@ -135,8 +190,8 @@ class FlatModel:
             if g is None:
                 g = torch.zeros_like(p, memory_format=torch.contiguous_format)
                 p.grad = g
-            elif not g.is_contiguous() or g.dtype != torch.float32:
-                g = g.to(torch.float32).contiguous()
+            elif not g.is_contiguous():  # the kernels read fp32 or bf16, densely
+                g = g.contiguous()
                 p.grad = g
             out.append(g)
         return out

@@ -105,11 +105,14 @@ class Trainer:
         # all-to-all one; PS / local SGD keep flat gradient views (they step on the local grad)
         ptr_grads = (self.cuda and cfg.topology == "allgather" and cfg.sync_every == 1
                      and not cfg.select_best and os.environ.get("EWDML_GRAD_VIEWS") != "1")
+        bf16_params = ptr_grads and cfg.amp == "bf16" and cfg.param_dtype == "auto"
         self.flat = FlatModel(model, bucket_bytes=int(cfg.bucket_mb * (1 << 20)),
-                              attach_grads=not ptr_grads)
+                              attach_grads=not ptr_grads, bf16_params=bf16_params)
         sync_params(self.flat, self.comm)
         sync_buffers(model, self.comm)
         lr = cfg.lr * (n_workers if cfg.lr_scale_world else 1)
+        self.base_lr = lr
+        self.n_workers = n_workers
         self.opt = make_optimizer(cfg.optimizer, self.flat, lr=lr, momentum=cfg.momentum,
                                   dampening=cfg.dampening, weight_decay=cfg.weight_decay,
                                   nesterov=cfg.nesterov)
@@ -156,13 +159,20 @@ class Trainer:
                               enabled=self.cuda or self.amp_dtype == torch.bfloat16,
                               cache_enabled=self.graph_mode == "off")
 
+    def _range(self, name):
+        """roctx range (``--roctx``; shows up in ``rocprofv3 --marker-trace``)."""
+        if not (self.cfg.roctx and self.cuda):
+            return contextlib.nullcontext()
+        return torch.cuda.nvtx.range(name)
+
     def forward_backward(self, x, y):
         self.flat.zero_grad()
         self.exchange.begin()
-        with self.autocast():
+        with self._range("forward"), self.autocast():
             out = self.model(x)
         loss = F.cross_entropy(out.float(), y)
-        loss.backward()
+        with self._range("backward+encode"):
+            loss.backward()
         return loss, out
 
     def stream_ctx(self):
@@ -181,9 +191,30 @@ class Trainer:
         torch.cuda.current_stream().wait_stream(self.gstream)
         return out
 
+    def lr_at(self, step: int) -> float:
+        """Learning-rate schedule: linear warmup from lr/W over --lr-warmup-epochs (Horovod's
+        LearningRateWarmupCallback, tensorflow_mnist.py:65-66), then step decay."""
+        cfg = self.cfg
+        spe = len(self.loader) if self.loader is not None else 1
+        epoch = step / max(1, spe)
+        lr = self.base_lr
+        if cfg.lr_warmup_epochs > 0 and epoch < cfg.lr_warmup_epochs:
+            w = max(1, self.n_workers)
+            lr = lr / w + (lr - lr / w) * epoch / cfg.lr_warmup_epochs
+        for e in [float(v) for v in cfg.lr_decay_epochs.split(",") if v.strip()]:
+            if epoch >= e:
+                lr *= cfg.lr_decay
+        return lr
+
     def _train_step(self, x=None, y=None):
         if self.fault is not None and self.fault == (self.rank, self.step):
             raise FaultInjected(f"injected fault on rank {self.rank} at step {self.step}")
+        if self.cfg.lr_warmup_epochs > 0 or self.cfg.lr_decay_epochs:
+            lr = self.lr_at(self.step)
+            if lr != self.opt.lr:
+                self.opt.lr = lr
+                if self._graphs is not None:  # the lr is a kernel argument of the graph
+                    self._graphs = None  # re-capture at this step (every rank: same schedule)
         if self.is_server:
             self.model.train()
             self.exchange.finish()
@@ -197,7 +228,8 @@ class Trainer:
                 return self._train_step(x, y)  # capture failed on some rank: all run eager
             return self._graph_step(x, y)
         loss, out = self.forward_backward(x, y)
-        self.exchange.finish()
+        with self._range("exchange+update"):
+            self.exchange.finish()
         self.step += 1
         return loss, (out, y)
 
@@ -266,7 +298,8 @@ class Trainer:
             self._gy.copy_(y)
         ex.set_device_key()
         if len(self._graphs) == 1:
-            self._graphs[0].replay()
+            with self._range("graph_step"):
+                self._graphs[0].replay()
         else:
             self._graphs[0].replay()
             ex.communicate()
@@ -328,7 +361,7 @@ class Trainer:
         if self.rank != 0:
             return None
         return ckpt.save(self.cfg.ckpt_dir, self.step, self.model, self.opt, self.epoch,
-                         extra=extra,
+                         extra=extra, model_state=self.flat.master_state_dict(self.model),
                          legacy_dir=self.cfg.train_dir if self.cfg.legacy_ckpt else None)
 
     def _resume(self):
@@ -338,7 +371,7 @@ class Trainer:
             self.log.info("resume: no checkpoint found, starting fresh")
             return
         st = ckpt.load(path)
-        self.model.load_state_dict(st["model"])
+        self.flat.load_state_dict(self.model, st["model"])
         # the params are views of the flat buffer; load_state_dict copies in place
         self.opt.load_state_dict({k: (v.to(self.device) if torch.is_tensor(v) else v)
                                   for k, v in st["optimizer"].items()})
@@ -387,7 +420,7 @@ class Trainer:
                 prof = None
             if self.step % cfg.log_interval == 0 or self.step == total:
                 rec = {"step": self.step, "epoch": self.epoch, "rank": self.rank,
-                       "time_s": time.time() - t_start}
+                       "time_s": time.time() - t_start, "lr": self.opt.lr}
                 if loss is not None:
                     out, y = outy
                     a1, a5 = accuracy(out.float(), y, (1, 5))

@@ -35,11 +35,12 @@ def _cpu(x):
     return x
 
 
-def save(ckpt_dir, step, model, optimizer, epoch=0, extra=None, legacy_dir=None, keep=3):
+def save(ckpt_dir, step, model, optimizer, epoch=0, extra=None, legacy_dir=None, keep=3,
+         model_state=None):
     state = {
         "step": int(step),
         "epoch": int(epoch),
-        "model": _cpu(model.state_dict()),
+        "model": _cpu(model_state if model_state is not None else model.state_dict()),
         "optimizer": _cpu(optimizer.state_dict()) if optimizer is not None else None,
         "rng_cpu": torch.get_rng_state(),
         "rng_cuda": torch.cuda.get_rng_state_all() if torch.cuda.is_available() else None,

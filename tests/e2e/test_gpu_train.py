@@ -89,3 +89,43 @@ def test_distributed_optimizer_on_gpu():
         F.nll_loss(m(x), y).backward()
         opt.step()
     assert any(not torch.equal(b, p) for b, p in zip(before, m.parameters()))
+
+
+def test_bf16_params_match_fp32_master_path():
+    """--param-dtype auto (bf16 compute copies of conv/linear weights) computes what autocast
+    computes from fp32 parameters: same trajectory up to kernel nondeterminism."""
+    base = ["--network", "VGG11", "--dataset", "Cifar10", "--batch-size", "32",
+            "--synthetic-size", "256", "--momentum", "0.9", "--eval-freq", "0", "--quiet",
+            "--device", "cuda", "--hip-graph", "off", "--compress", "topk_qsgd"]
+    a, la = _run(base + ["--param-dtype", "auto"], 4)
+    b, lb = _run(base + ["--param-dtype", "fp32"], 4)
+    assert a.flat.shadow is not None and b.flat.shadow is None
+    rel = (a.flat.data - b.flat.data).norm() / b.flat.data.norm()
+    assert rel < 1e-3, rel
+    assert abs(la[-1] - lb[-1]) < 5e-2
+    # the bf16 compute copy equals the rounded master
+    assert torch.equal(a.flat.shadow, a.flat.data.to(torch.bfloat16))
+
+
+def test_bf16_params_checkpoint_holds_fp32_master(tmp_path):
+    from ewdml.runtime import Trainer
+    from ewdml.utils import checkpoint as ckpt
+
+    flags = ["--network", "LeNet", "--dataset", "MNIST", "--batch-size", "32", "--synthetic-size",
+             "256", "--eval-freq", "2", "--quiet", "--device", "cuda", "--max-steps", "2",
+             "--train-dir", str(tmp_path) + "/"]
+    tr = Trainer(ewdml.parse_args(flags))
+    tr.fit()
+    st = ckpt.load(ckpt.latest(str(tmp_path)))
+    assert st["model"]["conv1.weight"].dtype == torch.float32
+    torch.testing.assert_close(st["model"]["conv1.weight"].cuda(),
+                               tr.flat.master_view(tr.model.conv1.weight))
+
+
+def test_capture_after_single_eager_step():
+    """bench.py may capture after one eager step (driver's --warmup 2): must work."""
+    flags = ["--network", "VGG11", "--dataset", "Cifar10", "--batch-size", "16",
+             "--synthetic-size", "256", "--momentum", "0.9", "--eval-freq", "0", "--quiet",
+             "--device", "cuda", "--hip-graph", "full", "--graph-warmup", "1"]
+    tr, losses = _run(flags, 4)
+    assert tr._graphs is not None and all(torch.isfinite(torch.tensor(losses)))

@@ -238,3 +238,89 @@ def test_bad_operands_rejected():
     with pytest.raises(ValueError):
         ops.topk_encode(dp, torch.zeros(plan.length, device=DEV), torch.zeros(
             lay.nbytes, dtype=torch.uint8, device=DEV), lay, 200, "max", 0)
+
+
+def _split(plan, g, dtype=torch.float32):
+    return [g[o:o + n].clone().to(dtype).to(DEV) for o, n in zip(plan.offsets, plan.numels)]
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("kind", ["topk_qsgd", "qsgd"])
+def test_encode_from_per_tensor_pointers(dtype, kind):
+    """Encoding autograd's own per-tensor gradients (fp32 or bf16, read through the pointer
+    table) equals encoding the same values from a flat fp32 buffer."""
+    ops.require()
+    plan = _plan([8192 + 7, 64, 30000, 5], 0.02, bucket_offset=256)
+    lay = Layout.build(kind, plan, 8)
+    g = _grad(plan, seed=3)
+    if dtype == torch.bfloat16:  # the flat reference holds the same (bf16-representable) values
+        for o, n in zip(plan.offsets, plan.numels):
+            g[o:o + n] = g[o:o + n].to(torch.bfloat16).float()
+    key = stream_key(2, 5, 1)
+    enc = oracle.encode_qsgd if kind == "qsgd" else oracle.encode_topk
+    ref = enc(g.clone(), plan, lay, 127, "max", key)
+    dp = ops.DevicePlan(plan, DEV)
+    pay = torch.zeros(lay.nbytes, dtype=torch.uint8, device=DEV)
+    fn = ops.qsgd_encode if kind == "qsgd" else ops.topk_encode
+    fn(dp, _split(plan, g, dtype), pay, lay, 127, "max", key)
+    assert torch.equal(pay.cpu(), ref)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_error_feedback_bf16_grads_stage_in_residual(dtype):
+    ops.require()
+    plan = _plan([20000, 300], 0.01)
+    lay = Layout.build("topk_qsgd", plan, 8)
+    g = _grad(plan, seed=7)
+    for o, n in zip(plan.offsets, plan.numels):
+        g[o:o + n] = g[o:o + n].to(dtype).float()
+    r0 = _grad(plan, seed=8) * 0.05
+    key = stream_key(0, 3, 0)
+    r_ref = r0.clone()
+    ref = oracle.encode_topk(g.clone(), plan, lay, 127, "max", key, residual=r_ref)
+    dp = ops.DevicePlan(plan, DEV)
+    pay = torch.zeros(lay.nbytes, dtype=torch.uint8, device=DEV)
+    grads = _split(plan, g, dtype)
+    before = [t.clone() for t in grads]
+    r_dev = r0.to(DEV)
+    ops.topk_encode(dp, grads, pay, lay, 127, "max", key, resid=r_dev)
+    assert torch.equal(pay.cpu(), ref)
+    for o, n in zip(plan.offsets, plan.numels):
+        assert torch.equal(r_dev.cpu()[o:o + n], r_ref[o:o + n])
+    for a, b in zip(grads, before):  # the gradients themselves are not modified
+        assert torch.equal(a, b)
+
+
+def test_decode_writes_bf16_shadow():
+    ops.require()
+    plan = _plan([9000, 64, 33333], 0.05)
+    lay = Layout.build("topk_qsgd", plan, 8)
+    recv = torch.stack([oracle.encode_topk(_grad(plan, seed=r), plan, lay, 127, "max",
+                                           stream_key(0, 0, r)) for r in range(2)]).to(DEV)
+    dp = ops.DevicePlan(plan, DEV)
+    p = torch.randn(plan.length, device=DEV)
+    m = torch.zeros(plan.length, device=DEV)
+    sh = torch.zeros(plan.length, dtype=torch.bfloat16, device=DEV)
+    ops.topk_decode_apply(dp, recv, lay, 127, param=p, mom=m, lr=0.1, momentum=0.9,
+                          grad_scale=0.5, first=True, shadow=sh)
+    for o, n in zip(plan.offsets, plan.numels):
+        assert torch.equal(sh[o:o + n], p[o:o + n].to(torch.bfloat16))
+    # flat SGD shadow too
+    g = torch.randn(plan.length, device=DEV)
+    sh2 = torch.zeros_like(sh)
+    ops.sgd_flat(p, m, g, 0.1, 0.9, shadow=sh2)
+    assert torch.equal(sh2, p.to(torch.bfloat16))
+
+
+def test_pack_grads_mixed_dtypes():
+    ops.require()
+    plan = _plan([1000, 8192 * 2 + 3, 17], 1.0)
+    dp = ops.DevicePlan(plan, DEV)
+    g = _grad(plan, seed=11)
+    grads = _split(plan, g, torch.float32)
+    grads[1] = grads[1].to(torch.bfloat16)
+    for dt in (torch.float32, torch.bfloat16):
+        dst = torch.zeros(plan.length, dtype=dt, device=DEV)
+        ops.pack_grads(dp, grads, dst, 0.5)
+        for t, o, n in zip(grads, plan.offsets, plan.numels):
+            assert torch.equal(dst[o:o + n], (t.float() * 0.5).to(dt))
