@@ -86,7 +86,7 @@ def main(argv=None):
              "--compress", a.compress, "--topk-ratio", str(a.topk_ratio), "--qsgd-bits",
              str(a.qsgd_bits), "--qsgd-levels", str(levels), "--momentum", "0.9", "--lr", "0.01",
              "--bucket-mb", str(a.bucket_mb), "--amp", a.amp, "--synthetic-size",
-             str(max(2048, 4 * a.batch_size * world)),
+             str(max(16384, 4 * a.batch_size * world)),
              "--eval-freq", "0", "--log-interval", "1000000", "--quiet",
              "--max-steps", str(a.steps + a.warmup)]
     if a.channels_last:

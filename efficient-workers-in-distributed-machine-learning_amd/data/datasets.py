@@ -103,14 +103,20 @@ def _svhn(root, train):
     return torch.from_numpy(x), torch.from_numpy(y)
 
 
-def synthetic(shape, num_classes, size, seed=0, device="cpu", noise=0.6):
-    """Learnable synthetic uint8 images: per-class template + noise, labels uniform."""
-    g = torch.Generator(device="cpu").manual_seed(1234 + seed)
-    templates = torch.rand((num_classes,) + tuple(shape), generator=g)
-    y = torch.randint(0, num_classes, (size,), generator=g)
-    x = templates[y] + noise * torch.randn((size,) + tuple(shape), generator=g) * 0.25
-    x = (x.clamp(0, 1) * 255).to(torch.uint8)
-    return x.to(device), y.to(device)
+def synthetic(shape, num_classes, size, seed=0, device="cpu", noise=0.6, chunk=2048):
+    """Learnable synthetic uint8 images: per-class template + noise, labels uniform.  Generated on
+    ``device`` in chunks (a 224x224 set never materialises in fp32 all at once)."""
+    dev = torch.device(device)
+    g = torch.Generator(device=dev).manual_seed(1234 + seed)
+    templates = torch.rand((num_classes,) + tuple(shape), generator=g, device=dev)
+    y = torch.randint(0, num_classes, (size,), generator=g, device=dev)
+    x = torch.empty((size,) + tuple(shape), dtype=torch.uint8, device=dev)
+    for s in range(0, size, chunk):
+        yy = y[s:s + chunk]
+        v = templates[yy] + (noise * 0.25) * torch.randn((yy.numel(),) + tuple(shape),
+                                                         generator=g, device=dev)
+        x[s:s + chunk] = (v.clamp_(0, 1) * 255).to(torch.uint8)
+    return x, y
 
 
 def load_dataset(name: str, root: str = None, train: bool = True, synthetic_size: int = 0,
@@ -135,6 +141,6 @@ def load_dataset(name: str, root: str = None, train: bool = True, synthetic_size
         n = synthetic_size or (50000 if key != "mnist" else 60000)
         if not train:
             n = max(1000, n // 5)
-        x, y = synthetic(shape, ncls, n, seed=seed + (0 if train else 1), device="cpu")
+        x, y = synthetic(shape, ncls, n, seed=seed + (0 if train else 1), device=device)
     return x.to(device), y.to(device), {"name": key, "shape": shape, "classes": ncls,
                                         "mean": mean, "std": std, "synthetic": use_syn}

@@ -58,8 +58,11 @@ class DeviceLoader:
         self.epoch = epoch
         n = self.x.shape[0]
         if self.shuffle:
-            g = torch.Generator(device="cpu").manual_seed(self.seed * 100003 + epoch)
-            perm = torch.randperm(n, generator=g).to(self.device)
+            # generated on the device: no host round trip (a CPU permutation + copy would block
+            # the host until the GPU drains, a bubble at every epoch start); the same seed gives
+            # the same permutation on every rank
+            g = torch.Generator(device=self.device).manual_seed(self.seed * 100003 + epoch)
+            perm = torch.randperm(n, generator=g, device=self.device)
         else:
             perm = torch.arange(n, device=self.device)
         self._idx = perm[self.rank::self.world][:self.per_rank]
