@@ -56,6 +56,8 @@ def parse(argv=None):
     p.add_argument("--bucket-mb", type=float, default=64.0)
     p.add_argument("--amp", default="bf16")
     p.add_argument("--channels-last", action="store_true")
+    p.add_argument("--layout", default="auto", choices=["auto", "nchw", "nhwc"])
+    p.add_argument("--fused-nn", default="on", choices=["on", "off"])
     p.add_argument("--no-overlap", action="store_true")
     p.add_argument("--error-feedback", action="store_true")
     p.add_argument("--hip-graph", default="full", choices=["off", "split", "full"])
@@ -91,6 +93,7 @@ def main(argv=None):
              "--max-steps", str(a.steps + a.warmup)]
     if a.channels_last:
         flags.append("--channels-last")
+    flags += ["--layout", a.layout, "--fused-nn", a.fused_nn]
     if a.no_overlap:
         flags.append("--no-overlap")
     if a.error_feedback:
@@ -156,7 +159,9 @@ def main(argv=None):
                    a.compress, "optimizer": "sgd(momentum=0.9)", "overlap": not a.no_overlap,
                    "buckets": len(tr.flat.buckets), "hip_graph": tr.graph_mode,
                    "bf16_params": tr.flat.shadow is not None,
-                   "grad_mode": "views" if tr.flat.attach_grads else "pointers"},
+                   "grad_mode": "views" if tr.flat.attach_grads else "pointers",
+                   "layout": "nhwc" if tr.channels_last else "nchw",
+                   "fused_nn": a.fused_nn},
         "grad_bytes_per_step_on_wire": bytes_["wire_bytes_total"],
         "payload_bytes_per_rank": bytes_["payload_bytes_per_rank"],
         "dense_fp32_grad_bytes": bytes_["dense_fp32_bytes"],

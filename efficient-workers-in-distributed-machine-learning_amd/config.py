@@ -83,7 +83,9 @@ class Config:
     amp: str = "bf16"  # bf16 | fp16 | none  (autocast compute dtype; master weights fp32)
     param_dtype: str = "auto"  # auto: conv/linear weights kept in bf16 (fp32 master) under bf16
     #                            autocast on the GPU all-to-all path | fp32
-    channels_last: bool = False
+    channels_last: bool = False  # alias of layout="nhwc"
+    layout: str = "auto"  # auto (nhwc on the GPU when the fused NHWC kernels run) | nchw | nhwc
+    fused_nn: str = "on"  # on: conv-BN-ReLU-pool groups / 2x2 pools through ops/csrc/nn.hip | off
     hip_graph: str = "off"  # off | split (graphs around eager RCCL calls) | full (one graph)
     graph_warmup: int = 3  # eager steps (>= 1) before capture: MIOpen find, handles, momentum
 
@@ -131,6 +133,8 @@ class Config:
             raise ValueError("--graph-warmup must be >= 1 (one eager step initialises the stream)")
         if c.ckpt_dir is None:
             c.ckpt_dir = c.train_dir
+        if c.channels_last:
+            c.layout = "nhwc"
         return c
 
 
@@ -195,6 +199,8 @@ def build_parser(prog="distributed_nn.py") -> argparse.ArgumentParser:
     a("--amp", type=str, default=d.amp, choices=["bf16", "fp16", "none"])
     a("--param-dtype", type=str, default=d.param_dtype, choices=["auto", "fp32"])
     a("--channels-last", action="store_true", default=False)
+    a("--layout", type=str, default=d.layout, choices=["auto", "nchw", "nhwc"])
+    a("--fused-nn", type=str, default=d.fused_nn, choices=["on", "off"])
     a("--hip-graph", type=str, default=d.hip_graph, choices=["off", "split", "full"])
     a("--graph-warmup", type=int, default=d.graph_warmup)
     a("--data-dir", type=str, default=None)

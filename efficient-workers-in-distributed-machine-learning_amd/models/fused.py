@@ -1,0 +1,91 @@
+"""Execution of conv -> BatchNorm -> ReLU [-> MaxPool 2x2] stacks through the fused NHWC kernels.
+
+:class:`FusedFeatures` is an ``nn.Sequential`` (same modules, parameters and ``state_dict`` keys as
+the plain stack the reference builds in ``src/model_ops/vgg.py:39-52``) whose forward, on
+channels_last device activations, runs each ``Conv2d, BatchNorm2d, ReLU[, MaxPool2d(2, 2)]`` group
+as ``conv2d(x, w)`` (bias folded into the BN kernel) + :func:`ewdml.ops.nn.bn_relu`, and a lone
+``MaxPool2d(2, 2)`` as :func:`ewdml.ops.nn.maxpool2x2`.  On the CPU, or for shapes the kernels do
+not take, it is exactly ``nn.Sequential.forward``.
+
+``set_enabled(False)`` (``--fused-nn off``) restores the module-by-module path everywhere.
+"""
+import torch
+import torch.nn as nn
+
+_ENABLED = True
+
+
+def set_enabled(on: bool):
+    global _ENABLED
+    _ENABLED = bool(on)
+
+
+def enabled() -> bool:
+    return _ENABLED
+
+
+def is_pool2(m) -> bool:
+    def two(v):
+        return v == 2 or v == (2, 2)
+
+    return (isinstance(m, nn.MaxPool2d) and two(m.kernel_size)
+            and two(m.stride if m.stride is not None else m.kernel_size)
+            and m.padding in (0, (0, 0)) and m.dilation in (1, (1, 1)) and not m.ceil_mode
+            and not m.return_indices)
+
+
+def pool2(x):
+    """``F.max_pool2d(x, 2, 2)``, through the HIP kernel on the GPU."""
+    if _ENABLED and x.is_cuda:
+        from ..ops.nn import maxpool2x2
+
+        return maxpool2x2(x)
+    return torch.nn.functional.max_pool2d(x, 2, 2)
+
+
+class FusedFeatures(nn.Sequential):
+    def _plan(self):
+        plan = getattr(self, "_ew_plan", None)
+        if plan is not None and plan[0] == len(self):
+            return plan[1]
+        mods = list(self)
+        groups, i = [], 0
+        while i < len(mods):
+            m = mods[i]
+            if (isinstance(m, nn.Conv2d) and i + 2 < len(mods)
+                    and isinstance(mods[i + 1], nn.BatchNorm2d) and isinstance(mods[i + 2], nn.ReLU)
+                    and m.padding_mode == "zeros"):
+                pool = i + 3 < len(mods) and is_pool2(mods[i + 3])
+                groups.append(("cbr", mods[i:i + (4 if pool else 3)], pool))
+                i += 4 if pool else 3
+            elif is_pool2(m):
+                groups.append(("pool", [m], True))
+                i += 1
+            else:
+                groups.append(("mod", [m], False))
+                i += 1
+        self._ew_plan = (len(self), groups)
+        return groups
+
+    def forward(self, x):
+        if not (_ENABLED and x.is_cuda):
+            return super().forward(x)
+        from ..ops import nn as fnn
+
+        for kind, mods, pool in self._plan():
+            if kind == "cbr":
+                conv, bn = mods[0], mods[1]
+                h = conv._conv_forward(x, conv.weight, None)
+                if fnn.nhwc_supported(h, pool):
+                    x = fnn.bn_relu(h, conv.bias, bn, pool)
+                else:
+                    if conv.bias is not None:
+                        h = h + conv.bias.to(h.dtype).view(1, -1, 1, 1)
+                    for m in mods[1:]:
+                        h = m(h)
+                    x = h
+            elif kind == "pool":
+                x = fnn.maxpool2x2(x)
+            else:
+                x = mods[0](x)
+        return x

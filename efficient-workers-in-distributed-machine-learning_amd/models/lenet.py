@@ -10,6 +10,8 @@ the reference exactly).
 import torch.nn as nn
 import torch.nn.functional as F
 
+from .fused import pool2
+
 
 class LeNet(nn.Module):
     def __init__(self, num_classes: int = 10, fc_relu: bool = False):
@@ -21,8 +23,8 @@ class LeNet(nn.Module):
         self.fc_relu = fc_relu
 
     def forward(self, x):
-        x = F.relu(F.max_pool2d(self.conv1(x), 2, 2))
-        x = F.relu(F.max_pool2d(self.conv2(x), 2, 2))
+        x = F.relu(pool2(self.conv1(x)))
+        x = F.relu(pool2(self.conv2(x)))
         x = self.fc1(x.flatten(1))
         if self.fc_relu:
             x = F.relu(x)
@@ -45,8 +47,8 @@ class MnistNet(nn.Module):
         self.fc2 = nn.Linear(50, num_classes)
 
     def forward(self, x):
-        x = F.relu(F.max_pool2d(self.conv1(x), 2))
-        x = F.relu(F.max_pool2d(self.conv2_drop(self.conv2(x)), 2))
+        x = F.relu(pool2(self.conv1(x)))
+        x = F.relu(pool2(self.conv2_drop(self.conv2(x))))
         x = F.relu(self.fc1(x.flatten(1)))
         x = F.dropout(x, training=self.training)
         return F.log_softmax(self.fc2(x), dim=1)

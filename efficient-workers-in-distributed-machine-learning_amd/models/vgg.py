@@ -12,6 +12,8 @@ import math
 
 import torch.nn as nn
 
+from .fused import FusedFeatures
+
 _CFG = {
     "A": [64, "M", 128, "M", 256, 256, "M", 512, 512, "M", 512, 512, "M"],
     "B": [64, 64, "M", 128, 128, "M", 256, 256, "M", 512, 512, "M", 512, 512, "M"],
@@ -22,6 +24,8 @@ _CFG = {
 
 
 def _features(cfg, batch_norm: bool, in_channels: int = 3) -> nn.Sequential:
+    """The conv stack; a :class:`FusedFeatures` (runs conv-BN-ReLU-pool groups through the fused
+    NHWC kernels on the GPU, plain ``nn.Sequential`` semantics otherwise)."""
     layers = []
     c = in_channels
     for v in cfg:
@@ -33,7 +37,7 @@ def _features(cfg, batch_norm: bool, in_channels: int = 3) -> nn.Sequential:
             layers.append(nn.BatchNorm2d(v))
         layers.append(nn.ReLU(inplace=True))
         c = v
-    return nn.Sequential(*layers)
+    return FusedFeatures(*layers)
 
 
 class VGG(nn.Module):

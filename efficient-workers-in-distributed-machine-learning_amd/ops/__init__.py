@@ -74,12 +74,15 @@ def _ptr(t) -> int:
     return 0 if t is None else t.data_ptr()
 
 
-def _check(t, dtype, name, align=16):
+def _check(t, dtype, name, align=16, dense=False):
+    """``dense``: any non-overlapping dense layout is fine (the kernel reads the tensor in memory
+    order, e.g. a channels_last conv-weight gradient matching its channels_last parameter)."""
     if not t.is_cuda:
         raise ValueError(f"{name} must be a device tensor")
     if t.dtype != dtype:
         raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
-    if not t.is_contiguous():
+    if not (t.is_contiguous() or (dense and t.dim() == 4
+                                  and t.is_contiguous(memory_format=torch.channels_last))):
         raise ValueError(f"{name} must be contiguous")
     if t.data_ptr() % align:
         raise ValueError(f"{name} must be {align}-byte aligned")
@@ -123,10 +126,10 @@ def grad_pointers(dp, grad):
     ptrs = []
     for i, (t, n) in enumerate(zip(grad, plan.numels)):
         if t.dtype == torch.bfloat16:
-            _check(t, torch.bfloat16, "grad tensor", align=8)
+            _check(t, torch.bfloat16, "grad tensor", align=8, dense=True)
             mask[i >> 5] |= 1 << (i & 31)
         else:
-            _check(t, torch.float32, "grad tensor")
+            _check(t, torch.float32, "grad tensor", dense=True)
         if t.numel() != n:
             raise ValueError(f"gradient has {t.numel()} elements, plan expects {n}")
         ptrs.append(t.data_ptr())

@@ -87,3 +87,33 @@ void ew_pack_grads(const uintptr_t* grad_ptrs, int n_ptrs, const uint32_t* bf16_
 // dst (bf16 when to_bf16 else fp16) = src * scale
 void ew_cast_scale(uintptr_t src, uintptr_t dst, long long n, float scale, int to_bf16,
                    uintptr_t stream);
+
+// ---- model-side kernels (nn.hip) ----
+// NHWC BatchNorm + ReLU [+ 2x2 max pool]; h/y/dy/dx bf16 or fp32 ([N,H,W,C] memory), C % 8 == 0
+struct BnFwdArgs {
+  uintptr_t h, y, code, stats, part;        // stats fp32 [4][C]; part: ew_bn_part_floats() floats
+  uintptr_t gamma, beta, cbias, rmean, rvar, nbt;  // fp32 [C] (nullable), nbt int64 (nullable)
+  long long N;
+  int H, W, C;
+  int is_bf16, pool, training;
+  float momentum, eps;  // momentum < 0: cumulative average over *nbt batches
+  uintptr_t stream;
+};
+struct BnBwdArgs {
+  uintptr_t h, dy, code, stats, coef, part, dx;  // coef fp32 [2][C]
+  uintptr_t dgamma, dbeta, dcbias;               // fp32 [C] outputs (nullable)
+  long long N;
+  int H, W, C;  // of h (pre-pool)
+  int is_bf16, pool;
+  uintptr_t stream;
+};
+int ew_bn_part_floats();
+void ew_bn_relu_fwd(const BnFwdArgs& a);
+void ew_bn_relu_bwd(const BnBwdArgs& a);
+void ew_maxpool2_nhwc(uintptr_t x, uintptr_t y, uintptr_t code, long long N, int H, int W, int C,
+                      int is_bf16, int backward, uintptr_t stream);
+// NCHW 2x2 max pool: rows = N*C*H/2
+void ew_maxpool2_fwd(uintptr_t x, uintptr_t y, uintptr_t code, long long rows, int W, int is_bf16,
+                     uintptr_t stream);
+void ew_maxpool2_bwd(uintptr_t dy, uintptr_t code, uintptr_t dx, long long rows, int W,
+                     int is_bf16, uintptr_t stream);

@@ -1,0 +1,720 @@
+// Model-side kernels for the CNNs of the reference (gfx950, wave64).
+//
+// MaxPool 2x2 / stride 2 (VGG's five pools, LeNet's two), NCHW, bf16 or fp32.  PyTorch's kernel
+// stores an int64 argmax per output and its backward ran at 26 us per call on VGG-11 bs128
+// (profiles/vgg11_bs128_topk1pct_qsgd8_graph_bf16params.txt); here the argmax is a 1-byte window
+// position (0..3) and both directions are dense, coalesced streams: one thread per output reads
+// two 2-element row pairs (4 B each in bf16) and writes the max + its code; backward writes the
+// 2x2 window from dy and the code.  Tie / NaN semantics match PyTorch (first max in row-major
+// window order; a NaN wins).
+#include "common.h"
+#include "ewdml_ops.h"
+
+namespace {
+
+template <typename T>
+struct Pair;  // two consecutive elements loaded/stored as one word
+template <>
+struct Pair<uint16_t> {  // bf16
+  using W = uint32_t;
+  static __device__ __forceinline__ void split(W w, float& a, float& b) {
+    a = __uint_as_float((w & 0xffffu) << 16);
+    b = __uint_as_float(w & 0xffff0000u);
+  }
+  static __device__ __forceinline__ W join(float a, float b) {
+    return (uint32_t)ew_f2bf(a) | ((uint32_t)ew_f2bf(b) << 16);
+  }
+  static __device__ __forceinline__ float one(uint16_t v) { return __uint_as_float((uint32_t)v << 16); }
+  static __device__ __forceinline__ uint16_t make(float v) { return ew_f2bf(v); }
+};
+template <>
+struct Pair<float> {
+  using W = float2;
+  static __device__ __forceinline__ void split(W w, float& a, float& b) { a = w.x; b = w.y; }
+  static __device__ __forceinline__ W join(float a, float b) { return make_float2(a, b); }
+  static __device__ __forceinline__ float one(float v) { return v; }
+  static __device__ __forceinline__ float make(float v) { return v; }
+};
+
+template <typename T>
+__global__ __launch_bounds__(EW_BLOCK) void k_maxpool2_fwd(const T* __restrict__ x,
+                                                           T* __restrict__ y,
+                                                           uint8_t* __restrict__ code,
+                                                           long long total, int Wo, int W) {
+  using P = Pair<T>;
+  using Wd = typename P::W;
+  for (long long o = blockIdx.x * (long long)EW_BLOCK + threadIdx.x; o < total;
+       o += (long long)gridDim.x * EW_BLOCK) {
+    const long long r = o / Wo;  // output row index over (n, c, ho)
+    const int j = (int)(o - r * Wo);
+    const long long base = (2 * r) * W + 2 * j;  // input (n, c, 2*ho, 2*j)
+    float v[4];
+    P::split(*reinterpret_cast<const Wd*>(x + base), v[0], v[1]);
+    P::split(*reinterpret_cast<const Wd*>(x + base + W), v[2], v[3]);
+    float m = v[0];
+    int k = 0;
+#pragma unroll
+    for (int q = 1; q < 4; ++q) {
+      if (v[q] > m || isnan(v[q])) {
+        m = v[q];
+        k = q;
+      }
+    }
+    y[o] = P::make(m);
+    code[o] = (uint8_t)k;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(EW_BLOCK) void k_maxpool2_bwd(const T* __restrict__ dy,
+                                                           const uint8_t* __restrict__ code,
+                                                           T* __restrict__ dx, long long total,
+                                                           int Wo, int W) {
+  using P = Pair<T>;
+  using Wd = typename P::W;
+  for (long long o = blockIdx.x * (long long)EW_BLOCK + threadIdx.x; o < total;
+       o += (long long)gridDim.x * EW_BLOCK) {
+    const long long r = o / Wo;
+    const int j = (int)(o - r * Wo);
+    const long long base = (2 * r) * W + 2 * j;
+    const float g = P::one(dy[o]);
+    const int k = code[o];
+    *reinterpret_cast<Wd*>(dx + base) = P::join(k == 0 ? g : 0.0f, k == 1 ? g : 0.0f);
+    *reinterpret_cast<Wd*>(dx + base + W) = P::join(k == 2 ? g : 0.0f, k == 3 ? g : 0.0f);
+  }
+}
+
+
+// ================================================================================================
+// NHWC (channels_last) BatchNorm(train/eval) + ReLU [+ MaxPool 2x2] for conv outputs.
+//
+// The activation is a row-major [M, C] matrix (M = N*H*W, C % 8 == 0).  A thread owns 8 channels
+// (one 16-byte bf16 vector) of a row; tpr = C/8 threads cover a row, rpi = 256/tpr rows are in
+// flight per block.  Per layer and direction three kernels run:
+//   stats   : per-block partial sums (fp32 per thread, fixed-order LDS combine) -> part[s][blk][C]
+//   finalize: one wave per channel sums the block partials in double in a fixed shuffle order
+//             (deterministic), then writes the per-channel coefficients (+ running stats / dgamma,
+//             dbeta, dbias)
+//   apply   : elementwise, coefficients staged in LDS
+// The conv bias preceding the BN is folded in: it cancels in training-mode normalisation, so it
+// only enters the running mean (and eval-mode shift); its gradient is sum(dx), computed
+// analytically from the backward sums.  The ReLU mask is recomputed in backward from the saved
+// conv output with the forward's exact fp32 arithmetic (-ffp-contract=off), so y is never saved.
+// With POOL the 2x2/2 max pool consumes the ReLU output inside the apply kernel (pre-pool
+// activation never written) and backward routes dy through the 1-byte window code.
+//
+// stats layout [4][C] fp32: mean, invstd, scale = gamma*invstd, shift = beta - mean*scale.
+// coef  layout [2][C] fp32 (backward): e = -scale*invstd*dgamma/M, f = -scale*dbeta/M,
+//   dx = scale*dz + e*(h - mean) + f.
+// ================================================================================================
+
+template <typename T>
+struct V8;
+template <>
+struct V8<uint16_t> {
+  static __device__ __forceinline__ void ld(const uint16_t* p, float v[8]) {
+    const uint4 w = *reinterpret_cast<const uint4*>(p);
+    const uint32_t a[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[2 * j] = __uint_as_float(a[j] << 16);
+      v[2 * j + 1] = __uint_as_float(a[j] & 0xffff0000u);
+    }
+  }
+  static __device__ __forceinline__ void st(uint16_t* p, const float v[8]) {
+    uint4 w;
+    w.x = (uint32_t)ew_f2bf(v[0]) | ((uint32_t)ew_f2bf(v[1]) << 16);
+    w.y = (uint32_t)ew_f2bf(v[2]) | ((uint32_t)ew_f2bf(v[3]) << 16);
+    w.z = (uint32_t)ew_f2bf(v[4]) | ((uint32_t)ew_f2bf(v[5]) << 16);
+    w.w = (uint32_t)ew_f2bf(v[6]) | ((uint32_t)ew_f2bf(v[7]) << 16);
+    *reinterpret_cast<uint4*>(p) = w;
+  }
+  static __device__ __forceinline__ float rnd(float v) {
+    return __uint_as_float((uint32_t)ew_f2bf(v) << 16);
+  }
+};
+template <>
+struct V8<float> {
+  static __device__ __forceinline__ void ld(const float* p, float v[8]) {
+    const float4 a = *reinterpret_cast<const float4*>(p);
+    const float4 b = *reinterpret_cast<const float4*>(p + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  }
+  static __device__ __forceinline__ void st(float* p, const float v[8]) {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  }
+  static __device__ __forceinline__ float rnd(float v) { return v; }
+};
+
+__device__ __forceinline__ float ew_relu(float v) { return (v > 0.0f || v != v) ? v : 0.0f; }
+__device__ __forceinline__ bool ew_relu_pass(float v) { return !(v <= 0.0f); }  // NaN passes
+
+__device__ __forceinline__ void ew_ld_code8(const uint8_t* p, uint8_t c[8]) {
+  const uint2 w = *reinterpret_cast<const uint2*>(p);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    c[j] = (uint8_t)(w.x >> (8 * j));
+    c[4 + j] = (uint8_t)(w.y >> (8 * j));
+  }
+}
+
+// input row of pooled row p, window position q (0..3 row-major)
+__device__ __forceinline__ long long ew_pool_row(long long p, int q, int Ho, int Wo) {
+  const long long n = p / ((long long)Ho * Wo);
+  const int rem = (int)(p - n * Ho * Wo);
+  const int ho = rem / Wo, wo = rem - (rem / Wo) * Wo;
+  const int W = 2 * Wo;
+  return (n * (2 * Ho) + 2 * ho + (q >> 1)) * (long long)W + 2 * wo + (q & 1);
+}
+
+// ---- forward statistics: sum(h), sum(h^2) per channel ----
+template <typename T>
+__global__ __launch_bounds__(EW_BLOCK) void k_bn_fwd_stats(const T* __restrict__ h, long long M,
+                                                           int C, int rows_per_blk,
+                                                           float* __restrict__ part) {
+  __shared__ float ls[2048], lq[2048];
+  const int tpr = C >> 3, rpi = EW_BLOCK / tpr;
+  const int t = threadIdx.x, g = t % tpr, r = t / tpr;
+  const long long row0 = (long long)blockIdx.x * rows_per_blk;
+  const long long row1 = min(row0 + rows_per_blk, M);
+  float s[8], q[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s[j] = q[j] = 0.0f;
+  if (r < rpi) {
+    for (long long row = row0 + r; row < row1; row += rpi) {
+      float v[8];
+      V8<T>::ld(h + row * C + g * 8, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s[j] += v[j];
+        q[j] += v[j] * v[j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      ls[r * C + g * 8 + j] = s[j];
+      lq[r * C + g * 8 + j] = q[j];
+    }
+  }
+  __syncthreads();
+  const long long nb = gridDim.x;
+  for (int c = t; c < C; c += EW_BLOCK) {
+    float a = 0.0f, b = 0.0f;
+    for (int i = 0; i < rpi; ++i) {
+      a += ls[i * C + c];
+      b += lq[i * C + c];
+    }
+    part[(long long)blockIdx.x * C + c] = a;
+    part[(nb + blockIdx.x) * C + c] = b;
+  }
+}
+
+__device__ __forceinline__ double ew_wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// one wave per channel: sum the nblk partials of nsum quantities in a fixed order
+template <int NS>
+__device__ __forceinline__ void ew_sum_parts(const float* __restrict__ part, int nblk, int C,
+                                             int c, int lane, double out[NS]) {
+  double acc[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) acc[s] = 0.0;
+  for (int b = lane; b < nblk; b += 64) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) acc[s] += (double)part[((long long)s * nblk + b) * C + c];
+  }
+#pragma unroll
+  for (int s = 0; s < NS; ++s) out[s] = ew_wave_sum_d(acc[s]);
+}
+
+__global__ __launch_bounds__(EW_BLOCK) void k_bn_fwd_finalize(
+    const float* __restrict__ part, int nblk, int C, long long M, const float* __restrict__ gamma,
+    const float* __restrict__ beta, const float* __restrict__ cbias, float* __restrict__ rmean,
+    float* __restrict__ rvar, const long long* __restrict__ nbt, float momentum, float eps,
+    float* __restrict__ stats) {
+  const int c = blockIdx.x * EW_WAVES + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (c >= C) return;
+  double sums[2];
+  ew_sum_parts<2>(part, nblk, C, c, lane, sums);
+  if (lane != 0) return;
+  const double mean = sums[0] / (double)M;
+  double var = sums[1] / (double)M - mean * mean;
+  if (var < 0.0) var = 0.0;
+  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  const float mf = (float)mean;
+  const float g = gamma ? gamma[c] : 1.0f;
+  const float bb = beta ? beta[c] : 0.0f;
+  const float scale = g * invstd;
+  stats[c] = mf;
+  stats[C + c] = invstd;
+  stats[2 * C + c] = scale;
+  stats[3 * C + c] = bb - mf * scale;
+  if (rmean) {
+    // momentum < 0: cumulative moving average (nn.BatchNorm2d(momentum=None)), 1/num_batches
+    const float f = momentum >= 0.0f ? momentum : 1.0f / (float)(*nbt);
+    const double unb = M > 1 ? var * (double)M / (double)(M - 1) : var;
+    const float bm = mf + (cbias ? cbias[c] : 0.0f);
+    rmean[c] = (1.0f - f) * rmean[c] + f * bm;
+    rvar[c] = (1.0f - f) * rvar[c] + f * (float)unb;
+  }
+}
+
+// ---- forward apply: y = relu(h*scale + shift) [-> 2x2 max pool + code] ----
+template <typename T, bool POOL>
+__global__ __launch_bounds__(EW_BLOCK) void k_bn_fwd_apply(const T* __restrict__ h,
+                                                           T* __restrict__ y,
+                                                           uint8_t* __restrict__ code,
+                                                           const float* __restrict__ stats,
+                                                           long long rows, int C, int Ho, int Wo) {
+  __shared__ float lsc[2048], lsh[2048];
+  for (int c = threadIdx.x; c < C; c += EW_BLOCK) {
+    lsc[c] = stats[2 * C + c];
+    lsh[c] = stats[3 * C + c];
+  }
+  __syncthreads();
+  const int tpr = C >> 3;
+  const long long nvec = rows * tpr;
+  for (long long v = blockIdx.x * (long long)EW_BLOCK + threadIdx.x; v < nvec;
+       v += (long long)gridDim.x * EW_BLOCK) {
+    const long long row = v / tpr;
+    const int c0 = (int)(v - row * tpr) * 8;
+    float sc[8], sh[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      sc[j] = lsc[c0 + j];
+      sh[j] = lsh[c0 + j];
+    }
+    if constexpr (!POOL) {
+      float x[8];
+      V8<T>::ld(h + row * C + c0, x);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] = ew_relu(x[j] * sc[j] + sh[j]);
+      V8<T>::st(y + row * C + c0, x);
+    } else {
+      float m[8];
+      uint32_t k[8];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float x[8];
+        V8<T>::ld(h + ew_pool_row(row, q, Ho, Wo) * C + c0, x);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float yv = V8<T>::rnd(ew_relu(x[j] * sc[j] + sh[j]));
+          if (q == 0 || yv > m[j] || yv != yv) {
+            m[j] = yv;
+            k[j] = q;
+          }
+        }
+      }
+      V8<T>::st(y + row * C + c0, m);
+      uint2 w;
+      w.x = k[0] | (k[1] << 8) | (k[2] << 16) | (k[3] << 24);
+      w.y = k[4] | (k[5] << 8) | (k[6] << 16) | (k[7] << 24);
+      *reinterpret_cast<uint2*>(code + row * C + c0) = w;
+    }
+  }
+}
+
+// ---- backward statistics: sum(dz), sum(dz*(h-mean)), sum(h-mean), dz = relu'(v) * dy ----
+template <typename T, bool POOL>
+__global__ __launch_bounds__(EW_BLOCK) void k_bn_bwd_stats(
+    const T* __restrict__ h, const T* __restrict__ dy, const uint8_t* __restrict__ code,
+    const float* __restrict__ stats, long long rows, int C, int Ho, int Wo, int rows_per_blk,
+    float* __restrict__ part) {
+  __shared__ float l1[2048], l2[2048], l3[2048];
+  const int tpr = C >> 3, rpi = EW_BLOCK / tpr;
+  const int t = threadIdx.x, g = t % tpr, r = t / tpr;
+  const long long row0 = (long long)blockIdx.x * rows_per_blk;
+  const long long row1 = min(row0 + rows_per_blk, rows);
+  float s1[8], s2[8], s3[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s1[j] = s2[j] = s3[j] = 0.0f;
+  if (r < rpi) {
+    const int c0 = g * 8;
+    float mean[8], sc[8], sh[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      mean[j] = stats[c0 + j];
+      sc[j] = stats[2 * C + c0 + j];
+      sh[j] = stats[3 * C + c0 + j];
+    }
+    for (long long row = row0 + r; row < row1; row += rpi) {
+      float d[8];
+      V8<T>::ld(dy + row * C + c0, d);
+      if constexpr (!POOL) {
+        float x[8];
+        V8<T>::ld(h + row * C + c0, x);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float dz = ew_relu_pass(x[j] * sc[j] + sh[j]) ? d[j] : 0.0f;
+          const float xc = x[j] - mean[j];
+          s1[j] += dz;
+          s2[j] += dz * xc;
+          s3[j] += xc;
+        }
+      } else {
+        uint8_t k[8];
+        ew_ld_code8(code + row * C + c0, k);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float x[8];
+          V8<T>::ld(h + ew_pool_row(row, q, Ho, Wo) * C + c0, x);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float dz = (k[j] == q && ew_relu_pass(x[j] * sc[j] + sh[j])) ? d[j] : 0.0f;
+            const float xc = x[j] - mean[j];
+            s1[j] += dz;
+            s2[j] += dz * xc;
+            s3[j] += xc;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      l1[r * C + c0 + j] = s1[j];
+      l2[r * C + c0 + j] = s2[j];
+      l3[r * C + c0 + j] = s3[j];
+    }
+  }
+  __syncthreads();
+  const long long nb = gridDim.x;
+  for (int c = t; c < C; c += EW_BLOCK) {
+    float a = 0.0f, b = 0.0f, e = 0.0f;
+    for (int i = 0; i < rpi; ++i) {
+      a += l1[i * C + c];
+      b += l2[i * C + c];
+      e += l3[i * C + c];
+    }
+    part[(long long)blockIdx.x * C + c] = a;
+    part[(nb + blockIdx.x) * C + c] = b;
+    part[(2 * nb + blockIdx.x) * C + c] = e;
+  }
+}
+
+__global__ __launch_bounds__(EW_BLOCK) void k_bn_bwd_finalize(
+    const float* __restrict__ part, int nblk, int C, long long M, const float* __restrict__ stats,
+    float* __restrict__ coef, float* __restrict__ dgamma, float* __restrict__ dbeta,
+    float* __restrict__ dcbias) {
+  const int c = blockIdx.x * EW_WAVES + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (c >= C) return;
+  double sums[3];
+  ew_sum_parts<3>(part, nblk, C, c, lane, sums);
+  if (lane != 0) return;
+  const double invstd = stats[C + c], scale = stats[2 * C + c];
+  const double db = sums[0];             // sum dz
+  const double dg = sums[1] * invstd;    // sum dz * xhat
+  const double e = -scale * invstd * dg / (double)M;
+  coef[c] = (float)e;
+  coef[C + c] = (float)(-scale * db / (double)M);
+  if (dgamma) dgamma[c] = (float)dg;
+  if (dbeta) dbeta[c] = (float)db;
+  if (dcbias) dcbias[c] = (float)(e * sums[2]);  // sum over rows of dx = e * sum(h - mean)
+}
+
+template <typename T, bool POOL>
+__global__ __launch_bounds__(EW_BLOCK) void k_bn_bwd_apply(
+    const T* __restrict__ h, const T* __restrict__ dy, const uint8_t* __restrict__ code,
+    const float* __restrict__ stats, const float* __restrict__ coef, T* __restrict__ dx,
+    long long rows, int C, int Ho, int Wo) {
+  __shared__ float lm[2048], lsc[2048], lsh[2048], le[2048], lf[2048];
+  for (int c = threadIdx.x; c < C; c += EW_BLOCK) {
+    lm[c] = stats[c];
+    lsc[c] = stats[2 * C + c];
+    lsh[c] = stats[3 * C + c];
+    le[c] = coef[c];
+    lf[c] = coef[C + c];
+  }
+  __syncthreads();
+  const int tpr = C >> 3;
+  const long long nvec = rows * tpr;
+  for (long long v = blockIdx.x * (long long)EW_BLOCK + threadIdx.x; v < nvec;
+       v += (long long)gridDim.x * EW_BLOCK) {
+    const long long row = v / tpr;
+    const int c0 = (int)(v - row * tpr) * 8;
+    float d[8];
+    V8<T>::ld(dy + row * C + c0, d);
+    if constexpr (!POOL) {
+      float x[8], o[8];
+      V8<T>::ld(h + row * C + c0, x);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int c = c0 + j;
+        const float dz = ew_relu_pass(x[j] * lsc[c] + lsh[c]) ? d[j] : 0.0f;
+        o[j] = lsc[c] * dz + le[c] * (x[j] - lm[c]) + lf[c];
+      }
+      V8<T>::st(dx + row * C + c0, o);
+    } else {
+      uint8_t k[8];
+      ew_ld_code8(code + row * C + c0, k);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const long long ir = ew_pool_row(row, q, Ho, Wo);
+        float x[8], o[8];
+        V8<T>::ld(h + ir * C + c0, x);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int c = c0 + j;
+          const float dz = (k[j] == q && ew_relu_pass(x[j] * lsc[c] + lsh[c])) ? d[j] : 0.0f;
+          o[j] = lsc[c] * dz + le[c] * (x[j] - lm[c]) + lf[c];
+        }
+        V8<T>::st(dx + ir * C + c0, o);
+      }
+    }
+  }
+}
+
+// ---- standalone NHWC 2x2 max pool (no BN in front) ----
+template <typename T>
+__global__ __launch_bounds__(EW_BLOCK) void k_maxpool2_nhwc_fwd(const T* __restrict__ x,
+                                                                T* __restrict__ y,
+                                                                uint8_t* __restrict__ code,
+                                                                long long rows, int C, int Ho,
+                                                                int Wo) {
+  const int tpr = C >> 3;
+  const long long nvec = rows * tpr;
+  for (long long v = blockIdx.x * (long long)EW_BLOCK + threadIdx.x; v < nvec;
+       v += (long long)gridDim.x * EW_BLOCK) {
+    const long long row = v / tpr;
+    const int c0 = (int)(v - row * tpr) * 8;
+    float m[8];
+    uint32_t k[8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float a[8];
+      V8<T>::ld(x + ew_pool_row(row, q, Ho, Wo) * C + c0, a);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (q == 0 || a[j] > m[j] || a[j] != a[j]) {
+          m[j] = a[j];
+          k[j] = q;
+        }
+      }
+    }
+    V8<T>::st(y + row * C + c0, m);
+    uint2 w;
+    w.x = k[0] | (k[1] << 8) | (k[2] << 16) | (k[3] << 24);
+    w.y = k[4] | (k[5] << 8) | (k[6] << 16) | (k[7] << 24);
+    *reinterpret_cast<uint2*>(code + row * C + c0) = w;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(EW_BLOCK) void k_maxpool2_nhwc_bwd(const T* __restrict__ dy,
+                                                                const uint8_t* __restrict__ code,
+                                                                T* __restrict__ dx,
+                                                                long long rows, int C, int Ho,
+                                                                int Wo) {
+  const int tpr = C >> 3;
+  const long long nvec = rows * tpr;
+  for (long long v = blockIdx.x * (long long)EW_BLOCK + threadIdx.x; v < nvec;
+       v += (long long)gridDim.x * EW_BLOCK) {
+    const long long row = v / tpr;
+    const int c0 = (int)(v - row * tpr) * 8;
+    float d[8];
+    uint8_t k[8];
+    V8<T>::ld(dy + row * C + c0, d);
+    ew_ld_code8(code + row * C + c0, k);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = k[j] == q ? d[j] : 0.0f;
+      V8<T>::st(dx + ew_pool_row(row, q, Ho, Wo) * C + c0, o);
+    }
+  }
+}
+
+inline int ew_grid1(long long n) {
+  long long b = (n + EW_BLOCK - 1) / EW_BLOCK;
+  return (int)(b < 4096 ? (b > 0 ? b : 1) : 4096);
+}
+
+}  // namespace
+
+void ew_maxpool2_fwd(uintptr_t x, uintptr_t y, uintptr_t code, long long rows, int W, int is_bf16,
+                     uintptr_t stream) {
+  // rows = N*C*H/2 output rows of Wo = W/2 outputs each
+  const int Wo = W / 2;
+  const long long total = rows * Wo;
+  hipStream_t s = (hipStream_t)stream;
+  if (is_bf16)
+    hipLaunchKernelGGL(k_maxpool2_fwd<uint16_t>, dim3(ew_grid1(total)), dim3(EW_BLOCK), 0, s,
+                       reinterpret_cast<const uint16_t*>(x), reinterpret_cast<uint16_t*>(y),
+                       reinterpret_cast<uint8_t*>(code), total, Wo, W);
+  else
+    hipLaunchKernelGGL(k_maxpool2_fwd<float>, dim3(ew_grid1(total)), dim3(EW_BLOCK), 0, s,
+                       reinterpret_cast<const float*>(x), reinterpret_cast<float*>(y),
+                       reinterpret_cast<uint8_t*>(code), total, Wo, W);
+  EW_CHECK_LAUNCH();
+}
+
+void ew_maxpool2_bwd(uintptr_t dy, uintptr_t code, uintptr_t dx, long long rows, int W,
+                     int is_bf16, uintptr_t stream) {
+  const int Wo = W / 2;
+  const long long total = rows * Wo;
+  hipStream_t s = (hipStream_t)stream;
+  if (is_bf16)
+    hipLaunchKernelGGL(k_maxpool2_bwd<uint16_t>, dim3(ew_grid1(total)), dim3(EW_BLOCK), 0, s,
+                       reinterpret_cast<const uint16_t*>(dy), reinterpret_cast<const uint8_t*>(code),
+                       reinterpret_cast<uint16_t*>(dx), total, Wo, W);
+  else
+    hipLaunchKernelGGL(k_maxpool2_bwd<float>, dim3(ew_grid1(total)), dim3(EW_BLOCK), 0, s,
+                       reinterpret_cast<const float*>(dy), reinterpret_cast<const uint8_t*>(code),
+                       reinterpret_cast<float*>(dx), total, Wo, W);
+  EW_CHECK_LAUNCH();
+}
+
+// ---------------------------------------------------------------------------------------------
+// host side of the NHWC BN kernels
+
+// blocks / rows-per-block of a stats pass: >= 4 row iterations per thread, <= 1024 blocks and
+// nblk*C <= 256K partial floats per quantity (the workspace size the Python side allocates)
+static void ew_bn_grid(long long rows, int C, int* nblk, int* rows_per_blk) {
+  const int tpr = C / 8, rpi = EW_BLOCK / tpr;
+  long long iters = (rows + rpi - 1) / rpi;
+  long long nb = iters / 4;
+  long long cap = (1LL << 18) / C;
+  if (cap > 1024) cap = 1024;
+  if (nb > cap) nb = cap;
+  if (nb < 1) nb = 1;
+  long long rpb = (rows + nb - 1) / nb;
+  rpb = (rpb + rpi - 1) / rpi * rpi;
+  *rows_per_blk = (int)rpb;
+  *nblk = (int)((rows + rpb - 1) / rpb);
+}
+
+int ew_bn_part_floats() { return 3 * (1 << 18); }
+
+static int ew_grid_vec(long long nvec) {
+  long long b = (nvec + EW_BLOCK - 1) / EW_BLOCK;
+  const long long cap = 256LL * 16;  // 16 blocks per CU, grid-stride beyond
+  return (int)(b < cap ? (b > 0 ? b : 1) : cap);
+}
+
+
+void ew_bn_relu_fwd(const BnFwdArgs& a) {
+  hipStream_t s = (hipStream_t)a.stream;
+  const long long M = a.N * (long long)a.H * a.W;
+  const int Ho = a.H / 2, Wo = a.W / 2;
+  const int C = a.C;
+  if (a.training) {
+    int nblk, rpb;
+    ew_bn_grid(M, C, &nblk, &rpb);
+    float* part = reinterpret_cast<float*>(a.part);
+    if (a.is_bf16)
+      hipLaunchKernelGGL(k_bn_fwd_stats<uint16_t>, dim3(nblk), dim3(EW_BLOCK), 0, s,
+                         reinterpret_cast<const uint16_t*>(a.h), M, C, rpb, part);
+    else
+      hipLaunchKernelGGL(k_bn_fwd_stats<float>, dim3(nblk), dim3(EW_BLOCK), 0, s,
+                         reinterpret_cast<const float*>(a.h), M, C, rpb, part);
+    EW_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_bn_fwd_finalize, dim3((C + EW_WAVES - 1) / EW_WAVES), dim3(EW_BLOCK), 0,
+                       s, part, nblk, C, M, reinterpret_cast<const float*>(a.gamma),
+                       reinterpret_cast<const float*>(a.beta),
+                       reinterpret_cast<const float*>(a.cbias),
+                       reinterpret_cast<float*>(a.rmean), reinterpret_cast<float*>(a.rvar),
+                       reinterpret_cast<const long long*>(a.nbt), a.momentum, a.eps,
+                       reinterpret_cast<float*>(a.stats));
+    EW_CHECK_LAUNCH();
+  }
+  const float* st = reinterpret_cast<const float*>(a.stats);
+  uint8_t* code = reinterpret_cast<uint8_t*>(a.code);
+  if (a.pool) {
+    const long long rows = a.N * (long long)Ho * Wo;
+    const int grid = ew_grid_vec(rows * (C / 8));
+    if (a.is_bf16)
+      hipLaunchKernelGGL((k_bn_fwd_apply<uint16_t, true>), dim3(grid), dim3(EW_BLOCK), 0, s,
+                         reinterpret_cast<const uint16_t*>(a.h), reinterpret_cast<uint16_t*>(a.y),
+                         code, st, rows, C, Ho, Wo);
+    else
+      hipLaunchKernelGGL((k_bn_fwd_apply<float, true>), dim3(grid), dim3(EW_BLOCK), 0, s,
+                         reinterpret_cast<const float*>(a.h), reinterpret_cast<float*>(a.y), code,
+                         st, rows, C, Ho, Wo);
+  } else {
+    const int grid = ew_grid_vec(M * (C / 8));
+    if (a.is_bf16)
+      hipLaunchKernelGGL((k_bn_fwd_apply<uint16_t, false>), dim3(grid), dim3(EW_BLOCK), 0, s,
+                         reinterpret_cast<const uint16_t*>(a.h), reinterpret_cast<uint16_t*>(a.y),
+                         code, st, M, C, 0, 0);
+    else
+      hipLaunchKernelGGL((k_bn_fwd_apply<float, false>), dim3(grid), dim3(EW_BLOCK), 0, s,
+                         reinterpret_cast<const float*>(a.h), reinterpret_cast<float*>(a.y), code,
+                         st, M, C, 0, 0);
+  }
+  EW_CHECK_LAUNCH();
+}
+
+template <typename T, bool POOL>
+static void ew_bn_bwd_impl(const BnBwdArgs& a) {
+  hipStream_t s = (hipStream_t)a.stream;
+  const long long M = a.N * (long long)a.H * a.W;
+  const int Ho = a.H / 2, Wo = a.W / 2;
+  const int C = a.C;
+  const long long rows = POOL ? a.N * (long long)Ho * Wo : M;
+  int nblk, rpb;
+  ew_bn_grid(rows, C, &nblk, &rpb);
+  float* part = reinterpret_cast<float*>(a.part);
+  const T* h = reinterpret_cast<const T*>(a.h);
+  const T* dy = reinterpret_cast<const T*>(a.dy);
+  const uint8_t* code = reinterpret_cast<const uint8_t*>(a.code);
+  const float* st = reinterpret_cast<const float*>(a.stats);
+  float* coef = reinterpret_cast<float*>(a.coef);
+  hipLaunchKernelGGL((k_bn_bwd_stats<T, POOL>), dim3(nblk), dim3(EW_BLOCK), 0, s, h, dy, code,
+                     st, rows, C, Ho, Wo, rpb, part);
+  EW_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + EW_WAVES - 1) / EW_WAVES), dim3(EW_BLOCK), 0,
+                     s, part, nblk, C, M, st, coef, reinterpret_cast<float*>(a.dgamma),
+                     reinterpret_cast<float*>(a.dbeta), reinterpret_cast<float*>(a.dcbias));
+  EW_CHECK_LAUNCH();
+  hipLaunchKernelGGL((k_bn_bwd_apply<T, POOL>), dim3(ew_grid_vec(rows * (C / 8))),
+                     dim3(EW_BLOCK), 0, s, h, dy, code, st, coef, reinterpret_cast<T*>(a.dx), rows,
+                     C, Ho, Wo);
+  EW_CHECK_LAUNCH();
+}
+
+void ew_bn_relu_bwd(const BnBwdArgs& a) {
+  if (a.is_bf16) {
+    if (a.pool) ew_bn_bwd_impl<uint16_t, true>(a);
+    else ew_bn_bwd_impl<uint16_t, false>(a);
+  } else {
+    if (a.pool) ew_bn_bwd_impl<float, true>(a);
+    else ew_bn_bwd_impl<float, false>(a);
+  }
+}
+
+void ew_maxpool2_nhwc(uintptr_t x, uintptr_t y, uintptr_t code, long long N, int H, int W, int C,
+                      int is_bf16, int backward, uintptr_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const int Ho = H / 2, Wo = W / 2;
+  const long long rows = N * (long long)Ho * Wo;
+  const int grid = ew_grid_vec(rows * (C / 8));
+  uint8_t* cd = reinterpret_cast<uint8_t*>(code);
+  if (!backward) {
+    if (is_bf16)
+      hipLaunchKernelGGL(k_maxpool2_nhwc_fwd<uint16_t>, dim3(grid), dim3(EW_BLOCK), 0, s,
+                         reinterpret_cast<const uint16_t*>(x), reinterpret_cast<uint16_t*>(y), cd,
+                         rows, C, Ho, Wo);
+    else
+      hipLaunchKernelGGL(k_maxpool2_nhwc_fwd<float>, dim3(grid), dim3(EW_BLOCK), 0, s,
+                         reinterpret_cast<const float*>(x), reinterpret_cast<float*>(y), cd, rows,
+                         C, Ho, Wo);
+  } else {  // x = dy (pooled), y = dx (full)
+    if (is_bf16)
+      hipLaunchKernelGGL(k_maxpool2_nhwc_bwd<uint16_t>, dim3(grid), dim3(EW_BLOCK), 0, s,
+                         reinterpret_cast<const uint16_t*>(x), cd, reinterpret_cast<uint16_t*>(y),
+                         rows, C, Ho, Wo);
+    else
+      hipLaunchKernelGGL(k_maxpool2_nhwc_bwd<float>, dim3(grid), dim3(EW_BLOCK), 0, s,
+                         reinterpret_cast<const float*>(x), cd, reinterpret_cast<float*>(y), rows,
+                         C, Ho, Wo);
+  }
+  EW_CHECK_LAUNCH();
+}

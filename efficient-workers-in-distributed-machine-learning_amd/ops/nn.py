@@ -1,0 +1,210 @@
+"""Autograd wrappers of the model-side gfx950 kernels (``ops/csrc/nn.hip``).
+
+* :func:`bn_relu` -- training/eval BatchNorm2d + ReLU (+ the preceding conv's bias, + an optional
+  2x2/2 max pool) on channels_last activations in three kernels per direction.  Replaces, per VGG
+  block, PyTorch's conv-bias add + bias-grad reduction, MIOpen's NHWC batch-norm (fwd: 3 kernels,
+  bwd: 3), the ReLU clamp / threshold-backward and the max-pool forward/backward (int64 indices):
+  see ``profiles/vgg11_bs128_topk1pct_channels_last.txt`` for what they cost.
+* :func:`maxpool2x2` -- 2x2/2 max pool, NCHW or channels_last, 1-byte argmax codes.
+
+Semantics follow ``nn.BatchNorm2d`` (biased batch variance for normalisation, unbiased for the
+running variance, ``momentum=None`` = cumulative average, ``num_batches_tracked``) followed by
+``nn.ReLU`` and ``nn.MaxPool2d(2, 2)`` (first maximum of the row-major window wins, NaN wins).
+The conv bias cancels in training-mode normalisation: it is added to the batch mean only for the
+running mean, and its gradient is the exact sum of dx (``e * sum(h - mean)``, ~0).
+
+Parity: the reference builds these layers from ``nn.Conv2d/BatchNorm2d/ReLU/MaxPool2d``
+(``src/model_ops/vgg.py:39-52``); these are faster kernels for the same modules (same parameters,
+buffers and ``state_dict`` keys), nothing in the reference corresponds to them directly.
+"""
+import torch
+
+from . import _ptr, _stream, require
+
+_WS = {}
+
+
+def _part(device):
+    """Per (device, stream) scratch for the block partials (kernels on one stream run in order)."""
+    key = (device.index, _stream())
+    w = _WS.get(key)
+    if w is None:
+        w = torch.empty(require().bn_part_floats(), dtype=torch.float32, device=device)
+        _WS[key] = w
+    return w
+
+
+def nhwc_supported(x, pool=False):
+    """True if ``x`` can take the NHWC kernels: a device channels_last bf16/fp32 4-D tensor with
+    C % 8 == 0, C <= 2048 (and even H, W for pooling)."""
+    if not (x.is_cuda and x.dim() == 4 and x.dtype in (torch.bfloat16, torch.float32)):
+        return False
+    N, C, H, W = x.shape
+    if C % 8 or C > 2048 or N * H * W == 0:
+        return False
+    if not x.is_contiguous(memory_format=torch.channels_last) or x.data_ptr() % 16:
+        return False
+    return not pool or (H % 2 == 0 and W % 2 == 0)
+
+
+def _f32(t):
+    return None if t is None else t.detach().float().contiguous()
+
+
+class _BNReLU(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h, cbias, gamma, beta, rmean, rvar, nbt, momentum, eps, pool):
+        C_ = require()
+        N, C, H, W = h.shape
+        dev = h.device
+        out_hw = (H // 2, W // 2) if pool else (H, W)
+        y = torch.empty((N, C) + out_hw, dtype=h.dtype, device=dev,
+                        memory_format=torch.channels_last)
+        code = torch.empty((N,) + out_hw + (C,), dtype=torch.uint8, device=dev) if pool else None
+        stats = torch.empty(4 * C, dtype=torch.float32, device=dev)
+        g32, b32 = _f32(gamma), _f32(beta)
+        C_.bn_relu_fwd(_ptr(h), _ptr(y), _ptr(code), _ptr(stats), _ptr(_part(dev)), _ptr(g32),
+                       _ptr(b32), _ptr(_f32(cbias)), _ptr(rmean), _ptr(rvar), _ptr(nbt), N, H, W,
+                       C, int(h.dtype == torch.bfloat16), int(pool), 1,
+                       -1.0 if momentum is None else float(momentum), float(eps), _stream())
+        ctx.pool = pool
+        ctx.cb_dtype = None if cbias is None else cbias.dtype
+        ctx.save_for_backward(h, code, stats)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        C_ = require()
+        h, code, stats = ctx.saved_tensors
+        N, C, H, W = h.shape
+        dev = h.device
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        if dy.dtype != h.dtype:
+            dy = dy.to(h.dtype)
+        need = ctx.needs_input_grad
+        dx = torch.empty_like(h, memory_format=torch.channels_last)
+        coef = torch.empty(2 * C, dtype=torch.float32, device=dev)
+        dcb = torch.empty(C, dtype=torch.float32, device=dev) if need[1] else None
+        dg = torch.empty(C, dtype=torch.float32, device=dev) if need[2] else None
+        db = torch.empty(C, dtype=torch.float32, device=dev) if need[3] else None
+        C_.bn_relu_bwd(_ptr(h), _ptr(dy), _ptr(code), _ptr(stats), _ptr(coef), _ptr(_part(dev)),
+                       _ptr(dx), _ptr(dg), _ptr(db), _ptr(dcb), N, H, W, C,
+                       int(h.dtype == torch.bfloat16), int(ctx.pool), _stream())
+        if dcb is not None and ctx.cb_dtype != torch.float32:
+            dcb = dcb.to(ctx.cb_dtype)
+        return dx, dcb, dg, db, None, None, None, None, None, None
+
+
+def _apply_eval(h, stats, pool):
+    """Eval-mode (running statistics) forward, no autograd (callers use the torch composition
+    when a gradient is needed in eval mode)."""
+    C_ = require()
+    N, C, H, W = h.shape
+    dev = h.device
+    out_hw = (H // 2, W // 2) if pool else (H, W)
+    y = torch.empty((N, C) + out_hw, dtype=h.dtype, device=dev, memory_format=torch.channels_last)
+    code = torch.empty((N,) + out_hw + (C,), dtype=torch.uint8, device=dev) if pool else None
+    C_.bn_relu_fwd(_ptr(h), _ptr(y), _ptr(code), _ptr(stats), 0, 0, 0, 0, 0, 0, 0, N, H, W, C,
+                   int(h.dtype == torch.bfloat16), int(pool), 0, 0.0, 0.0, _stream())
+    return y
+
+
+def bn_relu_reference(h, cbias, bn, pool=False):
+    """The unfused torch composition (CPU path and numerics oracle)."""
+    import torch.nn.functional as F
+
+    if cbias is not None:
+        h = h + cbias.to(h.dtype).view(1, -1, 1, 1)
+    y = F.relu(bn(h))
+    return F.max_pool2d(y, 2, 2) if pool else y
+
+
+def bn_relu(h, cbias, bn, pool=False):
+    """``maxpool?(relu(bn(h + cbias)))`` for a ``nn.BatchNorm2d`` module ``bn`` (its running
+    statistics and ``num_batches_tracked`` are updated like its own forward would)."""
+    if not nhwc_supported(h, pool):
+        return bn_relu_reference(h, cbias, bn, pool)
+    batch_stats = bn.training or bn.running_mean is None
+    if batch_stats:
+        momentum = bn.momentum
+        nbt = None
+        if bn.training and bn.track_running_stats:
+            bn.num_batches_tracked.add_(1)
+            if momentum is None:
+                nbt = bn.num_batches_tracked
+        track = bn.training and bn.running_mean is not None
+        return _BNReLU.apply(h, cbias, bn.weight, bn.bias,
+                             bn.running_mean if track else None,
+                             bn.running_var if track else None, nbt, momentum, bn.eps, pool)
+    if torch.is_grad_enabled() and (h.requires_grad or (bn.weight is not None
+                                                        and bn.weight.requires_grad)):
+        return bn_relu_reference(h, cbias, bn, pool)
+    with torch.no_grad():
+        invstd = torch.rsqrt(bn.running_var.float() + bn.eps)
+        scale = invstd if bn.weight is None else bn.weight.float() * invstd
+        shift = -bn.running_mean.float() * scale
+        if cbias is not None:
+            shift = shift + cbias.float() * scale
+        if bn.bias is not None:
+            shift = shift + bn.bias.float()
+        stats = torch.cat([bn.running_mean.float(), invstd, scale, shift]).contiguous()
+    return _apply_eval(h.detach(), stats, pool)
+
+
+class _MaxPool2(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        C_ = require()
+        N, C, H, W = x.shape
+        nhwc = not x.is_contiguous() and x.is_contiguous(memory_format=torch.channels_last)
+        bf = int(x.dtype == torch.bfloat16)
+        if nhwc:
+            y = torch.empty((N, C, H // 2, W // 2), dtype=x.dtype, device=x.device,
+                            memory_format=torch.channels_last)
+            code = torch.empty((N, H // 2, W // 2, C), dtype=torch.uint8, device=x.device)
+            C_.maxpool2_nhwc(_ptr(x), _ptr(y), _ptr(code), N, H, W, C, bf, 0, _stream())
+        else:
+            y = torch.empty((N, C, H // 2, W // 2), dtype=x.dtype, device=x.device)
+            code = torch.empty((N, C, H // 2, W // 2), dtype=torch.uint8, device=x.device)
+            C_.maxpool2_fwd(_ptr(x), _ptr(y), _ptr(code), N * C * (H // 2), W, bf, _stream())
+        ctx.nhwc = nhwc
+        ctx.shape = x.shape
+        ctx.save_for_backward(code)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        C_ = require()
+        (code,) = ctx.saved_tensors
+        N, C, H, W = ctx.shape
+        bf = int(dy.dtype == torch.bfloat16)
+        if ctx.nhwc:
+            dy = dy.contiguous(memory_format=torch.channels_last)
+            dx = torch.empty((N, C, H, W), dtype=dy.dtype, device=dy.device,
+                             memory_format=torch.channels_last)
+            C_.maxpool2_nhwc(_ptr(dy), _ptr(dx), _ptr(code), N, H, W, C, bf, 1, _stream())
+        else:
+            dy = dy.contiguous()
+            dx = torch.empty((N, C, H, W), dtype=dy.dtype, device=dy.device)
+            C_.maxpool2_bwd(_ptr(dy), _ptr(code), _ptr(dx), N * C * (H // 2), W, bf, _stream())
+        return dx
+
+
+def maxpool2x2(x):
+    """``F.max_pool2d(x, 2, 2)`` (even H, W); HIP kernels for device bf16/fp32 NCHW or
+    channels_last tensors, torch otherwise."""
+    import torch.nn.functional as F
+
+    ok = (x.is_cuda and x.dim() == 4 and x.dtype in (torch.bfloat16, torch.float32)
+          and x.shape[2] % 2 == 0 and x.shape[3] % 2 == 0 and x.numel() > 0
+          and x.data_ptr() % 16 == 0)
+    if ok:
+        if x.is_contiguous():
+            ok = True
+        elif x.is_contiguous(memory_format=torch.channels_last):
+            ok = x.shape[1] % 8 == 0
+        else:
+            ok = False
+    if not ok:
+        return F.max_pool2d(x, 2, 2)
+    return _MaxPool2.apply(x)

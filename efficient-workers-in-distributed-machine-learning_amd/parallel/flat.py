@@ -29,6 +29,11 @@ def _align(n, a=ALIGN):
     return (n + a - 1) // a * a
 
 
+def _same_layout(g, p):
+    """Same memory order (strides of non-singleton dims equal)."""
+    return all(a == b for a, b, n in zip(g.stride(), p.stride(), p.shape) if n > 1)
+
+
 @dataclass
 class Bucket:
     index: int
@@ -188,10 +193,15 @@ class FlatModel:
         for p in b.params:
             g = p.grad
             if g is None:
-                g = torch.zeros_like(p, memory_format=torch.contiguous_format)
+                g = torch.zeros_like(p)  # p's strides (its flat memory order)
                 p.grad = g
-            elif not g.is_contiguous():  # the kernels read fp32 or bf16, densely
-                g = g.contiguous()
+            elif not _same_layout(g, p):
+                # the kernels read each gradient densely in the memory order of its slot in the
+                # flat buffer, i.e. with the parameter's strides (channels_last conv weights
+                # included); autograd normally already produces that layout
+                h = torch.empty_like(p, dtype=g.dtype)
+                h.copy_(g)
+                g = h
                 p.grad = g
             out.append(g)
         return out

@@ -20,6 +20,7 @@ from ..compress.codecs import make_codec
 from ..config import Config
 from ..data import DeviceLoader, load_dataset
 from ..models import build_model, canonical_name, input_shape
+from ..models.fused import set_enabled as set_fused_nn
 from ..optim.flat import make_optimizer
 from ..parallel.comm import Comm, init_distributed
 from ..parallel.engine import GradientExchange, Stopwatch, sync_buffers, sync_params
@@ -72,6 +73,11 @@ class Trainer:
 
         # data -------------------------------------------------------------------------------
         net = canonical_name(cfg.network)
+        set_fused_nn(cfg.fused_nn == "on")
+        # activations channels_last where the fused NHWC conv-BN-ReLU-pool kernels run (VGG on the
+        # GPU): MIOpen's convolutions are NHWC internally, so NCHW pays a transpose per conv
+        self.channels_last = cfg.layout == "nhwc" or (
+            cfg.layout == "auto" and self.cuda and cfg.fused_nn == "on" and net.startswith("vgg"))
         x, y, info = load_dataset(cfg.dataset, cfg.data_dir, train=True,
                                   synthetic_size=cfg.synthetic_size, seed=cfg.seed,
                                   device=self.device)
@@ -87,18 +93,18 @@ class Trainer:
                                        world=n_workers, shuffle=True,
                                        augment=cfg.augment and info["shape"][0] == 3,
                                        seed=cfg.seed, device=self.device,
-                                       channels_last=cfg.channels_last)
+                                       channels_last=self.channels_last)
         tx, ty, _ = load_dataset(cfg.dataset, cfg.data_dir, train=False,
                                  synthetic_size=(cfg.synthetic_size // 5) if cfg.synthetic_size else 0,
                                  seed=cfg.seed, device=self.device)
         self.test_loader = DeviceLoader(tx, ty, info, min(cfg.test_batch_size, tx.shape[0]),
                                         shuffle=False, augment=False, seed=cfg.seed,
-                                        device=self.device, channels_last=cfg.channels_last,
+                                        device=self.device, channels_last=self.channels_last,
                                         drop_last=False)
 
         # model / flat buffers / optimizer ------------------------------------------------------
         model = build_model(net, info["classes"]).to(self.device)
-        if cfg.channels_last:
+        if self.channels_last:
             model = model.to(memory_format=torch.channels_last)
         self.model = model
         # pointer-mode gradients (read in place by the HIP kernels) when the exchange is the plain

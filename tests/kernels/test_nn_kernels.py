@@ -1,0 +1,218 @@
+"""Numerics of the model-side HIP kernels (ops/csrc/nn.hip) against plain PyTorch fp32.
+
+* fused NHWC BatchNorm(+conv bias)+ReLU(+2x2 max pool): forward output, running statistics,
+  num_batches_tracked, and the gradients of the input, gamma, beta and the conv bias;
+* 2x2 max pool (NCHW and channels_last): exact values, exact gradient routing (ties included);
+* VGG-11 with the fused feature stack vs the module-by-module stack.
+"""
+import copy
+
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _ops():
+    from ewdml import ops
+    from ewdml.ops import nn as fnn
+
+    ops.require()
+    return fnn
+
+
+def _ref(h32, cb, bn, pool):
+    z = h32 + cb.view(1, -1, 1, 1) if cb is not None else h32
+    y = F.relu(bn(z))
+    return F.max_pool2d(y, 2, 2) if pool else y
+
+
+def _rel(a, b):
+    a, b = a.detach().float(), b.detach().float()
+    return float((a - b).norm() / (b.norm() + 1e-30))
+
+
+@pytest.mark.parametrize("shape,pool", [((8, 64, 32, 32), True), ((8, 64, 16, 16), False),
+                                        ((4, 512, 2, 2), True), ((6, 24, 6, 10), False),
+                                        ((2, 2048, 4, 4), False)])
+@pytest.mark.parametrize("momentum", [0.1, None])
+def test_bn_relu_fp32_matches_torch(shape, pool, momentum):
+    fnn = _ops()
+    torch.manual_seed(0)
+    dev = "cuda"
+    N, C, H, W = shape
+    h = (torch.randn(shape, device=dev) * 2 + 0.5).contiguous(memory_format=torch.channels_last)
+    cb = torch.randn(C, device=dev) * 0.1
+    bn = nn.BatchNorm2d(C, momentum=momentum).to(dev)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.2, 0.2)
+        bn.running_mean.uniform_(-0.1, 0.1)
+        bn.running_var.uniform_(0.9, 1.1)
+    bn_ref = copy.deepcopy(bn)
+    hh = h.clone().requires_grad_(True)
+    cbb = cb.clone().requires_grad_(True)
+    y = fnn.bn_relu(hh, cbb, bn, pool)
+    hr = h.clone().contiguous().requires_grad_(True)
+    cbr = cb.clone().requires_grad_(True)
+    yr = _ref(hr, cbr, bn_ref, pool)
+    assert y.shape == yr.shape and y.is_contiguous(memory_format=torch.channels_last)
+    assert _rel(y, yr) < 1e-5
+    assert torch.allclose(bn.running_mean, bn_ref.running_mean, atol=1e-5, rtol=1e-5)
+    assert torch.allclose(bn.running_var, bn_ref.running_var, atol=1e-5, rtol=1e-5)
+    assert int(bn.num_batches_tracked) == int(bn_ref.num_batches_tracked) == 1
+    dy = torch.randn_like(yr)
+    y.backward(dy.contiguous(memory_format=torch.channels_last))
+    yr.backward(dy)
+    assert _rel(hh.grad, hr.grad) < 1e-4
+    assert _rel(bn.weight.grad, bn_ref.weight.grad) < 1e-4
+    assert _rel(bn.bias.grad, bn_ref.bias.grad) < 1e-4
+    # the conv bias cancels in batch-norm: both gradients are rounding noise around 0
+    scale = float(hr.grad.abs().sum())
+    assert float(cbb.grad.abs().max()) < 1e-3 * scale / C + 1e-3
+    assert float(cbr.grad.abs().max()) < 1e-3 * scale / C + 1e-3
+
+
+@pytest.mark.parametrize("pool", [False, True])
+def test_bn_relu_bf16_close_to_fp32(pool):
+    fnn = _ops()
+    torch.manual_seed(1)
+    dev = "cuda"
+    shape = (16, 128, 16, 16)
+    C = shape[1]
+    h32 = torch.randn(shape, device=dev) * 3 - 1
+    h = h32.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    bn = nn.BatchNorm2d(C).to(dev)
+    bn_ref = copy.deepcopy(bn)
+    hh = h.clone().requires_grad_(True)
+    y = fnn.bn_relu(hh, None, bn, pool)
+    assert y.dtype == torch.bfloat16
+    hr = h.float().contiguous().requires_grad_(True)
+    yr = _ref(hr, None, bn_ref, pool)
+    assert _rel(y, yr) < 1e-2
+    assert torch.allclose(bn.running_mean, bn_ref.running_mean, atol=1e-4, rtol=1e-4)
+    assert torch.allclose(bn.running_var, bn_ref.running_var, atol=1e-4, rtol=1e-4)
+    if not pool:  # pooled bf16 argmax may differ from fp32 on bf16 ties; see the next test
+        dy = torch.randn_like(yr)
+        y.backward(dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last))
+        yr.backward(dy.to(torch.bfloat16).float())
+        assert _rel(hh.grad, hr.grad) < 2e-2
+        assert _rel(bn.weight.grad, bn_ref.weight.grad) < 1e-2
+        assert _rel(bn.bias.grad, bn_ref.bias.grad) < 1e-2
+
+
+def test_bn_relu_pool_equals_unpooled_then_pool_bf16():
+    """The fused pool is exactly max_pool2d of the fused unpooled output (same bf16 values, same
+    first-max routing), and its gradient matches routing dy through torch's max-pool backward."""
+    fnn = _ops()
+    torch.manual_seed(2)
+    dev = "cuda"
+    shape = (8, 64, 8, 8)
+    h = (torch.randn(shape, device=dev)).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    bn1 = nn.BatchNorm2d(64).to(dev)
+    bn2 = copy.deepcopy(bn1)
+    a = h.clone().requires_grad_(True)
+    yp = fnn.bn_relu(a, None, bn1, True)
+    b = h.clone().requires_grad_(True)
+    yf = fnn.bn_relu(b, None, bn2, False)
+    yfp = F.max_pool2d(yf, 2, 2)
+    assert torch.equal(yp.float(), yfp.float())
+    dy = torch.randn(yp.shape, device=dev).to(torch.bfloat16)
+    yp.backward(dy.contiguous(memory_format=torch.channels_last))
+    yfp.backward(dy.contiguous(memory_format=torch.channels_last))
+    assert _rel(a.grad, b.grad) < 1e-2
+
+
+def test_bn_relu_eval_mode():
+    fnn = _ops()
+    torch.manual_seed(3)
+    dev = "cuda"
+    h = torch.randn(4, 32, 8, 8, device=dev).contiguous(memory_format=torch.channels_last)
+    cb = torch.randn(32, device=dev)
+    bn = nn.BatchNorm2d(32).to(dev)
+    with torch.no_grad():
+        bn.running_mean.uniform_(-1, 1)
+        bn.running_var.uniform_(0.5, 2)
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-1, 1)
+    bn.eval()
+    for pool in (False, True):
+        with torch.no_grad():
+            y = fnn.bn_relu(h, cb, bn, pool)
+            yr = _ref(h.contiguous(), cb, bn, pool)
+        assert _rel(y, yr) < 1e-5
+
+
+@pytest.mark.parametrize("layout", ["nchw", "nhwc"])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_maxpool2x2_exact(layout, dtype):
+    fnn = _ops()
+    torch.manual_seed(4)
+    x = torch.randint(-3, 4, (4, 16, 12, 10), device="cuda").to(dtype)  # many ties
+    x[0, 0, 0, 0] = float("nan")
+    if layout == "nhwc":
+        x = x.contiguous(memory_format=torch.channels_last)
+    a = x.clone().requires_grad_(True)
+    y = fnn.maxpool2x2(a)
+    b = x.clone().requires_grad_(True)
+    yr = F.max_pool2d(b, 2, 2)
+    assert torch.equal(torch.nan_to_num(y.float(), 99.0), torch.nan_to_num(yr.float(), 99.0))
+    dy = torch.randn(yr.shape, device="cuda").to(dtype)
+    y.backward(dy)
+    yr.backward(dy)
+    assert torch.equal(a.grad.float(), b.grad.float())
+
+
+def _vgg_run(model, x, y, fused_on, amp):
+    from ewdml.models import fused
+
+    fused.set_enabled(fused_on)
+    torch.manual_seed(7)  # same dropout masks in every run
+    try:
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+            out = model(x)
+        F.cross_entropy(out.float(), y).backward()
+    finally:
+        fused.set_enabled(True)
+    grads = {n: p.grad.detach().float().clone() for n, p in model.named_parameters()}
+    return out.detach().float(), grads
+
+
+def test_vgg11_fused_matches_modules():
+    """fp32: the fused feature stack equals the module stack to fp32 rounding.  bf16 autocast: the
+    fused stack is no further from the fp32 gradients than the module stack is."""
+    from ewdml.models import build_model
+
+    _ops()
+    torch.manual_seed(5)
+    base = build_model("vgg11", 10).cuda().to(memory_format=torch.channels_last)
+    for mod in base.modules():  # dropout draws differ between fp32 and bf16 kernels
+        if isinstance(mod, nn.Dropout):
+            mod.p = 0.0
+    x = torch.randn(32, 3, 32, 32, device="cuda").contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (32,), device="cuda")
+    runs = {}
+    for key in [(True, False), (False, False), (True, True), (False, True)]:
+        m = copy.deepcopy(base)
+        runs[key] = _vgg_run(m, x, y, *key) + (m,)
+    conv_bias = {n + ".bias" for n, mod in base.named_modules() if isinstance(mod, nn.Conv2d)
+                 and n.startswith("features")}
+    (o_f, g_f, m_f), (o_m, g_m, m_m) = runs[(True, False)], runs[(False, False)]
+    assert _rel(o_f, o_m) < 1e-4
+    for n in g_m:
+        if n in conv_bias:  # cancels in batch-norm: rounding noise around 0 in both
+            continue
+        assert _rel(g_f[n], g_m[n]) < 2e-3, n
+    for (n, b1), (_, b2) in zip(m_f.named_buffers(), m_m.named_buffers()):
+        assert torch.allclose(b1.float(), b2.float(), rtol=1e-4, atol=1e-5), n
+    (ob_f, gb_f, _), (ob_m, gb_m, _) = runs[(True, True)], runs[(False, True)]
+    assert _rel(ob_f, o_m) < 5e-2 and _rel(ob_m, o_m) < 5e-2
+    errs = {n: (_rel(gb_f[n], g_m[n]), _rel(gb_m[n], g_m[n])) for n in g_m if n not in conv_bias}
+    print("bf16 grad error vs fp32 (fused, modules):",
+          {n: (round(a, 4), round(b, 4)) for n, (a, b) in errs.items()})
+    err_f = sum(a for a, _ in errs.values())
+    err_m = sum(b for _, b in errs.values())
+    assert err_f < 1.5 * err_m + 1e-2, (err_f, err_m)

@@ -49,3 +49,41 @@ def test_imagenet_resnet50_224():
     m = build_model("resnet50_imagenet", 1000).eval()
     with torch.no_grad():
         assert m(torch.randn(1, 3, 224, 224)).shape == (1, 1000)
+
+
+def test_vgg_fused_features_is_a_plain_sequential_on_cpu():
+    """FusedFeatures keeps nn.Sequential's modules/state_dict keys and is exactly its forward on
+    the CPU; its plan groups conv-BN-ReLU[-pool]."""
+    import torch.nn as nn
+
+    from ewdml.models.fused import FusedFeatures
+
+    torch.manual_seed(0)
+    m = build_model("VGG11", 10).train()
+    assert isinstance(m.features, FusedFeatures)
+    keys = list(m.state_dict())
+    assert keys[:6] == ["features.0.weight", "features.0.bias", "features.1.weight",
+                        "features.1.bias", "features.1.running_mean", "features.1.running_var"]
+    plan = m.features._plan()
+    assert [k for k, _, _ in plan] == ["cbr"] * 8
+    assert [p for _, _, p in plan] == [True, True, False, True, False, True, False, True]
+    x = torch.randn(4, 3, 32, 32)
+    ref = nn.Sequential(*list(m.features))
+    torch.testing.assert_close(m.features(x), ref(x), rtol=0, atol=0)
+
+
+def test_flat_model_keeps_channels_last_param_layout():
+    from ewdml.parallel.flat import FlatModel
+
+    m = build_model("VGG11", 10).to(memory_format=torch.channels_last)
+    w = m.features[4].weight
+    flat = FlatModel(m, attach_grads=False)
+    assert w.is_contiguous(memory_format=torch.channels_last)
+    x = torch.randn(2, 3, 32, 32).contiguous(memory_format=torch.channels_last)
+    flat.zero_grad()
+    m(x).sum().backward()
+    g_before = w.grad
+    grads = [g for b in flat.buckets for g in flat.bucket_grads(b)]
+    # a gradient already in the parameter's memory order is read in place (no copy)
+    assert any(g.data_ptr() == g_before.data_ptr() for g in grads)
+    assert w.grad.stride() == w.stride()
