@@ -86,6 +86,7 @@ class Config:
     channels_last: bool = False  # alias of layout="nhwc"
     layout: str = "auto"  # auto (nhwc on the GPU when the fused NHWC kernels run) | nchw | nhwc
     fused_nn: str = "on"  # on: conv-BN-ReLU-pool groups / 2x2 pools through ops/csrc/nn.hip | off
+    fused_data: str = "on"  # on: training batches built by one graph-capturable kernel (GPU) | off
     hip_graph: str = "off"  # off | split (graphs around eager RCCL calls) | full (one graph)
     graph_warmup: int = 3  # eager steps (>= 1) before capture: MIOpen find, handles, momentum
 
@@ -201,6 +202,7 @@ def build_parser(prog="distributed_nn.py") -> argparse.ArgumentParser:
     a("--channels-last", action="store_true", default=False)
     a("--layout", type=str, default=d.layout, choices=["auto", "nchw", "nhwc"])
     a("--fused-nn", type=str, default=d.fused_nn, choices=["on", "off"])
+    a("--fused-data", type=str, default=d.fused_data, choices=["on", "off"])
     a("--hip-graph", type=str, default=d.hip_graph, choices=["off", "split", "full"])
     a("--graph-warmup", type=int, default=d.graph_warmup)
     a("--data-dir", type=str, default=None)

@@ -6,6 +6,12 @@ r, r+W, r+2W, ... truncated so that every rank gets exactly the same number of f
 (``torch.utils.data.DistributedSampler`` semantics with drop_last).  Batches are gathered by index,
 converted to float, optionally augmented (CIFAR: reflect-pad 4 / random crop 32 / h-flip, as
 ``util.py:38-48``) and normalised, all on the device.
+
+``fused=True`` (GPU training loaders): the whole batch is built by ONE kernel
+(``ops.make_batch``, ``ops/csrc/data.hip``) into static output buffers, with the batch position
+kept on the device so the launch can be captured in the training step's HIP graph
+(:meth:`emit`); the host only tracks the position to roll epochs over (:meth:`begin_step`).
+Augmentation draws then come from a counter hash instead of ``torch.Generator``.
 """
 import torch
 import torch.nn.functional as F
@@ -28,7 +34,8 @@ def augment_cifar(x: torch.Tensor, gen: torch.Generator = None, pad: int = 4) ->
 
 class DeviceLoader:
     def __init__(self, x, y, info, batch_size, rank=0, world=1, shuffle=True, augment=False,
-                 seed=0, device=None, channels_last=False, drop_last=True):
+                 seed=0, device=None, channels_last=False, drop_last=True, fused=False,
+                 out_dtype=torch.float32):
         self.device = torch.device(device) if device is not None else x.device
         self.x = x.to(self.device)
         self.y = y.to(self.device)
@@ -52,6 +59,23 @@ class DeviceLoader:
         self._gen = torch.Generator(device=self.device)
         self._idx = None
         self._pos = 0
+        self.fused = bool(fused) and drop_last and self.device.type == "cuda" and \
+            self.x.dim() == 4 and self.x.dtype == torch.uint8 and self.x.shape[1] <= 4
+        if self.fused:
+            from .. import ops
+
+            ops.require()
+            self.x = self.x.contiguous()
+            self._mean_l = [float(v) for v in info["mean"]]
+            self._istd_l = [1.0 / float(v) for v in info["std"]]
+            B, (C, H, W) = batch_size, self.x.shape[1:]
+            fmt = torch.channels_last if channels_last else torch.contiguous_format
+            self.bx = torch.empty((B, C, H, W), dtype=out_dtype, device=self.device,
+                                  memory_format=fmt)
+            self.by = torch.empty(B, dtype=torch.int64, device=self.device)
+            self._state = torch.zeros(2, dtype=torch.int64, device=self.device)  # pos, epoch
+            self._done = torch.zeros(1, dtype=torch.int32, device=self.device)
+            self._perm = torch.empty(self.per_rank, dtype=torch.int64, device=self.device)
         self._start_epoch(0)
 
     def _start_epoch(self, epoch):
@@ -68,6 +92,10 @@ class DeviceLoader:
         self._idx = perm[self.rank::self.world][:self.per_rank]
         self._gen.manual_seed(self.seed * 7919 + epoch * 31 + self.rank)
         self._pos = 0
+        if self.fused:  # device-side state read by the (possibly graph-captured) batch kernel
+            self._perm.copy_(self._idx)
+            self._state[0].zero_()
+            self._state[1].fill_(epoch)
 
     def __len__(self):
         return self.batches_per_epoch
@@ -84,10 +112,38 @@ class DeviceLoader:
             x = x.contiguous(memory_format=torch.channels_last)
         return x, self.y.index_select(0, idx)
 
-    def next(self):
-        """Next batch; rolls over to the next epoch (same count on every rank)."""
+    def begin_step(self):
+        """Roll over to the next epoch if this one is exhausted (host side; same on every rank)."""
         if self._pos >= self.batches_per_epoch:
             self._start_epoch(self.epoch + 1)
+
+    def emit(self):
+        """(fused) Launch the batch kernel for the device-side position and return the static
+        (x, y) buffers; graph-capturable.  The caller advances the host position (:meth:`advance`)."""
+        from .. import ops
+
+        ops.make_batch(self.x, self.y, self._perm, self._state, self._done, self.bx, self.by,
+                       self._mean_l, self._istd_l, pad=4, augment=self.augment,
+                       seed=self.seed * 7919 + 17, rank=self.rank)
+        return self.bx, self.by
+
+    def advance(self):
+        self._pos += 1
+
+    def seek(self, pos):
+        """Position within the current epoch (resume)."""
+        self._pos = int(pos)
+        if self.fused:
+            self._state[0].fill_(self._pos)
+
+    def next(self, static=False):
+        """Next batch; rolls over to the next epoch (same count on every rank).  Fused loaders
+        return their static buffers when ``static`` (overwritten by the next call), else copies."""
+        self.begin_step()
+        if self.fused:
+            x, y = self.emit()
+            self.advance()
+            return (x, y) if static else (x.clone(memory_format=torch.preserve_format), y.clone())
         s = self._pos * self.batch_size
         self._pos += 1
         return self._make(self._idx[s:s + self.batch_size])
@@ -98,3 +154,33 @@ class DeviceLoader:
             self._start_epoch(self.epoch + 1)
         for _ in range(self.batches_per_epoch - self._pos):
             yield self.next()
+
+
+def fused_draws(seed, rank, epoch, slot, pad=4):
+    """(dy, dx, flip) of the fused batch kernel for one sample slot (== ``csrc/data.hip``)."""
+    from ..compress.rng import M32, mix32_int
+
+    a = mix32_int((seed * 0x9E3779B9 + rank) & M32)
+    b = mix32_int((epoch * 0x85EBCA6B + slot) & M32)
+    h = mix32_int(a ^ b)
+    span = 2 * pad + 1
+    return (h & 0xFF) % span, ((h >> 8) & 0xFF) % span, (h >> 16) & 1
+
+
+def reference_fused_batch(x, y, perm, pos, batch, mean, inv_std, augment, seed, rank, epoch,
+                          pad=4):
+    """Torch oracle of ``ops.make_batch`` (fp32 NCHW; the kernel's arithmetic, same draws)."""
+    idx = perm[pos * batch:(pos + 1) * batch]
+    xs = x.index_select(0, idx).to(torch.float32)
+    n, c, h, w = xs.shape
+    if augment:
+        xp = F.pad(xs, (pad, pad, pad, pad), mode="reflect")
+        out = torch.empty_like(xs)
+        for b in range(n):
+            dy, dx, flip = fused_draws(seed, rank, epoch, pos * batch + b, pad)
+            crop = xp[b, :, dy:dy + h, dx:dx + w]
+            out[b] = crop.flip(-1) if flip else crop
+        xs = out
+    m = torch.tensor(mean, dtype=torch.float32, device=xs.device).view(1, -1, 1, 1)
+    s = torch.tensor(inv_std, dtype=torch.float32, device=xs.device).view(1, -1, 1, 1)
+    return (xs * (1.0 / 255.0) - m) * s, y.index_select(0, idx)

@@ -313,6 +313,39 @@ def cast_scale(src, dst, scale=1.0):
                  int(dst.dtype == torch.bfloat16), _stream())
 
 
+
+def make_batch(src, labels, perm, state, done, out, out_y, mean, inv_std, pad=4, augment=True,
+               seed=0, rank=0):
+    """Fused batch construction (``csrc/data.hip``): ``out[b] = normalise(augment(src[perm[pos*B
+    + b]]))``, ``out_y[b] = labels[...]`` with ``pos = state[0]`` (advanced by the kernel)."""
+    C_ = require()
+    B = out.shape[0]
+    N, C, H, W = src.shape
+    if src.dtype != torch.uint8 or not src.is_contiguous() or not src.is_cuda:
+        raise ValueError("src must be a contiguous uint8 device tensor [N, C, H, W]")
+    if C > 4 or len(mean) != C or len(inv_std) != C:
+        raise ValueError("make_batch supports C <= 4 channels with per-channel mean/std")
+    if tuple(out.shape) != (B, C, H, W) or out.dtype not in (torch.float32, torch.bfloat16):
+        raise ValueError("out must be fp32/bf16 [B, C, H, W]")
+    cl = not out.is_contiguous()
+    if cl and not out.is_contiguous(memory_format=torch.channels_last):
+        raise ValueError("out must be NCHW- or channels_last-contiguous")
+    for t, dt, n in ((labels, torch.int64, "labels"), (perm, torch.int64, "perm"),
+                     (state, torch.int64, "state"), (out_y, torch.int64, "out_y"),
+                     (done, torch.int32, "done")):
+        _check(t, dt, n, align=4)
+    if state.numel() != 2 or out_y.numel() != B or labels.numel() != N:
+        raise ValueError("state must be int64[2], out_y int64[B], labels int64[N]")
+    if perm.numel() < B or B * H * W >= 2 ** 31:
+        raise ValueError("perm shorter than one batch / batch too large")
+    if augment and 2 * pad + 1 > 256:
+        raise ValueError("pad too large")
+    C_.make_batch(_ptr(src), _ptr(labels), _ptr(perm), perm.numel(), _ptr(state), _ptr(done), _ptr(out),
+                  _ptr(out_y), B, C, H, W, int(pad), int(bool(augment)),
+                  int(out.dtype == torch.bfloat16), int(cl), int(seed) & 0xFFFFFFFF,
+                  int(rank) & 0xFFFFFFFF, [float(v) for v in mean], [float(v) for v in inv_std],
+                  _stream())
+
 def build(force: bool = False) -> str:
     from .build import build as _b
     return _b(force=force)

@@ -216,27 +216,45 @@ PYBIND11_MODULE(_C, m) {
         [](uintptr_t h, uintptr_t y, uintptr_t code, uintptr_t stats, uintptr_t part,
            uintptr_t gamma, uintptr_t beta, uintptr_t cbias, uintptr_t rmean, uintptr_t rvar,
            uintptr_t nbt, long long N, int H, int W, int C, int is_bf16, int pool, int training,
-           float momentum, float eps, uintptr_t stream) {
+           float momentum, float eps, int cb_bf16, uintptr_t stream) {
           BnFwdArgs a{};
           a.h = h; a.y = y; a.code = code; a.stats = stats; a.part = part;
           a.gamma = gamma; a.beta = beta; a.cbias = cbias; a.rmean = rmean; a.rvar = rvar;
           a.nbt = nbt; a.N = N; a.H = H; a.W = W; a.C = C;
           a.is_bf16 = is_bf16; a.pool = pool; a.training = training;
-          a.momentum = momentum; a.eps = eps; a.stream = stream;
+          a.momentum = momentum; a.eps = eps; a.cb_bf16 = cb_bf16; a.stream = stream;
           ew_bn_relu_fwd(a);
         });
   m.def("bn_relu_bwd",
         [](uintptr_t h, uintptr_t dy, uintptr_t code, uintptr_t stats, uintptr_t coef,
            uintptr_t part, uintptr_t dx, uintptr_t dgamma, uintptr_t dbeta, uintptr_t dcbias,
-           long long N, int H, int W, int C, int is_bf16, int pool, uintptr_t stream) {
+           long long N, int H, int W, int C, int is_bf16, int pool, int cb_bf16,
+           uintptr_t stream) {
           BnBwdArgs a{};
           a.h = h; a.dy = dy; a.code = code; a.stats = stats; a.coef = coef; a.part = part;
           a.dx = dx; a.dgamma = dgamma; a.dbeta = dbeta; a.dcbias = dcbias;
           a.N = N; a.H = H; a.W = W; a.C = C; a.is_bf16 = is_bf16; a.pool = pool;
-          a.stream = stream;
+          a.cb_bf16 = cb_bf16; a.stream = stream;
           ew_bn_relu_bwd(a);
         });
   m.def("maxpool2_nhwc", &ew_maxpool2_nhwc);
   m.def("maxpool2_fwd", &ew_maxpool2_fwd);
   m.def("maxpool2_bwd", &ew_maxpool2_bwd);
+  m.def("make_batch",
+        [](uintptr_t src, uintptr_t labels, uintptr_t perm, long long perm_len, uintptr_t state,
+           uintptr_t done, uintptr_t out, uintptr_t out_y, int B, int C, int H, int W, int pad, int augment,
+           int out_bf16, int channels_last, uint32_t seed, uint32_t rank,
+           const std::vector<float>& mean, const std::vector<float>& inv_std, uintptr_t stream) {
+          MakeBatchArgs a{};
+          a.src = src; a.labels = labels; a.perm = perm; a.perm_len = perm_len; a.state = state; a.done = done;
+          a.out = out; a.out_y = out_y; a.B = B; a.C = C; a.H = H; a.W = W; a.pad = pad;
+          a.augment = augment; a.out_bf16 = out_bf16; a.channels_last = channels_last;
+          a.seed = seed; a.rank = rank;
+          for (int c = 0; c < 4; ++c) {
+            a.mean[c] = c < (int)mean.size() ? mean[c] : 0.0f;
+            a.inv_std[c] = c < (int)inv_std.size() ? inv_std[c] : 1.0f;
+          }
+          a.stream = stream;
+          ew_make_batch(a);
+        });
 }

@@ -92,19 +92,20 @@ void ew_cast_scale(uintptr_t src, uintptr_t dst, long long n, float scale, int t
 // NHWC BatchNorm + ReLU [+ 2x2 max pool]; h/y/dy/dx bf16 or fp32 ([N,H,W,C] memory), C % 8 == 0
 struct BnFwdArgs {
   uintptr_t h, y, code, stats, part;        // stats fp32 [4][C]; part: ew_bn_part_floats() floats
-  uintptr_t gamma, beta, cbias, rmean, rvar, nbt;  // fp32 [C] (nullable), nbt int64 (nullable)
+  uintptr_t gamma, beta, cbias, rmean, rvar, nbt;  // fp32 [C] (nullable; cbias fp32 or bf16),
+  //                                                  nbt int64 (nullable): incremented once
   long long N;
   int H, W, C;
-  int is_bf16, pool, training;
+  int is_bf16, pool, training, cb_bf16;
   float momentum, eps;  // momentum < 0: cumulative average over *nbt batches
   uintptr_t stream;
 };
 struct BnBwdArgs {
   uintptr_t h, dy, code, stats, coef, part, dx;  // coef fp32 [2][C]
-  uintptr_t dgamma, dbeta, dcbias;               // fp32 [C] outputs (nullable)
+  uintptr_t dgamma, dbeta, dcbias;               // [C] outputs (nullable), dcbias bf16 if cb_bf16
   long long N;
   int H, W, C;  // of h (pre-pool)
-  int is_bf16, pool;
+  int is_bf16, pool, cb_bf16;
   uintptr_t stream;
 };
 int ew_bn_part_floats();
@@ -117,3 +118,19 @@ void ew_maxpool2_fwd(uintptr_t x, uintptr_t y, uintptr_t code, long long rows, i
                      uintptr_t stream);
 void ew_maxpool2_bwd(uintptr_t dy, uintptr_t code, uintptr_t dx, long long rows, int W,
                      int is_bf16, uintptr_t stream);
+
+// ---- fused input pipeline (data.hip) ----
+struct MakeBatchArgs {
+  uintptr_t src;     // uint8 [N, C, H, W] dataset
+  uintptr_t labels;  // int64 [N]
+  uintptr_t perm;    // int64 [>= (pos+1)*B] this rank's sample order for the epoch
+  uintptr_t state;   // int64 [2] {pos, epoch}; pos advanced by the kernel
+  uintptr_t done;    // uint32 [1] zero-initialised block counter (kernel resets it)
+  long long perm_len;
+  uintptr_t out, out_y;  // fp32/bf16 [B, C, H, W] (NCHW or channels_last), int64 [B]
+  int B, C, H, W, pad, augment, out_bf16, channels_last;
+  uint32_t seed, rank;
+  float mean[4], inv_std[4];
+  uintptr_t stream;
+};
+void ew_make_batch(const MakeBatchArgs& a);

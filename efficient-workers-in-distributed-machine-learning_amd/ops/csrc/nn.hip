@@ -160,13 +160,17 @@ __device__ __forceinline__ void ew_ld_code8(const uint8_t* p, uint8_t c[8]) {
   }
 }
 
-// input row of pooled row p, window position q (0..3 row-major)
-__device__ __forceinline__ long long ew_pool_row(long long p, int q, int Ho, int Wo) {
-  const long long n = p / ((long long)Ho * Wo);
-  const int rem = (int)(p - n * Ho * Wo);
-  const int ho = rem / Wo, wo = rem - (rem / Wo) * Wo;
-  const int W = 2 * Wo;
-  return (n * (2 * Ho) + 2 * ho + (q >> 1)) * (long long)W + 2 * wo + (q & 1);
+// first input row (window position 0) of pooled row p; positions 1, 2, 3 are +1, +W, +W+1.
+// 32-bit index math (the host guarantees rows * C < 2^31): 64-bit division is emulated.
+__device__ __forceinline__ uint32_t ew_pool_base(uint32_t p, uint32_t HoWo, uint32_t Wo) {
+  const uint32_t n = p / HoWo;
+  const uint32_t rem = p - n * HoWo;
+  const uint32_t ho = rem / Wo, wo = rem - ho * Wo;
+  // input row = ((n * H) + 2 ho) * W + 2 wo with H = 2 Ho, W = 2 Wo; n * H * W = 4 n HoWo
+  return 4 * n * HoWo + 4 * ho * Wo + 2 * wo;
+}
+__device__ __forceinline__ uint32_t ew_pool_off(int q, uint32_t Wo) {
+  return (q >> 1) * (2 * Wo) + (q & 1);
 }
 
 // ---- forward statistics: sum(h), sum(h^2) per channel ----
@@ -234,9 +238,9 @@ __device__ __forceinline__ void ew_sum_parts(const float* __restrict__ part, int
 
 __global__ __launch_bounds__(EW_BLOCK) void k_bn_fwd_finalize(
     const float* __restrict__ part, int nblk, int C, long long M, const float* __restrict__ gamma,
-    const float* __restrict__ beta, const float* __restrict__ cbias, float* __restrict__ rmean,
-    float* __restrict__ rvar, const long long* __restrict__ nbt, float momentum, float eps,
-    float* __restrict__ stats) {
+    const float* __restrict__ beta, const void* __restrict__ cbias, int cb_bf16,
+    float* __restrict__ rmean, float* __restrict__ rvar, const long long* __restrict__ nbt,
+    float momentum, float eps, float* __restrict__ stats) {
   const int c = blockIdx.x * EW_WAVES + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (c >= C) return;
@@ -256,10 +260,15 @@ __global__ __launch_bounds__(EW_BLOCK) void k_bn_fwd_finalize(
   stats[2 * C + c] = scale;
   stats[3 * C + c] = bb - mf * scale;
   if (rmean) {
-    // momentum < 0: cumulative moving average (nn.BatchNorm2d(momentum=None)), 1/num_batches
-    const float f = momentum >= 0.0f ? momentum : 1.0f / (float)(*nbt);
+    // momentum < 0: cumulative moving average (nn.BatchNorm2d(momentum=None)) over the batches
+    // seen including this one; num_batches_tracked itself is incremented by the apply kernel
+    const float f = momentum >= 0.0f ? momentum : 1.0f / (float)(*nbt + 1);
     const double unb = M > 1 ? var * (double)M / (double)(M - 1) : var;
-    const float bm = mf + (cbias ? cbias[c] : 0.0f);
+    float cb = 0.0f;
+    if (cbias)
+      cb = cb_bf16 ? ew_bf16f(reinterpret_cast<const uint16_t*>(cbias)[c])
+                   : reinterpret_cast<const float*>(cbias)[c];
+    const float bm = mf + cb;
     rmean[c] = (1.0f - f) * rmean[c] + f * bm;
     rvar[c] = (1.0f - f) * rvar[c] + f * (float)unb;
   }
@@ -271,18 +280,21 @@ __global__ __launch_bounds__(EW_BLOCK) void k_bn_fwd_apply(const T* __restrict__
                                                            T* __restrict__ y,
                                                            uint8_t* __restrict__ code,
                                                            const float* __restrict__ stats,
-                                                           long long rows, int C, int Ho, int Wo) {
-  __shared__ float lsc[2048], lsh[2048];
+                                                           long long rows, int C, int Ho, int Wo,
+                                                           long long* __restrict__ nbt) {
+  extern __shared__ float ew_dyn_lds[];  // 2*C floats (sized at launch: occupancy)
+  float* lsc = ew_dyn_lds;
+  float* lsh = ew_dyn_lds + C;
+  if (nbt && blockIdx.x == 0 && threadIdx.x == 0) *nbt += 1;  // after the finalize read it
   for (int c = threadIdx.x; c < C; c += EW_BLOCK) {
     lsc[c] = stats[2 * C + c];
     lsh[c] = stats[3 * C + c];
   }
   __syncthreads();
-  const int tpr = C >> 3;
-  const long long nvec = rows * tpr;
-  for (long long v = blockIdx.x * (long long)EW_BLOCK + threadIdx.x; v < nvec;
-       v += (long long)gridDim.x * EW_BLOCK) {
-    const long long row = v / tpr;
+  const uint32_t tpr = C >> 3, HoWo = (uint32_t)Ho * Wo;
+  const uint32_t nvec = (uint32_t)rows * tpr;
+  for (uint32_t v = blockIdx.x * EW_BLOCK + threadIdx.x; v < nvec; v += gridDim.x * EW_BLOCK) {
+    const uint32_t row = v / tpr;
     const int c0 = (int)(v - row * tpr) * 8;
     float sc[8], sh[8];
 #pragma unroll
@@ -292,17 +304,18 @@ __global__ __launch_bounds__(EW_BLOCK) void k_bn_fwd_apply(const T* __restrict__
     }
     if constexpr (!POOL) {
       float x[8];
-      V8<T>::ld(h + row * C + c0, x);
+      V8<T>::ld(h + (long long)row * C + c0, x);
 #pragma unroll
       for (int j = 0; j < 8; ++j) x[j] = ew_relu(x[j] * sc[j] + sh[j]);
-      V8<T>::st(y + row * C + c0, x);
+      V8<T>::st(y + (long long)row * C + c0, x);
     } else {
       float m[8];
       uint32_t k[8];
+      const uint32_t base = ew_pool_base(row, HoWo, Wo);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         float x[8];
-        V8<T>::ld(h + ew_pool_row(row, q, Ho, Wo) * C + c0, x);
+        V8<T>::ld(h + (long long)(base + ew_pool_off(q, Wo)) * C + c0, x);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float yv = V8<T>::rnd(ew_relu(x[j] * sc[j] + sh[j]));
@@ -312,11 +325,11 @@ __global__ __launch_bounds__(EW_BLOCK) void k_bn_fwd_apply(const T* __restrict__
           }
         }
       }
-      V8<T>::st(y + row * C + c0, m);
+      V8<T>::st(y + (long long)row * C + c0, m);
       uint2 w;
       w.x = k[0] | (k[1] << 8) | (k[2] << 16) | (k[3] << 24);
       w.y = k[4] | (k[5] << 8) | (k[6] << 16) | (k[7] << 24);
-      *reinterpret_cast<uint2*>(code + row * C + c0) = w;
+      *reinterpret_cast<uint2*>(code + (long long)row * C + c0) = w;
     }
   }
 }
@@ -361,10 +374,11 @@ __global__ __launch_bounds__(EW_BLOCK) void k_bn_bwd_stats(
       } else {
         uint8_t k[8];
         ew_ld_code8(code + row * C + c0, k);
+        const uint32_t base = ew_pool_base((uint32_t)row, (uint32_t)Ho * Wo, Wo);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           float x[8];
-          V8<T>::ld(h + ew_pool_row(row, q, Ho, Wo) * C + c0, x);
+          V8<T>::ld(h + (long long)(base + ew_pool_off(q, Wo)) * C + c0, x);
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             const float dz = (k[j] == q && ew_relu_pass(x[j] * sc[j] + sh[j])) ? d[j] : 0.0f;
@@ -401,7 +415,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_bn_bwd_stats(
 __global__ __launch_bounds__(EW_BLOCK) void k_bn_bwd_finalize(
     const float* __restrict__ part, int nblk, int C, long long M, const float* __restrict__ stats,
     float* __restrict__ coef, float* __restrict__ dgamma, float* __restrict__ dbeta,
-    float* __restrict__ dcbias) {
+    void* __restrict__ dcbias, int cb_bf16) {
   const int c = blockIdx.x * EW_WAVES + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (c >= C) return;
@@ -416,7 +430,11 @@ __global__ __launch_bounds__(EW_BLOCK) void k_bn_bwd_finalize(
   coef[C + c] = (float)(-scale * db / (double)M);
   if (dgamma) dgamma[c] = (float)dg;
   if (dbeta) dbeta[c] = (float)db;
-  if (dcbias) dcbias[c] = (float)(e * sums[2]);  // sum over rows of dx = e * sum(h - mean)
+  if (dcbias) {  // sum over rows of dx = e * sum(h - mean)
+    const float v = (float)(e * sums[2]);
+    if (cb_bf16) reinterpret_cast<uint16_t*>(dcbias)[c] = ew_f2bf(v);
+    else reinterpret_cast<float*>(dcbias)[c] = v;
+  }
 }
 
 template <typename T, bool POOL>
@@ -424,7 +442,12 @@ __global__ __launch_bounds__(EW_BLOCK) void k_bn_bwd_apply(
     const T* __restrict__ h, const T* __restrict__ dy, const uint8_t* __restrict__ code,
     const float* __restrict__ stats, const float* __restrict__ coef, T* __restrict__ dx,
     long long rows, int C, int Ho, int Wo) {
-  __shared__ float lm[2048], lsc[2048], lsh[2048], le[2048], lf[2048];
+  extern __shared__ float ew_dyn_lds[];  // 5*C floats
+  float* lm = ew_dyn_lds;
+  float* lsc = lm + C;
+  float* lsh = lsc + C;
+  float* le = lsh + C;
+  float* lf = le + C;
   for (int c = threadIdx.x; c < C; c += EW_BLOCK) {
     lm[c] = stats[c];
     lsc[c] = stats[2 * C + c];
@@ -433,30 +456,30 @@ __global__ __launch_bounds__(EW_BLOCK) void k_bn_bwd_apply(
     lf[c] = coef[C + c];
   }
   __syncthreads();
-  const int tpr = C >> 3;
-  const long long nvec = rows * tpr;
-  for (long long v = blockIdx.x * (long long)EW_BLOCK + threadIdx.x; v < nvec;
-       v += (long long)gridDim.x * EW_BLOCK) {
-    const long long row = v / tpr;
+  const uint32_t tpr = C >> 3, HoWo = (uint32_t)Ho * Wo;
+  const uint32_t nvec = (uint32_t)rows * tpr;
+  for (uint32_t v = blockIdx.x * EW_BLOCK + threadIdx.x; v < nvec; v += gridDim.x * EW_BLOCK) {
+    const uint32_t row = v / tpr;
     const int c0 = (int)(v - row * tpr) * 8;
     float d[8];
-    V8<T>::ld(dy + row * C + c0, d);
+    V8<T>::ld(dy + (long long)row * C + c0, d);
     if constexpr (!POOL) {
       float x[8], o[8];
-      V8<T>::ld(h + row * C + c0, x);
+      V8<T>::ld(h + (long long)row * C + c0, x);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int c = c0 + j;
         const float dz = ew_relu_pass(x[j] * lsc[c] + lsh[c]) ? d[j] : 0.0f;
         o[j] = lsc[c] * dz + le[c] * (x[j] - lm[c]) + lf[c];
       }
-      V8<T>::st(dx + row * C + c0, o);
+      V8<T>::st(dx + (long long)row * C + c0, o);
     } else {
       uint8_t k[8];
-      ew_ld_code8(code + row * C + c0, k);
+      ew_ld_code8(code + (long long)row * C + c0, k);
+      const uint32_t base = ew_pool_base(row, HoWo, Wo);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const long long ir = ew_pool_row(row, q, Ho, Wo);
+        const long long ir = base + ew_pool_off(q, Wo);
         float x[8], o[8];
         V8<T>::ld(h + ir * C + c0, x);
 #pragma unroll
@@ -478,18 +501,18 @@ __global__ __launch_bounds__(EW_BLOCK) void k_maxpool2_nhwc_fwd(const T* __restr
                                                                 uint8_t* __restrict__ code,
                                                                 long long rows, int C, int Ho,
                                                                 int Wo) {
-  const int tpr = C >> 3;
-  const long long nvec = rows * tpr;
-  for (long long v = blockIdx.x * (long long)EW_BLOCK + threadIdx.x; v < nvec;
-       v += (long long)gridDim.x * EW_BLOCK) {
-    const long long row = v / tpr;
+  const uint32_t tpr = C >> 3, HoWo = (uint32_t)Ho * Wo;
+  const uint32_t nvec = (uint32_t)rows * tpr;
+  for (uint32_t v = blockIdx.x * EW_BLOCK + threadIdx.x; v < nvec; v += gridDim.x * EW_BLOCK) {
+    const uint32_t row = v / tpr;
     const int c0 = (int)(v - row * tpr) * 8;
     float m[8];
     uint32_t k[8];
+    const uint32_t base = ew_pool_base(row, HoWo, Wo);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       float a[8];
-      V8<T>::ld(x + ew_pool_row(row, q, Ho, Wo) * C + c0, a);
+      V8<T>::ld(x + (long long)(base + ew_pool_off(q, Wo)) * C + c0, a);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         if (q == 0 || a[j] > m[j] || a[j] != a[j]) {
@@ -498,11 +521,11 @@ __global__ __launch_bounds__(EW_BLOCK) void k_maxpool2_nhwc_fwd(const T* __restr
         }
       }
     }
-    V8<T>::st(y + row * C + c0, m);
+    V8<T>::st(y + (long long)row * C + c0, m);
     uint2 w;
     w.x = k[0] | (k[1] << 8) | (k[2] << 16) | (k[3] << 24);
     w.y = k[4] | (k[5] << 8) | (k[6] << 16) | (k[7] << 24);
-    *reinterpret_cast<uint2*>(code + row * C + c0) = w;
+    *reinterpret_cast<uint2*>(code + (long long)row * C + c0) = w;
   }
 }
 
@@ -512,22 +535,22 @@ __global__ __launch_bounds__(EW_BLOCK) void k_maxpool2_nhwc_bwd(const T* __restr
                                                                 T* __restrict__ dx,
                                                                 long long rows, int C, int Ho,
                                                                 int Wo) {
-  const int tpr = C >> 3;
-  const long long nvec = rows * tpr;
-  for (long long v = blockIdx.x * (long long)EW_BLOCK + threadIdx.x; v < nvec;
-       v += (long long)gridDim.x * EW_BLOCK) {
-    const long long row = v / tpr;
+  const uint32_t tpr = C >> 3, HoWo = (uint32_t)Ho * Wo;
+  const uint32_t nvec = (uint32_t)rows * tpr;
+  for (uint32_t v = blockIdx.x * EW_BLOCK + threadIdx.x; v < nvec; v += gridDim.x * EW_BLOCK) {
+    const uint32_t row = v / tpr;
     const int c0 = (int)(v - row * tpr) * 8;
     float d[8];
     uint8_t k[8];
-    V8<T>::ld(dy + row * C + c0, d);
-    ew_ld_code8(code + row * C + c0, k);
+    V8<T>::ld(dy + (long long)row * C + c0, d);
+    ew_ld_code8(code + (long long)row * C + c0, k);
+    const uint32_t base = ew_pool_base(row, HoWo, Wo);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       float o[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = k[j] == q ? d[j] : 0.0f;
-      V8<T>::st(dx + ew_pool_row(row, q, Ho, Wo) * C + c0, o);
+      V8<T>::st(dx + (long long)(base + ew_pool_off(q, Wo)) * C + c0, o);
     }
   }
 }
@@ -619,7 +642,7 @@ void ew_bn_relu_fwd(const BnFwdArgs& a) {
     hipLaunchKernelGGL(k_bn_fwd_finalize, dim3((C + EW_WAVES - 1) / EW_WAVES), dim3(EW_BLOCK), 0,
                        s, part, nblk, C, M, reinterpret_cast<const float*>(a.gamma),
                        reinterpret_cast<const float*>(a.beta),
-                       reinterpret_cast<const float*>(a.cbias),
+                       reinterpret_cast<const void*>(a.cbias), a.cb_bf16,
                        reinterpret_cast<float*>(a.rmean), reinterpret_cast<float*>(a.rvar),
                        reinterpret_cast<const long long*>(a.nbt), a.momentum, a.eps,
                        reinterpret_cast<float*>(a.stats));
@@ -627,27 +650,29 @@ void ew_bn_relu_fwd(const BnFwdArgs& a) {
   }
   const float* st = reinterpret_cast<const float*>(a.stats);
   uint8_t* code = reinterpret_cast<uint8_t*>(a.code);
+  long long* nbt = a.training ? reinterpret_cast<long long*>(a.nbt) : nullptr;
+  const size_t lds = 2 * sizeof(float) * C;
   if (a.pool) {
     const long long rows = a.N * (long long)Ho * Wo;
     const int grid = ew_grid_vec(rows * (C / 8));
     if (a.is_bf16)
-      hipLaunchKernelGGL((k_bn_fwd_apply<uint16_t, true>), dim3(grid), dim3(EW_BLOCK), 0, s,
+      hipLaunchKernelGGL((k_bn_fwd_apply<uint16_t, true>), dim3(grid), dim3(EW_BLOCK), lds, s,
                          reinterpret_cast<const uint16_t*>(a.h), reinterpret_cast<uint16_t*>(a.y),
-                         code, st, rows, C, Ho, Wo);
+                         code, st, rows, C, Ho, Wo, nbt);
     else
-      hipLaunchKernelGGL((k_bn_fwd_apply<float, true>), dim3(grid), dim3(EW_BLOCK), 0, s,
+      hipLaunchKernelGGL((k_bn_fwd_apply<float, true>), dim3(grid), dim3(EW_BLOCK), lds, s,
                          reinterpret_cast<const float*>(a.h), reinterpret_cast<float*>(a.y), code,
-                         st, rows, C, Ho, Wo);
+                         st, rows, C, Ho, Wo, nbt);
   } else {
     const int grid = ew_grid_vec(M * (C / 8));
     if (a.is_bf16)
-      hipLaunchKernelGGL((k_bn_fwd_apply<uint16_t, false>), dim3(grid), dim3(EW_BLOCK), 0, s,
+      hipLaunchKernelGGL((k_bn_fwd_apply<uint16_t, false>), dim3(grid), dim3(EW_BLOCK), lds, s,
                          reinterpret_cast<const uint16_t*>(a.h), reinterpret_cast<uint16_t*>(a.y),
-                         code, st, M, C, 0, 0);
+                         code, st, M, C, 0, 0, nbt);
     else
-      hipLaunchKernelGGL((k_bn_fwd_apply<float, false>), dim3(grid), dim3(EW_BLOCK), 0, s,
+      hipLaunchKernelGGL((k_bn_fwd_apply<float, false>), dim3(grid), dim3(EW_BLOCK), lds, s,
                          reinterpret_cast<const float*>(a.h), reinterpret_cast<float*>(a.y), code,
-                         st, M, C, 0, 0);
+                         st, M, C, 0, 0, nbt);
   }
   EW_CHECK_LAUNCH();
 }
@@ -672,10 +697,11 @@ static void ew_bn_bwd_impl(const BnBwdArgs& a) {
   EW_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + EW_WAVES - 1) / EW_WAVES), dim3(EW_BLOCK), 0,
                      s, part, nblk, C, M, st, coef, reinterpret_cast<float*>(a.dgamma),
-                     reinterpret_cast<float*>(a.dbeta), reinterpret_cast<float*>(a.dcbias));
+                     reinterpret_cast<float*>(a.dbeta), reinterpret_cast<void*>(a.dcbias),
+                     a.cb_bf16);
   EW_CHECK_LAUNCH();
   hipLaunchKernelGGL((k_bn_bwd_apply<T, POOL>), dim3(ew_grid_vec(rows * (C / 8))),
-                     dim3(EW_BLOCK), 0, s, h, dy, code, st, coef, reinterpret_cast<T*>(a.dx), rows,
+                     dim3(EW_BLOCK), 5 * sizeof(float) * C, s, h, dy, code, st, coef, reinterpret_cast<T*>(a.dx), rows,
                      C, Ho, Wo);
   EW_CHECK_LAUNCH();
 }

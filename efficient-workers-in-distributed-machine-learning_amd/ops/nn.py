@@ -40,7 +40,7 @@ def nhwc_supported(x, pool=False):
     if not (x.is_cuda and x.dim() == 4 and x.dtype in (torch.bfloat16, torch.float32)):
         return False
     N, C, H, W = x.shape
-    if C % 8 or C > 2048 or N * H * W == 0:
+    if C % 8 or C > 2048 or N * H * W == 0 or x.numel() >= 2 ** 31:  # kernels index in 32 bit
         return False
     if not x.is_contiguous(memory_format=torch.channels_last) or x.data_ptr() % 16:
         return False
@@ -49,6 +49,15 @@ def nhwc_supported(x, pool=False):
 
 def _f32(t):
     return None if t is None else t.detach().float().contiguous()
+
+
+def _bias(t):
+    """(tensor, is_bf16): the conv bias as the kernels read it (fp32 or bf16, no cast kernel)."""
+    if t is None:
+        return None, 0
+    if t.dtype not in (torch.float32, torch.bfloat16):
+        t = t.float()
+    return t.detach().contiguous(), int(t.dtype == torch.bfloat16)
 
 
 class _BNReLU(torch.autograd.Function):
@@ -63,12 +72,14 @@ class _BNReLU(torch.autograd.Function):
         code = torch.empty((N,) + out_hw + (C,), dtype=torch.uint8, device=dev) if pool else None
         stats = torch.empty(4 * C, dtype=torch.float32, device=dev)
         g32, b32 = _f32(gamma), _f32(beta)
+        cb, cb_bf16 = _bias(cbias)
         C_.bn_relu_fwd(_ptr(h), _ptr(y), _ptr(code), _ptr(stats), _ptr(_part(dev)), _ptr(g32),
-                       _ptr(b32), _ptr(_f32(cbias)), _ptr(rmean), _ptr(rvar), _ptr(nbt), N, H, W,
+                       _ptr(b32), _ptr(cb), _ptr(rmean), _ptr(rvar), _ptr(nbt), N, H, W,
                        C, int(h.dtype == torch.bfloat16), int(pool), 1,
-                       -1.0 if momentum is None else float(momentum), float(eps), _stream())
+                       -1.0 if momentum is None else float(momentum), float(eps), cb_bf16,
+                       _stream())
         ctx.pool = pool
-        ctx.cb_dtype = None if cbias is None else cbias.dtype
+        ctx.cb_dtype = None if cb is None else cb.dtype
         ctx.save_for_backward(h, code, stats)
         return y
 
@@ -84,14 +95,13 @@ class _BNReLU(torch.autograd.Function):
         need = ctx.needs_input_grad
         dx = torch.empty_like(h, memory_format=torch.channels_last)
         coef = torch.empty(2 * C, dtype=torch.float32, device=dev)
-        dcb = torch.empty(C, dtype=torch.float32, device=dev) if need[1] else None
+        dcb = torch.empty(C, dtype=ctx.cb_dtype, device=dev) if need[1] else None
         dg = torch.empty(C, dtype=torch.float32, device=dev) if need[2] else None
         db = torch.empty(C, dtype=torch.float32, device=dev) if need[3] else None
         C_.bn_relu_bwd(_ptr(h), _ptr(dy), _ptr(code), _ptr(stats), _ptr(coef), _ptr(_part(dev)),
                        _ptr(dx), _ptr(dg), _ptr(db), _ptr(dcb), N, H, W, C,
-                       int(h.dtype == torch.bfloat16), int(ctx.pool), _stream())
-        if dcb is not None and ctx.cb_dtype != torch.float32:
-            dcb = dcb.to(ctx.cb_dtype)
+                       int(h.dtype == torch.bfloat16), int(ctx.pool),
+                       int(ctx.cb_dtype == torch.bfloat16), _stream())
         return dx, dcb, dg, db, None, None, None, None, None, None
 
 
@@ -105,7 +115,7 @@ def _apply_eval(h, stats, pool):
     y = torch.empty((N, C) + out_hw, dtype=h.dtype, device=dev, memory_format=torch.channels_last)
     code = torch.empty((N,) + out_hw + (C,), dtype=torch.uint8, device=dev) if pool else None
     C_.bn_relu_fwd(_ptr(h), _ptr(y), _ptr(code), _ptr(stats), 0, 0, 0, 0, 0, 0, 0, N, H, W, C,
-                   int(h.dtype == torch.bfloat16), int(pool), 0, 0.0, 0.0, _stream())
+                   int(h.dtype == torch.bfloat16), int(pool), 0, 0.0, 0.0, 0, _stream())
     return y
 
 
@@ -127,11 +137,8 @@ def bn_relu(h, cbias, bn, pool=False):
     batch_stats = bn.training or bn.running_mean is None
     if batch_stats:
         momentum = bn.momentum
-        nbt = None
-        if bn.training and bn.track_running_stats:
-            bn.num_batches_tracked.add_(1)
-            if momentum is None:
-                nbt = bn.num_batches_tracked
+        # num_batches_tracked is incremented by the apply kernel (no separate add kernel)
+        nbt = bn.num_batches_tracked if bn.training and bn.track_running_stats else None
         track = bn.training and bn.running_mean is not None
         return _BNReLU.apply(h, cbias, bn.weight, bn.bias,
                              bn.running_mean if track else None,
@@ -197,7 +204,7 @@ def maxpool2x2(x):
 
     ok = (x.is_cuda and x.dim() == 4 and x.dtype in (torch.bfloat16, torch.float32)
           and x.shape[2] % 2 == 0 and x.shape[3] % 2 == 0 and x.numel() > 0
-          and x.data_ptr() % 16 == 0)
+          and x.data_ptr() % 16 == 0 and x.numel() < 2 ** 31)
     if ok:
         if x.is_contiguous():
             ok = True

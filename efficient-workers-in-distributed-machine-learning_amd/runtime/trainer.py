@@ -93,7 +93,10 @@ class Trainer:
                                        world=n_workers, shuffle=True,
                                        augment=cfg.augment and info["shape"][0] == 3,
                                        seed=cfg.seed, device=self.device,
-                                       channels_last=self.channels_last)
+                                       channels_last=self.channels_last,
+                                       fused=self.cuda and cfg.fused_data == "on",
+                                       out_dtype=torch.bfloat16 if (self.cuda and cfg.amp == "bf16")
+                                       else torch.float32)
         tx, ty, _ = load_dataset(cfg.dataset, cfg.data_dir, train=False,
                                  synthetic_size=(cfg.synthetic_size // 5) if cfg.synthetic_size else 0,
                                  seed=cfg.seed, device=self.device)
@@ -144,6 +147,7 @@ class Trainer:
         if self.graph_mode != "off" and not isinstance(self.exchange, GradientExchange):
             raise ValueError("--hip-graph needs the all-to-all topology without local SGD")
         self._graphs = None
+        self._in_graph_batch = False
         # Graph mode: warmup, capture and replay all run on ONE dedicated stream, so MIOpen /
         # hipBLASLt create their per-stream handles and workspaces during the eager warmup and not
         # inside the capture (lazy per-stream init inside a capture crashes capture_end).
@@ -226,10 +230,19 @@ class Trainer:
             self.exchange.finish()
             self.step += 1
             return None, None
-        if x is None:
-            x, y = self.loader.next()
         self.model.train()
-        if self.graph_mode != "off" and self.step >= self.cfg.graph_warmup:
+        graphed = self.graph_mode != "off" and self.step >= self.cfg.graph_warmup
+        if x is None and graphed and self.loader.fused:
+            # the batch kernel is part of the graph: only the host-side epoch bookkeeping here
+            if self._graphs is not None and not self._in_graph_batch:
+                self._graphs = None  # captured around an explicit batch: re-capture
+            self.loader.begin_step()
+            if self._graphs is None and not self._try_capture(None, None):
+                return self._train_step()  # capture failed on some rank: all run eager
+            return self._graph_step(None, None)
+        if x is None:
+            x, y = self.loader.next(static=True)
+        if graphed:
             if self._graphs is None and not self._try_capture(x, y):
                 return self._train_step(x, y)  # capture failed on some rank: all run eager
             return self._graph_step(x, y)
@@ -268,8 +281,10 @@ class Trainer:
         collectives, fused decode+SGD.  ``split``: graph A (through encode) -> eager RCCL calls ->
         graph B (decode+SGD), for process groups whose collectives cannot be captured."""
         ex = self.exchange
-        self._gx = x.clone()
-        self._gy = y.clone()
+        self._in_graph_batch = x is None  # fused loader: the batch kernel is captured too
+        if x is not None:
+            self._gx = x.clone()
+            self._gy = y.clone()
         ex.use_dev_key = True
         saved = (ex.step_idx, self.opt.steps)
         mode = os.environ.get("EWDML_GRAPH_CAPTURE_MODE", "global")
@@ -277,6 +292,8 @@ class Trainer:
         if self.graph_mode == "full":
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, stream=self.gstream, capture_error_mode=mode):
+                if self._in_graph_batch:
+                    self._gx, self._gy = self.loader.emit()
                 loss, out = self.forward_backward(self._gx, self._gy)
                 ex.finish()
             self._graphs = (g,)
@@ -284,6 +301,8 @@ class Trainer:
             ex.defer_comm = True
             ga = torch.cuda.CUDAGraph()
             with torch.cuda.graph(ga, stream=self.gstream, capture_error_mode=mode):
+                if self._in_graph_batch:
+                    self._gx, self._gy = self.loader.emit()
                 loss, out = self.forward_backward(self._gx, self._gy)
                 ex.launch_pending()
                 ex.join_side()
@@ -299,7 +318,12 @@ class Trainer:
 
     def _graph_step(self, x, y):
         ex = self.exchange
-        if x is not self._gx:
+        if self._in_graph_batch:
+            if x is not None:  # an explicit batch after an in-graph-batch capture: re-capture
+                self._graphs = None
+                return self._train_step(x, y)
+            self.loader.advance()
+        elif x is not self._gx:
             self._gx.copy_(x)
             self._gy.copy_(y)
         ex.set_device_key()
@@ -394,7 +418,7 @@ class Trainer:
             self.exchange.step_idx = self.step
         if self.loader is not None:
             self.loader.set_epoch(self.epoch)
-            self.loader._pos = self.step % len(self.loader)
+            self.loader.seek(self.step % len(self.loader))
         self.log.info(f"resumed from {path} at step {self.step}")
 
     # --------------------------------------------------------------------------------------------

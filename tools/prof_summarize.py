@@ -79,6 +79,15 @@ def summarize(rows, frac=0.5, gap_ns=150_000_000, steps=None):
     for n, (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:60]:
         ps = f" {t / 1e3 / steps:>9.2f}" if steps else ""
         out.append(f"{c:>7} {t / 1e6:>10.3f} {t / c / 1e3:>9.2f}{ps}  {n}")
+    if steps:  # the last step's kernels in launch order: duration and idle gap before each
+        per_step = len(win) // steps
+        last = win[-per_step:]
+        out.append("")
+        out.append(f"last step, {per_step} kernels in order:  gap_us  dur_us  kernel")
+        prev_end = last[0][0]
+        for s, e, n in last:
+            out.append(f"{max(0, s - prev_end) / 1e3:>8.2f} {(e - s) / 1e3:>7.2f}  {short(n)[:90]}")
+            prev_end = max(prev_end, e)
     return "\n".join(out) + "\n"
 
 
