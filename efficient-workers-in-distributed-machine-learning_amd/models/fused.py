@@ -24,6 +24,11 @@ def enabled() -> bool:
     return _ENABLED
 
 
+def active(x) -> bool:
+    """Run the fused kernels for this activation (device tensor, fused path enabled)."""
+    return _ENABLED and x.is_cuda
+
+
 def is_pool2(m) -> bool:
     def two(v):
         return v == 2 or v == (2, 2)

@@ -10,9 +10,24 @@ Fixed reference defects:
     inputs but no longer crashes on other resolutions;
   * ``stem="imagenet"`` gives the standard 7x7/2 conv + 3x3/2 max-pool stem used for the
     224x224 ResNet-50 config (BASELINE.json config #5).
+
+On the GPU (``models.fused`` enabled) every BN runs through the fused NHWC kernels
+(``ewdml.ops.nn.bn_act``): conv-BN-ReLU, shortcut conv-BN, and the block output
+``relu(bn3(conv3) + shortcut)`` as one BN+add+ReLU kernel set; same modules and state_dict.
 """
 import torch.nn as nn
 import torch.nn.functional as F
+
+from . import fused
+
+
+def _shortcut(sc, x):
+    """Identity or projection (1x1 conv + BN, through the fused BN kernel)."""
+    if len(sc) == 0:
+        return x
+    from ..ops.nn import bn_act
+
+    return bn_act(sc[0](x), sc[1], "none")
 
 
 class BasicBlock(nn.Module):
@@ -32,6 +47,11 @@ class BasicBlock(nn.Module):
             )
 
     def forward(self, x):
+        if fused.active(x):
+            from ..ops.nn import bn_act
+
+            out = bn_act(self.conv1(x), self.bn1, "relu")
+            return bn_act(self.conv2(out), self.bn2, "add_relu", res=_shortcut(self.shortcut, x))
         out = F.relu(self.bn1(self.conv1(x)))
         out = self.bn2(self.conv2(out))
         return F.relu(out + self.shortcut(x))
@@ -56,6 +76,12 @@ class Bottleneck(nn.Module):
             )
 
     def forward(self, x):
+        if fused.active(x):
+            from ..ops.nn import bn_act
+
+            out = bn_act(self.conv1(x), self.bn1, "relu")
+            out = bn_act(self.conv2(out), self.bn2, "relu")
+            return bn_act(self.conv3(out), self.bn3, "add_relu", res=_shortcut(self.shortcut, x))
         out = F.relu(self.bn1(self.conv1(x)))
         out = F.relu(self.bn2(self.conv2(out)))
         out = self.bn3(self.conv3(out))
@@ -88,7 +114,12 @@ class ResNet(nn.Module):
         return nn.Sequential(*layers)
 
     def forward(self, x):
-        out = F.relu(self.bn1(self.conv1(x)))
+        if fused.active(x):
+            from ..ops.nn import bn_act
+
+            out = bn_act(self.conv1(x), self.bn1, "relu")
+        else:
+            out = F.relu(self.bn1(self.conv1(x)))
         if self.stem == "imagenet":
             out = F.max_pool2d(out, 3, 2, 1)
         out = self.layer4(self.layer3(self.layer2(self.layer1(out))))

@@ -213,28 +213,29 @@ PYBIND11_MODULE(_C, m) {
 
   m.def("bn_part_floats", &ew_bn_part_floats);
   m.def("bn_relu_fwd",
-        [](uintptr_t h, uintptr_t y, uintptr_t code, uintptr_t stats, uintptr_t part,
-           uintptr_t gamma, uintptr_t beta, uintptr_t cbias, uintptr_t rmean, uintptr_t rvar,
-           uintptr_t nbt, long long N, int H, int W, int C, int is_bf16, int pool, int training,
-           float momentum, float eps, int cb_bf16, uintptr_t stream) {
+        [](uintptr_t h, uintptr_t res, uintptr_t y, uintptr_t code, uintptr_t stats,
+           uintptr_t part, uintptr_t gamma, uintptr_t beta, uintptr_t cbias, uintptr_t rmean,
+           uintptr_t rvar, uintptr_t nbt, long long N, int H, int W, int C, int is_bf16,
+           int pool, int mode, int training, float momentum, float eps, int cb_bf16,
+           uintptr_t stream) {
           BnFwdArgs a{};
-          a.h = h; a.y = y; a.code = code; a.stats = stats; a.part = part;
+          a.h = h; a.res = res; a.y = y; a.code = code; a.stats = stats; a.part = part;
           a.gamma = gamma; a.beta = beta; a.cbias = cbias; a.rmean = rmean; a.rvar = rvar;
           a.nbt = nbt; a.N = N; a.H = H; a.W = W; a.C = C;
-          a.is_bf16 = is_bf16; a.pool = pool; a.training = training;
+          a.is_bf16 = is_bf16; a.pool = pool; a.mode = mode; a.training = training;
           a.momentum = momentum; a.eps = eps; a.cb_bf16 = cb_bf16; a.stream = stream;
           ew_bn_relu_fwd(a);
         });
   m.def("bn_relu_bwd",
-        [](uintptr_t h, uintptr_t dy, uintptr_t code, uintptr_t stats, uintptr_t coef,
-           uintptr_t part, uintptr_t dx, uintptr_t dgamma, uintptr_t dbeta, uintptr_t dcbias,
-           long long N, int H, int W, int C, int is_bf16, int pool, int cb_bf16,
-           uintptr_t stream) {
+        [](uintptr_t h, uintptr_t res, uintptr_t dy, uintptr_t code, uintptr_t stats,
+           uintptr_t coef, uintptr_t part, uintptr_t dx, uintptr_t dres, uintptr_t dgamma,
+           uintptr_t dbeta, uintptr_t dcbias, long long N, int H, int W, int C, int is_bf16,
+           int pool, int mode, int cb_bf16, uintptr_t stream) {
           BnBwdArgs a{};
-          a.h = h; a.dy = dy; a.code = code; a.stats = stats; a.coef = coef; a.part = part;
-          a.dx = dx; a.dgamma = dgamma; a.dbeta = dbeta; a.dcbias = dcbias;
-          a.N = N; a.H = H; a.W = W; a.C = C; a.is_bf16 = is_bf16; a.pool = pool;
-          a.cb_bf16 = cb_bf16; a.stream = stream;
+          a.h = h; a.res = res; a.dy = dy; a.code = code; a.stats = stats; a.coef = coef;
+          a.part = part; a.dx = dx; a.dres = dres; a.dgamma = dgamma; a.dbeta = dbeta;
+          a.dcbias = dcbias; a.N = N; a.H = H; a.W = W; a.C = C; a.is_bf16 = is_bf16;
+          a.pool = pool; a.mode = mode; a.cb_bf16 = cb_bf16; a.stream = stream;
           ew_bn_relu_bwd(a);
         });
   m.def("maxpool2_nhwc", &ew_maxpool2_nhwc);

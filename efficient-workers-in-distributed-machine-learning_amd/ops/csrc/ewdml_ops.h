@@ -90,22 +90,23 @@ void ew_cast_scale(uintptr_t src, uintptr_t dst, long long n, float scale, int t
 
 // ---- model-side kernels (nn.hip) ----
 // NHWC BatchNorm + ReLU [+ 2x2 max pool]; h/y/dy/dx bf16 or fp32 ([N,H,W,C] memory), C % 8 == 0
+// mode: 0 relu, 2 identity, 3 relu(bn + res) (pool = 1 forces relu + 2x2 pool)
 struct BnFwdArgs {
-  uintptr_t h, y, code, stats, part;        // stats fp32 [4][C]; part: ew_bn_part_floats() floats
+  uintptr_t h, res, y, code, stats, part;        // stats fp32 [4][C]; part: ew_bn_part_floats() floats
   uintptr_t gamma, beta, cbias, rmean, rvar, nbt;  // fp32 [C] (nullable; cbias fp32 or bf16),
   //                                                  nbt int64 (nullable): incremented once
   long long N;
   int H, W, C;
-  int is_bf16, pool, training, cb_bf16;
+  int is_bf16, pool, training, cb_bf16, mode;
   float momentum, eps;  // momentum < 0: cumulative average over *nbt batches
   uintptr_t stream;
 };
 struct BnBwdArgs {
-  uintptr_t h, dy, code, stats, coef, part, dx;  // coef fp32 [2][C]
+  uintptr_t h, res, dy, code, stats, coef, part, dx, dres;  // coef fp32 [2][C]
   uintptr_t dgamma, dbeta, dcbias;               // [C] outputs (nullable), dcbias bf16 if cb_bf16
   long long N;
   int H, W, C;  // of h (pre-pool)
-  int is_bf16, pool, cb_bf16;
+  int is_bf16, pool, cb_bf16, mode;
   uintptr_t stream;
 };
 int ew_bn_part_floats();

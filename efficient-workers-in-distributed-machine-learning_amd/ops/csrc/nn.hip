@@ -274,9 +274,23 @@ __global__ __launch_bounds__(EW_BLOCK) void k_bn_fwd_finalize(
   }
 }
 
-// ---- forward apply: y = relu(h*scale + shift) [-> 2x2 max pool + code] ----
-template <typename T, bool POOL>
+// ---- forward apply: y = act(h*scale + shift [+ res]) [-> 2x2 max pool + code] ----
+enum { EW_BN_RELU = 0, EW_BN_RELU_POOL = 1, EW_BN_NONE = 2, EW_BN_ADD_RELU = 3 };
+
+template <int MODE>
+__device__ __forceinline__ float ew_act(float v) {
+  if constexpr (MODE == EW_BN_NONE) return v;
+  else return ew_relu(v);
+}
+template <int MODE>
+__device__ __forceinline__ bool ew_act_pass(float v) {
+  if constexpr (MODE == EW_BN_NONE) return true;
+  else return ew_relu_pass(v);
+}
+
+template <typename T, int MODE>
 __global__ __launch_bounds__(EW_BLOCK) void k_bn_fwd_apply(const T* __restrict__ h,
+                                                           const T* __restrict__ res,
                                                            T* __restrict__ y,
                                                            uint8_t* __restrict__ code,
                                                            const float* __restrict__ stats,
@@ -302,11 +316,18 @@ __global__ __launch_bounds__(EW_BLOCK) void k_bn_fwd_apply(const T* __restrict__
       sc[j] = lsc[c0 + j];
       sh[j] = lsh[c0 + j];
     }
-    if constexpr (!POOL) {
+    if constexpr (MODE != EW_BN_RELU_POOL) {
       float x[8];
       V8<T>::ld(h + (long long)row * C + c0, x);
+      if constexpr (MODE == EW_BN_ADD_RELU) {
+        float r[8];
+        V8<T>::ld(res + (long long)row * C + c0, r);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) x[j] = ew_relu(x[j] * sc[j] + sh[j]);
+        for (int j = 0; j < 8; ++j) x[j] = ew_relu(x[j] * sc[j] + sh[j] + r[j]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[j] = ew_act<MODE>(x[j] * sc[j] + sh[j]);
+      }
       V8<T>::st(y + (long long)row * C + c0, x);
     } else {
       float m[8];
@@ -334,10 +355,11 @@ __global__ __launch_bounds__(EW_BLOCK) void k_bn_fwd_apply(const T* __restrict__
   }
 }
 
-// ---- backward statistics: sum(dz), sum(dz*(h-mean)), sum(h-mean), dz = relu'(v) * dy ----
-template <typename T, bool POOL>
+// ---- backward statistics: sum(dz), sum(dz*(h-mean)), sum(h-mean), dz = act'(v) * dy ----
+template <typename T, int MODE>
 __global__ __launch_bounds__(EW_BLOCK) void k_bn_bwd_stats(
-    const T* __restrict__ h, const T* __restrict__ dy, const uint8_t* __restrict__ code,
+    const T* __restrict__ h, const T* __restrict__ res, const T* __restrict__ dy,
+    const uint8_t* __restrict__ code,
     const float* __restrict__ stats, long long rows, int C, int Ho, int Wo, int rows_per_blk,
     float* __restrict__ part) {
   __shared__ float l1[2048], l2[2048], l3[2048];
@@ -360,12 +382,15 @@ __global__ __launch_bounds__(EW_BLOCK) void k_bn_bwd_stats(
     for (long long row = row0 + r; row < row1; row += rpi) {
       float d[8];
       V8<T>::ld(dy + row * C + c0, d);
-      if constexpr (!POOL) {
-        float x[8];
+      if constexpr (MODE != EW_BN_RELU_POOL) {
+        float x[8], rr[8];
         V8<T>::ld(h + row * C + c0, x);
+        if constexpr (MODE == EW_BN_ADD_RELU) V8<T>::ld(res + row * C + c0, rr);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float dz = ew_relu_pass(x[j] * sc[j] + sh[j]) ? d[j] : 0.0f;
+          float v = x[j] * sc[j] + sh[j];
+          if constexpr (MODE == EW_BN_ADD_RELU) v = v + rr[j];
+          const float dz = ew_act_pass<MODE>(v) ? d[j] : 0.0f;
           const float xc = x[j] - mean[j];
           s1[j] += dz;
           s2[j] += dz * xc;
@@ -437,11 +462,12 @@ __global__ __launch_bounds__(EW_BLOCK) void k_bn_bwd_finalize(
   }
 }
 
-template <typename T, bool POOL>
+template <typename T, int MODE>
 __global__ __launch_bounds__(EW_BLOCK) void k_bn_bwd_apply(
-    const T* __restrict__ h, const T* __restrict__ dy, const uint8_t* __restrict__ code,
-    const float* __restrict__ stats, const float* __restrict__ coef, T* __restrict__ dx,
-    long long rows, int C, int Ho, int Wo) {
+    const T* __restrict__ h, const T* __restrict__ res, const T* __restrict__ dy,
+    const uint8_t* __restrict__ code, const float* __restrict__ stats,
+    const float* __restrict__ coef, T* __restrict__ dx, T* __restrict__ dres, long long rows,
+    int C, int Ho, int Wo) {
   extern __shared__ float ew_dyn_lds[];  // 5*C floats
   float* lm = ew_dyn_lds;
   float* lsc = lm + C;
@@ -463,16 +489,21 @@ __global__ __launch_bounds__(EW_BLOCK) void k_bn_bwd_apply(
     const int c0 = (int)(v - row * tpr) * 8;
     float d[8];
     V8<T>::ld(dy + (long long)row * C + c0, d);
-    if constexpr (!POOL) {
-      float x[8], o[8];
+    if constexpr (MODE != EW_BN_RELU_POOL) {
+      float x[8], o[8], rr[8], dzs[8];
       V8<T>::ld(h + (long long)row * C + c0, x);
+      if constexpr (MODE == EW_BN_ADD_RELU) V8<T>::ld(res + (long long)row * C + c0, rr);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int c = c0 + j;
-        const float dz = ew_relu_pass(x[j] * lsc[c] + lsh[c]) ? d[j] : 0.0f;
+        float vv = x[j] * lsc[c] + lsh[c];
+        if constexpr (MODE == EW_BN_ADD_RELU) vv = vv + rr[j];
+        const float dz = ew_act_pass<MODE>(vv) ? d[j] : 0.0f;
+        dzs[j] = dz;
         o[j] = lsc[c] * dz + le[c] * (x[j] - lm[c]) + lf[c];
       }
       V8<T>::st(dx + (long long)row * C + c0, o);
+      if constexpr (MODE == EW_BN_ADD_RELU) V8<T>::st(dres + (long long)row * C + c0, dzs);
     } else {
       uint8_t k[8];
       ew_ld_code8(code + (long long)row * C + c0, k);
@@ -652,33 +683,33 @@ void ew_bn_relu_fwd(const BnFwdArgs& a) {
   uint8_t* code = reinterpret_cast<uint8_t*>(a.code);
   long long* nbt = a.training ? reinterpret_cast<long long*>(a.nbt) : nullptr;
   const size_t lds = 2 * sizeof(float) * C;
-  if (a.pool) {
-    const long long rows = a.N * (long long)Ho * Wo;
-    const int grid = ew_grid_vec(rows * (C / 8));
-    if (a.is_bf16)
-      hipLaunchKernelGGL((k_bn_fwd_apply<uint16_t, true>), dim3(grid), dim3(EW_BLOCK), lds, s,
-                         reinterpret_cast<const uint16_t*>(a.h), reinterpret_cast<uint16_t*>(a.y),
-                         code, st, rows, C, Ho, Wo, nbt);
-    else
-      hipLaunchKernelGGL((k_bn_fwd_apply<float, true>), dim3(grid), dim3(EW_BLOCK), lds, s,
-                         reinterpret_cast<const float*>(a.h), reinterpret_cast<float*>(a.y), code,
-                         st, rows, C, Ho, Wo, nbt);
-  } else {
-    const int grid = ew_grid_vec(M * (C / 8));
-    if (a.is_bf16)
-      hipLaunchKernelGGL((k_bn_fwd_apply<uint16_t, false>), dim3(grid), dim3(EW_BLOCK), lds, s,
-                         reinterpret_cast<const uint16_t*>(a.h), reinterpret_cast<uint16_t*>(a.y),
-                         code, st, M, C, 0, 0, nbt);
-    else
-      hipLaunchKernelGGL((k_bn_fwd_apply<float, false>), dim3(grid), dim3(EW_BLOCK), lds, s,
-                         reinterpret_cast<const float*>(a.h), reinterpret_cast<float*>(a.y), code,
-                         st, M, C, 0, 0, nbt);
+  const int mode = a.pool ? EW_BN_RELU_POOL : a.mode;
+  const long long rows = a.pool ? a.N * (long long)Ho * Wo : M;
+  const int grid = ew_grid_vec(rows * (C / 8));
+#define EW_FA(T, MODE)                                                                          \
+  hipLaunchKernelGGL((k_bn_fwd_apply<T, MODE>), dim3(grid), dim3(EW_BLOCK), lds, s,             \
+                     reinterpret_cast<const T*>(a.h), reinterpret_cast<const T*>(a.res),         \
+                     reinterpret_cast<T*>(a.y), code, st, rows, C, Ho, Wo, nbt)
+#define EW_FA_MODES(T)                                                                          \
+  switch (mode) {                                                                               \
+    case EW_BN_RELU: EW_FA(T, EW_BN_RELU); break;                                               \
+    case EW_BN_RELU_POOL: EW_FA(T, EW_BN_RELU_POOL); break;                                     \
+    case EW_BN_NONE: EW_FA(T, EW_BN_NONE); break;                                               \
+    default: EW_FA(T, EW_BN_ADD_RELU); break;                                                   \
   }
+  if (a.is_bf16) {
+    EW_FA_MODES(uint16_t)
+  } else {
+    EW_FA_MODES(float)
+  }
+#undef EW_FA_MODES
+#undef EW_FA
   EW_CHECK_LAUNCH();
 }
 
-template <typename T, bool POOL>
+template <typename T, int MODE>
 static void ew_bn_bwd_impl(const BnBwdArgs& a) {
+  constexpr bool POOL = MODE == EW_BN_RELU_POOL;
   hipStream_t s = (hipStream_t)a.stream;
   const long long M = a.N * (long long)a.H * a.W;
   const int Ho = a.H / 2, Wo = a.W / 2;
@@ -688,32 +719,38 @@ static void ew_bn_bwd_impl(const BnBwdArgs& a) {
   ew_bn_grid(rows, C, &nblk, &rpb);
   float* part = reinterpret_cast<float*>(a.part);
   const T* h = reinterpret_cast<const T*>(a.h);
+  const T* res = reinterpret_cast<const T*>(a.res);
   const T* dy = reinterpret_cast<const T*>(a.dy);
   const uint8_t* code = reinterpret_cast<const uint8_t*>(a.code);
   const float* st = reinterpret_cast<const float*>(a.stats);
   float* coef = reinterpret_cast<float*>(a.coef);
-  hipLaunchKernelGGL((k_bn_bwd_stats<T, POOL>), dim3(nblk), dim3(EW_BLOCK), 0, s, h, dy, code,
-                     st, rows, C, Ho, Wo, rpb, part);
+  hipLaunchKernelGGL((k_bn_bwd_stats<T, MODE>), dim3(nblk), dim3(EW_BLOCK), 0, s, h, res, dy,
+                     code, st, rows, C, Ho, Wo, rpb, part);
   EW_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + EW_WAVES - 1) / EW_WAVES), dim3(EW_BLOCK), 0,
                      s, part, nblk, C, M, st, coef, reinterpret_cast<float*>(a.dgamma),
                      reinterpret_cast<float*>(a.dbeta), reinterpret_cast<void*>(a.dcbias),
                      a.cb_bf16);
   EW_CHECK_LAUNCH();
-  hipLaunchKernelGGL((k_bn_bwd_apply<T, POOL>), dim3(ew_grid_vec(rows * (C / 8))),
-                     dim3(EW_BLOCK), 5 * sizeof(float) * C, s, h, dy, code, st, coef, reinterpret_cast<T*>(a.dx), rows,
-                     C, Ho, Wo);
+  hipLaunchKernelGGL((k_bn_bwd_apply<T, MODE>), dim3(ew_grid_vec(rows * (C / 8))),
+                     dim3(EW_BLOCK), 5 * sizeof(float) * C, s, h, res, dy, code, st, coef,
+                     reinterpret_cast<T*>(a.dx), reinterpret_cast<T*>(a.dres), rows, C, Ho, Wo);
   EW_CHECK_LAUNCH();
 }
 
-void ew_bn_relu_bwd(const BnBwdArgs& a) {
-  if (a.is_bf16) {
-    if (a.pool) ew_bn_bwd_impl<uint16_t, true>(a);
-    else ew_bn_bwd_impl<uint16_t, false>(a);
-  } else {
-    if (a.pool) ew_bn_bwd_impl<float, true>(a);
-    else ew_bn_bwd_impl<float, false>(a);
+template <typename T>
+static void ew_bn_bwd_modes(const BnBwdArgs& a) {
+  switch (a.pool ? (int)EW_BN_RELU_POOL : a.mode) {
+    case EW_BN_RELU: ew_bn_bwd_impl<T, EW_BN_RELU>(a); break;
+    case EW_BN_RELU_POOL: ew_bn_bwd_impl<T, EW_BN_RELU_POOL>(a); break;
+    case EW_BN_NONE: ew_bn_bwd_impl<T, EW_BN_NONE>(a); break;
+    default: ew_bn_bwd_impl<T, EW_BN_ADD_RELU>(a); break;
   }
+}
+
+void ew_bn_relu_bwd(const BnBwdArgs& a) {
+  if (a.is_bf16) ew_bn_bwd_modes<uint16_t>(a);
+  else ew_bn_bwd_modes<float>(a);
 }
 
 void ew_maxpool2_nhwc(uintptr_t x, uintptr_t y, uintptr_t code, long long N, int H, int W, int C,

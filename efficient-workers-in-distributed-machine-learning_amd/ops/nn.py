@@ -60,9 +60,12 @@ def _bias(t):
     return t.detach().contiguous(), int(t.dtype == torch.bfloat16)
 
 
-class _BNReLU(torch.autograd.Function):
+_MODES = {"relu": 0, "none": 2, "add_relu": 3}
+
+
+class _BNAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, h, cbias, gamma, beta, rmean, rvar, nbt, momentum, eps, pool):
+    def forward(ctx, h, res, cbias, gamma, beta, rmean, rvar, nbt, momentum, eps, pool, mode):
         C_ = require()
         N, C, H, W = h.shape
         dev = h.device
@@ -73,20 +76,20 @@ class _BNReLU(torch.autograd.Function):
         stats = torch.empty(4 * C, dtype=torch.float32, device=dev)
         g32, b32 = _f32(gamma), _f32(beta)
         cb, cb_bf16 = _bias(cbias)
-        C_.bn_relu_fwd(_ptr(h), _ptr(y), _ptr(code), _ptr(stats), _ptr(_part(dev)), _ptr(g32),
-                       _ptr(b32), _ptr(cb), _ptr(rmean), _ptr(rvar), _ptr(nbt), N, H, W,
-                       C, int(h.dtype == torch.bfloat16), int(pool), 1,
+        C_.bn_relu_fwd(_ptr(h), _ptr(res), _ptr(y), _ptr(code), _ptr(stats), _ptr(_part(dev)),
+                       _ptr(g32), _ptr(b32), _ptr(cb), _ptr(rmean), _ptr(rvar), _ptr(nbt), N, H,
+                       W, C, int(h.dtype == torch.bfloat16), int(pool), _MODES[mode], 1,
                        -1.0 if momentum is None else float(momentum), float(eps), cb_bf16,
                        _stream())
-        ctx.pool = pool
+        ctx.pool, ctx.mode = pool, mode
         ctx.cb_dtype = None if cb is None else cb.dtype
-        ctx.save_for_backward(h, code, stats)
+        ctx.save_for_backward(h, res, code, stats)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         C_ = require()
-        h, code, stats = ctx.saved_tensors
+        h, res, code, stats = ctx.saved_tensors
         N, C, H, W = h.shape
         dev = h.device
         dy = dy.contiguous(memory_format=torch.channels_last)
@@ -94,18 +97,20 @@ class _BNReLU(torch.autograd.Function):
             dy = dy.to(h.dtype)
         need = ctx.needs_input_grad
         dx = torch.empty_like(h, memory_format=torch.channels_last)
+        dres = torch.empty_like(h, memory_format=torch.channels_last) \
+            if ctx.mode == "add_relu" else None
         coef = torch.empty(2 * C, dtype=torch.float32, device=dev)
-        dcb = torch.empty(C, dtype=ctx.cb_dtype, device=dev) if need[1] else None
-        dg = torch.empty(C, dtype=torch.float32, device=dev) if need[2] else None
-        db = torch.empty(C, dtype=torch.float32, device=dev) if need[3] else None
-        C_.bn_relu_bwd(_ptr(h), _ptr(dy), _ptr(code), _ptr(stats), _ptr(coef), _ptr(_part(dev)),
-                       _ptr(dx), _ptr(dg), _ptr(db), _ptr(dcb), N, H, W, C,
-                       int(h.dtype == torch.bfloat16), int(ctx.pool),
-                       int(ctx.cb_dtype == torch.bfloat16), _stream())
-        return dx, dcb, dg, db, None, None, None, None, None, None
+        dcb = torch.empty(C, dtype=ctx.cb_dtype, device=dev) if need[2] else None
+        dg = torch.empty(C, dtype=torch.float32, device=dev) if need[3] else None
+        db = torch.empty(C, dtype=torch.float32, device=dev) if need[4] else None
+        C_.bn_relu_bwd(_ptr(h), _ptr(res), _ptr(dy), _ptr(code), _ptr(stats), _ptr(coef),
+                       _ptr(_part(dev)), _ptr(dx), _ptr(dres), _ptr(dg), _ptr(db), _ptr(dcb), N,
+                       H, W, C, int(h.dtype == torch.bfloat16), int(ctx.pool),
+                       _MODES[ctx.mode], int(ctx.cb_dtype == torch.bfloat16), _stream())
+        return dx, dres, dcb, dg, db, None, None, None, None, None, None, None
 
 
-def _apply_eval(h, stats, pool):
+def _apply_eval(h, stats, pool, mode="relu", res=None):
     """Eval-mode (running statistics) forward, no autograd (callers use the torch composition
     when a gradient is needed in eval mode)."""
     C_ = require()
@@ -114,38 +119,55 @@ def _apply_eval(h, stats, pool):
     out_hw = (H // 2, W // 2) if pool else (H, W)
     y = torch.empty((N, C) + out_hw, dtype=h.dtype, device=dev, memory_format=torch.channels_last)
     code = torch.empty((N,) + out_hw + (C,), dtype=torch.uint8, device=dev) if pool else None
-    C_.bn_relu_fwd(_ptr(h), _ptr(y), _ptr(code), _ptr(stats), 0, 0, 0, 0, 0, 0, 0, N, H, W, C,
-                   int(h.dtype == torch.bfloat16), int(pool), 0, 0.0, 0.0, 0, _stream())
+    C_.bn_relu_fwd(_ptr(h), _ptr(res), _ptr(y), _ptr(code), _ptr(stats), 0, 0, 0, 0, 0, 0, 0, N,
+                   H, W, C, int(h.dtype == torch.bfloat16), int(pool), _MODES[mode], 0, 0.0, 0.0,
+                   0, _stream())
     return y
 
 
-def bn_relu_reference(h, cbias, bn, pool=False):
+def bn_act_reference(h, cbias, bn, pool=False, mode="relu", res=None):
     """The unfused torch composition (CPU path and numerics oracle)."""
     import torch.nn.functional as F
 
     if cbias is not None:
         h = h + cbias.to(h.dtype).view(1, -1, 1, 1)
-    y = F.relu(bn(h))
+    y = bn(h)
+    if mode == "add_relu":
+        y = F.relu(y + res)
+    elif mode == "relu":
+        y = F.relu(y)
     return F.max_pool2d(y, 2, 2) if pool else y
 
 
-def bn_relu(h, cbias, bn, pool=False):
-    """``maxpool?(relu(bn(h + cbias)))`` for a ``nn.BatchNorm2d`` module ``bn`` (its running
-    statistics and ``num_batches_tracked`` are updated like its own forward would)."""
-    if not nhwc_supported(h, pool):
-        return bn_relu_reference(h, cbias, bn, pool)
+def bn_relu_reference(h, cbias, bn, pool=False):
+    return bn_act_reference(h, cbias, bn, pool, "relu")
+
+
+def bn_act(h, bn, mode="relu", res=None, cbias=None, pool=False):
+    """``maxpool?(act(bn(h + cbias) [+ res]))`` for a ``nn.BatchNorm2d`` ``bn``; ``mode`` is
+    ``relu``, ``none`` (BN only) or ``add_relu`` (``relu(bn(h) + res)``, the ResNet block
+    output).  Running statistics and ``num_batches_tracked`` are updated like ``bn``'s own
+    forward would.  Falls back to the torch composition for inputs the kernels do not take."""
+    if mode not in _MODES or (pool and mode != "relu") or ((res is None) != (mode != "add_relu")):
+        raise ValueError(f"bad bn_act combination mode={mode} pool={pool} res={res is not None}")
+    ok = nhwc_supported(h, pool)
+    if ok and res is not None:
+        ok = (res.shape == h.shape and res.dtype == h.dtype and res.data_ptr() % 16 == 0
+              and res.is_contiguous(memory_format=torch.channels_last))
+    if not ok:
+        return bn_act_reference(h, cbias, bn, pool, mode, res)
     batch_stats = bn.training or bn.running_mean is None
     if batch_stats:
-        momentum = bn.momentum
         # num_batches_tracked is incremented by the apply kernel (no separate add kernel)
         nbt = bn.num_batches_tracked if bn.training and bn.track_running_stats else None
         track = bn.training and bn.running_mean is not None
-        return _BNReLU.apply(h, cbias, bn.weight, bn.bias,
-                             bn.running_mean if track else None,
-                             bn.running_var if track else None, nbt, momentum, bn.eps, pool)
-    if torch.is_grad_enabled() and (h.requires_grad or (bn.weight is not None
-                                                        and bn.weight.requires_grad)):
-        return bn_relu_reference(h, cbias, bn, pool)
+        return _BNAct.apply(h, res, cbias, bn.weight, bn.bias,
+                            bn.running_mean if track else None,
+                            bn.running_var if track else None, nbt, bn.momentum, bn.eps, pool,
+                            mode)
+    if torch.is_grad_enabled() and (h.requires_grad or (res is not None and res.requires_grad)
+                                    or (bn.weight is not None and bn.weight.requires_grad)):
+        return bn_act_reference(h, cbias, bn, pool, mode, res)
     with torch.no_grad():
         invstd = torch.rsqrt(bn.running_var.float() + bn.eps)
         scale = invstd if bn.weight is None else bn.weight.float() * invstd
@@ -155,7 +177,13 @@ def bn_relu(h, cbias, bn, pool=False):
         if bn.bias is not None:
             shift = shift + bn.bias.float()
         stats = torch.cat([bn.running_mean.float(), invstd, scale, shift]).contiguous()
-    return _apply_eval(h.detach(), stats, pool)
+    return _apply_eval(h.detach(), stats, pool, mode,
+                       None if res is None else res.detach())
+
+
+def bn_relu(h, cbias, bn, pool=False):
+    """``maxpool?(relu(bn(h + cbias)))`` (VGG's conv-BN-ReLU[-pool] group)."""
+    return bn_act(h, bn, "relu", None, cbias, pool)
 
 
 class _MaxPool2(torch.autograd.Function):

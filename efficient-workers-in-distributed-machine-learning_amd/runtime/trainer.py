@@ -77,7 +77,8 @@ class Trainer:
         # activations channels_last where the fused NHWC conv-BN-ReLU-pool kernels run (VGG on the
         # GPU): MIOpen's convolutions are NHWC internally, so NCHW pays a transpose per conv
         self.channels_last = cfg.layout == "nhwc" or (
-            cfg.layout == "auto" and self.cuda and cfg.fused_nn == "on" and net.startswith("vgg"))
+            cfg.layout == "auto" and self.cuda and cfg.fused_nn == "on"
+            and net.startswith(("vgg", "resnet")))
         x, y, info = load_dataset(cfg.dataset, cfg.data_dir, train=True,
                                   synthetic_size=cfg.synthetic_size, seed=cfg.seed,
                                   device=self.device)

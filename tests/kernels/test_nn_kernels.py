@@ -216,3 +216,59 @@ def test_vgg11_fused_matches_modules():
     err_f = sum(a for a, _ in errs.values())
     err_m = sum(b for _, b in errs.values())
     assert err_f < 1.5 * err_m + 1e-2, (err_f, err_m)
+
+
+@pytest.mark.parametrize("mode", ["none", "add_relu"])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_bn_act_modes_match_torch(mode, dtype):
+    fnn = _ops()
+    torch.manual_seed(6)
+    dev = "cuda"
+    shape = (8, 256, 8, 8)
+    C = shape[1]
+    h = (torch.randn(shape, device=dev) * 1.5 + 0.3).to(dtype).contiguous(
+        memory_format=torch.channels_last)
+    r = torch.randn(shape, device=dev).to(dtype).contiguous(memory_format=torch.channels_last)
+    bn = nn.BatchNorm2d(C).to(dev)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.3, 0.3)
+    bn_ref = copy.deepcopy(bn)
+    hh = h.clone().requires_grad_(True)
+    rr = r.clone().requires_grad_(True) if mode == "add_relu" else None
+    y = fnn.bn_act(hh, bn, mode, res=rr)
+    hr = h.float().contiguous().requires_grad_(True)
+    rrr = r.float().contiguous().requires_grad_(True) if mode == "add_relu" else None
+    yr = fnn.bn_act_reference(hr, None, bn_ref, False, mode, rrr)
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert _rel(y, yr) < tol
+    assert torch.allclose(bn.running_mean, bn_ref.running_mean, atol=1e-4, rtol=1e-4)
+    dy = torch.randn_like(yr).to(dtype)
+    y.backward(dy.contiguous(memory_format=torch.channels_last))
+    yr.backward(dy.float())
+    gtol = 1e-4 if dtype == torch.float32 else 3e-2
+    assert _rel(hh.grad, hr.grad) < gtol
+    assert _rel(bn.weight.grad, bn_ref.weight.grad) < gtol
+    assert _rel(bn.bias.grad, bn_ref.bias.grad) < gtol
+    if mode == "add_relu":
+        assert _rel(rr.grad, rrr.grad) < gtol
+
+
+def test_resnet18_fused_matches_modules_fp32():
+    from ewdml.models import build_model
+
+    _ops()
+    torch.manual_seed(8)
+    base = build_model("resnet18", 10).cuda().to(memory_format=torch.channels_last)
+    x = torch.randn(16, 3, 32, 32, device="cuda").contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (16,), device="cuda")
+    runs = {}
+    for on in (True, False):
+        m = copy.deepcopy(base)
+        runs[on] = _vgg_run(m, x, y, on, False) + (m,)
+    (o_f, g_f, m_f), (o_m, g_m, m_m) = runs[True], runs[False]
+    assert _rel(o_f, o_m) < 1e-4
+    for n in g_m:  # 18 layers of fp32 rounding-order differences reach the stem
+        assert _rel(g_f[n], g_m[n]) < 1e-2, n
+    for (n, b1), (_, b2) in zip(m_f.named_buffers(), m_m.named_buffers()):
+        assert torch.allclose(b1.float(), b2.float(), rtol=1e-4, atol=1e-5), n
