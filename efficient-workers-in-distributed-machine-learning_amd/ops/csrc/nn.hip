@@ -187,9 +187,24 @@ __global__ __launch_bounds__(EW_BLOCK) void k_bn_fwd_stats(const T* __restrict__
 #pragma unroll
   for (int j = 0; j < 8; ++j) s[j] = q[j] = 0.0f;
   if (r < rpi) {
-    for (long long row = row0 + r; row < row1; row += rpi) {
+    const T* hp = h + g * 8;
+    long long row = row0 + r;
+    for (; row + 3 * rpi < row1; row += 4 * rpi) {  // 4 independent loads in flight
+      float v[4][8];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) V8<T>::ld(hp + (row + u * rpi) * C, v[u]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          s[j] += v[u][j];
+          q[j] += v[u][j] * v[u][j];
+        }
+      }
+    }
+    for (; row < row1; row += rpi) {
       float v[8];
-      V8<T>::ld(h + row * C + g * 8, v);
+      V8<T>::ld(hp + row * C, v);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         s[j] += v[j];
@@ -379,7 +394,33 @@ __global__ __launch_bounds__(EW_BLOCK) void k_bn_bwd_stats(
       sc[j] = stats[2 * C + c0 + j];
       sh[j] = stats[3 * C + c0 + j];
     }
-    for (long long row = row0 + r; row < row1; row += rpi) {
+    long long row = row0 + r;
+    if constexpr (MODE != EW_BN_RELU_POOL) {  // 2 rows per iteration: 4-6 loads in flight
+      for (; row + rpi < row1; row += 2 * rpi) {
+        float d2[2][8], x2[2][8], r2[2][8];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const long long o = (row + u * rpi) * C + c0;
+          V8<T>::ld(dy + o, d2[u]);
+          V8<T>::ld(h + o, x2[u]);
+          if constexpr (MODE == EW_BN_ADD_RELU) V8<T>::ld(res + o, r2[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            float v = x2[u][j] * sc[j] + sh[j];
+            if constexpr (MODE == EW_BN_ADD_RELU) v = v + r2[u][j];
+            const float dz = ew_act_pass<MODE>(v) ? d2[u][j] : 0.0f;
+            const float xc = x2[u][j] - mean[j];
+            s1[j] += dz;
+            s2[j] += dz * xc;
+            s3[j] += xc;
+          }
+        }
+      }
+    }
+    for (; row < row1; row += rpi) {
       float d[8];
       V8<T>::ld(dy + row * C + c0, d);
       if constexpr (MODE != EW_BN_RELU_POOL) {

