@@ -670,12 +670,12 @@ void ew_maxpool2_bwd(uintptr_t dy, uintptr_t code, uintptr_t dx, long long rows,
 // ---------------------------------------------------------------------------------------------
 // host side of the NHWC BN kernels
 
-// blocks / rows-per-block of a stats pass: >= 4 row iterations per thread, <= 1024 blocks and
+// blocks / rows-per-block of a stats pass: per_thread row iterations per thread, <= 1024 blocks,
 // nblk*C <= 256K partial floats per quantity (the workspace size the Python side allocates)
-static void ew_bn_grid(long long rows, int C, int* nblk, int* rows_per_blk) {
+static void ew_bn_grid(long long rows, int C, int* nblk, int* rows_per_blk, int per_thread) {
   const int tpr = C / 8, rpi = EW_BLOCK / tpr;
   long long iters = (rows + rpi - 1) / rpi;
-  long long nb = iters / 4;
+  long long nb = iters / per_thread;  // = the kernel's unroll: one unrolled iteration per thread
   long long cap = (1LL << 18) / C;
   if (cap > 1024) cap = 1024;
   if (nb > cap) nb = cap;
@@ -702,7 +702,7 @@ void ew_bn_relu_fwd(const BnFwdArgs& a) {
   const int C = a.C;
   if (a.training) {
     int nblk, rpb;
-    ew_bn_grid(M, C, &nblk, &rpb);
+    ew_bn_grid(M, C, &nblk, &rpb, 4);
     float* part = reinterpret_cast<float*>(a.part);
     if (a.is_bf16)
       hipLaunchKernelGGL(k_bn_fwd_stats<uint16_t>, dim3(nblk), dim3(EW_BLOCK), 0, s,
@@ -757,7 +757,7 @@ static void ew_bn_bwd_impl(const BnBwdArgs& a) {
   const int C = a.C;
   const long long rows = POOL ? a.N * (long long)Ho * Wo : M;
   int nblk, rpb;
-  ew_bn_grid(rows, C, &nblk, &rpb);
+  ew_bn_grid(rows, C, &nblk, &rpb, POOL ? 1 : 2);
   float* part = reinterpret_cast<float*>(a.part);
   const T* h = reinterpret_cast<const T*>(a.h);
   const T* res = reinterpret_cast<const T*>(a.res);

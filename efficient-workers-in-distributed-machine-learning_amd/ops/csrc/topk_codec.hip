@@ -25,6 +25,10 @@ namespace {
 constexpr int NB0 = 2048;  // pass-0 digit: key bits [30:20]
 constexpr int NB1 = 1024;  // pass-1 digit: key bits [19:10]
 constexpr int NB2 = 1024;  // pass-2 digit: key bits [9:0]
+// Global histograms (and the max key) are replicated NREP times, chosen by block index: the
+// chunks of a large tensor all hit the same few dozen bins (gradients cluster in a few exponent
+// bins), and one copy serialised ~300 global atomics per bin; the select kernel sums the copies.
+constexpr int NREP = 8;
 
 // state[t] = {prefix, k_rem, max_key, pad}
 template <bool EF>
@@ -32,7 +36,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_hist0(GradPtrs gp,
                                                          float* __restrict__ resid,
                                                          const ChunkRow* __restrict__ chunks,
                                                          uint32_t* __restrict__ hist,
-                                                         uint32_t* __restrict__ state) {
+                                                         uint32_t* __restrict__ kmaxr, int T) {
   // one private histogram per wave: gradients cluster in a few exponent bins, and four waves
   // hammering the same LDS words serialise; the waves' copies are summed at the flush
   __shared__ uint32_t hw[EW_WAVES][NB0];
@@ -66,10 +70,17 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_hist0(GradPtrs gp,
       }
     }
   }
+  __shared__ uint32_t wmax[EW_WAVES];
   kmax = ew_wave_max_u(kmax);
-  if ((threadIdx.x & 63) == 0) atomicMax(&state[c.tensor * 4 + 2], kmax);
+  if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = kmax;
   __syncthreads();
-  uint32_t* dst = hist + (size_t)c.tensor * NB0;
+  const int rep = blockIdx.x & (NREP - 1);
+  if (threadIdx.x == 0) {
+    uint32_t m = wmax[0];
+    for (int w = 1; w < EW_WAVES; ++w) m = max(m, wmax[w]);
+    atomicMax(&kmaxr[rep * T + c.tensor], m);
+  }
+  uint32_t* dst = hist + ((size_t)rep * T + c.tensor) * NB0;
   for (int i = threadIdx.x; i < NB0; i += EW_BLOCK) {
     uint32_t v = 0;
 #pragma unroll
@@ -83,7 +94,7 @@ template <int SHIFT, int MATCH>
 __global__ __launch_bounds__(EW_BLOCK) void k_topk_hist(GradPtrs gp, const float* __restrict__ flat,
                                                         const ChunkRow* __restrict__ chunks,
                                                         const uint32_t* __restrict__ state,
-                                                        uint32_t* __restrict__ hist) {
+                                                        uint32_t* __restrict__ hist, int T) {
   __shared__ uint32_t h[NB1];
   for (int i = threadIdx.x; i < NB1; i += EW_BLOCK) h[i] = 0;
   __syncthreads();
@@ -99,7 +110,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_hist(GradPtrs gp, const float
     }
   }
   __syncthreads();
-  uint32_t* dst = hist + (size_t)c.tensor * NB1;
+  uint32_t* dst = hist + ((size_t)(blockIdx.x & (NREP - 1)) * T + c.tensor) * NB1;
   for (int i = threadIdx.x; i < NB1; i += EW_BLOCK)
     if (h[i]) atomicAdd(&dst[i], h[i]);
 }
@@ -108,18 +119,29 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_hist(GradPtrs gp, const float
 template <int NB, int SHIFT, bool FIRST>
 __global__ __launch_bounds__(EW_BLOCK) void k_topk_select(const uint32_t* __restrict__ hist,
                                                           const TensorRow* __restrict__ tensors,
-                                                          uint32_t* __restrict__ state) {
+                                                          uint32_t* __restrict__ state,
+                                                          const uint32_t* __restrict__ kmaxr,
+                                                          int T) {
   constexpr int PER = NB / EW_BLOCK;
   __shared__ uint32_t ws[EW_WAVES];
   const int t = blockIdx.x;
   const uint32_t k_rem = FIRST ? (uint32_t)tensors[t].k : state[t * 4 + 1];
-  const uint32_t* ht = hist + (size_t)t * NB;
   uint32_t cnt[PER];
   uint32_t tsum = 0;
 #pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    cnt[j] = ht[NB - 1 - (threadIdx.x * PER + j)];
-    tsum += cnt[j];
+  for (int j = 0; j < PER; ++j) cnt[j] = 0;
+#pragma unroll
+  for (int r = 0; r < NREP; ++r) {
+    const uint32_t* ht = hist + ((size_t)r * T + t) * NB;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) cnt[j] += ht[NB - 1 - (threadIdx.x * PER + j)];
+  }
+#pragma unroll
+  for (int j = 0; j < PER; ++j) tsum += cnt[j];
+  if (FIRST && threadIdx.x == 0) {
+    uint32_t m = 0;
+    for (int r = 0; r < NREP; ++r) m = max(m, kmaxr[r * T + t]);
+    state[t * 4 + 2] = m;
   }
   uint32_t total;
   const uint32_t excl = ew_block_excl_scan(tsum, ws, total);
@@ -418,13 +440,15 @@ void ew_topk_encode(const TopkEncodeArgs& a) {
   auto* tensors = reinterpret_cast<const TensorRow*>(a.tensors);
   auto* scratch = reinterpret_cast<uint8_t*>(a.scratch);
   const int T = a.num_tensors, C = a.num_chunks;
-  // scratch layout (all zeroed at once): state[T*4] | hist0[T*NB0] | hist1[T*NB1] | hist2[T*NB2]
-  // | cnt_gt[C] | cnt_eq[C] | chunk_off[C] | chunk_ties[C] | chunk_sq[C] | inv[T]
+  // scratch layout (all zeroed at once): state[T*4] | kmaxr[NREP*T] | hist0[NREP*T*NB0]
+  // | hist1[NREP*T*NB1] | hist2[NREP*T*NB2] | cnt_gt[C] | cnt_eq[C] | chunk_off[C]
+  // | chunk_ties[C] | chunk_sq[C] | inv[T]
   uint32_t* state = reinterpret_cast<uint32_t*>(scratch);
-  uint32_t* hist0 = state + 4 * T;
-  uint32_t* hist1 = hist0 + (size_t)T * NB0;
-  uint32_t* hist2 = hist1 + (size_t)T * NB1;
-  uint32_t* cnt_gt = hist2 + (size_t)T * NB2;
+  uint32_t* kmaxr = state + 4 * T;
+  uint32_t* hist0 = kmaxr + NREP * T;
+  uint32_t* hist1 = hist0 + (size_t)NREP * T * NB0;
+  uint32_t* hist2 = hist1 + (size_t)NREP * T * NB1;
+  uint32_t* cnt_gt = hist2 + (size_t)NREP * T * NB2;
   uint32_t* cnt_eq = cnt_gt + C;
   uint32_t* chunk_off = cnt_eq + C;
   uint32_t* chunk_ties = chunk_off + C;
@@ -439,14 +463,14 @@ void ew_topk_encode(const TopkEncodeArgs& a) {
   float* resid = reinterpret_cast<float*>(a.resid);
   const float* src_flat = resid;  // passes after hist0 read the staged e = g + r under EF
   if (resid)
-    EW_LAUNCH(k_topk_hist0<true>, C, s, g, resid, chunks, hist0, state);
+    EW_LAUNCH(k_topk_hist0<true>, C, s, g, resid, chunks, hist0, kmaxr, T);
   else
-    EW_LAUNCH(k_topk_hist0<false>, C, s, g, resid, chunks, hist0, state);
-  EW_LAUNCH((k_topk_select<NB0, 20, true>), T, s, hist0, tensors, state);
-  EW_LAUNCH((k_topk_hist<10, 20>), C, s, g, src_flat, chunks, state, hist1);
-  EW_LAUNCH((k_topk_select<NB1, 10, false>), T, s, hist1, tensors, state);
-  EW_LAUNCH((k_topk_hist<0, 10>), C, s, g, src_flat, chunks, state, hist2);
-  EW_LAUNCH((k_topk_select<NB2, 0, false>), T, s, hist2, tensors, state);
+    EW_LAUNCH(k_topk_hist0<false>, C, s, g, resid, chunks, hist0, kmaxr, T);
+  EW_LAUNCH((k_topk_select<NB0, 20, true>), T, s, hist0, tensors, state, kmaxr, T);
+  EW_LAUNCH((k_topk_hist<10, 20>), C, s, g, src_flat, chunks, state, hist1, T);
+  EW_LAUNCH((k_topk_select<NB1, 10, false>), T, s, hist1, tensors, state, kmaxr, T);
+  EW_LAUNCH((k_topk_hist<0, 10>), C, s, g, src_flat, chunks, state, hist2, T);
+  EW_LAUNCH((k_topk_select<NB2, 0, false>), T, s, hist2, tensors, state, kmaxr, T);
   EW_LAUNCH(k_topk_count, C, s, g, src_flat, chunks, state, cnt_gt, cnt_eq, chunk_sq);
   auto* pay = reinterpret_cast<uint8_t*>(a.payload);
   EW_LAUNCH(k_topk_scan, T, s, tensors, state, cnt_gt, cnt_eq, chunk_sq, chunk_off, chunk_ties, inv,
@@ -467,7 +491,8 @@ void ew_topk_encode(const TopkEncodeArgs& a) {
 }
 
 size_t ew_topk_scratch_bytes(int T, int C) {
-  return sizeof(uint32_t) * ((size_t)4 * T + (size_t)T * (NB0 + NB1 + NB2) + 5 * (size_t)C + T);
+  return sizeof(uint32_t) *
+         ((size_t)4 * T + (size_t)NREP * T * (1 + NB0 + NB1 + NB2) + 5 * (size_t)C + T);
 }
 
 void ew_topk_decode_apply(const TopkDecodeArgs& a) {

@@ -79,6 +79,7 @@ class GradientExchange:
         self.defer_comm = False
         self.use_dev_key = False
         self.key_dev = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self._key_ring, self._key_slot = None, 0
         self._hooks = []
         if overlap:
             for p in flat.params:
@@ -194,7 +195,24 @@ class GradientExchange:
                              self.comm.rank)
         if key >= 1 << 31:
             key -= 1 << 32
-        self.key_dev.copy_(torch.tensor([key], dtype=torch.int32))
+        if self.key_dev.device.type != "cuda":
+            self.key_dev.fill_(key)
+            return
+        # asynchronous upload from a ring of pinned slots: a pageable host->device copy would
+        # block the host until the previous graph replay drained, leaving the GPU idle while the
+        # next replay is launched.  A slot is reused only after its previous copy completed.
+        if self._key_ring is None:
+            self._key_ring = [(torch.zeros(1, dtype=torch.int32).pin_memory(), None)
+                              for _ in range(8)]
+        host, ev = self._key_ring[self._key_slot]
+        if ev is not None:
+            ev.synchronize()
+        host[0] = key
+        self.key_dev.copy_(host, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._key_ring[self._key_slot] = (host, ev)
+        self._key_slot = (self._key_slot + 1) % len(self._key_ring)
 
     def finish(self, apply: bool = True):
         """Complete every bucket's exchange and (by default) apply the optimizer step."""
