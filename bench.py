@@ -123,6 +123,7 @@ def main(argv=None):
     loss = None
     for _ in range(a.steps):
         loss, _ = tr.train_step()
+    t_enq = time.perf_counter()  # host done enqueuing (the GPU may still be running)
     sync()
     t1 = time.perf_counter()
     tr.comm.barrier()
@@ -169,6 +170,7 @@ def main(argv=None):
         "ref_equiv_MiB_per_step": round(bytes_["ref_equiv_MiB_per_step"], 4),
         "ref_equiv_reduction": bytes_["ref_equiv_reduction"],
         "final_loss": final_loss,
+        "host_enqueue_ms_per_step": round((t_enq - t0) * 1e3 / a.steps, 4),
         "hip_ext": ewdml.ops.library_path() if cuda else None,
     }
     if tr.rank == 0:

@@ -16,7 +16,8 @@
 // first, so every rank emits exactly k entries per tensor (fixed-size all-gather).
 //
 // Encode launches per bucket: hist0, select0, hist1, select1, hist2, select2, count, scan, write.
-// The global state lives in one zero-initialised scratch block (one hipMemsetAsync).
+// The global state lives in one scratch block: zero-initialised once, histograms re-cleared by
+// k_topk_write after use, everything else fully rewritten per encode (no per-step memset).
 #include "common.h"
 #include "ewdml_ops.h"
 
@@ -126,6 +127,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_select(const uint32_t* __rest
   __shared__ uint32_t ws[EW_WAVES];
   const int t = blockIdx.x;
   const uint32_t k_rem = FIRST ? (uint32_t)tensors[t].k : state[t * 4 + 1];
+  if (FIRST && threadIdx.x == 0) state[t * 4 + 0] = 0u;  // (the scan below synchronises)
   uint32_t cnt[PER];
   uint32_t tsum = 0;
 #pragma unroll
@@ -267,8 +269,12 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_write(
     const uint32_t* __restrict__ chunk_off, const uint32_t* __restrict__ chunk_ties,
     const float* __restrict__ inv_arr, uint8_t* __restrict__ payload, int scales_off, int idx_off,
     int codes_off, float levels, float inv_levels, uint32_t key_arg, const uint32_t* __restrict__ keyp,
-    uint32_t bucket_offset) {
+    uint32_t bucket_offset, uint32_t* __restrict__ rezero, uint32_t rezero_words) {
   __shared__ uint32_t ws[EW_WAVES];
+  // the histograms / max-key replicas are dead once the thresholds are selected: clear them here
+  // for the next encode of this bucket (replaces a per-step memset node; first use: zero-alloc)
+  for (uint32_t i = blockIdx.x * EW_BLOCK + threadIdx.x; i < rezero_words; i += gridDim.x * EW_BLOCK)
+    rezero[i] = 0u;
   const uint32_t key = keyp ? *keyp : key_arg;  // device key: fresh per replay of a captured graph
   const ChunkRow c = chunks[blockIdx.x];
   const TensorRow tr = tensors[c.tensor];
@@ -455,7 +461,9 @@ void ew_topk_encode(const TopkEncodeArgs& a) {
   float* chunk_sq = reinterpret_cast<float*>(chunk_ties + C);
   float* inv = chunk_sq + C;
   hipStream_t s = (hipStream_t)a.stream;
-  EW_CHECK(hipMemsetAsync(scratch, 0, ew_topk_scratch_bytes(T, C), s));
+  // no scratch memset: state / count sections are fully rewritten each encode, and the histogram
+  // replicas are cleared by k_topk_write for the next one (zero-initialised at allocation)
+  const uint32_t rezero_words = (uint32_t)((size_t)NREP * T * (1 + NB0 + NB1 + NB2));
   if (a.value_kind == VK_Q4)  // nibbles are OR-ed in; every other section is fully overwritten
     EW_CHECK(hipMemsetAsync(reinterpret_cast<void*>(a.payload), 0, a.payload_bytes, s));
   GradPtrs g;
@@ -478,7 +486,7 @@ void ew_topk_encode(const TopkEncodeArgs& a) {
 #define EW_WRITE(VK, EFV)                                                                          \
   EW_LAUNCH((k_topk_write<VK, EFV>), C, s, g, resid, chunks, tensors, state, chunk_off, chunk_ties, \
             inv, pay, a.scales_off, a.idx_off, a.codes_off, a.levels, a.inv_levels, a.key,         \
-            reinterpret_cast<const uint32_t*>(a.key_ptr), a.bucket_offset)
+            reinterpret_cast<const uint32_t*>(a.key_ptr), a.bucket_offset, kmaxr, rezero_words)
   if (a.value_kind == VK_Q8) {
     if (resid) EW_WRITE(VK_Q8, true); else EW_WRITE(VK_Q8, false);
   } else if (a.value_kind == VK_Q4) {

@@ -60,6 +60,22 @@ def test_topk_encode_matches_oracle(numels, ratio, kind, bits):
     assert torch.equal(got, ref), f"payload mismatch at {(got != ref).nonzero()[:10].flatten()}"
 
 
+def test_topk_repeated_encodes_reuse_scratch():
+    """Consecutive encodes on one DevicePlan (no per-encode memset: the write kernel clears the
+    histograms for the next encode) stay bit-exact, including after a different gradient."""
+    ops.require()
+    plan = _plan([20 * 25, 20, 50 * 500, 50, 2359296], 0.01)
+    lay = Layout.build("topk_qsgd", plan, 8)
+    dp = ops.DevicePlan(plan, DEV)
+    pay = torch.zeros(lay.nbytes, dtype=torch.uint8, device=DEV)
+    for it in range(4):
+        g = _grad(plan, seed=10 + it, ties=(it == 2))
+        key = stream_key(5, it, 0)
+        ref = oracle.encode_topk(g.clone(), plan, lay, 127, "max", key)
+        ops.topk_encode(dp, g.to(DEV), pay, lay, 127, "max", key)
+        assert torch.equal(pay.cpu(), ref), f"encode {it} differs"
+
+
 def test_topk_ties_exact_count():
     ops.require()
     plan = _plan([8192 * 4 + 17, 333], 0.05)
