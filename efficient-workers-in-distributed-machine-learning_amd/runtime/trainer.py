@@ -227,11 +227,13 @@ class Trainer:
                 if self._graphs is not None:  # the lr is a kernel argument of the graph
                     self._graphs = None  # re-capture at this step (every rank: same schedule)
         if self.is_server:
-            self.model.train()
+            if not self.model.training:
+                self.model.train()
             self.exchange.finish()
             self.step += 1
             return None, None
-        self.model.train()
+        if not self.model.training:  # recursive; ~0.2 ms of host time per step otherwise
+            self.model.train()
         graphed = self.graph_mode != "off" and self.step >= self.cfg.graph_warmup
         if x is None and graphed and self.loader.fused:
             # the batch kernel is part of the graph: only the host-side epoch bookkeeping here
@@ -363,7 +365,8 @@ class Trainer:
             c1 += a1 * y.shape[0] / 100.0
             c5 += a5 * y.shape[0] / 100.0
             n += y.shape[0]
-        self.model.train()
+        if not self.model.training:  # recursive; ~0.2 ms of host time per step otherwise
+            self.model.train()
         n = max(n, 1)
         return {"test_loss": float(loss) / n, "top1": 100.0 * float(c1) / n,
                 "top5": 100.0 * float(c5) / n, "samples": n}
