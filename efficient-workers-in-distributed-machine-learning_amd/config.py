@@ -44,7 +44,8 @@ class Config:
     kill_threshold: float = 7.0  # seconds; comm watchdog timeout in 'kill' mode
     dataset: str = "MNIST"
     comm_type: str = "Bcast"  # accepted; the all-to-all exchange needs no choice here
-    num_aggregate: int = 5  # PS k-of-n aggregation (used with --topology ps --mode kill)
+    num_aggregate: int = 5  # PS k-of-n: with --topology ps --mode kill the server averages the
+    #                         first k worker gradients to arrive (parallel/ps.py)
     eval_freq: int = 50  # checkpoint (and evaluation) cadence in steps
     train_dir: str = "output/models/"
     compress_grad: str = "compress"  # 'none' forces --compress none (reference switch)

@@ -86,6 +86,17 @@ class Comm:
         else:
             dist.gather(t, None, dst=dst, group=self.group)
 
+    def isend(self, t: torch.Tensor, dst: int, tag: int = 0):
+        """Point-to-point send (RCCL / Gloo); returns the Work to wait on."""
+        return dist.isend(t, dst=dst, group=self.group, tag=tag)
+
+    def irecv(self, t: torch.Tensor, src: int, tag: int = 0):
+        return dist.irecv(t, src=src, group=self.group, tag=tag)
+
+    def recv_any(self, t: torch.Tensor, tag: int = 0) -> int:
+        """Blocking receive from whichever rank sends first (Gloo); returns the sender."""
+        return dist.recv(t, src=None, group=self.group, tag=tag)
+
     def all_to_all(self, out: torch.Tensor, inp: torch.Tensor):
         if self.world == 1:
             out.copy_(inp)

@@ -16,7 +16,16 @@ every method, with the codecs applied for real:
 
 Collectives are per bucket: one gather + one broadcast per bucket instead of 2 x #tensors
 blocking Gloo round trips per step.  The server runs no forward/backward.
+
+k-of-n aggregation (``--mode kill --num-aggregate k``, the reference's declared-but-unused
+straggler flags, ``distributed_nn.py:50-59``): the pushes become point-to-point sends, the server
+averages the first ``k`` worker gradients to ARRIVE (arrival order of the first bucket; the same
+workers for every bucket of the step) and drains the late ones without using them, so the step
+protocol stays in lockstep.  Which workers count is timing-dependent by design;
+``self.last_aggregated`` records them.
 """
+import time
+
 import torch
 
 from .engine import StepStats
@@ -25,7 +34,8 @@ from .engine import StepStats
 class PSExchange:
     server_rank = 0
 
-    def __init__(self, flat, comm, push_codec, pull_codec, optimizer, pull: str = "grad"):
+    def __init__(self, flat, comm, push_codec, pull_codec, optimizer, pull: str = "grad",
+                 aggregate: int = None):
         if comm.world < 2:
             raise ValueError("the ps topology needs at least 2 processes (1 server + workers)")
         self.flat, self.comm, self.opt, self.pull = flat, comm, optimizer, pull
@@ -46,6 +56,9 @@ class PSExchange:
             self.pull_buf.append(torch.zeros((1, Q), dtype=torch.uint8, device=self.device))
         self.avg = torch.zeros_like(flat.grad)
         self.last = StepStats()
+        W = self.N - 1
+        self.k = W if aggregate is None else max(1, min(int(aggregate), W))
+        self.last_aggregated = list(range(1, self.N))
 
     @staticmethod
     def _nbytes(codec, b):
@@ -71,6 +84,32 @@ class PSExchange:
     def begin(self):
         pass
 
+    def _push_k_of_n(self, bi):
+        """Point-to-point push; the server returns the worker ranks whose payload to use."""
+        if not self.is_server:
+            self.comm.isend(self.payload[bi], self.server_rank, tag=bi).wait()
+            return None
+        order = []
+        if self.comm.backend == "gloo":  # receive-from-any-source gives the arrival order
+            tmp = self.payload[bi]  # the server's own payload buffer is otherwise unused
+            for _ in range(self.N - 1):
+                src = self.comm.recv_any(tmp, tag=bi)
+                self.gathered[bi][src].copy_(tmp)
+                order.append(src)
+        else:  # RCCL: one receive per worker, arrival order by polling completion
+            works = {r: self.comm.irecv(self.gathered[bi][r], r, tag=bi)
+                     for r in range(1, self.N)}
+            while works:
+                done = [r for r, w in sorted(works.items()) if w.is_completed()]
+                for r in done:
+                    order.append(r)
+                    works.pop(r).wait()
+                if not done:
+                    time.sleep(0)
+        if bi == 0:  # the step's workers are chosen on the first bucket
+            self.last_aggregated = sorted(order[:self.k])
+        return self.last_aggregated
+
     def finish(self):
         W = self.N - 1
         rank = self.comm.rank
@@ -79,10 +118,17 @@ class PSExchange:
             g = self.flat.grad_view(b)
             if not self.is_server:
                 self._encode(self.push, bi, g, self.payload[bi], rank)
-            self.comm.gather(self.payload[bi], self.gathered[bi], dst=self.server_rank)
             av = self.avg[b.start:b.start + b.length]
-            if self.is_server:
-                self._decode(self.push, bi, self.gathered[bi][1:], av, 1.0 / W)
+            if self.k < W:
+                use = self._push_k_of_n(bi)
+                if self.is_server:
+                    rows = torch.tensor(use, device=self.device)
+                    self._decode(self.push, bi, self.gathered[bi].index_select(0, rows), av,
+                                 1.0 / len(use))
+            else:
+                self.comm.gather(self.payload[bi], self.gathered[bi], dst=self.server_rank)
+                if self.is_server:
+                    self._decode(self.push, bi, self.gathered[bi][1:], av, 1.0 / W)
             if self.pull == "grad":
                 if self.is_server:
                     self._encode(self.pullc, bi, av, self.pull_buf[bi][0], rank)

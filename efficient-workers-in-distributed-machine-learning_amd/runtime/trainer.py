@@ -133,7 +133,8 @@ class Trainer:
         if cfg.topology == "ps":
             self.exchange = PSExchange(self.flat, self.comm, make_codec(cfg.compress, **ckw),
                                        make_codec(cfg.pull_compress or cfg.compress, **ckw),
-                                       self.opt, pull=cfg.pull)
+                                       self.opt, pull=cfg.pull,
+                                       aggregate=cfg.num_aggregate if cfg.mode == "kill" else None)
         else:
             self.exchange = GradientExchange(self.flat, self.comm,
                                              make_codec(cfg.compress, **ckw), self.opt,

@@ -124,3 +124,37 @@ def test_payload_bytes_lenet(tmp_path):
     res = run_world(_train, 2, tmp_path, args=(["--compress", "topk_qsgd"], 1))
     assert res[0]["bytes"] == res[1]["bytes"]
     assert 431080 * 4 / res[0]["bytes"] > 125
+
+
+def _train_slow(rank, world, flags, steps, slow_rank, delay):
+    import time
+
+    import ewdml
+    from ewdml.runtime import Trainer
+
+    cfg = ewdml.parse_args(BASE + flags + ["--max-steps", str(steps)])
+    tr = Trainer(cfg)
+    chosen = []
+    for _ in range(steps):
+        if rank == slow_rank:
+            time.sleep(delay)  # a straggler: its push arrives after the others'
+        tr.train_step()
+        if rank == 0:
+            chosen.append(list(tr.exchange.last_aggregated))
+    return {"params": tr.flat.data.clone(), "chosen": chosen}
+
+
+def test_ps_k_of_n_aggregation_drops_straggler(tmp_path):
+    """--mode kill --num-aggregate 2 with 3 workers: the server averages the first two pushes to
+    arrive, so a consistently slow worker is left out every step; replicas stay identical."""
+    flags = ["--topology", "ps", "--mode", "kill", "--num-aggregate", "2", "--compress", "none",
+             "--amp", "none"]
+    res = run_world(_train_slow, 4, tmp_path, args=(flags, 3, 3, 0.6))
+    assert res[0]["chosen"] == [[1, 2]] * 3
+    _same_params(res)
+
+
+def test_ps_k_of_n_inactive_without_kill_mode(tmp_path):
+    flags = ["--topology", "ps", "--num-aggregate", "1", "--compress", "none", "--amp", "none"]
+    res = run_world(_train_slow, 3, tmp_path, args=(flags, 2, 2, 0.0))
+    assert res[0]["chosen"] == [[1, 2]] * 2
