@@ -75,12 +75,17 @@ class FusedFeatures(nn.Sequential):
     def forward(self, x):
         if not (_ENABLED and x.is_cuda):
             return super().forward(x)
+        from ..ops import conv as conv_hip
         from ..ops import nn as fnn
 
         for kind, mods, pool in self._plan():
             if kind == "cbr":
                 conv, bn = mods[0], mods[1]
-                h = conv._conv_forward(x, conv.weight, None)
+                if conv_hip.supported(x, conv.weight, conv.stride, conv.padding, conv.dilation,
+                                      conv.groups):
+                    h = conv_hip.conv3x3(x, conv.weight)  # MFMA implicit GEMM (ops/conv.py)
+                else:
+                    h = conv._conv_forward(x, conv.weight, None)
                 if fnn.nhwc_supported(h, pool):
                     x = fnn.bn_relu(h, conv.bias, bn, pool)
                 else:

@@ -1,0 +1,107 @@
+"""3x3 / stride 1 / pad 1 convolution on the gfx950 matrix cores (``ops/csrc/conv.hip``).
+
+:func:`conv3x3` is ``F.conv2d(x, w, padding=1)`` (no bias: the fused BN kernels fold the conv bias)
+for channels_last bf16 activations and weights, as an autograd function whose forward, backward-data
+and backward-weight are hand-written MFMA implicit-GEMM kernels (fp32 accumulation, bf16 results,
+like MIOpen's bf16 convolutions).  Shapes the kernels do not take (C_in or C_out not a multiple of 64, odd width, fp32,
+NCHW, other strides/padding) go to ``F.conv2d`` (MIOpen) -- e.g. VGG's first layer (3 input
+channels).  ``EWDML_CONV=miopen`` (or ``set_enabled(False)``) routes every call to MIOpen (A/B).
+
+Parity: the reference's convolutions are ``nn.Conv2d(..., kernel_size=3, padding=1)`` in
+``src/model_ops/vgg.py:46-59`` and ``resnet.py:14-36``; only the execution differs.
+"""
+import os
+
+import torch
+import torch.nn.functional as F
+
+from . import _ptr, _stream, require
+
+_ENABLED = os.environ.get("EWDML_CONV", "hip") != "miopen"
+_WS = {}
+
+
+def set_enabled(on: bool):
+    global _ENABLED
+    _ENABLED = bool(on)
+
+
+def enabled() -> bool:
+    return _ENABLED
+
+
+def _ws(device):
+    """fp32 split-reduction slabs, per (device, stream) (kernels on one stream run in order)."""
+    key = (device.index, _stream())
+    w = _WS.get(key)
+    if w is None:
+        w = torch.empty(require().conv_ws_floats(), dtype=torch.float32, device=device)
+        _WS[key] = w
+    return w
+
+
+def supported(x, w, stride=1, padding=1, dilation=1, groups=1) -> bool:
+    """True if the MFMA kernels take ``conv2d(x, w, padding=1)``."""
+    def one(v, want):
+        return v == want or v == (want, want) or v == [want, want]
+
+    if not (_ENABLED and x.is_cuda and x.dim() == 4 and w.dim() == 4):
+        return False
+    if not (one(stride, 1) and one(padding, 1) and one(dilation, 1) and groups == 1):
+        return False
+    if x.dtype != torch.bfloat16 or w.dtype != torch.bfloat16:
+        return False
+    N, C, H, W = x.shape
+    Nc = w.shape[0]
+    if tuple(w.shape[1:]) != (C, 3, 3) or C % 64 or Nc % 64 or (N * H * W) % 64 or W % 2:
+        return False
+    if x.numel() >= 2 ** 31 or N * H * W * Nc >= 2 ** 31:
+        return False
+    if not (x.is_contiguous(memory_format=torch.channels_last)
+            and w.is_contiguous(memory_format=torch.channels_last)):
+        return False
+    return x.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0
+
+
+class _Conv3x3(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w):
+        C_ = require()
+        N, C, H, W = x.shape
+        Nc = w.shape[0]
+        ws = _ws(x.device)
+        y = torch.empty((N, Nc, H, W), dtype=x.dtype, device=x.device,
+                        memory_format=torch.channels_last)
+        C_.conv3x3_fwd(_ptr(x), _ptr(w), _ptr(y), _ptr(ws), ws.numel(), N, H, W, C, Nc,
+                       _stream())
+        ctx.save_for_backward(x, w)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        C_ = require()
+        x, w = ctx.saved_tensors
+        N, C, H, W = x.shape
+        Nc = w.shape[0]
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        if dy.dtype != x.dtype:
+            dy = dy.to(x.dtype)
+        ws = _ws(x.device)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x, memory_format=torch.channels_last)
+            wt = torch.empty(w.numel(), dtype=w.dtype, device=w.device)
+            C_.conv3x3_bwd_data(_ptr(dy), _ptr(w), _ptr(wt), _ptr(dx), _ptr(ws), ws.numel(), N,
+                                H, W, C, Nc, _stream())
+        if ctx.needs_input_grad[1]:
+            dw = torch.empty_like(w, memory_format=torch.channels_last)
+            C_.conv3x3_wgrad(_ptr(dy), _ptr(x), _ptr(dw), _ptr(ws), ws.numel(), N, H, W, C, Nc,
+                             _stream())
+        return dx, dw
+
+
+def conv3x3(x, w):
+    """``F.conv2d(x, w, padding=1)`` through the MFMA kernels when :func:`supported`."""
+    if supported(x, w):
+        return _Conv3x3.apply(x, w)
+    return F.conv2d(x, w, padding=1)

@@ -238,6 +238,10 @@ PYBIND11_MODULE(_C, m) {
           a.pool = pool; a.mode = mode; a.cb_bf16 = cb_bf16; a.stream = stream;
           ew_bn_relu_bwd(a);
         });
+  m.def("conv_ws_floats", &ew_conv_ws_floats);
+  m.def("conv3x3_fwd", &ew_conv3x3_fwd);
+  m.def("conv3x3_bwd_data", &ew_conv3x3_bwd_data);
+  m.def("conv3x3_wgrad", &ew_conv3x3_wgrad);
   m.def("maxpool2_nhwc", &ew_maxpool2_nhwc);
   m.def("maxpool2_fwd", &ew_maxpool2_fwd);
   m.def("maxpool2_bwd", &ew_maxpool2_bwd);

@@ -1,0 +1,512 @@
+// 3x3 / stride 1 / pad 1 convolution as implicit GEMM on the gfx950 matrix cores (NHWC, bf16 in,
+// fp32 accumulate), forward + backward-data + backward-weight.
+//
+// Why: VGG-11 on 32x32 inputs at batch 128 is a chain of small GEMM-shaped convolutions (M = N*H*W
+// from 32768 down to 512 rows, K = 9*C up to 4608).  MIOpen runs them at 130-380 TF/s and its
+// NHWC backward solvers add a zero-fill and an fp32->bf16 cast kernel per call (~115 us per
+// training step, profiles/vgg11_bs128_fused_nhwc_graph.txt).  Here each direction is one MFMA
+// kernel (+ one reduction kernel when the reduction is split to fill 256 CUs).
+//
+//   forward     y[m][n]  = sum_{k=(r,s,c)} X~[m][k] * w[n][k]        X~ = im2col(x), implicit
+//   bwd data   dx[m][c]  = sum_{k=(r,s,n)} dY~[m][k] * w'[c][k]      w'[c][r][s][n] = w[n][2-r][2-s][c]
+//   bwd weight dw[n][k]  = sum_m dy[m][n] * X~[m][k]
+//
+// The first two are "NT" GEMMs (both operands contiguous along the reduction): 16-byte chunks go
+// global -> registers -> LDS (double buffered, one barrier per 64-deep k-step) and feed
+// v_mfma_f32_16x16x32_bf16 through ds_read_b128.  The weight gradient reduces over m, which is
+// the *slow* axis of both NHWC operands: each thread loads MR consecutive m rows x 8 channels,
+// transposes them in registers (v_perm) and writes [row][m] images of the same layout, so the
+// MFMA core is shared.  im2col is never materialised: a row's tap (r, s) is an offset of the
+// pixel index, out-of-image taps load zeros.
+//
+// LDS image of an operand tile: [rows][64] bf16, 128-B rows, 16-B chunk c of row r at chunk
+// c ^ ((r >> 1) & 7): the 16 rows a ds_read_b128 lane group fetches at one chunk land in 16
+// distinct 16-B bank slots (conflict-free), and the 8 lanes of a ds_write_b128 group (one row)
+// hit 8 distinct slots.
+//
+// Block = 256 threads = 4 waves in a 2 x 2 grid over the BM x BN output tile; wave tile
+// (BM/2) x (BN/2) of 16 x 16 MFMA tiles.  C/D map of 16x16x32: col = lane & 15,
+// row = 4 * (lane >> 4) + reg.
+#include "common.h"
+#include "ewdml_ops.h"
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int CV_BK = 64;  // reduction depth of one k-step (one 128-B LDS row per operand row)
+
+__device__ __forceinline__ int cv_off(int r, int c) {  // byte offset of chunk c of row r
+  return r * 128 + ((c ^ ((r >> 1) & 7)) << 4);
+}
+
+// MFMA over one k-step: acc[i][j] += A[rows of wave][64] * B[cols of wave][64]^T
+template <int MI, int NJ>
+__device__ __forceinline__ void cv_mma(const char* __restrict__ As, const char* __restrict__ Bs,
+                                       int arow0, int brow0, int lane, f32x4 (&acc)[MI][NJ]) {
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    const int ch = kk * 4 + (lane >> 4);
+    bf16x8 a[MI], b[NJ];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+      a[i] = *reinterpret_cast<const bf16x8*>(As + cv_off(arow0 + i * 16 + (lane & 15), ch));
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+      b[j] = *reinterpret_cast<const bf16x8*>(Bs + cv_off(brow0 + j * 16 + (lane & 15), ch));
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+  }
+}
+
+// Epilogue: bf16 output (ldo elements per row) or an fp32 split slab, straight from registers
+// (16 consecutive columns = 32 B / 64 B per row segment).
+template <int MI, int NJ>
+__device__ __forceinline__ void cv_store(const f32x4 (&acc)[MI][NJ], int row0, int col0, int lane,
+                                         uint16_t* __restrict__ out, float* __restrict__ slab,
+                                         long long ldo) {
+  const int c = col0 + (lane & 15);
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const long long r = row0 + i * 16 + 4 * (lane >> 4) + q;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        if (slab) slab[r * ldo + c + j * 16] = acc[i][j][q];
+        else out[r * ldo + c + j * 16] = ew_f2bf(acc[i][j][q]);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Both GEMM kernels run KG "k-groups" of 4 waves per block: group g takes the block's k-steps
+// g, g + KG, g + 2 KG, ... into its own double-buffered LDS stages, all groups share one barrier
+// per iteration, and at the end the groups' fp32 tiles are summed through LDS.  Small conv GEMMs
+// are latency-bound (each k-step waits on one global-load round trip); KG groups put KG k-steps
+// behind every round trip and KG x 4 waves on the CU, without the global traffic of a split-K
+// reduction (which is used on top only when the output has fewer tiles than the chip has CUs).
+
+// Sum the KG groups' accumulators into group 0's (LDS staging reused; call after a barrier).
+template <int KG, int MI, int NJ>
+__device__ __forceinline__ void cv_group_reduce(f32x4 (&acc)[MI][NJ], char* smem, int g, int wq,
+                                                int lane) {
+  if constexpr (KG > 1) {
+    float* red = reinterpret_cast<float*>(smem);
+    constexpr int PER = MI * NJ * 4 * 64;  // floats of one wave's accumulator
+    if (g > 0) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            red[((g - 1) * 4 + wq) * PER + ((i * NJ + j) * 4 + q) * 64 + lane] = acc[i][j][q];
+    }
+    __syncthreads();
+    if (g == 0) {
+#pragma unroll
+      for (int gg = 1; gg < KG; ++gg)
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              acc[i][j][q] += red[((gg - 1) * 4 + wq) * PER + ((i * NJ + j) * 4 + q) * 64 + lane];
+    }
+  }
+}
+
+// NT kernel (forward and backward-data).  x: [M][C] pixels of one NHWC tensor (M = N*H*W),
+// w: [Nc][9*C] (tap-major, channel-minor), out: [M][Nc] bf16, or fp32 slabs [split][M][Nc].
+// Split z covers k-steps [z*kps, min((z+1)*kps, ksteps)).  Requires C % 64 == 0, M % BM == 0,
+// Nc % BN == 0 (checked on the host).
+template <int BM, int BN, int KG>
+__global__ __launch_bounds__(EW_BLOCK * KG) void k_conv_nt(const uint16_t* __restrict__ x,
+                                                           const uint16_t* __restrict__ w,
+                                                           uint16_t* __restrict__ out,
+                                                           float* __restrict__ slab, int M, int H,
+                                                           int W, int C, int Nc, int kps) {
+  constexpr int PA = BM / 32, PB = BN / 32;   // 16-B vectors per thread per k-step
+  constexpr int MI = BM / 32, NJ = BN / 32;   // 16x16 tiles per wave (wave tile BM/2 x BN/2)
+  constexpr int STAGE = (BM + BN) * 128;      // bytes of one LDS stage (A then B)
+  __shared__ __attribute__((aligned(16))) char smem[KG * 2 * STAGE];
+  const int lane = threadIdx.x & 63, g = threadIdx.x >> 8, t = threadIdx.x & 255;
+  const int wq = t >> 6, wm = wq >> 1, wn = wq & 1;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int CB = C / CV_BK, ksteps = 9 * CB;
+  const int kbeg = blockIdx.z * kps;
+  const int kend = min(kbeg + kps, ksteps);
+  const int chunk = t & 7;
+  const long long K = 9LL * C;
+  char* gsm = smem + g * 2 * STAGE;
+
+  // per-thread A rows: pixel index and (h, w) (m = ((b*H)+h)*W + w)
+  int am[PA], ah[PA], aw[PA];
+#pragma unroll
+  for (int i = 0; i < PA; ++i) {
+    const int m = m0 + (t >> 3) + 32 * i;
+    am[i] = m;
+    const int hw = m % (H * W);
+    ah[i] = hw / W;
+    aw[i] = hw - ah[i] * W;
+  }
+  const uint16_t* wrow[PB];
+#pragma unroll
+  for (int i = 0; i < PB; ++i) wrow[i] = w + (long long)(n0 + (t >> 3) + 32 * i) * K + chunk * 8;
+
+  uint4 ra[PA], rb[PB];
+#define CV_NT_LOAD(S_)                                                                          \
+  do {                                                                                          \
+    const int tap_ = (S_) / CB, cb_ = (S_) - tap_ * CB;                                         \
+    const int dr_ = tap_ / 3 - 1, dc_ = tap_ - (tap_ / 3) * 3 - 1;                              \
+    _Pragma("unroll") for (int i = 0; i < PA; ++i) {                                            \
+      const int hh = ah[i] + dr_, ww = aw[i] + dc_;                                             \
+      const bool ok = (unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W;                 \
+      const uint16_t* src = x + (long long)(ok ? am[i] + dr_ * W + dc_ : 0) * C + cb_ * CV_BK + \
+                            chunk * 8;                                                          \
+      const uint4 v = *reinterpret_cast<const uint4*>(src);                                     \
+      ra[i] = ok ? v : make_uint4(0u, 0u, 0u, 0u);                                              \
+    }                                                                                           \
+    _Pragma("unroll") for (int i = 0; i < PB; ++i)                                              \
+      rb[i] = *reinterpret_cast<const uint4*>(wrow[i] + (S_) * CV_BK);                          \
+  } while (0)
+#define CV_NT_STORE(BUF_)                                                                       \
+  do {                                                                                          \
+    char* As_ = gsm + (BUF_) * STAGE;                                                           \
+    char* Bs_ = As_ + BM * 128;                                                                 \
+    _Pragma("unroll") for (int i = 0; i < PA; ++i)                                              \
+      *reinterpret_cast<uint4*>(As_ + cv_off((t >> 3) + 32 * i, chunk)) = ra[i];               \
+    _Pragma("unroll") for (int i = 0; i < PB; ++i)                                              \
+      *reinterpret_cast<uint4*>(Bs_ + cv_off((t >> 3) + 32 * i, chunk)) = rb[i];               \
+  } while (0)
+
+  f32x4 acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+
+  // group g: steps kbeg + g + KG*it; every group runs the same number of iterations (barriers)
+  const int iters = (kend - kbeg + KG - 1) / KG;
+  const int last = kend - 1;
+  int s = kbeg + g;
+  if (iters > 0) {
+    CV_NT_LOAD(min(s, last));
+    CV_NT_STORE(0);
+    __syncthreads();
+    int buf = 0;
+    for (int it = 0; it < iters; ++it, s += KG) {
+      // next step's loads in flight during this step's MFMAs (clamped: branch-free, keeps the
+      // staging registers out of scratch)
+      CV_NT_LOAD(min(s + KG, last));
+      if (s <= last) {  // wave-uniform: a group past the end only keeps the barrier count
+        const char* As = gsm + buf * STAGE;
+        cv_mma<MI, NJ>(As, As + BM * 128, wm * (BM / 2), wn * (BN / 2), lane, acc);
+      }
+      CV_NT_STORE(buf ^ 1);  // buffer last read one barrier ago
+      __syncthreads();
+      buf ^= 1;
+    }
+  }
+  cv_group_reduce<KG, MI, NJ>(acc, smem, g, wq, lane);
+  if (g != 0) return;
+  const int row0 = m0 + wm * (BM / 2), col0 = n0 + wn * (BN / 2);
+  if (slab)
+    cv_store<MI, NJ>(acc, row0, col0, lane, nullptr, slab + (long long)blockIdx.z * M * Nc, Nc);
+  else
+    cv_store<MI, NJ>(acc, row0, col0, lane, out, nullptr, Nc);
+#undef CV_NT_LOAD
+#undef CV_NT_STORE
+}
+
+// ---------------------------------------------------------------------------------------------
+// Weight-gradient kernel: dw[n][k] = sum_m dy[m][n] * X~[m][k], 64 rows of n x 64 columns of k
+// (one tap: k0 = tap*C + c0), 64 m per k-step; split z covers m-steps
+// [z*kps, min((z+1)*kps, msteps)).  dy: [M][Nc], x: [M][C].
+// Operand loader: a [64 m][64 cols] tile; thread t (of 256) takes m rows 2*(t%32), +1 and the
+// 8 columns 8*(t/32).. (16 B each), transposes the 2 x 8 block with v_perm and writes 8 dwords
+// [col][m, m+1].  The 16 lanes of a ds_write_b32 group share one row (column) and cover 16
+// distinct dwords of it: conflict-free.
+struct CvTLoad {
+  uint4 v0, v1;
+  __device__ __forceinline__ void put(char* S, int t) const {
+    const int mo = 2 * (t & 31), cc = t >> 5;
+    const uint32_t* u0 = reinterpret_cast<const uint32_t*>(&v0);
+    const uint32_t* u1 = reinterpret_cast<const uint32_t*>(&v1);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int row = cc * 8 + j;
+      // element j of each vector: half (j & 1) of dword (j >> 1); v_perm picks lo or hi halves
+      const uint32_t sel = (j & 1) ? 0x07060302u : 0x05040100u;
+      *reinterpret_cast<uint32_t*>(S + cv_off(row, mo >> 3) + (mo & 7) * 2) =
+          __builtin_amdgcn_perm(u1[j >> 1], u0[j >> 1], sel);
+    }
+  }
+};
+
+template <int KG>
+__global__ __launch_bounds__(EW_BLOCK * KG) void k_conv_wgrad(const uint16_t* __restrict__ dy,
+                                                              const uint16_t* __restrict__ x,
+                                                              uint16_t* __restrict__ dw,
+                                                              float* __restrict__ slab, int M,
+                                                              int H, int W, int C, int Nc,
+                                                              int kps) {
+  constexpr int BM = 64, BN = 64;
+  constexpr int MI = BM / 32, NJ = BN / 32;
+  constexpr int STAGE = (BM + BN) * 128;
+  __shared__ __attribute__((aligned(16))) char smem[KG * 2 * STAGE];
+  const int lane = threadIdx.x & 63, g = threadIdx.x >> 8, t = threadIdx.x & 255;
+  const int wq = t >> 6, wm = wq >> 1, wn = wq & 1;
+  const int n0 = blockIdx.x * BM;     // output rows (dy channels)
+  const int k0 = blockIdx.y * BN;     // output columns (tap, channel)
+  const int tap = k0 / C, c0 = k0 - tap * C;
+  const int dr = tap / 3 - 1, dc = tap - (tap / 3) * 3 - 1;
+  const int msteps = M / CV_BK;
+  const int sbeg = blockIdx.z * kps;
+  const int send = min(sbeg + kps, msteps);
+  const int HW = H * W;
+  const int mo = 2 * (t & 31), cc = t >> 5;
+  const uint16_t* dyp = dy + n0 + cc * 8;
+  const uint16_t* xp = x + c0 + cc * 8;
+  char* gsm = smem + g * 2 * STAGE;
+
+  CvTLoad la, lb;
+#define CV_WG_LOAD(S_)                                                                          \
+  do {                                                                                          \
+    const int m_ = (S_) * CV_BK + mo;                                                           \
+    la.v0 = *reinterpret_cast<const uint4*>(dyp + (long long)m_ * Nc);                          \
+    la.v1 = *reinterpret_cast<const uint4*>(dyp + (long long)(m_ + 1) * Nc);                    \
+    const int hw_ = m_ % HW;                                                                    \
+    const int h_ = hw_ / W, w_ = hw_ - h_ * W;                                                  \
+    /* m_ and W are even, so w_ is even and row m_ + 1 is pixel (h_, w_ + 1) of the same row */  \
+    const bool okh = (unsigned)(h_ + dr) < (unsigned)H;                                         \
+    const bool ok0 = okh && (unsigned)(w_ + dc) < (unsigned)W;                                  \
+    const bool ok1 = okh && (unsigned)(w_ + 1 + dc) < (unsigned)W;                              \
+    const long long o_ = (long long)(m_ + dr * W + dc) * C;                                     \
+    const uint4 x0_ = *reinterpret_cast<const uint4*>(xp + (ok0 ? o_ : 0));                     \
+    const uint4 x1_ = *reinterpret_cast<const uint4*>(xp + (ok1 ? o_ + C : 0));                 \
+    lb.v0 = ok0 ? x0_ : make_uint4(0u, 0u, 0u, 0u);                                             \
+    lb.v1 = ok1 ? x1_ : make_uint4(0u, 0u, 0u, 0u);                                             \
+  } while (0)
+
+  f32x4 acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+
+  const int iters = (send - sbeg + KG - 1) / KG;
+  const int last = send - 1;
+  int s = sbeg + g;
+  if (iters > 0) {
+    CV_WG_LOAD(min(s, last));
+    la.put(gsm, t);
+    lb.put(gsm + BM * 128, t);
+    __syncthreads();
+    int buf = 0;
+    for (int it = 0; it < iters; ++it, s += KG) {
+      CV_WG_LOAD(min(s + KG, last));
+      if (s <= last) {
+        const char* As = gsm + buf * STAGE;
+        cv_mma<MI, NJ>(As, As + BM * 128, wm * (BM / 2), wn * (BN / 2), lane, acc);
+      }
+      char* nx = gsm + (buf ^ 1) * STAGE;
+      la.put(nx, t);
+      lb.put(nx + BM * 128, t);
+      __syncthreads();
+      buf ^= 1;
+    }
+  }
+#undef CV_WG_LOAD
+  cv_group_reduce<KG, MI, NJ>(acc, smem, g, wq, lane);
+  if (g != 0) return;
+  const long long K = 9LL * C;
+  const int row0 = n0 + wm * (BM / 2), col0 = k0 + wn * (BN / 2);
+  if (slab)
+    cv_store<MI, NJ>(acc, row0, col0, lane, nullptr, slab + (long long)blockIdx.z * Nc * K, K);
+  else
+    cv_store<MI, NJ>(acc, row0, col0, lane, dw, nullptr, K);
+}
+
+// ---------------------------------------------------------------------------------------------
+// out_bf16[i] = bf16(sum_z slab[z][i]), 8 elements per thread (n % 8 == 0)
+__global__ __launch_bounds__(EW_BLOCK) void k_cv_slab_reduce(const float* __restrict__ slab,
+                                                             int nsplit, long long n,
+                                                             uint16_t* __restrict__ out) {
+  const long long nv = n / 8;
+  for (long long v = blockIdx.x * (long long)EW_BLOCK + threadIdx.x; v < nv;
+       v += (long long)gridDim.x * EW_BLOCK) {
+    float a[8];
+    const float4* p = reinterpret_cast<const float4*>(slab) + 2 * v;
+    float4 lo = p[0], hi = p[1];
+    a[0] = lo.x; a[1] = lo.y; a[2] = lo.z; a[3] = lo.w;
+    a[4] = hi.x; a[5] = hi.y; a[6] = hi.z; a[7] = hi.w;
+    for (int z = 1; z < nsplit; ++z) {
+      p += n / 4;
+      lo = p[0];
+      hi = p[1];
+      a[0] += lo.x; a[1] += lo.y; a[2] += lo.z; a[3] += lo.w;
+      a[4] += hi.x; a[5] += hi.y; a[6] += hi.z; a[7] += hi.w;
+    }
+    uint4 o;
+    o.x = (uint32_t)ew_f2bf(a[0]) | ((uint32_t)ew_f2bf(a[1]) << 16);
+    o.y = (uint32_t)ew_f2bf(a[2]) | ((uint32_t)ew_f2bf(a[3]) << 16);
+    o.z = (uint32_t)ew_f2bf(a[4]) | ((uint32_t)ew_f2bf(a[5]) << 16);
+    o.w = (uint32_t)ew_f2bf(a[6]) | ((uint32_t)ew_f2bf(a[7]) << 16);
+    reinterpret_cast<uint4*>(out)[v] = o;
+  }
+}
+
+// w'[c][8 - tap][n] = w[n][tap][c]: 64 x 64 (n, c) tiles of one tap through LDS
+__global__ __launch_bounds__(EW_BLOCK) void k_cv_wflip(const uint16_t* __restrict__ w,
+                                                       uint16_t* __restrict__ wt, int Nc, int C) {
+  __shared__ uint16_t tile[64][66];
+  const int tap = blockIdx.z, n0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int t = threadIdx.x;
+  for (int e = t; e < 64 * 64; e += EW_BLOCK) {
+    const int r = e >> 6, c = e & 63;  // r: n, c: channel (contiguous in w)
+    tile[r][c] = w[((long long)(n0 + r) * 9 + tap) * C + c0 + c];
+  }
+  __syncthreads();
+  for (int e = t; e < 64 * 64; e += EW_BLOCK) {
+    const int r = e >> 6, c = e & 63;  // r: channel, c: n (contiguous in wt)
+    wt[((long long)(c0 + r) * 9 + (8 - tap)) * Nc + n0 + c] = tile[c][r];
+  }
+}
+
+// Launch shape of one conv GEMM: tiles, global split of the reduction, k-groups per block.
+// Enough blocks for every CU (split-K slabs only below 128 tiles), then k-groups so that about
+// 16 waves share each CU: resident blocks per CU r = ceil(blocks / 256), KG = 4 / r (<= kgmax).
+struct CvPlan {
+  int split, kg, kps;
+};
+CvPlan cv_plan(long long tiles, int ksteps, int kgmax, long long out_floats, long long ws_floats) {
+  CvPlan p{1, 1, ksteps};
+  if (tiles < 128) {
+    while (tiles * p.split < 256 && ksteps / (p.split * 2) >= 8) p.split *= 2;
+    while (p.split > 1 && (long long)p.split * out_floats > ws_floats) p.split /= 2;
+  }
+  const long long blocks = tiles * p.split;
+  const long long r = (blocks + 255) / 256;
+  p.kg = (int)(r >= 4 ? 1 : 4 / r);
+  if (p.kg > kgmax) p.kg = kgmax;
+  if (p.kg == 3) p.kg = 2;
+  p.kps = (ksteps + p.split - 1) / p.split;
+  while (p.kg > 1 && p.kps < 2 * p.kg) p.kg /= 2;  // keep >= 2 steps per group
+  return p;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------------
+// host side
+
+long long ew_conv_ws_floats() { return 8LL << 20; }  // 32 MiB of fp32 split slabs per workspace
+
+#define CV_LAUNCH_NT(BM_, KG_)                                                                   \
+  hipLaunchKernelGGL((k_conv_nt<BM_, BM_, KG_>), grid, dim3(EW_BLOCK * KG_), 0, s, x, w, out,   \
+                     slab, M, H, W, C, Nc, p.kps)
+
+// NT GEMM (forward / backward-data): out[M][Nc] = sum X~[M][9C] w[Nc][9C]^T
+static void ew_conv_nt(const uint16_t* x, const uint16_t* w, uint16_t* out, float* ws,
+                       long long ws_floats, int M, int H, int W, int C, int Nc,
+                       hipStream_t s) {
+  if (C % CV_BK || Nc % 64 || M % 64)
+    throw std::runtime_error("ewdml conv: needs C % 64 == 0, Nc % 64 == 0, N*H*W % 64 == 0");
+  const int ksteps = 9 * (C / CV_BK);
+  const bool big = (M % 128 == 0) && (Nc % 128 == 0) && (long long)(M / 128) * (Nc / 128) >= 256;
+  const int BM = big ? 128 : 64;
+  const long long tiles = (long long)(M / BM) * (Nc / BM);
+  const CvPlan p = cv_plan(tiles, ksteps, big ? 2 : 4, (long long)M * Nc, ws_floats);
+  dim3 grid(M / BM, Nc / BM, p.split);
+  float* slab = p.split > 1 ? ws : nullptr;
+  if (big) {
+    if (p.kg == 2) CV_LAUNCH_NT(128, 2);
+    else CV_LAUNCH_NT(128, 1);
+  } else {
+    if (p.kg == 4) CV_LAUNCH_NT(64, 4);
+    else if (p.kg == 2) CV_LAUNCH_NT(64, 2);
+    else CV_LAUNCH_NT(64, 1);
+  }
+  EW_CHECK_LAUNCH();
+  if (p.split > 1) {
+    const long long n = (long long)M * Nc;
+    long long gr = (n / 8 + EW_BLOCK - 1) / EW_BLOCK;
+    if (gr > 2048) gr = 2048;
+    hipLaunchKernelGGL(k_cv_slab_reduce, dim3((int)gr), dim3(EW_BLOCK), 0, s, ws, p.split, n, out);
+    EW_CHECK_LAUNCH();
+  }
+}
+#undef CV_LAUNCH_NT
+
+void ew_conv3x3_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t ws, long long ws_floats,
+                    long long N, int H, int W, int C, int Nc, uintptr_t stream) {
+  ew_conv_nt(reinterpret_cast<const uint16_t*>(x), reinterpret_cast<const uint16_t*>(w),
+             reinterpret_cast<uint16_t*>(y), reinterpret_cast<float*>(ws), ws_floats,
+             (int)(N * H * W), H, W, C, Nc, (hipStream_t)stream);
+}
+
+void ew_conv3x3_bwd_data(uintptr_t dy, uintptr_t w, uintptr_t wt, uintptr_t dx, uintptr_t ws,
+                         long long ws_floats, long long N, int H, int W, int C, int Nc,
+                         uintptr_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (C % 64 || Nc % 64) throw std::runtime_error("ewdml conv: bwd-data needs C, Nc % 64 == 0");
+  hipLaunchKernelGGL(k_cv_wflip, dim3(C / 64, Nc / 64, 9), dim3(EW_BLOCK), 0, s,
+                     reinterpret_cast<const uint16_t*>(w), reinterpret_cast<uint16_t*>(wt), Nc, C);
+  EW_CHECK_LAUNCH();
+  // dx[m][c] = sum over (tap', n) of dY~[m][(tap', n)] * w'[c][(tap', n)]
+  ew_conv_nt(reinterpret_cast<const uint16_t*>(dy), reinterpret_cast<const uint16_t*>(wt),
+             reinterpret_cast<uint16_t*>(dx), reinterpret_cast<float*>(ws), ws_floats,
+             (int)(N * H * W), H, W, Nc, C, s);
+}
+
+void ew_conv3x3_wgrad(uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws, long long ws_floats,
+                      long long N, int H, int W, int C, int Nc, uintptr_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const long long M = N * H * W;
+  if (C % 64 || Nc % 64 || M % CV_BK || W % 2)
+    throw std::runtime_error("ewdml conv: wgrad needs C, Nc % 64 == 0 and an even width");
+  const long long K = 9LL * C;
+  const long long tiles = (long long)(Nc / 64) * (K / 64);
+  const int msteps = (int)(M / CV_BK);
+  CvPlan p{1, 1, msteps};
+  // blocks for every CU through the m split (slabs are Nc x 9C, small next to the activations)
+  while (tiles * p.split < 256 && msteps / (p.split * 2) >= 8) p.split *= 2;
+  while (p.split > 1 && (long long)p.split * Nc * K > ws_floats) p.split /= 2;
+  {
+    const CvPlan q = cv_plan(tiles * p.split, msteps / p.split, 4, 0, 0);
+    p.kg = q.kg;
+  }
+  p.kps = (msteps + p.split - 1) / p.split;
+  while (p.kg > 1 && p.kps < 2 * p.kg) p.kg /= 2;
+  dim3 grid(Nc / 64, (int)(K / 64), p.split);
+  float* slab = p.split > 1 ? reinterpret_cast<float*>(ws) : nullptr;
+  const uint16_t* dyp = reinterpret_cast<const uint16_t*>(dy);
+  const uint16_t* xp = reinterpret_cast<const uint16_t*>(x);
+  uint16_t* dwp = reinterpret_cast<uint16_t*>(dw);
+  if (p.kg == 4)
+    hipLaunchKernelGGL(k_conv_wgrad<4>, grid, dim3(EW_BLOCK * 4), 0, s, dyp, xp, dwp, slab,
+                       (int)M, H, W, C, Nc, p.kps);
+  else if (p.kg == 2)
+    hipLaunchKernelGGL(k_conv_wgrad<2>, grid, dim3(EW_BLOCK * 2), 0, s, dyp, xp, dwp, slab,
+                       (int)M, H, W, C, Nc, p.kps);
+  else
+    hipLaunchKernelGGL(k_conv_wgrad<1>, grid, dim3(EW_BLOCK), 0, s, dyp, xp, dwp, slab, (int)M,
+                       H, W, C, Nc, p.kps);
+  EW_CHECK_LAUNCH();
+  if (p.split > 1) {
+    const long long n = (long long)Nc * K;
+    long long g = (n / 8 + EW_BLOCK - 1) / EW_BLOCK;
+    if (g > 2048) g = 2048;
+    hipLaunchKernelGGL(k_cv_slab_reduce, dim3((int)g), dim3(EW_BLOCK), 0, s,
+                       reinterpret_cast<const float*>(ws), p.split, n, reinterpret_cast<uint16_t*>(dw));
+    EW_CHECK_LAUNCH();
+  }
+}

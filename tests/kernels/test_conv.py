@@ -1,0 +1,129 @@
+"""MFMA implicit-GEMM 3x3 convolution (ops/csrc/conv.hip) against plain PyTorch fp32.
+
+Inputs and weights are bf16; the reference is ``F.conv2d`` / its autograd in fp32 on the same
+(bf16-valued) tensors.  The kernels accumulate in fp32 and round the result to bf16 once, so the
+relative error is ~bf16 resolution (2^-8).  Shapes cover every tiling path: 128x128 tiles (M*N
+large), 64x64 tiles, split-K with the slab reduction (small M), H != W, and the VGG-11 layers.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _conv():
+    from ewdml import ops
+    from ewdml.ops import conv
+
+    ops.require()
+    conv.set_enabled(True)
+    return conv
+
+
+def _rel(a, b):
+    a, b = a.detach().float(), b.detach().float()
+    return float((a - b).norm() / (b.norm() + 1e-30))
+
+
+def _data(N, C, Nc, H, W, seed=0):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    x = torch.randn(N, C, H, W, device="cuda", generator=g).to(torch.bfloat16)
+    w = (torch.randn(Nc, C, 3, 3, device="cuda", generator=g) / (3.0 * C ** 0.5)).to(torch.bfloat16)
+    x = x.contiguous(memory_format=torch.channels_last)
+    w = w.contiguous(memory_format=torch.channels_last)
+    return x, w
+
+
+SHAPES = [
+    (128, 64, 128, 16, 16),   # VGG conv2: 128x128 tiles
+    (16, 128, 256, 8, 8),     # 64x64 tiles
+    (128, 256, 512, 4, 4),    # VGG conv5
+    (128, 512, 512, 2, 2),    # VGG conv7: split-K fwd / bwd-data
+    (2, 64, 128, 8, 16),      # H != W, small
+    (4, 192, 128, 4, 8),      # C not a power of two
+    (512, 64, 128, 16, 16),   # one k-group per block (many tiles)
+    (8, 128, 64, 8, 8),       # C_out = 64
+]
+
+
+@pytest.mark.parametrize("N,C,Nc,H,W", SHAPES)
+def test_conv3x3_forward(N, C, Nc, H, W):
+    conv = _conv()
+    x, w = _data(N, C, Nc, H, W)
+    assert conv.supported(x, w)
+    y = conv.conv3x3(x, w)
+    ref = F.conv2d(x.float(), w.float(), padding=1)
+    assert y.dtype == torch.bfloat16 and y.is_contiguous(memory_format=torch.channels_last)
+    assert _rel(y, ref) < 6e-3, _rel(y, ref)
+    # bf16 rounding of an fp32 result: every element within one bf16 ulp of the reference
+    err = (y.float() - ref).abs()
+    assert bool((err <= ref.abs() * 2 ** -7 + 1e-3).all()), float(err.max())
+
+
+@pytest.mark.parametrize("N,C,Nc,H,W", SHAPES)
+def test_conv3x3_backward(N, C, Nc, H, W):
+    conv = _conv()
+    x, w = _data(N, C, Nc, H, W, seed=1)
+    g = torch.Generator(device="cuda").manual_seed(7)
+    dy = torch.randn(N, Nc, H, W, device="cuda", generator=g).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    xa, wa = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
+    conv.conv3x3(xa, wa).backward(dy)
+    xr, wr = x.float().requires_grad_(True), w.float().requires_grad_(True)
+    F.conv2d(xr, wr, padding=1).backward(dy.float())
+    assert xa.grad.dtype == torch.bfloat16 and wa.grad.dtype == torch.bfloat16
+    assert _rel(xa.grad, xr.grad) < 6e-3, _rel(xa.grad, xr.grad)
+    assert _rel(wa.grad, wr.grad) < 6e-3, _rel(wa.grad, wr.grad)
+
+
+def test_conv3x3_deterministic_and_fallback():
+    conv = _conv()
+    x, w = _data(128, 512, 512, 2, 2, seed=3)
+    a = conv.conv3x3(x, w)
+    b = conv.conv3x3(x, w)
+    assert torch.equal(a, b)  # split-K slabs are summed in a fixed order
+    # unsupported shapes (3 input channels, fp32) take F.conv2d
+    x3 = torch.randn(2, 3, 8, 8, device="cuda", dtype=torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    w3 = torch.randn(128, 3, 3, 3, device="cuda", dtype=torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    assert not conv.supported(x3, w3)
+    assert torch.allclose(conv.conv3x3(x3, w3).float(), F.conv2d(x3, w3, padding=1).float())
+
+
+def test_vgg11_mfma_conv_matches_miopen_step():
+    """One bf16 training step of VGG-11-BN through the MFMA convs and through MIOpen, both against
+    the same step in fp32: the MFMA path's error must be no worse than MIOpen's (bf16 rounding
+    compounds through 8 conv+BN layers, so the two bf16 paths differ from each other by about as
+    much as each differs from fp32)."""
+    import copy
+
+    from ewdml.models import build_model
+
+    conv = _conv()
+    torch.manual_seed(0)
+    m0 = build_model("vgg11", 10).cuda().to(memory_format=torch.channels_last)
+    for mod in m0.modules():  # dropout masks would differ between the runs
+        if isinstance(mod, torch.nn.Dropout):
+            mod.p = 0.0
+    mref, m1 = copy.deepcopy(m0), copy.deepcopy(m0)
+    x = torch.randn(64, 3, 32, 32, device="cuda").contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (64,), device="cuda")
+    outs = []
+    for m, on, bf in ((mref, False, False), (m0, True, True), (m1, False, True)):
+        conv.set_enabled(on)
+        if bf:
+            for p in m.parameters():
+                p.data = p.data.to(torch.bfloat16).contiguous(
+                    memory_format=torch.channels_last if p.dim() == 4 else torch.contiguous_format)
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=bf):
+            out = m(x.to(torch.bfloat16) if bf else x)
+        F.cross_entropy(out.float(), y).backward()
+        outs.append((out.float(), [p.grad.float() for p in m.parameters()]))
+    conv.set_enabled(True)
+    (o_ref, g_ref), (o_hip, g_hip), (o_mio, g_mio) = outs
+    assert _rel(o_hip, o_ref) <= 1.5 * _rel(o_mio, o_ref) + 1e-3
+    e_hip = sum(_rel(a, b) for a, b in zip(g_hip, g_ref)) / len(g_ref)
+    e_mio = sum(_rel(a, b) for a, b in zip(g_mio, g_ref)) / len(g_ref)
+    assert e_hip <= 1.5 * e_mio + 1e-3, (e_hip, e_mio)
