@@ -3,7 +3,7 @@
 :func:`conv3x3` is ``F.conv2d(x, w, padding=1)`` (no bias: the fused BN kernels fold the conv bias)
 for channels_last bf16 activations and weights, as an autograd function whose forward, backward-data
 and backward-weight are hand-written MFMA implicit-GEMM kernels (fp32 accumulation, bf16 results,
-like MIOpen's bf16 convolutions).  Shapes the kernels do not take (C_in or C_out not a multiple of 64, odd width, fp32,
+like MIOpen's bf16 convolutions).  Shapes the kernels do not take (C_in or C_out not a multiple of 64, fp32,
 NCHW, other strides/padding) go to ``F.conv2d`` (MIOpen) -- e.g. VGG's first layer (3 input
 channels).  ``EWDML_CONV=miopen`` (or ``set_enabled(False)``) routes every call to MIOpen (A/B).
 
@@ -53,7 +53,7 @@ def supported(x, w, stride=1, padding=1, dilation=1, groups=1) -> bool:
         return False
     N, C, H, W = x.shape
     Nc = w.shape[0]
-    if tuple(w.shape[1:]) != (C, 3, 3) or C % 64 or Nc % 64 or (N * H * W) % 64 or W % 2:
+    if tuple(w.shape[1:]) != (C, 3, 3) or C % 64 or Nc % 64 or (N * H * W) % 64:
         return False
     if x.numel() >= 2 ** 31 or N * H * W * Nc >= 2 ** 31:
         return False

@@ -230,26 +230,55 @@ __global__ __launch_bounds__(EW_BLOCK * KG) void k_conv_nt(const uint16_t* __res
 // Weight-gradient kernel: dw[n][k] = sum_m dy[m][n] * X~[m][k], 64 rows of n x 64 columns of k
 // (one tap: k0 = tap*C + c0), 64 m per k-step; split z covers m-steps
 // [z*kps, min((z+1)*kps, msteps)).  dy: [M][Nc], x: [M][C].
-// Operand loader: a [64 m][64 cols] tile; thread t (of 256) takes m rows 2*(t%32), +1 and the
-// 8 columns 8*(t/32).. (16 B each), transposes the 2 x 8 block with v_perm and writes 8 dwords
-// [col][m, m+1].  The 16 lanes of a ds_write_b32 group share one row (column) and cover 16
-// distinct dwords of it: conflict-free.
-struct CvTLoad {
-  uint4 v0, v1;
-  __device__ __forceinline__ void put(char* S, int t) const {
-    const int mo = 2 * (t & 31), cc = t >> 5;
-    const uint32_t* u0 = reinterpret_cast<const uint32_t*>(&v0);
-    const uint32_t* u1 = reinterpret_cast<const uint32_t*>(&v1);
+// Both operands reduce over m, the slow axis of their NHWC tensors, so they are staged as they
+// lie -- [64 m][64 cols] images, 8 lanes per 128-B row (coalesced loads, conflict-free
+// ds_write_b128) -- and the MFMA fragments (8 consecutive m of one column) come from
+// ds_read_b64_tr_b16 transposed reads: a 16-lane group reads a 4 (m) x 16 (col) block and lane i
+// receives column i.  Image swizzle: chunk c of row r at c ^ cv_trf(r), which spreads the 8 rows
+// {r0..r0+3, r0+8..r0+11} a 32-lane half reads at two adjacent chunks over 16 distinct bank slots
+// and keeps each row's 8 chunks distinct for the writes.
+__device__ __forceinline__ int cv_trf(int r) { return (((r >> 1) & 1) << 1) | (((r >> 3) & 1) << 2); }
+__device__ __forceinline__ int cv_toff(int r, int c) { return r * 128 + ((c ^ cv_trf(r)) << 4); }
+
+typedef short cv_v4s __attribute__((ext_vector_type(4)));
+typedef short cv_v8s __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ cv_v4s cv_tr_read(const char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) cv_v4s*)(p));
+}
+
+// acc[i][j] += sum over the step's 64 m of A[m][acol0 + 16 i + .] * B[m][bcol0 + 16 j + .]
+template <int MI, int NJ>
+__device__ __forceinline__ void cv_mma_tr(const char* __restrict__ As, const char* __restrict__ Bs,
+                                          int acol0, int bcol0, int lane,
+                                          f32x4 (&acc)[MI][NJ]) {
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int row = cc * 8 + j;
-      // element j of each vector: half (j & 1) of dword (j >> 1); v_perm picks lo or hi halves
-      const uint32_t sel = (j & 1) ? 0x07060302u : 0x05040100u;
-      *reinterpret_cast<uint32_t*>(S + cv_off(row, mo >> 3) + (mo & 7) * 2) =
-          __builtin_amdgcn_perm(u1[j >> 1], u0[j >> 1], sel);
+  for (int kk = 0; kk < 2; ++kk) {
+    const int r0 = kk * 32 + 8 * g + q;  // rows r0 (elements 0..3) and r0 + 4 (elements 4..7)
+    bf16x8 a[MI], b[NJ];
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int col = acol0 + i * 16 + 4 * p;
+      const cv_v4s lo = cv_tr_read(As + cv_toff(r0, col >> 3) + (col & 7) * 2);
+      const cv_v4s hi = cv_tr_read(As + cv_toff(r0 + 4, col >> 3) + (col & 7) * 2);
+      a[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
     }
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int col = bcol0 + j * 16 + 4 * p;
+      const cv_v4s lo = cv_tr_read(Bs + cv_toff(r0, col >> 3) + (col & 7) * 2);
+      const cv_v4s hi = cv_tr_read(Bs + cv_toff(r0 + 4, col >> 3) + (col & 7) * 2);
+      b[j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+    }
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
   }
-};
+}
 
 template <int KG>
 __global__ __launch_bounds__(EW_BLOCK * KG) void k_conv_wgrad(const uint16_t* __restrict__ dy,
@@ -271,29 +300,58 @@ __global__ __launch_bounds__(EW_BLOCK * KG) void k_conv_wgrad(const uint16_t* __
   const int msteps = M / CV_BK;
   const int sbeg = blockIdx.z * kps;
   const int send = min(sbeg + kps, msteps);
-  const int HW = H * W;
-  const int mo = 2 * (t & 31), cc = t >> 5;
-  const uint16_t* dyp = dy + n0 + cc * 8;
-  const uint16_t* xp = x + c0 + cc * 8;
+  const int chunk = t & 7, r = t >> 3;  // this thread stages rows r and r + 32, chunk `chunk`
+  const uint16_t* dyp = dy + n0 + chunk * 8;
+  const uint16_t* xp = x + c0 + chunk * 8;
   char* gsm = smem + g * 2 * STAGE;
 
-  CvTLoad la, lb;
-#define CV_WG_LOAD(S_)                                                                          \
+  const int iters = (send - sbeg + KG - 1) / KG;
+  const int last = send - 1;
+  int s = sbeg + g;
+  // pixel (h, w) of rows r and r + 32 of the step being loaded, advanced by 64*KG pixels a step
+  int m = min(s, last) * CV_BK + r;
+  int h0, w0, h1, w1;
+  {
+    const int HW = H * W;
+    int hw = m % HW;
+    h0 = hw / W;
+    w0 = hw - h0 * W;
+    hw = (m + 32) % HW;
+    h1 = hw / W;
+    w1 = hw - h1 * W;
+  }
+  const int adv = CV_BK * KG, dH = (adv / W) % H, dW = adv % W;
+  uint4 ra0, ra1, rb0, rb1;
+#define CV_WG_LOAD()                                                                            \
   do {                                                                                          \
-    const int m_ = (S_) * CV_BK + mo;                                                           \
-    la.v0 = *reinterpret_cast<const uint4*>(dyp + (long long)m_ * Nc);                          \
-    la.v1 = *reinterpret_cast<const uint4*>(dyp + (long long)(m_ + 1) * Nc);                    \
-    const int hw_ = m_ % HW;                                                                    \
-    const int h_ = hw_ / W, w_ = hw_ - h_ * W;                                                  \
-    /* m_ and W are even, so w_ is even and row m_ + 1 is pixel (h_, w_ + 1) of the same row */  \
-    const bool okh = (unsigned)(h_ + dr) < (unsigned)H;                                         \
-    const bool ok0 = okh && (unsigned)(w_ + dc) < (unsigned)W;                                  \
-    const bool ok1 = okh && (unsigned)(w_ + 1 + dc) < (unsigned)W;                              \
-    const long long o_ = (long long)(m_ + dr * W + dc) * C;                                     \
-    const uint4 x0_ = *reinterpret_cast<const uint4*>(xp + (ok0 ? o_ : 0));                     \
-    const uint4 x1_ = *reinterpret_cast<const uint4*>(xp + (ok1 ? o_ + C : 0));                 \
-    lb.v0 = ok0 ? x0_ : make_uint4(0u, 0u, 0u, 0u);                                             \
-    lb.v1 = ok1 ? x1_ : make_uint4(0u, 0u, 0u, 0u);                                             \
+    ra0 = *reinterpret_cast<const uint4*>(dyp + (long long)m * Nc);                             \
+    ra1 = *reinterpret_cast<const uint4*>(dyp + (long long)(m + 32) * Nc);                      \
+    const bool ok0 = (unsigned)(h0 + dr) < (unsigned)H && (unsigned)(w0 + dc) < (unsigned)W;    \
+    const bool ok1 = (unsigned)(h1 + dr) < (unsigned)H && (unsigned)(w1 + dc) < (unsigned)W;    \
+    const uint4 x0_ = *reinterpret_cast<const uint4*>(                                          \
+        xp + (ok0 ? (long long)(m + dr * W + dc) * C : 0));                                     \
+    const uint4 x1_ = *reinterpret_cast<const uint4*>(                                          \
+        xp + (ok1 ? (long long)(m + 32 + dr * W + dc) * C : 0));                                \
+    rb0 = ok0 ? x0_ : make_uint4(0u, 0u, 0u, 0u);                                               \
+    rb1 = ok1 ? x1_ : make_uint4(0u, 0u, 0u, 0u);                                               \
+  } while (0)
+#define CV_WG_STORE(BUF_)                                                                       \
+  do {                                                                                          \
+    char* As_ = gsm + (BUF_) * STAGE;                                                           \
+    char* Bs_ = As_ + BM * 128;                                                                 \
+    *reinterpret_cast<uint4*>(As_ + cv_toff(r, chunk)) = ra0;                                   \
+    *reinterpret_cast<uint4*>(As_ + cv_toff(r + 32, chunk)) = ra1;                              \
+    *reinterpret_cast<uint4*>(Bs_ + cv_toff(r, chunk)) = rb0;                                   \
+    *reinterpret_cast<uint4*>(Bs_ + cv_toff(r + 32, chunk)) = rb1;                              \
+  } while (0)
+  // advance (m, h, w) by one group step when the next step exists (else reload: a dummy)
+#define CV_WG_ADVANCE(NEXT_)                                                                    \
+  do {                                                                                          \
+    if (NEXT_) {                                                                                \
+      m += adv;                                                                                 \
+      w0 += dW; h0 += dH; if (w0 >= W) { w0 -= W; ++h0; } if (h0 >= H) h0 -= H;                \
+      w1 += dW; h1 += dH; if (w1 >= W) { w1 -= W; ++h1; } if (h1 >= H) h1 -= H;                \
+    }                                                                                           \
   } while (0)
 
   f32x4 acc[MI][NJ];
@@ -302,29 +360,26 @@ __global__ __launch_bounds__(EW_BLOCK * KG) void k_conv_wgrad(const uint16_t* __
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
 
-  const int iters = (send - sbeg + KG - 1) / KG;
-  const int last = send - 1;
-  int s = sbeg + g;
   if (iters > 0) {
-    CV_WG_LOAD(min(s, last));
-    la.put(gsm, t);
-    lb.put(gsm + BM * 128, t);
+    CV_WG_LOAD();
+    CV_WG_STORE(0);
     __syncthreads();
     int buf = 0;
     for (int it = 0; it < iters; ++it, s += KG) {
-      CV_WG_LOAD(min(s + KG, last));
+      CV_WG_ADVANCE(s + KG <= last);
+      CV_WG_LOAD();
       if (s <= last) {
         const char* As = gsm + buf * STAGE;
-        cv_mma<MI, NJ>(As, As + BM * 128, wm * (BM / 2), wn * (BN / 2), lane, acc);
+        cv_mma_tr<MI, NJ>(As, As + BM * 128, wm * (BM / 2), wn * (BN / 2), lane, acc);
       }
-      char* nx = gsm + (buf ^ 1) * STAGE;
-      la.put(nx, t);
-      lb.put(nx + BM * 128, t);
+      CV_WG_STORE(buf ^ 1);
       __syncthreads();
       buf ^= 1;
     }
   }
 #undef CV_WG_LOAD
+#undef CV_WG_STORE
+#undef CV_WG_ADVANCE
   cv_group_reduce<KG, MI, NJ>(acc, smem, g, wq, lane);
   if (g != 0) return;
   const long long K = 9LL * C;
@@ -471,8 +526,8 @@ void ew_conv3x3_wgrad(uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws, lon
                       long long N, int H, int W, int C, int Nc, uintptr_t stream) {
   hipStream_t s = (hipStream_t)stream;
   const long long M = N * H * W;
-  if (C % 64 || Nc % 64 || M % CV_BK || W % 2)
-    throw std::runtime_error("ewdml conv: wgrad needs C, Nc % 64 == 0 and an even width");
+  if (C % 64 || Nc % 64 || M % CV_BK)
+    throw std::runtime_error("ewdml conv: wgrad needs C, Nc % 64 == 0");
   const long long K = 9LL * C;
   const long long tiles = (long long)(Nc / 64) * (K / 64);
   const int msteps = (int)(M / CV_BK);

@@ -44,6 +44,7 @@ SHAPES = [
     (4, 192, 128, 4, 8),      # C not a power of two
     (512, 64, 128, 16, 16),   # one k-group per block (many tiles)
     (8, 128, 64, 8, 8),       # C_out = 64
+    (8, 64, 128, 8, 5),       # odd width (row pairs cross image rows)
 ]
 
 
