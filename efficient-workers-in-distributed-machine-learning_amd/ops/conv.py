@@ -90,9 +90,8 @@ class _Conv3x3(torch.autograd.Function):
         dx = dw = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x, memory_format=torch.channels_last)
-            wt = torch.empty(w.numel(), dtype=w.dtype, device=w.device)
-            C_.conv3x3_bwd_data(_ptr(dy), _ptr(w), _ptr(wt), _ptr(dx), _ptr(ws), ws.numel(), N,
-                                H, W, C, Nc, _stream())
+            C_.conv3x3_bwd_data(_ptr(dy), _ptr(w), _ptr(dx), _ptr(ws), ws.numel(), N, H, W, C,
+                                Nc, _stream())
         if ctx.needs_input_grad[1]:
             dw = torch.empty_like(w, memory_format=torch.channels_last)
             C_.conv3x3_wgrad(_ptr(dy), _ptr(x), _ptr(dw), _ptr(ws), ws.numel(), N, H, W, C, Nc,

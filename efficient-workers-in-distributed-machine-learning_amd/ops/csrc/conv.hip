@@ -8,7 +8,7 @@
 // kernel (+ one reduction kernel when the reduction is split to fill 256 CUs).
 //
 //   forward     y[m][n]  = sum_{k=(r,s,c)} X~[m][k] * w[n][k]        X~ = im2col(x), implicit
-//   bwd data   dx[m][c]  = sum_{k=(r,s,n)} dY~[m][k] * w'[c][k]      w'[c][r][s][n] = w[n][2-r][2-s][c]
+//   bwd data   dx[m][c]  = sum_{k=(r,s,n)} dY~[m][k] * w[n][2-r][2-s][c]
 //   bwd weight dw[n][k]  = sum_m dy[m][n] * X~[m][k]
 //
 // The first two are "NT" GEMMs (both operands contiguous along the reduction): 16-byte chunks go
@@ -85,158 +85,7 @@ __device__ __forceinline__ void cv_store(const f32x4 (&acc)[MI][NJ], int row0, i
 }
 
 // ---------------------------------------------------------------------------------------------
-// Both GEMM kernels run KG "k-groups" of 4 waves per block: group g takes the block's k-steps
-// g, g + KG, g + 2 KG, ... into its own double-buffered LDS stages, all groups share one barrier
-// per iteration, and at the end the groups' fp32 tiles are summed through LDS.  Small conv GEMMs
-// are latency-bound (each k-step waits on one global-load round trip); KG groups put KG k-steps
-// behind every round trip and KG x 4 waves on the CU, without the global traffic of a split-K
-// reduction (which is used on top only when the output has fewer tiles than the chip has CUs).
-
-// Sum the KG groups' accumulators into group 0's (LDS staging reused; call after a barrier).
-template <int KG, int MI, int NJ>
-__device__ __forceinline__ void cv_group_reduce(f32x4 (&acc)[MI][NJ], char* smem, int g, int wq,
-                                                int lane) {
-  if constexpr (KG > 1) {
-    float* red = reinterpret_cast<float*>(smem);
-    constexpr int PER = MI * NJ * 4 * 64;  // floats of one wave's accumulator
-    if (g > 0) {
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < NJ; ++j)
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-            red[((g - 1) * 4 + wq) * PER + ((i * NJ + j) * 4 + q) * 64 + lane] = acc[i][j][q];
-    }
-    __syncthreads();
-    if (g == 0) {
-#pragma unroll
-      for (int gg = 1; gg < KG; ++gg)
-#pragma unroll
-        for (int i = 0; i < MI; ++i)
-#pragma unroll
-          for (int j = 0; j < NJ; ++j)
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-              acc[i][j][q] += red[((gg - 1) * 4 + wq) * PER + ((i * NJ + j) * 4 + q) * 64 + lane];
-    }
-  }
-}
-
-// NT kernel (forward and backward-data).  x: [M][C] pixels of one NHWC tensor (M = N*H*W),
-// w: [Nc][9*C] (tap-major, channel-minor), out: [M][Nc] bf16, or fp32 slabs [split][M][Nc].
-// Split z covers k-steps [z*kps, min((z+1)*kps, ksteps)).  Requires C % 64 == 0, M % BM == 0,
-// Nc % BN == 0 (checked on the host).
-template <int BM, int BN, int KG>
-__global__ __launch_bounds__(EW_BLOCK * KG) void k_conv_nt(const uint16_t* __restrict__ x,
-                                                           const uint16_t* __restrict__ w,
-                                                           uint16_t* __restrict__ out,
-                                                           float* __restrict__ slab, int M, int H,
-                                                           int W, int C, int Nc, int kps) {
-  constexpr int PA = BM / 32, PB = BN / 32;   // 16-B vectors per thread per k-step
-  constexpr int MI = BM / 32, NJ = BN / 32;   // 16x16 tiles per wave (wave tile BM/2 x BN/2)
-  constexpr int STAGE = (BM + BN) * 128;      // bytes of one LDS stage (A then B)
-  __shared__ __attribute__((aligned(16))) char smem[KG * 2 * STAGE];
-  const int lane = threadIdx.x & 63, g = threadIdx.x >> 8, t = threadIdx.x & 255;
-  const int wq = t >> 6, wm = wq >> 1, wn = wq & 1;
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
-  const int CB = C / CV_BK, ksteps = 9 * CB;
-  const int kbeg = blockIdx.z * kps;
-  const int kend = min(kbeg + kps, ksteps);
-  const int chunk = t & 7;
-  const long long K = 9LL * C;
-  char* gsm = smem + g * 2 * STAGE;
-
-  // per-thread A rows: pixel index and (h, w) (m = ((b*H)+h)*W + w)
-  int am[PA], ah[PA], aw[PA];
-#pragma unroll
-  for (int i = 0; i < PA; ++i) {
-    const int m = m0 + (t >> 3) + 32 * i;
-    am[i] = m;
-    const int hw = m % (H * W);
-    ah[i] = hw / W;
-    aw[i] = hw - ah[i] * W;
-  }
-  const uint16_t* wrow[PB];
-#pragma unroll
-  for (int i = 0; i < PB; ++i) wrow[i] = w + (long long)(n0 + (t >> 3) + 32 * i) * K + chunk * 8;
-
-  uint4 ra[PA], rb[PB];
-#define CV_NT_LOAD(S_)                                                                          \
-  do {                                                                                          \
-    const int tap_ = (S_) / CB, cb_ = (S_) - tap_ * CB;                                         \
-    const int dr_ = tap_ / 3 - 1, dc_ = tap_ - (tap_ / 3) * 3 - 1;                              \
-    _Pragma("unroll") for (int i = 0; i < PA; ++i) {                                            \
-      const int hh = ah[i] + dr_, ww = aw[i] + dc_;                                             \
-      const bool ok = (unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W;                 \
-      const uint16_t* src = x + (long long)(ok ? am[i] + dr_ * W + dc_ : 0) * C + cb_ * CV_BK + \
-                            chunk * 8;                                                          \
-      const uint4 v = *reinterpret_cast<const uint4*>(src);                                     \
-      ra[i] = ok ? v : make_uint4(0u, 0u, 0u, 0u);                                              \
-    }                                                                                           \
-    _Pragma("unroll") for (int i = 0; i < PB; ++i)                                              \
-      rb[i] = *reinterpret_cast<const uint4*>(wrow[i] + (S_) * CV_BK);                          \
-  } while (0)
-#define CV_NT_STORE(BUF_)                                                                       \
-  do {                                                                                          \
-    char* As_ = gsm + (BUF_) * STAGE;                                                           \
-    char* Bs_ = As_ + BM * 128;                                                                 \
-    _Pragma("unroll") for (int i = 0; i < PA; ++i)                                              \
-      *reinterpret_cast<uint4*>(As_ + cv_off((t >> 3) + 32 * i, chunk)) = ra[i];               \
-    _Pragma("unroll") for (int i = 0; i < PB; ++i)                                              \
-      *reinterpret_cast<uint4*>(Bs_ + cv_off((t >> 3) + 32 * i, chunk)) = rb[i];               \
-  } while (0)
-
-  f32x4 acc[MI][NJ];
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-
-  // group g: steps kbeg + g + KG*it; every group runs the same number of iterations (barriers)
-  const int iters = (kend - kbeg + KG - 1) / KG;
-  const int last = kend - 1;
-  int s = kbeg + g;
-  if (iters > 0) {
-    CV_NT_LOAD(min(s, last));
-    CV_NT_STORE(0);
-    __syncthreads();
-    int buf = 0;
-    for (int it = 0; it < iters; ++it, s += KG) {
-      // next step's loads in flight during this step's MFMAs (clamped: branch-free, keeps the
-      // staging registers out of scratch)
-      CV_NT_LOAD(min(s + KG, last));
-      if (s <= last) {  // wave-uniform: a group past the end only keeps the barrier count
-        const char* As = gsm + buf * STAGE;
-        cv_mma<MI, NJ>(As, As + BM * 128, wm * (BM / 2), wn * (BN / 2), lane, acc);
-      }
-      CV_NT_STORE(buf ^ 1);  // buffer last read one barrier ago
-      __syncthreads();
-      buf ^= 1;
-    }
-  }
-  cv_group_reduce<KG, MI, NJ>(acc, smem, g, wq, lane);
-  if (g != 0) return;
-  const int row0 = m0 + wm * (BM / 2), col0 = n0 + wn * (BN / 2);
-  if (slab)
-    cv_store<MI, NJ>(acc, row0, col0, lane, nullptr, slab + (long long)blockIdx.z * M * Nc, Nc);
-  else
-    cv_store<MI, NJ>(acc, row0, col0, lane, out, nullptr, Nc);
-#undef CV_NT_LOAD
-#undef CV_NT_STORE
-}
-
-// ---------------------------------------------------------------------------------------------
-// Weight-gradient kernel: dw[n][k] = sum_m dy[m][n] * X~[m][k], 64 rows of n x 64 columns of k
-// (one tap: k0 = tap*C + c0), 64 m per k-step; split z covers m-steps
-// [z*kps, min((z+1)*kps, msteps)).  dy: [M][Nc], x: [M][C].
-// Both operands reduce over m, the slow axis of their NHWC tensors, so they are staged as they
-// lie -- [64 m][64 cols] images, 8 lanes per 128-B row (coalesced loads, conflict-free
-// ds_write_b128) -- and the MFMA fragments (8 consecutive m of one column) come from
-// ds_read_b64_tr_b16 transposed reads: a 16-lane group reads a 4 (m) x 16 (col) block and lane i
-// receives column i.  Image swizzle: chunk c of row r at c ^ cv_trf(r), which spreads the 8 rows
-// {r0..r0+3, r0+8..r0+11} a 32-lane half reads at two adjacent chunks over 16 distinct bank slots
-// and keeps each row's 8 chunks distinct for the writes.
+// Transposed-operand images (weight gradient, backward data): [64 k][64 cols], 128-B rows.
 __device__ __forceinline__ int cv_trf(int r) { return (((r >> 1) & 1) << 1) | (((r >> 3) & 1) << 2); }
 __device__ __forceinline__ int cv_toff(int r, int c) { return r * 128 + ((c ^ cv_trf(r)) << 4); }
 
@@ -280,6 +129,204 @@ __device__ __forceinline__ void cv_mma_tr(const char* __restrict__ As, const cha
   }
 }
 
+
+// A fragments by ds_read_b128 from a [rows][64 k] image (cv_off), B fragments by transposed reads
+// from a [64 k][cols] image (cv_toff): the backward-data GEMM, whose weight operand is stored
+// with the reduction axis (the forward's output channel) slow.
+template <int MI, int NJ>
+__device__ __forceinline__ void cv_mma_mixed(const char* __restrict__ As,
+                                             const char* __restrict__ Bs, int arow0, int bcol0,
+                                             int lane, f32x4 (&acc)[MI][NJ]) {
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    const int ch = kk * 4 + g;
+    const int r0 = kk * 32 + 8 * g + q;
+    bf16x8 a[MI], b[NJ];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+      a[i] = *reinterpret_cast<const bf16x8*>(As + cv_off(arow0 + i * 16 + li, ch));
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int col = bcol0 + j * 16 + 4 * p;
+      const cv_v4s lo = cv_tr_read(Bs + cv_toff(r0, col >> 3) + (col & 7) * 2);
+      const cv_v4s hi = cv_tr_read(Bs + cv_toff(r0 + 4, col >> 3) + (col & 7) * 2);
+      b[j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+    }
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Both GEMM kernels run KG "k-groups" of 4 waves per block: group g takes the block's k-steps
+// g, g + KG, g + 2 KG, ... into its own double-buffered LDS stages, all groups share one barrier
+// per iteration, and at the end the groups' fp32 tiles are summed through LDS.  Small conv GEMMs
+// are latency-bound (each k-step waits on one global-load round trip); KG groups put KG k-steps
+// behind every round trip and KG x 4 waves on the CU, without the global traffic of a split-K
+// reduction (which is used on top only when the output has fewer tiles than the chip has CUs).
+
+// Sum the KG groups' accumulators into group 0's (LDS staging reused; call after a barrier).
+template <int KG, int MI, int NJ>
+__device__ __forceinline__ void cv_group_reduce(f32x4 (&acc)[MI][NJ], char* smem, int g, int wq,
+                                                int lane) {
+  if constexpr (KG > 1) {
+    float* red = reinterpret_cast<float*>(smem);
+    constexpr int PER = MI * NJ * 4 * 64;  // floats of one wave's accumulator
+    if (g > 0) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            red[((g - 1) * 4 + wq) * PER + ((i * NJ + j) * 4 + q) * 64 + lane] = acc[i][j][q];
+    }
+    __syncthreads();
+    if (g == 0) {
+#pragma unroll
+      for (int gg = 1; gg < KG; ++gg)
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              acc[i][j][q] += red[((gg - 1) * 4 + wq) * PER + ((i * NJ + j) * 4 + q) * 64 + lane];
+    }
+  }
+}
+
+// NT kernel (forward and backward-data).  x: [M][C] pixels of one NHWC tensor (M = N*H*W),
+// w: [Nc][9*C] (tap-major, channel-minor), out: [M][Nc] bf16, or fp32 slabs [split][M][Nc].
+// Split z covers k-steps [z*kps, min((z+1)*kps, ksteps)).  Requires C % 64 == 0, M % BM == 0,
+// Nc % BN == 0 (checked on the host).
+template <int BM, int BN, int KG, bool TRB>
+__global__ __launch_bounds__(EW_BLOCK * KG) void k_conv_nt(const uint16_t* __restrict__ x,
+                                                           const uint16_t* __restrict__ w,
+                                                           uint16_t* __restrict__ out,
+                                                           float* __restrict__ slab, int M, int H,
+                                                           int W, int C, int Nc, int kps) {
+  constexpr int PA = BM / 32, PB = BN / 32;   // 16-B vectors per thread per k-step
+  constexpr int MI = BM / 32, NJ = BN / 32;   // 16x16 tiles per wave (wave tile BM/2 x BN/2)
+  constexpr int STAGE = (BM + BN) * 128;      // bytes of one LDS stage (A then B)
+  __shared__ __attribute__((aligned(16))) char smem[KG * 2 * STAGE];
+  const int lane = threadIdx.x & 63, g = threadIdx.x >> 8, t = threadIdx.x & 255;
+  const int wq = t >> 6, wm = wq >> 1, wn = wq & 1;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int CB = C / CV_BK, ksteps = 9 * CB;
+  const int kbeg = blockIdx.z * kps;
+  const int kend = min(kbeg + kps, ksteps);
+  const int chunk = t & 7;
+  const long long K = 9LL * C;
+  char* gsm = smem + g * 2 * STAGE;
+
+  // per-thread A rows: pixel index and (h, w) (m = ((b*H)+h)*W + w)
+  int am[PA], ah[PA], aw[PA];
+#pragma unroll
+  for (int i = 0; i < PA; ++i) {
+    const int m = m0 + (t >> 3) + 32 * i;
+    am[i] = m;
+    const int hw = m % (H * W);
+    ah[i] = hw / W;
+    aw[i] = hw - ah[i] * W;
+  }
+  // B rows: weight rows n (forward: w[n][tap][c], contiguous along k) or, with TRB (backward
+  // data, BN = 64), the rows (64 forward-output channels) of a [64 k][64 cols] image of the
+  // forward weight w[k-channel][tap][out col], read transposed by the MFMA loop
+  static_assert(!TRB || BN == 64, "transposed B images are 64 columns wide");
+  const uint16_t* wrow[PB];
+#pragma unroll
+  for (int i = 0; i < PB; ++i)
+    wrow[i] = TRB ? w + (long long)((t >> 3) + 32 * i) * 9 * Nc + n0 + chunk * 8
+                  : w + (long long)(n0 + (t >> 3) + 32 * i) * K + chunk * 8;
+
+  uint4 ra[PA], rb[PB];
+#define CV_NT_LOAD(S_)                                                                          \
+  do {                                                                                          \
+    const int tap_ = (S_) / CB, cb_ = (S_) - tap_ * CB;                                         \
+    const int dr_ = tap_ / 3 - 1, dc_ = tap_ - (tap_ / 3) * 3 - 1;                              \
+    _Pragma("unroll") for (int i = 0; i < PA; ++i) {                                            \
+      const int hh = ah[i] + dr_, ww = aw[i] + dc_;                                             \
+      const bool ok = (unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W;                 \
+      const uint16_t* src = x + (long long)(ok ? am[i] + dr_ * W + dc_ : 0) * C + cb_ * CV_BK + \
+                            chunk * 8;                                                          \
+      const uint4 v = *reinterpret_cast<const uint4*>(src);                                     \
+      ra[i] = ok ? v : make_uint4(0u, 0u, 0u, 0u);                                              \
+    }                                                                                           \
+    /* TRB: k-block cb_ of tap tap_ = forward channels cb_*64.. at the flipped tap 8 - tap_ */  \
+    _Pragma("unroll") for (int i = 0; i < PB; ++i)                                              \
+      rb[i] = *reinterpret_cast<const uint4*>(                                                  \
+          TRB ? wrow[i] + ((long long)cb_ * CV_BK * 9 + (8 - tap_)) * Nc                         \
+              : wrow[i] + (S_) * CV_BK);                                                        \
+  } while (0)
+#define CV_NT_STORE(BUF_)                                                                       \
+  do {                                                                                          \
+    char* As_ = gsm + (BUF_) * STAGE;                                                           \
+    char* Bs_ = As_ + BM * 128;                                                                 \
+    _Pragma("unroll") for (int i = 0; i < PA; ++i)                                              \
+      *reinterpret_cast<uint4*>(As_ + cv_off((t >> 3) + 32 * i, chunk)) = ra[i];               \
+    _Pragma("unroll") for (int i = 0; i < PB; ++i)                                              \
+      *reinterpret_cast<uint4*>(Bs_ + (TRB ? cv_toff((t >> 3) + 32 * i, chunk)                  \
+                                           : cv_off((t >> 3) + 32 * i, chunk))) = rb[i];       \
+  } while (0)
+
+  f32x4 acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+
+  // group g: steps kbeg + g + KG*it; every group runs the same number of iterations (barriers)
+  const int iters = (kend - kbeg + KG - 1) / KG;
+  const int last = kend - 1;
+  int s = kbeg + g;
+  if (iters > 0) {
+    CV_NT_LOAD(min(s, last));
+    CV_NT_STORE(0);
+    __syncthreads();
+    int buf = 0;
+    for (int it = 0; it < iters; ++it, s += KG) {
+      // next step's loads in flight during this step's MFMAs (clamped: branch-free, keeps the
+      // staging registers out of scratch)
+      CV_NT_LOAD(min(s + KG, last));
+      if (s <= last) {  // wave-uniform: a group past the end only keeps the barrier count
+        const char* As = gsm + buf * STAGE;
+        if constexpr (TRB)
+          cv_mma_mixed<MI, NJ>(As, As + BM * 128, wm * (BM / 2), wn * (BN / 2), lane, acc);
+        else
+          cv_mma<MI, NJ>(As, As + BM * 128, wm * (BM / 2), wn * (BN / 2), lane, acc);
+      }
+      CV_NT_STORE(buf ^ 1);  // buffer last read one barrier ago
+      __syncthreads();
+      buf ^= 1;
+    }
+  }
+  cv_group_reduce<KG, MI, NJ>(acc, smem, g, wq, lane);
+  if (g != 0) return;
+  const int row0 = m0 + wm * (BM / 2), col0 = n0 + wn * (BN / 2);
+  if (slab)
+    cv_store<MI, NJ>(acc, row0, col0, lane, nullptr, slab + (long long)blockIdx.z * M * Nc, Nc);
+  else
+    cv_store<MI, NJ>(acc, row0, col0, lane, out, nullptr, Nc);
+#undef CV_NT_LOAD
+#undef CV_NT_STORE
+}
+
+// ---------------------------------------------------------------------------------------------
+// Weight-gradient kernel: dw[n][k] = sum_m dy[m][n] * X~[m][k], 64 rows of n x 64 columns of k
+// (one tap: k0 = tap*C + c0), 64 m per k-step; split z covers m-steps
+// [z*kps, min((z+1)*kps, msteps)).  dy: [M][Nc], x: [M][C].
+// Both operands reduce over m, the slow axis of their NHWC tensors, so they are staged as they
+// lie -- [64 m][64 cols] images, 8 lanes per 128-B row (coalesced loads, conflict-free
+// ds_write_b128) -- and the MFMA fragments (8 consecutive m of one column) come from
+// ds_read_b64_tr_b16 transposed reads: a 16-lane group reads a 4 (m) x 16 (col) block and lane i
+// receives column i.  Image swizzle: chunk c of row r at c ^ cv_trf(r), which spreads the 8 rows
+// {r0..r0+3, r0+8..r0+11} a 32-lane half reads at two adjacent chunks over 16 distinct bank slots
+// and keeps each row's 8 chunks distinct for the writes.
 template <int KG>
 __global__ __launch_bounds__(EW_BLOCK * KG) void k_conv_wgrad(const uint16_t* __restrict__ dy,
                                                               const uint16_t* __restrict__ x,
@@ -419,23 +466,6 @@ __global__ __launch_bounds__(EW_BLOCK) void k_cv_slab_reduce(const float* __rest
   }
 }
 
-// w'[c][8 - tap][n] = w[n][tap][c]: 64 x 64 (n, c) tiles of one tap through LDS
-__global__ __launch_bounds__(EW_BLOCK) void k_cv_wflip(const uint16_t* __restrict__ w,
-                                                       uint16_t* __restrict__ wt, int Nc, int C) {
-  __shared__ uint16_t tile[64][66];
-  const int tap = blockIdx.z, n0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
-  const int t = threadIdx.x;
-  for (int e = t; e < 64 * 64; e += EW_BLOCK) {
-    const int r = e >> 6, c = e & 63;  // r: n, c: channel (contiguous in w)
-    tile[r][c] = w[((long long)(n0 + r) * 9 + tap) * C + c0 + c];
-  }
-  __syncthreads();
-  for (int e = t; e < 64 * 64; e += EW_BLOCK) {
-    const int r = e >> 6, c = e & 63;  // r: channel, c: n (contiguous in wt)
-    wt[((long long)(c0 + r) * 9 + (8 - tap)) * Nc + n0 + c] = tile[c][r];
-  }
-}
-
 // Launch shape of one conv GEMM: tiles, global split of the reduction, k-groups per block.
 // Enough blocks for every CU (split-K slabs only below 128 tiles), then k-groups so that about
 // 16 waves share each CU: resident blocks per CU r = ceil(blocks / 256), KG = 4 / r (<= kgmax).
@@ -465,30 +495,37 @@ CvPlan cv_plan(long long tiles, int ksteps, int kgmax, long long out_floats, lon
 
 long long ew_conv_ws_floats() { return 8LL << 20; }  // 32 MiB of fp32 split slabs per workspace
 
-#define CV_LAUNCH_NT(BM_, KG_)                                                                   \
-  hipLaunchKernelGGL((k_conv_nt<BM_, BM_, KG_>), grid, dim3(EW_BLOCK * KG_), 0, s, x, w, out,   \
-                     slab, M, H, W, C, Nc, p.kps)
+#define CV_LAUNCH_NT(BM_, KG_, TRB_)                                                             \
+  hipLaunchKernelGGL((k_conv_nt<BM_, BM_, KG_, TRB_>), grid, dim3(EW_BLOCK * KG_), 0, s, x, w,  \
+                     out, slab, M, H, W, C, Nc, p.kps)
 
 // NT GEMM (forward / backward-data): out[M][Nc] = sum X~[M][9C] w[Nc][9C]^T
+// trb: w is the forward weight [C][9][Nc] of a backward-data GEMM (transposed B images, 64x64
+// tiles); otherwise w is [Nc][9][C].
 static void ew_conv_nt(const uint16_t* x, const uint16_t* w, uint16_t* out, float* ws,
-                       long long ws_floats, int M, int H, int W, int C, int Nc,
+                       long long ws_floats, int M, int H, int W, int C, int Nc, bool trb,
                        hipStream_t s) {
   if (C % CV_BK || Nc % 64 || M % 64)
     throw std::runtime_error("ewdml conv: needs C % 64 == 0, Nc % 64 == 0, N*H*W % 64 == 0");
   const int ksteps = 9 * (C / CV_BK);
-  const bool big = (M % 128 == 0) && (Nc % 128 == 0) && (long long)(M / 128) * (Nc / 128) >= 256;
+  const bool big = !trb && (M % 128 == 0) && (Nc % 128 == 0) &&
+                   (long long)(M / 128) * (Nc / 128) >= 256;
   const int BM = big ? 128 : 64;
   const long long tiles = (long long)(M / BM) * (Nc / BM);
   const CvPlan p = cv_plan(tiles, ksteps, big ? 2 : 4, (long long)M * Nc, ws_floats);
   dim3 grid(M / BM, Nc / BM, p.split);
   float* slab = p.split > 1 ? ws : nullptr;
   if (big) {
-    if (p.kg == 2) CV_LAUNCH_NT(128, 2);
-    else CV_LAUNCH_NT(128, 1);
+    if (p.kg == 2) CV_LAUNCH_NT(128, 2, false);
+    else CV_LAUNCH_NT(128, 1, false);
+  } else if (trb) {
+    if (p.kg == 4) CV_LAUNCH_NT(64, 4, true);
+    else if (p.kg == 2) CV_LAUNCH_NT(64, 2, true);
+    else CV_LAUNCH_NT(64, 1, true);
   } else {
-    if (p.kg == 4) CV_LAUNCH_NT(64, 4);
-    else if (p.kg == 2) CV_LAUNCH_NT(64, 2);
-    else CV_LAUNCH_NT(64, 1);
+    if (p.kg == 4) CV_LAUNCH_NT(64, 4, false);
+    else if (p.kg == 2) CV_LAUNCH_NT(64, 2, false);
+    else CV_LAUNCH_NT(64, 1, false);
   }
   EW_CHECK_LAUNCH();
   if (p.split > 1) {
@@ -505,21 +542,18 @@ void ew_conv3x3_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t ws, long lo
                     long long N, int H, int W, int C, int Nc, uintptr_t stream) {
   ew_conv_nt(reinterpret_cast<const uint16_t*>(x), reinterpret_cast<const uint16_t*>(w),
              reinterpret_cast<uint16_t*>(y), reinterpret_cast<float*>(ws), ws_floats,
-             (int)(N * H * W), H, W, C, Nc, (hipStream_t)stream);
+             (int)(N * H * W), H, W, C, Nc, false, (hipStream_t)stream);
 }
 
-void ew_conv3x3_bwd_data(uintptr_t dy, uintptr_t w, uintptr_t wt, uintptr_t dx, uintptr_t ws,
+void ew_conv3x3_bwd_data(uintptr_t dy, uintptr_t w, uintptr_t dx, uintptr_t ws,
                          long long ws_floats, long long N, int H, int W, int C, int Nc,
                          uintptr_t stream) {
-  hipStream_t s = (hipStream_t)stream;
+  // the flipped / transposed weight is read in place through transposed B images (no copy)
   if (C % 64 || Nc % 64) throw std::runtime_error("ewdml conv: bwd-data needs C, Nc % 64 == 0");
-  hipLaunchKernelGGL(k_cv_wflip, dim3(C / 64, Nc / 64, 9), dim3(EW_BLOCK), 0, s,
-                     reinterpret_cast<const uint16_t*>(w), reinterpret_cast<uint16_t*>(wt), Nc, C);
-  EW_CHECK_LAUNCH();
-  // dx[m][c] = sum over (tap', n) of dY~[m][(tap', n)] * w'[c][(tap', n)]
-  ew_conv_nt(reinterpret_cast<const uint16_t*>(dy), reinterpret_cast<const uint16_t*>(wt),
+  // dx[m][c] = sum over (tap', n) of dY~[m][(tap', n)] * w[n][8 - tap'][c]
+  ew_conv_nt(reinterpret_cast<const uint16_t*>(dy), reinterpret_cast<const uint16_t*>(w),
              reinterpret_cast<uint16_t*>(dx), reinterpret_cast<float*>(ws), ws_floats,
-             (int)(N * H * W), H, W, Nc, C, s);
+             (int)(N * H * W), H, W, Nc, C, true, (hipStream_t)stream);
 }
 
 void ew_conv3x3_wgrad(uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws, long long ws_floats,

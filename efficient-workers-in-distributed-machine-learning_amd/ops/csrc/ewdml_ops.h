@@ -138,11 +138,11 @@ void ew_make_batch(const MakeBatchArgs& a);
 
 // ---- 3x3 / stride 1 / pad 1 convolution, NHWC bf16, MFMA implicit GEMM (conv.hip) ----
 // x [N,H,W,C], w [Nc,3,3,C] (channels_last weight memory), y/dy [N,H,W,Nc]; ws: fp32 split slabs
-// (ws_floats of them); wt: [C,3,3,Nc] scratch for the flipped/transposed weight (bwd data)
+// (ws_floats of them)
 long long ew_conv_ws_floats();
 void ew_conv3x3_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t ws, long long ws_floats,
                     long long N, int H, int W, int C, int Nc, uintptr_t stream);
-void ew_conv3x3_bwd_data(uintptr_t dy, uintptr_t w, uintptr_t wt, uintptr_t dx, uintptr_t ws,
+void ew_conv3x3_bwd_data(uintptr_t dy, uintptr_t w, uintptr_t dx, uintptr_t ws,
                          long long ws_floats, long long N, int H, int W, int C, int Nc,
                          uintptr_t stream);
 void ew_conv3x3_wgrad(uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws, long long ws_floats,
