@@ -161,6 +161,25 @@ __device__ __forceinline__ void cv_mma_mixed(const char* __restrict__ As,
   }
 }
 
+// Staging registers of one operand (2 or 4 rows x 16 B per thread), named members instead of an
+// array: with arrays hipcc kept spilling the second staging set to scratch.
+// (native vector type: HIP's uint4 struct copies lower to memcpy through a stack slot)
+typedef unsigned cv_u4 __attribute__((ext_vector_type(4)));
+template <int P>
+struct CvRegs {
+  static_assert(P == 2 || P == 4, "2 or 4 rows per thread");
+  cv_u4 v0, v1, v2, v3;
+};
+#define CV_FOR_ROWS(P_, ...)                                                                    \
+  do {                                                                                          \
+    { constexpr int i = 0; cv_u4& v = R.v0; __VA_ARGS__; }                                      \
+    { constexpr int i = 1; cv_u4& v = R.v1; __VA_ARGS__; }                                      \
+    if constexpr (P_ > 2) {                                                                     \
+      { constexpr int i = 2; cv_u4& v = R.v2; __VA_ARGS__; }                                    \
+      { constexpr int i = 3; cv_u4& v = R.v3; __VA_ARGS__; }                                    \
+    }                                                                                           \
+  } while (0)
+
 // ---------------------------------------------------------------------------------------------
 // Both GEMM kernels run KG "k-groups" of 4 waves per block: group g takes the block's k-steps
 // g, g + KG, g + 2 KG, ... into its own double-buffered LDS stages, all groups share one barrier
@@ -238,40 +257,52 @@ __global__ __launch_bounds__(EW_BLOCK * KG) void k_conv_nt(const uint16_t* __res
   // data, BN = 64), the rows (64 forward-output channels) of a [64 k][64 cols] image of the
   // forward weight w[k-channel][tap][out col], read transposed by the MFMA loop
   static_assert(!TRB || BN == 64, "transposed B images are 64 columns wide");
-  const uint16_t* wrow[PB];
-#pragma unroll
-  for (int i = 0; i < PB; ++i)
-    wrow[i] = TRB ? w + (long long)((t >> 3) + 32 * i) * 9 * Nc + n0 + chunk * 8
-                  : w + (long long)(n0 + (t >> 3) + 32 * i) * K + chunk * 8;
+  // base of this thread's first B row; rows i are 32*i apart (row stride bstride elements)
+  const uint16_t* wb = TRB ? w + (long long)(t >> 3) * 9 * Nc + n0 + chunk * 8
+                           : w + (long long)(n0 + (t >> 3)) * K + chunk * 8;
+  const long long bstride = TRB ? 32LL * 9 * Nc : 32LL * K;
 
-  uint4 ra[PA], rb[PB];
-#define CV_NT_LOAD(S_)                                                                          \
+  // two staging register sets: step s+2KG is loaded while step s computes and step s+KG (loaded
+  // one iteration earlier) is written to LDS -- two k-group iterations to cover a global round trip
+  CvRegs<PA> ra0, ra1;
+  CvRegs<PB> rb0, rb1;
+#define CV_NT_LOAD(S_, RA_, RB_)                                                                \
   do {                                                                                          \
     const int tap_ = (S_) / CB, cb_ = (S_) - tap_ * CB;                                         \
     const int dr_ = tap_ / 3 - 1, dc_ = tap_ - (tap_ / 3) * 3 - 1;                              \
-    _Pragma("unroll") for (int i = 0; i < PA; ++i) {                                            \
-      const int hh = ah[i] + dr_, ww = aw[i] + dc_;                                             \
-      const bool ok = (unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W;                 \
-      const uint16_t* src = x + (long long)(ok ? am[i] + dr_ * W + dc_ : 0) * C + cb_ * CV_BK + \
-                            chunk * 8;                                                          \
-      const uint4 v = *reinterpret_cast<const uint4*>(src);                                     \
-      ra[i] = ok ? v : make_uint4(0u, 0u, 0u, 0u);                                              \
+    {                                                                                           \
+      auto& R = RA_;                                                                            \
+      CV_FOR_ROWS(PA, {                                                                         \
+        const int hh = ah[i] + dr_, ww = aw[i] + dc_;                                           \
+        const bool ok = (unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W;               \
+        const cv_u4 x_ = *reinterpret_cast<const cv_u4*>(                                       \
+            x + (long long)(ok ? am[i] + dr_ * W + dc_ : 0) * C + cb_ * CV_BK + chunk * 8);     \
+        v = ok ? x_ : cv_u4{0u, 0u, 0u, 0u};                                                    \
+      });                                                                                       \
     }                                                                                           \
     /* TRB: k-block cb_ of tap tap_ = forward channels cb_*64.. at the flipped tap 8 - tap_ */  \
-    _Pragma("unroll") for (int i = 0; i < PB; ++i)                                              \
-      rb[i] = *reinterpret_cast<const uint4*>(                                                  \
-          TRB ? wrow[i] + ((long long)cb_ * CV_BK * 9 + (8 - tap_)) * Nc                         \
-              : wrow[i] + (S_) * CV_BK);                                                        \
+    const long long bo_ = TRB ? ((long long)cb_ * CV_BK * 9 + (8 - tap_)) * Nc                   \
+                              : (long long)(S_) * CV_BK;                                        \
+    {                                                                                           \
+      auto& R = RB_;                                                                            \
+      CV_FOR_ROWS(PB, { v = *reinterpret_cast<const cv_u4*>(wb + i * bstride + bo_); });        \
+    }                                                                                           \
   } while (0)
-#define CV_NT_STORE(BUF_)                                                                       \
+#define CV_NT_STORE(BUF_, RA_, RB_)                                                             \
   do {                                                                                          \
     char* As_ = gsm + (BUF_) * STAGE;                                                           \
     char* Bs_ = As_ + BM * 128;                                                                 \
-    _Pragma("unroll") for (int i = 0; i < PA; ++i)                                              \
-      *reinterpret_cast<uint4*>(As_ + cv_off((t >> 3) + 32 * i, chunk)) = ra[i];               \
-    _Pragma("unroll") for (int i = 0; i < PB; ++i)                                              \
-      *reinterpret_cast<uint4*>(Bs_ + (TRB ? cv_toff((t >> 3) + 32 * i, chunk)                  \
-                                           : cv_off((t >> 3) + 32 * i, chunk))) = rb[i];       \
+    {                                                                                           \
+      auto& R = RA_;                                                                            \
+      CV_FOR_ROWS(PA, { *reinterpret_cast<cv_u4*>(As_ + cv_off((t >> 3) + 32 * i, chunk)) = v; }); \
+    }                                                                                           \
+    {                                                                                           \
+      auto& R = RB_;                                                                            \
+      CV_FOR_ROWS(PB, {                                                                         \
+        *reinterpret_cast<cv_u4*>(Bs_ + (TRB ? cv_toff((t >> 3) + 32 * i, chunk)                \
+                                             : cv_off((t >> 3) + 32 * i, chunk))) = v;          \
+      });                                                                                       \
+    }                                                                                           \
   } while (0)
 
   f32x4 acc[MI][NJ];
@@ -284,27 +315,35 @@ __global__ __launch_bounds__(EW_BLOCK * KG) void k_conv_nt(const uint16_t* __res
   const int iters = (kend - kbeg + KG - 1) / KG;
   const int last = kend - 1;
   int s = kbeg + g;
+#define CV_NT_MMA(BUF_)                                                                         \
+  do {                                                                                          \
+    const char* As_ = gsm + (BUF_) * STAGE;                                                     \
+    if constexpr (TRB)                                                                          \
+      cv_mma_mixed<MI, NJ>(As_, As_ + BM * 128, wm * (BM / 2), wn * (BN / 2), lane, acc);       \
+    else                                                                                        \
+      cv_mma<MI, NJ>(As_, As_ + BM * 128, wm * (BM / 2), wn * (BN / 2), lane, acc);             \
+  } while (0)
   if (iters > 0) {
-    CV_NT_LOAD(min(s, last));
-    CV_NT_STORE(0);
+    CV_NT_LOAD(min(s, last), ra0, rb0);
+    CV_NT_STORE(0, ra0, rb0);
+    CV_NT_LOAD(min(s + KG, last), ra1, rb1);
     __syncthreads();
-    int buf = 0;
-    for (int it = 0; it < iters; ++it, s += KG) {
-      // next step's loads in flight during this step's MFMAs (clamped: branch-free, keeps the
-      // staging registers out of scratch)
-      CV_NT_LOAD(min(s + KG, last));
-      if (s <= last) {  // wave-uniform: a group past the end only keeps the barrier count
-        const char* As = gsm + buf * STAGE;
-        if constexpr (TRB)
-          cv_mma_mixed<MI, NJ>(As, As + BM * 128, wm * (BM / 2), wn * (BN / 2), lane, acc);
-        else
-          cv_mma<MI, NJ>(As, As + BM * 128, wm * (BM / 2), wn * (BN / 2), lane, acc);
-      }
-      CV_NT_STORE(buf ^ 1);  // buffer last read one barrier ago
+    // loads are clamped to the last step (dummy re-loads at the end: branch-free, keeps the
+    // staging registers out of scratch); a group past the end only keeps the barrier count
+    for (int it = 0; it < iters; it += 2, s += 2 * KG) {
+      CV_NT_LOAD(min(s + 2 * KG, last), ra0, rb0);
+      if (s <= last) CV_NT_MMA(0);
+      CV_NT_STORE(1, ra1, rb1);  // buffer 1 last read one barrier ago
       __syncthreads();
-      buf ^= 1;
+      // second half unconditionally (an odd iteration count ends with an idle half: no MMA, one
+      // barrier), so the loop has no branch around a barrier and the sets stay in registers
+      CV_NT_LOAD(min(s + 3 * KG, last), ra1, rb1);
+      if (s + KG <= last) CV_NT_MMA(1);
+      CV_NT_STORE(0, ra0, rb0);
+      __syncthreads();
     }
   }
+#undef CV_NT_MMA
   cv_group_reduce<KG, MI, NJ>(acc, smem, g, wq, lane);
   if (g != 0) return;
   const int row0 = m0 + wm * (BM / 2), col0 = n0 + wn * (BN / 2);
@@ -368,8 +407,8 @@ __global__ __launch_bounds__(EW_BLOCK * KG) void k_conv_wgrad(const uint16_t* __
     w1 = hw - h1 * W;
   }
   const int adv = CV_BK * KG, dH = (adv / W) % H, dW = adv % W;
-  uint4 ra0, ra1, rb0, rb1;
-#define CV_WG_LOAD()                                                                            \
+  uint4 ra0, ra1, rb0, rb1, sa0, sa1, sb0, sb1;  // two staging sets (see k_conv_nt)
+#define CV_WG_LOAD(ra0, ra1, rb0, rb1)                                                          \
   do {                                                                                          \
     ra0 = *reinterpret_cast<const uint4*>(dyp + (long long)m * Nc);                             \
     ra1 = *reinterpret_cast<const uint4*>(dyp + (long long)(m + 32) * Nc);                      \
@@ -382,7 +421,7 @@ __global__ __launch_bounds__(EW_BLOCK * KG) void k_conv_wgrad(const uint16_t* __
     rb0 = ok0 ? x0_ : make_uint4(0u, 0u, 0u, 0u);                                               \
     rb1 = ok1 ? x1_ : make_uint4(0u, 0u, 0u, 0u);                                               \
   } while (0)
-#define CV_WG_STORE(BUF_)                                                                       \
+#define CV_WG_STORE(BUF_, ra0, ra1, rb0, rb1)                                                   \
   do {                                                                                          \
     char* As_ = gsm + (BUF_) * STAGE;                                                           \
     char* Bs_ = As_ + BM * 128;                                                                 \
@@ -408,20 +447,25 @@ __global__ __launch_bounds__(EW_BLOCK * KG) void k_conv_wgrad(const uint16_t* __
     for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
 
   if (iters > 0) {
-    CV_WG_LOAD();
-    CV_WG_STORE(0);
+    CV_WG_LOAD(ra0, ra1, rb0, rb1);
+    CV_WG_STORE(0, ra0, ra1, rb0, rb1);
+    CV_WG_ADVANCE(s + KG <= last);
+    CV_WG_LOAD(sa0, sa1, sb0, sb1);
     __syncthreads();
-    int buf = 0;
-    for (int it = 0; it < iters; ++it, s += KG) {
-      CV_WG_ADVANCE(s + KG <= last);
-      CV_WG_LOAD();
-      if (s <= last) {
-        const char* As = gsm + buf * STAGE;
-        cv_mma_tr<MI, NJ>(As, As + BM * 128, wm * (BM / 2), wn * (BN / 2), lane, acc);
-      }
-      CV_WG_STORE(buf ^ 1);
+    for (int it = 0; it < iters; it += 2, s += 2 * KG) {
+      CV_WG_ADVANCE(s + 2 * KG <= last);
+      CV_WG_LOAD(ra0, ra1, rb0, rb1);
+      if (s <= last)
+        cv_mma_tr<MI, NJ>(gsm, gsm + BM * 128, wm * (BM / 2), wn * (BN / 2), lane, acc);
+      CV_WG_STORE(1, sa0, sa1, sb0, sb1);
       __syncthreads();
-      buf ^= 1;
+      CV_WG_ADVANCE(s + 3 * KG <= last);
+      CV_WG_LOAD(sa0, sa1, sb0, sb1);
+      if (s + KG <= last)
+        cv_mma_tr<MI, NJ>(gsm + STAGE, gsm + STAGE + BM * 128, wm * (BM / 2), wn * (BN / 2),
+                          lane, acc);
+      CV_WG_STORE(0, ra0, ra1, rb0, rb1);
+      __syncthreads();
     }
   }
 #undef CV_WG_LOAD
