@@ -13,12 +13,21 @@ Fixed reference defects:
 
 On the GPU (``models.fused`` enabled) every BN runs through the fused NHWC kernels
 (``ewdml.ops.nn.bn_act``): conv-BN-ReLU, shortcut conv-BN, and the block output
-``relu(bn3(conv3) + shortcut)`` as one BN+add+ReLU kernel set; same modules and state_dict.
+``relu(bn3(conv3) + shortcut)`` as one BN+add+ReLU kernel set; the stride-1 3x3 and 1x1
+convolutions run the MFMA implicit-GEMM kernels (``ewdml.ops.conv``); same modules and state_dict.
 """
 import torch.nn as nn
 import torch.nn.functional as F
 
 from . import fused
+
+
+def _conv(m, x):
+    """``m(x)``; stride-1 3x3 / 1x1 layers on channels_last bf16 run the MFMA implicit-GEMM
+    kernels (``ewdml.ops.conv``), the others (strided, stem) MIOpen."""
+    from ..ops.conv import conv2d_module
+
+    return conv2d_module(m, x)
 
 
 def _shortcut(sc, x):
@@ -27,7 +36,7 @@ def _shortcut(sc, x):
         return x
     from ..ops.nn import bn_act
 
-    return bn_act(sc[0](x), sc[1], "none")
+    return bn_act(_conv(sc[0], x), sc[1], "none")
 
 
 class BasicBlock(nn.Module):
@@ -50,8 +59,9 @@ class BasicBlock(nn.Module):
         if fused.active(x):
             from ..ops.nn import bn_act
 
-            out = bn_act(self.conv1(x), self.bn1, "relu")
-            return bn_act(self.conv2(out), self.bn2, "add_relu", res=_shortcut(self.shortcut, x))
+            out = bn_act(_conv(self.conv1, x), self.bn1, "relu")
+            return bn_act(_conv(self.conv2, out), self.bn2, "add_relu",
+                          res=_shortcut(self.shortcut, x))
         out = F.relu(self.bn1(self.conv1(x)))
         out = self.bn2(self.conv2(out))
         return F.relu(out + self.shortcut(x))
@@ -79,9 +89,10 @@ class Bottleneck(nn.Module):
         if fused.active(x):
             from ..ops.nn import bn_act
 
-            out = bn_act(self.conv1(x), self.bn1, "relu")
-            out = bn_act(self.conv2(out), self.bn2, "relu")
-            return bn_act(self.conv3(out), self.bn3, "add_relu", res=_shortcut(self.shortcut, x))
+            out = bn_act(_conv(self.conv1, x), self.bn1, "relu")
+            out = bn_act(_conv(self.conv2, out), self.bn2, "relu")
+            return bn_act(_conv(self.conv3, out), self.bn3, "add_relu",
+                          res=_shortcut(self.shortcut, x))
         out = F.relu(self.bn1(self.conv1(x)))
         out = F.relu(self.bn2(self.conv2(out)))
         out = self.bn3(self.conv3(out))

@@ -1,9 +1,10 @@
-"""3x3 / stride 1 / pad 1 convolution on the gfx950 matrix cores (``ops/csrc/conv.hip``).
+"""Stride-1 3x3 (pad 1) and 1x1 convolutions on the gfx950 matrix cores (``ops/csrc/conv.hip``).
 
-:func:`conv3x3` is ``F.conv2d(x, w, padding=1)`` (no bias: the fused BN kernels fold the conv bias)
-for channels_last bf16 activations and weights, as an autograd function whose forward, backward-data
-and backward-weight are hand-written MFMA implicit-GEMM kernels (fp32 accumulation, bf16 results,
-like MIOpen's bf16 convolutions).  Shapes the kernels do not take (C_in or C_out not a multiple of 64, fp32,
+:func:`conv` is ``F.conv2d(x, w, padding=k // 2)`` (no bias: the fused BN kernels fold the conv
+bias) for channels_last bf16 activations and weights, as an autograd function whose forward,
+backward-data and backward-weight are hand-written MFMA implicit-GEMM kernels (fp32 accumulation,
+bf16 results, like MIOpen's bf16 convolutions).  :func:`conv2d_module` dispatches an
+``nn.Conv2d`` (VGG's and ResNet's stride-1 3x3 / 1x1 layers).  Shapes the kernels do not take (C_in or C_out not a multiple of 64, fp32,
 NCHW, other strides/padding) go to ``F.conv2d`` (MIOpen) -- e.g. VGG's first layer (3 input
 channels).  ``EWDML_CONV=miopen`` (or ``set_enabled(False)``) routes every call to MIOpen (A/B).
 
@@ -40,20 +41,26 @@ def _ws(device):
     return w
 
 
-def supported(x, w, stride=1, padding=1, dilation=1, groups=1) -> bool:
-    """True if the MFMA kernels take ``conv2d(x, w, padding=1)``."""
+def supported(x, w, stride=1, padding=None, dilation=1, groups=1) -> bool:
+    """True if the MFMA kernels take ``conv2d(x, w, stride, padding, dilation, groups)``: a 3x3
+    kernel with padding 1 or a 1x1 kernel with padding 0, stride 1."""
     def one(v, want):
         return v == want or v == (want, want) or v == [want, want]
 
     if not (_ENABLED and x.is_cuda and x.dim() == 4 and w.dim() == 4):
         return False
-    if not (one(stride, 1) and one(padding, 1) and one(dilation, 1) and groups == 1):
+    k = w.shape[-1]
+    if k not in (1, 3) or w.shape[-2] != k:
+        return False
+    if padding is None:
+        padding = k // 2
+    if not (one(stride, 1) and one(padding, k // 2) and one(dilation, 1) and groups == 1):
         return False
     if x.dtype != torch.bfloat16 or w.dtype != torch.bfloat16:
         return False
     N, C, H, W = x.shape
     Nc = w.shape[0]
-    if tuple(w.shape[1:]) != (C, 3, 3) or C % 64 or Nc % 64 or (N * H * W) % 64:
+    if w.shape[1] != C or C % 64 or Nc % 64 or (N * H * W) % 64:
         return False
     if x.numel() >= 2 ** 31 or N * H * W * Nc >= 2 ** 31:
         return False
@@ -63,17 +70,17 @@ def supported(x, w, stride=1, padding=1, dilation=1, groups=1) -> bool:
     return x.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0
 
 
-class _Conv3x3(torch.autograd.Function):
+class _Conv(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w):
         C_ = require()
         N, C, H, W = x.shape
-        Nc = w.shape[0]
+        Nc, k = w.shape[0], w.shape[-1]
         ws = _ws(x.device)
         y = torch.empty((N, Nc, H, W), dtype=x.dtype, device=x.device,
                         memory_format=torch.channels_last)
-        C_.conv3x3_fwd(_ptr(x), _ptr(w), _ptr(y), _ptr(ws), ws.numel(), N, H, W, C, Nc,
-                       _stream())
+        C_.conv_fwd(_ptr(x), _ptr(w), _ptr(y), _ptr(ws), ws.numel(), N, H, W, C, Nc, k,
+                    _stream())
         ctx.save_for_backward(x, w)
         return y
 
@@ -82,7 +89,7 @@ class _Conv3x3(torch.autograd.Function):
         C_ = require()
         x, w = ctx.saved_tensors
         N, C, H, W = x.shape
-        Nc = w.shape[0]
+        Nc, k = w.shape[0], w.shape[-1]
         dy = dy.contiguous(memory_format=torch.channels_last)
         if dy.dtype != x.dtype:
             dy = dy.to(x.dtype)
@@ -90,17 +97,30 @@ class _Conv3x3(torch.autograd.Function):
         dx = dw = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x, memory_format=torch.channels_last)
-            C_.conv3x3_bwd_data(_ptr(dy), _ptr(w), _ptr(dx), _ptr(ws), ws.numel(), N, H, W, C,
-                                Nc, _stream())
+            C_.conv_bwd_data(_ptr(dy), _ptr(w), _ptr(dx), _ptr(ws), ws.numel(), N, H, W, C, Nc,
+                             k, _stream())
         if ctx.needs_input_grad[1]:
             dw = torch.empty_like(w, memory_format=torch.channels_last)
-            C_.conv3x3_wgrad(_ptr(dy), _ptr(x), _ptr(dw), _ptr(ws), ws.numel(), N, H, W, C, Nc,
-                             _stream())
+            C_.conv_wgrad(_ptr(dy), _ptr(x), _ptr(dw), _ptr(ws), ws.numel(), N, H, W, C, Nc, k,
+                          _stream())
         return dx, dw
 
 
-def conv3x3(x, w):
-    """``F.conv2d(x, w, padding=1)`` through the MFMA kernels when :func:`supported`."""
+def conv(x, w):
+    """``F.conv2d(x, w, padding=k // 2)`` (k = 3 or 1) through the MFMA kernels when
+    :func:`supported`."""
     if supported(x, w):
-        return _Conv3x3.apply(x, w)
-    return F.conv2d(x, w, padding=1)
+        return _Conv.apply(x, w)
+    return F.conv2d(x, w, padding=w.shape[-1] // 2)
+
+
+conv3x3 = conv
+
+
+def conv2d_module(m, x):
+    """``m(x)`` for an ``nn.Conv2d`` ``m`` without bias, through the MFMA kernels when the layer
+    is a stride-1 3x3/pad-1 or 1x1/pad-0 convolution on channels_last bf16 (else ``m(x)``)."""
+    if (m.bias is None and m.padding_mode == "zeros"
+            and supported(x, m.weight, m.stride, m.padding, m.dilation, m.groups)):
+        return _Conv.apply(x, m.weight)
+    return m(x)

@@ -239,9 +239,9 @@ PYBIND11_MODULE(_C, m) {
           ew_bn_relu_bwd(a);
         });
   m.def("conv_ws_floats", &ew_conv_ws_floats);
-  m.def("conv3x3_fwd", &ew_conv3x3_fwd);
-  m.def("conv3x3_bwd_data", &ew_conv3x3_bwd_data);
-  m.def("conv3x3_wgrad", &ew_conv3x3_wgrad);
+  m.def("conv_fwd", &ew_conv_fwd);
+  m.def("conv_bwd_data", &ew_conv_bwd_data);
+  m.def("conv_wgrad", &ew_conv_wgrad);
   m.def("maxpool2_nhwc", &ew_maxpool2_nhwc);
   m.def("maxpool2_fwd", &ew_maxpool2_fwd);
   m.def("maxpool2_bwd", &ew_maxpool2_bwd);

@@ -228,7 +228,8 @@ __global__ __launch_bounds__(EW_BLOCK * KG) void k_conv_nt(const uint16_t* __res
                                                            const uint16_t* __restrict__ w,
                                                            uint16_t* __restrict__ out,
                                                            float* __restrict__ slab, int M, int H,
-                                                           int W, int C, int Nc, int kps) {
+                                                           int W, int C, int Nc, int kps,
+                                                           int taps) {
   constexpr int PA = BM / 32, PB = BN / 32;   // 16-B vectors per thread per k-step
   constexpr int MI = BM / 32, NJ = BN / 32;   // 16x16 tiles per wave (wave tile BM/2 x BN/2)
   constexpr int STAGE = (BM + BN) * 128;      // bytes of one LDS stage (A then B)
@@ -236,11 +237,11 @@ __global__ __launch_bounds__(EW_BLOCK * KG) void k_conv_nt(const uint16_t* __res
   const int lane = threadIdx.x & 63, g = threadIdx.x >> 8, t = threadIdx.x & 255;
   const int wq = t >> 6, wm = wq >> 1, wn = wq & 1;
   const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
-  const int CB = C / CV_BK, ksteps = 9 * CB;
+  const int CB = C / CV_BK, ksteps = taps * CB;  // taps: 9 (3x3) or 1 (1x1)
   const int kbeg = blockIdx.z * kps;
   const int kend = min(kbeg + kps, ksteps);
   const int chunk = t & 7;
-  const long long K = 9LL * C;
+  const long long K = (long long)taps * C;
   char* gsm = smem + g * 2 * STAGE;
 
   // per-thread A rows: pixel index and (h, w) (m = ((b*H)+h)*W + w)
@@ -258,9 +259,9 @@ __global__ __launch_bounds__(EW_BLOCK * KG) void k_conv_nt(const uint16_t* __res
   // forward weight w[k-channel][tap][out col], read transposed by the MFMA loop
   static_assert(!TRB || BN == 64, "transposed B images are 64 columns wide");
   // base of this thread's first B row; rows i are 32*i apart (row stride bstride elements)
-  const uint16_t* wb = TRB ? w + (long long)(t >> 3) * 9 * Nc + n0 + chunk * 8
+  const uint16_t* wb = TRB ? w + (long long)(t >> 3) * taps * Nc + n0 + chunk * 8
                            : w + (long long)(n0 + (t >> 3)) * K + chunk * 8;
-  const long long bstride = TRB ? 32LL * 9 * Nc : 32LL * K;
+  const long long bstride = TRB ? 32LL * taps * Nc : 32LL * K;
 
   // two staging register sets: step s+2KG is loaded while step s computes and step s+KG (loaded
   // one iteration earlier) is written to LDS -- two k-group iterations to cover a global round trip
@@ -269,7 +270,8 @@ __global__ __launch_bounds__(EW_BLOCK * KG) void k_conv_nt(const uint16_t* __res
 #define CV_NT_LOAD(S_, RA_, RB_)                                                                \
   do {                                                                                          \
     const int tap_ = (S_) / CB, cb_ = (S_) - tap_ * CB;                                         \
-    const int dr_ = tap_ / 3 - 1, dc_ = tap_ - (tap_ / 3) * 3 - 1;                              \
+    const int dr_ = taps == 1 ? 0 : tap_ / 3 - 1;                                               \
+    const int dc_ = taps == 1 ? 0 : tap_ - (tap_ / 3) * 3 - 1;                                  \
     {                                                                                           \
       auto& R = RA_;                                                                            \
       CV_FOR_ROWS(PA, {                                                                         \
@@ -280,8 +282,8 @@ __global__ __launch_bounds__(EW_BLOCK * KG) void k_conv_nt(const uint16_t* __res
         v = ok ? x_ : cv_u4{0u, 0u, 0u, 0u};                                                    \
       });                                                                                       \
     }                                                                                           \
-    /* TRB: k-block cb_ of tap tap_ = forward channels cb_*64.. at the flipped tap 8 - tap_ */  \
-    const long long bo_ = TRB ? ((long long)cb_ * CV_BK * 9 + (8 - tap_)) * Nc                   \
+    /* TRB: k-block cb_ of tap tap_ = forward channels cb_*64.. at the flipped tap */           \
+    const long long bo_ = TRB ? ((long long)cb_ * CV_BK * taps + (taps - 1 - tap_)) * Nc          \
                               : (long long)(S_) * CV_BK;                                        \
     {                                                                                           \
       auto& R = RB_;                                                                            \
@@ -372,7 +374,7 @@ __global__ __launch_bounds__(EW_BLOCK * KG) void k_conv_wgrad(const uint16_t* __
                                                               uint16_t* __restrict__ dw,
                                                               float* __restrict__ slab, int M,
                                                               int H, int W, int C, int Nc,
-                                                              int kps) {
+                                                              int kps, int taps) {
   constexpr int BM = 64, BN = 64;
   constexpr int MI = BM / 32, NJ = BN / 32;
   constexpr int STAGE = (BM + BN) * 128;
@@ -382,7 +384,7 @@ __global__ __launch_bounds__(EW_BLOCK * KG) void k_conv_wgrad(const uint16_t* __
   const int n0 = blockIdx.x * BM;     // output rows (dy channels)
   const int k0 = blockIdx.y * BN;     // output columns (tap, channel)
   const int tap = k0 / C, c0 = k0 - tap * C;
-  const int dr = tap / 3 - 1, dc = tap - (tap / 3) * 3 - 1;
+  const int dr = taps == 1 ? 0 : tap / 3 - 1, dc = taps == 1 ? 0 : tap - (tap / 3) * 3 - 1;
   const int msteps = M / CV_BK;
   const int sbeg = blockIdx.z * kps;
   const int send = min(sbeg + kps, msteps);
@@ -473,7 +475,7 @@ __global__ __launch_bounds__(EW_BLOCK * KG) void k_conv_wgrad(const uint16_t* __
 #undef CV_WG_ADVANCE
   cv_group_reduce<KG, MI, NJ>(acc, smem, g, wq, lane);
   if (g != 0) return;
-  const long long K = 9LL * C;
+  const long long K = (long long)taps * C;
   const int row0 = n0 + wm * (BM / 2), col0 = k0 + wn * (BN / 2);
   if (slab)
     cv_store<MI, NJ>(acc, row0, col0, lane, nullptr, slab + (long long)blockIdx.z * Nc * K, K);
@@ -541,17 +543,17 @@ long long ew_conv_ws_floats() { return 8LL << 20; }  // 32 MiB of fp32 split sla
 
 #define CV_LAUNCH_NT(BM_, KG_, TRB_)                                                             \
   hipLaunchKernelGGL((k_conv_nt<BM_, BM_, KG_, TRB_>), grid, dim3(EW_BLOCK * KG_), 0, s, x, w,  \
-                     out, slab, M, H, W, C, Nc, p.kps)
+                     out, slab, M, H, W, C, Nc, p.kps, taps)
 
 // NT GEMM (forward / backward-data): out[M][Nc] = sum X~[M][9C] w[Nc][9C]^T
 // trb: w is the forward weight [C][9][Nc] of a backward-data GEMM (transposed B images, 64x64
 // tiles); otherwise w is [Nc][9][C].
 static void ew_conv_nt(const uint16_t* x, const uint16_t* w, uint16_t* out, float* ws,
-                       long long ws_floats, int M, int H, int W, int C, int Nc, bool trb,
-                       hipStream_t s) {
+                       long long ws_floats, int M, int H, int W, int C, int Nc, int taps,
+                       bool trb, hipStream_t s) {
   if (C % CV_BK || Nc % 64 || M % 64)
     throw std::runtime_error("ewdml conv: needs C % 64 == 0, Nc % 64 == 0, N*H*W % 64 == 0");
-  const int ksteps = 9 * (C / CV_BK);
+  const int ksteps = taps * (C / CV_BK);
   const bool big = !trb && (M % 128 == 0) && (Nc % 128 == 0) &&
                    (long long)(M / 128) * (Nc / 128) >= 256;
   const int BM = big ? 128 : 64;
@@ -582,31 +584,37 @@ static void ew_conv_nt(const uint16_t* x, const uint16_t* w, uint16_t* out, floa
 }
 #undef CV_LAUNCH_NT
 
-void ew_conv3x3_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t ws, long long ws_floats,
-                    long long N, int H, int W, int C, int Nc, uintptr_t stream) {
-  ew_conv_nt(reinterpret_cast<const uint16_t*>(x), reinterpret_cast<const uint16_t*>(w),
-             reinterpret_cast<uint16_t*>(y), reinterpret_cast<float*>(ws), ws_floats,
-             (int)(N * H * W), H, W, C, Nc, false, (hipStream_t)stream);
+static int cv_taps(int ksize) {
+  if (ksize != 1 && ksize != 3) throw std::runtime_error("ewdml conv: kernel size must be 1 or 3");
+  return ksize * ksize;
 }
 
-void ew_conv3x3_bwd_data(uintptr_t dy, uintptr_t w, uintptr_t dx, uintptr_t ws,
-                         long long ws_floats, long long N, int H, int W, int C, int Nc,
-                         uintptr_t stream) {
+void ew_conv_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t ws, long long ws_floats,
+                 long long N, int H, int W, int C, int Nc, int ksize, uintptr_t stream) {
+  ew_conv_nt(reinterpret_cast<const uint16_t*>(x), reinterpret_cast<const uint16_t*>(w),
+             reinterpret_cast<uint16_t*>(y), reinterpret_cast<float*>(ws), ws_floats,
+             (int)(N * H * W), H, W, C, Nc, cv_taps(ksize), false, (hipStream_t)stream);
+}
+
+void ew_conv_bwd_data(uintptr_t dy, uintptr_t w, uintptr_t dx, uintptr_t ws,
+                      long long ws_floats, long long N, int H, int W, int C, int Nc, int ksize,
+                      uintptr_t stream) {
   // the flipped / transposed weight is read in place through transposed B images (no copy)
   if (C % 64 || Nc % 64) throw std::runtime_error("ewdml conv: bwd-data needs C, Nc % 64 == 0");
   // dx[m][c] = sum over (tap', n) of dY~[m][(tap', n)] * w[n][8 - tap'][c]
   ew_conv_nt(reinterpret_cast<const uint16_t*>(dy), reinterpret_cast<const uint16_t*>(w),
              reinterpret_cast<uint16_t*>(dx), reinterpret_cast<float*>(ws), ws_floats,
-             (int)(N * H * W), H, W, Nc, C, true, (hipStream_t)stream);
+             (int)(N * H * W), H, W, Nc, C, cv_taps(ksize), true, (hipStream_t)stream);
 }
 
-void ew_conv3x3_wgrad(uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws, long long ws_floats,
-                      long long N, int H, int W, int C, int Nc, uintptr_t stream) {
+void ew_conv_wgrad(uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws, long long ws_floats,
+                   long long N, int H, int W, int C, int Nc, int ksize, uintptr_t stream) {
+  const int taps = cv_taps(ksize);
   hipStream_t s = (hipStream_t)stream;
   const long long M = N * H * W;
   if (C % 64 || Nc % 64 || M % CV_BK)
     throw std::runtime_error("ewdml conv: wgrad needs C, Nc % 64 == 0");
-  const long long K = 9LL * C;
+  const long long K = (long long)taps * C;
   const long long tiles = (long long)(Nc / 64) * (K / 64);
   const int msteps = (int)(M / CV_BK);
   CvPlan p{1, 1, msteps};
@@ -626,13 +634,13 @@ void ew_conv3x3_wgrad(uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws, lon
   uint16_t* dwp = reinterpret_cast<uint16_t*>(dw);
   if (p.kg == 4)
     hipLaunchKernelGGL(k_conv_wgrad<4>, grid, dim3(EW_BLOCK * 4), 0, s, dyp, xp, dwp, slab,
-                       (int)M, H, W, C, Nc, p.kps);
+                       (int)M, H, W, C, Nc, p.kps, taps);
   else if (p.kg == 2)
     hipLaunchKernelGGL(k_conv_wgrad<2>, grid, dim3(EW_BLOCK * 2), 0, s, dyp, xp, dwp, slab,
-                       (int)M, H, W, C, Nc, p.kps);
+                       (int)M, H, W, C, Nc, p.kps, taps);
   else
     hipLaunchKernelGGL(k_conv_wgrad<1>, grid, dim3(EW_BLOCK), 0, s, dyp, xp, dwp, slab, (int)M,
-                       H, W, C, Nc, p.kps);
+                       H, W, C, Nc, p.kps, taps);
   EW_CHECK_LAUNCH();
   if (p.split > 1) {
     const long long n = (long long)Nc * K;

@@ -136,14 +136,14 @@ struct MakeBatchArgs {
 };
 void ew_make_batch(const MakeBatchArgs& a);
 
-// ---- 3x3 / stride 1 / pad 1 convolution, NHWC bf16, MFMA implicit GEMM (conv.hip) ----
-// x [N,H,W,C], w [Nc,3,3,C] (channels_last weight memory), y/dy [N,H,W,Nc]; ws: fp32 split slabs
-// (ws_floats of them)
+// ---- 3x3 (pad 1) or 1x1 (pad 0) stride-1 convolution, NHWC bf16, MFMA implicit GEMM (conv.hip) ----
+// x [N,H,W,C], w [Nc,k,k,C] (channels_last weight memory), y/dy [N,H,W,Nc]; ws: fp32 split slabs
+// (ws_floats of them); ksize 3 or 1
 long long ew_conv_ws_floats();
-void ew_conv3x3_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t ws, long long ws_floats,
-                    long long N, int H, int W, int C, int Nc, uintptr_t stream);
-void ew_conv3x3_bwd_data(uintptr_t dy, uintptr_t w, uintptr_t dx, uintptr_t ws,
-                         long long ws_floats, long long N, int H, int W, int C, int Nc,
-                         uintptr_t stream);
-void ew_conv3x3_wgrad(uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws, long long ws_floats,
-                      long long N, int H, int W, int C, int Nc, uintptr_t stream);
+void ew_conv_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t ws, long long ws_floats,
+                 long long N, int H, int W, int C, int Nc, int ksize, uintptr_t stream);
+void ew_conv_bwd_data(uintptr_t dy, uintptr_t w, uintptr_t dx, uintptr_t ws,
+                      long long ws_floats, long long N, int H, int W, int C, int Nc, int ksize,
+                      uintptr_t stream);
+void ew_conv_wgrad(uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws, long long ws_floats,
+                   long long N, int H, int W, int C, int Nc, int ksize, uintptr_t stream);

@@ -1,4 +1,4 @@
-"""MFMA implicit-GEMM 3x3 convolution (ops/csrc/conv.hip) against plain PyTorch fp32.
+"""MFMA implicit-GEMM 3x3 / 1x1 convolution (ops/csrc/conv.hip) against plain PyTorch fp32.
 
 Inputs and weights are bf16; the reference is ``F.conv2d`` / its autograd in fp32 on the same
 (bf16-valued) tensors.  The kernels accumulate in fp32 and round the result to bf16 once, so the
@@ -26,10 +26,10 @@ def _rel(a, b):
     return float((a - b).norm() / (b.norm() + 1e-30))
 
 
-def _data(N, C, Nc, H, W, seed=0):
+def _data(N, C, Nc, H, W, seed=0, k=3):
     g = torch.Generator(device="cuda").manual_seed(seed)
     x = torch.randn(N, C, H, W, device="cuda", generator=g).to(torch.bfloat16)
-    w = (torch.randn(Nc, C, 3, 3, device="cuda", generator=g) / (3.0 * C ** 0.5)).to(torch.bfloat16)
+    w = (torch.randn(Nc, C, k, k, device="cuda", generator=g) / (k * C ** 0.5)).to(torch.bfloat16)
     x = x.contiguous(memory_format=torch.channels_last)
     w = w.contiguous(memory_format=torch.channels_last)
     return x, w
@@ -46,15 +46,21 @@ SHAPES = [
     (8, 128, 64, 8, 8),       # C_out = 64
     (8, 64, 128, 8, 5),       # odd width (row pairs cross image rows)
 ]
+SHAPES = [s + (3,) for s in SHAPES] + [
+    (16, 64, 256, 32, 32, 1),     # ResNet bottleneck 1x1 expand
+    (16, 256, 64, 32, 32, 1),     # 1x1 reduce, C_out = 64
+    (32, 512, 2048, 4, 4, 1),     # stage 4 expand (small M: split-K)
+    (8, 128, 128, 8, 6, 1),
+]
 
 
-@pytest.mark.parametrize("N,C,Nc,H,W", SHAPES)
-def test_conv3x3_forward(N, C, Nc, H, W):
+@pytest.mark.parametrize("N,C,Nc,H,W,k", SHAPES)
+def test_conv_forward(N, C, Nc, H, W, k):
     conv = _conv()
-    x, w = _data(N, C, Nc, H, W)
+    x, w = _data(N, C, Nc, H, W, k=k)
     assert conv.supported(x, w)
-    y = conv.conv3x3(x, w)
-    ref = F.conv2d(x.float(), w.float(), padding=1)
+    y = conv.conv(x, w)
+    ref = F.conv2d(x.float(), w.float(), padding=k // 2)
     assert y.dtype == torch.bfloat16 and y.is_contiguous(memory_format=torch.channels_last)
     assert _rel(y, ref) < 6e-3, _rel(y, ref)
     # bf16 rounding of an fp32 result: every element within one bf16 ulp of the reference
@@ -62,17 +68,17 @@ def test_conv3x3_forward(N, C, Nc, H, W):
     assert bool((err <= ref.abs() * 2 ** -7 + 1e-3).all()), float(err.max())
 
 
-@pytest.mark.parametrize("N,C,Nc,H,W", SHAPES)
-def test_conv3x3_backward(N, C, Nc, H, W):
+@pytest.mark.parametrize("N,C,Nc,H,W,k", SHAPES)
+def test_conv_backward(N, C, Nc, H, W, k):
     conv = _conv()
-    x, w = _data(N, C, Nc, H, W, seed=1)
+    x, w = _data(N, C, Nc, H, W, seed=1, k=k)
     g = torch.Generator(device="cuda").manual_seed(7)
     dy = torch.randn(N, Nc, H, W, device="cuda", generator=g).to(torch.bfloat16).contiguous(
         memory_format=torch.channels_last)
     xa, wa = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
-    conv.conv3x3(xa, wa).backward(dy)
+    conv.conv(xa, wa).backward(dy)
     xr, wr = x.float().requires_grad_(True), w.float().requires_grad_(True)
-    F.conv2d(xr, wr, padding=1).backward(dy.float())
+    F.conv2d(xr, wr, padding=k // 2).backward(dy.float())
     assert xa.grad.dtype == torch.bfloat16 and wa.grad.dtype == torch.bfloat16
     assert _rel(xa.grad, xr.grad) < 6e-3, _rel(xa.grad, xr.grad)
     assert _rel(wa.grad, wr.grad) < 6e-3, _rel(wa.grad, wr.grad)
@@ -111,6 +117,37 @@ def test_vgg11_mfma_conv_matches_miopen_step():
     mref, m1 = copy.deepcopy(m0), copy.deepcopy(m0)
     x = torch.randn(64, 3, 32, 32, device="cuda").contiguous(memory_format=torch.channels_last)
     y = torch.randint(0, 10, (64,), device="cuda")
+    outs = []
+    for m, on, bf in ((mref, False, False), (m0, True, True), (m1, False, True)):
+        conv.set_enabled(on)
+        if bf:
+            for p in m.parameters():
+                p.data = p.data.to(torch.bfloat16).contiguous(
+                    memory_format=torch.channels_last if p.dim() == 4 else torch.contiguous_format)
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=bf):
+            out = m(x.to(torch.bfloat16) if bf else x)
+        F.cross_entropy(out.float(), y).backward()
+        outs.append((out.float(), [p.grad.float() for p in m.parameters()]))
+    conv.set_enabled(True)
+    (o_ref, g_ref), (o_hip, g_hip), (o_mio, g_mio) = outs
+    assert _rel(o_hip, o_ref) <= 1.5 * _rel(o_mio, o_ref) + 1e-3
+    e_hip = sum(_rel(a, b) for a, b in zip(g_hip, g_ref)) / len(g_ref)
+    e_mio = sum(_rel(a, b) for a, b in zip(g_mio, g_ref)) / len(g_ref)
+    assert e_hip <= 1.5 * e_mio + 1e-3, (e_hip, e_mio)
+
+
+def test_resnet50_mfma_conv_matches_miopen_step():
+    """ResNet-50 (CIFAR) bf16 step through the MFMA 3x3/1x1 convs vs MIOpen, both against fp32."""
+    import copy
+
+    from ewdml.models import build_model
+
+    conv = _conv()
+    torch.manual_seed(0)
+    m0 = build_model("resnet50", 10).cuda().to(memory_format=torch.channels_last)
+    mref, m1 = copy.deepcopy(m0), copy.deepcopy(m0)
+    x = torch.randn(32, 3, 32, 32, device="cuda").contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (32,), device="cuda")
     outs = []
     for m, on, bf in ((mref, False, False), (m0, True, True), (m1, False, True)):
         conv.set_enabled(on)

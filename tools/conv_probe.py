@@ -50,12 +50,12 @@ def hip_times(x, w, dy):
     dx = torch.empty_like(x)
     dw = torch.empty_like(w)
     st = ops._stream
-    tf = timeit(lambda: C_.conv3x3_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), ws.data_ptr(),
-                                       ws.numel(), N, H, W, C, Nc, st()))
-    tb = timeit(lambda: C_.conv3x3_bwd_data(dy.data_ptr(), w.data_ptr(), dx.data_ptr(),
-                                            ws.data_ptr(), ws.numel(), N, H, W, C, Nc, st()))
-    tw = timeit(lambda: C_.conv3x3_wgrad(dy.data_ptr(), x.data_ptr(), dw.data_ptr(),
-                                         ws.data_ptr(), ws.numel(), N, H, W, C, Nc, st()))
+    tf = timeit(lambda: C_.conv_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), ws.data_ptr(),
+                                       ws.numel(), N, H, W, C, Nc, 3, st()))
+    tb = timeit(lambda: C_.conv_bwd_data(dy.data_ptr(), w.data_ptr(), dx.data_ptr(),
+                                            ws.data_ptr(), ws.numel(), N, H, W, C, Nc, 3, st()))
+    tw = timeit(lambda: C_.conv_wgrad(dy.data_ptr(), x.data_ptr(), dw.data_ptr(),
+                                         ws.data_ptr(), ws.numel(), N, H, W, C, Nc, 3, st()))
     return tf, tb, tw
 
 
