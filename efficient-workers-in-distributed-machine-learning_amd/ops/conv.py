@@ -79,9 +79,14 @@ class _Conv(torch.autograd.Function):
         ws = _ws(x.device)
         y = torch.empty((N, Nc, H, W), dtype=x.dtype, device=x.device,
                         memory_format=torch.channels_last)
-        C_.conv_fwd(_ptr(x), _ptr(w), _ptr(y), _ptr(ws), ws.numel(), N, H, W, C, Nc, k,
-                    _stream())
+        # BatchNorm partial sums of y from the epilogue (bounded by 2 rows per 64 output rows);
+        # the following fused BN (ops/nn.py bn_act) skips its statistics pass when present
+        part = torch.empty(max(1, 4 * (N * H * W // 64) * Nc), dtype=torch.float32,
+                           device=x.device)
+        rows = C_.conv_fwd(_ptr(x), _ptr(w), _ptr(y), _ptr(ws), ws.numel(), N, H, W, C, Nc, k,
+                           _ptr(part), part.numel(), _stream())
         ctx.save_for_backward(x, w)
+        ctx.bn_part = (part, rows) if rows > 0 else None
         return y
 
     @staticmethod
@@ -106,11 +111,21 @@ class _Conv(torch.autograd.Function):
         return dx, dw
 
 
+def _apply(x, w):
+    y = _Conv.apply(x, w)
+    # hand the epilogue's BatchNorm partials to the consumer (bn_act reads ``_ew_bn_part``)
+    node = y.grad_fn  # the autograd ctx of _Conv (None under no_grad)
+    part = getattr(node, "bn_part", None) if node is not None else None
+    if part is not None:
+        y._ew_bn_part = part
+    return y
+
+
 def conv(x, w):
     """``F.conv2d(x, w, padding=k // 2)`` (k = 3 or 1) through the MFMA kernels when
     :func:`supported`."""
     if supported(x, w):
-        return _Conv.apply(x, w)
+        return _apply(x, w)
     return F.conv2d(x, w, padding=w.shape[-1] // 2)
 
 
@@ -122,5 +137,5 @@ def conv2d_module(m, x):
     is a stride-1 3x3/pad-1 or 1x1/pad-0 convolution on channels_last bf16 (else ``m(x)``)."""
     if (m.bias is None and m.padding_mode == "zeros"
             and supported(x, m.weight, m.stride, m.padding, m.dilation, m.groups)):
-        return _Conv.apply(x, m.weight)
+        return _apply(x, m.weight)
     return m(x)

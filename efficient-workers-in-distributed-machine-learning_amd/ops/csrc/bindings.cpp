@@ -217,8 +217,9 @@ PYBIND11_MODULE(_C, m) {
            uintptr_t part, uintptr_t gamma, uintptr_t beta, uintptr_t cbias, uintptr_t rmean,
            uintptr_t rvar, uintptr_t nbt, long long N, int H, int W, int C, int is_bf16,
            int pool, int mode, int training, float momentum, float eps, int cb_bf16,
-           uintptr_t stream) {
+           uintptr_t stream, int pre_nblk) {
           BnFwdArgs a{};
+          a.pre_nblk = pre_nblk;
           a.h = h; a.res = res; a.y = y; a.code = code; a.stats = stats; a.part = part;
           a.gamma = gamma; a.beta = beta; a.cbias = cbias; a.rmean = rmean; a.rvar = rvar;
           a.nbt = nbt; a.N = N; a.H = H; a.W = W; a.C = C;

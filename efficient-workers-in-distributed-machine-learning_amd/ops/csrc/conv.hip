@@ -229,7 +229,7 @@ __global__ __launch_bounds__(EW_BLOCK * KG) void k_conv_nt(const uint16_t* __res
                                                            uint16_t* __restrict__ out,
                                                            float* __restrict__ slab, int M, int H,
                                                            int W, int C, int Nc, int kps,
-                                                           int taps) {
+                                                           int taps, float* __restrict__ bnpart) {
   constexpr int PA = BM / 32, PB = BN / 32;   // 16-B vectors per thread per k-step
   constexpr int MI = BM / 32, NJ = BN / 32;   // 16x16 tiles per wave (wave tile BM/2 x BN/2)
   constexpr int STAGE = (BM + BN) * 128;      // bytes of one LDS stage (A then B)
@@ -347,12 +347,55 @@ __global__ __launch_bounds__(EW_BLOCK * KG) void k_conv_nt(const uint16_t* __res
   }
 #undef CV_NT_MMA
   cv_group_reduce<KG, MI, NJ>(acc, smem, g, wq, lane);
-  if (g != 0) return;
   const int row0 = m0 + wm * (BM / 2), col0 = n0 + wn * (BN / 2);
-  if (slab)
-    cv_store<MI, NJ>(acc, row0, col0, lane, nullptr, slab + (long long)blockIdx.z * M * Nc, Nc);
-  else
-    cv_store<MI, NJ>(acc, row0, col0, lane, out, nullptr, Nc);
+  if (slab) {
+    if (g == 0)
+      cv_store<MI, NJ>(acc, row0, col0, lane, nullptr, slab + (long long)blockIdx.z * M * Nc, Nc);
+    return;
+  }
+  if (g == 0) cv_store<MI, NJ>(acc, row0, col0, lane, out, nullptr, Nc);
+  if (bnpart) {  // every group keeps the barrier count; only group 0's values are used
+    // BatchNorm statistics of the stored (bf16-rounded) output, fused into the epilogue: per
+    // column, sum and sum of squares over the block's BM rows -> partial row blockIdx.x of
+    // bnpart[2][M/BM][Nc] (the BN finalize kernel's layout).  The two waves sharing columns
+    // (wm = 0, 1) combine through LDS.
+    float* red = reinterpret_cast<float*>(smem);  // [wn][2][BN/2]
+    const long long nrows = M / BM;
+    float sm[NJ], sq[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      sm[j] = sq[j] = 0.0f;
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float v = __uint_as_float((uint32_t)ew_f2bf(acc[i][j][q]) << 16);
+          sm[j] += v;
+          sq[j] += v * v;
+        }
+      sm[j] += __shfl_xor(sm[j], 16, 64);
+      sq[j] += __shfl_xor(sq[j], 16, 64);
+      sm[j] += __shfl_xor(sm[j], 32, 64);
+      sq[j] += __shfl_xor(sq[j], 32, 64);
+    }
+    __syncthreads();  // group reduce / main loop finished reading smem
+    if (g == 0 && wm == 1 && lane < 16) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        red[(wn * 2 + 0) * (BN / 2) + j * 16 + lane] = sm[j];
+        red[(wn * 2 + 1) * (BN / 2) + j * 16 + lane] = sq[j];
+      }
+    }
+    __syncthreads();
+    if (g == 0 && wm == 0 && lane < 16) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int c = col0 + j * 16 + lane;
+        bnpart[(long long)blockIdx.x * Nc + c] = sm[j] + red[(wn * 2 + 0) * (BN / 2) + j * 16 + lane];
+        bnpart[(nrows + blockIdx.x) * Nc + c] = sq[j] + red[(wn * 2 + 1) * (BN / 2) + j * 16 + lane];
+      }
+    }
+  }
 #undef CV_NT_LOAD
 #undef CV_NT_STORE
 }
@@ -543,14 +586,17 @@ long long ew_conv_ws_floats() { return 8LL << 20; }  // 32 MiB of fp32 split sla
 
 #define CV_LAUNCH_NT(BM_, KG_, TRB_)                                                             \
   hipLaunchKernelGGL((k_conv_nt<BM_, BM_, KG_, TRB_>), grid, dim3(EW_BLOCK * KG_), 0, s, x, w,  \
-                     out, slab, M, H, W, C, Nc, p.kps, taps)
+                     out, slab, M, H, W, C, Nc, p.kps, taps, bnp)
 
 // NT GEMM (forward / backward-data): out[M][Nc] = sum X~[M][9C] w[Nc][9C]^T
 // trb: w is the forward weight [C][9][Nc] of a backward-data GEMM (transposed B images, 64x64
 // tiles); otherwise w is [Nc][9][C].
-static void ew_conv_nt(const uint16_t* x, const uint16_t* w, uint16_t* out, float* ws,
-                       long long ws_floats, int M, int H, int W, int C, int Nc, int taps,
-                       bool trb, hipStream_t s) {
+// bnpart (nullable, bnpart_floats capacity): BatchNorm partial sums of the output written by the
+// epilogue when the launch has no split; returns the number of partial rows (0: not written).
+static int ew_conv_nt(const uint16_t* x, const uint16_t* w, uint16_t* out, float* ws,
+                      long long ws_floats, int M, int H, int W, int C, int Nc, int taps,
+                      bool trb, hipStream_t s, float* bnpart = nullptr,
+                      long long bnpart_floats = 0) {
   if (C % CV_BK || Nc % 64 || M % 64)
     throw std::runtime_error("ewdml conv: needs C % 64 == 0, Nc % 64 == 0, N*H*W % 64 == 0");
   const int ksteps = taps * (C / CV_BK);
@@ -561,6 +607,11 @@ static void ew_conv_nt(const uint16_t* x, const uint16_t* w, uint16_t* out, floa
   const CvPlan p = cv_plan(tiles, ksteps, big ? 2 : 4, (long long)M * Nc, ws_floats);
   dim3 grid(M / BM, Nc / BM, p.split);
   float* slab = p.split > 1 ? ws : nullptr;
+  // epilogue BN partials: one row per M-tile; beyond 1024 rows the BN statistics pass (<= 1024
+  // partial rows) leaves the finalize less to reduce
+  const long long prow = M / BM;
+  float* bnp = (bnpart && !slab && prow <= 1024 && 2 * prow * Nc <= bnpart_floats) ? bnpart
+                                                                                  : nullptr;
   if (big) {
     if (p.kg == 2) CV_LAUNCH_NT(128, 2, false);
     else CV_LAUNCH_NT(128, 1, false);
@@ -581,6 +632,7 @@ static void ew_conv_nt(const uint16_t* x, const uint16_t* w, uint16_t* out, floa
     hipLaunchKernelGGL(k_cv_slab_reduce, dim3((int)gr), dim3(EW_BLOCK), 0, s, ws, p.split, n, out);
     EW_CHECK_LAUNCH();
   }
+  return bnp ? (int)prow : 0;
 }
 #undef CV_LAUNCH_NT
 
@@ -589,11 +641,13 @@ static int cv_taps(int ksize) {
   return ksize * ksize;
 }
 
-void ew_conv_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t ws, long long ws_floats,
-                 long long N, int H, int W, int C, int Nc, int ksize, uintptr_t stream) {
-  ew_conv_nt(reinterpret_cast<const uint16_t*>(x), reinterpret_cast<const uint16_t*>(w),
-             reinterpret_cast<uint16_t*>(y), reinterpret_cast<float*>(ws), ws_floats,
-             (int)(N * H * W), H, W, C, Nc, cv_taps(ksize), false, (hipStream_t)stream);
+int ew_conv_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t ws, long long ws_floats,
+                long long N, int H, int W, int C, int Nc, int ksize, uintptr_t bnpart,
+                long long bnpart_floats, uintptr_t stream) {
+  return ew_conv_nt(reinterpret_cast<const uint16_t*>(x), reinterpret_cast<const uint16_t*>(w),
+                    reinterpret_cast<uint16_t*>(y), reinterpret_cast<float*>(ws), ws_floats,
+                    (int)(N * H * W), H, W, C, Nc, cv_taps(ksize), false, (hipStream_t)stream,
+                    reinterpret_cast<float*>(bnpart), bnpart_floats);
 }
 
 void ew_conv_bwd_data(uintptr_t dy, uintptr_t w, uintptr_t dx, uintptr_t ws,

@@ -100,6 +100,7 @@ struct BnFwdArgs {
   int is_bf16, pool, training, cb_bf16, mode;
   float momentum, eps;  // momentum < 0: cumulative average over *nbt batches
   uintptr_t stream;
+  int pre_nblk;  // > 0: `part` already holds [2][pre_nblk][C] partial sums (skip the stats pass)
 };
 struct BnBwdArgs {
   uintptr_t h, res, dy, code, stats, coef, part, dx, dres;  // coef fp32 [2][C]
@@ -140,8 +141,11 @@ void ew_make_batch(const MakeBatchArgs& a);
 // x [N,H,W,C], w [Nc,k,k,C] (channels_last weight memory), y/dy [N,H,W,Nc]; ws: fp32 split slabs
 // (ws_floats of them); ksize 3 or 1
 long long ew_conv_ws_floats();
-void ew_conv_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t ws, long long ws_floats,
-                 long long N, int H, int W, int C, int Nc, int ksize, uintptr_t stream);
+// bnpart (nullable): fp32 [2][rows][Nc] BatchNorm partial sums (sum, sum of squares) of y for the
+// BN that follows; returns rows (0 when not written: split-K launch or capacity too small)
+int ew_conv_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t ws, long long ws_floats,
+                long long N, int H, int W, int C, int Nc, int ksize, uintptr_t bnpart,
+                long long bnpart_floats, uintptr_t stream);
 void ew_conv_bwd_data(uintptr_t dy, uintptr_t w, uintptr_t dx, uintptr_t ws,
                       long long ws_floats, long long N, int H, int W, int C, int Nc, int ksize,
                       uintptr_t stream);

@@ -704,7 +704,9 @@ void ew_bn_relu_fwd(const BnFwdArgs& a) {
     int nblk, rpb;
     ew_bn_grid(M, C, &nblk, &rpb, 4);
     float* part = reinterpret_cast<float*>(a.part);
-    if (a.is_bf16)
+    if (a.pre_nblk > 0)  // statistics computed by the producing conv's epilogue
+      nblk = a.pre_nblk;
+    else if (a.is_bf16)
       hipLaunchKernelGGL(k_bn_fwd_stats<uint16_t>, dim3(nblk), dim3(EW_BLOCK), 0, s,
                          reinterpret_cast<const uint16_t*>(a.h), M, C, rpb, part);
     else

@@ -65,7 +65,8 @@ _MODES = {"relu": 0, "none": 2, "add_relu": 3}
 
 class _BNAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, h, res, cbias, gamma, beta, rmean, rvar, nbt, momentum, eps, pool, mode):
+    def forward(ctx, h, res, cbias, gamma, beta, rmean, rvar, nbt, momentum, eps, pool, mode,
+                pre=None):
         C_ = require()
         N, C, H, W = h.shape
         dev = h.device
@@ -76,11 +77,13 @@ class _BNAct(torch.autograd.Function):
         stats = torch.empty(4 * C, dtype=torch.float32, device=dev)
         g32, b32 = _f32(gamma), _f32(beta)
         cb, cb_bf16 = _bias(cbias)
-        C_.bn_relu_fwd(_ptr(h), _ptr(res), _ptr(y), _ptr(code), _ptr(stats), _ptr(_part(dev)),
+        # pre: (partials, rows) of the batch statistics from the producing MFMA conv's epilogue
+        part, pre_rows = (pre[0], pre[1]) if pre is not None else (_part(dev), 0)
+        C_.bn_relu_fwd(_ptr(h), _ptr(res), _ptr(y), _ptr(code), _ptr(stats), _ptr(part),
                        _ptr(g32), _ptr(b32), _ptr(cb), _ptr(rmean), _ptr(rvar), _ptr(nbt), N, H,
                        W, C, int(h.dtype == torch.bfloat16), int(pool), _MODES[mode], 1,
                        -1.0 if momentum is None else float(momentum), float(eps), cb_bf16,
-                       _stream())
+                       _stream(), int(pre_rows))
         ctx.pool, ctx.mode = pool, mode
         ctx.cb_dtype = None if cb is None else cb.dtype
         ctx.save_for_backward(h, res, code, stats)
@@ -107,7 +110,7 @@ class _BNAct(torch.autograd.Function):
                        _ptr(_part(dev)), _ptr(dx), _ptr(dres), _ptr(dg), _ptr(db), _ptr(dcb), N,
                        H, W, C, int(h.dtype == torch.bfloat16), int(ctx.pool),
                        _MODES[ctx.mode], int(ctx.cb_dtype == torch.bfloat16), _stream())
-        return dx, dres, dcb, dg, db, None, None, None, None, None, None, None
+        return dx, dres, dcb, dg, db, None, None, None, None, None, None, None, None
 
 
 def _apply_eval(h, stats, pool, mode="relu", res=None):
@@ -121,7 +124,7 @@ def _apply_eval(h, stats, pool, mode="relu", res=None):
     code = torch.empty((N,) + out_hw + (C,), dtype=torch.uint8, device=dev) if pool else None
     C_.bn_relu_fwd(_ptr(h), _ptr(res), _ptr(y), _ptr(code), _ptr(stats), 0, 0, 0, 0, 0, 0, 0, N,
                    H, W, C, int(h.dtype == torch.bfloat16), int(pool), _MODES[mode], 0, 0.0, 0.0,
-                   0, _stream())
+                   0, _stream(), 0)
     return y
 
 
@@ -164,7 +167,7 @@ def bn_act(h, bn, mode="relu", res=None, cbias=None, pool=False):
         return _BNAct.apply(h, res, cbias, bn.weight, bn.bias,
                             bn.running_mean if track else None,
                             bn.running_var if track else None, nbt, bn.momentum, bn.eps, pool,
-                            mode)
+                            mode, getattr(h, "_ew_bn_part", None))
     if torch.is_grad_enabled() and (h.requires_grad or (res is not None and res.requires_grad)
                                     or (bn.weight is not None and bn.weight.requires_grad)):
         return bn_act_reference(h, cbias, bn, pool, mode, res)

@@ -165,3 +165,28 @@ def test_resnet50_mfma_conv_matches_miopen_step():
     e_hip = sum(_rel(a, b) for a, b in zip(g_hip, g_ref)) / len(g_ref)
     e_mio = sum(_rel(a, b) for a, b in zip(g_mio, g_ref)) / len(g_ref)
     assert e_hip <= 1.5 * e_mio + 1e-3, (e_hip, e_mio)
+
+
+@pytest.mark.parametrize("N,C,Nc,H,W,k", [(128, 64, 128, 16, 16, 3), (16, 128, 256, 8, 8, 3),
+                                          (128, 512, 512, 2, 2, 3), (16, 64, 256, 32, 32, 1)])
+def test_conv_epilogue_bn_statistics(N, C, Nc, H, W, k):
+    """The forward epilogue's BatchNorm partial sums (consumed by the fused BN, which then skips
+    its statistics pass) give the same normalisation and running statistics as the BN kernels'
+    own statistics pass over the stored output."""
+    import copy
+
+    from ewdml.ops import nn as fnn
+
+    conv = _conv()
+    x, w = _data(N, C, Nc, H, W, seed=5, k=k)
+    bn0 = torch.nn.BatchNorm2d(Nc).cuda()
+    bn1 = copy.deepcopy(bn0)
+    h = conv.conv(x, w.clone().requires_grad_(True))
+    assert not (N * H * W == 512 and hasattr(h, "_ew_bn_part"))  # split-K launch: no partials
+    y0 = fnn.bn_act(h, bn0, "relu")
+    h2 = h.detach().clone()  # same values, no partials attached
+    y1 = fnn.bn_act(h2, bn1, "relu")
+    assert _rel(y0, y1) < 1e-3
+    assert torch.allclose(bn0.running_mean, bn1.running_mean, rtol=1e-4, atol=1e-6)
+    assert torch.allclose(bn0.running_var, bn1.running_var, rtol=1e-4, atol=1e-6)
+    assert int(bn0.num_batches_tracked) == int(bn1.num_batches_tracked) == 1
