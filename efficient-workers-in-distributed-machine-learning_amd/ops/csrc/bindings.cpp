@@ -239,6 +239,8 @@ PYBIND11_MODULE(_C, m) {
           a.pool = pool; a.mode = mode; a.cb_bf16 = cb_bf16; a.stream = stream;
           ew_bn_relu_bwd(a);
         });
+  m.def("cross_entropy_fwd", &ew_cross_entropy_fwd);
+  m.def("cross_entropy_bwd", &ew_cross_entropy_bwd);
   m.def("conv_ws_floats", &ew_conv_ws_floats);
   m.def("conv_fwd", &ew_conv_fwd);
   m.def("conv_bwd_data", &ew_conv_bwd_data);

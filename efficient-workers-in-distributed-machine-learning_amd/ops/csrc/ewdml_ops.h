@@ -151,3 +151,9 @@ void ew_conv_bwd_data(uintptr_t dy, uintptr_t w, uintptr_t dx, uintptr_t ws,
                       uintptr_t stream);
 void ew_conv_wgrad(uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws, long long ws_floats,
                    long long N, int H, int W, int C, int Nc, int ksize, uintptr_t stream);
+
+// ---- cross-entropy loss (nn.hip): mean over B rows of [B, K] logits (bf16 or fp32), int64 labels
+void ew_cross_entropy_fwd(uintptr_t x, uintptr_t y, int B, int K, int is_bf16, uintptr_t loss,
+                          uintptr_t lse, uintptr_t stream);
+void ew_cross_entropy_bwd(uintptr_t x, uintptr_t y, uintptr_t lse, uintptr_t grad, int B, int K,
+                          int is_bf16, uintptr_t dx, uintptr_t stream);

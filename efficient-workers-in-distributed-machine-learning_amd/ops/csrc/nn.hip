@@ -824,3 +824,109 @@ void ew_maxpool2_nhwc(uintptr_t x, uintptr_t y, uintptr_t code, long long N, int
   }
   EW_CHECK_LAUNCH();
 }
+
+// ================================================================================================
+// Cross-entropy loss (mean over the batch) of [B, K] logits (bf16 or fp32) and int64 labels, as
+// F.cross_entropy(logits.float(), y): forward = one block (one wave per row, fixed-order
+// reductions: deterministic), writing the loss and each row's log-sum-exp; backward = one
+// elementwise pass writing dlogits = (softmax - onehot) * grad / B in the logits' dtype.
+// Replaces PyTorch's cast + log_softmax + nll_loss forward and the fill / nll / log_softmax
+// backward / cast chain (9 launches per step).
+// ================================================================================================
+namespace {
+
+template <typename T>
+__device__ __forceinline__ float ew_ldf(const T* p, long long i);
+template <>
+__device__ __forceinline__ float ew_ldf<uint16_t>(const uint16_t* p, long long i) { return ew_bf16f(p[i]); }
+template <>
+__device__ __forceinline__ float ew_ldf<float>(const float* p, long long i) { return p[i]; }
+
+template <typename T>
+__global__ __launch_bounds__(1024) void k_ce_fwd(const T* __restrict__ x,
+                                                 const long long* __restrict__ y, int B, int K,
+                                                 float* __restrict__ loss,
+                                                 float* __restrict__ lse) {
+  __shared__ float lrow[16];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  float acc = 0.0f;  // this wave's sum of row losses (lane 0)
+  for (int r = wv; r < B; r += 16) {
+    const T* xr = x + (long long)r * K;
+    float m = -INFINITY;
+    for (int k = lane; k < K; k += 64) m = fmaxf(m, ew_ldf(xr, k));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    float s = 0.0f;
+    for (int k = lane; k < K; k += 64) s += expf(ew_ldf(xr, k) - m);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    const float l = m + logf(s);
+    if (lane == 0) {
+      lse[r] = l;
+      const long long t = y[r];
+      acc += l - ((t >= 0 && t < K) ? ew_ldf(xr, t) : 0.0f);
+    }
+  }
+  if (lane == 0) lrow[wv] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float tot = 0.0f;
+    for (int i = 0; i < 16; ++i) tot += lrow[i];
+    *loss = tot / (float)B;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(EW_BLOCK) void k_ce_bwd(const T* __restrict__ x,
+                                                     const long long* __restrict__ y,
+                                                     const float* __restrict__ lse,
+                                                     const float* __restrict__ grad, int B, int K,
+                                                     T* __restrict__ dx) {
+  const float g = *grad / (float)B;
+  const long long n = (long long)B * K;
+  for (long long i = blockIdx.x * (long long)EW_BLOCK + threadIdx.x; i < n;
+       i += (long long)gridDim.x * EW_BLOCK) {
+    const int r = (int)(i / K), k = (int)(i - (long long)r * K);
+    float v = expf(ew_ldf(x, i) - lse[r]);
+    if ((long long)k == y[r]) v -= 1.0f;
+    v *= g;
+    if constexpr (sizeof(T) == 2) dx[i] = ew_f2bf(v);
+    else dx[i] = v;
+  }
+}
+
+}  // namespace
+
+void ew_cross_entropy_fwd(uintptr_t x, uintptr_t y, int B, int K, int is_bf16, uintptr_t loss,
+                          uintptr_t lse, uintptr_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (is_bf16)
+    hipLaunchKernelGGL(k_ce_fwd<uint16_t>, dim3(1), dim3(1024), 0, s,
+                       reinterpret_cast<const uint16_t*>(x), reinterpret_cast<const long long*>(y),
+                       B, K, reinterpret_cast<float*>(loss), reinterpret_cast<float*>(lse));
+  else
+    hipLaunchKernelGGL(k_ce_fwd<float>, dim3(1), dim3(1024), 0, s,
+                       reinterpret_cast<const float*>(x), reinterpret_cast<const long long*>(y), B,
+                       K, reinterpret_cast<float*>(loss), reinterpret_cast<float*>(lse));
+  EW_CHECK_LAUNCH();
+}
+
+void ew_cross_entropy_bwd(uintptr_t x, uintptr_t y, uintptr_t lse, uintptr_t grad, int B, int K,
+                          int is_bf16, uintptr_t dx, uintptr_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const long long n = (long long)B * K;
+  long long g = (n + EW_BLOCK - 1) / EW_BLOCK;
+  if (g > 1024) g = 1024;
+  if (g < 1) g = 1;
+  if (is_bf16)
+    hipLaunchKernelGGL(k_ce_bwd<uint16_t>, dim3((int)g), dim3(EW_BLOCK), 0, s,
+                       reinterpret_cast<const uint16_t*>(x), reinterpret_cast<const long long*>(y),
+                       reinterpret_cast<const float*>(lse), reinterpret_cast<const float*>(grad), B,
+                       K, reinterpret_cast<uint16_t*>(dx));
+  else
+    hipLaunchKernelGGL(k_ce_bwd<float>, dim3((int)g), dim3(EW_BLOCK), 0, s,
+                       reinterpret_cast<const float*>(x), reinterpret_cast<const long long*>(y),
+                       reinterpret_cast<const float*>(lse), reinterpret_cast<const float*>(grad), B,
+                       K, reinterpret_cast<float*>(dx));
+  EW_CHECK_LAUNCH();
+}

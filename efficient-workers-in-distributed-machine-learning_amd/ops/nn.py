@@ -246,3 +246,41 @@ def maxpool2x2(x):
     if not ok:
         return F.max_pool2d(x, 2, 2)
     return _MaxPool2.apply(x)
+
+
+class _CrossEntropy(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, y):
+        C_ = require()
+        B, K = logits.shape
+        loss = torch.empty((), dtype=torch.float32, device=logits.device)
+        lse = torch.empty(B, dtype=torch.float32, device=logits.device)
+        C_.cross_entropy_fwd(_ptr(logits), _ptr(y), B, K, int(logits.dtype == torch.bfloat16),
+                             _ptr(loss), _ptr(lse), _stream())
+        ctx.save_for_backward(logits, y, lse)
+        return loss
+
+    @staticmethod
+    def backward(ctx, grad):
+        C_ = require()
+        logits, y, lse = ctx.saved_tensors
+        B, K = logits.shape
+        g = grad.detach().float().contiguous()
+        dx = torch.empty_like(logits)
+        C_.cross_entropy_bwd(_ptr(logits), _ptr(y), _ptr(lse), _ptr(g), B, K,
+                             int(logits.dtype == torch.bfloat16), _ptr(dx), _stream())
+        return dx, None
+
+
+def cross_entropy(logits, y):
+    """``F.cross_entropy(logits.float(), y)`` (mean reduction): one HIP kernel forward (loss and
+    per-row log-sum-exp), one backward (dlogits in the logits' dtype) for 2-D device bf16/fp32
+    logits; the torch composition otherwise."""
+    import torch.nn.functional as F
+
+    if (logits.is_cuda and logits.dim() == 2 and logits.dtype in (torch.bfloat16, torch.float32)
+            and logits.is_contiguous() and y.dtype == torch.int64 and y.dim() == 1
+            and y.is_contiguous() and y.shape[0] == logits.shape[0] and 0 < logits.shape[0]
+            and logits.numel() < 2 ** 31):
+        return _CrossEntropy.apply(logits, y)
+    return F.cross_entropy(logits.float(), y)

@@ -182,7 +182,12 @@ class Trainer:
         self.exchange.begin()
         with self._range("forward"), self.autocast():
             out = self.model(x)
-        loss = F.cross_entropy(out.float(), y)
+        if self.cuda and self.cfg.fused_nn == "on":
+            from ..ops.nn import cross_entropy  # one HIP kernel per direction
+
+            loss = cross_entropy(out, y)
+        else:
+            loss = F.cross_entropy(out.float(), y)
         with self._range("backward+encode"):
             loss.backward()
         return loss, out

@@ -272,3 +272,22 @@ def test_resnet18_fused_matches_modules_fp32():
         assert _rel(g_f[n], g_m[n]) < 1e-2, n
     for (n, b1), (_, b2) in zip(m_f.named_buffers(), m_m.named_buffers()):
         assert torch.allclose(b1.float(), b2.float(), rtol=1e-4, atol=1e-5), n
+
+
+@pytest.mark.parametrize("B,K,dtype", [(128, 10, torch.bfloat16), (64, 1000, torch.bfloat16),
+                                       (7, 10, torch.float32), (300, 37, torch.float32)])
+def test_cross_entropy_matches_torch(B, K, dtype):
+    fnn = _ops()
+    g = torch.Generator(device="cuda").manual_seed(B + K)
+    logits = (3 * torch.randn(B, K, device="cuda", generator=g)).to(dtype)
+    y = torch.randint(0, K, (B,), device="cuda", generator=g)
+    a = logits.clone().requires_grad_(True)
+    loss = fnn.cross_entropy(a, y)
+    (2.5 * loss).backward()
+    r = logits.clone().float().requires_grad_(True)
+    ref = F.cross_entropy(r, y)
+    (2.5 * ref).backward()
+    assert abs(float(loss) - float(ref)) <= 1e-5 * max(1.0, abs(float(ref)))
+    assert a.grad.dtype == dtype
+    tol = 1e-2 if dtype == torch.bfloat16 else 1e-5
+    assert _rel(a.grad, r.grad) < tol, _rel(a.grad, r.grad)
