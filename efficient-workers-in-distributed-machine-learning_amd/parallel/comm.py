@@ -57,12 +57,16 @@ class Comm:
 
     # -- collectives (return a Work handle or None when already complete) --------------------
     def all_gather(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = False):
-        """``out`` [world * n] <- concat of every rank's ``inp`` [n]."""
+        """``out`` [world * n] <- concat of every rank's ``inp`` [n] (``inp`` may be this rank's
+        slot of ``out``: in-place)."""
         if self._local:
-            out[:inp.numel()].copy_(inp)
+            if inp.data_ptr() != out.data_ptr():
+                out[:inp.numel()].copy_(inp)
             return None
         if self._gloo_ag:
             chunks = list(out.view(self.world, -1).unbind(0))
+            if inp.data_ptr() == chunks[self.rank].data_ptr():
+                inp = inp.clone()  # gloo copies its input into the output slot: no aliasing
             return dist.all_gather(chunks, inp, group=self.group, async_op=async_op)
         return dist.all_gather_into_tensor(out, inp, group=self.group, async_op=async_op)
 

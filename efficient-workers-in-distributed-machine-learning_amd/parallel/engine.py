@@ -58,8 +58,12 @@ class GradientExchange:
                     b.length, dtype=codec.wire_dtype, device=self.device))
             else:
                 P = codec.payload_bytes(b.index)
-                self.payload.append(torch.zeros(P, dtype=torch.uint8, device=self.device))
-                self.recv.append(torch.zeros(self.N * P, dtype=torch.uint8, device=self.device))
+                recv = torch.zeros(self.N * P, dtype=torch.uint8, device=self.device)
+                # encode straight into this rank's slot of the gather buffer: an in-place
+                # all-gather (RCCL: sendbuff == recvbuff + rank * count), no local copy
+                r = comm.rank
+                self.payload.append(recv[r * P:(r + 1) * P])
+                self.recv.append(recv)
                 self.send.append(None)
         self.resid = torch.zeros_like(flat.grad) if (error_feedback and not codec.allreduce) else None
         if not flat.attach_grads and not self.cuda:

@@ -129,3 +129,36 @@ def test_capture_after_single_eager_step():
              "--device", "cuda", "--hip-graph", "full", "--graph-warmup", "1"]
     tr, losses = _run(flags, 4)
     assert tr._graphs is not None and all(torch.isfinite(torch.tensor(losses)))
+
+
+def _free_port():
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("codec", ["topk_qsgd", "none"])
+def test_bench_through_rccl_process_group(codec):
+    """bench.py under torch.distributed.run with a real RCCL communicator (world of one,
+    EWDML_FORCE_PG=1): the multi-GPU code path -- RCCL all-gather of the packed payloads issued
+    in place from the payload slot (or the dense all-reduce), captured in the step's HIP graph --
+    that the 8-GPU scaling run takes, on the one GPU this box has."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    env = dict(os.environ, EWDML_FORCE_PG="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py",
+           "--gpus", "1", "--steps", "4", "--warmup", "4", "--batch-size", "64",
+           "--compress", codec]
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert rec["config"]["hip_graph"] == "full"  # the capture of the RCCL collective succeeded
+    assert rec["value"] > 0 and rec["n_gpus"] == 1
+    assert rec["final_loss"] == rec["final_loss"]  # not NaN
