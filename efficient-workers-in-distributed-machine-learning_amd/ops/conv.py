@@ -36,7 +36,8 @@ def _ws(device):
     key = (device.index, _stream())
     w = _WS.get(key)
     if w is None:
-        w = torch.empty(require().conv_ws_floats(), dtype=torch.float32, device=device)
+        # zeros: its last 64 floats are the DMA kernels' zero page (never written)
+        w = torch.zeros(require().conv_ws_floats(), dtype=torch.float32, device=device)
         _WS[key] = w
     return w
 

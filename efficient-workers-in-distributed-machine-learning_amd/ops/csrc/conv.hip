@@ -27,6 +27,8 @@
 // Block = 256 threads = 4 waves in a 2 x 2 grid over the BM x BN output tile; wave tile
 // (BM/2) x (BN/2) of 16 x 16 MFMA tiles.  C/D map of 16x16x32: col = lane & 15,
 // row = 4 * (lane >> 4) + reg.
+#include <cstdlib>
+
 #include "common.h"
 #include "ewdml_ops.h"
 
@@ -219,6 +221,66 @@ __device__ __forceinline__ void cv_group_reduce(f32x4 (&acc)[MI][NJ], char* smem
   }
 }
 
+// Epilogue of the NT kernels: fp32 split slab, or bf16 output + (optional) BatchNorm partial sums
+// of the stored output (see k_conv_nt).  Every thread of the block calls it (barriers inside);
+// only k-group 0 (g == 0) holds the reduced accumulators.
+template <int BM, int BN, int MI, int NJ>
+__device__ __forceinline__ void cv_nt_epilogue(const f32x4 (&acc)[MI][NJ], char* smem, int g,
+                                               int wm, int wn, int lane, int m0, int n0, int M,
+                                               int Nc, uint16_t* __restrict__ out,
+                                               float* __restrict__ slab,
+                                               float* __restrict__ bnpart) {
+  const int row0 = m0 + wm * (BM / 2), col0 = n0 + wn * (BN / 2);
+  if (slab) {
+    if (g == 0)
+      cv_store<MI, NJ>(acc, row0, col0, lane, nullptr, slab + (long long)blockIdx.z * M * Nc, Nc);
+    return;
+  }
+  if (g == 0) cv_store<MI, NJ>(acc, row0, col0, lane, out, nullptr, Nc);
+  if (bnpart) {  // every group keeps the barrier count; only group 0's values are used
+    // BatchNorm statistics of the stored (bf16-rounded) output, fused into the epilogue: per
+    // column, sum and sum of squares over the block's BM rows -> partial row blockIdx.x of
+    // bnpart[2][M/BM][Nc] (the BN finalize kernel's layout).  The two waves sharing columns
+    // (wm = 0, 1) combine through LDS.
+    float* red = reinterpret_cast<float*>(smem);  // [wn][2][BN/2]
+    const long long nrows = M / BM;
+    float sm[NJ], sq[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      sm[j] = sq[j] = 0.0f;
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float v = __uint_as_float((uint32_t)ew_f2bf(acc[i][j][q]) << 16);
+          sm[j] += v;
+          sq[j] += v * v;
+        }
+      sm[j] += __shfl_xor(sm[j], 16, 64);
+      sq[j] += __shfl_xor(sq[j], 16, 64);
+      sm[j] += __shfl_xor(sm[j], 32, 64);
+      sq[j] += __shfl_xor(sq[j], 32, 64);
+    }
+    __syncthreads();  // group reduce / main loop finished reading smem
+    if (g == 0 && wm == 1 && lane < 16) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        red[(wn * 2 + 0) * (BN / 2) + j * 16 + lane] = sm[j];
+        red[(wn * 2 + 1) * (BN / 2) + j * 16 + lane] = sq[j];
+      }
+    }
+    __syncthreads();
+    if (g == 0 && wm == 0 && lane < 16) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int c = col0 + j * 16 + lane;
+        bnpart[(long long)blockIdx.x * Nc + c] = sm[j] + red[(wn * 2 + 0) * (BN / 2) + j * 16 + lane];
+        bnpart[(nrows + blockIdx.x) * Nc + c] = sq[j] + red[(wn * 2 + 1) * (BN / 2) + j * 16 + lane];
+      }
+    }
+  }
+}
+
 // NT kernel (forward and backward-data).  x: [M][C] pixels of one NHWC tensor (M = N*H*W),
 // w: [Nc][9*C] (tap-major, channel-minor), out: [M][Nc] bf16, or fp32 slabs [split][M][Nc].
 // Split z covers k-steps [z*kps, min((z+1)*kps, ksteps)).  Requires C % 64 == 0, M % BM == 0,
@@ -347,57 +409,119 @@ __global__ __launch_bounds__(EW_BLOCK * KG) void k_conv_nt(const uint16_t* __res
   }
 #undef CV_NT_MMA
   cv_group_reduce<KG, MI, NJ>(acc, smem, g, wq, lane);
-  const int row0 = m0 + wm * (BM / 2), col0 = n0 + wn * (BN / 2);
-  if (slab) {
-    if (g == 0)
-      cv_store<MI, NJ>(acc, row0, col0, lane, nullptr, slab + (long long)blockIdx.z * M * Nc, Nc);
-    return;
-  }
-  if (g == 0) cv_store<MI, NJ>(acc, row0, col0, lane, out, nullptr, Nc);
-  if (bnpart) {  // every group keeps the barrier count; only group 0's values are used
-    // BatchNorm statistics of the stored (bf16-rounded) output, fused into the epilogue: per
-    // column, sum and sum of squares over the block's BM rows -> partial row blockIdx.x of
-    // bnpart[2][M/BM][Nc] (the BN finalize kernel's layout).  The two waves sharing columns
-    // (wm = 0, 1) combine through LDS.
-    float* red = reinterpret_cast<float*>(smem);  // [wn][2][BN/2]
-    const long long nrows = M / BM;
-    float sm[NJ], sq[NJ];
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      sm[j] = sq[j] = 0.0f;
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float v = __uint_as_float((uint32_t)ew_f2bf(acc[i][j][q]) << 16);
-          sm[j] += v;
-          sq[j] += v * v;
-        }
-      sm[j] += __shfl_xor(sm[j], 16, 64);
-      sq[j] += __shfl_xor(sq[j], 16, 64);
-      sm[j] += __shfl_xor(sm[j], 32, 64);
-      sq[j] += __shfl_xor(sq[j], 32, 64);
-    }
-    __syncthreads();  // group reduce / main loop finished reading smem
-    if (g == 0 && wm == 1 && lane < 16) {
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        red[(wn * 2 + 0) * (BN / 2) + j * 16 + lane] = sm[j];
-        red[(wn * 2 + 1) * (BN / 2) + j * 16 + lane] = sq[j];
-      }
-    }
-    __syncthreads();
-    if (g == 0 && wm == 0 && lane < 16) {
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const int c = col0 + j * 16 + lane;
-        bnpart[(long long)blockIdx.x * Nc + c] = sm[j] + red[(wn * 2 + 0) * (BN / 2) + j * 16 + lane];
-        bnpart[(nrows + blockIdx.x) * Nc + c] = sq[j] + red[(wn * 2 + 1) * (BN / 2) + j * 16 + lane];
-      }
-    }
-  }
+  cv_nt_epilogue<BM, BN, MI, NJ>(acc, smem, g, wm, wn, lane, m0, n0, M, Nc, out, slab, bnpart);
 #undef CV_NT_LOAD
 #undef CV_NT_STORE
+}
+
+// ---------------------------------------------------------------------------------------------
+// LDS-DMA variant of the NT kernel (one k-group, NS-deep stage ring): operand tiles go global ->
+// LDS directly with global_load_lds_dwordx4 (no staging registers, no ds_write), NS-1 k-steps in
+// flight.  A wave instruction fills 8 consecutive 128-B rows lane-linearly (lane l -> row l/8,
+// 16-B slot l%8), so each lane fetches the source chunk that the swizzled image stores at its
+// slot (chunk = slot ^ swz(row)); out-of-image im2col rows read a zero page.  Ordering: a counted
+// s_waitcnt vmcnt (the ring's younger stages stay in flight) + a raw s_barrier per k-step; the
+// stage overwritten after the barrier was last read one step earlier (WAR-safe).
+typedef __attribute__((address_space(3))) void* cv_lds_ptr;
+typedef __attribute__((address_space(1))) void* cv_gbl_ptr;
+
+__device__ __forceinline__ void cv_glds16(const void* src, char* lds_row_base) {
+  __builtin_amdgcn_global_load_lds((cv_gbl_ptr)(src), (cv_lds_ptr)(lds_row_base), 16, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void cv_wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  // gfx9 s_waitcnt encoding: vmcnt[3:0] + vmcnt_hi[15:14], expcnt[6:4] = 7, lgkmcnt[11:8] = 15
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+template <int BM, int BN, int NS, bool TRB>
+__global__ __launch_bounds__(EW_BLOCK) void k_conv_nt_dma(const uint16_t* __restrict__ x,
+                                                          const uint16_t* __restrict__ w,
+                                                          uint16_t* __restrict__ out,
+                                                          float* __restrict__ slab, int M, int H,
+                                                          int W, int C, int Nc, int kps, int taps,
+                                                          float* __restrict__ bnpart,
+                                                          const uint16_t* __restrict__ zero) {
+  constexpr int PA = BM / 32, PB = BN / 32;   // glds instructions per wave per k-step (8 rows each)
+  constexpr int MI = BM / 32, NJ = BN / 32;
+  constexpr int STAGE = (BM + BN) * 128;
+  constexpr int LPW = PA + PB;
+  static_assert(!TRB || BN == 64, "transposed B images are 64 columns wide");
+  __shared__ __attribute__((aligned(16))) char smem[NS * STAGE];
+  const int t = threadIdx.x, lane = t & 63, wq = t >> 6;
+  const int wm = wq >> 1, wn = wq & 1;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int CB = C / CV_BK, ksteps = taps * CB;
+  const int kbeg = blockIdx.z * kps;
+  const int kend = min(kbeg + kps, ksteps);
+  const long long K = (long long)taps * C;
+  const int lr = lane >> 3, slot = lane & 7;
+
+  // A rows of this lane: wave wq, instruction j -> tile row (wq*PA + j)*8 + lr
+  int am[PA], ah[PA], aw[PA], ac[PA];
+#pragma unroll
+  for (int j = 0; j < PA; ++j) {
+    const int row = (wq * PA + j) * 8 + lr;
+    const int m = m0 + row;
+    am[j] = m;
+    const int hw = m % (H * W);
+    ah[j] = hw / W;
+    aw[j] = hw - ah[j] * W;
+    ac[j] = slot ^ ((row >> 1) & 7);  // source chunk landing at this lane's slot
+  }
+  const uint16_t* bsrc[PB];
+#pragma unroll
+  for (int j = 0; j < PB; ++j) {
+    const int row = (wq * PB + j) * 8 + lr;
+    bsrc[j] = TRB ? w + (long long)row * taps * Nc + n0 + 8 * (slot ^ cv_trf(row))
+                  : w + (long long)(n0 + row) * K + 8 * (slot ^ ((row >> 1) & 7));
+  }
+
+  auto issue = [&](int st, int buf) {
+    const int tap = st / CB, cb = st - tap * CB;
+    const int dr = taps == 1 ? 0 : tap / 3 - 1, dc = taps == 1 ? 0 : tap - (tap / 3) * 3 - 1;
+    char* As = smem + buf * STAGE;
+    char* Bs = As + BM * 128;
+#pragma unroll
+    for (int j = 0; j < PA; ++j) {
+      const bool ok = (unsigned)(ah[j] + dr) < (unsigned)H && (unsigned)(aw[j] + dc) < (unsigned)W;
+      const uint16_t* src =
+          ok ? x + (long long)(am[j] + dr * W + dc) * C + cb * CV_BK + ac[j] * 8 : zero;
+      cv_glds16(src, As + (wq * PA + j) * 8 * 128);
+    }
+    const long long bo = TRB ? ((long long)cb * CV_BK * taps + (taps - 1 - tap)) * Nc
+                             : (long long)st * CV_BK;
+#pragma unroll
+    for (int j = 0; j < PB; ++j) cv_glds16(bsrc[j] + bo, Bs + (wq * PB + j) * 8 * 128);
+  };
+
+  f32x4 acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+
+  const int n = kend - kbeg;
+  if (n > 0) {
+    const int last = kend - 1;
+#pragma unroll
+    for (int j = 0; j < NS - 1; ++j) issue(min(kbeg + j, last), j);  // clamped: dummy re-loads
+    for (int i = 0; i < n; ++i) {
+      cv_wait_vm<LPW * (NS - 2)>();  // this step's stage landed (younger NS-2 stages in flight)
+      __builtin_amdgcn_s_barrier();  // ... for every wave; and step i-1's stage is free again
+      issue(min(kbeg + i + NS - 1, last), (i + NS - 1) % NS);
+      const char* As = smem + (i % NS) * STAGE;
+      if constexpr (TRB)
+        cv_mma_mixed<MI, NJ>(As, As + BM * 128, wm * (BM / 2), wn * (BN / 2), lane, acc);
+      else
+        cv_mma<MI, NJ>(As, As + BM * 128, wm * (BM / 2), wn * (BN / 2), lane, acc);
+    }
+    cv_wait_vm<0>();  // drain the dummy loads before the epilogue reuses the ring
+  }
+  __syncthreads();
+  cv_nt_epilogue<BM, BN, MI, NJ>(acc, smem, 0, wm, wn, lane, m0, n0, M, Nc, out, slab, bnpart);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -604,7 +728,15 @@ static int ew_conv_nt(const uint16_t* x, const uint16_t* w, uint16_t* out, float
                    (long long)(M / 128) * (Nc / 128) >= 256;
   const int BM = big ? 128 : 64;
   const long long tiles = (long long)(M / BM) * (Nc / BM);
-  const CvPlan p = cv_plan(tiles, ksteps, big ? 2 : 4, (long long)M * Nc, ws_floats);
+  // EWDML_CONV_DMA=1: the LDS-DMA stage-ring kernels (one k-group per block)
+  static const bool dma = [] {
+    const char* e = getenv("EWDML_CONV_DMA");
+    return e && e[0] == '1';
+  }();
+  // the last 64 floats of the workspace are a zero page (never part of a slab)
+  ws_floats -= 64;
+  const uint16_t* zero = reinterpret_cast<const uint16_t*>(ws + ws_floats);
+  const CvPlan p = cv_plan(tiles, ksteps, dma ? 1 : (big ? 2 : 4), (long long)M * Nc, ws_floats);
   dim3 grid(M / BM, Nc / BM, p.split);
   float* slab = p.split > 1 ? ws : nullptr;
   // epilogue BN partials: one row per M-tile; beyond 1024 rows the BN statistics pass (<= 1024
@@ -612,7 +744,14 @@ static int ew_conv_nt(const uint16_t* x, const uint16_t* w, uint16_t* out, float
   const long long prow = M / BM;
   float* bnp = (bnpart && !slab && prow <= 1024 && 2 * prow * Nc <= bnpart_floats) ? bnpart
                                                                                   : nullptr;
-  if (big) {
+#define CV_LAUNCH_DMA(BM_, TRB_)                                                                 \
+  hipLaunchKernelGGL((k_conv_nt_dma<BM_, BM_, 4, TRB_>), grid, dim3(EW_BLOCK), 0, s, x, w, out, \
+                     slab, M, H, W, C, Nc, p.kps, taps, bnp, zero)
+  if (dma) {
+    if (big) CV_LAUNCH_DMA(128, false);
+    else if (trb) CV_LAUNCH_DMA(64, true);
+    else CV_LAUNCH_DMA(64, false);
+  } else if (big) {
     if (p.kg == 2) CV_LAUNCH_NT(128, 2, false);
     else CV_LAUNCH_NT(128, 1, false);
   } else if (trb) {
@@ -635,6 +774,7 @@ static int ew_conv_nt(const uint16_t* x, const uint16_t* w, uint16_t* out, float
   return bnp ? (int)prow : 0;
 }
 #undef CV_LAUNCH_NT
+#undef CV_LAUNCH_DMA
 
 static int cv_taps(int ksize) {
   if (ksize != 1 && ksize != 3) throw std::runtime_error("ewdml conv: kernel size must be 1 or 3");
@@ -672,6 +812,7 @@ void ew_conv_wgrad(uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws, long l
   const long long tiles = (long long)(Nc / 64) * (K / 64);
   const int msteps = (int)(M / CV_BK);
   CvPlan p{1, 1, msteps};
+  ws_floats -= 64;  // zero page (see ew_conv_nt)
   // blocks for every CU through the m split (slabs are Nc x 9C, small next to the activations)
   while (tiles * p.split < 256 && msteps / (p.split * 2) >= 8) p.split *= 2;
   while (p.split > 1 && (long long)p.split * Nc * K > ws_floats) p.split /= 2;

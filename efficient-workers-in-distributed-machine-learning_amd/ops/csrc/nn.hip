@@ -850,6 +850,23 @@ __global__ __launch_bounds__(1024) void k_ce_fwd(const T* __restrict__ x,
   __shared__ float lrow[16];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   float acc = 0.0f;  // this wave's sum of row losses (lane 0)
+  if (K <= 32) {
+    // few classes (CIFAR / MNIST: 10): one row per thread, no cross-lane reductions
+    for (int r = threadIdx.x; r < B; r += 1024) {
+      const T* xr = x + (long long)r * K;
+      float m = -INFINITY;
+      for (int k = 0; k < K; ++k) m = fmaxf(m, ew_ldf(xr, k));
+      float s = 0.0f;
+      for (int k = 0; k < K; ++k) s += expf(ew_ldf(xr, k) - m);
+      const float l = m + logf(s);
+      lse[r] = l;
+      const long long t = y[r];
+      acc += l - ((t >= 0 && t < K) ? ew_ldf(xr, t) : 0.0f);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);  // fixed order
+    if (lane != 0) acc = 0.0f;
+  } else
   for (int r = wv; r < B; r += 16) {
     const T* xr = x + (long long)r * K;
     float m = -INFINITY;
