@@ -12,6 +12,7 @@ import math
 
 import torch.nn as nn
 
+from . import fused
 from .fused import FusedFeatures
 
 _CFG = {
@@ -60,7 +61,12 @@ class VGG(nn.Module):
                 m.bias.data.zero_()
 
     def forward(self, x):
-        return self.classifier(self.features(x).flatten(1))
+        f = self.features(x).flatten(1)
+        if fused.active(f):  # hipBLASLt GEMMs + fused activation/dropout kernels (ops/head.py)
+            from ..ops.head import vgg_head
+
+            return vgg_head(self.classifier, f)
+        return self.classifier(f)
 
 
 def _make(cfg_key, bn, num_classes=10):

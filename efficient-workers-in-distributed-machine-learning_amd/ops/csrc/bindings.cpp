@@ -239,6 +239,8 @@ PYBIND11_MODULE(_C, m) {
           a.pool = pool; a.mode = mode; a.cb_bf16 = cb_bf16; a.stream = stream;
           ew_bn_relu_bwd(a);
         });
+  m.def("act_dropout_fwd", &ew_act_dropout_fwd);
+  m.def("act_dropout_bwd", &ew_act_dropout_bwd);
   m.def("cross_entropy_fwd", &ew_cross_entropy_fwd);
   m.def("cross_entropy_bwd", &ew_cross_entropy_bwd);
   m.def("conv_ws_floats", &ew_conv_ws_floats);

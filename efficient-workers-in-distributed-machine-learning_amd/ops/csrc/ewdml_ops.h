@@ -157,3 +157,10 @@ void ew_cross_entropy_fwd(uintptr_t x, uintptr_t y, int B, int K, int is_bf16, u
                           uintptr_t lse, uintptr_t stream);
 void ew_cross_entropy_bwd(uintptr_t x, uintptr_t y, uintptr_t lse, uintptr_t grad, int B, int K,
                           int is_bf16, uintptr_t dx, uintptr_t stream);
+
+// ---- classifier-head activation + dropout (nn.hip), bf16 [rows, C]; ctr int32[2] per layer
+void ew_act_dropout_fwd(uintptr_t y, uintptr_t z, int n, float p, int relu, uintptr_t ctr,
+                        uint32_t salt, uintptr_t stream);
+void ew_act_dropout_bwd(uintptr_t dz, uintptr_t y, uintptr_t dy, uintptr_t db, int db_bf16,
+                        int rows, int C, float p, int relu, uintptr_t ctr, uint32_t salt,
+                        uintptr_t stream);

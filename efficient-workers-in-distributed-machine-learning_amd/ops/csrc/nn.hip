@@ -947,3 +947,109 @@ void ew_cross_entropy_bwd(uintptr_t x, uintptr_t y, uintptr_t lse, uintptr_t gra
                        K, reinterpret_cast<float*>(dx));
   EW_CHECK_LAUNCH();
 }
+
+// ================================================================================================
+// Classifier-head activations (VGG's Dropout / Linear-ReLU-Dropout / Linear-ReLU layers) on
+// [rows, C] bf16 activations:
+//   forward : z = act(y) * keep / (1 - p), keep = hash(key, i) >= p  (act = ReLU or identity)
+//   backward: dy = dz * keep / (1 - p) * act'(y), and db[c] = sum over rows of dy (the bias
+//             gradient of the Linear that produced y: no separate reduction kernel)
+// The dropout key comes from a per-layer device counter ctr[0]: forward and backward read it,
+// and the backward's last-arriving block (ticket ctr[1]) advances it -- a fresh mask every
+// step, also under HIP-graph replay, without PyTorch's per-replay RNG offset fills.  Masks are
+// recomputed, never stored.  Backward blocks own column strips, so the bias gradient needs no
+// cross-block reduction.
+// ================================================================================================
+namespace {
+
+__device__ __forceinline__ bool ew_keep(uint32_t i, uint32_t key, float p) {
+  return ew_uniform(i, key) >= p;
+}
+__device__ __forceinline__ uint32_t ew_drop_key(int ctr, uint32_t salt) {
+  return ew_mix32((uint32_t)ctr * 0x9E3779B9u + salt);
+}
+
+__global__ __launch_bounds__(EW_BLOCK) void k_act_dropout_fwd(const uint16_t* __restrict__ y,
+                                                              uint16_t* __restrict__ z, int n,
+                                                              float p, int relu,
+                                                              const int* __restrict__ ctr,
+                                                              uint32_t salt) {
+  const uint32_t key = ew_drop_key(ctr[0], salt);
+  const float scale = p > 0.0f ? 1.0f / (1.0f - p) : 1.0f;
+  for (int v = blockIdx.x * EW_BLOCK + threadIdx.x; 8 * v < n; v += gridDim.x * EW_BLOCK) {
+    const int i0 = 8 * v;  // n % 8 == 0 (host)
+    float x[8];
+    V8<uint16_t>::ld(y + i0, x);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (relu) x[j] = ew_relu(x[j]);
+      if (p > 0.0f) x[j] = ew_keep((uint32_t)(i0 + j), key, p) ? x[j] * scale : 0.0f;
+    }
+    V8<uint16_t>::st(z + i0, x);
+  }
+}
+
+// block b: columns [32 b, 32 b + 32) over all rows (its bias gradient is block-local: no
+// cross-block partials); thread t: column 32 b + t % 32, rows t / 32, + 8, ...
+__global__ __launch_bounds__(EW_BLOCK) void k_act_dropout_bwd(
+    const uint16_t* __restrict__ dz, const uint16_t* __restrict__ y, uint16_t* __restrict__ dy,
+    void* __restrict__ db, int db_bf16, int rows, int C, float p, int relu,
+    int* __restrict__ ctr, uint32_t salt) {
+  __shared__ float part[EW_BLOCK];
+  const uint32_t key = ew_drop_key(ctr[0], salt);
+  const float scale = p > 0.0f ? 1.0f / (1.0f - p) : 1.0f;
+  const int c = blockIdx.x * 32 + (threadIdx.x & 31), rg = threadIdx.x >> 5;
+  float s = 0.0f;
+  if (c < C) {
+    for (int r = rg; r < rows; r += EW_BLOCK / 32) {
+      const int i = r * C + c;
+      float g = ew_bf16f(dz[i]);
+      if (p > 0.0f) g = ew_keep((uint32_t)i, key, p) ? g * scale : 0.0f;
+      if (relu && !ew_relu_pass(ew_bf16f(y[i]))) g = 0.0f;
+      const uint16_t gb = ew_f2bf(g);
+      dy[i] = gb;
+      s += ew_bf16f(gb);  // the bias gradient of the rounded dy the GEMMs consume
+    }
+  }
+  part[threadIdx.x] = s;
+  __syncthreads();
+  if (db && threadIdx.x < 32 && c < C) {
+    float a = 0.0f;
+    for (int j = 0; j < EW_BLOCK / 32; ++j) a += part[j * 32 + threadIdx.x];  // fixed order
+    if (db_bf16) reinterpret_cast<uint16_t*>(db)[c] = ew_f2bf(a);
+    else reinterpret_cast<float*>(db)[c] = a;
+  }
+  // advance the key counter once every block has read it: arrival ticket ctr[1] (each block's
+  // read of ctr[0] completed before its ticket; the new value is seen by the next kernel)
+  if (threadIdx.x == 0) {
+    const int tk = __hip_atomic_fetch_add(&ctr[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tk == (int)gridDim.x - 1) {
+      ctr[1] = 0;
+      ctr[0] = ctr[0] + 1;
+    }
+  }
+}
+
+}  // namespace
+
+void ew_act_dropout_fwd(uintptr_t y, uintptr_t z, int n, float p, int relu, uintptr_t ctr,
+                        uint32_t salt, uintptr_t stream) {
+  if (n % 8) throw std::runtime_error("ewdml act_dropout_fwd: n % 8 != 0");
+  int g = (n / 8 + EW_BLOCK - 1) / EW_BLOCK;
+  g = g < 1 ? 1 : (g > 1024 ? 1024 : g);
+  hipLaunchKernelGGL(k_act_dropout_fwd, dim3(g), dim3(EW_BLOCK), 0, (hipStream_t)stream,
+                     reinterpret_cast<const uint16_t*>(y), reinterpret_cast<uint16_t*>(z), n, p,
+                     relu, reinterpret_cast<const int*>(ctr), salt);
+  EW_CHECK_LAUNCH();
+}
+
+void ew_act_dropout_bwd(uintptr_t dz, uintptr_t y, uintptr_t dy, uintptr_t db, int db_bf16,
+                        int rows, int C, float p, int relu, uintptr_t ctr, uint32_t salt,
+                        uintptr_t stream) {
+  const int g = (C + 31) / 32;
+  hipLaunchKernelGGL(k_act_dropout_bwd, dim3(g), dim3(EW_BLOCK), 0, (hipStream_t)stream,
+                     reinterpret_cast<const uint16_t*>(dz), reinterpret_cast<const uint16_t*>(y),
+                     reinterpret_cast<uint16_t*>(dy), reinterpret_cast<void*>(db), db_bf16, rows,
+                     C, p, relu, reinterpret_cast<int*>(ctr), salt);
+  EW_CHECK_LAUNCH();
+}

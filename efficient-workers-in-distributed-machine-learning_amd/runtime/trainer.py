@@ -66,6 +66,10 @@ class Trainer:
             if cfg.hip_graph != "off":
                 raise ValueError("--sync-debug synchronises after each launch: use --hip-graph off")
         torch.manual_seed(cfg.seed)
+        if self.cuda:
+            from ..ops import head as _head
+
+            _head.set_seed(cfg.seed, self.rank)  # dropout masks of the fused VGG head
         if self.cuda:  # MIOpen find once per shape during warmup (EWDML_CUDNN_BENCHMARK=0: heuristics)
             torch.backends.cudnn.benchmark = os.environ.get("EWDML_CUDNN_BENCHMARK", "1") == "1"
         self.log = MetricsLogger(cfg.metrics_file, self.rank, cfg.quiet)
@@ -296,7 +300,11 @@ class Trainer:
             self._gy = y.clone()
         ex.use_dev_key = True
         saved = (ex.step_idx, self.opt.steps)
-        mode = os.environ.get("EWDML_GRAPH_CAPTURE_MODE", "global")
+        # thread_local: only this thread's capture-unsafe HIP calls are refused.  In "global" mode
+        # the RCCL process group's watchdog thread, which polls its work events, hits
+        # hipErrorStreamCaptureUnsupported whenever a poll lands inside our capture, and that
+        # error terminates the process (seen with a real RCCL communicator).
+        mode = os.environ.get("EWDML_GRAPH_CAPTURE_MODE", "thread_local")
         torch.cuda.synchronize()
         if self.graph_mode == "full":
             g = torch.cuda.CUDAGraph()

@@ -291,3 +291,61 @@ def test_cross_entropy_matches_torch(B, K, dtype):
     assert a.grad.dtype == dtype
     tol = 1e-2 if dtype == torch.bfloat16 else 1e-5
     assert _rel(a.grad, r.grad) < tol, _rel(a.grad, r.grad)
+
+
+def _head_model():
+    from ewdml.models import build_model
+
+    torch.manual_seed(3)
+    m = build_model("vgg11", 10).cuda()
+    for p in m.classifier.parameters():
+        p.data = p.data.to(torch.bfloat16)
+    return m.classifier
+
+
+def test_vgg_head_matches_torch_without_dropout():
+    from ewdml.ops import head
+
+    _ops()
+    cls = _head_model()
+    for mod in cls:
+        if isinstance(mod, nn.Dropout):
+            mod.p = 0.0
+    x = torch.randn(128, 512, device="cuda").to(torch.bfloat16)
+    xa, xb = x.clone().requires_grad_(True), x.clone().requires_grad_(True)
+    assert head.supported(cls, xa)
+    out = head.vgg_head(cls, xa)
+    gout = torch.randn_like(out)
+    out.backward(gout)
+    ga = [p.grad.clone() for p in cls.parameters()]
+    for p in cls.parameters():
+        p.grad = None
+    ref = cls(xb)
+    ref.backward(gout)
+    assert _rel(out, ref) < 1e-2
+    assert _rel(xa.grad, xb.grad) < 2e-2
+    for a, p in zip(ga, cls.parameters()):
+        assert a.dtype == p.dtype
+        assert _rel(a, p.grad) < 2e-2, _rel(a, p.grad)
+
+
+def test_vgg_head_dropout_masks():
+    from ewdml.ops import head
+
+    fnn = _ops()
+    cls = _head_model()
+    x = torch.randn(128, 512, device="cuda").to(torch.bfloat16).requires_grad_(True)
+    d0 = cls[0]
+    z1 = head._ActDropout.apply(x, 0.5, False, head._ctr(d0, x.device))
+    kept = (z1 != 0) & (x != 0)
+    frac = float(kept.float().mean())
+    assert 0.47 < frac < 0.53, frac
+    assert torch.equal(z1[kept].float(), (2 * x[kept].float()).to(torch.bfloat16).float())
+    g = torch.ones_like(z1)
+    z1.backward(g)
+    # backward recomputes the forward's mask: grad 2 where kept, 0 where dropped
+    assert torch.equal(x.grad[kept].float(), torch.full_like(x.grad[kept].float(), 2.0))
+    assert float(x.grad[~kept & (x != 0)].abs().max()) == 0.0
+    z2 = head._ActDropout.apply(x.detach(), 0.5, False, head._ctr(d0, x.device))
+    assert not torch.equal(z1.detach(), z2)  # the device counter advanced: a new mask
+    del fnn
