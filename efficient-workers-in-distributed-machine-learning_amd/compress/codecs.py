@@ -124,15 +124,18 @@ class Codec:
         out[:plan.length].copy_(oracle.decode_sum(recv, plan, lay, self.levels, scale))
 
     def decode_apply_sgd(self, b: int, recv: torch.Tensor, scale: float, param: torch.Tensor,
-                         mom: torch.Tensor, hp: dict, first: bool, grad_out=None, shadow=None):
-        """Fused decode -> average -> SGD step of bucket ``b`` (one kernel on the GPU)."""
+                         mom: torch.Tensor, hp: dict, first: bool, grad_out=None, shadow=None,
+                         key_state=None, rank: int = 0):
+        """Fused decode -> average -> SGD step of bucket ``b`` (one kernel on the GPU).
+        ``key_state`` (device int32 {step, key}): also advance the RNG key to the next step."""
         plan, lay = self.plans[b], self.layouts[b]
         if recv.is_cuda:
             fn = ops.qsgd_decode_apply if self.kind == "qsgd" else ops.topk_decode_apply
             fn(self.dplans[b], recv, lay, self.levels, param=param, mom=mom, grad_out=grad_out,
                lr=hp["lr"], momentum=hp["momentum"], dampening=hp["dampening"],
                weight_decay=hp["weight_decay"], grad_scale=scale, nesterov=hp["nesterov"],
-               first=first, shadow=shadow)
+               first=first, shadow=shadow, key_state=key_state, key_seed=self.seed,
+               key_rank=rank)
             return
         g = oracle.decode_sum(recv, plan, lay, self.levels, scale)
         if grad_out is not None:

@@ -177,7 +177,8 @@ def topk_encode(dp: DevicePlan, grad, payload, layout, levels: int, norm: str, k
 
 def topk_decode_apply(dp: DevicePlan, recv, layout, levels: int, param=None, mom=None,
                       grad_out=None, lr=0.0, momentum=0.0, dampening=0.0, weight_decay=0.0,
-                      grad_scale=1.0, nesterov=False, first=False, shadow=None):
+                      grad_scale=1.0, nesterov=False, first=False, shadow=None,
+                      key_state=None, key_seed=0, key_rank=0):
     C = require()
     _check(recv, torch.uint8, "recv")
     if recv.dim() != 2 or recv.shape[1] != layout.nbytes:
@@ -198,7 +199,8 @@ def topk_decode_apply(dp: DevicePlan, recv, layout, levels: int, param=None, mom
                         _ptr(dp.tensors), dp.plan.num_chunks, layout.scales, layout.counts,
                         layout.idx, layout.codes, vk, float(1.0 / levels), _ptr(param), _ptr(mom),
                         _ptr(grad_out), _ptr(shadow), lr, momentum, dampening, weight_decay,
-                        grad_scale, int(nesterov), int(first), int(apply), _stream())
+                        grad_scale, int(nesterov), int(first), int(apply), _stream(),
+                        _keyp(key_state), key_seed & 0xFFFFFFFF, key_rank & 0xFFFFFFFF)
 
 
 def qsgd_encode(dp: DevicePlan, grad, payload, layout, levels: int, norm: str, key: int,
@@ -221,7 +223,8 @@ def qsgd_encode(dp: DevicePlan, grad, payload, layout, levels: int, norm: str, k
 
 def qsgd_decode_apply(dp: DevicePlan, recv, layout, levels: int, param=None, mom=None,
                       grad_out=None, lr=0.0, momentum=0.0, dampening=0.0, weight_decay=0.0,
-                      grad_scale=1.0, nesterov=False, first=False, shadow=None):
+                      grad_scale=1.0, nesterov=False, first=False, shadow=None,
+                      key_state=None, key_seed=0, key_rank=0):
     C = require()
     _check(recv, torch.uint8, "recv")
     if recv.dim() != 2 or recv.shape[1] != layout.nbytes:
@@ -239,7 +242,8 @@ def qsgd_decode_apply(dp: DevicePlan, recv, layout, levels: int, param=None, mom
                         _ptr(dp.tensors), dp.plan.num_chunks, layout.scales, layout.codes,
                         layout.bits, float(1.0 / levels), _ptr(param), _ptr(mom), _ptr(grad_out),
                         _ptr(shadow), lr, momentum, dampening, weight_decay, grad_scale,
-                        int(nesterov), int(first), int(apply), _stream())
+                        int(nesterov), int(first), int(apply), _stream(), _keyp(key_state),
+                        key_seed & 0xFFFFFFFF, key_rank & 0xFFFFFFFF)
 
 
 _GDT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}

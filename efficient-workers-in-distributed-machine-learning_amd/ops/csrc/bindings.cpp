@@ -60,8 +60,12 @@ PYBIND11_MODULE(_C, m) {
            int C, int scales_off, int counts_off, int idx_off, int codes_off, int value_kind,
            float inv_levels, uintptr_t param, uintptr_t mom, uintptr_t grad_out, uintptr_t shadow,
            float lr, float momentum, float dampening, float weight_decay, float grad_scale,
-           int nesterov, int first, int apply, uintptr_t stream) {
+           int nesterov, int first, int apply, uintptr_t stream, uintptr_t key_state,
+           uint32_t key_seed, uint32_t key_rank) {
           TopkDecodeArgs a{};
+          a.key_state = key_state;
+          a.key_seed = key_seed;
+          a.key_rank = key_rank;
           a.recv = recv;
           a.chunks = chunks;
           a.tensors = tensors;
@@ -127,8 +131,12 @@ PYBIND11_MODULE(_C, m) {
            int C, int scales_off, int codes_off, int bits, float inv_levels, uintptr_t param,
            uintptr_t mom, uintptr_t grad_out, uintptr_t shadow, float lr, float momentum,
            float dampening, float weight_decay, float grad_scale, int nesterov, int first,
-           int apply, uintptr_t stream) {
+           int apply, uintptr_t stream, uintptr_t key_state, uint32_t key_seed,
+           uint32_t key_rank) {
           QsgdDecodeArgs a{};
+          a.key_state = key_state;
+          a.key_seed = key_seed;
+          a.key_rank = key_rank;
           a.recv = recv;
           a.chunks = chunks;
           a.tensors = tensors;

@@ -109,6 +109,10 @@ __device__ __forceinline__ void ew_st4_bf16(uint16_t* dst, int n, const float v[
 struct SgdArgs {
   float lr, momentum, dampening, weight_decay, grad_scale;
   int nesterov, first;
+  // HIP-graph RNG key advance (nullable): key_state = {step, key} of the QSGD stream; the decode
+  // kernel of a step's last bucket moves it to the next step (no host->device key copy per step)
+  uint32_t* key_state;
+  uint32_t key_seed, key_rank;
 };
 
 // ---- counter-based RNG (must equal compress/rng.py) -------------------------------------------
@@ -122,6 +126,22 @@ __device__ __forceinline__ uint32_t ew_mix32(uint32_t x) {
 }
 __device__ __forceinline__ float ew_uniform(uint32_t idx, uint32_t key) {
   return (float)(ew_mix32(idx ^ key) >> 8) * (1.0f / 16777216.0f);
+}
+
+// compress/rng.py::stream_key
+__device__ __forceinline__ uint32_t ew_stream_key(uint32_t seed, uint32_t step, uint32_t rank) {
+  const uint32_t k = ew_mix32(step * 0x9E3779B9u + rank * 0x85EBCA6Bu + 0x632BE59Bu);
+  return ew_mix32(seed ^ k);
+}
+
+// One thread of the step's last decode kernel advances the device RNG key to the next step.  The
+// step's encode kernels (the only readers) ran before this kernel; the next step's run after it.
+__device__ __forceinline__ void ew_key_advance(const SgdArgs& sa) {
+  if (sa.key_state && blockIdx.x == 0 && threadIdx.x == 0) {
+    const uint32_t s = sa.key_state[0] + 1u;
+    sa.key_state[0] = s;
+    sa.key_state[1] = ew_stream_key(sa.key_seed, s, sa.key_rank);
+  }
 }
 
 // QSGD stochastic rounding of one value (compress/oracle.py::quantize).

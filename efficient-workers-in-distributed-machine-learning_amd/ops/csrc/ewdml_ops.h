@@ -29,6 +29,8 @@ struct TopkDecodeArgs {
   float inv_levels;
   float lr, momentum, dampening, weight_decay, grad_scale;
   int nesterov, first, apply;
+  uintptr_t key_state;  // nullable int32[2] {step, key}: advanced to the next step (HIP graphs)
+  uint32_t key_seed, key_rank;
 };
 
 struct QsgdEncodeArgs {
@@ -53,6 +55,8 @@ struct QsgdDecodeArgs {
   float inv_levels;
   float lr, momentum, dampening, weight_decay, grad_scale;
   int nesterov, first, apply;
+  uintptr_t key_state;  // see TopkDecodeArgs
+  uint32_t key_seed, key_rank;
 };
 
 struct SgdFlatArgs {

@@ -109,6 +109,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_qsgd_decode_apply(
     float* __restrict__ grad_out, uint16_t* __restrict__ shadow, SgdArgs sa, int apply) {
   const ChunkRow c = chunks[blockIdx.x];
   const TensorRow tr = tensors[c.tensor];
+  ew_key_advance(sa);
   const long long cbase = (long long)tr.code0 + (long long)c.local * EW_CHUNK;
   float* p = param + c.start;
   float* b = mom + c.start;
@@ -196,7 +197,8 @@ void ew_qsgd_encode(const QsgdEncodeArgs& a) {
 void ew_qsgd_decode_apply(const QsgdDecodeArgs& a) {
   auto* chunks = reinterpret_cast<const ChunkRow*>(a.chunks);
   auto* tensors = reinterpret_cast<const TensorRow*>(a.tensors);
-  SgdArgs sa{a.lr, a.momentum, a.dampening, a.weight_decay, a.grad_scale, a.nesterov, a.first};
+  SgdArgs sa{a.lr, a.momentum, a.dampening, a.weight_decay, a.grad_scale, a.nesterov, a.first,
+             reinterpret_cast<uint32_t*>(a.key_state), a.key_seed, a.key_rank};
   auto* recv = reinterpret_cast<const uint8_t*>(a.recv);
   auto* p = reinterpret_cast<float*>(a.param);
   auto* m = reinterpret_cast<float*>(a.mom);

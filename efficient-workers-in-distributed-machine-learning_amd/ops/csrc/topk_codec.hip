@@ -356,6 +356,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_decode_apply(
   float* acc = reinterpret_cast<float*>(acc4);
   const ChunkRow c = chunks[blockIdx.x];
   const TensorRow tr = tensors[c.tensor];
+  ew_key_advance(sa);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   for (int i = threadIdx.x; i < (c.len + 3) / 4; i += EW_BLOCK) acc4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   // entry offset of this chunk inside each rank's payload: entry0 + sum of earlier chunk counts
@@ -506,7 +507,8 @@ size_t ew_topk_scratch_bytes(int T, int C) {
 void ew_topk_decode_apply(const TopkDecodeArgs& a) {
   auto* chunks = reinterpret_cast<const ChunkRow*>(a.chunks);
   auto* tensors = reinterpret_cast<const TensorRow*>(a.tensors);
-  SgdArgs sa{a.lr, a.momentum, a.dampening, a.weight_decay, a.grad_scale, a.nesterov, a.first};
+  SgdArgs sa{a.lr, a.momentum, a.dampening, a.weight_decay, a.grad_scale, a.nesterov, a.first,
+             reinterpret_cast<uint32_t*>(a.key_state), a.key_seed, a.key_rank};
   auto* recv = reinterpret_cast<const uint8_t*>(a.recv);
   auto* p = reinterpret_cast<float*>(a.param);
   auto* m = reinterpret_cast<float*>(a.mom);

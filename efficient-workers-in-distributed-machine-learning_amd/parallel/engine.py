@@ -82,7 +82,11 @@ class GradientExchange:
         self.step_idx = 0
         self.defer_comm = False
         self.use_dev_key = False
-        self.key_dev = torch.zeros(1, dtype=torch.int32, device=self.device)
+        # device RNG state {step, key} read by the captured encode kernels; the step's last decode
+        # kernel advances it in place (dev_key_advance), so graph replays need no host upload
+        self.key_state = torch.zeros(2, dtype=torch.int32, device=self.device)
+        self.key_dev = self.key_state[1:2]
+        self.dev_key_advance = False
         self._key_ring, self._key_slot = None, 0
         self._hooks = []
         if overlap:
@@ -194,25 +198,25 @@ class GradientExchange:
         self._works = [None] * self.nb
 
     def set_device_key(self, step: int = None):
-        """Upload this step's RNG key (graph replay reads it from device memory)."""
-        key = self.codec.key((self.step_idx if step is None else step) + self.seed_offset,
-                             self.comm.rank)
-        if key >= 1 << 31:
-            key -= 1 << 32
-        if self.key_dev.device.type != "cuda":
-            self.key_dev.fill_(key)
+        """Upload this step's RNG state {step, key} (graph replay reads the key from device
+        memory; with ``dev_key_advance`` the decode kernel moves it on to the next step)."""
+        s = (self.step_idx if step is None else step) + self.seed_offset
+        key = self.codec.key(s, self.comm.rank)
+        vals = [((v + (1 << 31)) % (1 << 32)) - (1 << 31) for v in (s & 0xFFFFFFFF, key)]
+        if self.key_state.device.type != "cuda":
+            self.key_state.copy_(torch.tensor(vals, dtype=torch.int32))
             return
         # asynchronous upload from a ring of pinned slots: a pageable host->device copy would
         # block the host until the previous graph replay drained, leaving the GPU idle while the
         # next replay is launched.  A slot is reused only after its previous copy completed.
         if self._key_ring is None:
-            self._key_ring = [(torch.zeros(1, dtype=torch.int32).pin_memory(), None)
+            self._key_ring = [(torch.zeros(2, dtype=torch.int32).pin_memory(), None)
                               for _ in range(8)]
         host, ev = self._key_ring[self._key_slot]
         if ev is not None:
             ev.synchronize()
-        host[0] = key
-        self.key_dev.copy_(host, non_blocking=True)
+        host[0], host[1] = vals[0], vals[1]
+        self.key_state.copy_(host, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
         self._key_ring[self._key_slot] = (host, ev)
@@ -245,10 +249,13 @@ class GradientExchange:
             for b in self.flat.buckets:
                 recv = self.recv[b.index].view(self.N, -1)
                 if getattr(opt, "fusable", False):
+                    adv = self.dev_key_advance and self.use_dev_key and b.index == self.nb - 1
                     self.codec.decode_apply_sgd(b.index, recv, scale, self.flat.data_view(b),
                                                 opt.mom[b.start:b.start + b.length],
                                                 opt.hparams(), opt.first,
-                                                shadow=self.flat.shadow_view(b))
+                                                shadow=self.flat.shadow_view(b),
+                                                key_state=self.key_state if adv else None,
+                                                rank=self.comm.rank)
                 else:
                     gv = self.flat.grad_view(b)
                     self.codec.decode(b.index, recv, gv, scale)

@@ -154,6 +154,7 @@ class Trainer:
             raise ValueError("--hip-graph needs the all-to-all topology without local SGD")
         self._graphs = None
         self._in_graph_batch = False
+        self._key_synced = False
         # Graph mode: warmup, capture and replay all run on ONE dedicated stream, so MIOpen /
         # hipBLASLt create their per-stream handles and workspaces during the eager warmup and not
         # inside the capture (lazy per-stream init inside a capture crashes capture_end).
@@ -280,15 +281,15 @@ class Trainer:
             ex = self.exchange
             self._graphs = None
             self.graph_mode = "off"
-            ex.use_dev_key = ex.defer_comm = ex._active = False
+            ex.use_dev_key = ex.defer_comm = ex._active = ex.dev_key_advance = False
             torch.cuda.synchronize()
             self.log.info(f"HIP graph capture failed ({err!r} on this rank); running eagerly")
             return False
         return True
 
     def _capture(self, x, y):
-        """Capture the whole training step into HIP graph(s) (static input buffers; the QSGD RNG key
-        and the batch are refreshed in device memory before every replay).
+        """Capture the whole training step into HIP graph(s) (static input buffers; the batch
+        position and the QSGD RNG key advance in device memory from one replay to the next).
 
         ``full``: one graph = zero grads, fwd, bwd, hook-driven encode on the side stream, RCCL
         collectives, fused decode+SGD.  ``split``: graph A (through encode) -> eager RCCL calls ->
@@ -299,6 +300,8 @@ class Trainer:
             self._gx = x.clone()
             self._gy = y.clone()
         ex.use_dev_key = True
+        ex.dev_key_advance = True  # the captured decode advances the device RNG key per replay
+        self._key_synced = False
         saved = (ex.step_idx, self.opt.steps)
         # thread_local: only this thread's capture-unsafe HIP calls are refused.  In "global" mode
         # the RCCL process group's watchdog thread, which polls its work events, hits
@@ -343,7 +346,9 @@ class Trainer:
         elif x is not self._gx:
             self._gx.copy_(x)
             self._gy.copy_(y)
-        ex.set_device_key()
+        if not self._key_synced:  # once per capture; the replays advance the key on the device
+            ex.set_device_key()
+            self._key_synced = True
         if len(self._graphs) == 1:
             with self._range("graph_step"):
                 self._graphs[0].replay()
