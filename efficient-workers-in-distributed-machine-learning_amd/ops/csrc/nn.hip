@@ -989,35 +989,71 @@ __global__ __launch_bounds__(EW_BLOCK) void k_act_dropout_fwd(const uint16_t* __
   }
 }
 
-// block b: columns [32 b, 32 b + 32) over all rows (its bias gradient is block-local: no
-// cross-block partials); thread t: column 32 b + t % 32, rows t / 32, + 8, ...
+// block b: columns [16 b, 16 b + 16) over all rows, so its bias gradient is block-local (no
+// cross-block partials).  Thread t: column octet t & 1 (8 columns as one 16-byte access), rows
+// t >> 1, + 128, ...; the per-column sums are reduced across the wave's 32 row groups with
+// shuffles and across the 4 waves through LDS, in a fixed order.
+constexpr int EW_AD_TC = 2, EW_AD_RG = EW_BLOCK / EW_AD_TC;
 __global__ __launch_bounds__(EW_BLOCK) void k_act_dropout_bwd(
     const uint16_t* __restrict__ dz, const uint16_t* __restrict__ y, uint16_t* __restrict__ dy,
     void* __restrict__ db, int db_bf16, int rows, int C, float p, int relu,
     int* __restrict__ ctr, uint32_t salt) {
-  __shared__ float part[EW_BLOCK];
+  __shared__ float part[EW_WAVES][EW_AD_TC * 8];
   const uint32_t key = ew_drop_key(ctr[0], salt);
   const float scale = p > 0.0f ? 1.0f / (1.0f - p) : 1.0f;
-  const int c = blockIdx.x * 32 + (threadIdx.x & 31), rg = threadIdx.x >> 5;
-  float s = 0.0f;
-  if (c < C) {
-    for (int r = rg; r < rows; r += EW_BLOCK / 32) {
-      const int i = r * C + c;
-      float g = ew_bf16f(dz[i]);
-      if (p > 0.0f) g = ew_keep((uint32_t)i, key, p) ? g * scale : 0.0f;
-      if (relu && !ew_relu_pass(ew_bf16f(y[i]))) g = 0.0f;
-      const uint16_t gb = ew_f2bf(g);
-      dy[i] = gb;
-      s += ew_bf16f(gb);  // the bias gradient of the rounded dy the GEMMs consume
+  const int tc = threadIdx.x % EW_AD_TC, rg = threadIdx.x / EW_AD_TC;
+  const int c0 = (blockIdx.x * EW_AD_TC + tc) * 8;
+  float s[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s[j] = 0.0f;
+  if (c0 < C) {
+    for (int r0 = rg; r0 < rows; r0 += 2 * EW_AD_RG) {  // two rows in flight per thread
+      float g[2][8], yv[2][8];
+      const bool two = r0 + EW_AD_RG < rows;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int r = two ? r0 + u * EW_AD_RG : r0;
+        V8<uint16_t>::ld(dz + (long long)r * C + c0, g[u]);
+        if (relu) V8<uint16_t>::ld(y + (long long)r * C + c0, yv[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        if (u == 1 && !two) break;
+        const int r = r0 + u * EW_AD_RG;
+        const uint32_t i0 = (uint32_t)r * (uint32_t)C + (uint32_t)c0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float v = g[u][j];
+          if (p > 0.0f) v = ew_keep(i0 + j, key, p) ? v * scale : 0.0f;
+          if (relu && !ew_relu_pass(yv[u][j])) v = 0.0f;
+          g[u][j] = V8<uint16_t>::rnd(v);
+          s[j] += g[u][j];  // the bias gradient of the rounded dy the GEMMs consume
+        }
+        V8<uint16_t>::st(dy + (long long)r * C + c0, g[u]);
+      }
     }
   }
-  part[threadIdx.x] = s;
+  // sum over the wave's row groups (lanes with equal tc), then over the waves
+#pragma unroll
+  for (int o = EW_AD_TC; o < 64; o <<= 1) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s[j] += __shfl_xor(s[j], o, 64);
+  }
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane < EW_AD_TC) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) part[wave][lane * 8 + j] = s[j];
+  }
   __syncthreads();
-  if (db && threadIdx.x < 32 && c < C) {
-    float a = 0.0f;
-    for (int j = 0; j < EW_BLOCK / 32; ++j) a += part[j * 32 + threadIdx.x];  // fixed order
-    if (db_bf16) reinterpret_cast<uint16_t*>(db)[c] = ew_f2bf(a);
-    else reinterpret_cast<float*>(db)[c] = a;
+  if (db && threadIdx.x < EW_AD_TC * 8) {
+    const int c = blockIdx.x * EW_AD_TC * 8 + threadIdx.x;
+    if (c < C) {
+      float a = 0.0f;
+#pragma unroll
+      for (int w = 0; w < EW_WAVES; ++w) a += part[w][threadIdx.x];  // fixed order
+      if (db_bf16) reinterpret_cast<uint16_t*>(db)[c] = ew_f2bf(a);
+      else reinterpret_cast<float*>(db)[c] = a;
+    }
   }
   // advance the key counter once every block has read it: arrival ticket ctr[1] (each block's
   // read of ctr[0] completed before its ticket; the new value is seen by the next kernel)
@@ -1046,7 +1082,8 @@ void ew_act_dropout_fwd(uintptr_t y, uintptr_t z, int n, float p, int relu, uint
 void ew_act_dropout_bwd(uintptr_t dz, uintptr_t y, uintptr_t dy, uintptr_t db, int db_bf16,
                         int rows, int C, float p, int relu, uintptr_t ctr, uint32_t salt,
                         uintptr_t stream) {
-  const int g = (C + 31) / 32;
+  if (C % 8) throw std::runtime_error("ewdml act_dropout_bwd: C % 8 != 0");
+  const int g = (C + EW_AD_TC * 8 - 1) / (EW_AD_TC * 8);
   hipLaunchKernelGGL(k_act_dropout_bwd, dim3(g), dim3(EW_BLOCK), 0, (hipStream_t)stream,
                      reinterpret_cast<const uint16_t*>(dz), reinterpret_cast<const uint16_t*>(y),
                      reinterpret_cast<uint16_t*>(dy), reinterpret_cast<void*>(db), db_bf16, rows,

@@ -349,3 +349,32 @@ def test_vgg_head_dropout_masks():
     z2 = head._ActDropout.apply(x.detach(), 0.5, False, head._ctr(d0, x.device))
     assert not torch.equal(z1.detach(), z2)  # the device counter advanced: a new mask
     del fnn
+
+
+@pytest.mark.parametrize("rows,C,p", [(37, 24, 0.0), (300, 40, 0.3), (128, 512, 0.5)])
+def test_linear_act_dropout_backward_edges(rows, C, p):
+    """Linear + ReLU + dropout backward (mask recomputed, bias gradient fused) on row counts and
+    widths off the kernel's tiling (odd rows, C % 16 != 0): against the same mask
+    applied in PyTorch fp32."""
+    from ewdml.ops import head
+
+    _ops()
+    lin = nn.Linear(64, C).cuda()
+    x = torch.randn(rows, 64, device="cuda").to(torch.bfloat16).requires_grad_(True)
+    w = lin.weight.detach().to(torch.bfloat16).requires_grad_(True)
+    b = lin.bias.detach().to(torch.bfloat16).requires_grad_(True)
+    ctr = head._ctr(lin, x.device)
+    z = head._LinearActDropout.apply(x, w, b, p, True, ctr)
+    g = torch.randn_like(z)
+    z.backward(g)
+    y = torch.addmm(b.detach(), x.detach(), w.detach().t()).float()
+    scale = 1.0 / (1.0 - p)
+    keep = (z.float() != 0) | (y <= 0)  # where z == 0 but y > 0 the mask dropped the element
+    if p == 0.0:
+        assert bool(keep.all())
+    dyr = g.float() * (y > 0).float() * keep.float() * scale
+    dyr = dyr.to(torch.bfloat16).float()
+    assert b.grad.dtype == torch.bfloat16
+    assert torch.allclose(b.grad.float(), dyr.sum(0), rtol=1e-2, atol=1e-2)
+    assert _rel(x.grad, dyr @ w.detach().float()) < 1e-2
+    assert _rel(w.grad, dyr.t() @ x.detach().float()) < 1e-2
