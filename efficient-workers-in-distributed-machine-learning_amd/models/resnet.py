@@ -24,7 +24,8 @@ from . import fused
 
 def _conv(m, x):
     """``m(x)``; stride-1 3x3 / 1x1 layers on channels_last bf16 run the MFMA implicit-GEMM
-    kernels (``ewdml.ops.conv``), the others (strided, stem) MIOpen."""
+    kernels (``ewdml.ops.conv``), as does the 3-channel CIFAR stem; the others (strided, the
+    ImageNet 7x7/2 stem) MIOpen."""
     from ..ops.conv import conv2d_module
 
     return conv2d_module(m, x)
@@ -128,7 +129,7 @@ class ResNet(nn.Module):
         if fused.active(x):
             from ..ops.nn import bn_act
 
-            out = bn_act(self.conv1(x), self.bn1, "relu")
+            out = bn_act(_conv(self.conv1, x), self.bn1, "relu")  # CIFAR stem: MFMA stem kernels
         else:
             out = F.relu(self.bn1(self.conv1(x)))
         if self.stem == "imagenet":

@@ -1,12 +1,13 @@
-"""Stride-1 3x3 (pad 1) and 1x1 convolutions on the gfx950 matrix cores (``ops/csrc/conv.hip``).
+"""Stride-1 3x3 (pad 1) and 1x1 convolutions on the gfx950 matrix cores (``ops/csrc/conv.hip``),
+and the 3-input-channel 3x3 stem (``k_conv_stem_*``).
 
 :func:`conv` is ``F.conv2d(x, w, padding=k // 2)`` (no bias: the fused BN kernels fold the conv
 bias) for channels_last bf16 activations and weights, as an autograd function whose forward,
 backward-data and backward-weight are hand-written MFMA implicit-GEMM kernels (fp32 accumulation,
 bf16 results, like MIOpen's bf16 convolutions).  :func:`conv2d_module` dispatches an
 ``nn.Conv2d`` (VGG's and ResNet's stride-1 3x3 / 1x1 layers).  Shapes the kernels do not take (C_in or C_out not a multiple of 64, fp32,
-NCHW, other strides/padding) go to ``F.conv2d`` (MIOpen) -- e.g. VGG's first layer (3 input
-channels).  ``EWDML_CONV=miopen`` (or ``set_enabled(False)``) routes every call to MIOpen (A/B).
+NCHW, other strides/padding) go to ``F.conv2d`` (MIOpen) -- e.g. the ImageNet ResNet's 7x7/2
+stem.  ``EWDML_CONV=miopen`` (or ``set_enabled(False)``) routes every call to MIOpen (A/B).
 
 Parity: the reference's convolutions are ``nn.Conv2d(..., kernel_size=3, padding=1)`` in
 ``src/model_ops/vgg.py:46-59`` and ``resnet.py:14-36``; only the execution differs.
@@ -42,31 +43,50 @@ def _ws(device):
     return w
 
 
-def supported(x, w, stride=1, padding=None, dilation=1, groups=1) -> bool:
-    """True if the MFMA kernels take ``conv2d(x, w, stride, padding, dilation, groups)``: a 3x3
-    kernel with padding 1 or a 1x1 kernel with padding 0, stride 1."""
-    def one(v, want):
-        return v == want or v == (want, want) or v == [want, want]
+def _one(v, want):
+    return v == want or v == (want, want) or v == [want, want]
 
+
+def _geometry_ok(x, w, stride, padding, dilation, groups, sizes=(1, 3)):
     if not (_ENABLED and x.is_cuda and x.dim() == 4 and w.dim() == 4):
         return False
     k = w.shape[-1]
-    if k not in (1, 3) or w.shape[-2] != k:
+    if k not in sizes or w.shape[-2] != k:
         return False
     if padding is None:
         padding = k // 2
-    if not (one(stride, 1) and one(padding, k // 2) and one(dilation, 1) and groups == 1):
+    if not (_one(stride, 1) and _one(padding, k // 2) and _one(dilation, 1) and groups == 1):
         return False
-    if x.dtype != torch.bfloat16 or w.dtype != torch.bfloat16:
+    if x.dtype != torch.bfloat16 or w.dtype != torch.bfloat16 or w.shape[1] != x.shape[1]:
+        return False
+    return (x.is_contiguous(memory_format=torch.channels_last)
+            and w.is_contiguous(memory_format=torch.channels_last))
+
+
+def stem_supported(x, w, stride=1, padding=None, dilation=1, groups=1) -> bool:
+    """True for the stem kernels: a 3x3 / pad 1 / stride 1 conv over 3 input channels (VGG's
+    first layer, the CIFAR ResNet stem), C_out % 64 == 0, N*H*W % 256 == 0, W <= 256."""
+    if not _geometry_ok(x, w, stride, padding, dilation, groups, sizes=(3,)):
         return False
     N, C, H, W = x.shape
+    return (C == 3 and w.shape[0] % 64 == 0 and (N * H * W) % 256 == 0 and W <= 256
+            and N * H * W * 3 < 2 ** 31 and N * H * W * w.shape[0] < 2 ** 31
+            and x.data_ptr() % 16 == 0)
+
+
+def supported(x, w, stride=1, padding=None, dilation=1, groups=1) -> bool:
+    """True if the MFMA kernels take ``conv2d(x, w, stride, padding, dilation, groups)``: a 3x3
+    kernel with padding 1 or a 1x1 kernel with padding 0, stride 1 (C_in % 64 == 0), or the
+    3-channel stem (:func:`stem_supported`)."""
+    if not _geometry_ok(x, w, stride, padding, dilation, groups):
+        return False
+    if stem_supported(x, w, stride, padding, dilation, groups):
+        return True
+    N, C, H, W = x.shape
     Nc = w.shape[0]
-    if w.shape[1] != C or C % 64 or Nc % 64 or (N * H * W) % 64:
+    if C % 64 or Nc % 64 or (N * H * W) % 64:
         return False
     if x.numel() >= 2 ** 31 or N * H * W * Nc >= 2 ** 31:
-        return False
-    if not (x.is_contiguous(memory_format=torch.channels_last)
-            and w.is_contiguous(memory_format=torch.channels_last)):
         return False
     return x.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0
 
@@ -112,10 +132,53 @@ class _Conv(torch.autograd.Function):
         return dx, dw
 
 
+class _ConvStem(torch.autograd.Function):
+    """3-channel 3x3 stem: MFMA forward (+ BN partials) and weight gradient; the input gradient
+    (not needed when x is the network input) goes to MIOpen."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        C_ = require()
+        N, C, H, W = x.shape
+        Nc = w.shape[0]
+        y = torch.empty((N, Nc, H, W), dtype=x.dtype, device=x.device,
+                        memory_format=torch.channels_last)
+        part = torch.empty(max(1, 2 * (N * H * W // 128) * Nc), dtype=torch.float32,
+                           device=x.device)
+        rows = C_.conv_stem_fwd(_ptr(x), _ptr(w), _ptr(y), N, H, W, Nc, _ptr(part), part.numel(),
+                                _stream())
+        ctx.save_for_backward(x, w)
+        ctx.bn_part = (part, rows) if rows > 0 else None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        C_ = require()
+        x, w = ctx.saved_tensors
+        N, C, H, W = x.shape
+        Nc = w.shape[0]
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        if dy.dtype != x.dtype:
+            dy = dy.to(x.dtype)
+        if dy.data_ptr() % 16:  # 16-B loads of dy rows
+            dy = dy.clone(memory_format=torch.channels_last)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.ops.aten.convolution_backward(
+                dy, x, w, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1, [True, False, False])[0]
+        if ctx.needs_input_grad[1]:
+            ws = _ws(x.device)
+            dw = torch.empty_like(w, memory_format=torch.channels_last)
+            C_.conv_stem_wgrad(_ptr(dy), _ptr(x), _ptr(dw), _ptr(ws), ws.numel(), N, H, W, Nc,
+                               _stream())
+        return dx, dw
+
+
 def _apply(x, w):
-    y = _Conv.apply(x, w)
+    fn = _ConvStem if x.shape[1] == 3 else _Conv
+    y = fn.apply(x, w)
     # hand the epilogue's BatchNorm partials to the consumer (bn_act reads ``_ew_bn_part``)
-    node = y.grad_fn  # the autograd ctx of _Conv (None under no_grad)
+    node = y.grad_fn  # the autograd ctx of _Conv / _ConvStem (None under no_grad)
     part = getattr(node, "bn_part", None) if node is not None else None
     if part is not None:
         y._ew_bn_part = part

@@ -679,6 +679,221 @@ __global__ __launch_bounds__(EW_BLOCK) void k_cv_slab_reduce(const float* __rest
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Stem convolution: 3x3 / pad 1 / stride 1 over 3 input channels (VGG's first layer, the CIFAR
+// ResNet stem).  The reduction K = 9 taps x 3 channels = 27, in the order of the channels_last
+// weight [n][r][s][c], zero-padded to 32: one v_mfma_f32_16x16x32_bf16 step covers it, so the
+// layer is bound by writing its output (forward) or reading its output gradient (weight
+// gradient).  MIOpen runs it as a grouped-conv forward and, for the weight gradient, a zero-fill +
+// igemm + cast chain (~42 us per VGG-11 step, profiles/vgg11_bs128_*).
+typedef unsigned short cv_u16x8 __attribute__((ext_vector_type(8)));
+constexpr int ST_K = 27;
+
+constexpr int ST_WMAX = 256;  // image width bound of the LDS input patch
+
+// The input pixels a block of PIX output pixels [m0, m0 + PIX) reads, [m0 - W - 1, m0 + PIX + W
+// + 1) (clamped to the tensor), are one contiguous NHWC range: it goes to LDS as 16-B chunks and
+// the im2col gathers read LDS.  Returns the element offset of patch[0].
+template <int PIX>
+__device__ __forceinline__ int st_patch(const uint16_t* __restrict__ x, int m0, int W, int M,
+                                        uint16_t* patch, int t) {
+  int lo = (m0 - W - 1) * 3;
+  lo = lo < 0 ? 0 : (lo & ~7);
+  int hi = ((m0 + PIX + W + 1) * 3 + 7) & ~7;
+  hi = hi > 3 * M ? 3 * M : hi;
+  const int nch = (hi - lo) >> 3;
+  for (int c = t; c < nch; c += EW_BLOCK)
+    *reinterpret_cast<cv_u4*>(patch + 8 * c) = *reinterpret_cast<const cv_u4*>(x + lo + 8 * c);
+  return lo;
+}
+template <int PIX>
+constexpr int st_patch_elems() { return (PIX + 2 * ST_WMAX + 2) * 3 + 16; }
+
+// im2col element k (tap-major) of pixel m at (h, w) from the patch: 0 outside the image and for
+// k >= 27
+__device__ __forceinline__ uint16_t st_x(const uint16_t* patch, int lo, int m, int h, int w,
+                                         int H, int W, int k) {
+  const int tap = k / 3, c = k - 3 * tap;
+  const int dr = tap / 3 - 1, dc = tap - 3 * (tap / 3) - 1;
+  const bool ok = k < ST_K && (unsigned)(h + dr) < (unsigned)H && (unsigned)(w + dc) < (unsigned)W;
+  return ok ? patch[(m + dr * W + dc) * 3 + c - lo] : (uint16_t)0;
+}
+
+// Forward: block = 4 waves over 128 pixels x 64 output channels; wave v owns pixels
+// [32 v, 32 v + 32) (2 x 4 MFMA tiles).  A fragments are gathered from the LDS input patch
+// (each im2col element is read by exactly one lane), the weight tile goes through LDS, the bf16
+// tile is staged in LDS for 16-B coalesced stores, and the BatchNorm partial sums of the stored
+// values (one row per block, the BN finalize layout) come from the registers.
+__global__ __launch_bounds__(EW_BLOCK) void k_conv_stem_fwd(const uint16_t* __restrict__ x,
+                                                            const uint16_t* __restrict__ w,
+                                                            uint16_t* __restrict__ y, int H,
+                                                            int W, int Nc, int M,
+                                                            float* __restrict__ bnpart,
+                                                            int nrows) {
+  __shared__ __attribute__((aligned(16))) uint16_t patch[st_patch_elems<128>()];
+  __shared__ __attribute__((aligned(16))) uint16_t wsm[64 * 32];
+  __shared__ __attribute__((aligned(16))) uint16_t ysm[128 * 64];
+  __shared__ float red[EW_WAVES][2][64];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int m0 = blockIdx.x * 128, n0 = blockIdx.y * 64;
+  for (int e = t; e < 64 * 32; e += EW_BLOCK) {
+    const int n = e >> 5, k = e & 31;
+    wsm[e] = k < ST_K ? w[(long long)(n0 + n) * ST_K + k] : (uint16_t)0;
+  }
+  const int lo = st_patch<128>(x, m0, W, M, patch, t);
+  __syncthreads();
+  const int kb = 8 * (lane >> 4), HW = H * W;
+  bf16x8 a[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int m = m0 + 32 * wv + 16 * i + (lane & 15);
+    const int p = m % HW, h = p / W, ww = p - h * W;
+    cv_u16x8 v;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = st_x(patch, lo, m, h, ww, H, W, kb + e);
+    a[i] = __builtin_bit_cast(bf16x8, v);
+  }
+  f32x4 acc[2][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const bf16x8 b = *reinterpret_cast<const bf16x8*>(wsm + (16 * j + (lane & 15)) * 32 + kb);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+      acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b, acc[i][j], 0, 0, 0);
+    }
+  }
+  float sm[4], sq[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    sm[j] = sq[j] = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint16_t hb = ew_f2bf(acc[i][j][q]);
+        ysm[(32 * wv + 16 * i + 4 * (lane >> 4) + q) * 64 + 16 * j + (lane & 15)] = hb;
+        const float v = __uint_as_float((uint32_t)hb << 16);
+        sm[j] += v;
+        sq[j] += v * v;
+      }
+  }
+  if (bnpart) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      sm[j] += __shfl_xor(sm[j], 16, 64);
+      sq[j] += __shfl_xor(sq[j], 16, 64);
+      sm[j] += __shfl_xor(sm[j], 32, 64);
+      sq[j] += __shfl_xor(sq[j], 32, 64);
+    }
+    if (lane < 16) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        red[wv][0][16 * j + lane] = sm[j];
+        red[wv][1][16 * j + lane] = sq[j];
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int e = t + EW_BLOCK * u, r = e >> 3, ch = e & 7;
+    *reinterpret_cast<cv_u4*>(y + (long long)(m0 + r) * Nc + n0 + ch * 8) =
+        *reinterpret_cast<const cv_u4*>(ysm + r * 64 + ch * 8);
+  }
+  if (bnpart && t < 64) {
+    float s1 = 0.0f, s2 = 0.0f;
+#pragma unroll
+    for (int v = 0; v < EW_WAVES; ++v) {  // fixed order
+      s1 += red[v][0][t];
+      s2 += red[v][1][t];
+    }
+    bnpart[(long long)blockIdx.x * Nc + n0 + t] = s1;
+    bnpart[(long long)(nrows + blockIdx.x) * Nc + n0 + t] = s2;
+  }
+}
+
+// Weight gradient dw[n][k] = sum_m dy[m][n] x~[m][k]: block = 256 pixels x 64 output channels,
+// staged as four [64 m][64 n] dy images and four [64 m][32 k] im2col images (transposed-read
+// layout, cv_toff), wave v computes rows n0 + [16 v, 16 v + 16) x all 32 k; fp32 partial
+// [64][27] per block into the slab, summed by k_conv_stem_reduce.
+__global__ __launch_bounds__(EW_BLOCK) void k_conv_stem_wgrad(const uint16_t* __restrict__ dy,
+                                                              const uint16_t* __restrict__ x,
+                                                              float* __restrict__ slab, int H,
+                                                              int W, int Nc, int M) {
+  __shared__ __attribute__((aligned(16))) char As[4 * 8192];
+  __shared__ __attribute__((aligned(16))) char Bs[4 * 8192];
+  __shared__ __attribute__((aligned(16))) uint16_t patch[st_patch_elems<256>()];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int m0 = blockIdx.x * 256, n0 = blockIdx.y * 64, HW = H * W;
+  cv_u4 d[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int e = t + EW_BLOCK * u, r = e >> 3, ch = e & 7;
+    d[u] = *reinterpret_cast<const cv_u4*>(dy + (long long)(m0 + r) * Nc + n0 + ch * 8);
+  }
+  const int lo = st_patch<256>(x, m0, W, M, patch, t);
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int e = t + EW_BLOCK * u, r = e >> 2, ch = e & 3;
+    const int m = m0 + r, p = m % HW, h = p / W, ww = p - h * W;
+    cv_u16x8 v;
+#pragma unroll
+    for (int e2 = 0; e2 < 8; ++e2) v[e2] = st_x(patch, lo, m, h, ww, H, W, 8 * ch + e2);
+    *reinterpret_cast<cv_u16x8*>(Bs + (r >> 6) * 8192 + cv_toff(r & 63, ch)) = v;
+  }
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int e = t + EW_BLOCK * u, r = e >> 3, ch = e & 7;
+    *reinterpret_cast<cv_u4*>(As + (r >> 6) * 8192 + cv_toff(r & 63, ch)) = d[u];
+  }
+  __syncthreads();
+  f32x4 acc[1][2];
+  acc[0][0] = acc[0][1] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+  for (int img = 0; img < 4; ++img)
+    cv_mma_tr<1, 2>(As + img * 8192, Bs + img * 8192, 16 * wv, 0, lane, acc);
+  float* sp = slab + (long long)blockIdx.x * Nc * ST_K;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int k = 16 * j + (lane & 15);
+    if (k < ST_K) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        sp[(long long)(n0 + 16 * wv + 4 * (lane >> 4) + q) * ST_K + k] = acc[0][j][q];
+    }
+  }
+}
+
+// dw[o] = sum over the nb block partials slab[b][o] in a fixed order: block = 8 outputs x 32
+// partial chunks, chunk sums combined through LDS pairwise.
+__global__ __launch_bounds__(EW_BLOCK) void k_conv_stem_reduce(const float* __restrict__ slab,
+                                                               int nb, int n,
+                                                               uint16_t* __restrict__ dw) {
+  __shared__ float red[32][8];
+  const int t = threadIdx.x, o = blockIdx.x * 8 + (t & 7), ck = t >> 3;
+  float s = 0.0f;
+  if (o < n) {
+    const int per = (nb + 31) / 32, b0 = ck * per, b1 = min(b0 + per, nb);
+    int b = b0;
+    for (; b + 3 < b1; b += 4) {
+      const float v0 = slab[(long long)b * n + o], v1 = slab[(long long)(b + 1) * n + o];
+      const float v2 = slab[(long long)(b + 2) * n + o], v3 = slab[(long long)(b + 3) * n + o];
+      s += (v0 + v1) + (v2 + v3);
+    }
+    for (; b < b1; ++b) s += slab[(long long)b * n + o];
+  }
+  red[ck][t & 7] = s;
+  __syncthreads();
+#pragma unroll
+  for (int h = 16; h > 0; h >>= 1) {
+    if (ck < h) red[ck][t & 7] += red[ck + h][t & 7];
+    __syncthreads();
+  }
+  if (ck == 0 && o < n) dw[o] = ew_f2bf(red[0][t & 7]);
+}
+
 // Launch shape of one conv GEMM: tiles, global split of the reduction, k-groups per block.
 // Enough blocks for every CU (split-K slabs only below 128 tiles), then k-groups so that about
 // 16 waves share each CU: resident blocks per CU r = ceil(blocks / 256), KG = 4 / r (<= kgmax).
@@ -845,4 +1060,41 @@ void ew_conv_wgrad(uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws, long l
                        reinterpret_cast<const float*>(ws), p.split, n, reinterpret_cast<uint16_t*>(dw));
     EW_CHECK_LAUNCH();
   }
+}
+
+// ---- stem convolution (3 input channels) ----
+int ew_conv_stem_fwd(uintptr_t x, uintptr_t w, uintptr_t y, long long N, int H, int W, int Nc,
+                     uintptr_t bnpart, long long bnpart_floats, uintptr_t stream) {
+  const long long M = N * H * W;
+  if (M % 128 || Nc % 64 || M >= (1LL << 31) / 3 || W > ST_WMAX)
+    throw std::runtime_error("ewdml conv stem: needs N*H*W % 128 == 0, Nc % 64 == 0, W <= 256");
+  const int nrows = (int)(M / 128);
+  float* bnp = (bnpart && nrows <= 1024 && 2LL * nrows * Nc <= bnpart_floats)
+                   ? reinterpret_cast<float*>(bnpart) : nullptr;
+  hipLaunchKernelGGL(k_conv_stem_fwd, dim3(nrows, Nc / 64), dim3(EW_BLOCK), 0,
+                     (hipStream_t)stream, reinterpret_cast<const uint16_t*>(x),
+                     reinterpret_cast<const uint16_t*>(w), reinterpret_cast<uint16_t*>(y), H, W,
+                     Nc, (int)M, bnp, nrows);
+  EW_CHECK_LAUNCH();
+  return bnp ? nrows : 0;
+}
+
+void ew_conv_stem_wgrad(uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws,
+                        long long ws_floats, long long N, int H, int W, int Nc,
+                        uintptr_t stream) {
+  const long long M = N * H * W;
+  const long long nb = M / 256, n = (long long)Nc * ST_K;
+  if (M % 256 || Nc % 64 || nb * n > ws_floats - 64 || W > ST_WMAX ||
+      M >= (1LL << 31) / 3)
+    throw std::runtime_error("ewdml conv stem: wgrad needs N*H*W % 256 == 0, Nc % 64 == 0, "
+                             "W <= 256");
+  hipStream_t s = (hipStream_t)stream;
+  float* slab = reinterpret_cast<float*>(ws);
+  hipLaunchKernelGGL(k_conv_stem_wgrad, dim3((int)nb, Nc / 64), dim3(EW_BLOCK), 0, s,
+                     reinterpret_cast<const uint16_t*>(dy), reinterpret_cast<const uint16_t*>(x),
+                     slab, H, W, Nc, (int)M);
+  EW_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_conv_stem_reduce, dim3((int)((n + 7) / 8)), dim3(EW_BLOCK), 0, s, slab,
+                     (int)nb, (int)n, reinterpret_cast<uint16_t*>(dw));
+  EW_CHECK_LAUNCH();
 }

@@ -155,6 +155,12 @@ void ew_conv_bwd_data(uintptr_t dy, uintptr_t w, uintptr_t dx, uintptr_t ws,
                       uintptr_t stream);
 void ew_conv_wgrad(uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws, long long ws_floats,
                    long long N, int H, int W, int C, int Nc, int ksize, uintptr_t stream);
+// stem conv: 3x3 / pad 1 over C = 3 input channels (x [N,H,W,3], w [Nc,3,3,3] channels_last);
+// forward returns the BN partial rows written (0: none); wgrad uses ws as its partial slab
+int ew_conv_stem_fwd(uintptr_t x, uintptr_t w, uintptr_t y, long long N, int H, int W, int Nc,
+                     uintptr_t bnpart, long long bnpart_floats, uintptr_t stream);
+void ew_conv_stem_wgrad(uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws,
+                        long long ws_floats, long long N, int H, int W, int Nc, uintptr_t stream);
 
 // ---- cross-entropy loss (nn.hip): mean over B rows of [B, K] logits (bf16 or fp32), int64 labels
 void ew_cross_entropy_fwd(uintptr_t x, uintptr_t y, int B, int K, int is_bf16, uintptr_t loss,

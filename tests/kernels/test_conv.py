@@ -168,7 +168,8 @@ def test_resnet50_mfma_conv_matches_miopen_step():
 
 
 @pytest.mark.parametrize("N,C,Nc,H,W,k", [(128, 64, 128, 16, 16, 3), (16, 128, 256, 8, 8, 3),
-                                          (128, 512, 512, 2, 2, 3), (16, 64, 256, 32, 32, 1)])
+                                          (128, 512, 512, 2, 2, 3), (16, 64, 256, 32, 32, 1),
+                                          (128, 3, 64, 32, 32, 3)])
 def test_conv_epilogue_bn_statistics(N, C, Nc, H, W, k):
     """The forward epilogue's BatchNorm partial sums (consumed by the fused BN, which then skips
     its statistics pass) give the same normalisation and running statistics as the BN kernels'
@@ -190,3 +191,40 @@ def test_conv_epilogue_bn_statistics(N, C, Nc, H, W, k):
     assert torch.allclose(bn0.running_mean, bn1.running_mean, rtol=1e-4, atol=1e-6)
     assert torch.allclose(bn0.running_var, bn1.running_var, rtol=1e-4, atol=1e-6)
     assert int(bn0.num_batches_tracked) == int(bn1.num_batches_tracked) == 1
+
+
+STEM_SHAPES = [
+    (128, 64, 32, 32),   # VGG conv1 / CIFAR ResNet stem at batch 128
+    (8, 128, 16, 16),    # two output-channel tiles
+    (4, 64, 8, 8),       # M = 256: one weight-gradient block
+    (2, 64, 16, 24),     # H != W
+]
+
+
+@pytest.mark.parametrize("N,Nc,H,W", STEM_SHAPES)
+def test_conv_stem_forward_backward(N, Nc, H, W):
+    """3-input-channel stem kernels: forward and weight gradient against fp32 PyTorch; the input
+    gradient (MIOpen) when requested."""
+    conv = _conv()
+    x, w = _data(N, 3, Nc, H, W, seed=11)
+    assert conv.stem_supported(x, w) and conv.supported(x, w)
+    g = torch.Generator(device="cuda").manual_seed(12)
+    dy = torch.randn(N, Nc, H, W, device="cuda", generator=g).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    xa, wa = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
+    y = conv.conv(xa, wa)
+    assert y.grad_fn is not None and "Stem" in type(y.grad_fn).__name__
+    y.backward(dy)
+    xr, wr = x.float().requires_grad_(True), w.float().requires_grad_(True)
+    ref = F.conv2d(xr, wr, padding=1)
+    ref.backward(dy.float())
+    assert y.dtype == torch.bfloat16 and y.is_contiguous(memory_format=torch.channels_last)
+    err = (y.float() - ref.detach()).abs()
+    assert bool((err <= ref.detach().abs() * 2 ** -7 + 1e-3).all()), float(err.max())
+    assert wa.grad.dtype == torch.bfloat16
+    assert _rel(wa.grad, wr.grad) < 6e-3, _rel(wa.grad, wr.grad)
+    assert _rel(xa.grad, xr.grad) < 1e-2, _rel(xa.grad, xr.grad)
+    # the network-input case: no input gradient, weight gradient only
+    wb = w.clone().requires_grad_(True)
+    conv.conv(x, wb).backward(dy)
+    assert torch.equal(wb.grad, wa.grad)  # fixed-order partial reduction: deterministic

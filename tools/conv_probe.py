@@ -50,6 +50,12 @@ def hip_times(x, w, dy):
     dx = torch.empty_like(x)
     dw = torch.empty_like(w)
     st = ops._stream
+    if C == 3:  # stem kernels: forward and weight gradient (no input gradient)
+        tf = timeit(lambda: C_.conv_stem_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), N, H, W,
+                                             Nc, 0, 0, st()))
+        tw = timeit(lambda: C_.conv_stem_wgrad(dy.data_ptr(), x.data_ptr(), dw.data_ptr(),
+                                               ws.data_ptr(), ws.numel(), N, H, W, Nc, st()))
+        return tf, float("nan"), tw
     tf = timeit(lambda: C_.conv_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), ws.data_ptr(),
                                        ws.numel(), N, H, W, C, Nc, 3, 0, 0, st()))
     tb = timeit(lambda: C_.conv_bwd_data(dy.data_ptr(), w.data_ptr(), dx.data_ptr(),
@@ -93,7 +99,7 @@ def main():
         h = hip_times(x.detach(), w.detach(), dy.contiguous(memory_format=torch.channels_last))
         if h is not None:
             for i in range(3):
-                htot[i] += h[i]
+                htot[i] += h[i] if h[i] == h[i] else 0.0
             print(f"      hip mfma | fwd {h[0]:8.1f} ({fl / h[0] / 1e6:6.0f} TF/s) | bwd_data "
                   f"{h[1]:8.1f} ({fl / h[1] / 1e6:6.0f}) | wgrad {h[2]:8.1f} ({fl / h[2] / 1e6:6.0f})")
     print(f"total: fwd {tot[0]:.1f} gemm {tot[1]:.1f} bwd_data {tot[2]:.1f} wrw {tot[3]:.1f} us")
