@@ -4,7 +4,7 @@
 // (NCHW or channels_last) and dtype (fp32 or bf16) conversion, label gather.
 //
 // The batch position comes from a device-resident state {pos, epoch}, so the launch can live
-// inside the captured HIP graph: the last block to finish advances pos (threadfence + atomic
+// inside the captured HIP graph: the last block to finish advances pos (arrival-ticket
 // done-counter, reset by that block), the host only rewrites the state at an epoch boundary.
 // Augmentation draws are a counter hash of (seed, rank, epoch, sample slot): reproducible and
 // independent of launch order or graph replay.
@@ -60,19 +60,18 @@ __global__ __launch_bounds__(EW_BLOCK) void k_make_batch(
     }
     if (rem == 0) out_y[b] = labels[sample];
   }
-  // the last block to finish advances the batch position (every block has read it by then)
-  __shared__ bool last;
+  // The last block to arrive advances the batch position for the next launch.  No fences: the
+  // only cross-block hazard is a block reading state[0] after it was advanced, and every block's
+  // read completed before its barrier (the workgroup barrier waits for outstanding loads), hence
+  // before its arrival ticket; the next kernel sees the new value at the kernel boundary.  (An
+  // agent-scope release fence per block costs an L2 write-back on gfx950.)
   __syncthreads();
   if (threadIdx.x == 0) {
-    __threadfence();
-    last = atomicAdd(done, 1u) == gridDim.x - 1;
-  }
-  __syncthreads();
-  if (last && threadIdx.x == 0) {
-    __threadfence();
-    state[0] = pos + 1;
-    *done = 0u;
-    __threadfence();
+    const unsigned tk = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tk == gridDim.x - 1) {
+      state[0] = pos + 1;
+      *done = 0u;
+    }
   }
 }
 
