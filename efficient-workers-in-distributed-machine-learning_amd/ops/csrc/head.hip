@@ -1,0 +1,353 @@
+// Classifier-head Linear layers (VGG: Dropout, Linear, ReLU, Dropout, Linear, ReLU, Linear) as
+// small MFMA GEMMs with the elementwise work folded into their operand loads and epilogues.
+//
+// Why: at batch 128 every head GEMM is ~128 x 512 x 512 -- a few microseconds of work each -- and
+// PyTorch (hipBLASLt + separate ReLU / dropout / bias-gradient kernels) runs the head as 22
+// launches per step (~114 us, profiles/vgg11_*: more than 10% of the VGG-11 step).  Here one
+// kernel per Linear and direction (6 per step):
+//   forward   z = drop_out(act(drop_in(x) W^T + b))     drop_in applied to the A operand on load,
+//             bias / ReLU / dropout in the epilogue (pre-activation y stored for the backward)
+//   backward  dy = bf16(dz * act'(y) * keep_out / (1 - p_out)) recomputed on load, and one grid
+//             of two block roles: dW = dy^T drop_in(x) (+ db = sum over rows of dy) and
+//             dx = (dy W) * keep_in / (1 - p_in)
+// Masks come from the counter hash of ops/csrc/nn.hip (key from a per-layer device counter,
+// element index r * width + c); the backward's last block advances the counters (arrival
+// ticket, no fences: every block read them before arriving).
+//
+// Tiles: one 16 x 16 output tile per block (v_mfma_f32_16x16x32_bf16), the reduction split over
+// the block's 4 waves (every wave issues all its loads before its first MFMA; partial tiles summed
+// through LDS): a 128 x 512 x 512 GEMM is 256 blocks with ~4 loads in flight per lane instead of
+// a few long dependent k-loops.  Operands go straight from L2 into the fragment registers (each
+// fragment element is used by one lane; the whole head's operands are ~1.5 MB).
+#include "common.h"
+#include "ewdml_ops.h"
+
+namespace {
+
+typedef __bf16 hd_bf16x8 __attribute__((ext_vector_type(8)));
+typedef float hd_f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned short hd_u16x8 __attribute__((ext_vector_type(8)));
+
+struct HdDrop {
+  const int* ctr;  // device counter: ctr[0] = mask step, ctr[1] = backward arrival ticket
+  uint32_t salt;
+  float p;  // 0: no dropout
+};
+
+__device__ __forceinline__ uint32_t hd_key(const HdDrop& d) {
+  return d.p > 0.0f ? ew_mix32((uint32_t)d.ctr[0] * 0x9E3779B9u + d.salt) : 0u;
+}
+__device__ __forceinline__ float hd_scale(const HdDrop& d) {
+  return d.p > 0.0f ? 1.0f / (1.0f - d.p) : 1.0f;
+}
+// keep * 1/(1-p) of element i (the forward's mask)
+__device__ __forceinline__ float hd_mask(uint32_t i, uint32_t key, float p, float scale) {
+  return ew_uniform(i, key) >= p ? scale : 0.0f;
+}
+__device__ __forceinline__ float hd_f(uint16_t v) { return ew_bf16f(v); }
+// torch ReLU semantics (NaN propagates), as the NHWC BN kernels
+__device__ __forceinline__ float hd_relu(float v) { return (v > 0.0f || v != v) ? v : 0.0f; }
+__device__ __forceinline__ bool hd_relu_pass(float v) { return !(v <= 0.0f); }
+__device__ __forceinline__ float hd_rnd(float v) { return hd_f(ew_f2bf(v)); }
+
+// Sum the 4 waves' 16 x 16 accumulators (each wave took a quarter of the reduction) into wave 0's,
+// in a fixed order.
+__device__ __forceinline__ void hd_wave_reduce(hd_f32x4& acc, float* red, int wv, int lane) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) red[(wv * 4 + q) * 64 + lane] = acc[q];
+  __syncthreads();
+  if (wv == 0) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      acc[q] = (red[q * 64 + lane] + red[(4 + q) * 64 + lane]) +
+               (red[(8 + q) * 64 + lane] + red[(12 + q) * 64 + lane]);
+  }
+}
+
+// ---- forward: z[B][N] = drop_out(act(drop_in(x) w^T + b)), y = pre-activation (optional) ----
+// Block: one 16 x 16 output tile; wave v takes the k-steps v, v + 4, ... (all its loads issued
+// before the first MFMA), the 4 partial tiles are summed through LDS.
+template <bool RELU>
+__global__ __launch_bounds__(EW_BLOCK) void k_head_fwd(const uint16_t* __restrict__ x,
+                                                       const uint16_t* __restrict__ w,
+                                                       const uint16_t* __restrict__ b,
+                                                       uint16_t* __restrict__ z,
+                                                       uint16_t* __restrict__ y, int B, int N,
+                                                       int K, HdDrop din, HdDrop dout) {
+  __shared__ float red[16 * 64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, li = lane & 15;
+  const int r = blockIdx.x * 16 + li;  // A row (batch row) of this lane
+  const int n = blockIdx.y * 16 + li;  // B row (output feature) of this lane
+  const int kq = 8 * (lane >> 4);
+  const bool rok = r < B, nok = n < N;
+  const uint16_t* xp = x + (long long)(rok ? r : 0) * K + kq;
+  const uint16_t* wp = w + (long long)(nok ? n : 0) * K + kq;
+  const uint32_t kin = hd_key(din);
+  const float sin = hd_scale(din);
+  const hd_u16x8 zero = {0, 0, 0, 0, 0, 0, 0, 0};
+  const int nsteps = K / 32;
+  hd_f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+  for (int s0 = wv; s0 < nsteps; s0 += 16) {  // up to 4 steps of this wave in flight
+    hd_u16x8 av[4], bv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int s = s0 + 4 * u;
+      const bool ok = s < nsteps;
+      av[u] = (ok && rok) ? *reinterpret_cast<const hd_u16x8*>(xp + 32 * s) : zero;
+      bv[u] = (ok && nok) ? *reinterpret_cast<const hd_u16x8*>(wp + 32 * s) : zero;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int s = s0 + 4 * u;
+      if (s >= nsteps) break;
+      hd_u16x8 a = av[u];
+      if (din.p > 0.0f) {  // the head's input Dropout, on the A operand (rounded like a stored z)
+        const uint32_t i0 = (uint32_t)r * (uint32_t)K + (uint32_t)(32 * s + kq);
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          a[e] = ew_f2bf(hd_f(a[e]) * hd_mask(i0 + e, kin, din.p, sin));
+      }
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(hd_bf16x8, a),
+                                                    __builtin_bit_cast(hd_bf16x8, bv[u]), acc,
+                                                    0, 0, 0);
+    }
+  }
+  hd_wave_reduce(acc, red, wv, lane);
+  // C/D layout: column li (output feature), rows 4 (lane >> 4) + q (batch rows)
+  if (wv != 0 || !nok) return;
+  const float bias = b ? hd_f(b[n]) : 0.0f;
+  const uint32_t kout = hd_key(dout);
+  const float sout = hd_scale(dout);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int rr = blockIdx.x * 16 + 4 * (lane >> 4) + q;
+    if (rr >= B) continue;
+    const long long o = (long long)rr * N + n;
+    const uint16_t yb = ew_f2bf(acc[q] + bias);  // the GEMM's bf16 output (bias in fp32)
+    if (y) y[o] = yb;
+    float v = hd_f(yb);
+    if (RELU) v = hd_relu(v);
+    if (dout.p > 0.0f) v = v * hd_mask((uint32_t)o, kout, dout.p, sout);
+    z[o] = ew_f2bf(v);
+  }
+}
+
+// dy = bf16(dz * act'(y) * keep_out / (1 - p_out)) of element o (the value the GEMMs consume)
+template <bool RELU>
+__device__ __forceinline__ float hd_dyv(uint16_t dzv, uint16_t yv, uint32_t o, uint32_t kout,
+                                        const HdDrop& dout, float sout) {
+  float v = hd_f(dzv);
+  if (RELU && !hd_relu_pass(hd_f(yv))) v = 0.0f;
+  if (dout.p > 0.0f) v = v * hd_mask(o, kout, dout.p, sout);
+  return hd_rnd(v);
+}
+
+// ---- backward: blocks [0, nbw) 16 x 16 weight-gradient tiles (+ bias gradient), the rest
+// 16 x 16 input-gradient tiles; in both, wave v takes a quarter of the reduction ----
+template <bool RELU>
+__global__ __launch_bounds__(EW_BLOCK) void k_head_bwd(
+    const uint16_t* __restrict__ dz, const uint16_t* __restrict__ y,
+    const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, uint16_t* __restrict__ dx,
+    uint16_t* __restrict__ dw, void* __restrict__ db, int db_bf16, int B, int N, int K,
+    HdDrop dout, HdDrop din, int nbw, int* __restrict__ adv0, int* __restrict__ adv1) {
+  __shared__ float red[16 * 64];
+  __shared__ float dbr[4][16];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const uint32_t kout = hd_key(dout), kin = hd_key(din);
+  const float sout = hd_scale(dout), sin = hd_scale(din);
+  hd_f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+  const int n16 = (N + 15) / 16, b16 = (B + 15) / 16;
+  if ((int)blockIdx.x < nbw) {
+    // dW[n][k] = sum_r dy[r][n] x~[r][k]: A = dy^T (rows n), B = x~^T (rows k), reduction over
+    // the batch rows in 32-row steps; wave v: steps v, v + 4, ...
+    const int tn = blockIdx.x % n16, tk = blockIdx.x / n16;
+    const int n = tn * 16 + li, k = tk * 16 + li;
+    const bool nok = n < N, kok = k < K;
+    const int nc = nok ? n : 0, kc = kok ? k : 0;
+    float dbs = 0.0f;
+    for (int r0 = 32 * wv; r0 < B; r0 += 128) {
+      uint16_t dv[8], yv[8], xv[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {  // clamped rows: loads issued unconditionally, masked below
+        const int rc = min(r0 + 8 * g + e, B - 1);
+        dv[e] = dz[(long long)rc * N + nc];
+        yv[e] = RELU ? y[(long long)rc * N + nc] : (uint16_t)0;
+        xv[e] = x[(long long)rc * K + kc];
+      }
+      hd_u16x8 a, bb;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int rr = r0 + 8 * g + e;
+        const bool ok = rr < B;
+        const float d = (ok && nok)
+                            ? hd_dyv<RELU>(dv[e], yv[e], (uint32_t)rr * (uint32_t)N + (uint32_t)n,
+                                           kout, dout, sout)
+                            : 0.0f;
+        dbs += d;
+        a[e] = ew_f2bf(d);
+        float xf = 0.0f;
+        if (ok && kok) {
+          xf = hd_f(xv[e]);
+          if (din.p > 0.0f)
+            xf = hd_rnd(xf * hd_mask((uint32_t)rr * (uint32_t)K + (uint32_t)k, kin, din.p, sin));
+        }
+        bb[e] = ew_f2bf(xf);
+      }
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(hd_bf16x8, a),
+                                                    __builtin_bit_cast(hd_bf16x8, bb), acc, 0, 0,
+                                                    0);
+    }
+    // bias gradient (tiles of column block 0): the A operand's sums over the rows
+    dbs += __shfl_xor(dbs, 16, 64);
+    dbs += __shfl_xor(dbs, 32, 64);
+    if (g == 0) dbr[wv][li] = dbs;
+    hd_wave_reduce(acc, red, wv, lane);  // (its barrier also publishes dbr)
+    if (wv == 0) {
+      // C/D: column li -> k, rows 4 g + q -> n
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int nn = tn * 16 + 4 * g + q;
+        if (nn < N && kok) dw[(long long)nn * K + k] = ew_f2bf(acc[q]);
+      }
+      if (db && tk == 0 && g == 0 && nok) {
+        const float t = (dbr[0][li] + dbr[1][li]) + (dbr[2][li] + dbr[3][li]);
+        if (db_bf16) reinterpret_cast<uint16_t*>(db)[n] = ew_f2bf(t);
+        else reinterpret_cast<float*>(db)[n] = t;
+      }
+    }
+  } else if (dx) {
+    // dx[r][k] = (sum_n dy[r][n] w[n][k]) * keep_in: A = dy (rows r), B = w^T (rows k),
+    // reduction over the output features in 32-wide steps; wave v: steps v, v + 4, ...
+    const int bx = blockIdx.x - nbw, tr = bx % b16, tk = bx / b16;
+    const int r = tr * 16 + li, k = tk * 16 + li;
+    const bool rok = r < B, kok = k < K;
+    const int rc = rok ? r : 0, kc = kok ? k : 0;
+    const bool vec = (N % 8) == 0;
+    const int nsteps = (N + 31) / 32;
+    for (int s = wv; s < nsteps; s += 4) {
+      const int nb = 32 * s + 8 * g;
+      uint16_t dv[8], yv[8], wv8[8];
+      if (vec && nb < N) {  // 16-B loads of this row's dz / y (N % 8 == 0: nb + 8 <= N)
+        const long long o = (long long)rc * N + nb;
+        const hd_u16x8 d8 = *reinterpret_cast<const hd_u16x8*>(dz + o);
+        hd_u16x8 y8 = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (RELU) y8 = *reinterpret_cast<const hd_u16x8*>(y + o);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          dv[e] = d8[e];
+          yv[e] = y8[e];
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int nn = min(nb + e, N - 1);
+          dv[e] = dz[(long long)rc * N + nn];
+          yv[e] = RELU ? y[(long long)rc * N + nn] : (uint16_t)0;
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) wv8[e] = w[(long long)min(nb + e, N - 1) * K + kc];
+      hd_u16x8 a, bb;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int nn = nb + e;
+        const bool ok = nn < N;
+        a[e] = (ok && rok) ? ew_f2bf(hd_dyv<RELU>(dv[e], yv[e],
+                                                  (uint32_t)r * (uint32_t)N + (uint32_t)nn, kout,
+                                                  dout, sout))
+                           : (uint16_t)0;
+        bb[e] = (ok && kok) ? wv8[e] : (uint16_t)0;
+      }
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(hd_bf16x8, a),
+                                                    __builtin_bit_cast(hd_bf16x8, bb), acc, 0, 0,
+                                                    0);
+    }
+    hd_wave_reduce(acc, red, wv, lane);
+    if (wv == 0 && kok) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int rr = tr * 16 + 4 * g + q;
+        if (rr >= B) continue;
+        const long long o = (long long)rr * K + k;
+        float v = acc[q];
+        if (din.p > 0.0f) v = v * hd_mask((uint32_t)o, kin, din.p, sin);
+        dx[o] = ew_f2bf(v);
+      }
+    }
+  }
+  // advance the dropout counters once every block has read them (arrival ticket on adv0[1];
+  // each block's counter reads completed before its barrier, hence before its ticket)
+  if (adv0) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const int t = __hip_atomic_fetch_add(&adv0[1], 1, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+      if (t == (int)gridDim.x - 1) {
+        adv0[1] = 0;
+        adv0[0] = adv0[0] + 1;
+        if (adv1) adv1[0] = adv1[0] + 1;
+      }
+    }
+  }
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------------
+// host side
+
+static HdDrop hd_drop(uintptr_t ctr, uint32_t salt, float p) {
+  HdDrop d{reinterpret_cast<const int*>(ctr), salt, ctr ? p : 0.0f};
+  if (!(d.p >= 0.0f && d.p < 1.0f)) throw std::runtime_error("ewdml head: dropout p out of [0, 1)");
+  return d;
+}
+
+void ew_head_fwd(uintptr_t x, uintptr_t w, uintptr_t b, uintptr_t z, uintptr_t y, int B, int N,
+                 int K, int relu, uintptr_t ctr_in, uint32_t salt_in, float p_in,
+                 uintptr_t ctr_out, uint32_t salt_out, float p_out, uintptr_t stream) {
+  if (B <= 0 || N <= 0 || K % 32)
+    throw std::runtime_error("ewdml head: needs B, N > 0 and K % 32 == 0");
+  const HdDrop din = hd_drop(ctr_in, salt_in, p_in), dout = hd_drop(ctr_out, salt_out, p_out);
+  const dim3 grid((B + 15) / 16, (N + 15) / 16);
+#define HD_FWD(R)                                                                               \
+  hipLaunchKernelGGL(k_head_fwd<R>, grid, dim3(EW_BLOCK), 0, (hipStream_t)stream,              \
+                     reinterpret_cast<const uint16_t*>(x), reinterpret_cast<const uint16_t*>(w), \
+                     reinterpret_cast<const uint16_t*>(b), reinterpret_cast<uint16_t*>(z),      \
+                     reinterpret_cast<uint16_t*>(y), B, N, K, din, dout)
+  if (relu) HD_FWD(true);
+  else HD_FWD(false);
+#undef HD_FWD
+  EW_CHECK_LAUNCH();
+}
+
+void ew_head_bwd(uintptr_t dz, uintptr_t y, uintptr_t x, uintptr_t w, uintptr_t dx, uintptr_t dw,
+                 uintptr_t db, int db_bf16, int B, int N, int K, int relu, uintptr_t ctr_out,
+                 uint32_t salt_out, float p_out, uintptr_t ctr_in, uint32_t salt_in, float p_in,
+                 int advance, uintptr_t stream) {
+  if (B <= 0 || N <= 0 || K % 32)
+    throw std::runtime_error("ewdml head: needs B, N > 0 and K % 32 == 0");
+  if (relu && !y) throw std::runtime_error("ewdml head: ReLU backward needs the pre-activation");
+  const HdDrop dout = hd_drop(ctr_out, salt_out, p_out), din = hd_drop(ctr_in, salt_in, p_in);
+  const int nbw = ((N + 15) / 16) * ((K + 15) / 16);
+  const int nbx = dx ? ((B + 15) / 16) * ((K + 15) / 16) : 0;
+  // counters to advance: the masks this launch recomputed (forward and backward read one step)
+  int* a0 = nullptr;
+  int* a1 = nullptr;
+  if (advance) {
+    int* c_in = din.p > 0.0f ? reinterpret_cast<int*>(ctr_in) : nullptr;
+    int* c_out = dout.p > 0.0f ? reinterpret_cast<int*>(ctr_out) : nullptr;
+    a0 = c_in ? c_in : c_out;
+    a1 = (c_in && c_out && c_out != c_in) ? c_out : nullptr;
+  }
+#define HD_BWD(R)                                                                               \
+  hipLaunchKernelGGL(k_head_bwd<R>, dim3(nbw + nbx), dim3(EW_BLOCK), 0, (hipStream_t)stream,   \
+                     reinterpret_cast<const uint16_t*>(dz), reinterpret_cast<const uint16_t*>(y), \
+                     reinterpret_cast<const uint16_t*>(x), reinterpret_cast<const uint16_t*>(w), \
+                     reinterpret_cast<uint16_t*>(dx), reinterpret_cast<uint16_t*>(dw),          \
+                     reinterpret_cast<void*>(db), db_bf16, B, N, K, dout, din, nbw, a0, a1)
+  if (relu) HD_BWD(true);
+  else HD_BWD(false);
+#undef HD_BWD
+  EW_CHECK_LAUNCH();
+}

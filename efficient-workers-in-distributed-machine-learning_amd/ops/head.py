@@ -1,14 +1,16 @@
-"""VGG classifier head (``Dropout, Linear, ReLU, Dropout, Linear, ReLU, Linear``) on the GPU with
-hand-written activation/dropout kernels (``ops/csrc/nn.hip``: ``k_act_dropout_fwd/bwd``).
+"""VGG classifier head (``Dropout, Linear, ReLU, Dropout, Linear, ReLU, Linear``) on the GPU:
+one hand-written MFMA kernel per Linear and direction (``ops/csrc/head.hip``).
 
 Per step PyTorch runs the head as 9 forward and 13 backward kernels (dropout x2, ReLU clamps,
-GEMMs, bias-gradient reductions, dropout / threshold backward) plus two per-replay RNG offset
-fills under HIP graphs.  Here: the Linear GEMMs stay on hipBLASLt (``addmm`` with the bias in the
-epilogue), each ``ReLU -> Dropout`` / ``ReLU`` / ``Dropout`` is one kernel per direction, and the
-backward kernel also writes the preceding Linear's bias gradient -- 6 forward and 10 backward
-kernels, same math as ``nn.Dropout`` / ``nn.ReLU`` / ``nn.Linear`` (masks from a counter-based
-hash keyed per step by a device counter, so masks differ from PyTorch's generator; the keep
-probability and 1/(1-p) scaling are the same).
+hipBLASLt GEMMs, bias-gradient reductions, dropout / threshold backward) plus two per-replay RNG
+offset fills under HIP graphs (~114 us of a ~1.05 ms VGG-11 step).  Here 3 forward and 3 backward
+kernels: the input Dropout is applied to the first GEMM's operand on load, bias + ReLU + Dropout
+run in the GEMM epilogue, and each backward launch recomputes its masks on load and computes the
+weight, bias and input gradients together.  Same math as ``nn.Dropout`` / ``nn.ReLU`` /
+``nn.Linear`` with bf16 operands and fp32 accumulation; masks come from a counter-based hash keyed
+per step by a per-layer device counter (so they differ from PyTorch's generator; the keep
+probability and 1/(1-p) scaling are the same).  :class:`_ActDropout` (one act/dropout kernel per
+direction, ``ops/csrc/nn.hip``) remains as a standalone op.
 
 Parity: the reference's classifier, ``src/model_ops/vgg.py:15-43``.
 """
@@ -67,33 +69,54 @@ class _ActDropout(torch.autograd.Function):
         return dy, None, None, None
 
 
-class _LinearActDropout(torch.autograd.Function):
-    """z = act(x W^T + b) * mask / (1 - p); backward fuses the bias gradient into the mask pass."""
+def _drop_args(d):
+    """(counter pointer, salt, p) of a dropout spec ``(ctr, salt, p)`` or None."""
+    if d is None or d[2] <= 0.0:
+        return 0, 0, 0.0
+    return _ptr(d[0]), int(d[1]) & 0xFFFFFFFF, float(d[2])
+
+
+class _HeadLinear(torch.autograd.Function):
+    """z = drop_out(act(drop_in(x) W^T + b)); ``din`` / ``dout``: dropout specs (ctr, salt, p) or
+    None.  The backward launch advances the counters of the masks it recomputed when
+    ``advance``."""
 
     @staticmethod
-    def forward(ctx, x, w, b, p, relu, ctr):
+    def forward(ctx, x, w, b, relu, din, dout, advance):
         C_ = require()
-        y = torch.addmm(b, x, w.t())
-        z = torch.empty_like(y)
-        C_.act_dropout_fwd(_ptr(y), _ptr(z), y.numel(), p, int(relu), _ptr(ctr), _SALT, _stream())
-        ctx.p, ctx.relu, ctx.salt = p, relu, _SALT
-        ctx.save_for_backward(x, w, y, ctr)
+        B, K = x.shape
+        N = w.shape[0]
+        z = torch.empty((B, N), dtype=x.dtype, device=x.device)
+        y = torch.empty((B, N), dtype=x.dtype, device=x.device) if relu else None
+        C_.head_fwd(_ptr(x), _ptr(w), _ptr(b), _ptr(z), _ptr(y), B, N, K, int(relu),
+                    *_drop_args(din), *_drop_args(dout), _stream())
+        ctx.relu, ctx.din, ctx.dout, ctx.advance = relu, din, dout, advance
+        ctx.save_for_backward(x, w, y)
         return z
 
     @staticmethod
     def backward(ctx, dz):
         C_ = require()
-        x, w, y, ctr = ctx.saved_tensors
+        x, w, y = ctx.saved_tensors
         dz = dz.contiguous()
-        rows, C = y.shape
-        dy = torch.empty_like(y)
-        db = torch.empty(C, dtype=w.dtype, device=w.device)
-        C_.act_dropout_bwd(_ptr(dz), _ptr(y), _ptr(dy), _ptr(db), int(db.dtype == torch.bfloat16),
-                           rows, C, ctx.p, int(ctx.relu), _ptr(ctr), ctx.salt, _stream())
+        if dz.data_ptr() % 16:
+            dz = dz.clone()
+        B, K = x.shape
+        N = w.shape[0]
         need = ctx.needs_input_grad
-        dx = dy @ w if need[0] else None
-        dw = dy.t() @ x if need[1] else None
-        return dx, dw, (db if need[2] else None), None, None, None
+        dx = torch.empty_like(x) if need[0] else None
+        dw = torch.empty_like(w)
+        db = torch.empty(N, dtype=w.dtype, device=w.device)
+        C_.head_bwd(_ptr(dz), _ptr(y), _ptr(x), _ptr(w), _ptr(dx), _ptr(dw), _ptr(db),
+                    int(db.dtype == torch.bfloat16), B, N, K, int(ctx.relu),
+                    *_drop_args(ctx.dout), *_drop_args(ctx.din), int(ctx.advance), _stream())
+        return dx, (dw if need[1] else None), (db if need[2] else None), None, None, None, None
+
+
+def head_linear(x, lin, relu=False, din=None, dout=None, advance=True):
+    """``drop_out(act(lin(drop_in(x))))`` through the head kernels; ``din`` / ``dout``: dropout
+    specs ``(counter, salt, p)`` (see :func:`_ctr`) or None."""
+    return _HeadLinear.apply(x, lin.weight, lin.bias, bool(relu), din, dout, bool(advance))
 
 
 def _head_layout(cls):
@@ -107,17 +130,31 @@ def _head_layout(cls):
     return mods if ok else None
 
 
+def _lin_ok(lin, x_width):
+    w, b = lin.weight, lin.bias
+    return (b is not None and w.dtype == torch.bfloat16 and b.dtype == torch.bfloat16
+            and w.is_contiguous() and b.is_contiguous() and w.shape[1] == x_width
+            and x_width % 32 == 0 and w.data_ptr() % 16 == 0)
+
+
 def supported(cls, x) -> bool:
     mods = _head_layout(cls)
     if not _ENABLED or mods is None or not (x.is_cuda and x.dim() == 2 and x.dtype == torch.bfloat16):
         return False
-    l1, l2 = mods[1], mods[4]
-    for lin in (l1, l2):
-        if lin.bias is None or lin.weight.dtype != torch.bfloat16 or lin.bias.dtype != torch.bfloat16:
-            return False
-        if lin.out_features % 8:
-            return False
-    return x.is_contiguous() and x.numel() < 2 ** 31 and x.shape[1] % 8 == 0
+    l1, l2, l3 = mods[1], mods[4], mods[6]
+    if not (_lin_ok(l1, x.shape[1]) and _lin_ok(l2, l1.out_features)
+            and _lin_ok(l3, l2.out_features)):
+        return False
+    return (x.is_contiguous() and x.data_ptr() % 16 == 0 and 0 < x.shape[0]
+            and x.shape[0] * max(x.shape[1], l1.out_features, l2.out_features) < 2 ** 31)
+
+
+def _spec(d, device, layer):
+    """Dropout spec of module ``d`` (None when inactive): its counter, a per-layer salt."""
+    p = _p(d)
+    if p <= 0.0:
+        return None
+    return (_ctr(d, device), (_SALT ^ (0x9E3779B9 * (layer + 1))) & 0xFFFFFFFF, p)
 
 
 def vgg_head(cls, x):
@@ -125,7 +162,7 @@ def vgg_head(cls, x):
     if not supported(cls, x):
         return cls(x)
     d0, l1, _, d1, l2, _, l3 = list(cls)
-    h = _ActDropout.apply(x, _p(d0), False, _ctr(d0, x.device))
-    h = _LinearActDropout.apply(h, l1.weight, l1.bias, _p(d1), True, _ctr(d1, x.device))
-    h = _LinearActDropout.apply(h, l2.weight, l2.bias, 0.0, True, _ctr(l2, x.device))
-    return torch.nn.functional.linear(h, l3.weight, l3.bias)
+    dev = x.device
+    h = head_linear(x, l1, relu=True, din=_spec(d0, dev, 0), dout=_spec(d1, dev, 1))
+    h = head_linear(h, l2, relu=True)
+    return head_linear(h, l3)

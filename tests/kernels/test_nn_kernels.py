@@ -351,30 +351,63 @@ def test_vgg_head_dropout_masks():
     del fnn
 
 
-@pytest.mark.parametrize("rows,C,p", [(37, 24, 0.0), (300, 40, 0.3), (128, 512, 0.5)])
-def test_linear_act_dropout_backward_edges(rows, C, p):
-    """Linear + ReLU + dropout backward (mask recomputed, bias gradient fused) on row counts and
-    widths off the kernel's tiling (odd rows, C % 16 != 0): against the same mask
-    applied in PyTorch fp32."""
+@pytest.mark.parametrize("rows,C,p", [(37, 24, 0.0), (300, 40, 0.3), (128, 512, 0.5),
+                                      (128, 10, 0.0)])
+def test_head_linear_backward_edges(rows, C, p):
+    """Head Linear + ReLU + output dropout (ops/csrc/head.hip): forward and the one-launch
+    backward (mask recomputed, bias gradient fused) on row counts and widths off the 32 x 32
+    tiling, against the same mask applied in PyTorch fp32."""
     from ewdml.ops import head
 
     _ops()
-    lin = nn.Linear(64, C).cuda()
+    lin = nn.Linear(64, C).cuda().to(torch.bfloat16)
     x = torch.randn(rows, 64, device="cuda").to(torch.bfloat16).requires_grad_(True)
-    w = lin.weight.detach().to(torch.bfloat16).requires_grad_(True)
-    b = lin.bias.detach().to(torch.bfloat16).requires_grad_(True)
     ctr = head._ctr(lin, x.device)
-    z = head._LinearActDropout.apply(x, w, b, p, True, ctr)
-    g = torch.randn_like(z)
-    z.backward(g)
-    y = torch.addmm(b.detach(), x.detach(), w.detach().t()).float()
-    scale = 1.0 / (1.0 - p)
-    keep = (z.float() != 0) | (y <= 0)  # where z == 0 but y > 0 the mask dropped the element
+    spec = (ctr, 1234, p) if p > 0 else None
+    z = head.head_linear(x, lin, relu=True, dout=spec)
+    y = torch.addmm(lin.bias.float(), x.detach().float(), lin.weight.float().t())
+    # the forward: bf16(relu(bf16(y)) * mask)
+    keep = (z.float() != 0) | (y.to(torch.bfloat16).float() <= 0)
     if p == 0.0:
         assert bool(keep.all())
-    dyr = g.float() * (y > 0).float() * keep.float() * scale
+    else:
+        frac = float(keep[y > 0.05].float().mean())
+        assert abs(frac - (1 - p)) < 0.08, frac
+    scale = 1.0 / (1.0 - p)
+    zr = torch.relu(y.to(torch.bfloat16).float()) * keep.float() * scale
+    assert _rel(z, zr) < 1e-2
+    assert int(ctr[0]) == 0
+    g = torch.randn_like(z)
+    z.backward(g)
+    if p > 0:
+        assert int(ctr[0]) == 1 and int(ctr[1]) == 0  # advanced once, ticket reset
+    dyr = (g.float() * (y.to(torch.bfloat16).float() > 0).float() * keep.float() * scale)
     dyr = dyr.to(torch.bfloat16).float()
-    assert b.grad.dtype == torch.bfloat16
-    assert torch.allclose(b.grad.float(), dyr.sum(0), rtol=1e-2, atol=1e-2)
-    assert _rel(x.grad, dyr @ w.detach().float()) < 1e-2
-    assert _rel(w.grad, dyr.t() @ x.detach().float()) < 1e-2
+    assert lin.bias.grad.dtype == torch.bfloat16
+    assert torch.allclose(lin.bias.grad.float(), dyr.sum(0), rtol=1e-2, atol=1e-2)
+    assert _rel(x.grad, dyr @ lin.weight.detach().float()) < 1e-2
+    assert _rel(lin.weight.grad, dyr.t() @ x.detach().float()) < 1e-2
+
+
+def test_head_linear_input_dropout():
+    """The input dropout applied on the GEMM's operand load: with W = I the output shows the
+    mask; the input gradient carries the same mask and scale."""
+    from ewdml.ops import head
+
+    _ops()
+    K = 64
+    lin = nn.Linear(K, K).cuda().to(torch.bfloat16)
+    with torch.no_grad():
+        lin.weight.copy_(torch.eye(K))
+        lin.bias.zero_()
+    x = torch.ones(96, K, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    ctr = head._ctr(nn.Dropout(), x.device)
+    z = head.head_linear(x, lin, relu=False, din=(ctr, 77, 0.5))
+    kept = z.float() != 0
+    assert 0.4 < float(kept.float().mean()) < 0.6
+    assert torch.equal(z.float()[kept], torch.full_like(z.float()[kept], 2.0))
+    z.backward(torch.ones_like(z))
+    assert torch.equal(x.grad.float(), kept.float() * 2.0)
+    assert int(ctr[0]) == 1
+    z2 = head.head_linear(x.detach(), lin, relu=False, din=(ctr, 77, 0.5))
+    assert not torch.equal(z2, z.detach())  # next step: new mask
