@@ -74,7 +74,7 @@ class DeviceLoader:
                                   memory_format=fmt)
             self.by = torch.empty(B, dtype=torch.int64, device=self.device)
             self._state = torch.zeros(2, dtype=torch.int64, device=self.device)  # pos, epoch
-            self._done = torch.zeros(1, dtype=torch.int32, device=self.device)
+            self._done = torch.zeros(ops.TICKET_INTS, dtype=torch.int32, device=self.device)
             self._perm = torch.empty(self.per_rank, dtype=torch.int64, device=self.device)
         self._start_epoch(0)
 

@@ -318,6 +318,11 @@ def cast_scale(src, dst, scale=1.0):
 
 
 
+# int32 words of a grid arrival ticket (common.h ew_grid_last: 8 sub-counters + 1 top, 128 B
+# apart); zero-initialised, left zeroed by every launch
+TICKET_INTS = 9 * 32
+
+
 def make_batch(src, labels, perm, state, done, out, out_y, mean, inv_std, pad=4, augment=True,
                seed=0, rank=0):
     """Fused batch construction (``csrc/data.hip``): ``out[b] = normalise(augment(src[perm[pos*B
@@ -338,6 +343,8 @@ def make_batch(src, labels, perm, state, done, out, out_y, mean, inv_std, pad=4,
                      (state, torch.int64, "state"), (out_y, torch.int64, "out_y"),
                      (done, torch.int32, "done")):
         _check(t, dt, n, align=4)
+    if done.numel() < TICKET_INTS:
+        raise ValueError(f"done must hold TICKET_INTS ({TICKET_INTS}) zeroed int32")
     if state.numel() != 2 or out_y.numel() != B or labels.numel() != N:
         raise ValueError("state must be int64[2], out_y int64[B], labels int64[N]")
     if perm.numel() < B or B * H * W >= 2 ** 31:

@@ -262,6 +262,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("maxpool2_nhwc", &ew_maxpool2_nhwc);
   m.def("maxpool2_fwd", &ew_maxpool2_fwd);
   m.def("maxpool2_bwd", &ew_maxpool2_bwd);
+  m.def("ticket_ints", [] { return EW_TICKET_INTS; });
   m.def("make_batch",
         [](uintptr_t src, uintptr_t labels, uintptr_t perm, long long perm_len, uintptr_t state,
            uintptr_t done, uintptr_t out, uintptr_t out_y, int B, int C, int H, int W, int pad, int augment,

@@ -144,6 +144,27 @@ __device__ __forceinline__ void ew_key_advance(const SgdArgs& sa) {
   }
 }
 
+// Grid arrival ticket: called by thread 0 of every block (after the block's last read of the data
+// the winner will update); returns true in exactly one of them, the last block to arrive.  The
+// arrivals are spread over 8 sub-counters 128 B apart plus one top counter: a single counter
+// serialises one atomic per block on one L2 line (~10 us at ~1000 blocks).  `tk` holds
+// EW_TICKET_INTS (ewdml_ops.h) zero-initialised ints and is left zeroed.  No fences: the winner's
+// writes are consumed by later kernels (kernel boundary), and every block read before it arrived.
+__device__ __forceinline__ bool ew_grid_last(int* tk) {
+  const int G = (int)(gridDim.x * gridDim.y * gridDim.z);
+  const int b = (int)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z));
+  const int s = b & 7, members = (G - s + 7) >> 3, groups = G < 8 ? G : 8;
+  int* sub = tk + 32 * s;
+  if (__hip_atomic_fetch_add(sub, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != members - 1)
+    return false;
+  *sub = 0;
+  int* top = tk + 32 * 8;
+  if (__hip_atomic_fetch_add(top, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != groups - 1)
+    return false;
+  *top = 0;
+  return true;
+}
+
 // QSGD stochastic rounding of one value (compress/oracle.py::quantize).
 __device__ __forceinline__ int ew_quantize(float x, float inv, float levels, uint32_t gidx,
                                            uint32_t key) {

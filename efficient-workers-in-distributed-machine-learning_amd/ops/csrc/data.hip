@@ -4,8 +4,8 @@
 // (NCHW or channels_last) and dtype (fp32 or bf16) conversion, label gather.
 //
 // The batch position comes from a device-resident state {pos, epoch}, so the launch can live
-// inside the captured HIP graph: the last block to finish advances pos (arrival-ticket
-// done-counter, reset by that block), the host only rewrites the state at an epoch boundary.
+// inside the captured HIP graph: the last block to finish advances pos (grid arrival ticket in
+// `done`, EW_TICKET_INTS ints), the host only rewrites the state at an epoch boundary.
 // Augmentation draws are a counter hash of (seed, rank, epoch, sample slot): reproducible and
 // independent of launch order or graph replay.
 #include "common.h"
@@ -66,13 +66,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_make_batch(
   // before its arrival ticket; the next kernel sees the new value at the kernel boundary.  (An
   // agent-scope release fence per block costs an L2 write-back on gfx950.)
   __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned tk = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (tk == gridDim.x - 1) {
-      state[0] = pos + 1;
-      *done = 0u;
-    }
-  }
+  if (threadIdx.x == 0 && ew_grid_last(reinterpret_cast<int*>(done))) state[0] = pos + 1;
 }
 
 }  // namespace

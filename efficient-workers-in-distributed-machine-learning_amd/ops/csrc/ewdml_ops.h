@@ -155,6 +155,9 @@ void ew_conv_bwd_data(uintptr_t dy, uintptr_t w, uintptr_t dx, uintptr_t ws,
                       uintptr_t stream);
 void ew_conv_wgrad(uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws, long long ws_floats,
                    long long N, int H, int W, int C, int Nc, int ksize, uintptr_t stream);
+// int32 words of a grid arrival ticket (common.h ew_grid_last): 8 sub-counters + 1 top, 128 B apart
+#define EW_TICKET_INTS (9 * 32)
+
 // classifier-head Linear (head.hip): forward z = drop_out(act(drop_in(x) w^T + b)) (+ y = the
 // pre-activation), backward dw, db, dx from dz in one launch; dropout = (counter, salt, p)
 void ew_head_fwd(uintptr_t x, uintptr_t w, uintptr_t b, uintptr_t z, uintptr_t y, int B, int N,

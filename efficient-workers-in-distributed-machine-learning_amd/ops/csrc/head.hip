@@ -28,8 +28,11 @@ typedef __bf16 hd_bf16x8 __attribute__((ext_vector_type(8)));
 typedef float hd_f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned short hd_u16x8 __attribute__((ext_vector_type(8)));
 
+// device counter: ctr[0] = mask step, ctr[HD_TICKET ...] = the backward's arrival tickets
+// (EW_TICKET_INTS), HD_CTR_INTS ints in all
+constexpr int HD_TICKET = 32;
 struct HdDrop {
-  const int* ctr;  // device counter: ctr[0] = mask step, ctr[1] = backward arrival ticket
+  const int* ctr;
   uint32_t salt;
   float p;  // 0: no dropout
 };
@@ -276,18 +279,13 @@ __global__ __launch_bounds__(EW_BLOCK) void k_head_bwd(
       }
     }
   }
-  // advance the dropout counters once every block has read them (arrival ticket on adv0[1];
+  // advance the dropout counters once every block has read them (grid arrival ticket in adv0;
   // each block's counter reads completed before its barrier, hence before its ticket)
   if (adv0) {
     __syncthreads();
-    if (threadIdx.x == 0) {
-      const int t = __hip_atomic_fetch_add(&adv0[1], 1, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-      if (t == (int)gridDim.x - 1) {
-        adv0[1] = 0;
-        adv0[0] = adv0[0] + 1;
-        if (adv1) adv1[0] = adv1[0] + 1;
-      }
+    if (threadIdx.x == 0 && ew_grid_last(adv0 + HD_TICKET)) {
+      adv0[0] = adv0[0] + 1;
+      if (adv1) adv1[0] = adv1[0] + 1;
     }
   }
 }

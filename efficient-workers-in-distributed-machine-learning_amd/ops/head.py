@@ -31,11 +31,16 @@ def set_seed(seed: int, rank: int = 0):
     _SALT = (int(seed) * 1000003 + int(rank) * 7919 + 0x5EED) & 0xFFFFFFFF
 
 
+# counter words: [0] mask step, [1] act_dropout_bwd's ticket, [32, 32 + TICKET_INTS) the head
+# backward's grid arrival ticket (ops/csrc/head.hip HD_TICKET)
+_CTR_INTS = 32 + 9 * 32
+
+
 def _ctr(mod, device):
-    """Per-layer device counter: [key step, arrival ticket of the backward's blocks]."""
+    """Per-layer device dropout counter (zeros; see ``_CTR_INTS``)."""
     c = getattr(mod, "_ew_drop_ctr", None)
     if c is None or c.device != device:
-        c = torch.zeros(2, dtype=torch.int32, device=device)
+        c = torch.zeros(_CTR_INTS, dtype=torch.int32, device=device)
         mod._ew_drop_ctr = c
     return c
 

@@ -24,7 +24,7 @@ def test_make_batch_matches_oracle(augment, channels_last):
     B = 8
     perm = torch.randperm(64, generator=torch.Generator().manual_seed(1)).cuda()
     state = torch.tensor([2, 5], dtype=torch.int64, device="cuda")  # pos 2, epoch 5
-    done = torch.zeros(1, dtype=torch.int32, device="cuda")
+    done = torch.zeros(ops.TICKET_INTS, dtype=torch.int32, device="cuda")
     fmt = torch.channels_last if channels_last else torch.contiguous_format
     out = torch.empty((B, 3, 32, 32), device="cuda", memory_format=fmt)
     oy = torch.empty(B, dtype=torch.int64, device="cuda")
@@ -34,7 +34,7 @@ def test_make_batch_matches_oracle(augment, channels_last):
     ref, ry = reference_fused_batch(x, y, perm, 2, B, mean, istd, augment, 3, 1, 5)
     assert torch.equal(out.float(), ref)
     assert torch.equal(oy, ry)
-    assert state.tolist() == [3, 5] and int(done) == 0
+    assert state.tolist() == [3, 5] and int(done.abs().sum()) == 0
     # bf16 output = round-to-nearest of the fp32 result
     outb = torch.empty((B, 3, 32, 32), device="cuda", dtype=torch.bfloat16, memory_format=fmt)
     state[0] = 2

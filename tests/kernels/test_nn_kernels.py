@@ -380,7 +380,7 @@ def test_head_linear_backward_edges(rows, C, p):
     g = torch.randn_like(z)
     z.backward(g)
     if p > 0:
-        assert int(ctr[0]) == 1 and int(ctr[1]) == 0  # advanced once, ticket reset
+        assert int(ctr[0]) == 1 and int(ctr[1:].abs().sum()) == 0  # advanced once, tickets reset
     dyr = (g.float() * (y.to(torch.bfloat16).float() > 0).float() * keep.float() * scale)
     dyr = dyr.to(torch.bfloat16).float()
     assert lin.bias.grad.dtype == torch.bfloat16
