@@ -20,6 +20,9 @@ import torch.nn.functional as F
 from . import _ptr, _stream, require
 
 _ENABLED = os.environ.get("EWDML_CONV", "hip") != "miopen"
+# BN-backward statistics of the producing layer in the backward-data epilogue (EWDML_CONV_BN_BWD=0:
+# the BN backward's own statistics pass)
+_BN_BWD = os.environ.get("EWDML_CONV_BN_BWD", "1") != "0"
 _WS = {}
 
 
@@ -30,6 +33,11 @@ def set_enabled(on: bool):
 
 def enabled() -> bool:
     return _ENABLED
+
+
+def set_bn_bwd_fusion(on: bool):
+    global _BN_BWD
+    _BN_BWD = bool(on)
 
 
 def _ws(device):
@@ -91,9 +99,27 @@ def supported(x, w, stride=1, padding=None, dilation=1, groups=1) -> bool:
     return x.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0
 
 
+def _bn_bwd_link(node, x):
+    """(h, code, stats, relu) of the fused BN layer ``node`` whose output is ``x`` (see
+    ``ops.nn.bn_act``), for its backward statistics in this conv's backward-data epilogue."""
+    if node is None:
+        return None
+    try:
+        h, res, code, stats = node.saved_tensors
+    except RuntimeError:  # already freed
+        return None
+    if res is not None or h.dtype != torch.bfloat16 or node.mode not in ("relu", "none"):
+        return None
+    N, C, H, W = x.shape
+    scale = 2 if node.pool else 1
+    if tuple(h.shape) != (N, C, H * scale, W * scale):
+        return None
+    return h, code, stats, int(node.mode == "relu")
+
+
 class _Conv(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w):
+    def forward(ctx, x, w, bn_node=None):
         C_ = require()
         N, C, H, W = x.shape
         Nc, k = w.shape[0], w.shape[-1]
@@ -108,6 +134,7 @@ class _Conv(torch.autograd.Function):
                            _ptr(part), part.numel(), _stream())
         ctx.save_for_backward(x, w)
         ctx.bn_part = (part, rows) if rows > 0 else None
+        ctx.bn_node = bn_node
         return y
 
     @staticmethod
@@ -123,13 +150,26 @@ class _Conv(torch.autograd.Function):
         dx = dw = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x, memory_format=torch.channels_last)
-            C_.conv_bwd_data(_ptr(dy), _ptr(w), _ptr(dx), _ptr(ws), ws.numel(), N, H, W, C, Nc,
-                             k, _stream())
+            node, ctx.bn_node = ctx.bn_node, None
+            link = _bn_bwd_link(node, x)
+            if link is None:
+                C_.conv_bwd_data(_ptr(dy), _ptr(w), _ptr(dx), _ptr(ws), ws.numel(), N, H, W, C,
+                                 Nc, k, 0, 0, 0, 0, 0, 0, _stream())
+            else:
+                # the producing BN layer's backward sums (sum dz, sum dz*(h-mean)) per 64 rows
+                h, code, stats, relu = link
+                part = torch.empty(max(1, 2 * (N * H * W // 64) * C), dtype=torch.float32,
+                                   device=x.device)
+                rows = C_.conv_bwd_data(_ptr(dy), _ptr(w), _ptr(dx), _ptr(ws), ws.numel(), N, H,
+                                        W, C, Nc, k, _ptr(h), _ptr(code), _ptr(stats), relu,
+                                        _ptr(part), part.numel(), _stream())
+                if rows > 0:
+                    node._ew_pre_bwd = (part, rows, dx, dx._version)
         if ctx.needs_input_grad[1]:
             dw = torch.empty_like(w, memory_format=torch.channels_last)
             C_.conv_wgrad(_ptr(dy), _ptr(x), _ptr(dw), _ptr(ws), ws.numel(), N, H, W, C, Nc, k,
                           _stream())
-        return dx, dw
+        return dx, dw, None
 
 
 class _ConvStem(torch.autograd.Function):
@@ -175,8 +215,10 @@ class _ConvStem(torch.autograd.Function):
 
 
 def _apply(x, w):
-    fn = _ConvStem if x.shape[1] == 3 else _Conv
-    y = fn.apply(x, w)
+    if x.shape[1] == 3:
+        y = _ConvStem.apply(x, w)
+    else:
+        y = _Conv.apply(x, w, getattr(x, "_ew_bn_node", None) if _BN_BWD else None)
     # hand the epilogue's BatchNorm partials to the consumer (bn_act reads ``_ew_bn_part``)
     node = y.grad_fn  # the autograd ctx of _Conv / _ConvStem (None under no_grad)
     part = getattr(node, "bn_part", None) if node is not None else None

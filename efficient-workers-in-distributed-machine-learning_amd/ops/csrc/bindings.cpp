@@ -239,12 +239,13 @@ PYBIND11_MODULE(_C, m) {
         [](uintptr_t h, uintptr_t res, uintptr_t dy, uintptr_t code, uintptr_t stats,
            uintptr_t coef, uintptr_t part, uintptr_t dx, uintptr_t dres, uintptr_t dgamma,
            uintptr_t dbeta, uintptr_t dcbias, long long N, int H, int W, int C, int is_bf16,
-           int pool, int mode, int cb_bf16, uintptr_t stream) {
+           int pool, int mode, int cb_bf16, uintptr_t stream, int pre_nblk) {
           BnBwdArgs a{};
           a.h = h; a.res = res; a.dy = dy; a.code = code; a.stats = stats; a.coef = coef;
           a.part = part; a.dx = dx; a.dres = dres; a.dgamma = dgamma; a.dbeta = dbeta;
           a.dcbias = dcbias; a.N = N; a.H = H; a.W = W; a.C = C; a.is_bf16 = is_bf16;
           a.pool = pool; a.mode = mode; a.cb_bf16 = cb_bf16; a.stream = stream;
+          a.pre_nblk = pre_nblk;
           ew_bn_relu_bwd(a);
         });
   m.def("act_dropout_fwd", &ew_act_dropout_fwd);

@@ -221,6 +221,28 @@ __device__ __forceinline__ void cv_group_reduce(f32x4 (&acc)[MI][NJ], char* smem
   }
 }
 
+// BatchNorm-backward statistics folded into a backward-data epilogue.  The launch produces the
+// output gradient dy of a BN(+ReLU)(+2x2 max pool) layer L; with this set, the epilogue also sums,
+// per channel c over its rows, dz = act'(h * scale + shift) * dy and dz * (h - mean) (the
+// k_bn_bwd_stats quantities; sum(h - mean) is 0 up to rounding and is taken as 0), where h is
+// layer L's BN input and, pooled, dy reaches the window position of the forward's argmax code.
+// The BN backward then skips its statistics pass (ops/nn.py, ops/conv.py).
+struct CvBnBwd {
+  const uint16_t* h;      // layer L's BN input [rows (pre-pool)][C]; null: not requested
+  const uint8_t* code;    // pool window codes [rows][C] (null: no pool)
+  const float* stats;     // [4][C]: mean, invstd, scale, shift
+  int relu;               // 0: BN only
+  int Ho, Wo;             // pooled map dims (pool)
+};
+
+// pre-pool row of window position q of pooled row p (nn.hip ew_pool_base / ew_pool_off)
+__device__ __forceinline__ uint32_t cv_pool_row(uint32_t p, uint32_t HoWo, uint32_t Wo,
+                                                uint32_t q) {
+  const uint32_t n = p / HoWo, rem = p - n * HoWo;
+  const uint32_t ho = rem / Wo, wo = rem - ho * Wo;
+  return 4 * n * HoWo + 4 * ho * Wo + 2 * wo + (q >> 1) * (2 * Wo) + (q & 1);
+}
+
 // Epilogue of the NT kernels: fp32 split slab, or bf16 output + (optional) BatchNorm partial sums
 // of the stored output (see k_conv_nt).  Every thread of the block calls it (barriers inside);
 // only k-group 0 (g == 0) holds the reduced accumulators.
@@ -229,7 +251,8 @@ __device__ __forceinline__ void cv_nt_epilogue(const f32x4 (&acc)[MI][NJ], char*
                                                int wm, int wn, int lane, int m0, int n0, int M,
                                                int Nc, uint16_t* __restrict__ out,
                                                float* __restrict__ slab,
-                                               float* __restrict__ bnpart) {
+                                               float* __restrict__ bnpart,
+                                               const CvBnBwd& bb) {
   const int row0 = m0 + wm * (BM / 2), col0 = n0 + wn * (BN / 2);
   if (slab) {
     if (g == 0)
@@ -248,14 +271,36 @@ __device__ __forceinline__ void cv_nt_epilogue(const f32x4 (&acc)[MI][NJ], char*
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       sm[j] = sq[j] = 0.0f;
+      if (bb.h) {  // BN-backward sums of layer L (see CvBnBwd); group 0 only (loads)
+        if (g == 0) {
+          const int c = col0 + j * 16 + (lane & 15);
+          const float mean = bb.stats[c], sc = bb.stats[2 * Nc + c], sh = bb.stats[3 * Nc + c];
+          const uint32_t HoWo = (uint32_t)bb.Ho * bb.Wo;
 #pragma unroll
-      for (int i = 0; i < MI; ++i)
+          for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float v = __uint_as_float((uint32_t)ew_f2bf(acc[i][j][q]) << 16);
-          sm[j] += v;
-          sq[j] += v * v;
+            for (int q = 0; q < 4; ++q) {
+              const uint32_t r = row0 + i * 16 + 4 * (lane >> 4) + q;
+              const float d = __uint_as_float((uint32_t)ew_f2bf(acc[i][j][q]) << 16);
+              uint32_t hr = r;
+              if (bb.code) hr = cv_pool_row(r, HoWo, (uint32_t)bb.Wo, bb.code[(size_t)r * Nc + c]);
+              const float x = __uint_as_float((uint32_t)bb.h[(size_t)hr * Nc + c] << 16);
+              const float v = x * sc + sh;  // the BN kernels' exact arithmetic (no contraction)
+              const float dz = (bb.relu == 0 || !(v <= 0.0f)) ? d : 0.0f;
+              sm[j] += dz;
+              sq[j] += dz * (x - mean);
+            }
         }
+      } else {
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float v = __uint_as_float((uint32_t)ew_f2bf(acc[i][j][q]) << 16);
+            sm[j] += v;
+            sq[j] += v * v;
+          }
+      }
       sm[j] += __shfl_xor(sm[j], 16, 64);
       sq[j] += __shfl_xor(sq[j], 16, 64);
       sm[j] += __shfl_xor(sm[j], 32, 64);
@@ -291,7 +336,8 @@ __global__ __launch_bounds__(EW_BLOCK * KG) void k_conv_nt(const uint16_t* __res
                                                            uint16_t* __restrict__ out,
                                                            float* __restrict__ slab, int M, int H,
                                                            int W, int C, int Nc, int kps,
-                                                           int taps, float* __restrict__ bnpart) {
+                                                           int taps, float* __restrict__ bnpart,
+                                                           CvBnBwd bb) {
   constexpr int PA = BM / 32, PB = BN / 32;   // 16-B vectors per thread per k-step
   constexpr int MI = BM / 32, NJ = BN / 32;   // 16x16 tiles per wave (wave tile BM/2 x BN/2)
   constexpr int STAGE = (BM + BN) * 128;      // bytes of one LDS stage (A then B)
@@ -409,7 +455,8 @@ __global__ __launch_bounds__(EW_BLOCK * KG) void k_conv_nt(const uint16_t* __res
   }
 #undef CV_NT_MMA
   cv_group_reduce<KG, MI, NJ>(acc, smem, g, wq, lane);
-  cv_nt_epilogue<BM, BN, MI, NJ>(acc, smem, g, wm, wn, lane, m0, n0, M, Nc, out, slab, bnpart);
+  cv_nt_epilogue<BM, BN, MI, NJ>(acc, smem, g, wm, wn, lane, m0, n0, M, Nc, out, slab, bnpart,
+                                 bb);
 #undef CV_NT_LOAD
 #undef CV_NT_STORE
 }
@@ -443,7 +490,8 @@ __global__ __launch_bounds__(EW_BLOCK) void k_conv_nt_dma(const uint16_t* __rest
                                                           float* __restrict__ slab, int M, int H,
                                                           int W, int C, int Nc, int kps, int taps,
                                                           float* __restrict__ bnpart,
-                                                          const uint16_t* __restrict__ zero) {
+                                                          const uint16_t* __restrict__ zero,
+                                                          CvBnBwd bb) {
   constexpr int PA = BM / 32, PB = BN / 32;   // glds instructions per wave per k-step (8 rows each)
   constexpr int MI = BM / 32, NJ = BN / 32;
   constexpr int STAGE = (BM + BN) * 128;
@@ -521,7 +569,8 @@ __global__ __launch_bounds__(EW_BLOCK) void k_conv_nt_dma(const uint16_t* __rest
     cv_wait_vm<0>();  // drain the dummy loads before the epilogue reuses the ring
   }
   __syncthreads();
-  cv_nt_epilogue<BM, BN, MI, NJ>(acc, smem, 0, wm, wn, lane, m0, n0, M, Nc, out, slab, bnpart);
+  cv_nt_epilogue<BM, BN, MI, NJ>(acc, smem, 0, wm, wn, lane, m0, n0, M, Nc, out, slab, bnpart,
+                                 bb);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -925,7 +974,7 @@ long long ew_conv_ws_floats() { return 8LL << 20; }  // 32 MiB of fp32 split sla
 
 #define CV_LAUNCH_NT(BM_, KG_, TRB_)                                                             \
   hipLaunchKernelGGL((k_conv_nt<BM_, BM_, KG_, TRB_>), grid, dim3(EW_BLOCK * KG_), 0, s, x, w,  \
-                     out, slab, M, H, W, C, Nc, p.kps, taps, bnp)
+                     out, slab, M, H, W, C, Nc, p.kps, taps, bnp, bbv)
 
 // NT GEMM (forward / backward-data): out[M][Nc] = sum X~[M][9C] w[Nc][9C]^T
 // trb: w is the forward weight [C][9][Nc] of a backward-data GEMM (transposed B images, 64x64
@@ -935,7 +984,7 @@ long long ew_conv_ws_floats() { return 8LL << 20; }  // 32 MiB of fp32 split sla
 static int ew_conv_nt(const uint16_t* x, const uint16_t* w, uint16_t* out, float* ws,
                       long long ws_floats, int M, int H, int W, int C, int Nc, int taps,
                       bool trb, hipStream_t s, float* bnpart = nullptr,
-                      long long bnpart_floats = 0) {
+                      long long bnpart_floats = 0, const CvBnBwd* bnb = nullptr) {
   if (C % CV_BK || Nc % 64 || M % 64)
     throw std::runtime_error("ewdml conv: needs C % 64 == 0, Nc % 64 == 0, N*H*W % 64 == 0");
   const int ksteps = taps * (C / CV_BK);
@@ -959,9 +1008,10 @@ static int ew_conv_nt(const uint16_t* x, const uint16_t* w, uint16_t* out, float
   const long long prow = M / BM;
   float* bnp = (bnpart && !slab && prow <= 1024 && 2 * prow * Nc <= bnpart_floats) ? bnpart
                                                                                   : nullptr;
+  const CvBnBwd bbv = (bnp && bnb) ? *bnb : CvBnBwd{nullptr, nullptr, nullptr, 0, 0, 0};
 #define CV_LAUNCH_DMA(BM_, TRB_)                                                                 \
   hipLaunchKernelGGL((k_conv_nt_dma<BM_, BM_, 4, TRB_>), grid, dim3(EW_BLOCK), 0, s, x, w, out, \
-                     slab, M, H, W, C, Nc, p.kps, taps, bnp, zero)
+                     slab, M, H, W, C, Nc, p.kps, taps, bnp, zero, bbv)
   if (dma) {
     if (big) CV_LAUNCH_DMA(128, false);
     else if (trb) CV_LAUNCH_DMA(64, true);
@@ -1005,15 +1055,23 @@ int ew_conv_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t ws, long long w
                     reinterpret_cast<float*>(bnpart), bnpart_floats);
 }
 
-void ew_conv_bwd_data(uintptr_t dy, uintptr_t w, uintptr_t dx, uintptr_t ws,
-                      long long ws_floats, long long N, int H, int W, int C, int Nc, int ksize,
-                      uintptr_t stream) {
+int ew_conv_bwd_data(uintptr_t dy, uintptr_t w, uintptr_t dx, uintptr_t ws,
+                     long long ws_floats, long long N, int H, int W, int C, int Nc, int ksize,
+                     uintptr_t bn_h, uintptr_t bn_code, uintptr_t bn_stats, int bn_relu,
+                     uintptr_t bnpart, long long bnpart_floats, uintptr_t stream) {
   // the flipped / transposed weight is read in place through transposed B images (no copy)
   if (C % 64 || Nc % 64) throw std::runtime_error("ewdml conv: bwd-data needs C, Nc % 64 == 0");
+  // optional BN-backward sums of the layer whose output gradient dx is (CvBnBwd); with a pool,
+  // dx is at the pooled resolution H x W and bn_h at 2H x 2W
+  const CvBnBwd bb{reinterpret_cast<const uint16_t*>(bn_h),
+                   reinterpret_cast<const uint8_t*>(bn_code),
+                   reinterpret_cast<const float*>(bn_stats), bn_relu, H, W};
   // dx[m][c] = sum over (tap', n) of dY~[m][(tap', n)] * w[n][8 - tap'][c]
-  ew_conv_nt(reinterpret_cast<const uint16_t*>(dy), reinterpret_cast<const uint16_t*>(w),
-             reinterpret_cast<uint16_t*>(dx), reinterpret_cast<float*>(ws), ws_floats,
-             (int)(N * H * W), H, W, Nc, C, cv_taps(ksize), true, (hipStream_t)stream);
+  return ew_conv_nt(reinterpret_cast<const uint16_t*>(dy), reinterpret_cast<const uint16_t*>(w),
+                    reinterpret_cast<uint16_t*>(dx), reinterpret_cast<float*>(ws), ws_floats,
+                    (int)(N * H * W), H, W, Nc, C, cv_taps(ksize), true, (hipStream_t)stream,
+                    bn_h ? reinterpret_cast<float*>(bnpart) : nullptr, bnpart_floats,
+                    bn_h ? &bb : nullptr);
 }
 
 void ew_conv_wgrad(uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws, long long ws_floats,

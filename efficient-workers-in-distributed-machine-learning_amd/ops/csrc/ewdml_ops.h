@@ -113,6 +113,7 @@ struct BnBwdArgs {
   int H, W, C;  // of h (pre-pool)
   int is_bf16, pool, cb_bf16, mode;
   uintptr_t stream;
+  int pre_nblk;  // > 0: `part` already holds [2][pre_nblk][C] sums (sum dz, sum dz*(h-mean))
 };
 int ew_bn_part_floats();
 void ew_bn_relu_fwd(const BnFwdArgs& a);
@@ -150,9 +151,13 @@ long long ew_conv_ws_floats();
 int ew_conv_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t ws, long long ws_floats,
                 long long N, int H, int W, int C, int Nc, int ksize, uintptr_t bnpart,
                 long long bnpart_floats, uintptr_t stream);
-void ew_conv_bwd_data(uintptr_t dy, uintptr_t w, uintptr_t dx, uintptr_t ws,
-                      long long ws_floats, long long N, int H, int W, int C, int Nc, int ksize,
-                      uintptr_t stream);
+// bn_h (nullable): also write the BN-backward sums [2][rows][C] (sum dz, sum dz*(h-mean)) of the
+// BN(+ReLU)(+pool: bn_code) layer whose output gradient dx is into bnpart; returns rows (0: not
+// written, e.g. a split-K launch)
+int ew_conv_bwd_data(uintptr_t dy, uintptr_t w, uintptr_t dx, uintptr_t ws,
+                     long long ws_floats, long long N, int H, int W, int C, int Nc, int ksize,
+                     uintptr_t bn_h, uintptr_t bn_code, uintptr_t bn_stats, int bn_relu,
+                     uintptr_t bnpart, long long bnpart_floats, uintptr_t stream);
 void ew_conv_wgrad(uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws, long long ws_floats,
                    long long N, int H, int W, int C, int Nc, int ksize, uintptr_t stream);
 // int32 words of a grid arrival ticket (common.h ew_grid_last): 8 sub-counters + 1 top, 128 B apart

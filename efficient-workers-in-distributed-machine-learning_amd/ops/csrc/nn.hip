@@ -478,6 +478,9 @@ __global__ __launch_bounds__(EW_BLOCK) void k_bn_bwd_stats(
   }
 }
 
+// NS = 3: partials of k_bn_bwd_stats; NS = 2: of a backward-data conv epilogue (ops/csrc/conv.hip
+// CvBnBwd), whose sum(h - mean) -- 0 up to rounding -- is taken as 0
+template <int NS>
 __global__ __launch_bounds__(EW_BLOCK) void k_bn_bwd_finalize(
     const float* __restrict__ part, int nblk, int C, long long M, const float* __restrict__ stats,
     float* __restrict__ coef, float* __restrict__ dgamma, float* __restrict__ dbeta,
@@ -486,7 +489,8 @@ __global__ __launch_bounds__(EW_BLOCK) void k_bn_bwd_finalize(
   const int lane = threadIdx.x & 63;
   if (c >= C) return;
   double sums[3];
-  ew_sum_parts<3>(part, nblk, C, c, lane, sums);
+  ew_sum_parts<NS>(part, nblk, C, c, lane, sums);
+  if (NS == 2) sums[2] = 0.0;
   if (lane != 0) return;
   const double invstd = stats[C + c], scale = stats[2 * C + c];
   const double db = sums[0];             // sum dz
@@ -761,19 +765,27 @@ static void ew_bn_bwd_impl(const BnBwdArgs& a) {
   int nblk, rpb;
   ew_bn_grid(rows, C, &nblk, &rpb, POOL ? 1 : 2);
   float* part = reinterpret_cast<float*>(a.part);
+  const bool pre = a.pre_nblk > 0 && MODE != EW_BN_ADD_RELU;  // sums from the producing conv
   const T* h = reinterpret_cast<const T*>(a.h);
   const T* res = reinterpret_cast<const T*>(a.res);
   const T* dy = reinterpret_cast<const T*>(a.dy);
   const uint8_t* code = reinterpret_cast<const uint8_t*>(a.code);
   const float* st = reinterpret_cast<const float*>(a.stats);
   float* coef = reinterpret_cast<float*>(a.coef);
-  hipLaunchKernelGGL((k_bn_bwd_stats<T, MODE>), dim3(nblk), dim3(EW_BLOCK), 0, s, h, res, dy,
-                     code, st, rows, C, Ho, Wo, rpb, part);
-  EW_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + EW_WAVES - 1) / EW_WAVES), dim3(EW_BLOCK), 0,
-                     s, part, nblk, C, M, st, coef, reinterpret_cast<float*>(a.dgamma),
-                     reinterpret_cast<float*>(a.dbeta), reinterpret_cast<void*>(a.dcbias),
-                     a.cb_bf16);
+  if (pre) {
+    hipLaunchKernelGGL(k_bn_bwd_finalize<2>, dim3((C + EW_WAVES - 1) / EW_WAVES), dim3(EW_BLOCK),
+                       0, s, part, a.pre_nblk, C, M, st, coef, reinterpret_cast<float*>(a.dgamma),
+                       reinterpret_cast<float*>(a.dbeta), reinterpret_cast<void*>(a.dcbias),
+                       a.cb_bf16);
+  } else {
+    hipLaunchKernelGGL((k_bn_bwd_stats<T, MODE>), dim3(nblk), dim3(EW_BLOCK), 0, s, h, res, dy,
+                       code, st, rows, C, Ho, Wo, rpb, part);
+    EW_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_bn_bwd_finalize<3>, dim3((C + EW_WAVES - 1) / EW_WAVES), dim3(EW_BLOCK),
+                       0, s, part, nblk, C, M, st, coef, reinterpret_cast<float*>(a.dgamma),
+                       reinterpret_cast<float*>(a.dbeta), reinterpret_cast<void*>(a.dcbias),
+                       a.cb_bf16);
+  }
   EW_CHECK_LAUNCH();
   hipLaunchKernelGGL((k_bn_bwd_apply<T, MODE>), dim3(ew_grid_vec(rows * (C / 8))),
                      dim3(EW_BLOCK), 5 * sizeof(float) * C, s, h, res, dy, code, st, coef,

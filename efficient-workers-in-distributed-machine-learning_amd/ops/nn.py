@@ -61,6 +61,8 @@ def _bias(t):
 
 
 _MODES = {"relu": 0, "none": 2, "add_relu": 3}
+# BN backward passes that took their statistics from a conv epilogue (tests / diagnostics)
+PRE_BWD_USED = 0
 
 
 class _BNAct(torch.autograd.Function):
@@ -92,6 +94,7 @@ class _BNAct(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         C_ = require()
+        dy_in = dy
         h, res, code, stats = ctx.saved_tensors
         N, C, H, W = h.shape
         dev = h.device
@@ -106,10 +109,21 @@ class _BNAct(torch.autograd.Function):
         dcb = torch.empty(C, dtype=ctx.cb_dtype, device=dev) if need[2] else None
         dg = torch.empty(C, dtype=torch.float32, device=dev) if need[3] else None
         db = torch.empty(C, dtype=torch.float32, device=dev) if need[4] else None
+        # backward statistics already summed by the conv backward-data launch that produced dy
+        # (ops/conv.py): valid only if dy is exactly that tensor, unmodified (a second consumer
+        # of this layer's output would make dy a sum of gradients)
+        pre = getattr(ctx, "_ew_pre_bwd", None)
+        ctx._ew_pre_bwd = None
+        part, pre_rows = _part(dev), 0
+        if pre is not None and pre[2] is dy_in and dy_in._version == pre[3]:
+            part, pre_rows = pre[0], pre[1]
+            global PRE_BWD_USED
+            PRE_BWD_USED += 1
         C_.bn_relu_bwd(_ptr(h), _ptr(res), _ptr(dy), _ptr(code), _ptr(stats), _ptr(coef),
-                       _ptr(_part(dev)), _ptr(dx), _ptr(dres), _ptr(dg), _ptr(db), _ptr(dcb), N,
+                       _ptr(part), _ptr(dx), _ptr(dres), _ptr(dg), _ptr(db), _ptr(dcb), N,
                        H, W, C, int(h.dtype == torch.bfloat16), int(ctx.pool),
-                       _MODES[ctx.mode], int(ctx.cb_dtype == torch.bfloat16), _stream())
+                       _MODES[ctx.mode], int(ctx.cb_dtype == torch.bfloat16), _stream(),
+                       int(pre_rows))
         return dx, dres, dcb, dg, db, None, None, None, None, None, None, None, None
 
 
@@ -164,10 +178,15 @@ def bn_act(h, bn, mode="relu", res=None, cbias=None, pool=False):
         # num_batches_tracked is incremented by the apply kernel (no separate add kernel)
         nbt = bn.num_batches_tracked if bn.training and bn.track_running_stats else None
         track = bn.training and bn.running_mean is not None
-        return _BNAct.apply(h, res, cbias, bn.weight, bn.bias,
-                            bn.running_mean if track else None,
-                            bn.running_var if track else None, nbt, bn.momentum, bn.eps, pool,
-                            mode, getattr(h, "_ew_bn_part", None))
+        y = _BNAct.apply(h, res, cbias, bn.weight, bn.bias,
+                         bn.running_mean if track else None,
+                         bn.running_var if track else None, nbt, bn.momentum, bn.eps, pool,
+                         mode, getattr(h, "_ew_bn_part", None))
+        if mode != "add_relu" and y.grad_fn is not None:
+            # a following MFMA conv may sum this layer's backward statistics in its
+            # backward-data epilogue (ops/conv.py)
+            y._ew_bn_node = y.grad_fn
+        return y
     if torch.is_grad_enabled() and (h.requires_grad or (res is not None and res.requires_grad)
                                     or (bn.weight is not None and bn.weight.requires_grad)):
         return bn_act_reference(h, cbias, bn, pool, mode, res)

@@ -228,3 +228,41 @@ def test_conv_stem_forward_backward(N, Nc, H, W):
     wb = w.clone().requires_grad_(True)
     conv.conv(x, wb).backward(dy)
     assert torch.equal(wb.grad, wa.grad)  # fixed-order partial reduction: deterministic
+
+
+@pytest.mark.parametrize("mode,pool", [("relu", True), ("relu", False), ("none", False)])
+def test_bn_backward_sums_in_bwd_data_epilogue(mode, pool):
+    """conv -> BN(+ReLU)(+pool) -> conv: the second conv's backward-data epilogue sums the BN's
+    backward statistics (the BN skips its own pass); every gradient matches the unfused path."""
+    import copy
+
+    from ewdml.ops import nn as fnn
+
+    conv = _conv()
+    # 64 x 16 x 16 maps: the second conv's backward-data has >= 128 output tiles (no split-K
+    # launch, which would leave the statistics to the BN pass)
+    x0, w0 = _data(64, 64, 128, 16, 16, seed=21)
+    _, w1 = _data(8, 128, 64, 8, 8, seed=22)
+    bn0 = torch.nn.BatchNorm2d(128).cuda()
+    with torch.no_grad():
+        bn0.weight.uniform_(0.5, 1.5)
+        bn0.bias.uniform_(-0.3, 0.3)
+    g = None
+    grads = []
+    for fused in (True, False):
+        conv.set_bn_bwd_fusion(fused)
+        used = fnn.PRE_BWD_USED
+        bn = copy.deepcopy(bn0)
+        xa, wa, wb = (t.clone().requires_grad_(True) for t in (x0, w0, w1))
+        h = conv.conv(xa, wa)
+        y = fnn.bn_act(h, bn, mode, pool=pool)
+        z = conv.conv(y, wb)
+        if g is None:
+            g = torch.randn(z.shape, device="cuda").to(torch.bfloat16).contiguous(
+                memory_format=torch.channels_last)
+        z.backward(g)
+        assert (fnn.PRE_BWD_USED > used) == fused
+        grads.append([xa.grad, wa.grad, wb.grad, bn.weight.grad, bn.bias.grad])
+    conv.set_bn_bwd_fusion(True)
+    for a, b in zip(*grads):
+        assert _rel(a, b) < 2e-3, _rel(a, b)
