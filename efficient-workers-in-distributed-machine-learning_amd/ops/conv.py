@@ -99,6 +99,12 @@ def supported(x, w, stride=1, padding=None, dilation=1, groups=1) -> bool:
     return x.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0
 
 
+def _part_floats(M, C):
+    """Capacity of a BN partial-sum buffer [2][rows][C]: the epilogue writes one row per 64 (or
+    128) output rows, a split-K reduction up to min(M, 1024) rows (ops/csrc/conv.hip)."""
+    return max(1, 2 * max(M // 64, min(M, 1024)) * C)
+
+
 def _bn_bwd_link(node, x):
     """(h, code, stats, relu) of the fused BN layer ``node`` whose output is ``x`` (see
     ``ops.nn.bn_act``), for its backward statistics in this conv's backward-data epilogue."""
@@ -128,8 +134,7 @@ class _Conv(torch.autograd.Function):
                         memory_format=torch.channels_last)
         # BatchNorm partial sums of y from the epilogue (bounded by 2 rows per 64 output rows);
         # the following fused BN (ops/nn.py bn_act) skips its statistics pass when present
-        part = torch.empty(max(1, 4 * (N * H * W // 64) * Nc), dtype=torch.float32,
-                           device=x.device)
+        part = torch.empty(_part_floats(N * H * W, Nc), dtype=torch.float32, device=x.device)
         rows = C_.conv_fwd(_ptr(x), _ptr(w), _ptr(y), _ptr(ws), ws.numel(), N, H, W, C, Nc, k,
                            _ptr(part), part.numel(), _stream())
         ctx.save_for_backward(x, w)
@@ -158,7 +163,7 @@ class _Conv(torch.autograd.Function):
             else:
                 # the producing BN layer's backward sums (sum dz, sum dz*(h-mean)) per 64 rows
                 h, code, stats, relu = link
-                part = torch.empty(max(1, 2 * (N * H * W // 64) * C), dtype=torch.float32,
+                part = torch.empty(_part_floats(N * H * W, C), dtype=torch.float32,
                                    device=x.device)
                 rows = C_.conv_bwd_data(_ptr(dy), _ptr(w), _ptr(dx), _ptr(ws), ws.numel(), N, H,
                                         W, C, Nc, k, _ptr(h), _ptr(code), _ptr(stats), relu,

@@ -943,6 +943,96 @@ __global__ __launch_bounds__(EW_BLOCK) void k_conv_stem_reduce(const float* __re
   if (ck == 0 && o < n) dw[o] = ew_f2bf(red[0][t & 7]);
 }
 
+// Split-K reduction that also writes the BatchNorm partial sums of its output (the epilogue's job
+// when there is no split): forward sum / sum of squares of the bf16 output, or with bb.h the
+// BN-backward sums of CvBnBwd.  Block b: rows [b * rpb, (b + 1) * rpb) x all Nc columns, thread:
+// column octet t % tpr (tpr = Nc / 8), rows t / tpr + k * rpi; one partial row per block.
+__global__ __launch_bounds__(EW_BLOCK) void k_cv_slab_reduce_bn(const float* __restrict__ slab,
+                                                                int nsplit, int M, int Nc,
+                                                                uint16_t* __restrict__ out,
+                                                                float* __restrict__ bnpart,
+                                                                int rpb, CvBnBwd bb) {
+  __shared__ float red[2][EW_BLOCK * 8];  // [2][rpi][Nc]: rpi * Nc = 8 * EW_BLOCK
+  const int tpr = Nc >> 3, rpi = EW_BLOCK / tpr;
+  const int t = threadIdx.x, g = t % tpr, rg = t / tpr;
+  const int c0 = g * 8;
+  const long long n = (long long)M * Nc;
+  const int r0 = blockIdx.x * rpb, r1 = min(r0 + rpb, M);
+  float s1[8], s2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.0f;
+  float mean[8], sc[8], sh[8];
+  if (bb.h && rg < rpi) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      mean[j] = bb.stats[c0 + j];
+      sc[j] = bb.stats[2 * Nc + c0 + j];
+      sh[j] = bb.stats[3 * Nc + c0 + j];
+    }
+  }
+  const uint32_t HoWo = (uint32_t)bb.Ho * bb.Wo;
+  if (rg < rpi) {
+    for (int r = r0 + rg; r < r1; r += rpi) {
+      const long long o = (long long)r * Nc + c0;
+      float a[8];
+      {
+        const float4* p = reinterpret_cast<const float4*>(slab + o);
+        float4 lo = p[0], hi = p[1];
+        a[0] = lo.x; a[1] = lo.y; a[2] = lo.z; a[3] = lo.w;
+        a[4] = hi.x; a[5] = hi.y; a[6] = hi.z; a[7] = hi.w;
+        for (int z = 1; z < nsplit; ++z) {  // fixed order (as k_cv_slab_reduce)
+          p += n / 4;
+          lo = p[0];
+          hi = p[1];
+          a[0] += lo.x; a[1] += lo.y; a[2] += lo.z; a[3] += lo.w;
+          a[4] += hi.x; a[5] += hi.y; a[6] += hi.z; a[7] += hi.w;
+        }
+      }
+      uint16_t b[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) b[j] = ew_f2bf(a[j]);
+      uint4 ov;
+      ov.x = (uint32_t)b[0] | ((uint32_t)b[1] << 16);
+      ov.y = (uint32_t)b[2] | ((uint32_t)b[3] << 16);
+      ov.z = (uint32_t)b[4] | ((uint32_t)b[5] << 16);
+      ov.w = (uint32_t)b[6] | ((uint32_t)b[7] << 16);
+      *reinterpret_cast<uint4*>(out + o) = ov;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = __uint_as_float((uint32_t)b[j] << 16);
+        if (bb.h) {
+          uint32_t hr = (uint32_t)r;
+          if (bb.code) hr = cv_pool_row((uint32_t)r, HoWo, (uint32_t)bb.Wo, bb.code[o + j]);
+          const float x = __uint_as_float((uint32_t)bb.h[(size_t)hr * Nc + c0 + j] << 16);
+          const float v = x * sc[j] + sh[j];
+          const float dz = (bb.relu == 0 || !(v <= 0.0f)) ? d : 0.0f;
+          s1[j] += dz;
+          s2[j] += dz * (x - mean[j]);
+        } else {
+          s1[j] += d;
+          s2[j] += d * d;
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      red[0][rg * Nc + c0 + j] = s1[j];
+      red[1][rg * Nc + c0 + j] = s2[j];
+    }
+  }
+  __syncthreads();
+  const int nb = gridDim.x;
+  for (int c = t; c < Nc; c += EW_BLOCK) {
+    float a = 0.0f, q = 0.0f;
+    for (int i = 0; i < rpi; ++i) {  // fixed order
+      a += red[0][i * Nc + c];
+      q += red[1][i * Nc + c];
+    }
+    bnpart[(long long)blockIdx.x * Nc + c] = a;
+    bnpart[(long long)(nb + blockIdx.x) * Nc + c] = q;
+  }
+}
+
 // Launch shape of one conv GEMM: tiles, global split of the reduction, k-groups per block.
 // Enough blocks for every CU (split-K slabs only below 128 tiles), then k-groups so that about
 // 16 waves share each CU: resident blocks per CU r = ceil(blocks / 256), KG = 4 / r (<= kgmax).
@@ -1031,6 +1121,22 @@ static int ew_conv_nt(const uint16_t* x, const uint16_t* w, uint16_t* out, float
   EW_CHECK_LAUNCH();
   if (p.split > 1) {
     const long long n = (long long)M * Nc;
+    // with BN partials requested: the reduction writes them (one partial row per block of rpb
+    // rows, <= 1024 rows, as many blocks as possible)
+    const int tpr = Nc / 8, rpi = tpr <= EW_BLOCK ? EW_BLOCK / tpr : 0;
+    int rpb = rpi, nblk = 0;
+    if (bnpart && rpi > 0 && Nc <= 2048 && EW_BLOCK % tpr == 0) {
+      while ((M + rpb - 1) / rpb > 1024) rpb += rpi;
+      nblk = (M + rpb - 1) / rpb;
+      if (2LL * nblk * Nc > bnpart_floats) nblk = 0;
+    }
+    if (nblk > 0) {
+      const CvBnBwd bbr = bnb ? *bnb : CvBnBwd{nullptr, nullptr, nullptr, 0, 0, 0};
+      hipLaunchKernelGGL(k_cv_slab_reduce_bn, dim3(nblk), dim3(EW_BLOCK), 0, s, ws, p.split, M,
+                         Nc, out, bnpart, rpb, bbr);
+      EW_CHECK_LAUNCH();
+      return nblk;
+    }
     long long gr = (n / 8 + EW_BLOCK - 1) / EW_BLOCK;
     if (gr > 2048) gr = 2048;
     hipLaunchKernelGGL(k_cv_slab_reduce, dim3((int)gr), dim3(EW_BLOCK), 0, s, ws, p.split, n, out);

@@ -183,7 +183,8 @@ def test_conv_epilogue_bn_statistics(N, C, Nc, H, W, k):
     bn0 = torch.nn.BatchNorm2d(Nc).cuda()
     bn1 = copy.deepcopy(bn0)
     h = conv.conv(x, w.clone().requires_grad_(True))
-    assert not (N * H * W == 512 and hasattr(h, "_ew_bn_part"))  # split-K launch: no partials
+    # every launch hands its partials over (split-K ones from the slab reduction)
+    assert hasattr(h, "_ew_bn_part")
     y0 = fnn.bn_act(h, bn0, "relu")
     h2 = h.detach().clone()  # same values, no partials attached
     y1 = fnn.bn_act(h2, bn1, "relu")
@@ -231,17 +232,19 @@ def test_conv_stem_forward_backward(N, Nc, H, W):
 
 
 @pytest.mark.parametrize("mode,pool", [("relu", True), ("relu", False), ("none", False)])
-def test_bn_backward_sums_in_bwd_data_epilogue(mode, pool):
-    """conv -> BN(+ReLU)(+pool) -> conv: the second conv's backward-data epilogue sums the BN's
-    backward statistics (the BN skips its own pass); every gradient matches the unfused path."""
+@pytest.mark.parametrize("N,HW", [(64, 16), (32, 4)])
+def test_bn_backward_sums_in_bwd_data_epilogue(mode, pool, N, HW):
+    """conv -> BN(+ReLU)(+pool) -> conv: the second conv's backward-data epilogue (or, for the
+    small maps, its split-K slab reduction) sums the BN's backward statistics (the BN skips its
+    own pass); every gradient matches the unfused path."""
     import copy
 
     from ewdml.ops import nn as fnn
 
     conv = _conv()
-    # 64 x 16 x 16 maps: the second conv's backward-data has >= 128 output tiles (no split-K
-    # launch, which would leave the statistics to the BN pass)
-    x0, w0 = _data(64, 64, 128, 16, 16, seed=21)
+    # 64 x 16 x 16: the second conv's backward-data has >= 128 output tiles (epilogue sums);
+    # 32 x 4 x 4: a split-K launch (sums in the slab reduction)
+    x0, w0 = _data(N, 64, 128, HW, HW, seed=21)
     _, w1 = _data(8, 128, 64, 8, 8, seed=22)
     bn0 = torch.nn.BatchNorm2d(128).cuda()
     with torch.no_grad():
