@@ -268,23 +268,57 @@ __device__ __forceinline__ void cv_nt_epilogue(const f32x4 (&acc)[MI][NJ], char*
     float* red = reinterpret_cast<float*>(smem);  // [wn][2][BN/2]
     const long long nrows = M / BM;
     float sm[NJ], sq[NJ];
+    // BN-backward sums of layer L (see CvBnBwd), group 0 only: all window codes, then all h
+    // values are loaded before any use (two load round trips, not one per element)
+    float xv[NJ][MI][4];
+    if (bb.h && g == 0) {
+      const uint32_t HoWo = (uint32_t)bb.Ho * bb.Wo;
+      uint32_t hr[NJ][MI][4];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) hr[j][i][q] = row0 + i * 16 + 4 * (lane >> 4) + q;
+      if (bb.code) {
+        uint8_t kc[NJ][MI][4];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+          for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              kc[j][i][q] = bb.code[(size_t)hr[j][i][q] * Nc + col0 + j * 16 + (lane & 15)];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+          for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              hr[j][i][q] = cv_pool_row(hr[j][i][q], HoWo, (uint32_t)bb.Wo, kc[j][i][q]);
+      }
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            xv[j][i][q] = __uint_as_float(
+                (uint32_t)bb.h[(size_t)hr[j][i][q] * Nc + col0 + j * 16 + (lane & 15)] << 16);
+    }
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       sm[j] = sq[j] = 0.0f;
-      if (bb.h) {  // BN-backward sums of layer L (see CvBnBwd); group 0 only (loads)
+      if (bb.h) {
         if (g == 0) {
           const int c = col0 + j * 16 + (lane & 15);
           const float mean = bb.stats[c], sc = bb.stats[2 * Nc + c], sh = bb.stats[3 * Nc + c];
-          const uint32_t HoWo = (uint32_t)bb.Ho * bb.Wo;
 #pragma unroll
           for (int i = 0; i < MI; ++i)
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-              const uint32_t r = row0 + i * 16 + 4 * (lane >> 4) + q;
               const float d = __uint_as_float((uint32_t)ew_f2bf(acc[i][j][q]) << 16);
-              uint32_t hr = r;
-              if (bb.code) hr = cv_pool_row(r, HoWo, (uint32_t)bb.Wo, bb.code[(size_t)r * Nc + c]);
-              const float x = __uint_as_float((uint32_t)bb.h[(size_t)hr * Nc + c] << 16);
+              const float x = xv[j][i][q];
               const float v = x * sc + sh;  // the BN kernels' exact arithmetic (no contraction)
               const float dz = (bb.relu == 0 || !(v <= 0.0f)) ? d : 0.0f;
               sm[j] += dz;
