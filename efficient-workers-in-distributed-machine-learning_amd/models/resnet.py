@@ -31,6 +31,32 @@ def _conv(m, x):
     return conv2d_module(m, x)
 
 
+# identity-residual gradients through a GradSink (False: autograd sums them; A/B and tests)
+_RESIDUAL_SINK = True
+
+
+def set_residual_sink(on: bool):
+    global _RESIDUAL_SINK
+    _RESIDUAL_SINK = bool(on)
+
+
+def _residual_block(x, main, bn_last, sc):
+    """``relu(bn_last(main(x, sink)) + shortcut(x))`` on the fused kernels.  With an identity
+    shortcut and an MFMA first conv, the residual's gradient is not summed by autograd: the last
+    BN's backward deposits it in a :class:`GradSink` and the first conv's backward-data epilogue
+    adds it (one launch less per block, and the block input keeps a single consumer, so the
+    previous block's BN can take its backward statistics from that epilogue too)."""
+    from ..ops.conv import GradSink, epilogue_fusion_ok
+    from ..ops.nn import bn_act, kernel_path
+
+    sink = GradSink() if (_RESIDUAL_SINK and len(sc) == 0 and x.requires_grad
+                          and epilogue_fusion_ok(x)) else None
+    h, first_mfma = main(x, sink)
+    if sink is not None and first_mfma and kernel_path(h, bn_last, x):
+        return bn_act(h, bn_last, "add_relu", res=x.detach(), res_sink=sink)
+    return bn_act(h, bn_last, "add_relu", res=_shortcut(sc, x))
+
+
 def _shortcut(sc, x):
     """Identity or projection (1x1 conv + BN, through the fused BN kernel)."""
     if len(sc) == 0:
@@ -56,13 +82,19 @@ class BasicBlock(nn.Module):
                 nn.BatchNorm2d(planes * self.expansion),
             )
 
+    def _main(self, x, sink):
+        """conv2(relu(bn1(conv1(x)))) -> (h, whether conv1 took the sink)."""
+        from ..ops.conv import conv2d_module, module_supported
+        from ..ops.nn import bn_act
+
+        first = sink is not None and module_supported(self.conv1, x)
+        h = conv2d_module(self.conv1, x, sink if first else None)
+        out = bn_act(h, self.bn1, "relu")
+        return _conv(self.conv2, out), first
+
     def forward(self, x):
         if fused.active(x):
-            from ..ops.nn import bn_act
-
-            out = bn_act(_conv(self.conv1, x), self.bn1, "relu")
-            return bn_act(_conv(self.conv2, out), self.bn2, "add_relu",
-                          res=_shortcut(self.shortcut, x))
+            return _residual_block(x, self._main, self.bn2, self.shortcut)
         out = F.relu(self.bn1(self.conv1(x)))
         out = self.bn2(self.conv2(out))
         return F.relu(out + self.shortcut(x))
@@ -86,14 +118,20 @@ class Bottleneck(nn.Module):
                 nn.BatchNorm2d(planes * self.expansion),
             )
 
+    def _main(self, x, sink):
+        """conv3(relu(bn2(conv2(relu(bn1(conv1(x))))))) -> (h, whether conv1 took the sink)."""
+        from ..ops.conv import conv2d_module, module_supported
+        from ..ops.nn import bn_act
+
+        first = sink is not None and module_supported(self.conv1, x)
+        h = conv2d_module(self.conv1, x, sink if first else None)
+        out = bn_act(h, self.bn1, "relu")
+        out = bn_act(_conv(self.conv2, out), self.bn2, "relu")
+        return _conv(self.conv3, out), first
+
     def forward(self, x):
         if fused.active(x):
-            from ..ops.nn import bn_act
-
-            out = bn_act(_conv(self.conv1, x), self.bn1, "relu")
-            out = bn_act(_conv(self.conv2, out), self.bn2, "relu")
-            return bn_act(_conv(self.conv3, out), self.bn3, "add_relu",
-                          res=_shortcut(self.shortcut, x))
+            return _residual_block(x, self._main, self.bn3, self.shortcut)
         out = F.relu(self.bn1(self.conv1(x)))
         out = F.relu(self.bn2(self.conv2(out)))
         out = self.bn3(self.conv3(out))

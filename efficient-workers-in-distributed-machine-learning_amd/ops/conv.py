@@ -23,6 +23,15 @@ _ENABLED = os.environ.get("EWDML_CONV", "hip") != "miopen"
 # BN-backward statistics of the producing layer in the backward-data epilogue (EWDML_CONV_BN_BWD=0:
 # the BN backward's own statistics pass)
 _BN_BWD = os.environ.get("EWDML_CONV_BN_BWD", "1") != "0"
+# ... and the residual-gradient addend (GradSink), only for inputs of at most this many elements:
+# the epilogue reads the extra operands with 2-byte loads in the MFMA output layout, which on
+# large maps costs more than the separate, vectorised statistics / add kernels it replaces
+_EPI_MAX = int(os.environ.get("EWDML_EPI_MAX", str(1 << 23)))
+
+
+def epilogue_fusion_ok(x) -> bool:
+    """Whether a conv on input ``x`` takes the epilogue fusions (BN backward sums, addend)."""
+    return x.numel() <= _EPI_MAX
 _WS = {}
 
 
@@ -114,18 +123,18 @@ def _bn_bwd_link(node, x):
         h, res, code, stats = node.saved_tensors
     except RuntimeError:  # already freed
         return None
-    if res is not None or h.dtype != torch.bfloat16 or node.mode not in ("relu", "none"):
+    if h.dtype != torch.bfloat16 or node.mode not in ("relu", "none", "add_relu"):
         return None
     N, C, H, W = x.shape
     scale = 2 if node.pool else 1
     if tuple(h.shape) != (N, C, H * scale, W * scale):
         return None
-    return h, code, stats, int(node.mode == "relu")
+    return h, res, code, stats, int(node.mode != "none")
 
 
 class _Conv(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, bn_node=None):
+    def forward(ctx, x, w, bn_node=None, sink=None):
         C_ = require()
         N, C, H, W = x.shape
         Nc, k = w.shape[0], w.shape[-1]
@@ -140,6 +149,7 @@ class _Conv(torch.autograd.Function):
         ctx.save_for_backward(x, w)
         ctx.bn_part = (part, rows) if rows > 0 else None
         ctx.bn_node = bn_node
+        ctx.sink = sink
         return y
 
     @staticmethod
@@ -156,25 +166,35 @@ class _Conv(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x, memory_format=torch.channels_last)
             node, ctx.bn_node = ctx.bn_node, None
+            # a second gradient of x handed over by the BN backward of the block's identity
+            # residual (models/resnet.py): added in the epilogue instead of by autograd
+            sink, ctx.sink = ctx.sink, None
+            add = getattr(sink, "grad", None) if sink is not None else None
+            if add is not None and not (add.shape == x.shape and add.dtype == x.dtype
+                                        and add.is_contiguous(memory_format=torch.channels_last)
+                                        and add.data_ptr() % 16 == 0):
+                add = add.contiguous(memory_format=torch.channels_last).to(x.dtype)
             link = _bn_bwd_link(node, x)
             if link is None:
                 C_.conv_bwd_data(_ptr(dy), _ptr(w), _ptr(dx), _ptr(ws), ws.numel(), N, H, W, C,
-                                 Nc, k, 0, 0, 0, 0, 0, 0, _stream())
+                                 Nc, k, 0, 0, 0, 0, 0, 0, 0, _ptr(add), _stream())
             else:
                 # the producing BN layer's backward sums (sum dz, sum dz*(h-mean)) per 64 rows
-                h, code, stats, relu = link
+                h, res, code, stats, relu = link
                 part = torch.empty(_part_floats(N * H * W, C), dtype=torch.float32,
                                    device=x.device)
                 rows = C_.conv_bwd_data(_ptr(dy), _ptr(w), _ptr(dx), _ptr(ws), ws.numel(), N, H,
-                                        W, C, Nc, k, _ptr(h), _ptr(code), _ptr(stats), relu,
-                                        _ptr(part), part.numel(), _stream())
+                                        W, C, Nc, k, _ptr(h), _ptr(res), _ptr(code), _ptr(stats),
+                                        relu, _ptr(part), part.numel(), _ptr(add), _stream())
                 if rows > 0:
                     node._ew_pre_bwd = (part, rows, dx, dx._version)
+            if sink is not None:
+                sink.grad = None
         if ctx.needs_input_grad[1]:
             dw = torch.empty_like(w, memory_format=torch.channels_last)
             C_.conv_wgrad(_ptr(dy), _ptr(x), _ptr(dw), _ptr(ws), ws.numel(), N, H, W, C, Nc, k,
                           _stream())
-        return dx, dw, None
+        return dx, dw, None, None
 
 
 class _ConvStem(torch.autograd.Function):
@@ -219,11 +239,22 @@ class _ConvStem(torch.autograd.Function):
         return dx, dw
 
 
-def _apply(x, w):
+class GradSink:
+    """Hand-over slot for a second gradient of a conv's input (``grad``: set by the producer's
+    backward, consumed and cleared by the conv's backward-data launch)."""
+
+    __slots__ = ("grad",)
+
+    def __init__(self):
+        self.grad = None
+
+
+def _apply(x, w, sink=None):
     if x.shape[1] == 3:
         y = _ConvStem.apply(x, w)
     else:
-        y = _Conv.apply(x, w, getattr(x, "_ew_bn_node", None) if _BN_BWD else None)
+        node = getattr(x, "_ew_bn_node", None) if (_BN_BWD and epilogue_fusion_ok(x)) else None
+        y = _Conv.apply(x, w, node, sink)
     # hand the epilogue's BatchNorm partials to the consumer (bn_act reads ``_ew_bn_part``)
     node = y.grad_fn  # the autograd ctx of _Conv / _ConvStem (None under no_grad)
     part = getattr(node, "bn_part", None) if node is not None else None
@@ -243,10 +274,20 @@ def conv(x, w):
 conv3x3 = conv
 
 
-def conv2d_module(m, x):
+def module_supported(m, x) -> bool:
+    """True if :func:`conv2d_module` runs ``m`` on the MFMA kernels (not the stem)."""
+    return (m.bias is None and m.padding_mode == "zeros" and x.shape[1] != 3
+            and supported(x, m.weight, m.stride, m.padding, m.dilation, m.groups))
+
+
+def conv2d_module(m, x, sink=None):
     """``m(x)`` for an ``nn.Conv2d`` ``m`` without bias, through the MFMA kernels when the layer
-    is a stride-1 3x3/pad-1 or 1x1/pad-0 convolution on channels_last bf16 (else ``m(x)``)."""
+    is a stride-1 3x3/pad-1 or 1x1/pad-0 convolution on channels_last bf16 (else ``m(x)``).
+    ``sink`` (:class:`GradSink`, MFMA path only): a second gradient of ``x`` deposited there
+    before this conv's backward is added to its input gradient."""
     if (m.bias is None and m.padding_mode == "zeros"
             and supported(x, m.weight, m.stride, m.padding, m.dilation, m.groups)):
-        return _apply(x, m.weight)
+        return _apply(x, m.weight, sink)
+    if sink is not None:
+        raise ValueError("a gradient sink needs the MFMA conv path")
     return m(x)

@@ -229,6 +229,7 @@ __device__ __forceinline__ void cv_group_reduce(f32x4 (&acc)[MI][NJ], char* smem
 // The BN backward then skips its statistics pass (ops/nn.py, ops/conv.py).
 struct CvBnBwd {
   const uint16_t* h;      // layer L's BN input [rows (pre-pool)][C]; null: not requested
+  const uint16_t* res;    // its residual input [rows][C] (BN + residual + ReLU), or null
   const uint8_t* code;    // pool window codes [rows][C] (null: no pool)
   const float* stats;     // [4][C]: mean, invstd, scale, shift
   int relu;               // 0: BN only
@@ -247,13 +248,34 @@ __device__ __forceinline__ uint32_t cv_pool_row(uint32_t p, uint32_t HoWo, uint3
 // of the stored output (see k_conv_nt).  Every thread of the block calls it (barriers inside);
 // only k-group 0 (g == 0) holds the reduced accumulators.
 template <int BM, int BN, int MI, int NJ>
-__device__ __forceinline__ void cv_nt_epilogue(const f32x4 (&acc)[MI][NJ], char* smem, int g,
+__device__ __forceinline__ void cv_nt_epilogue(f32x4 (&acc)[MI][NJ], char* smem, int g,
                                                int wm, int wn, int lane, int m0, int n0, int M,
                                                int Nc, uint16_t* __restrict__ out,
                                                float* __restrict__ slab,
                                                float* __restrict__ bnpart,
-                                               const CvBnBwd& bb) {
+                                               const CvBnBwd& bb,
+                                               const uint16_t* __restrict__ addend) {
   const int row0 = m0 + wm * (BM / 2), col0 = n0 + wn * (BN / 2);
+  if (addend && !slab && g == 0) {
+    // out = this GEMM + addend (a second gradient of the same tensor, e.g. the identity
+    // residual's, so autograd does not add them in a separate kernel); loads first, then adds
+    float av[MI][NJ][4];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          av[i][j][q] = __uint_as_float(
+              (uint32_t)addend[(size_t)(row0 + i * 16 + 4 * (lane >> 4) + q) * Nc + col0 +
+                               j * 16 + (lane & 15)] << 16);
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[i][j][q] += av[i][j][q];
+  }
   if (slab) {
     if (g == 0)
       cv_store<MI, NJ>(acc, row0, col0, lane, nullptr, slab + (long long)blockIdx.z * M * Nc, Nc);
@@ -270,7 +292,7 @@ __device__ __forceinline__ void cv_nt_epilogue(const f32x4 (&acc)[MI][NJ], char*
     float sm[NJ], sq[NJ];
     // BN-backward sums of layer L (see CvBnBwd), group 0 only: all window codes, then all h
     // values are loaded before any use (two load round trips, not one per element)
-    float xv[NJ][MI][4];
+    float xv[NJ][MI][4], rv[NJ][MI][4];
     if (bb.h && g == 0) {
       const uint32_t HoWo = (uint32_t)bb.Ho * bb.Wo;
       uint32_t hr[NJ][MI][4];
@@ -302,9 +324,11 @@ __device__ __forceinline__ void cv_nt_epilogue(const f32x4 (&acc)[MI][NJ], char*
 #pragma unroll
         for (int i = 0; i < MI; ++i)
 #pragma unroll
-          for (int q = 0; q < 4; ++q)
-            xv[j][i][q] = __uint_as_float(
-                (uint32_t)bb.h[(size_t)hr[j][i][q] * Nc + col0 + j * 16 + (lane & 15)] << 16);
+          for (int q = 0; q < 4; ++q) {
+            const size_t o = (size_t)hr[j][i][q] * Nc + col0 + j * 16 + (lane & 15);
+            xv[j][i][q] = __uint_as_float((uint32_t)bb.h[o] << 16);
+            rv[j][i][q] = bb.res ? __uint_as_float((uint32_t)bb.res[o] << 16) : 0.0f;
+          }
     }
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
@@ -319,7 +343,8 @@ __device__ __forceinline__ void cv_nt_epilogue(const f32x4 (&acc)[MI][NJ], char*
             for (int q = 0; q < 4; ++q) {
               const float d = __uint_as_float((uint32_t)ew_f2bf(acc[i][j][q]) << 16);
               const float x = xv[j][i][q];
-              const float v = x * sc + sh;  // the BN kernels' exact arithmetic (no contraction)
+              float v = x * sc + sh;  // the BN kernels' exact arithmetic (no contraction)
+              if (bb.res) v = v + rv[j][i][q];
               const float dz = (bb.relu == 0 || !(v <= 0.0f)) ? d : 0.0f;
               sm[j] += dz;
               sq[j] += dz * (x - mean);
@@ -371,7 +396,8 @@ __global__ __launch_bounds__(EW_BLOCK * KG) void k_conv_nt(const uint16_t* __res
                                                            float* __restrict__ slab, int M, int H,
                                                            int W, int C, int Nc, int kps,
                                                            int taps, float* __restrict__ bnpart,
-                                                           CvBnBwd bb) {
+                                                           CvBnBwd bb,
+                                                           const uint16_t* __restrict__ addend) {
   constexpr int PA = BM / 32, PB = BN / 32;   // 16-B vectors per thread per k-step
   constexpr int MI = BM / 32, NJ = BN / 32;   // 16x16 tiles per wave (wave tile BM/2 x BN/2)
   constexpr int STAGE = (BM + BN) * 128;      // bytes of one LDS stage (A then B)
@@ -490,7 +516,7 @@ __global__ __launch_bounds__(EW_BLOCK * KG) void k_conv_nt(const uint16_t* __res
 #undef CV_NT_MMA
   cv_group_reduce<KG, MI, NJ>(acc, smem, g, wq, lane);
   cv_nt_epilogue<BM, BN, MI, NJ>(acc, smem, g, wm, wn, lane, m0, n0, M, Nc, out, slab, bnpart,
-                                 bb);
+                                 bb, addend);
 #undef CV_NT_LOAD
 #undef CV_NT_STORE
 }
@@ -525,7 +551,8 @@ __global__ __launch_bounds__(EW_BLOCK) void k_conv_nt_dma(const uint16_t* __rest
                                                           int W, int C, int Nc, int kps, int taps,
                                                           float* __restrict__ bnpart,
                                                           const uint16_t* __restrict__ zero,
-                                                          CvBnBwd bb) {
+                                                          CvBnBwd bb,
+                                                          const uint16_t* __restrict__ addend) {
   constexpr int PA = BM / 32, PB = BN / 32;   // glds instructions per wave per k-step (8 rows each)
   constexpr int MI = BM / 32, NJ = BN / 32;
   constexpr int STAGE = (BM + BN) * 128;
@@ -604,7 +631,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_conv_nt_dma(const uint16_t* __rest
   }
   __syncthreads();
   cv_nt_epilogue<BM, BN, MI, NJ>(acc, smem, 0, wm, wn, lane, m0, n0, M, Nc, out, slab, bnpart,
-                                 bb);
+                                 bb, addend);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -737,7 +764,8 @@ __global__ __launch_bounds__(EW_BLOCK * KG) void k_conv_wgrad(const uint16_t* __
 // out_bf16[i] = bf16(sum_z slab[z][i]), 8 elements per thread (n % 8 == 0)
 __global__ __launch_bounds__(EW_BLOCK) void k_cv_slab_reduce(const float* __restrict__ slab,
                                                              int nsplit, long long n,
-                                                             uint16_t* __restrict__ out) {
+                                                             uint16_t* __restrict__ out,
+                                                             const uint16_t* __restrict__ addend) {
   const long long nv = n / 8;
   for (long long v = blockIdx.x * (long long)EW_BLOCK + threadIdx.x; v < nv;
        v += (long long)gridDim.x * EW_BLOCK) {
@@ -752,6 +780,15 @@ __global__ __launch_bounds__(EW_BLOCK) void k_cv_slab_reduce(const float* __rest
       hi = p[1];
       a[0] += lo.x; a[1] += lo.y; a[2] += lo.z; a[3] += lo.w;
       a[4] += hi.x; a[5] += hi.y; a[6] += hi.z; a[7] += hi.w;
+    }
+    if (addend) {  // see cv_nt_epilogue
+      const uint4 w = reinterpret_cast<const uint4*>(addend)[v];
+      const uint32_t aw[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        a[2 * j] += __uint_as_float(aw[j] << 16);
+        a[2 * j + 1] += __uint_as_float(aw[j] & 0xffff0000u);
+      }
     }
     uint4 o;
     o.x = (uint32_t)ew_f2bf(a[0]) | ((uint32_t)ew_f2bf(a[1]) << 16);
@@ -985,7 +1022,8 @@ __global__ __launch_bounds__(EW_BLOCK) void k_cv_slab_reduce_bn(const float* __r
                                                                 int nsplit, int M, int Nc,
                                                                 uint16_t* __restrict__ out,
                                                                 float* __restrict__ bnpart,
-                                                                int rpb, CvBnBwd bb) {
+                                                                int rpb, CvBnBwd bb,
+                                                                const uint16_t* __restrict__ addend) {
   __shared__ float red[2][EW_BLOCK * 8];  // [2][rpi][Nc]: rpi * Nc = 8 * EW_BLOCK
   const int tpr = Nc >> 3, rpi = EW_BLOCK / tpr;
   const int t = threadIdx.x, g = t % tpr, rg = t / tpr;
@@ -1021,6 +1059,15 @@ __global__ __launch_bounds__(EW_BLOCK) void k_cv_slab_reduce_bn(const float* __r
           a[0] += lo.x; a[1] += lo.y; a[2] += lo.z; a[3] += lo.w;
           a[4] += hi.x; a[5] += hi.y; a[6] += hi.z; a[7] += hi.w;
         }
+        if (addend) {
+          const uint4 w = *reinterpret_cast<const uint4*>(addend + o);
+          const uint32_t aw[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            a[2 * j] += __uint_as_float(aw[j] << 16);
+            a[2 * j + 1] += __uint_as_float(aw[j] & 0xffff0000u);
+          }
+        }
       }
       uint16_t b[8];
 #pragma unroll
@@ -1038,7 +1085,8 @@ __global__ __launch_bounds__(EW_BLOCK) void k_cv_slab_reduce_bn(const float* __r
           uint32_t hr = (uint32_t)r;
           if (bb.code) hr = cv_pool_row((uint32_t)r, HoWo, (uint32_t)bb.Wo, bb.code[o + j]);
           const float x = __uint_as_float((uint32_t)bb.h[(size_t)hr * Nc + c0 + j] << 16);
-          const float v = x * sc[j] + sh[j];
+          float v = x * sc[j] + sh[j];
+          if (bb.res) v = v + __uint_as_float((uint32_t)bb.res[(size_t)hr * Nc + c0 + j] << 16);
           const float dz = (bb.relu == 0 || !(v <= 0.0f)) ? d : 0.0f;
           s1[j] += dz;
           s2[j] += dz * (x - mean[j]);
@@ -1098,7 +1146,7 @@ long long ew_conv_ws_floats() { return 8LL << 20; }  // 32 MiB of fp32 split sla
 
 #define CV_LAUNCH_NT(BM_, KG_, TRB_)                                                             \
   hipLaunchKernelGGL((k_conv_nt<BM_, BM_, KG_, TRB_>), grid, dim3(EW_BLOCK * KG_), 0, s, x, w,  \
-                     out, slab, M, H, W, C, Nc, p.kps, taps, bnp, bbv)
+                     out, slab, M, H, W, C, Nc, p.kps, taps, bnp, bbv, addend)
 
 // NT GEMM (forward / backward-data): out[M][Nc] = sum X~[M][9C] w[Nc][9C]^T
 // trb: w is the forward weight [C][9][Nc] of a backward-data GEMM (transposed B images, 64x64
@@ -1108,7 +1156,8 @@ long long ew_conv_ws_floats() { return 8LL << 20; }  // 32 MiB of fp32 split sla
 static int ew_conv_nt(const uint16_t* x, const uint16_t* w, uint16_t* out, float* ws,
                       long long ws_floats, int M, int H, int W, int C, int Nc, int taps,
                       bool trb, hipStream_t s, float* bnpart = nullptr,
-                      long long bnpart_floats = 0, const CvBnBwd* bnb = nullptr) {
+                      long long bnpart_floats = 0, const CvBnBwd* bnb = nullptr,
+                      const uint16_t* addend = nullptr) {
   if (C % CV_BK || Nc % 64 || M % 64)
     throw std::runtime_error("ewdml conv: needs C % 64 == 0, Nc % 64 == 0, N*H*W % 64 == 0");
   const int ksteps = taps * (C / CV_BK);
@@ -1132,10 +1181,10 @@ static int ew_conv_nt(const uint16_t* x, const uint16_t* w, uint16_t* out, float
   const long long prow = M / BM;
   float* bnp = (bnpart && !slab && prow <= 1024 && 2 * prow * Nc <= bnpart_floats) ? bnpart
                                                                                   : nullptr;
-  const CvBnBwd bbv = (bnp && bnb) ? *bnb : CvBnBwd{nullptr, nullptr, nullptr, 0, 0, 0};
+  const CvBnBwd bbv = (bnp && bnb) ? *bnb : CvBnBwd{nullptr, nullptr, nullptr, nullptr, 0, 0, 0};
 #define CV_LAUNCH_DMA(BM_, TRB_)                                                                 \
   hipLaunchKernelGGL((k_conv_nt_dma<BM_, BM_, 4, TRB_>), grid, dim3(EW_BLOCK), 0, s, x, w, out, \
-                     slab, M, H, W, C, Nc, p.kps, taps, bnp, zero, bbv)
+                     slab, M, H, W, C, Nc, p.kps, taps, bnp, zero, bbv, addend)
   if (dma) {
     if (big) CV_LAUNCH_DMA(128, false);
     else if (trb) CV_LAUNCH_DMA(64, true);
@@ -1165,15 +1214,16 @@ static int ew_conv_nt(const uint16_t* x, const uint16_t* w, uint16_t* out, float
       if (2LL * nblk * Nc > bnpart_floats) nblk = 0;
     }
     if (nblk > 0) {
-      const CvBnBwd bbr = bnb ? *bnb : CvBnBwd{nullptr, nullptr, nullptr, 0, 0, 0};
+      const CvBnBwd bbr = bnb ? *bnb : CvBnBwd{nullptr, nullptr, nullptr, nullptr, 0, 0, 0};
       hipLaunchKernelGGL(k_cv_slab_reduce_bn, dim3(nblk), dim3(EW_BLOCK), 0, s, ws, p.split, M,
-                         Nc, out, bnpart, rpb, bbr);
+                         Nc, out, bnpart, rpb, bbr, addend);
       EW_CHECK_LAUNCH();
       return nblk;
     }
     long long gr = (n / 8 + EW_BLOCK - 1) / EW_BLOCK;
     if (gr > 2048) gr = 2048;
-    hipLaunchKernelGGL(k_cv_slab_reduce, dim3((int)gr), dim3(EW_BLOCK), 0, s, ws, p.split, n, out);
+    hipLaunchKernelGGL(k_cv_slab_reduce, dim3((int)gr), dim3(EW_BLOCK), 0, s, ws, p.split, n, out,
+                       addend);
     EW_CHECK_LAUNCH();
   }
   return bnp ? (int)prow : 0;
@@ -1197,13 +1247,15 @@ int ew_conv_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t ws, long long w
 
 int ew_conv_bwd_data(uintptr_t dy, uintptr_t w, uintptr_t dx, uintptr_t ws,
                      long long ws_floats, long long N, int H, int W, int C, int Nc, int ksize,
-                     uintptr_t bn_h, uintptr_t bn_code, uintptr_t bn_stats, int bn_relu,
-                     uintptr_t bnpart, long long bnpart_floats, uintptr_t stream) {
+                     uintptr_t bn_h, uintptr_t bn_res, uintptr_t bn_code, uintptr_t bn_stats,
+                     int bn_relu, uintptr_t bnpart, long long bnpart_floats, uintptr_t addend,
+                     uintptr_t stream) {
   // the flipped / transposed weight is read in place through transposed B images (no copy)
   if (C % 64 || Nc % 64) throw std::runtime_error("ewdml conv: bwd-data needs C, Nc % 64 == 0");
   // optional BN-backward sums of the layer whose output gradient dx is (CvBnBwd); with a pool,
   // dx is at the pooled resolution H x W and bn_h at 2H x 2W
   const CvBnBwd bb{reinterpret_cast<const uint16_t*>(bn_h),
+                   reinterpret_cast<const uint16_t*>(bn_res),
                    reinterpret_cast<const uint8_t*>(bn_code),
                    reinterpret_cast<const float*>(bn_stats), bn_relu, H, W};
   // dx[m][c] = sum over (tap', n) of dY~[m][(tap', n)] * w[n][8 - tap'][c]
@@ -1211,7 +1263,7 @@ int ew_conv_bwd_data(uintptr_t dy, uintptr_t w, uintptr_t dx, uintptr_t ws,
                     reinterpret_cast<uint16_t*>(dx), reinterpret_cast<float*>(ws), ws_floats,
                     (int)(N * H * W), H, W, Nc, C, cv_taps(ksize), true, (hipStream_t)stream,
                     bn_h ? reinterpret_cast<float*>(bnpart) : nullptr, bnpart_floats,
-                    bn_h ? &bb : nullptr);
+                    bn_h ? &bb : nullptr, reinterpret_cast<const uint16_t*>(addend));
 }
 
 void ew_conv_wgrad(uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws, long long ws_floats,
@@ -1255,7 +1307,7 @@ void ew_conv_wgrad(uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws, long l
     long long g = (n / 8 + EW_BLOCK - 1) / EW_BLOCK;
     if (g > 2048) g = 2048;
     hipLaunchKernelGGL(k_cv_slab_reduce, dim3((int)g), dim3(EW_BLOCK), 0, s,
-                       reinterpret_cast<const float*>(ws), p.split, n, reinterpret_cast<uint16_t*>(dw));
+                       reinterpret_cast<const float*>(ws), p.split, n, reinterpret_cast<uint16_t*>(dw), nullptr);
     EW_CHECK_LAUNCH();
   }
 }

@@ -152,12 +152,13 @@ int ew_conv_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t ws, long long w
                 long long N, int H, int W, int C, int Nc, int ksize, uintptr_t bnpart,
                 long long bnpart_floats, uintptr_t stream);
 // bn_h (nullable): also write the BN-backward sums [2][rows][C] (sum dz, sum dz*(h-mean)) of the
-// BN(+ReLU)(+pool: bn_code) layer whose output gradient dx is into bnpart; returns rows (0: not
-// written, e.g. a split-K launch)
+// BN(+residual bn_res)(+ReLU)(+pool: bn_code) layer whose output gradient dx is into bnpart;
+// returns rows (0: not written).  addend (nullable, [rows][C] bf16): dx = this GEMM + addend.
 int ew_conv_bwd_data(uintptr_t dy, uintptr_t w, uintptr_t dx, uintptr_t ws,
                      long long ws_floats, long long N, int H, int W, int C, int Nc, int ksize,
-                     uintptr_t bn_h, uintptr_t bn_code, uintptr_t bn_stats, int bn_relu,
-                     uintptr_t bnpart, long long bnpart_floats, uintptr_t stream);
+                     uintptr_t bn_h, uintptr_t bn_res, uintptr_t bn_code, uintptr_t bn_stats,
+                     int bn_relu, uintptr_t bnpart, long long bnpart_floats, uintptr_t addend,
+                     uintptr_t stream);
 void ew_conv_wgrad(uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws, long long ws_floats,
                    long long N, int H, int W, int C, int Nc, int ksize, uintptr_t stream);
 // int32 words of a grid arrival ticket (common.h ew_grid_last): 8 sub-counters + 1 top, 128 B apart

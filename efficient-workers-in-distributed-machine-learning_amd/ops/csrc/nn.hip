@@ -765,7 +765,7 @@ static void ew_bn_bwd_impl(const BnBwdArgs& a) {
   int nblk, rpb;
   ew_bn_grid(rows, C, &nblk, &rpb, POOL ? 1 : 2);
   float* part = reinterpret_cast<float*>(a.part);
-  const bool pre = a.pre_nblk > 0 && MODE != EW_BN_ADD_RELU;  // sums from the producing conv
+  const bool pre = a.pre_nblk > 0;  // sums from the producing conv (ops/csrc/conv.hip CvBnBwd)
   const T* h = reinterpret_cast<const T*>(a.h);
   const T* res = reinterpret_cast<const T*>(a.res);
   const T* dy = reinterpret_cast<const T*>(a.dy);

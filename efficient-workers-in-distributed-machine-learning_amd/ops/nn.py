@@ -68,7 +68,7 @@ PRE_BWD_USED = 0
 class _BNAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, h, res, cbias, gamma, beta, rmean, rvar, nbt, momentum, eps, pool, mode,
-                pre=None):
+                pre=None, res_sink=None):
         C_ = require()
         N, C, H, W = h.shape
         dev = h.device
@@ -87,6 +87,7 @@ class _BNAct(torch.autograd.Function):
                        -1.0 if momentum is None else float(momentum), float(eps), cb_bf16,
                        _stream(), int(pre_rows))
         ctx.pool, ctx.mode = pool, mode
+        ctx.res_sink = res_sink
         ctx.cb_dtype = None if cb is None else cb.dtype
         ctx.save_for_backward(h, res, code, stats)
         return y
@@ -105,6 +106,7 @@ class _BNAct(torch.autograd.Function):
         dx = torch.empty_like(h, memory_format=torch.channels_last)
         dres = torch.empty_like(h, memory_format=torch.channels_last) \
             if ctx.mode == "add_relu" else None
+        sink, ctx.res_sink = ctx.res_sink, None
         coef = torch.empty(2 * C, dtype=torch.float32, device=dev)
         dcb = torch.empty(C, dtype=ctx.cb_dtype, device=dev) if need[2] else None
         dg = torch.empty(C, dtype=torch.float32, device=dev) if need[3] else None
@@ -124,7 +126,9 @@ class _BNAct(torch.autograd.Function):
                        H, W, C, int(h.dtype == torch.bfloat16), int(ctx.pool),
                        _MODES[ctx.mode], int(ctx.cb_dtype == torch.bfloat16), _stream(),
                        int(pre_rows))
-        return dx, dres, dcb, dg, db, None, None, None, None, None, None, None, None
+        if sink is not None:  # the residual's gradient goes to the block's first conv (ops/conv)
+            sink.grad, dres = dres, None
+        return dx, dres, dcb, dg, db, None, None, None, None, None, None, None, None, None
 
 
 def _apply_eval(h, stats, pool, mode="relu", res=None):
@@ -160,7 +164,17 @@ def bn_relu_reference(h, cbias, bn, pool=False):
     return bn_act_reference(h, cbias, bn, pool, "relu")
 
 
-def bn_act(h, bn, mode="relu", res=None, cbias=None, pool=False):
+def kernel_path(h, bn, res=None, pool=False) -> bool:
+    """True if :func:`bn_act` runs the fused training kernels for these inputs (batch
+    statistics, supported layout) -- the only path that honours ``res_sink``."""
+    ok = nhwc_supported(h, pool)
+    if ok and res is not None:
+        ok = (res.shape == h.shape and res.dtype == h.dtype and res.data_ptr() % 16 == 0
+              and res.is_contiguous(memory_format=torch.channels_last))
+    return ok and (bn.training or bn.running_mean is None)
+
+
+def bn_act(h, bn, mode="relu", res=None, cbias=None, pool=False, res_sink=None):
     """``maxpool?(act(bn(h + cbias) [+ res]))`` for a ``nn.BatchNorm2d`` ``bn``; ``mode`` is
     ``relu``, ``none`` (BN only) or ``add_relu`` (``relu(bn(h) + res)``, the ResNet block
     output).  Running statistics and ``num_batches_tracked`` are updated like ``bn``'s own
@@ -171,9 +185,11 @@ def bn_act(h, bn, mode="relu", res=None, cbias=None, pool=False):
     if ok and res is not None:
         ok = (res.shape == h.shape and res.dtype == h.dtype and res.data_ptr() % 16 == 0
               and res.is_contiguous(memory_format=torch.channels_last))
+    batch_stats = bn.training or bn.running_mean is None
+    if res_sink is not None and not (ok and batch_stats):
+        raise ValueError("res_sink needs the fused training kernels (see kernel_path)")
     if not ok:
         return bn_act_reference(h, cbias, bn, pool, mode, res)
-    batch_stats = bn.training or bn.running_mean is None
     if batch_stats:
         # num_batches_tracked is incremented by the apply kernel (no separate add kernel)
         nbt = bn.num_batches_tracked if bn.training and bn.track_running_stats else None
@@ -181,8 +197,8 @@ def bn_act(h, bn, mode="relu", res=None, cbias=None, pool=False):
         y = _BNAct.apply(h, res, cbias, bn.weight, bn.bias,
                          bn.running_mean if track else None,
                          bn.running_var if track else None, nbt, bn.momentum, bn.eps, pool,
-                         mode, getattr(h, "_ew_bn_part", None))
-        if mode != "add_relu" and y.grad_fn is not None:
+                         mode, getattr(h, "_ew_bn_part", None), res_sink)
+        if y.grad_fn is not None:
             # a following MFMA conv may sum this layer's backward statistics in its
             # backward-data epilogue (ops/conv.py)
             y._ew_bn_node = y.grad_fn

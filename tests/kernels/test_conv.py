@@ -269,3 +269,48 @@ def test_bn_backward_sums_in_bwd_data_epilogue(mode, pool, N, HW):
     conv.set_bn_bwd_fusion(True)
     for a, b in zip(*grads):
         assert _rel(a, b) < 2e-3, _rel(a, b)
+
+
+@pytest.mark.parametrize("net", ["resnet18", "resnet50"])
+def test_resnet_residual_grad_sink_and_bn_sums_match_autograd_sum(net):
+    """Identity-residual gradients handed to the block's first conv (added in its backward-data
+    epilogue) and BN backward sums from the epilogues: one bf16 ResNet step is as close to the
+    fp32 step as the bf16 step with autograd summing the residual gradients and the BN kernels'
+    own statistics passes."""
+    import copy
+
+    from ewdml.models import build_model, resnet
+    from ewdml.ops import nn as fnn
+
+    conv = _conv()
+    torch.manual_seed(0)
+    m0 = build_model(net, 10).cuda().to(memory_format=torch.channels_last)
+    x = torch.randn(32, 3, 32, 32, device="cuda").contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (32,), device="cuda")
+    res = []
+    for run in ("fp32", "fused", "unfused"):
+        fused = run == "fused"
+        resnet.set_residual_sink(fused)
+        conv.set_bn_bwd_fusion(fused)
+        m = copy.deepcopy(m0)
+        xx = x
+        if run != "fp32":
+            for p in m.parameters():
+                p.data = p.data.to(torch.bfloat16).contiguous(
+                    memory_format=torch.channels_last if p.dim() == 4 else torch.contiguous_format)
+            xx = x.to(torch.bfloat16)
+        used = fnn.PRE_BWD_USED
+        try:
+            out = m(xx)
+            torch.nn.functional.cross_entropy(out.float(), y).backward()
+        finally:
+            resnet.set_residual_sink(True)
+            conv.set_bn_bwd_fusion(True)
+        if fused:
+            assert fnn.PRE_BWD_USED > used
+        res.append((out.float(), [p.grad.float() for p in m.parameters()]))
+    (o_ref, g_ref), (o_f, g_f), (o_u, g_u) = res
+    assert _rel(o_f, o_ref) <= 1.25 * _rel(o_u, o_ref) + 1e-3
+    e_f = sum(_rel(a, b) for a, b in zip(g_f, g_ref)) / len(g_ref)
+    e_u = sum(_rel(a, b) for a, b in zip(g_u, g_ref)) / len(g_ref)
+    assert e_f <= 1.25 * e_u + 1e-3, (e_f, e_u)

@@ -32,7 +32,7 @@ def main():
             C_.conv_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), ws.data_ptr(), ws.numel(), B,
                         hw, hw, cin, cout, 3, 0, 0, st)
             C_.conv_bwd_data(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), ws.data_ptr(),
-                             ws.numel(), B, hw, hw, cin, cout, 3, 0, 0, 0, 0, 0, 0, st)
+                             ws.numel(), B, hw, hw, cin, cout, 3, 0, 0, 0, 0, 0, 0, 0, 0, st)
             C_.conv_wgrad(dy.data_ptr(), x.data_ptr(), dw.data_ptr(), ws.data_ptr(), ws.numel(),
                           B, hw, hw, cin, cout, 3, st)
     torch.cuda.synchronize()

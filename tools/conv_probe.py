@@ -60,7 +60,7 @@ def hip_times(x, w, dy):
                                        ws.numel(), N, H, W, C, Nc, 3, 0, 0, st()))
     tb = timeit(lambda: C_.conv_bwd_data(dy.data_ptr(), w.data_ptr(), dx.data_ptr(),
                                             ws.data_ptr(), ws.numel(), N, H, W, C, Nc, 3, 0, 0,
-                                            0, 0, 0, 0, st()))
+                                            0, 0, 0, 0, 0, 0, st()))
     tw = timeit(lambda: C_.conv_wgrad(dy.data_ptr(), x.data_ptr(), dw.data_ptr(),
                                          ws.data_ptr(), ws.numel(), N, H, W, C, Nc, 3, st()))
     return tf, tb, tw
