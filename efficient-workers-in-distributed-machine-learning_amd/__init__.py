@@ -18,6 +18,15 @@ Layout (see README.md):
 """
 __version__ = "0.1.0"
 
+import os as _os
+
+# Kernel arguments in device memory rather than host-coherent memory.  Must be set before the HIP
+# runtime initialises (first device call), which importing this package precedes.  Unprofiled
+# this matches the runtime default on MI355X (=0 costs ResNet-50 5-7 %); pinning it keeps it so
+# under rocprofv3, where the VGG-11 step graph otherwise shows a ~55 us mid-backward dispatch
+# stall that the unprofiled run does not have (profiles/ab/device_kernargs.txt).
+_os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
+
 from .config import Config, build_parser, parse_args  # noqa: E402
 from .parallel.horovod import (Adasum, Average, Compression, DistributedOptimizer,  # noqa: E402
                                Sum, allreduce, broadcast_optimizer_state,
