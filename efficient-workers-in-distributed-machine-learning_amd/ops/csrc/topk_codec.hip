@@ -38,12 +38,14 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_hist0(GradPtrs gp,
                                                          const ChunkRow* __restrict__ chunks,
                                                          uint32_t* __restrict__ hist,
                                                          uint32_t* __restrict__ kmaxr, int T) {
-  // one private histogram per wave: gradients cluster in a few exponent bins, and four waves
-  // hammering the same LDS words serialise; the waves' copies are summed at the flush
-  __shared__ uint32_t hw[EW_WAVES][NB0];
-  for (int i = threadIdx.x; i < EW_WAVES * NB0; i += EW_BLOCK) (&hw[0][0])[i] = 0;
+  // Gradients cluster in a few exponent bins, so most lanes of a wave add to the same bin and an
+  // LDS atomic serialises per conflicting lane.  HSUB copies per bin in consecutive words (banks),
+  // chosen by lane: a shared bin splits into HSUB bank groups; the copies are summed at the flush.
+  constexpr int HSUB = 4;
+  __shared__ uint32_t hs[NB0 * HSUB];
+  for (int i = threadIdx.x; i < NB0 * HSUB; i += EW_BLOCK) hs[i] = 0;
   __syncthreads();
-  uint32_t* h = hw[threadIdx.x >> 6];
+  uint32_t* h = hs + (threadIdx.x & (HSUB - 1));
   const ChunkRow c = chunks[blockIdx.x];
   uint32_t kmax = 0;
   for (int i = 4 * threadIdx.x; i < c.len; i += 4 * EW_BLOCK) {
@@ -66,7 +68,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_hist0(GradPtrs gp,
     for (int j = 0; j < 4; ++j) {
       if (i + j < c.len) {
         const uint32_t k = ew_key(xs[j]);
-        atomicAdd(&h[k >> 20], 1u);
+        atomicAdd(&h[(k >> 20) * HSUB], 1u);
         kmax = max(kmax, k);
       }
     }
@@ -85,7 +87,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_hist0(GradPtrs gp,
   for (int i = threadIdx.x; i < NB0; i += EW_BLOCK) {
     uint32_t v = 0;
 #pragma unroll
-    for (int w = 0; w < EW_WAVES; ++w) v += hw[w][i];
+    for (int j = 0; j < HSUB; ++j) v += hs[i * HSUB + j];
     if (v) atomicAdd(&dst[i], v);
   }
 }
