@@ -59,7 +59,8 @@ class Config:
     qsgd_levels: int = 127
     qsgd_bits: int = 8
     qsgd_norm: str = "max"  # max | l2 (the reference's L2 norm)
-    topology: str = "allgather"  # allgather (all-to-all) | ps (rank-0 parameter server)
+    topology: str = "allgather"  # allgather (all-to-all) | ps (rank-0 parameter server) |
+    #                               sharded (every rank owns 1/N of each bucket: parallel/sharded.py)
     pull: str = "grad"  # ps topology: pull averaged 'grad' or server 'weights'
     pull_compress: Optional[str] = None  # ps topology: codec of the pull (default = push codec)
     sync_every: int = 1  # local SGD: exchange every H steps (method 6)
@@ -129,8 +130,8 @@ class Config:
                 c.select_best = True
         if c.compress_grad.lower() == "none":
             c.compress = "none"
-        if c.topology not in ("allgather", "ps"):
-            raise ValueError("--topology must be allgather or ps")
+        if c.topology not in ("allgather", "ps", "sharded"):
+            raise ValueError("--topology must be allgather, ps or sharded")
         if c.graph_warmup < 1:
             raise ValueError("--graph-warmup must be >= 1 (one eager step initialises the stream)")
         if c.ckpt_dir is None:
@@ -175,7 +176,7 @@ def build_parser(prog="distributed_nn.py") -> argparse.ArgumentParser:
     a("--qsgd-levels", type=int, default=d.qsgd_levels)
     a("--qsgd-bits", type=int, default=d.qsgd_bits, choices=[4, 8])
     a("--qsgd-norm", type=str, default=d.qsgd_norm, choices=["max", "l2"])
-    a("--topology", type=str, default=d.topology, choices=["allgather", "ps"])
+    a("--topology", type=str, default=d.topology, choices=["allgather", "ps", "sharded"])
     a("--pull", type=str, default=d.pull, choices=["grad", "weights"])
     a("--pull-compress", type=str, default=None,
       choices=["none", "fp16", "bf16", "qsgd", "topk", "topk_qsgd"])

@@ -27,6 +27,7 @@ from ..parallel.engine import GradientExchange, Stopwatch, sync_buffers, sync_pa
 from ..parallel.flat import FlatModel
 from ..parallel.local_sgd import LocalSGDExchange
 from ..parallel.ps import PSExchange
+from ..parallel.sharded import ShardedPSExchange
 from ..utils import checkpoint as ckpt
 from ..utils.metrics import MetricsLogger, accuracy, byte_summary
 
@@ -139,6 +140,8 @@ class Trainer:
                                        make_codec(cfg.pull_compress or cfg.compress, **ckw),
                                        self.opt, pull=cfg.pull,
                                        aggregate=cfg.num_aggregate if cfg.mode == "kill" else None)
+        elif cfg.topology == "sharded":
+            self.exchange = ShardedPSExchange(self.flat, self.comm, cfg.compress, self.opt, **ckw)
         else:
             self.exchange = GradientExchange(self.flat, self.comm,
                                              make_codec(cfg.compress, **ckw), self.opt,

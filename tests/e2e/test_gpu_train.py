@@ -171,3 +171,18 @@ def test_bench_through_rccl_process_group(codec):
     assert rec["config"]["hip_graph"] == "full"  # the capture of the RCCL collective succeeded
     assert rec["value"] > 0 and rec["n_gpus"] == 1
     assert rec["final_loss"] == rec["final_loss"]  # not NaN
+
+
+@pytest.mark.parametrize("codec", ["topk_qsgd", "qsgd"])
+def test_sharded_topology_hip_codecs(codec):
+    """--topology sharded through the HIP codecs on shard plans (world of one: one shard per
+    bucket, bucket_offset of the shard = the bucket's): lossless top-k equals the dense step, the
+    compressing codecs train."""
+    ops.require()
+    ref, _ = _run(LENET + ["--compress", "none", "--hip-graph", "off"], 4)
+    tr, _ = _run(LENET + ["--compress", "topk", "--topk-ratio", "1.0", "--topology", "sharded"], 4)
+    rel = (tr.flat.data - ref.flat.data).norm() / ref.flat.data.norm()
+    assert rel < 1e-5, f"sharded lossless top-k differs from dense by {rel:.2e}"
+    tr, losses = _run(LENET + ["--compress", codec, "--topology", "sharded"], 6)
+    assert all(torch.isfinite(torch.tensor(losses)))
+    assert tr.exchange.last.payload_bytes > 0
