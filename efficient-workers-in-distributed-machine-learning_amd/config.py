@@ -187,7 +187,7 @@ def build_parser(prog="distributed_nn.py") -> argparse.ArgumentParser:
     a("--bucket-mb", type=float, default=d.bucket_mb)
     a("--no-overlap", dest="overlap", action="store_false", default=True)
     a("--predivide", type=float, default=d.predivide)
-    a("--sync-bn", action="store_true", default=False)
+    a("--sync-bn", "--sync-bn-buffers", dest="sync_bn", action="store_true", default=False)
     # optimizer
     a("--optimizer", type=str, default=d.optimizer, choices=["sgd", "adam", "amsgrad"])
     a("--weight-decay", type=float, default=d.weight_decay)

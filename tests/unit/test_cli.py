@@ -50,3 +50,18 @@ def test_compress_grad_none_switch():
 
 def test_ckpt_dir_defaults_to_train_dir():
     assert Config(train_dir="/a/").resolved().ckpt_dir == "/a/"
+
+
+def test_sync_bn_buffers_alias():
+    import ewdml
+
+    assert ewdml.parse_args(["--sync-bn-buffers"]).sync_bn
+    assert ewdml.parse_args(["--sync-bn"]).sync_bn
+    assert not ewdml.parse_args([]).sync_bn
+
+
+def test_topology_choices():
+    import ewdml
+
+    for t in ("allgather", "ps", "sharded"):
+        assert ewdml.parse_args(["--topology", t]).topology == t
