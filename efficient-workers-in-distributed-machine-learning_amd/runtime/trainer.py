@@ -155,6 +155,9 @@ class Trainer:
         self.graph_mode = cfg.hip_graph if self.cuda else "off"
         if self.graph_mode != "off" and not isinstance(self.exchange, GradientExchange):
             raise ValueError("--hip-graph needs the all-to-all topology without local SGD")
+        if self.graph_mode == "full" and self.comm.distributed and self.comm.backend == "gloo":
+            # gloo's CUDA collectives cannot be captured: graph the compute, issue them between
+            self.graph_mode = "split"
         self._graphs = None
         self._in_graph_batch = False
         self._key_synced = False
