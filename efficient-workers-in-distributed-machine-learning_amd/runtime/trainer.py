@@ -217,10 +217,11 @@ class Trainer:
         """One synchronous step.  Returns (loss tensor, logits) (server: (None, None))."""
         if self.gstream is None:
             return self._train_step(x, y)
-        self.gstream.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(self.gstream):
+        gs = self.gstream  # a failed capture drops self.gstream inside the step
+        gs.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(gs):
             out = self._train_step(x, y)
-        torch.cuda.current_stream().wait_stream(self.gstream)
+        torch.cuda.current_stream().wait_stream(gs)
         return out
 
     def lr_at(self, step: int) -> float:
@@ -292,7 +293,15 @@ class Trainer:
             self._graphs = None
             self.graph_mode = "off"
             ex.use_dev_key = ex.defer_comm = ex._active = ex.dev_key_advance = False
-            torch.cuda.synchronize()
+            # a stream forked into an aborted capture (the encode side stream, a backend's
+            # internal stream) can stay in capture mode: continue on fresh streams
+            self.gstream = None
+            if ex.side is not None:
+                ex.side = torch.cuda.Stream(device=self.device)
+            try:
+                torch.cuda.synchronize()
+            except Exception as e:  # noqa: BLE001 - the eager step below reports a real fault
+                self.log.info(f"synchronize after the failed capture: {e!r}")
             self.log.info(f"HIP graph capture failed ({err!r} on this rank); running eagerly")
             return False
         return True
@@ -322,19 +331,27 @@ class Trainer:
         if self.graph_mode == "full":
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, stream=self.gstream, capture_error_mode=mode):
-                if self._in_graph_batch:
-                    self._gx, self._gy = self.loader.emit()
-                loss, out = self.forward_backward(self._gx, self._gy)
-                ex.finish()
+                try:
+                    if self._in_graph_batch:
+                        self._gx, self._gy = self.loader.emit()
+                    loss, out = self.forward_backward(self._gx, self._gy)
+                    ex.finish()
+                except BaseException:
+                    self._rejoin_side()
+                    raise
             self._graphs = (g,)
         else:
             ex.defer_comm = True
             ga = torch.cuda.CUDAGraph()
             with torch.cuda.graph(ga, stream=self.gstream, capture_error_mode=mode):
-                if self._in_graph_batch:
-                    self._gx, self._gy = self.loader.emit()
-                loss, out = self.forward_backward(self._gx, self._gy)
-                ex.launch_pending()
+                try:
+                    if self._in_graph_batch:
+                        self._gx, self._gy = self.loader.emit()
+                    loss, out = self.forward_backward(self._gx, self._gy)
+                    ex.launch_pending()
+                except BaseException:
+                    self._rejoin_side()
+                    raise
                 ex.join_side()
             ex._active = False
             gb = torch.cuda.CUDAGraph()
@@ -345,6 +362,17 @@ class Trainer:
         ex.step_idx, self.opt.steps = saved
         self._gloss, self._gout = loss, out
         self._gbytes = ex.bytes_per_step()
+
+    def _rejoin_side(self):
+        """Join the encode side stream back into a capture being aborted: hipStreamEndCapture
+        refuses to close a capture with an unjoined fork and leaves the stream capturing."""
+        side = self.exchange.side
+        if side is None:
+            return
+        with torch.cuda.stream(side):
+            forked = torch.cuda.is_current_stream_capturing()
+        if forked:
+            torch.cuda.current_stream().wait_stream(side)
 
     def _graph_step(self, x, y):
         ex = self.exchange

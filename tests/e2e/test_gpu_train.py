@@ -136,6 +136,32 @@ def test_capture_after_single_eager_step():
     assert tr._graphs is not None and all(torch.isfinite(torch.tensor(losses)))
 
 
+def test_capture_failure_falls_back_to_eager(monkeypatch):
+    """A capture that fails after the encode was forked onto the side stream (the unjoined case)
+    must leave a trainer that keeps training eagerly, matching a never-graphed run."""
+    from ewdml.runtime import Trainer
+
+    ops.require()
+    ref, _ = _run(LENET + ["--compress", "topk_qsgd", "--hip-graph", "off"], 6)
+    torch.manual_seed(0)
+    tr = Trainer(ewdml.parse_args(LENET + ["--compress", "topk_qsgd", "--hip-graph", "full",
+                                           "--max-steps", "6"]))
+    orig = tr.exchange.finish
+
+    def finish(*a, **k):
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("injected capture failure")
+        return orig(*a, **k)
+
+    monkeypatch.setattr(tr.exchange, "finish", finish)
+    losses = [float(tr.train_step()[0].detach()) for _ in range(6)]
+    torch.cuda.synchronize()
+    assert tr.graph_mode == "off" and tr._graphs is None
+    assert all(l == l for l in losses)
+    rel = (tr.flat.data - ref.flat.data).norm() / ref.flat.data.norm()
+    assert rel < 1e-3, f"params differ from the eager run by {rel:.2e}"
+
+
 def _free_port():
     import socket
 
