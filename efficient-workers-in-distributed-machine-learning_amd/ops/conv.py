@@ -1,13 +1,20 @@
-"""Stride-1 3x3 (pad 1) and 1x1 convolutions on the gfx950 matrix cores (``ops/csrc/conv.hip``),
-and the 3-input-channel 3x3 stem (``k_conv_stem_*``).
+"""Stride-1 3x3 (pad 1) and 1x1 convolutions on the gfx950 matrix cores, and the
+3-input-channel 3x3 stem.
 
 :func:`conv` is ``F.conv2d(x, w, padding=k // 2)`` (no bias: the fused BN kernels fold the conv
-bias) for channels_last bf16 activations and weights, as an autograd function whose forward,
-backward-data and backward-weight are hand-written MFMA implicit-GEMM kernels (fp32 accumulation,
-bf16 results, like MIOpen's bf16 convolutions).  :func:`conv2d_module` dispatches an
-``nn.Conv2d`` (VGG's and ResNet's stride-1 3x3 / 1x1 layers).  Shapes the kernels do not take (C_in or C_out not a multiple of 64, fp32,
-NCHW, other strides/padding) go to ``F.conv2d`` (MIOpen) -- e.g. the ImageNet ResNet's 7x7/2
-stem.  ``EWDML_CONV=miopen`` (or ``set_enabled(False)``) routes every call to MIOpen (A/B).
+bias) for channels_last activations and weights, as an autograd function whose forward,
+backward-data and backward-weight are hand-written MFMA implicit-GEMM kernels:
+
+* bf16 operands (``ops/csrc/conv.hip``, ``v_mfma_f32_16x16x32_bf16``): fp32 accumulation, bf16
+  results, like MIOpen's bf16 convolutions;
+* fp32 operands (``ops/csrc/conv_f32.hip``, ``v_mfma_f32_16x16x4_f32``): exact fp32 products and
+  accumulation, fp32 results -- the reference's precision.
+
+:func:`conv2d_module` dispatches an ``nn.Conv2d`` (VGG's and ResNet's stride-1 3x3 / 1x1 layers).
+Shapes the kernels do not take (C_in or C_out not a multiple of 64, NCHW, other
+strides/padding) go to ``F.conv2d`` (MIOpen) -- e.g. the ImageNet ResNet's 7x7/2 stem.
+``EWDML_CONV=miopen`` (or ``set_enabled(False)``) routes every call to MIOpen (A/B),
+``EWDML_CONV_F32=miopen`` only the fp32 ones.
 
 Parity: the reference's convolutions are ``nn.Conv2d(..., kernel_size=3, padding=1)`` in
 ``src/model_ops/vgg.py:46-59`` and ``resnet.py:14-36``; only the execution differs.
@@ -20,6 +27,10 @@ import torch.nn.functional as F
 from . import _ptr, _stream, require
 
 _ENABLED = os.environ.get("EWDML_CONV", "hip") != "miopen"
+# operand dtypes the kernels take: bf16 (conv.hip) and fp32 (conv_f32.hip, reference precision);
+# EWDML_CONV_F32=miopen sends fp32 convolutions to MIOpen (A/B)
+_DTYPES = ((torch.bfloat16,) if os.environ.get("EWDML_CONV_F32", "hip") == "miopen"
+           else (torch.bfloat16, torch.float32))
 # BN-backward statistics of the producing layer in the backward-data epilogue (EWDML_CONV_BN_BWD=0:
 # the BN backward's own statistics pass)
 _BN_BWD = os.environ.get("EWDML_CONV_BN_BWD", "1") != "0"
@@ -74,7 +85,7 @@ def _geometry_ok(x, w, stride, padding, dilation, groups, sizes=(1, 3)):
         padding = k // 2
     if not (_one(stride, 1) and _one(padding, k // 2) and _one(dilation, 1) and groups == 1):
         return False
-    if x.dtype != torch.bfloat16 or w.dtype != torch.bfloat16 or w.shape[1] != x.shape[1]:
+    if x.dtype not in _DTYPES or w.dtype != x.dtype or w.shape[1] != x.shape[1]:
         return False
     return (x.is_contiguous(memory_format=torch.channels_last)
             and w.is_contiguous(memory_format=torch.channels_last))
@@ -123,7 +134,7 @@ def _bn_bwd_link(node, x):
         h, res, code, stats = node.saved_tensors
     except RuntimeError:  # already freed
         return None
-    if h.dtype != torch.bfloat16 or node.mode not in ("relu", "none", "add_relu"):
+    if h.dtype != x.dtype or node.mode not in ("relu", "none", "add_relu"):
         return None
     N, C, H, W = x.shape
     scale = 2 if node.pool else 1
@@ -144,8 +155,9 @@ class _Conv(torch.autograd.Function):
         # BatchNorm partial sums of y from the epilogue (bounded by 2 rows per 64 output rows);
         # the following fused BN (ops/nn.py bn_act) skips its statistics pass when present
         part = torch.empty(_part_floats(N * H * W, Nc), dtype=torch.float32, device=x.device)
-        rows = C_.conv_fwd(_ptr(x), _ptr(w), _ptr(y), _ptr(ws), ws.numel(), N, H, W, C, Nc, k,
-                           _ptr(part), part.numel(), _stream())
+        fwd = C_.conv_f32_fwd if x.dtype == torch.float32 else C_.conv_fwd
+        rows = fwd(_ptr(x), _ptr(w), _ptr(y), _ptr(ws), ws.numel(), N, H, W, C, Nc, k,
+                   _ptr(part), part.numel(), _stream())
         ctx.save_for_backward(x, w)
         ctx.bn_part = (part, rows) if rows > 0 else None
         ctx.bn_node = bn_node
@@ -162,6 +174,8 @@ class _Conv(torch.autograd.Function):
         if dy.dtype != x.dtype:
             dy = dy.to(x.dtype)
         ws = _ws(x.device)
+        f32 = x.dtype == torch.float32
+        bwd_data = C_.conv_f32_bwd_data if f32 else C_.conv_bwd_data
         dx = dw = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x, memory_format=torch.channels_last)
@@ -176,24 +190,25 @@ class _Conv(torch.autograd.Function):
                 add = add.contiguous(memory_format=torch.channels_last).to(x.dtype)
             link = _bn_bwd_link(node, x)
             if link is None:
-                C_.conv_bwd_data(_ptr(dy), _ptr(w), _ptr(dx), _ptr(ws), ws.numel(), N, H, W, C,
-                                 Nc, k, 0, 0, 0, 0, 0, 0, 0, _ptr(add), _stream())
+                bwd_data(_ptr(dy), _ptr(w), _ptr(dx), _ptr(ws), ws.numel(), N, H, W, C, Nc, k, 0,
+                         0, 0, 0, 0, 0, 0, _ptr(add), _stream())
             else:
                 # the producing BN layer's backward sums (sum dz, sum dz*(h-mean)) per 64 rows
                 h, res, code, stats, relu = link
                 part = torch.empty(_part_floats(N * H * W, C), dtype=torch.float32,
                                    device=x.device)
-                rows = C_.conv_bwd_data(_ptr(dy), _ptr(w), _ptr(dx), _ptr(ws), ws.numel(), N, H,
-                                        W, C, Nc, k, _ptr(h), _ptr(res), _ptr(code), _ptr(stats),
-                                        relu, _ptr(part), part.numel(), _ptr(add), _stream())
+                rows = bwd_data(_ptr(dy), _ptr(w), _ptr(dx), _ptr(ws), ws.numel(), N, H, W, C,
+                                Nc, k, _ptr(h), _ptr(res), _ptr(code), _ptr(stats), relu,
+                                _ptr(part), part.numel(), _ptr(add), _stream())
                 if rows > 0:
                     node._ew_pre_bwd = (part, rows, dx, dx._version)
             if sink is not None:
                 sink.grad = None
         if ctx.needs_input_grad[1]:
             dw = torch.empty_like(w, memory_format=torch.channels_last)
-            C_.conv_wgrad(_ptr(dy), _ptr(x), _ptr(dw), _ptr(ws), ws.numel(), N, H, W, C, Nc, k,
-                          _stream())
+            wgrad = C_.conv_f32_wgrad if f32 else C_.conv_wgrad
+            wgrad(_ptr(dy), _ptr(x), _ptr(dw), _ptr(ws), ws.numel(), N, H, W, C, Nc, k,
+                  _stream())
         return dx, dw, None, None
 
 
@@ -210,8 +225,8 @@ class _ConvStem(torch.autograd.Function):
                         memory_format=torch.channels_last)
         part = torch.empty(max(1, 2 * (N * H * W // 128) * Nc), dtype=torch.float32,
                            device=x.device)
-        rows = C_.conv_stem_fwd(_ptr(x), _ptr(w), _ptr(y), N, H, W, Nc, _ptr(part), part.numel(),
-                                _stream())
+        fwd = C_.conv_f32_stem_fwd if x.dtype == torch.float32 else C_.conv_stem_fwd
+        rows = fwd(_ptr(x), _ptr(w), _ptr(y), N, H, W, Nc, _ptr(part), part.numel(), _stream())
         ctx.save_for_backward(x, w)
         ctx.bn_part = (part, rows) if rows > 0 else None
         return y
@@ -234,8 +249,8 @@ class _ConvStem(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             ws = _ws(x.device)
             dw = torch.empty_like(w, memory_format=torch.channels_last)
-            C_.conv_stem_wgrad(_ptr(dy), _ptr(x), _ptr(dw), _ptr(ws), ws.numel(), N, H, W, Nc,
-                               _stream())
+            wgrad = C_.conv_f32_stem_wgrad if x.dtype == torch.float32 else C_.conv_stem_wgrad
+            wgrad(_ptr(dy), _ptr(x), _ptr(dw), _ptr(ws), ws.numel(), N, H, W, Nc, _stream())
         return dx, dw
 
 
@@ -282,7 +297,7 @@ def module_supported(m, x) -> bool:
 
 def conv2d_module(m, x, sink=None):
     """``m(x)`` for an ``nn.Conv2d`` ``m`` without bias, through the MFMA kernels when the layer
-    is a stride-1 3x3/pad-1 or 1x1/pad-0 convolution on channels_last bf16 (else ``m(x)``).
+    is a stride-1 3x3/pad-1 or 1x1/pad-0 convolution on channels_last bf16/fp32 (else ``m(x)``).
     ``sink`` (:class:`GradSink`, MFMA path only): a second gradient of ``x`` deposited there
     before this conv's backward is added to its input gradient."""
     if (m.bias is None and m.padding_mode == "zeros"

@@ -260,6 +260,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("head_fwd", &ew_head_fwd);
   m.def("head_bwd", &ew_head_bwd);
   m.def("conv_stem_wgrad", &ew_conv_stem_wgrad);
+  m.def("conv_f32_fwd", &ew_conv_f32_fwd);
+  m.def("conv_f32_bwd_data", &ew_conv_f32_bwd_data);
+  m.def("conv_f32_wgrad", &ew_conv_f32_wgrad);
+  m.def("conv_f32_stem_fwd", &ew_conv_f32_stem_fwd);
+  m.def("conv_f32_stem_wgrad", &ew_conv_f32_stem_wgrad);
   m.def("maxpool2_nhwc", &ew_maxpool2_nhwc);
   m.def("maxpool2_fwd", &ew_maxpool2_fwd);
   m.def("maxpool2_bwd", &ew_maxpool2_bwd);

@@ -1,0 +1,990 @@
+// fp32 convolutions on the gfx950 matrix cores: 3x3 / stride 1 / pad 1 and 1x1 implicit GEMMs
+// (NHWC, fp32 operands, fp32 accumulate, v_mfma_f32_16x16x4_f32) -- forward, backward-data and
+// backward-weight -- plus the 3-input-channel stem.  This is the reference-precision path: the
+// reference trains in plain fp32 (PyTorch-parameter-server/src/distributed_worker.py:249-251,
+// src/optim/sgd.py:59-91), so these kernels do exact fp32 products (no bf16/xf32 splitting).
+//
+// Budget.  fp32 MFMA runs at 64 FLOP/clk/SIMD (157 TF/s on 256 CUs), 1/16 of the bf16 rate, so a
+// fp32 conv GEMM is compute-bound as soon as a block keeps its matrix pipes fed: a 128x128 output
+// tile (4 waves x 64x64) does 4096 MFMA cycles per 32-deep k-step against 32 KB of operand loads
+// (~19 GB/s per CU, served by L2 / Infinity Cache).  MIOpen's fp32 NHWC solvers reach 100-123 TF/s
+// on VGG-11's forward layers but need a zero-fill kernel before every backward call and run the
+// backward passes at 60-100 TF/s (profiles/vgg11_fp32_miopen.txt).
+//
+//   forward     y[m][n]  = sum_{k=(tap,c)} X~[m][k] * w[n][k]          X~ = im2col(x), implicit
+//   bwd data   dx[m][c]  = sum_{k=(tap,n)} dY~[m][k] * w[n][8-tap][c]
+//   bwd weight dw[n][k]  = sum_m dy[m][n] * X~[m][k]
+//
+// Operand images in LDS, one 32-deep k-step per stage (double buffered, register staged):
+//  * KC ("k contiguous": forward A and B, backward-data A): [rows][32 floats], 128-B rows, 16-B
+//    chunk c of row r at c ^ ((r >> 1) & 7) (the bf16 kernels' swizzle: a ds_read_b128 lane group
+//    reading 16 rows at one chunk hits 16 distinct bank slots).  A lane reads 4 consecutive k of
+//    its row with one ds_read_b128.
+//  * RC ("rows contiguous": backward-data B, both weight-gradient operands): [32 k][cols + 4]
+//    floats as they lie in global memory; a lane reads one element per MFMA (ds_read_b32, the
+//    +4 pad puts k and k + 4 -- the two halves of a 32-lane group -- 16 banks apart).
+// The MFMA k order is permuted consistently in both operands: MFMA jj of half-step kk gives lane
+// group g the reduction index kk*16 + 4g + jj, which is what a b128 read of chunk kk*4 + g yields.
+//
+// 16x16x4 f32 MFMA operand map: A lane l = A[l & 15][l >> 4], B lane l = B[l >> 4][l & 15];
+// D lane l reg q = D[4 (l >> 4) + q][l & 15].
+#include <cstdio>
+#include <cstdlib>
+
+#include "common.h"
+#include "ewdml_ops.h"
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int CF_BK = 32;  // reduction depth of one k-step (floats)
+enum { CF_FWD = 0, CF_BWD = 1, CF_WGRAD = 2 };
+#ifndef CF_PRIO
+#define CF_PRIO 1  // s_setprio(1) around each MFMA cluster (cdna_hip_programming.md T5)
+#endif
+
+__device__ __forceinline__ int cf_off(int r, int c) {  // byte offset of chunk c of row r (KC)
+  return r * 128 + ((c ^ ((r >> 1) & 7)) << 4);
+}
+
+// Backward-statistics operands of the BN(+ReLU)(+2x2 max pool)(+residual) layer whose output
+// gradient a backward-data launch produces (conv.hip CvBnBwd, fp32 tensors): the epilogue sums
+// dz = act'(h * scale + shift [+ res]) * dx and dz * (h - mean) per channel (the BN backward then
+// skips its statistics pass).
+struct CfBnBwd {
+  const float* h;       // BN input [rows (pre-pool)][C]; null: not requested
+  const float* res;     // residual input (BN + residual + ReLU) or null
+  const uint8_t* code;  // pool window codes [rows][C] (null: no pool)
+  const float* stats;   // [4][C]: mean, invstd, scale, shift
+  int relu;
+  int Ho, Wo;           // pooled map dims (pool)
+};
+
+__device__ __forceinline__ uint32_t cf_pool_row(uint32_t p, uint32_t HoWo, uint32_t Wo,
+                                                uint32_t q) {
+  const uint32_t n = p / HoWo, rem = p - n * HoWo;
+  const uint32_t ho = rem / Wo, wo = rem - ho * Wo;
+  return 4 * n * HoWo + 4 * ho * Wo + 2 * wo + (q >> 1) * (2 * Wo) + (q & 1);
+}
+
+struct CfGeom {
+  int M;      // GEMM rows (fwd/bwd: pixels N*H*W; wgrad: output channels Nc)
+  int Ncol;   // GEMM columns (fwd: Nc; bwd: C; wgrad: taps*C)
+  int P;      // pixels N*H*W
+  int H, W;
+  int C;      // fwd/wgrad: input channels of x; bwd: output channels of dx
+  int Nc;     // fwd/wgrad: output channels; bwd: the reduction channels (forward's output)
+  int taps;   // 9 or 1
+  int ksteps, kps;
+};
+
+// Stage images: A then B, KC or RC by mode.
+template <int MODE, int BM, int BN>
+struct CfLayout {
+  static constexpr bool A_KC = MODE != CF_WGRAD;
+  static constexpr bool B_KC = MODE == CF_FWD;
+  static constexpr int PA = BM + 4, PB = BN + 4;  // RC row pitches (floats)
+  static constexpr int A_BYTES = A_KC ? BM * 128 : CF_BK * PA * 4;
+  static constexpr int B_BYTES = B_KC ? BN * 128 : CF_BK * PB * 4;
+  static constexpr int STAGE = A_BYTES + B_BYTES;
+};
+
+// fp32 MFMA shapes.  16x16x4 (4 accumulator regs, 32-cycle issue): A lane l = A[l & 15][l >> 4],
+// B lane l = B[l >> 4][l & 15], D lane l reg e = D[4 (l >> 4) + e][l & 15].  32x32x2 (16 regs,
+// 64-cycle issue, half the instructions per FLOP): A lane l = A[l & 31][l >> 5], B lane l =
+// B[l >> 5][l & 31], D lane l reg e = D[8 (e >> 2) + 4 (l >> 5) + (e & 3)][l & 31].
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+template <int SH>
+struct CfMfma;
+template <>
+struct CfMfma<16> {
+  typedef f32x4 acc_t;
+  static constexpr int E = 4, G = 4;  // accumulator regs; lane groups (k values per MFMA)
+  __device__ static __forceinline__ int out_row(int lane, int e) { return 4 * (lane >> 4) + e; }
+  __device__ static __forceinline__ acc_t mma(float a, float b, const acc_t& c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+  }
+};
+template <>
+struct CfMfma<32> {
+  typedef f32x16 acc_t;
+  static constexpr int E = 16, G = 2;
+  __device__ static __forceinline__ int out_row(int lane, int e) {
+    return 8 * (e >> 2) + 4 * (lane >> 5) + (e & 3);
+  }
+  __device__ static __forceinline__ acc_t mma(float a, float b, const acc_t& c) {
+    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+  }
+};
+
+// One k-step of MFMAs over a stage: acc[i][j] += A[wave rows][32] * B[wave cols][32]^T.  Lane
+// group g (lane / SH) takes the 8/G 16-B chunks r*G + g (r < 8/G) of the 32-deep step: read r
+// holds k = 4 (r G + g) + jj in element jj, and MFMA (r, jj) consumes element jj of both operands,
+// so every k is used exactly once with the same permutation in A and B.
+template <int MODE, int BM, int BN, int SH, int MI, int NJ>
+__device__ __forceinline__ void cf_mma(const char* __restrict__ As, const char* __restrict__ Bs,
+                                       int arow0, int bcol0, int lane,
+                                       typename CfMfma<SH>::acc_t (&acc)[MI][NJ]) {
+  using L = CfLayout<MODE, BM, BN>;
+  using F = CfMfma<SH>;
+  constexpr int R = 8 / F::G;
+  const int g = lane / SH, li = lane % SH;
+  f32x4 a[R][MI], b[R][NJ];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int ch = r * F::G + g;
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      if constexpr (L::A_KC) {
+        a[r][i] = *reinterpret_cast<const f32x4*>(As + cf_off(arow0 + i * SH + li, ch));
+      } else {
+        const float* ap = reinterpret_cast<const float*>(As) + 4 * ch * L::PA + arow0 + i * SH + li;
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) a[r][i][jj] = ap[jj * L::PA];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      if constexpr (L::B_KC) {
+        b[r][j] = *reinterpret_cast<const f32x4*>(Bs + cf_off(bcol0 + j * SH + li, ch));
+      } else {
+        const float* bp = reinterpret_cast<const float*>(Bs) + 4 * ch * L::PB + bcol0 + j * SH + li;
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) b[r][j][jj] = bp[jj * L::PB];
+      }
+    }
+  }
+  if (CF_PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = F::mma(a[r][i][jj], b[r][j][jj], acc[i][j]);
+  if (CF_PRIO) __builtin_amdgcn_s_setprio(0);
+}
+
+// Staging registers of one operand: R 16-B vectors per thread (named members: no scratch)
+struct CfRegs {
+  f32x4 v0, v1, v2, v3;
+};
+#define CF_FOR(R_, ...)                                                                         \
+  do {                                                                                          \
+    { constexpr int i = 0; auto& v = RG.v0; __VA_ARGS__; }                                     \
+    if constexpr (R_ > 1) { constexpr int i = 1; auto& v = RG.v1; __VA_ARGS__; }               \
+    if constexpr (R_ > 2) { constexpr int i = 2; auto& v = RG.v2; __VA_ARGS__; }               \
+    if constexpr (R_ > 3) { constexpr int i = 3; auto& v = RG.v3; __VA_ARGS__; }               \
+  } while (0)
+
+// Per-thread operand staging state (CF_NT threads).  KC tiles: thread t stages chunk t & 7 of rows
+// (t >> 3) + 64 i (i < BM/64).  RC tiles ([32 k][BN cols]): BN/4 chunks per k-row, thread t
+// stages chunk t % (BN/4) of k-rows t / (BN/4) + (2048/BN) i (i < BN/64).
+constexpr int CF_NT = 512;  // threads per GEMM block: 8 waves, two per SIMD
+constexpr int CF_D = 4;     // k-loop prefetch depth (staging register sets; even)
+template <int MODE, int BM, int BN>
+struct CfStager {
+  using L = CfLayout<MODE, BM, BN>;
+  static constexpr int RA = BM / 64, RB = BN / 64;
+  static constexpr int RCA = BM / 4, RCB = BN / 4;              // RC chunks per k-row
+  static constexpr int RPA = CF_NT / RCA, RPB = CF_NT / RCB;    // RC k-rows per pass
+  // KC im2col rows (fwd, bwd A): pixel and its (h, w)
+  int am[RA], ah[RA], aw[RA];
+  // wgrad B: the thread's column chunk's tap offset and channel
+  int bdr, bdc, bc;
+  const float* xa;  // A source
+  const float* xb;  // B source
+  int t, m0, n0;
+
+  __device__ __forceinline__ void init(const CfGeom& g, const float* a_src, const float* b_src,
+                                       int t_, int m0_, int n0_) {
+    t = t_;
+    m0 = m0_;
+    n0 = n0_;
+    xa = a_src;
+    xb = b_src;
+    if constexpr (L::A_KC) {
+#pragma unroll
+      for (int i = 0; i < RA; ++i) {
+        const int m = m0 + (t >> 3) + 64 * i;
+        am[i] = m;
+        const int hw = m % (g.H * g.W);
+        ah[i] = hw / g.W;
+        aw[i] = hw - ah[i] * g.W;
+      }
+    }
+    if constexpr (MODE == CF_WGRAD) {
+      const int k = n0 + (t % RCB) * 4;  // column (tap, c) of this thread's chunk
+      const int tap = k / g.C;
+      bc = k - tap * g.C;
+      bdr = g.taps == 1 ? 0 : tap / 3 - 1;
+      bdc = g.taps == 1 ? 0 : tap - (tap / 3) * 3 - 1;
+    }
+  }
+
+  // global -> registers for k-step s
+  __device__ __forceinline__ void load(const CfGeom& g, int s, CfRegs& ra, CfRegs& rb) const {
+    if constexpr (MODE == CF_FWD || MODE == CF_BWD) {
+      // A: im2col of x (fwd, channels C) or dy (bwd, channels Nc)
+      const int CH = MODE == CF_FWD ? g.C : g.Nc;
+      const int CB = CH / CF_BK;
+      const int tap = s / CB, cb = s - tap * CB;
+      const int dr = g.taps == 1 ? 0 : tap / 3 - 1, dc = g.taps == 1 ? 0 : tap - (tap / 3) * 3 - 1;
+      {
+        CfRegs& RG = ra;
+        CF_FOR(RA, {
+          const bool ok = (unsigned)(ah[i] + dr) < (unsigned)g.H &&
+                          (unsigned)(aw[i] + dc) < (unsigned)g.W;
+          const f32x4 x_ = *reinterpret_cast<const f32x4*>(
+              xa + (long long)(ok ? am[i] + dr * g.W + dc : 0) * CH + cb * CF_BK + (t & 7) * 4);
+          v = ok ? x_ : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        });
+      }
+      if constexpr (MODE == CF_FWD) {
+        // B: w[n][taps*C], k index s*32 + chunk*4
+        const long long K = (long long)g.taps * g.C;
+        CfRegs& RG = rb;
+        CF_FOR(RB, {
+          v = *reinterpret_cast<const f32x4*>(xb + (long long)(n0 + (t >> 3) + 64 * i) * K +
+                                              (long long)s * CF_BK + (t & 7) * 4);
+        });
+      } else {
+        // B (RC): k-row kr = reduction channel n = cb*32 + kr at the flipped tap; columns c
+        const int ft = g.taps - 1 - tap;
+        CfRegs& RG = rb;
+        CF_FOR(RB, {
+          const int kr = t / RCB + RPB * i;
+          v = *reinterpret_cast<const f32x4*>(
+              xb + ((long long)(cb * CF_BK + kr) * g.taps + ft) * g.C + n0 + (t % RCB) * 4);
+        });
+      }
+    } else {
+      // wgrad: k = pixel m = s*32 + kr.  A (RC): dy[m][rows m0..]; B (RC): im2col x[m][(tap,c)]
+      {
+        CfRegs& RG = ra;
+        CF_FOR(RA, {
+          const int kr = t / RCA + RPA * i;
+          v = *reinterpret_cast<const f32x4*>(xa + (long long)(s * CF_BK + kr) * g.Nc + m0 +
+                                              (t % RCA) * 4);
+        });
+      }
+      {
+        const int HW = g.H * g.W;
+        CfRegs& RG = rb;
+        CF_FOR(RB, {
+          const int m = s * CF_BK + t / RCB + RPB * i;
+          const int hw = m % HW, h = hw / g.W, w = hw - h * g.W;
+          const bool ok = (unsigned)(h + bdr) < (unsigned)g.H && (unsigned)(w + bdc) < (unsigned)g.W;
+          const f32x4 x_ = *reinterpret_cast<const f32x4*>(
+              xb + (long long)(ok ? m + bdr * g.W + bdc : 0) * g.C + bc);
+          v = ok ? x_ : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        });
+      }
+    }
+  }
+
+  // registers -> LDS stage
+  __device__ __forceinline__ void store(char* stage, const CfRegs& ra, const CfRegs& rb) const {
+    char* As = stage;
+    char* Bs = stage + L::A_BYTES;
+    {
+      const CfRegs& RG = ra;
+      if constexpr (L::A_KC) {
+        CF_FOR(RA, { *reinterpret_cast<f32x4*>(As + cf_off((t >> 3) + 64 * i, t & 7)) = v; });
+      } else {
+        CF_FOR(RA, {
+          *reinterpret_cast<f32x4*>(As + ((t / RCA + RPA * i) * L::PA + (t % RCA) * 4) * 4) = v;
+        });
+      }
+    }
+    {
+      const CfRegs& RG = rb;
+      if constexpr (L::B_KC) {
+        CF_FOR(RB, { *reinterpret_cast<f32x4*>(Bs + cf_off((t >> 3) + 64 * i, t & 7)) = v; });
+      } else {
+        CF_FOR(RB, {
+          *reinterpret_cast<f32x4*>(Bs + ((t / RCB + RPB * i) * L::PB + (t % RCB) * 4) * 4) = v;
+        });
+      }
+    }
+  }
+};
+
+// Epilogue: fp32 output (or split slab) + optional addend, forward BN partial sums of the output
+// (sum, sum of squares per column over the block's BM rows -> row blockIdx.x of
+// bnpart[2][M/BM][Ncol]) or the backward sums of CfBnBwd.  Waves form a WM x WN grid of
+// (BM/WM) x (BN/WN) tiles of MI x NJ SH x SH MFMA blocks.
+template <int BM, int BN, int WM, int WN, int SH, int MI, int NJ>
+__device__ __forceinline__ void cf_epilogue(typename CfMfma<SH>::acc_t (&acc)[MI][NJ], char* smem,
+                                            int wm, int wn, int lane, int m0, int n0, int M,
+                                            int Nc, float* __restrict__ out,
+                                            float* __restrict__ slab, float* __restrict__ bnpart,
+                                            const CfBnBwd& bb, const float* __restrict__ addend) {
+  using F = CfMfma<SH>;
+  constexpr int E = F::E;
+  const int row0 = m0 + wm * (BM / WM), col0 = n0 + wn * (BN / WN);
+  const int li = lane % SH;
+  auto row_of = [&](int i, int e) { return row0 + i * SH + F::out_row(lane, e); };
+  auto col_of = [&](int j) { return col0 + j * SH + li; };
+  if (slab) {
+    float* sp = slab + (long long)blockIdx.z * M * Nc;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int e = 0; e < E; ++e)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) sp[(long long)row_of(i, e) * Nc + col_of(j)] = acc[i][j][e];
+    return;
+  }
+  if (addend) {
+    float av[MI][NJ][E];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int e = 0; e < E; ++e)
+          av[i][j][e] = addend[(long long)row_of(i, e) * Nc + col_of(j)];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int e = 0; e < E; ++e) acc[i][j][e] += av[i][j][e];
+  }
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int e = 0; e < E; ++e)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) out[(long long)row_of(i, e) * Nc + col_of(j)] = acc[i][j][e];
+  if (!bnpart) return;
+  float* red = reinterpret_cast<float*>(smem);  // [wm][wn][2][BN/WN]
+  const long long nrows = M / BM;
+  float sm[NJ], sq[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    sm[j] = sq[j] = 0.0f;
+    const int c = col_of(j);
+    if (bb.h) {
+      const float mean = bb.stats[c], sc = bb.stats[2 * Nc + c], sh = bb.stats[3 * Nc + c];
+      const uint32_t HoWo = (uint32_t)bb.Ho * bb.Wo;
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        // all window codes, then all h values are loaded before any use (batched round trips)
+        uint32_t hr[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) hr[e] = row_of(i, e);
+        if (bb.code) {
+          uint8_t kc[E];
+#pragma unroll
+          for (int e = 0; e < E; ++e) kc[e] = bb.code[(size_t)hr[e] * Nc + c];
+#pragma unroll
+          for (int e = 0; e < E; ++e) hr[e] = cf_pool_row(hr[e], HoWo, (uint32_t)bb.Wo, kc[e]);
+        }
+        float xv[E], rv[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          xv[e] = bb.h[(size_t)hr[e] * Nc + c];
+          rv[e] = bb.res ? bb.res[(size_t)hr[e] * Nc + c] : 0.0f;
+        }
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const float d = acc[i][j][e];
+          float v = xv[e] * sc + sh;  // the BN kernels' arithmetic (no contraction)
+          if (bb.res) v = v + rv[e];
+          const float dz = (bb.relu == 0 || !(v <= 0.0f)) ? d : 0.0f;
+          sm[j] += dz;
+          sq[j] += dz * (xv[e] - mean);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const float v = acc[i][j][e];
+          sm[j] += v;
+          sq[j] += v * v;
+        }
+    }
+    // lanes holding the same column: SH = 16 -> l, l^16, l^32, l^48; SH = 32 -> l, l^32
+    if constexpr (SH == 16) {
+      sm[j] += __shfl_xor(sm[j], 16, 64);
+      sq[j] += __shfl_xor(sq[j], 16, 64);
+    }
+    sm[j] += __shfl_xor(sm[j], 32, 64);
+    sq[j] += __shfl_xor(sq[j], 32, 64);
+  }
+  __syncthreads();  // main loop finished reading smem
+  constexpr int CW = BN / WN;  // columns per wave
+  if (wm > 0 && lane < SH) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      red[((wm * WN + wn) * 2 + 0) * CW + j * SH + lane] = sm[j];
+      red[((wm * WN + wn) * 2 + 1) * CW + j * SH + lane] = sq[j];
+    }
+  }
+  __syncthreads();
+  if (wm == 0 && lane < SH) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      float a = sm[j], q = sq[j];
+#pragma unroll
+      for (int r = 1; r < WM; ++r) {  // fixed order
+        a += red[((r * WN + wn) * 2 + 0) * CW + j * SH + lane];
+        q += red[((r * WN + wn) * 2 + 1) * CW + j * SH + lane];
+      }
+      const int c = col0 + j * SH + lane;
+      bnpart[(long long)blockIdx.x * Nc + c] = a;
+      bnpart[(nrows + blockIdx.x) * Nc + c] = q;
+    }
+  }
+}
+
+// The GEMM kernel: block = 8 waves (two per SIMD) in a WM x (8/WM) grid over a BM x BN tile, one
+// 32-deep k-step per iteration through two LDS stages and two staging register sets (step s+2 is
+// loaded while s computes and s+1 is written), split z covers k-steps
+// [z*kps, min((z+1)*kps, ksteps)).
+template <int MODE, int BM, int BN, int WM, int SH>
+__global__ __launch_bounds__(CF_NT) void k_cf_gemm(const float* __restrict__ a_src,
+                                                   const float* __restrict__ b_src,
+                                                   float* __restrict__ out,
+                                                   float* __restrict__ slab, CfGeom geo,
+                                                   float* __restrict__ bnpart, CfBnBwd bb,
+                                                   const float* __restrict__ addend) {
+  using L = CfLayout<MODE, BM, BN>;
+  using acc_t = typename CfMfma<SH>::acc_t;
+  constexpr int WN = 8 / WM;
+  constexpr int MI = BM / WM / SH, NJ = BN / WN / SH;
+  static_assert(MI >= 1 && NJ >= 1 && MI * SH * WM == BM && NJ * SH * WN == BN, "wave tiling");
+  __shared__ __attribute__((aligned(16))) char smem[2 * L::STAGE];
+  const int t = threadIdx.x, lane = t & 63, wq = t >> 6;
+  const int wm = wq / WN, wn = wq % WN;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int kbeg = blockIdx.z * geo.kps;
+  const int kend = min(kbeg + geo.kps, geo.ksteps);
+  CfStager<MODE, BM, BN> st;
+  st.init(geo, a_src, b_src, t, m0, n0);
+
+  acc_t acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = acc_t{};
+
+  const int n = kend - kbeg;
+  if (n > 0) {
+    const int last = kend - 1;
+    // CF_D staging register sets: the loads of step i + CF_D are issued at iteration i into the
+    // set that held step i (written to LDS one iteration earlier), so a load has CF_D - 1
+    // iterations (~3-5 us) to land before its LDS write; two LDS stages, one barrier per step.
+    // Loads past the end are clamped re-loads of the last step (branch-free, no scratch).
+    CfRegs ra[CF_D], rb[CF_D];
+#pragma unroll
+    for (int j = 0; j < CF_D; ++j) st.load(geo, min(kbeg + j, last), ra[j], rb[j]);
+    st.store(smem, ra[0], rb[0]);
+    __syncthreads();
+    for (int i0 = 0; i0 < n; i0 += CF_D) {
+#pragma unroll
+      for (int u = 0; u < CF_D; ++u) {
+        const int i = i0 + u;
+        st.load(geo, min(kbeg + i + CF_D, last), ra[u], rb[u]);
+        char* cur = smem + (u & 1) * L::STAGE;
+        if (i < n)
+          cf_mma<MODE, BM, BN, SH, MI, NJ>(cur, cur + L::A_BYTES, wm * (BM / WM),
+                                           wn * (BN / WN), lane, acc);
+        st.store(smem + ((u + 1) & 1) * L::STAGE, ra[(u + 1) % CF_D], rb[(u + 1) % CF_D]);
+        __syncthreads();
+      }
+    }
+  }
+  cf_epilogue<BM, BN, WM, WN, SH, MI, NJ>(acc, smem, wm, wn, lane, m0, n0, geo.M, geo.Ncol,
+                                          out, slab, bnpart, bb, addend);
+}
+
+// out[i] = sum_z slab[z][i] (+ addend), 8 elements per thread
+__global__ __launch_bounds__(EW_BLOCK) void k_cf_slab_reduce(const float* __restrict__ slab,
+                                                             int nsplit, long long n,
+                                                             float* __restrict__ out,
+                                                             const float* __restrict__ addend) {
+  const long long nv = n / 4;
+  for (long long v = blockIdx.x * (long long)EW_BLOCK + threadIdx.x; v < nv;
+       v += (long long)gridDim.x * EW_BLOCK) {
+    const f32x4* p = reinterpret_cast<const f32x4*>(slab) + v;
+    f32x4 a = p[0];
+    for (int z = 1; z < nsplit; ++z) a += p[(long long)z * (n / 4)];  // fixed order
+    if (addend) a += reinterpret_cast<const f32x4*>(addend)[v];
+    reinterpret_cast<f32x4*>(out)[v] = a;
+  }
+}
+
+// Split-K reduction that also writes the BN partial sums of its output (forward sums or the
+// backward sums of CfBnBwd).  Block b: rows [b * rpb, (b + 1) * rpb) x all Nc columns; thread:
+// column quad t % tpr (tpr = Nc / 4), rows t / tpr + k * rpi; one partial row per block.
+__global__ __launch_bounds__(EW_BLOCK) void k_cf_slab_reduce_bn(const float* __restrict__ slab,
+                                                                int nsplit, int M, int Nc,
+                                                                float* __restrict__ out,
+                                                                float* __restrict__ bnpart,
+                                                                int rpb, CfBnBwd bb,
+                                                                const float* __restrict__ addend) {
+  __shared__ float red[2][EW_BLOCK * 4];  // [2][rpi][Nc]: rpi * Nc = 4 * EW_BLOCK
+  const int tpr = Nc >> 2, rpi = EW_BLOCK / tpr;
+  const int t = threadIdx.x, gq = t % tpr, rg = t / tpr;
+  const int c0 = gq * 4;
+  const long long n = (long long)M * Nc;
+  const int r0 = blockIdx.x * rpb, r1 = min(r0 + rpb, M);
+  float s1[4], s2[4], mean[4], sc[4], sh[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) s1[j] = s2[j] = 0.0f;
+  if (bb.h && rg < rpi) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      mean[j] = bb.stats[c0 + j];
+      sc[j] = bb.stats[2 * Nc + c0 + j];
+      sh[j] = bb.stats[3 * Nc + c0 + j];
+    }
+  }
+  const uint32_t HoWo = (uint32_t)bb.Ho * bb.Wo;
+  if (rg < rpi) {
+    for (int r = r0 + rg; r < r1; r += rpi) {
+      const long long o = (long long)r * Nc + c0;
+      const f32x4* p = reinterpret_cast<const f32x4*>(slab + o);
+      f32x4 a = p[0];
+      for (int z = 1; z < nsplit; ++z) a += p[(long long)z * (n / 4)];
+      if (addend) a += *reinterpret_cast<const f32x4*>(addend + o);
+      *reinterpret_cast<f32x4*>(out + o) = a;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float d = a[j];
+        if (bb.h) {
+          uint32_t hr = (uint32_t)r;
+          if (bb.code) hr = cf_pool_row((uint32_t)r, HoWo, (uint32_t)bb.Wo, bb.code[o + j]);
+          const float x = bb.h[(size_t)hr * Nc + c0 + j];
+          float v = x * sc[j] + sh[j];
+          if (bb.res) v = v + bb.res[(size_t)hr * Nc + c0 + j];
+          const float dz = (bb.relu == 0 || !(v <= 0.0f)) ? d : 0.0f;
+          s1[j] += dz;
+          s2[j] += dz * (x - mean[j]);
+        } else {
+          s1[j] += d;
+          s2[j] += d * d;
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      red[0][rg * Nc + c0 + j] = s1[j];
+      red[1][rg * Nc + c0 + j] = s2[j];
+    }
+  }
+  __syncthreads();
+  const int nb = gridDim.x;
+  for (int c = t; c < Nc; c += EW_BLOCK) {
+    float a = 0.0f, q = 0.0f;
+    for (int i = 0; i < rpi; ++i) {  // fixed order
+      a += red[0][i * Nc + c];
+      q += red[1][i * Nc + c];
+    }
+    bnpart[(long long)blockIdx.x * Nc + c] = a;
+    bnpart[(long long)(nb + blockIdx.x) * Nc + c] = q;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Stem (C = 3): K = 27 = 9 taps x 3 channels (the channels_last weight order), padded to 28 =
+// seven 16x16x4 MFMA steps.  Forward block = 128 pixels x 64 channels (wave v: pixels 32v..32v+31
+// = 2 x 4 tiles), im2col gathered from an LDS copy of the input rows the block touches, output
+// staged in LDS for 16-B stores, BN partial sums from the registers.
+constexpr int CS_K = 27, CS_KP = 28;
+constexpr int CS_WMAX = 256;
+template <int PIX>
+constexpr int cs_patch_floats() { return (PIX + 2 * CS_WMAX + 2) * 3 + 8; }
+
+template <int PIX>
+__device__ __forceinline__ int cs_patch(const float* __restrict__ x, int m0, int W, int M,
+                                        float* patch, int t) {
+  int lo = (m0 - W - 1) * 3;
+  lo = lo < 0 ? 0 : (lo & ~3);
+  int hi = ((m0 + PIX + W + 1) * 3 + 3) & ~3;
+  hi = hi > 3 * M ? 3 * M : hi;
+  const int nch = (hi - lo) >> 2;
+  for (int c = t; c < nch; c += EW_BLOCK)
+    *reinterpret_cast<f32x4*>(patch + 4 * c) = *reinterpret_cast<const f32x4*>(x + lo + 4 * c);
+  return lo;
+}
+
+__device__ __forceinline__ float cs_x(const float* patch, int lo, int m, int h, int w, int H,
+                                      int W, int k) {
+  const int tap = k / 3, c = k - 3 * tap;
+  const int dr = tap / 3 - 1, dc = tap - 3 * (tap / 3) - 1;
+  const bool ok = k < CS_K && (unsigned)(h + dr) < (unsigned)H && (unsigned)(w + dc) < (unsigned)W;
+  return ok ? patch[(m + dr * W + dc) * 3 + c - lo] : 0.0f;
+}
+
+__global__ __launch_bounds__(EW_BLOCK) void k_cf_stem_fwd(const float* __restrict__ x,
+                                                          const float* __restrict__ w,
+                                                          float* __restrict__ y, int H, int W,
+                                                          int Nc, int M,
+                                                          float* __restrict__ bnpart, int nrows) {
+  __shared__ __attribute__((aligned(16))) float patch[cs_patch_floats<128>()];
+  __shared__ __attribute__((aligned(16))) float wsm[64 * (CS_KP + 4)];
+  __shared__ __attribute__((aligned(16))) float ysm[128 * 68];
+  __shared__ float red[EW_WAVES][2][64];
+  constexpr int WP = CS_KP + 4;  // wsm pitch
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6, li = lane & 15, g = lane >> 4;
+  const int m0 = blockIdx.x * 128, n0 = blockIdx.y * 64;
+  for (int e = t; e < 64 * CS_KP; e += EW_BLOCK) {
+    const int nn = e / CS_KP, k = e - nn * CS_KP;
+    wsm[nn * WP + k] = k < CS_K ? w[(long long)(n0 + nn) * CS_K + k] : 0.0f;
+  }
+  const int lo = cs_patch<128>(x, m0, W, M, patch, t);
+  __syncthreads();
+  const int HW = H * W;
+  float a[2][7];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int m = m0 + 32 * wv + 16 * i + li;
+    const int p = m % HW, h = p / W, ww = p - h * W;
+#pragma unroll
+    for (int s = 0; s < 7; ++s) a[i][s] = cs_x(patch, lo, m, h, ww, H, W, 4 * s + g);
+  }
+  f32x4 acc[2][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int s = 0; s < 7; ++s) {
+      const float b = wsm[(16 * j + li) * WP + 4 * s + g];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][s], b, acc[i][j], 0, 0, 0);
+    }
+  }
+  float sm[4], sq[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    sm[j] = sq[j] = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float v = acc[i][j][q];
+        ysm[(32 * wv + 16 * i + 4 * g + q) * 68 + 16 * j + li] = v;
+        sm[j] += v;
+        sq[j] += v * v;
+      }
+  }
+  if (bnpart) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      sm[j] += __shfl_xor(sm[j], 16, 64);
+      sq[j] += __shfl_xor(sq[j], 16, 64);
+      sm[j] += __shfl_xor(sm[j], 32, 64);
+      sq[j] += __shfl_xor(sq[j], 32, 64);
+    }
+    if (lane < 16) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        red[wv][0][16 * j + lane] = sm[j];
+        red[wv][1][16 * j + lane] = sq[j];
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {  // 128 rows x 16 quads
+    const int e = t + EW_BLOCK * u, r = e >> 4, ch = e & 15;
+    *reinterpret_cast<f32x4*>(y + (long long)(m0 + r) * Nc + n0 + ch * 4) =
+        *reinterpret_cast<const f32x4*>(ysm + r * 68 + ch * 4);
+  }
+  if (bnpart && t < 64) {
+    float s1 = 0.0f, s2 = 0.0f;
+#pragma unroll
+    for (int v = 0; v < EW_WAVES; ++v) {  // fixed order
+      s1 += red[v][0][t];
+      s2 += red[v][1][t];
+    }
+    bnpart[(long long)blockIdx.x * Nc + n0 + t] = s1;
+    bnpart[(long long)(nrows + blockIdx.x) * Nc + n0 + t] = s2;
+  }
+}
+
+// Stem weight gradient dw[n][k] = sum_m dy[m][n] x~[m][k]: block = 256 pixels x 64 channels.
+// dy rows ([256 m][64 n], RC) and the im2col rows ([256 m][28 k], RC) go to LDS; wave v computes
+// n0 + [16 v, 16 v + 16) x k 0..31 (2 tiles) over all 256 m (64 MFMA k-steps), fp32 partial
+// [64][27] per block into the slab, summed by k_cf_stem_reduce.
+__global__ __launch_bounds__(EW_BLOCK) void k_cf_stem_wgrad(const float* __restrict__ dy,
+                                                            const float* __restrict__ x,
+                                                            float* __restrict__ slab, int H,
+                                                            int W, int Nc, int M) {
+  constexpr int DP = 64 + 4, XP = 32 + 4;  // pitches (floats): k and k + 4 16 banks apart
+  __shared__ __attribute__((aligned(16))) float dsm[256 * DP];
+  __shared__ __attribute__((aligned(16))) float xsm[256 * XP];
+  __shared__ __attribute__((aligned(16))) float patch[cs_patch_floats<256>()];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6, li = lane & 15, g = lane >> 4;
+  const int m0 = blockIdx.x * 256, n0 = blockIdx.y * 64, HW = H * W;
+  f32x4 d[16];
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {  // 256 rows x 16 quads
+    const int e = t + EW_BLOCK * u, r = e >> 4, ch = e & 15;
+    d[u] = *reinterpret_cast<const f32x4*>(dy + (long long)(m0 + r) * Nc + n0 + ch * 4);
+  }
+  const int lo = cs_patch<256>(x, m0, W, M, patch, t);
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int e = t + EW_BLOCK * u, r = e >> 4, ch = e & 15;
+    *reinterpret_cast<f32x4*>(dsm + r * DP + ch * 4) = d[u];
+  }
+  __syncthreads();
+  {
+    // im2col row r = t: k 0..31 (k >= 27 zero)
+    const int m = m0 + t, p = m % HW, h = p / W, ww = p - h * W;
+#pragma unroll
+    for (int k4 = 0; k4 < 8; ++k4) {
+      f32x4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = cs_x(patch, lo, m, h, ww, H, W, 4 * k4 + e);
+      *reinterpret_cast<f32x4*>(xsm + t * XP + 4 * k4) = v;
+    }
+  }
+  __syncthreads();
+  f32x4 acc[2];
+  acc[0] = acc[1] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll 8
+  for (int s = 0; s < 64; ++s) {
+    // reduction row of MFMA step s for lane group g: the four groups read rows 4 apart (the +4
+    // pitch pads put them 16 banks apart)
+    const int mr = (s >> 2) * 16 + 4 * g + (s & 3);
+    const float a = dsm[mr * DP + 16 * wv + li];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, xsm[mr * XP + 16 * j + li], acc[j], 0, 0, 0);
+  }
+  float* sp = slab + (long long)blockIdx.x * Nc * CS_K;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int k = 16 * j + li;
+    if (k < CS_K) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) sp[(long long)(n0 + 16 * wv + 4 * g + q) * CS_K + k] = acc[j][q];
+    }
+  }
+}
+
+// dw[o] = sum over the nb block partials slab[b][o] in a fixed order
+__global__ __launch_bounds__(EW_BLOCK) void k_cf_stem_reduce(const float* __restrict__ slab,
+                                                             int nb, int n,
+                                                             float* __restrict__ dw) {
+  __shared__ float red[32][8];
+  const int t = threadIdx.x, o = blockIdx.x * 8 + (t & 7), ck = t >> 3;
+  float s = 0.0f;
+  if (o < n) {
+    const int per = (nb + 31) / 32, b0 = ck * per, b1 = min(b0 + per, nb);
+    int b = b0;
+    for (; b + 3 < b1; b += 4) {
+      const float v0 = slab[(long long)b * n + o], v1 = slab[(long long)(b + 1) * n + o];
+      const float v2 = slab[(long long)(b + 2) * n + o], v3 = slab[(long long)(b + 3) * n + o];
+      s += (v0 + v1) + (v2 + v3);
+    }
+    for (; b < b1; ++b) s += slab[(long long)b * n + o];
+  }
+  red[ck][t & 7] = s;
+  __syncthreads();
+#pragma unroll
+  for (int h = 16; h > 0; h >>= 1) {
+    if (ck < h) red[ck][t & 7] += red[ck + h][t & 7];
+    __syncthreads();
+  }
+  if (ck == 0 && o < n) dw[o] = red[0][t & 7];
+}
+
+// Launch plan: tile shape and split of the reduction, from a small cost model (us): every block
+// k-step costs its MFMA time (bm*bn*32*2 FLOP at 614 GFLOP/s per CU, derated for the narrower
+// tiles' lower operand reuse), each block pays ~3 k-steps of prologue / epilogue, a CU runs
+// ceil(blocks / 256) blocks' worth of work, and a split pays its slab round trip (write + read
+// at ~4 TB/s) plus one reduction launch.
+struct CfPlan {
+  int bm, bn, split, kps;
+};
+CfPlan cf_plan(int M, int Ncol, int ksteps, long long ws_floats, bool allow_split) {
+  // EWDML_CF_PLAN="bm,bn,split": forced plan (measurement only; invalid shapes fall through)
+  static const char* force = getenv("EWDML_CF_PLAN");
+  if (force) {
+    int bm = 0, bn = 0, sp = 0;
+    if (sscanf(force, "%d,%d,%d", &bm, &bn, &sp) == 3 && (bm == 64 || bm == 128) &&
+        (bn == 64 || bn == 128) && sp >= 1 && M % bm == 0 && Ncol % bn == 0 &&
+        (sp == 1 || (long long)sp * M * Ncol <= ws_floats)) {
+      const int kps = (ksteps + sp - 1) / sp;
+      return CfPlan{bm, bn, (ksteps + kps - 1) / kps, kps};
+    }
+  }
+  static const int shapes[4][2] = {{128, 128}, {128, 64}, {64, 128}, {64, 64}};
+  static const double derate[4] = {1.0, 0.9, 0.9, 0.75};
+  CfPlan best{64, 64, 1, ksteps};
+  double best_t = 1e30;
+  for (int sh = 0; sh < 4; ++sh) {
+    const int bm = shapes[sh][0], bn = shapes[sh][1];
+    if (M % bm || Ncol % bn) continue;
+    const long long tiles = (long long)(M / bm) * (Ncol / bn);
+    const double step_us = (double)bm * bn * CF_BK * 2 / 614e3 / derate[sh];
+    for (int split = 1; split <= (allow_split ? 64 : 1); ++split) {
+      const int kps = (ksteps + split - 1) / split;
+      if (split > 1 && (kps < 4 || (long long)split * M * Ncol > ws_floats)) break;
+      const int sp = (ksteps + kps - 1) / kps;
+      const long long blocks = tiles * sp;
+      double t = (double)((blocks + 255) / 256) * step_us * (kps + 3);
+      if (sp > 1) t += 8.0 * sp * M * Ncol / 4e6 + 2.0;
+      if (t < best_t * 0.999) {
+        best_t = t;
+        best = CfPlan{bm, bn, sp, kps};
+      }
+    }
+  }
+  return best;
+}
+
+#define CF_LAUNCH(MODE_, BM_, BN_, WM_, SH_)                                                      \
+  hipLaunchKernelGGL((k_cf_gemm<MODE_, BM_, BN_, WM_, SH_>), grid, dim3(CF_NT), 0, s, a, b, out,  \
+                     slab, geo, bnp, bbv, addend)
+
+template <int MODE>
+int cf_gemm(const float* a, const float* b, float* out, float* ws, long long ws_floats,
+            CfGeom geo, hipStream_t s, float* bnpart, long long bnpart_floats,
+            const CfBnBwd* bnb, const float* addend) {
+  ws_floats -= 64;  // the workspace's last 64 floats are conv.hip's zero page (never a slab)
+  const CfPlan p = cf_plan(geo.M, geo.Ncol, geo.ksteps, ws_floats, true);
+  geo.kps = p.kps;
+  dim3 grid(geo.M / p.bm, geo.Ncol / p.bn, p.split);
+  float* slab = p.split > 1 ? ws : nullptr;
+  const long long prow = geo.M / p.bm;
+  float* bnp = (bnpart && !slab && prow <= 1024 && 2 * prow * geo.Ncol <= bnpart_floats) ? bnpart
+                                                                                      : nullptr;
+  const CfBnBwd none{nullptr, nullptr, nullptr, nullptr, 0, 0, 0};
+  const CfBnBwd bbv = (bnp && bnb) ? *bnb : none;
+  // wave grids: 128x128 -> 2x4 waves of 64x32; 128x64 -> 4x2 of 32x32; 64x128 -> 2x4 of 32x32;
+  // 64x64 -> 4x2 of 16x32
+  if (p.bm == 128 && p.bn == 128) CF_LAUNCH(MODE, 128, 128, 2, 32);
+  else if (p.bm == 128) CF_LAUNCH(MODE, 128, 64, 4, 32);
+  else if (p.bn == 128) CF_LAUNCH(MODE, 64, 128, 2, 32);
+  else CF_LAUNCH(MODE, 64, 64, 4, 16);
+  EW_CHECK_LAUNCH();
+  if (p.split > 1) {
+    const int M = geo.M, Nc = geo.Ncol;
+    const long long n = (long long)M * Nc;
+    const int tpr = Nc / 4, rpi = tpr <= EW_BLOCK ? EW_BLOCK / tpr : 0;
+    int rpb = rpi, nblk = 0;
+    if (bnpart && rpi > 0 && EW_BLOCK % tpr == 0) {
+      while ((M + rpb - 1) / rpb > 1024) rpb += rpi;
+      nblk = (M + rpb - 1) / rpb;
+      if (2LL * nblk * Nc > bnpart_floats) nblk = 0;
+    }
+    if (nblk > 0) {
+      const CfBnBwd bbr = bnb ? *bnb : none;
+      hipLaunchKernelGGL(k_cf_slab_reduce_bn, dim3(nblk), dim3(EW_BLOCK), 0, s, ws, p.split, M,
+                         Nc, out, bnpart, rpb, bbr, addend);
+      EW_CHECK_LAUNCH();
+      return nblk;
+    }
+    long long gr = (n / 4 + EW_BLOCK - 1) / EW_BLOCK;
+    if (gr > 2048) gr = 2048;
+    hipLaunchKernelGGL(k_cf_slab_reduce, dim3((int)gr), dim3(EW_BLOCK), 0, s, ws, p.split, n, out,
+                       addend);
+    EW_CHECK_LAUNCH();
+  }
+  return bnp ? (int)prow : 0;
+}
+#undef CF_LAUNCH
+
+int cf_taps(int ksize) {
+  if (ksize != 1 && ksize != 3) throw std::runtime_error("ewdml conv: kernel size must be 1 or 3");
+  return ksize * ksize;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------------
+// host side (shapes validated here: the kernels assume them)
+
+int ew_conv_f32_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t ws, long long ws_floats,
+                    long long N, int H, int W, int C, int Nc, int ksize, uintptr_t bnpart,
+                    long long bnpart_floats, uintptr_t stream) {
+  const long long P = N * H * W;
+  if (C % CF_BK || Nc % 64 || P % 64 || P * (long long)std::max(C, Nc) >= (1LL << 31))
+    throw std::runtime_error("ewdml conv f32: needs C % 32 == 0, Nc % 64 == 0, N*H*W % 64 == 0");
+  const int taps = cf_taps(ksize);
+  CfGeom g{(int)P, Nc, (int)P, H, W, C, Nc, taps, taps * C / CF_BK, 0};
+  return cf_gemm<CF_FWD>(reinterpret_cast<const float*>(x), reinterpret_cast<const float*>(w),
+                         reinterpret_cast<float*>(y), reinterpret_cast<float*>(ws), ws_floats, g,
+                         (hipStream_t)stream, reinterpret_cast<float*>(bnpart), bnpart_floats,
+                         nullptr, nullptr);
+}
+
+int ew_conv_f32_bwd_data(uintptr_t dy, uintptr_t w, uintptr_t dx, uintptr_t ws,
+                         long long ws_floats, long long N, int H, int W, int C, int Nc, int ksize,
+                         uintptr_t bn_h, uintptr_t bn_res, uintptr_t bn_code, uintptr_t bn_stats,
+                         int bn_relu, uintptr_t bnpart, long long bnpart_floats, uintptr_t addend,
+                         uintptr_t stream) {
+  const long long P = N * H * W;
+  if (C % 64 || Nc % CF_BK || P % 64 || P * (long long)std::max(C, Nc) >= (1LL << 31))
+    throw std::runtime_error("ewdml conv f32: bwd-data needs C % 64 == 0, Nc % 32 == 0");
+  const int taps = cf_taps(ksize);
+  CfGeom g{(int)P, C, (int)P, H, W, C, Nc, taps, taps * Nc / CF_BK, 0};
+  const CfBnBwd bb{reinterpret_cast<const float*>(bn_h), reinterpret_cast<const float*>(bn_res),
+                   reinterpret_cast<const uint8_t*>(bn_code),
+                   reinterpret_cast<const float*>(bn_stats), bn_relu, H, W};
+  return cf_gemm<CF_BWD>(reinterpret_cast<const float*>(dy), reinterpret_cast<const float*>(w),
+                         reinterpret_cast<float*>(dx), reinterpret_cast<float*>(ws), ws_floats, g,
+                         (hipStream_t)stream, bn_h ? reinterpret_cast<float*>(bnpart) : nullptr,
+                         bnpart_floats, bn_h ? &bb : nullptr,
+                         reinterpret_cast<const float*>(addend));
+}
+
+void ew_conv_f32_wgrad(uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws, long long ws_floats,
+                       long long N, int H, int W, int C, int Nc, int ksize, uintptr_t stream) {
+  const long long P = N * H * W;
+  const int taps = cf_taps(ksize);
+  if (C % 64 || Nc % 64 || P % CF_BK || P * (long long)std::max(C, Nc) >= (1LL << 31))
+    throw std::runtime_error("ewdml conv f32: wgrad needs C, Nc % 64 == 0, N*H*W % 32 == 0");
+  CfGeom g{Nc, taps * C, (int)P, H, W, C, Nc, taps, (int)(P / CF_BK), 0};
+  cf_gemm<CF_WGRAD>(reinterpret_cast<const float*>(dy), reinterpret_cast<const float*>(x),
+                    reinterpret_cast<float*>(dw), reinterpret_cast<float*>(ws), ws_floats, g,
+                    (hipStream_t)stream, nullptr, 0, nullptr, nullptr);
+}
+
+int ew_conv_f32_stem_fwd(uintptr_t x, uintptr_t w, uintptr_t y, long long N, int H, int W, int Nc,
+                         uintptr_t bnpart, long long bnpart_floats, uintptr_t stream) {
+  const long long M = N * H * W;
+  if (M % 128 || Nc % 64 || M >= (1LL << 31) / 64 || W > CS_WMAX)
+    throw std::runtime_error("ewdml conv f32 stem: needs N*H*W % 128 == 0, Nc % 64 == 0, W <= 256");
+  const int nrows = (int)(M / 128);
+  float* bnp = (bnpart && nrows <= 1024 && 2LL * nrows * Nc <= bnpart_floats)
+                   ? reinterpret_cast<float*>(bnpart) : nullptr;
+  hipLaunchKernelGGL(k_cf_stem_fwd, dim3(nrows, Nc / 64), dim3(EW_BLOCK), 0, (hipStream_t)stream,
+                     reinterpret_cast<const float*>(x), reinterpret_cast<const float*>(w),
+                     reinterpret_cast<float*>(y), H, W, Nc, (int)M, bnp, nrows);
+  EW_CHECK_LAUNCH();
+  return bnp ? nrows : 0;
+}
+
+void ew_conv_f32_stem_wgrad(uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws,
+                            long long ws_floats, long long N, int H, int W, int Nc,
+                            uintptr_t stream) {
+  const long long M = N * H * W;
+  const long long nb = M / 256, n = (long long)Nc * CS_K;
+  if (M % 256 || Nc % 64 || nb * n > ws_floats - 64 || W > CS_WMAX || M >= (1LL << 31) / 64)
+    throw std::runtime_error("ewdml conv f32 stem: wgrad needs N*H*W % 256 == 0, Nc % 64 == 0, "
+                             "W <= 256");
+  hipStream_t s = (hipStream_t)stream;
+  float* slab = reinterpret_cast<float*>(ws);
+  hipLaunchKernelGGL(k_cf_stem_wgrad, dim3((int)nb, Nc / 64), dim3(EW_BLOCK), 0, s,
+                     reinterpret_cast<const float*>(dy), reinterpret_cast<const float*>(x), slab,
+                     H, W, Nc, (int)M);
+  EW_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_cf_stem_reduce, dim3((int)((n + 7) / 8)), dim3(EW_BLOCK), 0, s, slab,
+                     (int)nb, (int)n, reinterpret_cast<float*>(dw));
+  EW_CHECK_LAUNCH();
+}

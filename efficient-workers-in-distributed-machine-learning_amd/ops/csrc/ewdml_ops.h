@@ -180,6 +180,24 @@ int ew_conv_stem_fwd(uintptr_t x, uintptr_t w, uintptr_t y, long long N, int H, 
 void ew_conv_stem_wgrad(uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws,
                         long long ws_floats, long long N, int H, int W, int Nc, uintptr_t stream);
 
+// ---- the same convolutions in fp32 (conv_f32.hip, v_mfma_f32_16x16x4_f32): fp32 tensors and
+// BN operands, same argument meaning as the bf16 entry points above
+int ew_conv_f32_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t ws, long long ws_floats,
+                    long long N, int H, int W, int C, int Nc, int ksize, uintptr_t bnpart,
+                    long long bnpart_floats, uintptr_t stream);
+int ew_conv_f32_bwd_data(uintptr_t dy, uintptr_t w, uintptr_t dx, uintptr_t ws,
+                         long long ws_floats, long long N, int H, int W, int C, int Nc, int ksize,
+                         uintptr_t bn_h, uintptr_t bn_res, uintptr_t bn_code, uintptr_t bn_stats,
+                         int bn_relu, uintptr_t bnpart, long long bnpart_floats, uintptr_t addend,
+                         uintptr_t stream);
+void ew_conv_f32_wgrad(uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws, long long ws_floats,
+                       long long N, int H, int W, int C, int Nc, int ksize, uintptr_t stream);
+int ew_conv_f32_stem_fwd(uintptr_t x, uintptr_t w, uintptr_t y, long long N, int H, int W, int Nc,
+                         uintptr_t bnpart, long long bnpart_floats, uintptr_t stream);
+void ew_conv_f32_stem_wgrad(uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws,
+                            long long ws_floats, long long N, int H, int W, int Nc,
+                            uintptr_t stream);
+
 // ---- cross-entropy loss (nn.hip): mean over B rows of [B, K] logits (bf16 or fp32), int64 labels
 void ew_cross_entropy_fwd(uintptr_t x, uintptr_t y, int B, int K, int is_bf16, uintptr_t loss,
                           uintptr_t lse, uintptr_t stream);

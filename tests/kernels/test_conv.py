@@ -294,6 +294,7 @@ def test_resnet_residual_grad_sink_and_bn_sums_match_autograd_sum(net):
         conv.set_bn_bwd_fusion(fused)
         m = copy.deepcopy(m0)
         xx = x
+        conv.set_enabled(run != "fp32")  # fp32 reference: MIOpen, not the fp32 MFMA kernels
         if run != "fp32":
             for p in m.parameters():
                 p.data = p.data.to(torch.bfloat16).contiguous(
@@ -306,6 +307,7 @@ def test_resnet_residual_grad_sink_and_bn_sums_match_autograd_sum(net):
         finally:
             resnet.set_residual_sink(True)
             conv.set_bn_bwd_fusion(True)
+            conv.set_enabled(True)
         if fused:
             assert fnn.PRE_BWD_USED > used
         res.append((out.float(), [p.grad.float() for p in m.parameters()]))

@@ -1,0 +1,254 @@
+"""fp32 MFMA implicit-GEMM convolutions (ops/csrc/conv_f32.hip, v_mfma_f32_16x16x4_f32) against a
+float64 PyTorch reference on the CPU.
+
+The kernels multiply and accumulate in fp32 with no reduced-precision operand step, so the
+relative error is a few fp32 ulps times the reduction length's growth: the bound used is 1e-5
+(bf16 would be ~4e-3, xf32/tf32 ~5e-4).  Shapes cover every tiling path: 128x128, 128x64, 64x128
+and 64x64 tiles, split-K slab reductions, H != W, odd widths, 1x1 and the 3-channel stem.
+"""
+import copy
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-5
+
+
+def _conv():
+    from ewdml import ops
+    from ewdml.ops import conv
+
+    ops.require()
+    conv.set_enabled(True)
+    return conv
+
+
+def _rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return float((a - b).norm() / (b.norm() + 1e-30))
+
+
+def _data(N, C, Nc, H, W, seed=0, k=3):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    x = torch.randn(N, C, H, W, device="cuda", generator=g)
+    w = torch.randn(Nc, C, k, k, device="cuda", generator=g) / (k * C ** 0.5)
+    return (x.contiguous(memory_format=torch.channels_last),
+            w.contiguous(memory_format=torch.channels_last))
+
+
+def _ref64(x, w, k, dy=None):
+    """float64 CPU forward (and grads for dy)."""
+    xr = x.detach().double().cpu().requires_grad_(dy is not None)
+    wr = w.detach().double().cpu().requires_grad_(dy is not None)
+    y = F.conv2d(xr, wr, padding=k // 2)
+    if dy is not None:
+        y.backward(dy.detach().double().cpu())
+        return y.detach(), xr.grad, wr.grad
+    return y.detach()
+
+
+SHAPES = [
+    (128, 64, 128, 16, 16, 3),   # VGG conv2: 128x128 tiles, no split
+    (128, 128, 256, 8, 8, 3),    # VGG conv3: 128x128, split 2
+    (64, 256, 512, 4, 4, 3),     # 128x128 split-K
+    (128, 512, 512, 2, 2, 3),    # VGG conv7: 64x64 split-K
+    (2, 64, 128, 8, 16, 3),      # H != W, small
+    (4, 192, 128, 4, 8, 3),      # C not a power of two
+    (8, 128, 64, 8, 8, 3),       # C_out = 64
+    (8, 64, 128, 8, 5, 3),       # odd width
+    (16, 64, 256, 32, 32, 1),    # 1x1 expand
+    (16, 256, 64, 32, 32, 1),    # 1x1 reduce
+    (32, 512, 2048, 4, 4, 1),    # 1x1, small M
+]
+
+
+@pytest.mark.parametrize("N,C,Nc,H,W,k", SHAPES)
+def test_conv_f32_forward(N, C, Nc, H, W, k):
+    conv = _conv()
+    x, w = _data(N, C, Nc, H, W, k=k)
+    assert conv.supported(x, w)
+    y = conv.conv(x, w)
+    assert y.grad_fn is None or "Conv" in type(y.grad_fn).__name__
+    assert y.dtype == torch.float32 and y.is_contiguous(memory_format=torch.channels_last)
+    ref = _ref64(x, w, k)
+    assert _rel(y, ref) < TOL, _rel(y, ref)
+
+
+@pytest.mark.parametrize("N,C,Nc,H,W,k", SHAPES)
+def test_conv_f32_backward(N, C, Nc, H, W, k):
+    conv = _conv()
+    x, w = _data(N, C, Nc, H, W, seed=1, k=k)
+    g = torch.Generator(device="cuda").manual_seed(7)
+    dy = torch.randn(N, Nc, H, W, device="cuda", generator=g).contiguous(
+        memory_format=torch.channels_last)
+    xa, wa = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
+    y = conv.conv(xa, wa)
+    assert "Conv" in type(y.grad_fn).__name__  # the HIP autograd function, not MIOpen
+    y.backward(dy)
+    _, gx, gw = _ref64(x, w, k, dy)
+    assert xa.grad.dtype == torch.float32 and wa.grad.dtype == torch.float32
+    assert _rel(xa.grad, gx) < TOL, _rel(xa.grad, gx)
+    assert _rel(wa.grad, gw) < TOL, _rel(wa.grad, gw)
+
+
+def test_conv_f32_deterministic():
+    conv = _conv()
+    x, w = _data(128, 512, 512, 2, 2, seed=3)
+    xa, wa = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
+    a = conv.conv(xa, wa)
+    b = conv.conv(x, w)
+    assert torch.equal(a, b)  # split-K slabs are summed in a fixed order
+    dy = torch.randn_like(a)
+    a.backward(dy)
+    g1 = (xa.grad.clone(), wa.grad.clone())
+    xa.grad = wa.grad = None
+    conv.conv(xa, wa).backward(dy)
+    assert torch.equal(g1[0], xa.grad) and torch.equal(g1[1], wa.grad)
+
+
+@pytest.mark.parametrize("N,Nc,H,W", [(128, 64, 32, 32), (8, 128, 16, 16), (4, 64, 8, 8),
+                                      (2, 64, 16, 24)])
+def test_conv_f32_stem(N, Nc, H, W):
+    conv = _conv()
+    x, w = _data(N, 3, Nc, H, W, seed=11)
+    assert conv.stem_supported(x, w)
+    g = torch.Generator(device="cuda").manual_seed(12)
+    dy = torch.randn(N, Nc, H, W, device="cuda", generator=g).contiguous(
+        memory_format=torch.channels_last)
+    wa = w.clone().requires_grad_(True)
+    y = conv.conv(x, wa)
+    assert "Stem" in type(y.grad_fn).__name__
+    y.backward(dy)
+    ref, _, gw = _ref64(x, w, 3, dy)
+    assert y.dtype == torch.float32
+    assert _rel(y, ref) < TOL, _rel(y, ref)
+    assert _rel(wa.grad, gw) < TOL, _rel(wa.grad, gw)
+    wb = w.clone().requires_grad_(True)
+    conv.conv(x, wb).backward(dy)
+    assert torch.equal(wb.grad, wa.grad)
+
+
+@pytest.mark.parametrize("N,C,Nc,H,W,k", [(128, 64, 128, 16, 16, 3), (16, 128, 256, 8, 8, 3),
+                                          (128, 512, 512, 2, 2, 3), (16, 64, 256, 32, 32, 1),
+                                          (128, 3, 64, 32, 32, 3)])
+def test_conv_f32_epilogue_bn_statistics(N, C, Nc, H, W, k):
+    """BatchNorm partial sums from the fp32 epilogue / slab reduction give the BN kernels' own
+    statistics."""
+    from ewdml.ops import nn as fnn
+
+    conv = _conv()
+    x, w = _data(N, C, Nc, H, W, seed=5, k=k)
+    bn0 = torch.nn.BatchNorm2d(Nc).cuda()
+    bn1 = copy.deepcopy(bn0)
+    h = conv.conv(x, w.clone().requires_grad_(True))
+    assert hasattr(h, "_ew_bn_part")
+    y0 = fnn.bn_act(h, bn0, "relu")
+    y1 = fnn.bn_act(h.detach().clone(), bn1, "relu")
+    assert _rel(y0, y1) < 1e-5
+    assert torch.allclose(bn0.running_mean, bn1.running_mean, rtol=1e-5, atol=1e-7)
+    assert torch.allclose(bn0.running_var, bn1.running_var, rtol=1e-5, atol=1e-7)
+
+
+@pytest.mark.parametrize("mode,pool", [("relu", True), ("relu", False), ("none", False)])
+@pytest.mark.parametrize("N,HW", [(64, 16), (32, 4)])
+def test_conv_f32_bn_backward_sums_in_bwd_data_epilogue(mode, pool, N, HW):
+    from ewdml.ops import nn as fnn
+
+    conv = _conv()
+    x0, w0 = _data(N, 64, 128, HW, HW, seed=21)
+    _, w1 = _data(8, 128, 64, 8, 8, seed=22)
+    bn0 = torch.nn.BatchNorm2d(128).cuda()
+    with torch.no_grad():
+        bn0.weight.uniform_(0.5, 1.5)
+        bn0.bias.uniform_(-0.3, 0.3)
+    g = None
+    grads = []
+    for fused in (True, False):
+        conv.set_bn_bwd_fusion(fused)
+        used = fnn.PRE_BWD_USED
+        bn = copy.deepcopy(bn0)
+        xa, wa, wb = (t.clone().requires_grad_(True) for t in (x0, w0, w1))
+        h = conv.conv(xa, wa)
+        y = fnn.bn_act(h, bn, mode, pool=pool)
+        z = conv.conv(y, wb)
+        if g is None:
+            g = torch.randn(z.shape, device="cuda").contiguous(memory_format=torch.channels_last)
+        z.backward(g)
+        assert (fnn.PRE_BWD_USED > used) == fused
+        grads.append([xa.grad, wa.grad, wb.grad, bn.weight.grad, bn.bias.grad])
+    conv.set_bn_bwd_fusion(True)
+    for a, b in zip(*grads):
+        assert _rel(a, b) < 1e-5, _rel(a, b)
+
+
+def test_fp32_vgg11_step_vs_fp64():
+    """One fp32 VGG-11-BN training step (fused NHWC path, fp32 MFMA convs) against the same step
+    in float64 on the CPU, and no worse than the step through MIOpen's fp32 convolutions."""
+    from ewdml.models import build_model
+
+    conv = _conv()
+    torch.manual_seed(0)
+    m0 = build_model("vgg11", 10).to(memory_format=torch.channels_last)
+    for mod in m0.modules():
+        if isinstance(mod, torch.nn.Dropout):
+            mod.p = 0.0
+    x = torch.randn(32, 3, 32, 32).contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (32,))
+    m64 = copy.deepcopy(m0).double()
+    out64 = m64(x.double())
+    F.cross_entropy(out64, y).backward()
+    g64 = [p.grad for p in m64.parameters()]
+    res = []
+    for on in (True, False):
+        m = copy.deepcopy(m0).cuda()
+        conv.set_enabled(on)
+        try:
+            out = m(x.cuda())
+            F.cross_entropy(out, y.cuda()).backward()
+        finally:
+            conv.set_enabled(True)
+        big = [(p.grad, r) for p, r in zip(m.parameters(), g64) if float(r.norm()) > 1e-6]
+        res.append((_rel(out, out64), max(_rel(a, b) for a, b in big)))
+    (o_h, e_h), (o_m, e_m) = res
+    assert o_h < 1e-5 and e_h < 1e-4, (o_h, e_h)
+    assert o_h <= 2 * o_m + 1e-6 and e_h <= 2 * e_m + 1e-5, (o_h, o_m, e_h, e_m)
+
+
+def test_fp32_resnet18_step_convs_in_situ():
+    """Every MFMA conv backward of one fp32 ResNet-18 step (BN-backward sums and residual sinks
+    on) against float64 on the tensors it actually received.  (The whole-network gradient is not
+    a usable oracle here: the BN bias gradients are sums with ~1e4x cancellation, so any two fp32
+    runs -- MIOpen against itself included -- differ by up to ~1e-3 after a few blocks.)"""
+    from ewdml.models import build_model
+    from ewdml.ops import conv as cmod
+
+    _conv()
+    recs = []
+    orig = cmod._Conv.backward
+
+    def bwd(ctx, dy):
+        x, w = ctx.saved_tensors
+        had_sink = ctx.sink is not None and getattr(ctx.sink, "grad", None) is not None
+        dx, dw, a, b = orig(ctx, dy)
+        recs.append((x.detach().clone(), w.detach().clone(), dy.detach().clone(),
+                     None if (dx is None or had_sink) else dx.detach().clone(), dw.detach().clone()))
+        return dx, dw, a, b
+
+    cmod._Conv.backward = staticmethod(bwd)
+    try:
+        torch.manual_seed(0)
+        m = build_model("resnet18", 10).to(memory_format=torch.channels_last).cuda()
+        x = torch.randn(32, 3, 32, 32, device="cuda").contiguous(memory_format=torch.channels_last)
+        y = torch.randint(0, 10, (32,), device="cuda")
+        F.cross_entropy(m(x), y).backward()
+    finally:
+        cmod._Conv.backward = orig
+    assert len(recs) >= 12
+    for x, w, dy, dx, dw in recs:
+        _, gx, gw = _ref64(x, w, w.shape[-1], dy)
+        assert _rel(dw, gw) < TOL, (tuple(x.shape), _rel(dw, gw))
+        if dx is not None:
+            assert _rel(dx, gx) < TOL, (tuple(x.shape), _rel(dx, gx))
