@@ -1,5 +1,6 @@
 """Flagship benchmark: VGG-11(-BN) on CIFAR-10-shaped synthetic data, top-1 % + 8-bit QSGD
-gradient exchange over RCCL, one process per MI355X.
+gradient exchange with error feedback over RCCL, one process per MI355X, fp32 (the reference's
+precision).
 
     python bench.py --gpus 1 --steps 50 --warmup 10
     python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
@@ -8,10 +9,15 @@ gradient exchange over RCCL, one process per MI355X.
 Metric (BASELINE.json): "grad bytes/step on wire + images/sec, VGG-11 CIFAR-10 at 1/2/4/8
 MI355X".  ``value`` = whole-job images/sec (sum over ranks: N x per-GPU batch x K / max-over-ranks
 time of the K timed steps).  Every timed step is a full training step: on-device batch gather +
-augmentation, bf16-autocast forward/backward (fp32 master weights), per-bucket top-k + QSGD encode
-(HIP) overlapped with backward, RCCL all-gather of the packed payloads, fused decode + average +
+augmentation, fp32 forward/backward on the hand-written fp32 MFMA kernels (the reference trains in
+fp32: ``src/distributed_worker.py:249-251``, ``src/optim/sgd.py:59-91``), per-bucket top-k + QSGD
+encode with error feedback (HIP), RCCL all-gather of the packed payloads, fused decode + average +
 SGD (HIP).  Weak scaling: the per-GPU batch is fixed as N grows.  The byte fields report the
 payload per rank, the algorithmic wire bytes, and the reference-equivalent MiB/step.
+
+Extra measured fields (same K / W, after the headline run): ``value_fp32_no_ef`` (the same step
+without error feedback: its cost) and ``value_bf16`` / ``ms_per_step_bf16`` (bf16 autocast with bf16
+weight copies, error feedback on).  ``--no-extras`` skips them.
 """
 import argparse
 import json
@@ -54,14 +60,16 @@ def parse(argv=None):
     p.add_argument("--qsgd-bits", type=int, default=None)
     p.add_argument("--qsgd-levels", type=int, default=None)
     p.add_argument("--bucket-mb", type=float, default=64.0)
-    p.add_argument("--amp", default="bf16")
+    p.add_argument("--amp", default="none", help="none = fp32 (reference precision), bf16")
     p.add_argument("--channels-last", action="store_true")
     p.add_argument("--layout", default="auto", choices=["auto", "nchw", "nhwc"])
     p.add_argument("--fused-nn", default="on", choices=["on", "off"])
     p.add_argument("--no-overlap", action="store_true")
-    p.add_argument("--error-feedback", action="store_true")
+    p.add_argument("--error-feedback", default="on", choices=["on", "off"])
+    p.add_argument("--no-extras", action="store_true", help="headline run only")
     p.add_argument("--hip-graph", default="full", choices=["off", "split", "full"])
     p.add_argument("--param-dtype", default="auto", choices=["auto", "fp32"])
+    p.add_argument("--json-out", default=None, help="also write the JSON line to this file")
     p.add_argument("--extra", default="", help="extra distributed_nn.py flags")
     a = p.parse_args(argv)
     pre = {"batch_size": 128, **PRESETS[a.preset]}
@@ -71,23 +79,12 @@ def parse(argv=None):
     return a
 
 
-def main(argv=None):
-    a = parse(argv)
-    import torch
-    import torch.distributed as dist
-
-    import ewdml
-    from ewdml.runtime.trainer import Trainer
-    from ewdml.utils.metrics import byte_summary
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world != a.gpus:
-        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}; launch with torch.distributed.run")
+def _flags(a, world, amp, ef):
     levels = a.qsgd_levels or (127 if a.qsgd_bits == 8 else 7)
     flags = ["--network", a.network, "--dataset", a.dataset, "--batch-size", str(a.batch_size),
              "--compress", a.compress, "--topk-ratio", str(a.topk_ratio), "--qsgd-bits",
              str(a.qsgd_bits), "--qsgd-levels", str(levels), "--momentum", "0.9", "--lr", "0.01",
-             "--bucket-mb", str(a.bucket_mb), "--amp", a.amp, "--synthetic-size",
+             "--bucket-mb", str(a.bucket_mb), "--amp", amp, "--synthetic-size",
              str(max(16384, 4 * a.batch_size * world)),
              "--eval-freq", "0", "--log-interval", "1000000", "--quiet",
              "--max-steps", str(a.steps + a.warmup)]
@@ -96,19 +93,29 @@ def main(argv=None):
     flags += ["--layout", a.layout, "--fused-nn", a.fused_nn]
     if a.no_overlap:
         flags.append("--no-overlap")
-    if a.error_feedback:
+    if ef:
         flags.append("--error-feedback")
     # graph capture happens inside the untimed warmup: eager steps, then the capturing step
     gw = max(1, min(3, a.warmup - 1))
     flags += ["--hip-graph", a.hip_graph, "--graph-warmup", str(gw), "--param-dtype",
-              a.param_dtype]
-    flags += a.extra.split()
-    cfg = ewdml.parse_args(flags, prog="bench.py")
-    tr = Trainer(cfg)
-    cuda = tr.cuda
+              a.param_dtype if amp != "none" else "fp32"]
+    return flags + a.extra.split(), gw
+
+
+def measure(a, world, amp, ef):
+    """Build a Trainer for this configuration, run W untimed warmup steps, then time exactly K
+    steps bracketed by barrier + synchronize on both sides; returns (max-over-ranks seconds,
+    trainer, final loss, host enqueue seconds)."""
+    import torch
+
+    import ewdml
+    from ewdml.runtime.trainer import Trainer
+
+    flags, gw = _flags(a, world, amp, ef)
+    tr = Trainer(ewdml.parse_args(flags, prog="bench.py"))
 
     def sync():
-        if cuda:
+        if tr.cuda:
             torch.cuda.synchronize()
 
     warm = a.warmup if a.hip_graph == "off" else max(a.warmup, gw + 1)
@@ -128,15 +135,32 @@ def main(argv=None):
     t1 = time.perf_counter()
     tr.comm.barrier()
     sync()
-    elapsed = t1 - t0
-    elapsed_max = tr.comm.all_reduce_scalars([elapsed], op="max")[0]
+    elapsed_max = tr.comm.all_reduce_scalars([t1 - t0], op="max")[0]
     final_loss = float(loss.detach()) if loss is not None else float("nan")
+    return elapsed_max, tr, final_loss, t_enq - t0
+
+
+def main(argv=None):
+    a = parse(argv)
+    import torch
+    import torch.distributed as dist
+
+    import ewdml
+    from ewdml.utils.metrics import byte_summary
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}; launch with torch.distributed.run")
+    ef = a.error_feedback == "on"
+    elapsed_max, tr, final_loss, enq = measure(a, world, a.amp, ef)
+    cuda = tr.cuda
     ms = elapsed_max * 1e3 / a.steps
     img_s = world * a.batch_size * a.steps / elapsed_max
     bytes_ = byte_summary(tr.exchange.last, world)
     metric = "grad bytes/step on wire + images/sec, VGG-11 CIFAR-10 at 1/2/4/8 MI355X"
     if a.preset != "vgg11":
         metric = f"grad bytes/step on wire + images/sec, {a.network} {a.dataset}"
+    nb = len(tr.flat.buckets)
     rec = {
         "metric": metric,
         "value": round(img_s, 2),
@@ -157,12 +181,15 @@ def main(argv=None):
                    a.network, "global_batch": world * a.batch_size, "per_gpu_batch": a.batch_size,
                    "seq_len": None, "parallelism": f"dp{world}",
                    "codec": tr.exchange.codec.describe() if hasattr(tr.exchange, "codec") else
-                   a.compress, "optimizer": "sgd(momentum=0.9)", "overlap": not a.no_overlap,
-                   "buckets": len(tr.flat.buckets), "hip_graph": tr.graph_mode,
+                   a.compress, "error_feedback": ef, "optimizer": "sgd(momentum=0.9)",
+                   "overlap": not a.no_overlap, "buckets": nb, "hip_graph": tr.graph_mode,
                    "bf16_params": tr.flat.shadow is not None,
                    "grad_mode": "views" if tr.flat.attach_grads else "pointers",
                    "layout": "nhwc" if tr.channels_last else "nchw",
                    "fused_nn": a.fused_nn},
+        # overlap that actually happens: more than one bucket (the first collective is issued
+        # while backward still runs) and a collective to hide (world > 1)
+        "overlap_effective": bool(nb > 1 and not a.no_overlap and world > 1),
         "grad_bytes_per_step_on_wire": bytes_["wire_bytes_total"],
         "payload_bytes_per_rank": bytes_["payload_bytes_per_rank"],
         "dense_fp32_grad_bytes": bytes_["dense_fp32_bytes"],
@@ -170,11 +197,34 @@ def main(argv=None):
         "ref_equiv_MiB_per_step": round(bytes_["ref_equiv_MiB_per_step"], 4),
         "ref_equiv_reduction": bytes_["ref_equiv_reduction"],
         "final_loss": final_loss,
-        "host_enqueue_ms_per_step": round((t_enq - t0) * 1e3 / a.steps, 4),
+        "host_enqueue_ms_per_step": round(enq * 1e3 / a.steps, 4),
         "hip_ext": ewdml.ops.library_path() if cuda else None,
     }
-    if tr.rank == 0:
-        print(json.dumps(rec), flush=True)
+    del tr
+    if not a.no_extras:
+        extras = []
+        if ef:
+            extras.append(("fp32_no_ef" if a.amp == "none" else f"{a.amp}_no_ef", a.amp, False))
+        if a.amp == "none":
+            extras.append(("bf16", "bf16", ef))
+        for key, amp, e in extras:
+            if cuda:
+                torch.cuda.empty_cache()
+            el, tr2, fl, _ = measure(a, world, amp, e)
+            rec[f"value_{key}"] = round(world * a.batch_size * a.steps / el, 2)
+            rec[f"ms_per_step_{key}"] = round(el * 1e3 / a.steps, 4)
+            rec[f"final_loss_{key}"] = fl
+            del tr2
+    if dist.is_initialized():
+        rank = dist.get_rank()
+    else:
+        rank = 0
+    if rank == 0:
+        line = json.dumps(rec)
+        print(line, flush=True)
+        if a.json_out:
+            with open(a.json_out, "w") as f:
+                f.write(line + "\n")
     if dist.is_initialized():
         dist.destroy_process_group()
     return rec

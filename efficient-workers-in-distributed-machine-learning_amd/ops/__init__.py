@@ -270,8 +270,13 @@ def sgd_flat(param, mom, grad, lr, momentum=0.0, dampening=0.0, weight_decay=0.0
 
 
 def adam_flat(param, exp_avg, exp_avg_sq, max_exp_avg_sq, grad, lr_step, beta1, beta2, eps,
-              weight_decay=0.0, grad_scale=1.0, amsgrad=False, shadow=None):
+              weight_decay=0.0, grad_scale=1.0, amsgrad=False, shadow=None, step=None, lr=0.0):
+    """Adam/AMSGrad over flat fp32 buffers.  ``step`` (int32 device tensor, optional): the kernel
+    reads t = step + 1 and derives ``lr_step = lr * sqrt(1 - beta2^t) / (1 - beta1^t)`` on the
+    device, so a captured graph follows the step count (``lr_step`` is then ignored)."""
     C = require()
+    if step is not None:
+        _check(step, torch.int32, "step", align=4)
     for t, nm in ((param, "param"), (exp_avg, "exp_avg"), (exp_avg_sq, "exp_avg_sq")):
         _check(t, torch.float32, nm)
     if amsgrad:
@@ -286,7 +291,7 @@ def adam_flat(param, exp_avg, exp_avg_sq, max_exp_avg_sq, grad, lr_step, beta1, 
             raise ValueError("shadow must match param")
     C.adam_flat(_ptr(param), _ptr(exp_avg), _ptr(exp_avg_sq), _ptr(max_exp_avg_sq), _ptr(grad),
                 _ptr(shadow), n, _GDT[grad.dtype], lr_step, beta1, beta2, eps, weight_decay,
-                grad_scale, int(amsgrad), _stream())
+                grad_scale, int(amsgrad), _stream(), _ptr(step), float(lr))
 
 
 _DDT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}

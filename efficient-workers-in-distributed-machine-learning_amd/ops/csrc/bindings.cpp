@@ -188,8 +188,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("adam_flat",
         [](uintptr_t param, uintptr_t m1, uintptr_t m2, uintptr_t vmax, uintptr_t grad,
            uintptr_t shadow, long long n, int grad_dtype, float lr_step, float beta1, float beta2,
-           float eps, float weight_decay, float grad_scale, int amsgrad, uintptr_t stream) {
+           float eps, float weight_decay, float grad_scale, int amsgrad, uintptr_t stream,
+           uintptr_t step, double lr) {
           AdamFlatArgs a{};
+          a.step = step;
+          a.lr = lr;
           a.param = param;
           a.exp_avg = m1;
           a.exp_avg_sq = m2;

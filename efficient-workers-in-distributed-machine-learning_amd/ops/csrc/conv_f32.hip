@@ -487,15 +487,26 @@ __global__ __launch_bounds__(CF_NT) void k_cf_gemm(const float* __restrict__ a_s
     for (int j = 0; j < CF_D; ++j) st.load(geo, min(kbeg + j, last), ra[j], rb[j]);
     st.store(smem, ra[0], rb[0]);
     __syncthreads();
-    for (int i0 = 0; i0 < n; i0 += CF_D) {
+    // full groups of CF_D steps carry no guard: a branch around the MFMAs makes hipcc's waitcnt
+    // pass drain the load ring at the loop latch (s_waitcnt vmcnt(2) instead of vmcnt(12))
+    const int nfull = n - n % CF_D;
+    for (int i0 = 0; i0 < nfull; i0 += CF_D) {
 #pragma unroll
       for (int u = 0; u < CF_D; ++u) {
-        const int i = i0 + u;
-        st.load(geo, min(kbeg + i + CF_D, last), ra[u], rb[u]);
+        st.load(geo, min(kbeg + i0 + u + CF_D, last), ra[u], rb[u]);
         char* cur = smem + (u & 1) * L::STAGE;
-        if (i < n)
-          cf_mma<MODE, BM, BN, SH, MI, NJ>(cur, cur + L::A_BYTES, wm * (BM / WM),
-                                           wn * (BN / WN), lane, acc);
+        cf_mma<MODE, BM, BN, SH, MI, NJ>(cur, cur + L::A_BYTES, wm * (BM / WM), wn * (BN / WN),
+                                         lane, acc);
+        st.store(smem + ((u + 1) & 1) * L::STAGE, ra[(u + 1) % CF_D], rb[(u + 1) % CF_D]);
+        __syncthreads();
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < CF_D - 1; ++u) {  // the last n % CF_D steps (already loaded: no loads)
+      if (u < n - nfull) {
+        char* cur = smem + (u & 1) * L::STAGE;
+        cf_mma<MODE, BM, BN, SH, MI, NJ>(cur, cur + L::A_BYTES, wm * (BM / WM), wn * (BN / WN),
+                                         lane, acc);
         st.store(smem + ((u + 1) & 1) * L::STAGE, ra[(u + 1) % CF_D], rb[(u + 1) % CF_D]);
         __syncthreads();
       }

@@ -73,6 +73,8 @@ struct AdamFlatArgs {
   int grad_dtype;
   float lr_step, beta1, beta2, eps, weight_decay, grad_scale, bc2_sqrt;
   int amsgrad;
+  uintptr_t step;  // int32 device step counter (nullable: use lr_step as given)
+  double lr;       // base lr for the device-side bias correction
 };
 
 size_t ew_topk_scratch_bytes(int num_tensors, int num_chunks);

@@ -56,7 +56,20 @@ __global__ __launch_bounds__(EW_BLOCK) void k_sgd_flat(float* __restrict__ p, fl
 struct AdamArgs {
   float lr_step, beta1, beta2, eps, weight_decay, grad_scale, bc2_sqrt;
   int amsgrad;
+  // device step counter (nullable): t = *step + 1 is read at run time and lr_step =
+  // lr * sqrt(1 - beta2^t) / (1 - beta1^t) computed from it, so a captured HIP graph replays
+  // the bias correction of the current step (the host value is frozen at capture)
+  const int* step;
+  double lr;
 };
+
+__device__ __forceinline__ void ew_adam_resolve(AdamArgs& a) {
+  if (a.step) {
+    const double t = (double)(*a.step + 1);
+    a.lr_step = (float)(a.lr * sqrt(1.0 - pow((double)a.beta2, t)) /
+                        (1.0 - pow((double)a.beta1, t)));
+  }
+}
 
 __device__ __forceinline__ void ew_adam(float& p, float& m, float& v, float& vm, float g,
                                         const AdamArgs& a) {
@@ -78,6 +91,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_adam_flat(float* __restrict__ p, f
                                                         float* __restrict__ v, float* __restrict__ vm,
                                                         const void* __restrict__ g, long long n4,
                                                         uint16_t* __restrict__ shadow, AdamArgs a) {
+  ew_adam_resolve(a);
   for (long long i = blockIdx.x * (long long)EW_BLOCK + threadIdx.x; i < n4;
        i += (long long)gridDim.x * EW_BLOCK) {
     float gv[4];
@@ -173,7 +187,9 @@ void ew_sgd_flat(const SgdFlatArgs& a) {
 }
 
 void ew_adam_flat(const AdamFlatArgs& a) {
-  AdamArgs aa{a.lr_step, a.beta1, a.beta2, a.eps, a.weight_decay, a.grad_scale, a.bc2_sqrt, a.amsgrad};
+  AdamArgs aa{a.lr_step, a.beta1,      a.beta2,   a.eps,
+              a.weight_decay, a.grad_scale, a.bc2_sqrt, a.amsgrad,
+              reinterpret_cast<const int*>(a.step), a.lr};
   const long long n4 = a.n / 4;
   auto* p = reinterpret_cast<float*>(a.param);
   auto* m = reinterpret_cast<float*>(a.exp_avg);

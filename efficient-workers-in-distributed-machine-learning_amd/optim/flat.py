@@ -82,6 +82,10 @@ class FlatAdam:
         self.exp_avg_sq = torch.zeros_like(flat.data)
         self.max_exp_avg_sq = torch.zeros_like(flat.data) if amsgrad else None
         self.steps = 0
+        # device copy of the step count: the kernel derives the bias correction from it, so a
+        # captured HIP graph replays the current step's correction (not the capture step's)
+        self.step_t = torch.zeros(1, dtype=torch.int32, device=flat.data.device) \
+            if flat.data.is_cuda else None
 
     def step_range(self, start, length, grad, grad_scale=1.0):
         t = self.steps + 1
@@ -93,7 +97,8 @@ class FlatAdam:
             lr_step = self.lr * math.sqrt(1 - b2 ** t) / (1 - b1 ** t)
             sh = self.flat.shadow[sl] if self.flat.shadow is not None else None
             ops.adam_flat(p, self.exp_avg[sl], self.exp_avg_sq[sl], vmax, grad, lr_step, b1, b2,
-                          self.eps, self.weight_decay, grad_scale, self.amsgrad, shadow=sh)
+                          self.eps, self.weight_decay, grad_scale, self.amsgrad, shadow=sh,
+                          step=self.step_t, lr=self.lr)
             return
         g = grad.to(torch.float32) * grad_scale
         oracle.adam_apply(p, self.exp_avg[sl], self.exp_avg_sq[sl],
@@ -106,6 +111,8 @@ class FlatAdam:
 
     def end_step(self):
         self.steps += 1
+        if self.step_t is not None:
+            self.step_t.add_(1)  # on the stream: captured into the step graph
 
     def state_dict(self):
         return {"kind": "adam", "exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq,
@@ -117,6 +124,8 @@ class FlatAdam:
         if self.amsgrad and sd.get("max_exp_avg_sq") is not None:
             self.max_exp_avg_sq.copy_(sd["max_exp_avg_sq"])
         self.steps = int(sd["steps"])
+        if self.step_t is not None:
+            self.step_t.fill_(self.steps)
         self.lr = sd.get("lr", self.lr)
 
 

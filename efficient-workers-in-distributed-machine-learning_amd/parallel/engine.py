@@ -289,10 +289,15 @@ def sync_params(flat, comm, src: int = 0):
     flat.sync_shadow()
 
 
-def sync_buffers(model, comm, src: int = 0):
+def sync_buffers(model, comm, src: int = 0, only_to: int = None):
+    """Broadcast the model's buffers (BN running statistics, counters) from ``src``.  With
+    ``only_to``, only that rank (and ``src``) keeps the values: the others receive into scratch
+    copies, so their own statistics are untouched."""
     for buf in model.buffers():
         if buf.dtype.is_floating_point or buf.dtype in (torch.int64, torch.int32):
-            comm.broadcast(buf.data, src=src)
+            keep = only_to is None or comm.rank in (src, only_to)
+            t = buf.data if keep else buf.data.clone()
+            comm.broadcast(t, src=src)
 
 
 class Stopwatch:

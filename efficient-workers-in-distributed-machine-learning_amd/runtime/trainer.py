@@ -328,38 +328,40 @@ class Trainer:
         # error terminates the process (seen with a real RCCL communicator).
         mode = os.environ.get("EWDML_GRAPH_CAPTURE_MODE", "thread_local")
         torch.cuda.synchronize()
-        if self.graph_mode == "full":
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, stream=self.gstream, capture_error_mode=mode):
-                try:
-                    if self._in_graph_batch:
-                        self._gx, self._gy = self.loader.emit()
-                    loss, out = self.forward_backward(self._gx, self._gy)
-                    ex.finish()
-                except BaseException:
-                    self._rejoin_side()
-                    raise
-            self._graphs = (g,)
-        else:
-            ex.defer_comm = True
-            ga = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(ga, stream=self.gstream, capture_error_mode=mode):
-                try:
-                    if self._in_graph_batch:
-                        self._gx, self._gy = self.loader.emit()
-                    loss, out = self.forward_backward(self._gx, self._gy)
-                    ex.launch_pending()
-                except BaseException:
-                    self._rejoin_side()
-                    raise
-                ex.join_side()
-            ex._active = False
-            gb = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(gb, pool=ga.pool(), stream=self.gstream,
-                                  capture_error_mode=mode):
-                ex.apply()
-            self._graphs = (ga, gb)
-        ex.step_idx, self.opt.steps = saved
+        try:  # the counters come back on the failure path too (eager fallback stays in step)
+            if self.graph_mode == "full":
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=self.gstream, capture_error_mode=mode):
+                    try:
+                        if self._in_graph_batch:
+                            self._gx, self._gy = self.loader.emit()
+                        loss, out = self.forward_backward(self._gx, self._gy)
+                        ex.finish()
+                    except BaseException:
+                        self._rejoin_side()
+                        raise
+                self._graphs = (g,)
+            else:
+                ex.defer_comm = True
+                ga = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(ga, stream=self.gstream, capture_error_mode=mode):
+                    try:
+                        if self._in_graph_batch:
+                            self._gx, self._gy = self.loader.emit()
+                        loss, out = self.forward_backward(self._gx, self._gy)
+                        ex.launch_pending()
+                    except BaseException:
+                        self._rejoin_side()
+                        raise
+                    ex.join_side()
+                ex._active = False
+                gb = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gb, pool=ga.pool(), stream=self.gstream,
+                                      capture_error_mode=mode):
+                    ex.apply()
+                self._graphs = (ga, gb)
+        finally:
+            ex.step_idx, self.opt.steps = saved
         self._gloss, self._gout = loss, out
         self._gbytes = ex.bytes_per_step()
 
@@ -446,8 +448,18 @@ class Trainer:
             extra["ef_residual"] = allr
         return extra
 
+    @property
+    def buffer_src(self) -> int:
+        """Rank whose BN running statistics are the model's: in the parameter-server topology
+        rank 0 is the server and never runs a forward pass, so its buffers stay at their
+        initial values -- the first worker's are used (the reference's workers write
+        model_step_, ``distributed_worker.py:_save_model``)."""
+        return 1 if (self.cfg.topology == "ps" and self.world > 1) else 0
+
     def save_checkpoint(self):
         """Collective (every rank calls it); rank 0 writes."""
+        if self.buffer_src != 0:  # rank 0 (the server) saves the first worker's BN statistics
+            sync_buffers(self.model, self.comm, src=self.buffer_src, only_to=0)
         extra = self.state_extra()
         if self.rank != 0:
             return None
@@ -534,7 +546,7 @@ class Trainer:
                 summary = rec
             if cfg.eval_freq and self.step % cfg.eval_freq == 0:
                 if cfg.sync_bn:
-                    sync_buffers(self.model, self.comm, src=0 if not self.is_server else 0)
+                    sync_buffers(self.model, self.comm, src=self.buffer_src)
                 self.save_checkpoint()
                 if cfg.eval_on_ckpt and self.rank == (1 if cfg.topology == "ps" else 0):
                     ev = self.evaluate()

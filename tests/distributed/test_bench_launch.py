@@ -42,6 +42,12 @@ def test_bench_two_ranks_gloo(preset, batch):
     # every rank sends the same fixed-size payload: the wire total is world x payload
     assert rec["grad_bytes_per_step_on_wire"] == 2 * rec["payload_bytes_per_rank"]
     assert rec["compression_ratio"] > 100
+    # headline at the reference's precision with the accuracy-preserving codec; the extra
+    # configurations are measured in the same run
+    assert rec["dtype"] == "fp32" and rec["config"]["error_feedback"] is True
+    for k in ("value_fp32_no_ef", "value_bf16", "ms_per_step_bf16"):
+        assert rec[k] > 0, k
+    assert rec["overlap_effective"] is (rec["config"]["buckets"] > 1)
     if preset == "vgg11":
         assert rec["config"]["model"] == "vgg11_bn"
         assert rec["metric"].startswith("grad bytes/step on wire + images/sec, VGG-11")

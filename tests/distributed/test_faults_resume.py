@@ -80,3 +80,35 @@ def test_reference_lenet_checkpoint_loads():
     assert sum(v.numel() for v in sd.values()) == 431080
     with torch.no_grad():
         assert m(torch.zeros(1, 1, 28, 28)).shape == (1, 10)
+
+
+def _fit_bn(rank, world, flags):
+    import ewdml
+    from ewdml.runtime import Trainer
+
+    tr = Trainer(ewdml.parse_args(flags))
+    tr.fit()
+    bn = [m for m in tr.model.modules() if isinstance(m, torch.nn.BatchNorm2d)][0]
+    return {"rm": bn.running_mean.clone(), "nbt": int(bn.num_batches_tracked)}
+
+
+def test_ps_topology_checkpoint_holds_worker_bn_statistics(tmp_path):
+    """Parameter-server topology with a BN model: rank 0 (the server) never runs a forward, so
+    the checkpoint it writes must carry the first worker's running statistics, not the initial
+    ones; the other workers keep their own."""
+    d = str(tmp_path / "ck") + "/"
+    flags = ["--network", "VGG11", "--dataset", "Cifar10", "--batch-size", "4",
+             "--synthetic-size", "64", "--momentum", "0.9", "--lr", "0.01", "--quiet",
+             "--device", "cpu", "--log-interval", "1000", "--topology", "ps", "--compress",
+             "none", "--amp", "none", "--max-steps", "2", "--eval-freq", "2", "--train-dir", d]
+    res = run_world(_fit_bn, 3, tmp_path / "w", args=(flags,))
+    assert res[1]["nbt"] == 2 and float(res[1]["rm"].abs().sum()) > 0
+    from ewdml.utils import checkpoint as ckpt
+
+    st = ckpt.load(ckpt.latest(d))
+    rm = [v for k, v in st["model"].items() if k.endswith("running_mean")][0]
+    nbt = [v for k, v in st["model"].items() if k.endswith("num_batches_tracked")][0]
+    assert int(nbt) == 2
+    torch.testing.assert_close(rm, res[1]["rm"])
+    # worker 2 kept its own statistics (different data shard)
+    assert not torch.equal(res[2]["rm"], res[1]["rm"])

@@ -38,6 +38,21 @@ def test_graph_modes_match_eager(codec):
         assert abs(l[-1] - l_ref[-1]) < 1e-2
 
 
+@pytest.mark.parametrize("opt", ["adam", "amsgrad"])
+def test_adam_graph_matches_eager(opt):
+    """Adam's bias correction follows the step count inside a replayed HIP graph (a device step
+    counter, not the host value frozen at capture): graph and eager runs stay together."""
+    ops.require()
+    flags = LENET + ["--compress", "none", "--optimizer", opt, "--lr", "0.001"]
+    ref, l_ref = _run(flags + ["--hip-graph", "off"], 10)
+    for mode in ("split", "full"):
+        tr, l = _run(flags + ["--hip-graph", mode], 10)
+        assert tr._graphs is not None and tr.opt.steps == 10
+        assert int(tr.opt.step_t.item()) == 10
+        rel = float((tr.flat.data - ref.flat.data).norm() / ref.flat.data.norm())
+        assert rel < 1e-4, f"{mode}: params differ from eager by {rel:.2e}"
+
+
 def test_graph_replay_refreshes_rng_key():
     """The QSGD rounding key lives in device memory and changes every replay."""
     tr, _ = _run(LENET + ["--compress", "topk_qsgd", "--hip-graph", "full"], 5)
