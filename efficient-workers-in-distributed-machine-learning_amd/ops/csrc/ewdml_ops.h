@@ -166,15 +166,16 @@ void ew_conv_wgrad(uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws, long l
 // int32 words of a grid arrival ticket (common.h ew_grid_last): 8 sub-counters + 1 top, 128 B apart
 #define EW_TICKET_INTS (9 * 32)
 
-// classifier-head Linear (head.hip): forward z = drop_out(act(drop_in(x) w^T + b)) (+ y = the
+// classifier-head Linear (head.hip), bf16 or fp32 (is_f32) tensors: forward z = drop_out(act(drop_in(x) w^T + b)) (+ y = the
 // pre-activation), backward dw, db, dx from dz in one launch; dropout = (counter, salt, p)
 void ew_head_fwd(uintptr_t x, uintptr_t w, uintptr_t b, uintptr_t z, uintptr_t y, int B, int N,
                  int K, int relu, uintptr_t ctr_in, uint32_t salt_in, float p_in,
-                 uintptr_t ctr_out, uint32_t salt_out, float p_out, uintptr_t stream);
+                 uintptr_t ctr_out, uint32_t salt_out, float p_out, uintptr_t stream,
+                 int is_f32);
 void ew_head_bwd(uintptr_t dz, uintptr_t y, uintptr_t x, uintptr_t w, uintptr_t dx, uintptr_t dw,
                  uintptr_t db, int db_bf16, int B, int N, int K, int relu, uintptr_t ctr_out,
                  uint32_t salt_out, float p_out, uintptr_t ctr_in, uint32_t salt_in, float p_in,
-                 int advance, uintptr_t stream);
+                 int advance, uintptr_t stream, int is_f32);
 // stem conv: 3x3 / pad 1 over C = 3 input channels (x [N,H,W,3], w [Nc,3,3,3] channels_last);
 // forward returns the BN partial rows written (0: none); wgrad uses ws as its partial slab
 int ew_conv_stem_fwd(uintptr_t x, uintptr_t w, uintptr_t y, long long N, int H, int W, int Nc,

@@ -14,7 +14,11 @@
 // element index r * width + c); the backward's last block advances the counters (arrival
 // ticket, no fences: every block read them before arriving).
 //
-// Tiles: one 16 x 16 output tile per block (v_mfma_f32_16x16x32_bf16), the reduction split over
+// Element types: bf16 (v_mfma_f32_16x16x32_bf16, one MFMA per 32-deep step) or fp32 (the reference
+// precision: eight v_mfma_f32_16x16x4_f32 per 32-deep step, MFMA e taking element e of each lane's
+// 8 consecutive k -- the same k permutation in both operands; no rounding of intermediates).
+//
+// Tiles: one 16 x 16 output tile per block, the reduction split over
 // the block's 4 waves (every wave issues all its loads before its first MFMA; partial tiles summed
 // through LDS): a 128 x 512 x 512 GEMM is 256 blocks with ~4 loads in flight per lane instead of
 // a few long dependent k-loops.  Operands go straight from L2 into the fragment registers (each
@@ -53,6 +57,34 @@ __device__ __forceinline__ float hd_relu(float v) { return (v > 0.0f || v != v) 
 __device__ __forceinline__ bool hd_relu_pass(float v) { return !(v <= 0.0f); }
 __device__ __forceinline__ float hd_rnd(float v) { return hd_f(ew_f2bf(v)); }
 
+// Element-type traits: 8-wide operand vector, load / store / rounding, one 32-deep MFMA step
+typedef float hd_f32x8 __attribute__((ext_vector_type(8)));
+template <typename T>
+struct HdT;
+template <>
+struct HdT<uint16_t> {
+  typedef hd_u16x8 v8;
+  __device__ static __forceinline__ float f(uint16_t v) { return hd_f(v); }
+  __device__ static __forceinline__ uint16_t st(float v) { return ew_f2bf(v); }
+  __device__ static __forceinline__ float rnd(float v) { return hd_rnd(v); }
+  __device__ static __forceinline__ hd_f32x4 mma(const v8& a, const v8& b, hd_f32x4 acc) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(hd_bf16x8, a),
+                                                   __builtin_bit_cast(hd_bf16x8, b), acc, 0, 0, 0);
+  }
+};
+template <>
+struct HdT<float> {
+  typedef hd_f32x8 v8;
+  __device__ static __forceinline__ float f(float v) { return v; }
+  __device__ static __forceinline__ float st(float v) { return v; }
+  __device__ static __forceinline__ float rnd(float v) { return v; }
+  __device__ static __forceinline__ hd_f32x4 mma(const v8& a, const v8& b, hd_f32x4 acc) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[e], b[e], acc, 0, 0, 0);
+    return acc;
+  }
+};
+
 // Sum the 4 waves' 16 x 16 accumulators (each wave took a quarter of the reduction) into wave 0's,
 // in a fixed order.
 __device__ __forceinline__ void hd_wave_reduce(hd_f32x4& acc, float* red, int wv, int lane) {
@@ -70,55 +102,54 @@ __device__ __forceinline__ void hd_wave_reduce(hd_f32x4& acc, float* red, int wv
 // ---- forward: z[B][N] = drop_out(act(drop_in(x) w^T + b)), y = pre-activation (optional) ----
 // Block: one 16 x 16 output tile; wave v takes the k-steps v, v + 4, ... (all its loads issued
 // before the first MFMA), the 4 partial tiles are summed through LDS.
-template <bool RELU>
-__global__ __launch_bounds__(EW_BLOCK) void k_head_fwd(const uint16_t* __restrict__ x,
-                                                       const uint16_t* __restrict__ w,
-                                                       const uint16_t* __restrict__ b,
-                                                       uint16_t* __restrict__ z,
-                                                       uint16_t* __restrict__ y, int B, int N,
-                                                       int K, HdDrop din, HdDrop dout) {
+template <typename T, bool RELU>
+__global__ __launch_bounds__(EW_BLOCK) void k_head_fwd(const T* __restrict__ x,
+                                                       const T* __restrict__ w,
+                                                       const T* __restrict__ b,
+                                                       T* __restrict__ z, T* __restrict__ y, int B,
+                                                       int N, int K, HdDrop din, HdDrop dout) {
+  using H = HdT<T>;
+  typedef typename H::v8 v8;
   __shared__ float red[16 * 64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, li = lane & 15;
   const int r = blockIdx.x * 16 + li;  // A row (batch row) of this lane
   const int n = blockIdx.y * 16 + li;  // B row (output feature) of this lane
   const int kq = 8 * (lane >> 4);
   const bool rok = r < B, nok = n < N;
-  const uint16_t* xp = x + (long long)(rok ? r : 0) * K + kq;
-  const uint16_t* wp = w + (long long)(nok ? n : 0) * K + kq;
+  const T* xp = x + (long long)(rok ? r : 0) * K + kq;
+  const T* wp = w + (long long)(nok ? n : 0) * K + kq;
   const uint32_t kin = hd_key(din);
   const float sin = hd_scale(din);
-  const hd_u16x8 zero = {0, 0, 0, 0, 0, 0, 0, 0};
+  const v8 zero = {};
   const int nsteps = K / 32;
   hd_f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
   for (int s0 = wv; s0 < nsteps; s0 += 16) {  // up to 4 steps of this wave in flight
-    hd_u16x8 av[4], bv[4];
+    v8 av[4], bv[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int s = s0 + 4 * u;
       const bool ok = s < nsteps;
-      av[u] = (ok && rok) ? *reinterpret_cast<const hd_u16x8*>(xp + 32 * s) : zero;
-      bv[u] = (ok && nok) ? *reinterpret_cast<const hd_u16x8*>(wp + 32 * s) : zero;
+      av[u] = (ok && rok) ? *reinterpret_cast<const v8*>(xp + 32 * s) : zero;
+      bv[u] = (ok && nok) ? *reinterpret_cast<const v8*>(wp + 32 * s) : zero;
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int s = s0 + 4 * u;
       if (s >= nsteps) break;
-      hd_u16x8 a = av[u];
+      v8 a = av[u];
       if (din.p > 0.0f) {  // the head's input Dropout, on the A operand (rounded like a stored z)
         const uint32_t i0 = (uint32_t)r * (uint32_t)K + (uint32_t)(32 * s + kq);
 #pragma unroll
         for (int e = 0; e < 8; ++e)
-          a[e] = ew_f2bf(hd_f(a[e]) * hd_mask(i0 + e, kin, din.p, sin));
+          a[e] = H::st(H::f(a[e]) * hd_mask(i0 + e, kin, din.p, sin));
       }
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(hd_bf16x8, a),
-                                                    __builtin_bit_cast(hd_bf16x8, bv[u]), acc,
-                                                    0, 0, 0);
+      acc = H::mma(a, bv[u], acc);
     }
   }
   hd_wave_reduce(acc, red, wv, lane);
   // C/D layout: column li (output feature), rows 4 (lane >> 4) + q (batch rows)
   if (wv != 0 || !nok) return;
-  const float bias = b ? hd_f(b[n]) : 0.0f;
+  const float bias = b ? H::f(b[n]) : 0.0f;
   const uint32_t kout = hd_key(dout);
   const float sout = hd_scale(dout);
 #pragma unroll
@@ -126,33 +157,35 @@ __global__ __launch_bounds__(EW_BLOCK) void k_head_fwd(const uint16_t* __restric
     const int rr = blockIdx.x * 16 + 4 * (lane >> 4) + q;
     if (rr >= B) continue;
     const long long o = (long long)rr * N + n;
-    const uint16_t yb = ew_f2bf(acc[q] + bias);  // the GEMM's bf16 output (bias in fp32)
+    const T yb = H::st(acc[q] + bias);  // the GEMM's output (bias in fp32)
     if (y) y[o] = yb;
-    float v = hd_f(yb);
+    float v = H::f(yb);
     if (RELU) v = hd_relu(v);
     if (dout.p > 0.0f) v = v * hd_mask((uint32_t)o, kout, dout.p, sout);
-    z[o] = ew_f2bf(v);
+    z[o] = H::st(v);
   }
 }
 
 // dy = bf16(dz * act'(y) * keep_out / (1 - p_out)) of element o (the value the GEMMs consume)
-template <bool RELU>
-__device__ __forceinline__ float hd_dyv(uint16_t dzv, uint16_t yv, uint32_t o, uint32_t kout,
+template <typename T, bool RELU>
+__device__ __forceinline__ float hd_dyv(T dzv, T yv, uint32_t o, uint32_t kout,
                                         const HdDrop& dout, float sout) {
-  float v = hd_f(dzv);
-  if (RELU && !hd_relu_pass(hd_f(yv))) v = 0.0f;
+  float v = HdT<T>::f(dzv);
+  if (RELU && !hd_relu_pass(HdT<T>::f(yv))) v = 0.0f;
   if (dout.p > 0.0f) v = v * hd_mask(o, kout, dout.p, sout);
-  return hd_rnd(v);
+  return HdT<T>::rnd(v);
 }
 
 // ---- backward: blocks [0, nbw) 16 x 16 weight-gradient tiles (+ bias gradient), the rest
 // 16 x 16 input-gradient tiles; in both, wave v takes a quarter of the reduction ----
-template <bool RELU>
+template <typename T, bool RELU>
 __global__ __launch_bounds__(EW_BLOCK) void k_head_bwd(
-    const uint16_t* __restrict__ dz, const uint16_t* __restrict__ y,
-    const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, uint16_t* __restrict__ dx,
-    uint16_t* __restrict__ dw, void* __restrict__ db, int db_bf16, int B, int N, int K,
-    HdDrop dout, HdDrop din, int nbw, int* __restrict__ adv0, int* __restrict__ adv1) {
+    const T* __restrict__ dz, const T* __restrict__ y, const T* __restrict__ x,
+    const T* __restrict__ w, T* __restrict__ dx, T* __restrict__ dw, void* __restrict__ db,
+    int db_bf16, int B, int N, int K, HdDrop dout, HdDrop din, int nbw, int* __restrict__ adv0,
+    int* __restrict__ adv1) {
+  using H = HdT<T>;
+  typedef typename H::v8 v8;
   __shared__ float red[16 * 64];
   __shared__ float dbr[4][16];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -170,36 +203,35 @@ __global__ __launch_bounds__(EW_BLOCK) void k_head_bwd(
     const int nc = nok ? n : 0, kc = kok ? k : 0;
     float dbs = 0.0f;
     for (int r0 = 32 * wv; r0 < B; r0 += 128) {
-      uint16_t dv[8], yv[8], xv[8];
+      T dv[8], yv[8], xv[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) {  // clamped rows: loads issued unconditionally, masked below
         const int rc = min(r0 + 8 * g + e, B - 1);
         dv[e] = dz[(long long)rc * N + nc];
-        yv[e] = RELU ? y[(long long)rc * N + nc] : (uint16_t)0;
+        yv[e] = RELU ? y[(long long)rc * N + nc] : (T)0;
         xv[e] = x[(long long)rc * K + kc];
       }
-      hd_u16x8 a, bb;
+      v8 a, bb;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const int rr = r0 + 8 * g + e;
         const bool ok = rr < B;
         const float d = (ok && nok)
-                            ? hd_dyv<RELU>(dv[e], yv[e], (uint32_t)rr * (uint32_t)N + (uint32_t)n,
-                                           kout, dout, sout)
+                            ? hd_dyv<T, RELU>(dv[e], yv[e],
+                                              (uint32_t)rr * (uint32_t)N + (uint32_t)n, kout,
+                                              dout, sout)
                             : 0.0f;
         dbs += d;
-        a[e] = ew_f2bf(d);
+        a[e] = H::st(d);
         float xf = 0.0f;
         if (ok && kok) {
-          xf = hd_f(xv[e]);
+          xf = H::f(xv[e]);
           if (din.p > 0.0f)
-            xf = hd_rnd(xf * hd_mask((uint32_t)rr * (uint32_t)K + (uint32_t)k, kin, din.p, sin));
+            xf = H::rnd(xf * hd_mask((uint32_t)rr * (uint32_t)K + (uint32_t)k, kin, din.p, sin));
         }
-        bb[e] = ew_f2bf(xf);
+        bb[e] = H::st(xf);
       }
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(hd_bf16x8, a),
-                                                    __builtin_bit_cast(hd_bf16x8, bb), acc, 0, 0,
-                                                    0);
+      acc = H::mma(a, bb, acc);
     }
     // bias gradient (tiles of column block 0): the A operand's sums over the rows
     dbs += __shfl_xor(dbs, 16, 64);
@@ -211,7 +243,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_head_bwd(
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int nn = tn * 16 + 4 * g + q;
-        if (nn < N && kok) dw[(long long)nn * K + k] = ew_f2bf(acc[q]);
+        if (nn < N && kok) dw[(long long)nn * K + k] = H::st(acc[q]);
       }
       if (db && tk == 0 && g == 0 && nok) {
         const float t = (dbr[0][li] + dbr[1][li]) + (dbr[2][li] + dbr[3][li]);
@@ -230,12 +262,12 @@ __global__ __launch_bounds__(EW_BLOCK) void k_head_bwd(
     const int nsteps = (N + 31) / 32;
     for (int s = wv; s < nsteps; s += 4) {
       const int nb = 32 * s + 8 * g;
-      uint16_t dv[8], yv[8], wv8[8];
-      if (vec && nb < N) {  // 16-B loads of this row's dz / y (N % 8 == 0: nb + 8 <= N)
+      T dv[8], yv[8], wv8[8];
+      if (vec && nb < N) {  // vector loads of this row's dz / y (N % 8 == 0: nb + 8 <= N)
         const long long o = (long long)rc * N + nb;
-        const hd_u16x8 d8 = *reinterpret_cast<const hd_u16x8*>(dz + o);
-        hd_u16x8 y8 = {0, 0, 0, 0, 0, 0, 0, 0};
-        if (RELU) y8 = *reinterpret_cast<const hd_u16x8*>(y + o);
+        const v8 d8 = *reinterpret_cast<const v8*>(dz + o);
+        v8 y8 = {};
+        if (RELU) y8 = *reinterpret_cast<const v8*>(y + o);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           dv[e] = d8[e];
@@ -246,25 +278,23 @@ __global__ __launch_bounds__(EW_BLOCK) void k_head_bwd(
         for (int e = 0; e < 8; ++e) {
           const int nn = min(nb + e, N - 1);
           dv[e] = dz[(long long)rc * N + nn];
-          yv[e] = RELU ? y[(long long)rc * N + nn] : (uint16_t)0;
+          yv[e] = RELU ? y[(long long)rc * N + nn] : (T)0;
         }
       }
 #pragma unroll
       for (int e = 0; e < 8; ++e) wv8[e] = w[(long long)min(nb + e, N - 1) * K + kc];
-      hd_u16x8 a, bb;
+      v8 a, bb;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const int nn = nb + e;
         const bool ok = nn < N;
-        a[e] = (ok && rok) ? ew_f2bf(hd_dyv<RELU>(dv[e], yv[e],
-                                                  (uint32_t)r * (uint32_t)N + (uint32_t)nn, kout,
-                                                  dout, sout))
-                           : (uint16_t)0;
-        bb[e] = (ok && kok) ? wv8[e] : (uint16_t)0;
+        a[e] = (ok && rok) ? H::st(hd_dyv<T, RELU>(dv[e], yv[e],
+                                                   (uint32_t)r * (uint32_t)N + (uint32_t)nn,
+                                                   kout, dout, sout))
+                           : (T)0;
+        bb[e] = (ok && kok) ? wv8[e] : (T)0;
       }
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(hd_bf16x8, a),
-                                                    __builtin_bit_cast(hd_bf16x8, bb), acc, 0, 0,
-                                                    0);
+      acc = H::mma(a, bb, acc);
     }
     hd_wave_reduce(acc, red, wv, lane);
     if (wv == 0 && kok) {
@@ -275,7 +305,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_head_bwd(
         const long long o = (long long)rr * K + k;
         float v = acc[q];
         if (din.p > 0.0f) v = v * hd_mask((uint32_t)o, kin, din.p, sin);
-        dx[o] = ew_f2bf(v);
+        dx[o] = H::st(v);
       }
     }
   }
@@ -303,18 +333,23 @@ static HdDrop hd_drop(uintptr_t ctr, uint32_t salt, float p) {
 
 void ew_head_fwd(uintptr_t x, uintptr_t w, uintptr_t b, uintptr_t z, uintptr_t y, int B, int N,
                  int K, int relu, uintptr_t ctr_in, uint32_t salt_in, float p_in,
-                 uintptr_t ctr_out, uint32_t salt_out, float p_out, uintptr_t stream) {
+                 uintptr_t ctr_out, uint32_t salt_out, float p_out, uintptr_t stream, int is_f32) {
   if (B <= 0 || N <= 0 || K % 32)
     throw std::runtime_error("ewdml head: needs B, N > 0 and K % 32 == 0");
   const HdDrop din = hd_drop(ctr_in, salt_in, p_in), dout = hd_drop(ctr_out, salt_out, p_out);
   const dim3 grid((B + 15) / 16, (N + 15) / 16);
-#define HD_FWD(R)                                                                               \
-  hipLaunchKernelGGL(k_head_fwd<R>, grid, dim3(EW_BLOCK), 0, (hipStream_t)stream,              \
-                     reinterpret_cast<const uint16_t*>(x), reinterpret_cast<const uint16_t*>(w), \
-                     reinterpret_cast<const uint16_t*>(b), reinterpret_cast<uint16_t*>(z),      \
-                     reinterpret_cast<uint16_t*>(y), B, N, K, din, dout)
-  if (relu) HD_FWD(true);
-  else HD_FWD(false);
+#define HD_FWD(T, R)                                                                            \
+  hipLaunchKernelGGL((k_head_fwd<T, R>), grid, dim3(EW_BLOCK), 0, (hipStream_t)stream,         \
+                     reinterpret_cast<const T*>(x), reinterpret_cast<const T*>(w),               \
+                     reinterpret_cast<const T*>(b), reinterpret_cast<T*>(z),                     \
+                     reinterpret_cast<T*>(y), B, N, K, din, dout)
+  if (is_f32) {
+    if (relu) HD_FWD(float, true);
+    else HD_FWD(float, false);
+  } else {
+    if (relu) HD_FWD(uint16_t, true);
+    else HD_FWD(uint16_t, false);
+  }
 #undef HD_FWD
   EW_CHECK_LAUNCH();
 }
@@ -322,7 +357,7 @@ void ew_head_fwd(uintptr_t x, uintptr_t w, uintptr_t b, uintptr_t z, uintptr_t y
 void ew_head_bwd(uintptr_t dz, uintptr_t y, uintptr_t x, uintptr_t w, uintptr_t dx, uintptr_t dw,
                  uintptr_t db, int db_bf16, int B, int N, int K, int relu, uintptr_t ctr_out,
                  uint32_t salt_out, float p_out, uintptr_t ctr_in, uint32_t salt_in, float p_in,
-                 int advance, uintptr_t stream) {
+                 int advance, uintptr_t stream, int is_f32) {
   if (B <= 0 || N <= 0 || K % 32)
     throw std::runtime_error("ewdml head: needs B, N > 0 and K % 32 == 0");
   if (relu && !y) throw std::runtime_error("ewdml head: ReLU backward needs the pre-activation");
@@ -338,14 +373,19 @@ void ew_head_bwd(uintptr_t dz, uintptr_t y, uintptr_t x, uintptr_t w, uintptr_t 
     a0 = c_in ? c_in : c_out;
     a1 = (c_in && c_out && c_out != c_in) ? c_out : nullptr;
   }
-#define HD_BWD(R)                                                                               \
-  hipLaunchKernelGGL(k_head_bwd<R>, dim3(nbw + nbx), dim3(EW_BLOCK), 0, (hipStream_t)stream,   \
-                     reinterpret_cast<const uint16_t*>(dz), reinterpret_cast<const uint16_t*>(y), \
-                     reinterpret_cast<const uint16_t*>(x), reinterpret_cast<const uint16_t*>(w), \
-                     reinterpret_cast<uint16_t*>(dx), reinterpret_cast<uint16_t*>(dw),          \
+#define HD_BWD(T, R)                                                                            \
+  hipLaunchKernelGGL((k_head_bwd<T, R>), dim3(nbw + nbx), dim3(EW_BLOCK), 0, (hipStream_t)stream, \
+                     reinterpret_cast<const T*>(dz), reinterpret_cast<const T*>(y),              \
+                     reinterpret_cast<const T*>(x), reinterpret_cast<const T*>(w),               \
+                     reinterpret_cast<T*>(dx), reinterpret_cast<T*>(dw),                         \
                      reinterpret_cast<void*>(db), db_bf16, B, N, K, dout, din, nbw, a0, a1)
-  if (relu) HD_BWD(true);
-  else HD_BWD(false);
+  if (is_f32) {
+    if (relu) HD_BWD(float, true);
+    else HD_BWD(float, false);
+  } else {
+    if (relu) HD_BWD(uint16_t, true);
+    else HD_BWD(uint16_t, false);
+  }
 #undef HD_BWD
   EW_CHECK_LAUNCH();
 }

@@ -7,7 +7,8 @@ offset fills under HIP graphs (~114 us of a ~1.05 ms VGG-11 step).  Here 3 forwa
 kernels: the input Dropout is applied to the first GEMM's operand on load, bias + ReLU + Dropout
 run in the GEMM epilogue, and each backward launch recomputes its masks on load and computes the
 weight, bias and input gradients together.  Same math as ``nn.Dropout`` / ``nn.ReLU`` /
-``nn.Linear`` with bf16 operands and fp32 accumulation; masks come from a counter-based hash keyed
+``nn.Linear`` with bf16 or fp32 operands (``v_mfma_f32_16x16x32_bf16`` /
+``v_mfma_f32_16x16x4_f32``) and fp32 accumulation; masks come from a counter-based hash keyed
 per step by a per-layer device counter (so they differ from PyTorch's generator; the keep
 probability and 1/(1-p) scaling are the same).  :class:`_ActDropout` (one act/dropout kernel per
 direction, ``ops/csrc/nn.hip``) remains as a standalone op.
@@ -94,7 +95,7 @@ class _HeadLinear(torch.autograd.Function):
         z = torch.empty((B, N), dtype=x.dtype, device=x.device)
         y = torch.empty((B, N), dtype=x.dtype, device=x.device) if relu else None
         C_.head_fwd(_ptr(x), _ptr(w), _ptr(b), _ptr(z), _ptr(y), B, N, K, int(relu),
-                    *_drop_args(din), *_drop_args(dout), _stream())
+                    *_drop_args(din), *_drop_args(dout), _stream(), int(x.dtype == torch.float32))
         ctx.relu, ctx.din, ctx.dout, ctx.advance = relu, din, dout, advance
         ctx.save_for_backward(x, w, y)
         return z
@@ -114,7 +115,8 @@ class _HeadLinear(torch.autograd.Function):
         db = torch.empty(N, dtype=w.dtype, device=w.device)
         C_.head_bwd(_ptr(dz), _ptr(y), _ptr(x), _ptr(w), _ptr(dx), _ptr(dw), _ptr(db),
                     int(db.dtype == torch.bfloat16), B, N, K, int(ctx.relu),
-                    *_drop_args(ctx.dout), *_drop_args(ctx.din), int(ctx.advance), _stream())
+                    *_drop_args(ctx.dout), *_drop_args(ctx.din), int(ctx.advance), _stream(),
+                    int(x.dtype == torch.float32))
         return dx, (dw if need[1] else None), (db if need[2] else None), None, None, None, None
 
 
@@ -135,20 +137,22 @@ def _head_layout(cls):
     return mods if ok else None
 
 
-def _lin_ok(lin, x_width):
+def _lin_ok(lin, x_width, dtype):
     w, b = lin.weight, lin.bias
-    return (b is not None and w.dtype == torch.bfloat16 and b.dtype == torch.bfloat16
+    return (b is not None and w.dtype == dtype and b.dtype == dtype
             and w.is_contiguous() and b.is_contiguous() and w.shape[1] == x_width
             and x_width % 32 == 0 and w.data_ptr() % 16 == 0)
 
 
 def supported(cls, x) -> bool:
     mods = _head_layout(cls)
-    if not _ENABLED or mods is None or not (x.is_cuda and x.dim() == 2 and x.dtype == torch.bfloat16):
+    if not _ENABLED or mods is None or not (x.is_cuda and x.dim() == 2
+                                            and x.dtype in (torch.bfloat16, torch.float32)):
         return False
     l1, l2, l3 = mods[1], mods[4], mods[6]
-    if not (_lin_ok(l1, x.shape[1]) and _lin_ok(l2, l1.out_features)
-            and _lin_ok(l3, l2.out_features)):
+    dt = x.dtype
+    if not (_lin_ok(l1, x.shape[1], dt) and _lin_ok(l2, l1.out_features, dt)
+            and _lin_ok(l3, l2.out_features, dt)):
         return False
     return (x.is_contiguous() and x.data_ptr() % 16 == 0 and 0 < x.shape[0]
             and x.shape[0] * max(x.shape[1], l1.out_features, l2.out_features) < 2 ** 31)

@@ -34,6 +34,11 @@ def _rel(a, b):
     return float((a - b).norm() / (b.norm() + 1e-30))
 
 
+def _rel64(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return float((a - b).norm() / (b.norm() + 1e-30))
+
+
 @pytest.mark.parametrize("shape,pool", [((8, 64, 32, 32), True), ((8, 64, 16, 16), False),
                                         ((4, 512, 2, 2), True), ((6, 24, 6, 10), False),
                                         ((2, 2048, 4, 4), False)])
@@ -411,3 +416,58 @@ def test_head_linear_input_dropout():
     assert int(ctr[0]) == 1
     z2 = head.head_linear(x.detach(), lin, relu=False, din=(ctr, 77, 0.5))
     assert not torch.equal(z2, z.detach())  # next step: new mask
+
+
+def test_vgg_head_fp32_matches_float64():
+    """fp32 head kernels (eight v_mfma_f32_16x16x4_f32 per 32-deep step): forward and all
+    gradients against float64 PyTorch, no dropout."""
+    from ewdml.models import build_model
+    from ewdml.ops import head
+
+    _ops()
+    cls = build_model("vgg11", 10).cuda().classifier
+    for mod in cls:
+        if isinstance(mod, nn.Dropout):
+            mod.p = 0.0
+    x = torch.randn(128, 512, device="cuda")
+    xa = x.clone().requires_grad_(True)
+    assert head.supported(cls, xa)
+    out = head.vgg_head(cls, xa)
+    assert out.dtype == torch.float32 and out.grad_fn is not None
+    assert "Head" in type(out.grad_fn).__name__
+    gout = torch.randn_like(out)
+    out.backward(gout)
+    c64 = copy.deepcopy(cls).double().cpu()
+    xr = x.double().cpu().requires_grad_(True)
+    ref = c64(xr)
+    ref.backward(gout.double().cpu())
+    assert _rel64(out, ref) < 1e-5, _rel64(out, ref)
+    assert _rel64(xa.grad, xr.grad) < 1e-5, _rel64(xa.grad, xr.grad)
+    for p, q in zip(cls.parameters(), c64.parameters()):
+        assert p.grad.dtype == torch.float32
+        assert _rel64(p.grad, q.grad) < 1e-5, _rel64(p.grad, q.grad)
+
+
+@pytest.mark.parametrize("rows,C,p", [(37, 24, 0.0), (300, 40, 0.3), (128, 512, 0.5)])
+def test_head_linear_fp32_dropout_edges(rows, C, p):
+    """fp32 head Linear + ReLU + output dropout on off-tile shapes: the forward's mask applied in
+    float64 reproduces output and gradients to fp32 accuracy."""
+    from ewdml.ops import head
+
+    _ops()
+    lin = nn.Linear(64, C).cuda()
+    x = torch.randn(rows, 64, device="cuda").requires_grad_(True)
+    ctr = head._ctr(lin, x.device)
+    spec = (ctr, 4321, p) if p > 0 else None
+    z = head.head_linear(x, lin, relu=True, dout=spec)
+    y = torch.addmm(lin.bias.double(), x.detach().double(), lin.weight.double().t())
+    keep = (z.double() != 0) | (y <= 0)
+    scale = 1.0 / (1.0 - p)
+    zr = torch.relu(y) * keep.double() * scale
+    assert _rel64(z, zr) < 1e-5
+    g = torch.randn_like(z)
+    z.backward(g)
+    dyr = g.double() * (y > 0).double() * keep.double() * scale
+    assert torch.allclose(lin.bias.grad.double(), dyr.sum(0), rtol=1e-5, atol=1e-5)
+    assert _rel64(x.grad, dyr @ lin.weight.detach().double()) < 1e-5
+    assert _rel64(lin.weight.grad, dyr.t() @ x.detach().double()) < 1e-5
