@@ -118,52 +118,63 @@ struct CfMfma<32> {
   }
 };
 
-// One k-step of MFMAs over a stage: acc[i][j] += A[wave rows][32] * B[wave cols][32]^T.  Lane
-// group g (lane / SH) takes the 8/G 16-B chunks r*G + g (r < 8/G) of the 32-deep step: read r
-// holds k = 4 (r G + g) + jj in element jj, and MFMA (r, jj) consumes element jj of both operands,
-// so every k is used exactly once with the same permutation in A and B.
-template <int MODE, int BM, int BN, int SH, int MI, int NJ>
-__device__ __forceinline__ void cf_mma(const char* __restrict__ As, const char* __restrict__ Bs,
-                                       int arow0, int bcol0, int lane,
-                                       typename CfMfma<SH>::acc_t (&acc)[MI][NJ]) {
-  using L = CfLayout<MODE, BM, BN>;
-  using F = CfMfma<SH>;
-  constexpr int R = 8 / F::G;
-  const int g = lane / SH, li = lane % SH;
+// One k-step's MFMA operand fragments of a wave, read from an LDS stage.  Lane group g
+// (lane / SH) takes the 8/G 16-B chunks r*G + g (r < 8/G) of the 32-deep step: read r holds
+// k = 4 (r G + g) + jj in element jj, and MFMA (r, jj) consumes element jj of both operands, so
+// every k is used exactly once with the same permutation in A and B.
+template <int SH, int MI, int NJ>
+struct CfFrag {
+  static constexpr int R = 8 / CfMfma<SH>::G;
   f32x4 a[R][MI], b[R][NJ];
+};
+
+template <int MODE, int BM, int BN, int SH, int MI, int NJ>
+__device__ __forceinline__ void cf_frag_read(const char* __restrict__ As,
+                                             const char* __restrict__ Bs, int arow0, int bcol0,
+                                             int lane, CfFrag<SH, MI, NJ>& f) {
+  using L = CfLayout<MODE, BM, BN>;
+  constexpr int R = CfFrag<SH, MI, NJ>::R;
+  const int g = lane / SH, li = lane % SH;
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    const int ch = r * F::G + g;
+    const int ch = r * CfMfma<SH>::G + g;
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
       if constexpr (L::A_KC) {
-        a[r][i] = *reinterpret_cast<const f32x4*>(As + cf_off(arow0 + i * SH + li, ch));
+        f.a[r][i] = *reinterpret_cast<const f32x4*>(As + cf_off(arow0 + i * SH + li, ch));
       } else {
         const float* ap = reinterpret_cast<const float*>(As) + 4 * ch * L::PA + arow0 + i * SH + li;
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) a[r][i][jj] = ap[jj * L::PA];
+        for (int jj = 0; jj < 4; ++jj) f.a[r][i][jj] = ap[jj * L::PA];
       }
     }
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       if constexpr (L::B_KC) {
-        b[r][j] = *reinterpret_cast<const f32x4*>(Bs + cf_off(bcol0 + j * SH + li, ch));
+        f.b[r][j] = *reinterpret_cast<const f32x4*>(Bs + cf_off(bcol0 + j * SH + li, ch));
       } else {
         const float* bp = reinterpret_cast<const float*>(Bs) + 4 * ch * L::PB + bcol0 + j * SH + li;
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) b[r][j][jj] = bp[jj * L::PB];
+        for (int jj = 0; jj < 4; ++jj) f.b[r][j][jj] = bp[jj * L::PB];
       }
     }
   }
+}
+
+// MFMAs of fragment reads [R0, R1) of a step: acc[i][j] += A[rows] * B[cols]^T over those k
+template <int SH, int MI, int NJ, int R0, int R1>
+__device__ __forceinline__ void cf_mma(const CfFrag<SH, MI, NJ>& f,
+                                       typename CfMfma<SH>::acc_t (&acc)[MI][NJ]) {
+  using F = CfMfma<SH>;
   if (CF_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-  for (int r = 0; r < R; ++r)
+  for (int r = R0; r < R1; ++r)
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj)
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) acc[i][j] = F::mma(a[r][i][jj], b[r][j][jj], acc[i][j]);
+        for (int j = 0; j < NJ; ++j) acc[i][j] = F::mma(f.a[r][i][jj], f.b[r][j][jj], acc[i][j]);
   if (CF_PRIO) __builtin_amdgcn_s_setprio(0);
 }
 
@@ -179,17 +190,16 @@ struct CfRegs {
     if constexpr (R_ > 3) { constexpr int i = 3; auto& v = RG.v3; __VA_ARGS__; }               \
   } while (0)
 
-// Per-thread operand staging state (CF_NT threads).  KC tiles: thread t stages chunk t & 7 of rows
-// (t >> 3) + 64 i (i < BM/64).  RC tiles ([32 k][BN cols]): BN/4 chunks per k-row, thread t
-// stages chunk t % (BN/4) of k-rows t / (BN/4) + (2048/BN) i (i < BN/64).
-constexpr int CF_NT = 512;  // threads per GEMM block: 8 waves, two per SIMD
-constexpr int CF_D = 4;     // k-loop prefetch depth (staging register sets; even)
-template <int MODE, int BM, int BN>
+// Per-thread operand staging state (NT threads).  KC tiles: thread t stages chunk t & 7 of rows
+// (t >> 3) + (NT / 8) i (i < 8 BM / NT).  RC tiles ([32 k][BN cols]): BN/4 chunks per k-row,
+// thread t stages chunk t % (BN/4) of k-rows t / (BN/4) + (4 NT / BN) i (i < 8 BN / NT).
+template <int MODE, int BM, int BN, int NT>
 struct CfStager {
   using L = CfLayout<MODE, BM, BN>;
-  static constexpr int RA = BM / 64, RB = BN / 64;
-  static constexpr int RCA = BM / 4, RCB = BN / 4;              // RC chunks per k-row
-  static constexpr int RPA = CF_NT / RCA, RPB = CF_NT / RCB;    // RC k-rows per pass
+  static constexpr int RA = 8 * BM / NT, RB = 8 * BN / NT;    // 16-B vectors per thread
+  static_assert(RA >= 1 && RA <= 4 && RB >= 1 && RB <= 4, "staging registers");
+  static constexpr int RCA = BM / 4, RCB = BN / 4;            // RC chunks per k-row
+  static constexpr int RPA = NT / RCA, RPB = NT / RCB;        // RC k-rows per pass
   // KC im2col rows (fwd, bwd A): pixel and its (h, w)
   int am[RA], ah[RA], aw[RA];
   // wgrad B: the thread's column chunk's tap offset and channel
@@ -208,7 +218,7 @@ struct CfStager {
     if constexpr (L::A_KC) {
 #pragma unroll
       for (int i = 0; i < RA; ++i) {
-        const int m = m0 + (t >> 3) + 64 * i;
+        const int m = m0 + (t >> 3) + (NT / 8) * i;
         am[i] = m;
         const int hw = m % (g.H * g.W);
         ah[i] = hw / g.W;
@@ -247,7 +257,7 @@ struct CfStager {
         const long long K = (long long)g.taps * g.C;
         CfRegs& RG = rb;
         CF_FOR(RB, {
-          v = *reinterpret_cast<const f32x4*>(xb + (long long)(n0 + (t >> 3) + 64 * i) * K +
+          v = *reinterpret_cast<const f32x4*>(xb + (long long)(n0 + (t >> 3) + (NT / 8) * i) * K +
                                               (long long)s * CF_BK + (t & 7) * 4);
         });
       } else {
@@ -292,7 +302,7 @@ struct CfStager {
     {
       const CfRegs& RG = ra;
       if constexpr (L::A_KC) {
-        CF_FOR(RA, { *reinterpret_cast<f32x4*>(As + cf_off((t >> 3) + 64 * i, t & 7)) = v; });
+        CF_FOR(RA, { *reinterpret_cast<f32x4*>(As + cf_off((t >> 3) + (NT / 8) * i, t & 7)) = v; });
       } else {
         CF_FOR(RA, {
           *reinterpret_cast<f32x4*>(As + ((t / RCA + RPA * i) * L::PA + (t % RCA) * 4) * 4) = v;
@@ -302,7 +312,7 @@ struct CfStager {
     {
       const CfRegs& RG = rb;
       if constexpr (L::B_KC) {
-        CF_FOR(RB, { *reinterpret_cast<f32x4*>(Bs + cf_off((t >> 3) + 64 * i, t & 7)) = v; });
+        CF_FOR(RB, { *reinterpret_cast<f32x4*>(Bs + cf_off((t >> 3) + (NT / 8) * i, t & 7)) = v; });
       } else {
         CF_FOR(RB, {
           *reinterpret_cast<f32x4*>(Bs + ((t / RCB + RPB * i) * L::PB + (t % RCB) * 4) * 4) = v;
@@ -448,8 +458,8 @@ __device__ __forceinline__ void cf_epilogue(typename CfMfma<SH>::acc_t (&acc)[MI
 // 32-deep k-step per iteration through two LDS stages and two staging register sets (step s+2 is
 // loaded while s computes and s+1 is written), split z covers k-steps
 // [z*kps, min((z+1)*kps, ksteps)).
-template <int MODE, int BM, int BN, int WM, int SH>
-__global__ __launch_bounds__(CF_NT) void k_cf_gemm(const float* __restrict__ a_src,
+template <int MODE, int BM, int BN, int WM, int WN, int SH>
+__global__ __launch_bounds__(64 * WM * WN) void k_cf_gemm(const float* __restrict__ a_src,
                                                    const float* __restrict__ b_src,
                                                    float* __restrict__ out,
                                                    float* __restrict__ slab, CfGeom geo,
@@ -457,7 +467,7 @@ __global__ __launch_bounds__(CF_NT) void k_cf_gemm(const float* __restrict__ a_s
                                                    const float* __restrict__ addend) {
   using L = CfLayout<MODE, BM, BN>;
   using acc_t = typename CfMfma<SH>::acc_t;
-  constexpr int WN = 8 / WM;
+  constexpr int NT = 64 * WM * WN;
   constexpr int MI = BM / WM / SH, NJ = BN / WN / SH;
   static_assert(MI >= 1 && NJ >= 1 && MI * SH * WM == BM && NJ * SH * WN == BN, "wave tiling");
   __shared__ __attribute__((aligned(16))) char smem[2 * L::STAGE];
@@ -466,7 +476,7 @@ __global__ __launch_bounds__(CF_NT) void k_cf_gemm(const float* __restrict__ a_s
   const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
   const int kbeg = blockIdx.z * geo.kps;
   const int kend = min(kbeg + geo.kps, geo.ksteps);
-  CfStager<MODE, BM, BN> st;
+  CfStager<MODE, BM, BN, NT> st;
   st.init(geo, a_src, b_src, t, m0, n0);
 
   acc_t acc[MI][NJ];
@@ -475,43 +485,40 @@ __global__ __launch_bounds__(CF_NT) void k_cf_gemm(const float* __restrict__ a_s
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[i][j] = acc_t{};
 
+  // Two LDS stages and two staging register sets: step s + 2 is loaded while step s computes
+  // and step s + 1 (loaded one step earlier) is written; one barrier per step.  Loads past the
+  // end are clamped re-loads of the last step.
+  using Frag = CfFrag<SH, MI, NJ>;
+  const int arow0 = wm * (BM / WM), bcol0 = wn * (BN / WN);
   const int n = kend - kbeg;
   if (n > 0) {
     const int last = kend - 1;
-    // CF_D staging register sets: the loads of step i + CF_D are issued at iteration i into the
-    // set that held step i (written to LDS one iteration earlier), so a load has CF_D - 1
-    // iterations (~3-5 us) to land before its LDS write; two LDS stages, one barrier per step.
-    // Loads past the end are clamped re-loads of the last step (branch-free, no scratch).
-    CfRegs ra[CF_D], rb[CF_D];
-#pragma unroll
-    for (int j = 0; j < CF_D; ++j) st.load(geo, min(kbeg + j, last), ra[j], rb[j]);
+    CfRegs ra[2], rb[2];
+    st.load(geo, kbeg, ra[0], rb[0]);
     st.store(smem, ra[0], rb[0]);
+    st.load(geo, min(kbeg + 1, last), ra[1], rb[1]);
     __syncthreads();
-    // full groups of CF_D steps carry no guard: a branch around the MFMAs makes hipcc's waitcnt
-    // pass drain the load ring at the loop latch (s_waitcnt vmcnt(2) instead of vmcnt(12))
-    const int nfull = n - n % CF_D;
-    for (int i0 = 0; i0 < nfull; i0 += CF_D) {
+    // pairs of steps without a guard (a branch around the MFMAs de-pipelines hipcc's waits)
+    const int nfull = n - (n & 1);
+    for (int i0 = 0; i0 < nfull; i0 += 2) {
 #pragma unroll
-      for (int u = 0; u < CF_D; ++u) {
-        st.load(geo, min(kbeg + i0 + u + CF_D, last), ra[u], rb[u]);
-        char* cur = smem + (u & 1) * L::STAGE;
-        cf_mma<MODE, BM, BN, SH, MI, NJ>(cur, cur + L::A_BYTES, wm * (BM / WM), wn * (BN / WN),
-                                         lane, acc);
-        st.store(smem + ((u + 1) & 1) * L::STAGE, ra[(u + 1) % CF_D], rb[(u + 1) % CF_D]);
+      for (int u = 0; u < 2; ++u) {
+        st.load(geo, min(kbeg + i0 + u + 2, last), ra[u], rb[u]);
+        const char* cs = smem + u * L::STAGE;
+        Frag fr;
+        cf_frag_read<MODE, BM, BN, SH, MI, NJ>(cs, cs + L::A_BYTES, arow0, bcol0, lane, fr);
+        cf_mma<SH, MI, NJ, 0, Frag::R>(fr, acc);
+        st.store(smem + (u ^ 1) * L::STAGE, ra[u ^ 1], rb[u ^ 1]);
         __syncthreads();
       }
     }
-#pragma unroll
-    for (int u = 0; u < CF_D - 1; ++u) {  // the last n % CF_D steps (already loaded: no loads)
-      if (u < n - nfull) {
-        char* cur = smem + (u & 1) * L::STAGE;
-        cf_mma<MODE, BM, BN, SH, MI, NJ>(cur, cur + L::A_BYTES, wm * (BM / WM), wn * (BN / WN),
-                                         lane, acc);
-        st.store(smem + ((u + 1) & 1) * L::STAGE, ra[(u + 1) % CF_D], rb[(u + 1) % CF_D]);
-        __syncthreads();
-      }
+    if (n & 1) {  // the last step (stage 0)
+      Frag fr;
+      cf_frag_read<MODE, BM, BN, SH, MI, NJ>(smem, smem + L::A_BYTES, arow0, bcol0, lane, fr);
+      cf_mma<SH, MI, NJ, 0, Frag::R>(fr, acc);
     }
   }
+  __syncthreads();  // the epilogue reuses smem
   cf_epilogue<BM, BN, WM, WN, SH, MI, NJ>(acc, smem, wm, wn, lane, m0, n0, geo.M, geo.Ncol,
                                           out, slab, bnpart, bb, addend);
 }
@@ -858,9 +865,9 @@ CfPlan cf_plan(int M, int Ncol, int ksteps, long long ws_floats, bool allow_spli
   return best;
 }
 
-#define CF_LAUNCH(MODE_, BM_, BN_, WM_, SH_)                                                      \
-  hipLaunchKernelGGL((k_cf_gemm<MODE_, BM_, BN_, WM_, SH_>), grid, dim3(CF_NT), 0, s, a, b, out,  \
-                     slab, geo, bnp, bbv, addend)
+#define CF_LAUNCH(MODE_, BM_, BN_, WM_, WN_, SH_)                                                 \
+  hipLaunchKernelGGL((k_cf_gemm<MODE_, BM_, BN_, WM_, WN_, SH_>), grid, dim3(64 * WM_ * WN_), 0, s, \
+                     a, b, out, slab, geo, bnp, bbv, addend)
 
 template <int MODE>
 int cf_gemm(const float* a, const float* b, float* out, float* ws, long long ws_floats,
@@ -878,10 +885,20 @@ int cf_gemm(const float* a, const float* b, float* out, float* ws, long long ws_
   const CfBnBwd bbv = (bnp && bnb) ? *bnb : none;
   // wave grids: 128x128 -> 2x4 waves of 64x32; 128x64 -> 4x2 of 32x32; 64x128 -> 2x4 of 32x32;
   // 64x64 -> 4x2 of 16x32
-  if (p.bm == 128 && p.bn == 128) CF_LAUNCH(MODE, 128, 128, 2, 32);
-  else if (p.bm == 128) CF_LAUNCH(MODE, 128, 64, 4, 32);
-  else if (p.bn == 128) CF_LAUNCH(MODE, 64, 128, 2, 32);
-  else CF_LAUNCH(MODE, 64, 64, 4, 16);
+  static const int w4 = [] {  // EWDML_CF_WAVES=4: 4-wave 128x128 blocks (64x64 wave tiles)
+    const char* e = getenv("EWDML_CF_WAVES");
+    return e && e[0] == '4';
+  }();
+  if (p.bm == 128 && p.bn == 128) {
+    if (w4) CF_LAUNCH(MODE, 128, 128, 2, 2, 32);
+    else CF_LAUNCH(MODE, 128, 128, 2, 4, 32);
+  } else if (p.bm == 128) {
+    CF_LAUNCH(MODE, 128, 64, 4, 2, 32);
+  } else if (p.bn == 128) {
+    CF_LAUNCH(MODE, 64, 128, 2, 4, 32);
+  } else {
+    CF_LAUNCH(MODE, 64, 64, 4, 2, 16);
+  }
   EW_CHECK_LAUNCH();
   if (p.split > 1) {
     const int M = geo.M, Nc = geo.Ncol;

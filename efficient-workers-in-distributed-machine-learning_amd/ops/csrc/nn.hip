@@ -236,19 +236,51 @@ __device__ __forceinline__ double ew_wave_sum_d(double v) {
   return v;
 }
 
-// one wave per channel: sum the nblk partials of nsum quantities in a fixed order
+// Sum the nblk partial rows of NS quantities per channel in a fixed order.  Block = 16 channels
+// (t & 15) x 16 row slices (t >> 4): a wave's load covers 4 rows x 16 consecutive channels (64-B
+// segments, not one channel per lane -- the channel-strided form was 5-10 us per call), each
+// thread keeps 4 rows of every quantity in flight, slices are combined through LDS in order.
+// Returns true (for the 16 threads of slice 0, c < C) with out[] holding the channel's sums.
+constexpr int EW_FIN_CH = 16;
 template <int NS>
-__device__ __forceinline__ void ew_sum_parts(const float* __restrict__ part, int nblk, int C,
-                                             int c, int lane, double out[NS]) {
+__device__ __forceinline__ bool ew_sum_parts(const float* __restrict__ part, int nblk, int C,
+                                             int c, double out[NS]) {
+  __shared__ double red[NS][EW_BLOCK];
+  const int t = threadIdx.x, rs = t / EW_FIN_CH;
+  constexpr int RS = EW_BLOCK / EW_FIN_CH;  // row slices
   double acc[NS];
 #pragma unroll
   for (int s = 0; s < NS; ++s) acc[s] = 0.0;
-  for (int b = lane; b < nblk; b += 64) {
+  if (c < C) {
+    int b = rs;
+    for (; b + 3 * RS < nblk; b += 4 * RS) {
+      float v[NS][4];
 #pragma unroll
-    for (int s = 0; s < NS; ++s) acc[s] += (double)part[((long long)s * nblk + b) * C + c];
+      for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[s][u] = part[((long long)s * nblk + b + u * RS) * C + c];
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc[s] += (double)v[s][u];
+    }
+    for (; b < nblk; b += RS) {
+#pragma unroll
+      for (int s = 0; s < NS; ++s) acc[s] += (double)part[((long long)s * nblk + b) * C + c];
+    }
   }
 #pragma unroll
-  for (int s = 0; s < NS; ++s) out[s] = ew_wave_sum_d(acc[s]);
+  for (int s = 0; s < NS; ++s) red[s][t] = acc[s];
+  __syncthreads();
+  if (rs != 0 || c >= C) return false;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    double a = 0.0;
+#pragma unroll
+    for (int r = 0; r < RS; ++r) a += red[s][r * EW_FIN_CH + t];
+    out[s] = a;
+  }
+  return true;
 }
 
 __global__ __launch_bounds__(EW_BLOCK) void k_bn_fwd_finalize(
@@ -256,12 +288,9 @@ __global__ __launch_bounds__(EW_BLOCK) void k_bn_fwd_finalize(
     const float* __restrict__ beta, const void* __restrict__ cbias, int cb_bf16,
     float* __restrict__ rmean, float* __restrict__ rvar, const long long* __restrict__ nbt,
     float momentum, float eps, float* __restrict__ stats) {
-  const int c = blockIdx.x * EW_WAVES + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (c >= C) return;
+  const int c = blockIdx.x * EW_FIN_CH + (threadIdx.x % EW_FIN_CH);
   double sums[2];
-  ew_sum_parts<2>(part, nblk, C, c, lane, sums);
-  if (lane != 0) return;
+  if (!ew_sum_parts<2>(part, nblk, C, c, sums)) return;
   const double mean = sums[0] / (double)M;
   double var = sums[1] / (double)M - mean * mean;
   if (var < 0.0) var = 0.0;
@@ -485,13 +514,10 @@ __global__ __launch_bounds__(EW_BLOCK) void k_bn_bwd_finalize(
     const float* __restrict__ part, int nblk, int C, long long M, const float* __restrict__ stats,
     float* __restrict__ coef, float* __restrict__ dgamma, float* __restrict__ dbeta,
     void* __restrict__ dcbias, int cb_bf16) {
-  const int c = blockIdx.x * EW_WAVES + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (c >= C) return;
+  const int c = blockIdx.x * EW_FIN_CH + (threadIdx.x % EW_FIN_CH);
   double sums[3];
-  ew_sum_parts<NS>(part, nblk, C, c, lane, sums);
+  if (!ew_sum_parts<NS>(part, nblk, C, c, sums)) return;
   if (NS == 2) sums[2] = 0.0;
-  if (lane != 0) return;
   const double invstd = stats[C + c], scale = stats[2 * C + c];
   const double db = sums[0];             // sum dz
   const double dg = sums[1] * invstd;    // sum dz * xhat
@@ -717,7 +743,7 @@ void ew_bn_relu_fwd(const BnFwdArgs& a) {
       hipLaunchKernelGGL(k_bn_fwd_stats<float>, dim3(nblk), dim3(EW_BLOCK), 0, s,
                          reinterpret_cast<const float*>(a.h), M, C, rpb, part);
     EW_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_bn_fwd_finalize, dim3((C + EW_WAVES - 1) / EW_WAVES), dim3(EW_BLOCK), 0,
+    hipLaunchKernelGGL(k_bn_fwd_finalize, dim3((C + EW_FIN_CH - 1) / EW_FIN_CH), dim3(EW_BLOCK), 0,
                        s, part, nblk, C, M, reinterpret_cast<const float*>(a.gamma),
                        reinterpret_cast<const float*>(a.beta),
                        reinterpret_cast<const void*>(a.cbias), a.cb_bf16,
@@ -773,7 +799,7 @@ static void ew_bn_bwd_impl(const BnBwdArgs& a) {
   const float* st = reinterpret_cast<const float*>(a.stats);
   float* coef = reinterpret_cast<float*>(a.coef);
   if (pre) {
-    hipLaunchKernelGGL(k_bn_bwd_finalize<2>, dim3((C + EW_WAVES - 1) / EW_WAVES), dim3(EW_BLOCK),
+    hipLaunchKernelGGL(k_bn_bwd_finalize<2>, dim3((C + EW_FIN_CH - 1) / EW_FIN_CH), dim3(EW_BLOCK),
                        0, s, part, a.pre_nblk, C, M, st, coef, reinterpret_cast<float*>(a.dgamma),
                        reinterpret_cast<float*>(a.dbeta), reinterpret_cast<void*>(a.dcbias),
                        a.cb_bf16);
@@ -781,7 +807,7 @@ static void ew_bn_bwd_impl(const BnBwdArgs& a) {
     hipLaunchKernelGGL((k_bn_bwd_stats<T, MODE>), dim3(nblk), dim3(EW_BLOCK), 0, s, h, res, dy,
                        code, st, rows, C, Ho, Wo, rpb, part);
     EW_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_bn_bwd_finalize<3>, dim3((C + EW_WAVES - 1) / EW_WAVES), dim3(EW_BLOCK),
+    hipLaunchKernelGGL(k_bn_bwd_finalize<3>, dim3((C + EW_FIN_CH - 1) / EW_FIN_CH), dim3(EW_BLOCK),
                        0, s, part, nblk, C, M, st, coef, reinterpret_cast<float*>(a.dgamma),
                        reinterpret_cast<float*>(a.dbeta), reinterpret_cast<void*>(a.dcbias),
                        a.cb_bf16);

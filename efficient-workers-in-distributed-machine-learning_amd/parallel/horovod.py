@@ -89,17 +89,38 @@ def broadcast_parameters(params, root_rank: int = 0):
 
 
 def broadcast_optimizer_state(optimizer, root_rank: int = 0):
+    """Every rank ends with the root's optimizer state and hyper-parameters.  State the root has
+    but a rank has not created yet (a fresh optimizer has empty ``state``) is first allocated
+    from the root's description, so every rank issues the same sequence of broadcasts."""
     c = _comm()
     if c.world == 1:
         return
     inner = getattr(optimizer, "optimizer", optimizer)
-    for group in inner.param_groups:
-        for p in group["params"]:
+    params = [p for g in inner.param_groups for p in g["params"]]
+    spec = None
+    if c.rank == root_rank:
+        spec = []
+        for p in params:
             st = inner.state.get(p, {})
-            for v in st.values():
-                if torch.is_tensor(v) and v.numel() > 0:
-                    c.broadcast(v.data if v.device.type != "cpu" or c.backend == "gloo" else v,
-                                src=root_rank)
+            spec.append([(k, tuple(v.shape), str(v.dtype), v.device.type)
+                         for k, v in sorted(st.items()) if torch.is_tensor(v)])
+    spec = c.broadcast_object(spec, src=root_rank)
+    for p, entries in zip(params, spec):
+        st = inner.state.setdefault(p, {})
+        for k, shape, dt, devtype in entries:
+            v = st.get(k)
+            if not (torch.is_tensor(v) and tuple(v.shape) == tuple(shape)):
+                dtype = getattr(torch, dt.replace("torch.", ""))
+                v = torch.zeros(shape, dtype=dtype, device=p.device if devtype != "cpu" else "cpu")
+                st[k] = v
+            if v.numel() == 0:
+                continue
+            if v.device.type == "cpu" and c.backend not in ("gloo", "local"):
+                t = v.to(p.device)  # RCCL broadcasts device memory only
+                c.broadcast(t, src=root_rank)
+                v.copy_(t.cpu())
+            else:
+                c.broadcast(v.data, src=root_rank)
     hp = c.broadcast_object([{k: v for k, v in g.items() if k != "params"}
                              for g in inner.param_groups], src=root_rank)
     for g, h in zip(inner.param_groups, hp):
@@ -183,7 +204,6 @@ class _DistributedOptimizer:
         self.exchange = GradientExchange(self.flat, self.comm, codec, _OptAdapter(),
                                          overlap=(self.bpps == 1 and op != Adasum),
                                          predivide=gradient_predivide_factor)
-        self._passes = 0
         self._synced = False
         self.exchange.begin()
 
@@ -217,9 +237,9 @@ class _DistributedOptimizer:
         self._synced = True
 
     def step(self, closure=None):
-        self._passes += 1
-        if self._passes % self.bpps:
-            return None
+        """Reduce the gradients accumulated over the preceding ``backward_passes_per_step``
+        backward passes (autograd sums them in place) and apply the wrapped optimizer, as
+        Horovod's ``backward_passes_per_step`` prescribes: N backward passes, then one step."""
         self.synchronize()
         out = self.optimizer.step(closure) if closure is not None else self.optimizer.step()
         self._synced = False

@@ -13,7 +13,10 @@ Modes:
     since the last sync with the wrapped exchange's codec, the deltas are averaged and added to the
     common anchor (compressed model averaging).
 ``select_best`` then broadcasts the weights (and BN statistics) of the best rank, measured on a
-fixed held-out batch.  Those bytes are counted (the report's 1.48 MB figure omits them).
+fixed held-out batch.  Those bytes are counted (the report's 1.48 MB figure omits them).  In
+``grad`` mode without ``select_best`` the replicas have drifted apart over the local steps and the
+same averaged gradient does not bring them back, so rank 0's weights are broadcast at every sync
+point (counted the same way; the reference's commented code never re-synchronised).
 """
 import torch
 
@@ -58,11 +61,17 @@ class LocalSGDExchange:
         stats = StepStats()
         if sync:
             stats = self.inner.bytes_per_step()
+            src = None
             if self.select_best and self.comm.world > 1:
                 self._adopt_best()
+                src = self.best_rank_history[-1]
+            elif self.mode == "grad" and self.comm.world > 1:
+                self._adopt(0)  # re-converge the drifted replicas on rank 0's weights
+                src = 0
+            if src is not None:
                 n = self.flat.numel * 4
-                stats.wire_bytes_sent += n if self.comm.rank == self.best_rank_history[-1] else 0
-                stats.wire_bytes_recv += 0 if self.comm.rank == self.best_rank_history[-1] else n
+                stats.wire_bytes_sent += n if self.comm.rank == src else 0
+                stats.wire_bytes_recv += 0 if self.comm.rank == src else n
         self.last = stats
         self.step_idx += 1
 
@@ -71,8 +80,13 @@ class LocalSGDExchange:
         scores = self.comm.all_gather_object(score)
         best = max(range(len(scores)), key=lambda r: (scores[r], -r))
         self.best_rank_history.append(best)
-        self.comm.broadcast(self.flat.data, src=best)
-        sync_buffers(self.flat.model, self.comm, src=best)
+        self._adopt(best)
+
+    def _adopt(self, src: int):
+        self.comm.broadcast(self.flat.data, src=src)
+        self.flat.sync_shadow()
+        if self.flat.model is not None:
+            sync_buffers(self.flat.model, self.comm, src=src)
         if self.anchor is not None:
             self.anchor.copy_(self.flat.data)
 

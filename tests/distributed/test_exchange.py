@@ -113,6 +113,14 @@ def test_method6_local_sgd_select_best(tmp_path):
     _same_params(res)  # after the step-6 sync everyone holds the best rank's weights
 
 
+def test_local_sgd_grad_mode_resyncs_replicas(tmp_path):
+    """grad mode without best-worker selection: local steps drift the replicas apart; every sync
+    point re-broadcasts rank 0's weights, so after a sync step all ranks hold the same model."""
+    res = run_world(_train, 2, tmp_path, args=(["--compress", "topk_qsgd", "--sync-every", "3",
+                                                "--sync-mode", "grad"], 6))
+    _same_params(res)
+
+
 def test_local_sgd_model_mode(tmp_path):
     res = run_world(_train, 2, tmp_path,
                     args=(["--compress", "topk_qsgd", "--topk-ratio", "0.2", "--sync-every", "2",
