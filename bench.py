@@ -186,7 +186,7 @@ def main(argv=None):
                    "bf16_params": tr.flat.shadow is not None,
                    "grad_mode": "views" if tr.flat.attach_grads else "pointers",
                    "layout": "nhwc" if tr.channels_last else "nchw",
-                   "fused_nn": a.fused_nn},
+                   "fused_nn": a.fused_nn, "comm": tr.comm.kind},
         # overlap that actually happens: more than one bucket (the first collective is issued
         # while backward still runs) and a collective to hide (world > 1)
         "overlap_effective": bool(nb > 1 and not a.no_overlap and world > 1),

@@ -263,6 +263,17 @@ PYBIND11_MODULE(_C, m) {
   m.def("head_fwd", &ew_head_fwd);
   m.def("head_bwd", &ew_head_bwd);
   m.def("conv_stem_wgrad", &ew_conv_stem_wgrad);
+  m.def("rccl_unique_id", [] { return pybind11::bytes(ew_rccl_unique_id()); });
+  m.def("rccl_version", &ew_rccl_version);
+  m.def("rccl_init", [](pybind11::bytes uid, int nranks, int rank, int device) {
+    return ew_rccl_init(std::string(uid), nranks, rank, device);
+  });
+  m.def("rccl_destroy", &ew_rccl_destroy);
+  m.def("rccl_all_gather", &ew_rccl_all_gather);
+  m.def("rccl_all_reduce", &ew_rccl_all_reduce);
+  m.def("rccl_reduce_scatter", &ew_rccl_reduce_scatter);
+  m.def("rccl_broadcast", &ew_rccl_broadcast);
+  m.def("rccl_all_to_all", &ew_rccl_all_to_all);
   m.def("conv_f32_fwd", &ew_conv_f32_fwd);
   m.def("conv_f32_bwd_data", &ew_conv_f32_bwd_data);
   m.def("conv_f32_wgrad", &ew_conv_f32_wgrad);

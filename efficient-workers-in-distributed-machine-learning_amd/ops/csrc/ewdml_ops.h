@@ -1,6 +1,7 @@
 // Host-side entry points of the ewdml HIP kernels (C++ only, no HIP types), bound to Python in
 // bindings.cpp.  Pointers are device addresses passed as integers; `stream` is a hipStream_t.
 #pragma once
+#include <string>
 #include <stddef.h>
 #include <stdint.h>
 
@@ -200,6 +201,23 @@ int ew_conv_f32_stem_fwd(uintptr_t x, uintptr_t w, uintptr_t y, long long N, int
 void ew_conv_f32_stem_wgrad(uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws,
                             long long ws_floats, long long N, int H, int W, int Nc,
                             uintptr_t stream);
+
+// ---- RCCL communicator issuing collectives on the caller's stream (rccl_comm.hip) ----
+// dtype codes: 0 f32, 1 bf16, 2 f16, 3 u8, 4 i32, 5 f64, 6 i64; op: 0 sum, 1 max, 2 min, 3 avg
+std::string ew_rccl_unique_id();
+int ew_rccl_version();
+uintptr_t ew_rccl_init(const std::string& uid, int nranks, int rank, int device);
+void ew_rccl_destroy(uintptr_t h);
+void ew_rccl_all_gather(uintptr_t h, uintptr_t send, uintptr_t recv, long long count, int dtype,
+                        uintptr_t stream);
+void ew_rccl_all_reduce(uintptr_t h, uintptr_t send, uintptr_t recv, long long count, int dtype,
+                        int op, uintptr_t stream);
+void ew_rccl_reduce_scatter(uintptr_t h, uintptr_t send, uintptr_t recv, long long count,
+                            int dtype, int op, uintptr_t stream);
+void ew_rccl_broadcast(uintptr_t h, uintptr_t send, uintptr_t recv, long long count, int dtype,
+                       int root, uintptr_t stream);
+void ew_rccl_all_to_all(uintptr_t h, uintptr_t send, uintptr_t recv, long long count, int dtype,
+                        int nranks, uintptr_t stream);
 
 // ---- cross-entropy loss (nn.hip): mean over B rows of [B, K] logits (bf16 or fp32), int64 labels
 void ew_cross_entropy_fwd(uintptr_t x, uintptr_t y, int B, int K, int is_bf16, uintptr_t loss,

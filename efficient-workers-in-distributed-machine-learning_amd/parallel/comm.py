@@ -1,9 +1,15 @@
 """Thin communicator over ``torch.distributed``.
 
-On the GPU the process group is ``nccl``, which on ROCm *is* RCCL: every collective runs on RCCL's
-internal HIP stream over xGMI peer links, ordered after the work already queued on the caller's
-current stream.  On the CPU it is ``gloo`` (tests, ``BASELINE.json`` config #1).  A world of one
-process needs no process group at all: collectives degenerate to local copies.
+On the GPU the process group is ``nccl``, which on ROCm *is* RCCL.  The data-plane collectives of
+the training step (all-gather of packed payloads, all-reduce of dense buckets, broadcast,
+all-to-all) go through a communicator of our own (``ops/csrc/rccl_comm.hip``): RCCL over xGMI,
+enqueued on the caller's current HIP stream, so a captured step stays one linear graph (no fork into
+the process group's private stream, no watchdog polling during capture).  ``EWDML_COMM=pg`` keeps
+them on the process group instead (A/B; also the fallback if the communicator cannot be created).
+Control-plane calls (barrier, scalar/object collectives, the parameter server's point-to-point
+messages) stay on the process group.  On the CPU it is ``gloo`` (tests, ``BASELINE.json`` config
+#1).  A world of one process needs no process group at all: collectives degenerate to local
+copies.
 
 Parity: replaces the reference's per-layer ``dist.gather`` / ``dist.broadcast`` call sites
 (``distributed_worker.py:256,278,350``, ``sync_replicas_master_nn.py:212,223``) and Horovod's
@@ -50,6 +56,50 @@ class Comm:
         # graph capture of collectives on a single-GPU box)
         self._local = self.world == 1 and not (os.environ.get("EWDML_FORCE_PG") == "1"
                                                and self.backend != "local")
+        self.rccl = None  # handle of the stream-ordered RCCL communicator (see module doc)
+        if (self.backend == "nccl" and not self._local and group is None
+                and os.environ.get("EWDML_COMM", "rccl") != "pg"):
+            self.rccl = self._make_rccl()
+
+    def _make_rccl(self):
+        """Create the RCCL communicator (collective over the process group: rank 0's unique id
+        is broadcast as an object).  Every rank must end up with one or none alike."""
+        try:
+            from .. import ops
+
+            C = ops.require()
+            uid = C.rccl_unique_id() if self.rank == 0 else None
+            uid = self.broadcast_object(uid, src=0)
+            h = C.rccl_init(uid, self.world, self.rank, torch.cuda.current_device())
+            ok = 1.0
+        except Exception as e:  # noqa: BLE001 - fall back to the process group everywhere
+            import logging
+
+            logging.getLogger("ewdml").warning(f"RCCL communicator unavailable ({e!r}); "
+                                               "collectives stay on the process group")
+            h, ok = None, 0.0
+        if self.all_reduce_scalars([ok], op="min")[0] < 1.0:
+            if h is not None:
+                ops.require().rccl_destroy(h)
+            return None
+        return h
+
+    def _rc(self):
+        from .. import ops
+
+        return ops.require()
+
+    @staticmethod
+    def _dt(t):
+        return _RC_DT[t.dtype]
+
+    @property
+    def kind(self) -> str:
+        """Where the step's data-plane collectives run: ``rccl-stream`` (own communicator on the
+        caller's stream), ``process-group`` (torch.distributed), or ``local`` (world of one)."""
+        if self._local:
+            return "local"
+        return "rccl-stream" if self.rccl is not None else "process-group"
 
     @property
     def distributed(self) -> bool:
@@ -63,6 +113,12 @@ class Comm:
             if inp.data_ptr() != out.data_ptr():
                 out[:inp.numel()].copy_(inp)
             return None
+        if self.rccl is not None and out.is_cuda:
+            from ..ops import _ptr, _stream
+
+            self._rc().rccl_all_gather(self.rccl, _ptr(inp), _ptr(out), inp.numel(),
+                                       self._dt(inp), _stream())
+            return None
         if self._gloo_ag:
             chunks = list(out.view(self.world, -1).unbind(0))
             if inp.data_ptr() == chunks[self.rank].data_ptr():
@@ -73,10 +129,22 @@ class Comm:
     def all_reduce(self, t: torch.Tensor, op=dist.ReduceOp.SUM, async_op: bool = False):
         if self._local:
             return None
+        if self.rccl is not None and t.is_cuda and op in _RC_OP:
+            from ..ops import _ptr, _stream
+
+            self._rc().rccl_all_reduce(self.rccl, _ptr(t), _ptr(t), t.numel(), self._dt(t),
+                                       _RC_OP[op], _stream())
+            return None
         return dist.all_reduce(t, op=op, group=self.group, async_op=async_op)
 
     def broadcast(self, t: torch.Tensor, src: int = 0, async_op: bool = False):
         if self.world == 1:
+            return None
+        if self.rccl is not None and t.is_cuda and t.is_contiguous():
+            from ..ops import _ptr, _stream
+
+            self._rc().rccl_broadcast(self.rccl, _ptr(t), _ptr(t), t.numel(), self._dt(t), src,
+                                      _stream())
             return None
         return dist.broadcast(t, src=src, group=self.group, async_op=async_op)
 
@@ -104,6 +172,12 @@ class Comm:
     def all_to_all(self, out: torch.Tensor, inp: torch.Tensor):
         if self.world == 1:
             out.copy_(inp)
+            return
+        if self.rccl is not None and out.is_cuda:
+            from ..ops import _ptr, _stream
+
+            self._rc().rccl_all_to_all(self.rccl, _ptr(inp), _ptr(out), inp.numel() // self.world,
+                                       self._dt(inp), self.world, _stream())
             return
         dist.all_to_all_single(out, inp, group=self.group)
 
@@ -138,6 +212,11 @@ class Comm:
         lst = [obj]
         dist.broadcast_object_list(lst, src=src, group=self.group)
         return lst[0]
+
+
+_RC_DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2, torch.uint8: 3,
+          torch.int8: 3, torch.int32: 4, torch.float64: 5, torch.int64: 6}
+_RC_OP = {dist.ReduceOp.SUM: 0, dist.ReduceOp.MAX: 1, dist.ReduceOp.MIN: 2}
 
 
 def shutdown():

@@ -185,6 +185,40 @@ def _free_port():
         return s.getsockname()[1]
 
 
+def _bench_pg(codec, comm, extra=()):
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    env = dict(os.environ, EWDML_FORCE_PG="1", EWDML_COMM=comm)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py",
+           "--gpus", "1", "--steps", "4", "--warmup", "4", "--batch-size", "64",
+           "--compress", codec, "--no-extras", *extra]
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=300)
+    if r.returncode != 0:
+        errs = [ln for ln in r.stderr.splitlines()
+                if ("rror" in ln or "what()" in ln or "Watchdog" in ln) and "frame #" not in ln]
+        raise AssertionError("bench failed (rc %d):\n%s\n--- stdout tail:\n%s"
+                             % (r.returncode, "\n".join(errs[:30]), r.stdout[-1500:]))
+    return json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+
+
+@pytest.mark.parametrize("codec", ["topk_qsgd", "none"])
+def test_own_rccl_communicator_matches_process_group(codec):
+    """The stream-ordered RCCL communicator (ops/csrc/rccl_comm.hip) in a world of one
+    (EWDML_FORCE_PG=1): the step graph captures its collectives, and the training trajectory is
+    bit-identical to the same run with the collectives on the process group."""
+    own = _bench_pg(codec, "rccl")
+    pg = _bench_pg(codec, "pg")
+    assert own["config"]["comm"] == "rccl-stream" and pg["config"]["comm"] == "process-group"
+    assert own["config"]["hip_graph"] == "full" and pg["config"]["hip_graph"] == "full"
+    assert own["final_loss"] == pg["final_loss"]
+    assert own["payload_bytes_per_rank"] == pg["payload_bytes_per_rank"]
+
+
 @pytest.mark.parametrize("codec", ["topk_qsgd", "none"])
 def test_bench_through_rccl_process_group(codec):
     """bench.py under torch.distributed.run with a real RCCL communicator (world of one,
@@ -201,7 +235,7 @@ def test_bench_through_rccl_process_group(codec):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py",
            "--gpus", "1", "--steps", "4", "--warmup", "4", "--batch-size", "64",
-           "--compress", codec]
+           "--compress", codec, "--no-extras"]
     r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=300)
     if r.returncode != 0:
         errs = [ln for ln in r.stderr.splitlines()
@@ -210,6 +244,7 @@ def test_bench_through_rccl_process_group(codec):
                              % (r.returncode, "\n".join(errs[:30]), r.stdout[-1500:]))
     rec = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     assert rec["config"]["hip_graph"] == "full"  # the capture of the RCCL collective succeeded
+    assert rec["config"]["comm"] == "rccl-stream"
     assert rec["value"] > 0 and rec["n_gpus"] == 1
     assert rec["final_loss"] == rec["final_loss"]  # not NaN
 
