@@ -94,6 +94,9 @@ class Config:
 
     data_dir: Optional[str] = None  # None -> synthetic data of the dataset's shape
     synthetic_size: int = 0
+    # > 0: train on the test split minus its last N samples and evaluate on those N (for data
+    # directories that hold only a test split, e.g. the reference's MNIST t10k files)
+    holdout_from_test: int = 0
     augment: bool = True
     # ---- checkpoint / metrics / faults -----------------------------------------------------------
     ckpt_dir: Optional[str] = None  # defaults to train_dir
@@ -208,6 +211,7 @@ def build_parser(prog="distributed_nn.py") -> argparse.ArgumentParser:
     a("--hip-graph", type=str, default=d.hip_graph, choices=["off", "split", "full"])
     a("--graph-warmup", type=int, default=d.graph_warmup)
     a("--data-dir", type=str, default=None)
+    a("--holdout-from-test", type=int, default=d.holdout_from_test)
     a("--synthetic-size", type=int, default=0)
     a("--no-augment", dest="augment", action="store_false", default=True)
     # checkpoint / metrics / faults

@@ -7,7 +7,9 @@ Per step (``begin`` -> ``loss.backward()`` -> ``finish``):
    codec's encode kernels and issues the bucket's collective (RCCL all-gather of the packed
    payloads, or all-reduce for dense codecs).  Backward of the earlier layers keeps running on the
    compute stream meanwhile -- the overlap that the reference only prototyped with per-layer MPI
-   ``Isend`` in ``LeNetSplit.backward_normal`` (``model_ops/lenet.py:111-186``).
+   ``Isend`` in ``LeNetSplit.backward_normal`` (``model_ops/lenet.py:111-186``).  Captured steps
+   (``side_stream=False``) issue the same work at the same point on the compute stream: a fork
+   would turn the step graph into a DAG, which ROCm replays node by node from the host.
 2. ``finish`` makes the compute stream wait for every collective, then per bucket runs ONE fused
    kernel: decode all N payloads in rank order -> scale 1/N -> SGD update of that bucket's
    parameters (``Codec.decode_apply_sgd``).  Dense codecs get one flat SGD kernel.
@@ -40,7 +42,8 @@ class GradientExchange:
     """All-to-all exchange: all-reduce for dense codecs, all-gather of payloads otherwise."""
 
     def __init__(self, flat, comm, codec, optimizer, overlap: bool = True,
-                 error_feedback: bool = False, predivide: float = 1.0, seed_offset: int = 0):
+                 error_feedback: bool = False, predivide: float = 1.0, seed_offset: int = 0,
+                 side_stream: bool = True):
         self.flat, self.comm, self.codec, self.opt = flat, comm, codec, optimizer
         self.device = flat.data.device
         self.cuda = self.device.type == "cuda"
@@ -71,7 +74,10 @@ class GradientExchange:
         self._pack_plans = [ops.DevicePlan(b.plan, self.device) for b in flat.buckets] \
             if (codec.allreduce and not flat.attach_grads) else None
         self.overlap = overlap
-        self.side = torch.cuda.Stream(device=self.device) if (self.cuda and overlap) else None
+        # overlap without side_stream: each bucket is still encoded and exchanged as soon as its
+        # gradients exist (interleaved with the rest of backward), in the compute stream's order
+        self.side = torch.cuda.Stream(device=self.device) \
+            if (self.cuda and overlap and side_stream) else None
         self._bucket_of = flat.bucket_of()
         self._sizes = [len(b.params) for b in flat.buckets]
         self._count = [0] * self.nb

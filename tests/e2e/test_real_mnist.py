@@ -1,7 +1,7 @@
 """Accuracy on real data: the reference checkout ships the 10K MNIST *test* images
 (``data/MNIST/raw/t10k-images-idx3-ubyte.gz``).  LeNet is trained on 9K of them and scored on the
 held-out 1K, per codec.  The report's LeNet accuracies are 96.5-98 %; top-1 % without
-error feedback is expected a few points lower (the reference's Method 5 used K = 0.4)."""
+error feedback is expected a few points lower (the reference's Method 5 used K = 0.4, also tested)."""
 import os
 
 import pytest
@@ -22,11 +22,14 @@ pytestmark = [pytest.mark.slow,
                                  reason="reference MNIST test images not mounted")]
 
 
-@pytest.mark.parametrize("kind,ef,norm,floor", [("none", False, "max", 95.0),
-                                                ("topk_qsgd", False, "max", 90.0),
-                                                ("topk_qsgd", True, "max", 95.0),
-                                                ("qsgd", False, "l2", 95.0)])
-def test_lenet_real_mnist_holdout(kind, ef, norm, floor):
+# floors: the report's lowest LeNet accuracy (Method 5, 96.5 %) for every accuracy-preserving
+# configuration; top-1 % without error feedback (132x fewer bytes, no residual) loses ~3 points
+@pytest.mark.parametrize("kind,ef,norm,ratio,floor", [("none", False, "max", 0.01, 96.5),
+                                                      ("topk_qsgd", False, "max", 0.01, 93.0),
+                                                      ("topk_qsgd", True, "max", 0.01, 96.5),
+                                                      ("topk_qsgd", False, "l2", 0.4, 96.5),
+                                                      ("qsgd", False, "l2", 0.01, 96.5)])
+def test_lenet_real_mnist_holdout(kind, ef, norm, ratio, floor):
     torch.manual_seed(0)
     x, y = _mnist(ROOT, train=False)
     info = {"mean": DATASETS["mnist"][2], "std": DATASETS["mnist"][3]}
@@ -35,9 +38,9 @@ def test_lenet_real_mnist_holdout(kind, ef, norm, floor):
     m = build_model("LeNet")
     flat = FlatModel(m)
     opt = FlatSGD(flat, lr=0.01, momentum=0.9)
-    ex = GradientExchange(flat, Comm(), make_codec(kind, ratio=0.01, norm=norm), opt,
+    ex = GradientExchange(flat, Comm(), make_codec(kind, ratio=ratio, norm=norm), opt,
                           error_feedback=ef)
-    for _ in range(600):
+    for _ in range(1500):
         xb, yb = tr.next()
         flat.zero_grad()
         ex.begin()
