@@ -1,0 +1,179 @@
+"""Measured reproduction of the report's Methods 1-6 (``Report.zip:main.tex:80-119``).
+
+Every method runs the real ``Trainer`` on the reference's own data (the MNIST t10k images shipped
+in its checkout, ``tests/fixtures/mnist``: 9K train / 1K held out) in its own setup: one parameter
+server + two workers over Gloo (``src/run_pytorch_single.sh``), batch 64 per worker, SGD with
+momentum 0.9.  Methods 1-5 use ``--topology ps`` (1, 2 pull weights; 3-5 pull gradients); Method 6 is
+Method 5 with local SGD, a sync every 20 steps and best-worker selection, over two ranks (it has no
+server).  Top-k uses the report's K = 0.4 unless ``--ratio`` says otherwise.
+
+Measured per method (from the exchanges' byte counters, not from layouts):
+  * bytes per iteration = sum over the 2 workers of (bytes pushed + bytes pulled), averaged over
+    the run -- the report's "average communication cost per iteration" (BASELINE.md);
+  * held-out top-1 after the run, and the first evaluation step reaching --target.
+
+    python tools/methods_eval.py [--steps 1500] [--ratio 0.4] [--out RESULTS_methods.md]
+"""
+import argparse
+import json
+import os
+import socket
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+MNIST = os.path.join(ROOT, "tests", "fixtures", "mnist")
+MiB = float(1 << 20)
+PUBLISHED_MIB = [6.56, 4.1, 6.56, 1.64, 1.312, 0.066]  # LeNet, BASELINE.md / Comm Cost.png
+PUBLISHED_TOP1 = [98, 97, 97, 98, 96.5, 97]  # LeNet, Top1 Accuracy.png
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _flags(method, ratio, steps):
+    f = ["--network", "LeNet", "--dataset", "MNIST", "--data-dir", MNIST,
+         "--holdout-from-test", "1000", "--batch-size", "64", "--lr", "0.01", "--momentum", "0.9",
+         "--eval-freq", "0", "--quiet", "--device", "cpu", "--amp", "none", "--method",
+         str(method), "--topk-ratio", str(ratio), "--qsgd-norm", "l2", "--test-batch-size",
+         "1000", "--max-steps", str(steps), "--log-interval", "1000000"]
+    if method <= 5:
+        f += ["--topology", "ps"]
+    return f
+
+
+def _worker(rank, world, port, method, ratio, steps, every, target, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import torch
+
+    torch.set_num_threads(2)
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import ewdml
+        from ewdml.runtime import Trainer
+
+        torch.manual_seed(0)
+        tr = Trainer(ewdml.parse_args(_flags(method, ratio, steps)))
+        worker = not getattr(tr, "is_server", False)
+        sent = recv = 0
+        curve, reached = [], None
+        for s in range(1, steps + 1):
+            tr.train_step()
+            st = tr.exchange.last
+            sent += st.wire_bytes_sent
+            recv += st.wire_bytes_recv
+            if s % every == 0 or s == steps:
+                # every rank evaluates its replica (the server holds the model in PS methods)
+                top1 = tr.evaluate()["top1"]
+                curve.append((s, top1))
+                if reached is None and top1 >= target:
+                    reached = s
+        res = {"rank": rank, "worker": worker, "sent": sent, "recv": recv, "steps": steps,
+               "curve": curve, "reached": reached, "top1": curve[-1][1]}
+        with open(os.path.join(out, f"r{rank}.json"), "w") as f:
+            json.dump(res, f)
+    finally:
+        dist.destroy_process_group()
+
+
+def run_method(method, ratio, steps, every, target):
+    import torch.multiprocessing as mp
+
+    world = 3 if method <= 5 else 2
+    with tempfile.TemporaryDirectory() as out:
+        ctx = mp.start_processes(_worker, nprocs=world, join=False, start_method="spawn",
+                                 args=(world, _free_port(), method, ratio, steps, every, target,
+                                       out))
+        while not ctx.join(timeout=600):
+            pass
+        res = [json.load(open(os.path.join(out, f"r{r}.json"))) for r in range(world)]
+    workers = [r for r in res if r["worker"]]
+    per_iter = sum(r["sent"] + r["recv"] for r in workers) / steps
+    # the model is the server's in PS methods, every rank's (identical or best-adopted) otherwise
+    model = res[0] if method <= 5 else workers[0]
+    return {"method": method, "ratio": ratio, "steps": steps, "world": world,
+            "bytes_per_iter": per_iter, "MiB_per_iter": per_iter / MiB,
+            "top1": model["top1"], "reached": model["reached"], "curve": model["curve"]}
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=1500)
+    ap.add_argument("--ratio", type=float, default=0.4)
+    ap.add_argument("--every", type=int, default=100, help="evaluation interval (steps)")
+    ap.add_argument("--target", type=float, default=95.0, help="top-1 for steps-to-target")
+    ap.add_argument("--methods", default="1,2,3,4,5,6")
+    ap.add_argument("--out", default=None, help="write a markdown table here")
+    ap.add_argument("--json", default=None)
+    a = ap.parse_args(argv)
+    rows = []
+    for m in [int(v) for v in a.methods.split(",")]:
+        t0 = time.time()
+        r = run_method(m, a.ratio, a.steps, a.every, a.target)
+        r["wall_s"] = round(time.time() - t0, 1)
+        rows.append(r)
+        print(json.dumps({k: v for k, v in r.items() if k != "curve"}), flush=True)
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump(rows, f, indent=1)
+    if a.out:
+        from tools.methods_table import table
+
+        static = table("LeNet", a.ratio)
+        lines = [
+            "# Methods 1-6, measured (LeNet, real MNIST)",
+            "",
+            f"Generated by `python tools/methods_eval.py --steps {a.steps} --ratio {a.ratio} "
+            f"--out RESULTS_methods.md` on the CPU (Gloo).  Setup as the report's: one parameter "
+            "server + two workers (Methods 1-5, `--topology ps`), batch 64 per worker, SGD with "
+            "momentum 0.9, lr 0.01; Method 6 = Method 5 + local SGD (sync every 20 steps) + "
+            "best-worker selection on two ranks.  Data: the reference's MNIST t10k images "
+            "(`tests/fixtures/mnist`), 9,000 for training, the last 1,000 held out.  Top-k ratio "
+            f"K = {a.ratio} (the report's).  Bytes are the exchanges' measured wire counters: per "
+            "iteration, summed over the two workers, push + pull (the report's metric); the "
+            "static column is `tools/methods_table.py` from the packed layouts.  The report trained "
+            f"to convergence on 60K images; here {a.steps} steps on 9K, so accuracies are a "
+            "lower-bound comparison.",
+            "",
+            "| Method | measured MiB/iter | layout MiB/iter | published MiB | held-out top-1 % | "
+            f"published top-1 % | steps to {a.target:g} % |",
+            "|---|---|---|---|---|---|---|",
+        ]
+        for r in rows:
+            m = r["method"]
+            lines.append(f"| {m} | {r['MiB_per_iter']:.4f} | {static[m - 1]:.4f} | "
+                         f"{PUBLISHED_MIB[m - 1]} | {r['top1']:.1f} | {PUBLISHED_TOP1[m - 1]} | "
+                         f"{r['reached'] if r['reached'] else '-'} |")
+        lines += [
+            "",
+            "Notes on the byte column:",
+            "",
+            "* Methods 1-3: dense legs move the flat buffer, i.e. the parameters plus 16-float "
+            "alignment padding per tensor (864 B for LeNet), hence the 0.002-0.003 MiB over the "
+            "layout column.",
+            "* Method 5: top-k values travel as int8 QSGD codes with u16 chunk-local indices "
+            "(3 B per kept element); the report's 1.312 MB counts 1 B per value and 1 B per index "
+            "(0.8 D at K = 0.4, BASELINE.md), so ours is 1.5x that figure by construction.",
+            "* Method 6: besides Method 5's payload every 20 steps, the best worker's weights are "
+            "broadcast at each sync (`--select-best`), which the report's 0.066 MB leaves out.",
+            "",
+            "Accuracy curves (step: held-out top-1 %):", ""]
+        for r in rows:
+            lines.append(f"* Method {r['method']}: " +
+                         ", ".join(f"{s}: {v:.1f}" for s, v in r["curve"]))
+        with open(a.out, "w") as f:
+            f.write("\n".join(lines) + "\n")
+    return rows
+
+
+if __name__ == "__main__":
+    main()
