@@ -8,7 +8,10 @@ backward-data and backward-weight are hand-written MFMA implicit-GEMM kernels:
 * bf16 operands (``ops/csrc/conv.hip``, ``v_mfma_f32_16x16x32_bf16``): fp32 accumulation, bf16
   results, like MIOpen's bf16 convolutions;
 * fp32 operands (``ops/csrc/conv_f32.hip``, ``v_mfma_f32_16x16x4_f32``): exact fp32 products and
-  accumulation, fp32 results -- the reference's precision.
+  accumulation, fp32 results -- the reference's precision.  fp32 3x3 layers with at least
+  ``EWDML_WINO_MIN_C`` (default 128) input and output channels run forward and backward-data as
+  Winograd F(2x2, 3x3) (``ops/csrc/winograd_f32.hip``: 2.25x fewer MFMA FLOPs, fp32 transforms;
+  ``EWDML_WINOGRAD=0`` keeps the direct kernels); weight gradients stay direct.
 
 :func:`conv2d_module` dispatches an ``nn.Conv2d`` (VGG's and ResNet's stride-1 3x3 / 1x1 layers).
 Shapes the kernels do not take (C_in or C_out not a multiple of 64, NCHW, other
@@ -38,6 +41,37 @@ _BN_BWD = os.environ.get("EWDML_CONV_BN_BWD", "1") != "0"
 # the epilogue reads the extra operands with 2-byte loads in the MFMA output layout, which on
 # large maps costs more than the separate, vectorised statistics / add kernels it replaces
 _EPI_MAX = int(os.environ.get("EWDML_EPI_MAX", str(1 << 23)))
+
+
+# Winograd F(2x2, 3x3) for fp32 3x3 layers with min(C_in, C_out) >= _WINO_MIN_C (the deep layers,
+# where the GEMM outweighs the transforms' 4x-activation traffic: tools/conv_f32_probe.py --wino)
+_WINO = os.environ.get("EWDML_WINOGRAD", "1") != "0"
+_WINO_MIN_C = int(os.environ.get("EWDML_WINO_MIN_C", "128"))
+
+
+def set_winograd(on: bool, min_c: int = None):
+    global _WINO, _WINO_MIN_C
+    _WINO = bool(on)
+    if min_c is not None:
+        _WINO_MIN_C = int(min_c)
+
+
+def _pow2(v):
+    return v > 0 and v & (v - 1) == 0
+
+
+def wino_ok(x, w) -> bool:
+    """Whether the fp32 conv of ``x`` by ``w`` (already :func:`supported`) takes the Winograd
+    path: 3x3, even H and W, N*H*W/4 % 64 == 0, power-of-two channel counts in
+    [_WINO_MIN_C, 1024]."""
+    if not _WINO or x.dtype != torch.float32 or w.shape[-1] != 3:
+        return False
+    N, C, H, W = x.shape
+    Nc = w.shape[0]
+    t = N * (H // 2) * (W // 2)
+    return (H % 2 == 0 and W % 2 == 0 and t % 64 == 0 and _pow2(C) and _pow2(Nc)
+            and _WINO_MIN_C <= min(C, Nc) and max(C, Nc) <= 1024
+            and 16 * t * max(C, Nc) < 2 ** 31)
 
 
 def epilogue_fusion_ok(x) -> bool:
@@ -155,9 +189,20 @@ class _Conv(torch.autograd.Function):
         # BatchNorm partial sums of y from the epilogue (bounded by 2 rows per 64 output rows);
         # the following fused BN (ops/nn.py bn_act) skips its statistics pass when present
         part = torch.empty(_part_floats(N * H * W, Nc), dtype=torch.float32, device=x.device)
-        fwd = C_.conv_f32_fwd if x.dtype == torch.float32 else C_.conv_fwd
-        rows = fwd(_ptr(x), _ptr(w), _ptr(y), _ptr(ws), ws.numel(), N, H, W, C, Nc, k,
-                   _ptr(part), part.numel(), _stream())
+        ctx.wino = None
+        if wino_ok(x, w):
+            # transformed weight U[16][Nc][C], kept for the backward-data GEMMs (read flipped)
+            U = torch.empty(16 * Nc * C, dtype=torch.float32, device=x.device)
+            C_.wino_f32_weight(_ptr(w), _ptr(U), Nc, C, _stream())
+            t = N * (H // 2) * (W // 2)
+            buf = torch.empty(16 * t * (C + Nc), dtype=torch.float32, device=x.device)
+            rows = C_.wino_f32_fwd(_ptr(x), _ptr(U), _ptr(y), _ptr(buf), _ptr(buf) + 64 * t * C,
+                                   N, H, W, C, Nc, _ptr(part), part.numel(), _stream())
+            ctx.wino = U
+        else:
+            fwd = C_.conv_f32_fwd if x.dtype == torch.float32 else C_.conv_fwd
+            rows = fwd(_ptr(x), _ptr(w), _ptr(y), _ptr(ws), ws.numel(), N, H, W, C, Nc, k,
+                       _ptr(part), part.numel(), _stream())
         ctx.save_for_backward(x, w)
         ctx.bn_part = (part, rows) if rows > 0 else None
         ctx.bn_node = bn_node
@@ -189,6 +234,14 @@ class _Conv(torch.autograd.Function):
                                         and add.data_ptr() % 16 == 0):
                 add = add.contiguous(memory_format=torch.channels_last).to(x.dtype)
             link = _bn_bwd_link(node, x)
+            U, ctx.wino = ctx.wino, None
+            if U is not None:
+                t = N * (H // 2) * (W // 2)
+                buf = torch.empty(16 * t * (C + Nc), dtype=torch.float32, device=x.device)
+
+                def bwd_data(dy_, w_, dx_, ws_, wsn, *rest):  # same contract, Winograd
+                    return C_.wino_f32_bwd_data(dy_, _ptr(U), dx_, _ptr(buf),
+                                                _ptr(buf) + 64 * t * Nc, *rest[:5], *rest[6:])
             if link is None:
                 bwd_data(_ptr(dy), _ptr(w), _ptr(dx), _ptr(ws), ws.numel(), N, H, W, C, Nc, k, 0,
                          0, 0, 0, 0, 0, 0, _ptr(add), _stream())

@@ -279,6 +279,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_f32_wgrad", &ew_conv_f32_wgrad);
   m.def("conv_f32_stem_fwd", &ew_conv_f32_stem_fwd);
   m.def("conv_f32_stem_wgrad", &ew_conv_f32_stem_wgrad);
+  m.def("wino_f32_weight", &ew_wino_f32_weight);
+  m.def("wino_f32_fwd", &ew_wino_f32_fwd);
+  m.def("wino_f32_bwd_data", &ew_wino_f32_bwd_data);
   m.def("maxpool2_nhwc", &ew_maxpool2_nhwc);
   m.def("maxpool2_fwd", &ew_maxpool2_fwd);
   m.def("maxpool2_bwd", &ew_maxpool2_bwd);

@@ -32,6 +32,7 @@
 #include <cstdlib>
 
 #include "common.h"
+#include "conv_f32.h"
 #include "ewdml_ops.h"
 
 namespace {
@@ -48,26 +49,6 @@ __device__ __forceinline__ int cf_off(int r, int c) {  // byte offset of chunk c
   return r * 128 + ((c ^ ((r >> 1) & 7)) << 4);
 }
 
-// Backward-statistics operands of the BN(+ReLU)(+2x2 max pool)(+residual) layer whose output
-// gradient a backward-data launch produces (conv.hip CvBnBwd, fp32 tensors): the epilogue sums
-// dz = act'(h * scale + shift [+ res]) * dx and dz * (h - mean) per channel (the BN backward then
-// skips its statistics pass).
-struct CfBnBwd {
-  const float* h;       // BN input [rows (pre-pool)][C]; null: not requested
-  const float* res;     // residual input (BN + residual + ReLU) or null
-  const uint8_t* code;  // pool window codes [rows][C] (null: no pool)
-  const float* stats;   // [4][C]: mean, invstd, scale, shift
-  int relu;
-  int Ho, Wo;           // pooled map dims (pool)
-};
-
-__device__ __forceinline__ uint32_t cf_pool_row(uint32_t p, uint32_t HoWo, uint32_t Wo,
-                                                uint32_t q) {
-  const uint32_t n = p / HoWo, rem = p - n * HoWo;
-  const uint32_t ho = rem / Wo, wo = rem - ho * Wo;
-  return 4 * n * HoWo + 4 * ho * Wo + 2 * wo + (q >> 1) * (2 * Wo) + (q & 1);
-}
-
 struct CfGeom {
   int M;      // GEMM rows (fwd/bwd: pixels N*H*W; wgrad: output channels Nc)
   int Ncol;   // GEMM columns (fwd: Nc; bwd: C; wgrad: taps*C)
@@ -77,7 +58,19 @@ struct CfGeom {
   int Nc;     // fwd/wgrad: output channels; bwd: the reduction channels (forward's output)
   int taps;   // 9 or 1
   int ksteps, kps;
+  // batched GEMMs (Winograd: one per transform position): blockIdx.z = batch * nsplit + split,
+  // operand / output pointers advance by these strides (elements) per batch
+  int nsplit;
+  long long a_bs, b_bs, o_bs;
+  // B batch index = the 4x4 position (i, j) of the A batch with 0 <-> 3 swapped on both axes (the
+  // Winograd transform of the 180-degree-rotated kernel: G J = rows 0 and 3 of G exchanged)
+  int b_flip;
 };
+
+__device__ __forceinline__ int cf_flip4(int z) {  // (i, j) -> (p(i), p(j)), p: 0 <-> 3
+  const int i = z >> 2, j = z & 3;
+  return (((i == 0 || i == 3) ? 3 - i : i) << 2) | ((j == 0 || j == 3) ? 3 - j : j);
+}
 
 // Stage images: A then B, KC or RC by mode.
 template <int MODE, int BM, int BN>
@@ -474,7 +467,11 @@ __global__ __launch_bounds__(64 * WM * WN) void k_cf_gemm(const float* __restric
   const int t = threadIdx.x, lane = t & 63, wq = t >> 6;
   const int wm = wq / WN, wn = wq % WN;
   const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
-  const int kbeg = blockIdx.z * geo.kps;
+  const int zb = blockIdx.z / geo.nsplit, zs = blockIdx.z - zb * geo.nsplit;
+  a_src += zb * geo.a_bs;
+  b_src += (geo.b_flip ? cf_flip4(zb) : zb) * geo.b_bs;
+  out += zb * geo.o_bs;
+  const int kbeg = zs * geo.kps;
   const int kend = min(kbeg + geo.kps, geo.ksteps);
   CfStager<MODE, BM, BN, NT> st;
   st.init(geo, a_src, b_src, t, m0, n0);
@@ -828,14 +825,16 @@ __global__ __launch_bounds__(EW_BLOCK) void k_cf_stem_reduce(const float* __rest
 struct CfPlan {
   int bm, bn, split, kps;
 };
-CfPlan cf_plan(int M, int Ncol, int ksteps, long long ws_floats, bool allow_split) {
+// batch > 1: that many independent GEMMs share the grid (blockIdx.z), no split-K
+CfPlan cf_plan(int M, int Ncol, int ksteps, long long ws_floats, int batch) {
+  const bool allow_split = batch == 1;
   // EWDML_CF_PLAN="bm,bn,split": forced plan (measurement only; invalid shapes fall through)
   static const char* force = getenv("EWDML_CF_PLAN");
   if (force) {
     int bm = 0, bn = 0, sp = 0;
     if (sscanf(force, "%d,%d,%d", &bm, &bn, &sp) == 3 && (bm == 64 || bm == 128) &&
         (bn == 64 || bn == 128) && sp >= 1 && M % bm == 0 && Ncol % bn == 0 &&
-        (sp == 1 || (long long)sp * M * Ncol <= ws_floats)) {
+        (sp == 1 || (allow_split && (long long)sp * M * Ncol <= ws_floats))) {
       const int kps = (ksteps + sp - 1) / sp;
       return CfPlan{bm, bn, (ksteps + kps - 1) / kps, kps};
     }
@@ -847,7 +846,7 @@ CfPlan cf_plan(int M, int Ncol, int ksteps, long long ws_floats, bool allow_spli
   for (int sh = 0; sh < 4; ++sh) {
     const int bm = shapes[sh][0], bn = shapes[sh][1];
     if (M % bm || Ncol % bn) continue;
-    const long long tiles = (long long)(M / bm) * (Ncol / bn);
+    const long long tiles = (long long)(M / bm) * (Ncol / bn) * batch;
     const double step_us = (double)bm * bn * CF_BK * 2 / 614e3 / derate[sh];
     for (int split = 1; split <= (allow_split ? 64 : 1); ++split) {
       const int kps = (ksteps + split - 1) / split;
@@ -874,9 +873,11 @@ int cf_gemm(const float* a, const float* b, float* out, float* ws, long long ws_
             CfGeom geo, hipStream_t s, float* bnpart, long long bnpart_floats,
             const CfBnBwd* bnb, const float* addend) {
   ws_floats -= 64;  // the workspace's last 64 floats are conv.hip's zero page (never a slab)
-  const CfPlan p = cf_plan(geo.M, geo.Ncol, geo.ksteps, ws_floats, true);
+  const int batch = geo.nsplit;  // callers pass the batch count here (1: no batching)
+  const CfPlan p = cf_plan(geo.M, geo.Ncol, geo.ksteps, ws_floats, batch);
   geo.kps = p.kps;
-  dim3 grid(geo.M / p.bm, geo.Ncol / p.bn, p.split);
+  geo.nsplit = p.split;
+  dim3 grid(geo.M / p.bm, geo.Ncol / p.bn, p.split * batch);
   float* slab = p.split > 1 ? ws : nullptr;
   const long long prow = geo.M / p.bm;
   float* bnp = (bnpart && !slab && prow <= 1024 && 2 * prow * geo.Ncol <= bnpart_floats) ? bnpart
@@ -937,6 +938,27 @@ int cf_taps(int ksize) {
 // ------------------------------------------------------------------------------------------------
 // host side (shapes validated here: the kernels assume them)
 
+// out[b][M][N] = A[b][M][K] * B[b][N][K]^T for b < batch (row-major, K contiguous): the forward
+// GEMM as a 1x1 "convolution" over M pixels, batched over blockIdx.z (winograd_f32.hip).
+// out[z][M][N] = A[z][M][K] * op(B[z'])  for z < batch (row-major, K contiguous in A): the conv
+// GEMMs as 1x1 "convolutions" over M pixels, batched over blockIdx.z (winograd_f32.hip).
+// nt: B[z] is [N][K] (the forward's weight image); else B[z'] is [K][N] (backward data) with
+// z' = cf_flip4(z) when flip.
+void ew_cf_gemm_batched(const float* a, const float* b, float* out, int M, int N, int K, int batch,
+                        long long a_bs, long long b_bs, long long o_bs, bool nt, bool flip,
+                        hipStream_t s) {
+  if (M % 64 || N % 64 || K % CF_BK || (long long)M * std::max(N, K) >= (1LL << 31) ||
+      (flip && batch != 16))
+    throw std::runtime_error("ewdml gemm f32: needs M, N % 64 == 0, K % 32 == 0");
+  if (nt) {
+    CfGeom g{M, N, M, 1, 1, K, N, 1, K / CF_BK, 0, batch, a_bs, b_bs, o_bs, 0};
+    cf_gemm<CF_FWD>(a, b, out, nullptr, 64, g, s, nullptr, 0, nullptr, nullptr);
+  } else {
+    CfGeom g{M, N, M, 1, 1, N, K, 1, K / CF_BK, 0, batch, a_bs, b_bs, o_bs, flip ? 1 : 0};
+    cf_gemm<CF_BWD>(a, b, out, nullptr, 64, g, s, nullptr, 0, nullptr, nullptr);
+  }
+}
+
 int ew_conv_f32_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t ws, long long ws_floats,
                     long long N, int H, int W, int C, int Nc, int ksize, uintptr_t bnpart,
                     long long bnpart_floats, uintptr_t stream) {
@@ -944,7 +966,7 @@ int ew_conv_f32_fwd(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t ws, long lo
   if (C % CF_BK || Nc % 64 || P % 64 || P * (long long)std::max(C, Nc) >= (1LL << 31))
     throw std::runtime_error("ewdml conv f32: needs C % 32 == 0, Nc % 64 == 0, N*H*W % 64 == 0");
   const int taps = cf_taps(ksize);
-  CfGeom g{(int)P, Nc, (int)P, H, W, C, Nc, taps, taps * C / CF_BK, 0};
+  CfGeom g{(int)P, Nc, (int)P, H, W, C, Nc, taps, taps * C / CF_BK, 0, 1, 0, 0, 0};
   return cf_gemm<CF_FWD>(reinterpret_cast<const float*>(x), reinterpret_cast<const float*>(w),
                          reinterpret_cast<float*>(y), reinterpret_cast<float*>(ws), ws_floats, g,
                          (hipStream_t)stream, reinterpret_cast<float*>(bnpart), bnpart_floats,
@@ -960,7 +982,7 @@ int ew_conv_f32_bwd_data(uintptr_t dy, uintptr_t w, uintptr_t dx, uintptr_t ws,
   if (C % 64 || Nc % CF_BK || P % 64 || P * (long long)std::max(C, Nc) >= (1LL << 31))
     throw std::runtime_error("ewdml conv f32: bwd-data needs C % 64 == 0, Nc % 32 == 0");
   const int taps = cf_taps(ksize);
-  CfGeom g{(int)P, C, (int)P, H, W, C, Nc, taps, taps * Nc / CF_BK, 0};
+  CfGeom g{(int)P, C, (int)P, H, W, C, Nc, taps, taps * Nc / CF_BK, 0, 1, 0, 0, 0};
   const CfBnBwd bb{reinterpret_cast<const float*>(bn_h), reinterpret_cast<const float*>(bn_res),
                    reinterpret_cast<const uint8_t*>(bn_code),
                    reinterpret_cast<const float*>(bn_stats), bn_relu, H, W};
@@ -977,7 +999,7 @@ void ew_conv_f32_wgrad(uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws, lo
   const int taps = cf_taps(ksize);
   if (C % 64 || Nc % 64 || P % CF_BK || P * (long long)std::max(C, Nc) >= (1LL << 31))
     throw std::runtime_error("ewdml conv f32: wgrad needs C, Nc % 64 == 0, N*H*W % 32 == 0");
-  CfGeom g{Nc, taps * C, (int)P, H, W, C, Nc, taps, (int)(P / CF_BK), 0};
+  CfGeom g{Nc, taps * C, (int)P, H, W, C, Nc, taps, (int)(P / CF_BK), 0, 1, 0, 0, 0};
   cf_gemm<CF_WGRAD>(reinterpret_cast<const float*>(dy), reinterpret_cast<const float*>(x),
                     reinterpret_cast<float*>(dw), reinterpret_cast<float*>(ws), ws_floats, g,
                     (hipStream_t)stream, nullptr, 0, nullptr, nullptr);

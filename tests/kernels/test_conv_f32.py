@@ -1,5 +1,6 @@
-"""fp32 MFMA implicit-GEMM convolutions (ops/csrc/conv_f32.hip, v_mfma_f32_16x16x4_f32) against a
-float64 PyTorch reference on the CPU.
+"""fp32 MFMA implicit-GEMM convolutions (ops/csrc/conv_f32.hip, v_mfma_f32_16x16x4_f32) and the
+Winograd F(2x2, 3x3) path (ops/csrc/winograd_f32.hip) against a float64 PyTorch reference on the
+CPU.
 
 The kernels multiply and accumulate in fp32 with no reduced-precision operand step, so the
 relative error is a few fp32 ulps times the reduction length's growth: the bound used is 1e-5
@@ -17,13 +18,25 @@ pytestmark = pytest.mark.gpu
 TOL = 1e-5
 
 
-def _conv():
+def _conv(wino=False, min_c=64):
+    """The conv module with the Winograd path off (direct implicit GEMM for every shape) or on
+    for every layer with at least ``min_c`` channels."""
     from ewdml import ops
     from ewdml.ops import conv
 
     ops.require()
     conv.set_enabled(True)
+    conv.set_winograd(wino, min_c)
     return conv
+
+
+@pytest.fixture(autouse=True)
+def _restore_winograd():
+    from ewdml.ops import conv
+
+    saved = (conv._WINO, conv._WINO_MIN_C)
+    yield
+    conv.set_winograd(*saved)
 
 
 def _rel(a, b):
@@ -184,12 +197,120 @@ def test_conv_f32_bn_backward_sums_in_bwd_data_epilogue(mode, pool, N, HW):
         assert _rel(a, b) < 1e-5, _rel(a, b)
 
 
+WINO_SHAPES = [
+    (128, 128, 256, 8, 8),    # VGG conv3
+    (128, 256, 256, 8, 8),    # VGG conv4
+    (128, 512, 512, 4, 4),    # VGG conv6
+    (128, 512, 512, 2, 2),    # VGG conv8: one tile per image, mostly padding
+    (8, 64, 128, 16, 16),     # 64 input channels
+    (2, 128, 64, 8, 16),      # H != W, 64 output channels
+    (16, 1024, 128, 4, 4),    # wide input
+]
+
+
+@pytest.mark.parametrize("N,C,Nc,H,W", WINO_SHAPES)
+def test_conv_f32_winograd_forward_backward(N, C, Nc, H, W):
+    conv = _conv(wino=True)
+    x, w = _data(N, C, Nc, H, W, seed=31)
+    assert conv.supported(x, w) and conv.wino_ok(x, w)
+    g = torch.Generator(device="cuda").manual_seed(32)
+    dy = torch.randn(N, Nc, H, W, device="cuda", generator=g).contiguous(
+        memory_format=torch.channels_last)
+    xa, wa = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
+    y = conv.conv(xa, wa)
+    y.backward(dy)
+    ref, gx, gw = _ref64(x, w, 3, dy)
+    assert y.dtype == torch.float32 and y.is_contiguous(memory_format=torch.channels_last)
+    assert _rel(y, ref) < TOL, _rel(y, ref)
+    assert _rel(xa.grad, gx) < TOL, _rel(xa.grad, gx)
+    assert _rel(wa.grad, gw) < TOL, _rel(wa.grad, gw)
+    # bit-for-bit repeatable (fixed-order transforms, no split-K)
+    xb, wb = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
+    y2 = conv.conv(xb, wb)
+    y2.backward(dy)
+    assert torch.equal(y, y2) and torch.equal(xa.grad, xb.grad)
+    # and close to the direct kernels (both within rounding of float64)
+    d = _conv(wino=False)
+    assert not d.wino_ok(x, w)
+    assert _rel(d.conv(x, w), y) < 2 * TOL
+
+
+def test_conv_f32_winograd_only_where_chosen():
+    conv = _conv(wino=True, min_c=128)
+    x, w = _data(8, 64, 128, 16, 16)
+    assert not conv.wino_ok(x, w)  # 64 input channels < min_c
+    x, w = _data(8, 128, 128, 16, 16)
+    assert conv.wino_ok(x, w)
+    x, w = _data(8, 128, 128, 16, 16, k=1)
+    assert not conv.wino_ok(x, w)  # 1x1
+    x, w = _data(8, 128, 128, 8, 5)
+    assert not conv.wino_ok(x, w)  # odd width
+    x, w = _data(8, 192, 128, 8, 8)
+    assert not conv.wino_ok(x, w)  # C not a power of two
+
+
+@pytest.mark.parametrize("N,C,Nc,H,W", [(16, 128, 256, 8, 8), (128, 512, 512, 2, 2),
+                                        (32, 256, 512, 4, 4)])
+def test_conv_f32_winograd_bn_statistics(N, C, Nc, H, W):
+    """BatchNorm partial sums from the Winograd output transform give the BN kernels' own
+    statistics."""
+    from ewdml.ops import nn as fnn
+
+    conv = _conv(wino=True)
+    x, w = _data(N, C, Nc, H, W, seed=35)
+    assert conv.wino_ok(x, w)
+    bn0 = torch.nn.BatchNorm2d(Nc).cuda()
+    bn1 = copy.deepcopy(bn0)
+    h = conv.conv(x, w.clone().requires_grad_(True))
+    assert hasattr(h, "_ew_bn_part")
+    y0 = fnn.bn_act(h, bn0, "relu")
+    y1 = fnn.bn_act(h.detach().clone(), bn1, "relu")
+    assert _rel(y0, y1) < 1e-5
+    assert torch.allclose(bn0.running_mean, bn1.running_mean, rtol=1e-5, atol=1e-7)
+    assert torch.allclose(bn0.running_var, bn1.running_var, rtol=1e-5, atol=1e-7)
+
+
+@pytest.mark.parametrize("mode,pool", [("relu", True), ("relu", False), ("none", False)])
+def test_conv_f32_winograd_bn_backward_sums(mode, pool):
+    """The Winograd backward-data output transform produces the producing BN layer's backward
+    sums (and the BN backward then skips its statistics pass): same gradients as unfused."""
+    from ewdml.ops import nn as fnn
+
+    conv = _conv(wino=True)
+    N, HW = 32, 16
+    x0, w0 = _data(N, 128, 128, HW, HW, seed=41)
+    _, w1 = _data(8, 128, 128, 8, 8, seed=42)
+    bn0 = torch.nn.BatchNorm2d(128).cuda()
+    with torch.no_grad():
+        bn0.weight.uniform_(0.5, 1.5)
+        bn0.bias.uniform_(-0.3, 0.3)
+    g = None
+    grads = []
+    for fused in (True, False):
+        conv.set_bn_bwd_fusion(fused)
+        used = fnn.PRE_BWD_USED
+        bn = copy.deepcopy(bn0)
+        xa, wa, wb = (t.clone().requires_grad_(True) for t in (x0, w0, w1))
+        h = conv.conv(xa, wa)
+        y = fnn.bn_act(h, bn, mode, pool=pool)
+        assert conv.wino_ok(y, wb)
+        z = conv.conv(y, wb)
+        if g is None:
+            g = torch.randn(z.shape, device="cuda").contiguous(memory_format=torch.channels_last)
+        z.backward(g)
+        assert (fnn.PRE_BWD_USED > used) == fused
+        grads.append([xa.grad, wa.grad, wb.grad, bn.weight.grad, bn.bias.grad])
+    conv.set_bn_bwd_fusion(True)
+    for a, b in zip(*grads):
+        assert _rel(a, b) < 1e-5, _rel(a, b)
+
+
 def test_fp32_vgg11_step_vs_fp64():
     """One fp32 VGG-11-BN training step (fused NHWC path, fp32 MFMA convs) against the same step
     in float64 on the CPU, and no worse than the step through MIOpen's fp32 convolutions."""
     from ewdml.models import build_model
 
-    conv = _conv()
+    conv = _conv(wino=True, min_c=128)  # the production choice
     torch.manual_seed(0)
     m0 = build_model("vgg11", 10).to(memory_format=torch.channels_last)
     for mod in m0.modules():
@@ -225,7 +346,7 @@ def test_fp32_resnet18_step_convs_in_situ():
     from ewdml.models import build_model
     from ewdml.ops import conv as cmod
 
-    _conv()
+    _conv(wino=True, min_c=128)  # the production choice
     recs = []
     orig = cmod._Conv.backward
 

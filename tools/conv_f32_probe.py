@@ -1,7 +1,9 @@
 """Time the fp32 MFMA conv kernels per VGG-11 layer shape (forward, backward-data, weight
 gradient) with HIP events; prints us and TF/s per direction.
 
-    python tools/conv_f32_probe.py [--batch 128] [--reps 20] [--shapes vgg|big]
+    python tools/conv_f32_probe.py [--batch 128] [--reps 20] [--shapes vgg|big] [--wino]
+--wino adds the Winograd F(2x2, 3x3) forward (weight + input transforms, 16 GEMMs, output
+transform: "wfwd") and backward data ("wbwd") on the same shapes (TF/s counted at direct FLOPs).
 EWDML_CF_PLAN="bm,bn,split" forces a launch plan (ops/csrc/conv_f32.hip cf_plan).
 """
 import argparse
@@ -28,6 +30,7 @@ def main():
     a.add_argument("--shapes", default="vgg")
     a.add_argument("--dirs", default="fwd,bwd,wgrad")
     a.add_argument("--miopen", action="store_true", help="also time F.conv2d (MIOpen) forward")
+    a.add_argument("--wino", action="store_true", help="also time the Winograd path")
     args = a.parse_args()
     C_ = ops.require()
     dev = torch.device("cuda")
@@ -50,12 +53,24 @@ def main():
             "wgrad": lambda: C_.conv_f32_wgrad(_ptr(y), _ptr(x), _ptr(dw), _ptr(ws), ws.numel(), N,
                                                HW, HW, C, Nc, 3, _stream()),
         }
+        if args.wino:
+            t = N * (HW // 2) * (HW // 2)
+            U = torch.empty(16 * Nc * C, device=dev)
+            buf = torch.empty(16 * t * (C + Nc), device=dev)
+            calls["wfwd"] = lambda: (
+                C_.wino_f32_weight(_ptr(w), _ptr(U), Nc, C, _stream()),
+                C_.wino_f32_fwd(_ptr(x), _ptr(U), _ptr(y), _ptr(buf), _ptr(buf) + 64 * t * C, N,
+                                HW, HW, C, Nc, 0, 0, _stream()))
+            calls["wbwd"] = lambda: C_.wino_f32_bwd_data(
+                _ptr(y), _ptr(U), _ptr(dx), _ptr(buf), _ptr(buf) + 64 * t * Nc, N, HW, HW, C, Nc,
+                0, 0, 0, 0, 0, 0, 0, 0, _stream())
         if args.miopen:
             xm = x.permute(0, 3, 1, 2)  # NCHW view of NHWC memory: channels_last
             wm = w.permute(0, 3, 1, 2)
             calls["miopen_fwd"] = lambda: torch.nn.functional.conv2d(xm, wm, padding=1)
         line = f"C={C:4d} Nc={Nc:4d} HW={HW:3d}"
-        for d in args.dirs.split(",") + (["miopen_fwd"] if args.miopen else []):
+        extra = (["miopen_fwd"] if args.miopen else []) + (["wfwd", "wbwd"] if args.wino else [])
+        for d in args.dirs.split(",") + extra:
             f = calls[d]
             for _ in range(3):
                 f()
