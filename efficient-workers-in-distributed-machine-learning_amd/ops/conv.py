@@ -11,7 +11,8 @@ backward-data and backward-weight are hand-written MFMA implicit-GEMM kernels:
   accumulation, fp32 results -- the reference's precision.  fp32 3x3 layers with at least
   ``EWDML_WINO_MIN_C`` (default 128) input and output channels run forward and backward-data as
   Winograd F(2x2, 3x3) (``ops/csrc/winograd_f32.hip``: 2.25x fewer MFMA FLOPs, fp32 transforms;
-  ``EWDML_WINOGRAD=0`` keeps the direct kernels); weight gradients stay direct.
+  ``EWDML_WINOGRAD=0`` keeps the direct kernels) -- forward, backward data and weight gradient
+  (the forward's transformed input is kept for it).
 
 :func:`conv2d_module` dispatches an ``nn.Conv2d`` (VGG's and ResNet's stride-1 3x3 / 1x1 layers).
 Shapes the kernels do not take (C_in or C_out not a multiple of 64, NCHW, other
@@ -47,6 +48,8 @@ _EPI_MAX = int(os.environ.get("EWDML_EPI_MAX", str(1 << 23)))
 # where the GEMM outweighs the transforms' 4x-activation traffic: tools/conv_f32_probe.py --wino)
 _WINO = os.environ.get("EWDML_WINOGRAD", "1") != "0"
 _WINO_MIN_C = int(os.environ.get("EWDML_WINO_MIN_C", "128"))
+# most K-splits of a Winograd weight-gradient GEMM (slab memory: splits x 16 x C_out x C_in floats)
+_WINO_WG_SPLITS = int(os.environ.get("EWDML_WINO_WG_SPLITS", "4"))
 
 
 def set_winograd(on: bool, min_c: int = None):
@@ -195,10 +198,12 @@ class _Conv(torch.autograd.Function):
             U = torch.empty(16 * Nc * C, dtype=torch.float32, device=x.device)
             C_.wino_f32_weight(_ptr(w), _ptr(U), Nc, C, _stream())
             t = N * (H // 2) * (W // 2)
-            buf = torch.empty(16 * t * (C + Nc), dtype=torch.float32, device=x.device)
-            rows = C_.wino_f32_fwd(_ptr(x), _ptr(U), _ptr(y), _ptr(buf), _ptr(buf) + 64 * t * C,
-                                   N, H, W, C, Nc, _ptr(part), part.numel(), _stream())
-            ctx.wino = U
+            # V (the transformed input) is kept for the weight-gradient GEMMs
+            V = torch.empty(16 * t * C, dtype=torch.float32, device=x.device)
+            Mo = torch.empty(16 * t * Nc, dtype=torch.float32, device=x.device)
+            rows = C_.wino_f32_fwd(_ptr(x), _ptr(U), _ptr(y), _ptr(V), _ptr(Mo), N, H, W, C, Nc,
+                                   _ptr(part), part.numel(), _stream())
+            ctx.wino = (U, V)
         else:
             fwd = C_.conv_f32_fwd if x.dtype == torch.float32 else C_.conv_fwd
             rows = fwd(_ptr(x), _ptr(w), _ptr(y), _ptr(ws), ws.numel(), N, H, W, C, Nc, k,
@@ -234,7 +239,7 @@ class _Conv(torch.autograd.Function):
                                         and add.data_ptr() % 16 == 0):
                 add = add.contiguous(memory_format=torch.channels_last).to(x.dtype)
             link = _bn_bwd_link(node, x)
-            U, ctx.wino = ctx.wino, None
+            U = ctx.wino[0] if ctx.wino is not None else None
             if U is not None:
                 t = N * (H // 2) * (W // 2)
                 buf = torch.empty(16 * t * (C + Nc), dtype=torch.float32, device=x.device)
@@ -259,9 +264,21 @@ class _Conv(torch.autograd.Function):
                 sink.grad = None
         if ctx.needs_input_grad[1]:
             dw = torch.empty_like(w, memory_format=torch.channels_last)
-            wgrad = C_.conv_f32_wgrad if f32 else C_.conv_wgrad
-            wgrad(_ptr(dy), _ptr(x), _ptr(dw), _ptr(ws), ws.numel(), N, H, W, C, Nc, k,
-                  _stream())
+            if ctx.wino is not None:
+                # dw = G^T (sum over tiles of (A dy A^T) V) G: 16 GEMMs of K = N*H*W/4
+                V = ctx.wino[1]
+                t = N * (H // 2) * (W // 2)
+                D = torch.empty(16 * t * Nc, dtype=torch.float32, device=x.device)
+                dU = torch.empty(16 * Nc * C, dtype=torch.float32, device=x.device)
+                slabs = torch.empty(_WINO_WG_SPLITS * 16 * Nc * C + 64, dtype=torch.float32,
+                                    device=x.device)
+                C_.wino_f32_wgrad(_ptr(dy), _ptr(V), _ptr(dw), _ptr(D), _ptr(dU), _ptr(slabs),
+                                  slabs.numel(), N, H, W, C, Nc, _stream())
+            else:
+                wgrad = C_.conv_f32_wgrad if f32 else C_.conv_wgrad
+                wgrad(_ptr(dy), _ptr(x), _ptr(dw), _ptr(ws), ws.numel(), N, H, W, C, Nc, k,
+                      _stream())
+        ctx.wino = None
         return dx, dw, None, None
 
 

@@ -282,6 +282,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("wino_f32_weight", &ew_wino_f32_weight);
   m.def("wino_f32_fwd", &ew_wino_f32_fwd);
   m.def("wino_f32_bwd_data", &ew_wino_f32_bwd_data);
+  m.def("wino_f32_wgrad", &ew_wino_f32_wgrad);
   m.def("maxpool2_nhwc", &ew_maxpool2_nhwc);
   m.def("maxpool2_fwd", &ew_maxpool2_fwd);
   m.def("maxpool2_bwd", &ew_maxpool2_bwd);

@@ -332,7 +332,7 @@ __device__ __forceinline__ void cf_epilogue(typename CfMfma<SH>::acc_t (&acc)[MI
   auto row_of = [&](int i, int e) { return row0 + i * SH + F::out_row(lane, e); };
   auto col_of = [&](int j) { return col0 + j * SH + li; };
   if (slab) {
-    float* sp = slab + (long long)blockIdx.z * M * Nc;
+    float* sp = slab;  // this block's split slab (k_cf_gemm offsets it)
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -471,6 +471,8 @@ __global__ __launch_bounds__(64 * WM * WN) void k_cf_gemm(const float* __restric
   a_src += zb * geo.a_bs;
   b_src += (geo.b_flip ? cf_flip4(zb) : zb) * geo.b_bs;
   out += zb * geo.o_bs;
+  // slabs [split][batch][M][Ncol]: the reduction sums the splits of a contiguous batch run
+  if (slab) slab += (long long)(zs * (gridDim.z / geo.nsplit) + zb) * geo.M * geo.Ncol;
   const int kbeg = zs * geo.kps;
   const int kend = min(kbeg + geo.kps, geo.ksteps);
   CfStager<MODE, BM, BN, NT> st;
@@ -825,16 +827,17 @@ __global__ __launch_bounds__(EW_BLOCK) void k_cf_stem_reduce(const float* __rest
 struct CfPlan {
   int bm, bn, split, kps;
 };
-// batch > 1: that many independent GEMMs share the grid (blockIdx.z), no split-K
+// batch > 1: that many independent GEMMs share the grid (blockIdx.z); a split needs
+// split * batch * M * Ncol slab floats
 CfPlan cf_plan(int M, int Ncol, int ksteps, long long ws_floats, int batch) {
-  const bool allow_split = batch == 1;
+  const long long slab1 = (long long)batch * M * Ncol;  // slab floats per split
   // EWDML_CF_PLAN="bm,bn,split": forced plan (measurement only; invalid shapes fall through)
   static const char* force = getenv("EWDML_CF_PLAN");
   if (force) {
     int bm = 0, bn = 0, sp = 0;
     if (sscanf(force, "%d,%d,%d", &bm, &bn, &sp) == 3 && (bm == 64 || bm == 128) &&
         (bn == 64 || bn == 128) && sp >= 1 && M % bm == 0 && Ncol % bn == 0 &&
-        (sp == 1 || (allow_split && (long long)sp * M * Ncol <= ws_floats))) {
+        (sp == 1 || sp * slab1 <= ws_floats)) {
       const int kps = (ksteps + sp - 1) / sp;
       return CfPlan{bm, bn, (ksteps + kps - 1) / kps, kps};
     }
@@ -848,13 +851,13 @@ CfPlan cf_plan(int M, int Ncol, int ksteps, long long ws_floats, int batch) {
     if (M % bm || Ncol % bn) continue;
     const long long tiles = (long long)(M / bm) * (Ncol / bn) * batch;
     const double step_us = (double)bm * bn * CF_BK * 2 / 614e3 / derate[sh];
-    for (int split = 1; split <= (allow_split ? 64 : 1); ++split) {
+    for (int split = 1; split <= 64; ++split) {
       const int kps = (ksteps + split - 1) / split;
-      if (split > 1 && (kps < 4 || (long long)split * M * Ncol > ws_floats)) break;
+      if (split > 1 && (kps < 4 || split * slab1 > ws_floats)) break;
       const int sp = (ksteps + kps - 1) / kps;
       const long long blocks = tiles * sp;
       double t = (double)((blocks + 255) / 256) * step_us * (kps + 3);
-      if (sp > 1) t += 8.0 * sp * M * Ncol / 4e6 + 2.0;
+      if (sp > 1) t += 8.0 * sp * slab1 / 4e6 + 2.0;
       if (t < best_t * 0.999) {
         best_t = t;
         best = CfPlan{bm, bn, sp, kps};
@@ -871,7 +874,7 @@ CfPlan cf_plan(int M, int Ncol, int ksteps, long long ws_floats, int batch) {
 template <int MODE>
 int cf_gemm(const float* a, const float* b, float* out, float* ws, long long ws_floats,
             CfGeom geo, hipStream_t s, float* bnpart, long long bnpart_floats,
-            const CfBnBwd* bnb, const float* addend) {
+            const CfBnBwd* bnb, const float* addend, int* split_out = nullptr) {
   ws_floats -= 64;  // the workspace's last 64 floats are conv.hip's zero page (never a slab)
   const int batch = geo.nsplit;  // callers pass the batch count here (1: no batching)
   const CfPlan p = cf_plan(geo.M, geo.Ncol, geo.ksteps, ws_floats, batch);
@@ -901,6 +904,12 @@ int cf_gemm(const float* a, const float* b, float* out, float* ws, long long ws_
     CF_LAUNCH(MODE, 64, 64, 4, 2, 16);
   }
   EW_CHECK_LAUNCH();
+  if (split_out) {  // the caller reduces the slabs (ws[split][batch][M][Ncol]) itself
+    *split_out = p.split;
+    return 0;
+  }
+  if (p.split > 1 && batch > 1)
+    throw std::runtime_error("ewdml conv f32: a batched split GEMM needs the caller's reduction");
   if (p.split > 1) {
     const int M = geo.M, Nc = geo.Ncol;
     const long long n = (long long)M * Nc;
@@ -940,6 +949,20 @@ int cf_taps(int ksize) {
 
 // out[b][M][N] = A[b][M][K] * B[b][N][K]^T for b < batch (row-major, K contiguous): the forward
 // GEMM as a 1x1 "convolution" over M pixels, batched over blockIdx.z (winograd_f32.hip).
+// dU[z][M][N] = sum_k A[z][k][M] B[z][k][N] (both row-major over k; the weight-gradient GEMM),
+// K-split into ws slabs [split][batch][M][N] that the caller reduces; returns the split count
+// (1: written to out directly).
+int ew_cf_gemm_tn_batched(const float* a, const float* b, float* out, float* ws,
+                          long long ws_floats, int M, int N, int K, int batch, long long a_bs,
+                          long long b_bs, hipStream_t s) {
+  if (M % 64 || N % 64 || K % CF_BK || (long long)K * std::max(M, N) >= (1LL << 31))
+    throw std::runtime_error("ewdml gemm f32: needs M, N % 64 == 0, K % 32 == 0");
+  CfGeom g{M, N, K, 1, 1, N, M, 1, K / CF_BK, 0, batch, a_bs, b_bs, (long long)M * N, 0};
+  int split = 1;
+  cf_gemm<CF_WGRAD>(a, b, out, ws, ws_floats, g, s, nullptr, 0, nullptr, nullptr, &split);
+  return split;
+}
+
 // out[z][M][N] = A[z][M][K] * op(B[z'])  for z < batch (row-major, K contiguous in A): the conv
 // GEMMs as 1x1 "convolutions" over M pixels, batched over blockIdx.z (winograd_f32.hip).
 // nt: B[z] is [N][K] (the forward's weight image); else B[z'] is [K][N] (backward data) with

@@ -213,6 +213,9 @@ int ew_wino_f32_bwd_data(uintptr_t dy, uintptr_t U, uintptr_t dx, uintptr_t V, u
                          uintptr_t bn_res, uintptr_t bn_code, uintptr_t bn_stats, int bn_relu,
                          uintptr_t bnpart, long long bnpart_floats, uintptr_t addend,
                          uintptr_t stream);
+void ew_wino_f32_wgrad(uintptr_t dy, uintptr_t V, uintptr_t dw, uintptr_t D, uintptr_t U_scratch,
+                       uintptr_t ws, long long ws_floats, long long N, int H, int W, int C, int Nc,
+                       uintptr_t stream);
 
 // ---- RCCL communicator issuing collectives on the caller's stream (rccl_comm.hip) ----
 // dtype codes: 0 f32, 1 bf16, 2 f16, 3 u8, 4 i32, 5 f64, 6 i64; op: 0 sum, 1 max, 2 min, 3 avg

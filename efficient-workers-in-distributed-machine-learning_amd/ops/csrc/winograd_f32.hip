@@ -30,6 +30,9 @@
 #include "conv_f32.h"
 #include "ewdml_ops.h"
 
+int ew_cf_gemm_tn_batched(const float* a, const float* b, float* out, float* ws,
+                          long long ws_floats, int M, int N, int K, int batch, long long a_bs,
+                          long long b_bs, hipStream_t s);
 void ew_cf_gemm_batched(const float* a, const float* b, float* out, int M, int N, int K, int batch,
                         long long a_bs, long long b_bs, long long o_bs, bool nt, bool flip,
                         hipStream_t s);
@@ -209,6 +212,81 @@ __global__ __launch_bounds__(EW_BLOCK) void k_wg_output(const float* __restrict_
   }
 }
 
+// Weight gradient, the transpose of the forward: dMo = A dy A^T per tile and channel
+// (k_wg_dy), dU[xi][Nc][C] = sum over tiles of dMo[xi][tile][Nc] V[xi][tile][C] (the forward's V,
+// kept for the backward; one K = tiles GEMM per position, K-split into slabs), then
+// dw = G^T dU G summed over the splits in a fixed order (k_wg_wgrad_out).
+// A = [1 0; 1 1; 1 -1; 0 -1], G^T = [1 .5 .5 0; 0 .5 -.5 0; 0 .5 .5 1].
+__global__ __launch_bounds__(EW_BLOCK) void k_wg_dy(const float* __restrict__ dy,
+                                                    float* __restrict__ D, int H, int W, int Nc,
+                                                    long long tiles) {
+  const int cq = Nc >> 2;
+  const long long g = (long long)blockIdx.x * EW_BLOCK + threadIdx.x;
+  if (g >= tiles * cq) return;
+  const long long tl = g / cq;
+  const int c = (int)(g - tl * cq) * 4;
+  const int tw = W >> 1, tpi = (H >> 1) * tw;
+  const int n = (int)(tl / tpi), rem = (int)(tl - (long long)n * tpi);
+  const int ty = rem / tw, tx = rem - ty * tw;
+  const float* p = dy + (((long long)n * H + 2 * ty) * W + 2 * tx) * Nc + c;
+  const f32x4 d00 = *reinterpret_cast<const f32x4*>(p);
+  const f32x4 d01 = *reinterpret_cast<const f32x4*>(p + Nc);
+  const f32x4 d10 = *reinterpret_cast<const f32x4*>(p + (long long)W * Nc);
+  const f32x4 d11 = *reinterpret_cast<const f32x4*>(p + (long long)W * Nc + Nc);
+  f32x4 t[4][2];  // A dy
+  t[0][0] = d00;
+  t[0][1] = d01;
+  t[1][0] = d00 + d10;
+  t[1][1] = d01 + d11;
+  t[2][0] = d00 - d10;
+  t[2][1] = d01 - d11;
+  t[3][0] = -d10;
+  t[3][1] = -d11;
+  const long long xs = tiles * Nc;
+  float* o = D + tl * Nc + c;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {  // (A dy) A^T
+    *reinterpret_cast<f32x4*>(o + (i * 4 + 0) * xs) = t[i][0];
+    *reinterpret_cast<f32x4*>(o + (i * 4 + 1) * xs) = t[i][0] + t[i][1];
+    *reinterpret_cast<f32x4*>(o + (i * 4 + 2) * xs) = t[i][0] - t[i][1];
+    *reinterpret_cast<f32x4*>(o + (i * 4 + 3) * xs) = -t[i][1];
+  }
+}
+
+// dw[o][r][s][i..i+3] = (G^T (sum_z dU_z[xi]) G)[r][s], dU_z = src + z * 16 * Nc * C
+__global__ __launch_bounds__(EW_BLOCK) void k_wg_wgrad_out(const float* __restrict__ src,
+                                                           int nsplit, float* __restrict__ dw,
+                                                           int Nc, int C) {
+  const int cq = C >> 2;
+  const long long g = (long long)blockIdx.x * EW_BLOCK + threadIdx.x;
+  if (g >= (long long)Nc * cq) return;
+  const int o = (int)(g / cq), i = (int)(g - (long long)o * cq) * 4;
+  const long long xs = (long long)Nc * C;
+  const float* p = src + (long long)o * C + i;
+  f32x4 u[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) u[q] = *reinterpret_cast<const f32x4*>(p + q * xs);
+  for (int z = 1; z < nsplit; ++z) {  // fixed order
+    const float* pz = p + (long long)z * 16 * xs;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) u[q] += *reinterpret_cast<const f32x4*>(pz + q * xs);
+  }
+  f32x4 t[3][4];  // G^T dU
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    t[0][j] = u[j] + 0.5f * (u[4 + j] + u[8 + j]);
+    t[1][j] = 0.5f * (u[4 + j] - u[8 + j]);
+    t[2][j] = 0.5f * (u[4 + j] + u[8 + j]) + u[12 + j];
+  }
+  float* w = dw + (long long)o * 9 * C + i;
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {  // (G^T dU) G
+    *reinterpret_cast<f32x4*>(w + (r * 3 + 0) * C) = t[r][0] + 0.5f * (t[r][1] + t[r][2]);
+    *reinterpret_cast<f32x4*>(w + (r * 3 + 1) * C) = 0.5f * (t[r][1] - t[r][2]);
+    *reinterpret_cast<f32x4*>(w + (r * 3 + 2) * C) = 0.5f * (t[r][1] + t[r][2]) + t[r][3];
+  }
+}
+
 long long wg_tiles(long long N, int H, int W) { return N * (H / 2) * (W / 2); }
 
 void wg_check(long long N, int H, int W, int Cin, int Cout, const char* what) {
@@ -298,4 +376,29 @@ int ew_wino_f32_bwd_data(uintptr_t dy, uintptr_t U, uintptr_t dx, uintptr_t V, u
   return wg_output(mo, reinterpret_cast<float*>(dx), N, H, W, C,
                    bn_h ? reinterpret_cast<float*>(bnpart) : nullptr, bnpart_floats, bb,
                    reinterpret_cast<const float*>(addend), s);
+}
+
+// dw (channels_last [Nc][3][3][C]) from dy and the forward's V; D: 16 * tiles * Nc floats;
+// ws: K-split slabs (the plan uses what fits, ws_floats - 64 of it)
+void ew_wino_f32_wgrad(uintptr_t dy, uintptr_t V, uintptr_t dw, uintptr_t D, uintptr_t U_scratch,
+                       uintptr_t ws, long long ws_floats, long long N, int H, int W, int C, int Nc,
+                       uintptr_t stream) {
+  wg_check(N, H, W, C, Nc, "weight gradient");
+  if (C % 64) throw std::runtime_error("ewdml winograd f32: weight gradient needs C % 64 == 0");
+  hipStream_t s = (hipStream_t)stream;
+  const long long tiles = wg_tiles(N, H, W);
+  float* d = reinterpret_cast<float*>(D);
+  const long long n = tiles * (Nc / 4);
+  hipLaunchKernelGGL(k_wg_dy, dim3((unsigned)((n + EW_BLOCK - 1) / EW_BLOCK)), dim3(EW_BLOCK), 0,
+                     s, reinterpret_cast<const float*>(dy), d, H, W, Nc, tiles);
+  EW_CHECK_LAUNCH();
+  float* du = reinterpret_cast<float*>(U_scratch);
+  const int split = ew_cf_gemm_tn_batched(d, reinterpret_cast<const float*>(V), du,
+                                          reinterpret_cast<float*>(ws), ws_floats, Nc, C,
+                                          (int)tiles, 16, tiles * Nc, tiles * C, s);
+  const long long m = (long long)Nc * (C / 4);
+  hipLaunchKernelGGL(k_wg_wgrad_out, dim3((unsigned)((m + EW_BLOCK - 1) / EW_BLOCK)),
+                     dim3(EW_BLOCK), 0, s, split > 1 ? reinterpret_cast<const float*>(ws) : du,
+                     split, reinterpret_cast<float*>(dw), Nc, C);
+  EW_CHECK_LAUNCH();
 }

@@ -224,11 +224,11 @@ def test_conv_f32_winograd_forward_backward(N, C, Nc, H, W):
     assert _rel(y, ref) < TOL, _rel(y, ref)
     assert _rel(xa.grad, gx) < TOL, _rel(xa.grad, gx)
     assert _rel(wa.grad, gw) < TOL, _rel(wa.grad, gw)
-    # bit-for-bit repeatable (fixed-order transforms, no split-K)
+    # bit-for-bit repeatable (fixed-order transforms and split sums)
     xb, wb = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
     y2 = conv.conv(xb, wb)
     y2.backward(dy)
-    assert torch.equal(y, y2) and torch.equal(xa.grad, xb.grad)
+    assert torch.equal(y, y2) and torch.equal(xa.grad, xb.grad) and torch.equal(wa.grad, wb.grad)
     # and close to the direct kernels (both within rounding of float64)
     d = _conv(wino=False)
     assert not d.wino_ok(x, w)

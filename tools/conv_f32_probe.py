@@ -3,7 +3,7 @@ gradient) with HIP events; prints us and TF/s per direction.
 
     python tools/conv_f32_probe.py [--batch 128] [--reps 20] [--shapes vgg|big] [--wino]
 --wino adds the Winograd F(2x2, 3x3) forward (weight + input transforms, 16 GEMMs, output
-transform: "wfwd") and backward data ("wbwd") on the same shapes (TF/s counted at direct FLOPs).
+transform: "wfwd"), backward data ("wbwd") and weight gradient ("wwgrad") on the same shapes (TF/s counted at direct FLOPs).
 EWDML_CF_PLAN="bm,bn,split" forces a launch plan (ops/csrc/conv_f32.hip cf_plan).
 """
 import argparse
@@ -64,12 +64,19 @@ def main():
             calls["wbwd"] = lambda: C_.wino_f32_bwd_data(
                 _ptr(y), _ptr(U), _ptr(dx), _ptr(buf), _ptr(buf) + 64 * t * Nc, N, HW, HW, C, Nc,
                 0, 0, 0, 0, 0, 0, 0, 0, _stream())
+            D = torch.empty(16 * t * Nc, device=dev)
+            dU = torch.empty(16 * Nc * C, device=dev)
+            slabs = torch.empty(4 * 16 * Nc * C + 64, device=dev)
+            calls["wwgrad"] = lambda: C_.wino_f32_wgrad(
+                _ptr(y), _ptr(buf), _ptr(dw), _ptr(D), _ptr(dU), _ptr(slabs), slabs.numel(), N,
+                HW, HW, C, Nc, _stream())
         if args.miopen:
             xm = x.permute(0, 3, 1, 2)  # NCHW view of NHWC memory: channels_last
             wm = w.permute(0, 3, 1, 2)
             calls["miopen_fwd"] = lambda: torch.nn.functional.conv2d(xm, wm, padding=1)
         line = f"C={C:4d} Nc={Nc:4d} HW={HW:3d}"
-        extra = (["miopen_fwd"] if args.miopen else []) + (["wfwd", "wbwd"] if args.wino else [])
+        extra = (["miopen_fwd"] if args.miopen else []) + (["wfwd", "wbwd", "wwgrad"] if args.wino
+                                                            else [])
         for d in args.dirs.split(",") + extra:
             f = calls[d]
             for _ in range(3):
