@@ -196,13 +196,12 @@ class _Conv(torch.autograd.Function):
         if wino_ok(x, w):
             # transformed weight U[16][Nc][C], kept for the backward-data GEMMs (read flipped)
             U = torch.empty(16 * Nc * C, dtype=torch.float32, device=x.device)
-            C_.wino_f32_weight(_ptr(w), _ptr(U), Nc, C, _stream())
             t = N * (H // 2) * (W // 2)
             # V (the transformed input) is kept for the weight-gradient GEMMs
             V = torch.empty(16 * t * C, dtype=torch.float32, device=x.device)
             Mo = torch.empty(16 * t * Nc, dtype=torch.float32, device=x.device)
-            rows = C_.wino_f32_fwd(_ptr(x), _ptr(U), _ptr(y), _ptr(V), _ptr(Mo), N, H, W, C, Nc,
-                                   _ptr(part), part.numel(), _stream())
+            rows = C_.wino_f32_fwd(_ptr(x), _ptr(w), _ptr(U), _ptr(y), _ptr(V), _ptr(Mo), N, H, W,
+                                   C, Nc, _ptr(part), part.numel(), _stream())
             ctx.wino = (U, V)
         else:
             fwd = C_.conv_f32_fwd if x.dtype == torch.float32 else C_.conv_fwd
@@ -227,6 +226,11 @@ class _Conv(torch.autograd.Function):
         f32 = x.dtype == torch.float32
         bwd_data = C_.conv_f32_bwd_data if f32 else C_.conv_bwd_data
         dx = dw = None
+        D = None  # Winograd: the weight gradient's dy transform, made by the bwd-data pass
+        if ctx.wino is not None and ctx.needs_input_grad[1]:
+            D = torch.empty(16 * N * (H // 2) * (W // 2) * Nc, dtype=torch.float32,
+                            device=x.device)
+        d_ready = 0
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x, memory_format=torch.channels_last)
             node, ctx.bn_node = ctx.bn_node, None
@@ -246,7 +250,9 @@ class _Conv(torch.autograd.Function):
 
                 def bwd_data(dy_, w_, dx_, ws_, wsn, *rest):  # same contract, Winograd
                     return C_.wino_f32_bwd_data(dy_, _ptr(U), dx_, _ptr(buf),
-                                                _ptr(buf) + 64 * t * Nc, *rest[:5], *rest[6:])
+                                                _ptr(buf) + 64 * t * Nc, *rest[:5], *rest[6:-1],
+                                                _ptr(D), rest[-1])
+                d_ready = int(D is not None)
             if link is None:
                 bwd_data(_ptr(dy), _ptr(w), _ptr(dx), _ptr(ws), ws.numel(), N, H, W, C, Nc, k, 0,
                          0, 0, 0, 0, 0, 0, _ptr(add), _stream())
@@ -267,13 +273,11 @@ class _Conv(torch.autograd.Function):
             if ctx.wino is not None:
                 # dw = G^T (sum over tiles of (A dy A^T) V) G: 16 GEMMs of K = N*H*W/4
                 V = ctx.wino[1]
-                t = N * (H // 2) * (W // 2)
-                D = torch.empty(16 * t * Nc, dtype=torch.float32, device=x.device)
                 dU = torch.empty(16 * Nc * C, dtype=torch.float32, device=x.device)
                 slabs = torch.empty(_WINO_WG_SPLITS * 16 * Nc * C + 64, dtype=torch.float32,
                                     device=x.device)
-                C_.wino_f32_wgrad(_ptr(dy), _ptr(V), _ptr(dw), _ptr(D), _ptr(dU), _ptr(slabs),
-                                  slabs.numel(), N, H, W, C, Nc, _stream())
+                C_.wino_f32_wgrad(_ptr(dy), _ptr(V), _ptr(dw), _ptr(D), d_ready, _ptr(dU),
+                                  _ptr(slabs), slabs.numel(), N, H, W, C, Nc, _stream())
             else:
                 wgrad = C_.conv_f32_wgrad if f32 else C_.conv_wgrad
                 wgrad(_ptr(dy), _ptr(x), _ptr(dw), _ptr(ws), ws.numel(), N, H, W, C, Nc, k,

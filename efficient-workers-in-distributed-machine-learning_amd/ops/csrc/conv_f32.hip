@@ -857,6 +857,9 @@ CfPlan cf_plan(int M, int Ncol, int ksteps, long long ws_floats, int batch) {
       const int sp = (ksteps + kps - 1) / kps;
       const long long blocks = tiles * sp;
       double t = (double)((blocks + 255) / 256) * step_us * (kps + 3);
+      // operand traffic: every block streams (bm + bn) x K floats, ~6 TB/s from HBM / MALL
+      // (small tiles over a long K -- the Winograd weight-gradient GEMMs -- are bound by it)
+      t = std::max(t, (double)tiles * (bm + bn) * ksteps * CF_BK * 4 / 6e6);
       if (sp > 1) t += 8.0 * sp * slab1 / 4e6 + 2.0;
       if (t < best_t * 0.999) {
         best_t = t;

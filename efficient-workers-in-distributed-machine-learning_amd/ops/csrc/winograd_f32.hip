@@ -4,8 +4,8 @@
 // 9-tap implicit GEMM of conv_f32.hip (2*P*C*Nc*9 FLOPs) becomes 16 batched GEMMs over the
 // tiles (2*(P/4)*16*C*Nc FLOPs, 2.25x fewer):
 //
-//   U[xi][Nc][C]    = (G g G^T)[xi]           weight transform, once per step (k_wg_weight)
-//   V[xi][tiles][C] = (B^T d B)[xi]           input transform (k_wg_input)
+//   U[xi][Nc][C]    = (G g G^T)[xi]           weight transform, once per step
+//   V[xi][tiles][C] = (B^T d B)[xi]           input transform (one launch for both: k_wg_input)
 //   Mo[xi][tiles][Nc] = V[xi] U[xi]^T          16 fp32 MFMA GEMMs (conv_f32.hip k_cf_gemm, batched)
 //   y = A^T Mo A                              output transform (k_wg_output), with the BatchNorm
 //                                             partial sums (forward) or the producing BN layer's
@@ -42,10 +42,9 @@ namespace {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // U[xi][o][i..i+3] = (G g G^T)[xi], g(r, s) = w[o][r][s][i..i+3] (channels_last [Nc][3][3][C])
-__global__ __launch_bounds__(EW_BLOCK) void k_wg_weight(const float* __restrict__ w,
-                                                        float* __restrict__ U, int Nc, int C) {
+__device__ __forceinline__ void wg_weight(const float* __restrict__ w, float* __restrict__ U,
+                                          int Nc, int C, long long g) {
   const int cq = C >> 2;
-  const long long g = (long long)blockIdx.x * EW_BLOCK + threadIdx.x;
   if (g >= (long long)Nc * cq) return;
   const int o = (int)(g / cq), i = (int)(g - (long long)o * cq) * 4;
   f32x4 k[3][3];
@@ -75,11 +74,14 @@ __global__ __launch_bounds__(EW_BLOCK) void k_wg_weight(const float* __restrict_
 
 // V[xi][tile][c..c+3] = (B^T d B)[xi], d = the 4x4 patch at (2 ty - 1, 2 tx - 1) of x[N][H][W][C]
 // (zero outside).  Thread: one tile x one channel quad; consecutive threads, consecutive quads.
-__global__ __launch_bounds__(EW_BLOCK) void k_wg_input(const float* __restrict__ x,
-                                                       float* __restrict__ V, int H, int W, int C,
-                                                       long long tiles) {
+__device__ __forceinline__ void wg_dy_store(float* __restrict__ D, long long xs, f32x4 d00,
+                                            f32x4 d01, f32x4 d10, f32x4 d11);
+
+// (with D: also the weight-gradient transform A dy A^T of the patch's inner 2x2, see k_wg_dy)
+__device__ __forceinline__ void wg_input(const float* __restrict__ x, float* __restrict__ V,
+                                         int H, int W, int C, long long tiles, long long g,
+                                         float* __restrict__ D = nullptr) {
   const int cq = C >> 2;
-  const long long g = (long long)blockIdx.x * EW_BLOCK + threadIdx.x;
   if (g >= tiles * cq) return;
   const long long tl = g / cq;
   const int c = (int)(g - tl * cq) * 4;
@@ -98,6 +100,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_wg_input(const float* __restrict__
           x + (ok ? (((long long)n * H + h) * W + w) * C + c : c));
       d[i][j] = ok ? v : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
     }
+  if (D) wg_dy_store(D + tl * C + c, tiles * C, d[1][1], d[1][2], d[2][1], d[2][2]);
   f32x4 t[4][4];  // B^T d
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -115,6 +118,25 @@ __global__ __launch_bounds__(EW_BLOCK) void k_wg_input(const float* __restrict__
     *reinterpret_cast<f32x4*>(v + (i * 4 + 2) * xs) = t[i][2] - t[i][1];
     *reinterpret_cast<f32x4*>(v + (i * 4 + 3) * xs) = t[i][1] - t[i][3];
   }
+}
+
+// the input transform over blocks [0, nbi) and, when w is given, the weight transform over the
+// rest (one launch for both: each alone is a few-microsecond kernel)
+__global__ __launch_bounds__(EW_BLOCK) void k_wg_input(const float* __restrict__ x,
+                                                       float* __restrict__ V, int H, int W, int C,
+                                                       long long tiles, int nbi,
+                                                       const float* __restrict__ w,
+                                                       float* __restrict__ U, int Nc,
+                                                       float* __restrict__ D) {
+  if ((int)blockIdx.x < nbi)
+    wg_input(x, V, H, W, C, tiles, (long long)blockIdx.x * EW_BLOCK + threadIdx.x, D);
+  else
+    wg_weight(w, U, Nc, C, (long long)(blockIdx.x - nbi) * EW_BLOCK + threadIdx.x);
+}
+
+__global__ __launch_bounds__(EW_BLOCK) void k_wg_weight(const float* __restrict__ w,
+                                                        float* __restrict__ U, int Nc, int C) {
+  wg_weight(w, U, Nc, C, (long long)blockIdx.x * EW_BLOCK + threadIdx.x);
 }
 
 // y = A^T Mo A per tile (+ addend), with the BatchNorm partial sums of y (forward: sum, sum of
@@ -229,10 +251,14 @@ __global__ __launch_bounds__(EW_BLOCK) void k_wg_dy(const float* __restrict__ dy
   const int n = (int)(tl / tpi), rem = (int)(tl - (long long)n * tpi);
   const int ty = rem / tw, tx = rem - ty * tw;
   const float* p = dy + (((long long)n * H + 2 * ty) * W + 2 * tx) * Nc + c;
-  const f32x4 d00 = *reinterpret_cast<const f32x4*>(p);
-  const f32x4 d01 = *reinterpret_cast<const f32x4*>(p + Nc);
-  const f32x4 d10 = *reinterpret_cast<const f32x4*>(p + (long long)W * Nc);
-  const f32x4 d11 = *reinterpret_cast<const f32x4*>(p + (long long)W * Nc + Nc);
+  wg_dy_store(D + tl * Nc + c, tiles * Nc, *reinterpret_cast<const f32x4*>(p),
+              *reinterpret_cast<const f32x4*>(p + Nc),
+              *reinterpret_cast<const f32x4*>(p + (long long)W * Nc),
+              *reinterpret_cast<const f32x4*>(p + (long long)W * Nc + Nc));
+}
+
+__device__ __forceinline__ void wg_dy_store(float* __restrict__ o, long long xs, f32x4 d00,
+                                            f32x4 d01, f32x4 d10, f32x4 d11) {
   f32x4 t[4][2];  // A dy
   t[0][0] = d00;
   t[0][1] = d01;
@@ -242,8 +268,6 @@ __global__ __launch_bounds__(EW_BLOCK) void k_wg_dy(const float* __restrict__ dy
   t[2][1] = d01 - d11;
   t[3][0] = -d10;
   t[3][1] = -d11;
-  const long long xs = tiles * Nc;
-  float* o = D + tl * Nc + c;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {  // (A dy) A^T
     *reinterpret_cast<f32x4*>(o + (i * 4 + 0) * xs) = t[i][0];
@@ -322,10 +346,14 @@ int wg_output(const float* Mo, float* y, long long N, int H, int W, int Nc, floa
   return bnpart ? (int)nblk : 0;
 }
 
-void wg_input(const float* x, float* V, long long N, int H, int W, int C, hipStream_t s) {
+// input transform of x [N][H][W][C] into V; with w, also U[16][Nc][C] from w [Nc][3][3][C]
+void wg_input(const float* x, float* V, long long N, int H, int W, int C, hipStream_t s,
+              const float* w = nullptr, float* U = nullptr, int Nc = 0, float* D = nullptr) {
   const long long n = wg_tiles(N, H, W) * (C / 4);
-  hipLaunchKernelGGL(k_wg_input, dim3((unsigned)((n + EW_BLOCK - 1) / EW_BLOCK)), dim3(EW_BLOCK),
-                     0, s, x, V, H, W, C, wg_tiles(N, H, W));
+  const int nbi = (int)((n + EW_BLOCK - 1) / EW_BLOCK);
+  const int nbw = w ? (int)(((long long)Nc * (C / 4) + EW_BLOCK - 1) / EW_BLOCK) : 0;
+  hipLaunchKernelGGL(k_wg_input, dim3(nbi + nbw), dim3(EW_BLOCK), 0, s, x, V, H, W, C,
+                     wg_tiles(N, H, W), nbi, w, U, Nc, D);
   EW_CHECK_LAUNCH();
 }
 
@@ -340,15 +368,16 @@ void ew_wino_f32_weight(uintptr_t w, uintptr_t U, int Nc, int C, uintptr_t strea
   EW_CHECK_LAUNCH();
 }
 
-int ew_wino_f32_fwd(uintptr_t x, uintptr_t U, uintptr_t y, uintptr_t V, uintptr_t Mo, long long N,
-                    int H, int W, int C, int Nc, uintptr_t bnpart, long long bnpart_floats,
-                    uintptr_t stream) {
+int ew_wino_f32_fwd(uintptr_t x, uintptr_t w, uintptr_t U, uintptr_t y, uintptr_t V, uintptr_t Mo,
+                    long long N, int H, int W, int C, int Nc, uintptr_t bnpart,
+                    long long bnpart_floats, uintptr_t stream) {
   wg_check(N, H, W, C, Nc, "forward");
   hipStream_t s = (hipStream_t)stream;
   const long long tiles = wg_tiles(N, H, W);
   float* v = reinterpret_cast<float*>(V);
   float* mo = reinterpret_cast<float*>(Mo);
-  wg_input(reinterpret_cast<const float*>(x), v, N, H, W, C, s);
+  wg_input(reinterpret_cast<const float*>(x), v, N, H, W, C, s, reinterpret_cast<const float*>(w),
+           reinterpret_cast<float*>(U), Nc);
   ew_cf_gemm_batched(v, reinterpret_cast<const float*>(U), mo, (int)tiles, Nc, C, 16, tiles * C,
                      (long long)Nc * C, tiles * Nc, true, false, s);
   const CfBnBwd none{nullptr, nullptr, nullptr, nullptr, 0, 0, 0};
@@ -360,13 +389,15 @@ int ew_wino_f32_bwd_data(uintptr_t dy, uintptr_t U, uintptr_t dx, uintptr_t V, u
                          long long N, int H, int W, int C, int Nc, uintptr_t bn_h,
                          uintptr_t bn_res, uintptr_t bn_code, uintptr_t bn_stats, int bn_relu,
                          uintptr_t bnpart, long long bnpart_floats, uintptr_t addend,
-                         uintptr_t stream) {
+                         uintptr_t D, uintptr_t stream) {
   wg_check(N, H, W, Nc, C, "backward data");
   hipStream_t s = (hipStream_t)stream;
   const long long tiles = wg_tiles(N, H, W);
   float* v = reinterpret_cast<float*>(V);
   float* mo = reinterpret_cast<float*>(Mo);
-  wg_input(reinterpret_cast<const float*>(dy), v, N, H, W, Nc, s);
+  // D != 0: the weight gradient's dy transform from the same reads (ew_wino_f32_wgrad d_ready)
+  wg_input(reinterpret_cast<const float*>(dy), v, N, H, W, Nc, s, nullptr, nullptr, 0,
+           reinterpret_cast<float*>(D));
   // Mo'[xi][tile][c] = sum_n V'[xi][tile][n] U[p(xi)][n][c]
   ew_cf_gemm_batched(v, reinterpret_cast<const float*>(U), mo, (int)tiles, C, Nc, 16, tiles * Nc,
                      (long long)Nc * C, tiles * C, false, true, s);
@@ -380,18 +411,20 @@ int ew_wino_f32_bwd_data(uintptr_t dy, uintptr_t U, uintptr_t dx, uintptr_t V, u
 
 // dw (channels_last [Nc][3][3][C]) from dy and the forward's V; D: 16 * tiles * Nc floats;
 // ws: K-split slabs (the plan uses what fits, ws_floats - 64 of it)
-void ew_wino_f32_wgrad(uintptr_t dy, uintptr_t V, uintptr_t dw, uintptr_t D, uintptr_t U_scratch,
-                       uintptr_t ws, long long ws_floats, long long N, int H, int W, int C, int Nc,
-                       uintptr_t stream) {
+void ew_wino_f32_wgrad(uintptr_t dy, uintptr_t V, uintptr_t dw, uintptr_t D, int d_ready,
+                       uintptr_t U_scratch, uintptr_t ws, long long ws_floats, long long N, int H,
+                       int W, int C, int Nc, uintptr_t stream) {
   wg_check(N, H, W, C, Nc, "weight gradient");
   if (C % 64) throw std::runtime_error("ewdml winograd f32: weight gradient needs C % 64 == 0");
   hipStream_t s = (hipStream_t)stream;
   const long long tiles = wg_tiles(N, H, W);
   float* d = reinterpret_cast<float*>(D);
-  const long long n = tiles * (Nc / 4);
-  hipLaunchKernelGGL(k_wg_dy, dim3((unsigned)((n + EW_BLOCK - 1) / EW_BLOCK)), dim3(EW_BLOCK), 0,
-                     s, reinterpret_cast<const float*>(dy), d, H, W, Nc, tiles);
-  EW_CHECK_LAUNCH();
+  if (!d_ready) {
+    const long long n = tiles * (Nc / 4);
+    hipLaunchKernelGGL(k_wg_dy, dim3((unsigned)((n + EW_BLOCK - 1) / EW_BLOCK)), dim3(EW_BLOCK),
+                       0, s, reinterpret_cast<const float*>(dy), d, H, W, Nc, tiles);
+    EW_CHECK_LAUNCH();
+  }
   float* du = reinterpret_cast<float*>(U_scratch);
   const int split = ew_cf_gemm_tn_batched(d, reinterpret_cast<const float*>(V), du,
                                           reinterpret_cast<float*>(ws), ws_floats, Nc, C,

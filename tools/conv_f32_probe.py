@@ -57,18 +57,17 @@ def main():
             t = N * (HW // 2) * (HW // 2)
             U = torch.empty(16 * Nc * C, device=dev)
             buf = torch.empty(16 * t * (C + Nc), device=dev)
-            calls["wfwd"] = lambda: (
-                C_.wino_f32_weight(_ptr(w), _ptr(U), Nc, C, _stream()),
-                C_.wino_f32_fwd(_ptr(x), _ptr(U), _ptr(y), _ptr(buf), _ptr(buf) + 64 * t * C, N,
-                                HW, HW, C, Nc, 0, 0, _stream()))
+            calls["wfwd"] = lambda: C_.wino_f32_fwd(
+                _ptr(x), _ptr(w), _ptr(U), _ptr(y), _ptr(buf), _ptr(buf) + 64 * t * C, N, HW, HW,
+                C, Nc, 0, 0, _stream())
             calls["wbwd"] = lambda: C_.wino_f32_bwd_data(
                 _ptr(y), _ptr(U), _ptr(dx), _ptr(buf), _ptr(buf) + 64 * t * Nc, N, HW, HW, C, Nc,
-                0, 0, 0, 0, 0, 0, 0, 0, _stream())
+                0, 0, 0, 0, 0, 0, 0, 0, 0, _stream())
             D = torch.empty(16 * t * Nc, device=dev)
             dU = torch.empty(16 * Nc * C, device=dev)
             slabs = torch.empty(4 * 16 * Nc * C + 64, device=dev)
             calls["wwgrad"] = lambda: C_.wino_f32_wgrad(
-                _ptr(y), _ptr(buf), _ptr(dw), _ptr(D), _ptr(dU), _ptr(slabs), slabs.numel(), N,
+                _ptr(y), _ptr(buf), _ptr(dw), _ptr(D), 0, _ptr(dU), _ptr(slabs), slabs.numel(), N,
                 HW, HW, C, Nc, _stream())
         if args.miopen:
             xm = x.permute(0, 3, 1, 2)  # NCHW view of NHWC memory: channels_last
