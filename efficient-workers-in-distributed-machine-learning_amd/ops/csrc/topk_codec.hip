@@ -15,7 +15,9 @@
 // threshold key and the number of threshold ties to keep are known; ties are kept lowest index
 // first, so every rank emits exactly k entries per tensor (fixed-size all-gather).
 //
-// Encode launches per bucket: hist0, select0, hist1, select1, hist2, select2, count, scan, write.
+// Encode launches per bucket: hist0, hist1, hist2, count, write.  The per-tensor steps between
+// them (digit select after each histogram pass, tie allocation / offsets / scale after the count)
+// run in the tensor's last-arriving chunk block (topk_tensor_last), not as separate launches.
 // The global state lives in one scratch block: zero-initialised once, histograms re-cleared by
 // k_topk_write after use, everything else fully rewritten per encode (no per-step memset).
 #include "common.h"
@@ -30,6 +32,38 @@ constexpr int NB2 = 1024;  // pass-2 digit: key bits [9:0]
 // chunks of a large tensor all hit the same few dozen bins (gradients cluster in a few exponent
 // bins), and one copy serialised ~300 global atomics per bin; the select kernel sums the copies.
 constexpr int NREP = 8;
+constexpr int TICK_STRIDE = 32;  // ints per ticket (one 128-B line)
+
+// Per-tensor hand-off from the chunk blocks of a pass to the tensor's last-arriving block, which
+// then runs the pass's per-tensor step itself (select / scan) instead of a one-block-per-tensor
+// launch.  Everything handed off is written by device-scope atomics (histograms, max key) or
+// agent-scope (sc1, write-through) stores (the count pass's per-chunk words), so no release fence
+// (a per-block L2 write-back): every wave drains them (vmcnt), lane 0 draws the ticket, and only
+// the last drawer acquires (cdna_hip_programming.md Guideline 16, sc1 form).  Tickets are zero at
+// allocation and re-zeroed by the last drawer.
+__device__ __forceinline__ bool topk_tensor_last(int* tick, int nchunks, int* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int prev = __hip_atomic_fetch_add(tick, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = prev == nchunks - 1;
+    if (last) {
+      __hip_atomic_store(tick, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    *flag = last;
+  }
+  __syncthreads();
+  return *flag != 0;
+}
+
+// Tensor t's digit (scanning from the top) holding its k_rem-th largest key, run by one block.
+template <int NB, int SHIFT, bool FIRST>
+__device__ __forceinline__ void topk_select(const uint32_t* __restrict__ hist,
+                                            const TensorRow* __restrict__ tensors,
+                                            uint32_t* __restrict__ state,
+                                            const uint32_t* __restrict__ kmaxr, int T, int t);
 
 // state[t] = {prefix, k_rem, max_key, pad}
 template <bool EF>
@@ -37,7 +71,10 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_hist0(GradPtrs gp,
                                                          float* __restrict__ resid,
                                                          const ChunkRow* __restrict__ chunks,
                                                          uint32_t* __restrict__ hist,
-                                                         uint32_t* __restrict__ kmaxr, int T) {
+                                                         uint32_t* __restrict__ kmaxr, int T,
+                                                         const TensorRow* __restrict__ tensors,
+                                                         uint32_t* __restrict__ state,
+                                                         int* __restrict__ tick) {
   // Gradients cluster in a few exponent bins, so most lanes of a wave add to the same bin and an
   // LDS atomic serialises per conflicting lane.  HSUB copies per bin in consecutive words (banks),
   // chosen by lane: a shared bin splits into HSUB bank groups; the copies are summed at the flush.
@@ -90,14 +127,19 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_hist0(GradPtrs gp,
     for (int j = 0; j < HSUB; ++j) v += hs[i * HSUB + j];
     if (v) atomicAdd(&dst[i], v);
   }
+  if (topk_tensor_last(tick + TICK_STRIDE * c.tensor, tensors[c.tensor].nchunks, reinterpret_cast<int*>(wmax)))
+    topk_select<NB0, 20, true>(hist, tensors, state, kmaxr, T, c.tensor);
 }
 
 // Histogram of key bits [SHIFT+9 : SHIFT] over elements whose bits above MATCH equal the prefix.
 template <int SHIFT, int MATCH>
 __global__ __launch_bounds__(EW_BLOCK) void k_topk_hist(GradPtrs gp, const float* __restrict__ flat,
                                                         const ChunkRow* __restrict__ chunks,
-                                                        const uint32_t* __restrict__ state,
-                                                        uint32_t* __restrict__ hist, int T) {
+                                                        uint32_t* __restrict__ state,
+                                                        uint32_t* __restrict__ hist, int T,
+                                                        const TensorRow* __restrict__ tensors,
+                                                        const uint32_t* __restrict__ kmaxr,
+                                                        int* __restrict__ tick) {
   __shared__ uint32_t h[NB1];
   for (int i = threadIdx.x; i < NB1; i += EW_BLOCK) h[i] = 0;
   __syncthreads();
@@ -116,20 +158,19 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_hist(GradPtrs gp, const float
   uint32_t* dst = hist + ((size_t)(blockIdx.x & (NREP - 1)) * T + c.tensor) * NB1;
   for (int i = threadIdx.x; i < NB1; i += EW_BLOCK)
     if (h[i]) atomicAdd(&dst[i], h[i]);
+  if (topk_tensor_last(tick + TICK_STRIDE * c.tensor, tensors[c.tensor].nchunks, reinterpret_cast<int*>(h)))
+    topk_select<NB1, SHIFT, false>(hist, tensors, state, kmaxr, T, c.tensor);
 }
 
-// One block per tensor: find the digit (scanning from the top) that holds the k_rem-th largest.
 template <int NB, int SHIFT, bool FIRST>
-__global__ __launch_bounds__(EW_BLOCK) void k_topk_select(const uint32_t* __restrict__ hist,
-                                                          const TensorRow* __restrict__ tensors,
-                                                          uint32_t* __restrict__ state,
-                                                          const uint32_t* __restrict__ kmaxr,
-                                                          int T) {
+__device__ __forceinline__ void topk_select(const uint32_t* __restrict__ hist,
+                                            const TensorRow* __restrict__ tensors,
+                                            uint32_t* __restrict__ state,
+                                            const uint32_t* __restrict__ kmaxr, int T, int t) {
   constexpr int PER = NB / EW_BLOCK;
   __shared__ uint32_t ws[EW_WAVES];
-  const int t = blockIdx.x;
   const uint32_t k_rem = FIRST ? (uint32_t)tensors[t].k : state[t * 4 + 1];
-  if (FIRST && threadIdx.x == 0) state[t * 4 + 0] = 0u;  // (the scan below synchronises)
+  uint32_t prefix = FIRST ? 0u : state[t * 4 + 0];
   uint32_t cnt[PER];
   uint32_t tsum = 0;
 #pragma unroll
@@ -155,7 +196,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_select(const uint32_t* __rest
     for (int j = 0; j < PER; ++j) {
       if (run + cnt[j] >= k_rem) {
         const uint32_t bin = NB - 1 - (threadIdx.x * PER + j);
-        state[t * 4 + 0] |= bin << SHIFT;
+        state[t * 4 + 0] = prefix | (bin << SHIFT);
         state[t * 4 + 1] = k_rem - run;
         break;
       }
@@ -165,12 +206,21 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_select(const uint32_t* __rest
 }
 
 // Per chunk: #(key > thr), #(key == thr) and sum of squares of the key > thr values.
-__global__ __launch_bounds__(EW_BLOCK) void k_topk_count(GradPtrs gp, const float* __restrict__ flat,
-                                                         const ChunkRow* __restrict__ chunks,
-                                                         const uint32_t* __restrict__ state,
-                                                         uint32_t* __restrict__ cnt_gt,
-                                                         uint32_t* __restrict__ cnt_eq,
-                                                         float* __restrict__ chunk_sq) {
+__device__ __forceinline__ void topk_scan(
+    const TensorRow* __restrict__ tensors, const uint32_t* __restrict__ state,
+    const uint32_t* __restrict__ cnt_gt, const uint32_t* __restrict__ cnt_eq,
+    const float* __restrict__ chunk_sq, uint32_t* __restrict__ chunk_off,
+    uint32_t* __restrict__ chunk_ties, float* __restrict__ inv_out, uint8_t* __restrict__ payload,
+    int scales_off, int counts_off, float levels, int norm_l2, int t);
+
+__global__ __launch_bounds__(EW_BLOCK) void k_topk_count(
+    GradPtrs gp, const float* __restrict__ flat, const ChunkRow* __restrict__ chunks,
+    const uint32_t* __restrict__ state, uint32_t* __restrict__ cnt_gt,
+    uint32_t* __restrict__ cnt_eq, float* __restrict__ chunk_sq,
+    const TensorRow* __restrict__ tensors, int* __restrict__ tick,
+    uint32_t* __restrict__ chunk_off, uint32_t* __restrict__ chunk_ties,
+    float* __restrict__ inv_out, uint8_t* __restrict__ payload, int scales_off, int counts_off,
+    float levels, int norm_l2) {
   __shared__ float wsf[EW_WAVES];
   __shared__ uint32_t wsu[2 * EW_WAVES];
   const ChunkRow c = chunks[blockIdx.x];
@@ -205,23 +255,26 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_count(GradPtrs gp, const floa
       a += wsu[i];
       b += wsu[EW_WAVES + i];
     }
-    cnt_gt[blockIdx.x] = a;
-    cnt_eq[blockIdx.x] = b;
-    chunk_sq[blockIdx.x] = s;
+    // sc1 stores: read by the tensor's last block in this launch
+    __hip_atomic_store(cnt_gt + blockIdx.x, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(cnt_eq + blockIdx.x, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(chunk_sq + blockIdx.x, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  if (topk_tensor_last(tick + TICK_STRIDE * c.tensor, tensors[c.tensor].nchunks, reinterpret_cast<int*>(wsu)))
+    topk_scan(tensors, state, cnt_gt, cnt_eq, chunk_sq, chunk_off, chunk_ties, inv_out, payload,
+              scales_off, counts_off, levels, norm_l2, c.tensor);
 }
 
-// One block per tensor: allocate threshold ties to chunks (lowest index first), chunk entry
+// Tensor t, one block: allocate threshold ties to chunks (lowest index first), chunk entry
 // offsets, the per-chunk uint16 counts of the payload, and the tensor's QSGD scale.
-__global__ __launch_bounds__(EW_BLOCK) void k_topk_scan(
+__device__ __forceinline__ void topk_scan(
     const TensorRow* __restrict__ tensors, const uint32_t* __restrict__ state,
     const uint32_t* __restrict__ cnt_gt, const uint32_t* __restrict__ cnt_eq,
     const float* __restrict__ chunk_sq, uint32_t* __restrict__ chunk_off,
     uint32_t* __restrict__ chunk_ties, float* __restrict__ inv_out, uint8_t* __restrict__ payload,
-    int scales_off, int counts_off, float levels, int norm_l2) {
+    int scales_off, int counts_off, float levels, int norm_l2, int t) {
   __shared__ uint32_t ws[EW_WAVES];
   __shared__ float wsf[EW_WAVES];
-  const int t = blockIdx.x;
   const TensorRow tr = tensors[t];
   const uint32_t need = state[t * 4 + 1];
   const uint32_t thr = state[t * 4 + 0];
@@ -451,7 +504,7 @@ void ew_topk_encode(const TopkEncodeArgs& a) {
   const int T = a.num_tensors, C = a.num_chunks;
   // scratch layout (all zeroed at once): state[T*4] | kmaxr[NREP*T] | hist0[NREP*T*NB0]
   // | hist1[NREP*T*NB1] | hist2[NREP*T*NB2] | cnt_gt[C] | cnt_eq[C] | chunk_off[C]
-  // | chunk_ties[C] | chunk_sq[C] | inv[T]
+  // | chunk_ties[C] | chunk_sq[C] | inv[T] | tickets[4*T]
   uint32_t* state = reinterpret_cast<uint32_t*>(scratch);
   uint32_t* kmaxr = state + 4 * T;
   uint32_t* hist0 = kmaxr + NREP * T;
@@ -463,6 +516,10 @@ void ew_topk_encode(const TopkEncodeArgs& a) {
   uint32_t* chunk_ties = chunk_off + C;
   float* chunk_sq = reinterpret_cast<float*>(chunk_ties + C);
   float* inv = chunk_sq + C;
+  // [4][T] per-pass tensor tickets, one 128-B line each (blocks of different tensors must not
+  // serialise on one line's atomics)
+  int* tick = reinterpret_cast<int*>(
+      (reinterpret_cast<uintptr_t>(inv + T) + TICK_STRIDE * 4 - 1) & ~(uintptr_t)(TICK_STRIDE * 4 - 1));
   hipStream_t s = (hipStream_t)a.stream;
   // no scratch memset: state / count sections are fully rewritten each encode, and the histogram
   // replicas are cleared by k_topk_write for the next one (zero-initialised at allocation)
@@ -473,19 +530,19 @@ void ew_topk_encode(const TopkEncodeArgs& a) {
   ew_fill_ptrs(g, a.grad_ptrs, a.n_grad_ptrs, T, a.bf16_mask, a.n_bf16_mask);
   float* resid = reinterpret_cast<float*>(a.resid);
   const float* src_flat = resid;  // passes after hist0 read the staged e = g + r under EF
+  // each pass's per-tensor step (select / scan) runs in the tensor's last-arriving chunk block
   if (resid)
-    EW_LAUNCH(k_topk_hist0<true>, C, s, g, resid, chunks, hist0, kmaxr, T);
+    EW_LAUNCH(k_topk_hist0<true>, C, s, g, resid, chunks, hist0, kmaxr, T, tensors, state, tick);
   else
-    EW_LAUNCH(k_topk_hist0<false>, C, s, g, resid, chunks, hist0, kmaxr, T);
-  EW_LAUNCH((k_topk_select<NB0, 20, true>), T, s, hist0, tensors, state, kmaxr, T);
-  EW_LAUNCH((k_topk_hist<10, 20>), C, s, g, src_flat, chunks, state, hist1, T);
-  EW_LAUNCH((k_topk_select<NB1, 10, false>), T, s, hist1, tensors, state, kmaxr, T);
-  EW_LAUNCH((k_topk_hist<0, 10>), C, s, g, src_flat, chunks, state, hist2, T);
-  EW_LAUNCH((k_topk_select<NB2, 0, false>), T, s, hist2, tensors, state, kmaxr, T);
-  EW_LAUNCH(k_topk_count, C, s, g, src_flat, chunks, state, cnt_gt, cnt_eq, chunk_sq);
+    EW_LAUNCH(k_topk_hist0<false>, C, s, g, resid, chunks, hist0, kmaxr, T, tensors, state, tick);
+  EW_LAUNCH((k_topk_hist<10, 20>), C, s, g, src_flat, chunks, state, hist1, T, tensors, kmaxr,
+            tick + TICK_STRIDE * T);
+  EW_LAUNCH((k_topk_hist<0, 10>), C, s, g, src_flat, chunks, state, hist2, T, tensors, kmaxr,
+            tick + 2 * TICK_STRIDE * T);
   auto* pay = reinterpret_cast<uint8_t*>(a.payload);
-  EW_LAUNCH(k_topk_scan, T, s, tensors, state, cnt_gt, cnt_eq, chunk_sq, chunk_off, chunk_ties, inv,
-            pay, a.scales_off, a.counts_off, a.levels, a.norm_l2);
+  EW_LAUNCH(k_topk_count, C, s, g, src_flat, chunks, state, cnt_gt, cnt_eq, chunk_sq, tensors,
+            tick + 3 * TICK_STRIDE * T, chunk_off, chunk_ties, inv, pay, a.scales_off, a.counts_off, a.levels,
+            a.norm_l2);
 #define EW_WRITE(VK, EFV)                                                                          \
   EW_LAUNCH((k_topk_write<VK, EFV>), C, s, g, resid, chunks, tensors, state, chunk_off, chunk_ties, \
             inv, pay, a.scales_off, a.idx_off, a.codes_off, a.levels, a.inv_levels, a.key,         \
@@ -503,7 +560,8 @@ void ew_topk_encode(const TopkEncodeArgs& a) {
 
 size_t ew_topk_scratch_bytes(int T, int C) {
   return sizeof(uint32_t) *
-         ((size_t)4 * T + (size_t)NREP * T * (1 + NB0 + NB1 + NB2) + 5 * (size_t)C + T);
+         ((size_t)4 * T + (size_t)NREP * T * (1 + NB0 + NB1 + NB2) + 5 * (size_t)C + T +
+          (4 * (size_t)T + 1) * TICK_STRIDE);
 }
 
 void ew_topk_decode_apply(const TopkDecodeArgs& a) {
