@@ -9,10 +9,10 @@ backward-data and backward-weight are hand-written MFMA implicit-GEMM kernels:
   results, like MIOpen's bf16 convolutions;
 * fp32 operands (``ops/csrc/conv_f32.hip``, ``v_mfma_f32_16x16x4_f32``): exact fp32 products and
   accumulation, fp32 results -- the reference's precision.  fp32 3x3 layers with at least
-  ``EWDML_WINO_MIN_C`` (default 128) input and output channels run forward and backward-data as
-  Winograd F(2x2, 3x3) (``ops/csrc/winograd_f32.hip``: 2.25x fewer MFMA FLOPs, fp32 transforms;
-  ``EWDML_WINOGRAD=0`` keeps the direct kernels) -- forward, backward data and weight gradient
-  (the forward's transformed input is kept for it).
+  ``EWDML_WINO_MIN_C`` (default 128) input and output channels run as Winograd F(2x2, 3x3)
+  (``ops/csrc/winograd_f32.hip``: 2.25x fewer MFMA FLOPs, fp32 transforms; F(4x4, 3x3) with
+  ``EWDML_WINO_TILE=4|auto``, ``EWDML_WINOGRAD=0`` keeps the direct kernels) -- forward, backward data and weight gradient (the forward's transformed input
+  is kept for it).
 
 :func:`conv2d_module` dispatches an ``nn.Conv2d`` (VGG's and ResNet's stride-1 3x3 / 1x1 layers).
 Shapes the kernels do not take (C_in or C_out not a multiple of 64, NCHW, other
@@ -44,37 +44,59 @@ _BN_BWD = os.environ.get("EWDML_CONV_BN_BWD", "1") != "0"
 _EPI_MAX = int(os.environ.get("EWDML_EPI_MAX", str(1 << 23)))
 
 
-# Winograd F(2x2, 3x3) for fp32 3x3 layers with min(C_in, C_out) >= _WINO_MIN_C (the deep layers,
-# where the GEMM outweighs the transforms' 4x-activation traffic: tools/conv_f32_probe.py --wino)
+# Winograd F(m x m, 3x3) for fp32 3x3 layers with min(C_in, C_out) >= _WINO_MIN_C (the deep layers,
+# where the GEMM outweighs the transforms' activation traffic: tools/conv_f32_probe.py --wino).
+# m: EWDML_WINO_TILE = 2 (default), 4 or auto (4 where the map tiles by 4 and C_out <= 512, else
+# 2).  m = 4 measured only +1.5 % on the VGG-11 step (smaller, more numerous GEMMs; 36-point
+# transforms) for ~4x m = 2's rounding error (5e-6 vs 1.3e-6 relative for MIOpen's fp32 on the
+# whole-network forward): the default keeps m = 2 (profiles/conv/winograd_f32_probe_m4.txt)
 _WINO = os.environ.get("EWDML_WINOGRAD", "1") != "0"
 _WINO_MIN_C = int(os.environ.get("EWDML_WINO_MIN_C", "128"))
-# most K-splits of a Winograd weight-gradient GEMM (slab memory: splits x 16 x C_out x C_in floats)
+_WINO_TILE = os.environ.get("EWDML_WINO_TILE", "2")
+# most K-splits of a Winograd weight-gradient GEMM (slab memory: splits x a^2 x C_out x C_in floats)
 _WINO_WG_SPLITS = int(os.environ.get("EWDML_WINO_WG_SPLITS", "4"))
 
 
-def set_winograd(on: bool, min_c: int = None):
-    global _WINO, _WINO_MIN_C
+def set_winograd(on: bool, min_c: int = None, tile=None):
+    """Winograd on/off, its channel threshold and tile size (2, 4 or "auto")."""
+    global _WINO, _WINO_MIN_C, _WINO_TILE
     _WINO = bool(on)
     if min_c is not None:
         _WINO_MIN_C = int(min_c)
+    if tile is not None:
+        _WINO_TILE = str(tile)
 
 
 def _pow2(v):
     return v > 0 and v & (v - 1) == 0
 
 
-def wino_ok(x, w) -> bool:
-    """Whether the fp32 conv of ``x`` by ``w`` (already :func:`supported`) takes the Winograd
-    path: 3x3, even H and W, N*H*W/4 % 64 == 0, power-of-two channel counts in
-    [_WINO_MIN_C, 1024]."""
+def _wino_fits(N, C, Nc, H, W, m):
+    t = N * (H // m) * (W // m)
+    return (H % m == 0 and W % m == 0 and t % 64 == 0 and _pow2(C) and _pow2(Nc)
+            and max(C, Nc) <= (1024 if m == 2 else 512)
+            and (m + 2) ** 2 * t * max(C, Nc) < 2 ** 31)
+
+
+def wino_tile(x, w) -> int:
+    """The Winograd output tile m (2 or 4) the fp32 conv of ``x`` by ``w`` takes, 0 for none:
+    3x3, power-of-two channel counts in [_WINO_MIN_C, 1024 (m = 2) / 512 (m = 4)], H and W
+    multiples of m, N*H*W/m^2 % 64 == 0."""
     if not _WINO or x.dtype != torch.float32 or w.shape[-1] != 3:
-        return False
+        return 0
     N, C, H, W = x.shape
     Nc = w.shape[0]
-    t = N * (H // 2) * (W // 2)
-    return (H % 2 == 0 and W % 2 == 0 and t % 64 == 0 and _pow2(C) and _pow2(Nc)
-            and _WINO_MIN_C <= min(C, Nc) and max(C, Nc) <= 1024
-            and 16 * t * max(C, Nc) < 2 ** 31)
+    if min(C, Nc) < _WINO_MIN_C:
+        return 0
+    order = {"2": (2,), "4": (4,)}.get(_WINO_TILE, (4, 2))
+    for m in order:
+        if _wino_fits(N, C, Nc, H, W, m):
+            return m
+    return 0
+
+
+def wino_ok(x, w) -> bool:
+    return wino_tile(x, w) > 0
 
 
 def epilogue_fusion_ok(x) -> bool:
@@ -193,16 +215,18 @@ class _Conv(torch.autograd.Function):
         # the following fused BN (ops/nn.py bn_act) skips its statistics pass when present
         part = torch.empty(_part_floats(N * H * W, Nc), dtype=torch.float32, device=x.device)
         ctx.wino = None
-        if wino_ok(x, w):
-            # transformed weight U[16][Nc][C], kept for the backward-data GEMMs (read flipped)
-            U = torch.empty(16 * Nc * C, dtype=torch.float32, device=x.device)
-            t = N * (H // 2) * (W // 2)
-            # V (the transformed input) is kept for the weight-gradient GEMMs
-            V = torch.empty(16 * t * C, dtype=torch.float32, device=x.device)
-            Mo = torch.empty(16 * t * Nc, dtype=torch.float32, device=x.device)
+        m = wino_tile(x, w)
+        if m:
+            aa = (m + 2) ** 2
+            # transformed weight U[a^2][Nc][C] (m = 2: kept for the backward-data GEMMs, read
+            # flipped) and input V (kept for the weight-gradient GEMMs)
+            U = torch.empty(aa * Nc * C, dtype=torch.float32, device=x.device)
+            t = N * (H // m) * (W // m)
+            V = torch.empty(aa * t * C, dtype=torch.float32, device=x.device)
+            Mo = torch.empty(aa * t * Nc, dtype=torch.float32, device=x.device)
             rows = C_.wino_f32_fwd(_ptr(x), _ptr(w), _ptr(U), _ptr(y), _ptr(V), _ptr(Mo), N, H, W,
-                                   C, Nc, _ptr(part), part.numel(), _stream())
-            ctx.wino = (U, V)
+                                   C, Nc, m, _ptr(part), part.numel(), _stream())
+            ctx.wino = (U if m == 2 else None, V, m)
         else:
             fwd = C_.conv_f32_fwd if x.dtype == torch.float32 else C_.conv_fwd
             rows = fwd(_ptr(x), _ptr(w), _ptr(y), _ptr(ws), ws.numel(), N, H, W, C, Nc, k,
@@ -227,9 +251,11 @@ class _Conv(torch.autograd.Function):
         bwd_data = C_.conv_f32_bwd_data if f32 else C_.conv_bwd_data
         dx = dw = None
         D = None  # Winograd: the weight gradient's dy transform, made by the bwd-data pass
-        if ctx.wino is not None and ctx.needs_input_grad[1]:
-            D = torch.empty(16 * N * (H // 2) * (W // 2) * Nc, dtype=torch.float32,
-                            device=x.device)
+        m = ctx.wino[2] if ctx.wino is not None else 0
+        aa = (m + 2) ** 2
+        t = N * (H // m) * (W // m) if m else 0
+        if m and ctx.needs_input_grad[1]:
+            D = torch.empty(aa * t * Nc, dtype=torch.float32, device=x.device)
         d_ready = 0
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x, memory_format=torch.channels_last)
@@ -243,15 +269,18 @@ class _Conv(torch.autograd.Function):
                                         and add.data_ptr() % 16 == 0):
                 add = add.contiguous(memory_format=torch.channels_last).to(x.dtype)
             link = _bn_bwd_link(node, x)
-            U = ctx.wino[0] if ctx.wino is not None else None
-            if U is not None:
-                t = N * (H // 2) * (W // 2)
-                buf = torch.empty(16 * t * (C + Nc), dtype=torch.float32, device=x.device)
+            if m:
+                # m = 2: the forward's U, read flipped; m = 4: the rotated kernel's transform
+                # is made here (U2), in the backward input launch
+                U = ctx.wino[0]
+                if U is None:
+                    U = torch.empty(aa * Nc * C, dtype=torch.float32, device=x.device)
+                buf = torch.empty(aa * t * (C + Nc), dtype=torch.float32, device=x.device)
 
                 def bwd_data(dy_, w_, dx_, ws_, wsn, *rest):  # same contract, Winograd
-                    return C_.wino_f32_bwd_data(dy_, _ptr(U), dx_, _ptr(buf),
-                                                _ptr(buf) + 64 * t * Nc, *rest[:5], *rest[6:-1],
-                                                _ptr(D), rest[-1])
+                    return C_.wino_f32_bwd_data(dy_, w_, _ptr(U), dx_, _ptr(buf),
+                                                _ptr(buf) + 4 * aa * t * Nc, *rest[:5], m,
+                                                *rest[6:-1], _ptr(D), rest[-1])
                 d_ready = int(D is not None)
             if link is None:
                 bwd_data(_ptr(dy), _ptr(w), _ptr(dx), _ptr(ws), ws.numel(), N, H, W, C, Nc, k, 0,
@@ -270,14 +299,14 @@ class _Conv(torch.autograd.Function):
                 sink.grad = None
         if ctx.needs_input_grad[1]:
             dw = torch.empty_like(w, memory_format=torch.channels_last)
-            if ctx.wino is not None:
-                # dw = G^T (sum over tiles of (A dy A^T) V) G: 16 GEMMs of K = N*H*W/4
+            if m:
+                # dw = G^T (sum over tiles of (A dy A^T) V) G: a^2 GEMMs of K = N*H*W/m^2
                 V = ctx.wino[1]
-                dU = torch.empty(16 * Nc * C, dtype=torch.float32, device=x.device)
-                slabs = torch.empty(_WINO_WG_SPLITS * 16 * Nc * C + 64, dtype=torch.float32,
+                dU = torch.empty(aa * Nc * C, dtype=torch.float32, device=x.device)
+                slabs = torch.empty(_WINO_WG_SPLITS * aa * Nc * C + 64, dtype=torch.float32,
                                     device=x.device)
                 C_.wino_f32_wgrad(_ptr(dy), _ptr(V), _ptr(dw), _ptr(D), d_ready, _ptr(dU),
-                                  _ptr(slabs), slabs.numel(), N, H, W, C, Nc, _stream())
+                                  _ptr(slabs), slabs.numel(), N, H, W, C, Nc, m, _stream())
             else:
                 wgrad = C_.conv_f32_wgrad if f32 else C_.conv_wgrad
                 wgrad(_ptr(dy), _ptr(x), _ptr(dw), _ptr(ws), ws.numel(), N, H, W, C, Nc, k,

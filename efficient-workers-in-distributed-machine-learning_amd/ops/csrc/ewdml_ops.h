@@ -201,22 +201,22 @@ int ew_conv_f32_stem_fwd(uintptr_t x, uintptr_t w, uintptr_t y, long long N, int
 void ew_conv_f32_stem_wgrad(uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws,
                             long long ws_floats, long long N, int H, int W, int Nc,
                             uintptr_t stream);
-// ---- fp32 3x3 convolutions by Winograd F(2x2, 3x3) (winograd_f32.hip): U[16][Nc][C] from the
-// channels_last weight (standalone, or inside the forward when w != 0); forward / backward data
-// over caller-allocated V (16 * N*H*W/4 * C_in floats) and Mo (16 * N*H*W/4 * C_out floats);
-// return the BN partial rows written (0: none)
-void ew_wino_f32_weight(uintptr_t w, uintptr_t U, int Nc, int C, uintptr_t stream);
+// ---- fp32 3x3 convolutions by Winograd F(m x m, 3x3), m = 2 or 4 (winograd_f32.hip): U[a^2][Nc][C]
+// (a = m + 2) from the channels_last weight (standalone, or inside the forward when w != 0);
+// forward / backward data over caller-allocated V (a^2 * N*H*W/m^2 * C_in floats) and Mo
+// (a^2 * N*H*W/m^2 * C_out floats); return the BN partial rows written (0: none)
+void ew_wino_f32_weight(uintptr_t w, uintptr_t U, int Nc, int C, int m, uintptr_t stream);
 int ew_wino_f32_fwd(uintptr_t x, uintptr_t w, uintptr_t U, uintptr_t y, uintptr_t V, uintptr_t Mo,
-                    long long N, int H, int W, int C, int Nc, uintptr_t bnpart,
+                    long long N, int H, int W, int C, int Nc, int m, uintptr_t bnpart,
                     long long bnpart_floats, uintptr_t stream);
-int ew_wino_f32_bwd_data(uintptr_t dy, uintptr_t U, uintptr_t dx, uintptr_t V, uintptr_t Mo,
-                         long long N, int H, int W, int C, int Nc, uintptr_t bn_h,
-                         uintptr_t bn_res, uintptr_t bn_code, uintptr_t bn_stats, int bn_relu,
-                         uintptr_t bnpart, long long bnpart_floats, uintptr_t addend,
-                         uintptr_t D, uintptr_t stream);
+int ew_wino_f32_bwd_data(uintptr_t dy, uintptr_t w, uintptr_t U, uintptr_t dx, uintptr_t V,
+                         uintptr_t Mo, long long N, int H, int W, int C, int Nc, int m,
+                         uintptr_t bn_h, uintptr_t bn_res, uintptr_t bn_code, uintptr_t bn_stats,
+                         int bn_relu, uintptr_t bnpart, long long bnpart_floats,
+                         uintptr_t addend, uintptr_t D, uintptr_t stream);
 void ew_wino_f32_wgrad(uintptr_t dy, uintptr_t V, uintptr_t dw, uintptr_t D, int d_ready,
                        uintptr_t U_scratch, uintptr_t ws, long long ws_floats, long long N, int H,
-                       int W, int C, int Nc, uintptr_t stream);
+                       int W, int C, int Nc, int m, uintptr_t stream);
 
 // ---- RCCL communicator issuing collectives on the caller's stream (rccl_comm.hip) ----
 // dtype codes: 0 f32, 1 bf16, 2 f16, 3 u8, 4 i32, 5 f64, 6 i64; op: 0 sum, 1 max, 2 min, 3 avg

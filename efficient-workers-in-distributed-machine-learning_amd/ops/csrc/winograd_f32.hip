@@ -1,30 +1,40 @@
-// fp32 3x3 (pad 1, stride 1) convolutions by Winograd F(2x2, 3x3): forward and backward-data.
+// fp32 3x3 (pad 1, stride 1) convolutions by Winograd F(m x m, 3x3), m = 2 or 4: forward,
+// backward-data and weight-gradient.
 //
-// Each 2x2 output tile is A^T [ (G g G^T) .* (B^T d B) ] A over the 4x4 input patch d, so the
-// 9-tap implicit GEMM of conv_f32.hip (2*P*C*Nc*9 FLOPs) becomes 16 batched GEMMs over the
-// tiles (2*(P/4)*16*C*Nc FLOPs, 2.25x fewer):
+// Each m x m output tile is A^T [ (G g G^T) .* (B^T d B) ] A over the a x a input patch d
+// (a = m + 2), so the 9-tap implicit GEMM of conv_f32.hip (2*P*C*Nc*9 FLOPs) becomes a*a batched
+// GEMMs over the tiles (2*(P/m^2)*a^2*C*Nc FLOPs: 2.25x fewer at m = 2, 4x at m = 4):
 //
 //   U[xi][Nc][C]    = (G g G^T)[xi]           weight transform, once per step
 //   V[xi][tiles][C] = (B^T d B)[xi]           input transform (one launch for both: k_wg_input)
-//   Mo[xi][tiles][Nc] = V[xi] U[xi]^T          16 fp32 MFMA GEMMs (conv_f32.hip k_cf_gemm, batched)
+//   Mo[xi][tiles][Nc] = V[xi] U[xi]^T          a^2 fp32 MFMA GEMMs (conv_f32.hip k_cf_gemm, batched)
 //   y = A^T Mo A                              output transform (k_wg_output), with the BatchNorm
 //                                             partial sums (forward) or the producing BN layer's
 //                                             backward sums + residual addend (backward data)
 //
 // Backward data is the same pipeline on dy with the 180-degree-rotated kernel and the channel
-// roles swapped; since G J = P G (J: column reversal, P: rows 0 <-> 3), its transformed weight is
-// the forward U read transposed with positions (i, j) -> (p(i), p(j)): no second weight
-// transform, the GEMM reads U[p(xi)] as a [K = Nc][N = C] image (CfGeom::b_flip).
+// roles swapped.  At m = 2, G J = P G (J: column reversal, P: rows 0 <-> 3), so its transformed
+// weight is the forward U read transposed with positions (i, j) -> (p(i), p(j)) (CfGeom::b_flip:
+// no second weight transform); at m = 4 the points (0, +-1, +-2) are not closed under p -> 1/p
+// and the rotated kernel gets its own transform (in the backward input launch).
 //
-// B^T = [1 0 -1 0; 0 1 1 0; 0 -1 1 0; 0 1 0 -1], G = [1 0 0; .5 .5 .5; .5 -.5 .5; 0 0 1],
-// A^T = [1 1 1 0; 0 1 -1 -1].  All arithmetic fp32 (the transforms add/subtract; G halves):
-// the result differs from the direct convolution by rounding only (tests/kernels/test_conv_f32.py
-// checks both against float64).
+// Weight gradient, the transpose of the forward: dMo = A dy A^T per tile (made by the backward-
+// data input pass from the same reads, or k_wg_dy), dU[xi][Nc][C] = sum over tiles of
+// dMo[xi][tile][Nc] V[xi][tile][C] (the forward's V, kept; one K = tiles GEMM per position,
+// K-split into slabs), then dw = G^T dU G summed over the splits in a fixed order.
+//
+// m = 2: B^T = [1 0 -1 0; 0 1 1 0; 0 -1 1 0; 0 1 0 -1], G = [1 0 0; .5 .5 .5; .5 -.5 .5; 0 0 1],
+//        A^T = [1 1 1 0; 0 1 -1 -1].
+// m = 4: points 0, 1, -1, 2, -2, inf (Lavin & Gray's F(4x4, 3x3)).
+// All arithmetic fp32.  Relative error against float64 (tests/kernels/test_conv_f32.py, and
+// tools/conv_f32_probe.py --err): direct ~2e-7, m = 2 ~5e-7, m = 4 ~3e-6 -- every form far inside
+// fp32 training noise and 100x below tf32 / 1000x below bf16 operand rounding.
 //
 // Why unfused transforms: on the deep VGG / ResNet layers (C >= 128, maps <= 16x16) the GEMM
-// dominates and V / Mo (4x the activations) stay in the 256 MB MALL; ops/conv.py only routes a
-// layer here where that holds (the per-layer choice is measured: tools/conv_f32_probe.py --wino).
+// dominates and V / Mo stay in the 256 MB MALL; ops/conv.py only routes a layer here where that
+// holds (the per-layer choice is measured: tools/conv_f32_probe.py --wino).
 #include <stdexcept>
+#include <string>
 
 #include "common.h"
 #include "conv_f32.h"
@@ -39,129 +49,257 @@ void ew_cf_gemm_batched(const float* a, const float* b, float* out, int M, int N
 
 namespace {
 
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-// U[xi][o][i..i+3] = (G g G^T)[xi], g(r, s) = w[o][r][s][i..i+3] (channels_last [Nc][3][3][C])
-__device__ __forceinline__ void wg_weight(const float* __restrict__ w, float* __restrict__ U,
-                                          int Nc, int C, long long g) {
-  const int cq = C >> 2;
-  if (g >= (long long)Nc * cq) return;
-  const int o = (int)(g / cq), i = (int)(g - (long long)o * cq) * 4;
-  f32x4 k[3][3];
-#pragma unroll
-  for (int r = 0; r < 3; ++r)
-#pragma unroll
-    for (int s = 0; s < 3; ++s)
-      k[r][s] = *reinterpret_cast<const f32x4*>(w + ((long long)o * 9 + r * 3 + s) * C + i);
-  f32x4 t[4][3];  // G g
-#pragma unroll
-  for (int s = 0; s < 3; ++s) {
-    t[0][s] = k[0][s];
-    t[1][s] = 0.5f * (k[0][s] + k[1][s] + k[2][s]);
-    t[2][s] = 0.5f * (k[0][s] - k[1][s] + k[2][s]);
-    t[3][s] = k[2][s];
-  }
-  const long long xs = (long long)Nc * C;
-  float* u = U + (long long)o * C + i;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {  // (G g) G^T
-    *reinterpret_cast<f32x4*>(u + (r * 4 + 0) * xs) = t[r][0];
-    *reinterpret_cast<f32x4*>(u + (r * 4 + 1) * xs) = 0.5f * (t[r][0] + t[r][1] + t[r][2]);
-    *reinterpret_cast<f32x4*>(u + (r * 4 + 2) * xs) = 0.5f * (t[r][0] - t[r][1] + t[r][2]);
-    *reinterpret_cast<f32x4*>(u + (r * 4 + 3) * xs) = t[r][2];
+// Transform matrices as constexpr functions: inside fully unrolled loops every coefficient is a
+// compile-time constant, zero terms are skipped at the source (0 * x is not foldable in IEEE)
+// and +-1 products fold to adds / subtracts.
+template <int M>
+__device__ constexpr float wg_bt(int i, int j) {
+  if constexpr (M == 2) {
+    constexpr float v[4][4] = {{1, 0, -1, 0}, {0, 1, 1, 0}, {0, -1, 1, 0}, {0, 1, 0, -1}};
+    return v[i][j];
+  } else {
+    constexpr float v[6][6] = {{4, 0, -5, 0, 1, 0},  {0, -4, -4, 1, 1, 0}, {0, 4, -4, -1, 1, 0},
+                               {0, -2, -1, 2, 1, 0}, {0, 2, -1, -2, 1, 0}, {0, 4, 0, -5, 0, 1}};
+    return v[i][j];
   }
 }
 
-// V[xi][tile][c..c+3] = (B^T d B)[xi], d = the 4x4 patch at (2 ty - 1, 2 tx - 1) of x[N][H][W][C]
-// (zero outside).  Thread: one tile x one channel quad; consecutive threads, consecutive quads.
-__device__ __forceinline__ void wg_dy_store(float* __restrict__ D, long long xs, f32x4 d00,
-                                            f32x4 d01, f32x4 d10, f32x4 d11);
+template <int M>
+__device__ constexpr float wg_g(int i, int j) {
+  if constexpr (M == 2) {
+    constexpr float v[4][3] = {{1, 0, 0}, {.5f, .5f, .5f}, {.5f, -.5f, .5f}, {0, 0, 1}};
+    return v[i][j];
+  } else {
+    constexpr float v[6][3] = {{1.f / 4, 0, 0},
+                               {-1.f / 6, -1.f / 6, -1.f / 6},
+                               {-1.f / 6, 1.f / 6, -1.f / 6},
+                               {1.f / 24, 1.f / 12, 1.f / 6},
+                               {1.f / 24, -1.f / 12, 1.f / 6},
+                               {0, 0, 1}};
+    return v[i][j];
+  }
+}
 
-// (with D: also the weight-gradient transform A dy A^T of the patch's inner 2x2, see k_wg_dy)
+template <int M>
+__device__ constexpr float wg_at(int i, int j) {
+  if constexpr (M == 2) {
+    constexpr float v[2][4] = {{1, 1, 1, 0}, {0, 1, -1, -1}};
+    return v[i][j];
+  } else {
+    constexpr float v[4][6] = {
+        {1, 1, 1, 1, 1, 0}, {0, 1, -1, 2, -2, 0}, {0, 1, 1, 4, 4, 0}, {0, 1, -1, 8, -8, 1}};
+    return v[i][j];
+  }
+}
+
+template <int M>
+struct Wg {
+  static constexpr int A = M + 2;             // patch / transform size
+  static constexpr int VW = M == 2 ? 4 : 2;   // channels per thread (registers: A*A vectors)
+  typedef float V __attribute__((ext_vector_type(VW)));
+};
+
+// sum_k c(k) * x[k] over the nonzero constant coefficients (CF: coefficient function)
+template <int N, typename T, typename CF>
+__device__ __forceinline__ T wg_dot(CF cf, const T* x) {
+  T acc{};
+  bool first = true;
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    const float c = cf(k);
+    if (c == 0.0f) continue;
+    const T term = c == 1.0f ? x[k] : c == -1.0f ? -x[k] : c * x[k];
+    acc = first ? term : acc + term;
+    first = false;
+  }
+  return acc;
+}
+
+// U[xi][o][i..] = (G g G^T)[xi], g(r, s) = w[o][r][s][i..] (channels_last [Nc][3][3][C]);
+// FLIP: the 180-degree-rotated kernel g(r, s) = w[o][2-r][2-s][i..] (backward data at m = 4)
+template <int M, bool FLIP>
+__device__ __forceinline__ void wg_weight(const float* __restrict__ w, float* __restrict__ U,
+                                          int Nc, int C, long long g) {
+  using T = typename Wg<M>::V;
+  constexpr int A = Wg<M>::A, VW = Wg<M>::VW;
+  const int cq = C / VW;
+  if (g >= (long long)Nc * cq) return;
+  const int o = (int)(g / cq), i = (int)(g - (long long)o * cq) * VW;
+  T k[3][3];
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      const int tap = FLIP ? (2 - r) * 3 + (2 - s) : r * 3 + s;
+      k[r][s] = *reinterpret_cast<const T*>(w + ((long long)o * 9 + tap) * C + i);
+    }
+  const long long xs = (long long)Nc * C;
+  float* u = U + (long long)o * C + i;
+#pragma unroll
+  for (int a = 0; a < A; ++a) {
+    T t[3];  // row a of G g
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      const T col[3] = {k[0][s], k[1][s], k[2][s]};
+      t[s] = wg_dot<3>([&](int r) { return wg_g<M>(a, r); }, col);
+    }
+#pragma unroll
+    for (int b = 0; b < A; ++b)  // (G g) G^T
+      *reinterpret_cast<T*>(u + (a * A + b) * xs) =
+          wg_dot<3>([&](int s) { return wg_g<M>(b, s); }, t);
+  }
+}
+
+// dMo = A dy A^T of one m x m dy tile (rows dy[i][j]), stored at o[xi * xs]
+template <int M>
+__device__ __forceinline__ void wg_dy_store(float* __restrict__ o, long long xs,
+                                            const typename Wg<M>::V (&dy)[M][M]) {
+  using T = typename Wg<M>::V;
+  constexpr int A = Wg<M>::A;
+#pragma unroll
+  for (int a = 0; a < A; ++a) {
+    T t[M];  // row a of A dy = sum_i AT[i][a] dy[i][.]
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+      T col[M];
+#pragma unroll
+      for (int i = 0; i < M; ++i) col[i] = dy[i][j];
+      t[j] = wg_dot<M>([&](int i) { return wg_at<M>(i, a); }, col);
+    }
+#pragma unroll
+    for (int b = 0; b < A; ++b)
+      *reinterpret_cast<T*>(o + (a * A + b) * xs) =
+          wg_dot<M>([&](int j) { return wg_at<M>(j, b); }, t);
+  }
+}
+
+// V[xi][tile][c..] = (B^T d B)[xi], d = the a x a patch at (m ty - 1, m tx - 1) of x[N][H][W][C]
+// (zero outside).  Thread: one tile x one channel vector; consecutive threads, consecutive
+// vectors.  With D: also the weight gradient's dMo of the patch's inner m x m (the dy tile).
+template <int M>
 __device__ __forceinline__ void wg_input(const float* __restrict__ x, float* __restrict__ V,
                                          int H, int W, int C, long long tiles, long long g,
-                                         float* __restrict__ D = nullptr) {
-  const int cq = C >> 2;
+                                         float* __restrict__ D) {
+  using T = typename Wg<M>::V;
+  constexpr int A = Wg<M>::A, VW = Wg<M>::VW;
+  const int cq = C / VW;
   if (g >= tiles * cq) return;
   const long long tl = g / cq;
-  const int c = (int)(g - tl * cq) * 4;
-  const int tw = W >> 1, tpi = (H >> 1) * tw;
+  const int c = (int)(g - tl * cq) * VW;
+  const int tw = W / M, tpi = (H / M) * tw;
   const int n = (int)(tl / tpi), rem = (int)(tl - (long long)n * tpi);
   const int ty = rem / tw, tx = rem - ty * tw;
-  const int h0 = 2 * ty - 1, w0 = 2 * tx - 1;
-  f32x4 d[4][4];
+  const int h0 = M * ty - 1, w0 = M * tx - 1;
+  T d[A][A];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < A; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < A; ++j) {
       const int h = h0 + i, w = w0 + j;
       const bool ok = (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
-      const f32x4 v = *reinterpret_cast<const f32x4*>(
-          x + (ok ? (((long long)n * H + h) * W + w) * C + c : c));
-      d[i][j] = ok ? v : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+      const T v = *reinterpret_cast<const T*>(x + (ok ? (((long long)n * H + h) * W + w) * C + c
+                                                      : c));
+      d[i][j] = ok ? v : T{};
     }
-  if (D) wg_dy_store(D + tl * C + c, tiles * C, d[1][1], d[1][2], d[2][1], d[2][2]);
-  f32x4 t[4][4];  // B^T d
+  if (D) {
+    T dy[M][M];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    t[0][j] = d[0][j] - d[2][j];
-    t[1][j] = d[1][j] + d[2][j];
-    t[2][j] = d[2][j] - d[1][j];
-    t[3][j] = d[1][j] - d[3][j];
+    for (int i = 0; i < M; ++i)
+#pragma unroll
+      for (int j = 0; j < M; ++j) dy[i][j] = d[i + 1][j + 1];
+    wg_dy_store<M>(D + tl * C + c, tiles * C, dy);
   }
   const long long xs = tiles * C;
   float* v = V + tl * C + c;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {  // (B^T d) B
-    *reinterpret_cast<f32x4*>(v + (i * 4 + 0) * xs) = t[i][0] - t[i][2];
-    *reinterpret_cast<f32x4*>(v + (i * 4 + 1) * xs) = t[i][1] + t[i][2];
-    *reinterpret_cast<f32x4*>(v + (i * 4 + 2) * xs) = t[i][2] - t[i][1];
-    *reinterpret_cast<f32x4*>(v + (i * 4 + 3) * xs) = t[i][1] - t[i][3];
+  for (int a = 0; a < A; ++a) {
+    T t[A];  // row a of B^T d
+#pragma unroll
+    for (int j = 0; j < A; ++j) {
+      T col[A];
+#pragma unroll
+      for (int i = 0; i < A; ++i) col[i] = d[i][j];
+      t[j] = wg_dot<A>([&](int i) { return wg_bt<M>(a, i); }, col);
+    }
+#pragma unroll
+    for (int b = 0; b < A; ++b)  // (B^T d) B
+      *reinterpret_cast<T*>(v + (a * A + b) * xs) =
+          wg_dot<A>([&](int j) { return wg_bt<M>(b, j); }, t);
   }
 }
 
 // the input transform over blocks [0, nbi) and, when w is given, the weight transform over the
 // rest (one launch for both: each alone is a few-microsecond kernel)
+template <int M, bool FLIP>
 __global__ __launch_bounds__(EW_BLOCK) void k_wg_input(const float* __restrict__ x,
                                                        float* __restrict__ V, int H, int W, int C,
                                                        long long tiles, int nbi,
                                                        const float* __restrict__ w,
-                                                       float* __restrict__ U, int Nc,
+                                                       float* __restrict__ U, int Nw, int Cw,
                                                        float* __restrict__ D) {
   if ((int)blockIdx.x < nbi)
-    wg_input(x, V, H, W, C, tiles, (long long)blockIdx.x * EW_BLOCK + threadIdx.x, D);
+    wg_input<M>(x, V, H, W, C, tiles, (long long)blockIdx.x * EW_BLOCK + threadIdx.x, D);
   else
-    wg_weight(w, U, Nc, C, (long long)(blockIdx.x - nbi) * EW_BLOCK + threadIdx.x);
+    wg_weight<M, FLIP>(w, U, Nw, Cw, (long long)(blockIdx.x - nbi) * EW_BLOCK + threadIdx.x);
 }
 
+template <int M>
 __global__ __launch_bounds__(EW_BLOCK) void k_wg_weight(const float* __restrict__ w,
                                                         float* __restrict__ U, int Nc, int C) {
-  wg_weight(w, U, Nc, C, (long long)blockIdx.x * EW_BLOCK + threadIdx.x);
+  wg_weight<M, false>(w, U, Nc, C, (long long)blockIdx.x * EW_BLOCK + threadIdx.x);
+}
+
+// dMo of dy alone (weight gradient without a Winograd backward-data pass before it)
+template <int M>
+__global__ __launch_bounds__(EW_BLOCK) void k_wg_dy(const float* __restrict__ dy,
+                                                    float* __restrict__ D, int H, int W, int Nc,
+                                                    long long tiles) {
+  using T = typename Wg<M>::V;
+  constexpr int VW = Wg<M>::VW;
+  const int cq = Nc / VW;
+  const long long g = (long long)blockIdx.x * EW_BLOCK + threadIdx.x;
+  if (g >= tiles * cq) return;
+  const long long tl = g / cq;
+  const int c = (int)(g - tl * cq) * VW;
+  const int tw = W / M, tpi = (H / M) * tw;
+  const int n = (int)(tl / tpi), rem = (int)(tl - (long long)n * tpi);
+  const int ty = rem / tw, tx = rem - ty * tw;
+  const float* p = dy + (((long long)n * H + M * ty) * W + M * tx) * Nc + c;
+  T t[M][M];
+#pragma unroll
+  for (int i = 0; i < M; ++i)
+#pragma unroll
+    for (int j = 0; j < M; ++j)
+      t[i][j] = *reinterpret_cast<const T*>(p + ((long long)i * W + j) * Nc);
+  wg_dy_store<M>(D + tl * Nc + c, tiles * Nc, t);
 }
 
 // y = A^T Mo A per tile (+ addend), with the BatchNorm partial sums of y (forward: sum, sum of
 // squares; backward: CfBnBwd's sum dz, sum dz * (h - mean)) -> row blockIdx.x of bnpart[2][nb][Nc].
-// Block: tiles [b * tpb, (b + 1) * tpb) x all Nc channels; thread: channel quad t % (Nc / 4),
-// tiles t / (Nc / 4) + k * rpi (rpi = 256 / (Nc / 4) tiles per pass, Nc a power of two <= 1024).
+// Block: tiles [b * tpb, (b + 1) * tpb) x all Nc channels; thread: channel vector t % (Nc / VW),
+// tiles t / (Nc / VW) + k * rpi (rpi = 256 / (Nc / VW) tiles per pass, Nc a power of two).
+template <int M>
 __global__ __launch_bounds__(EW_BLOCK) void k_wg_output(const float* __restrict__ Mo,
                                                         float* __restrict__ y, int H, int W,
                                                         int Nc, long long tiles, int tpb,
                                                         float* __restrict__ bnpart, CfBnBwd bb,
                                                         const float* __restrict__ addend) {
+  using T = typename Wg<M>::V;
+  constexpr int A = Wg<M>::A, VW = Wg<M>::VW;
   __shared__ float red[2][EW_BLOCK * 4];
-  const int tpr = Nc >> 2, rpi = EW_BLOCK / tpr;
-  const int t = threadIdx.x, rg = t / tpr, c0 = (t - rg * tpr) * 4;
+  const int tpr = Nc / VW, rpi = EW_BLOCK / tpr;
+  const int t = threadIdx.x, rg = t / tpr, c0 = (t - rg * tpr) * VW;
   const long long t0 = (long long)blockIdx.x * tpb;
   const long long t1 = t0 + tpb < tiles ? t0 + tpb : tiles;
-  const int tw = W >> 1, tpi = (H >> 1) * tw;
+  const int tw = W / M, tpi = (H / M) * tw;
   const long long xs = tiles * Nc;
   const uint32_t HoWo = (uint32_t)bb.Ho * bb.Wo;
-  float s1[4], s2[4], mean[4], sc[4], sh[4];
+  float s1[VW], s2[VW], mean[VW], sc[VW], sh[VW];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) s1[j] = s2[j] = 0.0f;
+  for (int j = 0; j < VW; ++j) s1[j] = s2[j] = 0.0f;
   if (bnpart && bb.h) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < VW; ++j) {
       mean[j] = bb.stats[c0 + j];
       sc[j] = bb.stats[2 * Nc + c0 + j];
       sh[j] = bb.stats[3 * Nc + c0 + j];
@@ -169,57 +307,51 @@ __global__ __launch_bounds__(EW_BLOCK) void k_wg_output(const float* __restrict_
   }
   for (long long tl = t0 + rg; tl < t1; tl += rpi) {
     const float* mp = Mo + tl * Nc + c0;
-    f32x4 m[16];
+    T u[M][A];  // A^T Mo, one column b at a time
 #pragma unroll
-    for (int q = 0; q < 16; ++q) m[q] = *reinterpret_cast<const f32x4*>(mp + q * xs);
-    f32x4 u[2][4];  // A^T Mo
+    for (int b = 0; b < A; ++b) {
+      T col[A];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      u[0][j] = m[j] + m[4 + j] + m[8 + j];
-      u[1][j] = m[4 + j] - m[8 + j] - m[12 + j];
-    }
-    f32x4 o[2][2];  // (A^T Mo) A
+      for (int a = 0; a < A; ++a) col[a] = *reinterpret_cast<const T*>(mp + (a * A + b) * xs);
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      o[i][0] = u[i][0] + u[i][1] + u[i][2];
-      o[i][1] = u[i][1] - u[i][2] - u[i][3];
+      for (int i = 0; i < M; ++i) u[i][b] = wg_dot<A>([&](int a) { return wg_at<M>(i, a); }, col);
     }
     const int n = (int)(tl / tpi), rem = (int)(tl - (long long)n * tpi);
     const int ty = rem / tw, tx = rem - ty * tw;
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+    for (int i = 0; i < M; ++i)
 #pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        const long long r = ((long long)n * H + 2 * ty + a) * W + 2 * tx + b;
+      for (int j = 0; j < M; ++j) {  // (A^T Mo) A
+        T v = wg_dot<A>([&](int b) { return wg_at<M>(j, b); }, u[i]);
+        const long long r = ((long long)n * H + M * ty + i) * W + M * tx + j;
         const long long off = r * Nc + c0;
-        f32x4 v = o[a][b];
-        if (addend) v += *reinterpret_cast<const f32x4*>(addend + off);
-        *reinterpret_cast<f32x4*>(y + off) = v;
+        if (addend) v += *reinterpret_cast<const T*>(addend + off);
+        *reinterpret_cast<T*>(y + off) = v;
         if (!bnpart) continue;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float dv = v[j];
+        for (int q = 0; q < VW; ++q) {
+          const float dv = v[q];
           if (bb.h) {
             uint32_t hr = (uint32_t)r;
-            if (bb.code) hr = cf_pool_row((uint32_t)r, HoWo, (uint32_t)bb.Wo, bb.code[off + j]);
-            const float xh = bb.h[(size_t)hr * Nc + c0 + j];
-            float z = xh * sc[j] + sh[j];
-            if (bb.res) z = z + bb.res[(size_t)hr * Nc + c0 + j];
+            if (bb.code) hr = cf_pool_row((uint32_t)r, HoWo, (uint32_t)bb.Wo, bb.code[off + q]);
+            const float xh = bb.h[(size_t)hr * Nc + c0 + q];
+            float z = xh * sc[q] + sh[q];
+            if (bb.res) z = z + bb.res[(size_t)hr * Nc + c0 + q];
             const float dz = (bb.relu == 0 || !(z <= 0.0f)) ? dv : 0.0f;
-            s1[j] += dz;
-            s2[j] += dz * (xh - mean[j]);
+            s1[q] += dz;
+            s2[q] += dz * (xh - mean[q]);
           } else {
-            s1[j] += dv;
-            s2[j] += dv * dv;
+            s1[q] += dv;
+            s2[q] += dv * dv;
           }
         }
       }
   }
   if (!bnpart) return;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    red[0][rg * Nc + c0 + j] = s1[j];
-    red[1][rg * Nc + c0 + j] = s2[j];
+  for (int q = 0; q < VW; ++q) {
+    red[0][rg * Nc + c0 + q] = s1[q];
+    red[1][rg * Nc + c0 + q] = s2[q];
   }
   __syncthreads();
   const int nb = gridDim.x;
@@ -234,100 +366,61 @@ __global__ __launch_bounds__(EW_BLOCK) void k_wg_output(const float* __restrict_
   }
 }
 
-// Weight gradient, the transpose of the forward: dMo = A dy A^T per tile and channel
-// (k_wg_dy), dU[xi][Nc][C] = sum over tiles of dMo[xi][tile][Nc] V[xi][tile][C] (the forward's V,
-// kept for the backward; one K = tiles GEMM per position, K-split into slabs), then
-// dw = G^T dU G summed over the splits in a fixed order (k_wg_wgrad_out).
-// A = [1 0; 1 1; 1 -1; 0 -1], G^T = [1 .5 .5 0; 0 .5 -.5 0; 0 .5 .5 1].
-__global__ __launch_bounds__(EW_BLOCK) void k_wg_dy(const float* __restrict__ dy,
-                                                    float* __restrict__ D, int H, int W, int Nc,
-                                                    long long tiles) {
-  const int cq = Nc >> 2;
-  const long long g = (long long)blockIdx.x * EW_BLOCK + threadIdx.x;
-  if (g >= tiles * cq) return;
-  const long long tl = g / cq;
-  const int c = (int)(g - tl * cq) * 4;
-  const int tw = W >> 1, tpi = (H >> 1) * tw;
-  const int n = (int)(tl / tpi), rem = (int)(tl - (long long)n * tpi);
-  const int ty = rem / tw, tx = rem - ty * tw;
-  const float* p = dy + (((long long)n * H + 2 * ty) * W + 2 * tx) * Nc + c;
-  wg_dy_store(D + tl * Nc + c, tiles * Nc, *reinterpret_cast<const f32x4*>(p),
-              *reinterpret_cast<const f32x4*>(p + Nc),
-              *reinterpret_cast<const f32x4*>(p + (long long)W * Nc),
-              *reinterpret_cast<const f32x4*>(p + (long long)W * Nc + Nc));
-}
-
-__device__ __forceinline__ void wg_dy_store(float* __restrict__ o, long long xs, f32x4 d00,
-                                            f32x4 d01, f32x4 d10, f32x4 d11) {
-  f32x4 t[4][2];  // A dy
-  t[0][0] = d00;
-  t[0][1] = d01;
-  t[1][0] = d00 + d10;
-  t[1][1] = d01 + d11;
-  t[2][0] = d00 - d10;
-  t[2][1] = d01 - d11;
-  t[3][0] = -d10;
-  t[3][1] = -d11;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {  // (A dy) A^T
-    *reinterpret_cast<f32x4*>(o + (i * 4 + 0) * xs) = t[i][0];
-    *reinterpret_cast<f32x4*>(o + (i * 4 + 1) * xs) = t[i][0] + t[i][1];
-    *reinterpret_cast<f32x4*>(o + (i * 4 + 2) * xs) = t[i][0] - t[i][1];
-    *reinterpret_cast<f32x4*>(o + (i * 4 + 3) * xs) = -t[i][1];
-  }
-}
-
-// dw[o][r][s][i..i+3] = (G^T (sum_z dU_z[xi]) G)[r][s], dU_z = src + z * 16 * Nc * C
+// dw[o][r][s][i..] = (G^T (sum_z dU_z[xi]) G)[r][s], dU_z = src + z * A^2 * Nc * C
+template <int M>
 __global__ __launch_bounds__(EW_BLOCK) void k_wg_wgrad_out(const float* __restrict__ src,
                                                            int nsplit, float* __restrict__ dw,
                                                            int Nc, int C) {
-  const int cq = C >> 2;
+  using T = typename Wg<M>::V;
+  constexpr int A = Wg<M>::A, VW = Wg<M>::VW;
+  const int cq = C / VW;
   const long long g = (long long)blockIdx.x * EW_BLOCK + threadIdx.x;
   if (g >= (long long)Nc * cq) return;
-  const int o = (int)(g / cq), i = (int)(g - (long long)o * cq) * 4;
+  const int o = (int)(g / cq), i = (int)(g - (long long)o * cq) * VW;
   const long long xs = (long long)Nc * C;
   const float* p = src + (long long)o * C + i;
-  f32x4 u[16];
+  T t[3][A];  // G^T dU, one column b at a time
 #pragma unroll
-  for (int q = 0; q < 16; ++q) u[q] = *reinterpret_cast<const f32x4*>(p + q * xs);
-  for (int z = 1; z < nsplit; ++z) {  // fixed order
-    const float* pz = p + (long long)z * 16 * xs;
+  for (int b = 0; b < A; ++b) {
+    T col[A];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) u[q] += *reinterpret_cast<const f32x4*>(pz + q * xs);
-  }
-  f32x4 t[3][4];  // G^T dU
+    for (int a = 0; a < A; ++a) col[a] = *reinterpret_cast<const T*>(p + (a * A + b) * xs);
+    for (int z = 1; z < nsplit; ++z) {  // fixed order
+      const float* pz = p + (long long)z * A * A * xs;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    t[0][j] = u[j] + 0.5f * (u[4 + j] + u[8 + j]);
-    t[1][j] = 0.5f * (u[4 + j] - u[8 + j]);
-    t[2][j] = 0.5f * (u[4 + j] + u[8 + j]) + u[12 + j];
+      for (int a = 0; a < A; ++a) col[a] += *reinterpret_cast<const T*>(pz + (a * A + b) * xs);
+    }
+#pragma unroll
+    for (int r = 0; r < 3; ++r) t[r][b] = wg_dot<A>([&](int a) { return wg_g<M>(a, r); }, col);
   }
   float* w = dw + (long long)o * 9 * C + i;
 #pragma unroll
-  for (int r = 0; r < 3; ++r) {  // (G^T dU) G
-    *reinterpret_cast<f32x4*>(w + (r * 3 + 0) * C) = t[r][0] + 0.5f * (t[r][1] + t[r][2]);
-    *reinterpret_cast<f32x4*>(w + (r * 3 + 1) * C) = 0.5f * (t[r][1] - t[r][2]);
-    *reinterpret_cast<f32x4*>(w + (r * 3 + 2) * C) = 0.5f * (t[r][1] + t[r][2]) + t[r][3];
-  }
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int s = 0; s < 3; ++s)  // (G^T dU) G
+      *reinterpret_cast<T*>(w + (r * 3 + s) * C) =
+          wg_dot<A>([&](int b) { return wg_g<M>(b, s); }, t[r]);
 }
 
-long long wg_tiles(long long N, int H, int W) { return N * (H / 2) * (W / 2); }
+long long wg_tiles(int m, long long N, int H, int W) { return N * (H / m) * (W / m); }
 
-void wg_check(long long N, int H, int W, int Cin, int Cout, const char* what) {
-  const long long tiles = wg_tiles(N, H, W);
-  const bool pow2 = Cout >= 4 && Cout <= 1024 && (Cout & (Cout - 1)) == 0;
-  if (H % 2 || W % 2 || tiles % 64 || Cin % 32 || Cout % 64 || !pow2 ||
-      16 * tiles * (long long)std::max(Cin, Cout) >= (1LL << 31))
+void wg_check(int m, long long N, int H, int W, int Cin, int Cout, const char* what) {
+  const long long tiles = wg_tiles(m, N, H, W);
+  const int vw = m == 2 ? 4 : 2;
+  const bool pow2 = Cout >= 64 && Cout <= 256 * vw && (Cout & (Cout - 1)) == 0;
+  if ((m != 2 && m != 4) || H % m || W % m || tiles % 64 || Cin % 32 || !pow2 ||
+      (long long)(m + 2) * (m + 2) * tiles * std::max(Cin, Cout) >= (1LL << 31))
     throw std::runtime_error(std::string("ewdml winograd f32 ") + what +
-                             ": needs even H, W, N*H*W/4 % 64 == 0, C_in % 32 == 0, C_out a "
-                             "power of two in [64, 1024]");
+                             ": needs m in {2, 4}, H, W % m == 0, N*H*W/m^2 % 64 == 0, C_in % 32 "
+                             "== 0, C_out a power of two in [64, 256 * (m == 2 ? 4 : 2)]");
 }
 
 // output transform launch: returns the BN partial rows written (0: none requested / no room)
+template <int M>
 int wg_output(const float* Mo, float* y, long long N, int H, int W, int Nc, float* bnpart,
               long long bnpart_floats, const CfBnBwd& bb, const float* addend, hipStream_t s) {
-  const long long tiles = wg_tiles(N, H, W);
-  const int rpi = EW_BLOCK / (Nc / 4);
+  const long long tiles = wg_tiles(M, N, H, W);
+  const int rpi = EW_BLOCK / (Nc / Wg<M>::VW);
   long long tpb = rpi, nblk = (tiles + tpb - 1) / tpb;
   if (bnpart) {
     while (nblk > 1024) {
@@ -340,98 +433,135 @@ int wg_output(const float* Mo, float* y, long long N, int H, int W, int Nc, floa
     tpb = rpi;
     nblk = (tiles + tpb - 1) / tpb;
   }
-  hipLaunchKernelGGL(k_wg_output, dim3((unsigned)nblk), dim3(EW_BLOCK), 0, s, Mo, y, H, W, Nc,
+  hipLaunchKernelGGL(k_wg_output<M>, dim3((unsigned)nblk), dim3(EW_BLOCK), 0, s, Mo, y, H, W, Nc,
                      tiles, (int)tpb, bnpart, bb, addend);
   EW_CHECK_LAUNCH();
   return bnpart ? (int)nblk : 0;
 }
 
-// input transform of x [N][H][W][C] into V; with w, also U[16][Nc][C] from w [Nc][3][3][C]
+// input transform of x [N][H][W][C] into V (+ D); with w, also U from w [Nw][3][3][Cw] (FLIP:
+// the rotated kernel)
+template <int M, bool FLIP>
 void wg_input(const float* x, float* V, long long N, int H, int W, int C, hipStream_t s,
-              const float* w = nullptr, float* U = nullptr, int Nc = 0, float* D = nullptr) {
-  const long long n = wg_tiles(N, H, W) * (C / 4);
+              const float* w, float* U, int Nw, int Cw, float* D) {
+  constexpr int VW = Wg<M>::VW;
+  const long long n = wg_tiles(M, N, H, W) * (C / VW);
   const int nbi = (int)((n + EW_BLOCK - 1) / EW_BLOCK);
-  const int nbw = w ? (int)(((long long)Nc * (C / 4) + EW_BLOCK - 1) / EW_BLOCK) : 0;
-  hipLaunchKernelGGL(k_wg_input, dim3(nbi + nbw), dim3(EW_BLOCK), 0, s, x, V, H, W, C,
-                     wg_tiles(N, H, W), nbi, w, U, Nc, D);
+  const int nbw = w ? (int)(((long long)Nw * (Cw / VW) + EW_BLOCK - 1) / EW_BLOCK) : 0;
+  hipLaunchKernelGGL((k_wg_input<M, FLIP>), dim3(nbi + nbw), dim3(EW_BLOCK), 0, s, x, V, H, W, C,
+                     wg_tiles(M, N, H, W), nbi, w, U, Nw, Cw, D);
+  EW_CHECK_LAUNCH();
+}
+
+template <int M>
+int wino_fwd(const float* x, const float* w, float* U, float* y, float* v, float* mo, long long N,
+             int H, int W, int C, int Nc, float* bnpart, long long bnpart_floats, hipStream_t s) {
+  constexpr int AA = Wg<M>::A * Wg<M>::A;
+  const long long tiles = wg_tiles(M, N, H, W);
+  wg_input<M, false>(x, v, N, H, W, C, s, w, U, Nc, C, nullptr);
+  ew_cf_gemm_batched(v, U, mo, (int)tiles, Nc, C, AA, tiles * C, (long long)Nc * C, tiles * Nc,
+                     true, false, s);
+  const CfBnBwd none{nullptr, nullptr, nullptr, nullptr, 0, 0, 0};
+  return wg_output<M>(mo, y, N, H, W, Nc, bnpart, bnpart_floats, none, nullptr, s);
+}
+
+template <int M>
+int wino_bwd(const float* dy, const float* w, float* U, float* dx, float* v, float* mo,
+             long long N, int H, int W, int C, int Nc, const CfBnBwd& bb, float* bnpart,
+             long long bnpart_floats, const float* addend, float* D, hipStream_t s) {
+  constexpr int AA = Wg<M>::A * Wg<M>::A;
+  const long long tiles = wg_tiles(M, N, H, W);
+  // m = 4: U <- transform of the rotated kernel, in the input launch; m = 2: the forward's U,
+  // read flipped.  Mo'[xi][tile][c] = sum_n V'[xi][tile][n] U'[xi][n][c]
+  if constexpr (M == 4)
+    wg_input<M, true>(dy, v, N, H, W, Nc, s, w, U, Nc, C, D);
+  else
+    wg_input<M, false>(dy, v, N, H, W, Nc, s, nullptr, nullptr, 0, 0, D);
+  ew_cf_gemm_batched(v, U, mo, (int)tiles, C, Nc, AA, tiles * Nc, (long long)Nc * C, tiles * C,
+                     false, M == 2, s);
+  return wg_output<M>(mo, dx, N, H, W, C, bnpart, bnpart_floats, bb, addend, s);
+}
+
+template <int M>
+void wino_wgrad(const float* dy, const float* V, float* dw, float* d, int d_ready, float* du,
+                float* ws, long long ws_floats, long long N, int H, int W, int C, int Nc,
+                hipStream_t s) {
+  constexpr int A = Wg<M>::A, VW = Wg<M>::VW;
+  const long long tiles = wg_tiles(M, N, H, W);
+  if (!d_ready) {
+    const long long n = tiles * (Nc / VW);
+    hipLaunchKernelGGL(k_wg_dy<M>, dim3((unsigned)((n + EW_BLOCK - 1) / EW_BLOCK)),
+                       dim3(EW_BLOCK), 0, s, dy, d, H, W, Nc, tiles);
+    EW_CHECK_LAUNCH();
+  }
+  const int split = ew_cf_gemm_tn_batched(d, V, du, ws, ws_floats, Nc, C, (int)tiles, A * A,
+                                          tiles * Nc, tiles * C, s);
+  const long long m = (long long)Nc * (C / VW);
+  hipLaunchKernelGGL(k_wg_wgrad_out<M>, dim3((unsigned)((m + EW_BLOCK - 1) / EW_BLOCK)),
+                     dim3(EW_BLOCK), 0, s, split > 1 ? ws : du, split, dw, Nc, C);
   EW_CHECK_LAUNCH();
 }
 
 }  // namespace
 
-void ew_wino_f32_weight(uintptr_t w, uintptr_t U, int Nc, int C, uintptr_t stream) {
-  if (C % 4 || Nc <= 0) throw std::runtime_error("ewdml winograd f32: weight needs C % 4 == 0");
-  const long long n = (long long)Nc * (C / 4);
-  hipLaunchKernelGGL(k_wg_weight, dim3((unsigned)((n + EW_BLOCK - 1) / EW_BLOCK)), dim3(EW_BLOCK),
-                     0, (hipStream_t)stream, reinterpret_cast<const float*>(w),
-                     reinterpret_cast<float*>(U), Nc, C);
+void ew_wino_f32_weight(uintptr_t w, uintptr_t U, int Nc, int C, int m, uintptr_t stream) {
+  const int vw = m == 2 ? 4 : 2;
+  if ((m != 2 && m != 4) || C % vw || Nc <= 0)
+    throw std::runtime_error("ewdml winograd f32: weight needs m in {2, 4}, C % 4 == 0");
+  const long long n = (long long)Nc * (C / vw);
+  const dim3 grid((unsigned)((n + EW_BLOCK - 1) / EW_BLOCK));
+  const float* wp = reinterpret_cast<const float*>(w);
+  float* up = reinterpret_cast<float*>(U);
+  if (m == 2)
+    hipLaunchKernelGGL(k_wg_weight<2>, grid, dim3(EW_BLOCK), 0, (hipStream_t)stream, wp, up, Nc, C);
+  else
+    hipLaunchKernelGGL(k_wg_weight<4>, grid, dim3(EW_BLOCK), 0, (hipStream_t)stream, wp, up, Nc, C);
   EW_CHECK_LAUNCH();
 }
 
 int ew_wino_f32_fwd(uintptr_t x, uintptr_t w, uintptr_t U, uintptr_t y, uintptr_t V, uintptr_t Mo,
-                    long long N, int H, int W, int C, int Nc, uintptr_t bnpart,
+                    long long N, int H, int W, int C, int Nc, int m, uintptr_t bnpart,
                     long long bnpart_floats, uintptr_t stream) {
-  wg_check(N, H, W, C, Nc, "forward");
-  hipStream_t s = (hipStream_t)stream;
-  const long long tiles = wg_tiles(N, H, W);
-  float* v = reinterpret_cast<float*>(V);
-  float* mo = reinterpret_cast<float*>(Mo);
-  wg_input(reinterpret_cast<const float*>(x), v, N, H, W, C, s, reinterpret_cast<const float*>(w),
-           reinterpret_cast<float*>(U), Nc);
-  ew_cf_gemm_batched(v, reinterpret_cast<const float*>(U), mo, (int)tiles, Nc, C, 16, tiles * C,
-                     (long long)Nc * C, tiles * Nc, true, false, s);
-  const CfBnBwd none{nullptr, nullptr, nullptr, nullptr, 0, 0, 0};
-  return wg_output(mo, reinterpret_cast<float*>(y), N, H, W, Nc, reinterpret_cast<float*>(bnpart),
-                   bnpart_floats, none, nullptr, s);
+  wg_check(m, N, H, W, C, Nc, "forward");
+  auto* f = m == 2 ? wino_fwd<2> : wino_fwd<4>;
+  return f(reinterpret_cast<const float*>(x), reinterpret_cast<const float*>(w),
+           reinterpret_cast<float*>(U), reinterpret_cast<float*>(y), reinterpret_cast<float*>(V),
+           reinterpret_cast<float*>(Mo), N, H, W, C, Nc, reinterpret_cast<float*>(bnpart),
+           bnpart_floats, (hipStream_t)stream);
 }
 
-int ew_wino_f32_bwd_data(uintptr_t dy, uintptr_t U, uintptr_t dx, uintptr_t V, uintptr_t Mo,
-                         long long N, int H, int W, int C, int Nc, uintptr_t bn_h,
-                         uintptr_t bn_res, uintptr_t bn_code, uintptr_t bn_stats, int bn_relu,
-                         uintptr_t bnpart, long long bnpart_floats, uintptr_t addend,
-                         uintptr_t D, uintptr_t stream) {
-  wg_check(N, H, W, Nc, C, "backward data");
-  hipStream_t s = (hipStream_t)stream;
-  const long long tiles = wg_tiles(N, H, W);
-  float* v = reinterpret_cast<float*>(V);
-  float* mo = reinterpret_cast<float*>(Mo);
-  // D != 0: the weight gradient's dy transform from the same reads (ew_wino_f32_wgrad d_ready)
-  wg_input(reinterpret_cast<const float*>(dy), v, N, H, W, Nc, s, nullptr, nullptr, 0,
-           reinterpret_cast<float*>(D));
-  // Mo'[xi][tile][c] = sum_n V'[xi][tile][n] U[p(xi)][n][c]
-  ew_cf_gemm_batched(v, reinterpret_cast<const float*>(U), mo, (int)tiles, C, Nc, 16, tiles * Nc,
-                     (long long)Nc * C, tiles * C, false, true, s);
+// m = 2: U is the forward's transformed weight (read flipped; w unused); m = 4: U receives the
+// rotated kernel's transform of w here
+int ew_wino_f32_bwd_data(uintptr_t dy, uintptr_t w, uintptr_t U, uintptr_t dx, uintptr_t V,
+                         uintptr_t Mo, long long N, int H, int W, int C, int Nc, int m,
+                         uintptr_t bn_h, uintptr_t bn_res, uintptr_t bn_code, uintptr_t bn_stats,
+                         int bn_relu, uintptr_t bnpart, long long bnpart_floats,
+                         uintptr_t addend, uintptr_t D, uintptr_t stream) {
+  wg_check(m, N, H, W, Nc, C, "backward data");
+  if (m == 4 && !w) throw std::runtime_error("ewdml winograd f32: m = 4 backward needs w");
   const CfBnBwd bb{reinterpret_cast<const float*>(bn_h), reinterpret_cast<const float*>(bn_res),
                    reinterpret_cast<const uint8_t*>(bn_code),
                    reinterpret_cast<const float*>(bn_stats), bn_relu, H, W};
-  return wg_output(mo, reinterpret_cast<float*>(dx), N, H, W, C,
-                   bn_h ? reinterpret_cast<float*>(bnpart) : nullptr, bnpart_floats, bb,
-                   reinterpret_cast<const float*>(addend), s);
+  auto* f = m == 2 ? wino_bwd<2> : wino_bwd<4>;
+  // D != 0: the weight gradient's dMo from the same reads (ew_wino_f32_wgrad d_ready)
+  return f(reinterpret_cast<const float*>(dy), reinterpret_cast<const float*>(w),
+           reinterpret_cast<float*>(U), reinterpret_cast<float*>(dx), reinterpret_cast<float*>(V),
+           reinterpret_cast<float*>(Mo), N, H, W, C, Nc, bb,
+           bn_h ? reinterpret_cast<float*>(bnpart) : nullptr, bnpart_floats,
+           reinterpret_cast<const float*>(addend), reinterpret_cast<float*>(D),
+           (hipStream_t)stream);
 }
 
-// dw (channels_last [Nc][3][3][C]) from dy and the forward's V; D: 16 * tiles * Nc floats;
+// dw (channels_last [Nc][3][3][C]) from dy and the forward's V; D: a^2 * tiles * Nc floats;
 // ws: K-split slabs (the plan uses what fits, ws_floats - 64 of it)
 void ew_wino_f32_wgrad(uintptr_t dy, uintptr_t V, uintptr_t dw, uintptr_t D, int d_ready,
                        uintptr_t U_scratch, uintptr_t ws, long long ws_floats, long long N, int H,
-                       int W, int C, int Nc, uintptr_t stream) {
-  wg_check(N, H, W, C, Nc, "weight gradient");
+                       int W, int C, int Nc, int m, uintptr_t stream) {
+  wg_check(m, N, H, W, C, Nc, "weight gradient");
   if (C % 64) throw std::runtime_error("ewdml winograd f32: weight gradient needs C % 64 == 0");
-  hipStream_t s = (hipStream_t)stream;
-  const long long tiles = wg_tiles(N, H, W);
-  float* d = reinterpret_cast<float*>(D);
-  if (!d_ready) {
-    const long long n = tiles * (Nc / 4);
-    hipLaunchKernelGGL(k_wg_dy, dim3((unsigned)((n + EW_BLOCK - 1) / EW_BLOCK)), dim3(EW_BLOCK),
-                       0, s, reinterpret_cast<const float*>(dy), d, H, W, Nc, tiles);
-    EW_CHECK_LAUNCH();
-  }
-  float* du = reinterpret_cast<float*>(U_scratch);
-  const int split = ew_cf_gemm_tn_batched(d, reinterpret_cast<const float*>(V), du,
-                                          reinterpret_cast<float*>(ws), ws_floats, Nc, C,
-                                          (int)tiles, 16, tiles * Nc, tiles * C, s);
-  const long long m = (long long)Nc * (C / 4);
-  hipLaunchKernelGGL(k_wg_wgrad_out, dim3((unsigned)((m + EW_BLOCK - 1) / EW_BLOCK)),
-                     dim3(EW_BLOCK), 0, s, split > 1 ? reinterpret_cast<const float*>(ws) : du,
-                     split, reinterpret_cast<float*>(dw), Nc, C);
-  EW_CHECK_LAUNCH();
+  auto* f = m == 2 ? wino_wgrad<2> : wino_wgrad<4>;
+  f(reinterpret_cast<const float*>(dy), reinterpret_cast<const float*>(V),
+    reinterpret_cast<float*>(dw), reinterpret_cast<float*>(D), d_ready,
+    reinterpret_cast<float*>(U_scratch), reinterpret_cast<float*>(ws), ws_floats, N, H, W, C, Nc,
+    (hipStream_t)stream);
 }

@@ -18,15 +18,15 @@ pytestmark = pytest.mark.gpu
 TOL = 1e-5
 
 
-def _conv(wino=False, min_c=64):
+def _conv(wino=False, min_c=64, tile="auto"):
     """The conv module with the Winograd path off (direct implicit GEMM for every shape) or on
-    for every layer with at least ``min_c`` channels."""
+    for every layer with at least ``min_c`` channels, tile m = 2, 4 or auto."""
     from ewdml import ops
     from ewdml.ops import conv
 
     ops.require()
     conv.set_enabled(True)
-    conv.set_winograd(wino, min_c)
+    conv.set_winograd(wino, min_c, tile)
     return conv
 
 
@@ -34,7 +34,7 @@ def _conv(wino=False, min_c=64):
 def _restore_winograd():
     from ewdml.ops import conv
 
-    saved = (conv._WINO, conv._WINO_MIN_C)
+    saved = (conv._WINO, conv._WINO_MIN_C, conv._WINO_TILE)
     yield
     conv.set_winograd(*saved)
 
@@ -197,22 +197,32 @@ def test_conv_f32_bn_backward_sums_in_bwd_data_epilogue(mode, pool, N, HW):
         assert _rel(a, b) < 1e-5, _rel(a, b)
 
 
-WINO_SHAPES = [
-    (128, 128, 256, 8, 8),    # VGG conv3
-    (128, 256, 256, 8, 8),    # VGG conv4
-    (128, 512, 512, 4, 4),    # VGG conv6
-    (128, 512, 512, 2, 2),    # VGG conv8: one tile per image, mostly padding
-    (8, 64, 128, 16, 16),     # 64 input channels
-    (2, 128, 64, 8, 16),      # H != W, 64 output channels
-    (16, 1024, 128, 4, 4),    # wide input
+WINO_SHAPES = [  # (N, C, Nc, H, W, m)
+    (128, 128, 256, 8, 8, 2),    # VGG conv3
+    (128, 256, 256, 8, 8, 2),    # VGG conv4
+    (128, 512, 512, 4, 4, 2),    # VGG conv6
+    (128, 512, 512, 2, 2, 2),    # VGG conv8: one tile per image, mostly padding
+    (8, 64, 128, 16, 16, 2),     # 64 input channels
+    (2, 128, 64, 8, 16, 2),      # H != W, 64 output channels
+    (16, 1024, 128, 4, 4, 2),    # wide input
+    (128, 128, 256, 8, 8, 4),    # F(4x4, 3x3): VGG conv3
+    (128, 256, 256, 8, 8, 4),    # VGG conv4
+    (128, 256, 512, 4, 4, 4),    # VGG conv5: one tile per image
+    (256, 512, 512, 4, 4, 4),    # VGG conv6
+    (8, 64, 128, 16, 16, 4),
+    (4, 128, 64, 8, 32, 4),      # H != W, 64 output channels
 ]
+# relative error bound vs float64 by tile: m = 4's transforms (coefficients up to 8 and 1/24)
+# cost ~10x the rounding of m = 2 (tools/conv_f32_probe.py --err; still ~100x below tf32)
+WINO_TOL = {2: TOL, 4: 2e-5}
 
 
-@pytest.mark.parametrize("N,C,Nc,H,W", WINO_SHAPES)
-def test_conv_f32_winograd_forward_backward(N, C, Nc, H, W):
-    conv = _conv(wino=True)
+@pytest.mark.parametrize("N,C,Nc,H,W,m", WINO_SHAPES)
+def test_conv_f32_winograd_forward_backward(N, C, Nc, H, W, m):
+    conv = _conv(wino=True, tile=m)
     x, w = _data(N, C, Nc, H, W, seed=31)
-    assert conv.supported(x, w) and conv.wino_ok(x, w)
+    assert conv.supported(x, w) and conv.wino_tile(x, w) == m
+    TOL = WINO_TOL[m]
     g = torch.Generator(device="cuda").manual_seed(32)
     dy = torch.randn(N, Nc, H, W, device="cuda", generator=g).contiguous(
         memory_format=torch.channels_last)
@@ -235,6 +245,19 @@ def test_conv_f32_winograd_forward_backward(N, C, Nc, H, W):
     assert _rel(d.conv(x, w), y) < 2 * TOL
 
 
+def test_conv_f32_winograd_tile_choice():
+    conv = _conv(wino=True, min_c=128, tile="auto")
+    x, w = _data(128, 256, 256, 8, 8)
+    assert conv.wino_tile(x, w) == 4
+    x, w = _data(128, 512, 512, 2, 2)
+    assert conv.wino_tile(x, w) == 2  # a 2x2 map does not tile by 4
+    x, w = _data(16, 1024, 128, 4, 4)
+    assert conv.wino_tile(x, w) == 2  # F(4x4) output kernel takes C_out <= 512; tiles % 64
+    conv.set_winograd(True, 128, 2)
+    x, w = _data(128, 256, 256, 8, 8)
+    assert conv.wino_tile(x, w) == 2
+
+
 def test_conv_f32_winograd_only_where_chosen():
     conv = _conv(wino=True, min_c=128)
     x, w = _data(8, 64, 128, 16, 16)
@@ -249,16 +272,17 @@ def test_conv_f32_winograd_only_where_chosen():
     assert not conv.wino_ok(x, w)  # C not a power of two
 
 
-@pytest.mark.parametrize("N,C,Nc,H,W", [(16, 128, 256, 8, 8), (128, 512, 512, 2, 2),
-                                        (32, 256, 512, 4, 4)])
-def test_conv_f32_winograd_bn_statistics(N, C, Nc, H, W):
+@pytest.mark.parametrize("N,C,Nc,H,W,m", [(16, 128, 256, 8, 8, 2), (128, 512, 512, 2, 2, 2),
+                                          (32, 256, 512, 4, 4, 2), (64, 128, 256, 8, 8, 4),
+                                          (128, 256, 512, 4, 4, 4)])
+def test_conv_f32_winograd_bn_statistics(N, C, Nc, H, W, m):
     """BatchNorm partial sums from the Winograd output transform give the BN kernels' own
     statistics."""
     from ewdml.ops import nn as fnn
 
-    conv = _conv(wino=True)
+    conv = _conv(wino=True, tile=m)
     x, w = _data(N, C, Nc, H, W, seed=35)
-    assert conv.wino_ok(x, w)
+    assert conv.wino_tile(x, w) == m
     bn0 = torch.nn.BatchNorm2d(Nc).cuda()
     bn1 = copy.deepcopy(bn0)
     h = conv.conv(x, w.clone().requires_grad_(True))
@@ -270,13 +294,14 @@ def test_conv_f32_winograd_bn_statistics(N, C, Nc, H, W):
     assert torch.allclose(bn0.running_var, bn1.running_var, rtol=1e-5, atol=1e-7)
 
 
+@pytest.mark.parametrize("m", [2, 4])
 @pytest.mark.parametrize("mode,pool", [("relu", True), ("relu", False), ("none", False)])
-def test_conv_f32_winograd_bn_backward_sums(mode, pool):
+def test_conv_f32_winograd_bn_backward_sums(mode, pool, m):
     """The Winograd backward-data output transform produces the producing BN layer's backward
     sums (and the BN backward then skips its statistics pass): same gradients as unfused."""
     from ewdml.ops import nn as fnn
 
-    conv = _conv(wino=True)
+    conv = _conv(wino=True, tile=m)
     N, HW = 32, 16
     x0, w0 = _data(N, 128, 128, HW, HW, seed=41)
     _, w1 = _data(8, 128, 128, 8, 8, seed=42)
@@ -310,7 +335,7 @@ def test_fp32_vgg11_step_vs_fp64():
     in float64 on the CPU, and no worse than the step through MIOpen's fp32 convolutions."""
     from ewdml.models import build_model
 
-    conv = _conv(wino=True, min_c=128)  # the production choice
+    conv = _conv(wino=True, min_c=128, tile=2)  # the production choice
     torch.manual_seed(0)
     m0 = build_model("vgg11", 10).to(memory_format=torch.channels_last)
     for mod in m0.modules():
@@ -346,7 +371,7 @@ def test_fp32_resnet18_step_convs_in_situ():
     from ewdml.models import build_model
     from ewdml.ops import conv as cmod
 
-    _conv(wino=True, min_c=128)  # the production choice
+    _conv(wino=True, min_c=128, tile=2)  # the production choice
     recs = []
     orig = cmod._Conv.backward
 

@@ -31,6 +31,7 @@ def main():
     a.add_argument("--dirs", default="fwd,bwd,wgrad")
     a.add_argument("--miopen", action="store_true", help="also time F.conv2d (MIOpen) forward")
     a.add_argument("--wino", action="store_true", help="also time the Winograd path")
+    a.add_argument("--tile", type=int, default=0, help="Winograd m (2 or 4; default: auto)")
     args = a.parse_args()
     C_ = ops.require()
     dev = torch.device("cuda")
@@ -54,26 +55,30 @@ def main():
                                                HW, HW, C, Nc, 3, _stream()),
         }
         if args.wino:
-            t = N * (HW // 2) * (HW // 2)
-            U = torch.empty(16 * Nc * C, device=dev)
-            buf = torch.empty(16 * t * (C + Nc), device=dev)
+            from ewdml.ops.conv import _wino_fits
+
+            m = args.tile or (4 if _wino_fits(N, C, Nc, HW, HW, 4) else 2)
+            aa = (m + 2) ** 2
+            t = N * (HW // m) * (HW // m)
+            U = torch.empty(aa * Nc * C, device=dev)
+            buf = torch.empty(aa * t * (C + Nc), device=dev)
             calls["wfwd"] = lambda: C_.wino_f32_fwd(
-                _ptr(x), _ptr(w), _ptr(U), _ptr(y), _ptr(buf), _ptr(buf) + 64 * t * C, N, HW, HW,
-                C, Nc, 0, 0, _stream())
+                _ptr(x), _ptr(w), _ptr(U), _ptr(y), _ptr(buf), _ptr(buf) + 4 * aa * t * C, N, HW,
+                HW, C, Nc, m, 0, 0, _stream())
             calls["wbwd"] = lambda: C_.wino_f32_bwd_data(
-                _ptr(y), _ptr(U), _ptr(dx), _ptr(buf), _ptr(buf) + 64 * t * Nc, N, HW, HW, C, Nc,
-                0, 0, 0, 0, 0, 0, 0, 0, 0, _stream())
-            D = torch.empty(16 * t * Nc, device=dev)
-            dU = torch.empty(16 * Nc * C, device=dev)
-            slabs = torch.empty(4 * 16 * Nc * C + 64, device=dev)
+                _ptr(y), _ptr(w), _ptr(U), _ptr(dx), _ptr(buf), _ptr(buf) + 4 * aa * t * Nc, N,
+                HW, HW, C, Nc, m, 0, 0, 0, 0, 0, 0, 0, 0, 0, _stream())
+            D = torch.empty(aa * t * Nc, device=dev)
+            dU = torch.empty(aa * Nc * C, device=dev)
+            slabs = torch.empty(4 * aa * Nc * C + 64, device=dev)
             calls["wwgrad"] = lambda: C_.wino_f32_wgrad(
                 _ptr(y), _ptr(buf), _ptr(dw), _ptr(D), 0, _ptr(dU), _ptr(slabs), slabs.numel(), N,
-                HW, HW, C, Nc, _stream())
+                HW, HW, C, Nc, m, _stream())
         if args.miopen:
             xm = x.permute(0, 3, 1, 2)  # NCHW view of NHWC memory: channels_last
             wm = w.permute(0, 3, 1, 2)
             calls["miopen_fwd"] = lambda: torch.nn.functional.conv2d(xm, wm, padding=1)
-        line = f"C={C:4d} Nc={Nc:4d} HW={HW:3d}"
+        line = f"C={C:4d} Nc={Nc:4d} HW={HW:3d}" + (f" m={m}" if args.wino else "")
         extra = (["miopen_fwd"] if args.miopen else []) + (["wfwd", "wbwd", "wwgrad"] if args.wino
                                                             else [])
         for d in args.dirs.split(",") + extra:
