@@ -6,7 +6,7 @@ Parity: ``PyTorch-parameter-server/src/util.py:7-18`` (``build_model``).  The re
 aliases (``ResNet`` -> ResNet18, ``Resnet50``) work, every model honours ``num_classes`` and an
 unknown name raises.
 """
-from .lenet import LeNet, MnistNet
+from .lenet import KerasMnistCNN, LeNet, MnistNet
 from .resnet import ResNet, ResNet18, ResNet34, ResNet50, ResNet101, ResNet152
 from .vgg import (VGG, vgg11, vgg11_bn, vgg13, vgg13_bn, vgg16, vgg16_bn, vgg19,
                   vgg19_bn)
@@ -15,6 +15,7 @@ from .vgg import (VGG, vgg11, vgg11_bn, vgg13, vgg13_bn, vgg16, vgg16_bn, vgg19,
 _REGISTRY = {
     "lenet": (lambda n, **kw: LeNet(n, **kw), (1, 28, 28)),
     "mnistnet": (lambda n, **kw: MnistNet(n), (1, 28, 28)),
+    "kerasmnistcnn": (lambda n, **kw: KerasMnistCNN(n), (1, 28, 28)),
     "vgg11": (lambda n, **kw: vgg11_bn(n), (3, 32, 32)),  # reference "VGG11" is the BN variant
     "vgg11_bn": (lambda n, **kw: vgg11_bn(n), (3, 32, 32)),
     "vgg11_nobn": (lambda n, **kw: vgg11(n), (3, 32, 32)),
@@ -56,7 +57,7 @@ def build_model(name: str, num_classes: int = 10, **kw):
 
 
 __all__ = [
-    "LeNet", "MnistNet", "VGG", "ResNet", "ResNet18", "ResNet34", "ResNet50", "ResNet101",
+    "KerasMnistCNN", "LeNet", "MnistNet", "VGG", "ResNet", "ResNet18", "ResNet34", "ResNet50", "ResNet101",
     "ResNet152", "vgg11", "vgg11_bn", "vgg13", "vgg13_bn", "vgg16", "vgg16_bn", "vgg19",
     "vgg19_bn", "build_model", "canonical_name", "input_shape", "model_names",
 ]

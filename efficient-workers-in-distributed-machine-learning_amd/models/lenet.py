@@ -52,3 +52,25 @@ class MnistNet(nn.Module):
         x = F.relu(self.fc1(x.flatten(1)))
         x = F.dropout(x, training=self.training)
         return F.log_softmax(self.fc2(x), dim=1)
+
+
+class KerasMnistCNN(nn.Module):
+    """The Horovod TF/Keras example network (``tensorflow_mnist.py:27-36``): Conv2D(32, 3x3, relu)
+    -> Conv2D(64, 3x3, relu) -> MaxPool 2x2 -> Dropout 0.25 -> Flatten -> Dense(128, relu) ->
+    Dropout 0.5 -> Dense(10).  Keras 'valid' padding; logits out (the loss applies the softmax,
+    as SparseCategoricalCrossentropy on the softmax output does)."""
+
+    def __init__(self, num_classes: int = 10):
+        super().__init__()
+        self.conv1 = nn.Conv2d(1, 32, kernel_size=3)
+        self.conv2 = nn.Conv2d(32, 64, kernel_size=3)
+        self.drop1 = nn.Dropout(0.25)
+        self.fc1 = nn.Linear(64 * 12 * 12, 128)
+        self.drop2 = nn.Dropout(0.5)
+        self.fc2 = nn.Linear(128, num_classes)
+
+    def forward(self, x):
+        x = F.relu(self.conv2(F.relu(self.conv1(x))))
+        x = self.drop1(pool2(x))
+        x = self.drop2(F.relu(self.fc1(x.flatten(1))))
+        return self.fc2(x)
