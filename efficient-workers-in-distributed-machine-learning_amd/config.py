@@ -41,7 +41,7 @@ class Config:
     log_interval: int = 10
     network: str = "LeNet"
     mode: str = "normal"  # straggler mode; 'kill' enables the --kill-threshold step timeout
-    kill_threshold: float = 7.0  # seconds; comm watchdog timeout in 'kill' mode
+    kill_threshold: float = 7.0  # seconds a PS k-of-n push may lag the k-th arrival in kill mode
     dataset: str = "MNIST"
     comm_type: str = "Bcast"  # accepted; the all-to-all exchange needs no choice here
     num_aggregate: int = 5  # PS k-of-n: with --topology ps --mode kill the server averages the
@@ -82,7 +82,9 @@ class Config:
     lr_decay: float = 0.1
     # ---- execution -------------------------------------------------------------------------------
     device: str = "auto"  # auto | cuda | cpu
-    amp: str = "bf16"  # bf16 | fp16 | none  (autocast compute dtype; master weights fp32)
+    # none (fp32 compute: the reference's precision, the default) | bf16 | fp16 (autocast compute
+    # dtype; master weights fp32 either way)
+    amp: str = "none"
     param_dtype: str = "auto"  # auto: conv/linear weights kept in bf16 (fp32 master) under bf16
     #                            autocast on the GPU all-to-all path | fp32
     channels_last: bool = False  # alias of layout="nhwc"

@@ -21,9 +21,11 @@ k-of-n aggregation (``--mode kill --num-aggregate k``, the reference's declared-
 straggler flags, ``distributed_nn.py:50-59``): the pushes become point-to-point sends, the server
 averages the first ``k`` worker gradients to ARRIVE (arrival order of the first bucket; the same
 workers for every bucket of the step) and drains the late ones without using them, so the step
-protocol stays in lockstep.  Which workers count is timing-dependent by design;
+protocol stays in lockstep; a worker still missing ``--kill-threshold`` seconds after the k-th
+arrival aborts the job.  Which workers count is timing-dependent by design;
 ``self.last_aggregated`` records them.
 """
+import datetime
 import time
 
 import torch
@@ -35,7 +37,7 @@ class PSExchange:
     server_rank = 0
 
     def __init__(self, flat, comm, push_codec, pull_codec, optimizer, pull: str = "grad",
-                 aggregate: int = None):
+                 aggregate: int = None, kill_threshold: float = None):
         if comm.world < 2:
             raise ValueError("the ps topology needs at least 2 processes (1 server + workers)")
         self.flat, self.comm, self.opt, self.pull = flat, comm, optimizer, pull
@@ -58,6 +60,7 @@ class PSExchange:
         self.last = StepStats()
         W = self.N - 1
         self.k = W if aggregate is None else max(1, min(int(aggregate), W))
+        self.kill_threshold = kill_threshold
         self.last_aggregated = list(range(1, self.N))
 
     @staticmethod
@@ -90,20 +93,49 @@ class PSExchange:
             self.comm.isend(self.payload[bi], self.server_rank, tag=bi).wait()
             return None
         order = []
-        if self.comm.backend == "gloo":  # receive-from-any-source gives the arrival order
+        # once k pushes have arrived the late ones get --kill-threshold seconds, then the step
+        # (and the job) is aborted: the threshold bounds only this per-step push; setup /
+        # checkpoint / eval collectives keep the process group's --comm-timeout
+        thr = self.kill_threshold
+
+        def stalled(ranks):
+            return RuntimeError(f"--mode kill: worker(s) {sorted(ranks)} did not push bucket {bi} "
+                                f"within {thr:g} s of the first {self.k}")
+
+        if self.comm.backend == "gloo":
+            # receive-from-any-source gives the arrival order of the first k (Gloo's irecv never
+            # reports completion before wait()); the rest are waited for with the deadline
             tmp = self.payload[bi]  # the server's own payload buffer is otherwise unused
-            for _ in range(self.N - 1):
+            for _ in range(self.k):
                 src = self.comm.recv_any(tmp, tag=bi)
                 self.gathered[bi][src].copy_(tmp)
                 order.append(src)
+            deadline = time.monotonic() + thr if thr else None
+            rest = [r for r in range(1, self.N) if r not in order]
+            works = {r: self.comm.irecv(self.gathered[bi][r], r, tag=bi) for r in rest}
+            for r in rest:
+                try:
+                    if deadline is None:
+                        works[r].wait()
+                    else:
+                        left = max(deadline - time.monotonic(), 1e-3)
+                        works[r].wait(timeout=datetime.timedelta(seconds=left))
+                except RuntimeError as e:
+                    raise stalled([q for q in rest if q not in order]) from e
+                order.append(r)
         else:  # RCCL: one receive per worker, arrival order by polling completion
             works = {r: self.comm.irecv(self.gathered[bi][r], r, tag=bi)
                      for r in range(1, self.N)}
+            t_quorum = None
             while works:
                 done = [r for r, w in sorted(works.items()) if w.is_completed()]
                 for r in done:
                     order.append(r)
                     works.pop(r).wait()
+                if t_quorum is None and len(order) >= self.k:
+                    t_quorum = time.monotonic()
+                if works and t_quorum is not None and thr and time.monotonic() - t_quorum > thr:
+                    raise stalled(works)
                 if not done:
                     time.sleep(0)
         if bi == 0:  # the step's workers are chosen on the first bucket

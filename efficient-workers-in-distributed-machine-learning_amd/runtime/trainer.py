@@ -53,9 +53,10 @@ class Trainer:
     def __init__(self, cfg: Config, comm: Comm = None):
         self.cfg = cfg = cfg.resolved()
         self.device = resolve_device(cfg)
-        # straggler mode 'kill' (distributed_nn.py:50-53): a rank that stalls longer than
-        # --kill-threshold seconds in a collective aborts the job instead of hanging it
-        timeout = cfg.kill_threshold if cfg.mode == "kill" else cfg.comm_timeout
+        # straggler mode 'kill' (distributed_nn.py:50-53) bounds only the per-step push
+        # (parallel/ps.py k-of-n receive): setup, MIOpen find, graph capture, checkpoint and
+        # eval collectives keep --comm-timeout
+        timeout = cfg.comm_timeout
         self.comm = comm or init_distributed(timeout_s=timeout,
                                              device=self.device if self.device.type == "cuda"
                                              else None)
@@ -147,7 +148,9 @@ class Trainer:
             self.exchange = PSExchange(self.flat, self.comm, make_codec(cfg.compress, **ckw),
                                        make_codec(cfg.pull_compress or cfg.compress, **ckw),
                                        self.opt, pull=cfg.pull,
-                                       aggregate=cfg.num_aggregate if cfg.mode == "kill" else None)
+                                       aggregate=cfg.num_aggregate if cfg.mode == "kill" else None,
+                                       kill_threshold=cfg.kill_threshold if cfg.mode == "kill"
+                                       else None)
         elif cfg.topology == "sharded":
             self.exchange = ShardedPSExchange(self.flat, self.comm, cfg.compress, self.opt, **ckw)
         else:

@@ -162,6 +162,16 @@ def test_ps_k_of_n_aggregation_drops_straggler(tmp_path):
     _same_params(res)
 
 
+def test_ps_kill_threshold_aborts_on_a_stalled_worker(tmp_path):
+    """A worker still missing --kill-threshold seconds after the k-th push arrived aborts the job
+    (the server raises) instead of hanging it; the threshold applies to that push only."""
+    flags = ["--topology", "ps", "--mode", "kill", "--num-aggregate", "1", "--compress", "none",
+             "--amp", "none", "--kill-threshold", "0.5", "--comm-timeout", "60"]
+    assert run_world(_train_slow, 3, tmp_path, args=(flags, 2, 2, 4.0), expect_fail=True) is None
+    err = [f for f in tmp_path.iterdir() if f.name.endswith(".err")]
+    assert any("did not push bucket" in f.read_text() for f in err)
+
+
 def test_ps_k_of_n_inactive_without_kill_mode(tmp_path):
     flags = ["--topology", "ps", "--num-aggregate", "1", "--compress", "none", "--amp", "none"]
     res = run_world(_train_slow, 3, tmp_path, args=(flags, 2, 2, 0.0))

@@ -66,7 +66,7 @@ def test_vgg11_bf16_full_graph_step():
     ops.require()
     flags = ["--network", "VGG11", "--dataset", "Cifar10", "--batch-size", "16",
              "--synthetic-size", "256", "--momentum", "0.9", "--eval-freq", "0", "--quiet",
-             "--device", "cuda", "--hip-graph", "full", "--graph-warmup", "2"]
+             "--device", "cuda", "--hip-graph", "full", "--graph-warmup", "2", "--amp", "bf16"]
     tr, losses = _run(flags, 6)
     assert all(torch.isfinite(torch.tensor(losses)))
     assert tr.exchange.last.payload_bytes == 295312
@@ -116,7 +116,7 @@ def test_bf16_params_match_fp32_master_path(monkeypatch):
     monkeypatch.setattr(head, "_ENABLED", False)
     base = ["--network", "VGG11", "--dataset", "Cifar10", "--batch-size", "32",
             "--synthetic-size", "256", "--momentum", "0.9", "--eval-freq", "0", "--quiet",
-            "--device", "cuda", "--hip-graph", "off", "--compress", "topk_qsgd"]
+            "--device", "cuda", "--hip-graph", "off", "--compress", "topk_qsgd", "--amp", "bf16"]
     a, la = _run(base + ["--param-dtype", "auto"], 4)
     b, lb = _run(base + ["--param-dtype", "fp32"], 4)
     assert a.flat.shadow is not None and b.flat.shadow is None
@@ -133,7 +133,7 @@ def test_bf16_params_checkpoint_holds_fp32_master(tmp_path):
 
     flags = ["--network", "LeNet", "--dataset", "MNIST", "--batch-size", "32", "--synthetic-size",
              "256", "--eval-freq", "2", "--quiet", "--device", "cuda", "--max-steps", "2",
-             "--train-dir", str(tmp_path) + "/"]
+             "--train-dir", str(tmp_path) + "/", "--amp", "bf16"]
     tr = Trainer(ewdml.parse_args(flags))
     tr.fit()
     st = ckpt.load(ckpt.latest(str(tmp_path)))
