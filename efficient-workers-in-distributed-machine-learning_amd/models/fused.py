@@ -9,10 +9,15 @@ not take, it is exactly ``nn.Sequential.forward``.
 
 ``set_enabled(False)`` (``--fused-nn off``) restores the module-by-module path everywhere.
 """
+import os
+
 import torch
 import torch.nn as nn
 
 _ENABLED = True
+# BN layers feeding a Winograd conv leave their apply (forward and backward) to that conv's input
+# transforms (EWDML_LAZY_BN=0: always materialise the activations)
+_LAZY = os.environ.get("EWDML_LAZY_BN", "1") != "0"
 
 
 def set_enabled(on: bool):
@@ -72,13 +77,31 @@ class FusedFeatures(nn.Sequential):
         self._ew_plan = (len(self), groups)
         return groups
 
+    @staticmethod
+    def _lazy_into(plan, gi, h, pool) -> bool:
+        """Whether group gi's BN-ReLU(-pool) output feeds only the next group's conv and that
+        conv runs Winograd on it: then the conv's input transform applies the BN layer
+        (ops/nn.py bn_relu(lazy=True)) and the activation is never written."""
+        if not _LAZY or gi + 1 >= len(plan) or plan[gi + 1][0] != "cbr":
+            return False
+        from ..ops import conv as conv_hip
+
+        nxt = plan[gi + 1][1][0]
+        if not (nxt.stride in (1, (1, 1)) and nxt.padding in (1, (1, 1))
+                and nxt.dilation in (1, (1, 1)) and nxt.groups == 1):
+            return False
+        N, C, H, W = h.shape
+        shape = (N, C, H // 2, W // 2) if pool else (N, C, H, W)
+        return conv_hip.enabled() and conv_hip.wino_tile_for(shape, h.dtype, nxt.weight) > 0
+
     def forward(self, x):
         if not (_ENABLED and x.is_cuda):
             return super().forward(x)
         from ..ops import conv as conv_hip
         from ..ops import nn as fnn
 
-        for kind, mods, pool in self._plan():
+        plan = self._plan()
+        for gi, (kind, mods, pool) in enumerate(plan):
             if kind == "cbr":
                 conv, bn = mods[0], mods[1]
                 if conv_hip.supported(x, conv.weight, conv.stride, conv.padding, conv.dilation,
@@ -87,7 +110,7 @@ class FusedFeatures(nn.Sequential):
                 else:
                     h = conv._conv_forward(x, conv.weight, None)
                 if fnn.nhwc_supported(h, pool):
-                    x = fnn.bn_relu(h, conv.bias, bn, pool)
+                    x = fnn.bn_relu(h, conv.bias, bn, pool, lazy=self._lazy_into(plan, gi, h, pool))
                 else:
                     if conv.bias is not None:
                         h = h + conv.bias.to(h.dtype).view(1, -1, 1, 1)

@@ -82,10 +82,17 @@ def wino_tile(x, w) -> int:
     """The Winograd output tile m (2 or 4) the fp32 conv of ``x`` by ``w`` takes, 0 for none:
     3x3, power-of-two channel counts in [_WINO_MIN_C, 1024 (m = 2) / 512 (m = 4)], H and W
     multiples of m, N*H*W/m^2 % 64 == 0."""
-    if not _WINO or x.dtype != torch.float32 or w.shape[-1] != 3:
+    return wino_tile_for(tuple(x.shape), x.dtype, w)
+
+
+def wino_tile_for(shape, dtype, w) -> int:
+    """:func:`wino_tile` for an input of this shape and dtype (before it exists)."""
+    if not _WINO or dtype != torch.float32 or w.shape[-1] != 3 or w.dtype != dtype:
         return 0
-    N, C, H, W = x.shape
+    N, C, H, W = shape
     Nc = w.shape[0]
+    if w.shape[1] != C:
+        return 0
     if min(C, Nc) < _WINO_MIN_C:
         return 0
     order = {"2": (2,), "4": (4,)}.get(_WINO_TILE, (4, 2))
@@ -216,6 +223,14 @@ class _Conv(torch.autograd.Function):
         part = torch.empty(_part_floats(N * H * W, Nc), dtype=torch.float32, device=x.device)
         ctx.wino = None
         m = wino_tile(x, w)
+        # x may be the lazily applied output of a fused BN layer (ops/nn.py bn_relu(lazy=True)):
+        # the Winograd input transform applies that layer on the fly; anything else needs it
+        lazy = getattr(x, "_ew_lazy_fwd", None)
+        if lazy is not None and not m:
+            from .nn import materialize
+
+            materialize(x)
+            lazy = None
         if m:
             aa = (m + 2) ** 2
             # transformed weight U[a^2][Nc][C] (m = 2: kept for the backward-data GEMMs, read
@@ -224,8 +239,17 @@ class _Conv(torch.autograd.Function):
             t = N * (H // m) * (W // m)
             V = torch.empty(aa * t * C, dtype=torch.float32, device=x.device)
             Mo = torch.empty(aa * t * Nc, dtype=torch.float32, device=x.device)
-            rows = C_.wino_f32_fwd(_ptr(x), _ptr(w), _ptr(U), _ptr(y), _ptr(V), _ptr(Mo), N, H, W,
-                                   C, Nc, m, _ptr(part), part.numel(), _stream())
+            if lazy is not None:
+                bh, bstats, bcode, bnbt, bpool = lazy
+                rows = C_.wino_f32_fwd_bn(_ptr(bh), _ptr(bstats), _ptr(bcode), _ptr(bnbt),
+                                          int(bpool), _ptr(w), _ptr(U), _ptr(y), _ptr(V),
+                                          _ptr(Mo), N, H, W, C, Nc, m, _ptr(part), part.numel(),
+                                          _stream())
+                # a later materialisation must not count the batch twice
+                x._ew_materialize = getattr(x, "_ew_materialize_no_nbt", None)
+            else:
+                rows = C_.wino_f32_fwd(_ptr(x), _ptr(w), _ptr(U), _ptr(y), _ptr(V), _ptr(Mo), N,
+                                       H, W, C, Nc, m, _ptr(part), part.numel(), _stream())
             ctx.wino = (U if m == 2 else None, V, m)
         else:
             fwd = C_.conv_f32_fwd if x.dtype == torch.float32 else C_.conv_fwd
@@ -243,6 +267,15 @@ class _Conv(torch.autograd.Function):
         x, w = ctx.saved_tensors
         N, C, H, W = x.shape
         Nc, k = w.shape[0], w.shape[-1]
+        # dy may be the lazily formed input gradient of the BN layer this conv feeds (ops/nn.py):
+        # the Winograd backward-data input transform forms it on the fly, anything else needs it
+        lazy = getattr(dy, "_ew_lazy_bwd", None)
+        if lazy is not None and not (ctx.wino is not None and ctx.needs_input_grad[0]
+                                     and dy.dtype == x.dtype):
+            from .nn import materialize
+
+            materialize(dy)
+            lazy = None
         dy = dy.contiguous(memory_format=torch.channels_last)
         if dy.dtype != x.dtype:
             dy = dy.to(x.dtype)
@@ -278,6 +311,12 @@ class _Conv(torch.autograd.Function):
                 buf = torch.empty(aa * t * (C + Nc), dtype=torch.float32, device=x.device)
 
                 def bwd_data(dy_, w_, dx_, ws_, wsn, *rest):  # same contract, Winograd
+                    if lazy is not None:  # dy formed from the BN layer's backward on the fly
+                        oh, odn, ocode, ostats, ocoef, opool = lazy
+                        return C_.wino_f32_bwd_data_bn(
+                            _ptr(oh), _ptr(odn), _ptr(ocode), _ptr(ostats), _ptr(ocoef),
+                            int(opool), w_, _ptr(U), dx_, _ptr(buf), _ptr(buf) + 4 * aa * t * Nc,
+                            *rest[:5], m, *rest[6:-1], _ptr(D), rest[-1])
                     return C_.wino_f32_bwd_data(dy_, w_, _ptr(U), dx_, _ptr(buf),
                                                 _ptr(buf) + 4 * aa * t * Nc, *rest[:5], m,
                                                 *rest[6:-1], _ptr(D), rest[-1])
@@ -378,6 +417,8 @@ def _apply(x, w, sink=None):
     part = getattr(node, "bn_part", None) if node is not None else None
     if part is not None:
         y._ew_bn_part = part
+    if node is not None and getattr(node, "wino", None) is not None:
+        y._ew_wino_out = True  # the BN layer it feeds may leave its backward apply to us
     return y
 
 
@@ -386,7 +427,9 @@ def conv(x, w):
     :func:`supported`."""
     if supported(x, w):
         return _apply(x, w)
-    return F.conv2d(x, w, padding=w.shape[-1] // 2)
+    from .nn import materialize
+
+    return F.conv2d(materialize(x), w, padding=w.shape[-1] // 2)
 
 
 conv3x3 = conv

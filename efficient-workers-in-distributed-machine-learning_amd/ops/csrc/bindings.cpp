@@ -228,9 +228,10 @@ PYBIND11_MODULE(_C, m) {
            uintptr_t part, uintptr_t gamma, uintptr_t beta, uintptr_t cbias, uintptr_t rmean,
            uintptr_t rvar, uintptr_t nbt, long long N, int H, int W, int C, int is_bf16,
            int pool, int mode, int training, float momentum, float eps, int cb_bf16,
-           uintptr_t stream, int pre_nblk) {
+           uintptr_t stream, int pre_nblk, int phase) {
           BnFwdArgs a{};
           a.pre_nblk = pre_nblk;
+          a.phase = phase;
           a.h = h; a.res = res; a.y = y; a.code = code; a.stats = stats; a.part = part;
           a.gamma = gamma; a.beta = beta; a.cbias = cbias; a.rmean = rmean; a.rvar = rvar;
           a.nbt = nbt; a.N = N; a.H = H; a.W = W; a.C = C;
@@ -242,8 +243,9 @@ PYBIND11_MODULE(_C, m) {
         [](uintptr_t h, uintptr_t res, uintptr_t dy, uintptr_t code, uintptr_t stats,
            uintptr_t coef, uintptr_t part, uintptr_t dx, uintptr_t dres, uintptr_t dgamma,
            uintptr_t dbeta, uintptr_t dcbias, long long N, int H, int W, int C, int is_bf16,
-           int pool, int mode, int cb_bf16, uintptr_t stream, int pre_nblk) {
+           int pool, int mode, int cb_bf16, uintptr_t stream, int pre_nblk, int phase) {
           BnBwdArgs a{};
+          a.phase = phase;
           a.h = h; a.res = res; a.dy = dy; a.code = code; a.stats = stats; a.coef = coef;
           a.part = part; a.dx = dx; a.dres = dres; a.dgamma = dgamma; a.dbeta = dbeta;
           a.dcbias = dcbias; a.N = N; a.H = H; a.W = W; a.C = C; a.is_bf16 = is_bf16;
@@ -283,6 +285,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("wino_f32_fwd", &ew_wino_f32_fwd);
   m.def("wino_f32_bwd_data", &ew_wino_f32_bwd_data);
   m.def("wino_f32_wgrad", &ew_wino_f32_wgrad);
+  m.def("wino_f32_fwd_bn", &ew_wino_f32_fwd_bn);
+  m.def("wino_f32_bwd_data_bn", &ew_wino_f32_bwd_data_bn);
   m.def("maxpool2_nhwc", &ew_maxpool2_nhwc);
   m.def("maxpool2_fwd", &ew_maxpool2_fwd);
   m.def("maxpool2_bwd", &ew_maxpool2_bwd);

@@ -108,6 +108,7 @@ struct BnFwdArgs {
   float momentum, eps;  // momentum < 0: cumulative average over *nbt batches
   uintptr_t stream;
   int pre_nblk;  // > 0: `part` already holds [2][pre_nblk][C] partial sums (skip the stats pass)
+  int phase;     // 0: statistics + apply, 1: statistics only (the consumer applies: lazy), 2: apply
 };
 struct BnBwdArgs {
   uintptr_t h, res, dy, code, stats, coef, part, dx, dres;  // coef fp32 [2][C]
@@ -117,6 +118,7 @@ struct BnBwdArgs {
   int is_bf16, pool, cb_bf16, mode;
   uintptr_t stream;
   int pre_nblk;  // > 0: `part` already holds [2][pre_nblk][C] sums (sum dz, sum dz*(h-mean))
+  int phase;     // 0: statistics + apply, 1: statistics only (coef, dgamma, dbeta), 2: apply
 };
 int ew_bn_part_floats();
 void ew_bn_relu_fwd(const BnFwdArgs& a);
@@ -214,6 +216,20 @@ int ew_wino_f32_bwd_data(uintptr_t dy, uintptr_t w, uintptr_t U, uintptr_t dx, u
                          uintptr_t bn_h, uintptr_t bn_res, uintptr_t bn_code, uintptr_t bn_stats,
                          int bn_relu, uintptr_t bnpart, long long bnpart_floats,
                          uintptr_t addend, uintptr_t D, uintptr_t stream);
+// the same with the BatchNorm(+ReLU)(+2x2 pool) layer in front applied in the input transform
+// (forward; its pool codes written here) / the BatchNorm backward of this conv's output formed
+// in the input transform (backward data): winograd_f32.hip WgSrc
+int ew_wino_f32_fwd_bn(uintptr_t bn_h, uintptr_t bn_stats, uintptr_t bn_code, uintptr_t nbt,
+                       int pool, uintptr_t w, uintptr_t U, uintptr_t y, uintptr_t V,
+                       uintptr_t Mo, long long N, int H, int W, int C, int Nc, int m,
+                       uintptr_t bnpart, long long bnpart_floats, uintptr_t stream);
+int ew_wino_f32_bwd_data_bn(uintptr_t out_h, uintptr_t out_dnext, uintptr_t out_code,
+                            uintptr_t out_stats, uintptr_t out_coef, int out_pool, uintptr_t w,
+                            uintptr_t U, uintptr_t dx, uintptr_t V, uintptr_t Mo, long long N,
+                            int H, int W, int C, int Nc, int m, uintptr_t bn_h, uintptr_t bn_res,
+                            uintptr_t bn_code, uintptr_t bn_stats, int bn_relu, uintptr_t bnpart,
+                            long long bnpart_floats, uintptr_t addend, uintptr_t D,
+                            uintptr_t stream);
 void ew_wino_f32_wgrad(uintptr_t dy, uintptr_t V, uintptr_t dw, uintptr_t D, int d_ready,
                        uintptr_t U_scratch, uintptr_t ws, long long ws_floats, long long N, int H,
                        int W, int C, int Nc, int m, uintptr_t stream);

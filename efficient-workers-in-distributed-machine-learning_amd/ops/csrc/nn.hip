@@ -730,7 +730,7 @@ void ew_bn_relu_fwd(const BnFwdArgs& a) {
   const long long M = a.N * (long long)a.H * a.W;
   const int Ho = a.H / 2, Wo = a.W / 2;
   const int C = a.C;
-  if (a.training) {
+  if (a.training && a.phase != 2) {
     int nblk, rpb;
     ew_bn_grid(M, C, &nblk, &rpb, 4);
     float* part = reinterpret_cast<float*>(a.part);
@@ -752,6 +752,7 @@ void ew_bn_relu_fwd(const BnFwdArgs& a) {
                        reinterpret_cast<float*>(a.stats));
     EW_CHECK_LAUNCH();
   }
+  if (a.phase == 1) return;  // lazy: the consumer applies (winograd_f32.hip WgSrc KIND 1)
   const float* st = reinterpret_cast<const float*>(a.stats);
   uint8_t* code = reinterpret_cast<uint8_t*>(a.code);
   long long* nbt = a.training ? reinterpret_cast<long long*>(a.nbt) : nullptr;
@@ -798,7 +799,9 @@ static void ew_bn_bwd_impl(const BnBwdArgs& a) {
   const uint8_t* code = reinterpret_cast<const uint8_t*>(a.code);
   const float* st = reinterpret_cast<const float*>(a.stats);
   float* coef = reinterpret_cast<float*>(a.coef);
-  if (pre) {
+  if (a.phase == 2) {
+    // apply only (a lazy backward materialised after all): coef from the earlier phase-1 call
+  } else if (pre) {
     hipLaunchKernelGGL(k_bn_bwd_finalize<2>, dim3((C + EW_FIN_CH - 1) / EW_FIN_CH), dim3(EW_BLOCK),
                        0, s, part, a.pre_nblk, C, M, st, coef, reinterpret_cast<float*>(a.dgamma),
                        reinterpret_cast<float*>(a.dbeta), reinterpret_cast<void*>(a.dcbias),
@@ -813,6 +816,7 @@ static void ew_bn_bwd_impl(const BnBwdArgs& a) {
                        a.cb_bf16);
   }
   EW_CHECK_LAUNCH();
+  if (a.phase == 1) return;  // lazy: the producing conv's input transform forms dx (KIND 2)
   hipLaunchKernelGGL((k_bn_bwd_apply<T, MODE>), dim3(ew_grid_vec(rows * (C / 8))),
                      dim3(EW_BLOCK), 5 * sizeof(float) * C, s, h, res, dy, code, st, coef,
                      reinterpret_cast<T*>(a.dx), reinterpret_cast<T*>(a.dres), rows, C, Ho, Wo);

@@ -173,16 +173,38 @@ __device__ __forceinline__ void wg_dy_store(float* __restrict__ o, long long xs,
   }
 }
 
+// Where the input transform's operand comes from (KIND):
+//  0: x itself (a materialised activation or gradient);
+//  1: the forward of the BatchNorm(+ReLU)(+2x2 max pool) layer in front, applied on the fly:
+//     x = maxpool?(relu(h * scale + shift)) with h that layer's BN input (2H x 2W when pooled);
+//     the pool's window codes are written by the tile that owns the position (the patch's
+//     inner m x m), num_batches_tracked incremented once -- the BN apply kernel and the x round
+//     trip disappear (ops/nn.py lazy forward);
+//  2: the backward of the BatchNorm(+ReLU)(+pool) layer whose input is this conv's output, on the
+//     fly: dy = scale * dz + e * (h - mean) + f (nn.hip k_bn_bwd_apply's formula, coef = (e, f)),
+//     dz = relu'(h * scale + shift) * (pool ? [code == q] dnext[pooled] : dnext), h this conv's
+//     output -- the BN backward's apply kernel and the dh round trip disappear.
+struct WgSrc {
+  const float* h;       // KIND 1: the BN input in front; KIND 2: this conv's output
+  const float* stats;   // [4][C]: mean, invstd, scale, shift
+  uint8_t* code;        // pool window codes at the pooled resolution (KIND 1 writes, 2 reads)
+  const float* coef;    // KIND 2: [2][C] (e, f)
+  const float* dnext;   // KIND 2: gradient of the BN layer's (pooled) output
+  long long* nbt;       // KIND 1: num_batches_tracked (incremented by thread 0 of block 0)
+  int pool;
+};
+
 // V[xi][tile][c..] = (B^T d B)[xi], d = the a x a patch at (m ty - 1, m tx - 1) of x[N][H][W][C]
 // (zero outside).  Thread: one tile x one channel vector; consecutive threads, consecutive
 // vectors.  With D: also the weight gradient's dMo of the patch's inner m x m (the dy tile).
-template <int M>
+template <int M, int KIND>
 __device__ __forceinline__ void wg_input(const float* __restrict__ x, float* __restrict__ V,
                                          int H, int W, int C, long long tiles, long long g,
-                                         float* __restrict__ D) {
+                                         float* __restrict__ D, const WgSrc& src) {
   using T = typename Wg<M>::V;
   constexpr int A = Wg<M>::A, VW = Wg<M>::VW;
   const int cq = C / VW;
+  if (KIND == 1 && src.nbt && g == 0) *src.nbt += 1;
   if (g >= tiles * cq) return;
   const long long tl = g / cq;
   const int c = (int)(g - tl * cq) * VW;
@@ -190,6 +212,19 @@ __device__ __forceinline__ void wg_input(const float* __restrict__ x, float* __r
   const int n = (int)(tl / tpi), rem = (int)(tl - (long long)n * tpi);
   const int ty = rem / tw, tx = rem - ty * tw;
   const int h0 = M * ty - 1, w0 = M * tx - 1;
+  T sc{}, sh{}, mean{}, ce{}, cf{};
+  if constexpr (KIND != 0) {
+#pragma unroll
+    for (int q = 0; q < VW; ++q) {
+      sc[q] = src.stats[2 * C + c + q];
+      sh[q] = src.stats[3 * C + c + q];
+      if constexpr (KIND == 2) {
+        mean[q] = src.stats[c + q];
+        ce[q] = src.coef[c + q];
+        cf[q] = src.coef[C + c + q];
+      }
+    }
+  }
   T d[A][A];
 #pragma unroll
   for (int i = 0; i < A; ++i)
@@ -197,8 +232,73 @@ __device__ __forceinline__ void wg_input(const float* __restrict__ x, float* __r
     for (int j = 0; j < A; ++j) {
       const int h = h0 + i, w = w0 + j;
       const bool ok = (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
-      const T v = *reinterpret_cast<const T*>(x + (ok ? (((long long)n * H + h) * W + w) * C + c
-                                                      : c));
+      const long long r = ok ? ((long long)n * H + h) * W + w : 0;  // row at this resolution
+      T v{};
+      if constexpr (KIND == 0) {
+        v = *reinterpret_cast<const T*>(x + r * C + c);
+      } else if constexpr (KIND == 1) {
+        if (!src.pool) {
+          const T hv = *reinterpret_cast<const T*>(src.h + r * C + c);
+#pragma unroll
+          for (int q = 0; q < VW; ++q) {
+            const float z = hv[q] * sc[q] + sh[q];  // as k_bn_fwd_apply writes it
+            v[q] = (z > 0.0f || z != z) ? z : 0.0f;
+          }
+        } else {  // max over the 2x2 window of the 2H x 2W map, first max wins (k_bn_fwd_apply)
+          const int W2 = 2 * W;
+          const long long r0 = ((long long)n * 2 * H + 2 * h) * W2 + 2 * w;
+          uint32_t k[VW];
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq) {
+            const T hv = *reinterpret_cast<const T*>(
+                src.h + (ok ? r0 + (qq >> 1) * W2 + (qq & 1) : 0) * C + c);
+#pragma unroll
+            for (int q = 0; q < VW; ++q) {
+              const float z = hv[q] * sc[q] + sh[q];
+              const float y = (z > 0.0f || z != z) ? z : 0.0f;
+              if (qq == 0 || y > v[q] || y != y) {
+                v[q] = y;
+                k[q] = qq;
+              }
+            }
+          }
+          if (ok && i >= 1 && i <= M && j >= 1 && j <= M) {  // the owning tile writes the code
+            uint32_t wd = 0;
+#pragma unroll
+            for (int q = 0; q < VW; ++q) wd |= k[q] << (8 * q);
+            if constexpr (VW == 4)
+              *reinterpret_cast<uint32_t*>(src.code + r * C + c) = wd;
+            else
+              *reinterpret_cast<uint16_t*>(src.code + r * C + c) = (uint16_t)wd;
+          }
+        }
+      } else {  // KIND 2
+        const T hv = *reinterpret_cast<const T*>(src.h + r * C + c);
+        T dp;
+        if (src.pool) {
+          const int Wo = W / 2;
+          // (h, w) may lie in the zero padding: index row 0 there (the value is masked below)
+          const long long pr = ok ? ((long long)n * (H / 2) + (h >> 1)) * Wo + (w >> 1) : 0;
+          const T dn = *reinterpret_cast<const T*>(src.dnext + pr * C + c);
+          const uint32_t qq = (uint32_t)((h & 1) * 2 + (w & 1));
+          uint32_t kw;
+          if constexpr (VW == 4)
+            kw = *reinterpret_cast<const uint32_t*>(src.code + pr * C + c);
+          else
+            kw = *reinterpret_cast<const uint16_t*>(src.code + pr * C + c);
+#pragma unroll
+          for (int q = 0; q < VW; ++q) dp[q] = ((kw >> (8 * q)) & 0xffu) == qq ? dn[q] : 0.0f;
+        } else {
+          dp = *reinterpret_cast<const T*>(src.dnext + r * C + c);
+        }
+#pragma unroll
+        for (int q = 0; q < VW; ++q) {
+          // the expressions of k_bn_bwd_apply: the same contraction, the same bits
+          const float z = hv[q] * sc[q] + sh[q];
+          const float dz = !(z <= 0.0f) ? dp[q] : 0.0f;
+          v[q] = sc[q] * dz + ce[q] * (hv[q] - mean[q]) + cf[q];
+        }
+      }
       d[i][j] = ok ? v : T{};
     }
   if (D) {
@@ -230,15 +330,16 @@ __device__ __forceinline__ void wg_input(const float* __restrict__ x, float* __r
 
 // the input transform over blocks [0, nbi) and, when w is given, the weight transform over the
 // rest (one launch for both: each alone is a few-microsecond kernel)
-template <int M, bool FLIP>
+template <int M, bool FLIP, int KIND>
 __global__ __launch_bounds__(EW_BLOCK) void k_wg_input(const float* __restrict__ x,
                                                        float* __restrict__ V, int H, int W, int C,
                                                        long long tiles, int nbi,
                                                        const float* __restrict__ w,
                                                        float* __restrict__ U, int Nw, int Cw,
-                                                       float* __restrict__ D) {
+                                                       float* __restrict__ D, WgSrc src) {
   if ((int)blockIdx.x < nbi)
-    wg_input<M>(x, V, H, W, C, tiles, (long long)blockIdx.x * EW_BLOCK + threadIdx.x, D);
+    wg_input<M, KIND>(x, V, H, W, C, tiles, (long long)blockIdx.x * EW_BLOCK + threadIdx.x, D,
+                      src);
   else
     wg_weight<M, FLIP>(w, U, Nw, Cw, (long long)(blockIdx.x - nbi) * EW_BLOCK + threadIdx.x);
 }
@@ -443,22 +544,31 @@ int wg_output(const float* Mo, float* y, long long N, int H, int W, int Nc, floa
 // the rotated kernel)
 template <int M, bool FLIP>
 void wg_input(const float* x, float* V, long long N, int H, int W, int C, hipStream_t s,
-              const float* w, float* U, int Nw, int Cw, float* D) {
+              const float* w, float* U, int Nw, int Cw, float* D, const WgSrc* src = nullptr,
+              int kind = 0) {
   constexpr int VW = Wg<M>::VW;
   const long long n = wg_tiles(M, N, H, W) * (C / VW);
   const int nbi = (int)((n + EW_BLOCK - 1) / EW_BLOCK);
   const int nbw = w ? (int)(((long long)Nw * (Cw / VW) + EW_BLOCK - 1) / EW_BLOCK) : 0;
-  hipLaunchKernelGGL((k_wg_input<M, FLIP>), dim3(nbi + nbw), dim3(EW_BLOCK), 0, s, x, V, H, W, C,
-                     wg_tiles(M, N, H, W), nbi, w, U, Nw, Cw, D);
+  const WgSrc none{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0};
+  const WgSrc& sr = src ? *src : none;
+#define WG_IN(K_)                                                                                \
+  hipLaunchKernelGGL((k_wg_input<M, FLIP, K_>), dim3(nbi + nbw), dim3(EW_BLOCK), 0, s, x, V, H, W, \
+                     C, wg_tiles(M, N, H, W), nbi, w, U, Nw, Cw, D, sr)
+  if (kind == 1) WG_IN(1);
+  else if (kind == 2) WG_IN(2);
+  else WG_IN(0);
+#undef WG_IN
   EW_CHECK_LAUNCH();
 }
 
 template <int M>
 int wino_fwd(const float* x, const float* w, float* U, float* y, float* v, float* mo, long long N,
-             int H, int W, int C, int Nc, float* bnpart, long long bnpart_floats, hipStream_t s) {
+             int H, int W, int C, int Nc, float* bnpart, long long bnpart_floats, hipStream_t s,
+             const WgSrc* src) {
   constexpr int AA = Wg<M>::A * Wg<M>::A;
   const long long tiles = wg_tiles(M, N, H, W);
-  wg_input<M, false>(x, v, N, H, W, C, s, w, U, Nc, C, nullptr);
+  wg_input<M, false>(x, v, N, H, W, C, s, w, U, Nc, C, nullptr, src, src ? 1 : 0);
   ew_cf_gemm_batched(v, U, mo, (int)tiles, Nc, C, AA, tiles * C, (long long)Nc * C, tiles * Nc,
                      true, false, s);
   const CfBnBwd none{nullptr, nullptr, nullptr, nullptr, 0, 0, 0};
@@ -468,15 +578,17 @@ int wino_fwd(const float* x, const float* w, float* U, float* y, float* v, float
 template <int M>
 int wino_bwd(const float* dy, const float* w, float* U, float* dx, float* v, float* mo,
              long long N, int H, int W, int C, int Nc, const CfBnBwd& bb, float* bnpart,
-             long long bnpart_floats, const float* addend, float* D, hipStream_t s) {
+             long long bnpart_floats, const float* addend, float* D, hipStream_t s,
+             const WgSrc* src) {
+  const int kind = src ? 2 : 0;
   constexpr int AA = Wg<M>::A * Wg<M>::A;
   const long long tiles = wg_tiles(M, N, H, W);
   // m = 4: U <- transform of the rotated kernel, in the input launch; m = 2: the forward's U,
   // read flipped.  Mo'[xi][tile][c] = sum_n V'[xi][tile][n] U'[xi][n][c]
   if constexpr (M == 4)
-    wg_input<M, true>(dy, v, N, H, W, Nc, s, w, U, Nc, C, D);
+    wg_input<M, true>(dy, v, N, H, W, Nc, s, w, U, Nc, C, D, src, kind);
   else
-    wg_input<M, false>(dy, v, N, H, W, Nc, s, nullptr, nullptr, 0, 0, D);
+    wg_input<M, false>(dy, v, N, H, W, Nc, s, nullptr, nullptr, 0, 0, D, src, kind);
   ew_cf_gemm_batched(v, U, mo, (int)tiles, C, Nc, AA, tiles * Nc, (long long)Nc * C, tiles * C,
                      false, M == 2, s);
   return wg_output<M>(mo, dx, N, H, W, C, bnpart, bnpart_floats, bb, addend, s);
@@ -527,7 +639,26 @@ int ew_wino_f32_fwd(uintptr_t x, uintptr_t w, uintptr_t U, uintptr_t y, uintptr_
   return f(reinterpret_cast<const float*>(x), reinterpret_cast<const float*>(w),
            reinterpret_cast<float*>(U), reinterpret_cast<float*>(y), reinterpret_cast<float*>(V),
            reinterpret_cast<float*>(Mo), N, H, W, C, Nc, reinterpret_cast<float*>(bnpart),
-           bnpart_floats, (hipStream_t)stream);
+           bnpart_floats, (hipStream_t)stream, nullptr);
+}
+
+// The forward whose input is the BatchNorm(+ReLU)(+pool) of bn_h, applied in the input transform
+// (WgSrc KIND 1): bn_stats [4][C] of that layer, bn_code its pool codes (written here), nbt its
+// num_batches_tracked (nullable).  H, W: this conv's (pooled) resolution.
+int ew_wino_f32_fwd_bn(uintptr_t bn_h, uintptr_t bn_stats, uintptr_t bn_code, uintptr_t nbt,
+                       int pool, uintptr_t w, uintptr_t U, uintptr_t y, uintptr_t V,
+                       uintptr_t Mo, long long N, int H, int W, int C, int Nc, int m,
+                       uintptr_t bnpart, long long bnpart_floats, uintptr_t stream) {
+  wg_check(m, N, H, W, C, Nc, "forward");
+  if (pool && !bn_code) throw std::runtime_error("ewdml winograd f32: pooled input needs codes");
+  const WgSrc src{reinterpret_cast<const float*>(bn_h), reinterpret_cast<const float*>(bn_stats),
+                  reinterpret_cast<uint8_t*>(bn_code), nullptr, nullptr,
+                  reinterpret_cast<long long*>(nbt), pool};
+  auto* f = m == 2 ? wino_fwd<2> : wino_fwd<4>;
+  return f(nullptr, reinterpret_cast<const float*>(w), reinterpret_cast<float*>(U),
+           reinterpret_cast<float*>(y), reinterpret_cast<float*>(V), reinterpret_cast<float*>(Mo),
+           N, H, W, C, Nc, reinterpret_cast<float*>(bnpart), bnpart_floats, (hipStream_t)stream,
+           &src);
 }
 
 // m = 2: U is the forward's transformed weight (read flipped; w unused); m = 4: U receives the
@@ -549,7 +680,36 @@ int ew_wino_f32_bwd_data(uintptr_t dy, uintptr_t w, uintptr_t U, uintptr_t dx, u
            reinterpret_cast<float*>(Mo), N, H, W, C, Nc, bb,
            bn_h ? reinterpret_cast<float*>(bnpart) : nullptr, bnpart_floats,
            reinterpret_cast<const float*>(addend), reinterpret_cast<float*>(D),
-           (hipStream_t)stream);
+           (hipStream_t)stream, nullptr);
+}
+
+// Backward data whose dy is the BatchNorm(+ReLU)(+pool) backward of this conv's output, formed in
+// the input transform (WgSrc KIND 2): out_h = this conv's output (that BN layer's input),
+// out_dnext = the gradient of the BN layer's (pooled) output, out_code its pool codes,
+// out_stats [4][Nc] / out_coef [2][Nc] (e, f) of that layer.  Otherwise ew_wino_f32_bwd_data.
+int ew_wino_f32_bwd_data_bn(uintptr_t out_h, uintptr_t out_dnext, uintptr_t out_code,
+                            uintptr_t out_stats, uintptr_t out_coef, int out_pool, uintptr_t w,
+                            uintptr_t U, uintptr_t dx, uintptr_t V, uintptr_t Mo, long long N,
+                            int H, int W, int C, int Nc, int m, uintptr_t bn_h, uintptr_t bn_res,
+                            uintptr_t bn_code, uintptr_t bn_stats, int bn_relu, uintptr_t bnpart,
+                            long long bnpart_floats, uintptr_t addend, uintptr_t D,
+                            uintptr_t stream) {
+  wg_check(m, N, H, W, Nc, C, "backward data");
+  if (m == 4 && !w) throw std::runtime_error("ewdml winograd f32: m = 4 backward needs w");
+  if (out_pool && (H % 2 || W % 2 || !out_code))
+    throw std::runtime_error("ewdml winograd f32: pooled BN backward needs even maps and codes");
+  const WgSrc src{reinterpret_cast<const float*>(out_h), reinterpret_cast<const float*>(out_stats),
+                  reinterpret_cast<uint8_t*>(out_code), reinterpret_cast<const float*>(out_coef),
+                  reinterpret_cast<const float*>(out_dnext), nullptr, out_pool};
+  const CfBnBwd bb{reinterpret_cast<const float*>(bn_h), reinterpret_cast<const float*>(bn_res),
+                   reinterpret_cast<const uint8_t*>(bn_code),
+                   reinterpret_cast<const float*>(bn_stats), bn_relu, H, W};
+  auto* f = m == 2 ? wino_bwd<2> : wino_bwd<4>;
+  return f(nullptr, reinterpret_cast<const float*>(w), reinterpret_cast<float*>(U),
+           reinterpret_cast<float*>(dx), reinterpret_cast<float*>(V), reinterpret_cast<float*>(Mo),
+           N, H, W, C, Nc, bb, bn_h ? reinterpret_cast<float*>(bnpart) : nullptr, bnpart_floats,
+           reinterpret_cast<const float*>(addend), reinterpret_cast<float*>(D),
+           (hipStream_t)stream, &src);
 }
 
 // dw (channels_last [Nc][3][3][C]) from dy and the forward's V; D: a^2 * tiles * Nc floats;

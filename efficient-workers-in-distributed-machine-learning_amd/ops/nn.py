@@ -17,6 +17,8 @@ Parity: the reference builds these layers from ``nn.Conv2d/BatchNorm2d/ReLU/MaxP
 (``src/model_ops/vgg.py:39-52``); these are faster kernels for the same modules (same parameters,
 buffers and ``state_dict`` keys), nothing in the reference corresponds to them directly.
 """
+import os
+
 import torch
 
 from . import _ptr, _stream, require
@@ -65,10 +67,14 @@ _MODES = {"relu": 0, "none": 2, "add_relu": 3}
 PRE_BWD_USED = 0
 
 
+# BN backward left to the Winograd conv that produced its input (EWDML_LAZY_BN=0: materialised)
+_LAZY_BWD = os.environ.get("EWDML_LAZY_BN", "1") != "0"
+
+
 class _BNAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, h, res, cbias, gamma, beta, rmean, rvar, nbt, momentum, eps, pool, mode,
-                pre=None, res_sink=None):
+                pre=None, res_sink=None, lazy=False):
         C_ = require()
         N, C, H, W = h.shape
         dev = h.device
@@ -81,11 +87,24 @@ class _BNAct(torch.autograd.Function):
         cb, cb_bf16 = _bias(cbias)
         # pre: (partials, rows) of the batch statistics from the producing MFMA conv's epilogue
         part, pre_rows = (pre[0], pre[1]) if pre is not None else (_part(dev), 0)
-        C_.bn_relu_fwd(_ptr(h), _ptr(res), _ptr(y), _ptr(code), _ptr(stats), _ptr(part),
-                       _ptr(g32), _ptr(b32), _ptr(cb), _ptr(rmean), _ptr(rvar), _ptr(nbt), N, H,
-                       W, C, int(h.dtype == torch.bfloat16), int(pool), _MODES[mode], 1,
-                       -1.0 if momentum is None else float(momentum), float(eps), cb_bf16,
-                       _stream(), int(pre_rows))
+        args = (_ptr(h), _ptr(res), _ptr(y), _ptr(code), _ptr(stats), _ptr(part), _ptr(g32),
+                _ptr(b32), _ptr(cb), _ptr(rmean), _ptr(rvar), _ptr(nbt), N, H, W, C,
+                int(h.dtype == torch.bfloat16), int(pool), _MODES[mode], 1,
+                -1.0 if momentum is None else float(momentum), float(eps), cb_bf16, _stream(),
+                int(pre_rows))
+        lazy = bool(lazy) and mode == "relu" and res is None and h.dtype == torch.float32
+        C_.bn_relu_fwd(*args, 1 if lazy else 0)
+        if lazy:
+            # statistics only: the consuming Winograd conv applies this layer in its input
+            # transform (ops/conv.py, winograd_f32.hip WgSrc), writing the pool codes and
+            # counting num_batches_tracked; y is never written unless materialised
+            y._ew_lazy_fwd = (h, stats, code, nbt, pool)
+            y._ew_materialize = lambda: C_.bn_relu_fwd(*args, 2)
+            no_nbt = args[:11] + (0,) + args[12:]  # after a consumer counted the batch
+            y._ew_materialize_no_nbt = lambda: C_.bn_relu_fwd(*no_nbt, 2)
+        # the backward may leave its apply to the Winograd conv that produced h
+        ctx.lazy_bwd = (_LAZY_BWD and getattr(h, "_ew_wino_out", False) and mode == "relu"
+                        and res is None and h.dtype == torch.float32)
         ctx.pool, ctx.mode = pool, mode
         ctx.res_sink = res_sink
         ctx.cb_dtype = None if cb is None else cb.dtype
@@ -121,14 +140,20 @@ class _BNAct(torch.autograd.Function):
             part, pre_rows = pre[0], pre[1]
             global PRE_BWD_USED
             PRE_BWD_USED += 1
-        C_.bn_relu_bwd(_ptr(h), _ptr(res), _ptr(dy), _ptr(code), _ptr(stats), _ptr(coef),
-                       _ptr(part), _ptr(dx), _ptr(dres), _ptr(dg), _ptr(db), _ptr(dcb), N,
-                       H, W, C, int(h.dtype == torch.bfloat16), int(ctx.pool),
-                       _MODES[ctx.mode], int(ctx.cb_dtype == torch.bfloat16), _stream(),
-                       int(pre_rows))
+        args = (_ptr(h), _ptr(res), _ptr(dy), _ptr(code), _ptr(stats), _ptr(coef), _ptr(part),
+                _ptr(dx), _ptr(dres), _ptr(dg), _ptr(db), _ptr(dcb), N, H, W, C,
+                int(h.dtype == torch.bfloat16), int(ctx.pool), _MODES[ctx.mode],
+                int(ctx.cb_dtype == torch.bfloat16), _stream(), int(pre_rows))
+        lazy = ctx.lazy_bwd and sink is None
+        C_.bn_relu_bwd(*args, 1 if lazy else 0)
+        if lazy:
+            # statistics only (coef, dgamma, dbeta): the Winograd conv that produced h forms dx
+            # in its backward input transform (ops/conv.py); dx is written only if materialised
+            dx._ew_lazy_bwd = (h, dy, code, stats, coef, ctx.pool)
+            dx._ew_materialize = lambda: C_.bn_relu_bwd(*args, 2)
         if sink is not None:  # the residual's gradient goes to the block's first conv (ops/conv)
             sink.grad, dres = dres, None
-        return dx, dres, dcb, dg, db, None, None, None, None, None, None, None, None, None
+        return dx, dres, dcb, dg, db, None, None, None, None, None, None, None, None, None, None
 
 
 def _apply_eval(h, stats, pool, mode="relu", res=None):
@@ -142,7 +167,7 @@ def _apply_eval(h, stats, pool, mode="relu", res=None):
     code = torch.empty((N,) + out_hw + (C,), dtype=torch.uint8, device=dev) if pool else None
     C_.bn_relu_fwd(_ptr(h), _ptr(res), _ptr(y), _ptr(code), _ptr(stats), 0, 0, 0, 0, 0, 0, 0, N,
                    H, W, C, int(h.dtype == torch.bfloat16), int(pool), _MODES[mode], 0, 0.0, 0.0,
-                   0, _stream(), 0)
+                   0, _stream(), 0, 0)
     return y
 
 
@@ -174,7 +199,7 @@ def kernel_path(h, bn, res=None, pool=False) -> bool:
     return ok and (bn.training or bn.running_mean is None)
 
 
-def bn_act(h, bn, mode="relu", res=None, cbias=None, pool=False, res_sink=None):
+def bn_act(h, bn, mode="relu", res=None, cbias=None, pool=False, res_sink=None, lazy=False):
     """``maxpool?(act(bn(h + cbias) [+ res]))`` for a ``nn.BatchNorm2d`` ``bn``; ``mode`` is
     ``relu``, ``none`` (BN only) or ``add_relu`` (``relu(bn(h) + res)``, the ResNet block
     output).  Running statistics and ``num_batches_tracked`` are updated like ``bn``'s own
@@ -197,7 +222,7 @@ def bn_act(h, bn, mode="relu", res=None, cbias=None, pool=False, res_sink=None):
         y = _BNAct.apply(h, res, cbias, bn.weight, bn.bias,
                          bn.running_mean if track else None,
                          bn.running_var if track else None, nbt, bn.momentum, bn.eps, pool,
-                         mode, getattr(h, "_ew_bn_part", None), res_sink)
+                         mode, getattr(h, "_ew_bn_part", None), res_sink, lazy)
         if y.grad_fn is not None:
             # a following MFMA conv may sum this layer's backward statistics in its
             # backward-data epilogue (ops/conv.py)
@@ -219,9 +244,22 @@ def bn_act(h, bn, mode="relu", res=None, cbias=None, pool=False, res_sink=None):
                        None if res is None else res.detach())
 
 
-def bn_relu(h, cbias, bn, pool=False):
-    """``maxpool?(relu(bn(h + cbias)))`` (VGG's conv-BN-ReLU[-pool] group)."""
-    return bn_act(h, bn, "relu", None, cbias, pool)
+def bn_relu(h, cbias, bn, pool=False, lazy=False):
+    """``maxpool?(relu(bn(h + cbias)))`` (VGG's conv-BN-ReLU[-pool] group).  ``lazy``: the output
+    feeds only an fp32 Winograd conv, which applies this layer in its input transform (the
+    returned tensor is materialised on demand by :func:`materialize`)."""
+    return bn_act(h, bn, "relu", None, cbias, pool, lazy=lazy)
+
+
+def materialize(t):
+    """Write a lazily produced BN output / BN input gradient (``_ew_lazy_*``) for a consumer that
+    cannot form it on the fly; no-op for ordinary tensors."""
+    f = getattr(t, "_ew_materialize", None)
+    if f is not None:
+        f()
+        t._ew_materialize = None
+        t._ew_lazy_fwd = t._ew_lazy_bwd = None
+    return t
 
 
 class _MaxPool2(torch.autograd.Function):
