@@ -186,6 +186,9 @@ struct CfRegs {
 // Per-thread operand staging state (NT threads).  KC tiles: thread t stages chunk t & 7 of rows
 // (t >> 3) + (NT / 8) i (i < 8 BM / NT).  RC tiles ([32 k][BN cols]): BN/4 chunks per k-row,
 // thread t stages chunk t % (BN/4) of k-rows t / (BN/4) + (4 NT / BN) i (i < 8 BN / NT).
+// 16 zero bytes in device memory (zero-initialised at module load), read by masked-out loads
+__device__ __attribute__((aligned(16))) float cf_zero_page[4];
+
 template <int MODE, int BM, int BN, int NT>
 struct CfStager {
   using L = CfLayout<MODE, BM, BN>;
@@ -236,13 +239,17 @@ struct CfStager {
       const int tap = s / CB, cb = s - tap * CB;
       const int dr = g.taps == 1 ? 0 : tap / 3 - 1, dc = g.taps == 1 ? 0 : tap - (tap / 3) * 3 - 1;
       {
+        // out-of-image taps load the zero page: a select on the loaded VALUE would make hipcc
+        // wait for this step's loads before the step's MFMAs (s_waitcnt vmcnt ahead of the
+        // masking), a select on the ADDRESS does not
         CfRegs& RG = ra;
         CF_FOR(RA, {
           const bool ok = (unsigned)(ah[i] + dr) < (unsigned)g.H &&
                           (unsigned)(aw[i] + dc) < (unsigned)g.W;
-          const f32x4 x_ = *reinterpret_cast<const f32x4*>(
-              xa + (long long)(ok ? am[i] + dr * g.W + dc : 0) * CH + cb * CF_BK + (t & 7) * 4);
-          v = ok ? x_ : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+          const float* src = ok ? xa + (long long)(am[i] + dr * g.W + dc) * CH + cb * CF_BK +
+                                      (t & 7) * 4
+                                : cf_zero_page;
+          v = *reinterpret_cast<const f32x4*>(src);
         });
       }
       if constexpr (MODE == CF_FWD) {
@@ -280,9 +287,8 @@ struct CfStager {
           const int m = s * CF_BK + t / RCB + RPB * i;
           const int hw = m % HW, h = hw / g.W, w = hw - h * g.W;
           const bool ok = (unsigned)(h + bdr) < (unsigned)g.H && (unsigned)(w + bdc) < (unsigned)g.W;
-          const f32x4 x_ = *reinterpret_cast<const f32x4*>(
-              xb + (long long)(ok ? m + bdr * g.W + bdc : 0) * g.C + bc);
-          v = ok ? x_ : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+          const float* src = ok ? xb + (long long)(m + bdr * g.W + bdc) * g.C + bc : cf_zero_page;
+          v = *reinterpret_cast<const f32x4*>(src);
         });
       }
     }
