@@ -82,7 +82,11 @@ class FusedFeatures(nn.Sequential):
         """Whether group gi's BN-ReLU(-pool) output feeds only the next group's conv and that
         conv runs Winograd on it: then the conv's input transform applies the BN layer
         (ops/nn.py bn_relu(lazy=True)) and the activation is never written."""
-        if not _LAZY or gi + 1 >= len(plan) or plan[gi + 1][0] != "cbr":
+        # pooled layers stay materialised: recomputing the 2x2 max for every patch element
+        # (16 reads of h per element) costs more than the apply kernel it would save
+        # (profiles/vgg11_bs128_fp32_current_graph.txt: conv3/5/7 input 20/17.5/16.7 us lazy
+        # against 16.2/10.9/10.4 us apply + transform); their backward stays lazy
+        if not _LAZY or pool or gi + 1 >= len(plan) or plan[gi + 1][0] != "cbr":
             return False
         from ..ops import conv as conv_hip
 
