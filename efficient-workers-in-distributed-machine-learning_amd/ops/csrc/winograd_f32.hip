@@ -429,22 +429,51 @@ __global__ __launch_bounds__(EW_BLOCK) void k_wg_output(const float* __restrict_
         if (addend) v += *reinterpret_cast<const T*>(addend + off);
         *reinterpret_cast<T*>(y + off) = v;
         if (!bnpart) continue;
+        if (!bb.h) {  // forward: this output's own statistics
+#pragma unroll
+          for (int q = 0; q < VW; ++q) {
+            s1[q] += v[q];
+            s2[q] += v[q] * v[q];
+          }
+          continue;
+        }
+        // backward sums of the BN layer whose (pooled) output this gradient is: its input h
+        // (and residual) at the row the pool routed each channel from -- the window's four
+        // candidate rows as vector loads, picked per channel by its code
+        T xh, rr{};
+        if (bb.code) {
+          const uint32_t p = (uint32_t)r, nn = p / HoWo, rm = p - nn * HoWo;
+          const uint32_t ho = rm / (uint32_t)bb.Wo, wo = rm - ho * (uint32_t)bb.Wo;
+          const uint32_t base = 4 * nn * HoWo + 4 * ho * (uint32_t)bb.Wo + 2 * wo;
+          uint32_t kw;
+          if constexpr (VW == 4)
+            kw = *reinterpret_cast<const uint32_t*>(bb.code + off);
+          else
+            kw = *reinterpret_cast<const uint16_t*>(bb.code + off);
+          T hq[4], rq[4];
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq) {
+            const size_t hr = base + (qq >> 1) * (2 * (uint32_t)bb.Wo) + (qq & 1);
+            hq[qq] = *reinterpret_cast<const T*>(bb.h + hr * Nc + c0);
+            if (bb.res) rq[qq] = *reinterpret_cast<const T*>(bb.res + hr * Nc + c0);
+          }
+#pragma unroll
+          for (int q = 0; q < VW; ++q) {
+            const uint32_t k = (kw >> (8 * q)) & 3u;
+            xh[q] = k == 0 ? hq[0][q] : k == 1 ? hq[1][q] : k == 2 ? hq[2][q] : hq[3][q];
+            if (bb.res) rr[q] = k == 0 ? rq[0][q] : k == 1 ? rq[1][q] : k == 2 ? rq[2][q] : rq[3][q];
+          }
+        } else {
+          xh = *reinterpret_cast<const T*>(bb.h + (size_t)r * Nc + c0);
+          if (bb.res) rr = *reinterpret_cast<const T*>(bb.res + (size_t)r * Nc + c0);
+        }
 #pragma unroll
         for (int q = 0; q < VW; ++q) {
-          const float dv = v[q];
-          if (bb.h) {
-            uint32_t hr = (uint32_t)r;
-            if (bb.code) hr = cf_pool_row((uint32_t)r, HoWo, (uint32_t)bb.Wo, bb.code[off + q]);
-            const float xh = bb.h[(size_t)hr * Nc + c0 + q];
-            float z = xh * sc[q] + sh[q];
-            if (bb.res) z = z + bb.res[(size_t)hr * Nc + c0 + q];
-            const float dz = (bb.relu == 0 || !(z <= 0.0f)) ? dv : 0.0f;
-            s1[q] += dz;
-            s2[q] += dz * (xh - mean[q]);
-          } else {
-            s1[q] += dv;
-            s2[q] += dv * dv;
-          }
+          float z = xh[q] * sc[q] + sh[q];
+          if (bb.res) z = z + rr[q];
+          const float dz = (bb.relu == 0 || !(z <= 0.0f)) ? v[q] : 0.0f;
+          s1[q] += dz;
+          s2[q] += dz * (xh[q] - mean[q]);
         }
       }
   }
