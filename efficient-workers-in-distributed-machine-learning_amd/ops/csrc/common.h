@@ -94,6 +94,56 @@ __device__ __forceinline__ void ew_ld4t(const GradPtrs& gp, const float* flat, c
     for (int j = 0; j < 4; ++j) xs[j] = (i + j < c.len) ? ew_ld1(gp, flat, c, i + j) : 0.0f;
   }
 }
+// A chunk is EW_CU slabs of 4 * EW_BLOCK elements; thread t owns elements [4t, 4t + 4) of each.
+// The whole chunk is loaded into registers with every load issued before any is used (a loop of
+// load -> use left one round trip per slab exposed: the codec passes ran at ~3 TB/s).  Elements
+// past c.len read as 0; callers mask them with ew_chunk_valid.
+#define EW_CU (EW_CHUNK / (4 * EW_BLOCK))
+__device__ __forceinline__ int ew_chunk_idx(int u) { return 4 * (int)threadIdx.x + u * 4 * EW_BLOCK; }
+__device__ __forceinline__ void ew_ld_chunk(const GradPtrs& gp, const float* flat, const ChunkRow& c,
+                                            float4 (&v)[EW_CU]) {
+  // source and type resolved once (uniform), so each case below is straight-line code
+  const size_t off = (size_t)c.local * EW_CHUNK;
+  const bool bf = !flat && ((gp.bf16[c.tensor >> 5] >> (c.tensor & 31)) & 1u);
+  const float* src = flat ? flat + c.start : reinterpret_cast<const float*>(gp.p[c.tensor]) + off;
+  if (c.len == EW_CHUNK && !bf) {
+#pragma unroll
+    for (int u = 0; u < EW_CU; ++u) v[u] = *reinterpret_cast<const float4*>(src + ew_chunk_idx(u));
+  } else if (c.len == EW_CHUNK) {
+    const uint16_t* s16 = reinterpret_cast<const uint16_t*>(gp.p[c.tensor]) + off;
+    uint2 r[EW_CU];
+#pragma unroll
+    for (int u = 0; u < EW_CU; ++u) r[u] = *reinterpret_cast<const uint2*>(s16 + ew_chunk_idx(u));
+#pragma unroll
+    for (int u = 0; u < EW_CU; ++u)
+      v[u] = make_float4(ew_bf16f(r[u].x), ew_bf16f(r[u].x >> 16), ew_bf16f(r[u].y),
+                         ew_bf16f(r[u].y >> 16));
+  } else {  // a tensor's last chunk
+#pragma unroll
+    for (int u = 0; u < EW_CU; ++u) {
+      float xs[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+      if (ew_chunk_idx(u) < c.len) ew_ld4t(gp, flat, c, ew_chunk_idx(u), xs);
+      v[u] = make_float4(xs[0], xs[1], xs[2], xs[3]);
+    }
+  }
+}
+__device__ __forceinline__ float ew_f4(const float4& v, int j) {
+  return j == 0 ? v.x : j == 1 ? v.y : j == 2 ? v.z : v.w;
+}
+// store back a chunk held as by ew_ld_chunk into a flat fp32 buffer (dst = chunk start)
+__device__ __forceinline__ void ew_st_chunk(float* dst, int len, const float4 (&v)[EW_CU]) {
+#pragma unroll
+  for (int u = 0; u < EW_CU; ++u) {
+    const int i = ew_chunk_idx(u);
+    if (i + 3 < len) {
+      *reinterpret_cast<float4*>(dst + i) = v[u];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (i + j < len) dst[i + j] = ew_f4(v[u], j);
+    }
+  }
+}
 // store 4 fp32 values as bf16 (8-byte store when whole)
 __device__ __forceinline__ void ew_st4_bf16(uint16_t* dst, int n, const float v[4]) {
   if (n >= 4) {

@@ -84,27 +84,23 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_hist0(GradPtrs gp,
   __syncthreads();
   uint32_t* h = hs + (threadIdx.x & (HSUB - 1));
   const ChunkRow c = chunks[blockIdx.x];
+  float4 v[EW_CU];
+  ew_ld_chunk(gp, nullptr, c, v);
+  if (EF) {  // error feedback: compress e = g + residual, staged in the residual buffer
+    float4 r[EW_CU];
+    ew_ld_chunk(gp, resid, c, r);
+#pragma unroll
+    for (int u = 0; u < EW_CU; ++u)
+      v[u] = make_float4(v[u].x + r[u].x, v[u].y + r[u].y, v[u].z + r[u].z, v[u].w + r[u].w);
+    ew_st_chunk(resid + c.start, c.len, v);
+  }
   uint32_t kmax = 0;
-  for (int i = 4 * threadIdx.x; i < c.len; i += 4 * EW_BLOCK) {
-    float xs[4];
-    ew_ld4t(gp, nullptr, c, i, xs);
-    if (EF) {  // error feedback: compress e = g + residual, staged in the residual buffer
-      float* r = resid + c.start + i;
-      if (i + 3 < c.len) {
-        float4 rv = *reinterpret_cast<float4*>(r);
-        xs[0] = xs[0] + rv.x; xs[1] = xs[1] + rv.y; xs[2] = xs[2] + rv.z; xs[3] = xs[3] + rv.w;
-        *reinterpret_cast<float4*>(r) = make_float4(xs[0], xs[1], xs[2], xs[3]);
-      } else {
-        for (int j = 0; j < 4 && i + j < c.len; ++j) {
-          xs[j] = xs[j] + r[j];
-          r[j] = xs[j];
-        }
-      }
-    }
+#pragma unroll
+  for (int u = 0; u < EW_CU; ++u) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      if (i + j < c.len) {
-        const uint32_t k = ew_key(xs[j]);
+      if (ew_chunk_idx(u) + j < c.len) {
+        const uint32_t k = ew_key(ew_f4(v[u], j));
         atomicAdd(&h[(k >> 20) * HSUB], 1u);
         kmax = max(kmax, k);
       }
@@ -145,13 +141,15 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_hist(GradPtrs gp, const float
   __syncthreads();
   const ChunkRow c = chunks[blockIdx.x];
   const uint32_t want = state[c.tensor * 4] >> MATCH;
-  for (int i = 4 * threadIdx.x; i < c.len; i += 4 * EW_BLOCK) {
-    float xs[4];
-    ew_ld4t(gp, flat, c, i, xs);
+  float4 v[EW_CU];
+  ew_ld_chunk(gp, flat, c, v);
+#pragma unroll
+  for (int u = 0; u < EW_CU; ++u) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const uint32_t k = ew_key(xs[j]);
-      if (i + j < c.len && (k >> MATCH) == want) atomicAdd(&h[(k >> SHIFT) & (NB1 - 1)], 1u);
+      const uint32_t k = ew_key(ew_f4(v[u], j));
+      if (ew_chunk_idx(u) + j < c.len && (k >> MATCH) == want)
+        atomicAdd(&h[(k >> SHIFT) & (NB1 - 1)], 1u);
     }
   }
   __syncthreads();
@@ -227,16 +225,18 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_count(
   const uint32_t thr = state[c.tensor * 4];
   uint32_t gt = 0, eq = 0;
   float sq = 0.0f;
-  for (int i = 4 * threadIdx.x; i < c.len; i += 4 * EW_BLOCK) {
-    float xs[4];
-    ew_ld4t(gp, flat, c, i, xs);
+  float4 v[EW_CU];
+  ew_ld_chunk(gp, flat, c, v);
+#pragma unroll
+  for (int u = 0; u < EW_CU; ++u) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      if (i + j < c.len) {
-        const uint32_t k = ew_key(xs[j]);
+      if (ew_chunk_idx(u) + j < c.len) {
+        const float x = ew_f4(v[u], j);
+        const uint32_t k = ew_key(x);
         if (k > thr) {
           ++gt;
-          sq = sq + xs[j] * xs[j];
+          sq = sq + x * x;
         }
         eq += (k == thr);
       }
@@ -344,14 +344,16 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_write(
   uint16_t* idx_out = reinterpret_cast<uint16_t*>(payload + idx_off);
   const uint32_t gbase = bucket_offset + (uint32_t)c.start;
   uint32_t carry_gt = 0, carry_eq = 0;
-  for (int it = 0; it < c.len; it += 4 * EW_BLOCK) {
-    const int i0 = it + 4 * threadIdx.x;
-    float xs[4];
+  float4 v[EW_CU];
+  ew_ld_chunk(gp, flat, c, v);
+#pragma unroll
+  for (int u = 0; u < EW_CU; ++u) {
+    if (u * 4 * EW_BLOCK >= c.len) break;  // uniform
+    const int i0 = ew_chunk_idx(u);
+    const float xs[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
     bool valid[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) valid[j] = (i0 + j) < c.len;
-    if (i0 < c.len) ew_ld4t(gp, flat, c, i0, xs);
-    else xs[0] = xs[1] = xs[2] = xs[3] = 0.0f;
     uint32_t ngt = 0, neq = 0;
     bool isgt[4], iseq[4];
 #pragma unroll
@@ -367,6 +369,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_write(
     const uint32_t gt_before = carry_gt + (ex & 0xffffu);
     uint32_t eqr = carry_eq + (ex >> 16);
     uint32_t pos = ebase + gt_before + min(ties, eqr);
+    float left[4];  // EF residual: what this rank did not send
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const bool sel = isgt[j] || (iseq[j] && eqr < ties);
@@ -389,7 +392,17 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_write(
         }
         ++pos;
       }
-      if (EF && valid[j]) resid[c.start + i0 + j] = xs[j] - sent;
+      left[j] = xs[j] - sent;
+    }
+    if (EF) {
+      float* r = resid + c.start + i0;
+      if (i0 + 3 < c.len) {
+        *reinterpret_cast<float4*>(r) = make_float4(left[0], left[1], left[2], left[3]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (valid[j]) r[j] = left[j];
+      }
     }
     carry_gt += tot & 0xffffu;
     carry_eq += tot >> 16;
@@ -411,6 +424,22 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_decode_apply(
   float* acc = reinterpret_cast<float*>(acc4);
   const ChunkRow c = chunks[blockIdx.x];
   const TensorRow tr = tensors[c.tensor];
+  float* p = param + c.start;
+  float* b = mom + c.start;
+  // chunk starts are 64-element aligned: float4 body + scalar tail.  The body's parameters and
+  // momenta are loaded here, before the scatter, so their latency hides behind it.
+  const int n4 = c.len >> 2;
+  float4 pv[EW_CU], bv[EW_CU];
+  if (apply) {
+#pragma unroll
+    for (int u = 0; u < EW_CU; ++u) {
+      const int i = threadIdx.x + u * EW_BLOCK;
+      if (i < n4) {
+        pv[u] = reinterpret_cast<const float4*>(p)[i];
+        bv[u] = reinterpret_cast<const float4*>(b)[i];
+      }
+    }
+  }
   ew_key_advance(sa);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   for (int i = threadIdx.x; i < (c.len + 3) / 4; i += EW_BLOCK) acc4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -452,26 +481,24 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_decode_apply(
     __syncthreads();
   }
   const float inv_n = sa.grad_scale;
-  float* p = param + c.start;
-  float* b = mom + c.start;
   float* go = grad_out ? grad_out + c.start : nullptr;
-  // chunk starts are 64-element aligned: float4 body + scalar tail
-  const int n4 = c.len >> 2;
-  for (int i = threadIdx.x; i < n4; i += EW_BLOCK) {
+#pragma unroll
+  for (int u = 0; u < EW_CU; ++u) {
+    const int i = threadIdx.x + u * EW_BLOCK;
+    if (i >= n4) break;
     const float4 a = acc4[i];
     const float4 gv = make_float4(a.x * inv_n, a.y * inv_n, a.z * inv_n, a.w * inv_n);
     if (go) reinterpret_cast<float4*>(go)[i] = gv;
     if (apply) {
-      float4 pv = reinterpret_cast<float4*>(p)[i];
-      float4 bv = reinterpret_cast<float4*>(b)[i];
-      ew_sgd(pv.x, bv.x, gv.x, sa);
-      ew_sgd(pv.y, bv.y, gv.y, sa);
-      ew_sgd(pv.z, bv.z, gv.z, sa);
-      ew_sgd(pv.w, bv.w, gv.w, sa);
-      reinterpret_cast<float4*>(p)[i] = pv;
-      reinterpret_cast<float4*>(b)[i] = bv;
+      float4 pu = pv[u], bu = bv[u];
+      ew_sgd(pu.x, bu.x, gv.x, sa);
+      ew_sgd(pu.y, bu.y, gv.y, sa);
+      ew_sgd(pu.z, bu.z, gv.z, sa);
+      ew_sgd(pu.w, bu.w, gv.w, sa);
+      reinterpret_cast<float4*>(p)[i] = pu;
+      reinterpret_cast<float4*>(b)[i] = bu;
       if (shadow) {  // bf16 compute copy of the updated master weights
-        const float v4[4] = {pv.x, pv.y, pv.z, pv.w};
+        const float v4[4] = {pu.x, pu.y, pu.z, pu.w};
         ew_st4_bf16(shadow + c.start + 4 * i, 4, v4);
       }
     }
