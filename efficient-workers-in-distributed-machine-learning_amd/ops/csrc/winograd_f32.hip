@@ -47,6 +47,13 @@ void ew_cf_gemm_batched(const float* a, const float* b, float* out, int M, int N
                         long long a_bs, long long b_bs, long long o_bs, bool nt, bool flip,
                         hipStream_t s);
 
+// channels per thread of the m = 2 transforms.  2 (twice the threads) was measured on VGG-11:
+// output transforms 114 -> 101 us/step, input transforms 132 -> 138, step time unchanged -- the
+// 8x8-map passes already run at ~5 TB/s -- and it would cap C_out at 512; kept at 4.
+#ifndef WG2_VW
+#define WG2_VW 4
+#endif
+
 namespace {
 
 // Transform matrices as constexpr functions: inside fully unrolled loops every coefficient is a
@@ -95,7 +102,7 @@ __device__ constexpr float wg_at(int i, int j) {
 template <int M>
 struct Wg {
   static constexpr int A = M + 2;             // patch / transform size
-  static constexpr int VW = M == 2 ? 4 : 2;   // channels per thread (registers: A*A vectors)
+  static constexpr int VW = M == 2 ? WG2_VW : 2;   // channels per thread (registers: A*A vectors)
   typedef float V __attribute__((ext_vector_type(VW)));
 };
 
@@ -536,7 +543,7 @@ long long wg_tiles(int m, long long N, int H, int W) { return N * (H / m) * (W /
 
 void wg_check(int m, long long N, int H, int W, int Cin, int Cout, const char* what) {
   const long long tiles = wg_tiles(m, N, H, W);
-  const int vw = m == 2 ? 4 : 2;
+  const int vw = m == 2 ? WG2_VW : 2;
   const bool pow2 = Cout >= 64 && Cout <= 256 * vw && (Cout & (Cout - 1)) == 0;
   if ((m != 2 && m != 4) || H % m || W % m || tiles % 64 || Cin % 32 || !pow2 ||
       (long long)(m + 2) * (m + 2) * tiles * std::max(Cin, Cout) >= (1LL << 31))
@@ -646,7 +653,7 @@ void wino_wgrad(const float* dy, const float* V, float* dw, float* d, int d_read
 }  // namespace
 
 void ew_wino_f32_weight(uintptr_t w, uintptr_t U, int Nc, int C, int m, uintptr_t stream) {
-  const int vw = m == 2 ? 4 : 2;
+  const int vw = m == 2 ? WG2_VW : 2;
   if ((m != 2 && m != 4) || C % vw || Nc <= 0)
     throw std::runtime_error("ewdml winograd f32: weight needs m in {2, 4}, C % 4 == 0");
   const long long n = (long long)Nc * (C / vw);
