@@ -238,46 +238,54 @@ __device__ __forceinline__ double ew_wave_sum_d(double v) {
 
 // Sum the nblk partial rows of NS quantities per channel in a fixed order.  Block = 16 channels
 // (t & 15) x 16 row slices (t >> 4): a wave's load covers 4 rows x 16 consecutive channels (64-B
-// segments, not one channel per lane -- the channel-strided form was 5-10 us per call), each
-// thread keeps 4 rows of every quantity in flight, slices are combined through LDS in order.
-// Returns true (for the 16 threads of slice 0, c < C) with out[] holding the channel's sums.
+// segments; 4 channels x 64 slices -- 16-B segments, 16 lines per load -- was slower, 5.7 -> 7.2
+// us), each thread issues the loads of 16 of its rows for every quantity before adding any (was 4:
+// ~8 dependent round trips for VGG's 512-row partials).  Slices combine by a fixed shuffle tree
+// within each wave (lanes with the same channel: xor 16, 32) and then over the 4 waves in order
+// through LDS.  Returns true (for lanes 0-15 of wave 0, c < C) with out[] holding the sums.
 constexpr int EW_FIN_CH = 16;
 template <int NS>
 __device__ __forceinline__ bool ew_sum_parts(const float* __restrict__ part, int nblk, int C,
                                              int c, double out[NS]) {
-  __shared__ double red[NS][EW_BLOCK];
-  const int t = threadIdx.x, rs = t / EW_FIN_CH;
+  __shared__ double red[NS][EW_WAVES][EW_FIN_CH];
+  const int t = threadIdx.x, rs = t / EW_FIN_CH, lane = t & 63, w = t >> 6;
   constexpr int RS = EW_BLOCK / EW_FIN_CH;  // row slices
+  constexpr int U = 16;                     // rows in flight per thread
   double acc[NS];
 #pragma unroll
   for (int s = 0; s < NS; ++s) acc[s] = 0.0;
   if (c < C) {
-    int b = rs;
-    for (; b + 3 * RS < nblk; b += 4 * RS) {
-      float v[NS][4];
+    for (int b0 = rs; b0 < nblk; b0 += U * RS) {
+      // unconditional loads of a clamped row, masked when added: a guarded load is a branch,
+      // and hipcc waits for every load at each branch merge (one round trip per row)
+      float v[NS][U];
 #pragma unroll
       for (int s = 0; s < NS; ++s)
 #pragma unroll
-        for (int u = 0; u < 4; ++u) v[s][u] = part[((long long)s * nblk + b + u * RS) * C + c];
+        for (int u = 0; u < U; ++u) {
+          const int b = min(b0 + u * RS, nblk - 1);
+          v[s][u] = part[((long long)s * nblk + b) * C + c];
+        }
 #pragma unroll
       for (int s = 0; s < NS; ++s)
 #pragma unroll
-        for (int u = 0; u < 4; ++u) acc[s] += (double)v[s][u];
-    }
-    for (; b < nblk; b += RS) {
-#pragma unroll
-      for (int s = 0; s < NS; ++s) acc[s] += (double)part[((long long)s * nblk + b) * C + c];
+        for (int u = 0; u < U; ++u)
+          if (b0 + u * RS < nblk) acc[s] += (double)v[s][u];
     }
   }
 #pragma unroll
-  for (int s = 0; s < NS; ++s) red[s][t] = acc[s];
+  for (int s = 0; s < NS; ++s) {
+#pragma unroll
+    for (int o = EW_FIN_CH; o < 64; o <<= 1) acc[s] += __shfl_xor(acc[s], o, 64);
+    if (lane < EW_FIN_CH) red[s][w][lane] = acc[s];
+  }
   __syncthreads();
-  if (rs != 0 || c >= C) return false;
+  if (t >= EW_FIN_CH || c >= C) return false;
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
-    double a = 0.0;
+    double a = red[s][0][t];
 #pragma unroll
-    for (int r = 0; r < RS; ++r) a += red[s][r * EW_FIN_CH + t];
+    for (int r = 1; r < EW_WAVES; ++r) a += red[s][r][t];
     out[s] = a;
   }
   return true;
