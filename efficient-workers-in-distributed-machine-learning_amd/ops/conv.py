@@ -53,6 +53,9 @@ _EPI_MAX = int(os.environ.get("EWDML_EPI_MAX", str(1 << 23)))
 _WINO = os.environ.get("EWDML_WINOGRAD", "1") != "0"
 _WINO_MIN_C = int(os.environ.get("EWDML_WINO_MIN_C", "128"))
 _WINO_TILE = os.environ.get("EWDML_WINO_TILE", "2")
+# m = 4 for the layers with min(C_in, C_out) <= this many channels (and m = EWDML_WINO_TILE above),
+# for layers below _WINO_MIN_C too: 0 = off
+_WINO_M4_MAX_C = int(os.environ.get("EWDML_WINO_M4_MAX_C", "0"))
 # most K-splits of a Winograd weight-gradient GEMM (slab memory: splits x a^2 x C_out x C_in floats)
 _WINO_WG_SPLITS = int(os.environ.get("EWDML_WINO_WG_SPLITS", "4"))
 
@@ -93,6 +96,8 @@ def wino_tile_for(shape, dtype, w) -> int:
     Nc = w.shape[0]
     if w.shape[1] != C:
         return 0
+    if min(C, Nc) <= _WINO_M4_MAX_C:
+        return 4 if min(C, Nc) >= 32 and _wino_fits(N, C, Nc, H, W, 4) else 0
     if min(C, Nc) < _WINO_MIN_C:
         return 0
     order = {"2": (2,), "4": (4,)}.get(_WINO_TILE, (4, 2))
