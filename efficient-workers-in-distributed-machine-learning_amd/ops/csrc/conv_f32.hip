@@ -652,11 +652,17 @@ __global__ __launch_bounds__(EW_BLOCK) void k_cf_stem_fwd(const float* __restric
                                                           float* __restrict__ y, int H, int W,
                                                           int Nc, int M,
                                                           float* __restrict__ bnpart, int nrows) {
-  __shared__ __attribute__((aligned(16))) float patch[cs_patch_floats<128>()];
-  __shared__ __attribute__((aligned(16))) float wsm[64 * (CS_KP + 4)];
-  __shared__ __attribute__((aligned(16))) float ysm[128 * 68];
+  // the output staging tile aliases the input patch and the weights (dead after the MFMAs): ~37
+  // KB of LDS, 4 blocks per CU -- the grid's 4 blocks per CU in one round (53 KB: 3 + a tail of 1)
+  constexpr int PF = (cs_patch_floats<128>() + 3) & ~3, WF = 64 * (CS_KP + 8), YF = 128 * 68;
+  __shared__ __attribute__((aligned(16))) float smem[PF + WF > YF ? PF + WF : YF];
   __shared__ float red[EW_WAVES][2][64];
-  constexpr int WP = CS_KP + 4;  // wsm pitch
+  float* patch = smem;
+  float* wsm = smem + PF;
+  float* ysm = smem;
+  // wsm pitch: 36 floats puts the 16 channel rows x 4 k of a b read on 64 distinct banks (32 put
+  // them on 8: 8-way conflicts on every weight read)
+  constexpr int WP = CS_KP + 8;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6, li = lane & 15, g = lane >> 4;
   const int m0 = blockIdx.x * 128, n0 = blockIdx.y * 64;
   for (int e = t; e < 64 * CS_KP; e += EW_BLOCK) {
@@ -688,6 +694,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_cf_stem_fwd(const float* __restric
     }
   }
   float sm[4], sq[4];
+  __syncthreads();  // every wave is done with patch / wsm before ysm overwrites them
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     sm[j] = sq[j] = 0.0f;

@@ -148,6 +148,17 @@ struct V8<float> {
   static __device__ __forceinline__ float rnd(float v) { return v; }
 };
 
+// 8 consecutive per-channel coefficients from LDS (p 32-B aligned: c0 % 8 == 0) as two b128 reads.
+// Lanes hold c0 = 8 * lane: eight scalar reads put 8 lanes on each bank (8-way conflicts: the
+// apply kernels ran ~20 conflict cycles per LDS instruction); a b128 read serves 8 lanes per pass
+// over 64 distinct banks.
+__device__ __forceinline__ void ew_lds8(const float* p, float v[8]) {
+  const float4 a = *reinterpret_cast<const float4*>(p);
+  const float4 b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
 __device__ __forceinline__ float ew_relu(float v) { return (v > 0.0f || v != v) ? v : 0.0f; }
 __device__ __forceinline__ bool ew_relu_pass(float v) { return !(v <= 0.0f); }  // NaN passes
 
@@ -363,11 +374,8 @@ __global__ __launch_bounds__(EW_BLOCK) void k_bn_fwd_apply(const T* __restrict__
     const uint32_t row = v / tpr;
     const int c0 = (int)(v - row * tpr) * 8;
     float sc[8], sh[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      sc[j] = lsc[c0 + j];
-      sh[j] = lsh[c0 + j];
-    }
+    ew_lds8(lsc + c0, sc);
+    ew_lds8(lsh + c0, sh);
     if constexpr (MODE != EW_BN_RELU_POOL) {
       float x[8];
       V8<T>::ld(h + (long long)row * C + c0, x);
@@ -568,18 +576,23 @@ __global__ __launch_bounds__(EW_BLOCK) void k_bn_bwd_apply(
     const int c0 = (int)(v - row * tpr) * 8;
     float d[8];
     V8<T>::ld(dy + (long long)row * C + c0, d);
+    float mn[8], sc[8], sh[8], ce[8], cf[8];
+    ew_lds8(lm + c0, mn);
+    ew_lds8(lsc + c0, sc);
+    ew_lds8(lsh + c0, sh);
+    ew_lds8(le + c0, ce);
+    ew_lds8(lf + c0, cf);
     if constexpr (MODE != EW_BN_RELU_POOL) {
       float x[8], o[8], rr[8], dzs[8];
       V8<T>::ld(h + (long long)row * C + c0, x);
       if constexpr (MODE == EW_BN_ADD_RELU) V8<T>::ld(res + (long long)row * C + c0, rr);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const int c = c0 + j;
-        float vv = x[j] * lsc[c] + lsh[c];
+        float vv = x[j] * sc[j] + sh[j];
         if constexpr (MODE == EW_BN_ADD_RELU) vv = vv + rr[j];
         const float dz = ew_act_pass<MODE>(vv) ? d[j] : 0.0f;
         dzs[j] = dz;
-        o[j] = lsc[c] * dz + le[c] * (x[j] - lm[c]) + lf[c];
+        o[j] = sc[j] * dz + ce[j] * (x[j] - mn[j]) + cf[j];
       }
       V8<T>::st(dx + (long long)row * C + c0, o);
       if constexpr (MODE == EW_BN_ADD_RELU) V8<T>::st(dres + (long long)row * C + c0, dzs);
@@ -594,9 +607,8 @@ __global__ __launch_bounds__(EW_BLOCK) void k_bn_bwd_apply(
         V8<T>::ld(h + ir * C + c0, x);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const int c = c0 + j;
-          const float dz = (k[j] == q && ew_relu_pass(x[j] * lsc[c] + lsh[c])) ? d[j] : 0.0f;
-          o[j] = lsc[c] * dz + le[c] * (x[j] - lm[c]) + lf[c];
+          const float dz = (k[j] == q && ew_relu_pass(x[j] * sc[j] + sh[j])) ? d[j] : 0.0f;
+          o[j] = sc[j] * dz + ce[j] * (x[j] - mn[j]) + cf[j];
         }
         V8<T>::st(dx + ir * C + c0, o);
       }
