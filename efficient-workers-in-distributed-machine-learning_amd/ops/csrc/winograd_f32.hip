@@ -47,9 +47,10 @@ void ew_cf_gemm_batched(const float* a, const float* b, float* out, int M, int N
                         long long a_bs, long long b_bs, long long o_bs, bool nt, bool flip,
                         hipStream_t s);
 
-// channels per thread of the m = 2 transforms.  2 (twice the threads) was measured on VGG-11:
-// output transforms 114 -> 101 us/step, input transforms 132 -> 138, step time unchanged -- the
-// 8x8-map passes already run at ~5 TB/s -- and it would cap C_out at 512; kept at 4.
+// channels per thread of the m = 2 input / weight / weight-gradient transforms.  2 (twice the
+// threads) was measured on VGG-11: input transforms 132 -> 138 us/step (the 8x8-map passes
+// already run at ~5 TB/s), output transforms 114 -> 101 -- so the output transform takes its own
+// width (k_wg_output's VW: 2 where C_out <= 512) and these stay at 4.
 #ifndef WG2_VW
 #define WG2_VW 4
 #endif
@@ -386,14 +387,16 @@ __global__ __launch_bounds__(EW_BLOCK) void k_wg_dy(const float* __restrict__ dy
 // squares; backward: CfBnBwd's sum dz, sum dz * (h - mean)) -> row blockIdx.x of bnpart[2][nb][Nc].
 // Block: tiles [b * tpb, (b + 1) * tpb) x all Nc channels; thread: channel vector t % (Nc / VW),
 // tiles t / (Nc / VW) + k * rpi (rpi = 256 / (Nc / VW) tiles per pass, Nc a power of two).
-template <int M>
+// VW channels per thread, independent of the other transforms' width: 2 where Nc <= 512 (twice
+// the threads of 4: 114 -> 101 us/step of output transforms on VGG-11, profiles/ab/README.md)
+template <int M, int VW>
 __global__ __launch_bounds__(EW_BLOCK) void k_wg_output(const float* __restrict__ Mo,
                                                         float* __restrict__ y, int H, int W,
                                                         int Nc, long long tiles, int tpb,
                                                         float* __restrict__ bnpart, CfBnBwd bb,
                                                         const float* __restrict__ addend) {
-  using T = typename Wg<M>::V;
-  constexpr int A = Wg<M>::A, VW = Wg<M>::VW;
+  typedef float T __attribute__((ext_vector_type(VW)));
+  constexpr int A = Wg<M>::A;
   __shared__ float red[2][EW_BLOCK * 4];
   const int tpr = Nc / VW, rpi = EW_BLOCK / tpr;
   const int t = threadIdx.x, rg = t / tpr, c0 = (t - rg * tpr) * VW;
@@ -557,7 +560,8 @@ template <int M>
 int wg_output(const float* Mo, float* y, long long N, int H, int W, int Nc, float* bnpart,
               long long bnpart_floats, const CfBnBwd& bb, const float* addend, hipStream_t s) {
   const long long tiles = wg_tiles(M, N, H, W);
-  const int rpi = EW_BLOCK / (Nc / Wg<M>::VW);
+  const int ovw = Nc <= 2 * EW_BLOCK ? 2 : 4;
+  const int rpi = EW_BLOCK / (Nc / ovw);
   long long tpb = rpi, nblk = (tiles + tpb - 1) / tpb;
   if (bnpart) {
     while (nblk > 1024) {
@@ -570,8 +574,12 @@ int wg_output(const float* Mo, float* y, long long N, int H, int W, int Nc, floa
     tpb = rpi;
     nblk = (tiles + tpb - 1) / tpb;
   }
-  hipLaunchKernelGGL(k_wg_output<M>, dim3((unsigned)nblk), dim3(EW_BLOCK), 0, s, Mo, y, H, W, Nc,
-                     tiles, (int)tpb, bnpart, bb, addend);
+  if (ovw == 2)
+    hipLaunchKernelGGL((k_wg_output<M, 2>), dim3((unsigned)nblk), dim3(EW_BLOCK), 0, s, Mo, y, H,
+                       W, Nc, tiles, (int)tpb, bnpart, bb, addend);
+  else
+    hipLaunchKernelGGL((k_wg_output<M, 4>), dim3((unsigned)nblk), dim3(EW_BLOCK), 0, s, Mo, y, H,
+                       W, Nc, tiles, (int)tpb, bnpart, bb, addend);
   EW_CHECK_LAUNCH();
   return bnpart ? (int)nblk : 0;
 }
