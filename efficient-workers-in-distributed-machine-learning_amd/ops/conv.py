@@ -58,6 +58,90 @@ _WINO_TILE = os.environ.get("EWDML_WINO_TILE", "2")
 _WINO_M4_MAX_C = int(os.environ.get("EWDML_WINO_M4_MAX_C", "0"))
 # most K-splits of a Winograd weight-gradient GEMM (slab memory: splits x a^2 x C_out x C_in floats)
 _WINO_WG_SPLITS = int(os.environ.get("EWDML_WINO_WG_SPLITS", "4"))
+# Deferred Winograd weight-gradient output transforms (dw = G^T dU G).  dw feeds only the
+# optimizer / codec, so its transform rides in the next same-m Winograd backward-data input launch
+# (ops/csrc/winograd_f32.hip WgOut) instead of a launch of its own.  Deferred only for a leaf
+# Parameter whose .grad is None when its conv's backward runs (no accumulate-add reads dw).  The
+# job holds the Parameter, not dw (an extra reference would make autograd's AccumulateGrad copy
+# the unwritten dw instead of adopting it), and writes into whatever .grad autograd installed:
+# the adopted dw, or a copy that the transform then overwrites.  Flushed as a launch of its own by
+# a second deferral, at the end of the backward pass (an autograd final callback, run on the
+# caller's current stream) and by the exchange engine before it encodes a bucket
+# (parallel/engine.py), so a bucket's gradients are complete when its encode starts.
+_DEFER_WOUT = os.environ.get("EWDML_WINO_DEFER_WOUT", "1") != "0"
+_PENDING = None  # (src, split, param, Nc, C, m, keep-alive tensors)
+_POISON_DW = False  # tests: NaN-fill each fresh dw, so a read before its transform shows
+
+
+def _job_dest(job):
+    """Pointer the job's transform writes (the parameter's .grad), or None (nothing to write),
+    and a (grad, temp) pair to copy afterwards when .grad has another layout."""
+    g = job[2].grad
+    if g is None:
+        return None, None
+    if g.dtype == torch.float32 and g.is_contiguous(memory_format=torch.channels_last):
+        return _ptr(g), None
+    tmp = torch.empty(g.shape, dtype=torch.float32, device=g.device,
+                      memory_format=torch.channels_last)
+    return _ptr(tmp), (g, tmp)
+
+
+def flush_pending(final=False):
+    """Run a deferred weight-gradient output transform now.  Returns False if one stays pending:
+    its parameter's .grad is not installed yet (dropped instead when ``final``: the end of the
+    backward pass, after which nothing will install it)."""
+    global _PENDING
+    job = _PENDING
+    if job is None:
+        return True
+    dest, fix = _job_dest(job)
+    if dest is None and not final:
+        return False
+    _PENDING = None
+    if dest is None:
+        return True
+    src, split, _p, Nc, C, m, _keep = job
+    require().wino_f32_wgrad_out(_ptr(src), split, dest, Nc, C, m, _stream())
+    if fix is not None:
+        fix[0].copy_(fix[1])
+    return True
+
+
+def _flush_final():
+    flush_pending(final=True)
+
+
+def _take_pending(m):
+    """The pending job as riding arguments of an m-tile backward-data call (zeros: none)."""
+    global _PENDING
+    job = _PENDING
+    if job is None:
+        return (0, 1, 0, 0, 0), None
+    if job[5] != m:
+        return (0, 1, 0, 0, 0), None
+    dest, fix = _job_dest(job)
+    if dest is None:  # .grad not installed yet: stays pending for a later flush
+        return (0, 1, 0, 0, 0), None
+    if fix is not None:  # an unusual .grad layout: a launch of its own (with the copy)
+        flush_pending()
+        return (0, 1, 0, 0, 0), None
+    _PENDING = None
+    src, split, _p, Nc, C = job[:5]
+    return (_ptr(src), split, dest, Nc, C), job
+
+
+def _can_defer(ctx):
+    # nothing may read the gradient before a flush: no tensor hooks on the weight, and no
+    # post-accumulate hooks but the exchange engine's (which flushes before it reads,
+    # parallel/engine.py marks them in _ew_engine_hooks)
+    p = getattr(ctx, "w_param", None)
+    if not (_DEFER_WOUT and p is not None and p.grad is None and p.dtype == torch.float32
+            and p.requires_grad and not torch.is_grad_enabled()):
+        return False
+    if getattr(p, "_backward_hooks", None):
+        return False
+    post = getattr(p, "_post_accumulate_grad_hooks", None)
+    return not post or len(post) <= getattr(p, "_ew_engine_hooks", 0)
 
 
 def set_winograd(on: bool, min_c: int = None, tile=None):
@@ -261,6 +345,9 @@ class _Conv(torch.autograd.Function):
             rows = fwd(_ptr(x), _ptr(w), _ptr(y), _ptr(ws), ws.numel(), N, H, W, C, Nc, k,
                        _ptr(part), part.numel(), _stream())
         ctx.save_for_backward(x, w)
+        # the leaf Parameter itself (not a cast / copy): its .grad decides whether the Winograd
+        # weight-gradient output transform may be deferred (_can_defer)
+        ctx.w_param = w if isinstance(w, torch.nn.Parameter) else None
         ctx.bn_part = (part, rows) if rows > 0 else None
         ctx.bn_node = bn_node
         ctx.sink = sink
@@ -284,6 +371,8 @@ class _Conv(torch.autograd.Function):
         dy = dy.contiguous(memory_format=torch.channels_last)
         if dy.dtype != x.dtype:
             dy = dy.to(x.dtype)
+        if ctx.wino is None:  # nothing here carries a deferred transform: run it while warm
+            flush_pending()
         ws = _ws(x.device)
         f32 = x.dtype == torch.float32
         bwd_data = C_.conv_f32_bwd_data if f32 else C_.conv_bwd_data
@@ -316,15 +405,20 @@ class _Conv(torch.autograd.Function):
                 buf = torch.empty(aa * t * (C + Nc), dtype=torch.float32, device=x.device)
 
                 def bwd_data(dy_, w_, dx_, ws_, wsn, *rest):  # same contract, Winograd
+                    # a deferred weight-gradient output transform of a later layer rides along
+                    wo, job = _take_pending(m)
                     if lazy is not None:  # dy formed from the BN layer's backward on the fly
                         oh, odn, ocode, ostats, ocoef, opool = lazy
-                        return C_.wino_f32_bwd_data_bn(
+                        r = C_.wino_f32_bwd_data_bn(
                             _ptr(oh), _ptr(odn), _ptr(ocode), _ptr(ostats), _ptr(ocoef),
                             int(opool), w_, _ptr(U), dx_, _ptr(buf), _ptr(buf) + 4 * aa * t * Nc,
-                            *rest[:5], m, *rest[6:-1], _ptr(D), rest[-1])
-                    return C_.wino_f32_bwd_data(dy_, w_, _ptr(U), dx_, _ptr(buf),
-                                                _ptr(buf) + 4 * aa * t * Nc, *rest[:5], m,
-                                                *rest[6:-1], _ptr(D), rest[-1])
+                            *rest[:5], m, *rest[6:-1], _ptr(D), *wo, rest[-1])
+                    else:
+                        r = C_.wino_f32_bwd_data(dy_, w_, _ptr(U), dx_, _ptr(buf),
+                                                 _ptr(buf) + 4 * aa * t * Nc, *rest[:5], m,
+                                                 *rest[6:-1], _ptr(D), *wo, rest[-1])
+                    del job  # enqueued: the stream orders any reuse of its buffers after it
+                    return r
                 d_ready = int(D is not None)
             if link is None:
                 bwd_data(_ptr(dy), _ptr(w), _ptr(dx), _ptr(ws), ws.numel(), N, H, W, C, Nc, k, 0,
@@ -349,8 +443,19 @@ class _Conv(torch.autograd.Function):
                 dU = torch.empty(aa * Nc * C, dtype=torch.float32, device=x.device)
                 slabs = torch.empty(_WINO_WG_SPLITS * aa * Nc * C + 64, dtype=torch.float32,
                                     device=x.device)
-                C_.wino_f32_wgrad(_ptr(dy), _ptr(V), _ptr(dw), _ptr(D), d_ready, _ptr(dU),
-                                  _ptr(slabs), slabs.numel(), N, H, W, C, Nc, m, _stream())
+                # one pending job at a time: an earlier one is flushed first (if it cannot be
+                # yet, this layer's transform runs now)
+                if _POISON_DW:
+                    dw.fill_(float("nan"))
+                defer = _can_defer(ctx) and flush_pending()
+                split = C_.wino_f32_wgrad(_ptr(dy), _ptr(V), _ptr(dw), _ptr(D), d_ready,
+                                          _ptr(dU), _ptr(slabs), slabs.numel(), N, H, W, C, Nc,
+                                          m, int(defer), _stream())
+                if defer:
+                    global _PENDING
+                    _PENDING = (slabs if split > 1 else dU, split, ctx.w_param, Nc, C, m,
+                                (dU, slabs))
+                    torch.autograd.Variable._execution_engine.queue_callback(_flush_final)
             else:
                 wgrad = C_.conv_f32_wgrad if f32 else C_.conv_wgrad
                 wgrad(_ptr(dy), _ptr(x), _ptr(dw), _ptr(ws), ws.numel(), N, H, W, C, Nc, k,
@@ -381,6 +486,7 @@ class _ConvStem(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         C_ = require()
+        flush_pending()  # a deferred Winograd weight-gradient transform, while its data is warm
         x, w = ctx.saved_tensors
         N, C, H, W = x.shape
         Nc = w.shape[0]

@@ -285,6 +285,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("wino_f32_fwd", &ew_wino_f32_fwd);
   m.def("wino_f32_bwd_data", &ew_wino_f32_bwd_data);
   m.def("wino_f32_wgrad", &ew_wino_f32_wgrad);
+  m.def("wino_f32_wgrad_out", &ew_wino_f32_wgrad_out);
   m.def("wino_f32_fwd_bn", &ew_wino_f32_fwd_bn);
   m.def("wino_f32_bwd_data_bn", &ew_wino_f32_bwd_data_bn);
   m.def("maxpool2_nhwc", &ew_maxpool2_nhwc);

@@ -215,7 +215,8 @@ int ew_wino_f32_bwd_data(uintptr_t dy, uintptr_t w, uintptr_t U, uintptr_t dx, u
                          uintptr_t Mo, long long N, int H, int W, int C, int Nc, int m,
                          uintptr_t bn_h, uintptr_t bn_res, uintptr_t bn_code, uintptr_t bn_stats,
                          int bn_relu, uintptr_t bnpart, long long bnpart_floats,
-                         uintptr_t addend, uintptr_t D, uintptr_t stream);
+                         uintptr_t addend, uintptr_t D, uintptr_t wo_src, int wo_split,
+                         uintptr_t wo_dw, int wo_Nc, int wo_C, uintptr_t stream);
 // the same with the BatchNorm(+ReLU)(+2x2 pool) layer in front applied in the input transform
 // (forward; its pool codes written here) / the BatchNorm backward of this conv's output formed
 // in the input transform (backward data): winograd_f32.hip WgSrc
@@ -229,10 +230,14 @@ int ew_wino_f32_bwd_data_bn(uintptr_t out_h, uintptr_t out_dnext, uintptr_t out_
                             int H, int W, int C, int Nc, int m, uintptr_t bn_h, uintptr_t bn_res,
                             uintptr_t bn_code, uintptr_t bn_stats, int bn_relu, uintptr_t bnpart,
                             long long bnpart_floats, uintptr_t addend, uintptr_t D,
+                            uintptr_t wo_src, int wo_split, uintptr_t wo_dw, int wo_Nc, int wo_C,
                             uintptr_t stream);
-void ew_wino_f32_wgrad(uintptr_t dy, uintptr_t V, uintptr_t dw, uintptr_t D, int d_ready,
-                       uintptr_t U_scratch, uintptr_t ws, long long ws_floats, long long N, int H,
-                       int W, int C, int Nc, int m, uintptr_t stream);
+// (wo_*: another layer's deferred weight-gradient output transform riding in the input launch)
+int ew_wino_f32_wgrad(uintptr_t dy, uintptr_t V, uintptr_t dw, uintptr_t D, int d_ready,
+                      uintptr_t U_scratch, uintptr_t ws, long long ws_floats, long long N, int H,
+                      int W, int C, int Nc, int m, int defer_out, uintptr_t stream);
+void ew_wino_f32_wgrad_out(uintptr_t src, int split, uintptr_t dw, int Nc, int C, int m,
+                           uintptr_t stream);
 
 // ---- RCCL communicator issuing collectives on the caller's stream (rccl_comm.hip) ----
 // dtype codes: 0 f32, 1 bf16, 2 f16, 3 u8, 4 i32, 5 f64, 6 i64; op: 0 sum, 1 max, 2 min, 3 avg

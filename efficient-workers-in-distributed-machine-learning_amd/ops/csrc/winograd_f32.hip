@@ -336,20 +336,37 @@ __device__ __forceinline__ void wg_input(const float* __restrict__ x, float* __r
   }
 }
 
-// the input transform over blocks [0, nbi) and, when w is given, the weight transform over the
-// rest (one launch for both: each alone is a few-microsecond kernel)
+// Another layer's weight-gradient output transform riding along in an input launch (deferred by
+// ops/conv.py: it only feeds the optimizer / codec, so it need not cost a launch of its own)
+struct WgOut {
+  const float* src;  // dU (nsplit 1) or the K-split slabs
+  float* dw;
+  int nsplit, Nc, C;
+};
+
+template <int M>
+__device__ __forceinline__ void wg_wgrad_out(const float* __restrict__ src, int nsplit,
+                                             float* __restrict__ dw, int Nc, int C, long long g);
+
+// the input transform over blocks [0, nbi), the weight transform (when w is given) over the next
+// nbw and a riding weight-gradient output transform (wo.src) over the rest: one launch for all
+// (each alone is a few-microsecond kernel)
 template <int M, bool FLIP, int KIND>
 __global__ __launch_bounds__(EW_BLOCK) void k_wg_input(const float* __restrict__ x,
                                                        float* __restrict__ V, int H, int W, int C,
                                                        long long tiles, int nbi,
                                                        const float* __restrict__ w,
                                                        float* __restrict__ U, int Nw, int Cw,
-                                                       float* __restrict__ D, WgSrc src) {
-  if ((int)blockIdx.x < nbi)
-    wg_input<M, KIND>(x, V, H, W, C, tiles, (long long)blockIdx.x * EW_BLOCK + threadIdx.x, D,
-                      src);
+                                                       float* __restrict__ D, WgSrc src, int nbw,
+                                                       WgOut wo) {
+  const int b = (int)blockIdx.x;
+  if (b < nbi)
+    wg_input<M, KIND>(x, V, H, W, C, tiles, (long long)b * EW_BLOCK + threadIdx.x, D, src);
+  else if (b < nbi + nbw)
+    wg_weight<M, FLIP>(w, U, Nw, Cw, (long long)(b - nbi) * EW_BLOCK + threadIdx.x);
   else
-    wg_weight<M, FLIP>(w, U, Nw, Cw, (long long)(blockIdx.x - nbi) * EW_BLOCK + threadIdx.x);
+    wg_wgrad_out<M>(wo.src, wo.nsplit, wo.dw, wo.Nc, wo.C,
+                    (long long)(b - nbi - nbw) * EW_BLOCK + threadIdx.x);
 }
 
 template <int M>
@@ -508,13 +525,11 @@ __global__ __launch_bounds__(EW_BLOCK) void k_wg_output(const float* __restrict_
 
 // dw[o][r][s][i..] = (G^T (sum_z dU_z[xi]) G)[r][s], dU_z = src + z * A^2 * Nc * C
 template <int M>
-__global__ __launch_bounds__(EW_BLOCK) void k_wg_wgrad_out(const float* __restrict__ src,
-                                                           int nsplit, float* __restrict__ dw,
-                                                           int Nc, int C) {
+__device__ __forceinline__ void wg_wgrad_out(const float* __restrict__ src, int nsplit,
+                                             float* __restrict__ dw, int Nc, int C, long long g) {
   using T = typename Wg<M>::V;
   constexpr int A = Wg<M>::A, VW = Wg<M>::VW;
   const int cq = C / VW;
-  const long long g = (long long)blockIdx.x * EW_BLOCK + threadIdx.x;
   if (g >= (long long)Nc * cq) return;
   const int o = (int)(g / cq), i = (int)(g - (long long)o * cq) * VW;
   const long long xs = (long long)Nc * C;
@@ -540,6 +555,13 @@ __global__ __launch_bounds__(EW_BLOCK) void k_wg_wgrad_out(const float* __restri
     for (int s = 0; s < 3; ++s)  // (G^T dU) G
       *reinterpret_cast<T*>(w + (r * 3 + s) * C) =
           wg_dot<A>([&](int b) { return wg_g<M>(b, s); }, t[r]);
+}
+
+template <int M>
+__global__ __launch_bounds__(EW_BLOCK) void k_wg_wgrad_out(const float* __restrict__ src,
+                                                           int nsplit, float* __restrict__ dw,
+                                                           int Nc, int C) {
+  wg_wgrad_out<M>(src, nsplit, dw, Nc, C, (long long)blockIdx.x * EW_BLOCK + threadIdx.x);
 }
 
 long long wg_tiles(int m, long long N, int H, int W) { return N * (H / m) * (W / m); }
@@ -589,16 +611,19 @@ int wg_output(const float* Mo, float* y, long long N, int H, int W, int Nc, floa
 template <int M, bool FLIP>
 void wg_input(const float* x, float* V, long long N, int H, int W, int C, hipStream_t s,
               const float* w, float* U, int Nw, int Cw, float* D, const WgSrc* src = nullptr,
-              int kind = 0) {
+              int kind = 0, const WgOut* rider = nullptr) {
   constexpr int VW = Wg<M>::VW;
   const long long n = wg_tiles(M, N, H, W) * (C / VW);
   const int nbi = (int)((n + EW_BLOCK - 1) / EW_BLOCK);
   const int nbw = w ? (int)(((long long)Nw * (Cw / VW) + EW_BLOCK - 1) / EW_BLOCK) : 0;
+  const WgOut no_out{nullptr, nullptr, 1, 0, 0};
+  const WgOut& wo = rider && rider->src ? *rider : no_out;
+  const int nbo = wo.src ? (int)(((long long)wo.Nc * (wo.C / VW) + EW_BLOCK - 1) / EW_BLOCK) : 0;
   const WgSrc none{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0};
   const WgSrc& sr = src ? *src : none;
 #define WG_IN(K_)                                                                                \
-  hipLaunchKernelGGL((k_wg_input<M, FLIP, K_>), dim3(nbi + nbw), dim3(EW_BLOCK), 0, s, x, V, H, W, \
-                     C, wg_tiles(M, N, H, W), nbi, w, U, Nw, Cw, D, sr)
+  hipLaunchKernelGGL((k_wg_input<M, FLIP, K_>), dim3(nbi + nbw + nbo), dim3(EW_BLOCK), 0, s, x, V, \
+                     H, W, C, wg_tiles(M, N, H, W), nbi, w, U, Nw, Cw, D, sr, nbw, wo)
   if (kind == 1) WG_IN(1);
   else if (kind == 2) WG_IN(2);
   else WG_IN(0);
@@ -623,25 +648,25 @@ template <int M>
 int wino_bwd(const float* dy, const float* w, float* U, float* dx, float* v, float* mo,
              long long N, int H, int W, int C, int Nc, const CfBnBwd& bb, float* bnpart,
              long long bnpart_floats, const float* addend, float* D, hipStream_t s,
-             const WgSrc* src) {
+             const WgSrc* src, const WgOut* rider) {
   const int kind = src ? 2 : 0;
   constexpr int AA = Wg<M>::A * Wg<M>::A;
   const long long tiles = wg_tiles(M, N, H, W);
   // m = 4: U <- transform of the rotated kernel, in the input launch; m = 2: the forward's U,
   // read flipped.  Mo'[xi][tile][c] = sum_n V'[xi][tile][n] U'[xi][n][c]
   if constexpr (M == 4)
-    wg_input<M, true>(dy, v, N, H, W, Nc, s, w, U, Nc, C, D, src, kind);
+    wg_input<M, true>(dy, v, N, H, W, Nc, s, w, U, Nc, C, D, src, kind, rider);
   else
-    wg_input<M, false>(dy, v, N, H, W, Nc, s, nullptr, nullptr, 0, 0, D, src, kind);
+    wg_input<M, false>(dy, v, N, H, W, Nc, s, nullptr, nullptr, 0, 0, D, src, kind, rider);
   ew_cf_gemm_batched(v, U, mo, (int)tiles, C, Nc, AA, tiles * Nc, (long long)Nc * C, tiles * C,
                      false, M == 2, s);
   return wg_output<M>(mo, dx, N, H, W, C, bnpart, bnpart_floats, bb, addend, s);
 }
 
 template <int M>
-void wino_wgrad(const float* dy, const float* V, float* dw, float* d, int d_ready, float* du,
-                float* ws, long long ws_floats, long long N, int H, int W, int C, int Nc,
-                hipStream_t s) {
+int wino_wgrad(const float* dy, const float* V, float* dw, float* d, int d_ready, float* du,
+               float* ws, long long ws_floats, long long N, int H, int W, int C, int Nc,
+               int defer_out, hipStream_t s) {
   constexpr int A = Wg<M>::A, VW = Wg<M>::VW;
   const long long tiles = wg_tiles(M, N, H, W);
   if (!d_ready) {
@@ -652,10 +677,12 @@ void wino_wgrad(const float* dy, const float* V, float* dw, float* d, int d_read
   }
   const int split = ew_cf_gemm_tn_batched(d, V, du, ws, ws_floats, Nc, C, (int)tiles, A * A,
                                           tiles * Nc, tiles * C, s);
+  if (defer_out) return split;  // the caller runs the output transform (src: split > 1 ? ws : du)
   const long long m = (long long)Nc * (C / VW);
   hipLaunchKernelGGL(k_wg_wgrad_out<M>, dim3((unsigned)((m + EW_BLOCK - 1) / EW_BLOCK)),
                      dim3(EW_BLOCK), 0, s, split > 1 ? ws : du, split, dw, Nc, C);
   EW_CHECK_LAUNCH();
+  return split;
 }
 
 }  // namespace
@@ -707,11 +734,22 @@ int ew_wino_f32_fwd_bn(uintptr_t bn_h, uintptr_t bn_stats, uintptr_t bn_code, ui
 
 // m = 2: U is the forward's transformed weight (read flipped; w unused); m = 4: U receives the
 // rotated kernel's transform of w here
+// wo_*: another layer's deferred weight-gradient output transform (ew_wino_f32_wgrad defer_out,
+// same m) run in this call's input launch; wo_src 0 = none
+static WgOut wg_rider(uintptr_t src, int split, uintptr_t dw, int Nc, int C, int m) {
+  const int vw = m == 2 ? WG2_VW : 2;
+  if (src && (!dw || split < 1 || Nc <= 0 || C % vw))
+    throw std::runtime_error("ewdml winograd f32: bad riding weight-gradient output transform");
+  return WgOut{reinterpret_cast<const float*>(src), reinterpret_cast<float*>(dw), split, Nc, C};
+}
+
 int ew_wino_f32_bwd_data(uintptr_t dy, uintptr_t w, uintptr_t U, uintptr_t dx, uintptr_t V,
                          uintptr_t Mo, long long N, int H, int W, int C, int Nc, int m,
                          uintptr_t bn_h, uintptr_t bn_res, uintptr_t bn_code, uintptr_t bn_stats,
                          int bn_relu, uintptr_t bnpart, long long bnpart_floats,
-                         uintptr_t addend, uintptr_t D, uintptr_t stream) {
+                         uintptr_t addend, uintptr_t D, uintptr_t wo_src, int wo_split,
+                         uintptr_t wo_dw, int wo_Nc, int wo_C, uintptr_t stream) {
+  const WgOut rider = wg_rider(wo_src, wo_split, wo_dw, wo_Nc, wo_C, m);
   wg_check(m, N, H, W, Nc, C, "backward data");
   if (m == 4 && !w) throw std::runtime_error("ewdml winograd f32: m = 4 backward needs w");
   const CfBnBwd bb{reinterpret_cast<const float*>(bn_h), reinterpret_cast<const float*>(bn_res),
@@ -724,7 +762,7 @@ int ew_wino_f32_bwd_data(uintptr_t dy, uintptr_t w, uintptr_t U, uintptr_t dx, u
            reinterpret_cast<float*>(Mo), N, H, W, C, Nc, bb,
            bn_h ? reinterpret_cast<float*>(bnpart) : nullptr, bnpart_floats,
            reinterpret_cast<const float*>(addend), reinterpret_cast<float*>(D),
-           (hipStream_t)stream, nullptr);
+           (hipStream_t)stream, nullptr, &rider);
 }
 
 // Backward data whose dy is the BatchNorm(+ReLU)(+pool) backward of this conv's output, formed in
@@ -737,7 +775,9 @@ int ew_wino_f32_bwd_data_bn(uintptr_t out_h, uintptr_t out_dnext, uintptr_t out_
                             int H, int W, int C, int Nc, int m, uintptr_t bn_h, uintptr_t bn_res,
                             uintptr_t bn_code, uintptr_t bn_stats, int bn_relu, uintptr_t bnpart,
                             long long bnpart_floats, uintptr_t addend, uintptr_t D,
+                            uintptr_t wo_src, int wo_split, uintptr_t wo_dw, int wo_Nc, int wo_C,
                             uintptr_t stream) {
+  const WgOut rider = wg_rider(wo_src, wo_split, wo_dw, wo_Nc, wo_C, m);
   wg_check(m, N, H, W, Nc, C, "backward data");
   if (m == 4 && !w) throw std::runtime_error("ewdml winograd f32: m = 4 backward needs w");
   if (out_pool && (H % 2 || W % 2 || !out_code))
@@ -753,19 +793,38 @@ int ew_wino_f32_bwd_data_bn(uintptr_t out_h, uintptr_t out_dnext, uintptr_t out_
            reinterpret_cast<float*>(dx), reinterpret_cast<float*>(V), reinterpret_cast<float*>(Mo),
            N, H, W, C, Nc, bb, bn_h ? reinterpret_cast<float*>(bnpart) : nullptr, bnpart_floats,
            reinterpret_cast<const float*>(addend), reinterpret_cast<float*>(D),
-           (hipStream_t)stream, &src);
+           (hipStream_t)stream, &src, &rider);
 }
 
 // dw (channels_last [Nc][3][3][C]) from dy and the forward's V; D: a^2 * tiles * Nc floats;
 // ws: K-split slabs (the plan uses what fits, ws_floats - 64 of it)
-void ew_wino_f32_wgrad(uintptr_t dy, uintptr_t V, uintptr_t dw, uintptr_t D, int d_ready,
-                       uintptr_t U_scratch, uintptr_t ws, long long ws_floats, long long N, int H,
-                       int W, int C, int Nc, int m, uintptr_t stream) {
+// defer_out: skip the output transform dw = G^T dU G and return the split count; the caller runs
+// it later (ew_wino_f32_wgrad_out, or riding in a backward-data input launch) from
+// split > 1 ? ws : U_scratch, which it keeps alive until then
+int ew_wino_f32_wgrad(uintptr_t dy, uintptr_t V, uintptr_t dw, uintptr_t D, int d_ready,
+                      uintptr_t U_scratch, uintptr_t ws, long long ws_floats, long long N, int H,
+                      int W, int C, int Nc, int m, int defer_out, uintptr_t stream) {
   wg_check(m, N, H, W, C, Nc, "weight gradient");
   if (C % 64) throw std::runtime_error("ewdml winograd f32: weight gradient needs C % 64 == 0");
   auto* f = m == 2 ? wino_wgrad<2> : wino_wgrad<4>;
-  f(reinterpret_cast<const float*>(dy), reinterpret_cast<const float*>(V),
-    reinterpret_cast<float*>(dw), reinterpret_cast<float*>(D), d_ready,
-    reinterpret_cast<float*>(U_scratch), reinterpret_cast<float*>(ws), ws_floats, N, H, W, C, Nc,
-    (hipStream_t)stream);
+  return f(reinterpret_cast<const float*>(dy), reinterpret_cast<const float*>(V),
+           reinterpret_cast<float*>(dw), reinterpret_cast<float*>(D), d_ready,
+           reinterpret_cast<float*>(U_scratch), reinterpret_cast<float*>(ws), ws_floats, N, H, W,
+           C, Nc, defer_out, (hipStream_t)stream);
+}
+
+void ew_wino_f32_wgrad_out(uintptr_t src, int split, uintptr_t dw, int Nc, int C, int m,
+                           uintptr_t stream) {
+  const WgOut wo = wg_rider(src, split, dw, Nc, C, m);
+  if (!wo.src) return;
+  const int vw = m == 2 ? WG2_VW : 2;
+  const long long n = (long long)Nc * (C / vw);
+  const dim3 grid((unsigned)((n + EW_BLOCK - 1) / EW_BLOCK));
+  if (m == 2)
+    hipLaunchKernelGGL(k_wg_wgrad_out<2>, grid, dim3(EW_BLOCK), 0, (hipStream_t)stream, wo.src,
+                       wo.nsplit, wo.dw, Nc, C);
+  else
+    hipLaunchKernelGGL(k_wg_wgrad_out<4>, grid, dim3(EW_BLOCK), 0, (hipStream_t)stream, wo.src,
+                       wo.nsplit, wo.dw, Nc, C);
+  EW_CHECK_LAUNCH();
 }

@@ -98,6 +98,8 @@ class GradientExchange:
         if overlap:
             for p in flat.params:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+                # ours flush deferred weight-gradient transforms before reading (ops/conv.py)
+                p._ew_engine_hooks = getattr(p, "_ew_engine_hooks", 0) + 1
         self.last = StepStats()
 
     # -- accounting ---------------------------------------------------------------------------
@@ -151,6 +153,10 @@ class GradientExchange:
     def _launch(self, bi: int):
         """Encode bucket ``bi`` on the side stream and (unless deferred) issue its collective."""
         self._launched[bi] = True
+        if self.cuda:  # a deferred Winograd weight-gradient output transform completes dw first
+            from ..ops.conv import flush_pending
+
+            flush_pending()
         with self._stream_ctx():
             self._encode(bi)
             if not self.defer_comm:
@@ -283,6 +289,9 @@ class GradientExchange:
                               self.flat.grad_view(b), scale)
 
     def close(self):
+        if self._hooks:
+            for p in self.flat.params:
+                p._ew_engine_hooks = max(0, getattr(p, "_ew_engine_hooks", 1) - 1)
         for h in self._hooks:
             h.remove()
         self._hooks = []

@@ -381,6 +381,8 @@ def test_fp32_resnet18_step_convs_in_situ():
     _conv(wino=True, min_c=128, tile=2)  # the production choice
     recs = []
     orig = cmod._Conv.backward
+    # dw is read right after each backward: its output transform must not be deferred
+    defer, cmod._DEFER_WOUT = cmod._DEFER_WOUT, False
 
     def bwd(ctx, dy):
         from ewdml.ops.nn import materialize
@@ -402,6 +404,7 @@ def test_fp32_resnet18_step_convs_in_situ():
         F.cross_entropy(m(x), y).backward()
     finally:
         cmod._Conv.backward = orig
+        cmod._DEFER_WOUT = defer
     assert len(recs) >= 12
     for x, w, dy, dx, dw in recs:
         _, gx, gw = _ref64(x, w, w.shape[-1], dy)
@@ -447,3 +450,69 @@ def test_lazy_bn_through_winograd_matches_materialised(steps):
     assert ll == le
     for (k, a), b in zip(ml.state_dict().items(), me.state_dict().values()):
         assert torch.equal(a, b), k  # incl. num_batches_tracked: counted once per step
+
+
+@pytest.mark.parametrize("m", [2, 4])
+def test_winograd_deferred_wgrad_output_transform(m):
+    """A Winograd layer's weight-gradient output transform is deferred (ops/conv.py _PENDING) and
+    rides in the next same-m backward-data input launch, or is flushed at the end of the backward
+    pass: the gradients are bitwise those of the immediate transform, also when a second backward
+    accumulates into existing .grad tensors (no deferral then) and through the exchange engine's
+    flush (conv.flush_pending)."""
+    conv = _conv(True, 64, str(m))
+    torch.manual_seed(0)
+    N, H = 16, 8
+    chans = [64, 128, 128, 64]
+    ws = [torch.nn.Parameter((torch.randn(co, ci, 3, 3, device="cuda") / (3 * ci ** 0.5))
+                             .contiguous(memory_format=torch.channels_last))
+          for ci, co in zip(chans[:-1], chans[1:])]
+    x = torch.randn(N, chans[0], H, H, device="cuda").contiguous(memory_format=torch.channels_last)
+    x.requires_grad_(True)
+    dy = torch.randn(N, chans[-1], H, H, device="cuda").contiguous(
+        memory_format=torch.channels_last)
+
+    def run(defer, passes=1):
+        conv._DEFER_WOUT = defer
+        conv._POISON_DW = True  # a read of dw before its transform ran would show as NaN
+        for w in ws:
+            w.grad = None
+        x.grad = None
+        seen = []
+        for _ in range(passes):
+            y = x
+            for w in ws:
+                assert conv.wino_tile(y, w) == m
+                y = conv.conv(y, w)
+            y.backward(dy)
+            seen.append(conv._PENDING is None)  # flushed by the end-of-backward callback
+        torch.cuda.synchronize()
+        return [w.grad.clone() for w in ws] + [x.grad.clone()], seen
+
+    try:
+        ref, _ = run(False)
+        got, seen = run(True)
+        assert all(seen)
+        for a, b in zip(got, ref):
+            assert not torch.isnan(a).any()
+            assert torch.equal(a, b)
+        ref2, _ = run(False, passes=2)
+        got2, seen2 = run(True, passes=2)
+        assert all(seen2)
+        for a, b in zip(got2, ref2):
+            assert torch.equal(a, b)
+        # the engine's explicit flush after the pass's own callback: idempotent
+        conv._DEFER_WOUT = True
+        conv._POISON_DW = True
+        for w in ws:
+            w.grad = None
+        y = x
+        for w in ws:
+            y = conv.conv(y, w)
+        y.backward(dy)
+        conv.flush_pending()
+        torch.cuda.synchronize()
+        for w, r in zip(ws, ref):
+            assert torch.equal(w.grad, r)
+    finally:
+        conv._DEFER_WOUT = True
+        conv._POISON_DW = False

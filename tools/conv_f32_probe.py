@@ -67,13 +67,13 @@ def main():
                 HW, C, Nc, m, 0, 0, _stream())
             calls["wbwd"] = lambda: C_.wino_f32_bwd_data(
                 _ptr(y), _ptr(w), _ptr(U), _ptr(dx), _ptr(buf), _ptr(buf) + 4 * aa * t * Nc, N,
-                HW, HW, C, Nc, m, 0, 0, 0, 0, 0, 0, 0, 0, 0, _stream())
+                HW, HW, C, Nc, m, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, _stream())
             D = torch.empty(aa * t * Nc, device=dev)
             dU = torch.empty(aa * Nc * C, device=dev)
             slabs = torch.empty(4 * aa * Nc * C + 64, device=dev)
             calls["wwgrad"] = lambda: C_.wino_f32_wgrad(
                 _ptr(y), _ptr(buf), _ptr(dw), _ptr(D), 0, _ptr(dU), _ptr(slabs), slabs.numel(), N,
-                HW, HW, C, Nc, m, _stream())
+                HW, HW, C, Nc, m, 0, _stream())
         if args.miopen:
             xm = x.permute(0, 3, 1, 2)  # NCHW view of NHWC memory: channels_last
             wm = w.permute(0, 3, 1, 2)
