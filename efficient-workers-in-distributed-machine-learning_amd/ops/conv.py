@@ -490,6 +490,23 @@ class _ConvStem(torch.autograd.Function):
         x, w = ctx.saved_tensors
         N, C, H, W = x.shape
         Nc = w.shape[0]
+        # dy may be the lazily formed input gradient of the BN layer this stem feeds (ops/nn.py):
+        # the fp32 weight-gradient kernel forms it on the fly; an input gradient needs it written
+        lazy = getattr(dy, "_ew_lazy_bwd", None)
+        if lazy is not None and (ctx.needs_input_grad[0] or not ctx.needs_input_grad[1]
+                                 or x.dtype != torch.float32):
+            from .nn import materialize
+
+            materialize(dy)
+            lazy = None
+        if lazy is not None:
+            oh, odn, ocode, ostats, ocoef, opool = lazy
+            ws = _ws(x.device)
+            dw = torch.empty_like(w, memory_format=torch.channels_last)
+            C_.conv_f32_stem_wgrad_bn(_ptr(oh), _ptr(odn), _ptr(ocode), _ptr(ostats), _ptr(ocoef),
+                                      int(opool), _ptr(x), _ptr(dw), _ptr(ws), ws.numel(), N, H,
+                                      W, Nc, _stream())
+            return None, dw
         dy = dy.contiguous(memory_format=torch.channels_last)
         if dy.dtype != x.dtype:
             dy = dy.to(x.dtype)
@@ -520,6 +537,8 @@ class GradSink:
 def _apply(x, w, sink=None):
     if x.shape[1] == 3:
         y = _ConvStem.apply(x, w)
+        if y.dtype == torch.float32 and y.grad_fn is not None:
+            y._ew_stem_out = True  # its BN layer may leave the backward apply to the stem
     else:
         node = getattr(x, "_ew_bn_node", None) if (_BN_BWD and epilogue_fusion_ok(x)) else None
         y = _Conv.apply(x, w, node, sink)

@@ -281,6 +281,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_f32_wgrad", &ew_conv_f32_wgrad);
   m.def("conv_f32_stem_fwd", &ew_conv_f32_stem_fwd);
   m.def("conv_f32_stem_wgrad", &ew_conv_f32_stem_wgrad);
+  m.def("conv_f32_stem_wgrad_bn", &ew_conv_f32_stem_wgrad_bn);
   m.def("wino_f32_weight", &ew_wino_f32_weight);
   m.def("wino_f32_fwd", &ew_wino_f32_fwd);
   m.def("wino_f32_bwd_data", &ew_wino_f32_bwd_data);

@@ -747,10 +747,24 @@ __global__ __launch_bounds__(EW_BLOCK) void k_cf_stem_fwd(const float* __restric
 // dy rows ([256 m][64 n], RC) and the im2col rows ([256 m][28 k], RC) go to LDS; wave v computes
 // n0 + [16 v, 16 v + 16) x k 0..31 (2 tiles) over all 256 m (64 MFMA k-steps), fp32 partial
 // [64][27] per block into the slab, summed by k_cf_stem_reduce.
+// LAZY: dy is not materialised -- it is the BatchNorm(+ReLU)(+2x2 pool) backward of the stem's
+// output, formed here from that layer's input h (= the stem output), the gradient of its
+// (pooled) output, its pool codes, stats [4][Nc] and coef [2][Nc] with k_bn_bwd_apply's
+// expressions (nn.hip: the same bits), so the BN backward's apply pass is not run at all.
+struct CsLazy {
+  const float* h;
+  const float* dnext;
+  const uint8_t* code;
+  const float* stats;
+  const float* coef;
+  int pool;
+};
+
+template <bool LAZY>
 __global__ __launch_bounds__(EW_BLOCK) void k_cf_stem_wgrad(const float* __restrict__ dy,
                                                             const float* __restrict__ x,
                                                             float* __restrict__ slab, int H,
-                                                            int W, int Nc, int M) {
+                                                            int W, int Nc, int M, CsLazy lz) {
   constexpr int DP = 64 + 4, XP = 32 + 4;  // pitches (floats): k and k + 4 16 banks apart
   __shared__ __attribute__((aligned(16))) float dsm[256 * DP];
   __shared__ __attribute__((aligned(16))) float xsm[256 * XP];
@@ -758,10 +772,55 @@ __global__ __launch_bounds__(EW_BLOCK) void k_cf_stem_wgrad(const float* __restr
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6, li = lane & 15, g = lane >> 4;
   const int m0 = blockIdx.x * 256, n0 = blockIdx.y * 64, HW = H * W;
   f32x4 d[16];
+  if constexpr (!LAZY) {
 #pragma unroll
-  for (int u = 0; u < 16; ++u) {  // 256 rows x 16 quads
-    const int e = t + EW_BLOCK * u, r = e >> 4, ch = e & 15;
-    d[u] = *reinterpret_cast<const f32x4*>(dy + (long long)(m0 + r) * Nc + n0 + ch * 4);
+    for (int u = 0; u < 16; ++u) {  // 256 rows x 16 quads
+      const int e = t + EW_BLOCK * u, r = e >> 4, ch = e & 15;
+      d[u] = *reinterpret_cast<const f32x4*>(dy + (long long)(m0 + r) * Nc + n0 + ch * 4);
+    }
+  } else {
+    // thread t always holds channels c0 .. c0 + 3 (e & 15 == t & 15): their coefficients once
+    const int c0 = n0 + (t & 15) * 4;
+    const f32x4 mn = *reinterpret_cast<const f32x4*>(lz.stats + c0);
+    const f32x4 sc = *reinterpret_cast<const f32x4*>(lz.stats + 2 * Nc + c0);
+    const f32x4 sh = *reinterpret_cast<const f32x4*>(lz.stats + 3 * Nc + c0);
+    const f32x4 ce = *reinterpret_cast<const f32x4*>(lz.coef + c0);
+    const f32x4 cf = *reinterpret_cast<const f32x4*>(lz.coef + Nc + c0);
+    const int Ho = H >> 1, Wo = W >> 1;
+#pragma unroll
+    for (int h8 = 0; h8 < 2; ++h8) {  // two halves of 8 rows: the loads of a half in flight
+      f32x4 hv[8], dn[8];
+      uint32_t kw[8], qq[8];
+#pragma unroll
+      for (int u8 = 0; u8 < 8; ++u8) {
+        const int u = 8 * h8 + u8, r = (t + EW_BLOCK * u) >> 4, m = m0 + r;
+        hv[u8] = *reinterpret_cast<const f32x4*>(lz.h + (long long)m * Nc + c0);
+        if (lz.pool) {
+          const int n = m / HW, p = m - n * HW, hh = p / W, ww = p - hh * W;
+          const long long pr = ((long long)n * Ho + (hh >> 1)) * Wo + (ww >> 1);
+          dn[u8] = *reinterpret_cast<const f32x4*>(lz.dnext + pr * Nc + c0);
+          kw[u8] = *reinterpret_cast<const uint32_t*>(lz.code + pr * Nc + c0);
+          qq[u8] = (uint32_t)((hh & 1) * 2 + (ww & 1));
+        } else {
+          dn[u8] = *reinterpret_cast<const f32x4*>(lz.dnext + (long long)m * Nc + c0);
+          kw[u8] = 0u;
+          qq[u8] = 0u;
+        }
+      }
+#pragma unroll
+      for (int u8 = 0; u8 < 8; ++u8) {
+        f32x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float xv = hv[u8][j];
+          const bool route = !lz.pool || ((kw[u8] >> (8 * j)) & 0xffu) == qq[u8];
+          const float z = xv * sc[j] + sh[j];  // k_bn_bwd_apply's expressions: the same bits
+          const float dz = (route && !(z <= 0.0f)) ? dn[u8][j] : 0.0f;
+          o[j] = sc[j] * dz + ce[j] * (xv - mn[j]) + cf[j];
+        }
+        d[8 * h8 + u8] = o;
+      }
+    }
   }
   const int lo = cs_patch<256>(x, m0, W, M, patch, t);
 #pragma unroll
@@ -1059,21 +1118,47 @@ int ew_conv_f32_stem_fwd(uintptr_t x, uintptr_t w, uintptr_t y, long long N, int
   return bnp ? nrows : 0;
 }
 
-void ew_conv_f32_stem_wgrad(uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws,
-                            long long ws_floats, long long N, int H, int W, int Nc,
-                            uintptr_t stream) {
+static void cf_stem_wgrad(const float* dy, const CsLazy* lz, uintptr_t x, uintptr_t dw,
+                          uintptr_t ws, long long ws_floats, long long N, int H, int W, int Nc,
+                          uintptr_t stream) {
   const long long M = N * H * W;
   const long long nb = M / 256, n = (long long)Nc * CS_K;
   if (M % 256 || Nc % 64 || nb * n > ws_floats - 64 || W > CS_WMAX || M >= (1LL << 31) / 64)
     throw std::runtime_error("ewdml conv f32 stem: wgrad needs N*H*W % 256 == 0, Nc % 64 == 0, "
                              "W <= 256");
+  if (lz && lz->pool && (H % 2 || W % 2 || !lz->code))
+    throw std::runtime_error("ewdml conv f32 stem: a pooled BN backward needs even maps, codes");
   hipStream_t s = (hipStream_t)stream;
   float* slab = reinterpret_cast<float*>(ws);
-  hipLaunchKernelGGL(k_cf_stem_wgrad, dim3((int)nb, Nc / 64), dim3(EW_BLOCK), 0, s,
-                     reinterpret_cast<const float*>(dy), reinterpret_cast<const float*>(x), slab,
-                     H, W, Nc, (int)M);
+  const CsLazy none{nullptr, nullptr, nullptr, nullptr, nullptr, 0};
+  if (lz)
+    hipLaunchKernelGGL(k_cf_stem_wgrad<true>, dim3((int)nb, Nc / 64), dim3(EW_BLOCK), 0, s,
+                       nullptr, reinterpret_cast<const float*>(x), slab, H, W, Nc, (int)M, *lz);
+  else
+    hipLaunchKernelGGL(k_cf_stem_wgrad<false>, dim3((int)nb, Nc / 64), dim3(EW_BLOCK), 0, s, dy,
+                       reinterpret_cast<const float*>(x), slab, H, W, Nc, (int)M, none);
   EW_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_cf_stem_reduce, dim3((int)((n + 7) / 8)), dim3(EW_BLOCK), 0, s, slab,
                      (int)nb, (int)n, reinterpret_cast<float*>(dw));
   EW_CHECK_LAUNCH();
+}
+
+void ew_conv_f32_stem_wgrad(uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws,
+                            long long ws_floats, long long N, int H, int W, int Nc,
+                            uintptr_t stream) {
+  cf_stem_wgrad(reinterpret_cast<const float*>(dy), nullptr, x, dw, ws, ws_floats, N, H, W, Nc,
+                stream);
+}
+
+// The weight gradient with dy formed from the BatchNorm(+ReLU)(+pool) backward of the stem's
+// output (see k_cf_stem_wgrad LAZY): h = the stem output, dnext = the gradient of the BN layer's
+// (pooled) output, code its pool codes, stats / coef that layer's [4][Nc] / [2][Nc].
+void ew_conv_f32_stem_wgrad_bn(uintptr_t h, uintptr_t dnext, uintptr_t code, uintptr_t stats,
+                               uintptr_t coef, int pool, uintptr_t x, uintptr_t dw, uintptr_t ws,
+                               long long ws_floats, long long N, int H, int W, int Nc,
+                               uintptr_t stream) {
+  const CsLazy lz{reinterpret_cast<const float*>(h), reinterpret_cast<const float*>(dnext),
+                  reinterpret_cast<const uint8_t*>(code), reinterpret_cast<const float*>(stats),
+                  reinterpret_cast<const float*>(coef), pool};
+  cf_stem_wgrad(nullptr, &lz, x, dw, ws, ws_floats, N, H, W, Nc, stream);
 }

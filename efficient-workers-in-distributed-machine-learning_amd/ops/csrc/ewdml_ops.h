@@ -203,6 +203,11 @@ int ew_conv_f32_stem_fwd(uintptr_t x, uintptr_t w, uintptr_t y, long long N, int
 void ew_conv_f32_stem_wgrad(uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws,
                             long long ws_floats, long long N, int H, int W, int Nc,
                             uintptr_t stream);
+// the same with dy formed from the BatchNorm(+ReLU)(+pool) backward of the stem's output
+void ew_conv_f32_stem_wgrad_bn(uintptr_t h, uintptr_t dnext, uintptr_t code, uintptr_t stats,
+                               uintptr_t coef, int pool, uintptr_t x, uintptr_t dw, uintptr_t ws,
+                               long long ws_floats, long long N, int H, int W, int Nc,
+                               uintptr_t stream);
 // ---- fp32 3x3 convolutions by Winograd F(m x m, 3x3), m = 2 or 4 (winograd_f32.hip): U[a^2][Nc][C]
 // (a = m + 2) from the channels_last weight (standalone, or inside the forward when w != 0);
 // forward / backward data over caller-allocated V (a^2 * N*H*W/m^2 * C_in floats) and Mo

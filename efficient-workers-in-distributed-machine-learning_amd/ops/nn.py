@@ -102,9 +102,11 @@ class _BNAct(torch.autograd.Function):
             y._ew_materialize = lambda: C_.bn_relu_fwd(*args, 2)
             no_nbt = args[:11] + (0,) + args[12:]  # after a consumer counted the batch
             y._ew_materialize_no_nbt = lambda: C_.bn_relu_fwd(*no_nbt, 2)
-        # the backward may leave its apply to the Winograd conv that produced h
-        ctx.lazy_bwd = (_LAZY_BWD and getattr(h, "_ew_wino_out", False) and mode == "relu"
-                        and res is None and h.dtype == torch.float32)
+        # the backward may leave its apply to the Winograd conv (or the fp32 stem, whose weight
+        # gradient forms it) that produced h
+        ctx.lazy_bwd = (_LAZY_BWD and (getattr(h, "_ew_wino_out", False)
+                                       or getattr(h, "_ew_stem_out", False))
+                        and mode == "relu" and res is None and h.dtype == torch.float32)
         ctx.pool, ctx.mode = pool, mode
         ctx.res_sink = res_sink
         ctx.cb_dtype = None if cb is None else cb.dtype

@@ -417,9 +417,12 @@ def test_fp32_resnet18_step_convs_in_situ():
 def test_lazy_bn_through_winograd_matches_materialised(steps):
     """VGG-11 fp32 training steps with the BN layers in front of / behind the Winograd convs
     applied inside the convs' input transforms (ops/nn.py lazy BN, winograd_f32.hip WgSrc) equal
-    the materialised path bit for bit: losses, weights, running statistics, batch counters."""
+    the materialised path bit for bit: losses, weights, running statistics, batch counters.
+    The lazy run also leaves the BN backward applies to the producing convs (ops/nn.py
+    _LAZY_BWD: the Winograd backward input transforms and the stem's weight gradient)."""
     from ewdml.models import build_model
     from ewdml.models import fused
+    from ewdml.ops import nn as onn
 
     _conv(wino=True, min_c=128, tile=2)
     torch.manual_seed(0)
@@ -430,8 +433,10 @@ def test_lazy_bn_through_winograd_matches_materialised(steps):
     x = torch.randn(64, 3, 32, 32, device="cuda").contiguous(memory_format=torch.channels_last)
     y = torch.randint(0, 10, (64,), device="cuda")
     runs = []
+    lazy_bwd = onn._LAZY_BWD
     for lazy in (True, False):
         fused._LAZY = lazy
+        onn._LAZY_BWD = lazy
         try:
             m = copy.deepcopy(m0)
             opt = torch.optim.SGD(m.parameters(), lr=0.05, momentum=0.9)
@@ -445,6 +450,7 @@ def test_lazy_bn_through_winograd_matches_materialised(steps):
             runs.append((m, losses))
         finally:
             fused._LAZY = True
+            onn._LAZY_BWD = lazy_bwd
     (ml, ll), (me, le) = runs
     # the input transforms evaluate the BN kernels' own expressions: bit-identical training
     assert ll == le
