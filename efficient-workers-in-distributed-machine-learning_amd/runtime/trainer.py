@@ -31,6 +31,10 @@ from ..parallel.sharded import ShardedPSExchange
 from ..utils import checkpoint as ckpt
 from ..utils.metrics import MetricsLogger, accuracy, byte_summary
 
+# full-step graph replays on the caller's stream (0: on the graph stream, with an event hop each
+# way per step)
+_SAME_STREAM_REPLAY = os.environ.get("EWDML_GRAPH_SAME_STREAM", "1") != "0"
+
 
 def resolve_device(cfg: Config) -> torch.device:
     want = cfg.device
@@ -233,6 +237,10 @@ class Trainer:
     def train_step(self, x=None, y=None):
         """One synchronous step.  Returns (loss tensor, logits) (server: (None, None))."""
         if self.gstream is None:
+            return self._train_step(x, y)
+        if self._graphs is not None and len(self._graphs) == 1 and _SAME_STREAM_REPLAY:
+            # a captured full-step graph replays on the caller's stream: no per-step event hop
+            # to the graph stream and back (re-captures name their capture stream themselves)
             return self._train_step(x, y)
         gs = self.gstream  # a failed capture drops self.gstream inside the step
         gs.wait_stream(torch.cuda.current_stream())

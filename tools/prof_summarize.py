@@ -79,6 +79,20 @@ def summarize(rows, frac=0.5, gap_ns=150_000_000, steps=None):
     for n, (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:60]:
         ps = f" {t / 1e3 / steps:>9.2f}" if steps else ""
         out.append(f"{c:>7} {t / 1e6:>10.3f} {t / c / 1e3:>9.2f}{ps}  {n}")
+    # where the idle time is: the largest gaps between consecutive kernels, with their neighbours
+    gaps, end_prev, name_prev = [], win[0][1], win[0][2]
+    for s, e, n in win[1:]:
+        if s > end_prev:
+            gaps.append((s - end_prev, name_prev, n))
+        if e >= end_prev:
+            end_prev, name_prev = e, n
+    if gaps:
+        tot = sum(g[0] for g in gaps)
+        out.append("")
+        out.append(f"idle: {tot / 1e3:.1f} us in {len(gaps)} gaps"
+                   + (f" ({tot / 1e3 / steps:.1f} us/step)" if steps else "") + "; largest:")
+        for g, a, b in sorted(gaps, reverse=True)[:8]:
+            out.append(f"{g / 1e3:>9.2f} us  {short(a)[:50]}  ->  {short(b)[:50]}")
     if steps:  # the last step's kernels in launch order: duration and idle gap before each
         per_step = len(win) // steps
         last = win[-per_step:]
