@@ -14,9 +14,10 @@ backward-data and backward-weight are hand-written MFMA implicit-GEMM kernels:
   ``EWDML_WINO_TILE=4|auto``, ``EWDML_WINOGRAD=0`` keeps the direct kernels) -- forward, backward data and weight gradient (the forward's transformed input
   is kept for it).
 
-:func:`conv2d_module` dispatches an ``nn.Conv2d`` (VGG's and ResNet's stride-1 3x3 / 1x1 layers).
-Shapes the kernels do not take (C_in or C_out not a multiple of 64, NCHW, other
-strides/padding) go to ``F.conv2d`` (MIOpen) -- e.g. the ImageNet ResNet's 7x7/2 stem.
+:func:`conv2d_module` dispatches an ``nn.Conv2d`` (VGG's and ResNet's stride-1 3x3 / 1x1 layers,
+and with ``EWDML_CONV_S2=1`` ResNet's fp32 stride-2 3x3 / 1x1 down-sampling convs: :func:`conv_s2`).  Shapes the kernels
+do not take (C_in or C_out not a multiple of 64, NCHW, other strides/padding) go to ``F.conv2d``
+(MIOpen) -- e.g. the ImageNet ResNet's 7x7/2 stem.
 ``EWDML_CONV=miopen`` (or ``set_enabled(False)``) routes every call to MIOpen (A/B),
 ``EWDML_CONV_F32=miopen`` only the fp32 ones.
 
@@ -69,6 +70,17 @@ _WINO_WG_SPLITS = int(os.environ.get("EWDML_WINO_WG_SPLITS", "4"))
 # caller's current stream) and by the exchange engine before it encodes a bucket
 # (parallel/engine.py), so a bucket's gradients are complete when its encode starts.
 _DEFER_WOUT = os.environ.get("EWDML_WINO_DEFER_WOUT", "1") != "0"
+# fp32 stride-2 3x3 / 1x1 convs (ResNet down-sampling) on the MFMA kernels: opt-in
+# (EWDML_CONV_S2=1).  Measured slower than MIOpen's tuned (find-mode) solvers on every ResNet-50
+# shape, 2078 vs 1740 us per step for the six layers, ResNet-50 CIFAR 8.38K vs 8.53K img/s
+# (profiles/ab/conv_stride2_vs_miopen.txt), so MIOpen keeps them by default
+_S2 = os.environ.get("EWDML_CONV_S2", "0") == "1"
+
+
+def set_stride2(on: bool):
+    """Route fp32 stride-2 3x3 / 1x1 convs through :func:`conv_s2` (True) or MIOpen."""
+    global _S2
+    _S2 = bool(on)
 _PENDING = None  # (src, split, param, Nc, C, m, keep-alive tensors)
 _POISON_DW = False  # tests: NaN-fill each fresh dw, so a read before its transform shows
 
@@ -272,6 +284,21 @@ def supported(x, w, stride=1, padding=None, dilation=1, groups=1) -> bool:
     if x.numel() >= 2 ** 31 or N * H * W * Nc >= 2 ** 31:
         return False
     return x.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0
+
+
+def s2_supported(x, w, stride=2, padding=None, dilation=1, groups=1) -> bool:
+    """True for the fp32 stride-2 kernels: 3x3 / pad 1 or 1x1 / pad 0 at stride 2 (the ResNet
+    down-sampling convs), channels_last fp32, even H and W, C_in and C_out % 64 == 0,
+    N*H*W/4 % 64 == 0."""
+    if not (_one(stride, 2) and x.dim() == 4 and w.dim() == 4 and w.dtype == torch.float32):
+        return False
+    if not _geometry_ok(x, w, 1, padding, dilation, groups):
+        return False
+    N, C, H, W = x.shape
+    Nc = w.shape[0]
+    return (H % 2 == 0 and W % 2 == 0 and C % 64 == 0 and Nc % 64 == 0
+            and (N * (H // 2) * (W // 2)) % 64 == 0 and x.numel() < 2 ** 31
+            and N * H * W * Nc < 2 ** 31 and x.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0)
 
 
 def _part_floats(M, C):
@@ -524,6 +551,72 @@ class _ConvStem(torch.autograd.Function):
         return dx, dw
 
 
+class _ConvS2(torch.autograd.Function):
+    """fp32 stride-2 3x3 / 1x1 convolution (``ops/csrc/conv_f32.hip`` ``k_cf_gemm<..., 2>``): the
+    forward and weight gradient gather the strided taps in their im2col loads; the backward data
+    runs the four dx phases (pixels (2i + ph, 2j + pw)) as one launch, each phase a GEMM over only
+    the taps that reach it (1, 2, 2 and 4 of a 3x3 kernel), so no zero-stuffed work."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        C_ = require()
+        N, C, H, W = x.shape
+        Nc, k = w.shape[0], w.shape[-1]
+        ws = _ws(x.device)
+        Ho, Wo = H // 2, W // 2
+        y = torch.empty((N, Nc, Ho, Wo), dtype=x.dtype, device=x.device,
+                        memory_format=torch.channels_last)
+        part = torch.empty(_part_floats(N * Ho * Wo, Nc), dtype=torch.float32, device=x.device)
+        rows = C_.conv_f32_fwd_s2(_ptr(x), _ptr(w), _ptr(y), _ptr(ws), ws.numel(), N, H, W, C, Nc,
+                                  k, _ptr(part), part.numel(), _stream())
+        ctx.save_for_backward(x, w)
+        ctx.bn_part = (part, rows) if rows > 0 else None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from .nn import materialize
+
+        C_ = require()
+        flush_pending()  # a deferred Winograd weight-gradient transform, while its data is warm
+        x, w = ctx.saved_tensors
+        N, C, H, W = x.shape
+        Nc, k = w.shape[0], w.shape[-1]
+        if getattr(dy, "_ew_lazy_bwd", None) is not None:
+            materialize(dy)
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        if dy.dtype != x.dtype:
+            dy = dy.to(x.dtype)
+        if dy.data_ptr() % 16:
+            dy = dy.clone(memory_format=torch.channels_last)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x, memory_format=torch.channels_last)
+            C_.conv_f32_bwd_data_s2(_ptr(dy), _ptr(w), _ptr(dx), N, H, W, C, Nc, k, 0, _stream())
+        if ctx.needs_input_grad[1]:
+            ws = _ws(x.device)
+            dw = torch.empty_like(w, memory_format=torch.channels_last)
+            C_.conv_f32_wgrad_s2(_ptr(dy), _ptr(x), _ptr(dw), _ptr(ws), ws.numel(), N, H, W, C,
+                                 Nc, k, _stream())
+        return dx, dw
+
+
+def conv_s2(x, w):
+    """``F.conv2d(x, w, stride=2, padding=k // 2)`` (k = 3 or 1) through the fp32 stride-2
+    kernels when :func:`s2_supported`, else MIOpen."""
+    from .nn import materialize
+
+    x = materialize(x)
+    if s2_supported(x, w):
+        y = _ConvS2.apply(x, w)
+        node = y.grad_fn
+        part = getattr(node, "bn_part", None) if node is not None else None
+        if part is not None:
+            y._ew_bn_part = part
+        return y
+    return F.conv2d(x, w, stride=2, padding=w.shape[-1] // 2)
+
+
 class GradSink:
     """Hand-over slot for a second gradient of a conv's input (``grad``: set by the producer's
     backward, consumed and cleared by the conv's backward-data launch)."""
@@ -581,4 +674,7 @@ def conv2d_module(m, x, sink=None):
         return _apply(x, m.weight, sink)
     if sink is not None:
         raise ValueError("a gradient sink needs the MFMA conv path")
+    if (_S2 and m.bias is None and m.padding_mode == "zeros" and x.is_cuda
+            and s2_supported(x, m.weight, m.stride, m.padding, m.dilation, m.groups)):
+        return conv_s2(x, m.weight)
     return m(x)

@@ -279,6 +279,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_f32_fwd", &ew_conv_f32_fwd);
   m.def("conv_f32_bwd_data", &ew_conv_f32_bwd_data);
   m.def("conv_f32_wgrad", &ew_conv_f32_wgrad);
+  m.def("conv_f32_fwd_s2", &ew_conv_f32_fwd_s2);
+  m.def("conv_f32_bwd_data_s2", &ew_conv_f32_bwd_data_s2);
+  m.def("conv_f32_wgrad_s2", &ew_conv_f32_wgrad_s2);
   m.def("conv_f32_stem_fwd", &ew_conv_f32_stem_fwd);
   m.def("conv_f32_stem_wgrad", &ew_conv_f32_stem_wgrad);
   m.def("conv_f32_stem_wgrad_bn", &ew_conv_f32_stem_wgrad_bn);

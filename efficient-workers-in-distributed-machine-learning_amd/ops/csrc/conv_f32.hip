@@ -65,7 +65,33 @@ struct CfGeom {
   // B batch index = the 4x4 position (i, j) of the A batch with 0 <-> 3 swapped on both axes (the
   // Winograd transform of the 180-degree-rotated kernel: G J = rows 0 and 3 of G exchanged)
   int b_flip;
+  // stride-2 convolutions (k_cf_gemm<..., STR = 2>): Ho x Wo = the output map (H / 2, W / 2).
+  // Forward / weight gradient: H, W = the input map, GEMM rows / reduction = output pixels.
+  // Backward data: H, W = Ho, Wo = dy's map, blockIdx.z = the dx phase (ph, pw) = (z >> 1, z & 1)
+  // -- dx pixels (2i + ph, 2j + pw) -- whose rows are dy's pixels (i, j): tap (kh, kw) of the
+  // kernel reaches dy pixel (i + eh, j + ew) with eh = 1 for (ph, kh) = (1, 0), else 0.  A phase
+  // has (1 + ph)(1 + pw) taps of a 3x3 kernel; only phase 0 has the 1x1 kernel's tap (the others
+  // are written as zeros)
+  int S, Ho, Wo;
 };
+
+// stride-2 backward data: taps of phase (ph, pw) and tap tp of it -> dy offset (eh, ew) on dy's
+// map and the kernel tap kh * 3 + kw it multiplies (1x1: phase 0's single tap)
+__host__ __device__ __forceinline__ int cf_s2_ntaps(int taps, int ph, int pw) {
+  return taps == 1 ? ((ph | pw) ? 0 : 1) : (1 + ph) * (1 + pw);
+}
+__device__ __forceinline__ void cf_s2_tap(int taps, int ph, int pw, int tp, int& eh, int& ew,
+                                          int& wtap) {
+  if (taps == 1) {
+    eh = ew = wtap = 0;
+    return;
+  }
+  const int nc = 1 + pw, a = tp / nc, b = tp - a * nc;
+  const int kh = ph ? 2 * a : 1, kw = pw ? 2 * b : 1;
+  eh = (ph && a == 0) ? 1 : 0;
+  ew = (pw && b == 0) ? 1 : 0;
+  wtap = kh * 3 + kw;
+}
 
 __device__ __forceinline__ int cf_flip4(int z) {  // (i, j) -> (p(i), p(j)), p: 0 <-> 3
   const int i = z >> 2, j = z & 3;
@@ -189,7 +215,7 @@ struct CfRegs {
 // 16 zero bytes in device memory (zero-initialised at module load), read by masked-out loads
 __device__ __attribute__((aligned(16))) float cf_zero_page[4];
 
-template <int MODE, int BM, int BN, int NT>
+template <int MODE, int BM, int BN, int NT, int STR = 1>
 struct CfStager {
   using L = CfLayout<MODE, BM, BN>;
   static constexpr int RA = 8 * BM / NT, RB = 8 * BN / NT;    // 16-B vectors per thread
@@ -203,22 +229,34 @@ struct CfStager {
   const float* xa;  // A source
   const float* xb;  // B source
   int t, m0, n0;
+  int ph, pw;  // stride-2 backward data: this block's dx phase
 
   __device__ __forceinline__ void init(const CfGeom& g, const float* a_src, const float* b_src,
-                                       int t_, int m0_, int n0_) {
+                                       int t_, int m0_, int n0_, int zb = 0) {
     t = t_;
     m0 = m0_;
     n0 = n0_;
     xa = a_src;
     xb = b_src;
+    ph = zb >> 1;
+    pw = zb & 1;
     if constexpr (L::A_KC) {
 #pragma unroll
       for (int i = 0; i < RA; ++i) {
         const int m = m0 + (t >> 3) + (NT / 8) * i;
-        am[i] = m;
-        const int hw = m % (g.H * g.W);
-        ah[i] = hw / g.W;
-        aw[i] = hw - ah[i] * g.W;
+        if constexpr (STR == 2 && MODE == CF_FWD) {
+          // row m = output pixel (n, oh, ow); its taps start at input pixel (n, 2 oh, 2 ow)
+          const int HoWo = g.Ho * g.Wo;
+          const int n = m / HoWo, hw = m - n * HoWo, oh = hw / g.Wo;
+          ah[i] = 2 * oh;
+          aw[i] = 2 * (hw - oh * g.Wo);
+          am[i] = n * g.H * g.W + ah[i] * g.W + aw[i];
+        } else {
+          am[i] = m;
+          const int hw = m % (g.H * g.W);
+          ah[i] = hw / g.W;
+          aw[i] = hw - ah[i] * g.W;
+        }
       }
     }
     if constexpr (MODE == CF_WGRAD) {
@@ -237,7 +275,14 @@ struct CfStager {
       const int CH = MODE == CF_FWD ? g.C : g.Nc;
       const int CB = CH / CF_BK;
       const int tap = s / CB, cb = s - tap * CB;
-      const int dr = g.taps == 1 ? 0 : tap / 3 - 1, dc = g.taps == 1 ? 0 : tap - (tap / 3) * 3 - 1;
+      int dr, dc, wtap;
+      if constexpr (STR == 2 && MODE == CF_BWD) {
+        cf_s2_tap(g.taps, ph, pw, tap, dr, dc, wtap);
+      } else {
+        dr = g.taps == 1 ? 0 : tap / 3 - 1;
+        dc = g.taps == 1 ? 0 : tap - (tap / 3) * 3 - 1;
+        wtap = g.taps - 1 - tap;  // backward data: the 180-degree-rotated kernel's tap
+      }
       {
         // out-of-image taps load the zero page: a select on the loaded VALUE would make hipcc
         // wait for this step's loads before the step's MFMAs (s_waitcnt vmcnt ahead of the
@@ -262,12 +307,11 @@ struct CfStager {
         });
       } else {
         // B (RC): k-row kr = reduction channel n = cb*32 + kr at the flipped tap; columns c
-        const int ft = g.taps - 1 - tap;
         CfRegs& RG = rb;
         CF_FOR(RB, {
           const int kr = t / RCB + RPB * i;
           v = *reinterpret_cast<const f32x4*>(
-              xb + ((long long)(cb * CF_BK + kr) * g.taps + ft) * g.C + n0 + (t % RCB) * 4);
+              xb + ((long long)(cb * CF_BK + kr) * g.taps + wtap) * g.C + n0 + (t % RCB) * 4);
         });
       }
     } else {
@@ -283,13 +327,29 @@ struct CfStager {
       {
         const int HW = g.H * g.W;
         CfRegs& RG = rb;
-        CF_FOR(RB, {
-          const int m = s * CF_BK + t / RCB + RPB * i;
-          const int hw = m % HW, h = hw / g.W, w = hw - h * g.W;
-          const bool ok = (unsigned)(h + bdr) < (unsigned)g.H && (unsigned)(w + bdc) < (unsigned)g.W;
-          const float* src = ok ? xb + (long long)(m + bdr * g.W + bdc) * g.C + bc : cf_zero_page;
-          v = *reinterpret_cast<const f32x4*>(src);
-        });
+        if constexpr (STR == 2) {
+          // reduction index m = output pixel (n, oh, ow); tap at input (2 oh + bdr, 2 ow + bdc)
+          const int HoWo = g.Ho * g.Wo;
+          CF_FOR(RB, {
+            const int m = s * CF_BK + t / RCB + RPB * i;
+            const int n = m / HoWo, hw = m - n * HoWo, oh = hw / g.Wo;
+            const int h = 2 * oh + bdr, w = 2 * (hw - oh * g.Wo) + bdc;
+            const bool ok = (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
+            const float* src =
+                ok ? xb + ((long long)n * HW + h * g.W + w) * g.C + bc : cf_zero_page;
+            v = *reinterpret_cast<const f32x4*>(src);
+          });
+        } else {
+          CF_FOR(RB, {
+            const int m = s * CF_BK + t / RCB + RPB * i;
+            const int hw = m % HW, h = hw / g.W, w = hw - h * g.W;
+            const bool ok =
+                (unsigned)(h + bdr) < (unsigned)g.H && (unsigned)(w + bdc) < (unsigned)g.W;
+            const float* src =
+                ok ? xb + (long long)(m + bdr * g.W + bdc) * g.C + bc : cf_zero_page;
+            v = *reinterpret_cast<const f32x4*>(src);
+          });
+        }
       }
     }
   }
@@ -325,18 +385,30 @@ struct CfStager {
 // (sum, sum of squares per column over the block's BM rows -> row blockIdx.x of
 // bnpart[2][M/BM][Ncol]) or the backward sums of CfBnBwd.  Waves form a WM x WN grid of
 // (BM/WM) x (BN/WN) tiles of MI x NJ SH x SH MFMA blocks.
-template <int BM, int BN, int WM, int WN, int SH, int MI, int NJ>
+// RMAP (stride-2 backward data): GEMM row r = dy pixel (n, i, j) of an rHo x rWo map is written
+// to dx pixel (n, 2 i + rph, 2 j + rpw) (out and addend; no slab, no BN sums on this path)
+template <int BM, int BN, int WM, int WN, int SH, int MI, int NJ, bool RMAP = false>
 __device__ __forceinline__ void cf_epilogue(typename CfMfma<SH>::acc_t (&acc)[MI][NJ], char* smem,
                                             int wm, int wn, int lane, int m0, int n0, int M,
                                             int Nc, float* __restrict__ out,
                                             float* __restrict__ slab, float* __restrict__ bnpart,
-                                            const CfBnBwd& bb, const float* __restrict__ addend) {
+                                            const CfBnBwd& bb, const float* __restrict__ addend,
+                                            int rHo = 0, int rWo = 0, int rph = 0, int rpw = 0) {
   using F = CfMfma<SH>;
   constexpr int E = F::E;
   const int row0 = m0 + wm * (BM / WM), col0 = n0 + wn * (BN / WN);
   const int li = lane % SH;
   auto row_of = [&](int i, int e) { return row0 + i * SH + F::out_row(lane, e); };
   auto col_of = [&](int j) { return col0 + j * SH + li; };
+  auto orow = [&](int r) -> long long {
+    if constexpr (!RMAP) {
+      return r;
+    } else {
+      const int HoWo = rHo * rWo;
+      const int n = r / HoWo, hw = r - n * HoWo, i = hw / rWo, j = hw - i * rWo;
+      return (long long)n * 4 * HoWo + (2 * i + rph) * (2 * rWo) + 2 * j + rpw;
+    }
+  };
   if (slab) {
     float* sp = slab;  // this block's split slab (k_cf_gemm offsets it)
 #pragma unroll
@@ -355,7 +427,7 @@ __device__ __forceinline__ void cf_epilogue(typename CfMfma<SH>::acc_t (&acc)[MI
       for (int j = 0; j < NJ; ++j)
 #pragma unroll
         for (int e = 0; e < E; ++e)
-          av[i][j][e] = addend[(long long)row_of(i, e) * Nc + col_of(j)];
+          av[i][j][e] = addend[orow(row_of(i, e)) * Nc + col_of(j)];
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -368,8 +440,8 @@ __device__ __forceinline__ void cf_epilogue(typename CfMfma<SH>::acc_t (&acc)[MI
 #pragma unroll
     for (int e = 0; e < E; ++e)
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) out[(long long)row_of(i, e) * Nc + col_of(j)] = acc[i][j][e];
-  if (!bnpart) return;
+      for (int j = 0; j < NJ; ++j) out[orow(row_of(i, e)) * Nc + col_of(j)] = acc[i][j][e];
+  if (RMAP || !bnpart) return;
   float* red = reinterpret_cast<float*>(smem);  // [wm][wn][2][BN/WN]
   const long long nrows = M / BM;
   float sm[NJ], sq[NJ];
@@ -457,7 +529,7 @@ __device__ __forceinline__ void cf_epilogue(typename CfMfma<SH>::acc_t (&acc)[MI
 // 32-deep k-step per iteration through two LDS stages and two staging register sets (step s+2 is
 // loaded while s computes and s+1 is written), split z covers k-steps
 // [z*kps, min((z+1)*kps, ksteps)).
-template <int MODE, int BM, int BN, int WM, int WN, int SH>
+template <int MODE, int BM, int BN, int WM, int WN, int SH, int STR = 1>
 __global__ __launch_bounds__(64 * WM * WN) void k_cf_gemm(const float* __restrict__ a_src,
                                                    const float* __restrict__ b_src,
                                                    float* __restrict__ out,
@@ -479,10 +551,16 @@ __global__ __launch_bounds__(64 * WM * WN) void k_cf_gemm(const float* __restric
   out += zb * geo.o_bs;
   // slabs [split][batch][M][Ncol]: the reduction sums the splits of a contiguous batch run
   if (slab) slab += (long long)(zs * (gridDim.z / geo.nsplit) + zb) * geo.M * geo.Ncol;
+  // stride-2 backward data: z = dx phase, heaviest first (3x3: z 0 = phase (1, 1) with 4 taps
+  // ... z 3 = phase (0, 0) with 1; blocks dispatch in z order, so the light phases backfill)
+  constexpr bool S2B = STR == 2 && MODE == CF_BWD;
+  const int phase = (S2B && geo.taps != 1) ? 3 - zb : zb;
   const int kbeg = zs * geo.kps;
-  const int kend = min(kbeg + geo.kps, geo.ksteps);
-  CfStager<MODE, BM, BN, NT> st;
-  st.init(geo, a_src, b_src, t, m0, n0);
+  const int ksteps =
+      S2B ? cf_s2_ntaps(geo.taps, phase >> 1, phase & 1) * (geo.Nc / CF_BK) : geo.ksteps;
+  const int kend = min(kbeg + geo.kps, ksteps);
+  CfStager<MODE, BM, BN, NT, STR> st;
+  st.init(geo, a_src, b_src, t, m0, n0, phase);
 
   acc_t acc[MI][NJ];
 #pragma unroll
@@ -524,8 +602,9 @@ __global__ __launch_bounds__(64 * WM * WN) void k_cf_gemm(const float* __restric
     }
   }
   __syncthreads();  // the epilogue reuses smem
-  cf_epilogue<BM, BN, WM, WN, SH, MI, NJ>(acc, smem, wm, wn, lane, m0, n0, geo.M, geo.Ncol,
-                                          out, slab, bnpart, bb, addend);
+  cf_epilogue<BM, BN, WM, WN, SH, MI, NJ, S2B>(acc, smem, wm, wn, lane, m0, n0, geo.M, geo.Ncol,
+                                               out, slab, bnpart, bb, addend, geo.H, geo.W,
+                                               phase >> 1, phase & 1);
 }
 
 // out[i] = sum_z slab[z][i] (+ addend), 8 elements per thread
@@ -942,11 +1021,11 @@ CfPlan cf_plan(int M, int Ncol, int ksteps, long long ws_floats, int batch) {
   return best;
 }
 
-#define CF_LAUNCH(MODE_, BM_, BN_, WM_, WN_, SH_)                                                 \
-  hipLaunchKernelGGL((k_cf_gemm<MODE_, BM_, BN_, WM_, WN_, SH_>), grid, dim3(64 * WM_ * WN_), 0, s, \
-                     a, b, out, slab, geo, bnp, bbv, addend)
+#define CF_LAUNCH(MODE_, BM_, BN_, WM_, WN_, SH_)                                          \
+  hipLaunchKernelGGL((k_cf_gemm<MODE_, BM_, BN_, WM_, WN_, SH_, STR>), grid, dim3(64 * WM_ * WN_), \
+                     0, s, a, b, out, slab, geo, bnp, bbv, addend)
 
-template <int MODE>
+template <int MODE, int STR = 1>
 int cf_gemm(const float* a, const float* b, float* out, float* ws, long long ws_floats,
             CfGeom geo, hipStream_t s, float* bnpart, long long bnpart_floats,
             const CfBnBwd* bnb, const float* addend, int* split_out = nullptr) {
@@ -1101,6 +1180,55 @@ void ew_conv_f32_wgrad(uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws, lo
   cf_gemm<CF_WGRAD>(reinterpret_cast<const float*>(dy), reinterpret_cast<const float*>(x),
                     reinterpret_cast<float*>(dw), reinterpret_cast<float*>(ws), ws_floats, g,
                     (hipStream_t)stream, nullptr, 0, nullptr, nullptr);
+}
+
+// ---- stride-2 3x3 / pad 1 and 1x1 / pad 0 convolutions (the ResNet down-sampling convs):
+// x [N][H][W][C] -> y [N][H/2][W/2][Nc], H and W even
+static void cf_s2_check(long long N, int H, int W, int C, int Nc, const char* what) {
+  const long long Po = N * (H / 2) * (W / 2);
+  if (H % 2 || W % 2 || C % 64 || Nc % 64 || Po % 64 ||
+      N * H * W * (long long)std::max(C, Nc) >= (1LL << 31))
+    throw std::runtime_error(std::string("ewdml conv f32 stride 2: ") + what +
+                             " needs even H, W, C % 64 == 0, Nc % 64 == 0, N*H*W/4 % 64 == 0");
+}
+
+int ew_conv_f32_fwd_s2(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t ws, long long ws_floats,
+                       long long N, int H, int W, int C, int Nc, int ksize, uintptr_t bnpart,
+                       long long bnpart_floats, uintptr_t stream) {
+  cf_s2_check(N, H, W, C, Nc, "forward");
+  const int taps = cf_taps(ksize), Ho = H / 2, Wo = W / 2;
+  const long long M = N * Ho * Wo;
+  CfGeom g{(int)M, Nc, (int)M, H, W, C, Nc, taps, taps * C / CF_BK, 0, 1, 0, 0, 0, 0, 2, Ho, Wo};
+  return cf_gemm<CF_FWD, 2>(reinterpret_cast<const float*>(x), reinterpret_cast<const float*>(w),
+                            reinterpret_cast<float*>(y), reinterpret_cast<float*>(ws), ws_floats,
+                            g, (hipStream_t)stream, reinterpret_cast<float*>(bnpart),
+                            bnpart_floats, nullptr, nullptr);
+}
+
+// dx [N][H][W][C] (every pixel written: the four phases, 1x1's empty ones as zeros (+ addend))
+void ew_conv_f32_bwd_data_s2(uintptr_t dy, uintptr_t w, uintptr_t dx, long long N, int H, int W,
+                             int C, int Nc, int ksize, uintptr_t addend, uintptr_t stream) {
+  cf_s2_check(N, H, W, C, Nc, "backward data");
+  const int taps = cf_taps(ksize), Ho = H / 2, Wo = W / 2;
+  const long long M = N * Ho * Wo;
+  const int kmax = cf_s2_ntaps(taps, 1, 1) > 1 ? 4 : 1;
+  // batch 4 = the phases; no split-K (ws_floats 64: nothing beyond the zero page)
+  CfGeom g{(int)M, C, (int)M, Ho, Wo, C, Nc, taps, kmax * Nc / CF_BK, 0, 4, 0, 0, 0, 0, 2, Ho, Wo};
+  cf_gemm<CF_BWD, 2>(reinterpret_cast<const float*>(dy), reinterpret_cast<const float*>(w),
+                     reinterpret_cast<float*>(dx), nullptr, 64, g, (hipStream_t)stream, nullptr, 0,
+                     nullptr, reinterpret_cast<const float*>(addend));
+}
+
+void ew_conv_f32_wgrad_s2(uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws,
+                          long long ws_floats, long long N, int H, int W, int C, int Nc, int ksize,
+                          uintptr_t stream) {
+  cf_s2_check(N, H, W, C, Nc, "weight gradient");
+  const int taps = cf_taps(ksize), Ho = H / 2, Wo = W / 2;
+  const long long P = N * Ho * Wo;
+  CfGeom g{Nc, taps * C, (int)P, H, W, C, Nc, taps, (int)(P / CF_BK), 0, 1, 0, 0, 0, 0, 2, Ho, Wo};
+  cf_gemm<CF_WGRAD, 2>(reinterpret_cast<const float*>(dy), reinterpret_cast<const float*>(x),
+                       reinterpret_cast<float*>(dw), reinterpret_cast<float*>(ws), ws_floats, g,
+                       (hipStream_t)stream, nullptr, 0, nullptr, nullptr);
 }
 
 int ew_conv_f32_stem_fwd(uintptr_t x, uintptr_t w, uintptr_t y, long long N, int H, int W, int Nc,

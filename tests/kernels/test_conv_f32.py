@@ -35,8 +35,10 @@ def _restore_winograd():
     from ewdml.ops import conv
 
     saved = (conv._WINO, conv._WINO_MIN_C, conv._WINO_TILE)
+    s2 = conv._S2
     yield
     conv.set_winograd(*saved)
+    conv.set_stride2(s2)
 
 
 def _rel(a, b):
@@ -195,6 +197,69 @@ def test_conv_f32_bn_backward_sums_in_bwd_data_epilogue(mode, pool, N, HW):
     conv.set_bn_bwd_fusion(True)
     for a, b in zip(*grads):
         assert _rel(a, b) < 1e-5, _rel(a, b)
+
+
+S2_SHAPES = [  # (N, C, Nc, H, W, k): stride 2, H x W the input map
+    (128, 128, 128, 32, 32, 3),   # ResNet-50 CIFAR layer2.0 conv2
+    (128, 256, 256, 16, 16, 3),   # layer3.0 conv2
+    (128, 512, 512, 8, 8, 3),     # layer4.0 conv2: split-K forward / weight gradient
+    (128, 256, 512, 32, 32, 1),   # layer2.0 shortcut
+    (128, 1024, 2048, 8, 8, 1),   # layer4.0 shortcut
+    (4, 64, 128, 16, 32, 3),      # H != W, small
+    (16, 64, 64, 8, 8, 1),        # 1x1, small
+]
+
+
+@pytest.mark.parametrize("N,C,Nc,H,W,k", S2_SHAPES)
+def test_conv_f32_stride2(N, C, Nc, H, W, k):
+    """Stride-2 3x3 / 1x1 kernels (phase-split backward data) against float64, through
+    ``conv2d_module`` as the ResNets call them."""
+    conv = _conv()
+    conv.set_stride2(True)
+    x, w = _data(N, C, Nc, H, W, seed=31, k=k)
+    m = torch.nn.Conv2d(C, Nc, k, 2, k // 2, bias=False).cuda()
+    with torch.no_grad():
+        m.weight.copy_(w)
+    m = m.to(memory_format=torch.channels_last)
+    assert conv.s2_supported(x, m.weight, m.stride, m.padding, m.dilation, m.groups)
+    g = torch.Generator(device="cuda").manual_seed(32)
+    dy = torch.randn(N, Nc, H // 2, W // 2, device="cuda", generator=g).contiguous(
+        memory_format=torch.channels_last)
+    xa = x.clone().requires_grad_(True)
+    y = conv.conv2d_module(m, xa)
+    assert "ConvS2" in type(y.grad_fn).__name__  # the HIP kernels, not MIOpen
+    assert y.shape == (N, Nc, H // 2, W // 2)
+    assert hasattr(y, "_ew_bn_part")
+    y.backward(dy)
+    xr = x.detach().double().cpu().requires_grad_(True)
+    wr = w.detach().double().cpu().requires_grad_(True)
+    yr = F.conv2d(xr, wr, stride=2, padding=k // 2)
+    yr.backward(dy.detach().double().cpu())
+    assert _rel(y, yr) < TOL, _rel(y, yr)
+    assert _rel(xa.grad, xr.grad) < TOL, _rel(xa.grad, xr.grad)
+    assert _rel(m.weight.grad, wr.grad) < TOL, _rel(m.weight.grad, wr.grad)
+    # deterministic (fixed-order split sums) and BN partials consistent with the BN kernels
+    xb = x.clone().requires_grad_(True)
+    gw = m.weight.grad.clone()
+    m.weight.grad = None
+    y2 = conv.conv2d_module(m, xb)
+    y2.backward(dy)
+    assert torch.equal(y, y2) and torch.equal(xa.grad, xb.grad) and torch.equal(gw, m.weight.grad)
+
+
+def test_conv_f32_stride2_bn_partials():
+    from ewdml.ops import nn as fnn
+
+    conv = _conv()
+    x, w = _data(64, 128, 256, 16, 16, seed=33)
+    bn0 = torch.nn.BatchNorm2d(256).cuda()
+    bn1 = copy.deepcopy(bn0)
+    h = conv.conv_s2(x, w.clone().requires_grad_(True))
+    assert hasattr(h, "_ew_bn_part")
+    y0 = fnn.bn_act(h, bn0, "relu")
+    y1 = fnn.bn_act(h.detach().clone(), bn1, "relu")
+    assert _rel(y0, y1) < 1e-5
+    assert torch.allclose(bn0.running_var, bn1.running_var, rtol=1e-5, atol=1e-7)
 
 
 WINO_SHAPES = [  # (N, C, Nc, H, W, m)
