@@ -15,7 +15,17 @@ import torch
 
 _IMPORT_ERROR = None
 try:  # torch is imported first so the extension binds to torch's already-loaded HIP runtime
-    _C = importlib.import_module(__name__ + "._C")
+    _ALT = os.environ.get("EWDML_EXT")  # A/B of a compile-time variant: another built _C .so
+    if _ALT:
+        import importlib.util
+        import sys as _sys
+
+        _spec = importlib.util.spec_from_file_location(__name__ + "._C", _ALT)
+        _C = importlib.util.module_from_spec(_spec)
+        _spec.loader.exec_module(_C)
+        _sys.modules[__name__ + "._C"] = _C
+    else:
+        _C = importlib.import_module(__name__ + "._C")
 except ImportError as e:  # pragma: no cover - depends on the build
     _C = None
     _IMPORT_ERROR = e

@@ -279,21 +279,26 @@ struct CfStager {
       if constexpr (STR == 2 && MODE == CF_BWD) {
         cf_s2_tap(g.taps, ph, pw, tap, dr, dc, wtap);
       } else {
-        dr = g.taps == 1 ? 0 : tap / 3 - 1;
-        dc = g.taps == 1 ? 0 : tap - (tap / 3) * 3 - 1;
+        // computed unconditionally and then selected: a conditional division became a scalar
+        // branch, which split the k-step's scheduling region
+        const int q = tap / 3, one = g.taps == 1;
+        dr = one ? 0 : q - 1;
+        dc = one ? 0 : tap - q * 3 - 1;
         wtap = g.taps - 1 - tap;  // backward data: the 180-degree-rotated kernel's tap
       }
       {
         // out-of-image taps load the zero page: a select on the loaded VALUE would make hipcc
         // wait for this step's loads before the step's MFMAs (s_waitcnt vmcnt ahead of the
         // masking), a select on the ADDRESS does not
+        // the address is formed unconditionally and then selected (a select of a computed
+        // value stays a v_cndmask; selecting between computing it or not became a branch,
+        // which split the k-step and kept the address arithmetic out of the MFMA stream)
         CfRegs& RG = ra;
         CF_FOR(RA, {
           const bool ok = (unsigned)(ah[i] + dr) < (unsigned)g.H &&
                           (unsigned)(aw[i] + dc) < (unsigned)g.W;
-          const float* src = ok ? xa + (long long)(am[i] + dr * g.W + dc) * CH + cb * CF_BK +
-                                      (t & 7) * 4
-                                : cf_zero_page;
+          const float* in = xa + (long long)(am[i] + dr * g.W + dc) * CH + cb * CF_BK + (t & 7) * 4;
+          const float* src = ok ? in : cf_zero_page;
           v = *reinterpret_cast<const f32x4*>(src);
         });
       }
@@ -529,8 +534,9 @@ __device__ __forceinline__ void cf_epilogue(typename CfMfma<SH>::acc_t (&acc)[MI
 // 32-deep k-step per iteration through two LDS stages and two staging register sets (step s+2 is
 // loaded while s computes and s+1 is written), split z covers k-steps
 // [z*kps, min((z+1)*kps, ksteps)).
-template <int MODE, int BM, int BN, int WM, int WN, int SH, int STR = 1>
-__global__ __launch_bounds__(64 * WM * WN) void k_cf_gemm(const float* __restrict__ a_src,
+// WPE: waves per SIMD the register allocation must allow (0: the compiler's choice)
+template <int MODE, int BM, int BN, int WM, int WN, int SH, int STR = 1, int WPE = 0>
+__global__ __launch_bounds__(64 * WM * WN, WPE) void k_cf_gemm(const float* __restrict__ a_src,
                                                    const float* __restrict__ b_src,
                                                    float* __restrict__ out,
                                                    float* __restrict__ slab, CfGeom geo,
@@ -586,10 +592,11 @@ __global__ __launch_bounds__(64 * WM * WN) void k_cf_gemm(const float* __restric
     for (int i0 = 0; i0 < nfull; i0 += 2) {
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
-        st.load(geo, min(kbeg + i0 + u + 2, last), ra[u], rb[u]);
         const char* cs = smem + u * L::STAGE;
         Frag fr;
+        // fragment reads first: the loads' address arithmetic then runs under their latency
         cf_frag_read<MODE, BM, BN, SH, MI, NJ>(cs, cs + L::A_BYTES, arow0, bcol0, lane, fr);
+        st.load(geo, min(kbeg + i0 + u + 2, last), ra[u], rb[u]);
         cf_mma<SH, MI, NJ, 0, Frag::R>(fr, acc);
         st.store(smem + (u ^ 1) * L::STAGE, ra[u ^ 1], rb[u ^ 1]);
         __syncthreads();
@@ -1021,9 +1028,10 @@ CfPlan cf_plan(int M, int Ncol, int ksteps, long long ws_floats, int batch) {
   return best;
 }
 
-#define CF_LAUNCH(MODE_, BM_, BN_, WM_, WN_, SH_)                                          \
-  hipLaunchKernelGGL((k_cf_gemm<MODE_, BM_, BN_, WM_, WN_, SH_, STR>), grid, dim3(64 * WM_ * WN_), \
-                     0, s, a, b, out, slab, geo, bnp, bbv, addend)
+#define CF_LAUNCH_W(MODE_, BM_, BN_, WM_, WN_, SH_, WPE_)                                   \
+  hipLaunchKernelGGL((k_cf_gemm<MODE_, BM_, BN_, WM_, WN_, SH_, STR, WPE_>), grid,                \
+                     dim3(64 * WM_ * WN_), 0, s, a, b, out, slab, geo, bnp, bbv, addend)
+#define CF_LAUNCH(MODE_, BM_, BN_, WM_, WN_, SH_) CF_LAUNCH_W(MODE_, BM_, BN_, WM_, WN_, SH_, 0)
 
 template <int MODE, int STR = 1>
 int cf_gemm(const float* a, const float* b, float* out, float* ws, long long ws_floats,
@@ -1047,13 +1055,24 @@ int cf_gemm(const float* a, const float* b, float* out, float* ws, long long ws_
     const char* e = getenv("EWDML_CF_WAVES");
     return e && e[0] == '4';
   }();
+  // The 8-wave 128x64 / 64x128 kernels held to 128 VGPRs (4 waves per SIMD: two blocks per CU)
+  // instead of the compiler's 130 (one block per CU), for grids of more than one block per CU:
+  // ResNet-50 CIFAR +1.1 %, VGG-11 (one block per CU at these tiles) unchanged either way
+  // (profiles/ab/README.md).  EWDML_CF_OCC=0: never, =2: always.
+  static const int occ_env = [] {
+    const char* e = getenv("EWDML_CF_OCC");
+    return e ? e[0] - '0' : 1;
+  }();
+  const bool occ2 = occ_env == 2 || (occ_env == 1 && (long long)grid.x * grid.y * grid.z > 256);
   if (p.bm == 128 && p.bn == 128) {
     if (w4) CF_LAUNCH(MODE, 128, 128, 2, 2, 32);
     else CF_LAUNCH(MODE, 128, 128, 2, 4, 32);
   } else if (p.bm == 128) {
-    CF_LAUNCH(MODE, 128, 64, 4, 2, 32);
+    if (occ2) CF_LAUNCH_W(MODE, 128, 64, 4, 2, 32, 4);
+    else CF_LAUNCH(MODE, 128, 64, 4, 2, 32);
   } else if (p.bn == 128) {
-    CF_LAUNCH(MODE, 64, 128, 2, 4, 32);
+    if (occ2) CF_LAUNCH_W(MODE, 64, 128, 2, 4, 32, 4);
+    else CF_LAUNCH(MODE, 64, 128, 2, 4, 32);
   } else {
     CF_LAUNCH(MODE, 64, 64, 4, 2, 16);
   }
@@ -1090,6 +1109,7 @@ int cf_gemm(const float* a, const float* b, float* out, float* ws, long long ws_
   return bnp ? (int)prow : 0;
 }
 #undef CF_LAUNCH
+#undef CF_LAUNCH_W
 
 int cf_taps(int ksize) {
   if (ksize != 1 && ksize != 3) throw std::runtime_error("ewdml conv: kernel size must be 1 or 3");
