@@ -38,7 +38,29 @@ __global__ __launch_bounds__(512) void k_loop(float* out, int steps, const float
   f32x4 g[4][4];
   // 32 KB per step per block: block b, step s reads line group ((b * 7 + s) mod 8192) of the
   // buffer (power-of-two wrap: no 64-bit modulo in the address path)
+  // V == 5: the real forward im2col pattern (C = 512 NHWC, 16x16 maps, K = 9 x 512): A rows =
+  // 128 pixels of this block, 8 threads per 128-B chunk of a row, rows 2 KB apart, the chunk
+  // walking the channels and the tap shifting the pixel; B = weights [128][4608] (18 KB rows)
+  auto gload5 = [&](int s, f32x4* d) {
+    const int tap = (s >> 4) % 9, cb = s & 15;
+    const int shift = (tap / 3 - 1) * 16 + (tap % 3 - 1);
+    const long long pix0 = (long long)blockIdx.x * 128 + 1024;  // away from the buffer start
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const long long row = pix0 + (t >> 3) + 64 * i + shift;
+      d[i] = *reinterpret_cast<const f32x4*>(src + row * 512 + cb * 32 + (t & 7) * 4);
+    }
+    const float* wb = src + (60LL << 20);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      d[2 + i] = *reinterpret_cast<const f32x4*>(wb + (long long)((t >> 3) + 64 * i) * 4608 +
+                                                  (s % 144) * 32 + (t & 7) * 4);
+  };
   auto gload = [&](int s, f32x4* d) {
+    if (V == 5) {
+      gload5(s, d);
+      return;
+    }
     const float* p = src + (size_t)(((unsigned)blockIdx.x * 7u + (unsigned)s) & 8191u) * 8192u;
 #pragma unroll
     for (int i = 0; i < 4; ++i) d[i] = *reinterpret_cast<const f32x4*>(p + (i * 512 + t) * 4);
@@ -129,6 +151,8 @@ int main() {
   printf("3 + lds writes         %6.1f TF/s\n", run<3>(out, blocks, steps, src, n));
   printf("4 + global loads (2)   %6.1f TF/s\n", run<4, 2>(out, blocks, steps, src, n));
   printf("4 + global loads (4)   %6.1f TF/s\n", run<4, 4>(out, blocks, steps, src, n));
+  printf("5 im2col pattern (2)   %6.1f TF/s\n", run<5, 2, true>(out, blocks, steps, src, n));
+  printf("5 im2col pattern (4)   %6.1f TF/s\n", run<5, 4, true>(out, blocks, steps, src, n));
   printf("random data: 1         %6.1f TF/s\n", run<1, 2, true>(out, blocks, steps, src, n));
   printf("random data: 4 (2)     %6.1f TF/s\n", run<4, 2, true>(out, blocks, steps, src, n));
   hipFree(src);
