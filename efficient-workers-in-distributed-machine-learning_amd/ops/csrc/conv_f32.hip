@@ -42,7 +42,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int CF_BK = 32;  // reduction depth of one k-step (floats)
 enum { CF_FWD = 0, CF_BWD = 1, CF_WGRAD = 2 };
 #ifndef CF_PRIO
-#define CF_PRIO 1  // s_setprio(1) around each MFMA cluster (cdna_hip_programming.md T5)
+#define CF_PRIO 0  // 1: s_setprio(1) around each MFMA cluster -- measured 3 % slower (profiles/ab/README.md)
 #endif
 
 __device__ __forceinline__ int cf_off(int r, int c) {  // byte offset of chunk c of row r (KC)
