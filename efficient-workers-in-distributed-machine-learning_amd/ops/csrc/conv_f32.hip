@@ -215,6 +215,16 @@ struct CfRegs {
 // 16 zero bytes in device memory (zero-initialised at module load), read by masked-out loads
 __device__ __attribute__((aligned(16))) float cf_zero_page[4];
 
+// Raw buffer descriptor over [p, p + bytes) (p and bytes wave-uniform) and a 16-B load through it;
+// offsets past the range read zeros (CF_OOB: never in range, the host keeps operands < 4 GB - 16)
+constexpr unsigned CF_OOB = 0xFFFFFFF0u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t cf_rsrc(const float* p, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ f32x4 cf_bload(__amdgpu_buffer_rsrc_t r, unsigned voff, int soff) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, soff, 0));
+}
+
 template <int MODE, int BM, int BN, int NT, int STR = 1>
 struct CfStager {
   using L = CfLayout<MODE, BM, BN>;
@@ -230,6 +240,12 @@ struct CfStager {
   const float* xb;  // B source
   int t, m0, n0;
   int ph, pw;  // stride-2 backward data: this block's dx phase
+  // Buffer loads (32-bit byte offsets from a wave-uniform descriptor; every operand < 4 GB, checked
+  // on the host): the per-lane part of each offset is fixed at init and the per-step part is a
+  // scalar, so a step's address work is a few 32-bit adds instead of 64-bit multiply-adds
+  // (fwd / bwd A: an add, the padding test and a select per load; B and wgrad A: soffset only).
+  __amdgpu_buffer_rsrc_t rsa, rsb;
+  unsigned aoff[RA], boff[RB];
 
   __device__ __forceinline__ void init(const CfGeom& g, const float* a_src, const float* b_src,
                                        int t_, int m0_, int n0_, int zb = 0) {
@@ -266,6 +282,35 @@ struct CfStager {
       bdr = g.taps == 1 ? 0 : tap / 3 - 1;
       bdc = g.taps == 1 ? 0 : tap - (tap / 3) * 3 - 1;
     }
+    if constexpr (MODE == CF_FWD || MODE == CF_BWD) {
+      const unsigned CH = MODE == CF_FWD ? g.C : g.Nc;
+      const unsigned rows = (STR == 2 && MODE == CF_FWD)
+                                ? (unsigned)(g.M / (g.Ho * g.Wo)) * g.H * g.W
+                                : (unsigned)g.M;
+      rsa = cf_rsrc(xa, rows * CH * 4u);
+#pragma unroll
+      for (int i = 0; i < RA; ++i) aoff[i] = ((unsigned)am[i] * CH + (t & 7) * 4) * 4u;
+      if constexpr (MODE == CF_FWD) {
+        // w[n][taps*C]: row n's chunk t & 7, the step adds s * 128 B
+        const unsigned K = (unsigned)g.taps * g.C;
+        rsb = cf_rsrc(xb, (unsigned)g.Ncol * K * 4u);
+#pragma unroll
+        for (int i = 0; i < RB; ++i)
+          boff[i] = ((unsigned)(n0 + (t >> 3) + (NT / 8) * i) * K + (t & 7) * 4) * 4u;
+      } else {
+        // w[Nc][taps][C]: k-row kr of the step's 32 channels; the step adds
+        // ((cb * 32) * taps + tap) * C floats
+        rsb = cf_rsrc(xb, (unsigned)g.Nc * g.taps * g.C * 4u);
+#pragma unroll
+        for (int i = 0; i < RB; ++i)
+          boff[i] = ((unsigned)(t / RCB + RPB * i) * g.taps * g.C + n0 + (t % RCB) * 4) * 4u;
+      }
+    } else {
+      // dy[m][Nc]: k-row kr of the step's 32 pixels, the step adds s * 32 * Nc floats
+      rsa = cf_rsrc(xa, (unsigned)g.ksteps * CF_BK * g.Nc * 4u);
+#pragma unroll
+      for (int i = 0; i < RA; ++i) aoff[i] = ((unsigned)(t / RCA + RPA * i) * g.Nc + m0 + (t % RCA) * 4) * 4u;
+    }
   }
 
   // global -> registers for k-step s
@@ -294,40 +339,29 @@ struct CfStager {
         // value stays a v_cndmask; selecting between computing it or not became a branch,
         // which split the k-step and kept the address arithmetic out of the MFMA stream)
         CfRegs& RG = ra;
+        const unsigned sa = (unsigned)(((dr * g.W + dc) * CH + cb * CF_BK) * 4);  // wave-uniform
         CF_FOR(RA, {
           const bool ok = (unsigned)(ah[i] + dr) < (unsigned)g.H &&
                           (unsigned)(aw[i] + dc) < (unsigned)g.W;
-          const float* in = xa + (long long)(am[i] + dr * g.W + dc) * CH + cb * CF_BK + (t & 7) * 4;
-          const float* src = ok ? in : cf_zero_page;
-          v = *reinterpret_cast<const f32x4*>(src);
+          // out-of-image taps: an offset past the descriptor's range reads zeros
+          v = cf_bload(rsa, ok ? aoff[i] + sa : CF_OOB, 0);
         });
       }
       if constexpr (MODE == CF_FWD) {
         // B: w[n][taps*C], k index s*32 + chunk*4
-        const long long K = (long long)g.taps * g.C;
         CfRegs& RG = rb;
-        CF_FOR(RB, {
-          v = *reinterpret_cast<const f32x4*>(xb + (long long)(n0 + (t >> 3) + (NT / 8) * i) * K +
-                                              (long long)s * CF_BK + (t & 7) * 4);
-        });
+        CF_FOR(RB, { v = cf_bload(rsb, boff[i], s * CF_BK * 4); });
       } else {
         // B (RC): k-row kr = reduction channel n = cb*32 + kr at the flipped tap; columns c
         CfRegs& RG = rb;
-        CF_FOR(RB, {
-          const int kr = t / RCB + RPB * i;
-          v = *reinterpret_cast<const f32x4*>(
-              xb + ((long long)(cb * CF_BK + kr) * g.taps + wtap) * g.C + n0 + (t % RCB) * 4);
-        });
+        const int sb = ((cb * CF_BK) * g.taps + wtap) * g.C * 4;
+        CF_FOR(RB, { v = cf_bload(rsb, boff[i], sb); });
       }
     } else {
       // wgrad: k = pixel m = s*32 + kr.  A (RC): dy[m][rows m0..]; B (RC): im2col x[m][(tap,c)]
       {
         CfRegs& RG = ra;
-        CF_FOR(RA, {
-          const int kr = t / RCA + RPA * i;
-          v = *reinterpret_cast<const f32x4*>(xa + (long long)(s * CF_BK + kr) * g.Nc + m0 +
-                                              (t % RCA) * 4);
-        });
+        CF_FOR(RA, { v = cf_bload(rsa, aoff[i], (int)((unsigned)s * CF_BK * g.Nc * 4u)); });
       }
       {
         const int HW = g.H * g.W;
@@ -1039,6 +1073,24 @@ int cf_gemm(const float* a, const float* b, float* out, float* ws, long long ws_
             const CfBnBwd* bnb, const float* addend, int* split_out = nullptr) {
   ws_floats -= 64;  // the workspace's last 64 floats are conv.hip's zero page (never a slab)
   const int batch = geo.nsplit;  // callers pass the batch count here (1: no batching)
+  {
+    // the buffer-load operands (per batch) must fit 32-bit byte offsets (CfStager)
+    const long long K = (long long)geo.taps * geo.C;
+    long long a_bytes, b_bytes = 0;
+    if (MODE == CF_FWD) {
+      const long long rows = STR == 2 ? (long long)(geo.M / (geo.Ho * geo.Wo)) * geo.H * geo.W
+                                      : (long long)geo.M;
+      a_bytes = rows * geo.C * 4;
+      b_bytes = (long long)geo.Ncol * K * 4;
+    } else if (MODE == CF_BWD) {
+      a_bytes = (long long)geo.M * geo.Nc * 4;
+      b_bytes = (long long)geo.Nc * K * 4;
+    } else {
+      a_bytes = (long long)geo.ksteps * CF_BK * geo.Nc * 4;
+    }
+    if (std::max(a_bytes, b_bytes) >= (long long)CF_OOB)
+      throw std::runtime_error("ewdml conv f32: an operand of 4 GB or more");
+  }
   const CfPlan p = cf_plan(geo.M, geo.Ncol, geo.ksteps, ws_floats, batch);
   geo.kps = p.kps;
   geo.nsplit = p.split;
