@@ -310,6 +310,12 @@ struct CfStager {
       rsa = cf_rsrc(xa, (unsigned)g.ksteps * CF_BK * g.Nc * 4u);
 #pragma unroll
       for (int i = 0; i < RA; ++i) aoff[i] = ((unsigned)(t / RCA + RPA * i) * g.Nc + m0 + (t % RCA) * 4) * 4u;
+      if constexpr (STR == 1) {
+        // x[m][C] (stride 1: one input pixel per output pixel): k-row kr, channel bc
+        rsb = cf_rsrc(xb, (unsigned)g.ksteps * CF_BK * g.C * 4u);
+#pragma unroll
+        for (int i = 0; i < RB; ++i) boff[i] = ((unsigned)(t / RCB + RPB * i) * g.C + bc) * 4u;
+      }
     }
   }
 
@@ -378,15 +384,18 @@ struct CfStager {
                 ok ? xb + ((long long)n * HW + h * g.W + w) * g.C + bc : cf_zero_page;
             v = *reinterpret_cast<const f32x4*>(src);
           });
+        } else if (g.taps == 1) {
+          // 1x1: the im2col row is the pixel itself -- no (h, w), no padding
+          CF_FOR(RB, { v = cf_bload(rsb, boff[i], (int)((unsigned)s * CF_BK * g.C * 4u)); });
         } else {
           CF_FOR(RB, {
             const int m = s * CF_BK + t / RCB + RPB * i;
             const int hw = m % HW, h = hw / g.W, w = hw - h * g.W;
             const bool ok =
                 (unsigned)(h + bdr) < (unsigned)g.H && (unsigned)(w + bdc) < (unsigned)g.W;
-            const float* src =
-                ok ? xb + (long long)(m + bdr * g.W + bdc) * g.C + bc : cf_zero_page;
-            v = *reinterpret_cast<const f32x4*>(src);
+            const unsigned off =
+                boff[i] + (unsigned)((s * CF_BK + bdr * g.W + bdc) * g.C) * 4u;
+            v = cf_bload(rsb, ok ? off : CF_OOB, 0);
           });
         }
       }
@@ -1087,6 +1096,7 @@ int cf_gemm(const float* a, const float* b, float* out, float* ws, long long ws_
       b_bytes = (long long)geo.Nc * K * 4;
     } else {
       a_bytes = (long long)geo.ksteps * CF_BK * geo.Nc * 4;
+      if (STR == 1) b_bytes = (long long)geo.ksteps * CF_BK * geo.C * 4;
     }
     if (std::max(a_bytes, b_bytes) >= (long long)CF_OOB)
       throw std::runtime_error("ewdml conv f32: an operand of 4 GB or more");
