@@ -111,8 +111,8 @@ class FusedFeatures(nn.Sequential):
                 if conv_hip.supported(x, conv.weight, conv.stride, conv.padding, conv.dilation,
                                       conv.groups):
                     h = conv_hip.conv3x3(x, conv.weight)  # MFMA implicit GEMM (ops/conv.py)
-                else:
-                    h = conv._conv_forward(x, conv.weight, None)
+                else:  # a lazily produced input (BN apply left to a Winograd conv) is written first
+                    h = conv._conv_forward(fnn.materialize(x), conv.weight, None)
                 if fnn.nhwc_supported(h, pool):
                     x = fnn.bn_relu(h, conv.bias, bn, pool, lazy=self._lazy_into(plan, gi, h, pool))
                 else:
@@ -122,7 +122,7 @@ class FusedFeatures(nn.Sequential):
                         h = m(h)
                     x = h
             elif kind == "pool":
-                x = fnn.maxpool2x2(x)
+                x = fnn.maxpool2x2(fnn.materialize(x))
             else:
-                x = mods[0](x)
+                x = mods[0](fnn.materialize(x))
         return x

@@ -46,7 +46,7 @@ _EPI_MAX = int(os.environ.get("EWDML_EPI_MAX", str(1 << 23)))
 
 
 # Winograd F(m x m, 3x3) for fp32 3x3 layers with min(C_in, C_out) >= _WINO_MIN_C (the deep layers,
-# where the GEMM outweighs the transforms' activation traffic: tools/conv_f32_probe.py --wino).
+# where the GEMM outweighs the transforms' activation traffic: tools/probes/conv_f32_probe.py --wino).
 # m: EWDML_WINO_TILE = 2 (default), 4 or auto (4 where the map tiles by 4 and C_out <= 512, else
 # 2).  m = 4 measured only +1.5 % on the VGG-11 step (smaller, more numerous GEMMs; 36-point
 # transforms) for ~4x m = 2's rounding error (5e-6 vs 1.3e-6 relative for MIOpen's fp32 on the
@@ -61,14 +61,18 @@ _WINO_M4_MAX_C = int(os.environ.get("EWDML_WINO_M4_MAX_C", "0"))
 _WINO_WG_SPLITS = int(os.environ.get("EWDML_WINO_WG_SPLITS", "4"))
 # Deferred Winograd weight-gradient output transforms (dw = G^T dU G).  dw feeds only the
 # optimizer / codec, so its transform rides in the next same-m Winograd backward-data input launch
-# (ops/csrc/winograd_f32.hip WgOut) instead of a launch of its own.  Deferred only for a leaf
-# Parameter whose .grad is None when its conv's backward runs (no accumulate-add reads dw).  The
-# job holds the Parameter, not dw (an extra reference would make autograd's AccumulateGrad copy
-# the unwritten dw instead of adopting it), and writes into whatever .grad autograd installed:
-# the adopted dw, or a copy that the transform then overwrites.  Flushed as a launch of its own by
-# a second deferral, at the end of the backward pass (an autograd final callback, run on the
-# caller's current stream) and by the exchange engine before it encodes a bucket
-# (parallel/engine.py), so a bucket's gradients are complete when its encode starts.
+# (ops/csrc/winograd_f32.hip WgOut) instead of a launch of its own.  Opt-in: deferred only for a
+# leaf Parameter whose .grad is None when its conv's backward runs and whose only post-accumulate
+# hooks are the exchange engine's (parallel/engine.py counts them in ``_ew_engine_hooks`` and
+# flushes before it reads a bucket), so no foreign hook (e.g. one on the AccumulateGrad node) can
+# read dw early.  The job writes into dw's own memory (it keeps dw's storage alive, not the tensor:
+# an extra tensor reference would stop AccumulateGrad from adopting dw), so the result is right
+# whoever ends up holding dw -- the adopted .grad, or the tensor torch.autograd.grad returns.  If
+# autograd installed a copy as .grad before the flush, the copy is refreshed from dw afterwards.
+# A job is never dropped: it is flushed as a launch of its own by a second deferral, at the end of
+# the backward pass (an autograd final callback, run on the caller's current stream) and by the
+# exchange engine before it encodes a bucket, so a bucket's gradients are complete when its
+# encode starts.
 _DEFER_WOUT = os.environ.get("EWDML_WINO_DEFER_WOUT", "1") != "0"
 # fp32 stride-2 3x3 / 1x1 convs (ResNet down-sampling) on the MFMA kernels: opt-in
 # (EWDML_CONV_S2=1).  Measured slower than MIOpen's tuned (find-mode) solvers on every ResNet-50
@@ -81,38 +85,33 @@ def set_stride2(on: bool):
     """Route fp32 stride-2 3x3 / 1x1 convs through :func:`conv_s2` (True) or MIOpen."""
     global _S2
     _S2 = bool(on)
-_PENDING = None  # (src, split, param, Nc, C, m, keep-alive tensors)
+_PENDING = None  # (src, split, param, Nc, C, m, keep-alive tensors, dw storage, shape, stride)
 _POISON_DW = False  # tests: NaN-fill each fresh dw, so a read before its transform shows
 
 
-def _job_dest(job):
-    """Pointer the job's transform writes (the parameter's .grad), or None (nothing to write),
-    and a (grad, temp) pair to copy afterwards when .grad has another layout."""
+def _job_fixup(job):
+    """(dw pointer, copy) of a job: the transform writes dw's memory; if autograd installed a
+    different tensor as the parameter's .grad (a copy of the unwritten dw), ``copy`` is the
+    (grad, dw view) pair to refresh afterwards."""
+    store, shape, stride = job[7], job[8], job[9]
+    dst = store.data_ptr()
     g = job[2].grad
-    if g is None:
-        return None, None
-    if g.dtype == torch.float32 and g.is_contiguous(memory_format=torch.channels_last):
-        return _ptr(g), None
-    tmp = torch.empty(g.shape, dtype=torch.float32, device=g.device,
-                      memory_format=torch.channels_last)
-    return _ptr(tmp), (g, tmp)
+    if g is None or g.data_ptr() == dst:
+        return dst, None
+    dw = torch.empty(0, dtype=torch.float32, device=g.device).set_(store, 0, shape, stride)
+    return dst, (g, dw)
 
 
 def flush_pending(final=False):
-    """Run a deferred weight-gradient output transform now.  Returns False if one stays pending:
-    its parameter's .grad is not installed yet (dropped instead when ``final``: the end of the
-    backward pass, after which nothing will install it)."""
+    """Run a deferred weight-gradient output transform now (``final`` is accepted for the end-of-
+    backward callback; every flush runs the job).  Returns True."""
     global _PENDING
     job = _PENDING
     if job is None:
         return True
-    dest, fix = _job_dest(job)
-    if dest is None and not final:
-        return False
     _PENDING = None
-    if dest is None:
-        return True
-    src, split, _p, Nc, C, m, _keep = job
+    dest, fix = _job_fixup(job)
+    src, split, _p, Nc, C, m = job[:6]
     require().wino_f32_wgrad_out(_ptr(src), split, dest, Nc, C, m, _stream())
     if fix is not None:
         fix[0].copy_(fix[1])
@@ -123,18 +122,19 @@ def _flush_final():
     flush_pending(final=True)
 
 
+def pending() -> bool:
+    """True while a deferred transform has not been enqueued yet."""
+    return _PENDING is not None
+
+
 def _take_pending(m):
     """The pending job as riding arguments of an m-tile backward-data call (zeros: none)."""
     global _PENDING
     job = _PENDING
-    if job is None:
+    if job is None or job[5] != m:
         return (0, 1, 0, 0, 0), None
-    if job[5] != m:
-        return (0, 1, 0, 0, 0), None
-    dest, fix = _job_dest(job)
-    if dest is None:  # .grad not installed yet: stays pending for a later flush
-        return (0, 1, 0, 0, 0), None
-    if fix is not None:  # an unusual .grad layout: a launch of its own (with the copy)
+    dest, fix = _job_fixup(job)
+    if fix is not None:  # .grad is already a copy: a launch of its own, then the refresh
         flush_pending()
         return (0, 1, 0, 0, 0), None
     _PENDING = None
@@ -143,17 +143,17 @@ def _take_pending(m):
 
 
 def _can_defer(ctx):
-    # nothing may read the gradient before a flush: no tensor hooks on the weight, and no
-    # post-accumulate hooks but the exchange engine's (which flushes before it reads,
-    # parallel/engine.py marks them in _ew_engine_hooks)
+    # opt-in: only parameters whose sole post-accumulate hooks are the exchange engine's (which
+    # flushes before it reads); no tensor hooks on the weight (they would see dw unwritten)
     p = getattr(ctx, "w_param", None)
     if not (_DEFER_WOUT and p is not None and p.grad is None and p.dtype == torch.float32
             and p.requires_grad and not torch.is_grad_enabled()):
         return False
     if getattr(p, "_backward_hooks", None):
         return False
+    eng = getattr(p, "_ew_engine_hooks", 0)
     post = getattr(p, "_post_accumulate_grad_hooks", None)
-    return not post or len(post) <= getattr(p, "_ew_engine_hooks", 0)
+    return eng > 0 and (not post or len(post) <= eng)
 
 
 def set_winograd(on: bool, min_c: int = None, tile=None):
@@ -481,7 +481,7 @@ class _Conv(torch.autograd.Function):
                 if defer:
                     global _PENDING
                     _PENDING = (slabs if split > 1 else dU, split, ctx.w_param, Nc, C, m,
-                                (dU, slabs))
+                                (dU, slabs), dw.untyped_storage(), tuple(dw.shape), dw.stride())
                     torch.autograd.Variable._execution_engine.queue_callback(_flush_final)
             else:
                 wgrad = C_.conv_f32_wgrad if f32 else C_.conv_wgrad

@@ -64,23 +64,33 @@ class Comm:
     def _make_rccl(self):
         """Create the RCCL communicator (collective over the process group: rank 0's unique id
         is broadcast as an object).  Every rank must end up with one or none alike."""
-        try:
-            from .. import ops
+        import logging
 
-            C = ops.require()
-            uid = C.rccl_unique_id() if self.rank == 0 else None
-            uid = self.broadcast_object(uid, src=0)
-            h = C.rccl_init(uid, self.world, self.rank, torch.cuda.current_device())
-            ok = 1.0
-        except Exception as e:  # noqa: BLE001 - fall back to the process group everywhere
-            import logging
+        from .. import ops
 
-            logging.getLogger("ewdml").warning(f"RCCL communicator unavailable ({e!r}); "
-                                               "collectives stay on the process group")
-            h, ok = None, 0.0
+        log = logging.getLogger("ewdml")
+        # every rank issues the same process-group collectives whatever fails where: rank 0
+        # always broadcasts (the unique id, or None after a local failure) and everyone skips
+        # ncclCommInitRank on None, then all agree on the outcome
+        uid = None
+        if self.rank == 0:
+            try:
+                uid = ops.require().rccl_unique_id()
+            except Exception as e:  # noqa: BLE001 - fall back to the process group everywhere
+                log.warning(f"RCCL unique id unavailable ({e!r})")
+        uid = self.broadcast_object(uid, src=0)
+        h, ok = None, 0.0
+        if uid is not None:
+            try:
+                h = ops.require().rccl_init(uid, self.world, self.rank,
+                                            torch.cuda.current_device())
+                ok = 1.0
+            except Exception as e:  # noqa: BLE001
+                log.warning(f"RCCL communicator init failed ({e!r})")
         if self.all_reduce_scalars([ok], op="min")[0] < 1.0:
             if h is not None:
                 ops.require().rccl_destroy(h)
+            log.warning("RCCL communicator unavailable: collectives stay on the process group")
             return None
         return h
 

@@ -154,9 +154,10 @@ class GradientExchange:
         """Encode bucket ``bi`` on the side stream and (unless deferred) issue its collective."""
         self._launched[bi] = True
         if self.cuda:  # a deferred Winograd weight-gradient output transform completes dw first
-            from ..ops.conv import flush_pending
+            from ..ops.conv import flush_pending, pending
 
             flush_pending()
+            assert not pending(), "deferred weight-gradient transform still pending at encode"
         with self._stream_ctx():
             self._encode(bi)
             if not self.defer_comm:

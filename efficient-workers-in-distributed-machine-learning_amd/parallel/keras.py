@@ -84,6 +84,13 @@ class MetricAverageCallback(Callback):
 
 
 class LearningRateWarmupCallback(Callback):
+    """Horovod's linear LR warm-up (``tensorflow_mnist.py:65-66``).  Horovod's momentum
+    correction (momentum *= new_lr / old_lr while the lr changes) exists because Keras SGD keeps
+    the lr inside its velocity (v = m v - lr g).  torch.optim.SGD applies the lr outside the
+    buffer (p -= lr * buf), so an lr change already rescales the whole history: there the
+    correction would double-scale momentum, and it is applied only to optimizers that declare
+    ``lr_in_velocity = True``."""
+
     def __init__(self, initial_lr: float, warmup_epochs: int = 5, momentum_correction: bool = True,
                  steps_per_epoch: Optional[int] = None, verbose: int = 0):
         self.initial_lr = float(initial_lr)
@@ -115,7 +122,8 @@ class LearningRateWarmupCallback(Callback):
         for g in opt.param_groups:
             old = g["lr"]
             g["lr"] = new_lr
-            if self.momentum_correction and g.get("momentum") and old > 0 and old != new_lr:
+            if (self.momentum_correction and getattr(opt, "lr_in_velocity", False)
+                    and g.get("momentum") and old > 0 and old != new_lr):
                 self._restore.append((g, g["momentum"]))
                 g["momentum"] = g["momentum"] * new_lr / old
 

@@ -70,7 +70,7 @@ def test_keras_example_two_ranks(tmp_path):
         assert torch.equal(p, v), k
 
 
-def _warmup_momentum(rank, world):
+def _warmup_momentum(rank, world, lr_in_velocity=False):
     from ewdml.parallel import horovod as hvd
     from ewdml.parallel import keras as hk
 
@@ -78,6 +78,8 @@ def _warmup_momentum(rank, world):
     torch.manual_seed(0)
     model = torch.nn.Linear(4, 2)
     opt = torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9)
+    if lr_in_velocity:  # a Keras-style optimizer (v = m v - lr g): Horovod's correction applies
+        opt.lr_in_velocity = True
     seen = []
 
     class Probe(hk.Callback):
@@ -93,14 +95,22 @@ def _warmup_momentum(rank, world):
     return {"seen": seen, "final": opt.param_groups[0]["lr"], "mom": opt.param_groups[0]["momentum"]}
 
 
-def test_lr_warmup_momentum_correction(tmp_path):
-    res = run_world(_warmup_momentum, 2, tmp_path)
+def _warmup_keras_style(rank, world):
+    return _warmup_momentum(rank, world, lr_in_velocity=True)
+
+
+@pytest.mark.parametrize("keras_style", [False, True])
+def test_lr_warmup_momentum_correction(tmp_path, keras_style):
+    """Momentum correction only for an optimizer whose lr sits inside the velocity (Keras SGD);
+    torch.optim.SGD (p -= lr * buf) gets the plain warm-up: an lr change already rescales it."""
+    res = run_world(_warmup_keras_style if keras_style else _warmup_momentum, 2, tmp_path)
     seen = res[0]["seen"]
     lrs = [0.4 / 2 * ((b + 1) / 4 * (2 - 1) / 1 + 1) for b in range(4)]
     old = [0.1] + lrs[:-1]
     for b in range(4):  # warm-up batches: lr and momentum * new / old for that batch only
         assert seen[b][0] == pytest.approx(lrs[b])
-        assert seen[b][1] == pytest.approx(0.9 * lrs[b] / old[b])
+        want = 0.9 * lrs[b] / old[b] if keras_style else 0.9
+        assert seen[b][1] == pytest.approx(want)
     for b in range(4, 8):  # after warm-up: initial_lr, momentum restored
         assert seen[b] == (pytest.approx(0.4), pytest.approx(0.9))
     assert res[0]["final"] == pytest.approx(0.4) and res[0]["mom"] == 0.9

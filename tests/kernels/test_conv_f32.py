@@ -278,7 +278,7 @@ WINO_SHAPES = [  # (N, C, Nc, H, W, m)
     (4, 128, 64, 8, 32, 4),      # H != W, 64 output channels
 ]
 # relative error bound vs float64 by tile: m = 4's transforms (coefficients up to 8 and 1/24)
-# cost ~10x the rounding of m = 2 (tools/conv_f32_probe.py --err; still ~100x below tf32)
+# cost ~10x the rounding of m = 2 (tools/probes/conv_f32_probe.py --err; still ~100x below tf32)
 WINO_TOL = {2: TOL, 4: 2e-5}
 
 
@@ -541,6 +541,7 @@ def test_winograd_deferred_wgrad_output_transform(m):
     x.requires_grad_(True)
     dy = torch.randn(N, chans[-1], H, H, device="cuda").contiguous(
         memory_format=torch.channels_last)
+    handles = _opt_in(ws)
 
     def run(defer, passes=1):
         conv._DEFER_WOUT = defer
@@ -587,3 +588,57 @@ def test_winograd_deferred_wgrad_output_transform(m):
     finally:
         conv._DEFER_WOUT = True
         conv._POISON_DW = False
+        _opt_out(ws, handles)
+
+
+def _opt_in(ws):
+    """Mark parameters the way parallel/engine.py does (a post-accumulate hook it owns, counted
+    in _ew_engine_hooks): only those defer their weight-gradient output transform."""
+    hs = []
+    for w in ws:
+        hs.append(w.register_post_accumulate_grad_hook(lambda p: None))
+        w._ew_engine_hooks = 1
+    return hs
+
+
+def _opt_out(ws, hs):
+    for w, h in zip(ws, hs):
+        h.remove()
+        w._ew_engine_hooks = 0
+
+
+@pytest.mark.parametrize("opt_in", [False, True])
+def test_winograd_autograd_grad_matches_fp64(opt_in):
+    """torch.autograd.grad never installs .grad: a deferred transform must still land in the dw
+    tensor it returns (the job writes dw's own memory at the end-of-backward callback), and a
+    foreign post-accumulate hook disables deferral."""
+    conv = _conv(True, 64, "2")
+    torch.manual_seed(3)
+    N, H, C, Nc = 16, 8, 128, 128
+    x, w0 = _data(N, C, Nc, H, H, seed=4)
+    ws = [torch.nn.Parameter(w0.clone())]
+    hs = _opt_in(ws) if opt_in else []
+    g = torch.Generator(device="cuda").manual_seed(9)
+    dy = torch.randn(N, Nc, H, H, device="cuda", generator=g).contiguous(
+        memory_format=torch.channels_last)
+    try:
+        conv._POISON_DW = True
+        xa = x.clone().requires_grad_(True)
+        y = conv.conv(xa, ws[0])
+        gx, gw = torch.autograd.grad(y, [xa, ws[0]], dy)
+        assert conv._PENDING is None
+        torch.cuda.synchronize()
+        _, rx, rw = _ref64(x, w0, 3, dy)
+        assert not torch.isnan(gw).any()
+        assert _rel(gw, rw) < TOL and _rel(gx, rx) < TOL
+        assert ws[0].grad is None
+        # a foreign hook on an opted-in parameter: no deferral, .backward() still exact
+        extra = ws[0].register_post_accumulate_grad_hook(lambda p: None)
+        y = conv.conv(x, ws[0])
+        y.backward(dy)
+        extra.remove()
+        torch.cuda.synchronize()
+        assert _rel(ws[0].grad, rw) < TOL
+    finally:
+        conv._POISON_DW = False
+        _opt_out(ws, hs)

@@ -1,7 +1,7 @@
 """Time the fp32 MFMA conv kernels per VGG-11 layer shape (forward, backward-data, weight
 gradient) with HIP events; prints us and TF/s per direction.
 
-    python tools/conv_f32_probe.py [--batch 128] [--reps 20] [--shapes vgg|big] [--wino]
+    python tools/probes/conv_f32_probe.py [--batch 128] [--reps 20] [--shapes vgg|big] [--wino]
 --wino adds the Winograd F(2x2, 3x3) forward (weight + input transforms, 16 GEMMs, output
 transform: "wfwd"), backward data ("wbwd") and weight gradient ("wwgrad") on the same shapes (TF/s counted at direct FLOPs).
 EWDML_CF_PLAN="bm,bn,split" forces a launch plan (ops/csrc/conv_f32.hip cf_plan).
@@ -10,7 +10,7 @@ import argparse
 import os
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 import torch
 

@@ -36,7 +36,7 @@ def hip_times(x, w, dy):
     """(fwd, bwd_data, wgrad) us of the MFMA kernels (ops/conv.py), None if unsupported."""
     import os
     import sys
-    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
     from ewdml import ops
     from ewdml.ops import conv
 

@@ -5,7 +5,7 @@ workgroups) once on a single stream and once forked over two streams (event fork
 both and prints the per-replay times.  If the two-stream graph is not faster, the runtime
 serialises graph branches and side-stream overlap inside the step graph buys nothing.
 
-    python tools/graph_branch_probe.py
+    python tools/probes/graph_branch_probe.py
 """
 import torch
 

@@ -4,7 +4,7 @@
 // Variants (argv[1]): 0 = MFMAs only (operands in registers), 1 = + LDS fragment reads,
 // 2 = + a barrier per step, 3 = + 4 ds_write_b128 per thread per step before the barrier (the
 // real loop minus global loads).  Prints TF/s per variant; the fp32 MFMA peak is ~157 TF/s.
-//   hipcc -O3 --offload-arch=gfx950 -o /tmp/mfma_loop_probe tools/mfma_loop_probe.hip
+//   hipcc -O3 --offload-arch=gfx950 -o /tmp/mfma_loop_probe tools/probes/mfma_loop_probe.hip
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
