@@ -137,6 +137,8 @@ def measure(a, world, amp, ef):
     sync()
     elapsed_max = tr.comm.all_reduce_scalars([t1 - t0], op="max")[0]
     final_loss = float(loss.detach()) if loss is not None else float("nan")
+    tr.comm_kind = tr.comm.kind
+    tr.close()  # watchdog and own RCCL communicator (the next measure() builds its own)
     return elapsed_max, tr, final_loss, t_enq - t0
 
 
@@ -186,7 +188,7 @@ def main(argv=None):
                    "bf16_params": tr.flat.shadow is not None,
                    "grad_mode": "views" if tr.flat.attach_grads else "pointers",
                    "layout": "nhwc" if tr.channels_last else "nchw",
-                   "fused_nn": a.fused_nn, "comm": tr.comm.kind},
+                   "fused_nn": a.fused_nn, "comm": tr.comm_kind},
         # overlap that actually happens: more than one bucket (the first collective is issued
         # while backward still runs) and a collective to hide (world > 1)
         "overlap_effective": bool(nb > 1 and not a.no_overlap and world > 1),

@@ -23,7 +23,7 @@ KINDS = ("none", "fp16", "bf16", "qsgd", "topk", "topk_qsgd")
 
 class Codec:
     def __init__(self, kind: str = "topk_qsgd", ratio: float = 0.01, levels: int = 127,
-                 bits: int = 8, norm: str = "max", seed: int = 0):
+                 bits: int = 8, norm: str = "max", seed: int = 0, dense_below: int = 0):
         if kind not in KINDS:
             raise ValueError(f"unknown codec {kind!r}; choose from {KINDS}")
         if bits not in (4, 8):
@@ -36,6 +36,7 @@ class Codec:
             raise ValueError("top-k ratio must be in (0, 1]")
         self.kind, self.ratio, self.levels, self.bits, self.norm = kind, ratio, levels, bits, norm
         self.seed = seed
+        self.dense_below = int(dense_below)
         self.plans = []
         self.layouts = []
         self.dplans = []
@@ -64,19 +65,43 @@ class Codec:
     def bind(self, plans, device):
         self.device = torch.device(device)
         self.plans = list(plans)
+        self._bound = {}  # ratio -> (plans, layouts, device plans): see set_ratio
         if self.allreduce:
             self.layouts = [None] * len(self.plans)
             return self
         lk = "qsgd" if self.kind == "qsgd" else self.kind
         if self.kind in ("topk", "topk_qsgd"):
             # the plans carry k; rebuild with this codec's ratio if needed
-            self.plans = [p if p.ratio == self.ratio else BucketPlan(
-                p.numels, p.offsets, self.ratio, p.bucket_offset, p.length) for p in self.plans]
+            self.plans = [p if (p.ratio == self.ratio and p.dense_below == self.dense_below)
+                          else BucketPlan(p.numels, p.offsets, self.ratio, p.bucket_offset,
+                                          p.length, self.dense_below) for p in self.plans]
         self.layouts = [Layout.build(lk, p, self.bits) for p in self.plans]
         if self.device.type == "cuda":
             if ops.hip_required():
                 ops.require()
             self.dplans = [ops.DevicePlan(p, self.device) for p in self.plans]
+        self._bound[self.ratio] = (self.plans, self.layouts, self.dplans)
+        return self
+
+    def set_ratio(self, ratio: float):
+        """Switch a bound top-k codec to another density (top-k warm-up): the per-tensor k, the
+        payload layouts and the device tables change; bindings are cached per ratio."""
+        if self.kind not in ("topk", "topk_qsgd"):
+            raise ValueError("only top-k codecs have a density")
+        if not 0.0 < ratio <= 1.0:
+            raise ValueError("top-k ratio must be in (0, 1]")
+        if ratio == self.ratio:
+            return self
+        hit = self._bound.get(ratio)
+        if hit is None:
+            plans = [BucketPlan(p.numels, p.offsets, ratio, p.bucket_offset, p.length,
+                                self.dense_below) for p in self.plans]
+            layouts = [Layout.build(self.kind, p, self.bits) for p in plans]
+            dplans = ([ops.DevicePlan(p, self.device) for p in plans]
+                      if self.device.type == "cuda" else [])
+            hit = self._bound[ratio] = (plans, layouts, dplans)
+        self.ratio = ratio
+        self.plans, self.layouts, self.dplans = hit
         return self
 
     def payload_bytes(self, b: int) -> int:
@@ -93,8 +118,11 @@ class Codec:
 
     # -- encode / decode ----------------------------------------------------------------------
     def encode(self, b: int, grad: torch.Tensor, payload: torch.Tensor, step: int, rank: int,
-               resid: torch.Tensor = None, key_tensor: torch.Tensor = None):
-        """Compress bucket ``b`` of the flat gradient (``grad`` = that bucket's view)."""
+               resid: torch.Tensor = None, key_tensor: torch.Tensor = None, dgc: dict = None):
+        """Compress bucket ``b`` of the flat gradient (``grad`` = that bucket's view).  ``dgc``:
+        error feedback with momentum correction (top-k codecs; ``oracle.dgc_accumulate``)."""
+        if dgc is not None and (resid is None or self.kind not in ("topk", "topk_qsgd")):
+            raise ValueError("momentum correction needs a top-k codec and a residual")
         plan, lay = self.plans[b], self.layouts[b]
         key = self.key(step, rank)
         on_dev = (grad[0] if isinstance(grad, (list, tuple)) else grad).is_cuda
@@ -104,14 +132,14 @@ class Codec:
                                 resid, key_tensor)
             else:
                 ops.topk_encode(self.dplans[b], grad, payload, lay, self.levels, self.norm, key,
-                                resid, key_tensor)
+                                resid, key_tensor, dgc=dgc)
             return
         if isinstance(grad, (list, tuple)):
             raise TypeError("CPU encode takes the bucket's flat gradient view")
         if self.kind == "qsgd":
             out = oracle.encode_qsgd(grad, plan, lay, self.levels, self.norm, key, resid)
         else:
-            out = oracle.encode_topk(grad, plan, lay, self.levels, self.norm, key, resid)
+            out = oracle.encode_topk(grad, plan, lay, self.levels, self.norm, key, resid, dgc)
         payload[:lay.nbytes].copy_(out)
 
     def decode(self, b: int, recv: torch.Tensor, out: torch.Tensor, scale: float):
@@ -127,7 +155,11 @@ class Codec:
                          mom: torch.Tensor, hp: dict, first: bool, grad_out=None, shadow=None,
                          key_state=None, rank: int = 0):
         """Fused decode -> average -> SGD step of bucket ``b`` (one kernel on the GPU).
-        ``key_state`` (device int32 {step, key}): also advance the RNG key to the next step."""
+        ``key_state`` (device int32 {step, key}): also advance the RNG key to the next step.
+        ``mom`` may be None with ``hp["momentum"] == 0`` (momentum-corrected error feedback: the
+        momentum ran on the sender, the update is p -= lr * mean)."""
+        if mom is None and hp["momentum"] != 0:
+            raise ValueError("a momentum step needs the momentum buffer")
         plan, lay = self.plans[b], self.layouts[b]
         if recv.is_cuda:
             fn = ops.qsgd_decode_apply if self.kind == "qsgd" else ops.topk_decode_apply
@@ -141,7 +173,8 @@ class Codec:
         if grad_out is not None:
             grad_out[:plan.length].copy_(g)
         for off, n in zip(plan.offsets, plan.numels):
-            oracle.sgd_apply(param[off:off + n], mom[off:off + n], g[off:off + n], hp["lr"],
+            oracle.sgd_apply(param[off:off + n], None if mom is None else mom[off:off + n],
+                             g[off:off + n], hp["lr"],
                              hp["momentum"], hp["dampening"], hp["weight_decay"],
                              hp["nesterov"], first)
 

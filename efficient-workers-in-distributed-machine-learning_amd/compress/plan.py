@@ -38,6 +38,9 @@ class BucketPlan:
     ratio: float = 1.0
     bucket_offset: int = 0  # element offset of the bucket inside the flat buffer
     length: int = 0  # bucket length in elements (>= last offset + numel; includes align pad)
+    # tensors of at most this many elements are sent whole (k = numel): BatchNorm scales/shifts
+    # and biases, whose sparsified updates would otherwise arrive once per ~1/ratio steps
+    dense_below: int = 0
     ks: List[int] = field(default_factory=list)
     chunk_tensor: List[int] = field(default_factory=list)
     chunk_start: List[int] = field(default_factory=list)  # relative to bucket start
@@ -51,7 +54,8 @@ class BucketPlan:
         assert len(self.numels) == len(self.offsets) and self.numels
         if not self.length:
             self.length = self.offsets[-1] + self.numels[-1]
-        self.ks = [max(1, int(n * self.ratio)) for n in self.numels]
+        self.ks = [n if n <= self.dense_below else max(1, int(n * self.ratio))
+                   for n in self.numels]
         e = c = 0
         for t, (n, off) in enumerate(zip(self.numels, self.offsets)):
             nch = (n + CHUNK - 1) // CHUNK

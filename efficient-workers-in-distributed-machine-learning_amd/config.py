@@ -56,6 +56,7 @@ class Config:
     method: Optional[int] = None
     compress: str = "topk_qsgd"  # none | fp16 | bf16 | qsgd | topk | topk_qsgd
     topk_ratio: float = 0.01
+    topk_dense_below: int = 0  # tensors of <= N elements go whole (k = numel) through top-k codecs
     qsgd_levels: int = 127
     qsgd_bits: int = 8
     qsgd_norm: str = "max"  # max | l2 (the reference's L2 norm)
@@ -67,6 +68,14 @@ class Config:
     sync_mode: str = "grad"  # grad: compressed gradient on sync steps | model: compressed delta
     select_best: bool = False  # method 6: adopt the weights of the best-accuracy rank at sync
     error_feedback: bool = False
+    # dgc: momentum correction + momentum factor masking (the sender runs the momentum before
+    # top-k; oracle.dgc_accumulate) | plain: residual of the raw gradient, momentum after decode
+    ef_mode: str = "dgc"
+    # top-k density warm-up (DGC's "exponentially decreasing sparsity"): comma-separated ratios
+    # used in turn over the first --topk-warmup-epochs epochs, then --topk-ratio (e.g. "0.25,0.0625,
+    # 0.015625"); each change re-plans the payloads (and re-captures a HIP graph)
+    topk_warmup: str = ""
+    topk_warmup_epochs: float = 1.0
     bucket_mb: float = 16.0
     overlap: bool = True
     predivide: float = 1.0  # Horovod gradient_predivide_factor
@@ -178,6 +187,7 @@ def build_parser(prog="distributed_nn.py") -> argparse.ArgumentParser:
     a("--compress", type=str, default=d.compress,
       choices=["none", "fp16", "bf16", "qsgd", "topk", "topk_qsgd"])
     a("--topk-ratio", type=float, default=d.topk_ratio)
+    a("--topk-dense-below", type=int, default=d.topk_dense_below)
     a("--qsgd-levels", type=int, default=d.qsgd_levels)
     a("--qsgd-bits", type=int, default=d.qsgd_bits, choices=[4, 8])
     a("--qsgd-norm", type=str, default=d.qsgd_norm, choices=["max", "l2"])
@@ -189,6 +199,9 @@ def build_parser(prog="distributed_nn.py") -> argparse.ArgumentParser:
     a("--sync-mode", type=str, default=d.sync_mode, choices=["grad", "model"])
     a("--select-best", action="store_true", default=False)
     a("--error-feedback", action="store_true", default=False)
+    a("--ef-mode", type=str, default=d.ef_mode, choices=["dgc", "plain"])
+    a("--topk-warmup", type=str, default=d.topk_warmup)
+    a("--topk-warmup-epochs", type=float, default=d.topk_warmup_epochs)
     a("--bucket-mb", type=float, default=d.bucket_mb)
     a("--no-overlap", dest="overlap", action="store_false", default=True)
     a("--predivide", type=float, default=d.predivide)

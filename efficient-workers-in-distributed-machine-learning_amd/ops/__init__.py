@@ -162,7 +162,9 @@ def _keyp(key_tensor):
 
 
 def topk_encode(dp: DevicePlan, grad, payload, layout, levels: int, norm: str, key: int,
-                resid=None, key_tensor=None):
+                resid=None, key_tensor=None, dgc=None):
+    """``dgc``: momentum-corrected error feedback, ``{velocity, momentum, dampening, nesterov,
+    weight_decay, param}`` (bucket views; compress/oracle.py dgc_accumulate)."""
     C = require()
     ptrs, mask = grad_pointers(dp, grad)
     _check(payload, torch.uint8, "payload")
@@ -178,11 +180,26 @@ def topk_encode(dp: DevicePlan, grad, payload, layout, levels: int, norm: str, k
         vk = VK_Q4
     if vk != VK_F32 and not (1 <= levels <= (127 if layout.bits == 8 else 7)):
         raise ValueError(f"levels={levels} does not fit {layout.bits}-bit codes")
+    vel = par = None
+    mom = damp1 = wd = 0.0
+    nest = 0
+    if dgc is not None:
+        if resid is None:
+            raise ValueError("momentum correction needs the residual")
+        vel, mom = dgc["velocity"], float(dgc["momentum"])
+        _check_bucket(dp, vel, "velocity")
+        damp1 = float(1.0 - dgc.get("dampening", 0.0))
+        wd = float(dgc.get("weight_decay", 0.0))
+        nest = int(bool(dgc.get("nesterov", False)))
+        if wd != 0.0:
+            par = dgc["param"]
+            _check_bucket(dp, par, "param")
     C.topk_encode(ptrs, mask, _ptr(resid), _ptr(dp.chunks), _ptr(dp.tensors), _ptr(dp.scratch),
                   _ptr(payload), layout.nbytes, dp.plan.num_tensors, dp.plan.num_chunks,
                   layout.scales, layout.counts, layout.idx, layout.codes, vk,
                   1 if norm == "l2" else 0, float(levels), float(1.0 / levels), key & 0xFFFFFFFF,
-                  dp.plan.bucket_offset & 0xFFFFFFFF, _keyp(key_tensor), _stream())
+                  dp.plan.bucket_offset & 0xFFFFFFFF, _keyp(key_tensor), _stream(), _ptr(vel),
+                  _ptr(par), mom, damp1, wd, nest)
 
 
 def topk_decode_apply(dp: DevicePlan, recv, layout, levels: int, param=None, mom=None,
@@ -198,7 +215,10 @@ def topk_decode_apply(dp: DevicePlan, recv, layout, levels: int, param=None, mom
     apply = param is not None
     if apply:
         _check_bucket(dp, param, "param")
-        _check_bucket(dp, mom, "mom")
+        if mom is not None:
+            _check_bucket(dp, mom, "mom")
+        elif momentum != 0.0 or nesterov:
+            raise ValueError("a momentum step needs the momentum buffer")
     if grad_out is not None:
         _check_bucket(dp, grad_out, "grad_out")
     if not apply and grad_out is None:

@@ -26,8 +26,16 @@ PYBIND11_MODULE(_C, m) {
            uintptr_t tensors, uintptr_t scratch, uintptr_t payload, long long payload_bytes,
            int T, int C, int scales_off, int counts_off, int idx_off, int codes_off,
            int value_kind, int norm_l2, float levels, float inv_levels, uint32_t key,
-           uint32_t bucket_offset, uintptr_t key_ptr, uintptr_t stream) {
+           uint32_t bucket_offset, uintptr_t key_ptr, uintptr_t stream, uintptr_t vel,
+           uintptr_t param, float dgc_momentum, float dgc_damp1, float dgc_wd,
+           int dgc_nesterov) {
           TopkEncodeArgs a{};
+          a.vel = vel;
+          a.param = param;
+          a.dgc_momentum = dgc_momentum;
+          a.dgc_damp1 = dgc_damp1;
+          a.dgc_wd = dgc_wd;
+          a.dgc_nesterov = dgc_nesterov;
           a.grad_ptrs = grads.data();
           a.n_grad_ptrs = (int)grads.size();
           a.bf16_mask = mask.data();
@@ -271,6 +279,16 @@ PYBIND11_MODULE(_C, m) {
     return ew_rccl_init(std::string(uid), nranks, rank, device);
   });
   m.def("rccl_destroy", &ew_rccl_destroy);
+  m.def("rccl_abort", &ew_rccl_abort);
+  m.def("rccl_watchdog_start", &ew_rccl_watchdog_start);
+  m.def("rccl_watch", &ew_rccl_watch);
+  m.def("rccl_watch_pending", &ew_rccl_watch_pending);
+  m.def("rccl_watchdog_stop", &ew_rccl_watchdog_stop,
+        pybind11::call_guard<pybind11::gil_scoped_release>());
+  m.def("test_flag_alloc", &ew_test_flag_alloc);
+  m.def("test_flag_free", &ew_test_flag_free);
+  m.def("watchdog_release_flag", &ew_watchdog_release_flag);
+  m.def("test_spin", &ew_test_spin);
   m.def("rccl_all_gather", &ew_rccl_all_gather);
   m.def("rccl_all_reduce", &ew_rccl_all_reduce);
   m.def("rccl_reduce_scatter", &ew_rccl_reduce_scatter);

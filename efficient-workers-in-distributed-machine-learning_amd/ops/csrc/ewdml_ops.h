@@ -19,6 +19,11 @@ struct TopkEncodeArgs {
   float levels, inv_levels;
   uint32_t key, bucket_offset;
   uintptr_t key_ptr;  // optional device uint32 overriding `key` (graph replay)
+  // error feedback with momentum correction (DGC; compress/oracle.py dgc_accumulate): per-rank
+  // velocity (0: plain error feedback) and the bucket's fp32 parameters (read when dgc_wd != 0)
+  uintptr_t vel, param;
+  float dgc_momentum, dgc_damp1, dgc_wd;  // damp1 = 1 - dampening
+  int dgc_nesterov;
 };
 
 struct TopkDecodeArgs {
@@ -259,6 +264,15 @@ std::string ew_rccl_unique_id();
 int ew_rccl_version();
 uintptr_t ew_rccl_init(const std::string& uid, int nranks, int rank, int device);
 void ew_rccl_destroy(uintptr_t h);
+void ew_rccl_abort(uintptr_t h);
+uintptr_t ew_rccl_watchdog_start(uintptr_t comm, int device, double timeout_s, int exit_code);
+void ew_rccl_watch(uintptr_t wd, uintptr_t stream);
+int ew_rccl_watch_pending(uintptr_t wd);
+void ew_rccl_watchdog_stop(uintptr_t wd);
+uintptr_t ew_test_flag_alloc();
+void ew_test_flag_free(uintptr_t f);
+void ew_watchdog_release_flag(uintptr_t wd, uintptr_t f);
+void ew_test_spin(uintptr_t flag, double max_s, uintptr_t stream);
 void ew_rccl_all_gather(uintptr_t h, uintptr_t send, uintptr_t recv, long long count, int dtype,
                         uintptr_t stream);
 void ew_rccl_all_reduce(uintptr_t h, uintptr_t send, uintptr_t recv, long long count, int dtype,

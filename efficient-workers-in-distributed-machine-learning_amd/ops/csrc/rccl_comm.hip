@@ -14,9 +14,16 @@
 #include <dlfcn.h>
 #include <rccl/rccl.h>
 
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "common.h"
@@ -194,4 +201,158 @@ void ew_rccl_all_to_all(uintptr_t h, uintptr_t send, uintptr_t recv, long long c
              "ncclRecv");
   }
   rc_check(a.group_end(), "ncclGroupEnd");
+}
+
+void ew_rccl_abort(uintptr_t h) {
+  if (h) rc_check(rc_api().abort(rc_comm(h)), "ncclCommAbort");
+}
+
+// ---------------------------------------------------------------------------------------------
+// Step watchdog.  The data-plane collectives run on the step's own stream (no process-group
+// watchdog sees them), so a stalled peer would hang the surviving ranks inside a graph replay or a
+// synchronize.  After each step the host records an event on the step stream (ew_rccl_watch); a
+// thread polls the oldest outstanding event and, once one has been pending for longer than the
+// timeout, aborts the communicator (RCCL kernels waiting on a peer return), releases the test
+// spin flags, waits a bounded moment for the stream to drain, and ends the process with a non-zero
+// exit code.  No exec, no retry: the launcher sees the failure (the reference's
+// straggler kill intent, src/distributed_nn.py:50-59, src/model_ops/lenet.py:188-255).
+// ---------------------------------------------------------------------------------------------
+namespace {
+
+struct Watchdog {
+  ncclComm_t comm = nullptr;
+  int device = 0;
+  double timeout_s = 600.0;
+  int exit_code = 3;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<std::pair<hipEvent_t, std::chrono::steady_clock::time_point>> pending;
+  std::vector<hipEvent_t> pool;
+  std::vector<volatile int*> release;  // host flags set to 1 on abort (test spin kernels)
+  bool stop = false;
+  std::thread th;
+
+  void fire(const char* why, double waited) {
+    std::fprintf(stderr,
+                 "ewdml watchdog: %s after %.1f s (timeout %.1f s); aborting the RCCL "
+                 "communicator and exiting with code %d\n",
+                 why, waited, timeout_s, exit_code);
+    std::fflush(stderr);
+    if (comm) rc_api().abort(comm);
+    for (volatile int* f : release) *f = 1;
+    // let the stream drain (aborted collectives and released kernels return), at most 5 s
+    hipEvent_t ev = pending.empty() ? nullptr : pending.front().first;
+    const auto t0 = std::chrono::steady_clock::now();
+    while (ev && hipEventQuery(ev) == hipErrorNotReady &&
+           std::chrono::steady_clock::now() - t0 < std::chrono::seconds(5))
+      std::this_thread::sleep_for(std::chrono::milliseconds(20));
+    std::_Exit(exit_code);
+  }
+
+  void loop() {
+    (void)hipSetDevice(device);
+    std::unique_lock<std::mutex> lk(mu);
+    while (!stop) {
+      cv.wait_for(lk, std::chrono::milliseconds(50));
+      while (!pending.empty()) {
+        auto& fr = pending.front();
+        const hipError_t q = hipEventQuery(fr.first);
+        const double waited =
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - fr.second).count();
+        if (q == hipSuccess) {
+          pool.push_back(fr.first);
+          pending.pop_front();
+          continue;
+        }
+        if (q != hipErrorNotReady) fire(hipGetErrorString(q), waited);
+        if (waited > timeout_s) fire("a step's collectives did not complete", waited);
+        break;
+      }
+    }
+  }
+};
+
+Watchdog* wd_of(uintptr_t h) {
+  if (!h) throw std::runtime_error("ewdml watchdog: null handle");
+  return reinterpret_cast<Watchdog*>(h);
+}
+
+__global__ void k_test_spin(const int* flag, unsigned long long max_ticks) {
+  // test-only stall: waits for a host-pinned flag, bounded by max_ticks of the 100 MHz constant
+  // clock so the grid always drains on its own
+  const unsigned long long t0 = wall_clock64();
+  while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0 &&
+         wall_clock64() - t0 < max_ticks)
+    __builtin_amdgcn_s_sleep(64);
+}
+
+}  // namespace
+
+uintptr_t ew_rccl_watchdog_start(uintptr_t comm, int device, double timeout_s, int exit_code) {
+  auto* w = new Watchdog();
+  w->comm = comm ? rc_comm(comm) : nullptr;
+  if (comm) rc_api();  // resolve ncclCommAbort now, not inside fire()
+  w->device = device;
+  w->timeout_s = timeout_s;
+  w->exit_code = exit_code;
+  w->th = std::thread([w] { w->loop(); });
+  return reinterpret_cast<uintptr_t>(w);
+}
+
+void ew_rccl_watch(uintptr_t h, uintptr_t stream) {
+  Watchdog* w = wd_of(h);
+  hipEvent_t ev;
+  {
+    std::lock_guard<std::mutex> lk(w->mu);
+    if (w->pool.empty()) {
+      EW_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    } else {
+      ev = w->pool.back();
+      w->pool.pop_back();
+    }
+  }
+  EW_CHECK(hipEventRecord(ev, (hipStream_t)stream));
+  std::lock_guard<std::mutex> lk(w->mu);
+  w->pending.emplace_back(ev, std::chrono::steady_clock::now());
+}
+
+int ew_rccl_watch_pending(uintptr_t h) {
+  Watchdog* w = wd_of(h);
+  std::lock_guard<std::mutex> lk(w->mu);
+  return (int)w->pending.size();
+}
+
+void ew_rccl_watchdog_stop(uintptr_t h) {
+  Watchdog* w = wd_of(h);
+  {
+    std::lock_guard<std::mutex> lk(w->mu);
+    w->stop = true;
+  }
+  w->cv.notify_all();
+  if (w->th.joinable()) w->th.join();
+  for (auto& p : w->pending) (void)hipEventDestroy(p.first);
+  for (hipEvent_t e : w->pool) (void)hipEventDestroy(e);
+  delete w;
+}
+
+// test hooks: a host-pinned flag released by the watchdog on abort, and a kernel stalling a
+// stream on it (bounded)
+uintptr_t ew_test_flag_alloc() {
+  void* p = nullptr;
+  EW_CHECK(hipHostMalloc(&p, 64, hipHostMallocCoherent));
+  std::memset(p, 0, 64);
+  return reinterpret_cast<uintptr_t>(p);
+}
+void ew_test_flag_free(uintptr_t f) {
+  if (f) EW_CHECK(hipHostFree(reinterpret_cast<void*>(f)));
+}
+void ew_watchdog_release_flag(uintptr_t h, uintptr_t f) {
+  Watchdog* w = wd_of(h);
+  std::lock_guard<std::mutex> lk(w->mu);
+  w->release.push_back(reinterpret_cast<volatile int*>(f));
+}
+void ew_test_spin(uintptr_t flag, double max_s, uintptr_t stream) {
+  hipLaunchKernelGGL(k_test_spin, dim3(1), dim3(64), 0, (hipStream_t)stream,
+                     reinterpret_cast<const int*>(flag), (unsigned long long)(max_s * 1e8));
+  EW_CHECK_LAUNCH();
 }

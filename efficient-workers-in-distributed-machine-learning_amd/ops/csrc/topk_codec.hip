@@ -65,9 +65,21 @@ __device__ __forceinline__ void topk_select(const uint32_t* __restrict__ hist,
                                             uint32_t* __restrict__ state,
                                             const uint32_t* __restrict__ kmaxr, int T, int t);
 
+// Momentum-corrected error feedback (DGC): velocity, parameters (weight decay) and hyper-
+// parameters, by value.
+struct DgcArgs {
+  float* vel;
+  const float* param;
+  float momentum, damp1, wd;
+  int nesterov;
+};
+
+// error-feedback mode of the encode: none, plain (e = g + r), momentum-corrected (DGC)
+enum EfMode { EF_NONE = 0, EF_PLAIN = 1, EF_DGC = 2 };
+
 // state[t] = {prefix, k_rem, max_key, pad}
-template <bool EF>
-__global__ __launch_bounds__(EW_BLOCK) void k_topk_hist0(GradPtrs gp,
+template <int EFM>
+__global__ __launch_bounds__(EW_BLOCK) void k_topk_hist0(GradPtrs gp, DgcArgs dg,
                                                          float* __restrict__ resid,
                                                          const ChunkRow* __restrict__ chunks,
                                                          uint32_t* __restrict__ hist,
@@ -86,12 +98,44 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_hist0(GradPtrs gp,
   const ChunkRow c = chunks[blockIdx.x];
   float4 v[EW_CU];
   ew_ld_chunk(gp, nullptr, c, v);
-  if (EF) {  // error feedback: compress e = g + residual, staged in the residual buffer
+  if (EFM == EF_PLAIN) {  // error feedback: compress e = g + residual, staged in the residual
     float4 r[EW_CU];
     ew_ld_chunk(gp, resid, c, r);
 #pragma unroll
     for (int u = 0; u < EW_CU; ++u)
       v[u] = make_float4(v[u].x + r[u].x, v[u].y + r[u].y, v[u].z + r[u].z, v[u].w + r[u].w);
+    ew_st_chunk(resid + c.start, c.len, v);
+  } else if (EFM == EF_DGC) {
+    // momentum correction (oracle.dgc_accumulate, every product / sum rounded on its own):
+    // g' = g + wd p ; u = m u + (1 - d) g' ; d = g' + m u (Nesterov) | u ; e = r + d
+    float4 r[EW_CU], uv[EW_CU], pv[EW_CU];
+    ew_ld_chunk(gp, resid, c, r);
+    ew_ld_chunk(gp, dg.vel, c, uv);
+    if (dg.wd != 0.0f) ew_ld_chunk(gp, dg.param, c, pv);  // uniform branch
+#pragma unroll
+    for (int u = 0; u < EW_CU; ++u) {
+      float g4[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+      float u4[4] = {uv[u].x, uv[u].y, uv[u].z, uv[u].w};
+      const float r4[4] = {r[u].x, r[u].y, r[u].z, r[u].w};
+      float e4[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float g = g4[j];
+        if (dg.wd != 0.0f) g = g + ew_f4(pv[u], j) * dg.wd;
+        const float a = u4[j] * dg.momentum;
+        const float b = g * dg.damp1;
+        u4[j] = a + b;
+        float d = u4[j];
+        if (dg.nesterov) {
+          const float mu = u4[j] * dg.momentum;
+          d = g + mu;
+        }
+        e4[j] = r4[j] + d;
+      }
+      uv[u] = make_float4(u4[0], u4[1], u4[2], u4[3]);
+      v[u] = make_float4(e4[0], e4[1], e4[2], e4[3]);
+    }
+    ew_st_chunk(dg.vel + c.start, c.len, uv);
     ew_st_chunk(resid + c.start, c.len, v);
   }
   uint32_t kmax = 0;
@@ -324,7 +368,8 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_write(
     const uint32_t* __restrict__ chunk_off, const uint32_t* __restrict__ chunk_ties,
     const float* __restrict__ inv_arr, uint8_t* __restrict__ payload, int scales_off, int idx_off,
     int codes_off, float levels, float inv_levels, uint32_t key_arg, const uint32_t* __restrict__ keyp,
-    uint32_t bucket_offset, uint32_t* __restrict__ rezero, uint32_t rezero_words) {
+    uint32_t bucket_offset, uint32_t* __restrict__ rezero, uint32_t rezero_words,
+    float* __restrict__ vel) {
   __shared__ uint32_t ws[EW_WAVES];
   // the histograms / max-key replicas are dead once the thresholds are selected: clear them here
   // for the next encode of this bucket (replaces a per-step memset node; first use: zero-alloc)
@@ -390,6 +435,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_write(
           }
           sent = (float)q * step;
         }
+        if (vel) vel[c.start + i0 + j] = 0.0f;  // DGC momentum factor masking: sent coordinates
         ++pos;
       }
       left[j] = xs[j] - sent;
@@ -425,18 +471,21 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_decode_apply(
   const ChunkRow c = chunks[blockIdx.x];
   const TensorRow tr = tensors[c.tensor];
   float* p = param + c.start;
-  float* b = mom + c.start;
+  float* b = mom ? mom + c.start : nullptr;
   // chunk starts are 64-element aligned: float4 body + scalar tail.  The body's parameters and
   // momenta are loaded here, before the scatter, so their latency hides behind it.
   const int n4 = c.len >> 2;
   float4 pv[EW_CU], bv[EW_CU];
+  // mom == nullptr: a step without momentum buffer (momentum-corrected error feedback ran the
+  // momentum on the sender; the host passes momentum = 0)
+  const bool has_mom = mom != nullptr;
   if (apply) {
 #pragma unroll
     for (int u = 0; u < EW_CU; ++u) {
       const int i = threadIdx.x + u * EW_BLOCK;
       if (i < n4) {
         pv[u] = reinterpret_cast<const float4*>(p)[i];
-        bv[u] = reinterpret_cast<const float4*>(b)[i];
+        bv[u] = has_mom ? reinterpret_cast<const float4*>(b)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
       }
     }
   }
@@ -496,7 +545,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_decode_apply(
       ew_sgd(pu.z, bu.z, gv.z, sa);
       ew_sgd(pu.w, bu.w, gv.w, sa);
       reinterpret_cast<float4*>(p)[i] = pu;
-      reinterpret_cast<float4*>(b)[i] = bu;
+      if (has_mom) reinterpret_cast<float4*>(b)[i] = bu;
       if (shadow) {  // bf16 compute copy of the updated master weights
         const float v4[4] = {pu.x, pu.y, pu.z, pu.w};
         ew_st4_bf16(shadow + c.start + 4 * i, 4, v4);
@@ -507,10 +556,10 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_decode_apply(
     const float gv = acc[i] * inv_n;
     if (go) go[i] = gv;
     if (apply) {
-      float pv = p[i], bv = b[i];
+      float pv = p[i], bv = has_mom ? b[i] : 0.0f;
       ew_sgd(pv, bv, gv, sa);
       p[i] = pv;
-      b[i] = bv;
+      if (has_mom) b[i] = bv;
       if (shadow) shadow[c.start + i] = ew_f2bf(pv);
     }
   }
@@ -558,10 +607,17 @@ void ew_topk_encode(const TopkEncodeArgs& a) {
   float* resid = reinterpret_cast<float*>(a.resid);
   const float* src_flat = resid;  // passes after hist0 read the staged e = g + r under EF
   // each pass's per-tensor step (select / scan) runs in the tensor's last-arriving chunk block
-  if (resid)
-    EW_LAUNCH(k_topk_hist0<true>, C, s, g, resid, chunks, hist0, kmaxr, T, tensors, state, tick);
+  DgcArgs dg{reinterpret_cast<float*>(a.vel), reinterpret_cast<const float*>(a.param),
+             a.dgc_momentum, a.dgc_damp1, a.dgc_wd, a.dgc_nesterov};
+  if (dg.vel && !resid) throw std::runtime_error("ewdml topk: momentum correction needs a residual");
+  if (dg.vel && dg.wd != 0.0f && !dg.param)
+    throw std::runtime_error("ewdml topk: weight decay in the momentum correction needs params");
+  if (dg.vel)
+    EW_LAUNCH(k_topk_hist0<EF_DGC>, C, s, g, dg, resid, chunks, hist0, kmaxr, T, tensors, state, tick);
+  else if (resid)
+    EW_LAUNCH(k_topk_hist0<EF_PLAIN>, C, s, g, dg, resid, chunks, hist0, kmaxr, T, tensors, state, tick);
   else
-    EW_LAUNCH(k_topk_hist0<false>, C, s, g, resid, chunks, hist0, kmaxr, T, tensors, state, tick);
+    EW_LAUNCH(k_topk_hist0<EF_NONE>, C, s, g, dg, resid, chunks, hist0, kmaxr, T, tensors, state, tick);
   EW_LAUNCH((k_topk_hist<10, 20>), C, s, g, src_flat, chunks, state, hist1, T, tensors, kmaxr,
             tick + TICK_STRIDE * T);
   EW_LAUNCH((k_topk_hist<0, 10>), C, s, g, src_flat, chunks, state, hist2, T, tensors, kmaxr,
@@ -573,7 +629,8 @@ void ew_topk_encode(const TopkEncodeArgs& a) {
 #define EW_WRITE(VK, EFV)                                                                          \
   EW_LAUNCH((k_topk_write<VK, EFV>), C, s, g, resid, chunks, tensors, state, chunk_off, chunk_ties, \
             inv, pay, a.scales_off, a.idx_off, a.codes_off, a.levels, a.inv_levels, a.key,         \
-            reinterpret_cast<const uint32_t*>(a.key_ptr), a.bucket_offset, kmaxr, rezero_words)
+            reinterpret_cast<const uint32_t*>(a.key_ptr), a.bucket_offset, kmaxr, rezero_words,   \
+            dg.vel)
   if (a.value_kind == VK_Q8) {
     if (resid) EW_WRITE(VK_Q8, true); else EW_WRITE(VK_Q8, false);
   } else if (a.value_kind == VK_Q4) {
@@ -594,6 +651,8 @@ size_t ew_topk_scratch_bytes(int T, int C) {
 void ew_topk_decode_apply(const TopkDecodeArgs& a) {
   auto* chunks = reinterpret_cast<const ChunkRow*>(a.chunks);
   auto* tensors = reinterpret_cast<const TensorRow*>(a.tensors);
+  if (a.apply && !a.mom && (a.momentum != 0.0f || a.nesterov))
+    throw std::runtime_error("ewdml topk decode: a momentum step needs the momentum buffer");
   SgdArgs sa{a.lr, a.momentum, a.dampening, a.weight_decay, a.grad_scale, a.nesterov, a.first,
              reinterpret_cast<uint32_t*>(a.key_state), a.key_seed, a.key_rank};
   auto* recv = reinterpret_cast<const uint8_t*>(a.recv);

@@ -57,6 +57,7 @@ class Comm:
         self._local = self.world == 1 and not (os.environ.get("EWDML_FORCE_PG") == "1"
                                                and self.backend != "local")
         self.rccl = None  # handle of the stream-ordered RCCL communicator (see module doc)
+        self.watchdog = None  # native step watchdog (arm_watchdog)
         if (self.backend == "nccl" and not self._local and group is None
                 and os.environ.get("EWDML_COMM", "rccl") != "pg"):
             self.rccl = self._make_rccl()
@@ -98,6 +99,46 @@ class Comm:
         from .. import ops
 
         return ops.require()
+
+    # -- failure detection on the data plane -------------------------------------
+    def arm_watchdog(self, timeout_s: float, exit_code: int = 3, force: bool = False):
+        """Start the native step watchdog (``ops/csrc/rccl_comm.hip``): after :meth:`watch`
+        records a step's completion event, a host thread aborts the RCCL communicator and ends the
+        process with ``exit_code`` if that event is still pending after ``timeout_s`` (a dead or
+        stalled peer).  Armed only when the own communicator carries the collectives (the
+        process group has its own watchdog) unless ``force``."""
+        if self.watchdog is not None or not timeout_s or timeout_s <= 0:
+            return self.watchdog
+        if self.rccl is None and not force:
+            return None
+        self.watchdog = self._rc().rccl_watchdog_start(self.rccl or 0,
+                                                       torch.cuda.current_device(),
+                                                       float(timeout_s), int(exit_code))
+        return self.watchdog
+
+    def watch(self):
+        """Record the current stream's position for the watchdog (call after a step's last
+        collective was enqueued; never inside a graph capture)."""
+        if self.watchdog is not None:
+            from ..ops import _stream
+
+            self._rc().rccl_watch(self.watchdog, _stream())
+
+    def abort(self):
+        """ncclCommAbort of the own communicator (peers blocked in a collective return)."""
+        if self.rccl is not None:
+            self._rc().rccl_abort(self.rccl)
+            self.rccl = None
+
+    def close(self):
+        """Stop the watchdog and destroy the own communicator (the process group stays)."""
+        if self.watchdog is not None:
+            self._rc().rccl_watchdog_stop(self.watchdog)
+            self.watchdog = None
+        if self.rccl is not None:
+            torch.cuda.synchronize()
+            self._rc().rccl_destroy(self.rccl)
+            self.rccl = None
 
     @staticmethod
     def _dt(t):
@@ -229,6 +270,8 @@ _RC_DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2, torch.uint8: 3,
 _RC_OP = {dist.ReduceOp.SUM: 0, dist.ReduceOp.MAX: 1, dist.ReduceOp.MIN: 2}
 
 
-def shutdown():
+def shutdown(comm: "Comm" = None):
+    if comm is not None:
+        comm.close()
     if dist.is_available() and dist.is_initialized():
         dist.destroy_process_group()

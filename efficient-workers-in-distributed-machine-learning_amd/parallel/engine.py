@@ -43,7 +43,7 @@ class GradientExchange:
 
     def __init__(self, flat, comm, codec, optimizer, overlap: bool = True,
                  error_feedback: bool = False, predivide: float = 1.0, seed_offset: int = 0,
-                 side_stream: bool = True):
+                 side_stream: bool = True, ef_mode: str = "dgc"):
         self.flat, self.comm, self.codec, self.opt = flat, comm, codec, optimizer
         self.device = flat.data.device
         self.cuda = self.device.type == "cuda"
@@ -60,15 +60,24 @@ class GradientExchange:
                 self.send.append(None if codec.wire_dtype == torch.float32 else torch.zeros(
                     b.length, dtype=codec.wire_dtype, device=self.device))
             else:
-                P = codec.payload_bytes(b.index)
-                recv = torch.zeros(self.N * P, dtype=torch.uint8, device=self.device)
-                # encode straight into this rank's slot of the gather buffer: an in-place
-                # all-gather (RCCL: sendbuff == recvbuff + rank * count), no local copy
-                r = comm.rank
-                self.payload.append(recv[r * P:(r + 1) * P])
-                self.recv.append(recv)
+                self.payload.append(None)
+                self.recv.append(None)
                 self.send.append(None)
+        if not codec.allreduce:
+            self._alloc_payloads()
         self.resid = torch.zeros_like(flat.grad) if (error_feedback and not codec.allreduce) else None
+        # error feedback with momentum correction (DGC, oracle.dgc_accumulate): the sender runs the
+        # momentum before top-k and keeps a per-rank velocity; the decode then steps without one.
+        # Only for top-k codecs under momentum SGD (dense QSGD's residual holds just the rounding
+        # error, and Adam has no velocity to correct): plain error feedback otherwise.
+        if ef_mode not in ("dgc", "plain"):
+            raise ValueError("ef_mode must be 'dgc' or 'plain'")
+        self.dgc = (self.resid is not None and ef_mode == "dgc"
+                    and codec.kind in ("topk", "topk_qsgd")
+                    and getattr(optimizer, "fusable", False)
+                    and getattr(optimizer, "momentum", 0.0) != 0.0)
+        self.ef_mode = None if self.resid is None else ("dgc" if self.dgc else "plain")
+        self.vel = torch.zeros_like(flat.grad) if self.dgc else None
         if not flat.attach_grads and not self.cuda:
             raise ValueError("pointer-mode gradients need the HIP kernels (device tensors)")
         self._pack_plans = [ops.DevicePlan(b.plan, self.device) for b in flat.buckets] \
@@ -101,6 +110,26 @@ class GradientExchange:
                 # ours flush deferred weight-gradient transforms before reading (ops/conv.py)
                 p._ew_engine_hooks = getattr(p, "_ew_engine_hooks", 0) + 1
         self.last = StepStats()
+
+    def _alloc_payloads(self):
+        for b in self.flat.buckets:
+            P = self.codec.payload_bytes(b.index)
+            recv = torch.zeros(self.N * P, dtype=torch.uint8, device=self.device)
+            # encode straight into this rank's slot of the gather buffer: an in-place
+            # all-gather (RCCL: sendbuff == recvbuff + rank * count), no local copy
+            r = self.comm.rank
+            self.payload[b.index] = recv[r * P:(r + 1) * P]
+            self.recv[b.index] = recv
+
+    def set_ratio(self, ratio: float):
+        """Top-k density warm-up: re-plan the codec and the payload buffers for ``ratio``
+        (every rank switches at the same step, so the fixed-size all-gathers still match; a
+        captured step graph must be re-captured)."""
+        if self.codec.allreduce or ratio == self.codec.ratio:
+            return False
+        self.codec.set_ratio(ratio)
+        self._alloc_payloads()
+        return True
 
     # -- accounting ---------------------------------------------------------------------------
     def bytes_per_step(self) -> StepStats:
@@ -179,9 +208,15 @@ class GradientExchange:
                 self.send[bi].copy_(g * (1.0 / self.predivide))
             return
         resid = None if self.resid is None else self.resid[b.start:b.start + b.length]
+        dgc = None
+        if self.dgc:
+            o = self.opt
+            dgc = dict(velocity=self.vel[b.start:b.start + b.length], momentum=o.momentum,
+                       dampening=o.dampening, nesterov=o.nesterov, weight_decay=o.weight_decay,
+                       param=self.flat.data_view(b))
         self.codec.encode(bi, g, self.payload[bi], self.step_idx + self.seed_offset,
                           self.comm.rank, resid,
-                          key_tensor=self.key_dev if self.use_dev_key else None)
+                          key_tensor=self.key_dev if self.use_dev_key else None, dgc=dgc)
 
     def _collective(self, bi: int):
         if self.codec.allreduce:
@@ -263,9 +298,13 @@ class GradientExchange:
                 recv = self.recv[b.index].view(self.N, -1)
                 if getattr(opt, "fusable", False):
                     adv = self.dev_key_advance and self.use_dev_key and b.index == self.nb - 1
+                    hp, mom = opt.hparams(), opt.mom[b.start:b.start + b.length]
+                    if self.dgc:  # momentum and weight decay already ran on the sender
+                        hp = dict(hp, momentum=0.0, dampening=0.0, weight_decay=0.0,
+                                  nesterov=False)
+                        mom = None
                     self.codec.decode_apply_sgd(b.index, recv, scale, self.flat.data_view(b),
-                                                opt.mom[b.start:b.start + b.length],
-                                                opt.hparams(), opt.first,
+                                                mom, hp, opt.first,
                                                 shadow=self.flat.shadow_view(b),
                                                 key_state=self.key_state if adv else None,
                                                 rank=self.comm.rank)

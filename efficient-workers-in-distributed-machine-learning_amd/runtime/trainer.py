@@ -61,6 +61,7 @@ class Trainer:
         # (parallel/ps.py k-of-n receive): setup, MIOpen find, graph capture, checkpoint and
         # eval collectives keep --comm-timeout
         timeout = cfg.comm_timeout
+        self._own_comm = comm is None
         self.comm = comm or init_distributed(timeout_s=timeout,
                                              device=self.device if self.device.type == "cuda"
                                              else None)
@@ -147,7 +148,9 @@ class Trainer:
 
         # exchange ---------------------------------------------------------------------------------
         ckw = dict(ratio=cfg.topk_ratio, levels=cfg.qsgd_levels, bits=cfg.qsgd_bits,
-                   norm=cfg.qsgd_norm, seed=cfg.seed)
+                   norm=cfg.qsgd_norm, seed=cfg.seed, dense_below=cfg.topk_dense_below)
+        if cfg.topk_warmup and cfg.topology != "allgather":
+            raise ValueError("--topk-warmup needs the all-to-all topology")
         if cfg.topology == "ps":
             self.exchange = PSExchange(self.flat, self.comm, make_codec(cfg.compress, **ckw),
                                        make_codec(cfg.pull_compress or cfg.compress, **ckw),
@@ -168,7 +171,8 @@ class Trainer:
                                              make_codec(cfg.compress, **ckw), self.opt,
                                              overlap=cfg.overlap,
                                              error_feedback=cfg.error_feedback,
-                                             predivide=cfg.predivide, side_stream=side)
+                                             predivide=cfg.predivide, side_stream=side,
+                                             ef_mode=cfg.ef_mode)
             if cfg.sync_every > 1 or cfg.select_best:
                 self.exchange = LocalSGDExchange(self.exchange, cfg.sync_every, cfg.sync_mode,
                                                  cfg.select_best, score_fn=self._holdout_score)
@@ -186,6 +190,10 @@ class Trainer:
         # hipBLASLt create their per-stream handles and workspaces during the eager warmup and not
         # inside the capture (lazy per-stream init inside a capture crashes capture_end).
         self.gstream = torch.cuda.Stream(device=self.device) if self.graph_mode != "off" else None
+        # data-plane failure detection: the own RCCL communicator's collectives are bounded by
+        # --comm-timeout through the native step watchdog (abort + non-zero exit)
+        if self.cuda:
+            self.comm.arm_watchdog(cfg.comm_timeout)
         self.step = 0
         self.epoch = 0
         self.fault = None
@@ -237,17 +245,26 @@ class Trainer:
     def train_step(self, x=None, y=None):
         """One synchronous step.  Returns (loss tensor, logits) (server: (None, None))."""
         if self.gstream is None:
-            return self._train_step(x, y)
-        if self._graphs is not None and len(self._graphs) == 1 and _SAME_STREAM_REPLAY:
+            out = self._train_step(x, y)
+        elif self._graphs is not None and len(self._graphs) == 1 and _SAME_STREAM_REPLAY:
             # a captured full-step graph replays on the caller's stream: no per-step event hop
             # to the graph stream and back (re-captures name their capture stream themselves)
-            return self._train_step(x, y)
-        gs = self.gstream  # a failed capture drops self.gstream inside the step
-        gs.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(gs):
             out = self._train_step(x, y)
-        torch.cuda.current_stream().wait_stream(gs)
+        else:
+            gs = self.gstream  # a failed capture drops self.gstream inside the step
+            gs.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(gs):
+                out = self._train_step(x, y)
+            torch.cuda.current_stream().wait_stream(gs)
+        self.comm.watch()  # the step's collectives are behind this point of the stream
         return out
+
+    def close(self):
+        """Release the exchange hooks, the watchdog and the own RCCL communicator (collective:
+        every rank calls it).  The process group stays up."""
+        self.exchange.close()
+        if self._own_comm:
+            self.comm.close()
 
     def lr_at(self, step: int) -> float:
         """Learning-rate schedule: linear warmup from lr/W over --lr-warmup-epochs (Horovod's
@@ -264,9 +281,29 @@ class Trainer:
                 lr *= cfg.lr_decay
         return lr
 
+    def ratio_at(self, step: int):
+        """Top-k density at ``step``: the --topk-warmup stages, each an equal share of
+        --topk-warmup-epochs, then --topk-ratio (DGC's exponentially decreasing density)."""
+        cfg = self.cfg
+        stages = [float(v) for v in cfg.topk_warmup.split(",") if v.strip()]
+        if not stages:
+            return cfg.topk_ratio
+        spe = len(self.loader) if self.loader is not None else 1
+        span = cfg.topk_warmup_epochs * max(1, spe)
+        i = int(step * len(stages) // max(1.0, span)) if span > 0 else len(stages)
+        return stages[i] if i < len(stages) else cfg.topk_ratio
+
+    def _apply_ratio_schedule(self):
+        ex = getattr(self.exchange, "inner", self.exchange)
+        if not self.cfg.topk_warmup or not hasattr(ex, "set_ratio"):
+            return
+        if ex.set_ratio(self.ratio_at(self.step)):
+            self._graphs = None  # payload sizes changed: re-capture at this step (every rank)
+
     def _train_step(self, x=None, y=None):
         if self.fault is not None and self.fault == (self.rank, self.step):
             raise FaultInjected(f"injected fault on rank {self.rank} at step {self.step}")
+        self._apply_ratio_schedule()
         if self.cfg.lr_warmup_epochs > 0 or self.cfg.lr_decay_epochs:
             lr = self.lr_at(self.step)
             if lr != self.opt.lr:
@@ -465,12 +502,13 @@ class Trainer:
         extra = {"config": {k: v for k, v in vars(self.cfg).items()
                             if isinstance(v, (int, float, str, bool)) or v is None},
                  "world": self.world}
-        if getattr(inner, "resid", None) is not None:
-            # the error-feedback residual is per-rank state: keep every rank's row
-            r = inner.resid
-            allr = torch.zeros((self.world, r.numel()), dtype=r.dtype, device=r.device)
-            self.comm.all_gather(allr.view(-1), r)
-            extra["ef_residual"] = allr
+        for name, attr in (("ef_residual", "resid"), ("ef_velocity", "vel")):
+            r = getattr(inner, attr, None)
+            if r is not None:
+                # error-feedback residual / DGC velocity are per-rank state: keep every rank's row
+                allr = torch.zeros((self.world, r.numel()), dtype=r.dtype, device=r.device)
+                self.comm.all_gather(allr.view(-1), r)
+                extra[name] = allr
         return extra
 
     @property
@@ -506,12 +544,14 @@ class Trainer:
         self.step = int(st["step"])
         self.epoch = int(st["epoch"])
         inner = getattr(self.exchange, "inner", self.exchange)
-        r = st["extra"].get("ef_residual")
-        if r is not None and getattr(inner, "resid", None) is not None:
-            if r.dim() == 2 and r.shape[0] == self.world:
-                inner.resid.copy_(r[self.rank].to(self.device))
-            else:
-                self.log.info("resume: world size changed, error-feedback residual reset")
+        for name, attr in (("ef_residual", "resid"), ("ef_velocity", "vel")):
+            r = st["extra"].get(name)
+            mine = getattr(inner, attr, None)
+            if r is not None and mine is not None:
+                if r.dim() == 2 and r.shape[0] == self.world:
+                    mine.copy_(r[self.rank].to(self.device))
+                else:
+                    self.log.info(f"resume: world size changed, {name} reset")
         if hasattr(self.exchange, "step_idx"):
             self.exchange.step_idx = self.step
         if self.loader is not None:
@@ -581,7 +621,7 @@ class Trainer:
         self.comm.barrier()
         wall = time.time() - t_start
         self.log.info(f"total time {wall:.1f}s for {total} steps")
-        self.exchange.close()
+        self.close()
         self.log.close()
         return {"steps": total, "wall_s": wall, "last": summary}
 

@@ -43,12 +43,46 @@ def _same_params(results, ranks=None):
     ["--compress", "none"],
     ["--compress", "bf16"],
     ["--compress", "topk_qsgd", "--error-feedback"],
+    ["--compress", "topk_qsgd", "--error-feedback", "--ef-mode", "plain"],
+    ["--compress", "topk_qsgd", "--error-feedback", "--weight-decay", "5e-4", "--nesterov",
+     "--topk-warmup", "0.25,0.05", "--topk-warmup-epochs", "0.25", "--topk-dense-below", "64"],
     ["--compress", "topk_qsgd", "--no-overlap", "--bucket-mb", "0.5"],
 ])
 def test_allgather_replicas_identical(tmp_path, flags):
     res = run_world(_train, 2, tmp_path, args=(flags, 4))
     _same_params(res)
     assert all(res[0]["losses"])
+
+
+def _warmup_schedule(rank, world):
+    import ewdml
+    from ewdml.runtime import Trainer
+
+    cfg = ewdml.parse_args(BASE + ["--compress", "topk_qsgd", "--error-feedback", "--topk-warmup",
+                                   "0.25,0.0625", "--topk-warmup-epochs", "1", "--max-steps",
+                                   "40"])
+    tr = Trainer(cfg)
+    spe = len(tr.loader)
+    seen = []
+    for _ in range(2 * spe + 1):
+        tr.train_step()
+        seen.append((tr.exchange.codec.ratio, tr.exchange.last.payload_bytes))
+    return {"seen": seen, "spe": spe, "ef": tr.exchange.ef_mode,
+            "params": tr.flat.data.clone()}
+
+
+def test_topk_warmup_schedule(tmp_path):
+    """--topk-warmup: 25 % for the first half epoch, 6.25 % for the second, then --topk-ratio;
+    payload sizes follow; replicas stay identical; momentum-corrected EF by default."""
+    res = run_world(_warmup_schedule, 2, tmp_path)
+    _same_params(res)
+    seen, spe = res[0]["seen"], res[0]["spe"]
+    half = spe // 2
+    assert res[0]["ef"] == "dgc"
+    assert all(r == 0.25 for r, _ in seen[:half])
+    assert all(r == 0.0625 for r, _ in seen[half + 1:spe])
+    assert all(r == 0.01 for r, _ in seen[spe:])
+    assert seen[0][1] > seen[spe - 1][1] > seen[-1][1]
 
 
 def test_world3_topk_qsgd_identical(tmp_path):

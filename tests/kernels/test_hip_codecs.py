@@ -173,6 +173,61 @@ def test_topk_error_feedback_matches_oracle():
         assert torch.equal(r_dev.cpu()[off:off + n], r_ref[off:off + n])
 
 
+@pytest.mark.parametrize("kind,bits", [("topk_qsgd", 8), ("topk_qsgd", 4), ("topk", 8)])
+@pytest.mark.parametrize("wd,nesterov,damp", [(0.0, False, 0.0), (5e-4, False, 0.1),
+                                              (1e-4, True, 0.0)])
+def test_topk_dgc_matches_oracle(kind, bits, wd, nesterov, damp):
+    """Momentum-corrected error feedback (DGC): velocity, residual and payload bitwise equal to
+    oracle.dgc_accumulate + encode_topk over consecutive steps (the velocity is cleared at the
+    sent coordinates, so the selection moves from step to step)."""
+    ops.require()
+    plan = _plan([40000, 1000, 8192 * 3 + 5], 0.01, bucket_offset=256)
+    lay = Layout.build(kind, plan, bits)
+    levels = 127 if bits == 8 else 7
+    dp = ops.DevicePlan(plan, DEV)
+    pay = torch.zeros(lay.nbytes, dtype=torch.uint8, device=DEV)
+    p0 = _grad(plan, seed=40)
+    r_ref, v_ref = torch.zeros(plan.length), torch.zeros(plan.length)
+    r_dev, v_dev, p_dev = r_ref.to(DEV), v_ref.to(DEV), p0.to(DEV)
+    for it in range(3):
+        g = _grad(plan, seed=30 + it)
+        key = stream_key(2, it, 1)
+        hp = dict(momentum=0.9, dampening=damp, nesterov=nesterov, weight_decay=wd)
+        ref = oracle.encode_topk(g.clone(), plan, lay, levels, "max", key, residual=r_ref,
+                                 dgc=dict(velocity=v_ref, param=p0, **hp))
+        ops.topk_encode(dp, g.to(DEV), pay, lay, levels, "max", key, resid=r_dev,
+                        dgc=dict(velocity=v_dev, param=p_dev, **hp))
+        assert torch.equal(pay.cpu(), ref), f"step {it}: payload"
+        for off, n in zip(plan.offsets, plan.numels):
+            assert torch.equal(r_dev.cpu()[off:off + n], r_ref[off:off + n]), f"step {it}: resid"
+            assert torch.equal(v_dev.cpu()[off:off + n], v_ref[off:off + n]), f"step {it}: vel"
+        assert (v_ref == 0).sum() >= plan.total_k  # masked where sent
+
+
+def test_topk_decode_without_momentum_buffer():
+    """mom=None (momentum ran on the sender): p -= lr * mean, the momentum buffer untouched."""
+    ops.require()
+    plan = _plan([9000, 64, 33333], 0.05)
+    lay = Layout.build("topk_qsgd", plan, 8)
+    N = 3
+    recv = torch.stack([oracle.encode_topk(_grad(plan, seed=r), plan, lay, 127, "max",
+                                           stream_key(0, 0, r)) for r in range(N)])
+    p0 = torch.randn(plan.length)
+    g = oracle.decode_sum(recv, plan, lay, 127, 1.0 / N)
+    p = p0.clone()
+    for off, n in zip(plan.offsets, plan.numels):
+        oracle.sgd_apply(p[off:off + n], None, g[off:off + n], 0.05, 0.0, 0.0, 0.0, False, False)
+    dp = ops.DevicePlan(plan, DEV)
+    pd = p0.to(DEV)
+    ops.topk_decode_apply(dp, recv.to(DEV), lay, 127, param=pd, mom=None, lr=0.05,
+                          grad_scale=1.0 / N)
+    for off, n in zip(plan.offsets, plan.numels):  # torch's CPU add(alpha=) may fuse: ~1 ulp
+        torch.testing.assert_close(pd.cpu()[off:off + n], p[off:off + n], rtol=1e-6, atol=1e-7)
+    with pytest.raises(ValueError):
+        ops.topk_decode_apply(dp, recv.to(DEV), lay, 127, param=pd, mom=None, lr=0.05,
+                              momentum=0.9)
+
+
 @pytest.mark.parametrize("bits,norm", [(8, "max"), (4, "max"), (8, "l2")])
 def test_qsgd_dense_roundtrip(bits, norm):
     ops.require()

@@ -166,3 +166,60 @@ def test_fp32_step_rounding_consistency():
     s = oracle.dequant_step(127, 0.3)
     assert s == float(np.float32(0.3) * np.float32(1 / 127))
     assert oracle.inv_scale(127, 0.0) == 0.0
+
+
+def test_dgc_conservation_and_masking():
+    """Momentum-corrected error feedback (oracle.dgc_accumulate): what is sent plus the new
+    residual equals the old residual plus the velocity step, and the velocity is zero exactly at
+    the sent coordinates (momentum factor masking)."""
+    plan = _plan([3000, 700], 0.02)
+    lay = Layout.build("topk", plan, 8)
+    gen = torch.Generator().manual_seed(0)
+    r = torch.zeros(plan.length)
+    u = torch.zeros(plan.length)
+    for step in range(4):
+        g = torch.randn(plan.length, generator=gen)
+        r_old, u_old = r.clone(), u.clone()
+        pay = oracle.encode_topk(g.clone(), plan, lay, 127, "max", step, residual=r,
+                                 dgc=dict(velocity=u, momentum=0.9))
+        sent = oracle.decode_sum(pay[None], plan, lay, 127, 1.0)
+        u_new = u_old * 0.9 + g
+        e = r_old + u_new
+        torch.testing.assert_close(sent + r, e, rtol=0, atol=0)  # plain top-k: exact values
+        mask = sent != 0
+        assert int(mask.sum()) == plan.total_k
+        assert torch.equal(u[mask], torch.zeros(int(mask.sum())))
+        assert torch.equal(u[~mask], u_new[~mask])
+
+
+def test_dgc_without_momentum_is_plain_error_feedback():
+    plan = _plan([5000], 0.01)
+    lay = Layout.build("topk_qsgd", plan, 8)
+    g = torch.randn(plan.length)
+    r1, r2, u = torch.randn(plan.length) * 0.1, None, torch.zeros(plan.length)
+    r2 = r1.clone()
+    a = oracle.encode_topk(g.clone(), plan, lay, 127, "max", 5, residual=r1)
+    b = oracle.encode_topk(g.clone(), plan, lay, 127, "max", 5, residual=r2,
+                           dgc=dict(velocity=u, momentum=0.0))
+    assert torch.equal(a, b) and torch.equal(r1, r2)
+
+
+def test_dense_below_sends_small_tensors_whole():
+    plan = BucketPlan([64, 64, 100000], [0, 64, 128], 0.01, dense_below=64)
+    assert plan.ks == [64, 64, 1000]
+    lay = Layout.build("topk_qsgd", plan, 8)
+    g = torch.randn(plan.length)
+    pay = oracle.encode_topk(g, plan, lay, 127, "max", 1)
+    dec = oracle.decode_sum(pay[None], plan, lay, 127, 1.0)
+    assert bool((dec[:128] != 0).all())
+
+
+def test_codec_set_ratio_replans():
+    from ewdml.compress.codecs import make_codec
+
+    c = make_codec("topk_qsgd", ratio=0.01).bind([_plan([100000, 5000], 1.0)], "cpu")
+    n1 = c.payload_bytes(0)
+    c.set_ratio(0.25)
+    assert c.plans[0].ks == [25000, 1250] and c.payload_bytes(0) > 20 * n1
+    c.set_ratio(0.01)
+    assert c.payload_bytes(0) == n1 and c.plans[0].ks == [1000, 50]
