@@ -145,7 +145,8 @@ def encode_topk(g: torch.Tensor, plan: BucketPlan, layout: Layout, levels: int, 
     T, C, K = plan.num_tensors, plan.num_chunks, plan.total_k
     scales = _section(out, layout.scales, T, torch.float32)
     counts = _section(out, layout.counts, C, torch.int16)
-    idx = _section(out, layout.idx, K, torch.int16)
+    idx = _section(out, layout.idx, plan.total_idx, torch.int16)
+    bm = _section(out, layout.bitmap, plan.total_bm_words, torch.int32)
     codes_all = []
     sent = torch.zeros_like(g) if residual is not None else None
     for t in range(T):
@@ -155,9 +156,17 @@ def encode_topk(g: torch.Tensor, plan: BucketPlan, layout: Layout, levels: int, 
         vals = x[sel]
         if vel is not None:
             vel[off + sel] = 0.0
-        c0, nch, e0 = plan.tensor_chunk0[t], plan.tensor_nchunks[t], plan.tensor_entry0[t]
+        c0, nch = plan.tensor_chunk0[t], plan.tensor_nchunks[t]
         counts[c0:c0 + nch] = torch.bincount(sel // CHUNK, minlength=nch).to(torch.int16)
-        idx[e0:e0 + k] = (sel % CHUNK).to(torch.int16)
+        if plan.tensor_bm0[t] >= 0:  # one bit per element, flat over the tensor's chunks
+            words = torch.zeros((n + 31) // 32, dtype=torch.int64, device=g.device)
+            words.index_add_(0, sel // 32, torch.ones_like(sel) << (sel % 32))
+            words = ((words + (1 << 31)) % (1 << 32)) - (1 << 31)  # uint32 bits as int32
+            w0 = plan.tensor_bm0[t]
+            bm[w0:w0 + words.numel()] = words.to(torch.int32)
+        else:
+            i0 = plan.tensor_idx0[t]
+            idx[i0:i0 + k] = (sel % CHUNK).to(torch.int16)
         scale = _scale_of(vals, norm)
         scales[t] = scale  # plain top-k keeps the scale in the header too (uniform layout)
         if layout.kind == "topk":
@@ -219,17 +228,29 @@ def _decoded_entries(pay: torch.Tensor, plan: BucketPlan, layout: Layout, levels
     T, C, K = plan.num_tensors, plan.num_chunks, plan.total_k
     scales = _section(pay, layout.scales, T, torch.float32)
     counts = _section(pay, layout.counts, C, torch.int16).to(torch.int64)
-    idx = _section(pay, layout.idx, K, torch.int16).to(torch.int64) & 0xFFFF
+    idx = _section(pay, layout.idx, plan.total_idx, torch.int16).to(torch.int64) & 0xFFFF
+    bm = _section(pay, layout.bitmap, plan.total_bm_words, torch.int32).to(torch.int64) \
+        & 0xFFFFFFFF
     if layout.kind == "topk":
         vals = _section(pay, layout.codes, K, torch.float32)
     elif layout.bits == 8:
         vals = _section(pay, layout.codes, K, torch.int8).to(torch.float32)
     else:
         vals = _unpack4(pay[layout.codes:layout.codes + (K + 1) // 2], K).to(torch.float32)
-    # chunk id of every entry (entries of a tensor are ordered by chunk)
-    chunk_of_entry = torch.repeat_interleave(torch.arange(C, device=pay.device), counts)
-    start = torch.tensor(plan.chunk_start, dtype=torch.int64, device=pay.device)
-    pos = start[chunk_of_entry] + idx
+    pos = torch.zeros(K, dtype=torch.int64, device=pay.device)
+    bits = torch.arange(32, device=pay.device)
+    for t in range(T):
+        off, n, k, e0 = plan.offsets[t], plan.numels[t], plan.ks[t], plan.tensor_entry0[t]
+        if plan.tensor_bm0[t] >= 0:  # entries in element order: the set bits, ascending
+            w0 = plan.tensor_bm0[t]
+            w = bm[w0:w0 + (n + 31) // 32]
+            el = (((w[:, None] >> bits) & 1).flatten()).nonzero().flatten()[:k]
+            pos[e0:e0 + el.numel()] = off + el
+        else:  # chunk of every entry from the per-chunk counts, then the chunk-local index
+            c0, nch, i0 = plan.tensor_chunk0[t], plan.tensor_nchunks[t], plan.tensor_idx0[t]
+            ch = torch.repeat_interleave(torch.arange(nch, device=pay.device),
+                                         counts[c0:c0 + nch])[:k]
+            pos[e0:e0 + ch.numel()] = off + ch * CHUNK + idx[i0:i0 + ch.numel()]
     if layout.kind != "topk":
         tensor_of_entry = torch.repeat_interleave(
             torch.arange(T, device=pay.device),

@@ -10,6 +10,12 @@ a chunk-local ``uint16`` offset plus its code, and one ``uint16`` count per chun
 entries each chunk owns.  That is what gets VGG-11 at top-1 % + 8-bit QSGD to ~132x fewer bytes than
 dense fp32 instead of the 80x that int32 indices would give.
 
+Dense selections index better with a bitmap: a tensor whose k is above ~1/16 of its elements
+(the report's K = 0.4, or small tensors sent whole) stores one bit per element (uint32 words,
+``bitmap`` section) instead of 2 bytes per entry; the choice is made per tensor at plan time from
+k and numel alone, so every rank still sends the same fixed size.  At K = 0.4 with 8-bit codes
+that is 0.525 B per element against the list's 1.2 B and the report's 0.8 B (value + index byte).
+
 Payload layouts (every section starts 16-byte aligned; all ranks send identical sizes, so the
 exchange is a fixed-size all-gather with no size handshake):
 
@@ -23,6 +29,7 @@ from typing import List
 import torch
 
 CHUNK = 8192
+BM_WORDS = CHUNK // 32  # bitmap words per chunk
 
 
 def _align(n: int, a: int = 16) -> int:
@@ -41,6 +48,9 @@ class BucketPlan:
     # tensors of at most this many elements are sent whole (k = numel): BatchNorm scales/shifts
     # and biases, whose sparsified updates would otherwise arrive once per ~1/ratio steps
     dense_below: int = 0
+    # "auto": per tensor, u16 index list or a 1-bit-per-element bitmap, whichever is smaller;
+    # "list": always the index list
+    index_mode: str = "auto"
     ks: List[int] = field(default_factory=list)
     chunk_tensor: List[int] = field(default_factory=list)
     chunk_start: List[int] = field(default_factory=list)  # relative to bucket start
@@ -49,6 +59,8 @@ class BucketPlan:
     tensor_nchunks: List[int] = field(default_factory=list)
     tensor_entry0: List[int] = field(default_factory=list)
     tensor_code0: List[int] = field(default_factory=list)  # dense code offset (16-aligned)
+    tensor_idx0: List[int] = field(default_factory=list)  # index-list position (-1: bitmap)
+    tensor_bm0: List[int] = field(default_factory=list)  # bitmap word offset (-1: index list)
 
     def __post_init__(self):
         assert len(self.numels) == len(self.offsets) and self.numels
@@ -56,7 +68,9 @@ class BucketPlan:
             self.length = self.offsets[-1] + self.numels[-1]
         self.ks = [n if n <= self.dense_below else max(1, int(n * self.ratio))
                    for n in self.numels]
-        e = c = 0
+        if self.index_mode not in ("auto", "list"):
+            raise ValueError("index_mode must be 'auto' or 'list'")
+        e = c = ix = bw = 0
         for t, (n, off) in enumerate(zip(self.numels, self.offsets)):
             nch = (n + CHUNK - 1) // CHUNK
             self.tensor_chunk0.append(len(self.chunk_tensor))
@@ -69,8 +83,19 @@ class BucketPlan:
             e += self.ks[t]
             self.tensor_code0.append(c)
             c += _align(n, 16)
+            words = (n + 31) // 32  # chunk j's words start at 256 j: one flat bit per element
+            if self.index_mode == "auto" and 4 * words < 2 * self.ks[t]:
+                self.tensor_idx0.append(-1)
+                self.tensor_bm0.append(bw)
+                bw += words
+            else:
+                self.tensor_idx0.append(ix)
+                self.tensor_bm0.append(-1)
+                ix += self.ks[t]
         self.total_k = e
         self.total_codes = c
+        self.total_idx = ix
+        self.total_bm_words = bw
 
     @property
     def num_tensors(self) -> int:
@@ -86,10 +111,12 @@ class BucketPlan:
 
     # ---- device tables consumed by the kernels -------------------------------------------
     def tensor_table(self, device) -> torch.Tensor:
-        """int32 [T, 8]: offset, numel, k, chunk0, nchunks, entry0, code0, 0."""
-        rows = [[o, n, k, c0, nc, e0, d0, 0] for o, n, k, c0, nc, e0, d0 in zip(
-            self.offsets, self.numels, self.ks, self.tensor_chunk0, self.tensor_nchunks,
-            self.tensor_entry0, self.tensor_code0)]
+        """int32 [T, 12]: offset, numel, k, chunk0, nchunks, entry0, code0, idx0, bm0, 0, 0, 0
+        (csrc/common.h TensorRow)."""
+        rows = [[o, n, k, c0, nc, e0, d0, i0, b0, 0, 0, 0]
+                for o, n, k, c0, nc, e0, d0, i0, b0 in zip(
+                    self.offsets, self.numels, self.ks, self.tensor_chunk0, self.tensor_nchunks,
+                    self.tensor_entry0, self.tensor_code0, self.tensor_idx0, self.tensor_bm0)]
         return torch.tensor(rows, dtype=torch.int32, device=device)
 
     def chunk_table(self, device) -> torch.Tensor:
@@ -111,17 +138,21 @@ class Layout:
     idx: int
     codes: int
     nbytes: int
+    bitmap: int = 0  # byte offset of the uint32 bitmap words (top-k kinds)
 
     @staticmethod
     def build(kind: str, plan: BucketPlan, bits: int = 8) -> "Layout":
         T, C, K = plan.num_tensors, plan.num_chunks, plan.total_k
         scales = 0
         off = _align(4 * T)
+        bitmap = 0
         if kind in ("topk_qsgd", "topk"):
             counts = off
             off = _align(off + 2 * C)
             idx = off
-            off = _align(off + 2 * K)
+            off = _align(off + 2 * plan.total_idx)
+            bitmap = off
+            off = _align(off + 4 * plan.total_bm_words)
             codes = off
             if kind == "topk":
                 off += 4 * K
@@ -133,4 +164,4 @@ class Layout:
             off += plan.total_codes if bits == 8 else plan.total_codes // 2
         else:
             raise ValueError(kind)
-        return Layout(kind, bits, scales, counts, idx, codes, _align(off))
+        return Layout(kind, bits, scales, counts, idx, codes, _align(off), bitmap)

@@ -66,6 +66,7 @@ class Config:
     pull_compress: Optional[str] = None  # ps topology: codec of the pull (default = push codec)
     sync_every: int = 1  # local SGD: exchange every H steps (method 6)
     sync_mode: str = "grad"  # grad: compressed gradient on sync steps | model: compressed delta
+    sync_mode_default: bool = True  # --sync-mode not given (--method 6 then selects 'model')
     select_best: bool = False  # method 6: adopt the weights of the best-accuracy rank at sync
     error_feedback: bool = False
     # dgc: momentum correction + momentum factor masking (the sender runs the momentum before
@@ -142,6 +143,8 @@ class Config:
                 if c.sync_every == 1:
                     c.sync_every = 20
                 c.select_best = True
+                if c.sync_mode_default:  # compressed model delta, winner's delta adopted
+                    c.sync_mode = "model"
         if c.compress_grad.lower() == "none":
             c.compress = "none"
         if c.topology not in ("allgather", "ps", "sharded"):
@@ -196,7 +199,7 @@ def build_parser(prog="distributed_nn.py") -> argparse.ArgumentParser:
     a("--pull-compress", type=str, default=None,
       choices=["none", "fp16", "bf16", "qsgd", "topk", "topk_qsgd"])
     a("--sync-every", type=int, default=d.sync_every)
-    a("--sync-mode", type=str, default=d.sync_mode, choices=["grad", "model"])
+    a("--sync-mode", type=str, default=None, choices=["grad", "model"])
     a("--select-best", action="store_true", default=False)
     a("--error-feedback", action="store_true", default=False)
     a("--ef-mode", type=str, default=d.ef_mode, choices=["dgc", "plain"])
@@ -246,5 +249,8 @@ def build_parser(prog="distributed_nn.py") -> argparse.ArgumentParser:
 
 def parse_args(argv=None, prog="distributed_nn.py") -> Config:
     ns = build_parser(prog).parse_args(argv)
+    ns.sync_mode_default = ns.sync_mode is None
+    if ns.sync_mode is None:
+        ns.sync_mode = Config.sync_mode
     fields = {f.name for f in dataclasses.fields(Config)}
     return Config(**{k: v for k, v in vars(ns).items() if k in fields}).resolved()

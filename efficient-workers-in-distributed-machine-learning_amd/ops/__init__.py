@@ -199,7 +199,7 @@ def topk_encode(dp: DevicePlan, grad, payload, layout, levels: int, norm: str, k
                   layout.scales, layout.counts, layout.idx, layout.codes, vk,
                   1 if norm == "l2" else 0, float(levels), float(1.0 / levels), key & 0xFFFFFFFF,
                   dp.plan.bucket_offset & 0xFFFFFFFF, _keyp(key_tensor), _stream(), _ptr(vel),
-                  _ptr(par), mom, damp1, wd, nest)
+                  _ptr(par), mom, damp1, wd, nest, layout.bitmap)
 
 
 def topk_decode_apply(dp: DevicePlan, recv, layout, levels: int, param=None, mom=None,
@@ -230,7 +230,8 @@ def topk_decode_apply(dp: DevicePlan, recv, layout, levels: int, param=None, mom
                         layout.idx, layout.codes, vk, float(1.0 / levels), _ptr(param), _ptr(mom),
                         _ptr(grad_out), _ptr(shadow), lr, momentum, dampening, weight_decay,
                         grad_scale, int(nesterov), int(first), int(apply), _stream(),
-                        _keyp(key_state), key_seed & 0xFFFFFFFF, key_rank & 0xFFFFFFFF)
+                        _keyp(key_state), key_seed & 0xFFFFFFFF, key_rank & 0xFFFFFFFF,
+                        layout.bitmap)
 
 
 def qsgd_encode(dp: DevicePlan, grad, payload, layout, levels: int, norm: str, key: int,

@@ -28,8 +28,9 @@ PYBIND11_MODULE(_C, m) {
            int value_kind, int norm_l2, float levels, float inv_levels, uint32_t key,
            uint32_t bucket_offset, uintptr_t key_ptr, uintptr_t stream, uintptr_t vel,
            uintptr_t param, float dgc_momentum, float dgc_damp1, float dgc_wd,
-           int dgc_nesterov) {
+           int dgc_nesterov, int bitmap_off) {
           TopkEncodeArgs a{};
+          a.bitmap_off = bitmap_off;
           a.vel = vel;
           a.param = param;
           a.dgc_momentum = dgc_momentum;
@@ -69,8 +70,9 @@ PYBIND11_MODULE(_C, m) {
            float inv_levels, uintptr_t param, uintptr_t mom, uintptr_t grad_out, uintptr_t shadow,
            float lr, float momentum, float dampening, float weight_decay, float grad_scale,
            int nesterov, int first, int apply, uintptr_t stream, uintptr_t key_state,
-           uint32_t key_seed, uint32_t key_rank) {
+           uint32_t key_seed, uint32_t key_rank, int bitmap_off) {
           TopkDecodeArgs a{};
+          a.bitmap_off = bitmap_off;
           a.key_state = key_state;
           a.key_seed = key_seed;
           a.key_rank = key_rank;

@@ -30,8 +30,11 @@
 #define EW_MAX_RANKS 64
 
 struct TensorRow {  // mirrors BucketPlan.tensor_table()
-  int off, numel, k, chunk0, nchunks, entry0, code0, pad;
+  // idx0: position in the u16 index list (-1: bitmap-indexed); bm0: word offset of the tensor's
+  // bitmap (-1: index list).  code0: dense QSGD code offset.
+  int off, numel, k, chunk0, nchunks, entry0, code0, idx0, bm0, pad0, pad1, pad2;
 };
+#define EW_BM_WORDS (EW_CHUNK / 32)  // bitmap words per chunk
 struct ChunkRow {  // mirrors BucketPlan.chunk_table()
   int tensor, start, len, local;
 };

@@ -13,7 +13,7 @@ struct TopkEncodeArgs {
   uintptr_t resid, chunks, tensors, scratch, payload, stream;
   long long payload_bytes;
   int num_tensors, num_chunks;
-  int scales_off, counts_off, idx_off, codes_off;
+  int scales_off, counts_off, idx_off, codes_off, bitmap_off;
   int value_kind;  // 0 = int8 QSGD, 1 = int4 QSGD, 2 = fp32 values (plain top-k)
   int norm_l2;     // 0 = max-norm scale, 1 = L2 norm of the selected values
   float levels, inv_levels;
@@ -30,7 +30,7 @@ struct TopkDecodeArgs {
   uintptr_t recv, chunks, tensors, param, mom, grad_out, shadow, stream;
   long long stride;
   int nranks, num_chunks;
-  int scales_off, counts_off, idx_off, codes_off;
+  int scales_off, counts_off, idx_off, codes_off, bitmap_off;
   int value_kind;
   float inv_levels;
   float lr, momentum, dampening, weight_decay, grad_scale;

@@ -367,7 +367,8 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_write(
     const TensorRow* __restrict__ tensors, const uint32_t* __restrict__ state,
     const uint32_t* __restrict__ chunk_off, const uint32_t* __restrict__ chunk_ties,
     const float* __restrict__ inv_arr, uint8_t* __restrict__ payload, int scales_off, int idx_off,
-    int codes_off, float levels, float inv_levels, uint32_t key_arg, const uint32_t* __restrict__ keyp,
+    int codes_off, int bitmap_off, float levels, float inv_levels, uint32_t key_arg,
+    const uint32_t* __restrict__ keyp,
     uint32_t bucket_offset, uint32_t* __restrict__ rezero, uint32_t rezero_words,
     float* __restrict__ vel) {
   __shared__ uint32_t ws[EW_WAVES];
@@ -386,7 +387,13 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_write(
   const float inv = inv_arr[c.tensor];
   float step = 0.0f;
   if (VK != VK_F32) step = reinterpret_cast<const float*>(payload + scales_off)[c.tensor] * inv_levels;
-  uint16_t* idx_out = reinterpret_cast<uint16_t*>(payload + idx_off);
+  // entries' indices: the tensor's u16 list (chunk-local offsets), or its bitmap (one bit per
+  // element; a wave's 256 elements of a slab are 8 whole words)
+  const bool bitmap = tr.bm0 >= 0;
+  uint16_t* idx_out = reinterpret_cast<uint16_t*>(payload + idx_off) + (bitmap ? 0 : tr.idx0) -
+                      tr.entry0;
+  uint32_t* bm_out = reinterpret_cast<uint32_t*>(payload + bitmap_off) +
+                     (bitmap ? tr.bm0 + c.local * EW_BM_WORDS : 0);
   const uint32_t gbase = bucket_offset + (uint32_t)c.start;
   uint32_t carry_gt = 0, carry_eq = 0;
   float4 v[EW_CU];
@@ -415,13 +422,15 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_write(
     uint32_t eqr = carry_eq + (ex >> 16);
     uint32_t pos = ebase + gt_before + min(ties, eqr);
     float left[4];  // EF residual: what this rank did not send
+    uint32_t nib = 0;  // bitmap bits of this thread's 4 elements
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const bool sel = isgt[j] || (iseq[j] && eqr < ties);
       eqr += iseq[j];
       float sent = 0.0f;
       if (sel && pos < eend) {
-        idx_out[pos] = (uint16_t)(i0 + j);
+        if (!bitmap) idx_out[pos] = (uint16_t)(i0 + j);
+        nib |= 1u << j;
         if (VK == VK_F32) {
           reinterpret_cast<float*>(payload + codes_off)[pos] = xs[j];
           sent = xs[j];
@@ -440,6 +449,14 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_write(
       }
       left[j] = xs[j] - sent;
     }
+    if (bitmap) {  // uniform per block: 8 lanes' nibbles make one word; every word is written
+      uint32_t w = nib << (4 * (threadIdx.x & 7));
+      w |= __shfl_xor(w, 1, 64);
+      w |= __shfl_xor(w, 2, 64);
+      w |= __shfl_xor(w, 4, 64);
+      const int wi = i0 >> 5;
+      if ((threadIdx.x & 7) == 0 && wi * 32 < c.len) bm_out[wi] = w;
+    }
     if (EF) {
       float* r = resid + c.start + i0;
       if (i0 + 3 < c.len) {
@@ -455,6 +472,16 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_write(
   }
 }
 
+// Value of payload entry `pe` (fp32 value, or the int8 / int4 QSGD code as a float).
+template <int VK>
+__device__ __forceinline__ float ew_topk_code(const uint8_t* pay, int codes_off, uint32_t pe) {
+  if (VK == VK_F32) return reinterpret_cast<const float*>(pay + codes_off)[pe];
+  if (VK == VK_Q8) return (float)reinterpret_cast<const int8_t*>(pay + codes_off)[pe];
+  const uint32_t b = pay[codes_off + (pe >> 1)];
+  const int q = (int)((pe & 1u) ? (b >> 4) : (b & 0xfu));
+  return (float)(q >= 8 ? q - 16 : q);
+}
+
 // Receive side: one block per chunk.  Sum the N ranks' entries for this chunk in rank order in an
 // LDS accumulator (indices are unique within a rank, so no atomics), scale by 1/N, then either
 // write the averaged gradient and/or apply the SGD update to the chunk's parameters.
@@ -462,11 +489,13 @@ template <int VK>
 __global__ __launch_bounds__(EW_BLOCK) void k_topk_decode_apply(
     const uint8_t* __restrict__ recv, int nranks, long long stride,
     const ChunkRow* __restrict__ chunks, const TensorRow* __restrict__ tensors, int scales_off,
-    int counts_off, int idx_off, int codes_off, float inv_levels, float* __restrict__ param,
+    int counts_off, int idx_off, int codes_off, int bitmap_off, float inv_levels,
+    float* __restrict__ param,
     float* __restrict__ mom, float* __restrict__ grad_out, uint16_t* __restrict__ shadow,
     SgdArgs sa, int apply) {
   __shared__ float4 acc4[EW_CHUNK / 4];
   __shared__ uint32_t s_off[EW_MAX_RANKS];
+  __shared__ uint32_t ws[EW_WAVES];
   float* acc = reinterpret_cast<float*>(acc4);
   const ChunkRow c = chunks[blockIdx.x];
   const TensorRow tr = tensors[c.tensor];
@@ -508,24 +537,31 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_decode_apply(
     const uint32_t eend = (uint32_t)(tr.entry0 + tr.k);
     uint32_t cnt = reinterpret_cast<const uint16_t*>(pay + counts_off)[blockIdx.x];
     cnt = off >= eend ? 0u : min(cnt, eend - off);
-    const uint16_t* idx = reinterpret_cast<const uint16_t*>(pay + idx_off) + off;
     float step = 1.0f;
     if (VK != VK_F32) step = reinterpret_cast<const float*>(pay + scales_off)[c.tensor] * inv_levels;
-    for (uint32_t e = threadIdx.x; e < cnt; e += EW_BLOCK) {
-      float v;
-      if (VK == VK_F32) {
-        v = reinterpret_cast<const float*>(pay + codes_off)[off + e];
-      } else if (VK == VK_Q8) {
-        v = (float)reinterpret_cast<const int8_t*>(pay + codes_off)[off + e];
-      } else {
-        const uint32_t pe = off + e;
-        const uint32_t b = pay[codes_off + (pe >> 1)];
-        int q = (int)((pe & 1u) ? (b >> 4) : (b & 0xfu));
-        v = (float)(q >= 8 ? q - 16 : q);
+    if (tr.bm0 >= 0) {
+      // bitmap-indexed tensor: thread t owns word t of the chunk (256 words = 8192 elements);
+      // a block scan of the popcounts gives each word's first entry
+      const uint32_t* bw = reinterpret_cast<const uint32_t*>(pay + bitmap_off) + tr.bm0 +
+                           c.local * EW_BM_WORDS;
+      uint32_t word = (int)threadIdx.x * 32 < c.len ? bw[threadIdx.x] : 0u;
+      uint32_t tot;
+      uint32_t e = ew_block_excl_scan((uint32_t)__popc(word), ws, tot);
+      while (word) {
+        const int b = __ffs(word) - 1;
+        word &= word - 1u;
+        const int i = (int)threadIdx.x * 32 + b;
+        if (e < cnt && i < c.len) acc[i] = acc[i] + ew_topk_code<VK>(pay, codes_off, off + e) * step;
+        ++e;
       }
-      const float prod = v * step;
-      const int i = idx[e];
-      if (i < c.len) acc[i] = acc[i] + prod;
+    } else {
+      const uint16_t* idx = reinterpret_cast<const uint16_t*>(pay + idx_off) + tr.idx0 +
+                            (off - (uint32_t)tr.entry0);
+      for (uint32_t e = threadIdx.x; e < cnt; e += EW_BLOCK) {
+        const float prod = ew_topk_code<VK>(pay, codes_off, off + e) * step;
+        const int i = idx[e];
+        if (i < c.len) acc[i] = acc[i] + prod;
+      }
     }
     __syncthreads();
   }
@@ -628,7 +664,8 @@ void ew_topk_encode(const TopkEncodeArgs& a) {
             a.norm_l2);
 #define EW_WRITE(VK, EFV)                                                                          \
   EW_LAUNCH((k_topk_write<VK, EFV>), C, s, g, resid, chunks, tensors, state, chunk_off, chunk_ties, \
-            inv, pay, a.scales_off, a.idx_off, a.codes_off, a.levels, a.inv_levels, a.key,         \
+            inv, pay, a.scales_off, a.idx_off, a.codes_off, a.bitmap_off, a.levels, a.inv_levels,  \
+            a.key,                                                                                   \
             reinterpret_cast<const uint32_t*>(a.key_ptr), a.bucket_offset, kmaxr, rezero_words,   \
             dg.vel)
   if (a.value_kind == VK_Q8) {
@@ -663,7 +700,8 @@ void ew_topk_decode_apply(const TopkDecodeArgs& a) {
   const int C = a.num_chunks;
 #define EW_DEC(VK)                                                                                   \
   EW_LAUNCH(k_topk_decode_apply<VK>, C, a.stream, recv, a.nranks, a.stride, chunks, tensors,         \
-            a.scales_off, a.counts_off, a.idx_off, a.codes_off, a.inv_levels, p, m, go, sh, sa,      \
+            a.scales_off, a.counts_off, a.idx_off, a.codes_off, a.bitmap_off, a.inv_levels, p, m, go, \
+            sh, sa,                                                                                  \
             a.apply)
   if (a.value_kind == VK_Q8) EW_DEC(VK_Q8);
   else if (a.value_kind == VK_Q4) EW_DEC(VK_Q4);

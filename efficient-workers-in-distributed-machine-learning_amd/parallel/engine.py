@@ -328,6 +328,15 @@ class GradientExchange:
             self.codec.decode(b.index, self.recv[b.index].view(self.N, -1),
                               self.flat.grad_view(b), scale)
 
+    def decode_rank(self, src: int):
+        """Write rank ``src``'s decoded payload (unscaled) into ``flat.grad``: local SGD's
+        best-worker adoption reads the winner's compressed delta out of the all-gather."""
+        if self.codec.allreduce:
+            raise ValueError("decode_rank needs a compressing (all-gather) codec")
+        for b in self.flat.buckets:
+            rows = self.recv[b.index].view(self.N, -1)
+            self.codec.decode(b.index, rows[src:src + 1], self.flat.grad_view(b), 1.0)
+
     def close(self):
         if self._hooks:
             for p in self.flat.params:

@@ -172,7 +172,11 @@ class Trainer:
                                              overlap=cfg.overlap,
                                              error_feedback=cfg.error_feedback,
                                              predivide=cfg.predivide, side_stream=side,
-                                             ef_mode=cfg.ef_mode)
+                                             # local SGD compresses model deltas / steps locally:
+                                             # no sender-side momentum there
+                                             ef_mode=cfg.ef_mode if (cfg.sync_every == 1 and
+                                                                     not cfg.select_best)
+                                             else "plain")
             if cfg.sync_every > 1 or cfg.select_best:
                 self.exchange = LocalSGDExchange(self.exchange, cfg.sync_every, cfg.sync_mode,
                                                  cfg.select_best, score_fn=self._holdout_score)

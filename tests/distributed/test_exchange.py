@@ -147,6 +147,40 @@ def test_method6_local_sgd_select_best(tmp_path):
     _same_params(res)  # after the step-6 sync everyone holds the best rank's weights
 
 
+def _method6(rank, world):
+    import ewdml
+    from ewdml.runtime import Trainer
+
+    cfg = ewdml.parse_args(BASE + ["--method", "6", "--sync-every", "3", "--max-steps", "3"])
+    tr = Trainer(cfg)
+    ex = tr.exchange
+    for _ in range(2):
+        tr.train_step()
+    tr.loader.seek(2)
+    x, y = tr.loader.next()
+    anchor = ex.anchor.clone()
+    tr.train_step(x, y)  # the sync step
+    best = ex.best_rank_history[-1]
+    inner = ex.inner
+    rows = inner.recv[0].view(inner.N, -1)
+    delta = torch.zeros_like(tr.flat.grad)
+    inner.codec.decode(0, rows[best:best + 1], delta, 1.0)
+    return {"mode": ex.mode, "params": tr.flat.data.clone(), "expect": anchor + delta,
+            "wire": ex.last.wire_bytes_sent + ex.last.wire_bytes_recv,
+            "dense": tr.flat.numel * 4, "nb": len(tr.flat.buckets)}
+
+
+def test_method6_adopts_the_winners_compressed_delta(tmp_path):
+    """--method 6 defaults to compressed model-delta sync: every rank applies the best rank's
+    compressed delta out of the all-gather (no dense weight broadcast)."""
+    res = run_world(_method6, 2, tmp_path)
+    _same_params(res)
+    r = res[0]
+    assert r["mode"] == "model" and r["nb"] == 1
+    torch.testing.assert_close(r["params"], r["expect"], rtol=0, atol=0)
+    assert r["wire"] < r["dense"] / 20  # a compressed payload each way, no dense weights
+
+
 def test_local_sgd_grad_mode_resyncs_replicas(tmp_path):
     """grad mode without best-worker selection: local steps drift the replicas apart; every sync
     point re-broadcasts rank 0's weights, so after a sync step all ranks hold the same model."""

@@ -112,9 +112,13 @@ def test_topk_l2_norm_close():
 
 
 @pytest.mark.parametrize("kind,bits", [("topk_qsgd", 8), ("topk_qsgd", 4), ("topk", 8)])
-def test_topk_decode_matches_oracle(kind, bits):
+@pytest.mark.parametrize("ratio", [0.03, 0.4])
+def test_topk_decode_matches_oracle(kind, bits, ratio):
+    """ratio 0.4: most tensors are bitmap-indexed (plan.py), the 20-element one keeps the list."""
     ops.require()
-    plan = _plan([20 * 25, 20, 8192 * 5 + 3, 50, 70001], 0.03, bucket_offset=128)
+    plan = _plan([20 * 25, 20, 8192 * 5 + 3, 50, 70001], ratio, bucket_offset=128)
+    if ratio > 0.1:
+        assert plan.tensor_bm0[2] >= 0 and plan.total_bm_words > 0
     lay = Layout.build(kind, plan, bits)
     levels = 127 if bits == 8 else 7
     N = 5
