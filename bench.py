@@ -67,7 +67,7 @@ def parse(argv=None):
     p.add_argument("--no-overlap", action="store_true")
     p.add_argument("--error-feedback", default="on", choices=["on", "off"])
     p.add_argument("--no-extras", action="store_true", help="headline run only")
-    p.add_argument("--hip-graph", default="full", choices=["off", "split", "full"])
+    p.add_argument("--hip-graph", default="full", choices=["off", "split", "full", "segmented"])
     p.add_argument("--param-dtype", default="auto", choices=["auto", "fp32"])
     p.add_argument("--json-out", default=None, help="also write the JSON line to this file")
     p.add_argument("--extra", default="", help="extra distributed_nn.py flags")

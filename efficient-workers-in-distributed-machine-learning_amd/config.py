@@ -101,7 +101,10 @@ class Config:
     layout: str = "auto"  # auto (nhwc on the GPU when the fused NHWC kernels run) | nchw | nhwc
     fused_nn: str = "on"  # on: conv-BN-ReLU-pool groups / 2x2 pools through ops/csrc/nn.hip | off
     fused_data: str = "on"  # on: training batches built by one graph-capturable kernel (GPU) | off
-    hip_graph: str = "off"  # off | split (graphs around eager RCCL calls) | full (one graph)
+    # auto (full where the step can be captured, else eager) | off | split (graphs around eager
+    # RCCL calls) | full (one graph) | segmented (linear compute segments + per-bucket comm graphs
+    # on their own stream: collectives overlap backward)
+    hip_graph: str = "auto"
     graph_warmup: int = 3  # eager steps (>= 1) before capture: MIOpen find, handles, momentum
 
     data_dir: Optional[str] = None  # None -> synthetic data of the dataset's shape
@@ -226,7 +229,8 @@ def build_parser(prog="distributed_nn.py") -> argparse.ArgumentParser:
     a("--layout", type=str, default=d.layout, choices=["auto", "nchw", "nhwc"])
     a("--fused-nn", type=str, default=d.fused_nn, choices=["on", "off"])
     a("--fused-data", type=str, default=d.fused_data, choices=["on", "off"])
-    a("--hip-graph", type=str, default=d.hip_graph, choices=["off", "split", "full"])
+    a("--hip-graph", type=str, default=d.hip_graph,
+      choices=["auto", "off", "split", "full", "segmented"])
     a("--graph-warmup", type=int, default=d.graph_warmup)
     a("--data-dir", type=str, default=None)
     a("--holdout-from-test", type=int, default=d.holdout_from_test)

@@ -23,7 +23,8 @@ from ..models import build_model, canonical_name, input_shape
 from ..models.fused import set_enabled as set_fused_nn
 from ..optim.flat import make_optimizer
 from ..parallel.comm import Comm, init_distributed
-from ..parallel.engine import GradientExchange, Stopwatch, sync_buffers, sync_params
+from ..parallel.engine import (GradientExchange, SegmentedCapture, Stopwatch, sync_buffers,
+                               sync_params)
 from ..parallel.flat import FlatModel
 from ..parallel.local_sgd import LocalSGDExchange
 from ..parallel.ps import PSExchange
@@ -70,7 +71,7 @@ class Trainer:
         if cfg.sync_debug:
             from .. import ops
             ops.set_sync_debug(True)
-            if cfg.hip_graph != "off":
+            if cfg.hip_graph not in ("off", "auto"):
                 raise ValueError("--sync-debug synchronises after each launch: use --hip-graph off")
         torch.manual_seed(cfg.seed)
         if self.cuda:
@@ -181,12 +182,20 @@ class Trainer:
                 self.exchange = LocalSGDExchange(self.exchange, cfg.sync_every, cfg.sync_mode,
                                                  cfg.select_best, score_fn=self._holdout_score)
         self.amp_dtype = {"bf16": torch.bfloat16, "fp16": torch.float16}.get(cfg.amp)
-        self.graph_mode = cfg.hip_graph if self.cuda else "off"
+        self.graph_mode = cfg.hip_graph if (self.cuda and not cfg.sync_debug) else "off"
+        if self.graph_mode == "auto":
+            # graphs wherever the step can be captured: the all-to-all exchange (the parameter
+            # server's k-of-n polling, local SGD's host-side best-worker choice and the sharded
+            # exchange run eagerly)
+            self.graph_mode = "full" if isinstance(self.exchange, GradientExchange) else "off"
         if self.graph_mode != "off" and not isinstance(self.exchange, GradientExchange):
             raise ValueError("--hip-graph needs the all-to-all topology without local SGD")
-        if self.graph_mode == "full" and self.comm.distributed and self.comm.backend == "gloo":
+        if (self.graph_mode in ("full", "segmented") and self.comm.distributed
+                and self.comm.backend == "gloo"):
             # gloo's CUDA collectives cannot be captured: graph the compute, issue them between
             self.graph_mode = "split"
+        if self.graph_mode == "segmented":  # collectives on their own stream, beside backward
+            self.exchange.comm_stream = torch.cuda.Stream(device=self.device)
         self._graphs = None
         self._in_graph_batch = False
         self._key_synced = False
@@ -378,7 +387,10 @@ class Trainer:
 
         ``full``: one graph = zero grads, fwd, bwd, hook-driven encode on the side stream, RCCL
         collectives, fused decode+SGD.  ``split``: graph A (through encode) -> eager RCCL calls ->
-        graph B (decode+SGD), for process groups whose collectives cannot be captured."""
+        graph B (decode+SGD), for process groups whose collectives cannot be captured.
+        ``segmented``: linear compute segments split at bucket boundaries, one encode + collective
+        graph per bucket on the comm stream, and the apply graph (``SegmentedCapture``): the
+        collectives overlap the rest of backward."""
         ex = self.exchange
         self._in_graph_batch = x is None  # fused loader: the batch kernel is captured too
         if x is not None:
@@ -407,6 +419,29 @@ class Trainer:
                         self._rejoin_side()
                         raise
                 self._graphs = (g,)
+            elif self.graph_mode == "segmented":
+                seg = SegmentedCapture(self.gstream, ex.comm_stream, mode="relaxed")
+                ex.seg = seg
+                try:
+                    seg.begin()
+                    if self._in_graph_batch:
+                        self._gx, self._gy = self.loader.emit()
+                    loss, out = self.forward_backward(self._gx, self._gy)
+                    ex.launch_pending()
+                    seg.end()
+                except BaseException:
+                    seg.abort()
+                    raise
+                finally:
+                    ex.seg = None
+                ex._active = False
+                # the apply waits for every comm graph (replay joins the comm stream first)
+                ga = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(ga, pool=seg.pool, stream=self.gstream,
+                                      capture_error_mode=mode):
+                    ex.apply()
+                seg.apply = ga
+                self._graphs = ("segmented", seg)
             else:
                 ex.defer_comm = True
                 ga = torch.cuda.CUDAGraph()
@@ -458,6 +493,9 @@ class Trainer:
         if len(self._graphs) == 1:
             with self._range("graph_step"):
                 self._graphs[0].replay()
+        elif self._graphs[0] == "segmented":
+            with self._range("graph_step"):
+                self._graphs[1].replay()
         else:
             self._graphs[0].replay()
             ex.communicate()

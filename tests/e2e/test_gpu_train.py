@@ -30,7 +30,7 @@ def _run(flags, steps):
 def test_graph_modes_match_eager(codec):
     ops.require()
     ref, l_ref = _run(LENET + ["--compress", codec, "--hip-graph", "off"], 8)
-    for mode in ("split", "full"):
+    for mode in ("split", "full", "segmented"):
         tr, l = _run(LENET + ["--compress", codec, "--hip-graph", mode], 8)
         assert tr.graph_mode == mode and tr._graphs is not None
         rel = (tr.flat.data - ref.flat.data).norm() / ref.flat.data.norm()
@@ -51,6 +51,27 @@ def test_adam_graph_matches_eager(opt):
         assert int(tr.opt.step_t.item()) == 10
         rel = float((tr.flat.data - ref.flat.data).norm() / ref.flat.data.norm())
         assert rel < 1e-4, f"{mode}: params differ from eager by {rel:.2e}"
+
+
+@pytest.mark.parametrize("codec", ["topk_qsgd", "none"])
+def test_segmented_graph_matches_full_graph(codec):
+    """--hip-graph segmented (linear compute segments split at bucket boundaries, per-bucket
+    encode + collective graphs on the comm stream, apply graph): same kernels on the same data
+    as the one-graph step, so the trajectory is bitwise the full graph's; the comm graphs are
+    real (several buckets, one launch each)."""
+    ops.require()
+    flags = ["--network", "VGG11", "--dataset", "Cifar10", "--batch-size", "32",
+             "--synthetic-size", "512", "--momentum", "0.9", "--eval-freq", "0", "--quiet",
+             "--device", "cuda", "--graph-warmup", "2", "--amp", "none", "--bucket-mb", "6",
+             "--compress", codec, "--error-feedback"]
+    full, lf = _run(flags + ["--hip-graph", "full"], 7)
+    seg, ls = _run(flags + ["--hip-graph", "segmented"], 7)
+    assert seg.graph_mode == "segmented" and seg._graphs[0] == "segmented"
+    sc = seg._graphs[1]
+    assert len(seg.flat.buckets) >= 3 and len(sc.comms) >= 2
+    assert len(sc.segments) == len(sc.comms) + 1 and sc.apply is not None
+    assert lf == ls
+    assert torch.equal(full.flat.data, seg.flat.data)
 
 
 def test_graph_replay_refreshes_rng_key():

@@ -2,8 +2,10 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/kernels/test_hip_codecs.py tests/kernels/test_conv_f32.py -x -q --timeout 120 --timeout-method thread -k "dgc or momentum_buffer or error_feedback or deferred or autograd_grad or topk_encode_matches or watchdog" tests/e2e/test_watchdog.py > gpurun_out/codec_tests.log 2>&1 || { tail -40 gpurun_out/codec_tests.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests/kernels/test_hip_codecs.py tests/e2e/test_watchdog.py -x -q --timeout 120 --timeout-method thread > gpurun_out/codec_tests.log 2>&1 || { tail -40 gpurun_out/codec_tests.log; exit 1; }
 tail -1 gpurun_out/codec_tests.log
+timeout -k 10 600 python -u -m pytest tests/kernels/test_conv_f32.py -x -q --timeout 120 --timeout-method thread -k "deferred or autograd_grad" > gpurun_out/conv_tests.log 2>&1 || { tail -40 gpurun_out/conv_tests.log; exit 1; }
+tail -1 gpurun_out/conv_tests.log
 P="python -u tools/ef_probe.py --device cuda --batch 128 --steps 300 --synthetic 16384 --hip-graph full"
 run() { timeout -k 10 300 $P "$@" >> gpurun_out/ef_sweep.jsonl 2>> gpurun_out/ef_sweep.err || { tail -20 gpurun_out/ef_sweep.err; exit 1; }; tail -1 gpurun_out/ef_sweep.jsonl | cut -c1-220; }
 run --compress none --modes none
