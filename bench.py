@@ -93,8 +93,8 @@ def _flags(a, world, amp, ef):
     flags += ["--layout", a.layout, "--fused-nn", a.fused_nn]
     if a.no_overlap:
         flags.append("--no-overlap")
-    if ef:
-        flags.append("--error-feedback")
+    if ef:  # the timed steps run the steady-state codec: no density / lr warm-up phase
+        flags += ["--error-feedback", "--ef-warmup", "none"]
     # graph capture happens inside the untimed warmup: eager steps, then the capturing step
     gw = max(1, min(3, a.warmup - 1))
     flags += ["--hip-graph", a.hip_graph, "--graph-warmup", str(gw), "--param-dtype",
@@ -102,7 +102,7 @@ def _flags(a, world, amp, ef):
     return flags + a.extra.split(), gw
 
 
-def measure(a, world, amp, ef):
+def measure(a, world, amp, ef, extra=()):
     """Build a Trainer for this configuration, run W untimed warmup steps, then time exactly K
     steps bracketed by barrier + synchronize on both sides; returns (max-over-ranks seconds,
     trainer, final loss, host enqueue seconds)."""
@@ -112,7 +112,7 @@ def measure(a, world, amp, ef):
     from ewdml.runtime.trainer import Trainer
 
     flags, gw = _flags(a, world, amp, ef)
-    tr = Trainer(ewdml.parse_args(flags, prog="bench.py"))
+    tr = Trainer(ewdml.parse_args(flags + list(extra), prog="bench.py"))
 
     def sync():
         if tr.cuda:
@@ -206,16 +206,26 @@ def main(argv=None):
     if not a.no_extras:
         extras = []
         if ef:
-            extras.append(("fp32_no_ef" if a.amp == "none" else f"{a.amp}_no_ef", a.amp, False))
+            extras.append(("fp32_no_ef" if a.amp == "none" else f"{a.amp}_no_ef", a.amp, False,
+                           ()))
         if a.amp == "none":
-            extras.append(("bf16", "bf16", ef))
-        for key, amp, e in extras:
+            extras.append(("bf16", "bf16", ef, ()))
+            # the reference's live path (Method 3: dense fp32 gradients, all-reduce) and its
+            # lowest-traffic one (Method 6: Method 5 + local SGD, sync every 20 steps)
+            extras.append(("dense_fp32", "none", False, ("--compress", "none")))
+            extras.append(("method6", "none", False, ("--method", "6")))
+        for key, amp, e, xf in extras:
             if cuda:
                 torch.cuda.empty_cache()
-            el, tr2, fl, _ = measure(a, world, amp, e)
+            el, tr2, fl, _ = measure(a, world, amp, e, xf)
             rec[f"value_{key}"] = round(world * a.batch_size * a.steps / el, 2)
             rec[f"ms_per_step_{key}"] = round(el * 1e3 / a.steps, 4)
             rec[f"final_loss_{key}"] = fl
+            if key == "method6":
+                ex = tr2.exchange
+                rec["method6_sync_every"] = ex.every
+                rec["method6_payload_bytes_per_sync"] = ex.bytes_per_step().payload_bytes
+                rec["method6_hip_graph"] = tr2.graph_mode
             del tr2
     if dist.is_initialized():
         rank = dist.get_rank()

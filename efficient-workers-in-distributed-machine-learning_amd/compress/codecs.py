@@ -11,9 +11,15 @@
 Device tensors go through the HIP kernels (``ops``); CPU tensors through the torch oracle.  On a
 GPU box a missing extension raises instead of silently falling back.
 """
+import os
+
 import torch
 
 from .. import ops
+
+# EWDML_ORACLE=1: run the torch oracle on device tensors too (eager experiments with codec
+# variants before they have kernels; needs flat gradient views, EWDML_GRAD_VIEWS=1)
+_FORCE_ORACLE = os.environ.get("EWDML_ORACLE") == "1"
 from . import oracle
 from .plan import BucketPlan, Layout
 from .rng import stream_key
@@ -118,7 +124,8 @@ class Codec:
 
     # -- encode / decode ----------------------------------------------------------------------
     def encode(self, b: int, grad: torch.Tensor, payload: torch.Tensor, step: int, rank: int,
-               resid: torch.Tensor = None, key_tensor: torch.Tensor = None, dgc: dict = None):
+               resid: torch.Tensor = None, key_tensor: torch.Tensor = None, dgc: dict = None,
+               ef21: bool = False):
         """Compress bucket ``b`` of the flat gradient (``grad`` = that bucket's view).  ``dgc``:
         error feedback with momentum correction (top-k codecs; ``oracle.dgc_accumulate``)."""
         if dgc is not None and (resid is None or self.kind not in ("topk", "topk_qsgd")):
@@ -126,7 +133,11 @@ class Codec:
         plan, lay = self.plans[b], self.layouts[b]
         key = self.key(step, rank)
         on_dev = (grad[0] if isinstance(grad, (list, tuple)) else grad).is_cuda
-        if on_dev:
+        if ef21 and (resid is None or self.kind not in ("topk", "topk_qsgd")):
+            raise ValueError("EF21 needs a top-k codec and the gradient estimate")
+        if on_dev and not _FORCE_ORACLE:
+            if ef21:
+                raise NotImplementedError("EF21 encode on the GPU: run with EWDML_ORACLE=1")
             if self.kind == "qsgd":
                 ops.qsgd_encode(self.dplans[b], grad, payload, lay, self.levels, self.norm, key,
                                 resid, key_tensor)
@@ -139,13 +150,14 @@ class Codec:
         if self.kind == "qsgd":
             out = oracle.encode_qsgd(grad, plan, lay, self.levels, self.norm, key, resid)
         else:
-            out = oracle.encode_topk(grad, plan, lay, self.levels, self.norm, key, resid, dgc)
+            out = oracle.encode_topk(grad, plan, lay, self.levels, self.norm, key, resid, dgc,
+                                     ef21)
         payload[:lay.nbytes].copy_(out)
 
     def decode(self, b: int, recv: torch.Tensor, out: torch.Tensor, scale: float):
         """``out`` (bucket view) = scale * sum over ranks of the decoded payloads in ``recv``."""
         plan, lay = self.plans[b], self.layouts[b]
-        if recv.is_cuda:
+        if recv.is_cuda and not _FORCE_ORACLE:
             fn = ops.qsgd_decode_apply if self.kind == "qsgd" else ops.topk_decode_apply
             fn(self.dplans[b], recv, lay, self.levels, grad_out=out, grad_scale=scale)
             return
@@ -161,13 +173,13 @@ class Codec:
         if mom is None and hp["momentum"] != 0:
             raise ValueError("a momentum step needs the momentum buffer")
         plan, lay = self.plans[b], self.layouts[b]
-        if recv.is_cuda:
+        if recv.is_cuda and not _FORCE_ORACLE:
             fn = ops.qsgd_decode_apply if self.kind == "qsgd" else ops.topk_decode_apply
             fn(self.dplans[b], recv, lay, self.levels, param=param, mom=mom, grad_out=grad_out,
                lr=hp["lr"], momentum=hp["momentum"], dampening=hp["dampening"],
                weight_decay=hp["weight_decay"], grad_scale=scale, nesterov=hp["nesterov"],
                first=first, shadow=shadow, key_state=key_state, key_seed=self.seed,
-               key_rank=rank)
+               key_rank=rank, lr_tensor=hp.get("lr_t"))
             return
         g = oracle.decode_sum(recv, plan, lay, self.levels, scale)
         if grad_out is not None:

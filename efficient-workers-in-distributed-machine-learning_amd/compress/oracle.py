@@ -97,7 +97,7 @@ def _scale_of(vals: torch.Tensor, norm: str) -> float:
 # ---------------------------------------------------------------------------------------------
 def dgc_accumulate(g: torch.Tensor, residual: torch.Tensor, velocity: torch.Tensor, momentum: float,
                    dampening: float = 0.0, nesterov: bool = False, weight_decay: float = 0.0,
-                   param: torch.Tensor = None) -> torch.Tensor:
+                   param: torch.Tensor = None, lr: float = None) -> torch.Tensor:
     """Momentum correction of Deep Gradient Compression (Lin et al., ICLR 2018): the momentum is
     applied on the worker *before* sparsification and the residual accumulates the velocity,
     not the raw gradient.  Updates ``velocity`` in place and returns ``residual + d`` (the vector
@@ -117,6 +117,8 @@ def dgc_accumulate(g: torch.Tensor, residual: torch.Tensor, velocity: torch.Tens
         g = g + param * float(f32(weight_decay))
     velocity.copy_(velocity * float(f32(momentum)) + g * float(f32(1.0 - dampening)))
     d = g + velocity * float(f32(momentum)) if nesterov else velocity
+    if lr is not None:  # error feedback on the update (lr inside): --ef-mode local
+        d = d * float(f32(lr))
     return residual + d
 
 
@@ -124,21 +126,29 @@ def dgc_accumulate(g: torch.Tensor, residual: torch.Tensor, velocity: torch.Tens
 # encode
 # ---------------------------------------------------------------------------------------------
 def encode_topk(g: torch.Tensor, plan: BucketPlan, layout: Layout, levels: int, norm: str,
-                key: int, residual: torch.Tensor = None, dgc: dict = None) -> torch.Tensor:
+                key: int, residual: torch.Tensor = None, dgc: dict = None,
+                ef21: bool = False) -> torch.Tensor:
     """Top-k (+QSGD when ``layout.kind == 'topk_qsgd'``) of one bucket -> uint8 payload.
 
     ``g`` is the bucket's flat fp32 gradient (length ``plan.length``).  With ``residual`` (error
     feedback) the compressed vector is ``g + residual`` and ``residual`` is overwritten with what was
     not transmitted.  With ``dgc`` (``{velocity, momentum, dampening, nesterov, weight_decay,
     param}``: momentum correction, :func:`dgc_accumulate`) the compressed vector is ``residual +
-    d`` and the velocity is cleared at the transmitted coordinates (momentum factor masking).
+    d`` and the velocity is cleared at the transmitted coordinates (momentum factor masking;
+    ``dgc["mask"] = False`` keeps it, and ``dgc["lr"]`` accumulates lr-scaled updates).  With
+    ``ef21`` (EF21, Richtarik et al. 2021) ``residual`` is this rank's running gradient estimate
+    h: the compressed vector is ``g - h`` and ``h += sent``; the receivers add the average of
+    the sent vectors to the global estimate and step on that (``parallel/engine.py``).
     """
     vel = None
+    g_in = g
     if dgc is not None:
-        vel = dgc["velocity"]
-        g = dgc_accumulate(g, residual, vel, dgc["momentum"], dgc.get("dampening", 0.0),
-                           dgc.get("nesterov", False), dgc.get("weight_decay", 0.0),
-                           dgc.get("param"))
+        vel = dgc["velocity"] if dgc.get("mask", True) else None
+        g = dgc_accumulate(g, residual, dgc["velocity"], dgc["momentum"],
+                           dgc.get("dampening", 0.0), dgc.get("nesterov", False),
+                           dgc.get("weight_decay", 0.0), dgc.get("param"), dgc.get("lr"))
+    elif ef21:
+        g = g - residual
     elif residual is not None:
         g = g + residual
     out = torch.zeros(layout.nbytes, dtype=torch.uint8, device=g.device)
@@ -186,8 +196,11 @@ def encode_topk(g: torch.Tensor, plan: BucketPlan, layout: Layout, levels: int, 
     else:
         p = _pack4(codes)
         out[layout.codes:layout.codes + p.numel()] = p
-    if residual is not None:
+    if ef21:
+        residual.copy_(residual + sent)
+    elif residual is not None:
         residual.copy_(g - sent)
+    del g_in
     return out
 
 

@@ -27,6 +27,10 @@ def _str2bool(v) -> bool:
     return str(v).strip().lower() not in ("", "0", "false", "no", "off", "none")
 
 
+# density stages of the error-feedback warm-up (DGC's exponentially decreasing density)
+EF_WARMUP_STAGES = (0.25, 0.125, 0.0625, 0.03125, 0.015625)
+
+
 @dataclass
 class Config:
     # ---- reference flags (distributed_nn.py:24-72) -----------------------------------------
@@ -76,7 +80,12 @@ class Config:
     # used in turn over the first --topk-warmup-epochs epochs, then --topk-ratio (e.g. "0.25,0.0625,
     # 0.015625"); each change re-plans the payloads (and re-captures a HIP graph)
     topk_warmup: str = ""
-    topk_warmup_epochs: float = 1.0
+    topk_warmup_epochs: float = 2.0
+    # auto: --error-feedback with a top-k codec brings its stability recipe unless set explicitly:
+    # the density warm-up 25 % -> 12.5 % -> 6.25 % -> 3.125 % -> 1.5625 % (stages above
+    # --topk-ratio) over --topk-warmup-epochs, and a linear lr warm-up from 0.1 lr over 2 epochs
+    # (measured on ResNet-50: profiles/validation/ef_stability_r03.md) | none
+    ef_warmup: str = "auto"
     bucket_mb: float = 16.0
     overlap: bool = True
     predivide: float = 1.0  # Horovod gradient_predivide_factor
@@ -88,6 +97,7 @@ class Config:
     nesterov: bool = False
     lr_scale_world: bool = False  # Horovod: lr *= world size
     lr_warmup_epochs: float = 0.0  # Horovod LearningRateWarmupCallback: lr/W -> lr linearly
+    lr_warmup_start: Optional[float] = None  # warm-up's first lr as a fraction of lr (None: 1/W)
     lr_decay_epochs: str = ""  # e.g. "30,60,90": multiply lr by --lr-decay at these epochs
     lr_decay: float = 0.1
     # ---- execution -------------------------------------------------------------------------------
@@ -150,6 +160,15 @@ class Config:
                     c.sync_mode = "model"
         if c.compress_grad.lower() == "none":
             c.compress = "none"
+        if (c.ef_warmup == "auto" and c.error_feedback and c.compress in ("topk", "topk_qsgd")
+                and c.sync_every == 1 and not c.select_best):
+            stages = [r for r in EF_WARMUP_STAGES if r > c.topk_ratio]
+            if not c.topk_warmup:
+                c.topk_warmup = ",".join(f"{r:g}" for r in stages)
+            if stages and c.lr_warmup_epochs <= 0:
+                c.lr_warmup_epochs = 2.0
+                if c.lr_warmup_start is None:
+                    c.lr_warmup_start = 0.1
         if c.topology not in ("allgather", "ps", "sharded"):
             raise ValueError("--topology must be allgather, ps or sharded")
         if c.graph_warmup < 1:
@@ -205,9 +224,10 @@ def build_parser(prog="distributed_nn.py") -> argparse.ArgumentParser:
     a("--sync-mode", type=str, default=None, choices=["grad", "model"])
     a("--select-best", action="store_true", default=False)
     a("--error-feedback", action="store_true", default=False)
-    a("--ef-mode", type=str, default=d.ef_mode, choices=["dgc", "plain"])
+    a("--ef-mode", type=str, default=d.ef_mode, choices=["dgc", "plain", "local", "ef21"])
     a("--topk-warmup", type=str, default=d.topk_warmup)
     a("--topk-warmup-epochs", type=float, default=d.topk_warmup_epochs)
+    a("--ef-warmup", type=str, default=d.ef_warmup, choices=["auto", "none"])
     a("--bucket-mb", type=float, default=d.bucket_mb)
     a("--no-overlap", dest="overlap", action="store_false", default=True)
     a("--predivide", type=float, default=d.predivide)
@@ -219,6 +239,7 @@ def build_parser(prog="distributed_nn.py") -> argparse.ArgumentParser:
     a("--nesterov", action="store_true", default=False)
     a("--lr-scale-world", action="store_true", default=False)
     a("--lr-warmup-epochs", type=float, default=d.lr_warmup_epochs)
+    a("--lr-warmup-start", type=float, default=None)
     a("--lr-decay-epochs", type=str, default=d.lr_decay_epochs)
     a("--lr-decay", type=float, default=d.lr_decay)
     # execution

@@ -180,9 +180,9 @@ def topk_encode(dp: DevicePlan, grad, payload, layout, levels: int, norm: str, k
         vk = VK_Q4
     if vk != VK_F32 and not (1 <= levels <= (127 if layout.bits == 8 else 7)):
         raise ValueError(f"levels={levels} does not fit {layout.bits}-bit codes")
-    vel = par = None
+    vel = par = lrt = None
     mom = damp1 = wd = 0.0
-    nest = 0
+    nest, dmask = 0, 1
     if dgc is not None:
         if resid is None:
             raise ValueError("momentum correction needs the residual")
@@ -191,6 +191,11 @@ def topk_encode(dp: DevicePlan, grad, payload, layout, levels: int, norm: str, k
         damp1 = float(1.0 - dgc.get("dampening", 0.0))
         wd = float(dgc.get("weight_decay", 0.0))
         nest = int(bool(dgc.get("nesterov", False)))
+        dmask = int(bool(dgc.get("mask", True)))
+        if dgc.get("lr") is not None:  # error feedback on the update: the lr inside
+            lrt = dgc.get("lr_t")
+            if lrt is None:
+                raise ValueError("lr-scaled accumulation on the GPU needs the device lr (lr_t)")
         if wd != 0.0:
             par = dgc["param"]
             _check_bucket(dp, par, "param")
@@ -199,13 +204,22 @@ def topk_encode(dp: DevicePlan, grad, payload, layout, levels: int, norm: str, k
                   layout.scales, layout.counts, layout.idx, layout.codes, vk,
                   1 if norm == "l2" else 0, float(levels), float(1.0 / levels), key & 0xFFFFFFFF,
                   dp.plan.bucket_offset & 0xFFFFFFFF, _keyp(key_tensor), _stream(), _ptr(vel),
-                  _ptr(par), mom, damp1, wd, nest, layout.bitmap)
+                  _ptr(par), mom, damp1, wd, nest, layout.bitmap, dmask, _lrp(lrt))
+
+
+def _lrp(lr_tensor):
+    """Device fp32 learning rate read by the kernels at run time (None: the ``lr`` argument)."""
+    if lr_tensor is None:
+        return 0
+    if not lr_tensor.is_cuda or lr_tensor.dtype != torch.float32 or lr_tensor.numel() < 1:
+        raise ValueError("lr_tensor must be a device fp32 tensor")
+    return lr_tensor.data_ptr()
 
 
 def topk_decode_apply(dp: DevicePlan, recv, layout, levels: int, param=None, mom=None,
                       grad_out=None, lr=0.0, momentum=0.0, dampening=0.0, weight_decay=0.0,
                       grad_scale=1.0, nesterov=False, first=False, shadow=None,
-                      key_state=None, key_seed=0, key_rank=0):
+                      key_state=None, key_seed=0, key_rank=0, lr_tensor=None):
     C = require()
     _check(recv, torch.uint8, "recv")
     if recv.dim() != 2 or recv.shape[1] != layout.nbytes:
@@ -231,7 +245,7 @@ def topk_decode_apply(dp: DevicePlan, recv, layout, levels: int, param=None, mom
                         _ptr(grad_out), _ptr(shadow), lr, momentum, dampening, weight_decay,
                         grad_scale, int(nesterov), int(first), int(apply), _stream(),
                         _keyp(key_state), key_seed & 0xFFFFFFFF, key_rank & 0xFFFFFFFF,
-                        layout.bitmap)
+                        layout.bitmap, _lrp(lr_tensor))
 
 
 def qsgd_encode(dp: DevicePlan, grad, payload, layout, levels: int, norm: str, key: int,
@@ -255,7 +269,7 @@ def qsgd_encode(dp: DevicePlan, grad, payload, layout, levels: int, norm: str, k
 def qsgd_decode_apply(dp: DevicePlan, recv, layout, levels: int, param=None, mom=None,
                       grad_out=None, lr=0.0, momentum=0.0, dampening=0.0, weight_decay=0.0,
                       grad_scale=1.0, nesterov=False, first=False, shadow=None,
-                      key_state=None, key_seed=0, key_rank=0):
+                      key_state=None, key_seed=0, key_rank=0, lr_tensor=None):
     C = require()
     _check(recv, torch.uint8, "recv")
     if recv.dim() != 2 or recv.shape[1] != layout.nbytes:
@@ -274,14 +288,14 @@ def qsgd_decode_apply(dp: DevicePlan, recv, layout, levels: int, param=None, mom
                         layout.bits, float(1.0 / levels), _ptr(param), _ptr(mom), _ptr(grad_out),
                         _ptr(shadow), lr, momentum, dampening, weight_decay, grad_scale,
                         int(nesterov), int(first), int(apply), _stream(), _keyp(key_state),
-                        key_seed & 0xFFFFFFFF, key_rank & 0xFFFFFFFF)
+                        key_seed & 0xFFFFFFFF, key_rank & 0xFFFFFFFF, _lrp(lr_tensor))
 
 
 _GDT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
 
 
 def sgd_flat(param, mom, grad, lr, momentum=0.0, dampening=0.0, weight_decay=0.0,
-             grad_scale=1.0, nesterov=False, first=False, shadow=None):
+             grad_scale=1.0, nesterov=False, first=False, shadow=None, lr_tensor=None):
     C = require()
     _check(param, torch.float32, "param")
     _check(mom, torch.float32, "mom")
@@ -297,11 +311,12 @@ def sgd_flat(param, mom, grad, lr, momentum=0.0, dampening=0.0, weight_decay=0.0
             raise ValueError("shadow must match param")
     C.sgd_flat(_ptr(param), _ptr(mom), _ptr(grad), _ptr(shadow), n, _GDT[grad.dtype], lr,
                momentum, dampening, weight_decay, grad_scale, int(nesterov), int(first),
-               _stream())
+               _stream(), _lrp(lr_tensor))
 
 
 def adam_flat(param, exp_avg, exp_avg_sq, max_exp_avg_sq, grad, lr_step, beta1, beta2, eps,
-              weight_decay=0.0, grad_scale=1.0, amsgrad=False, shadow=None, step=None, lr=0.0):
+              weight_decay=0.0, grad_scale=1.0, amsgrad=False, shadow=None, step=None, lr=0.0,
+              lr_tensor=None):
     """Adam/AMSGrad over flat fp32 buffers.  ``step`` (int32 device tensor, optional): the kernel
     reads t = step + 1 and derives ``lr_step = lr * sqrt(1 - beta2^t) / (1 - beta1^t)`` on the
     device, so a captured graph follows the step count (``lr_step`` is then ignored)."""
@@ -322,7 +337,7 @@ def adam_flat(param, exp_avg, exp_avg_sq, max_exp_avg_sq, grad, lr_step, beta1, 
             raise ValueError("shadow must match param")
     C.adam_flat(_ptr(param), _ptr(exp_avg), _ptr(exp_avg_sq), _ptr(max_exp_avg_sq), _ptr(grad),
                 _ptr(shadow), n, _GDT[grad.dtype], lr_step, beta1, beta2, eps, weight_decay,
-                grad_scale, int(amsgrad), _stream(), _ptr(step), float(lr))
+                grad_scale, int(amsgrad), _stream(), _ptr(step), float(lr), _lrp(lr_tensor))
 
 
 _DDT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}

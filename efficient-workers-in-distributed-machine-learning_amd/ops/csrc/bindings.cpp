@@ -28,8 +28,10 @@ PYBIND11_MODULE(_C, m) {
            int value_kind, int norm_l2, float levels, float inv_levels, uint32_t key,
            uint32_t bucket_offset, uintptr_t key_ptr, uintptr_t stream, uintptr_t vel,
            uintptr_t param, float dgc_momentum, float dgc_damp1, float dgc_wd,
-           int dgc_nesterov, int bitmap_off) {
+           int dgc_nesterov, int bitmap_off, int dgc_mask, uintptr_t dgc_lr_ptr) {
           TopkEncodeArgs a{};
+          a.dgc_mask = dgc_mask;
+          a.dgc_lr_ptr = dgc_lr_ptr;
           a.bitmap_off = bitmap_off;
           a.vel = vel;
           a.param = param;
@@ -70,8 +72,9 @@ PYBIND11_MODULE(_C, m) {
            float inv_levels, uintptr_t param, uintptr_t mom, uintptr_t grad_out, uintptr_t shadow,
            float lr, float momentum, float dampening, float weight_decay, float grad_scale,
            int nesterov, int first, int apply, uintptr_t stream, uintptr_t key_state,
-           uint32_t key_seed, uint32_t key_rank, int bitmap_off) {
+           uint32_t key_seed, uint32_t key_rank, int bitmap_off, uintptr_t lr_ptr) {
           TopkDecodeArgs a{};
+          a.lr_ptr = lr_ptr;
           a.bitmap_off = bitmap_off;
           a.key_state = key_state;
           a.key_seed = key_seed;
@@ -142,8 +145,9 @@ PYBIND11_MODULE(_C, m) {
            uintptr_t mom, uintptr_t grad_out, uintptr_t shadow, float lr, float momentum,
            float dampening, float weight_decay, float grad_scale, int nesterov, int first,
            int apply, uintptr_t stream, uintptr_t key_state, uint32_t key_seed,
-           uint32_t key_rank) {
+           uint32_t key_rank, uintptr_t lr_ptr) {
           QsgdDecodeArgs a{};
+          a.lr_ptr = lr_ptr;
           a.key_state = key_state;
           a.key_seed = key_seed;
           a.key_rank = key_rank;
@@ -176,8 +180,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("sgd_flat",
         [](uintptr_t param, uintptr_t mom, uintptr_t grad, uintptr_t shadow, long long n,
            int grad_dtype, float lr, float momentum, float dampening, float weight_decay,
-           float grad_scale, int nesterov, int first, uintptr_t stream) {
+           float grad_scale, int nesterov, int first, uintptr_t stream, uintptr_t lr_ptr) {
           SgdFlatArgs a{};
+          a.lr_ptr = lr_ptr;
           a.param = param;
           a.mom = mom;
           a.grad = grad;
@@ -199,8 +204,9 @@ PYBIND11_MODULE(_C, m) {
         [](uintptr_t param, uintptr_t m1, uintptr_t m2, uintptr_t vmax, uintptr_t grad,
            uintptr_t shadow, long long n, int grad_dtype, float lr_step, float beta1, float beta2,
            float eps, float weight_decay, float grad_scale, int amsgrad, uintptr_t stream,
-           uintptr_t step, double lr) {
+           uintptr_t step, double lr, uintptr_t lr_ptr) {
           AdamFlatArgs a{};
+          a.lr_ptr = lr_ptr;
           a.step = step;
           a.lr = lr;
           a.param = param;

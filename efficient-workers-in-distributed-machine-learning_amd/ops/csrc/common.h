@@ -166,7 +166,13 @@ struct SgdArgs {
   // kernel of a step's last bucket moves it to the next step (no host->device key copy per step)
   uint32_t* key_state;
   uint32_t key_seed, key_rank;
+  // device learning rate (nullable): read at run time, so an lr schedule needs no graph
+  // re-capture (the host value is frozen into a captured kernel's arguments)
+  const float* lr_ptr;
 };
+__device__ __forceinline__ void ew_sgd_resolve(SgdArgs& a) {
+  if (a.lr_ptr) a.lr = *a.lr_ptr;
+}
 
 // ---- counter-based RNG (must equal compress/rng.py) -------------------------------------------
 __device__ __forceinline__ uint32_t ew_mix32(uint32_t x) {

@@ -24,6 +24,8 @@ struct TopkEncodeArgs {
   uintptr_t vel, param;
   float dgc_momentum, dgc_damp1, dgc_wd;  // damp1 = 1 - dampening
   int dgc_nesterov;
+  int dgc_mask;          // clear the velocity at sent coordinates (DGC) or keep it (local)
+  uintptr_t dgc_lr_ptr;  // nullable device lr: residual accumulates lr-scaled updates
 };
 
 struct TopkDecodeArgs {
@@ -37,6 +39,7 @@ struct TopkDecodeArgs {
   int nesterov, first, apply;
   uintptr_t key_state;  // nullable int32[2] {step, key}: advanced to the next step (HIP graphs)
   uint32_t key_seed, key_rank;
+  uintptr_t lr_ptr;  // nullable device fp32 learning rate (overrides lr)
 };
 
 struct QsgdEncodeArgs {
@@ -63,6 +66,7 @@ struct QsgdDecodeArgs {
   int nesterov, first, apply;
   uintptr_t key_state;  // see TopkDecodeArgs
   uint32_t key_seed, key_rank;
+  uintptr_t lr_ptr;
 };
 
 struct SgdFlatArgs {
@@ -71,6 +75,7 @@ struct SgdFlatArgs {
   int grad_dtype;  // 0 = fp32, 1 = bf16, 2 = fp16
   float lr, momentum, dampening, weight_decay, grad_scale;
   int nesterov, first;
+  uintptr_t lr_ptr;
 };
 
 struct AdamFlatArgs {
@@ -81,6 +86,7 @@ struct AdamFlatArgs {
   int amsgrad;
   uintptr_t step;  // int32 device step counter (nullable: use lr_step as given)
   double lr;       // base lr for the device-side bias correction
+  uintptr_t lr_ptr;  // nullable device fp32 base lr (overrides lr)
 };
 
 size_t ew_topk_scratch_bytes(int num_tensors, int num_chunks);

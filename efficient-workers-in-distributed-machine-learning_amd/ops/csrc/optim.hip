@@ -34,6 +34,7 @@ template <int GT>
 __global__ __launch_bounds__(EW_BLOCK) void k_sgd_flat(float* __restrict__ p, float* __restrict__ mom,
                                                        const void* __restrict__ g, long long n4,
                                                        uint16_t* __restrict__ shadow, SgdArgs sa) {
+  ew_sgd_resolve(sa);
   for (long long v = blockIdx.x * (long long)EW_BLOCK + threadIdx.x; v < n4;
        v += (long long)gridDim.x * EW_BLOCK) {
     float gv[4];
@@ -61,12 +62,14 @@ struct AdamArgs {
   // the bias correction of the current step (the host value is frozen at capture)
   const int* step;
   double lr;
+  const float* lr_ptr;  // nullable device base lr
 };
 
 __device__ __forceinline__ void ew_adam_resolve(AdamArgs& a) {
   if (a.step) {
     const double t = (double)(*a.step + 1);
-    a.lr_step = (float)(a.lr * sqrt(1.0 - pow((double)a.beta2, t)) /
+    const double lr = a.lr_ptr ? (double)*a.lr_ptr : a.lr;
+    a.lr_step = (float)(lr * sqrt(1.0 - pow((double)a.beta2, t)) /
                         (1.0 - pow((double)a.beta1, t)));
   }
 }
@@ -171,6 +174,7 @@ inline int ew_grid(long long n4) {
 
 void ew_sgd_flat(const SgdFlatArgs& a) {
   SgdArgs sa{a.lr, a.momentum, a.dampening, a.weight_decay, a.grad_scale, a.nesterov, a.first};
+  sa.lr_ptr = reinterpret_cast<const float*>(a.lr_ptr);
   const long long n4 = a.n / 4;
   auto* p = reinterpret_cast<float*>(a.param);
   auto* m = reinterpret_cast<float*>(a.mom);
@@ -189,7 +193,8 @@ void ew_sgd_flat(const SgdFlatArgs& a) {
 void ew_adam_flat(const AdamFlatArgs& a) {
   AdamArgs aa{a.lr_step, a.beta1,      a.beta2,   a.eps,
               a.weight_decay, a.grad_scale, a.bc2_sqrt, a.amsgrad,
-              reinterpret_cast<const int*>(a.step), a.lr};
+              reinterpret_cast<const int*>(a.step), a.lr,
+              reinterpret_cast<const float*>(a.lr_ptr)};
   const long long n4 = a.n / 4;
   auto* p = reinterpret_cast<float*>(a.param);
   auto* m = reinterpret_cast<float*>(a.exp_avg);

@@ -108,6 +108,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_qsgd_decode_apply(
     int codes_off, float inv_levels, float* __restrict__ param, float* __restrict__ mom,
     float* __restrict__ grad_out, uint16_t* __restrict__ shadow, SgdArgs sa, int apply) {
   const ChunkRow c = chunks[blockIdx.x];
+  ew_sgd_resolve(sa);
   const TensorRow tr = tensors[c.tensor];
   ew_key_advance(sa);
   const long long cbase = (long long)tr.code0 + (long long)c.local * EW_CHUNK;
@@ -199,6 +200,7 @@ void ew_qsgd_decode_apply(const QsgdDecodeArgs& a) {
   auto* tensors = reinterpret_cast<const TensorRow*>(a.tensors);
   SgdArgs sa{a.lr, a.momentum, a.dampening, a.weight_decay, a.grad_scale, a.nesterov, a.first,
              reinterpret_cast<uint32_t*>(a.key_state), a.key_seed, a.key_rank};
+  sa.lr_ptr = reinterpret_cast<const float*>(a.lr_ptr);
   auto* recv = reinterpret_cast<const uint8_t*>(a.recv);
   auto* p = reinterpret_cast<float*>(a.param);
   auto* m = reinterpret_cast<float*>(a.mom);

@@ -210,63 +210,72 @@ void ew_rccl_abort(uintptr_t h) {
 // ---------------------------------------------------------------------------------------------
 // Step watchdog.  The data-plane collectives run on the step's own stream (no process-group
 // watchdog sees them), so a stalled peer would hang the surviving ranks inside a graph replay or a
-// synchronize.  After each step the host records an event on the step stream (ew_rccl_watch); a
-// thread polls the oldest outstanding event and, once one has been pending for longer than the
-// timeout, aborts the communicator (RCCL kernels waiting on a peer return), releases the test
-// spin flags, waits a bounded moment for the stream to drain, and ends the process with a non-zero
-// exit code.  No exec, no retry: the launcher sees the failure (the reference's
-// straggler kill intent, src/distributed_nn.py:50-59, src/model_ops/lenet.py:188-255).
+// synchronize.  After each step the host enqueues a one-thread kernel that writes the step's
+// sequence number into host-pinned memory (ew_rccl_watch); a thread compares it with the issued
+// sequence and, once a step has been outstanding for longer than the timeout, releases the test
+// spin flags, aborts the communicator (RCCL kernels waiting on a peer return) from a helper thread,
+// waits a bounded moment for the stream to drain, and ends the process with a non-zero exit code.
+// The watchdog thread makes no HIP call while it watches: a thread blocked in a device
+// synchronize can hold the runtime's locks, and an hipEventQuery would wait behind it.  No exec,
+// no retry: the launcher sees the failure (the reference's straggler kill intent,
+// src/distributed_nn.py:50-59, src/model_ops/lenet.py:188-255).
 // ---------------------------------------------------------------------------------------------
 namespace {
 
+__global__ void k_watch_mark(unsigned long long* done, unsigned long long seq) {
+  __hip_atomic_store(done, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 struct Watchdog {
   ncclComm_t comm = nullptr;
-  int device = 0;
   double timeout_s = 600.0;
   int exit_code = 3;
+  unsigned long long* done = nullptr;  // host-pinned, written by k_watch_mark
+  unsigned long long issued = 0;
   std::mutex mu;
   std::condition_variable cv;
-  std::deque<std::pair<hipEvent_t, std::chrono::steady_clock::time_point>> pending;
-  std::vector<hipEvent_t> pool;
+  std::deque<std::pair<unsigned long long, std::chrono::steady_clock::time_point>> pending;
   std::vector<volatile int*> release;  // host flags set to 1 on abort (test spin kernels)
   bool stop = false;
   std::thread th;
 
-  void fire(const char* why, double waited) {
+  unsigned long long completed() const {
+    return __atomic_load_n(done, __ATOMIC_ACQUIRE);
+  }
+
+  [[noreturn]] void fire(double waited) {
     std::fprintf(stderr,
-                 "ewdml watchdog: %s after %.1f s (timeout %.1f s); aborting the RCCL "
-                 "communicator and exiting with code %d\n",
-                 why, waited, timeout_s, exit_code);
+                 "ewdml watchdog: a step's collectives did not complete after %.1f s (timeout "
+                 "%.1f s); aborting the RCCL communicator and exiting with code %d\n",
+                 waited, timeout_s, exit_code);
     std::fflush(stderr);
-    if (comm) rc_api().abort(comm);
     for (volatile int* f : release) *f = 1;
-    // let the stream drain (aborted collectives and released kernels return), at most 5 s
-    hipEvent_t ev = pending.empty() ? nullptr : pending.front().first;
+    std::atomic<bool> aborted{false};
+    if (comm) {  // ncclCommAbort may block on the runtime: bounded wait, then exit regardless
+      ncclComm_t c = comm;
+      std::thread([c, &aborted] {
+        rc_api().abort(c);
+        aborted = true;
+      }).detach();
+    }
+    const unsigned long long want = pending.empty() ? 0 : pending.front().first;
     const auto t0 = std::chrono::steady_clock::now();
-    while (ev && hipEventQuery(ev) == hipErrorNotReady &&
-           std::chrono::steady_clock::now() - t0 < std::chrono::seconds(5))
+    while (std::chrono::steady_clock::now() - t0 < std::chrono::seconds(4) &&
+           !(aborted.load() && completed() >= want))
       std::this_thread::sleep_for(std::chrono::milliseconds(20));
     std::_Exit(exit_code);
   }
 
   void loop() {
-    (void)hipSetDevice(device);
     std::unique_lock<std::mutex> lk(mu);
     while (!stop) {
       cv.wait_for(lk, std::chrono::milliseconds(50));
-      while (!pending.empty()) {
-        auto& fr = pending.front();
-        const hipError_t q = hipEventQuery(fr.first);
-        const double waited =
-            std::chrono::duration<double>(std::chrono::steady_clock::now() - fr.second).count();
-        if (q == hipSuccess) {
-          pool.push_back(fr.first);
-          pending.pop_front();
-          continue;
-        }
-        if (q != hipErrorNotReady) fire(hipGetErrorString(q), waited);
-        if (waited > timeout_s) fire("a step's collectives did not complete", waited);
-        break;
+      const unsigned long long c = completed();
+      while (!pending.empty() && pending.front().first <= c) pending.pop_front();
+      if (!pending.empty()) {
+        const double waited = std::chrono::duration<double>(std::chrono::steady_clock::now() -
+                                                            pending.front().second).count();
+        if (waited > timeout_s) fire(waited);
       }
     }
   }
@@ -292,7 +301,11 @@ uintptr_t ew_rccl_watchdog_start(uintptr_t comm, int device, double timeout_s, i
   auto* w = new Watchdog();
   w->comm = comm ? rc_comm(comm) : nullptr;
   if (comm) rc_api();  // resolve ncclCommAbort now, not inside fire()
-  w->device = device;
+  EW_CHECK(hipSetDevice(device));
+  void* p = nullptr;
+  EW_CHECK(hipHostMalloc(&p, 64, hipHostMallocCoherent));
+  std::memset(p, 0, 64);
+  w->done = reinterpret_cast<unsigned long long*>(p);
   w->timeout_s = timeout_s;
   w->exit_code = exit_code;
   w->th = std::thread([w] { w->loop(); });
@@ -301,25 +314,23 @@ uintptr_t ew_rccl_watchdog_start(uintptr_t comm, int device, double timeout_s, i
 
 void ew_rccl_watch(uintptr_t h, uintptr_t stream) {
   Watchdog* w = wd_of(h);
-  hipEvent_t ev;
+  unsigned long long seq;
   {
     std::lock_guard<std::mutex> lk(w->mu);
-    if (w->pool.empty()) {
-      EW_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-    } else {
-      ev = w->pool.back();
-      w->pool.pop_back();
-    }
+    seq = ++w->issued;
+    w->pending.emplace_back(seq, std::chrono::steady_clock::now());
   }
-  EW_CHECK(hipEventRecord(ev, (hipStream_t)stream));
-  std::lock_guard<std::mutex> lk(w->mu);
-  w->pending.emplace_back(ev, std::chrono::steady_clock::now());
+  hipLaunchKernelGGL(k_watch_mark, dim3(1), dim3(1), 0, (hipStream_t)stream, w->done, seq);
+  EW_CHECK_LAUNCH();
 }
 
 int ew_rccl_watch_pending(uintptr_t h) {
   Watchdog* w = wd_of(h);
   std::lock_guard<std::mutex> lk(w->mu);
-  return (int)w->pending.size();
+  const unsigned long long c = w->completed();
+  int n = 0;
+  for (auto& p : w->pending) n += p.first > c;
+  return n;
 }
 
 void ew_rccl_watchdog_stop(uintptr_t h) {
@@ -330,8 +341,7 @@ void ew_rccl_watchdog_stop(uintptr_t h) {
   }
   w->cv.notify_all();
   if (w->th.joinable()) w->th.join();
-  for (auto& p : w->pending) (void)hipEventDestroy(p.first);
-  for (hipEvent_t e : w->pool) (void)hipEventDestroy(e);
+  (void)hipHostFree(w->done);
   delete w;
 }
 

@@ -72,6 +72,8 @@ struct DgcArgs {
   const float* param;
   float momentum, damp1, wd;
   int nesterov;
+  int mask;              // momentum factor masking (DGC) | keep the velocity (--ef-mode local)
+  const float* lr_ptr;   // nullable: accumulate lr-scaled updates (--ef-mode local)
 };
 
 // error-feedback mode of the encode: none, plain (e = g + r), momentum-corrected (DGC)
@@ -109,6 +111,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_hist0(GradPtrs gp, DgcArgs dg
     // momentum correction (oracle.dgc_accumulate, every product / sum rounded on its own):
     // g' = g + wd p ; u = m u + (1 - d) g' ; d = g' + m u (Nesterov) | u ; e = r + d
     float4 r[EW_CU], uv[EW_CU], pv[EW_CU];
+    const float lr = dg.lr_ptr ? *dg.lr_ptr : 1.0f;
     ew_ld_chunk(gp, resid, c, r);
     ew_ld_chunk(gp, dg.vel, c, uv);
     if (dg.wd != 0.0f) ew_ld_chunk(gp, dg.param, c, pv);  // uniform branch
@@ -130,6 +133,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_hist0(GradPtrs gp, DgcArgs dg
           const float mu = u4[j] * dg.momentum;
           d = g + mu;
         }
+        if (dg.lr_ptr) d = d * lr;
         e4[j] = r4[j] + d;
       }
       uv[u] = make_float4(u4[0], u4[1], u4[2], u4[3]);
@@ -494,6 +498,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_decode_apply(
     float* __restrict__ mom, float* __restrict__ grad_out, uint16_t* __restrict__ shadow,
     SgdArgs sa, int apply) {
   __shared__ float4 acc4[EW_CHUNK / 4];
+  ew_sgd_resolve(sa);
   __shared__ uint32_t s_off[EW_MAX_RANKS];
   __shared__ uint32_t ws[EW_WAVES];
   float* acc = reinterpret_cast<float*>(acc4);
@@ -644,7 +649,8 @@ void ew_topk_encode(const TopkEncodeArgs& a) {
   const float* src_flat = resid;  // passes after hist0 read the staged e = g + r under EF
   // each pass's per-tensor step (select / scan) runs in the tensor's last-arriving chunk block
   DgcArgs dg{reinterpret_cast<float*>(a.vel), reinterpret_cast<const float*>(a.param),
-             a.dgc_momentum, a.dgc_damp1, a.dgc_wd, a.dgc_nesterov};
+             a.dgc_momentum, a.dgc_damp1, a.dgc_wd, a.dgc_nesterov, a.dgc_mask,
+             reinterpret_cast<const float*>(a.dgc_lr_ptr)};
   if (dg.vel && !resid) throw std::runtime_error("ewdml topk: momentum correction needs a residual");
   if (dg.vel && dg.wd != 0.0f && !dg.param)
     throw std::runtime_error("ewdml topk: weight decay in the momentum correction needs params");
@@ -667,7 +673,7 @@ void ew_topk_encode(const TopkEncodeArgs& a) {
             inv, pay, a.scales_off, a.idx_off, a.codes_off, a.bitmap_off, a.levels, a.inv_levels,  \
             a.key,                                                                                   \
             reinterpret_cast<const uint32_t*>(a.key_ptr), a.bucket_offset, kmaxr, rezero_words,   \
-            dg.vel)
+            dg.mask ? dg.vel : nullptr)
   if (a.value_kind == VK_Q8) {
     if (resid) EW_WRITE(VK_Q8, true); else EW_WRITE(VK_Q8, false);
   } else if (a.value_kind == VK_Q4) {
@@ -692,6 +698,7 @@ void ew_topk_decode_apply(const TopkDecodeArgs& a) {
     throw std::runtime_error("ewdml topk decode: a momentum step needs the momentum buffer");
   SgdArgs sa{a.lr, a.momentum, a.dampening, a.weight_decay, a.grad_scale, a.nesterov, a.first,
              reinterpret_cast<uint32_t*>(a.key_state), a.key_seed, a.key_rank};
+  sa.lr_ptr = reinterpret_cast<const float*>(a.lr_ptr);
   auto* recv = reinterpret_cast<const uint8_t*>(a.recv);
   auto* p = reinterpret_cast<float*>(a.param);
   auto* m = reinterpret_cast<float*>(a.mom);

@@ -15,7 +15,53 @@ from .. import ops
 from ..compress import oracle
 
 
-class FlatSGD:
+class DeviceScalar:
+    """An fp32 scalar in device memory that the kernels read at run time (a captured HIP graph
+    keeps its kernels' arguments frozen, so a learning-rate schedule is fed through this), updated
+    by stream-ordered copies from a ring of pinned host slots (no host synchronisation)."""
+
+    def __init__(self, value: float, device):
+        self.t = torch.full((1,), float(value), dtype=torch.float32, device=device)
+        self._ring = [(torch.zeros(1, dtype=torch.float32).pin_memory(), None) for _ in range(8)]
+        self._slot = 0
+
+    def set(self, value: float):
+        host, ev = self._ring[self._slot]
+        if ev is not None:
+            ev.synchronize()  # the slot's previous copy has been consumed
+        host[0] = float(value)
+        self.t.copy_(host, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._ring[self._slot] = (host, ev)
+        self._slot = (self._slot + 1) % len(self._ring)
+
+
+class _LrMixin:
+    """``lr`` as a host value mirrored into ``lr_t`` (device) on the GPU."""
+
+    @property
+    def lr(self) -> float:
+        return self._lr
+
+    @lr.setter
+    def lr(self, value: float):
+        self._lr = float(value)
+        dev = getattr(self, "_lr_dev", None)
+        if dev is not None:
+            dev.set(self._lr)
+
+    @property
+    def lr_t(self):
+        dev = getattr(self, "_lr_dev", None)
+        return None if dev is None else dev.t
+
+    def _init_lr(self, lr, device):
+        self._lr_dev = DeviceScalar(lr, device) if device.type == "cuda" else None
+        self._lr = float(lr)
+
+
+class FlatSGD(_LrMixin):
     fusable = True
 
     def __init__(self, flat, lr=0.01, momentum=0.0, dampening=0.0, weight_decay=0.0,
@@ -23,7 +69,8 @@ class FlatSGD:
         if nesterov and (momentum <= 0 or dampening != 0):
             raise ValueError("Nesterov momentum requires a momentum and zero dampening")
         self.flat = flat
-        self.lr, self.momentum, self.dampening = lr, momentum, dampening
+        self._init_lr(lr, flat.data.device)
+        self.momentum, self.dampening = momentum, dampening
         self.weight_decay, self.nesterov = weight_decay, nesterov
         self.mom = torch.zeros_like(flat.data)
         self.steps = 0
@@ -34,7 +81,7 @@ class FlatSGD:
 
     def hparams(self) -> dict:
         return dict(lr=self.lr, momentum=self.momentum, dampening=self.dampening,
-                    weight_decay=self.weight_decay, nesterov=self.nesterov)
+                    weight_decay=self.weight_decay, nesterov=self.nesterov, lr_t=self.lr_t)
 
     def step_range(self, start: int, length: int, grad: torch.Tensor, grad_scale: float = 1.0):
         """Apply SGD to ``flat.data[start:start+length]`` with ``grad`` (same length) * scale."""
@@ -43,7 +90,7 @@ class FlatSGD:
         if p.is_cuda:
             sh = self.flat.shadow[start:start + length] if self.flat.shadow is not None else None
             ops.sgd_flat(p, m, grad, self.lr, self.momentum, self.dampening, self.weight_decay,
-                         grad_scale, self.nesterov, self.first, shadow=sh)
+                         grad_scale, self.nesterov, self.first, shadow=sh, lr_tensor=self.lr_t)
             return
         g = grad.to(torch.float32)
         if grad_scale != 1.0:
@@ -60,7 +107,8 @@ class FlatSGD:
         self.steps += 1
 
     def state_dict(self):
-        return {"kind": "sgd", "mom": self.mom, "steps": self.steps, **self.hparams()}
+        hp = {k: v for k, v in self.hparams().items() if k != "lr_t"}
+        return {"kind": "sgd", "mom": self.mom, "steps": self.steps, **hp}
 
     def load_state_dict(self, sd):
         self.mom.copy_(sd["mom"])
@@ -70,13 +118,14 @@ class FlatSGD:
                 setattr(self, k, sd[k])
 
 
-class FlatAdam:
+class FlatAdam(_LrMixin):
     fusable = False
 
     def __init__(self, flat, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0,
                  amsgrad=False):
         self.flat = flat
-        self.lr, self.betas, self.eps = lr, betas, eps
+        self._init_lr(lr, flat.data.device)
+        self.betas, self.eps = betas, eps
         self.weight_decay, self.amsgrad = weight_decay, amsgrad
         self.exp_avg = torch.zeros_like(flat.data)
         self.exp_avg_sq = torch.zeros_like(flat.data)
@@ -98,7 +147,7 @@ class FlatAdam:
             sh = self.flat.shadow[sl] if self.flat.shadow is not None else None
             ops.adam_flat(p, self.exp_avg[sl], self.exp_avg_sq[sl], vmax, grad, lr_step, b1, b2,
                           self.eps, self.weight_decay, grad_scale, self.amsgrad, shadow=sh,
-                          step=self.step_t, lr=self.lr)
+                          step=self.step_t, lr=self.lr, lr_tensor=self.lr_t)
             return
         g = grad.to(torch.float32) * grad_scale
         oracle.adam_apply(p, self.exp_avg[sl], self.exp_avg_sq[sl],

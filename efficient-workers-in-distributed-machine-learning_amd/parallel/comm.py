@@ -132,11 +132,13 @@ class Comm:
 
     def close(self):
         """Stop the watchdog and destroy the own communicator (the process group stays)."""
+        if self.watchdog is None and self.rccl is None:
+            return
+        torch.cuda.synchronize()  # pending watch marks write the watchdog's host memory
         if self.watchdog is not None:
             self._rc().rccl_watchdog_stop(self.watchdog)
             self.watchdog = None
         if self.rccl is not None:
-            torch.cuda.synchronize()
             self._rc().rccl_destroy(self.rccl)
             self.rccl = None
 

@@ -70,14 +70,22 @@ class GradientExchange:
         # momentum before top-k and keeps a per-rank velocity; the decode then steps without one.
         # Only for top-k codecs under momentum SGD (dense QSGD's residual holds just the rounding
         # error, and Adam has no velocity to correct): plain error feedback otherwise.
-        if ef_mode not in ("dgc", "plain"):
-            raise ValueError("ef_mode must be 'dgc' or 'plain'")
-        self.dgc = (self.resid is not None and ef_mode == "dgc"
-                    and codec.kind in ("topk", "topk_qsgd")
-                    and getattr(optimizer, "fusable", False)
-                    and getattr(optimizer, "momentum", 0.0) != 0.0)
-        self.ef_mode = None if self.resid is None else ("dgc" if self.dgc else "plain")
+        # local: the same sender-side momentum without masking and with the lr inside the
+        # residual (error feedback on the update).  ef21: EF21 -- every rank keeps a running
+        # estimate h of its gradient and sends top-k(g - h); all ranks add the average to a
+        # global estimate G and take an ordinary momentum step on G every step (no bursts).
+        if ef_mode not in ("dgc", "plain", "local", "ef21"):
+            raise ValueError("ef_mode must be 'dgc', 'plain', 'local' or 'ef21'")
+        topk = codec.kind in ("topk", "topk_qsgd")
+        sgd_m = (getattr(optimizer, "fusable", False)
+                 and getattr(optimizer, "momentum", 0.0) != 0.0)
+        self.dgc = self.resid is not None and ef_mode in ("dgc", "local") and topk and sgd_m
+        self.dgc_mask = ef_mode == "dgc"
+        self.ef21 = self.resid is not None and ef_mode == "ef21" and topk
+        self.ef_mode = None if self.resid is None else (
+            ef_mode if (self.dgc or self.ef21) else "plain")
         self.vel = torch.zeros_like(flat.grad) if self.dgc else None
+        self.gest = torch.zeros_like(flat.grad) if self.ef21 else None  # EF21's global G
         if not flat.attach_grads and not self.cuda:
             raise ValueError("pointer-mode gradients need the HIP kernels (device tensors)")
         self._pack_plans = [ops.DevicePlan(b.plan, self.device) for b in flat.buckets] \
@@ -229,10 +237,13 @@ class GradientExchange:
             o = self.opt
             dgc = dict(velocity=self.vel[b.start:b.start + b.length], momentum=o.momentum,
                        dampening=o.dampening, nesterov=o.nesterov, weight_decay=o.weight_decay,
-                       param=self.flat.data_view(b))
+                       param=self.flat.data_view(b), mask=self.dgc_mask,
+                       lr=None if self.dgc_mask else o.lr,
+                       lr_t=None if self.dgc_mask else getattr(o, "lr_t", None))
         self.codec.encode(bi, g, self.payload[bi], self.step_idx + self.seed_offset,
                           self.comm.rank, resid,
-                          key_tensor=self.key_dev if self.use_dev_key else None, dgc=dgc)
+                          key_tensor=self.key_dev if self.use_dev_key else None, dgc=dgc,
+                          ef21=self.ef21)
 
     def _collective(self, bi: int):
         if self.codec.allreduce:
@@ -312,12 +323,20 @@ class GradientExchange:
         else:
             for b in self.flat.buckets:
                 recv = self.recv[b.index].view(self.N, -1)
-                if getattr(opt, "fusable", False):
+                if self.ef21:  # G += mean of the sent differences; momentum step on G
+                    gv = self.flat.grad_view(b)
+                    self.codec.decode(b.index, recv, gv, scale)
+                    G = self.gest[b.start:b.start + b.length]
+                    G.add_(gv)
+                    opt.step_range(b.start, b.length, G, 1.0)
+                elif getattr(opt, "fusable", False):
                     adv = self.dev_key_advance and self.use_dev_key and b.index == self.nb - 1
                     hp, mom = opt.hparams(), opt.mom[b.start:b.start + b.length]
                     if self.dgc:  # momentum and weight decay already ran on the sender
                         hp = dict(hp, momentum=0.0, dampening=0.0, weight_decay=0.0,
                                   nesterov=False)
+                        if not self.dgc_mask:  # ... and the lr: p -= mean(sent)
+                            hp.update(lr=1.0, lr_t=None)
                         mom = None
                     self.codec.decode_apply_sgd(b.index, recv, scale, self.flat.data_view(b),
                                                 mom, hp, opt.first,

@@ -23,8 +23,8 @@ from ..models import build_model, canonical_name, input_shape
 from ..models.fused import set_enabled as set_fused_nn
 from ..optim.flat import make_optimizer
 from ..parallel.comm import Comm, init_distributed
-from ..parallel.engine import (GradientExchange, SegmentedCapture, Stopwatch, sync_buffers,
-                               sync_params)
+from ..parallel.engine import (GradientExchange, SegmentedCapture, StepStats, Stopwatch,
+                               sync_buffers, sync_params)
 from ..parallel.flat import FlatModel
 from ..parallel.local_sgd import LocalSGDExchange
 from ..parallel.ps import PSExchange
@@ -183,20 +183,25 @@ class Trainer:
                                                  cfg.select_best, score_fn=self._holdout_score)
         self.amp_dtype = {"bf16": torch.bfloat16, "fp16": torch.float16}.get(cfg.amp)
         self.graph_mode = cfg.hip_graph if (self.cuda and not cfg.sync_debug) else "off"
+        self.local_sgd = isinstance(self.exchange, LocalSGDExchange)
         if self.graph_mode == "auto":
-            # graphs wherever the step can be captured: the all-to-all exchange (the parameter
-            # server's k-of-n polling, local SGD's host-side best-worker choice and the sharded
-            # exchange run eagerly)
-            self.graph_mode = "full" if isinstance(self.exchange, GradientExchange) else "off"
-        if self.graph_mode != "off" and not isinstance(self.exchange, GradientExchange):
-            raise ValueError("--hip-graph needs the all-to-all topology without local SGD")
+            # graphs wherever the step can be captured: the all-to-all exchange, and local SGD's
+            # local steps (its sync steps -- compressed delta, host-side best-worker choice --
+            # run eagerly); the parameter server's k-of-n polling and the sharded exchange stay
+            # eager
+            self.graph_mode = ("full" if isinstance(self.exchange, GradientExchange)
+                               or self.local_sgd else "off")
+        if self.graph_mode != "off" and not (isinstance(self.exchange, GradientExchange) or
+                                             (self.local_sgd and self.graph_mode == "full")):
+            raise ValueError("--hip-graph needs the all-to-all topology (local SGD: full only)")
         if (self.graph_mode in ("full", "segmented") and self.comm.distributed
-                and self.comm.backend == "gloo"):
+                and self.comm.backend == "gloo" and not self.local_sgd):
             # gloo's CUDA collectives cannot be captured: graph the compute, issue them between
             self.graph_mode = "split"
         if self.graph_mode == "segmented":  # collectives on their own stream, beside backward
             self.exchange.comm_stream = torch.cuda.Stream(device=self.device)
         self._graphs = None
+        self.captures = 0  # graph captures so far (a schedule change should not force one)
         self._in_graph_batch = False
         self._key_synced = False
         # Graph mode: warmup, capture and replay all run on ONE dedicated stream, so MIOpen /
@@ -280,15 +285,17 @@ class Trainer:
             self.comm.close()
 
     def lr_at(self, step: int) -> float:
-        """Learning-rate schedule: linear warmup from lr/W over --lr-warmup-epochs (Horovod's
-        LearningRateWarmupCallback, tensorflow_mnist.py:65-66), then step decay."""
+        """Learning-rate schedule: linear warmup from lr/W (or --lr-warmup-start x lr) over
+        --lr-warmup-epochs (Horovod's LearningRateWarmupCallback, tensorflow_mnist.py:65-66;
+        Goyal et al.'s gradual warm-up), then step decay."""
         cfg = self.cfg
         spe = len(self.loader) if self.loader is not None else 1
         epoch = step / max(1, spe)
         lr = self.base_lr
         if cfg.lr_warmup_epochs > 0 and epoch < cfg.lr_warmup_epochs:
-            w = max(1, self.n_workers)
-            lr = lr / w + (lr - lr / w) * epoch / cfg.lr_warmup_epochs
+            lo = lr * cfg.lr_warmup_start if cfg.lr_warmup_start is not None \
+                else lr / max(1, self.n_workers)
+            lr = lo + (lr - lo) * epoch / cfg.lr_warmup_epochs
         for e in [float(v) for v in cfg.lr_decay_epochs.split(",") if v.strip()]:
             if epoch >= e:
                 lr *= cfg.lr_decay
@@ -320,9 +327,9 @@ class Trainer:
         if self.cfg.lr_warmup_epochs > 0 or self.cfg.lr_decay_epochs:
             lr = self.lr_at(self.step)
             if lr != self.opt.lr:
-                self.opt.lr = lr
-                if self._graphs is not None:  # the lr is a kernel argument of the graph
-                    self._graphs = None  # re-capture at this step (every rank: same schedule)
+                self.opt.lr = lr  # on the GPU also into the device lr the kernels read
+                if self._graphs is not None and getattr(self.opt, "lr_t", None) is None:
+                    self._graphs = None  # the lr is a kernel argument: re-capture (all ranks)
         if self.is_server:
             if not self.model.training:
                 self.model.train()
@@ -332,6 +339,8 @@ class Trainer:
         if not self.model.training:  # recursive; ~0.2 ms of host time per step otherwise
             self.model.train()
         graphed = self.graph_mode != "off" and self.step >= self.cfg.graph_warmup
+        if graphed and self.local_sgd and self.exchange.is_sync:
+            graphed = False  # the sync step (delta exchange, best-worker choice) runs eagerly
         if x is None and graphed and self.loader.fused:
             # the batch kernel is part of the graph: only the host-side epoch bookkeeping here
             if self._graphs is not None and not self._in_graph_batch:
@@ -392,6 +401,7 @@ class Trainer:
         graph per bucket on the comm stream, and the apply graph (``SegmentedCapture``): the
         collectives overlap the rest of backward."""
         ex = self.exchange
+        self.captures += 1
         self._in_graph_batch = x is None  # fused loader: the batch kernel is captured too
         if x is not None:
             self._gx = x.clone()
@@ -487,8 +497,8 @@ class Trainer:
         elif x is not self._gx:
             self._gx.copy_(x)
             self._gy.copy_(y)
-        if not self._key_synced:  # once per capture; the replays advance the key on the device
-            ex.set_device_key()
+        if not self._key_synced and not self.local_sgd:
+            ex.set_device_key()  # once per capture; the replays advance the key on the device
             self._key_synced = True
         if len(self._graphs) == 1:
             with self._range("graph_step"):
@@ -503,7 +513,7 @@ class Trainer:
             self._graphs[1].replay()
         ex.step_idx += 1
         self.opt.steps += 1
-        ex.last = self._gbytes
+        ex.last = StepStats() if self.local_sgd else self._gbytes  # a local step sends nothing
         self.step += 1
         return self._gloss, (self._gout, self._gy)
 
@@ -544,7 +554,8 @@ class Trainer:
         extra = {"config": {k: v for k, v in vars(self.cfg).items()
                             if isinstance(v, (int, float, str, bool)) or v is None},
                  "world": self.world}
-        for name, attr in (("ef_residual", "resid"), ("ef_velocity", "vel")):
+        for name, attr in (("ef_residual", "resid"), ("ef_velocity", "vel"),
+                           ("ef_global", "gest")):
             r = getattr(inner, attr, None)
             if r is not None:
                 # error-feedback residual / DGC velocity are per-rank state: keep every rank's row
@@ -586,7 +597,8 @@ class Trainer:
         self.step = int(st["step"])
         self.epoch = int(st["epoch"])
         inner = getattr(self.exchange, "inner", self.exchange)
-        for name, attr in (("ef_residual", "resid"), ("ef_velocity", "vel")):
+        for name, attr in (("ef_residual", "resid"), ("ef_velocity", "vel"),
+                           ("ef_global", "gest")):
             r = st["extra"].get(name)
             mine = getattr(inner, attr, None)
             if r is not None and mine is not None:

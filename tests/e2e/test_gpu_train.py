@@ -74,6 +74,25 @@ def test_segmented_graph_matches_full_graph(codec):
     assert torch.equal(full.flat.data, seg.flat.data)
 
 
+@pytest.mark.parametrize("opt", ["sgd", "adam"])
+def test_lr_schedule_in_graph_without_recapture(opt):
+    """The learning rate lives in device memory (optim/flat.py DeviceScalar): a warm-up schedule
+    changes it every step without re-capturing the step graph, and the trajectory follows the
+    eager run's."""
+    ops.require()
+    flags = LENET + ["--compress", "topk_qsgd", "--optimizer", opt, "--lr-warmup-epochs", "1",
+                     "--lr-warmup-start", "0.1", "--graph-warmup", "1"]
+    if opt == "adam":
+        flags += ["--compress", "none", "--lr", "0.001"]
+    ref, _ = _run(flags + ["--hip-graph", "off"], 12)
+    tr, _ = _run(flags + ["--hip-graph", "full"], 12)
+    assert tr.captures == 1 and tr._graphs is not None
+    assert float(tr.opt.lr_t.item()) == pytest.approx(tr.opt.lr)
+    assert tr.opt.lr < tr.base_lr  # still warming up
+    rel = float((tr.flat.data - ref.flat.data).norm() / ref.flat.data.norm())
+    assert rel < 1e-4, rel
+
+
 def test_graph_replay_refreshes_rng_key():
     """The QSGD rounding key lives in device memory and changes every replay."""
     tr, _ = _run(LENET + ["--compress", "topk_qsgd", "--hip-graph", "full"], 5)

@@ -1,8 +1,9 @@
 """The measured Methods 1-6 harness (tools/methods_eval.py): its byte column equals the packed
 layouts' (tools/methods_table.py, plus the flat buffer's alignment padding on dense legs) -- the
 wire counters of a real 1-server + 2-worker Gloo run
-move exactly the bytes the layouts predict; Method 6 adds the best-worker weight broadcast that
-the report's 0.066 MB LeNet figure leaves out."""
+move exactly the bytes the layouts predict.  Method 6 syncs compressed model deltas and adopts the
+best worker's delta out of the same all-gather (no weight broadcast; LeNet has no BN buffers), so
+it is Method 5's payload every 20 steps."""
 import os
 import sys
 
@@ -32,7 +33,6 @@ def test_methods_eval_bytes_match_layouts(method):
     if method <= 5:
         expect = static[method - 1] + dense_legs * pad
     else:
-        n = flat.numel * 4  # weights sent by the best rank
-        expect = (static[4] + 2 * n / MiB) / 20
+        expect = static[4] / 20
     assert r["MiB_per_iter"] == pytest.approx(expect, rel=1e-9)
     assert 0 < r["top1"] <= 100

@@ -180,7 +180,8 @@ def test_topk_error_feedback_matches_oracle():
 @pytest.mark.parametrize("kind,bits", [("topk_qsgd", 8), ("topk_qsgd", 4), ("topk", 8)])
 @pytest.mark.parametrize("wd,nesterov,damp", [(0.0, False, 0.0), (5e-4, False, 0.1),
                                               (1e-4, True, 0.0)])
-def test_topk_dgc_matches_oracle(kind, bits, wd, nesterov, damp):
+@pytest.mark.parametrize("mode", ["dgc", "local"])
+def test_topk_dgc_matches_oracle(kind, bits, wd, nesterov, damp, mode):
     """Momentum-corrected error feedback (DGC): velocity, residual and payload bitwise equal to
     oracle.dgc_accumulate + encode_topk over consecutive steps (the velocity is cleared at the
     sent coordinates, so the selection moves from step to step)."""
@@ -197,15 +198,20 @@ def test_topk_dgc_matches_oracle(kind, bits, wd, nesterov, damp):
         g = _grad(plan, seed=30 + it)
         key = stream_key(2, it, 1)
         hp = dict(momentum=0.9, dampening=damp, nesterov=nesterov, weight_decay=wd)
+        if mode == "local":  # no masking, lr-scaled residual (the device lr)
+            lr = 0.05 * (it + 1)
+            hp.update(mask=False, lr=lr)
         ref = oracle.encode_topk(g.clone(), plan, lay, levels, "max", key, residual=r_ref,
                                  dgc=dict(velocity=v_ref, param=p0, **hp))
+        lr_t = torch.tensor([hp.get("lr", 0.0)], dtype=torch.float32, device=DEV)
         ops.topk_encode(dp, g.to(DEV), pay, lay, levels, "max", key, resid=r_dev,
-                        dgc=dict(velocity=v_dev, param=p_dev, **hp))
+                        dgc=dict(velocity=v_dev, param=p_dev, lr_t=lr_t, **hp))
         assert torch.equal(pay.cpu(), ref), f"step {it}: payload"
         for off, n in zip(plan.offsets, plan.numels):
             assert torch.equal(r_dev.cpu()[off:off + n], r_ref[off:off + n]), f"step {it}: resid"
             assert torch.equal(v_dev.cpu()[off:off + n], v_ref[off:off + n]), f"step {it}: vel"
-        assert (v_ref == 0).sum() >= plan.total_k  # masked where sent
+        if mode == "dgc":
+            assert (v_ref == 0).sum() >= plan.total_k  # masked where sent
 
 
 def test_topk_decode_without_momentum_buffer():

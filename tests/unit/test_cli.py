@@ -65,3 +65,18 @@ def test_topology_choices():
 
     for t in ("allgather", "ps", "sharded"):
         assert ewdml.parse_args(["--topology", t]).topology == t
+
+
+def test_error_feedback_brings_its_warmup_recipe():
+    import ewdml
+
+    c = ewdml.parse_args(["--compress", "topk_qsgd", "--error-feedback", "--topk-ratio", "0.01"])
+    assert c.ef_mode == "dgc"
+    assert c.topk_warmup == "0.25,0.125,0.0625,0.03125,0.015625"
+    assert c.lr_warmup_epochs == 2.0 and c.lr_warmup_start == 0.1
+    c = ewdml.parse_args(["--compress", "topk_qsgd", "--error-feedback", "--ef-warmup", "none"])
+    assert c.topk_warmup == "" and c.lr_warmup_epochs == 0
+    c = ewdml.parse_args(["--compress", "topk_qsgd", "--error-feedback", "--topk-ratio", "0.4"])
+    assert c.topk_warmup == "" and c.lr_warmup_epochs == 0  # nothing denser to warm up from
+    c = ewdml.parse_args(["--compress", "topk_qsgd"])
+    assert c.topk_warmup == "" and c.lr_warmup_epochs == 0

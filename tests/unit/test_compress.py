@@ -257,3 +257,20 @@ def test_codec_set_ratio_replans():
     assert c.plans[0].ks == [25000, 1250] and c.payload_bytes(0) > 8 * n1
     c.set_ratio(0.01)
     assert c.payload_bytes(0) == n1 and c.plans[0].ks == [1000, 50]
+
+
+def test_ef21_estimate_tracks_the_gradient():
+    """EF21: h accumulates what was sent; with a constant gradient the estimate converges to it
+    (the difference g - h shrinks every step), so nothing is ever sent in bursts."""
+    plan = _plan([4000], 0.05)
+    lay = Layout.build("topk", plan, 8)
+    g = torch.randn(plan.length)
+    h = torch.zeros(plan.length)
+    G = torch.zeros(plan.length)
+    errs = []
+    for step in range(25):
+        pay = oracle.encode_topk(g.clone(), plan, lay, 127, "max", step, residual=h, ef21=True)
+        G += oracle.decode_sum(pay[None], plan, lay, 127, 1.0)
+        errs.append(float((g[:4000] - G[:4000]).norm()))
+    assert torch.equal(G, h)  # world of one: the global estimate is the local one
+    assert errs[-1] < 0.3 * errs[0] and all(b <= a + 1e-6 for a, b in zip(errs, errs[1:]))

@@ -157,14 +157,17 @@ def main(argv=None):
             "",
             "Notes on the byte column:",
             "",
-            "* Methods 1-3: dense legs move the flat buffer, i.e. the parameters plus 16-float "
-            "alignment padding per tensor (864 B for LeNet), hence the 0.002-0.003 MiB over the "
-            "layout column.",
-            "* Method 5: top-k values travel as int8 QSGD codes with u16 chunk-local indices "
-            "(3 B per kept element); the report's 1.312 MB counts 1 B per value and 1 B per index "
-            "(0.8 D at K = 0.4, BASELINE.md), so ours is 1.5x that figure by construction.",
-            "* Method 6: besides Method 5's payload every 20 steps, the best worker's weights are "
-            "broadcast at each sync (`--select-best`), which the report's 0.066 MB leaves out.",
+            "* Methods 1-4 move exactly the report's byte model (4 D, 2.5 D, 4 D, D with D the "
+            "dense fp32 gradient, 1.644 MiB for LeNet: BASELINE.md); the published 6.56 / 4.1 / "
+            "1.64 are those values read off the chart and rounded down.  Dense legs move the flat "
+            "buffer, i.e. the parameters plus 16-float alignment padding per tensor (864 B for "
+            "LeNet), hence the 0.002-0.003 MiB over the layout column.",
+            "* Method 5: at K = 0.4 a tensor's kept elements are indexed by a bitmap (1 bit per "
+            "element, `compress/plan.py`) instead of u16 offsets, so an int8 QSGD code plus its "
+            "index costs 0.525 B per element against the report's 0.8 B (1 B value + 1 B index).",
+            "* Method 6: compressed model deltas every 20 steps (`--sync-mode model`); the best "
+            "worker's delta is decoded out of the same all-gather, so adopting it moves no extra "
+            "weights (LeNet has no BN buffers to send).",
             "",
             "Accuracy curves (step: held-out top-1 %):", ""]
         for r in rows:
