@@ -138,6 +138,8 @@ def measure(a, world, amp, ef, extra=()):
     elapsed_max = tr.comm.all_reduce_scalars([t1 - t0], op="max")[0]
     final_loss = float(loss.detach()) if loss is not None else float("nan")
     tr.comm_kind = tr.comm.kind
+    g = getattr(tr, "_graphs", None)
+    tr.overlap_comm_graphs = len(g[1].comms) if (g and g[0] == "segmented") else 0
     tr.close()  # watchdog and own RCCL communicator (the next measure() builds its own)
     return elapsed_max, tr, final_loss, t_enq - t0
 
@@ -189,9 +191,12 @@ def main(argv=None):
                    "grad_mode": "views" if tr.flat.attach_grads else "pointers",
                    "layout": "nhwc" if tr.channels_last else "nchw",
                    "fused_nn": a.fused_nn, "comm": tr.comm_kind},
-        # overlap that actually happens: more than one bucket (the first collective is issued
-        # while backward still runs) and a collective to hide (world > 1)
-        "overlap_effective": bool(nb > 1 and not a.no_overlap and world > 1),
+        # overlap that actually happens: a collective to hide (world > 1) issued while backward
+        # still runs -- a segmented graph with at least one comm-stream graph, or eager steps
+        # with the side stream and more than one bucket
+        "overlap_effective": bool(world > 1 and not a.no_overlap and (
+            tr.overlap_comm_graphs > 0 or (tr.graph_mode == "off" and nb > 1))),
+        "overlap_comm_graphs": tr.overlap_comm_graphs,
         "grad_bytes_per_step_on_wire": bytes_["wire_bytes_total"],
         "payload_bytes_per_rank": bytes_["payload_bytes_per_rank"],
         "dense_fp32_grad_bytes": bytes_["dense_fp32_bytes"],

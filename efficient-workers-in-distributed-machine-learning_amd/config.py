@@ -88,6 +88,7 @@ class Config:
     ef_warmup: str = "auto"
     bucket_mb: float = 16.0
     overlap: bool = True
+    overlap_splits: int = 1  # --hip-graph segmented: comm graphs per step (split points)
     predivide: float = 1.0  # Horovod gradient_predivide_factor
     sync_bn: bool = False  # broadcast BN running stats from rank 0 at every checkpoint/eval
     # ---- optimizer -------------------------------------------------------------------------------
@@ -230,6 +231,7 @@ def build_parser(prog="distributed_nn.py") -> argparse.ArgumentParser:
     a("--ef-warmup", type=str, default=d.ef_warmup, choices=["auto", "none"])
     a("--bucket-mb", type=float, default=d.bucket_mb)
     a("--no-overlap", dest="overlap", action="store_false", default=True)
+    a("--overlap-splits", type=int, default=d.overlap_splits)
     a("--predivide", type=float, default=d.predivide)
     a("--sync-bn", "--sync-bn-buffers", dest="sync_bn", action="store_true", default=False)
     # optimizer

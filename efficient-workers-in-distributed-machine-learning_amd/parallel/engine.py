@@ -113,6 +113,7 @@ class GradientExchange:
         self._key_ring, self._key_slot = None, 0
         self._hooks = []
         self.seg = None  # SegmentedCapture while a segmented step capture is recording
+        self._final = False
         if overlap:
             for p in flat.params:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
@@ -204,11 +205,27 @@ class GradientExchange:
             flush_pending()
             assert not pending(), "deferred weight-gradient transform still pending at encode"
         if self.seg is not None:
-            def issue():
-                for bi in bis:
+            # segmented capture: buckets wait for the next split point (a byte threshold of the
+            # step's gradient); their encode + collective then become one comm-stream graph
+            # that overlaps the rest of backward.  Past the last split (and at the end of the
+            # backward pass) they are issued in-stream, into the current compute segment.
+            seg = self.seg
+            seg.pending += list(bis)
+            seg.ready_bytes += sum(4 * self.flat.buckets[bi].length for bi in bis)
+            if seg.want_split(self._final):
+                group = seg.pending
+                seg.pending = []
+
+                def issue():
+                    for bi in group:
+                        self._encode(bi)
+                        self._works[bi] = self._collective(bi)
+                seg.split(issue)
+            elif self._final or seg.splits_left == 0:
+                group, seg.pending = seg.pending, []
+                for bi in group:
                     self._encode(bi)
                     self._works[bi] = self._collective(bi)
-            self.seg.split(issue)
             return
         for bi in bis:
             with self._stream_ctx():
@@ -254,8 +271,12 @@ class GradientExchange:
 
     def launch_pending(self):
         rest = [bi for bi in range(self.nb) if not self._launched[bi]]
-        if rest:
-            self._launch_group(rest)
+        self._final = True  # backward is over: nothing left to overlap with
+        try:
+            if rest or (self.seg is not None and self.seg.pending):
+                self._launch_group(rest)
+        finally:
+            self._final = False
 
     def join_side(self):
         if self.side is not None:
@@ -402,14 +423,30 @@ class SegmentedCapture:
     (``horvod_pytorch.py:197-201``).  Captures use the relaxed mode: a split may end a capture
     begun on another thread (autograd's device thread runs the hooks)."""
 
-    def __init__(self, gstream, cstream, mode: str = "relaxed"):
+    def __init__(self, gstream, cstream, mode: str = "relaxed", total_bytes: int = 0,
+                 splits: int = 1):
         self.gs, self.cs, self.mode = gstream, cstream, mode
+        # split points: the first time the ready gradient bytes reach k / (splits + 1) of the
+        # step's total; each split costs a graph boundary and a stream hop, so a few large
+        # comm graphs beat one per bucket
+        self.thresholds = [total_bytes * k / (splits + 1) for k in range(1, splits + 1)]
+        self.pending, self.ready_bytes = [], 0
         self.pool = torch.cuda.graph_pool_handle()
         self.cpool = torch.cuda.graph_pool_handle()  # comm graphs run beside the segments
         self.segments, self.comms, self.apply = [], [], None
         self.cur = None
         self._evs = []
         self._done = torch.cuda.Event()
+
+    @property
+    def splits_left(self) -> int:
+        return len(self.thresholds) - len(self.comms)
+
+    def want_split(self, final: bool) -> bool:
+        """Split now?  Not at the end of backward (nothing left to overlap)."""
+        if final or not self.pending or self.splits_left <= 0:
+            return False
+        return self.ready_bytes >= self.thresholds[len(self.comms)]
 
     def begin(self):
         self.cur = torch.cuda.CUDAGraph()

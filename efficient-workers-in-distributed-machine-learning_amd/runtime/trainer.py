@@ -430,7 +430,9 @@ class Trainer:
                         raise
                 self._graphs = (g,)
             elif self.graph_mode == "segmented":
-                seg = SegmentedCapture(self.gstream, ex.comm_stream, mode="relaxed")
+                seg = SegmentedCapture(self.gstream, ex.comm_stream, mode="relaxed",
+                                       total_bytes=4 * self.flat.numel,
+                                       splits=self.cfg.overlap_splits)
                 ex.seg = seg
                 try:
                     seg.begin()

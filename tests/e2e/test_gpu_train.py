@@ -53,8 +53,8 @@ def test_adam_graph_matches_eager(opt):
         assert rel < 1e-4, f"{mode}: params differ from eager by {rel:.2e}"
 
 
-@pytest.mark.parametrize("codec", ["topk_qsgd", "none"])
-def test_segmented_graph_matches_full_graph(codec):
+@pytest.mark.parametrize("codec,splits", [("topk_qsgd", 2), ("none", 1), ("none", 3)])
+def test_segmented_graph_matches_full_graph(codec, splits):
     """--hip-graph segmented (linear compute segments split at bucket boundaries, per-bucket
     encode + collective graphs on the comm stream, apply graph): same kernels on the same data
     as the one-graph step, so the trajectory is bitwise the full graph's; the comm graphs are
@@ -63,12 +63,12 @@ def test_segmented_graph_matches_full_graph(codec):
     flags = ["--network", "VGG11", "--dataset", "Cifar10", "--batch-size", "32",
              "--synthetic-size", "512", "--momentum", "0.9", "--eval-freq", "0", "--quiet",
              "--device", "cuda", "--graph-warmup", "2", "--amp", "none", "--bucket-mb", "6",
-             "--compress", codec, "--error-feedback"]
+             "--compress", codec, "--error-feedback", "--ef-warmup", "none"]
     full, lf = _run(flags + ["--hip-graph", "full"], 7)
-    seg, ls = _run(flags + ["--hip-graph", "segmented"], 7)
+    seg, ls = _run(flags + ["--hip-graph", "segmented", "--overlap-splits", str(splits)], 7)
     assert seg.graph_mode == "segmented" and seg._graphs[0] == "segmented"
     sc = seg._graphs[1]
-    assert len(seg.flat.buckets) >= 3 and len(sc.comms) >= 2
+    assert len(seg.flat.buckets) >= 3 and 1 <= len(sc.comms) <= splits
     assert len(sc.segments) == len(sc.comms) + 1 and sc.apply is not None
     assert lf == ls
     assert torch.equal(full.flat.data, seg.flat.data)
