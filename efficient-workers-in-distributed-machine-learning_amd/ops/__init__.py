@@ -106,8 +106,16 @@ class DevicePlan:
         self.tensors = plan.tensor_table(device)
         self.chunks = plan.chunk_table(device)
         C, T = plan.num_chunks, plan.num_tensors
-        nbytes = max(require().topk_scratch_bytes(T, C), require().qsgd_scratch_bytes(T, C))
+        nbytes = max(require().topk_scratch_bytes(T, C, plan.length),
+                     require().qsgd_scratch_bytes(T, C))
         self.scratch = torch.zeros(nbytes, dtype=torch.uint8, device=device)
+
+
+def topk_lookback_errors(dp) -> int:
+    """Times a top-k write block gave up waiting on a predecessor's look-back word (bounded spin;
+    0 unless something is badly wrong).  Synchronises."""
+    return require().topk_lookback_errors(_ptr(dp.scratch), dp.plan.num_tensors,
+                                          dp.plan.num_chunks)
 
 
 def _check_bucket(dp, grad, name="grad"):
@@ -204,7 +212,7 @@ def topk_encode(dp: DevicePlan, grad, payload, layout, levels: int, norm: str, k
                   layout.scales, layout.counts, layout.idx, layout.codes, vk,
                   1 if norm == "l2" else 0, float(levels), float(1.0 / levels), key & 0xFFFFFFFF,
                   dp.plan.bucket_offset & 0xFFFFFFFF, _keyp(key_tensor), _stream(), _ptr(vel),
-                  _ptr(par), mom, damp1, wd, nest, layout.bitmap, dmask, _lrp(lrt))
+                  _ptr(par), mom, damp1, wd, nest, layout.bitmap, dmask, _lrp(lrt), dp.plan.length)
 
 
 def _lrp(lr_tensor):

@@ -19,6 +19,7 @@ PYBIND11_MODULE(_C, m) {
   m.attr("arch") = "gfx950";
 
   m.def("topk_scratch_bytes", &ew_topk_scratch_bytes);
+  m.def("topk_lookback_errors", &ew_topk_lookback_errors);
   m.def("qsgd_scratch_bytes", &ew_qsgd_scratch_bytes);
 
   m.def("topk_encode",
@@ -28,8 +29,10 @@ PYBIND11_MODULE(_C, m) {
            int value_kind, int norm_l2, float levels, float inv_levels, uint32_t key,
            uint32_t bucket_offset, uintptr_t key_ptr, uintptr_t stream, uintptr_t vel,
            uintptr_t param, float dgc_momentum, float dgc_damp1, float dgc_wd,
-           int dgc_nesterov, int bitmap_off, int dgc_mask, uintptr_t dgc_lr_ptr) {
+           int dgc_nesterov, int bitmap_off, int dgc_mask, uintptr_t dgc_lr_ptr,
+           long long bucket_len) {
           TopkEncodeArgs a{};
+          a.bucket_len = bucket_len;
           a.dgc_mask = dgc_mask;
           a.dgc_lr_ptr = dgc_lr_ptr;
           a.bitmap_off = bitmap_off;

@@ -26,6 +26,7 @@ struct TopkEncodeArgs {
   int dgc_nesterov;
   int dgc_mask;          // clear the velocity at sent coordinates (DGC) or keep it (local)
   uintptr_t dgc_lr_ptr;  // nullable device lr: residual accumulates lr-scaled updates
+  long long bucket_len;  // elements (sizes the candidate list in the scratch)
 };
 
 struct TopkDecodeArgs {
@@ -89,7 +90,8 @@ struct AdamFlatArgs {
   uintptr_t lr_ptr;  // nullable device fp32 base lr (overrides lr)
 };
 
-size_t ew_topk_scratch_bytes(int num_tensors, int num_chunks);
+size_t ew_topk_scratch_bytes(int num_tensors, int num_chunks, long long bucket_len);
+int ew_topk_lookback_errors(uintptr_t scratch, int num_tensors, int num_chunks);
 void ew_topk_encode(const TopkEncodeArgs& a);
 void ew_topk_decode_apply(const TopkDecodeArgs& a);
 

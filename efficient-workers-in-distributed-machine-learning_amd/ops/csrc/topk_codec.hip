@@ -15,9 +15,14 @@
 // threshold key and the number of threshold ties to keep are known; ties are kept lowest index
 // first, so every rank emits exactly k entries per tensor (fixed-size all-gather).
 //
-// Encode launches per bucket: hist0, hist1, hist2, count, write.  The per-tensor steps between
-// them (digit select after each histogram pass, tie allocation / offsets / scale after the count)
-// run in the tensor's last-arriving chunk block (topk_tensor_last), not as separate launches.
+// Encode launches per bucket: hist0, hist1, hist2, write (max-norm scale) or hist0, hist1, hist2,
+// count, write (L2 scale, which needs the selected values' sum of squares before quantising).
+// The per-tensor steps between them (digit select after each histogram pass, tie allocation /
+// offsets / scale after the count) run in the tensor's last-arriving chunk block
+// (topk_tensor_last), not as separate launches.  hist1 also compacts the keys that match the
+// selected top digit into a per-tensor candidate list, so hist2 reads a few % of the bucket instead
+// of all of it; with the max-norm scale the write pass finds its chunk's entry offset and tie
+// share by a decoupled look-back over the tensor's earlier chunks instead of a count pass.
 // The global state lives in one scratch block: zero-initialised once, histograms re-cleared by
 // k_topk_write after use, everything else fully rewritten per encode (no per-step memset).
 #include "common.h"
@@ -82,6 +87,7 @@ enum EfMode { EF_NONE = 0, EF_PLAIN = 1, EF_DGC = 2 };
 // state[t] = {prefix, k_rem, max_key, pad}
 template <int EFM>
 __global__ __launch_bounds__(EW_BLOCK) void k_topk_hist0(GradPtrs gp, DgcArgs dg,
+                                                         unsigned long long* __restrict__ lb,
                                                          float* __restrict__ resid,
                                                          const ChunkRow* __restrict__ chunks,
                                                          uint32_t* __restrict__ hist,
@@ -98,6 +104,8 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_hist0(GradPtrs gp, DgcArgs dg
   __syncthreads();
   uint32_t* h = hs + (threadIdx.x & (HSUB - 1));
   const ChunkRow c = chunks[blockIdx.x];
+  // the write pass's look-back word of this chunk, from the previous encode (stream-ordered)
+  if (threadIdx.x == 0) lb[blockIdx.x] = 0ull;
   float4 v[EW_CU];
   ew_ld_chunk(gp, nullptr, c, v);
   if (EFM == EF_PLAIN) {  // error feedback: compress e = g + residual, staged in the residual
@@ -175,37 +183,94 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_hist0(GradPtrs gp, DgcArgs dg
     topk_select<NB0, 20, true>(hist, tensors, state, kmaxr, T, c.tensor);
 }
 
-// Histogram of key bits [SHIFT+9 : SHIFT] over elements whose bits above MATCH equal the prefix.
-template <int SHIFT, int MATCH>
-__global__ __launch_bounds__(EW_BLOCK) void k_topk_hist(GradPtrs gp, const float* __restrict__ flat,
-                                                        const ChunkRow* __restrict__ chunks,
-                                                        uint32_t* __restrict__ state,
-                                                        uint32_t* __restrict__ hist, int T,
-                                                        const TensorRow* __restrict__ tensors,
-                                                        const uint32_t* __restrict__ kmaxr,
-                                                        int* __restrict__ tick) {
+// Histogram of key bits [19:10] over the elements whose top 11 bits equal the selected digit; those
+// keys (the candidates of the last pass) are appended to the tensor's candidate list
+// cand[tensor.off + 0 .. cand_n), at most numel of them, in no particular order.
+__global__ __launch_bounds__(EW_BLOCK) void k_topk_hist1(GradPtrs gp, const float* __restrict__ flat,
+                                                         const ChunkRow* __restrict__ chunks,
+                                                         uint32_t* __restrict__ state,
+                                                         uint32_t* __restrict__ hist, int T,
+                                                         const TensorRow* __restrict__ tensors,
+                                                         const uint32_t* __restrict__ kmaxr,
+                                                         int* __restrict__ tick,
+                                                         uint32_t* __restrict__ cand,
+                                                         int* __restrict__ cand_n) {
   __shared__ uint32_t h[NB1];
+  __shared__ uint32_t ws[EW_WAVES];
+  __shared__ uint32_t s_base;
   for (int i = threadIdx.x; i < NB1; i += EW_BLOCK) h[i] = 0;
   __syncthreads();
   const ChunkRow c = chunks[blockIdx.x];
-  const uint32_t want = state[c.tensor * 4] >> MATCH;
+  const uint32_t want = state[c.tensor * 4] >> 20;
   float4 v[EW_CU];
   ew_ld_chunk(gp, flat, c, v);
+  uint32_t nm = 0;
 #pragma unroll
   for (int u = 0; u < EW_CU; ++u) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const uint32_t k = ew_key(ew_f4(v[u], j));
-      if (ew_chunk_idx(u) + j < c.len && (k >> MATCH) == want)
-        atomicAdd(&h[(k >> SHIFT) & (NB1 - 1)], 1u);
+      if (ew_chunk_idx(u) + j < c.len && (k >> 20) == want) {
+        atomicAdd(&h[(k >> 10) & (NB1 - 1)], 1u);
+        ++nm;
+      }
     }
   }
+  uint32_t tot;
+  const uint32_t ex = ew_block_excl_scan(nm, ws, tot);  // contains __syncthreads
+  if (threadIdx.x == 0 && tot)
+    s_base = (uint32_t)atomicAdd(cand_n + TICK_STRIDE * c.tensor, (int)tot);
   __syncthreads();
+  if (nm) {
+    uint32_t* dst = cand + tensors[c.tensor].off + s_base + ex;
+#pragma unroll
+    for (int u = 0; u < EW_CU; ++u) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t k = ew_key(ew_f4(v[u], j));
+        if (ew_chunk_idx(u) + j < c.len && (k >> 20) == want) *dst++ = k;
+      }
+    }
+  }
   uint32_t* dst = hist + ((size_t)(blockIdx.x & (NREP - 1)) * T + c.tensor) * NB1;
   for (int i = threadIdx.x; i < NB1; i += EW_BLOCK)
     if (h[i]) atomicAdd(&dst[i], h[i]);
   if (topk_tensor_last(tick + TICK_STRIDE * c.tensor, tensors[c.tensor].nchunks, reinterpret_cast<int*>(h)))
-    topk_select<NB1, SHIFT, false>(hist, tensors, state, kmaxr, T, c.tensor);
+    topk_select<NB1, 10, false>(hist, tensors, state, kmaxr, T, c.tensor);
+}
+
+// Histogram of key bits [9:0] over the tensor's candidates matching the 21-bit prefix: the block of
+// chunk j reads candidates [8192 j, 8192 (j + 1)) of its tensor's list (most blocks have none).
+// The tensor's last block selects the threshold and resets the candidate count for the next encode.
+__global__ __launch_bounds__(EW_BLOCK) void k_topk_hist2(const ChunkRow* __restrict__ chunks,
+                                                         uint32_t* __restrict__ state,
+                                                         uint32_t* __restrict__ hist, int T,
+                                                         const TensorRow* __restrict__ tensors,
+                                                         const uint32_t* __restrict__ kmaxr,
+                                                         int* __restrict__ tick,
+                                                         const uint32_t* __restrict__ cand,
+                                                         int* __restrict__ cand_n) {
+  __shared__ uint32_t h[NB2];
+  for (int i = threadIdx.x; i < NB2; i += EW_BLOCK) h[i] = 0;
+  __syncthreads();
+  const ChunkRow c = chunks[blockIdx.x];
+  const uint32_t want = state[c.tensor * 4] >> 10;
+  const int n = __hip_atomic_load(cand_n + TICK_STRIDE * c.tensor, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t* src = cand + tensors[c.tensor].off;
+  const int i1 = min(n, (c.local + 1) * EW_CHUNK);
+  for (int i = c.local * EW_CHUNK + (int)threadIdx.x; i < i1; i += EW_BLOCK) {
+    const uint32_t k = src[i];
+    if ((k >> 10) == want) atomicAdd(&h[k & (NB2 - 1)], 1u);
+  }
+  __syncthreads();
+  uint32_t* dst = hist + ((size_t)(blockIdx.x & (NREP - 1)) * T + c.tensor) * NB2;
+  for (int i = threadIdx.x; i < NB2; i += EW_BLOCK)
+    if (h[i]) atomicAdd(&dst[i], h[i]);
+  if (topk_tensor_last(tick + TICK_STRIDE * c.tensor, tensors[c.tensor].nchunks, reinterpret_cast<int*>(h))) {
+    topk_select<NB2, 0, false>(hist, tensors, state, kmaxr, T, c.tensor);
+    if (threadIdx.x == 0) cand_n[TICK_STRIDE * c.tensor] = 0;  // every block read it before arriving
+  }
 }
 
 template <int NB, int SHIFT, bool FIRST>
@@ -365,7 +430,15 @@ __device__ __forceinline__ void topk_scan(
 enum ValueKind { VK_Q8 = 0, VK_Q4 = 1, VK_F32 = 2 };
 
 // Ordered stream compaction of the selected entries of one chunk + fused quantisation.
-template <int VK, bool EF>
+// Decoupled look-back word of a chunk: status (1 = its own counts, 2 = inclusive prefix over the
+// tensor's chunks up to it) | #(key > thr) | #(key == thr), 31 bits each.
+constexpr unsigned long long LB_AGG = 1ull << 62, LB_INC = 2ull << 62;
+constexpr unsigned long long LB_SPIN_TICKS = 20000000ull;  // 0.2 s of the 100 MHz clock: never hang
+__device__ __forceinline__ unsigned long long lb_pack(uint32_t gt, uint32_t eq) {
+  return ((unsigned long long)gt << 31) | (unsigned long long)eq;
+}
+
+template <int VK, bool EF, bool LB>
 __global__ __launch_bounds__(EW_BLOCK) void k_topk_write(
     GradPtrs gp, float* __restrict__ resid, const ChunkRow* __restrict__ chunks,
     const TensorRow* __restrict__ tensors, const uint32_t* __restrict__ state,
@@ -374,8 +447,10 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_write(
     int codes_off, int bitmap_off, float levels, float inv_levels, uint32_t key_arg,
     const uint32_t* __restrict__ keyp,
     uint32_t bucket_offset, uint32_t* __restrict__ rezero, uint32_t rezero_words,
-    float* __restrict__ vel) {
+    float* __restrict__ vel, unsigned long long* __restrict__ lb, int counts_off,
+    int* __restrict__ lb_err) {
   __shared__ uint32_t ws[EW_WAVES];
+  __shared__ uint32_t s_lb[2 * EW_WAVES];
   // the histograms / max-key replicas are dead once the thresholds are selected: clear them here
   // for the next encode of this bucket (replaces a per-step memset node; first use: zero-alloc)
   for (uint32_t i = blockIdx.x * EW_BLOCK + threadIdx.x; i < rezero_words; i += gridDim.x * EW_BLOCK)
@@ -385,12 +460,89 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_write(
   const TensorRow tr = tensors[c.tensor];
   const float* flat = EF ? resid : nullptr;  // EF: hist0 staged e = g + r in the residual
   const uint32_t thr = state[c.tensor * 4];
-  const uint32_t ties = chunk_ties[blockIdx.x];
-  const uint32_t ebase = (uint32_t)tr.entry0 + chunk_off[blockIdx.x];
   const uint32_t eend = (uint32_t)(tr.entry0 + tr.k);  // never write past this tensor's entries
-  const float inv = inv_arr[c.tensor];
-  float step = 0.0f;
-  if (VK != VK_F32) step = reinterpret_cast<const float*>(payload + scales_off)[c.tensor] * inv_levels;
+  float4 v[EW_CU];
+  ew_ld_chunk(gp, flat, c, v);
+  uint32_t ties, ebase;
+  float inv, step = 0.0f;
+  if (LB) {
+    // this chunk's #(key > thr) and #(key == thr), then the exclusive prefix over the tensor's
+    // earlier chunks by decoupled look-back: the entry offset and the chunk's share of the
+    // threshold ties (lowest index first) without a counting pass
+    uint32_t gt = 0, eq = 0;
+#pragma unroll
+    for (int u = 0; u < EW_CU; ++u) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t k = ew_key(ew_f4(v[u], j));
+        const bool ok = ew_chunk_idx(u) + j < c.len;
+        gt += ok && k > thr;
+        eq += ok && k == thr;
+      }
+    }
+    gt = ew_wave_sum_u(gt);
+    eq = ew_wave_sum_u(eq);
+    if ((threadIdx.x & 63) == 0) {
+      s_lb[threadIdx.x >> 6] = gt;
+      s_lb[EW_WAVES + (threadIdx.x >> 6)] = eq;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      gt = eq = 0;
+      for (int w = 0; w < EW_WAVES; ++w) {
+        gt += s_lb[w];
+        eq += s_lb[EW_WAVES + w];
+      }
+      unsigned long long* my = lb + blockIdx.x;
+      uint32_t gb = 0, eb = 0;
+      if (c.local == 0) {
+        __hip_atomic_store(my, LB_INC | lb_pack(gt, eq), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        __hip_atomic_store(my, LB_AGG | lb_pack(gt, eq), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // predecessors are earlier blocks of this launch (chunk rows of a tensor are consecutive
+        // and dispatched in order), so they are resident or done; the spin is still bounded
+        int p = (int)blockIdx.x - 1;
+        const unsigned long long t0 = wall_clock64();
+        while (true) {
+          const unsigned long long w =
+              __hip_atomic_load(lb + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const unsigned long long st = w & (3ull << 62);
+          if (st == 0) {
+            if (wall_clock64() - t0 > LB_SPIN_TICKS) {
+              atomicAdd(lb_err, 1);
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+          }
+          gb += (uint32_t)(w >> 31) & 0x7fffffffu;
+          eb += (uint32_t)w & 0x7fffffffu;
+          if (st == LB_INC || p == tr.chunk0) break;
+          --p;
+        }
+        __hip_atomic_store(my, LB_INC | lb_pack(gb + gt, eb + eq), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      }
+      const uint32_t need = state[c.tensor * 4 + 1];
+      const uint32_t tc = need > eb ? min(need - eb, eq) : 0u;
+      s_lb[0] = tc;
+      s_lb[1] = gb + min(eb, need);
+      reinterpret_cast<uint16_t*>(payload + counts_off)[blockIdx.x] = (uint16_t)(gt + tc);
+    }
+    __syncthreads();
+    ties = s_lb[0];
+    ebase = (uint32_t)tr.entry0 + s_lb[1];
+    // max-norm scale: the largest selected |e| is the tensor's max key (hist0)
+    const float scale = __uint_as_float(state[c.tensor * 4 + 2]);
+    inv = scale > 0.0f ? levels / scale : 0.0f;
+    if (VK != VK_F32) step = scale * inv_levels;
+    if (threadIdx.x == 0 && c.local == 0) reinterpret_cast<float*>(payload + scales_off)[c.tensor] = scale;
+  } else {
+    ties = chunk_ties[blockIdx.x];
+    ebase = (uint32_t)tr.entry0 + chunk_off[blockIdx.x];
+    inv = inv_arr[c.tensor];
+    if (VK != VK_F32) step = reinterpret_cast<const float*>(payload + scales_off)[c.tensor] * inv_levels;
+  }
   // entries' indices: the tensor's u16 list (chunk-local offsets), or its bitmap (one bit per
   // element; a wave's 256 elements of a slab are 8 whole words)
   const bool bitmap = tr.bm0 >= 0;
@@ -400,8 +552,6 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_write(
                      (bitmap ? tr.bm0 + c.local * EW_BM_WORDS : 0);
   const uint32_t gbase = bucket_offset + (uint32_t)c.start;
   uint32_t carry_gt = 0, carry_eq = 0;
-  float4 v[EW_CU];
-  ew_ld_chunk(gp, flat, c, v);
 #pragma unroll
   for (int u = 0; u < EW_CU; ++u) {
     if (u * 4 * EW_BLOCK >= c.len) break;  // uniform
@@ -634,9 +784,15 @@ void ew_topk_encode(const TopkEncodeArgs& a) {
   float* chunk_sq = reinterpret_cast<float*>(chunk_ties + C);
   float* inv = chunk_sq + C;
   // [4][T] per-pass tensor tickets, one 128-B line each (blocks of different tensors must not
-  // serialise on one line's atomics)
+  // serialise on one line's atomics), then [T] candidate counts (same stride), the look-back error
+  // counter, the look-back words u64[C] and the candidate keys u32[L]
   int* tick = reinterpret_cast<int*>(
       (reinterpret_cast<uintptr_t>(inv + T) + TICK_STRIDE * 4 - 1) & ~(uintptr_t)(TICK_STRIDE * 4 - 1));
+  int* cand_n = tick + 4 * TICK_STRIDE * T;
+  int* lb_err = cand_n + TICK_STRIDE * T;
+  auto* lb = reinterpret_cast<unsigned long long*>(lb_err + TICK_STRIDE);
+  uint32_t* cand = reinterpret_cast<uint32_t*>(lb + C);
+  if (a.bucket_len <= 0) throw std::runtime_error("ewdml topk: bucket length missing");
   hipStream_t s = (hipStream_t)a.stream;
   // no scratch memset: state / count sections are fully rewritten each encode, and the histogram
   // replicas are cleared by k_topk_write for the next one (zero-initialised at allocation)
@@ -655,40 +811,66 @@ void ew_topk_encode(const TopkEncodeArgs& a) {
   if (dg.vel && dg.wd != 0.0f && !dg.param)
     throw std::runtime_error("ewdml topk: weight decay in the momentum correction needs params");
   if (dg.vel)
-    EW_LAUNCH(k_topk_hist0<EF_DGC>, C, s, g, dg, resid, chunks, hist0, kmaxr, T, tensors, state, tick);
+    EW_LAUNCH(k_topk_hist0<EF_DGC>, C, s, g, dg, lb, resid, chunks, hist0, kmaxr, T, tensors, state,
+              tick);
   else if (resid)
-    EW_LAUNCH(k_topk_hist0<EF_PLAIN>, C, s, g, dg, resid, chunks, hist0, kmaxr, T, tensors, state, tick);
+    EW_LAUNCH(k_topk_hist0<EF_PLAIN>, C, s, g, dg, lb, resid, chunks, hist0, kmaxr, T, tensors,
+              state, tick);
   else
-    EW_LAUNCH(k_topk_hist0<EF_NONE>, C, s, g, dg, resid, chunks, hist0, kmaxr, T, tensors, state, tick);
-  EW_LAUNCH((k_topk_hist<10, 20>), C, s, g, src_flat, chunks, state, hist1, T, tensors, kmaxr,
-            tick + TICK_STRIDE * T);
-  EW_LAUNCH((k_topk_hist<0, 10>), C, s, g, src_flat, chunks, state, hist2, T, tensors, kmaxr,
-            tick + 2 * TICK_STRIDE * T);
+    EW_LAUNCH(k_topk_hist0<EF_NONE>, C, s, g, dg, lb, resid, chunks, hist0, kmaxr, T, tensors, state,
+              tick);
+  EW_LAUNCH(k_topk_hist1, C, s, g, src_flat, chunks, state, hist1, T, tensors, kmaxr,
+            tick + TICK_STRIDE * T, cand, cand_n);
+  EW_LAUNCH(k_topk_hist2, C, s, chunks, state, hist2, T, tensors, kmaxr, tick + 2 * TICK_STRIDE * T,
+            cand, cand_n);
   auto* pay = reinterpret_cast<uint8_t*>(a.payload);
-  EW_LAUNCH(k_topk_count, C, s, g, src_flat, chunks, state, cnt_gt, cnt_eq, chunk_sq, tensors,
-            tick + 3 * TICK_STRIDE * T, chunk_off, chunk_ties, inv, pay, a.scales_off, a.counts_off, a.levels,
-            a.norm_l2);
-#define EW_WRITE(VK, EFV)                                                                          \
-  EW_LAUNCH((k_topk_write<VK, EFV>), C, s, g, resid, chunks, tensors, state, chunk_off, chunk_ties, \
-            inv, pay, a.scales_off, a.idx_off, a.codes_off, a.bitmap_off, a.levels, a.inv_levels,  \
-            a.key,                                                                                   \
-            reinterpret_cast<const uint32_t*>(a.key_ptr), a.bucket_offset, kmaxr, rezero_words,   \
-            dg.mask ? dg.vel : nullptr)
+  // the L2 scale needs the selected values' sum of squares before any code is written: a count
+  // pass; the max-norm scale is hist0's max key and the write pass looks back for its offsets
+  const bool lbk = !a.norm_l2;
+  if (!lbk)
+    EW_LAUNCH(k_topk_count, C, s, g, src_flat, chunks, state, cnt_gt, cnt_eq, chunk_sq, tensors,
+              tick + 3 * TICK_STRIDE * T, chunk_off, chunk_ties, inv, pay, a.scales_off, a.counts_off,
+              a.levels, a.norm_l2);
+#define EW_WRITE(VK, EFV, LBV)                                                                     \
+  EW_LAUNCH((k_topk_write<VK, EFV, LBV>), C, s, g, resid, chunks, tensors, state, chunk_off,        \
+            chunk_ties, inv, pay, a.scales_off, a.idx_off, a.codes_off, a.bitmap_off, a.levels,     \
+            a.inv_levels, a.key, reinterpret_cast<const uint32_t*>(a.key_ptr), a.bucket_offset,     \
+            kmaxr, rezero_words, dg.mask ? dg.vel : nullptr, lb, a.counts_off, lb_err)
+#define EW_WRITE2(VK, EFV) \
+  do { if (lbk) EW_WRITE(VK, EFV, true); else EW_WRITE(VK, EFV, false); } while (0)
   if (a.value_kind == VK_Q8) {
-    if (resid) EW_WRITE(VK_Q8, true); else EW_WRITE(VK_Q8, false);
+    if (resid) EW_WRITE2(VK_Q8, true); else EW_WRITE2(VK_Q8, false);
   } else if (a.value_kind == VK_Q4) {
-    if (resid) EW_WRITE(VK_Q4, true); else EW_WRITE(VK_Q4, false);
+    if (resid) EW_WRITE2(VK_Q4, true); else EW_WRITE2(VK_Q4, false);
   } else {
-    if (resid) EW_WRITE(VK_F32, true); else EW_WRITE(VK_F32, false);
+    if (resid) EW_WRITE2(VK_F32, true); else EW_WRITE2(VK_F32, false);
   }
+#undef EW_WRITE2
 #undef EW_WRITE
   EW_CHECK_LAUNCH();
 }
 
-size_t ew_topk_scratch_bytes(int T, int C) {
+size_t ew_topk_scratch_bytes(int T, int C, long long L) {
+  // state .. inv, alignment slack + tickets + candidate counts + error counter, look-back words,
+  // candidate keys
   return sizeof(uint32_t) *
-         ((size_t)4 * T + (size_t)NREP * T * (1 + NB0 + NB1 + NB2) + 5 * (size_t)C + T +
-          (4 * (size_t)T + 1) * TICK_STRIDE);
+             ((size_t)4 * T + (size_t)NREP * T * (1 + NB0 + NB1 + NB2) + 5 * (size_t)C + T +
+              (5 * (size_t)T + 2) * TICK_STRIDE + (size_t)L) +
+         sizeof(unsigned long long) * (size_t)C + 128;
+}
+
+int ew_topk_lookback_errors(uintptr_t scratch, int T, int C) {
+  // same carving as ew_topk_encode
+  uint32_t* state = reinterpret_cast<uint32_t*>(scratch);
+  uint32_t* kmaxr = state + 4 * T;
+  uint32_t* hist2 = kmaxr + NREP * T + (size_t)NREP * T * NB0 + (size_t)NREP * T * NB1;
+  float* inv = reinterpret_cast<float*>(hist2 + (size_t)NREP * T * NB2 + 5 * (size_t)C);
+  int* tick = reinterpret_cast<int*>(
+      (reinterpret_cast<uintptr_t>(inv + T) + TICK_STRIDE * 4 - 1) & ~(uintptr_t)(TICK_STRIDE * 4 - 1));
+  int* lb_err = tick + 5 * TICK_STRIDE * T;
+  int v = 0;
+  EW_CHECK(hipMemcpy(&v, lb_err, sizeof(int), hipMemcpyDeviceToHost));
+  return v;
 }
 
 void ew_topk_decode_apply(const TopkDecodeArgs& a) {

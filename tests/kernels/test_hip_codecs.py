@@ -74,6 +74,8 @@ def test_topk_repeated_encodes_reuse_scratch():
         ref = oracle.encode_topk(g.clone(), plan, lay, 127, "max", key)
         ops.topk_encode(dp, g.to(DEV), pay, lay, 127, "max", key)
         assert torch.equal(pay.cpu(), ref), f"encode {it} differs"
+    # the write pass's look-back (max-norm scale) never had to give up on a predecessor
+    assert ops.topk_lookback_errors(dp) == 0
 
 
 def test_topk_ties_exact_count():
