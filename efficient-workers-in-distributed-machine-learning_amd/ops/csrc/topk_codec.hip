@@ -487,7 +487,8 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_write(
       s_lb[EW_WAVES + (threadIdx.x >> 6)] = eq;
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (threadIdx.x < 64) {  // wave 0: publish, then look back 64 predecessors at a time
+      const int lane = threadIdx.x;
       gt = eq = 0;
       for (int w = 0; w < EW_WAVES; ++w) {
         gt += s_lb[w];
@@ -495,43 +496,61 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_write(
       }
       unsigned long long* my = lb + blockIdx.x;
       uint32_t gb = 0, eb = 0;
-      if (c.local == 0) {
-        __hip_atomic_store(my, LB_INC | lb_pack(gt, eq), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      } else {
-        __hip_atomic_store(my, LB_AGG | lb_pack(gt, eq), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane == 0)
+        __hip_atomic_store(my, (c.local == 0 ? LB_INC : LB_AGG) | lb_pack(gt, eq),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (c.local > 0) {
         // predecessors are earlier blocks of this launch (chunk rows of a tensor are consecutive
         // and dispatched in order), so they are resident or done; the spin is still bounded
         int p = (int)blockIdx.x - 1;
         const unsigned long long t0 = wall_clock64();
         while (true) {
-          const unsigned long long w =
-              __hip_atomic_load(lb + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const int q = p - lane;  // lane 0: the nearest predecessor
+          // the tensor's first chunk always publishes an inclusive word: nothing before it
+          const unsigned long long w = q >= tr.chunk0
+              ? __hip_atomic_load(lb + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+              : LB_INC;
           const unsigned long long st = w & (3ull << 62);
-          if (st == 0) {
+          const unsigned long long inc = __ballot(st == LB_INC);
+          const unsigned long long none = __ballot(st == 0);
+          const int last = inc ? __ffsll((long long)inc) - 1 : 63;  // lanes 0..last contribute
+          const unsigned long long need_mask = last == 63 ? ~0ull : ((2ull << last) - 1ull);
+          if (none & need_mask) {  // a predecessor not published yet: read the window again
             if (wall_clock64() - t0 > LB_SPIN_TICKS) {
-              atomicAdd(lb_err, 1);
+              if (lane == 0) atomicAdd(lb_err, 1);
               break;
             }
             __builtin_amdgcn_s_sleep(1);
             continue;
           }
-          gb += (uint32_t)(w >> 31) & 0x7fffffffu;
-          eb += (uint32_t)w & 0x7fffffffu;
-          if (st == LB_INC || p == tr.chunk0) break;
-          --p;
+          const bool use = lane <= last;
+          const uint32_t wg = use ? ((uint32_t)(w >> 31) & 0x7fffffffu) : 0u;
+          const uint32_t we = use ? ((uint32_t)w & 0x7fffffffu) : 0u;
+          gb += ew_wave_sum_u(wg);  // valid in lane 0
+          eb += ew_wave_sum_u(we);
+          if (inc) break;
+          p -= 64;
         }
-        __hip_atomic_store(my, LB_INC | lb_pack(gb + gt, eb + eq), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0)
+          __hip_atomic_store(my, LB_INC | lb_pack(gb + gt, eb + eq), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
       }
-      const uint32_t need = state[c.tensor * 4 + 1];
-      const uint32_t tc = need > eb ? min(need - eb, eq) : 0u;
-      s_lb[0] = tc;
-      s_lb[1] = gb + min(eb, need);
-      reinterpret_cast<uint16_t*>(payload + counts_off)[blockIdx.x] = (uint16_t)(gt + tc);
+      if (lane == 0) {
+        s_lb[0] = gb;
+        s_lb[1] = eb;
+        s_lb[2] = gt;
+        s_lb[3] = eq;
+      }
     }
     __syncthreads();
-    ties = s_lb[0];
-    ebase = (uint32_t)tr.entry0 + s_lb[1];
+    // ties go to the lowest-index chunks: this chunk keeps what the earlier ones left of `need`
+    const uint32_t need = state[c.tensor * 4 + 1];
+    const uint32_t gb = s_lb[0], eb = s_lb[1], gtc = s_lb[2], eqc = s_lb[3];
+    const uint32_t left_ties = need > eb ? need - eb : 0u;
+    ties = left_ties < eqc ? left_ties : eqc;
+    ebase = (uint32_t)tr.entry0 + gb + (need < eb ? need : eb);
+    if (threadIdx.x == 0)
+      reinterpret_cast<uint16_t*>(payload + counts_off)[blockIdx.x] = (uint16_t)(gtc + ties);
     // max-norm scale: the largest selected |e| is the tensor's max key (hist0)
     const float scale = __uint_as_float(state[c.tensor * 4 + 2]);
     inv = scale > 0.0f ? levels / scale : 0.0f;
