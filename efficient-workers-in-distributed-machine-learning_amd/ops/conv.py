@@ -142,6 +142,14 @@ def _take_pending(m):
     return (_ptr(src), split, dest, Nc, C), job
 
 
+_USE_EPOCH = [0]
+
+
+def new_pass():
+    """Start of a forward pass (the exchange engine's ``begin``): resets the tied-weight count."""
+    _USE_EPOCH[0] += 1
+
+
 def _can_defer(ctx):
     # opt-in: only parameters whose sole post-accumulate hooks are the exchange engine's (which
     # flushes before it reads); no tensor hooks on the weight (they would see dw unwritten)
@@ -149,7 +157,7 @@ def _can_defer(ctx):
     if not (_DEFER_WOUT and p is not None and p.grad is None and p.dtype == torch.float32
             and p.requires_grad and not torch.is_grad_enabled()):
         return False
-    if getattr(p, "_backward_hooks", None):
+    if getattr(p, "_backward_hooks", None) or getattr(p, "_ew_tied", False):
         return False
     eng = getattr(p, "_ew_engine_hooks", 0)
     post = getattr(p, "_post_accumulate_grad_hooks", None)
@@ -375,6 +383,12 @@ class _Conv(torch.autograd.Function):
         # the leaf Parameter itself (not a cast / copy): its .grad decides whether the Winograd
         # weight-gradient output transform may be deferred (_can_defer)
         ctx.w_param = w if isinstance(w, torch.nn.Parameter) else None
+        if ctx.w_param is not None:
+            # a weight used twice in one pass (tied weights) gets its dw summed with the other
+            # use's in autograd's input buffer before any hook runs: never deferred (_can_defer)
+            if getattr(w, "_ew_use_epoch", None) == _USE_EPOCH[0]:
+                w._ew_tied = True
+            w._ew_use_epoch = _USE_EPOCH[0]
         ctx.bn_part = (part, rows) if rows > 0 else None
         ctx.bn_node = bn_node
         ctx.sink = sink

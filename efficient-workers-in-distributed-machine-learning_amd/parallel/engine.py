@@ -163,6 +163,10 @@ class GradientExchange:
     # -- step protocol ------------------------------------------------------------------------
     def begin(self):
         """Call before ``loss.backward()``; gradients must be zero (``flat.zero_grad()``)."""
+        if self.cuda:
+            from ..ops.conv import new_pass
+
+            new_pass()  # tied-weight detection of the deferred weight-gradient transforms
         self._count = [0] * self.nb
         self._launched = [False] * self.nb
         self._works = [None] * self.nb

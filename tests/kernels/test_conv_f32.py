@@ -642,3 +642,55 @@ def test_winograd_autograd_grad_matches_fp64(opt_in):
     finally:
         conv._POISON_DW = False
         _opt_out(ws, hs)
+
+
+def test_exchange_tied_winograd_weights():
+    """A Winograd conv weight used twice in one pass under the exchange engine, which opts its
+    parameters into deferred weight-gradient transforms (pointer-mode gradients: .grad is None
+    when backward starts, as in the trainer): autograd sums the two dw contributions in its input
+    buffer before any hook runs, so that weight must not defer; the exchanged gradient equals the
+    float64 reference on every pass."""
+    conv = _conv(True, 64, "2")
+    from ewdml.compress.codecs import make_codec
+    from ewdml.optim.flat import FlatSGD
+    from ewdml.parallel.comm import Comm
+    from ewdml.parallel.engine import GradientExchange
+    from ewdml.parallel.flat import FlatModel
+
+    torch.manual_seed(5)
+    N, H, C = 16, 8, 128
+    w = torch.nn.Parameter((torch.randn(C, C, 3, 3, device="cuda") / (3 * C ** 0.5))
+                           .contiguous(memory_format=torch.channels_last))
+    other = torch.nn.Parameter((torch.randn(C, C, 3, 3, device="cuda") / (3 * C ** 0.5))
+                               .contiguous(memory_format=torch.channels_last))
+    x = torch.randn(N, C, H, H, device="cuda").contiguous(memory_format=torch.channels_last)
+    dy = torch.randn(N, C, H, H, device="cuda").contiguous(memory_format=torch.channels_last)
+    flat = FlatModel([w, other], attach_grads=False)
+    ex = GradientExchange(flat, Comm(), make_codec("none"), FlatSGD(flat, lr=0.0))
+    try:
+        conv._POISON_DW = True
+        for it in range(2):
+            flat.zero_grad()
+            ex.begin()
+            assert conv.wino_tile(x, w) == 2
+            y = conv.conv(conv.conv(conv.conv(x, w), other), w)
+            y.backward(dy)
+            ex.finish(apply=False)
+            ex.decode_average()
+            torch.cuda.synchronize()
+            xr = x.double().cpu()
+            wr = w.detach().double().cpu().requires_grad_(True)
+            orr = other.detach().double().cpu().requires_grad_(True)
+            yr = F.conv2d(F.conv2d(F.conv2d(xr, wr, padding=1), orr, padding=1), wr, padding=1)
+            yr.backward(dy.double().cpu())
+            def gview(p):  # the parameter's slot of the flat gradient, in its own layout
+                o = flat.offsets[next(i for i, q in enumerate(flat.params) if q is p)]
+                return flat.grad[o:o + p.numel()].as_strided(p.shape, p.stride())
+
+            assert not torch.isnan(flat.grad).any()
+            assert _rel(gview(w), wr.grad) < TOL, (it, _rel(gview(w), wr.grad))
+            assert _rel(gview(other), orr.grad) < TOL, (it, _rel(gview(other), orr.grad))
+        assert getattr(w, "_ew_tied", False) and not getattr(other, "_ew_tied", False)
+    finally:
+        conv._POISON_DW = False
+        ex.close()
