@@ -294,7 +294,7 @@ void ew_rccl_all_to_all(uintptr_t h, uintptr_t send, uintptr_t recv, long long c
 
 // ---- cross-entropy loss (nn.hip): mean over B rows of [B, K] logits (bf16 or fp32), int64 labels
 void ew_cross_entropy_fwd(uintptr_t x, uintptr_t y, int B, int K, int is_bf16, uintptr_t loss,
-                          uintptr_t lse, uintptr_t stream);
+                          uintptr_t lse, uintptr_t stream, uintptr_t dx);
 void ew_cross_entropy_bwd(uintptr_t x, uintptr_t y, uintptr_t lse, uintptr_t grad, int B, int K,
                           int is_bf16, uintptr_t dx, uintptr_t stream);
 

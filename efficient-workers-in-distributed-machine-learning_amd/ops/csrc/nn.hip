@@ -908,7 +908,10 @@ template <typename T>
 __global__ __launch_bounds__(1024) void k_ce_fwd(const T* __restrict__ x,
                                                  const long long* __restrict__ y, int B, int K,
                                                  float* __restrict__ loss,
-                                                 float* __restrict__ lse) {
+                                                 float* __restrict__ lse, T* __restrict__ dx) {
+  // dx (nullable): d(mean loss)/d logits for an upstream gradient of exactly 1, written here so
+  // the backward needs no launch (k_ce_bwd's expressions with g = 1 / B: bit-identical)
+  const float g1 = 1.0f / (float)B;
   __shared__ float lrow[16];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   float acc = 0.0f;  // this wave's sum of row losses (lane 0)
@@ -924,6 +927,15 @@ __global__ __launch_bounds__(1024) void k_ce_fwd(const T* __restrict__ x,
       lse[r] = l;
       const long long t = y[r];
       acc += l - ((t >= 0 && t < K) ? ew_ldf(xr, t) : 0.0f);
+      if (dx) {
+        for (int k = 0; k < K; ++k) {
+          float v = expf(ew_ldf(xr, k) - l);
+          if ((long long)k == t) v -= 1.0f;
+          v *= g1;
+          if constexpr (sizeof(T) == 2) dx[(long long)r * K + k] = ew_f2bf(v);
+          else dx[(long long)r * K + k] = v;
+        }
+      }
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);  // fixed order
@@ -944,6 +956,16 @@ __global__ __launch_bounds__(1024) void k_ce_fwd(const T* __restrict__ x,
       lse[r] = l;
       const long long t = y[r];
       acc += l - ((t >= 0 && t < K) ? ew_ldf(xr, t) : 0.0f);
+    }
+    if (dx) {
+      const long long t = y[r];
+      for (int k = lane; k < K; k += 64) {
+        float v = expf(ew_ldf(xr, k) - l);
+        if ((long long)k == t) v -= 1.0f;
+        v *= g1;
+        if constexpr (sizeof(T) == 2) dx[(long long)r * K + k] = ew_f2bf(v);
+        else dx[(long long)r * K + k] = v;
+      }
     }
   }
   if (lane == 0) lrow[wv] = acc;
@@ -977,16 +999,18 @@ __global__ __launch_bounds__(EW_BLOCK) void k_ce_bwd(const T* __restrict__ x,
 }  // namespace
 
 void ew_cross_entropy_fwd(uintptr_t x, uintptr_t y, int B, int K, int is_bf16, uintptr_t loss,
-                          uintptr_t lse, uintptr_t stream) {
+                          uintptr_t lse, uintptr_t stream, uintptr_t dx) {
   hipStream_t s = (hipStream_t)stream;
   if (is_bf16)
     hipLaunchKernelGGL(k_ce_fwd<uint16_t>, dim3(1), dim3(1024), 0, s,
                        reinterpret_cast<const uint16_t*>(x), reinterpret_cast<const long long*>(y),
-                       B, K, reinterpret_cast<float*>(loss), reinterpret_cast<float*>(lse));
+                       B, K, reinterpret_cast<float*>(loss), reinterpret_cast<float*>(lse),
+                       reinterpret_cast<uint16_t*>(dx));
   else
     hipLaunchKernelGGL(k_ce_fwd<float>, dim3(1), dim3(1024), 0, s,
                        reinterpret_cast<const float*>(x), reinterpret_cast<const long long*>(y), B,
-                       K, reinterpret_cast<float*>(loss), reinterpret_cast<float*>(lse));
+                       K, reinterpret_cast<float*>(loss), reinterpret_cast<float*>(lse),
+                       reinterpret_cast<float*>(dx));
   EW_CHECK_LAUNCH();
 }
 

@@ -323,6 +323,15 @@ def maxpool2x2(x):
     return _MaxPool2.apply(x)
 
 
+_UNIT_GRAD = [0]  # data pointer of the trainer's persistent d(loss)/d(loss) = 1 seed
+
+
+def set_unit_grad(seed):
+    """Register the persistent all-ones loss seed: a cross-entropy whose backward receives it
+    returns the d(loss)/d(logits) its forward kernel already wrote (no backward launch)."""
+    _UNIT_GRAD[0] = seed.data_ptr() if (seed is not None and seed.numel() == 1) else 0
+
+
 class _CrossEntropy(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logits, y):
@@ -330,15 +339,22 @@ class _CrossEntropy(torch.autograd.Function):
         B, K = logits.shape
         loss = torch.empty((), dtype=torch.float32, device=logits.device)
         lse = torch.empty(B, dtype=torch.float32, device=logits.device)
+        # with a registered unit seed the gradient for an upstream 1 is formed in the same launch
+        dx = torch.empty_like(logits) if _UNIT_GRAD[0] else None
         C_.cross_entropy_fwd(_ptr(logits), _ptr(y), B, K, int(logits.dtype == torch.bfloat16),
-                             _ptr(loss), _ptr(lse), _stream())
+                             _ptr(loss), _ptr(lse), _stream(), _ptr(dx))
         ctx.save_for_backward(logits, y, lse)
+        ctx.dx1 = dx
         return loss
 
     @staticmethod
     def backward(ctx, grad):
         C_ = require()
         logits, y, lse = ctx.saved_tensors
+        dx1, ctx.dx1 = ctx.dx1, None
+        if dx1 is not None and grad.numel() == 1 and grad.data_ptr() == _UNIT_GRAD[0] \
+                and grad.dtype == torch.float32:
+            return dx1, None
         B, K = logits.shape
         g = grad.detach().float().contiguous()
         dx = torch.empty_like(logits)

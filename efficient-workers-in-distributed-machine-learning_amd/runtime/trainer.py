@@ -251,6 +251,10 @@ class Trainer:
             seed = getattr(self, "_loss_seed", None)
             if seed is None or seed.device != loss.device or seed.dtype != loss.dtype:
                 seed = self._loss_seed = torch.ones((), dtype=loss.dtype, device=loss.device)
+                if self.cuda:  # never written: the cross-entropy kernel may pre-form its grad
+                    from ..ops.nn import set_unit_grad
+
+                    set_unit_grad(seed)
             loss.backward(seed)
         return loss, out
 
@@ -281,6 +285,11 @@ class Trainer:
         """Release the exchange hooks, the watchdog and the own RCCL communicator (collective:
         every rank calls it).  The process group stays up."""
         self.exchange.close()
+        if self.cuda and getattr(self, "_loss_seed", None) is not None:
+            from ..ops.nn import set_unit_grad
+
+            set_unit_grad(None)
+            self._loss_seed = None
         if self._own_comm:
             self.comm.close()
 

@@ -298,6 +298,32 @@ def test_cross_entropy_matches_torch(B, K, dtype):
     assert _rel(a.grad, r.grad) < tol, _rel(a.grad, r.grad)
 
 
+@pytest.mark.parametrize("B,K", [(128, 10), (64, 1000)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_cross_entropy_unit_seed_grad_formed_in_forward(B, K, dtype):
+    """With the trainer's all-ones loss seed registered, the forward kernel writes d(loss)/d(logits)
+    and the backward launches nothing: bitwise the gradient of the backward kernel; any other
+    upstream gradient still takes the backward kernel."""
+    fnn = _ops()
+    g = torch.Generator(device="cuda").manual_seed(B * K)
+    logits = (3 * torch.randn(B, K, device="cuda", generator=g)).to(dtype)
+    y = torch.randint(0, K, (B,), device="cuda", generator=g)
+    seed = torch.ones((), device="cuda")
+    ref = logits.clone().requires_grad_(True)
+    fnn.cross_entropy(ref, y).backward(seed.clone())  # not the registered seed: kernel path
+    try:
+        fnn.set_unit_grad(seed)
+        a = logits.clone().requires_grad_(True)
+        loss = fnn.cross_entropy(a, y)
+        loss.backward(seed)
+        assert torch.equal(a.grad, ref.grad)
+        b = logits.clone().requires_grad_(True)
+        fnn.cross_entropy(b, y).backward(2 * seed)
+        torch.testing.assert_close(b.grad.float(), 2 * ref.grad.float(), rtol=1e-2, atol=1e-6)
+    finally:
+        fnn.set_unit_grad(None)
+
+
 def _head_model():
     from ewdml.models import build_model
 
