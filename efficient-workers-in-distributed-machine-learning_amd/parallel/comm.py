@@ -206,6 +206,14 @@ class Comm:
         if self.world == 1:
             out[0].copy_(t)
             return
+        if self.backend == "gloo" and t.is_cuda:  # Gloo gathers host tensors only
+            h = t.cpu()
+            ho = torch.empty(out.shape, dtype=out.dtype) if self.rank == dst else None
+            dist.gather(h, list(ho.unbind(0)) if ho is not None else None, dst=dst,
+                        group=self.group)
+            if ho is not None:
+                out.copy_(ho)
+            return
         if self.rank == dst:
             dist.gather(t, list(out.unbind(0)), dst=dst, group=self.group)
         else:

@@ -17,6 +17,12 @@ every method, with the codecs applied for real:
 Collectives are per bucket: one gather + one broadcast per bucket instead of 2 x #tensors
 blocking Gloo round trips per step.  The server runs no forward/backward.
 
+A step is three phases -- :meth:`launch_pending` (workers encode their push payloads),
+:meth:`communicate` (gather, server decode / average / re-encode, broadcast) and :meth:`apply`
+(workers decode the pull and step) -- so a worker's step can run as HIP graph A (forward,
+backward, push encode) -> eager collectives -> graph B (pull decode + update), the trainer's
+``split`` graph mode; the push codec then reads its RNG key from device memory.
+
 k-of-n aggregation (``--mode kill --num-aggregate k``, the reference's declared-but-unused
 straggler flags, ``distributed_nn.py:50-59``): the pushes become point-to-point sends, the server
 averages the first ``k`` worker gradients to ARRIVE (arrival order of the first bucket; the same
@@ -62,6 +68,13 @@ class PSExchange:
         self.k = W if aggregate is None else max(1, min(int(aggregate), W))
         self.kill_threshold = kill_threshold
         self.last_aggregated = list(range(1, self.N))
+        # split-graph protocol (runtime/trainer.py): the push encode in graph A reads the key of
+        # step_idx from key_state (set_device_key), everything else is stream-ordered
+        self.use_dev_key = self.dev_key_advance = self.defer_comm = self._active = False
+        self.key_state = torch.zeros(2, dtype=torch.int32, device=self.device)
+        self.key_dev = self.key_state[1:2]
+        self.side = None
+        self._encoded = False
 
     @staticmethod
     def _nbytes(codec, b):
@@ -70,11 +83,33 @@ class PSExchange:
         return codec.payload_bytes(b.index)
 
     # dense codecs ship the gradient bytes themselves
-    def _encode(self, codec, bi, src, out, rank):
+    def _encode(self, codec, bi, src, out, rank, key_tensor=None):
         if codec.allreduce:
             out.view(codec.wire_dtype).copy_(src.to(codec.wire_dtype))
         else:
-            codec.encode(bi, src, out, self.step_idx, rank)
+            codec.encode(bi, src, out, self.step_idx, rank, key_tensor=key_tensor)
+
+    def set_device_key(self, step: int = None):
+        """Upload the push codec's key of ``step`` (default: the current step) for graph A."""
+        s = self.step_idx if step is None else step
+        key = self.push.key(s, self.comm.rank) if not self.push.allreduce else 0
+        vals = [((v + (1 << 31)) % (1 << 32)) - (1 << 31) for v in (s & 0xFFFFFFFF, key)]
+        if self.key_state.device.type != "cuda":
+            self.key_state.copy_(torch.tensor(vals, dtype=torch.int32))
+            return
+        # stream-ordered upload from a ring of pinned slots (no host synchronisation)
+        if getattr(self, "_ring", None) is None:
+            self._ring = [(torch.zeros(2, dtype=torch.int32).pin_memory(), None) for _ in range(8)]
+            self._slot = 0
+        host, ev = self._ring[self._slot]
+        if ev is not None:
+            ev.synchronize()
+        host[0], host[1] = vals[0], vals[1]
+        self.key_state.copy_(host, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._ring[self._slot] = (host, ev)
+        self._slot = (self._slot + 1) % len(self._ring)
 
     def _decode(self, codec, bi, recv, out, scale):
         if codec.allreduce:
@@ -85,7 +120,7 @@ class PSExchange:
             codec.decode(bi, recv, out, scale)
 
     def begin(self):
-        pass
+        self._encoded = False
 
     def _push_k_of_n(self, bi):
         """Point-to-point push; the server returns the worker ranks whose payload to use."""
@@ -142,14 +177,29 @@ class PSExchange:
             self.last_aggregated = sorted(order[:self.k])
         return self.last_aggregated
 
-    def finish(self):
+    def launch_pending(self):
+        """Phase 1 (workers): encode every bucket's push payload."""
+        if self._encoded or self.is_server:
+            return
+        rank = self.comm.rank
+        kt = self.key_dev if self.use_dev_key else None
+        for b in self.flat.buckets:
+            self._encode(self.push, b.index, self.flat.grad_view(b), self.payload[b.index], rank,
+                         kt)
+        self._encoded = True
+
+    def join_side(self):
+        pass
+
+    def wait(self):
+        pass
+
+    def communicate(self):
+        """Phase 2: gather the pushes, the server averages (and re-encodes the pull), broadcast."""
         W = self.N - 1
         rank = self.comm.rank
         for b in self.flat.buckets:
             bi = b.index
-            g = self.flat.grad_view(b)
-            if not self.is_server:
-                self._encode(self.push, bi, g, self.payload[bi], rank)
             av = self.avg[b.start:b.start + b.length]
             if self.k < W:
                 use = self._push_k_of_n(bi)
@@ -165,15 +215,27 @@ class PSExchange:
                 if self.is_server:
                     self._encode(self.pullc, bi, av, self.pull_buf[bi][0], rank)
                 self.comm.broadcast(self.pull_buf[bi], src=self.server_rank)
-                self._decode(self.pullc, bi, self.pull_buf[bi], av, 1.0)
-        if self.pull == "grad":
-            self.opt.step(grad=self.avg)
-        else:
+        if self.pull != "grad":
             if self.is_server:
                 self.opt.step(grad=self.avg)
-            else:
-                self.opt.end_step()
             self.comm.broadcast(self.flat.data, src=self.server_rank)
+
+    def apply(self):
+        """Phase 3: decode the pulled average and step (weights pull: already applied)."""
+        if self.pull == "grad":
+            for b in self.flat.buckets:
+                bi = b.index
+                self._decode(self.pullc, bi, self.pull_buf[bi],
+                             self.avg[b.start:b.start + b.length], 1.0)
+            self.opt.step(grad=self.avg)
+        elif not self.is_server:
+            self.opt.end_step()
+
+    def finish(self):
+        self.launch_pending()
+        self.communicate()
+        self.apply()
+        self._encoded = False
         self.last = self.bytes_per_step()
         self.step_idx += 1
 

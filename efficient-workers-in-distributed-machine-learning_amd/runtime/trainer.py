@@ -184,18 +184,25 @@ class Trainer:
         self.amp_dtype = {"bf16": torch.bfloat16, "fp16": torch.float16}.get(cfg.amp)
         self.graph_mode = cfg.hip_graph if (self.cuda and not cfg.sync_debug) else "off"
         self.local_sgd = isinstance(self.exchange, LocalSGDExchange)
+        ps_split = isinstance(self.exchange, PSExchange) and self.exchange.k == self.world - 1
+        self.ps_graph = ps_split
         if self.graph_mode == "auto":
-            # graphs wherever the step can be captured: the all-to-all exchange, and local SGD's
+            # graphs wherever the step can be captured: the all-to-all exchange, local SGD's
             # local steps (its sync steps -- compressed delta, host-side best-worker choice --
-            # run eagerly); the parameter server's k-of-n polling and the sharded exchange stay
-            # eager
-            self.graph_mode = ("full" if isinstance(self.exchange, GradientExchange)
-                               or self.local_sgd else "off")
+            # run eagerly) and the parameter server's workers (graph A: forward, backward, push
+            # encode -> eager gather / broadcast -> graph B: pull decode + update); the k-of-n
+            # arrival polling and the sharded exchange stay eager
+            if isinstance(self.exchange, GradientExchange) or self.local_sgd:
+                self.graph_mode = "full"
+            else:
+                self.graph_mode = "split" if ps_split else "off"
         if self.graph_mode != "off" and not (isinstance(self.exchange, GradientExchange) or
-                                             (self.local_sgd and self.graph_mode == "full")):
-            raise ValueError("--hip-graph needs the all-to-all topology (local SGD: full only)")
+                                             (self.local_sgd and self.graph_mode == "full") or
+                                             (ps_split and self.graph_mode == "split")):
+            raise ValueError("--hip-graph: all-to-all topology (local SGD: full only; parameter "
+                             "server without k-of-n: split only)")
         if (self.graph_mode in ("full", "segmented") and self.comm.distributed
-                and self.comm.backend == "gloo" and not self.local_sgd):
+                and self.comm.backend == "gloo" and not self.local_sgd and not self.ps_graph):
             # gloo's CUDA collectives cannot be captured: graph the compute, issue them between
             self.graph_mode = "split"
         if self.graph_mode == "segmented":  # collectives on their own stream, beside backward
@@ -380,7 +387,13 @@ class Trainer:
             self._capture(x, y)
         except Exception as e:  # noqa: BLE001 - any capture failure falls back to eager
             err = e
-        bad = self.comm.all_reduce_scalars([0.0 if err is None else 1.0], op="max")[0]
+        if self.ps_graph:
+            # a parameter-server worker's graphs hold no collectives (the gather / broadcast run
+            # eagerly between them), so one worker falling back to eager cannot desynchronise
+            # the protocol -- and the server, which captures nothing, is not there to agree
+            bad = err is not None
+        else:
+            bad = self.comm.all_reduce_scalars([0.0 if err is None else 1.0], op="max")[0]
         if bad:
             ex = self.exchange
             self._graphs = None
@@ -508,7 +521,9 @@ class Trainer:
         elif x is not self._gx:
             self._gx.copy_(x)
             self._gy.copy_(y)
-        if not self._key_synced and not self.local_sgd:
+        if self.ps_graph:
+            ex.set_device_key()  # the push encode's key of this step (no decode advances it)
+        elif not self._key_synced and not self.local_sgd:
             ex.set_device_key()  # once per capture; the replays advance the key on the device
             self._key_synced = True
         if len(self._graphs) == 1:

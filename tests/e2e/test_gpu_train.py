@@ -302,3 +302,37 @@ def test_sharded_topology_hip_codecs(codec):
     tr, losses = _run(LENET + ["--compress", codec, "--topology", "sharded"], 6)
     assert all(torch.isfinite(torch.tensor(losses)))
     assert tr.exchange.last.payload_bytes > 0
+
+
+def _ps_rank(rank, world, flags, steps):
+    import os
+
+    os.environ["LOCAL_RANK"] = "0"  # every rank on the box's one GPU (Gloo between them)
+    from ewdml.runtime import Trainer
+
+    torch.manual_seed(0)
+    tr = Trainer(ewdml.parse_args(LENET + flags + ["--max-steps", str(steps)]))
+    for _ in range(steps):
+        tr.train_step()
+    torch.cuda.synchronize()
+    return {"params": tr.flat.data.cpu(), "mode": tr.graph_mode,
+            "graphs": tr._graphs is not None, "bytes": tr.exchange.last.payload_bytes}
+
+
+@pytest.mark.parametrize("method", [1, 4])
+def test_ps_worker_split_graphs_match_eager(tmp_path, method):
+    """Parameter-server workers (server + 2 workers on the one GPU, Gloo between them) run
+    graph A (forward, backward, push encode with the step's device RNG key) -> eager gather /
+    broadcast -> graph B (pull decode + update): same trajectory as the eager protocol."""
+    from ..distributed.helpers import run_world
+
+    ops.require()
+    flags = ["--topology", "ps", "--method", str(method)]
+    eager = run_world(_ps_rank, 3, tmp_path / "eager", args=(flags + ["--hip-graph", "off"], 6))
+    graph = run_world(_ps_rank, 3, tmp_path / "graph", args=(flags + ["--hip-graph", "auto"], 6))
+    for r in (1, 2):
+        assert graph[r]["mode"] == "split" and graph[r]["graphs"]
+        rel = float((graph[r]["params"] - eager[r]["params"]).norm() / eager[r]["params"].norm())
+        assert rel < 1e-4, f"worker {r}: graph run differs from eager by {rel:.2e}"
+    torch.testing.assert_close(graph[1]["params"], graph[2]["params"], rtol=0, atol=0)
+    assert graph[1]["bytes"] == eager[1]["bytes"] > 0
