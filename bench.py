@@ -119,6 +119,10 @@ def measure(a, world, amp, ef, extra=()):
             torch.cuda.synchronize()
 
     warm = a.warmup if a.hip_graph == "off" else max(a.warmup, gw + 1)
+    every = getattr(tr.exchange, "every", 1)
+    if a.hip_graph != "off" and every > 1:
+        # local SGD captures two steps (local, sync): both before the clock starts
+        warm = max(warm, every + gw)
     for _ in range(warm):
         tr.train_step()
     sync()

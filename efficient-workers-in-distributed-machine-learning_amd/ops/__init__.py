@@ -364,6 +364,22 @@ def pack_grads(dp, grads, dst, scale=1.0):
                  _DDT[dst.dtype], float(scale), _stream())
 
 
+def sgd_ptrs(dp, grads, param, mom, lr, momentum=0.0, dampening=0.0, weight_decay=0.0,
+             grad_scale=1.0, nesterov=False, first=False, shadow=None, lr_tensor=None):
+    """SGD of one bucket (``param`` / ``mom`` / ``shadow``: its flat views) from autograd's
+    per-tensor gradients, read in place through the pointer table (one launch)."""
+    C = require()
+    ptrs, mask = grad_pointers(dp, grads)
+    for t, nm in ((param, "param"), (mom, "mom")):
+        _check(t, torch.float32, nm)
+        if t.numel() < dp.plan.length:
+            raise ValueError(f"{nm} too small for the bucket")
+    _check_shadow(dp, shadow)
+    C.sgd_ptrs(ptrs, mask, dp.plan.num_tensors, _ptr(dp.chunks), dp.plan.num_chunks, _ptr(param),
+               _ptr(mom), _ptr(shadow), lr, momentum, dampening, weight_decay, grad_scale,
+               int(nesterov), int(first), _stream(), _lrp(lr_tensor))
+
+
 def cast_scale(src, dst, scale=1.0):
     C = require()
     _check(src, torch.float32, "src")

@@ -241,6 +241,29 @@ PYBIND11_MODULE(_C, m) {
                         C, dst, dst_dtype, scale, stream);
         });
 
+  m.def("sgd_ptrs",
+        [](const Ptrs& grads, const Mask& mask, int T, uintptr_t chunks, int C, uintptr_t param,
+           uintptr_t mom, uintptr_t shadow, float lr, float momentum, float dampening,
+           float weight_decay, float grad_scale, int nesterov, int first, uintptr_t stream,
+           uintptr_t lr_ptr) {
+          SgdFlatArgs a{};
+          a.param = param;
+          a.mom = mom;
+          a.shadow = shadow;
+          a.stream = stream;
+          a.lr = lr;
+          a.momentum = momentum;
+          a.dampening = dampening;
+          a.weight_decay = weight_decay;
+          a.grad_scale = grad_scale;
+          a.nesterov = nesterov;
+          a.first = first;
+          a.lr_ptr = lr_ptr;
+          ew_sgd_ptrs(grads.data(), (int)grads.size(), mask.data(), (int)mask.size(), T, chunks,
+                      C, a);
+        });
+
+  m.def("cf_set_glds", &ew_cf_set_glds);
   m.def("bn_part_floats", &ew_bn_part_floats);
   m.def("bn_relu_fwd",
         [](uintptr_t h, uintptr_t res, uintptr_t y, uintptr_t code, uintptr_t stats,

@@ -657,6 +657,139 @@ __global__ __launch_bounds__(64 * WM * WN, WPE) void k_cf_gemm(const float* __re
                                                phase >> 1, phase & 1);
 }
 
+// ---------------------------------------------------------------------------------------------
+// LDS-DMA staging (buffer_load_dwordx4 ... lds): the forward GEMM's KC operand tiles go from global
+// memory straight into LDS, no staging registers and no ds_write pass.  One wave instruction fills
+// 1 KB = 8 consecutive 128-B rows lane-linearly (lane l -> byte 16 l), so the KC swizzle moves to
+// the SOURCE: lane l loads chunk (l & 7) ^ ((r >> 1) & 7) of its row r, which lands at slot l & 7 =
+// the position cf_off(r, chunk) expects (the permutation is an involution; the fragment reads are
+// unchanged).  Padding taps read zeros through an out-of-range buffer offset, as in CfStager.
+// s_waitcnt on the vector-memory counter only (expcnt / lgkmcnt left at their maxima)
+template <int N>
+__device__ __forceinline__ void cf_wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+typedef __attribute__((address_space(3))) void* cf_lds_ptr;
+
+template <int BM, int BN, int NT>
+struct CfGlds {
+  static constexpr int RA = 8 * BM / NT, RB = 8 * BN / NT;  // wave instructions per operand
+  static constexpr int LPS = RA + RB;                        // loads per k-step per thread
+  static constexpr int A_BYTES = BM * 128;
+  __amdgpu_buffer_rsrc_t rsa, rsb;
+  unsigned aoff[RA], boff[RB];
+  int ah[RA], aw[RA];
+  int dst0;  // this wave's first 1-KB row group in a stage image (bytes)
+
+  __device__ __forceinline__ void init(const CfGeom& g, const float* a_src, const float* b_src,
+                                       int t, int m0, int n0) {
+    dst0 = (t >> 6) * 8 * 128;
+    const unsigned K = (unsigned)g.taps * g.C;
+    rsa = cf_rsrc(a_src, (unsigned)g.M * g.C * 4u);
+    rsb = cf_rsrc(b_src, (unsigned)g.Ncol * K * 4u);
+#pragma unroll
+    for (int i = 0; i < RA; ++i) {
+      const int r = (t >> 3) + (NT / 8) * i;
+      const int m = m0 + r;
+      const int hw = m % (g.H * g.W);
+      ah[i] = hw / g.W;
+      aw[i] = hw - ah[i] * g.W;
+      const unsigned c = (unsigned)((t & 7) ^ ((r >> 1) & 7));
+      aoff[i] = ((unsigned)m * g.C + c * 4) * 4u;
+    }
+#pragma unroll
+    for (int i = 0; i < RB; ++i) {
+      const int r = (t >> 3) + (NT / 8) * i;
+      const unsigned c = (unsigned)((t & 7) ^ ((r >> 1) & 7));
+      boff[i] = ((unsigned)(n0 + r) * K + c * 4) * 4u;
+    }
+  }
+
+  // DMA k-step s into the stage image at `stage`
+  __device__ __forceinline__ void issue(const CfGeom& g, int s, char* stage) const {
+    const int CB = g.C / CF_BK;
+    const int tap = s / CB, cb = s - tap * CB;
+    const int q = tap / 3, one = g.taps == 1;
+    const int dr = one ? 0 : q - 1, dc = one ? 0 : tap - q * 3 - 1;
+    const unsigned sa = (unsigned)(((dr * g.W + dc) * g.C + cb * CF_BK) * 4);
+#pragma unroll
+    for (int i = 0; i < RA; ++i) {
+      const bool ok = (unsigned)(ah[i] + dr) < (unsigned)g.H && (unsigned)(aw[i] + dc) < (unsigned)g.W;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rsa, (cf_lds_ptr)(stage + dst0 + (NT / 8) * i * 128), 16, ok ? aoff[i] + sa : CF_OOB, 0,
+          0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < RB; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rsb, (cf_lds_ptr)(stage + A_BYTES + dst0 + (NT / 8) * i * 128), 16, boff[i],
+          s * CF_BK * 4, 0, 0);
+  }
+};
+
+// Forward GEMM (stride 1) with LDS-DMA staging through three stage images: step s + 2 is in flight
+// while s computes; one counted vmcnt (step s landed, s + 1 may not have) and one raw barrier per
+// step, never a vmcnt(0) inside the loop (a __syncthreads() would drain the DMA queue)
+template <int BM, int BN, int WM, int WN, int SH, int WPE = 0>
+__global__ __launch_bounds__(64 * WM * WN, WPE) void k_cf_gemm_gl(const float* __restrict__ a_src,
+                                                      const float* __restrict__ b_src,
+                                                      float* __restrict__ out,
+                                                      float* __restrict__ slab, CfGeom geo,
+                                                      float* __restrict__ bnpart, CfBnBwd bb,
+                                                      const float* __restrict__ addend) {
+  using L = CfLayout<CF_FWD, BM, BN>;
+  using acc_t = typename CfMfma<SH>::acc_t;
+  constexpr int NT = 64 * WM * WN;
+  constexpr int MI = BM / WM / SH, NJ = BN / WN / SH;
+  static_assert(MI >= 1 && NJ >= 1 && MI * SH * WM == BM && NJ * SH * WN == BN, "wave tiling");
+  __shared__ __attribute__((aligned(16))) char smem[3 * L::STAGE];
+  const int t = threadIdx.x, lane = t & 63, wq = t >> 6;
+  const int wm = wq / WN, wn = wq % WN;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int zb = blockIdx.z / geo.nsplit, zs = blockIdx.z - zb * geo.nsplit;
+  a_src += zb * geo.a_bs;
+  b_src += (geo.b_flip ? cf_flip4(zb) : zb) * geo.b_bs;
+  out += zb * geo.o_bs;
+  if (slab) slab += (long long)(zs * (gridDim.z / geo.nsplit) + zb) * geo.M * geo.Ncol;
+  const int kbeg = zs * geo.kps;
+  const int kend = min(kbeg + geo.kps, geo.ksteps);
+  CfGlds<BM, BN, NT> st;
+  st.init(geo, a_src, b_src, t, m0, n0);
+
+  acc_t acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = acc_t{};
+
+  using Frag = CfFrag<SH, MI, NJ>;
+  const int arow0 = wm * (BM / WM), bcol0 = wn * (BN / WN);
+  const int n = kend - kbeg;
+  if (n > 0) {
+    const int last = kend - 1;
+    st.issue(geo, kbeg, smem);
+    st.issue(geo, min(kbeg + 1, last), smem + L::STAGE);
+    int cur = 0;  // stage of step i; step i + 2 goes to the stage read at step i - 1
+    for (int i = 0; i < n; ++i) {
+      cf_wait_vm<CfGlds<BM, BN, NT>::LPS>();
+      __builtin_amdgcn_s_barrier();
+      const int nxt = cur == 0 ? 2 : cur - 1;
+      st.issue(geo, min(kbeg + i + 2, last), smem + nxt * L::STAGE);
+      const char* cs = smem + cur * L::STAGE;
+      Frag fr;
+      cf_frag_read<CF_FWD, BM, BN, SH, MI, NJ>(cs, cs + L::A_BYTES, arow0, bcol0, lane, fr);
+      cf_mma<SH, MI, NJ, 0, Frag::R>(fr, acc);
+      cur = cur == 2 ? 0 : cur + 1;
+    }
+  }
+  cf_wait_vm<0>();
+  __syncthreads();  // the epilogue reuses smem
+  cf_epilogue<BM, BN, WM, WN, SH, MI, NJ, false>(acc, smem, wm, wn, lane, m0, n0, geo.M,
+                                                 geo.Ncol, out, slab, bnpart, bb, addend);
+}
+
 // out[i] = sum_z slab[z][i] (+ addend), 8 elements per thread
 __global__ __launch_bounds__(EW_BLOCK) void k_cf_slab_reduce(const float* __restrict__ slab,
                                                              int nsplit, long long n,
@@ -1020,6 +1153,17 @@ __global__ __launch_bounds__(EW_BLOCK) void k_cf_stem_reduce(const float* __rest
   if (ck == 0 && o < n) dw[o] = red[0][t & 7];
 }
 
+// Forward GEMMs through the LDS-DMA kernel (k_cf_gemm_gl): EWDML_CF_GLDS=1/0 at load, or
+// ew_cf_set_glds at run time (tests compare both paths in one process)
+int g_cf_glds = -1;
+bool cf_glds_on() {
+  if (g_cf_glds < 0) {
+    const char* e = getenv("EWDML_CF_GLDS");
+    g_cf_glds = (e && e[0] == '1') ? 1 : 0;
+  }
+  return g_cf_glds == 1;
+}
+
 // Launch plan: tile shape and split of the reduction, from a small cost model (us): every block
 // k-step costs its MFMA time (bm*bn*32*2 FLOP at 614 GFLOP/s per CU, derated for the narrower
 // tiles' lower operand reuse), each block pays ~3 k-steps of prologue / epilogue, a CU runs
@@ -1075,6 +1219,9 @@ CfPlan cf_plan(int M, int Ncol, int ksteps, long long ws_floats, int batch) {
   hipLaunchKernelGGL((k_cf_gemm<MODE_, BM_, BN_, WM_, WN_, SH_, STR, WPE_>), grid,                \
                      dim3(64 * WM_ * WN_), 0, s, a, b, out, slab, geo, bnp, bbv, addend)
 #define CF_LAUNCH(MODE_, BM_, BN_, WM_, WN_, SH_) CF_LAUNCH_W(MODE_, BM_, BN_, WM_, WN_, SH_, 0)
+#define CF_LAUNCH_GL(BM_, BN_, WM_, WN_, SH_, WPE_)                                           \
+  hipLaunchKernelGGL((k_cf_gemm_gl<BM_, BN_, WM_, WN_, SH_, WPE_>), grid, dim3(64 * WM_ * WN_), 0, \
+                     s, a, b, out, slab, geo, bnp, bbv, addend)
 
 template <int MODE, int STR = 1>
 int cf_gemm(const float* a, const float* b, float* out, float* ws, long long ws_floats,
@@ -1126,7 +1273,22 @@ int cf_gemm(const float* a, const float* b, float* out, float* ws, long long ws_
     return e ? e[0] - '0' : 1;
   }();
   const bool occ2 = occ_env == 2 || (occ_env == 1 && (long long)grid.x * grid.y * grid.z > 256);
-  if (p.bm == 128 && p.bn == 128) {
+  bool launched = false;
+  if constexpr (MODE == CF_FWD && STR == 1) {
+    if (cf_glds_on() && !w4) {
+      if (p.bm == 128 && p.bn == 128)
+        CF_LAUNCH_GL(128, 128, 2, 4, 32, 0);
+      else if (p.bm == 128)  // held to 128 VGPRs: two blocks per CU (72 KB of LDS each)
+        CF_LAUNCH_GL(128, 64, 4, 2, 32, 4);
+      else if (p.bn == 128)
+        CF_LAUNCH_GL(64, 128, 2, 4, 32, 4);
+      else
+        CF_LAUNCH_GL(64, 64, 4, 2, 16, 0);
+      launched = true;
+    }
+  }
+  if (launched) {
+  } else if (p.bm == 128 && p.bn == 128) {
     if (w4) CF_LAUNCH(MODE, 128, 128, 2, 2, 32);
     else CF_LAUNCH(MODE, 128, 128, 2, 4, 32);
   } else if (p.bm == 128) {
@@ -1172,6 +1334,7 @@ int cf_gemm(const float* a, const float* b, float* out, float* ws, long long ws_
 }
 #undef CF_LAUNCH
 #undef CF_LAUNCH_W
+#undef CF_LAUNCH_GL
 
 int cf_taps(int ksize) {
   if (ksize != 1 && ksize != 3) throw std::runtime_error("ewdml conv: kernel size must be 1 or 3");
@@ -1182,6 +1345,12 @@ int cf_taps(int ksize) {
 
 // ------------------------------------------------------------------------------------------------
 // host side (shapes validated here: the kernels assume them)
+
+int ew_cf_set_glds(int on) {
+  const int prev = cf_glds_on() ? 1 : 0;
+  if (on >= 0) g_cf_glds = on ? 1 : 0;
+  return prev;
+}
 
 // out[b][M][N] = A[b][M][K] * B[b][N][K]^T for b < batch (row-major, K contiguous): the forward
 // GEMM as a 1x1 "convolution" over M pixels, batched over blockIdx.z (winograd_f32.hip).

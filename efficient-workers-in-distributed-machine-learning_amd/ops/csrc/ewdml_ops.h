@@ -101,6 +101,13 @@ void ew_qsgd_decode_apply(const QsgdDecodeArgs& a);
 
 void ew_sgd_flat(const SgdFlatArgs& a);
 void ew_adam_flat(const AdamFlatArgs& a);
+// fp32 forward conv GEMMs through LDS-DMA staging (k_cf_gemm_gl) when on (-1: query only);
+// returns the previous setting
+int ew_cf_set_glds(int on);
+// SGD of one bucket from its per-tensor gradients (pointer table; a.grad / a.n / a.grad_dtype
+// unused): param / mom / shadow are the bucket's flat views, chunk rows address them
+void ew_sgd_ptrs(const uintptr_t* grad_ptrs, int n_ptrs, const uint32_t* bf16_mask, int n_mask,
+                 int num_tensors, uintptr_t chunks, int num_chunks, const SgdFlatArgs& a);
 void ew_pack_grads(const uintptr_t* grad_ptrs, int n_ptrs, const uint32_t* bf16_mask, int n_mask,
                    int num_tensors, uintptr_t chunks, int num_chunks, uintptr_t dst,
                    int dst_dtype, float scale, uintptr_t stream);

@@ -165,6 +165,43 @@ __global__ __launch_bounds__(EW_BLOCK) void k_pack_grads(GradPtrs gp,
   }
 }
 
+// SGD step of one bucket straight from autograd's per-tensor gradients (pointer table): the
+// local steps of local SGD (Method 6) read each gradient in place, as the codec passes do -- no
+// accumulate-add into a flat gradient buffer, no separate gather.  Block = one chunk row.
+__global__ __launch_bounds__(EW_BLOCK) void k_sgd_ptrs(GradPtrs gp,
+                                                       const ChunkRow* __restrict__ chunks,
+                                                       float* __restrict__ p,
+                                                       float* __restrict__ mom,
+                                                       uint16_t* __restrict__ shadow, SgdArgs sa) {
+  ew_sgd_resolve(sa);
+  const ChunkRow c = chunks[blockIdx.x];
+  for (int i = 4 * threadIdx.x; i < c.len; i += 4 * EW_BLOCK) {
+    float gv[4];
+    ew_ld4t(gp, nullptr, c, i, gv);
+    const long long o = (long long)c.start + i;
+    const int k = c.len - i < 4 ? c.len - i : 4;
+    if (k == 4) {
+      float4 pv = *reinterpret_cast<float4*>(p + o);
+      float4 bv = *reinterpret_cast<float4*>(mom + o);
+      ew_sgd(pv.x, bv.x, gv[0] * sa.grad_scale, sa);
+      ew_sgd(pv.y, bv.y, gv[1] * sa.grad_scale, sa);
+      ew_sgd(pv.z, bv.z, gv[2] * sa.grad_scale, sa);
+      ew_sgd(pv.w, bv.w, gv[3] * sa.grad_scale, sa);
+      *reinterpret_cast<float4*>(p + o) = pv;
+      *reinterpret_cast<float4*>(mom + o) = bv;
+      if (shadow) {
+        const float w[4] = {pv.x, pv.y, pv.z, pv.w};
+        ew_st4_bf16(shadow + o, 4, w);
+      }
+    } else {
+      for (int j = 0; j < k; ++j) {
+        ew_sgd(p[o + j], mom[o + j], gv[j] * sa.grad_scale, sa);
+        if (shadow) shadow[o + j] = ew_f32_to_bf16(p[o + j]);
+      }
+    }
+  }
+}
+
 inline int ew_grid(long long n4) {
   long long b = (n4 + EW_BLOCK - 1) / EW_BLOCK;
   return (int)(b < 2048 ? (b > 0 ? b : 1) : 2048);  // 8 blocks per CU, grid-stride the rest
@@ -220,6 +257,18 @@ void ew_pack_grads(const uintptr_t* grad_ptrs, int n_ptrs, const uint32_t* bf16_
   hipLaunchKernelGGL(k_pack_grads, dim3(num_chunks), dim3(EW_BLOCK), 0, (hipStream_t)stream, g,
                      reinterpret_cast<const ChunkRow*>(chunks), reinterpret_cast<void*>(dst),
                      dst_dtype, scale);
+  EW_CHECK_LAUNCH();
+}
+
+void ew_sgd_ptrs(const uintptr_t* grad_ptrs, int n_ptrs, const uint32_t* bf16_mask, int n_mask,
+                 int num_tensors, uintptr_t chunks, int num_chunks, const SgdFlatArgs& a) {
+  GradPtrs g;
+  ew_fill_ptrs(g, grad_ptrs, n_ptrs, num_tensors, bf16_mask, n_mask);
+  SgdArgs sa{a.lr, a.momentum, a.dampening, a.weight_decay, a.grad_scale, a.nesterov, a.first};
+  sa.lr_ptr = reinterpret_cast<const float*>(a.lr_ptr);
+  hipLaunchKernelGGL(k_sgd_ptrs, dim3(num_chunks), dim3(EW_BLOCK), 0, (hipStream_t)a.stream, g,
+                     reinterpret_cast<const ChunkRow*>(chunks), reinterpret_cast<float*>(a.param),
+                     reinterpret_cast<float*>(a.mom), reinterpret_cast<uint16_t*>(a.shadow), sa);
   EW_CHECK_LAUNCH();
 }
 

@@ -103,6 +103,15 @@ class FlatSGD(_LrMixin):
         self.step_range(0, self.flat.numel, self.flat.grad if grad is None else grad, grad_scale)
         self.end_step()
 
+    def step_bucket_ptrs(self, b, dp, grads, grad_scale: float = 1.0):
+        """SGD of bucket ``b`` from its per-tensor gradients ``grads`` (pointer mode), one
+        launch; no :meth:`end_step`."""
+        p = self.flat.data_view(b)
+        m = self.mom[b.start:b.start + b.length]
+        ops.sgd_ptrs(dp, grads, p, m, self.lr, self.momentum, self.dampening, self.weight_decay,
+                     grad_scale, self.nesterov, self.first, shadow=self.flat.shadow_view(b),
+                     lr_tensor=self.lr_t)
+
     def end_step(self):
         self.steps += 1
 

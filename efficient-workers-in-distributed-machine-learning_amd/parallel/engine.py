@@ -104,6 +104,9 @@ class GradientExchange:
         self._active = False
         self.step_idx = 0
         self.defer_comm = False
+        # encode from flat.grad instead of autograd's tensors (local SGD's model deltas live
+        # there even when the step's gradients are read through pointer tables)
+        self.src_flat = False
         self.use_dev_key = False
         # device RNG state {step, key} read by the captured encode kernels; the step's last decode
         # kernel advances it in place (dev_key_advance), so graph replays need no host upload
@@ -239,10 +242,10 @@ class GradientExchange:
 
     def _encode(self, bi: int):
         b = self.flat.buckets[bi]
-        g = self.flat.bucket_grads(b)
+        g = self.flat.grad_view(b) if self.src_flat else self.flat.bucket_grads(b)
         if self.codec.allreduce:
             dst = self.flat.grad_view(b) if self.send[bi] is None else self.send[bi]
-            if not self.flat.attach_grads:  # one gather(+cast) kernel from autograd's tensors
+            if not (self.flat.attach_grads or self.src_flat):  # one gather(+cast) kernel
                 ops.pack_grads(self._pack_plans[bi], g, dst, 1.0 / self.predivide)
             elif self.send[bi] is None:
                 if self.predivide != 1.0:
@@ -388,14 +391,17 @@ class GradientExchange:
             self.codec.decode(b.index, self.recv[b.index].view(self.N, -1),
                               self.flat.grad_view(b), scale)
 
-    def decode_rank(self, src: int):
+    def decode_rank(self, src):
         """Write rank ``src``'s decoded payload (unscaled) into ``flat.grad``: local SGD's
-        best-worker adoption reads the winner's compressed delta out of the all-gather."""
+        best-worker adoption reads the winner's compressed delta out of the all-gather.  ``src``
+        may be a device index tensor (the row is then selected on the device)."""
         if self.codec.allreduce:
             raise ValueError("decode_rank needs a compressing (all-gather) codec")
         for b in self.flat.buckets:
             rows = self.recv[b.index].view(self.N, -1)
-            self.codec.decode(b.index, rows[src:src + 1], self.flat.grad_view(b), 1.0)
+            row = rows.index_select(0, src.reshape(1)) if torch.is_tensor(src) \
+                else rows[src:src + 1]
+            self.codec.decode(b.index, row, self.flat.grad_view(b), 1.0)
 
     def close(self):
         if self._hooks:

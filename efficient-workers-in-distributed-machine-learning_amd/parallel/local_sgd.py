@@ -19,9 +19,16 @@ Modes:
     of rank 0 (or of the best rank with ``select_best``) are broadcast densely at every sync
     point (counted; the reference's commented code never re-synchronised).
 The best rank is measured on a fixed held-out batch (``score_fn``).
+
+With pointer-mode gradients (``FlatModel(attach_grads=False)``, the GPU default) a local step
+reads autograd's gradient tensors in place: one fused SGD launch per bucket (``ops.sgd_ptrs``), or
+a gather into ``flat.grad`` per bucket for other optimizers -- never the per-parameter
+accumulate-adds of attached ``.grad`` views.  The model delta of a sync step is staged in
+``flat.grad`` and the wrapped exchange encodes from there (``src_flat``).
 """
 import torch
 
+from .. import ops
 from .engine import StepStats, sync_buffers
 
 
@@ -37,6 +44,8 @@ class LocalSGDExchange:
         self.anchor = self.flat.data.clone() if mode == "model" else None
         self.last = StepStats()
         self.best_rank_history = []
+        self.best_t = None  # device index of the last sync's winner (model mode)
+        self._plans = None  # pointer mode: per-bucket device plans of the local step
 
     @property
     def is_sync(self) -> bool:
@@ -60,20 +69,27 @@ class LocalSGDExchange:
                 stats.wire_bytes_sent += n if self.comm.rank == src else 0
                 stats.wire_bytes_recv += 0 if self.comm.rank == src else n
         else:
-            self.opt.step(grad=self.flat.grad)  # local step with the rank's own gradient
+            self.local_step()  # with the rank's own gradient
             if sync:  # model mode
                 delta = self.flat.grad
                 torch.sub(self.flat.data, self.anchor, out=delta)
-                self.inner.begin()
-                self.inner.finish(apply=False)
+                self.inner.src_flat = True
+                try:
+                    self.inner.begin()
+                    self.inner.finish(apply=False)
+                finally:
+                    self.inner.src_flat = False
                 stats = self.inner.bytes_per_step()
                 if self.select_best and self.comm.world > 1:
-                    # every rank holds every rank's compressed delta: apply the winner's
-                    src = self._best()
-                    self.inner.decode_rank(src)
-                    buf = self._sync_bn(src)
-                    stats.wire_bytes_sent += buf if self.comm.rank == src else 0
-                    stats.wire_bytes_recv += 0 if self.comm.rank == src else buf
+                    # every rank holds every rank's compressed delta: apply the winner's.  The
+                    # choice stays on the device (scores all-gathered, argmax, the winner's
+                    # payload row and BN buffers selected by index), so this step has no host
+                    # round trip and is captured as a HIP graph like the local steps
+                    best = self._best_dev()
+                    self.inner.decode_rank(best)
+                    buf = self._sync_bn_dev(best)
+                    stats.wire_bytes_sent += (self.comm.world - 1) * buf
+                    stats.wire_bytes_recv += (self.comm.world - 1) * buf
                 else:
                     self.inner.decode_average()
                 torch.add(self.anchor, self.flat.grad, out=self.flat.data)
@@ -82,12 +98,66 @@ class LocalSGDExchange:
         self.last = stats
         self.step_idx += 1
 
+    def local_step(self):
+        """Optimizer step with this rank's own gradient."""
+        flat = self.flat
+        if flat.attach_grads:
+            self.opt.step(grad=flat.grad)
+            return
+        if self._plans is None:
+            self._plans = [ops.DevicePlan(b.plan, flat.data.device) for b in flat.buckets]
+        if getattr(self.opt, "fusable", False):
+            for b, dp in zip(flat.buckets, self._plans):
+                self.opt.step_bucket_ptrs(b, dp, flat.bucket_grads(b))
+            self.opt.end_step()
+            return
+        for b, dp in zip(flat.buckets, self._plans):  # other optimizers: gather, then step
+            ops.pack_grads(dp, flat.bucket_grads(b), flat.grad_view(b))
+        self.opt.step(grad=flat.grad)
+
     def _best(self) -> int:
         score = float(self.score_fn()) if self.score_fn is not None else 0.0
         scores = self.comm.all_gather_object(score)
         best = max(range(len(scores)), key=lambda r: (scores[r], -r))
         self.best_rank_history.append(best)
         return best
+
+    def _best_dev(self) -> torch.Tensor:
+        """Index (int64 [1], on the device) of the rank with the highest held-out score, lowest
+        rank on ties -- the same choice as :meth:`_best` without leaving the device."""
+        dev = self.flat.data.device
+        s = self.score_fn() if self.score_fn is not None else 0.0
+        s = torch.as_tensor(s, dtype=torch.float32, device=dev).reshape(1)
+        scores = torch.empty(self.comm.world, dtype=torch.float32, device=dev)
+        self.comm.all_gather(scores, s)
+        best = torch.argmax(scores).reshape(1)  # first maximum: lowest rank on ties
+        if not (dev.type == "cuda" and torch.cuda.is_current_stream_capturing()):
+            self.best_rank_history.append(int(best))
+        self.best_t = best
+        return best
+
+    def _sync_bn_dev(self, best: torch.Tensor) -> int:
+        """Every rank takes rank ``best``'s buffers (BN running statistics): one all-gather per
+        buffer dtype and an index select on the device.  Returns the bytes per rank."""
+        model = self.flat.model
+        if model is None:
+            return 0
+        groups = {}
+        for b in model.buffers():
+            if b.dtype.is_floating_point or b.dtype in (torch.int64, torch.int32):
+                groups.setdefault(b.dtype, []).append(b)
+        nbytes = 0
+        for dt, bufs in groups.items():
+            mine = torch.cat([b.detach().reshape(-1) for b in bufs])
+            allb = torch.empty(self.comm.world * mine.numel(), dtype=dt, device=mine.device)
+            self.comm.all_gather(allb, mine)
+            win = allb.view(self.comm.world, -1).index_select(0, best)[0]
+            o = 0
+            for b in bufs:
+                b.data.copy_(win[o:o + b.numel()].view_as(b))
+                o += b.numel()
+            nbytes += mine.numel() * mine.element_size()
+        return nbytes
 
     def _sync_bn(self, src: int) -> int:
         """Broadcast the model's buffers (BN running statistics) from ``src``; returns bytes."""

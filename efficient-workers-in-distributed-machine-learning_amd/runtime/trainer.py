@@ -131,10 +131,11 @@ class Trainer:
         if self.channels_last:
             model = model.to(memory_format=torch.channels_last)
         self.model = model
-        # pointer-mode gradients (read in place by the HIP kernels) when the exchange is the plain
-        # all-to-all one; PS / local SGD keep flat gradient views (they step on the local grad)
-        ptr_grads = (self.cuda and cfg.topology == "allgather" and cfg.sync_every == 1
-                     and not cfg.select_best and os.environ.get("EWDML_GRAD_VIEWS") != "1")
+        # pointer-mode gradients (read in place by the HIP kernels) for the all-to-all exchange
+        # and local SGD (its local steps read them through the same pointer tables); the
+        # parameter server keeps flat gradient views
+        ptr_grads = (self.cuda and cfg.topology == "allgather"
+                     and os.environ.get("EWDML_GRAD_VIEWS") != "1")
         bf16_params = ptr_grads and cfg.amp == "bf16" and cfg.param_dtype == "auto"
         self.flat = FlatModel(model, bucket_bytes=int(cfg.bucket_mb * (1 << 20)),
                               attach_grads=not ptr_grads, bf16_params=bf16_params)
@@ -184,6 +185,8 @@ class Trainer:
         self.amp_dtype = {"bf16": torch.bfloat16, "fp16": torch.float16}.get(cfg.amp)
         self.graph_mode = cfg.hip_graph if (self.cuda and not cfg.sync_debug) else "off"
         self.local_sgd = isinstance(self.exchange, LocalSGDExchange)
+        if self.local_sgd and cfg.select_best:
+            self._holdout_batch()
         ps_split = isinstance(self.exchange, PSExchange) and self.exchange.k == self.world - 1
         self.ps_graph = ps_split
         if self.graph_mode == "auto":
@@ -208,6 +211,9 @@ class Trainer:
         if self.graph_mode == "segmented":  # collectives on their own stream, beside backward
             self.exchange.comm_stream = torch.cuda.Stream(device=self.device)
         self._graphs = None
+        # local SGD keeps two captured steps: "local" and (model mode without best-worker choice)
+        # "sync"; the idle one waits here with its static inputs and outputs
+        self._gkind, self._gslots = "local", {}
         self.captures = 0  # graph captures so far (a schedule change should not force one)
         self._in_graph_batch = False
         self._key_synced = False
@@ -271,8 +277,34 @@ class Trainer:
             return contextlib.nullcontext()
         return torch.cuda.stream(self.gstream)
 
+    def _drop_graphs(self):
+        """Forget every captured step (the next graphed step re-captures)."""
+        self._graphs = None
+        self._gslots = {}
+
+    def _graph_kind(self):
+        """Local SGD: make the captured graph of this step's kind current."""
+        kind = "sync" if self.exchange.is_sync else "local"
+        if kind == self._gkind:
+            return
+        fields = ("_graphs", "_gloss", "_gout", "_gbytes", "_gx", "_gy", "_in_graph_batch")
+        self._gslots[self._gkind] = tuple(getattr(self, f, None) for f in fields)
+        vals = self._gslots.pop(kind, (None,) * len(fields))
+        for f, v in zip(fields, vals):
+            setattr(self, f, v)
+        if self._in_graph_batch is None:
+            self._in_graph_batch = False
+        self._gkind = kind
+
+    def _sync_graphable(self) -> bool:
+        # model mode: delta encode, all-gather and the on-device best-worker choice are all
+        # device work; grad mode's dense re-broadcast roots at a host-chosen rank
+        return self.exchange.mode == "model"
+
     def train_step(self, x=None, y=None):
         """One synchronous step.  Returns (loss tensor, logits) (server: (None, None))."""
+        if self.local_sgd and self.graph_mode != "off":
+            self._graph_kind()
         if self.gstream is None:
             out = self._train_step(x, y)
         elif self._graphs is not None and len(self._graphs) == 1 and _SAME_STREAM_REPLAY:
@@ -334,7 +366,7 @@ class Trainer:
         if not self.cfg.topk_warmup or not hasattr(ex, "set_ratio"):
             return
         if ex.set_ratio(self.ratio_at(self.step)):
-            self._graphs = None  # payload sizes changed: re-capture at this step (every rank)
+            self._drop_graphs()  # payload sizes changed: re-capture at this step (every rank)
 
     def _train_step(self, x=None, y=None):
         if self.fault is not None and self.fault == (self.rank, self.step):
@@ -345,7 +377,7 @@ class Trainer:
             if lr != self.opt.lr:
                 self.opt.lr = lr  # on the GPU also into the device lr the kernels read
                 if self._graphs is not None and getattr(self.opt, "lr_t", None) is None:
-                    self._graphs = None  # the lr is a kernel argument: re-capture (all ranks)
+                    self._drop_graphs()  # the lr is a kernel argument: re-capture (all ranks)
         if self.is_server:
             if not self.model.training:
                 self.model.train()
@@ -355,12 +387,12 @@ class Trainer:
         if not self.model.training:  # recursive; ~0.2 ms of host time per step otherwise
             self.model.train()
         graphed = self.graph_mode != "off" and self.step >= self.cfg.graph_warmup
-        if graphed and self.local_sgd and self.exchange.is_sync:
-            graphed = False  # the sync step (delta exchange, best-worker choice) runs eagerly
+        if graphed and self.local_sgd and self.exchange.is_sync and not self._sync_graphable():
+            graphed = False  # dense re-sync / best-worker choice (host decisions): eager
         if x is None and graphed and self.loader.fused:
             # the batch kernel is part of the graph: only the host-side epoch bookkeeping here
             if self._graphs is not None and not self._in_graph_batch:
-                self._graphs = None  # captured around an explicit batch: re-capture
+                self._drop_graphs()  # captured around an explicit batch: re-capture
             self.loader.begin_step()
             if self._graphs is None and not self._try_capture(None, None):
                 return self._train_step()  # capture failed on some rank: all run eager
@@ -396,9 +428,11 @@ class Trainer:
             bad = self.comm.all_reduce_scalars([0.0 if err is None else 1.0], op="max")[0]
         if bad:
             ex = self.exchange
-            self._graphs = None
+            self._drop_graphs()
             self.graph_mode = "off"
-            ex.use_dev_key = ex.defer_comm = ex._active = ex.dev_key_advance = False
+            for e in (ex, getattr(ex, "inner", None)):
+                if e is not None:
+                    e.use_dev_key = e.defer_comm = e._active = e.dev_key_advance = False
             # a stream forked into an aborted capture (the encode side stream, a backend's
             # internal stream) can stay in capture mode: continue on fresh streams
             self.gstream = None
@@ -431,7 +465,12 @@ class Trainer:
         ex.use_dev_key = True
         ex.dev_key_advance = True  # the captured decode advances the device RNG key per replay
         self._key_synced = False
-        saved = (ex.step_idx, self.opt.steps)
+        inner = getattr(ex, "inner", None)  # local SGD's wrapped exchange
+        saved = (ex.step_idx, self.opt.steps, inner.step_idx if inner is not None else 0)
+        if inner is not None:
+            # the sync graph's delta encode reads its RNG key from device memory, set before
+            # every replay (_graph_step)
+            inner.use_dev_key = self._gkind == "sync"
         # thread_local: only this thread's capture-unsafe HIP calls are refused.  In "global" mode
         # the RCCL process group's watchdog thread, which polls its work events, hits
         # hipErrorStreamCaptureUnsupported whenever a poll lands inside our capture, and that
@@ -496,7 +535,9 @@ class Trainer:
                     ex.apply()
                 self._graphs = (ga, gb)
         finally:
-            ex.step_idx, self.opt.steps = saved
+            ex.step_idx, self.opt.steps = saved[:2]
+            if inner is not None:
+                inner.step_idx = saved[2]
         self._gloss, self._gout = loss, out
         self._gbytes = ex.bytes_per_step()
 
@@ -515,7 +556,7 @@ class Trainer:
         ex = self.exchange
         if self._in_graph_batch:
             if x is not None:  # an explicit batch after an in-graph-batch capture: re-capture
-                self._graphs = None
+                self._drop_graphs()
                 return self._train_step(x, y)
             self.loader.advance()
         elif x is not self._gx:
@@ -526,6 +567,10 @@ class Trainer:
         elif not self._key_synced and not self.local_sgd:
             ex.set_device_key()  # once per capture; the replays advance the key on the device
             self._key_synced = True
+        elif self.local_sgd and self._gkind == "sync":
+            # the delta encode's key of this sync (the eager path's inner.finish count)
+            ex.inner.set_device_key(ex.inner.step_idx)
+            ex.inner.step_idx += 1
         if len(self._graphs) == 1:
             with self._range("graph_step"):
                 self._graphs[0].replay()
@@ -539,7 +584,8 @@ class Trainer:
             self._graphs[1].replay()
         ex.step_idx += 1
         self.opt.steps += 1
-        ex.last = StepStats() if self.local_sgd else self._gbytes  # a local step sends nothing
+        # a local step sends nothing
+        ex.last = StepStats() if (self.local_sgd and self._gkind == "local") else self._gbytes
         self.step += 1
         return self._gloss, (self._gout, self._gy)
 
@@ -570,8 +616,25 @@ class Trainer:
         return {"test_loss": float(loss) / n, "top1": 100.0 * float(c1) / n,
                 "top5": 100.0 * float(c5) / n, "samples": n}
 
+    def _holdout_batch(self):
+        """The first held-out batch as static tensors (made once, outside any capture)."""
+        hb = getattr(self, "_hold_batch", None)
+        if hb is None:
+            self.test_loader.set_epoch(0)
+            x, y = next(iter(self.test_loader))
+            hb = self._hold_batch = (x.clone(), y.clone())
+        return hb
+
     def _holdout_score(self):
-        return self.evaluate(max_batches=1)["top1"]
+        """Top-1 (%) of this replica on the first held-out batch, as a 0-dim device tensor (no
+        host synchronisation: Method 6's best-worker choice runs inside the sync step's graph;
+        the same batch and the same value as ``evaluate(max_batches=1)["top1"]``)."""
+        x, y = self._holdout_batch()
+        self.model.eval()
+        with torch.no_grad(), self.autocast():
+            out = self.model(x)
+        self.model.train()
+        return (out.float().argmax(1) == y).sum(dtype=torch.float32) * (100.0 / y.shape[0])
 
     # --------------------------------------------------------------------------------------------
     def state_extra(self):

@@ -93,6 +93,28 @@ def test_conv_f32_forward(N, C, Nc, H, W, k):
 
 
 @pytest.mark.parametrize("N,C,Nc,H,W,k", SHAPES)
+def test_conv_f32_forward_lds_dma_staging(N, C, Nc, H, W, k):
+    """The forward GEMM with LDS-DMA operand staging (buffer_load ... lds, swizzle on the source
+    address, three stage images) writes bitwise what the register-staged kernel writes: the same
+    LDS images, the same MFMA order; padding taps read zeros through out-of-range offsets."""
+    from ewdml import ops
+
+    conv = _conv()
+    C_ = ops.require()
+    x, w = _data(N, C, Nc, H, W, seed=3, k=k)
+    prev = C_.cf_set_glds(0)
+    try:
+        y0 = conv.conv(x, w)
+        C_.cf_set_glds(1)
+        y1 = conv.conv(x, w)
+        torch.cuda.synchronize()
+    finally:
+        C_.cf_set_glds(prev)
+    torch.testing.assert_close(y1, y0, rtol=0, atol=0)
+    assert _rel(y1, _ref64(x, w, k)) < TOL
+
+
+@pytest.mark.parametrize("N,C,Nc,H,W,k", SHAPES)
 def test_conv_f32_backward(N, C, Nc, H, W, k):
     conv = _conv()
     x, w = _data(N, C, Nc, H, W, seed=1, k=k)
