@@ -298,7 +298,10 @@ class Trainer:
 
     def _sync_graphable(self) -> bool:
         # model mode: delta encode, all-gather and the on-device best-worker choice are all
-        # device work; grad mode's dense re-broadcast roots at a host-chosen rank
+        # device work; grad mode's dense re-broadcast roots at a host-chosen rank, and Gloo's
+        # CUDA collectives stage through the host (not capturable)
+        if self.comm.distributed and self.comm.backend == "gloo":
+            return False
         return self.exchange.mode == "model"
 
     def train_step(self, x=None, y=None):
@@ -436,8 +439,9 @@ class Trainer:
             # a stream forked into an aborted capture (the encode side stream, a backend's
             # internal stream) can stay in capture mode: continue on fresh streams
             self.gstream = None
-            if ex.side is not None:
-                ex.side = torch.cuda.Stream(device=self.device)
+            ge = getattr(ex, "inner", ex)  # the exchange that owns the encode side stream
+            if getattr(ge, "side", None) is not None:
+                ge.side = torch.cuda.Stream(device=self.device)
             try:
                 torch.cuda.synchronize()
             except Exception as e:  # noqa: BLE001 - the eager step below reports a real fault
@@ -544,7 +548,7 @@ class Trainer:
     def _rejoin_side(self):
         """Join the encode side stream back into a capture being aborted: hipStreamEndCapture
         refuses to close a capture with an unjoined fork and leaves the stream capturing."""
-        side = self.exchange.side
+        side = getattr(getattr(self.exchange, "inner", self.exchange), "side", None)
         if side is None:
             return
         with torch.cuda.stream(side):

@@ -371,3 +371,34 @@ def test_local_sgd_pointer_grads_match_views(monkeypatch):
     # LeNet's MIOpen convolutions are not run-to-run bitwise: compare at a tight tolerance
     rel = float((ptr.flat.data - views.flat.data).norm() / views.flat.data.norm())
     assert rel < 1e-5, f"pointer-mode local steps differ from views mode by {rel:.2e}"
+
+
+def _m6_rank(rank, world, steps):
+    import os
+
+    os.environ["LOCAL_RANK"] = "0"  # both ranks on the box's one GPU (Gloo between them)
+    from ewdml.runtime import Trainer
+
+    torch.manual_seed(0)
+    tr = Trainer(ewdml.parse_args(LENET + ["--method", "6", "--sync-every", "3", "--seed",
+                                           str(rank), "--max-steps", str(steps)]))
+    for _ in range(steps):
+        tr.train_step()
+    torch.cuda.synchronize()
+    ex = tr.exchange
+    return {"params": tr.flat.data.cpu(), "best": list(ex.best_rank_history),
+            "bn": [b.cpu() for b in tr.model.buffers()], "mode": tr.graph_mode}
+
+
+def test_method6_device_best_worker_two_ranks(tmp_path):
+    """Method 6 with two ranks on the GPU: the on-device best-worker choice (all-gathered scores,
+    argmax, the winner's payload row and BN buffers by index) leaves both replicas identical
+    after every sync, with the same winner recorded on both."""
+    from ..distributed.helpers import run_world
+
+    ops.require()
+    res = run_world(_m6_rank, 2, tmp_path, args=(6,))
+    torch.testing.assert_close(res[0]["params"], res[1]["params"], rtol=0, atol=0)
+    for a, b in zip(res[0]["bn"], res[1]["bn"]):
+        torch.testing.assert_close(a, b, rtol=0, atol=0)
+    assert res[0]["best"] == res[1]["best"] and len(res[0]["best"]) == 2

@@ -407,3 +407,54 @@ def test_pack_grads_mixed_dtypes():
         ops.pack_grads(dp, grads, dst, 0.5)
         for t, o, n in zip(grads, plan.offsets, plan.numels):
             assert torch.equal(dst[o:o + n], (t.float() * 0.5).to(dt))
+
+
+def test_topk_decode_sparse_update_bitwise():
+    """Without momentum buffer and weight decay the decode reads and writes only the float4s
+    whose averaged gradient is non-zero: bitwise the dense update (p - lr * (+0) is p, -0.0
+    parameters included), shadow copy too."""
+    ops.require()
+    plan = _plan([9000, 64, 33333], 0.01)
+    lay = Layout.build("topk_qsgd", plan, 8)
+    N = 2
+    recv = torch.stack([oracle.encode_topk(_grad(plan, seed=r), plan, lay, 127, "max",
+                                           stream_key(0, 0, r)) for r in range(N)]).to(DEV)
+    p0 = torch.randn(plan.length, device=DEV)
+    p0[::7] = -0.0
+    dp = ops.DevicePlan(plan, DEV)
+    sparse, sh_s = p0.clone(), torch.zeros(plan.length, dtype=torch.bfloat16, device=DEV)
+    ops.topk_decode_apply(dp, recv, lay, 127, param=sparse, mom=None, lr=0.05,
+                          grad_scale=1.0 / N, shadow=sh_s)
+    dense, sh_d = p0.clone(), torch.zeros(plan.length, dtype=torch.bfloat16, device=DEV)
+    mom = torch.zeros(plan.length, device=DEV)  # a momentum buffer forces the dense pass
+    ops.topk_decode_apply(dp, recv, lay, 127, param=dense, mom=mom, lr=0.05, momentum=0.0,
+                          grad_scale=1.0 / N, shadow=sh_d)
+    torch.cuda.synchronize()
+    assert torch.equal(sparse.view(torch.int32), dense.view(torch.int32))
+    changed = sparse.view(torch.int32) != p0.view(torch.int32)
+    assert 0 < int(changed.sum()) <= N * plan.total_k
+    # the shadow is written where the parameters were (the rest stays as it was: zeros here)
+    assert torch.equal(sh_s[changed], sh_d[changed])
+
+
+def test_sgd_from_pointer_table_matches_flat():
+    """Local SGD's fused step reads each tensor's gradient in place (pointer table, fp32 and
+    bf16): bitwise the flat-buffer SGD over the gathered gradient."""
+    ops.require()
+    plan = _plan([9000, 64, 33333, 5], 1.0)
+    dp = ops.DevicePlan(plan, DEV)
+    grads = [torch.randn(n, device=DEV) for n in plan.numels]
+    grads[1] = grads[1].to(torch.bfloat16)
+    flat_g = torch.zeros(plan.length, device=DEV)
+    for g, off, n in zip(grads, plan.offsets, plan.numels):
+        flat_g[off:off + n] = g.float()
+    p0, m0 = torch.randn(plan.length, device=DEV), torch.randn(plan.length, device=DEV)
+    hp = dict(lr=0.1, momentum=0.9, dampening=0.0, weight_decay=1e-3, nesterov=True)
+    p1, m1 = p0.clone(), m0.clone()
+    ops.sgd_ptrs(dp, grads, p1, m1, first=False, **hp)
+    p2, m2 = p0.clone(), m0.clone()
+    ops.sgd_flat(p2, m2, flat_g, first=False, **hp)
+    torch.cuda.synchronize()
+    for off, n in zip(plan.offsets, plan.numels):
+        assert torch.equal(p1[off:off + n], p2[off:off + n])
+        assert torch.equal(m1[off:off + n], m2[off:off + n])
