@@ -594,7 +594,6 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_write(
     const uint32_t gt_before = carry_gt + (ex & 0xffffu);
     uint32_t eqr = carry_eq + (ex >> 16);
     uint32_t pos = ebase + gt_before + min(ties, eqr);
-    float left[4];  // EF residual: what this rank did not send
     uint32_t nib = 0;  // bitmap bits of this thread's 4 elements
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -618,9 +617,12 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_write(
           sent = (float)q * step;
         }
         if (vel) vel[c.start + i0 + j] = 0.0f;  // DGC momentum factor masking: sent coordinates
+        // EF residual: what this rank did not send.  hist0 staged e in the residual, and e - 0
+        // is e bit for bit, so only the sent coordinates are rewritten (a sparse store instead
+        // of rewriting the whole bucket)
+        if (EF) resid[c.start + i0 + j] = xs[j] - sent;
         ++pos;
       }
-      left[j] = xs[j] - sent;
     }
     if (bitmap) {  // uniform per block: 8 lanes' nibbles make one word; every word is written
       uint32_t w = nib << (4 * (threadIdx.x & 7));
@@ -629,16 +631,6 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_write(
       w |= __shfl_xor(w, 4, 64);
       const int wi = i0 >> 5;
       if ((threadIdx.x & 7) == 0 && wi * 32 < c.len) bm_out[wi] = w;
-    }
-    if (EF) {
-      float* r = resid + c.start + i0;
-      if (i0 + 3 < c.len) {
-        *reinterpret_cast<float4*>(r) = make_float4(left[0], left[1], left[2], left[3]);
-      } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (valid[j]) r[j] = left[j];
-      }
     }
     carry_gt += tot & 0xffffu;
     carry_eq += tot >> 16;

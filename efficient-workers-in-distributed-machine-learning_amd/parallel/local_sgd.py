@@ -80,7 +80,7 @@ class LocalSGDExchange:
                 finally:
                     self.inner.src_flat = False
                 stats = self.inner.bytes_per_step()
-                if self.select_best and self.comm.world > 1:
+                if self.select_best and (self.comm.world > 1 or self.comm.kind != "local"):
                     # every rank holds every rank's compressed delta: apply the winner's.  The
                     # choice stays on the device (scores all-gathered, argmax, the winner's
                     # payload row and BN buffers selected by index), so this step has no host

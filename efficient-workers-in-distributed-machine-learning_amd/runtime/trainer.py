@@ -204,9 +204,12 @@ class Trainer:
                                              (ps_split and self.graph_mode == "split")):
             raise ValueError("--hip-graph: all-to-all topology (local SGD: full only; parameter "
                              "server without k-of-n: split only)")
-        if (self.graph_mode in ("full", "segmented") and self.comm.distributed
-                and self.comm.backend == "gloo" and not self.local_sgd and not self.ps_graph):
-            # gloo's CUDA collectives cannot be captured: graph the compute, issue them between
+        if (self.graph_mode in ("full", "segmented") and self._pg_collectives()
+                and not self.local_sgd and not self.ps_graph):
+            # the step's collectives on the process group: Gloo's CUDA collectives cannot be
+            # captured, and a captured RCCL process-group collective leaves a work event recorded
+            # in the capture that the group's watchdog thread then queries (hipErrorCapturedEvent
+            # kills the process) -- graph the compute, issue the collectives between the graphs
             self.graph_mode = "split"
         if self.graph_mode == "segmented":  # collectives on their own stream, beside backward
             self.exchange.comm_stream = torch.cuda.Stream(device=self.device)
@@ -296,11 +299,16 @@ class Trainer:
             self._in_graph_batch = False
         self._gkind = kind
 
+    def _pg_collectives(self) -> bool:
+        """The step's data-plane collectives go through the process group (Gloo, or RCCL when
+        the own communicator is off): not capturable in a HIP graph."""
+        return self.comm.kind == "process-group"
+
     def _sync_graphable(self) -> bool:
         # model mode: delta encode, all-gather and the on-device best-worker choice are all
-        # device work; grad mode's dense re-broadcast roots at a host-chosen rank, and Gloo's
-        # CUDA collectives stage through the host (not capturable)
-        if self.comm.distributed and self.comm.backend == "gloo":
+        # device work on the own communicator; grad mode's dense re-broadcast roots at a
+        # host-chosen rank
+        if self._pg_collectives():
             return False
         return self.exchange.mode == "model"
 

@@ -254,7 +254,9 @@ def test_own_rccl_communicator_matches_process_group(codec):
     own = _bench_pg(codec, "rccl")
     pg = _bench_pg(codec, "pg")
     assert own["config"]["comm"] == "rccl-stream" and pg["config"]["comm"] == "process-group"
-    assert own["config"]["hip_graph"] == "full" and pg["config"]["hip_graph"] == "full"
+    # process-group collectives stay outside the graphs (split): their watchdog must not see an
+    # event recorded inside a capture
+    assert own["config"]["hip_graph"] == "full" and pg["config"]["hip_graph"] == "split"
     assert own["final_loss"] == pg["final_loss"]
     assert own["payload_bytes_per_rank"] == pg["payload_bytes_per_rank"]
 
@@ -287,6 +289,16 @@ def test_bench_through_rccl_process_group(codec):
     assert rec["config"]["comm"] == "rccl-stream"
     assert rec["value"] > 0 and rec["n_gpus"] == 1
     assert rec["final_loss"] == rec["final_loss"]  # not NaN
+
+
+def test_method6_sync_graph_through_rccl():
+    """Method 6 under torch.distributed.run with the own RCCL communicator (world of one,
+    EWDML_FORCE_PG=1): the sync step -- compressed delta all-gather, the on-device best-worker
+    choice (score all-gather, argmax) and the BN-buffer all-gathers -- is captured with its RCCL
+    collectives, as the 8-GPU run needs."""
+    rec = _bench_pg("topk_qsgd", "rccl", extra=("--extra=--method 6 --sync-every 3",))
+    assert rec["config"]["comm"] == "rccl-stream" and rec["config"]["hip_graph"] == "full"
+    assert rec["final_loss"] == rec["final_loss"]
 
 
 @pytest.mark.parametrize("codec", ["topk_qsgd", "qsgd"])
