@@ -114,16 +114,17 @@ def test_topk_l2_norm_close():
 
 
 @pytest.mark.parametrize("kind,bits", [("topk_qsgd", 8), ("topk_qsgd", 4), ("topk", 8)])
-@pytest.mark.parametrize("ratio", [0.03, 0.4])
-def test_topk_decode_matches_oracle(kind, bits, ratio):
-    """ratio 0.4: most tensors are bitmap-indexed (plan.py), the 20-element one keeps the list."""
+@pytest.mark.parametrize("ratio,N", [(0.03, 5), (0.06, 5), (0.03, 11), (0.4, 5)])
+def test_topk_decode_matches_oracle(kind, bits, ratio, N):
+    """ratio 0.4: most tensors are bitmap-indexed (plan.py), the 20-element one keeps the list;
+    0.06: u16 lists with more entries per chunk than threads; N = 11: past the ranks whose first
+    entries the decode prefetches."""
     ops.require()
     plan = _plan([20 * 25, 20, 8192 * 5 + 3, 50, 70001], ratio, bucket_offset=128)
     if ratio > 0.1:
         assert plan.tensor_bm0[2] >= 0 and plan.total_bm_words > 0
     lay = Layout.build(kind, plan, bits)
     levels = 127 if bits == 8 else 7
-    N = 5
     pays = []
     for r in range(N):
         g = _grad(plan, seed=100 + r)
