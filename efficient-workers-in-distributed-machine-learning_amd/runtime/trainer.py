@@ -663,6 +663,20 @@ class Trainer:
                 allr = torch.zeros((self.world, r.numel()), dtype=r.dtype, device=r.device)
                 self.comm.all_gather(allr.view(-1), r)
                 extra[name] = allr
+        if self.local_sgd:
+            # between syncs every replica (and its momentum) has drifted on its own: keep every
+            # rank's row, the common anchor of the model-delta exchange and the sync count (the
+            # delta encode's RNG stream)
+            rows = {"local_params": self.flat.data}
+            if getattr(self.opt, "mom", None) is not None:
+                rows["local_mom"] = self.opt.mom
+            for name, r in rows.items():
+                allr = torch.zeros((self.world, r.numel()), dtype=r.dtype, device=r.device)
+                self.comm.all_gather(allr.view(-1), r)
+                extra[name] = allr
+            if ex.anchor is not None:
+                extra["local_anchor"] = ex.anchor
+            extra["local_syncs"] = inner.step_idx
         return extra
 
     @property
@@ -707,6 +721,18 @@ class Trainer:
                     mine.copy_(r[self.rank].to(self.device))
                 else:
                     self.log.info(f"resume: world size changed, {name} reset")
+        if self.local_sgd:
+            ex, ext = self.exchange, st["extra"]
+            rows = [(ext.get("local_params"), self.flat.data),
+                    (ext.get("local_mom"), getattr(self.opt, "mom", None))]
+            for r, mine in rows:
+                if r is not None and mine is not None and r.dim() == 2 and r.shape[0] == self.world:
+                    mine.copy_(r[self.rank].to(self.device))
+            self.flat.sync_shadow()
+            if ex.anchor is not None and ext.get("local_anchor") is not None:
+                ex.anchor.copy_(ext["local_anchor"].to(self.device))
+            if "local_syncs" in ext:
+                inner.step_idx = int(ext["local_syncs"])
         if hasattr(self.exchange, "step_idx"):
             self.exchange.step_idx = self.step
         if self.loader is not None:

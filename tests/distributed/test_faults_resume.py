@@ -41,6 +41,24 @@ def test_resume_reproduces_uninterrupted_run(tmp_path):
     assert torch.equal(res[1]["params"], res[0]["params"])
 
 
+def test_local_sgd_resume_reproduces_uninterrupted_run(tmp_path):
+    """Method 6 (compressed model deltas, best-worker choice) resumed between two syncs: every
+    rank's drifted replica and momentum, the common anchor and the sync count come back, so the
+    run continues exactly as the uninterrupted one."""
+    m6 = ["--method", "6", "--sync-every", "4", "--eval-freq", "0"]
+    full = run_world(_fit, 2, tmp_path / "a", args=(m6 + ["--max-steps", "9", "--train-dir",
+                                                          str(tmp_path / "ca") + "/"],))
+    d = str(tmp_path / "cb") + "/"
+    run_world(_fit, 2, tmp_path / "b", args=(m6[:-1] + ["3", "--max-steps", "6",
+                                                        "--train-dir", d],))
+    res = run_world(_fit, 2, tmp_path / "c", args=(m6 + ["--max-steps", "9", "--resume",
+                                                         "--train-dir", d],))
+    for r in (0, 1):
+        assert res[r]["step"] == 9
+        assert torch.equal(res[r]["params"], full[r]["params"])
+        assert torch.equal(res[r]["mom"], full[r]["mom"])
+
+
 def test_injected_fault_aborts_all_ranks_without_hang(tmp_path):
     port = free_port()
     procs = []
