@@ -240,7 +240,8 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_hist1(GradPtrs gp, const floa
 }
 
 // Histogram of key bits [9:0] over the tensor's candidates matching the 21-bit prefix: the block of
-// chunk j reads candidates [8192 j, 8192 (j + 1)) of its tensor's list (most blocks have none).
+// chunk j reads candidates [8192 j, 8192 (j + 1)) of its tensor's list (most blocks have none and
+// return at once).
 // The tensor's last block selects the threshold and resets the candidate count for the next encode.
 __global__ __launch_bounds__(EW_BLOCK) void k_topk_hist2(const ChunkRow* __restrict__ chunks,
                                                          uint32_t* __restrict__ state,
@@ -251,12 +252,18 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_hist2(const ChunkRow* __restr
                                                          const uint32_t* __restrict__ cand,
                                                          int* __restrict__ cand_n) {
   __shared__ uint32_t h[NB2];
-  for (int i = threadIdx.x; i < NB2; i += EW_BLOCK) h[i] = 0;
-  __syncthreads();
   const ChunkRow c = chunks[blockIdx.x];
-  const uint32_t want = state[c.tensor * 4] >> 10;
   const int n = __hip_atomic_load(cand_n + TICK_STRIDE * c.tensor, __ATOMIC_RELAXED,
                                   __HIP_MEMORY_SCOPE_AGENT);
+  // only the first ceil(n / EW_CHUNK) chunk blocks of a tensor have candidates to read: the rest
+  // leave at once (no histogram, no ticket), so the tensor's ticket counts just the readers.  A
+  // reader reads n before it arrives and the count is reset only after the last arrival, so every
+  // reader sees the same n; a block that sees the reset value is not a reader either way.
+  const int readers = max(1, (n + EW_CHUNK - 1) / EW_CHUNK);  // chunk 0 always runs the select
+  if (c.local >= readers) return;
+  for (int i = threadIdx.x; i < NB2; i += EW_BLOCK) h[i] = 0;
+  __syncthreads();
+  const uint32_t want = state[c.tensor * 4] >> 10;
   const uint32_t* src = cand + tensors[c.tensor].off;
   const int i1 = min(n, (c.local + 1) * EW_CHUNK);
   for (int i = c.local * EW_CHUNK + (int)threadIdx.x; i < i1; i += EW_BLOCK) {
@@ -267,9 +274,9 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_hist2(const ChunkRow* __restr
   uint32_t* dst = hist + ((size_t)(blockIdx.x & (NREP - 1)) * T + c.tensor) * NB2;
   for (int i = threadIdx.x; i < NB2; i += EW_BLOCK)
     if (h[i]) atomicAdd(&dst[i], h[i]);
-  if (topk_tensor_last(tick + TICK_STRIDE * c.tensor, tensors[c.tensor].nchunks, reinterpret_cast<int*>(h))) {
+  if (topk_tensor_last(tick + TICK_STRIDE * c.tensor, readers, reinterpret_cast<int*>(h))) {
     topk_select<NB2, 0, false>(hist, tensors, state, kmaxr, T, c.tensor);
-    if (threadIdx.x == 0) cand_n[TICK_STRIDE * c.tensor] = 0;  // every block read it before arriving
+    if (threadIdx.x == 0) cand_n[TICK_STRIDE * c.tensor] = 0;  // every reader read it before arriving
   }
 }
 
