@@ -77,6 +77,7 @@ SHAPES = [
     (16, 64, 256, 32, 32, 1),    # 1x1 expand
     (16, 256, 64, 32, 32, 1),    # 1x1 reduce
     (32, 512, 2048, 4, 4, 1),    # 1x1, small M
+    (32, 256, 64, 32, 32, 1),    # ResNet layer-1 1x1 reduce: 64x256 weight-gradient tile, split-K
 ]
 
 
