@@ -171,7 +171,12 @@ class ResNet(nn.Module):
         else:
             out = F.relu(self.bn1(self.conv1(x)))
         if self.stem == "imagenet":
-            out = F.max_pool2d(out, 3, 2, 1)
+            if fused.active(x):
+                from ..ops.nn import maxpool3x3s2  # NHWC HIP kernels (gather backward)
+
+                out = maxpool3x3s2(out)
+            else:
+                out = F.max_pool2d(out, 3, 2, 1)
         out = self.layer4(self.layer3(self.layer2(self.layer1(out))))
         out = F.adaptive_avg_pool2d(out, 1).flatten(1)
         return self.linear(out)

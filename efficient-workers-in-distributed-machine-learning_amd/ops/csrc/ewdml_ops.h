@@ -145,6 +145,10 @@ void ew_bn_relu_fwd(const BnFwdArgs& a);
 void ew_bn_relu_bwd(const BnBwdArgs& a);
 void ew_maxpool2_nhwc(uintptr_t x, uintptr_t y, uintptr_t code, long long N, int H, int W, int C,
                       int is_bf16, int backward, uintptr_t stream);
+// NHWC 3x3 / stride 2 / pad 1 max pool (C % 8 == 0): forward y + 1-byte tap codes, backward dx
+// (x = dy, y = dx) gathered from the windows whose code points at each pixel
+void ew_maxpool3s2_nhwc(uintptr_t x, uintptr_t y, uintptr_t code, long long N, int H, int W,
+                        int C, int is_bf16, int backward, uintptr_t stream);
 // NCHW 2x2 max pool: rows = N*C*H/2
 void ew_maxpool2_fwd(uintptr_t x, uintptr_t y, uintptr_t code, long long rows, int W, int is_bf16,
                      uintptr_t stream);

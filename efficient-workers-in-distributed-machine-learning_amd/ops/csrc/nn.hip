@@ -677,6 +677,94 @@ __global__ __launch_bounds__(EW_BLOCK) void k_maxpool2_nhwc_bwd(const T* __restr
   }
 }
 
+// ---- standalone NHWC 3x3 / stride 2 / pad 1 max pool (the ImageNet ResNet stem) ----
+// Forward: thread = (output pixel, 8 channels); the window's taps in (kh, kw) order, padding as
+// -inf, a tap wins on > or NaN (F.max_pool2d's rule); the winning tap 0..8 is the 1-byte code.
+// Backward as a gather (no atomics, deterministic): thread = (input pixel, 8 channels), summing in
+// (oh, ow) order the dy of the (at most 2 x 2) windows whose code points at this pixel.
+template <typename T>
+__global__ __launch_bounds__(EW_BLOCK) void k_maxpool3s2_nhwc_fwd(const T* __restrict__ x,
+                                                                  T* __restrict__ y,
+                                                                  uint8_t* __restrict__ code,
+                                                                  long long rows, int C, int H,
+                                                                  int W, int Ho, int Wo) {
+  const uint32_t tpr = C >> 3, HoWo = (uint32_t)Ho * Wo;
+  const uint32_t nvec = (uint32_t)rows * tpr;
+  for (uint32_t v = blockIdx.x * EW_BLOCK + threadIdx.x; v < nvec; v += gridDim.x * EW_BLOCK) {
+    const uint32_t row = v / tpr;
+    const int c0 = (int)(v - row * tpr) * 8;
+    const uint32_t n = row / HoWo, rem = row - n * HoWo;
+    const int oh = (int)(rem / (uint32_t)Wo), ow = (int)(rem - (uint32_t)oh * Wo);
+    float m[8];
+    uint32_t k[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      m[j] = -INFINITY;
+      k[j] = 0;
+    }
+#pragma unroll
+    for (int q = 0; q < 9; ++q) {
+      const int h = 2 * oh - 1 + q / 3, w = 2 * ow - 1 + q % 3;
+      if ((unsigned)h >= (unsigned)H || (unsigned)w >= (unsigned)W) continue;
+      float a[8];
+      V8<T>::ld(x + (((long long)n * H + h) * W + w) * C + c0, a);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (a[j] > m[j] || a[j] != a[j]) {
+          m[j] = a[j];
+          k[j] = q;
+        }
+      }
+    }
+    V8<T>::st(y + (long long)row * C + c0, m);
+    uint2 cw;
+    cw.x = k[0] | (k[1] << 8) | (k[2] << 16) | (k[3] << 24);
+    cw.y = k[4] | (k[5] << 8) | (k[6] << 16) | (k[7] << 24);
+    *reinterpret_cast<uint2*>(code + (long long)row * C + c0) = cw;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(EW_BLOCK) void k_maxpool3s2_nhwc_bwd(const T* __restrict__ dy,
+                                                                  const uint8_t* __restrict__ code,
+                                                                  T* __restrict__ dx,
+                                                                  long long rows, int C, int H,
+                                                                  int W, int Ho, int Wo) {
+  const uint32_t tpr = C >> 3, HW = (uint32_t)H * W;
+  const uint32_t nvec = (uint32_t)rows * tpr;  // rows = N H W input pixels
+  for (uint32_t v = blockIdx.x * EW_BLOCK + threadIdx.x; v < nvec; v += gridDim.x * EW_BLOCK) {
+    const uint32_t row = v / tpr;
+    const int c0 = (int)(v - row * tpr) * 8;
+    const uint32_t n = row / HW, rem = row - n * HW;
+    const int h = (int)(rem / (uint32_t)W), w = (int)(rem - (uint32_t)h * W);
+    // windows oh with 2 oh - 1 <= h <= 2 oh + 1
+    const int oh0 = h >> 1, oh1 = (h + 1) >> 1, ow0 = w >> 1, ow1 = (w + 1) >> 1;
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = 0.0f;
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const int oh = a ? oh1 : oh0;
+      if ((a && oh1 == oh0) || oh >= Ho) continue;
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int ow = b ? ow1 : ow0;
+        if ((b && ow1 == ow0) || ow >= Wo) continue;
+        const uint32_t q = (uint32_t)((h - 2 * oh + 1) * 3 + (w - 2 * ow + 1));
+        const long long r = ((long long)n * Ho + oh) * Wo + ow;
+        float d[8];
+        uint8_t kc[8];
+        V8<T>::ld(dy + r * C + c0, d);
+        ew_ld_code8(code + r * C + c0, kc);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (kc[j] == q) o[j] += d[j];
+      }
+    }
+    V8<T>::st(dx + (long long)row * C + c0, o);
+  }
+}
+
 inline int ew_grid1(long long n) {
   long long b = (n + EW_BLOCK - 1) / EW_BLOCK;
   return (int)(b < 4096 ? (b > 0 ? b : 1) : 4096);
@@ -883,6 +971,37 @@ void ew_maxpool2_nhwc(uintptr_t x, uintptr_t y, uintptr_t code, long long N, int
       hipLaunchKernelGGL(k_maxpool2_nhwc_bwd<float>, dim3(grid), dim3(EW_BLOCK), 0, s,
                          reinterpret_cast<const float*>(x), cd, reinterpret_cast<float*>(y), rows,
                          C, Ho, Wo);
+  }
+  EW_CHECK_LAUNCH();
+}
+
+void ew_maxpool3s2_nhwc(uintptr_t x, uintptr_t y, uintptr_t code, long long N, int H, int W,
+                        int C, int is_bf16, int backward, uintptr_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;  // kernel 3, stride 2, pad 1
+  uint8_t* cd = reinterpret_cast<uint8_t*>(code);
+  if (!backward) {
+    const long long rows = N * (long long)Ho * Wo;
+    const int grid = ew_grid_vec(rows * (C / 8));
+    if (is_bf16)
+      hipLaunchKernelGGL(k_maxpool3s2_nhwc_fwd<uint16_t>, dim3(grid), dim3(EW_BLOCK), 0, s,
+                         reinterpret_cast<const uint16_t*>(x), reinterpret_cast<uint16_t*>(y), cd,
+                         rows, C, H, W, Ho, Wo);
+    else
+      hipLaunchKernelGGL(k_maxpool3s2_nhwc_fwd<float>, dim3(grid), dim3(EW_BLOCK), 0, s,
+                         reinterpret_cast<const float*>(x), reinterpret_cast<float*>(y), cd, rows,
+                         C, H, W, Ho, Wo);
+  } else {  // x = dy (pooled), y = dx (full)
+    const long long rows = N * (long long)H * W;
+    const int grid = ew_grid_vec(rows * (C / 8));
+    if (is_bf16)
+      hipLaunchKernelGGL(k_maxpool3s2_nhwc_bwd<uint16_t>, dim3(grid), dim3(EW_BLOCK), 0, s,
+                         reinterpret_cast<const uint16_t*>(x), cd, reinterpret_cast<uint16_t*>(y),
+                         rows, C, H, W, Ho, Wo);
+    else
+      hipLaunchKernelGGL(k_maxpool3s2_nhwc_bwd<float>, dim3(grid), dim3(EW_BLOCK), 0, s,
+                         reinterpret_cast<const float*>(x), cd, reinterpret_cast<float*>(y), rows,
+                         C, H, W, Ho, Wo);
   }
   EW_CHECK_LAUNCH();
 }

@@ -21,7 +21,7 @@ import os
 
 import torch
 
-from . import _ptr, _stream, require
+from . import _ptr, _stream, available, require
 
 _WS = {}
 
@@ -321,6 +321,49 @@ def maxpool2x2(x):
     if not ok:
         return F.max_pool2d(x, 2, 2)
     return _MaxPool2.apply(x)
+
+
+class _MaxPool3s2(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        C_ = require()
+        N, C, H, W = x.shape
+        Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+        bf = int(x.dtype == torch.bfloat16)
+        y = torch.empty((N, C, Ho, Wo), dtype=x.dtype, device=x.device,
+                        memory_format=torch.channels_last)
+        code = torch.empty((N, Ho, Wo, C), dtype=torch.uint8, device=x.device)
+        C_.maxpool3s2_nhwc(_ptr(x), _ptr(y), _ptr(code), N, H, W, C, bf, 0, _stream())
+        ctx.shape = x.shape
+        ctx.save_for_backward(code)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        C_ = require()
+        (code,) = ctx.saved_tensors
+        N, C, H, W = ctx.shape
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        dx = torch.empty((N, C, H, W), dtype=dy.dtype, device=dy.device,
+                         memory_format=torch.channels_last)
+        C_.maxpool3s2_nhwc(_ptr(dy), _ptr(dx), _ptr(code), N, H, W, C,
+                           int(dy.dtype == torch.bfloat16), 1, _stream())
+        return dx
+
+
+def maxpool3x3s2(x):
+    """``F.max_pool2d(x, 3, 2, 1)`` (the ImageNet ResNet stem's pool): HIP kernels for device
+    bf16/fp32 channels_last tensors with C % 8 == 0 (backward a deterministic gather), torch
+    otherwise."""
+    import torch.nn.functional as F
+
+    ok = (x.is_cuda and x.dim() == 4 and x.dtype in (torch.bfloat16, torch.float32)
+          and x.numel() > 0 and x.numel() < 2 ** 31 and x.shape[1] % 8 == 0
+          and x.is_contiguous(memory_format=torch.channels_last) and x.data_ptr() % 16 == 0
+          and available())
+    if not ok:
+        return F.max_pool2d(x, 3, 2, 1)
+    return _MaxPool3s2.apply(x)
 
 
 _UNIT_GRAD = [0]  # data pointer of the trainer's persistent d(loss)/d(loss) = 1 seed

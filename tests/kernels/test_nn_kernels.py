@@ -171,6 +171,34 @@ def test_maxpool2x2_exact(layout, dtype):
     assert torch.equal(a.grad.float(), b.grad.float())
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("hw", [(12, 10), (13, 9), (112, 112)])
+def test_maxpool3x3s2_matches_torch(dtype, hw):
+    """3x3 / stride 2 / pad 1 max pool (the ImageNet ResNet stem's): values and tap choice as
+    F.max_pool2d (first maximum in (kh, kw) order, NaN wins; ties included), gradient gathered
+    from every window whose winner is the pixel -- against PyTorch's CPU pool in float64 (its
+    scatter adds the same terms; overlapping windows share a pixel)."""
+    fnn = _ops()
+    torch.manual_seed(5)
+    H, W = hw
+    N = 2 if H > 64 else 4
+    x = torch.randint(-3, 4, (N, 16, H, W), device="cuda").to(dtype)  # many ties
+    x[0, 0, 0, 0] = float("nan")
+    x = x.contiguous(memory_format=torch.channels_last)
+    a = x.clone().requires_grad_(True)
+    y = fnn.maxpool3x3s2(a)
+    assert y.grad_fn is not None and "MaxPool3s2" in type(y.grad_fn).__name__
+    b = x.detach().cpu().double().requires_grad_(True)
+    yr = F.max_pool2d(b, 3, 2, 1)
+    assert torch.equal(torch.nan_to_num(y.double().cpu(), 99.0), torch.nan_to_num(yr, 99.0))
+    dy = torch.randn(yr.shape).to(dtype)
+    y.backward(dy.cuda().contiguous(memory_format=torch.channels_last))
+    yr.backward(dy.double())
+    torch.testing.assert_close(a.grad.double().cpu(), b.grad, rtol=1e-2 if dtype ==
+                               torch.bfloat16 else 1e-6, atol=1e-2 if dtype == torch.bfloat16
+                               else 1e-6)
+
+
 def _vgg_run(model, x, y, fused_on, amp):
     from ewdml.models import fused
 
