@@ -2,4 +2,4 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT; export TMPDIR=/tmp; mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/kernels/test_hip_codecs.py > gpurun_out/codec_tests.log 2>&1 || { tail -40 gpurun_out/codec_tests.log; exit 1; }
 tail -1 gpurun_out/codec_tests.log
-bash tools/gpu_encode_ab.sh
+bash tools/ab/gpu_encode_ab.sh
