@@ -40,9 +40,12 @@ _DTYPES = ((torch.bfloat16,) if os.environ.get("EWDML_CONV_F32", "hip") == "miop
 # the BN backward's own statistics pass)
 _BN_BWD = os.environ.get("EWDML_CONV_BN_BWD", "1") != "0"
 # ... and the residual-gradient addend (GradSink), only for inputs of at most this many elements:
-# the epilogue reads the extra operands with 2-byte loads in the MFMA output layout, which on
-# large maps costs more than the separate, vectorised statistics / add kernels it replaces
-_EPI_MAX = int(os.environ.get("EWDML_EPI_MAX", str(1 << 23)))
+# the bf16 epilogue reads the extra operands with 2-byte loads in the MFMA output layout, which on
+# large maps costs more than the separate, vectorised statistics / add kernels it replaces; the
+# fp32 epilogue's 4-byte loads pay everywhere (ResNet-50 fp32 with no limit: CIFAR +1.0 %, 224 px
+# +2.2 %; bf16 with it lifted: -0.2 % / -0.9 %: profiles/ab/epilogue_fusion_size_gate.txt)
+_EPI_MAX = int(os.environ.get("EWDML_EPI_MAX", str(1 << 23)))  # bf16 inputs
+_EPI_MAX_F32 = int(os.environ.get("EWDML_EPI_MAX_F32", str(1 << 62)))
 
 
 # Winograd F(m x m, 3x3) for fp32 3x3 layers with min(C_in, C_out) >= _WINO_MIN_C (the deep layers,
@@ -217,7 +220,7 @@ def wino_ok(x, w) -> bool:
 
 def epilogue_fusion_ok(x) -> bool:
     """Whether a conv on input ``x`` takes the epilogue fusions (BN backward sums, addend)."""
-    return x.numel() <= _EPI_MAX
+    return x.numel() <= (_EPI_MAX_F32 if x.dtype == torch.float32 else _EPI_MAX)
 _WS = {}
 
 
