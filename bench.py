@@ -208,6 +208,11 @@ def main(argv=None):
         "ref_equiv_MiB_per_step": round(bytes_["ref_equiv_MiB_per_step"], 4),
         "ref_equiv_reduction": bytes_["ref_equiv_reduction"],
         "final_loss": final_loss,
+        # a throughput run, not a convergence one: W + K steps from random init with the
+        # steady-state codec (no EF density / lr warm-up, which the CLI default --ef-warmup auto
+        # runs); convergence with error feedback: profiles/validation/ef_stability_r03.md
+        "final_loss_note": f"{a.warmup + a.steps} steps from random init, steady-state codec "
+                           "without the EF warm-up (see profiles/validation/ef_stability_r03.md)",
         "host_enqueue_ms_per_step": round(enq * 1e3 / a.steps, 4),
         "hip_ext": ewdml.ops.library_path() if cuda else None,
     }
