@@ -214,8 +214,8 @@ class Trainer:
         if self.graph_mode == "segmented":  # collectives on their own stream, beside backward
             self.exchange.comm_stream = torch.cuda.Stream(device=self.device)
         self._graphs = None
-        # local SGD keeps two captured steps: "local" and (model mode without best-worker choice)
-        # "sync"; the idle one waits here with its static inputs and outputs
+        # local SGD keeps two captured steps, "local" and (model mode, own communicator) "sync";
+        # the idle one waits here with its static inputs and outputs
         self._gkind, self._gslots = "local", {}
         self.captures = 0  # graph captures so far (a schedule change should not force one)
         self._in_graph_batch = False
