@@ -50,13 +50,17 @@ _EPI_MAX_F32 = int(os.environ.get("EWDML_EPI_MAX_F32", str(1 << 62)))
 
 # Winograd F(m x m, 3x3) for fp32 3x3 layers with min(C_in, C_out) >= _WINO_MIN_C (the deep layers,
 # where the GEMM outweighs the transforms' activation traffic: tools/probes/conv_f32_probe.py --wino).
-# m: EWDML_WINO_TILE = 2 (default), 4 or auto (4 where the map tiles by 4 and C_out <= 512, else
-# 2).  m = 4 measured only +1.5 % on the VGG-11 step (smaller, more numerous GEMMs; 36-point
+# m: EWDML_WINO_TILE = size (default, below), 2, 4 or auto (4 where the map tiles by 4 and C_out <=
+# 512, else 2).  m = 4 measured only +1.5 % on the VGG-11 step (smaller, more numerous GEMMs; 36-point
 # transforms) for ~4x m = 2's rounding error (5e-6 vs 1.3e-6 relative for MIOpen's fp32 on the
 # whole-network forward): the default keeps m = 2 (profiles/conv/winograd_f32_probe_m4.txt)
 _WINO = os.environ.get("EWDML_WINOGRAD", "1") != "0"
 _WINO_MIN_C = int(os.environ.get("EWDML_WINO_MIN_C", "128"))
-_WINO_TILE = os.environ.get("EWDML_WINO_TILE", "2")
+# "size" (default): m = 4 where it fits and leaves at least _WINO_M4_MIN_TILES output tiles (the
+# batched GEMMs' rows), else m = 2 -- ResNet-50's 16x16 / 28x28 layers gain from m = 4 (+2.2 % /
+# +1.6 % with every fitting layer at m = 4), VGG-11's 8x8 / 4x4 ones lose (few, short GEMMs)
+_WINO_TILE = os.environ.get("EWDML_WINO_TILE", "size")
+_WINO_M4_MIN_TILES = int(os.environ.get("EWDML_WINO_M4_MIN_TILES", "2048"))
 # m = 4 for the layers with min(C_in, C_out) <= this many channels (and m = EWDML_WINO_TILE above),
 # for layers below _WINO_MIN_C too: 0 = off
 _WINO_M4_MAX_C = int(os.environ.get("EWDML_WINO_M4_MAX_C", "0"))
@@ -210,6 +214,9 @@ def wino_tile_for(shape, dtype, w) -> int:
     order = {"2": (2,), "4": (4,)}.get(_WINO_TILE, (4, 2))
     for m in order:
         if _wino_fits(N, C, Nc, H, W, m):
+            if (m == 4 and _WINO_TILE == "size"
+                    and N * (H // 4) * (W // 4) < _WINO_M4_MIN_TILES):
+                continue
             return m
     return 0
 

@@ -89,8 +89,10 @@ def test_lr_schedule_in_graph_without_recapture(opt):
     assert tr.captures == 1 and tr._graphs is not None
     assert float(tr.opt.lr_t.item()) == pytest.approx(tr.opt.lr)
     assert tr.opt.lr < tr.base_lr  # still warming up
+    # LeNet's MIOpen convolutions are not bitwise between eager and captured runs, and a last-bit
+    # difference can move a top-k choice: the same 1e-3 bound as test_graph_modes_match_eager
     rel = float((tr.flat.data - ref.flat.data).norm() / ref.flat.data.norm())
-    assert rel < 1e-4, rel
+    assert rel < 1e-3, rel
 
 
 def test_graph_replay_refreshes_rng_key():

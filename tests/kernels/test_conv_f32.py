@@ -344,6 +344,10 @@ def test_conv_f32_winograd_tile_choice():
     conv.set_winograd(True, 128, 2)
     x, w = _data(128, 256, 256, 8, 8)
     assert conv.wino_tile(x, w) == 2
+    conv.set_winograd(True, 128, "size")  # m = 4 only with >= 2048 output tiles
+    assert conv.wino_tile(x, w) == 2  # 128 x 2 x 2 = 512 tiles
+    x, w = _data(128, 128, 128, 16, 16)
+    assert conv.wino_tile(x, w) == 4  # 128 x 4 x 4 = 2048 tiles
 
 
 def test_conv_f32_winograd_only_where_chosen():
