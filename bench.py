@@ -190,7 +190,7 @@ def main(argv=None):
                    "seq_len": None, "parallelism": f"dp{world}",
                    "codec": tr.exchange.codec.describe() if hasattr(tr.exchange, "codec") else
                    a.compress, "error_feedback": ef, "optimizer": "sgd(momentum=0.9)",
-                   "overlap": not a.no_overlap, "buckets": nb, "hip_graph": tr.graph_mode,
+                   "overlap_requested": not a.no_overlap, "buckets": nb, "hip_graph": tr.graph_mode,
                    "bf16_params": tr.flat.shadow is not None,
                    "grad_mode": "views" if tr.flat.attach_grads else "pointers",
                    "layout": "nhwc" if tr.channels_last else "nchw",
