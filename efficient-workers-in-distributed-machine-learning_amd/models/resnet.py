@@ -16,6 +16,8 @@ On the GPU (``models.fused`` enabled) every BN runs through the fused NHWC kerne
 ``relu(bn3(conv3) + shortcut)`` as one BN+add+ReLU kernel set; the stride-1 3x3 and 1x1
 convolutions run the MFMA implicit-GEMM kernels (``ewdml.ops.conv``); same modules and state_dict.
 """
+import os
+
 import torch.nn as nn
 import torch.nn.functional as F
 
@@ -33,6 +35,8 @@ def _conv(m, x):
 
 # identity-residual gradients through a GradSink (False: autograd sums them; A/B and tests)
 _RESIDUAL_SINK = True
+# ... for projection shortcuts too (EWDML_PROJ_SINK=0: identity shortcuts only; A/B)
+_PROJ_SINK = os.environ.get("EWDML_PROJ_SINK", "1") != "0"
 
 
 def set_residual_sink(on: bool):
@@ -41,19 +45,22 @@ def set_residual_sink(on: bool):
 
 
 def _residual_block(x, main, bn_last, sc):
-    """``relu(bn_last(main(x, sink)) + shortcut(x))`` on the fused kernels.  With an identity
-    shortcut and an MFMA first conv, the residual's gradient is not summed by autograd: the last
-    BN's backward deposits it in a :class:`GradSink` and the first conv's backward-data epilogue
-    adds it (one launch less per block, and the block input keeps a single consumer, so the
-    previous block's BN can take its backward statistics from that epilogue too)."""
-    from ..ops.conv import GradSink, epilogue_fusion_ok
+    """``relu(bn_last(main(x, sink)) + shortcut(x))`` on the fused kernels.  With an MFMA first
+    conv, the shortcut's gradient of the block input is not summed by autograd: the last BN's
+    backward (identity shortcut) or the projection conv's backward (through ``sink_tap``)
+    deposits it in a :class:`GradSink` and the first conv's backward-data epilogue adds it (one
+    launch less per block, and the block input's gradient is that conv's output alone, so the
+    previous block's BN can take its backward statistics from the same epilogue)."""
+    from ..ops.conv import GradSink, epilogue_fusion_ok, sink_tap
     from ..ops.nn import bn_act, kernel_path
 
-    sink = GradSink() if (_RESIDUAL_SINK and len(sc) == 0 and x.requires_grad
-                          and epilogue_fusion_ok(x)) else None
+    sink = GradSink() if (_RESIDUAL_SINK and x.requires_grad and epilogue_fusion_ok(x)) else None
     h, first_mfma = main(x, sink)
-    if sink is not None and first_mfma and kernel_path(h, bn_last, x):
-        return bn_act(h, bn_last, "add_relu", res=x.detach(), res_sink=sink)
+    if sink is not None and first_mfma:
+        if len(sc) and _PROJ_SINK:
+            return bn_act(h, bn_last, "add_relu", res=_shortcut(sc, sink_tap(x, sink)))
+        if not len(sc) and kernel_path(h, bn_last, x):
+            return bn_act(h, bn_last, "add_relu", res=x.detach(), res_sink=sink)
     return bn_act(h, bn_last, "add_relu", res=_shortcut(sc, x))
 
 

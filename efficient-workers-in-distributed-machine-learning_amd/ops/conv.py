@@ -446,6 +446,9 @@ class _Conv(torch.autograd.Function):
                                         and add.is_contiguous(memory_format=torch.channels_last)
                                         and add.data_ptr() % 16 == 0):
                 add = add.contiguous(memory_format=torch.channels_last).to(x.dtype)
+            if add is not None:
+                global SINK_ADDS
+                SINK_ADDS += 1
             link = _bn_bwd_link(node, x)
             if m:
                 # m = 2: the forward's U, read flipped; m = 4: the rotated kernel's transform
@@ -485,7 +488,7 @@ class _Conv(torch.autograd.Function):
                 if rows > 0:
                     node._ew_pre_bwd = (part, rows, dx, dx._version)
             if sink is not None:
-                sink.grad = None
+                sink.grad, sink.taken = None, True
         if ctx.needs_input_grad[1]:
             dw = torch.empty_like(w, memory_format=torch.channels_last)
             if m:
@@ -641,14 +644,45 @@ def conv_s2(x, w):
     return F.conv2d(x, w, stride=2, padding=w.shape[-1] // 2)
 
 
+SINK_ADDS = 0  # backward-data launches that added a sink's gradient (tests)
+
+
 class GradSink:
     """Hand-over slot for a second gradient of a conv's input (``grad``: set by the producer's
-    backward, consumed and cleared by the conv's backward-data launch)."""
+    backward, consumed and cleared by the conv's backward-data launch; ``taken``: that launch has
+    run, so a later producer must hand its gradient to autograd instead)."""
 
-    __slots__ = ("grad",)
+    __slots__ = ("grad", "taken")
 
     def __init__(self):
         self.grad = None
+        self.taken = False
+
+
+class _SinkTap(torch.autograd.Function):
+    """Identity on ``x`` whose backward deposits the incoming gradient in ``sink`` (returning
+    none to autograd) while the sink's conv has not run its backward yet.  ResNet projection
+    shortcuts read the block input through it: the shortcut branch is recorded after the main
+    branch, so autograd runs its backward first and the block's first conv adds its input
+    gradient in the backward-data epilogue (models/resnet.py)."""
+
+    @staticmethod
+    def forward(ctx, x, sink):
+        ctx.sink = sink
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        sink, ctx.sink = ctx.sink, None
+        if sink is None or sink.taken:
+            return g, None
+        sink.grad = g
+        return None, None
+
+
+def sink_tap(x, sink):
+    """``x`` for a second consumer whose input gradient goes to ``sink`` (:class:`_SinkTap`)."""
+    return _SinkTap.apply(x, sink)
 
 
 def _apply(x, w, sink=None):

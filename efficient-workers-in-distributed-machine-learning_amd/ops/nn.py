@@ -153,7 +153,7 @@ class _BNAct(torch.autograd.Function):
             # in its backward input transform (ops/conv.py); dx is written only if materialised
             dx._ew_lazy_bwd = (h, dy, code, stats, coef, ctx.pool)
             dx._ew_materialize = lambda: C_.bn_relu_bwd(*args, 2)
-        if sink is not None:  # the residual's gradient goes to the block's first conv (ops/conv)
+        if sink is not None and not sink.taken:  # to the block's first conv (ops/conv)
             sink.grad, dres = dres, None
         return dx, dres, dcb, dg, db, None, None, None, None, None, None, None, None, None, None
 

@@ -721,3 +721,52 @@ def test_exchange_tied_winograd_weights():
     finally:
         conv._POISON_DW = False
         ex.close()
+
+
+@pytest.mark.parametrize("s2", [True, False])
+def test_projection_shortcut_gradient_sink_matches_autograd_sum(s2):
+    """ResNet-50 projection shortcuts (stride 1 in layer 1 on the MFMA conv; stride 2 on our
+    stride-2 kernels or MIOpen) hand the block input's shortcut gradient to conv1's backward-data
+    epilogue through a GradSink (models/resnet.py): one fp32 step with the sinks matches the step
+    where autograd sums the two input gradients (bitwise forward on our kernels; MIOpen's fp32
+    solvers are not run-to-run deterministic)."""
+    from ewdml.models import build_model, resnet
+    from ewdml.ops import conv as cmod
+
+    _conv(wino=True, min_c=128, tile="size")
+    cmod.set_stride2(s2)
+    torch.manual_seed(0)
+    m0 = build_model("resnet50", 10).cuda().to(memory_format=torch.channels_last)
+    x = torch.randn(8, 3, 32, 32, device="cuda").contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (8,), device="cuda")
+    # MIOpen (the stride-2 convs) picks its solvers on the first call: settle them first
+    F.cross_entropy(copy.deepcopy(m0)(x), y).backward()
+    res = []
+    # MIOpen: a second run without sinks measures the run-to-run noise (BN's cancellations
+    # amplify fp32 solver differences to ~1e-2 in the gradients after 50 layers)
+    for sink in (True, False) if s2 else (True, False, False):
+        resnet.set_residual_sink(sink)
+        m = copy.deepcopy(m0)
+        adds = cmod.SINK_ADDS
+        try:
+            out = m(x)
+            F.cross_entropy(out, y).backward()
+        finally:
+            resnet.set_residual_sink(True)
+        n = cmod.SINK_ADDS - adds
+        # 16 blocks: 12 identity + 4 projection sinks; none with the sinks off
+        assert n == (16 if sink else 0), n
+        res.append((out.detach(), [p.grad.detach().clone() for p in m.parameters()]))
+    (o_a, g_a), (o_b, g_b) = res[:2]
+    errs = [_rel(a, b) for a, b in zip(g_a, g_b)]
+    e = sum(errs) / len(errs)
+    if s2:
+        assert torch.equal(o_a, o_b)
+        assert e < 1e-5, (e, max(errs))
+    else:
+        g_c = res[2][1]
+        noise = [_rel(a, b) for a, b in zip(g_c, g_b)]
+        e_n = sum(noise) / len(noise)
+        assert _rel(o_a, o_b) < 1e-4, _rel(o_a, o_b)
+        assert e <= 3 * e_n + 1e-5 and max(errs) <= 3 * max(noise) + 1e-5, (e, e_n, max(errs),
+                                                                             max(noise))
