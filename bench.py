@@ -67,7 +67,10 @@ def parse(argv=None):
     p.add_argument("--no-overlap", action="store_true")
     p.add_argument("--error-feedback", default="on", choices=["on", "off"])
     p.add_argument("--no-extras", action="store_true", help="headline run only")
-    p.add_argument("--hip-graph", default="full", choices=["off", "split", "full", "segmented"])
+    # auto: the one-graph step at N = 1 and for top-k payloads; per-bucket collectives overlapped
+    # with backward (segmented graphs) for large dense collectives at N > 1 (plan_graph_mode)
+    p.add_argument("--hip-graph", default="auto",
+                   choices=["auto", "off", "split", "full", "segmented"])
     p.add_argument("--param-dtype", default="auto", choices=["auto", "fp32"])
     p.add_argument("--json-out", default=None, help="also write the JSON line to this file")
     p.add_argument("--extra", default="", help="extra distributed_nn.py flags")
@@ -95,6 +98,8 @@ def _flags(a, world, amp, ef):
         flags.append("--no-overlap")
     if ef:  # the timed steps run the steady-state codec: no density / lr warm-up phase
         flags += ["--error-feedback", "--ef-warmup", "none"]
+    else:
+        flags.append("--no-error-feedback")
     # graph capture happens inside the untimed warmup: eager steps, then the capturing step
     gw = max(1, min(3, a.warmup - 1))
     flags += ["--hip-graph", a.hip_graph, "--graph-warmup", str(gw), "--param-dtype",
@@ -105,7 +110,13 @@ def _flags(a, world, amp, ef):
 def measure(a, world, amp, ef, extra=()):
     """Build a Trainer for this configuration, run W untimed warmup steps, then time exactly K
     steps bracketed by barrier + synchronize on both sides; returns (max-over-ranks seconds,
-    trainer, final loss, host enqueue seconds)."""
+    trainer, final loss, host enqueue seconds, per-rank seconds [min, max], replica check).
+
+    After the timed steps every rank fingerprints its flat parameters (fp64 sums and the XOR of
+    the raw words) and all ranks compare them: synchronous data parallelism must leave the
+    replicas bitwise identical, so a wrong collective on a first multi-GPU run shows up here
+    instead of as a plausible img/s (local SGD's replicas legitimately differ between syncs:
+    no check there)."""
     import torch
 
     import ewdml
@@ -140,12 +151,18 @@ def measure(a, world, amp, ef, extra=()):
     tr.comm.barrier()
     sync()
     elapsed_max = tr.comm.all_reduce_scalars([t1 - t0], op="max")[0]
+    elapsed_min = -tr.comm.all_reduce_scalars([-(t1 - t0)], op="max")[0]
+    from ewdml.parallel.engine import check_replicas
+
+    rep = None if every > 1 else check_replicas(tr.comm, tr.flat.data)
     final_loss = float(loss.detach()) if loss is not None else float("nan")
     tr.comm_kind = tr.comm.kind
+    tr.comm_probe = None if tr.comm.probe is None else {
+        k: tr.comm.probe[k] for k in ("ok", "eager", "graph")}
     g = getattr(tr, "_graphs", None)
     tr.overlap_comm_graphs = len(g[1].comms) if (g and g[0] == "segmented") else 0
     tr.close()  # watchdog and own RCCL communicator (the next measure() builds its own)
-    return elapsed_max, tr, final_loss, t_enq - t0
+    return elapsed_max, tr, final_loss, t_enq - t0, (elapsed_min, elapsed_max), rep
 
 
 def main(argv=None):
@@ -160,7 +177,7 @@ def main(argv=None):
     if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}; launch with torch.distributed.run")
     ef = a.error_feedback == "on"
-    elapsed_max, tr, final_loss, enq = measure(a, world, a.amp, ef)
+    elapsed_max, tr, final_loss, enq, span, rep = measure(a, world, a.amp, ef)
     cuda = tr.cuda
     ms = elapsed_max * 1e3 / a.steps
     img_s = world * a.batch_size * a.steps / elapsed_max
@@ -214,6 +231,16 @@ def main(argv=None):
         "final_loss_note": f"{a.warmup + a.steps} steps from random init, steady-state codec "
                            "without the EF warm-up (see profiles/validation/ef_stability_r03.md)",
         "host_enqueue_ms_per_step": round(enq * 1e3 / a.steps, 4),
+        # multi-GPU self-validation: replicas bitwise identical after the timed steps, the
+        # data-plane communicator and its first-contact probe (parallel/probe.py)
+        "replicas_identical": rep["identical"],
+        "replica_fingerprint": rep["fingerprints"][0],
+        "comm": tr.comm_kind,
+        "rccl_world": world if tr.comm_kind == "rccl-stream" else 0,
+        "comm_probe": tr.comm_probe,
+        "graph_plan": tr.graph_plan,
+        "step_ms_min": round(span[0] * 1e3 / a.steps, 4),
+        "step_ms_max": round(span[1] * 1e3 / a.steps, 4),
         "hip_ext": ewdml.ops.library_path() if cuda else None,
     }
     del tr
@@ -231,7 +258,9 @@ def main(argv=None):
         for key, amp, e, xf in extras:
             if cuda:
                 torch.cuda.empty_cache()
-            el, tr2, fl, _ = measure(a, world, amp, e, xf)
+            el, tr2, fl, _, _, rep2 = measure(a, world, amp, e, xf)
+            if rep2 is not None:
+                rec[f"replicas_identical_{key}"] = rep2["identical"]
             rec[f"value_{key}"] = round(world * a.batch_size * a.steps / el, 2)
             rec[f"ms_per_step_{key}"] = round(el * 1e3 / a.steps, 4)
             rec[f"final_loss_{key}"] = fl
@@ -251,8 +280,12 @@ def main(argv=None):
         if a.json_out:
             with open(a.json_out, "w") as f:
                 f.write(line + "\n")
+    diverged = [k for k, v in rec.items() if k.startswith("replicas_identical") and v is False]
     if dist.is_initialized():
         dist.destroy_process_group()
+    if diverged:  # every rank knows (the check is collective): fail the job loudly
+        raise SystemExit(f"replicas differ after the timed steps ({', '.join(diverged)}): the "
+                         "data-plane collectives are wrong; the img/s above is not valid")
     return rec
 
 

@@ -72,7 +72,10 @@ class Config:
     sync_mode: str = "grad"  # grad: compressed gradient on sync steps | model: compressed delta
     sync_mode_default: bool = True  # --sync-mode not given (--method 6 then selects 'model')
     select_best: bool = False  # method 6: adopt the weights of the best-accuracy rank at sync
-    error_feedback: bool = False
+    # None (auto): on for the top-k codecs -- top-k at 1 % without error feedback trains 10-80x
+    # slower than dense (profiles/validation/ef_stability_r03.md) -- off otherwise;
+    # --no-error-feedback gives the reference's Methods 5/6 as published (no residual)
+    error_feedback: Optional[bool] = None
     # dgc: momentum correction + momentum factor masking (the sender runs the momentum before
     # top-k; oracle.dgc_accumulate) | plain: residual of the raw gradient, momentum after decode
     ef_mode: str = "dgc"
@@ -132,6 +135,11 @@ class Config:
     metrics_file: Optional[str] = None  # per-step JSONL
     profile: int = 0  # wrap N steps in torch.profiler
     roctx: bool = False  # roctx ranges per phase (rocprofv3 --marker-trace)
+    # per-step phase times (forward / backward / encode / collective / decode_update, or per graph
+    # segment) from HIP events on the step's stream, in the JSONL and summary.json; serialises the
+    # eager step (no side stream) and makes --hip-graph auto split the graph at the collectives
+    phase_timing: bool = False
+    summary_file: Optional[str] = None  # rank 0's run summary (default <train_dir>/summary.json)
     inject_fault: Optional[str] = None  # "rank:step" -> that rank raises at that step (tests)
     comm_timeout: float = 600.0
     sync_debug: bool = False  # synchronise after every custom kernel (race / fault localisation)
@@ -161,6 +169,19 @@ class Config:
                     c.sync_mode = "model"
         if c.compress_grad.lower() == "none":
             c.compress = "none"
+        if c.error_feedback is None:
+            c.error_feedback = c.compress in ("topk", "topk_qsgd")
+        if c.ef_mode == "ef21" and c.error_feedback and c.device != "cpu" and not c.no_cuda:
+            import os
+
+            # the EF21 encode exists only in the torch oracle (flat gradient views)
+            if not (os.environ.get("EWDML_ORACLE") == "1"
+                    and os.environ.get("EWDML_GRAD_VIEWS") == "1"):
+                import torch
+
+                if c.device == "cuda" or torch.cuda.is_available():
+                    raise ValueError("--ef-mode ef21 has no HIP encode kernel: run it on the CPU, "
+                                     "or on the GPU with EWDML_ORACLE=1 EWDML_GRAD_VIEWS=1")
         if (c.ef_warmup == "auto" and c.error_feedback and c.compress in ("topk", "topk_qsgd")
                 and c.sync_every == 1 and not c.select_best):
             stages = [r for r in EF_WARMUP_STAGES if r > c.topk_ratio]
@@ -224,7 +245,8 @@ def build_parser(prog="distributed_nn.py") -> argparse.ArgumentParser:
     a("--sync-every", type=int, default=d.sync_every)
     a("--sync-mode", type=str, default=None, choices=["grad", "model"])
     a("--select-best", action="store_true", default=False)
-    a("--error-feedback", action="store_true", default=False)
+    a("--error-feedback", dest="error_feedback", action="store_true", default=None)
+    a("--no-error-feedback", dest="error_feedback", action="store_false")
     a("--ef-mode", type=str, default=d.ef_mode, choices=["dgc", "plain", "local", "ef21"])
     a("--topk-warmup", type=str, default=d.topk_warmup)
     a("--topk-warmup-epochs", type=float, default=d.topk_warmup_epochs)
@@ -267,6 +289,8 @@ def build_parser(prog="distributed_nn.py") -> argparse.ArgumentParser:
     a("--metrics-file", type=str, default=None)
     a("--profile", type=int, default=0)
     a("--roctx", action="store_true", default=False)
+    a("--phase-timing", action="store_true", default=False)
+    a("--summary-file", type=str, default=None)
     a("--inject-fault", type=str, default=None)
     a("--comm-timeout", type=float, default=d.comm_timeout)
     a("--sync-debug", action="store_true", default=False)

@@ -393,12 +393,6 @@ class _Conv(torch.autograd.Function):
         # the leaf Parameter itself (not a cast / copy): its .grad decides whether the Winograd
         # weight-gradient output transform may be deferred (_can_defer)
         ctx.w_param = w if isinstance(w, torch.nn.Parameter) else None
-        if ctx.w_param is not None:
-            # a weight used twice in one pass (tied weights) gets its dw summed with the other
-            # use's in autograd's input buffer before any hook runs: never deferred (_can_defer)
-            if getattr(w, "_ew_use_epoch", None) == _USE_EPOCH[0]:
-                w._ew_tied = True
-            w._ew_use_epoch = _USE_EPOCH[0]
         ctx.bn_part = (part, rows) if rows > 0 else None
         ctx.bn_node = bn_node
         ctx.sink = sink
@@ -695,6 +689,15 @@ def _apply(x, w, sink=None):
         y = _Conv.apply(x, w, node, sink)
     # hand the epilogue's BatchNorm partials to the consumer (bn_act reads ``_ew_bn_part``)
     node = y.grad_fn  # the autograd ctx of _Conv / _ConvStem (None under no_grad)
+    wp = getattr(node, "w_param", None) if node is not None else None
+    if wp is not None:
+        # a weight used twice in one pass (tied weights) gets its dw summed with the other use's
+        # in autograd's input buffer before any hook runs: never deferred (_can_defer).  Only
+        # forwards that record autograd history count (node is None under no_grad): an eval or
+        # best-worker scoring forward in the same step is no second use.
+        if getattr(wp, "_ew_use_epoch", None) == _USE_EPOCH[0]:
+            wp._ew_tied = True
+        wp._ew_use_epoch = _USE_EPOCH[0]
     part = getattr(node, "bn_part", None) if node is not None else None
     if part is not None:
         y._ew_bn_part = part

@@ -366,24 +366,42 @@ def maxpool3x3s2(x):
     return _MaxPool3s2.apply(x)
 
 
-_UNIT_GRAD = [0]  # data pointer of the trainer's persistent d(loss)/d(loss) = 1 seed
+_UNIT_GRAD = [None]  # (weakref to the trainer's persistent d(loss)/d(loss) = 1 seed, version)
 
 
 def set_unit_grad(seed):
     """Register the persistent all-ones loss seed: a cross-entropy whose backward receives it
-    returns the d(loss)/d(logits) its forward kernel already wrote (no backward launch)."""
-    _UNIT_GRAD[0] = seed.data_ptr() if (seed is not None and seed.numel() == 1) else 0
+    returns the d(loss)/d(logits) its forward kernel already wrote (no backward launch).  Only a
+    weak reference is kept: a seed that was dropped can never match (its memory may be reused),
+    and one written since registration no longer holds 1 and does not match either."""
+    import weakref
+
+    if seed is None or seed.numel() != 1 or seed.dtype != torch.float32:
+        _UNIT_GRAD[0] = None
+        return
+    _UNIT_GRAD[0] = (weakref.ref(seed), seed._version)
+
+
+def _unit_seed():
+    reg = _UNIT_GRAD[0]
+    if reg is None:
+        return None
+    seed = reg[0]()
+    if seed is None or seed._version != reg[1]:
+        return None
+    return seed
 
 
 class _CrossEntropy(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, logits, y):
+    def forward(ctx, logits, y, want_dx):
         C_ = require()
         B, K = logits.shape
         loss = torch.empty((), dtype=torch.float32, device=logits.device)
         lse = torch.empty(B, dtype=torch.float32, device=logits.device)
         # with a registered unit seed the gradient for an upstream 1 is formed in the same launch
-        dx = torch.empty_like(logits) if _UNIT_GRAD[0] else None
+        # (only when a backward can follow: not under no_grad / for eval forwards)
+        dx = torch.empty_like(logits) if want_dx else None
         C_.cross_entropy_fwd(_ptr(logits), _ptr(y), B, K, int(logits.dtype == torch.bfloat16),
                              _ptr(loss), _ptr(lse), _stream(), _ptr(dx))
         ctx.save_for_backward(logits, y, lse)
@@ -395,15 +413,16 @@ class _CrossEntropy(torch.autograd.Function):
         C_ = require()
         logits, y, lse = ctx.saved_tensors
         dx1, ctx.dx1 = ctx.dx1, None
-        if dx1 is not None and grad.numel() == 1 and grad.data_ptr() == _UNIT_GRAD[0] \
-                and grad.dtype == torch.float32:
-            return dx1, None
+        seed = _unit_seed()
+        if (dx1 is not None and seed is not None and grad.numel() == 1
+                and grad.dtype == torch.float32 and grad.data_ptr() == seed.data_ptr()):
+            return dx1, None, None
         B, K = logits.shape
         g = grad.detach().float().contiguous()
         dx = torch.empty_like(logits)
         C_.cross_entropy_bwd(_ptr(logits), _ptr(y), _ptr(lse), _ptr(g), B, K,
                              int(logits.dtype == torch.bfloat16), _ptr(dx), _stream())
-        return dx, None
+        return dx, None, None
 
 
 def cross_entropy(logits, y):
@@ -416,5 +435,7 @@ def cross_entropy(logits, y):
             and logits.is_contiguous() and y.dtype == torch.int64 and y.dim() == 1
             and y.is_contiguous() and y.shape[0] == logits.shape[0] and 0 < logits.shape[0]
             and logits.numel() < 2 ** 31):
-        return _CrossEntropy.apply(logits, y)
+        want = (logits.requires_grad and torch.is_grad_enabled()
+                and _unit_seed() is not None)
+        return _CrossEntropy.apply(logits, y, want)
     return F.cross_entropy(logits.float(), y)

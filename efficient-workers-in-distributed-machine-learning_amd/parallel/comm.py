@@ -58,9 +58,36 @@ class Comm:
                                                and self.backend != "local")
         self.rccl = None  # handle of the stream-ordered RCCL communicator (see module doc)
         self.watchdog = None  # native step watchdog (arm_watchdog)
+        self.probe = None  # outcome of the first-contact collective probe (parallel/probe.py)
         if (self.backend == "nccl" and not self._local and group is None
                 and os.environ.get("EWDML_COMM", "rccl") != "pg"):
             self.rccl = self._make_rccl()
+            if self.rccl is not None and os.environ.get("EWDML_COMM_PROBE", "1") != "0":
+                self._verify_rccl()
+
+    def _verify_rccl(self):
+        """Probe the own communicator (eager and graph-captured collectives against their closed
+        forms, all ranks agreeing); on any failure every rank destroys it and the data plane
+        falls back to the process group (whose collectives the trainer keeps outside its graphs:
+        split graphs)."""
+        import logging
+
+        from .probe import probe_collectives
+
+        log = logging.getLogger("ewdml")
+        res = probe_collectives(self, torch.device("cuda", torch.cuda.current_device()))
+        self.probe = res
+        if res["ok"]:
+            return
+        log.warning(f"RCCL communicator probe failed on at least one rank (this rank: eager="
+                    f"{res['eager']} graph={res['graph']} error={res['error']}): collectives "
+                    "fall back to the process group on every rank")
+        torch.cuda.synchronize()
+        try:
+            self._rc().rccl_destroy(self.rccl)
+        except Exception as e:  # noqa: BLE001 - the handle is dropped either way
+            log.warning(f"destroying the failed communicator: {e!r}")
+        self.rccl = None
 
     def _make_rccl(self):
         """Create the RCCL communicator (collective over the process group: rank 0's unique id
@@ -191,7 +218,7 @@ class Comm:
         return dist.all_reduce(t, op=op, group=self.group, async_op=async_op)
 
     def broadcast(self, t: torch.Tensor, src: int = 0, async_op: bool = False):
-        if self.world == 1:
+        if self._local:
             return None
         if self.rccl is not None and t.is_cuda and t.is_contiguous():
             from ..ops import _ptr, _stream

@@ -19,6 +19,8 @@ re-broadcasting weights.  That is the all-to-all counterpart of the reference's 
 (``sync_replicas_master_nn.py:158-232``: gather -> sum -> /(N-1) -> broadcast) with no idle server.
 """
 import contextlib
+import math
+import os
 import time
 
 import torch
@@ -117,6 +119,7 @@ class GradientExchange:
         self._hooks = []
         self.seg = None  # SegmentedCapture while a segmented step capture is recording
         self._final = False
+        self.clock = None  # Stopwatch of --phase-timing (marks on the step's stream)
         if overlap:
             for p in flat.params:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
@@ -234,11 +237,18 @@ class GradientExchange:
                     self._encode(bi)
                     self._works[bi] = self._collective(bi)
             return
+        clk = self.clock if self.side is None else None  # marks partition ONE stream
         for bi in bis:
             with self._stream_ctx():
+                if clk is not None:
+                    clk.mark("backward")  # the compute since the previous mark
                 self._encode(bi)
+                if clk is not None:
+                    clk.mark("encode")
                 if not self.defer_comm:
                     self._works[bi] = self._collective(bi)
+                    if clk is not None:
+                        clk.mark("collective")
 
     def _encode(self, bi: int):
         b = self.flat.buckets[bi]
@@ -333,9 +343,13 @@ class GradientExchange:
             self.communicate()
         self.wait()
         self.join_side()
+        if self.clock is not None:
+            self.clock.mark("collective")  # waiting for the issued collectives
         self._active = False
         if apply:
             self.apply()
+            if self.clock is not None:
+                self.clock.mark("decode_update")
         self.last = self.bytes_per_step()
         self.step_idx += 1
 
@@ -463,11 +477,26 @@ class SegmentedCapture:
         with torch.cuda.stream(self.gs):
             self.cur.capture_begin(pool=self.pool, capture_error_mode=self.mode)
 
-    def split(self, issue):
-        with torch.cuda.stream(self.gs):
-            self.cur.capture_end()
-        self.segments.append(self.cur)
+    def _end_segment(self):
+        """End the current compute segment's capture; an empty one (a split right at the end of
+        backward, nothing captured since) is kept as ``None`` and never replayed."""
+        import warnings
+
+        with warnings.catch_warnings(record=True) as caught:
+            warnings.simplefilter("always")
+            with torch.cuda.stream(self.gs):
+                self.cur.capture_end()
+        empty = False
+        for w in caught:
+            if "Graph is empty" in str(w.message):
+                empty = True
+            else:  # anything else is re-issued
+                warnings.warn_explicit(w.message, w.category, w.filename, w.lineno)
+        self.segments.append(None if empty else self.cur)
         self.cur = None
+
+    def split(self, issue):
+        self._end_segment()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.stream(self.cs):
             g.capture_begin(pool=self.cpool, capture_error_mode=self.mode)
@@ -480,10 +509,7 @@ class SegmentedCapture:
         self.begin()
 
     def end(self):
-        with torch.cuda.stream(self.gs):
-            self.cur.capture_end()
-        self.segments.append(self.cur)
-        self.cur = None
+        self._end_segment()
 
     def abort(self):
         """End a capture left open by a failure (the stream must not stay capturing)."""
@@ -497,23 +523,115 @@ class SegmentedCapture:
 
     @property
     def launches(self) -> int:
-        return len(self.segments) + len(self.comms) + (self.apply is not None)
+        return (sum(s is not None for s in self.segments) + len(self.comms)
+                + (self.apply is not None))
 
-    def replay(self):
+    def replay(self, clock=None):
+        """Replay the step.  ``clock`` (--phase-timing): compute segments are booked as
+        ``compute``, the compute stream's wait for the comm graphs as ``comm_wait`` (the exposed
+        part of the collectives), the apply as ``decode_update``, and each comm graph's own span
+        on the comm stream as the overlapped side interval ``comm_graph``."""
         cur = torch.cuda.current_stream()
         for i, seg in enumerate(self.segments):
-            seg.replay()
+            if seg is not None:
+                seg.replay()
+            if clock is not None:
+                clock.mark("compute")
             if i < len(self.comms):
                 ev = self._evs[i]
                 ev.record(cur)
                 self.cs.wait_event(ev)
                 with torch.cuda.stream(self.cs):
+                    t0 = clock.event(self.cs) if clock is not None else None
                     self.comms[i].replay()
+                    if clock is not None:
+                        clock.side("comm_graph", t0, clock.event(self.cs))
         if self.comms:
             self._done.record(self.cs)
             cur.wait_event(self._done)
+            if clock is not None:
+                clock.mark("comm_wait")
         if self.apply is not None:
             self.apply.replay()
+            if clock is not None:
+                clock.mark("decode_update")
+
+
+# --hip-graph auto: a dense collective at least this large per rank per step (algorithmic wire
+# bytes) is worth overlapping with backward at N > 1
+OVERLAP_MIN_WIRE_BYTES = int(float(os.environ.get("EWDML_OVERLAP_MIN_MB", "4")) * (1 << 20))
+# one comm graph per this many payload bytes (each split costs a graph boundary, ~0.1 ms at N=1)
+OVERLAP_BYTES_PER_SPLIT = 32 << 20
+OVERLAP_MAX_SPLITS = 3
+
+
+def plan_graph_mode(world: int, comm_kind: str, codec_kind: str, grad_numel: int,
+                    bits: int = 8, overlap: bool = True, bucket_bytes: int = 16 << 20) -> dict:
+    """``--hip-graph auto`` for the all-to-all exchange (``GradientExchange``).
+
+    * N = 1, or collectives on the process group (not capturable), or ``--no-overlap``: the
+      one-graph step (``full``; the trainer demotes it to ``split`` for process-group
+      collectives).  At N = 1 there is nothing to hide: the segmented step only adds graph
+      boundaries (+11 % on dense VGG-11, profiles/ab/segmented_overlap.txt).
+    * Top-k codecs: ``full`` at every N.  Their all-gather is a few hundred KiB per rank (tens of
+      microseconds over 7 xGMI links) while their encode, which has to run on the comm stream in a
+      segmented step, slows the concurrent backward GEMMs by more than it hides (+20 % at N = 1).
+    * Dense codecs (fp32 / half all-reduce, dense QSGD all-gather) at N > 1 whose per-rank wire
+      bytes reach ``OVERLAP_MIN_WIRE_BYTES``: ``segmented`` -- per-bucket collectives on their
+      own stream overlap the rest of backward, as Horovod's background all-reduce does
+      (``horvod_pytorch.py:197-201``) and the reference's ``LeNetSplit`` prototyped
+      (``src/model_ops/lenet.py:111-186``).  One split per 32 MiB of payload (at most 3), and
+      buckets small enough that every split point has buckets on both sides.
+
+    Returns ``{"mode", "splits", "bucket_bytes", "wire_bytes", "reason"}``."""
+    per_elem = {"none": 4.0, "fp16": 2.0, "bf16": 2.0, "qsgd": bits / 8.0}.get(codec_kind)
+    payload = grad_numel * (per_elem or 0.0)
+    if codec_kind in ("none", "fp16", "bf16"):
+        wire = 2.0 * (world - 1) / max(world, 1) * payload  # ring all-reduce
+    else:
+        wire = (world - 1) * payload  # all-gather
+    out = {"mode": "full", "splits": 1, "bucket_bytes": int(bucket_bytes), "wire_bytes": int(wire)}
+    if world <= 1:
+        return dict(out, reason="one rank: nothing to overlap")
+    if comm_kind != "rccl-stream":
+        return dict(out, reason="process-group collectives are not captured")
+    if not overlap:
+        return dict(out, reason="--no-overlap")
+    if per_elem is None:
+        return dict(out, reason="top-k payloads are small; the encode would slow backward")
+    if wire < OVERLAP_MIN_WIRE_BYTES:
+        return dict(out, reason="collective below the overlap threshold")
+    splits = int(min(OVERLAP_MAX_SPLITS, max(1, math.ceil(payload / OVERLAP_BYTES_PER_SPLIT))))
+    want = (4 * grad_numel) // (2 * (splits + 1))
+    bb = int(min(bucket_bytes, max(1 << 20, want)))
+    return {"mode": "segmented", "splits": splits, "bucket_bytes": bb, "wire_bytes": int(wire),
+            "reason": "dense collective overlapped with backward"}
+
+
+def replica_fingerprint(t: torch.Tensor) -> dict:
+    """Order-sensitive fingerprint of a replica's flat fp32 parameters: the fp64 sum, an fp64
+    position-weighted sum, and the XOR fold of the raw 32-bit words (bit-exact)."""
+    x = t.detach().reshape(-1)
+    if x.dtype != torch.float32:
+        x = x.float()
+    w = (torch.arange(x.numel(), device=x.device, dtype=torch.int64) % 65521 + 1).double()
+    bits = x.contiguous().view(torch.int32)
+    while bits.numel() > 1:
+        if bits.numel() % 2:
+            bits = torch.cat([bits, bits.new_zeros(1)])
+        bits = torch.bitwise_xor(bits[0::2], bits[1::2])
+    return {"sum": float(x.double().sum()), "wsum": float((x.double() * w).sum()),
+            "xor": int(bits.item()) & 0xFFFFFFFF if bits.numel() else 0}
+
+
+def check_replicas(comm, t: torch.Tensor) -> dict:
+    """Collective: every rank's fingerprint of ``t``; ``identical`` when all are bitwise equal
+    (synchronous data parallelism keeps every replica identical -- the property the reference's
+    broadcast of the averaged gradient is meant to give, ``sync_replicas_master_nn.py:193-212``)."""
+    fp = replica_fingerprint(t)
+    allfp = comm.all_gather_object(fp)
+    key = [(repr(f["sum"]), repr(f["wsum"]), f["xor"]) for f in allfp]  # NaN-safe comparison
+    return {"identical": all(k == key[0] for k in key), "fingerprints": allfp}
 
 
 def sync_params(flat, comm, src: int = 0):
@@ -535,13 +653,29 @@ def sync_buffers(model, comm, src: int = 0, only_to: int = None):
 
 
 class Stopwatch:
-    """HIP-event (GPU) or wall-clock (CPU) phase timer."""
+    """Phase clock: HIP events on the step's stream (GPU) or wall clock (CPU).
+
+    ``mark(name)`` closes the interval since the previous mark and books it under ``name``, so
+    the marks of one step partition its timeline: the phases sum to the step time exactly
+    (``--phase-timing``; the reference's per-worker ``time_send`` / ``time_recieve`` /
+    computation split, ``src/distributed_worker.py:130-155, 214-231``).  Repeated names
+    accumulate (e.g. one ``encode`` + ``collective`` pair per bucket).  ``side(name, a, b)`` books
+    an interval of another stream (a collective overlapped with backward) that is not part of
+    the partition.  Marks are skipped while a HIP graph is being captured."""
+
+    COMM_PHASES = ("collective", "comm_wait")  # exposed communication (the rest is compute)
 
     def __init__(self, cuda: bool):
         self.cuda = cuda
         self.marks = []
+        self.sides = []
+
+    def _capturing(self) -> bool:
+        return self.cuda and torch.cuda.is_current_stream_capturing()
 
     def mark(self, name: str):
+        if self._capturing():
+            return
         if self.cuda:
             e = torch.cuda.Event(enable_timing=True)
             e.record()
@@ -549,16 +683,51 @@ class Stopwatch:
         else:
             self.marks.append((name, time.perf_counter()))
 
-    def phases(self):
-        """{phase: ms} between consecutive marks (synchronises on GPU)."""
+    def event(self, stream=None):
+        """A timing event recorded on ``stream`` (GPU), or the wall clock (CPU)."""
+        if not self.cuda:
+            return time.perf_counter()
+        e = torch.cuda.Event(enable_timing=True)
+        e.record(stream)
+        return e
+
+    def side(self, name: str, start, end):
+        self.sides.append((name, start, end))
+
+    def _ms(self, a, b) -> float:
+        return a.elapsed_time(b) if self.cuda else (b - a) * 1e3
+
+    def phases(self) -> dict:
+        """{phase: ms} summed over the step's intervals (synchronises on the GPU); ``side:*``
+        entries are the overlapped intervals of other streams."""
         out = {}
+        if self.cuda and (self.marks or self.sides):
+            torch.cuda.synchronize()
+        for (_, a), (n1, b) in zip(self.marks, self.marks[1:]):
+            out[n1] = out.get(n1, 0.0) + self._ms(a, b)
+        for n, a, b in self.sides:
+            key = "side:" + n
+            out[key] = out.get(key, 0.0) + self._ms(a, b)
+        return out
+
+    def total(self) -> float:
+        """The step time: first to last mark."""
         if len(self.marks) < 2:
-            return out
+            return 0.0
         if self.cuda:
             self.marks[-1][1].synchronize()
-        for (n0, a), (n1, b) in zip(self.marks, self.marks[1:]):
-            out[n1] = a.elapsed_time(b) if self.cuda else (b - a) * 1e3
-        return out
+        return self._ms(self.marks[0][1], self.marks[-1][1])
+
+    @classmethod
+    def split(cls, phases: dict) -> tuple:
+        """(communication ms, computation ms) of a phase dict: the reference report's
+        "Communication and Computation Time" split (exposed communication only; overlapped
+        collectives are compute-stream time)."""
+        comm = sum(v for k, v in phases.items() if k in cls.COMM_PHASES)
+        comp = sum(v for k, v in phases.items() if not k.startswith("side:")
+                   and k not in cls.COMM_PHASES)
+        return comm, comp
 
     def reset(self):
         self.marks = []
+        self.sides = []

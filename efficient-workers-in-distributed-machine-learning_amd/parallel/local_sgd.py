@@ -10,9 +10,14 @@ Modes:
   * ``model`` (Method 6's default) -- local steps everywhere; on sync steps each rank compresses
     its *model delta* since the last sync with the wrapped exchange's codec and all-gathers it;
     the deltas are averaged and added to the common anchor (compressed model averaging).  With
-    ``select_best`` every rank instead applies the *best rank's* compressed delta, which the
-    all-gather already delivered: adopting the winner costs no extra weight traffic, only its BN
-    statistics (counted).
+    ``select_best`` every rank -- the winner included -- sets its weights to
+    ``anchor + decode(payload of the best rank)``, which the all-gather already delivered:
+    adopting the winner costs no extra weight traffic, only its BN statistics (counted), and the
+    replicas stay bitwise identical.  The adoption is lossy by the codec's error: the part of the
+    winner's delta that top-k dropped is not applied at this sync.  With error feedback (the
+    default for top-k codecs) it is not lost either: the winner keeps it in its residual and
+    sends it with its next delta, while the other ranks zero their residuals (their own unsent
+    drift belongs to a trajectory that was abandoned).
   * ``grad`` -- on sync steps the step's gradient goes through the wrapped exchange (compressed,
     averaged, applied); other steps apply the local gradient.  The replicas have drifted apart
     over the local steps and the same averaged gradient does not bring them back, so the weights
@@ -87,6 +92,10 @@ class LocalSGDExchange:
                     # round trip and is captured as a HIP graph like the local steps
                     best = self._best_dev()
                     self.inner.decode_rank(best)
+                    resid = self.inner.resid
+                    if resid is not None:  # only the winner's unsent delta carries over
+                        won = (best == self.comm.rank).to(resid.dtype)
+                        resid.mul_(won)
                     buf = self._sync_bn_dev(best)
                     stats.wire_bytes_sent += (self.comm.world - 1) * buf
                     stats.wire_bytes_recv += (self.comm.world - 1) * buf

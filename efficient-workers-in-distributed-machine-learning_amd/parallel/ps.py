@@ -75,6 +75,7 @@ class PSExchange:
         self.key_dev = self.key_state[1:2]
         self.side = None
         self._encoded = False
+        self.clock = None  # Stopwatch of --phase-timing
 
     @staticmethod
     def _nbytes(codec, b):
@@ -183,10 +184,14 @@ class PSExchange:
             return
         rank = self.comm.rank
         kt = self.key_dev if self.use_dev_key else None
+        if self.clock is not None:
+            self.clock.mark("backward")
         for b in self.flat.buckets:
             self._encode(self.push, b.index, self.flat.grad_view(b), self.payload[b.index], rank,
                          kt)
         self._encoded = True
+        if self.clock is not None:
+            self.clock.mark("encode")
 
     def join_side(self):
         pass
@@ -198,27 +203,39 @@ class PSExchange:
         """Phase 2: gather the pushes, the server averages (and re-encodes the pull), broadcast."""
         W = self.N - 1
         rank = self.comm.rank
+        clk = self.clock
+
+        def mark(name):
+            if clk is not None:
+                clk.mark(name)
+
         for b in self.flat.buckets:
             bi = b.index
             av = self.avg[b.start:b.start + b.length]
             if self.k < W:
                 use = self._push_k_of_n(bi)
+                mark("collective")  # push (send / gather): the reference's time_send
                 if self.is_server:
                     rows = torch.tensor(use, device=self.device)
                     self._decode(self.push, bi, self.gathered[bi].index_select(0, rows), av,
                                  1.0 / len(use))
             else:
                 self.comm.gather(self.payload[bi], self.gathered[bi], dst=self.server_rank)
+                mark("collective")
                 if self.is_server:
                     self._decode(self.push, bi, self.gathered[bi][1:], av, 1.0 / W)
             if self.pull == "grad":
                 if self.is_server:
                     self._encode(self.pullc, bi, av, self.pull_buf[bi][0], rank)
+                    mark("aggregate")  # the server's decode / average / re-encode
                 self.comm.broadcast(self.pull_buf[bi], src=self.server_rank)
+                mark("collective")  # pull (broadcast): the reference's time_recieve
         if self.pull != "grad":
             if self.is_server:
                 self.opt.step(grad=self.avg)
+                mark("aggregate")
             self.comm.broadcast(self.flat.data, src=self.server_rank)
+            mark("collective")
 
     def apply(self):
         """Phase 3: decode the pulled average and step (weights pull: already applied)."""
@@ -235,6 +252,8 @@ class PSExchange:
         self.launch_pending()
         self.communicate()
         self.apply()
+        if self.clock is not None:
+            self.clock.mark("decode_update")
         self._encoded = False
         self.last = self.bytes_per_step()
         self.step_idx += 1

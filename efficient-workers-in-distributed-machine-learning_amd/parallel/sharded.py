@@ -85,26 +85,80 @@ class ShardedPSExchange:
         self.avg = torch.zeros_like(flat.grad)
         self.last = StepStats()
 
-    def begin(self):
-        pass
+        # split-graph protocol (runtime/trainer.py, as the parameter server's): graph A =
+        # forward, backward and the push encodes (RNG key of step_idx from key_state), then the
+        # eager collectives with the owners' average / re-encode between them, then graph B =
+        # decode of every shard + optimizer step
+        self.use_dev_key = self.dev_key_advance = self.defer_comm = self._active = False
+        self.key_state = torch.zeros(2, dtype=torch.int32, device=self.device)
+        self.key_dev = self.key_state[1:2]
+        self.side = None
+        self._encoded = False
+        self.clock = None  # Stopwatch of --phase-timing
 
-    def finish(self):
-        N, me = self.N, self.rank
+    def _mark(self, name):
+        if self.clock is not None:
+            self.clock.mark(name)
+
+    def begin(self):
+        self._encoded = False
+
+    def set_device_key(self, step: int = None):
+        """Upload the push encodes' key of ``step`` (default: the current step) for graph A."""
+        from .ps import PSExchange
+
+        PSExchange.set_device_key(self, step)
+
+    @property
+    def push(self):  # the push codec (PSExchange.set_device_key reads it)
+        return self.codec
+
+    def launch_pending(self):
+        """Phase 1: encode every shard of every bucket of this rank's gradient."""
+        if self._encoded:
+            return
+        self._mark("backward")
+        kt = self.key_dev if self.use_dev_key else None
         for b in self.flat.buckets:
-            bi, P = b.index, self.P[b.index]
             g = self.flat.grad_view(b)
-            av = self.avg[b.start:b.start + b.length]
-            for r, (s0, ln, j) in enumerate(self.shards[bi]):
+            for r, (s0, ln, j) in enumerate(self.shards[b.index]):
                 if j >= 0:
                     Pj = self.codec.payload_bytes(j)
-                    self.codec.encode(j, g[s0:s0 + ln], self.send[bi][r, :Pj], self.step_idx, me)
+                    self.codec.encode(j, g[s0:s0 + ln], self.send[b.index][r, :Pj],
+                                      self.step_idx, self.rank, key_tensor=kt)
+        self._encoded = True
+        self._mark("encode")
+
+    def join_side(self):
+        pass
+
+    def wait(self):
+        pass
+
+    def communicate(self):
+        """Phase 2: all-to-all of the shard payloads; each owner averages its N pushes and
+        re-encodes the average; all-gather of the owners' payloads."""
+        N, me = self.N, self.rank
+        for b in self.flat.buckets:
+            bi = b.index
+            av = self.avg[b.start:b.start + b.length]
             self.comm.all_to_all(self.recv[bi], self.send[bi])
+            self._mark("collective")
             s0, ln, j = self.shards[bi][me]
             if j >= 0:  # owner: average the N pushes of its shard, re-encode the average
                 Pj = self.codec.payload_bytes(j)
                 self.codec.decode(j, self.recv[bi][:, :Pj].contiguous(), av[s0:s0 + ln], 1.0 / N)
                 self.codec.encode(j, av[s0:s0 + ln], self.own[bi][:Pj], self.step_idx, N + me)
+            self._mark("aggregate")
             self.comm.all_gather(self.gathered[bi], self.own[bi])
+            self._mark("collective")
+
+    def apply(self):
+        """Phase 3: decode every owner's averaged shard and take the optimizer step."""
+        N = self.N
+        for b in self.flat.buckets:
+            bi, P = b.index, self.P[b.index]
+            av = self.avg[b.start:b.start + b.length]
             rows = self.gathered[bi].view(N, P)
             for r, (s0, ln, j) in enumerate(self.shards[bi]):
                 if j >= 0:
@@ -113,6 +167,13 @@ class ShardedPSExchange:
                 else:
                     av[s0:s0 + ln].zero_()
         self.opt.step(grad=self.avg)
+
+    def finish(self):
+        self.launch_pending()
+        self.communicate()
+        self.apply()
+        self._mark("decode_update")
+        self._encoded = False
         self.last = self.bytes_per_step()
         self.step_idx += 1
 

@@ -24,7 +24,7 @@ from ..models.fused import set_enabled as set_fused_nn
 from ..optim.flat import make_optimizer
 from ..parallel.comm import Comm, init_distributed
 from ..parallel.engine import (GradientExchange, SegmentedCapture, StepStats, Stopwatch,
-                               sync_buffers, sync_params)
+                               plan_graph_mode, sync_buffers, sync_params)
 from ..parallel.flat import FlatModel
 from ..parallel.local_sgd import LocalSGDExchange
 from ..parallel.ps import PSExchange
@@ -137,7 +137,19 @@ class Trainer:
         ptr_grads = (self.cuda and cfg.topology == "allgather"
                      and os.environ.get("EWDML_GRAD_VIEWS") != "1")
         bf16_params = ptr_grads and cfg.amp == "bf16" and cfg.param_dtype == "auto"
-        self.flat = FlatModel(model, bucket_bytes=int(cfg.bucket_mb * (1 << 20)),
+        bucket_bytes = int(cfg.bucket_mb * (1 << 20))
+        # --hip-graph auto for the all-to-all exchange: overlap large dense collectives with
+        # backward at N > 1 (segmented graphs), one graph otherwise (plan_graph_mode); decided
+        # here because the segmented step wants smaller buckets
+        self.graph_plan = None
+        if (cfg.hip_graph == "auto" and self.cuda and not cfg.sync_debug
+                and cfg.topology == "allgather" and cfg.sync_every == 1 and not cfg.select_best):
+            self.graph_plan = plan_graph_mode(
+                self.world, self.comm.kind, cfg.compress,
+                sum(p.numel() for p in model.parameters() if p.requires_grad),
+                bits=cfg.qsgd_bits, overlap=cfg.overlap, bucket_bytes=bucket_bytes)
+            bucket_bytes = self.graph_plan["bucket_bytes"]
+        self.flat = FlatModel(model, bucket_bytes=bucket_bytes,
                               attach_grads=not ptr_grads, bf16_params=bf16_params)
         sync_params(self.flat, self.comm)
         sync_buffers(model, self.comm)
@@ -167,8 +179,8 @@ class Trainer:
             # fork makes the graph a DAG, which ROCm 7.2 replays node by node from the host (~7.9
             # ms per ResNet-50 step against 0.16 ms linear: profiles/ab/bucket_overlap.txt).
             # Eager steps overlap encode with backward on a side stream.
-            side = (self.cuda and (cfg.hip_graph == "off"
-                                   or os.environ.get("EWDML_SIDE_STREAM") == "1"))
+            side = (self.cuda and not cfg.phase_timing  # phase marks partition ONE stream
+                    and (cfg.hip_graph == "off" or os.environ.get("EWDML_SIDE_STREAM") == "1"))
             self.exchange = GradientExchange(self.flat, self.comm,
                                              make_codec(cfg.compress, **ckw), self.opt,
                                              overlap=cfg.overlap,
@@ -187,15 +199,21 @@ class Trainer:
         self.local_sgd = isinstance(self.exchange, LocalSGDExchange)
         if self.local_sgd and cfg.select_best:
             self._holdout_batch()
-        ps_split = isinstance(self.exchange, PSExchange) and self.exchange.k == self.world - 1
+        # split graphs around eager collectives: the parameter server's workers (without k-of-n)
+        # and the sharded exchange (graph A: forward, backward, push encodes -> eager all-to-all,
+        # owner average + re-encode, all-gather -> graph B: decode + update)
+        ps_split = ((isinstance(self.exchange, PSExchange) and self.exchange.k == self.world - 1)
+                    or isinstance(self.exchange, ShardedPSExchange))
         self.ps_graph = ps_split
         if self.graph_mode == "auto":
             # graphs wherever the step can be captured: the all-to-all exchange, local SGD's
             # local steps (its sync steps -- compressed delta, host-side best-worker choice --
-            # run eagerly) and the parameter server's workers (graph A: forward, backward, push
-            # encode -> eager gather / broadcast -> graph B: pull decode + update); the k-of-n
-            # arrival polling and the sharded exchange stay eager
-            if isinstance(self.exchange, GradientExchange) or self.local_sgd:
+            # run eagerly), the parameter server's workers and the sharded exchange (graph A:
+            # forward, backward, push encode -> eager collectives -> graph B: pull decode +
+            # update); the k-of-n arrival polling stays eager
+            if self.graph_plan is not None:
+                self.graph_mode = self.graph_plan["mode"]
+            elif isinstance(self.exchange, GradientExchange) or self.local_sgd:
                 self.graph_mode = "full"
             else:
                 self.graph_mode = "split" if ps_split else "off"
@@ -203,7 +221,7 @@ class Trainer:
                                              (self.local_sgd and self.graph_mode == "full") or
                                              (ps_split and self.graph_mode == "split")):
             raise ValueError("--hip-graph: all-to-all topology (local SGD: full only; parameter "
-                             "server without k-of-n: split only)")
+                             "server without k-of-n and sharded: split only)")
         if (self.graph_mode in ("full", "segmented") and self._pg_collectives()
                 and not self.local_sgd and not self.ps_graph):
             # the step's collectives on the process group: Gloo's CUDA collectives cannot be
@@ -211,6 +229,19 @@ class Trainer:
             # in the capture that the group's watchdog thread then queries (hipErrorCapturedEvent
             # kills the process) -- graph the compute, issue the collectives between the graphs
             self.graph_mode = "split"
+        if (cfg.phase_timing and cfg.hip_graph == "auto" and self.graph_mode == "full"
+                and not self.local_sgd):
+            # one graph has no inside to time: cut it at the collectives (graph A -> eager
+            # collectives -> graph B) so the communication / computation split is measured
+            self.graph_mode = "split"
+        # --phase-timing: the step's phase clock, shared with the exchange (engine.Stopwatch)
+        self.clock = Stopwatch(self.cuda) if cfg.phase_timing else None
+        for e in (self.exchange, getattr(self.exchange, "inner", None)):
+            if e is not None and hasattr(e, "clock"):
+                e.clock = self.clock
+        self.overlap_splits = (self.graph_plan["splits"] if (self.graph_plan is not None and
+                                                             self.graph_mode == "segmented")
+                               else cfg.overlap_splits)
         if self.graph_mode == "segmented":  # collectives on their own stream, beside backward
             self.exchange.comm_stream = torch.cuda.Stream(device=self.device)
         self._graphs = None
@@ -256,6 +287,8 @@ class Trainer:
         self.exchange.begin()
         with self._range("forward"), self.autocast():
             out = self.model(x)
+        if self.clock is not None:
+            self.clock.mark("forward")
         if self.cuda and self.cfg.fused_nn == "on":
             from ..ops.nn import cross_entropy  # one HIP kernel per direction
 
@@ -272,6 +305,8 @@ class Trainer:
 
                     set_unit_grad(seed)
             loss.backward(seed)
+        if self.clock is not None:
+            self.clock.mark("backward")
         return loss, out
 
     def stream_ctx(self):
@@ -316,6 +351,9 @@ class Trainer:
         """One synchronous step.  Returns (loss tensor, logits) (server: (None, None))."""
         if self.local_sgd and self.graph_mode != "off":
             self._graph_kind()
+        if self.clock is not None:
+            self.clock.reset()
+            self.clock.mark("start")
         if self.gstream is None:
             out = self._train_step(x, y)
         elif self._graphs is not None and len(self._graphs) == 1 and _SAME_STREAM_REPLAY:
@@ -329,6 +367,8 @@ class Trainer:
                 out = self._train_step(x, y)
             torch.cuda.current_stream().wait_stream(gs)
         self.comm.watch()  # the step's collectives are behind this point of the stream
+        if self.clock is not None:
+            self.clock.mark("other")  # anything after the last phase mark (host bookkeeping)
         return out
 
     def close(self):
@@ -505,7 +545,7 @@ class Trainer:
             elif self.graph_mode == "segmented":
                 seg = SegmentedCapture(self.gstream, ex.comm_stream, mode="relaxed",
                                        total_bytes=4 * self.flat.numel,
-                                       splits=self.cfg.overlap_splits)
+                                       splits=self.overlap_splits)
                 ex.seg = seg
                 try:
                     seg.begin()
@@ -583,17 +623,26 @@ class Trainer:
             # the delta encode's key of this sync (the eager path's inner.finish count)
             ex.inner.set_device_key(ex.inner.step_idx)
             ex.inner.step_idx += 1
+        clk = self.clock
         if len(self._graphs) == 1:
             with self._range("graph_step"):
                 self._graphs[0].replay()
+            if clk is not None:
+                clk.mark("step")  # one graph: no phases inside
         elif self._graphs[0] == "segmented":
             with self._range("graph_step"):
-                self._graphs[1].replay()
+                self._graphs[1].replay(clk)
         else:
             self._graphs[0].replay()
+            if clk is not None:
+                clk.mark("compute")  # graph A: forward, backward, encode
             ex.communicate()
             ex.wait()
+            if clk is not None:
+                clk.mark("collective")
             self._graphs[1].replay()
+            if clk is not None:
+                clk.mark("decode_update")  # graph B
         ex.step_idx += 1
         self.opt.steps += 1
         # a local step sends nothing
@@ -751,6 +800,10 @@ class Trainer:
         t_start = time.time()
         summary = None
         prof = None
+        # run totals: cumulative bytes (the reference's per-worker "total send / recieve memory",
+        # src/distributed_worker.py:228-231), phase times (--phase-timing), sampled step times
+        acc = {"bytes_sent": 0, "bytes_recv": 0, "payload_bytes": 0, "steps": 0,
+               "phase_ms": {}, "phase_steps": 0, "step_ms": []}
         if cfg.profile and self.rank == 0:
             prof = torch.profiler.profile(
                 activities=[torch.profiler.ProfilerActivity.CPU] +
@@ -763,6 +816,17 @@ class Trainer:
             sw.mark("start")
             loss, outy = self.train_step()
             sw.mark("step")
+            st = self.exchange.last
+            acc["bytes_sent"] += st.wire_bytes_sent
+            acc["bytes_recv"] += st.wire_bytes_recv
+            acc["payload_bytes"] += st.payload_bytes
+            acc["steps"] += 1
+            phases = None
+            if self.clock is not None:
+                phases = self.clock.phases()
+                for k, v in phases.items():
+                    acc["phase_ms"][k] = acc["phase_ms"].get(k, 0.0) + v
+                acc["phase_steps"] += 1
             if prof is not None and self.step == cfg.profile:
                 prof.__exit__(None, None, None)
                 prof.export_chrome_trace(os.path.join(cfg.train_dir, "trace.json"))
@@ -775,20 +839,32 @@ class Trainer:
                     a1, a5 = accuracy(out.float(), y, (1, 5))
                     rec.update(loss=float(loss.detach()), acc1=float(a1), acc5=float(a5))
                 rec["step_ms"] = sw.phases().get("step")
+                acc["step_ms"].append(rec["step_ms"] or 0.0)
                 if self.world > 1:  # straggler report: slowest / fastest rank's step time
                     mx, mn = self.comm.all_reduce_scalars([rec["step_ms"] or 0.0], op="max")[0], \
                         -self.comm.all_reduce_scalars([-(rec["step_ms"] or 0.0)], op="max")[0]
                     rec["step_ms_max"], rec["step_ms_min"] = mx, mn
                 rec.update(byte_summary(self.exchange.last, self.world))
+                rec["bytes_sent_total"] = acc["bytes_sent"]
+                rec["bytes_recv_total"] = acc["bytes_recv"]
+                rec["payload_bytes_total"] = acc["payload_bytes"]
+                if phases is not None:
+                    rec["phase_ms"] = {k: round(v, 4) for k, v in phases.items()}
+                    comm_ms, comp_ms = Stopwatch.split(phases)
+                    rec["comm_ms"], rec["compute_ms"] = round(comm_ms, 4), round(comp_ms, 4)
                 rec["images_per_sec_rank"] = (cfg.batch_size * 1e3 / rec["step_ms"]
                                               if rec["step_ms"] else None)
                 self.log.record(rec)
                 if loss is not None:
+                    ph = (f" comm {rec['comm_ms']:.2f} ms compute {rec['compute_ms']:.2f} ms"
+                          if phases is not None else "")
                     self.log.info(
                         f"Worker {self.rank} Step {self.step}/{total} loss {rec['loss']:.4f} "
                         f"acc@1 {rec['acc1']:.1f} acc@5 {rec['acc5']:.1f} "
                         f"payload {rec['payload_bytes_per_rank'] / 1024:.1f} KiB "
-                        f"(x{(rec['compression_ratio'] or 0):.0f}) step {rec['step_ms'] or 0:.2f} ms")
+                        f"(x{(rec['compression_ratio'] or 0):.0f}) step {rec['step_ms'] or 0:.2f} ms"
+                        f"{ph} sent {acc['bytes_sent'] / 2**20:.1f} MiB "
+                        f"recv {acc['bytes_recv'] / 2**20:.1f} MiB")
                 summary = rec
             if cfg.eval_freq and self.step % cfg.eval_freq == 0:
                 if cfg.sync_bn:
@@ -802,9 +878,63 @@ class Trainer:
         self.comm.barrier()
         wall = time.time() - t_start
         self.log.info(f"total time {wall:.1f}s for {total} steps")
+        run_summary = self.write_summary(acc, wall)
         self.close()
         self.log.close()
-        return {"steps": total, "wall_s": wall, "last": summary}
+        return {"steps": total, "wall_s": wall, "last": summary, "summary": run_summary}
+
+    def write_summary(self, acc: dict, wall: float) -> dict:
+        """Collective: every rank's run totals; rank 0 writes ``summary.json`` with
+        each rank's figures and their mean and max over ranks -- the per-method comm / compute
+        minutes the report charts (``Report.zip: VGG11 Communication and Computation Time``)."""
+        n = max(1, acc["phase_steps"])
+        mine = {"rank": self.rank, "steps": acc["steps"], "wall_s": wall,
+                "bytes_sent_total": acc["bytes_sent"], "bytes_recv_total": acc["bytes_recv"],
+                "payload_bytes_total": acc["payload_bytes"],
+                "step_ms_mean": (sum(acc["step_ms"]) / len(acc["step_ms"])
+                                 if acc["step_ms"] else None)}
+        if acc["phase_steps"]:
+            ph = {k: v / n for k, v in acc["phase_ms"].items()}
+            mine["phase_ms_mean"] = ph
+            comm_ms, comp_ms = Stopwatch.split(ph)
+            mine["comm_ms_mean"], mine["compute_ms_mean"] = comm_ms, comp_ms
+            mine["comm_s_total"] = comm_ms * acc["steps"] / 1e3
+            mine["compute_s_total"] = comp_ms * acc["steps"] / 1e3
+        ranks = self.comm.all_gather_object(mine)
+        if self.rank != 0:
+            return None
+
+        def agg(fn):
+            out = {}
+            for k in ("wall_s", "bytes_sent_total", "bytes_recv_total", "payload_bytes_total",
+                      "step_ms_mean", "comm_ms_mean", "compute_ms_mean", "comm_s_total",
+                      "compute_s_total"):
+                vals = [r[k] for r in ranks if r.get(k) is not None]
+                if vals:
+                    out[k] = fn(vals)
+            keys = sorted({k for r in ranks for k in r.get("phase_ms_mean", {})})
+            if keys:
+                out["phase_ms_mean"] = {k: fn([r["phase_ms_mean"].get(k, 0.0) for r in ranks
+                                               if "phase_ms_mean" in r]) for k in keys}
+            return out
+
+        cfg = self.cfg
+        summary = {"world": self.world, "network": cfg.network, "dataset": cfg.dataset,
+                   "method": cfg.method, "compress": cfg.compress, "topology": cfg.topology,
+                   "hip_graph": self.graph_mode, "batch_size": cfg.batch_size,
+                   "phase_timing": cfg.phase_timing, "ranks": ranks,
+                   "mean": agg(lambda v: sum(v) / len(v)), "max": agg(max)}
+        path = cfg.summary_file or os.path.join(cfg.train_dir, "summary.json")
+        d = os.path.dirname(path)
+        if d:
+            os.makedirs(d, exist_ok=True)
+        import json
+
+        tmp = path + ".tmp"
+        with open(tmp, "w") as f:
+            json.dump(summary, f, indent=1)
+        os.replace(tmp, path)  # atomic: a reader never sees a half-written summary
+        return summary
 
 
 def run(cfg: Config):

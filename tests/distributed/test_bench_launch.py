@@ -48,6 +48,13 @@ def test_bench_two_ranks_gloo(preset, batch):
     for k in ("value_fp32_no_ef", "value_bf16", "ms_per_step_bf16"):
         assert rec[k] > 0, k
     assert rec["overlap_effective"] is (rec["config"]["buckets"] > 1)
+    # the self-validation of a multi-rank run: every measured configuration left the replicas
+    # bitwise identical (local SGD's replicas legitimately differ between syncs: not checked)
+    assert rec["replicas_identical"] is True
+    for k in ("fp32_no_ef", "bf16", "dense_fp32"):
+        assert rec[f"replicas_identical_{k}"] is True, k
+    assert rec["comm"] == "process-group" and rec["rccl_world"] == 0
+    assert rec["step_ms_min"] <= rec["step_ms_max"] == pytest.approx(rec["ms_per_step"], rel=1e-3)
     if preset == "vgg11":
         assert rec["config"]["model"] == "vgg11_bn"
         assert rec["metric"].startswith("grad bytes/step on wire + images/sec, VGG-11")

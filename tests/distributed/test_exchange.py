@@ -11,7 +11,7 @@ pytestmark = pytest.mark.slow
 
 BASE = ["--network", "LeNet", "--dataset", "MNIST", "--batch-size", "16", "--synthetic-size",
         "512", "--momentum", "0.9", "--lr", "0.05", "--eval-freq", "0", "--quiet",
-        "--device", "cpu", "--log-interval", "1000"]
+        "--device", "cpu", "--log-interval", "1000", "--no-error-feedback"]
 
 
 def _train(rank, world, flags, steps):
@@ -147,11 +147,12 @@ def test_method6_local_sgd_select_best(tmp_path):
     _same_params(res)  # after the step-6 sync everyone holds the best rank's weights
 
 
-def _method6(rank, world):
+def _method6(rank, world, ef=False):
     import ewdml
     from ewdml.runtime import Trainer
 
-    cfg = ewdml.parse_args(BASE + ["--method", "6", "--sync-every", "3", "--max-steps", "3"])
+    cfg = ewdml.parse_args(BASE + ["--method", "6", "--sync-every", "3", "--max-steps", "3"] +
+                           (["--error-feedback"] if ef else []))
     tr = Trainer(cfg)
     ex = tr.exchange
     for _ in range(2):
@@ -165,9 +166,11 @@ def _method6(rank, world):
     rows = inner.recv[0].view(inner.N, -1)
     delta = torch.zeros_like(tr.flat.grad)
     inner.codec.decode(0, rows[best:best + 1], delta, 1.0)
+    resid = inner.resid
     return {"mode": ex.mode, "params": tr.flat.data.clone(), "expect": anchor + delta,
             "wire": ex.last.wire_bytes_sent + ex.last.wire_bytes_recv,
-            "dense": tr.flat.numel * 4, "nb": len(tr.flat.buckets)}
+            "dense": tr.flat.numel * 4, "nb": len(tr.flat.buckets), "best": best,
+            "resid": None if resid is None else float(resid.abs().sum())}
 
 
 def test_method6_adopts_the_winners_compressed_delta(tmp_path):
@@ -179,6 +182,21 @@ def test_method6_adopts_the_winners_compressed_delta(tmp_path):
     assert r["mode"] == "model" and r["nb"] == 1
     torch.testing.assert_close(r["params"], r["expect"], rtol=0, atol=0)
     assert r["wire"] < r["dense"] / 20  # a compressed payload each way, no dense weights
+
+
+def test_method6_error_feedback_keeps_only_the_winners_residual(tmp_path):
+    """Method 6 with error feedback (the CLI default for top-k codecs): every rank adopts
+    anchor + decode(winner's payload) as documented in parallel/local_sgd.py; the winner keeps the
+    part of its delta that top-k dropped in its residual (sent with its next delta), the other
+    ranks zero theirs."""
+    res = run_world(_method6, 2, tmp_path, args=(True,))
+    _same_params(res)
+    best = res[0]["best"]
+    assert res[1]["best"] == best
+    for r in res:
+        torch.testing.assert_close(r["params"], r["expect"], rtol=0, atol=0)
+    assert res[best]["resid"] > 0
+    assert res[1 - best]["resid"] == 0
 
 
 def test_local_sgd_grad_mode_resyncs_replicas(tmp_path):

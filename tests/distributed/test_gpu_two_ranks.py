@@ -13,7 +13,7 @@ pytestmark = pytest.mark.gpu
 
 BASE = ["--network", "LeNet", "--dataset", "MNIST", "--batch-size", "16", "--synthetic-size",
         "512", "--momentum", "0.9", "--lr", "0.05", "--eval-freq", "0", "--quiet",
-        "--device", "cuda", "--log-interval", "1000"]
+        "--device", "cuda", "--log-interval", "1000", "--no-error-feedback"]
 
 
 def _train(rank, world, flags, steps):
@@ -50,3 +50,22 @@ def test_two_ranks_on_one_gpu_identical(tmp_path, flags, graph):
     assert all(l is not None and l == l for l in res[0]["losses"])
     assert res[0]["bytes"] == res[1]["bytes"] > 0
     assert res[0]["graph"] == res[1]["graph"] == graph
+
+
+@pytest.mark.parametrize("flags,graph", [
+    (["--compress", "topk_qsgd", "--hip-graph", "auto", "--graph-warmup", "1"], "split"),
+    (["--compress", "topk_qsgd", "--topology", "sharded", "--graph-warmup", "1"], "split"),
+    (["--compress", "topk_qsgd", "--topology", "ps", "--graph-warmup", "1"], None),
+])
+def test_four_ranks_on_one_gpu_identical(tmp_path, flags, graph):
+    """Four ranks on the box's one GPU (Gloo between them): the all-gather exchange with N = 4
+    payload strides, the 4-way sharded exchange and a 1 + 3 parameter server, split-graphed where
+    the topology allows; the replicas stay bitwise identical."""
+    res = run_world(_train, 4, tmp_path, args=(flags, 4))
+    assert torch.isfinite(res[0]["params"]).all()
+    for r in res[1:]:
+        assert torch.equal(res[0]["params"], r["params"])
+    if graph is not None:
+        assert all(r["graph"] == graph for r in res)
+    else:  # parameter server: the workers split-graph, the server captures nothing
+        assert all(r["graph"] == "split" for r in res[1:])

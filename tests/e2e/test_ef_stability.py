@@ -51,7 +51,8 @@ def test_resnet50_error_feedback_tracks_dense():
     assert ef_tr.exchange.ef_mode == "dgc" and ef_tr.exchange.codec.ratio == 0.01
     assert ef_tr.cfg.topk_warmup and ef_tr.cfg.lr_warmup_epochs == 2.0
     _, dense = _curve(["--compress", "none"] + LR_WARMUP)
-    _, noef = _curve(["--compress", "topk_qsgd", "--topk-ratio", "0.01"] + LR_WARMUP)
+    _, noef = _curve(["--compress", "topk_qsgd", "--topk-ratio", "0.01", "--no-error-feedback"]
+                     + LR_WARMUP)
 
     def tail(c):
         return sum(c[-60:]) / 60

@@ -50,7 +50,8 @@ def test_lenet_real_mnist_gpu(codec, amp):
     extra = {"dense": ["--compress", "none"],
              "topk1_qsgd_ef": ["--compress", "topk_qsgd", "--topk-ratio", "0.01",
                                "--error-feedback"],
-             "method5": ["--compress", "topk_qsgd", "--topk-ratio", "0.4", "--qsgd-norm", "l2"]}
+             "method5": ["--compress", "topk_qsgd", "--topk-ratio", "0.4", "--qsgd-norm", "l2",
+                         "--no-error-feedback"]}
     tr, losses = _train(LENET + ["--amp", amp] + extra[codec], 1500)
     assert tr.graph_mode == "full" and tr._graphs is not None
     ev = tr.evaluate()

@@ -10,7 +10,7 @@ pytestmark = pytest.mark.gpu
 
 LENET = ["--network", "LeNet", "--dataset", "MNIST", "--batch-size", "32", "--synthetic-size",
          "1024", "--momentum", "0.9", "--lr", "0.05", "--eval-freq", "0", "--quiet", "--device",
-         "cuda", "--amp", "none", "--graph-warmup", "2"]
+         "cuda", "--amp", "none", "--graph-warmup", "2", "--no-error-feedback"]
 
 
 def _run(flags, steps):
@@ -29,9 +29,15 @@ def _run(flags, steps):
 @pytest.mark.parametrize("codec", ["topk_qsgd", "qsgd", "none", "bf16"])
 def test_graph_modes_match_eager(codec):
     ops.require()
+    import warnings
+
     ref, l_ref = _run(LENET + ["--compress", codec, "--hip-graph", "off"], 8)
     for mode in ("split", "full", "segmented"):
-        tr, l = _run(LENET + ["--compress", codec, "--hip-graph", mode], 8)
+        with warnings.catch_warnings(record=True) as caught:
+            warnings.simplefilter("always")
+            tr, l = _run(LENET + ["--compress", codec, "--hip-graph", mode], 8)
+        # an empty trailing compute segment is dropped, not captured as an empty graph
+        assert not [w for w in caught if "Graph is empty" in str(w.message)], mode
         assert tr.graph_mode == mode and tr._graphs is not None
         rel = (tr.flat.data - ref.flat.data).norm() / ref.flat.data.norm()
         assert rel < 1e-3, f"{mode}: params differ from eager by {rel:.2e}"
@@ -227,14 +233,14 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _bench_pg(codec, comm, extra=()):
+def _bench_pg(codec, comm, extra=(), env_extra=None):
     import json
     import os
     import subprocess
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-    env = dict(os.environ, EWDML_FORCE_PG="1", EWDML_COMM=comm)
+    env = dict(os.environ, EWDML_FORCE_PG="1", EWDML_COMM=comm, **(env_extra or {}))
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py",
            "--gpus", "1", "--steps", "4", "--warmup", "4", "--batch-size", "64",
@@ -261,6 +267,25 @@ def test_own_rccl_communicator_matches_process_group(codec):
     assert own["config"]["hip_graph"] == "full" and pg["config"]["hip_graph"] == "split"
     assert own["final_loss"] == pg["final_loss"]
     assert own["payload_bytes_per_rank"] == pg["payload_bytes_per_rank"]
+
+
+def test_comm_probe_passes_and_failure_falls_back_to_process_group():
+    """The first-contact probe of the own RCCL communicator (parallel/probe.py: rank-coded
+    all-gather / all-reduce / broadcast, eager and captured in a HIP graph replayed twice) passes
+    on the real communicator; with one rank's probe result corrupted (EWDML_PROBE_CORRUPT) the
+    communicator is dropped and the step's collectives run on the process group with split
+    graphs -- and the run still trains with identical bytes."""
+    ok = _bench_pg("topk_qsgd", "rccl")
+    assert ok["comm_probe"] == {"ok": True, "eager": True, "graph": True}
+    assert ok["config"]["comm"] == "rccl-stream" and ok["config"]["hip_graph"] == "full"
+    assert ok["replicas_identical"] is True and ok["rccl_world"] == 1
+    bad = _bench_pg("topk_qsgd", "rccl", env_extra={"EWDML_PROBE_CORRUPT": "0:graph"})
+    assert bad["comm_probe"]["ok"] is False and bad["comm_probe"]["eager"] is True
+    assert bad["comm_probe"]["graph"] is False
+    assert bad["config"]["comm"] == "process-group" and bad["config"]["hip_graph"] == "split"
+    assert bad["rccl_world"] == 0
+    assert bad["final_loss"] == ok["final_loss"]  # same trajectory on the fallback transport
+    assert bad["payload_bytes_per_rank"] == ok["payload_bytes_per_rank"]
 
 
 @pytest.mark.parametrize("codec", ["topk_qsgd", "none"])
@@ -311,6 +336,8 @@ def test_sharded_topology_hip_codecs(codec):
     ops.require()
     ref, _ = _run(LENET + ["--compress", "none", "--hip-graph", "off"], 4)
     tr, _ = _run(LENET + ["--compress", "topk", "--topk-ratio", "1.0", "--topology", "sharded"], 4)
+    # graph A (forward, backward, push encodes) -> eager collectives -> graph B (decode + step)
+    assert tr.graph_mode == "split" and tr._graphs is not None
     rel = (tr.flat.data - ref.flat.data).norm() / ref.flat.data.norm()
     assert rel < 1e-5, f"sharded lossless top-k differs from dense by {rel:.2e}"
     tr, losses = _run(LENET + ["--compress", codec, "--topology", "sharded"], 6)

@@ -348,6 +348,12 @@ def test_cross_entropy_unit_seed_grad_formed_in_forward(B, K, dtype):
         b = logits.clone().requires_grad_(True)
         fnn.cross_entropy(b, y).backward(2 * seed)
         torch.testing.assert_close(b.grad.float(), 2 * ref.grad.float(), rtol=1e-2, atol=1e-6)
+        with torch.no_grad():  # an eval forward: no backward can follow, no dx is formed
+            fnn.cross_entropy(logits, y)
+        seed.fill_(1.0)  # written since it was registered: no longer trusted as the unit seed
+        c = logits.clone().requires_grad_(True)
+        fnn.cross_entropy(c, y).backward(seed)
+        assert torch.equal(c.grad, ref.grad)  # the backward kernel's (identical) bits
     finally:
         fnn.set_unit_grad(None)
 

@@ -78,5 +78,37 @@ def test_error_feedback_brings_its_warmup_recipe():
     assert c.topk_warmup == "" and c.lr_warmup_epochs == 0
     c = ewdml.parse_args(["--compress", "topk_qsgd", "--error-feedback", "--topk-ratio", "0.4"])
     assert c.topk_warmup == "" and c.lr_warmup_epochs == 0  # nothing denser to warm up from
-    c = ewdml.parse_args(["--compress", "topk_qsgd"])
+    c = ewdml.parse_args(["--compress", "topk_qsgd", "--no-error-feedback"])
+    assert not c.error_feedback
     assert c.topk_warmup == "" and c.lr_warmup_epochs == 0
+
+
+def test_error_feedback_is_the_default_for_topk_codecs():
+    """Top-k at 1 % without error feedback trains 10-80x slower than dense
+    (profiles/validation/ef_stability_r03.md): the CLI turns it on, with its warm-up recipe, for
+    the top-k codecs; --no-error-feedback gives the reference's Method 5/6 as published."""
+    import ewdml
+
+    for codec in ("topk_qsgd", "topk"):
+        c = ewdml.parse_args(["--compress", codec])
+        assert c.error_feedback and c.ef_mode == "dgc"
+        assert c.topk_warmup and c.lr_warmup_epochs == 2.0
+    assert ewdml.parse_args([]).error_feedback  # the default codec is top-k + QSGD
+    for codec in ("none", "qsgd", "bf16"):
+        assert not ewdml.parse_args(["--compress", codec]).error_feedback
+    assert ewdml.parse_args(["--method", "5"]).error_feedback
+    assert not ewdml.parse_args(["--method", "5", "--no-error-feedback"]).error_feedback
+    assert not ewdml.parse_args(["--method", "3"]).error_feedback
+
+
+def test_ef21_rejected_at_parse_time_on_the_gpu(monkeypatch):
+    """EF21 has only the torch-oracle encode: a GPU run is refused when the configuration is
+    parsed, not after the model, buffers and communicator are set up."""
+    import ewdml
+
+    assert ewdml.parse_args(["--ef-mode", "ef21", "--device", "cpu"]).ef_mode == "ef21"
+    with pytest.raises(ValueError, match="ef21"):
+        ewdml.parse_args(["--ef-mode", "ef21", "--device", "cuda"])
+    monkeypatch.setenv("EWDML_ORACLE", "1")
+    monkeypatch.setenv("EWDML_GRAD_VIEWS", "1")
+    assert ewdml.parse_args(["--ef-mode", "ef21", "--device", "cuda"]).ef_mode == "ef21"
