@@ -154,6 +154,10 @@ def measure(a, world, amp, ef, extra=()):
     elapsed_min = -tr.comm.all_reduce_scalars([-(t1 - t0)], op="max")[0]
     from ewdml.parallel.engine import check_replicas
 
+    ge = getattr(tr.exchange, "inner", tr.exchange)
+    # top-k encode counters; raises if a write block gave up on its look-back (corrupt payload)
+    tr.codec_health = ge.codec_health() if hasattr(ge, "codec_health") else {}
+
     rep = None if every > 1 else check_replicas(tr.comm, tr.flat.data)
     final_loss = float(loss.detach()) if loss is not None else float("nan")
     tr.comm_kind = tr.comm.kind
@@ -239,6 +243,7 @@ def main(argv=None):
         "rccl_world": world if tr.comm_kind == "rccl-stream" else 0,
         "comm_probe": tr.comm_probe,
         "graph_plan": tr.graph_plan,
+        "codec_health": tr.codec_health,
         "step_ms_min": round(span[0] * 1e3 / a.steps, 4),
         "step_ms_max": round(span[1] * 1e3 / a.steps, 4),
         "hip_ext": ewdml.ops.library_path() if cuda else None,

@@ -30,6 +30,11 @@ import torch
 
 CHUNK = 8192
 BM_WORDS = CHUNK // 32  # bitmap words per chunk
+# predictive top-k encode (ops/csrc/topk_codec.hip): a tensor keeps at most this many candidates
+# (elements at or above its predicted threshold) per step: CAND_K_MULT * k + CAND_SLACK, capped at
+# numel; more (or fewer than k) and that tensor takes the exact full-pass path for the step
+CAND_K_MULT = 8
+CAND_SLACK = 4096
 
 
 def _align(n: int, a: int = 16) -> int:
@@ -61,6 +66,8 @@ class BucketPlan:
     tensor_code0: List[int] = field(default_factory=list)  # dense code offset (16-aligned)
     tensor_idx0: List[int] = field(default_factory=list)  # index-list position (-1: bitmap)
     tensor_bm0: List[int] = field(default_factory=list)  # bitmap word offset (-1: index list)
+    tensor_cap: List[int] = field(default_factory=list)  # candidate capacity (predictive encode)
+    tensor_cap0: List[int] = field(default_factory=list)  # its offset in the candidate list
 
     def __post_init__(self):
         assert len(self.numels) == len(self.offsets) and self.numels
@@ -96,6 +103,13 @@ class BucketPlan:
         self.total_codes = c
         self.total_idx = ix
         self.total_bm_words = bw
+        cap0 = 0
+        for n, k in zip(self.numels, self.ks):
+            cap = min(n, CAND_K_MULT * k + CAND_SLACK)
+            self.tensor_cap.append(cap)
+            self.tensor_cap0.append(cap0)
+            cap0 += cap
+        self.total_cap = cap0
 
     @property
     def num_tensors(self) -> int:
@@ -110,13 +124,29 @@ class BucketPlan:
         return sum(self.numels)
 
     # ---- device tables consumed by the kernels -------------------------------------------
+    @property
+    def tensor_cblocks(self) -> List[int]:
+        """Blocks per tensor of the predictive encode's candidate passes (one per CHUNK
+        candidates of capacity)."""
+        return [max(1, (c + CHUNK - 1) // CHUNK) for c in self.tensor_cap]
+
+    @property
+    def num_cblocks(self) -> int:
+        return sum(self.tensor_cblocks)
+
     def tensor_table(self, device) -> torch.Tensor:
-        """int32 [T, 12]: offset, numel, k, chunk0, nchunks, entry0, code0, idx0, bm0, 0, 0, 0
-        (csrc/common.h TensorRow)."""
-        rows = [[o, n, k, c0, nc, e0, d0, i0, b0, 0, 0, 0]
-                for o, n, k, c0, nc, e0, d0, i0, b0 in zip(
+        """int32 [T, 12]: offset, numel, k, chunk0, nchunks, entry0, code0, idx0, bm0, cap0, cap,
+        candidate blocks (csrc/common.h TensorRow)."""
+        rows = [[o, n, k, c0, nc, e0, d0, i0, b0, q0, q, nb]
+                for o, n, k, c0, nc, e0, d0, i0, b0, q0, q, nb in zip(
                     self.offsets, self.numels, self.ks, self.tensor_chunk0, self.tensor_nchunks,
-                    self.tensor_entry0, self.tensor_code0, self.tensor_idx0, self.tensor_bm0)]
+                    self.tensor_entry0, self.tensor_code0, self.tensor_idx0, self.tensor_bm0,
+                    self.tensor_cap0, self.tensor_cap, self.tensor_cblocks)]
+        return torch.tensor(rows, dtype=torch.int32, device=device)
+
+    def cblock_table(self, device) -> torch.Tensor:
+        """int32 [G, 2]: tensor, block index within the tensor (predictive encode passes)."""
+        rows = [[t, j] for t, nb in enumerate(self.tensor_cblocks) for j in range(nb)]
         return torch.tensor(rows, dtype=torch.int32, device=device)
 
     def chunk_table(self, device) -> torch.Tensor:

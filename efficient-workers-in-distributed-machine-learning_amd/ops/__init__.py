@@ -105,10 +105,32 @@ class DevicePlan:
         self.plan = plan
         self.tensors = plan.tensor_table(device)
         self.chunks = plan.chunk_table(device)
+        self.cblocks = plan.cblock_table(device)  # predictive top-k encode's candidate passes
         C, T = plan.num_chunks, plan.num_tensors
-        nbytes = max(require().topk_scratch_bytes(T, C, plan.length),
+        nbytes = max(require().topk_scratch_bytes(T, C, plan.length, plan.total_cap),
                      require().qsgd_scratch_bytes(T, C))
         self.scratch = torch.zeros(nbytes, dtype=torch.uint8, device=device)
+
+
+# EWDML_TOPK_PREDICT=0: every top-k encode takes the full passes (A/B of the predictive encode)
+_TOPK_PREDICT = os.environ.get("EWDML_TOPK_PREDICT", "1") != "0"
+_LB_FAULT = [False]
+
+
+def set_lookback_fault(on: bool):
+    """Test hook: the next top-k encodes' first chunks skip their look-back word, so every later
+    chunk of a tensor polls to the bound and reports through the error counter."""
+    _LB_FAULT[0] = bool(on)
+
+
+def topk_stats(dp) -> dict:
+    """Counters of a bucket's top-k encodes (synchronises): ``lookback_errors`` (write blocks that
+    gave up waiting on a predecessor's look-back word: their payload offsets are wrong -- must be
+    0), and the tensor-encodes of the predictive encode on the ``fast`` (candidates only) and the
+    ``full`` path."""
+    e, fast, full = require().topk_stats(_ptr(dp.scratch), dp.plan.num_tensors,
+                                         dp.plan.num_chunks)
+    return {"lookback_errors": e, "fast": fast, "full": full}
 
 
 def topk_lookback_errors(dp) -> int:
@@ -212,7 +234,8 @@ def topk_encode(dp: DevicePlan, grad, payload, layout, levels: int, norm: str, k
                   layout.scales, layout.counts, layout.idx, layout.codes, vk,
                   1 if norm == "l2" else 0, float(levels), float(1.0 / levels), key & 0xFFFFFFFF,
                   dp.plan.bucket_offset & 0xFFFFFFFF, _keyp(key_tensor), _stream(), _ptr(vel),
-                  _ptr(par), mom, damp1, wd, nest, layout.bitmap, dmask, _lrp(lrt), dp.plan.length)
+                  _ptr(par), mom, damp1, wd, nest, layout.bitmap, dmask, _lrp(lrt), dp.plan.length,
+                  _ptr(dp.cblocks), dp.plan.num_cblocks, int(_TOPK_PREDICT), int(_LB_FAULT[0]))
 
 
 def _lrp(lr_tensor):

@@ -20,6 +20,7 @@ PYBIND11_MODULE(_C, m) {
 
   m.def("topk_scratch_bytes", &ew_topk_scratch_bytes);
   m.def("topk_lookback_errors", &ew_topk_lookback_errors);
+  m.def("topk_stats", &ew_topk_stats);
   m.def("qsgd_scratch_bytes", &ew_qsgd_scratch_bytes);
 
   m.def("topk_encode",
@@ -30,9 +31,14 @@ PYBIND11_MODULE(_C, m) {
            uint32_t bucket_offset, uintptr_t key_ptr, uintptr_t stream, uintptr_t vel,
            uintptr_t param, float dgc_momentum, float dgc_damp1, float dgc_wd,
            int dgc_nesterov, int bitmap_off, int dgc_mask, uintptr_t dgc_lr_ptr,
-           long long bucket_len) {
+           long long bucket_len, uintptr_t cblocks, int num_cblocks, int predict,
+           int lb_fault) {
           TopkEncodeArgs a{};
+          a.lb_fault = lb_fault;
           a.bucket_len = bucket_len;
+          a.cblocks = cblocks;
+          a.num_cblocks = num_cblocks;
+          a.predict = predict;
           a.dgc_mask = dgc_mask;
           a.dgc_lr_ptr = dgc_lr_ptr;
           a.bitmap_off = bitmap_off;

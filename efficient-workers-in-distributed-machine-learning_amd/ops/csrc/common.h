@@ -31,8 +31,12 @@
 
 struct TensorRow {  // mirrors BucketPlan.tensor_table()
   // idx0: position in the u16 index list (-1: bitmap-indexed); bm0: word offset of the tensor's
-  // bitmap (-1: index list).  code0: dense QSGD code offset.
-  int off, numel, k, chunk0, nchunks, entry0, code0, idx0, bm0, pad0, pad1, pad2;
+  // bitmap (-1: index list).  code0: dense QSGD code offset.  cap0 / cap / ncb: the predictive
+  // top-k encode's candidate list offset, capacity and candidate-pass blocks.
+  int off, numel, k, chunk0, nchunks, entry0, code0, idx0, bm0, cap0, cap, ncb;
+};
+struct CBlockRow {  // mirrors BucketPlan.cblock_table()
+  int tensor, j;
 };
 #define EW_BM_WORDS (EW_CHUNK / 32)  // bitmap words per chunk
 struct ChunkRow {  // mirrors BucketPlan.chunk_table()

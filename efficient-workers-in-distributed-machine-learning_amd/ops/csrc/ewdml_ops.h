@@ -2,6 +2,7 @@
 // bindings.cpp.  Pointers are device addresses passed as integers; `stream` is a hipStream_t.
 #pragma once
 #include <string>
+#include <vector>
 #include <stddef.h>
 #include <stdint.h>
 
@@ -27,6 +28,11 @@ struct TopkEncodeArgs {
   int dgc_mask;          // clear the velocity at sent coordinates (DGC) or keep it (local)
   uintptr_t dgc_lr_ptr;  // nullable device lr: residual accumulates lr-scaled updates
   long long bucket_len;  // elements (sizes the candidate list in the scratch)
+  // predictive encode (max-norm scale only): candidate-pass block table (CBlockRow[num_cblocks])
+  uintptr_t cblocks;
+  int num_cblocks;
+  int predict;
+  int lb_fault;  // test hook: tensors' first chunks skip their look-back word (lb_err path)
 };
 
 struct TopkDecodeArgs {
@@ -90,7 +96,9 @@ struct AdamFlatArgs {
   uintptr_t lr_ptr;  // nullable device fp32 base lr (overrides lr)
 };
 
-size_t ew_topk_scratch_bytes(int num_tensors, int num_chunks, long long bucket_len);
+size_t ew_topk_scratch_bytes(int num_tensors, int num_chunks, long long bucket_len,
+                             long long total_cap);
+std::vector<int> ew_topk_stats(uintptr_t scratch, int num_tensors, int num_chunks);
 int ew_topk_lookback_errors(uintptr_t scratch, int num_tensors, int num_chunks);
 void ew_topk_encode(const TopkEncodeArgs& a);
 void ew_topk_decode_apply(const TopkDecodeArgs& a);

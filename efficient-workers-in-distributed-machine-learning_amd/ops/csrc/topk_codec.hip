@@ -84,30 +84,13 @@ struct DgcArgs {
 // error-feedback mode of the encode: none, plain (e = g + r), momentum-corrected (DGC)
 enum EfMode { EF_NONE = 0, EF_PLAIN = 1, EF_DGC = 2 };
 
-// state[t] = {prefix, k_rem, max_key, pad}
+// Error-feedback staging of one chunk held in registers (v = the gradient on entry, the vector to
+// compress on exit): plain e = g + r, or DGC's momentum correction; e (and DGC's velocity) are
+// written back, so later passes read e from the residual.
 template <int EFM>
-__global__ __launch_bounds__(EW_BLOCK) void k_topk_hist0(GradPtrs gp, DgcArgs dg,
-                                                         unsigned long long* __restrict__ lb,
-                                                         float* __restrict__ resid,
-                                                         const ChunkRow* __restrict__ chunks,
-                                                         uint32_t* __restrict__ hist,
-                                                         uint32_t* __restrict__ kmaxr, int T,
-                                                         const TensorRow* __restrict__ tensors,
-                                                         uint32_t* __restrict__ state,
-                                                         int* __restrict__ tick) {
-  // Gradients cluster in a few exponent bins, so most lanes of a wave add to the same bin and an
-  // LDS atomic serialises per conflicting lane.  HSUB copies per bin in consecutive words (banks),
-  // chosen by lane: a shared bin splits into HSUB bank groups; the copies are summed at the flush.
-  constexpr int HSUB = 4;
-  __shared__ uint32_t hs[NB0 * HSUB];
-  for (int i = threadIdx.x; i < NB0 * HSUB; i += EW_BLOCK) hs[i] = 0;
-  __syncthreads();
-  uint32_t* h = hs + (threadIdx.x & (HSUB - 1));
-  const ChunkRow c = chunks[blockIdx.x];
-  // the write pass's look-back word of this chunk, from the previous encode (stream-ordered)
-  if (threadIdx.x == 0) lb[blockIdx.x] = 0ull;
-  float4 v[EW_CU];
-  ew_ld_chunk(gp, nullptr, c, v);
+__device__ __forceinline__ void topk_ef_stage(const GradPtrs& gp, const DgcArgs& dg,
+                                              float* __restrict__ resid, const ChunkRow& c,
+                                              float4 (&v)[EW_CU]) {
   if (EFM == EF_PLAIN) {  // error feedback: compress e = g + residual, staged in the residual
     float4 r[EW_CU];
     ew_ld_chunk(gp, resid, c, r);
@@ -150,6 +133,33 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_hist0(GradPtrs gp, DgcArgs dg
     ew_st_chunk(dg.vel + c.start, c.len, uv);
     ew_st_chunk(resid + c.start, c.len, v);
   }
+}
+
+// state[t] = {prefix, k_rem, max_key, pad}
+template <int EFM>
+__global__ __launch_bounds__(EW_BLOCK) void k_topk_hist0(GradPtrs gp, DgcArgs dg,
+                                                         unsigned long long* __restrict__ lb,
+                                                         float* __restrict__ resid,
+                                                         const ChunkRow* __restrict__ chunks,
+                                                         uint32_t* __restrict__ hist,
+                                                         uint32_t* __restrict__ kmaxr, int T,
+                                                         const TensorRow* __restrict__ tensors,
+                                                         uint32_t* __restrict__ state,
+                                                         int* __restrict__ tick) {
+  // Gradients cluster in a few exponent bins, so most lanes of a wave add to the same bin and an
+  // LDS atomic serialises per conflicting lane.  HSUB copies per bin in consecutive words (banks),
+  // chosen by lane: a shared bin splits into HSUB bank groups; the copies are summed at the flush.
+  constexpr int HSUB = 4;
+  __shared__ uint32_t hs[NB0 * HSUB];
+  for (int i = threadIdx.x; i < NB0 * HSUB; i += EW_BLOCK) hs[i] = 0;
+  __syncthreads();
+  uint32_t* h = hs + (threadIdx.x & (HSUB - 1));
+  const ChunkRow c = chunks[blockIdx.x];
+  // the write pass's look-back word of this chunk, from the previous encode (stream-ordered)
+  if (threadIdx.x == 0) lb[blockIdx.x] = 0ull;
+  float4 v[EW_CU];
+  ew_ld_chunk(gp, nullptr, c, v);
+  topk_ef_stage<EFM>(gp, dg, resid, c, v);
   uint32_t kmax = 0;
 #pragma unroll
   for (int u = 0; u < EW_CU; ++u) {
@@ -436,16 +446,183 @@ __device__ __forceinline__ void topk_scan(
 
 enum ValueKind { VK_Q8 = 0, VK_Q4 = 1, VK_F32 = 2 };
 
+
 // Ordered stream compaction of the selected entries of one chunk + fused quantisation.
 // Decoupled look-back word of a chunk: status (1 = its own counts, 2 = inclusive prefix over the
 // tensor's chunks up to it) | #(key > thr) | #(key == thr), 31 bits each.
 constexpr unsigned long long LB_AGG = 1ull << 62, LB_INC = 2ull << 62;
-constexpr unsigned long long LB_SPIN_TICKS = 20000000ull;  // 0.2 s of the 100 MHz clock: never hang
+// Look-back spin bound, counted in polls (each ~1 us of s_sleep): never hang, and time a wave spends
+// descheduled (CWSR time-slicing between processes sharing the GPU) does not count against it, as
+// it would with a wall-clock bound.  A predecessor is an earlier block of the same launch (resident
+// or done), so a healthy wait is a few polls; reaching the bound bumps the error counter, which the
+// trainer checks (GradientExchange.check_codec_health) and turns into a loud failure.
+constexpr uint32_t LB_MAX_POLLS = 1u << 18;
 __device__ __forceinline__ unsigned long long lb_pack(uint32_t gt, uint32_t eq) {
   return ((unsigned long long)gt << 31) | (unsigned long long)eq;
 }
 
-template <int VK, bool EF, bool LB>
+// Decoupled look-back over a tensor's chunks (consecutive blocks of one launch, dispatched in
+// order): publish this chunk's per-thread counts gt (#key > thr) and eq (#key == thr) summed over
+// the block, then sum the words of the earlier chunks (64 per poll) until an inclusive one.
+// Leaves {gt before, eq before, gt, eq} of this chunk in s_lb[0..3] (after a __syncthreads).
+__device__ __forceinline__ void topk_lookback(uint32_t gt, uint32_t eq, const ChunkRow& c,
+                                              const TensorRow& tr,
+                                              unsigned long long* __restrict__ lb,
+                                              int* __restrict__ lb_err, uint32_t* s_lb,
+                                              int lb_fault) {
+  gt = ew_wave_sum_u(gt);
+  eq = ew_wave_sum_u(eq);
+  if ((threadIdx.x & 63) == 0) {
+    s_lb[threadIdx.x >> 6] = gt;
+    s_lb[EW_WAVES + (threadIdx.x >> 6)] = eq;
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {  // wave 0: publish, then look back 64 predecessors at a time
+    const int lane = threadIdx.x;
+    gt = eq = 0;
+    for (int w = 0; w < EW_WAVES; ++w) {
+      gt += s_lb[w];
+      eq += s_lb[EW_WAVES + w];
+    }
+    unsigned long long* my = lb + blockIdx.x;
+    uint32_t gb = 0, eb = 0;
+    // lb_fault (test hook): a tensor's first chunk never publishes, so its successors reach the
+    // poll bound and report through lb_err
+    if (lane == 0 && !(lb_fault && c.local == 0))
+      __hip_atomic_store(my, (c.local == 0 ? LB_INC : LB_AGG) | lb_pack(gt, eq),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (c.local > 0) {
+      // predecessors are earlier blocks of this launch (chunk rows of a tensor are consecutive
+      // and dispatched in order), so they are resident or done; the spin is still bounded
+      int p = (int)blockIdx.x - 1;
+      uint32_t polls = 0;
+      while (true) {
+        const int q = p - lane;  // lane 0: the nearest predecessor
+        // the tensor's first chunk always publishes an inclusive word: nothing before it
+        const unsigned long long w = q >= tr.chunk0
+            ? __hip_atomic_load(lb + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+            : LB_INC;
+        const unsigned long long st = w & (3ull << 62);
+        const unsigned long long inc = __ballot(st == LB_INC);
+        const unsigned long long none = __ballot(st == 0);
+        const int last = inc ? __ffsll((long long)inc) - 1 : 63;  // lanes 0..last contribute
+        const unsigned long long need_mask = last == 63 ? ~0ull : ((2ull << last) - 1ull);
+        if (none & need_mask) {  // a predecessor not published yet: read the window again
+          if (++polls > LB_MAX_POLLS) {
+            if (lane == 0) atomicAdd(lb_err, 1);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(16);
+          continue;
+        }
+        const bool use = lane <= last;
+        const uint32_t wg = use ? ((uint32_t)(w >> 31) & 0x7fffffffu) : 0u;
+        const uint32_t we = use ? ((uint32_t)w & 0x7fffffffu) : 0u;
+        gb += ew_wave_sum_u(wg);  // valid in lane 0
+        eb += ew_wave_sum_u(we);
+        if (inc) break;
+        p -= 64;
+      }
+      if (lane == 0)
+        __hip_atomic_store(my, LB_INC | lb_pack(gb + gt, eb + eq), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (lane == 0) {
+      s_lb[0] = gb;
+      s_lb[1] = eb;
+      s_lb[2] = gt;
+      s_lb[3] = eq;
+    }
+  }
+  __syncthreads();
+}
+
+// Predictive encode, write pass of a tensor on the fast path: the chunk's candidates (every
+// element at or above the predicted threshold, which the fast path guarantees is <= the exact
+// one) were compacted by k_pk_hist0 in index order, so this block reads only them -- ~3 % of the
+// chunk -- instead of the chunk.  Same selection, positions, codes, bitmap words and residual /
+// velocity updates as the full pass below, bit for bit.
+template <int VK, bool EF>
+__device__ __forceinline__ void topk_write_cands(
+    const ChunkRow& c, const TensorRow& tr, float* __restrict__ resid, float* __restrict__ vel,
+    const uint32_t* __restrict__ state, uint8_t* __restrict__ payload, int scales_off,
+    int idx_off, int codes_off, int bitmap_off, int counts_off, float levels, float inv_levels,
+    uint32_t key, uint32_t bucket_offset, unsigned long long* __restrict__ lb,
+    int* __restrict__ lb_err, uint32_t n, const uint2* __restrict__ cs, uint32_t* ws,
+    uint32_t* s_lb, int lb_fault) {
+  __shared__ uint32_t bm[EW_BM_WORDS];
+  const uint32_t thr = state[c.tensor * 4];
+  const uint32_t eend = (uint32_t)(tr.entry0 + tr.k);
+  const bool bitmap = tr.bm0 >= 0;
+  if (bitmap)
+    for (int i = threadIdx.x; i < EW_BM_WORDS; i += EW_BLOCK) bm[i] = 0u;
+  uint32_t gt = 0, eq = 0;
+  for (uint32_t i = threadIdx.x; i < n; i += EW_BLOCK) {
+    const uint32_t k = cs[i].x & 0x7fffffffu;
+    gt += k > thr;
+    eq += k == thr;
+  }
+  topk_lookback(gt, eq, c, tr, lb, lb_err, s_lb, lb_fault);  // ends with __syncthreads
+  const uint32_t need = state[c.tensor * 4 + 1];
+  const uint32_t gb = s_lb[0], eb = s_lb[1], gtc = s_lb[2], eqc = s_lb[3];
+  const uint32_t left_ties = need > eb ? need - eb : 0u;
+  const uint32_t ties = left_ties < eqc ? left_ties : eqc;
+  const uint32_t ebase = (uint32_t)tr.entry0 + gb + (need < eb ? need : eb);
+  if (threadIdx.x == 0)
+    reinterpret_cast<uint16_t*>(payload + counts_off)[blockIdx.x] = (uint16_t)(gtc + ties);
+  const float scale = __uint_as_float(state[c.tensor * 4 + 2]);
+  const float inv = scale > 0.0f ? levels / scale : 0.0f;
+  const float step = VK != VK_F32 ? scale * inv_levels : 0.0f;
+  if (threadIdx.x == 0 && c.local == 0) reinterpret_cast<float*>(payload + scales_off)[c.tensor] = scale;
+  uint16_t* idx_out = reinterpret_cast<uint16_t*>(payload + idx_off) + (bitmap ? 0 : tr.idx0) -
+                      tr.entry0;
+  const uint32_t gbase = bucket_offset + (uint32_t)c.start;
+  const int ibase = c.local * EW_CHUNK;
+  uint32_t carry_gt = 0, carry_eq = 0;
+  for (uint32_t r0 = 0; r0 < n; r0 += EW_BLOCK) {  // uniform: n is the block's
+    const uint32_t i = r0 + threadIdx.x;
+    const bool valid = i < n;
+    const uint2 e = valid ? cs[i] : make_uint2(0u, 0u);
+    const float x = __uint_as_float(e.x);
+    const uint32_t k = e.x & 0x7fffffffu;
+    const bool isgt = valid && k > thr, iseq = valid && k == thr;
+    uint32_t tot;
+    const uint32_t ex = ew_block_excl_scan((uint32_t)isgt | ((uint32_t)iseq << 16), ws, tot);
+    const uint32_t eqr = carry_eq + (ex >> 16);
+    const uint32_t pos = ebase + carry_gt + (ex & 0xffffu) + min(ties, eqr);
+    if ((isgt || (iseq && eqr < ties)) && pos < eend) {
+      const int li = (int)e.y - ibase;  // chunk-local index
+      if (bitmap) atomicOr(&bm[li >> 5], 1u << (li & 31));
+      else idx_out[pos] = (uint16_t)li;
+      float sent;
+      if (VK == VK_F32) {
+        reinterpret_cast<float*>(payload + codes_off)[pos] = x;
+        sent = x;
+      } else {
+        const int q = ew_quantize(x, inv, levels, gbase + (uint32_t)li, key);
+        if (VK == VK_Q8) {
+          reinterpret_cast<int8_t*>(payload + codes_off)[pos] = (int8_t)q;
+        } else {
+          atomicOr(reinterpret_cast<uint32_t*>(payload + codes_off) + (pos >> 3),
+                   ((uint32_t)q & 0xfu) << ((pos & 7u) * 4u));
+        }
+        sent = (float)q * step;
+      }
+      if (vel) vel[c.start + li] = 0.0f;
+      if (EF) resid[c.start + li] = x - sent;
+    }
+    carry_gt += tot & 0xffffu;
+    carry_eq += tot >> 16;
+  }
+  if (bitmap) {
+    __syncthreads();
+    uint32_t* bm_out = reinterpret_cast<uint32_t*>(payload + bitmap_off) + tr.bm0 +
+                       c.local * EW_BM_WORDS;
+    for (int w = threadIdx.x; w * 32 < c.len; w += EW_BLOCK) bm_out[w] = bm[w];
+  }
+}
+
+template <int VK, bool EF, bool LB, bool PK>
 __global__ __launch_bounds__(EW_BLOCK) void k_topk_write(
     GradPtrs gp, float* __restrict__ resid, const ChunkRow* __restrict__ chunks,
     const TensorRow* __restrict__ tensors, const uint32_t* __restrict__ state,
@@ -455,7 +632,9 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_write(
     const uint32_t* __restrict__ keyp,
     uint32_t bucket_offset, uint32_t* __restrict__ rezero, uint32_t rezero_words,
     float* __restrict__ vel, unsigned long long* __restrict__ lb, int counts_off,
-    int* __restrict__ lb_err) {
+    int* __restrict__ lb_err, const uint32_t* __restrict__ pst,
+    const uint32_t* __restrict__ cbase, const uint32_t* __restrict__ ccnt,
+    const uint2* __restrict__ pcand, int lb_fault) {
   __shared__ uint32_t ws[EW_WAVES];
   __shared__ uint32_t s_lb[2 * EW_WAVES];
   // the histograms / max-key replicas are dead once the thresholds are selected: clear them here
@@ -465,6 +644,13 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_write(
   const uint32_t key = keyp ? *keyp : key_arg;  // device key: fresh per replay of a captured graph
   const ChunkRow c = chunks[blockIdx.x];
   const TensorRow tr = tensors[c.tensor];
+  if (PK && pst[c.tensor * 8 + 3]) {  // predictive fast path: the chunk's candidates only
+    topk_write_cands<VK, EF>(c, tr, resid, vel, state, payload, scales_off, idx_off, codes_off,
+                             bitmap_off, counts_off, levels, inv_levels, key, bucket_offset, lb,
+                             lb_err, ccnt[blockIdx.x], pcand + tr.cap0 + cbase[blockIdx.x], ws,
+                             s_lb, lb_fault);
+    return;
+  }
   const float* flat = EF ? resid : nullptr;  // EF: hist0 staged e = g + r in the residual
   const uint32_t thr = state[c.tensor * 4];
   const uint32_t eend = (uint32_t)(tr.entry0 + tr.k);  // never write past this tensor's entries
@@ -487,69 +673,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_write(
         eq += ok && k == thr;
       }
     }
-    gt = ew_wave_sum_u(gt);
-    eq = ew_wave_sum_u(eq);
-    if ((threadIdx.x & 63) == 0) {
-      s_lb[threadIdx.x >> 6] = gt;
-      s_lb[EW_WAVES + (threadIdx.x >> 6)] = eq;
-    }
-    __syncthreads();
-    if (threadIdx.x < 64) {  // wave 0: publish, then look back 64 predecessors at a time
-      const int lane = threadIdx.x;
-      gt = eq = 0;
-      for (int w = 0; w < EW_WAVES; ++w) {
-        gt += s_lb[w];
-        eq += s_lb[EW_WAVES + w];
-      }
-      unsigned long long* my = lb + blockIdx.x;
-      uint32_t gb = 0, eb = 0;
-      if (lane == 0)
-        __hip_atomic_store(my, (c.local == 0 ? LB_INC : LB_AGG) | lb_pack(gt, eq),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (c.local > 0) {
-        // predecessors are earlier blocks of this launch (chunk rows of a tensor are consecutive
-        // and dispatched in order), so they are resident or done; the spin is still bounded
-        int p = (int)blockIdx.x - 1;
-        const unsigned long long t0 = wall_clock64();
-        while (true) {
-          const int q = p - lane;  // lane 0: the nearest predecessor
-          // the tensor's first chunk always publishes an inclusive word: nothing before it
-          const unsigned long long w = q >= tr.chunk0
-              ? __hip_atomic_load(lb + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-              : LB_INC;
-          const unsigned long long st = w & (3ull << 62);
-          const unsigned long long inc = __ballot(st == LB_INC);
-          const unsigned long long none = __ballot(st == 0);
-          const int last = inc ? __ffsll((long long)inc) - 1 : 63;  // lanes 0..last contribute
-          const unsigned long long need_mask = last == 63 ? ~0ull : ((2ull << last) - 1ull);
-          if (none & need_mask) {  // a predecessor not published yet: read the window again
-            if (wall_clock64() - t0 > LB_SPIN_TICKS) {
-              if (lane == 0) atomicAdd(lb_err, 1);
-              break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-            continue;
-          }
-          const bool use = lane <= last;
-          const uint32_t wg = use ? ((uint32_t)(w >> 31) & 0x7fffffffu) : 0u;
-          const uint32_t we = use ? ((uint32_t)w & 0x7fffffffu) : 0u;
-          gb += ew_wave_sum_u(wg);  // valid in lane 0
-          eb += ew_wave_sum_u(we);
-          if (inc) break;
-          p -= 64;
-        }
-        if (lane == 0)
-          __hip_atomic_store(my, LB_INC | lb_pack(gb + gt, eb + eq), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-      }
-      if (lane == 0) {
-        s_lb[0] = gb;
-        s_lb[1] = eb;
-        s_lb[2] = gt;
-        s_lb[3] = eq;
-      }
-    }
-    __syncthreads();
+    topk_lookback(gt, eq, c, tr, lb, lb_err, s_lb, lb_fault);
     // ties go to the lowest-index chunks: this chunk keeps what the earlier ones left of `need`
     const uint32_t need = state[c.tensor * 4 + 1];
     const uint32_t gb = s_lb[0], eb = s_lb[1], gtc = s_lb[2], eqc = s_lb[3];
@@ -641,6 +765,299 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_write(
     }
     carry_gt += tot & 0xffffu;
     carry_eq += tot >> 16;
+  }
+}
+
+// =============================================================================================
+// Predictive encode (max-norm scale).  Under error feedback the vector to compress changes little
+// from one step to the next, so the exact threshold of the previous encode predicts this one's.
+// k_pk_hist0 stages e (error feedback) and, in the same pass over the bucket, compacts every
+// element whose key is >= P = key(beta * previous threshold) into a per-tensor candidate list
+// (value, index; chunk segments in index order).  If a tensor's candidates number at least k (so
+// its exact threshold is >= P and every element the selection can take is a candidate) and fit
+// the list, the three radix passes and the write pass read only the candidates (~3 % of the
+// bucket) instead of re-reading the bucket twice; otherwise that tensor takes the full passes for
+// this step.  Either way the selection is exact: same entries, codes, ties, residual and
+// velocity as the full path, bit for bit.  beta adapts per tensor (k_pk_pass2's tail).
+//
+// pst[8 t + ...]: 0 P (key used by this encode), 1 beta (float bits; 0 = not yet set), 2 M (this
+// encode's candidates), 3 fast flag, 4 P valid (a previous encode set it).
+// =============================================================================================
+constexpr float PK_BETA0 = 0.85f;
+
+// block-exclusive scan of two packed u64 words (4 x 16-bit fields each) in thread order
+__device__ __forceinline__ void pk_scan2(unsigned long long& a, unsigned long long& b,
+                                         unsigned long long* ws, unsigned long long& ta,
+                                         unsigned long long& tb) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  unsigned long long ia = a, ib = b;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const unsigned long long xa = __shfl_up(ia, d, 64), xb = __shfl_up(ib, d, 64);
+    if (lane >= d) {
+      ia += xa;
+      ib += xb;
+    }
+  }
+  if (lane == 63) {
+    ws[w] = ia;
+    ws[EW_WAVES + w] = ib;
+  }
+  __syncthreads();
+  unsigned long long ba = 0, bb = 0, sa = 0, sb = 0;
+#pragma unroll
+  for (int i = 0; i < EW_WAVES; ++i) {
+    const unsigned long long xa = ws[i], xb = ws[EW_WAVES + i];
+    ba += i < w ? xa : 0ull;
+    bb += i < w ? xb : 0ull;
+    sa += xa;
+    sb += xb;
+  }
+  __syncthreads();
+  ta = sa;
+  tb = sb;
+  a = ba + ia - a;
+  b = bb + ib - b;
+}
+
+template <int EFM>
+__global__ __launch_bounds__(EW_BLOCK) void k_pk_hist0(
+    GradPtrs gp, DgcArgs dg, unsigned long long* __restrict__ lb, float* __restrict__ resid,
+    const ChunkRow* __restrict__ chunks, uint32_t* __restrict__ kmaxr, int T,
+    const TensorRow* __restrict__ tensors, uint32_t* __restrict__ pst, int* __restrict__ tick,
+    int* __restrict__ ccount, uint32_t* __restrict__ cbase, uint32_t* __restrict__ ccnt,
+    uint2* __restrict__ pcand, int* __restrict__ stats) {
+  __shared__ unsigned long long ws2[2 * EW_WAVES];
+  __shared__ uint32_t wmax[EW_WAVES];
+  __shared__ uint32_t s_base;
+  const ChunkRow c = chunks[blockIdx.x];
+  const TensorRow tr = tensors[c.tensor];
+  if (threadIdx.x == 0) lb[blockIdx.x] = 0ull;  // the write pass's look-back word
+  float4 v[EW_CU];
+  ew_ld_chunk(gp, nullptr, c, v);
+  topk_ef_stage<EFM>(gp, dg, resid, c, v);
+  const uint32_t P = pst[c.tensor * 8];
+  uint32_t kmax = 0;
+  unsigned long long pa = 0, pb = 0;  // candidates per slab, 16-bit fields (slabs 0-3, 4-7)
+#pragma unroll
+  for (int u = 0; u < EW_CU; ++u) {
+    uint32_t n = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (ew_chunk_idx(u) + j < c.len) {
+        const uint32_t k = ew_key(ew_f4(v[u], j));
+        kmax = max(kmax, k);
+        n += k >= P;
+      }
+    }
+    if (u < 4) pa |= (unsigned long long)n << (16 * u);
+    else pb |= (unsigned long long)n << (16 * (u - 4));
+  }
+  kmax = ew_wave_max_u(kmax);
+  if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = kmax;
+  unsigned long long ta, tb;
+  pk_scan2(pa, pb, ws2, ta, tb);  // contains __syncthreads: wmax visible
+  // slab starts within the chunk's candidate segment (index order: slab, then thread, then j)
+  uint32_t start[EW_CU];
+  uint32_t run = 0;
+#pragma unroll
+  for (int u = 0; u < EW_CU; ++u) {
+    start[u] = run;
+    run += (uint32_t)(((u < 4 ? ta : tb) >> (16 * (u & 3))) & 0xffffull);
+  }
+  const uint32_t tot = run;
+  if (threadIdx.x == 0) {
+    uint32_t m = wmax[0];
+    for (int w = 1; w < EW_WAVES; ++w) m = max(m, wmax[w]);
+    atomicMax(&kmaxr[(blockIdx.x & (NREP - 1)) * T + c.tensor], m);
+    const uint32_t base = tot ? (uint32_t)atomicAdd(ccount + TICK_STRIDE * c.tensor, (int)tot) : 0u;
+    s_base = base;
+    cbase[blockIdx.x] = base;
+    ccnt[blockIdx.x] = tot;
+  }
+  __syncthreads();
+  if (tot) {
+    uint2* dst = pcand + tr.cap0;
+    const uint32_t cap = (uint32_t)tr.cap, base = s_base;
+#pragma unroll
+    for (int u = 0; u < EW_CU; ++u) {
+      uint32_t pos = base + start[u] +
+                     (uint32_t)(((u < 4 ? pa : pb) >> (16 * (u & 3))) & 0xffffull);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int i = ew_chunk_idx(u) + j;
+        const float x = ew_f4(v[u], j);
+        if (i < c.len && ew_key(x) >= P) {
+          if (pos < cap) dst[pos] = make_uint2(__float_as_uint(x), (uint32_t)(c.local * EW_CHUNK + i));
+          ++pos;
+        }
+      }
+    }
+  }
+  if (topk_tensor_last(tick + TICK_STRIDE * c.tensor, tr.nchunks, reinterpret_cast<int*>(wmax)) &&
+      threadIdx.x == 0) {
+    int* cc = ccount + TICK_STRIDE * c.tensor;
+    const uint32_t M = (uint32_t)__hip_atomic_load(cc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(cc, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t fast = M >= (uint32_t)tr.k && M <= (uint32_t)tr.cap;
+    pst[c.tensor * 8 + 2] = M;
+    pst[c.tensor * 8 + 3] = fast;
+    atomicAdd(stats + (fast ? 0 : 1), 1);
+  }
+}
+
+// Calls f(key) (f(key, value) not needed) for this candidate-pass block's share of tensor t: its
+// candidates [8192 j, 8192 (j + 1)) on the fast path, else every ncb-th chunk from j of the tensor
+// (the full pass, read from the staged e or the gradients).
+template <typename F>
+__device__ __forceinline__ void pk_visit(const GradPtrs& gp, const float* flat,
+                                         const ChunkRow* __restrict__ chunks, const TensorRow& tr,
+                                         int j, bool fast, uint32_t M,
+                                         const uint2* __restrict__ pcand, F&& f) {
+  if (fast) {
+    const uint2* src = pcand + tr.cap0;
+    const uint32_t i1 = min(M, (uint32_t)(j + 1) * EW_CHUNK);
+    for (uint32_t i = (uint32_t)j * EW_CHUNK + threadIdx.x; i < i1; i += EW_BLOCK)
+      f(src[i].x & 0x7fffffffu);
+    return;
+  }
+  for (int lc = j; lc < tr.nchunks; lc += tr.ncb) {
+    const ChunkRow c = chunks[tr.chunk0 + lc];
+    float4 v[EW_CU];
+    ew_ld_chunk(gp, flat, c, v);
+#pragma unroll
+    for (int u = 0; u < EW_CU; ++u)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj)
+        if (ew_chunk_idx(u) + jj < c.len) f(ew_key(ew_f4(v[u], jj)));
+  }
+}
+
+// wave-aggregated append: one atomic per wave per call (order within the list does not matter)
+__device__ __forceinline__ void pk_append(bool pred, uint32_t key, int* counter, uint32_t* dst) {
+  const unsigned long long m = __ballot(pred);
+  if (!m) return;
+  const int lane = threadIdx.x & 63;
+  const int leader = __ffsll((long long)m) - 1;
+  uint32_t base = 0;
+  if (lane == leader) base = (uint32_t)atomicAdd(counter, __popcll(m));
+  base = __shfl(base, leader, 64);
+  if (pred) dst[base + __popcll(m & ((1ull << lane) - 1ull))] = key;
+}
+
+// Radix pass 0 (key bits [30:20]) over the candidates (fast) or the tensor (full).
+__global__ __launch_bounds__(EW_BLOCK) void k_pk_pass0(
+    GradPtrs gp, const float* __restrict__ flat, const ChunkRow* __restrict__ chunks,
+    const CBlockRow* __restrict__ cblocks, const TensorRow* __restrict__ tensors,
+    const uint32_t* __restrict__ pst, const uint2* __restrict__ pcand, uint32_t* __restrict__ hist,
+    const uint32_t* __restrict__ kmaxr, uint32_t* __restrict__ state, int T, int* __restrict__ tick) {
+  constexpr int HSUB = 4;
+  __shared__ uint32_t hs[NB0 * HSUB];
+  for (int i = threadIdx.x; i < NB0 * HSUB; i += EW_BLOCK) hs[i] = 0;
+  __syncthreads();
+  uint32_t* h = hs + (threadIdx.x & (HSUB - 1));
+  const CBlockRow cb = cblocks[blockIdx.x];
+  const int t = cb.tensor;
+  const TensorRow tr = tensors[t];
+  pk_visit(gp, flat, chunks, tr, cb.j, pst[t * 8 + 3] != 0, pst[t * 8 + 2], pcand,
+           [&](uint32_t k) { atomicAdd(&h[(k >> 20) * HSUB], 1u); });
+  __syncthreads();
+  uint32_t* dst = hist + ((size_t)(blockIdx.x & (NREP - 1)) * T + t) * NB0;
+  for (int i = threadIdx.x; i < NB0; i += EW_BLOCK) {
+    uint32_t x = 0;
+#pragma unroll
+    for (int q = 0; q < HSUB; ++q) x += hs[i * HSUB + q];
+    if (x) atomicAdd(&dst[i], x);
+  }
+  if (topk_tensor_last(tick + TICK_STRIDE * t, tr.ncb, reinterpret_cast<int*>(hs)))
+    topk_select<NB0, 20, true>(hist, tensors, state, kmaxr, T, t);
+}
+
+// Radix pass 1 (bits [19:10]) over the keys in the selected top digit, which are also appended to
+// the tensor's key list cand[tensor.off ..) for pass 2.
+__global__ __launch_bounds__(EW_BLOCK) void k_pk_pass1(
+    GradPtrs gp, const float* __restrict__ flat, const ChunkRow* __restrict__ chunks,
+    const CBlockRow* __restrict__ cblocks, const TensorRow* __restrict__ tensors,
+    const uint32_t* __restrict__ pst, const uint2* __restrict__ pcand, uint32_t* __restrict__ hist,
+    const uint32_t* __restrict__ kmaxr, uint32_t* __restrict__ state, int T, int* __restrict__ tick,
+    uint32_t* __restrict__ cand, int* __restrict__ cand_n) {
+  __shared__ uint32_t h[NB1];
+  for (int i = threadIdx.x; i < NB1; i += EW_BLOCK) h[i] = 0;
+  __syncthreads();
+  const CBlockRow cb = cblocks[blockIdx.x];
+  const int t = cb.tensor;
+  const TensorRow tr = tensors[t];
+  const uint32_t want = state[t * 4] >> 20;
+  int* cn = cand_n + TICK_STRIDE * t;
+  uint32_t* cdst = cand + tr.off;
+  pk_visit(gp, flat, chunks, tr, cb.j, pst[t * 8 + 3] != 0, pst[t * 8 + 2], pcand,
+           [&](uint32_t k) {
+             const bool m = (k >> 20) == want;
+             if (m) atomicAdd(&h[(k >> 10) & (NB1 - 1)], 1u);
+             pk_append(m, k, cn, cdst);
+           });
+  __syncthreads();
+  uint32_t* dst = hist + ((size_t)(blockIdx.x & (NREP - 1)) * T + t) * NB1;
+  for (int i = threadIdx.x; i < NB1; i += EW_BLOCK)
+    if (h[i]) atomicAdd(&dst[i], h[i]);
+  if (topk_tensor_last(tick + TICK_STRIDE * t, tr.ncb, reinterpret_cast<int*>(h)))
+    topk_select<NB1, 10, false>(hist, tensors, state, kmaxr, T, t);
+}
+
+// Radix pass 2 (bits [9:0]) over the pass-1 keys; the tensor's last block fixes the exact
+// threshold and the ties, then predicts the next encode's candidate bound.
+__global__ __launch_bounds__(EW_BLOCK) void k_pk_pass2(
+    const CBlockRow* __restrict__ cblocks, const TensorRow* __restrict__ tensors,
+    uint32_t* __restrict__ pst, uint32_t* __restrict__ hist, const uint32_t* __restrict__ kmaxr,
+    uint32_t* __restrict__ state, int T, int* __restrict__ tick, const uint32_t* __restrict__ cand,
+    int* __restrict__ cand_n) {
+  __shared__ uint32_t h[NB2];
+  for (int i = threadIdx.x; i < NB2; i += EW_BLOCK) h[i] = 0;
+  __syncthreads();
+  const CBlockRow cb = cblocks[blockIdx.x];
+  const int t = cb.tensor;
+  const TensorRow tr = tensors[t];
+  const uint32_t n = (uint32_t)__hip_atomic_load(cand_n + TICK_STRIDE * t, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t want = state[t * 4] >> 10;
+  const uint32_t* src = cand + tr.off;
+  const uint32_t stride = (uint32_t)tr.ncb * EW_CHUNK;
+  for (uint32_t b0 = (uint32_t)cb.j * EW_CHUNK; b0 < n; b0 += stride) {
+    const uint32_t i1 = min(n, b0 + EW_CHUNK);
+    for (uint32_t i = b0 + threadIdx.x; i < i1; i += EW_BLOCK) {
+      const uint32_t k = src[i];
+      if ((k >> 10) == want) atomicAdd(&h[k & (NB2 - 1)], 1u);
+    }
+  }
+  __syncthreads();
+  uint32_t* dst = hist + ((size_t)(blockIdx.x & (NREP - 1)) * T + t) * NB2;
+  for (int i = threadIdx.x; i < NB2; i += EW_BLOCK)
+    if (h[i]) atomicAdd(&dst[i], h[i]);
+  if (topk_tensor_last(tick + TICK_STRIDE * t, tr.ncb, reinterpret_cast<int*>(h))) {
+    topk_select<NB2, 0, false>(hist, tensors, state, kmaxr, T, t);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      cand_n[TICK_STRIDE * t] = 0;  // every block read n before it arrived
+      // next encode's candidate bound: beta x this exact threshold, beta steered so the
+      // candidates stay between ~2k and 3/4 of the list
+      // written by this block's select just now (agent-scope load: not a stale L1 line)
+      const uint32_t thr = __hip_atomic_load(state + t * 4, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t M = pst[t * 8 + 2], fast = pst[t * 8 + 3], had = pst[t * 8 + 4];
+      float beta = __uint_as_float(pst[t * 8 + 1]);
+      if (!(beta > 0.0f)) beta = PK_BETA0;
+      const uint32_t k = (uint32_t)tr.k, cap = (uint32_t)tr.cap;
+      if (had) {
+        if (!fast && M > cap) beta = beta + (1.0f - beta) * 0.5f;  // too many: tighter
+        else if (!fast) beta = beta * 0.8f;                        // too few: the bound was above
+        else if (M > cap - cap / 4) beta = beta + (1.0f - beta) * 0.25f;
+        else if (M < 2u * k) beta = beta * 0.95f;
+      }
+      beta = fminf(fmaxf(beta, 0.25f), 0.99f);
+      pst[t * 8 + 1] = __float_as_uint(beta);
+      pst[t * 8 + 0] = ew_key(__uint_as_float(thr) * beta);
+      pst[t * 8 + 4] = 1u;
+    }
   }
 }
 
@@ -816,9 +1233,18 @@ void ew_topk_encode(const TopkEncodeArgs& a) {
       (reinterpret_cast<uintptr_t>(inv + T) + TICK_STRIDE * 4 - 1) & ~(uintptr_t)(TICK_STRIDE * 4 - 1));
   int* cand_n = tick + 4 * TICK_STRIDE * T;
   int* lb_err = cand_n + TICK_STRIDE * T;
+  int* pk_stats = lb_err + 2;  // predictive encode: tensor-encodes on the fast / full path
   auto* lb = reinterpret_cast<unsigned long long*>(lb_err + TICK_STRIDE);
   uint32_t* cand = reinterpret_cast<uint32_t*>(lb + C);
   if (a.bucket_len <= 0) throw std::runtime_error("ewdml topk: bucket length missing");
+  // predictive encode state after the candidate keys: pstate u32[8 T] | chunk candidate base and
+  // count u32[C] each | candidate counters [T] (one line each) | candidate list u64[total_cap]
+  uint32_t* pst = cand + a.bucket_len;
+  uint32_t* cbase = pst + 8 * T;
+  uint32_t* ccnt = cbase + C;
+  int* ccount = reinterpret_cast<int*>(ccnt + C);
+  auto* pcand = reinterpret_cast<uint2*>(
+      (reinterpret_cast<uintptr_t>(ccount + TICK_STRIDE * T) + 15) & ~(uintptr_t)15);
   hipStream_t s = (hipStream_t)a.stream;
   // no scratch memset: state / count sections are fully rewritten each encode, and the histogram
   // replicas are cleared by k_topk_write for the next one (zero-initialised at allocation)
@@ -836,6 +1262,42 @@ void ew_topk_encode(const TopkEncodeArgs& a) {
   if (dg.vel && !resid) throw std::runtime_error("ewdml topk: momentum correction needs a residual");
   if (dg.vel && dg.wd != 0.0f && !dg.param)
     throw std::runtime_error("ewdml topk: weight decay in the momentum correction needs params");
+  auto* pay = reinterpret_cast<uint8_t*>(a.payload);
+  const bool pk = a.predict && !a.norm_l2 && a.cblocks && a.num_cblocks > 0;
+  if (pk) {
+    // predictive path: hist0 (+ candidates) -> 3 radix passes over the candidates -> write
+    auto* cbl = reinterpret_cast<const CBlockRow*>(a.cblocks);
+    const int G = a.num_cblocks;
+#define EW_PKH(EFM)                                                                              \
+  EW_LAUNCH(k_pk_hist0<EFM>, C, s, g, dg, lb, resid, chunks, kmaxr, T, tensors, pst, tick, ccount, \
+            cbase, ccnt, pcand, pk_stats)
+    if (dg.vel) EW_PKH(EF_DGC);
+    else if (resid) EW_PKH(EF_PLAIN);
+    else EW_PKH(EF_NONE);
+#undef EW_PKH
+    EW_LAUNCH(k_pk_pass0, G, s, g, src_flat, chunks, cbl, tensors, pst, pcand, hist0, kmaxr, state,
+              T, tick + TICK_STRIDE * T);
+    EW_LAUNCH(k_pk_pass1, G, s, g, src_flat, chunks, cbl, tensors, pst, pcand, hist1, kmaxr, state,
+              T, tick + 2 * TICK_STRIDE * T, cand, cand_n);
+    EW_LAUNCH(k_pk_pass2, G, s, cbl, tensors, pst, hist2, kmaxr, state, T,
+              tick + 3 * TICK_STRIDE * T, cand, cand_n);
+#define EW_PKW(VK, EFV)                                                                          \
+  EW_LAUNCH((k_topk_write<VK, EFV, true, true>), C, s, g, resid, chunks, tensors, state, chunk_off, \
+            chunk_ties, inv, pay, a.scales_off, a.idx_off, a.codes_off, a.bitmap_off, a.levels,   \
+            a.inv_levels, a.key, reinterpret_cast<const uint32_t*>(a.key_ptr), a.bucket_offset,   \
+            kmaxr, rezero_words, dg.mask ? dg.vel : nullptr, lb, a.counts_off, lb_err, pst, cbase, \
+            ccnt, pcand, a.lb_fault)
+    if (a.value_kind == VK_Q8) {
+      if (resid) EW_PKW(VK_Q8, true); else EW_PKW(VK_Q8, false);
+    } else if (a.value_kind == VK_Q4) {
+      if (resid) EW_PKW(VK_Q4, true); else EW_PKW(VK_Q4, false);
+    } else {
+      if (resid) EW_PKW(VK_F32, true); else EW_PKW(VK_F32, false);
+    }
+#undef EW_PKW
+    EW_CHECK_LAUNCH();
+    return;
+  }
   if (dg.vel)
     EW_LAUNCH(k_topk_hist0<EF_DGC>, C, s, g, dg, lb, resid, chunks, hist0, kmaxr, T, tensors, state,
               tick);
@@ -849,7 +1311,6 @@ void ew_topk_encode(const TopkEncodeArgs& a) {
             tick + TICK_STRIDE * T, cand, cand_n);
   EW_LAUNCH(k_topk_hist2, C, s, chunks, state, hist2, T, tensors, kmaxr, tick + 2 * TICK_STRIDE * T,
             cand, cand_n);
-  auto* pay = reinterpret_cast<uint8_t*>(a.payload);
   // the L2 scale needs the selected values' sum of squares before any code is written: a count
   // pass; the max-norm scale is hist0's max key and the write pass looks back for its offsets
   const bool lbk = !a.norm_l2;
@@ -858,10 +1319,11 @@ void ew_topk_encode(const TopkEncodeArgs& a) {
               tick + 3 * TICK_STRIDE * T, chunk_off, chunk_ties, inv, pay, a.scales_off, a.counts_off,
               a.levels, a.norm_l2);
 #define EW_WRITE(VK, EFV, LBV)                                                                     \
-  EW_LAUNCH((k_topk_write<VK, EFV, LBV>), C, s, g, resid, chunks, tensors, state, chunk_off,        \
+  EW_LAUNCH((k_topk_write<VK, EFV, LBV, false>), C, s, g, resid, chunks, tensors, state, chunk_off, \
             chunk_ties, inv, pay, a.scales_off, a.idx_off, a.codes_off, a.bitmap_off, a.levels,     \
             a.inv_levels, a.key, reinterpret_cast<const uint32_t*>(a.key_ptr), a.bucket_offset,     \
-            kmaxr, rezero_words, dg.mask ? dg.vel : nullptr, lb, a.counts_off, lb_err)
+            kmaxr, rezero_words, dg.mask ? dg.vel : nullptr, lb, a.counts_off, lb_err, nullptr,     \
+            nullptr, nullptr, nullptr, a.lb_fault)
 #define EW_WRITE2(VK, EFV) \
   do { if (lbk) EW_WRITE(VK, EFV, true); else EW_WRITE(VK, EFV, false); } while (0)
   if (a.value_kind == VK_Q8) {
@@ -876,13 +1338,30 @@ void ew_topk_encode(const TopkEncodeArgs& a) {
   EW_CHECK_LAUNCH();
 }
 
-size_t ew_topk_scratch_bytes(int T, int C, long long L) {
+size_t ew_topk_scratch_bytes(int T, int C, long long L, long long total_cap) {
   // state .. inv, alignment slack + tickets + candidate counts + error counter, look-back words,
-  // candidate keys
+  // candidate keys; predictive state, chunk candidate tables, counters, candidate list
   return sizeof(uint32_t) *
              ((size_t)4 * T + (size_t)NREP * T * (1 + NB0 + NB1 + NB2) + 5 * (size_t)C + T +
               (5 * (size_t)T + 2) * TICK_STRIDE + (size_t)L) +
-         sizeof(unsigned long long) * (size_t)C + 128;
+         sizeof(unsigned long long) * (size_t)C + 128 +
+         sizeof(uint32_t) * (8 * (size_t)T + 2 * (size_t)C + (size_t)TICK_STRIDE * T) + 16 +
+         sizeof(uint2) * (size_t)total_cap;
+}
+
+std::vector<int> ew_topk_stats(uintptr_t scratch, int T, int C) {
+  // same carving as ew_topk_encode: {look-back errors, fast tensor-encodes, full tensor-encodes}
+  uint32_t* state = reinterpret_cast<uint32_t*>(scratch);
+  uint32_t* kmaxr = state + 4 * T;
+  uint32_t* hist2 = kmaxr + NREP * T + (size_t)NREP * T * NB0 + (size_t)NREP * T * NB1;
+  float* inv = reinterpret_cast<float*>(hist2 + (size_t)NREP * T * NB2 + 5 * (size_t)C);
+  int* tick = reinterpret_cast<int*>(
+      (reinterpret_cast<uintptr_t>(inv + T) + TICK_STRIDE * 4 - 1) & ~(uintptr_t)(TICK_STRIDE * 4 - 1));
+  int* lb_err = tick + 5 * TICK_STRIDE * T;
+  std::vector<int> v(3, 0);
+  EW_CHECK(hipMemcpy(v.data(), lb_err, sizeof(int), hipMemcpyDeviceToHost));
+  EW_CHECK(hipMemcpy(v.data() + 1, lb_err + 2, 2 * sizeof(int), hipMemcpyDeviceToHost));
+  return v;
 }
 
 int ew_topk_lookback_errors(uintptr_t scratch, int T, int C) {

@@ -417,6 +417,28 @@ class GradientExchange:
                 else rows[src:src + 1]
             self.codec.decode(b.index, row, self.flat.grad_view(b), 1.0)
 
+    def codec_health(self) -> dict:
+        """Counters of this exchange's HIP top-k encodes (synchronises): the predictive encode's
+        fast / full tensor-encodes, and look-back failures -- a write block that gave up waiting
+        on its predecessor (bounded spin) wrote its entries at wrong offsets, so every rank would
+        decode a corrupted gradient: that raises here instead of training on silently."""
+        codec = self.codec
+        if not self.cuda or codec.kind not in ("topk", "topk_qsgd") or codec.allreduce:
+            return {}
+        tot = {"lookback_errors": 0, "fast": 0, "full": 0}
+        seen = set()
+        for _, _, dplans in getattr(codec, "_bound", {}).values():
+            for dp in dplans:
+                if id(dp) in seen:
+                    continue
+                seen.add(id(dp))
+                for k, v in ops.topk_stats(dp).items():
+                    tot[k] += v
+        if tot["lookback_errors"]:
+            raise RuntimeError(f"top-k encode: {tot['lookback_errors']} write block(s) gave up on "
+                               "the decoupled look-back; the payload offsets are corrupt")
+        return {"topk_encode_fast": tot["fast"], "topk_encode_full": tot["full"]}
+
     def close(self):
         if self._hooks:
             for p in self.flat.params:

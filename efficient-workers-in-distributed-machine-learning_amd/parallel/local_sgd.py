@@ -51,6 +51,7 @@ class LocalSGDExchange:
         self.best_rank_history = []
         self.best_t = None  # device index of the last sync's winner (model mode)
         self._plans = None  # pointer mode: per-bucket device plans of the local step
+        self.clock = None  # Stopwatch of --phase-timing (the trainer sets it here and on inner)
 
     @property
     def is_sync(self) -> bool:
@@ -74,7 +75,11 @@ class LocalSGDExchange:
                 stats.wire_bytes_sent += n if self.comm.rank == src else 0
                 stats.wire_bytes_recv += 0 if self.comm.rank == src else n
         else:
+            if self.clock is not None:
+                self.clock.mark("backward")
             self.local_step()  # with the rank's own gradient
+            if self.clock is not None:
+                self.clock.mark("decode_update")
             if sync:  # model mode
                 delta = self.flat.grad
                 torch.sub(self.flat.data, self.anchor, out=delta)
@@ -104,6 +109,8 @@ class LocalSGDExchange:
                 torch.add(self.anchor, self.flat.grad, out=self.flat.data)
                 self.anchor.copy_(self.flat.data)
                 self.flat.sync_shadow()
+                if self.clock is not None:
+                    self.clock.mark("decode_update")
         self.last = stats
         self.step_idx += 1
 

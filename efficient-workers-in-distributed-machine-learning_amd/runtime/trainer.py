@@ -845,6 +845,11 @@ class Trainer:
                         -self.comm.all_reduce_scalars([-(rec["step_ms"] or 0.0)], op="max")[0]
                     rec["step_ms_max"], rec["step_ms_min"] = mx, mn
                 rec.update(byte_summary(self.exchange.last, self.world))
+                # the codec's health at every log record (synchronises: the record already did):
+                # a look-back failure of the top-k encode raises here
+                ge = getattr(self.exchange, "inner", self.exchange)
+                if hasattr(ge, "codec_health"):
+                    rec.update(ge.codec_health())
                 rec["bytes_sent_total"] = acc["bytes_sent"]
                 rec["bytes_recv_total"] = acc["bytes_recv"]
                 rec["payload_bytes_total"] = acc["payload_bytes"]

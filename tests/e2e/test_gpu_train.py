@@ -114,7 +114,8 @@ def test_vgg11_bf16_full_graph_step():
     ops.require()
     flags = ["--network", "VGG11", "--dataset", "Cifar10", "--batch-size", "16",
              "--synthetic-size", "256", "--momentum", "0.9", "--eval-freq", "0", "--quiet",
-             "--device", "cuda", "--hip-graph", "full", "--graph-warmup", "2", "--amp", "bf16"]
+             "--device", "cuda", "--hip-graph", "full", "--graph-warmup", "2", "--amp", "bf16",
+             "--no-error-feedback"]
     tr, losses = _run(flags, 6)
     assert all(torch.isfinite(torch.tensor(losses)))
     assert tr.exchange.last.payload_bytes == 295312
@@ -164,7 +165,8 @@ def test_bf16_params_match_fp32_master_path(monkeypatch):
     monkeypatch.setattr(head, "_ENABLED", False)
     base = ["--network", "VGG11", "--dataset", "Cifar10", "--batch-size", "32",
             "--synthetic-size", "256", "--momentum", "0.9", "--eval-freq", "0", "--quiet",
-            "--device", "cuda", "--hip-graph", "off", "--compress", "topk_qsgd", "--amp", "bf16"]
+            "--device", "cuda", "--hip-graph", "off", "--compress", "topk_qsgd", "--amp", "bf16",
+            "--no-error-feedback"]
     a, la = _run(base + ["--param-dtype", "auto"], 4)
     b, lb = _run(base + ["--param-dtype", "fp32"], 4)
     assert a.flat.shadow is not None and b.flat.shadow is None

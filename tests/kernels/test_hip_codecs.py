@@ -459,3 +459,100 @@ def test_sgd_from_pointer_table_matches_flat():
     for off, n in zip(plan.offsets, plan.numels):
         assert torch.equal(p1[off:off + n], p2[off:off + n])
         assert torch.equal(m1[off:off + n], m2[off:off + n])
+
+
+@pytest.mark.parametrize("kind,bits", [("topk_qsgd", 8), ("topk_qsgd", 4), ("topk", 8)])
+@pytest.mark.parametrize("ratio", [0.01, 0.4])
+def test_topk_predictive_encode_fast_and_full_paths(kind, bits, ratio):
+    """The predictive encode (candidates at or above beta x the previous threshold; ops/csrc/
+    topk_codec.hip k_pk_*) is bitwise the oracle on both paths: the fast path (a tensor's
+    candidates number >= k and fit its list) and the full passes it falls back to when the
+    threshold moved too far -- down (too few candidates: the gradient shrank 1000x) or up (too
+    many: it grew back).  The counters record which path each tensor took."""
+    ops.require()
+    plan = _plan([20 * 25, 20, 50 * 500, 50, 8192 * 3 + 5, 2359296, 100003], ratio,
+                 bucket_offset=512)
+    lay = Layout.build(kind, plan, bits)
+    levels = 127 if bits == 8 else 7
+    dp = ops.DevicePlan(plan, DEV)
+    pay = torch.zeros(lay.nbytes, dtype=torch.uint8, device=DEV)
+    g0 = _grad(plan, seed=21)
+    noise = _grad(plan, seed=22) * 0.01
+    seq = [g0, g0 * 1.02 + noise, g0 * 1e-3, g0, g0 * 1.01 - noise]
+    big = [n > c for n, c in zip(plan.numels, plan.tensor_cap)]
+    T, nbig = plan.num_tensors, sum(big)
+    full_steps = {0, 2, 3}  # first encode (no prediction), shrink (too few), growth (too many)
+    for it, g in enumerate(seq):
+        key = stream_key(4, it, 2)
+        ref = oracle.encode_topk(g.clone(), plan, lay, levels, "max", key)
+        ops.topk_encode(dp, g.to(DEV), pay, lay, levels, "max", key)
+        assert torch.equal(pay.cpu(), ref), f"encode {it}: payload differs"
+    st = ops.topk_stats(dp)
+    assert st["lookback_errors"] == 0
+    assert st["full"] == nbig * len(full_steps)
+    assert st["fast"] == T * len(seq) - st["full"]
+    if ratio == 0.01:
+        assert nbig >= 3  # the fallback really ran
+
+
+def test_topk_predictive_encode_dgc_steady_state():
+    """Momentum-corrected error feedback over 8 steps (VGG's largest tensor among others): from
+    the second encode on every tensor takes the candidate path, and payload, residual and velocity
+    stay bitwise the oracle's."""
+    ops.require()
+    plan = _plan([1728, 64, 2359296, 512, 262144, 5120], 0.01, bucket_offset=64)
+    lay = Layout.build("topk_qsgd", plan, 8)
+    dp = ops.DevicePlan(plan, DEV)
+    pay = torch.zeros(lay.nbytes, dtype=torch.uint8, device=DEV)
+    r_ref, v_ref = torch.zeros(plan.length), torch.zeros(plan.length)
+    r_dev, v_dev = r_ref.to(DEV), v_ref.to(DEV)
+    hp = dict(momentum=0.9, dampening=0.0, nesterov=False, weight_decay=0.0)
+    for it in range(8):
+        g = _grad(plan, seed=60 + it)
+        key = stream_key(1, it, 0)
+        ref = oracle.encode_topk(g.clone(), plan, lay, 127, "max", key, residual=r_ref,
+                                 dgc=dict(velocity=v_ref, param=None, **hp))
+        ops.topk_encode(dp, g.to(DEV), pay, lay, 127, "max", key, resid=r_dev,
+                        dgc=dict(velocity=v_dev, param=None, **hp))
+        assert torch.equal(pay.cpu(), ref), f"step {it}: payload"
+        assert torch.equal(r_dev.cpu(), r_ref), f"step {it}: resid"
+        assert torch.equal(v_dev.cpu(), v_ref), f"step {it}: vel"
+    st = ops.topk_stats(dp)
+    big = sum(n > c for n, c in zip(plan.numels, plan.tensor_cap))
+    assert st["lookback_errors"] == 0 and st["full"] <= big + 2  # the first encode, a rare miss
+    assert st["fast"] >= 8 * plan.num_tensors - st["full"]
+
+
+@pytest.mark.parametrize("predict", ["1", "0"])
+def test_lookback_failure_is_reported(monkeypatch, predict):
+    """a write block that gives up on its decoupled look-back (bounded by polls, not
+    wall time) must not pass silently -- the counter reports it, and the exchange's health check
+    (read at every log record and by bench.py) raises."""
+    ops.require()
+    monkeypatch.setattr(ops, "_TOPK_PREDICT", predict == "1")
+    plan = _plan([8192 * 6, 100], 0.01)
+    lay = Layout.build("topk_qsgd", plan, 8)
+    dp = ops.DevicePlan(plan, DEV)
+    pay = torch.zeros(lay.nbytes, dtype=torch.uint8, device=DEV)
+    g = _grad(plan, seed=3).to(DEV)
+    ops.topk_encode(dp, g, pay, lay, 127, "max", 1)
+    assert ops.topk_stats(dp)["lookback_errors"] == 0
+    ops.set_lookback_fault(True)
+    try:
+        ops.topk_encode(dp, g, pay, lay, 127, "max", 2)
+        torch.cuda.synchronize()
+    finally:
+        ops.set_lookback_fault(False)
+    assert ops.topk_stats(dp)["lookback_errors"] == 5  # chunks 1..5 of the 6-chunk tensor
+
+    class _Ex:  # the exchange's check on a codec holding this plan
+        cuda = True
+
+        class codec:
+            kind, allreduce = "topk_qsgd", False
+            _bound = {0.01: (None, None, [dp])}
+
+    from ewdml.parallel.engine import GradientExchange
+
+    with pytest.raises(RuntimeError, match="look-back"):
+        GradientExchange.codec_health(_Ex)

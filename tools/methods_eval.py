@@ -10,7 +10,11 @@ server).  Top-k uses the report's K = 0.4 unless ``--ratio`` says otherwise.
 Measured per method (from the exchanges' byte counters, not from layouts):
   * bytes per iteration = sum over the 2 workers of (bytes pushed + bytes pulled), averaged over
     the run -- the report's "average communication cost per iteration" (BASELINE.md);
-  * held-out top-1 after the run, and the first evaluation step reaching --target.
+  * held-out top-1 after the run, and the first evaluation step reaching --target;
+  * communication and computation time per worker (``--phase-timing``: the step's timeline
+    partitioned into forward / backward / encode / collective / decode_update, the reference's
+    time_send / time_recieve / computation split, ``src/distributed_worker.py:130-155, 214-231``),
+    next to the report's "Communication and Computation Time" chart (VGG-11, minutes).
 
     python tools/methods_eval.py [--steps 1500] [--ratio 0.4] [--out RESULTS_methods.md]
 """
@@ -29,6 +33,10 @@ MNIST = os.path.join(ROOT, "tests", "fixtures", "mnist")
 MiB = float(1 << 20)
 PUBLISHED_MIB = [6.56, 4.1, 6.56, 1.64, 1.312, 0.066]  # LeNet, BASELINE.md / Comm Cost.png
 PUBLISHED_TOP1 = [98, 97, 97, 98, 96.5, 97]  # LeNet, Top1 Accuracy.png
+# VGG-11 communication / computation minutes per method (Report.zip: VGG11 Communication and
+# Computation Time .png); the report publishes no LeNet split
+PUBLISHED_VGG_COMM_MIN = [20, 17, 20, 16, 10, 5]
+PUBLISHED_VGG_COMP_MIN = [380, 382, 380, 383, 385, 381]
 
 
 def _free_port():
@@ -42,7 +50,8 @@ def _flags(method, ratio, steps):
          "--holdout-from-test", "1000", "--batch-size", "64", "--lr", "0.01", "--momentum", "0.9",
          "--eval-freq", "0", "--quiet", "--device", "cpu", "--amp", "none", "--method",
          str(method), "--topk-ratio", str(ratio), "--qsgd-norm", "l2", "--test-batch-size",
-         "1000", "--max-steps", str(steps), "--log-interval", "1000000"]
+         "1000", "--max-steps", str(steps), "--log-interval", "1000000", "--phase-timing",
+         "--no-error-feedback"]
     if method <= 5:
         f += ["--topology", "ps"]
     return f
@@ -64,13 +73,23 @@ def _worker(rank, world, port, method, ratio, steps, every, target, out):
         torch.manual_seed(0)
         tr = Trainer(ewdml.parse_args(_flags(method, ratio, steps)))
         worker = not getattr(tr, "is_server", False)
+        from ewdml.parallel.engine import Stopwatch
+
         sent = recv = 0
+        comm_ms = comp_ms = 0.0
+        phases = {}
         curve, reached = [], None
         for s in range(1, steps + 1):
             tr.train_step()
             st = tr.exchange.last
             sent += st.wire_bytes_sent
             recv += st.wire_bytes_recv
+            ph = tr.clock.phases()
+            for k, v in ph.items():
+                phases[k] = phases.get(k, 0.0) + v
+            c, p = Stopwatch.split(ph)
+            comm_ms += c
+            comp_ms += p
             if s % every == 0 or s == steps:
                 # every rank evaluates its replica (the server holds the model in PS methods)
                 top1 = tr.evaluate()["top1"]
@@ -78,7 +97,9 @@ def _worker(rank, world, port, method, ratio, steps, every, target, out):
                 if reached is None and top1 >= target:
                     reached = s
         res = {"rank": rank, "worker": worker, "sent": sent, "recv": recv, "steps": steps,
-               "curve": curve, "reached": reached, "top1": curve[-1][1]}
+               "curve": curve, "reached": reached, "top1": curve[-1][1],
+               "comm_s": comm_ms / 1e3, "compute_s": comp_ms / 1e3,
+               "phase_ms_per_step": {k: v / steps for k, v in phases.items()}}
         with open(os.path.join(out, f"r{rank}.json"), "w") as f:
             json.dump(res, f)
     finally:
@@ -100,9 +121,13 @@ def run_method(method, ratio, steps, every, target):
     per_iter = sum(r["sent"] + r["recv"] for r in workers) / steps
     # the model is the server's in PS methods, every rank's (identical or best-adopted) otherwise
     model = res[0] if method <= 5 else workers[0]
+    comm = sum(r["comm_s"] for r in workers) / len(workers)
+    comp = sum(r["compute_s"] for r in workers) / len(workers)
     return {"method": method, "ratio": ratio, "steps": steps, "world": world,
             "bytes_per_iter": per_iter, "MiB_per_iter": per_iter / MiB,
-            "top1": model["top1"], "reached": model["reached"], "curve": model["curve"]}
+            "top1": model["top1"], "reached": model["reached"], "curve": model["curve"],
+            "comm_s": comm, "compute_s": comp, "comm_frac": comm / max(comm + comp, 1e-12),
+            "worker_phase_ms": workers[0]["phase_ms_per_step"]}
 
 
 def main(argv=None):
@@ -153,6 +178,31 @@ def main(argv=None):
             lines.append(f"| {m} | {r['MiB_per_iter']:.4f} | {static[m - 1]:.4f} | "
                          f"{PUBLISHED_MIB[m - 1]} | {r['top1']:.1f} | {PUBLISHED_TOP1[m - 1]} | "
                          f"{r['reached'] if r['reached'] else '-'} |")
+        lines += [
+            "",
+            "## Communication vs computation time (per worker, measured with `--phase-timing`)",
+            "",
+            "Mean over the workers of the summed phase times of the run (exposed communication = "
+            "the collective phases: gather / broadcast / all-gather and the waits for them; "
+            "computation = forward, backward, encode, the server-side aggregate seen as wait by "
+            "the workers excluded, decode + update).  The report charts the same split for VGG-11 "
+            "trained to convergence on CPUs (minutes); its communication share is the comparable "
+            "figure.",
+            "",
+            "| Method | comm s | compute s | comm share % | ms/step: forward / backward / "
+            "encode / collective / decode+update | report VGG-11 comm / compute min | report "
+            "comm share % |",
+            "|---|---|---|---|---|---|---|",
+        ]
+        for r in rows:
+            m = r["method"]
+            ph = r["worker_phase_ms"]
+            pc, pp = PUBLISHED_VGG_COMM_MIN[m - 1], PUBLISHED_VGG_COMP_MIN[m - 1]
+            split = " / ".join(f"{ph.get(k, 0.0):.2f}" for k in
+                               ("forward", "backward", "encode", "collective", "decode_update"))
+            lines.append(f"| {m} | {r['comm_s']:.2f} | {r['compute_s']:.2f} | "
+                         f"{100 * r['comm_frac']:.1f} | {split} | {pc} / {pp} | "
+                         f"{100 * pc / (pc + pp):.1f} |")
         lines += [
             "",
             "Notes on the byte column:",
