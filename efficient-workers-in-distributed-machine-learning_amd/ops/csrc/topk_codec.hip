@@ -902,6 +902,23 @@ __global__ __launch_bounds__(EW_BLOCK) void k_pk_hist0(
     const uint32_t fast = M >= (uint32_t)tr.k && M <= (uint32_t)tr.cap;
     pst[c.tensor * 8 + 2] = M;
     pst[c.tensor * 8 + 3] = fast;
+    // digit geometry of the radix passes (pk_select): relative to P over the candidates, the
+    // key's own bits on the full passes
+    uint32_t B = 0u, s0 = 20u, s1 = 10u;
+    if (fast) {
+      uint32_t kmax = 0;
+      for (int r = 0; r < NREP; ++r)
+        kmax = max(kmax, __hip_atomic_load(kmaxr + r * T + c.tensor, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT));
+      B = P;
+      const uint32_t span = kmax - P;  // >= 0: M >= k >= 1 candidates are >= P
+      const int bl = span ? 32 - __clz(span) : 0;
+      s0 = bl > 11 ? (uint32_t)(bl - 11) : 0u;
+      s1 = s0 > 10 ? s0 - 10 : 0u;
+    }
+    pst[c.tensor * 8 + 5] = B;
+    pst[c.tensor * 8 + 6] = s0;
+    pst[c.tensor * 8 + 7] = s1;
     atomicAdd(stats + (fast ? 0 : 1), 1);
   }
 }
@@ -915,10 +932,21 @@ __device__ __forceinline__ void pk_visit(const GradPtrs& gp, const float* flat,
                                          int j, bool fast, uint32_t M,
                                          const uint2* __restrict__ pcand, F&& f) {
   if (fast) {
-    const uint2* src = pcand + tr.cap0;
+    // all of this thread's candidate loads in flight before the first use (a load -> atomic
+    // loop leaves one round trip per iteration exposed)
+    constexpr int R = EW_CHUNK / EW_BLOCK;
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(pcand + tr.cap0);
+    const uint32_t i0 = (uint32_t)j * EW_CHUNK + threadIdx.x;
     const uint32_t i1 = min(M, (uint32_t)(j + 1) * EW_CHUNK);
-    for (uint32_t i = (uint32_t)j * EW_CHUNK + threadIdx.x; i < i1; i += EW_BLOCK)
-      f(src[i].x & 0x7fffffffu);
+    uint32_t kv[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const uint32_t i = i0 + r * EW_BLOCK;
+      kv[r] = i < i1 ? src[2 * i] : 0u;
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+      if (i0 + r * EW_BLOCK < i1) f(kv[r] & 0x7fffffffu);
     return;
   }
   for (int lc = j; lc < tr.nchunks; lc += tr.ncb) {
@@ -945,7 +973,58 @@ __device__ __forceinline__ void pk_append(bool pred, uint32_t key, int* counter,
   if (pred) dst[base + __popcll(m & ((1ull << lane) - 1ull))] = key;
 }
 
-// Radix pass 0 (key bits [30:20]) over the candidates (fast) or the tensor (full).
+// Radix select over a tensor's keys in *relative* digits: rel = key - B, digit 0 = rel >> s0
+// (< 2048), digit 1 = the next s0 - s1 bits, digit 2 = the last s1 bits (s0 <= 20, s1 <= 10).  The
+// full passes use B = 0, s0 = 20, s1 = 10 (the key's bits [30:20], [19:10], [9:0]); the candidate
+// passes use B = the predicted bound P and s0 = bit length of (max key - P) - 11, so the keys
+// between P and the max spread over all 2048 pass-0 bins instead of the few bins of their
+// exponent (an LDS-atomic hot spot).  pst[8 t + 5..7] = B, s0, s1 (set by k_pk_hist0).
+// Tensor t's digit holding its k_rem-th largest key (run by one block); state[4 t] holds the
+// relative prefix until pass 2 turns it into the absolute threshold key.
+template <int NB, bool FIRST>
+__device__ __forceinline__ void pk_select(const uint32_t* __restrict__ hist,
+                                          const TensorRow* __restrict__ tensors,
+                                          uint32_t* __restrict__ state,
+                                          const uint32_t* __restrict__ kmaxr, int T, int t,
+                                          uint32_t shift) {
+  constexpr int PER = NB / EW_BLOCK;
+  __shared__ uint32_t ws[EW_WAVES];
+  const uint32_t k_rem = FIRST ? (uint32_t)tensors[t].k : state[t * 4 + 1];
+  const uint32_t prefix = FIRST ? 0u : state[t * 4 + 0];
+  uint32_t cnt[PER];
+  uint32_t tsum = 0;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) cnt[j] = 0;
+  {  // the candidate passes use one histogram copy (<= ncb blocks per tensor add to it)
+    const uint32_t* ht = hist + (size_t)t * NB;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) cnt[j] = ht[NB - 1 - (threadIdx.x * PER + j)];
+  }
+#pragma unroll
+  for (int j = 0; j < PER; ++j) tsum += cnt[j];
+  if (FIRST && threadIdx.x == 0) {
+    uint32_t m = 0;
+    for (int r = 0; r < NREP; ++r) m = max(m, kmaxr[r * T + t]);
+    state[t * 4 + 2] = m;
+  }
+  uint32_t total;
+  const uint32_t excl = ew_block_excl_scan(tsum, ws, total);
+  if (excl < k_rem && k_rem <= excl + tsum) {
+    uint32_t run = excl;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      if (run + cnt[j] >= k_rem) {
+        const uint32_t bin = NB - 1 - (threadIdx.x * PER + j);
+        state[t * 4 + 0] = prefix | (bin << shift);
+        state[t * 4 + 1] = k_rem - run;
+        break;
+      }
+      run += cnt[j];
+    }
+  }
+}
+
+// Radix pass 0 over the candidates (fast) or the tensor (full).
 __global__ __launch_bounds__(EW_BLOCK) void k_pk_pass0(
     GradPtrs gp, const float* __restrict__ flat, const ChunkRow* __restrict__ chunks,
     const CBlockRow* __restrict__ cblocks, const TensorRow* __restrict__ tensors,
@@ -959,10 +1038,11 @@ __global__ __launch_bounds__(EW_BLOCK) void k_pk_pass0(
   const CBlockRow cb = cblocks[blockIdx.x];
   const int t = cb.tensor;
   const TensorRow tr = tensors[t];
+  const uint32_t B = pst[t * 8 + 5], s0 = pst[t * 8 + 6];
   pk_visit(gp, flat, chunks, tr, cb.j, pst[t * 8 + 3] != 0, pst[t * 8 + 2], pcand,
-           [&](uint32_t k) { atomicAdd(&h[(k >> 20) * HSUB], 1u); });
+           [&](uint32_t k) { atomicAdd(&h[((k - B) >> s0) * HSUB], 1u); });
   __syncthreads();
-  uint32_t* dst = hist + ((size_t)(blockIdx.x & (NREP - 1)) * T + t) * NB0;
+  uint32_t* dst = hist + (size_t)t * NB0;
   for (int i = threadIdx.x; i < NB0; i += EW_BLOCK) {
     uint32_t x = 0;
 #pragma unroll
@@ -970,11 +1050,12 @@ __global__ __launch_bounds__(EW_BLOCK) void k_pk_pass0(
     if (x) atomicAdd(&dst[i], x);
   }
   if (topk_tensor_last(tick + TICK_STRIDE * t, tr.ncb, reinterpret_cast<int*>(hs)))
-    topk_select<NB0, 20, true>(hist, tensors, state, kmaxr, T, t);
+    pk_select<NB0, true>(hist, tensors, state, kmaxr, T, t, s0);
 }
 
-// Radix pass 1 (bits [19:10]) over the keys in the selected top digit, which are also appended to
-// the tensor's key list cand[tensor.off ..) for pass 2.
+// Radix pass 1 over the keys in the selected digit 0; they are also appended to the tensor's key
+// list cand[tensor.off ..) for pass 2 (fast path: one atomic per block, order within a block
+// kept; full path: one per wave).
 __global__ __launch_bounds__(EW_BLOCK) void k_pk_pass1(
     GradPtrs gp, const float* __restrict__ flat, const ChunkRow* __restrict__ chunks,
     const CBlockRow* __restrict__ cblocks, const TensorRow* __restrict__ tensors,
@@ -982,30 +1063,69 @@ __global__ __launch_bounds__(EW_BLOCK) void k_pk_pass1(
     const uint32_t* __restrict__ kmaxr, uint32_t* __restrict__ state, int T, int* __restrict__ tick,
     uint32_t* __restrict__ cand, int* __restrict__ cand_n) {
   __shared__ uint32_t h[NB1];
+  __shared__ uint32_t ws[EW_WAVES];
+  __shared__ uint32_t s_base;
   for (int i = threadIdx.x; i < NB1; i += EW_BLOCK) h[i] = 0;
   __syncthreads();
   const CBlockRow cb = cblocks[blockIdx.x];
   const int t = cb.tensor;
   const TensorRow tr = tensors[t];
-  const uint32_t want = state[t * 4] >> 20;
+  const uint32_t B = pst[t * 8 + 5], s0 = pst[t * 8 + 6], s1 = pst[t * 8 + 7];
+  const uint32_t want = state[t * 4] >> s0;
+  const uint32_t dmask = (1u << (s0 - s1)) - 1u;
   int* cn = cand_n + TICK_STRIDE * t;
   uint32_t* cdst = cand + tr.off;
-  pk_visit(gp, flat, chunks, tr, cb.j, pst[t * 8 + 3] != 0, pst[t * 8 + 2], pcand,
-           [&](uint32_t k) {
-             const bool m = (k >> 20) == want;
-             if (m) atomicAdd(&h[(k >> 10) & (NB1 - 1)], 1u);
-             pk_append(m, k, cn, cdst);
-           });
+  const bool fast = pst[t * 8 + 3] != 0;
+  if (fast) {
+    constexpr int R = EW_CHUNK / EW_BLOCK;
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(pcand + tr.cap0);
+    const uint32_t M = pst[t * 8 + 2];
+    const uint32_t i0 = (uint32_t)cb.j * EW_CHUNK + threadIdx.x;
+    const uint32_t i1 = min(M, (uint32_t)cb.j * EW_CHUNK + EW_CHUNK);
+    uint32_t kv[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const uint32_t i = i0 + r * EW_BLOCK;
+      kv[r] = i < i1 ? (src[2 * i] & 0x7fffffffu) : 0u;
+    }
+    uint32_t nm = 0, mbits = 0;  // matches of this thread (bit r: kv[r] matched)
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const uint32_t rel = kv[r] - B;
+      if (i0 + r * EW_BLOCK < i1 && (rel >> s0) == want) {
+        atomicAdd(&h[(rel >> s1) & dmask], 1u);
+        ++nm;
+        mbits |= 1u << r;
+      }
+    }
+    uint32_t tot;
+    const uint32_t ex = ew_block_excl_scan(nm, ws, tot);
+    if (threadIdx.x == 0) s_base = tot ? (uint32_t)atomicAdd(cn, (int)tot) : 0u;
+    __syncthreads();
+    if (nm) {
+      uint32_t pos = s_base + ex;
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        if ((mbits >> r) & 1u) cdst[pos++] = kv[r];
+    }
+  } else {
+    pk_visit(gp, flat, chunks, tr, cb.j, false, 0u, pcand, [&](uint32_t k) {
+      const uint32_t rel = k - B;
+      const bool m = (rel >> s0) == want;
+      if (m) atomicAdd(&h[(rel >> s1) & dmask], 1u);
+      pk_append(m, k, cn, cdst);
+    });
+  }
   __syncthreads();
-  uint32_t* dst = hist + ((size_t)(blockIdx.x & (NREP - 1)) * T + t) * NB1;
+  uint32_t* dst = hist + (size_t)t * NB1;
   for (int i = threadIdx.x; i < NB1; i += EW_BLOCK)
     if (h[i]) atomicAdd(&dst[i], h[i]);
   if (topk_tensor_last(tick + TICK_STRIDE * t, tr.ncb, reinterpret_cast<int*>(h)))
-    topk_select<NB1, 10, false>(hist, tensors, state, kmaxr, T, t);
+    pk_select<NB1, false>(hist, tensors, state, kmaxr, T, t, s1);
 }
 
-// Radix pass 2 (bits [9:0]) over the pass-1 keys; the tensor's last block fixes the exact
-// threshold and the ties, then predicts the next encode's candidate bound.
+// Radix pass 2 over the pass-1 keys; the tensor's last block fixes the exact threshold (absolute
+// key) and the ties, then predicts the next encode's candidate bound.
 __global__ __launch_bounds__(EW_BLOCK) void k_pk_pass2(
     const CBlockRow* __restrict__ cblocks, const TensorRow* __restrict__ tensors,
     uint32_t* __restrict__ pst, uint32_t* __restrict__ hist, const uint32_t* __restrict__ kmaxr,
@@ -1019,30 +1139,41 @@ __global__ __launch_bounds__(EW_BLOCK) void k_pk_pass2(
   const TensorRow tr = tensors[t];
   const uint32_t n = (uint32_t)__hip_atomic_load(cand_n + TICK_STRIDE * t, __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_AGENT);
-  const uint32_t want = state[t * 4] >> 10;
+  const uint32_t B = pst[t * 8 + 5], s1 = pst[t * 8 + 7];
+  const uint32_t want = state[t * 4] >> s1;
+  const uint32_t dmask = (1u << s1) - 1u;
   const uint32_t* src = cand + tr.off;
   const uint32_t stride = (uint32_t)tr.ncb * EW_CHUNK;
+  constexpr int R = EW_CHUNK / EW_BLOCK;
   for (uint32_t b0 = (uint32_t)cb.j * EW_CHUNK; b0 < n; b0 += stride) {
-    const uint32_t i1 = min(n, b0 + EW_CHUNK);
-    for (uint32_t i = b0 + threadIdx.x; i < i1; i += EW_BLOCK) {
-      const uint32_t k = src[i];
-      if ((k >> 10) == want) atomicAdd(&h[k & (NB2 - 1)], 1u);
+    const uint32_t i0 = b0 + threadIdx.x, i1 = min(n, b0 + EW_CHUNK);
+    uint32_t kv[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const uint32_t i = i0 + r * EW_BLOCK;
+      kv[r] = i < i1 ? src[i] : 0u;
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const uint32_t rel = kv[r] - B;
+      if (i0 + r * EW_BLOCK < i1 && (rel >> s1) == want) atomicAdd(&h[rel & dmask], 1u);
     }
   }
   __syncthreads();
-  uint32_t* dst = hist + ((size_t)(blockIdx.x & (NREP - 1)) * T + t) * NB2;
+  uint32_t* dst = hist + (size_t)t * NB2;
   for (int i = threadIdx.x; i < NB2; i += EW_BLOCK)
     if (h[i]) atomicAdd(&dst[i], h[i]);
   if (topk_tensor_last(tick + TICK_STRIDE * t, tr.ncb, reinterpret_cast<int*>(h))) {
-    topk_select<NB2, 0, false>(hist, tensors, state, kmaxr, T, t);
+    pk_select<NB2, false>(hist, tensors, state, kmaxr, T, t, 0u);
     __syncthreads();
     if (threadIdx.x == 0) {
       cand_n[TICK_STRIDE * t] = 0;  // every block read n before it arrived
+      // written by this block's select just now (agent-scope load: not a stale L1 line)
+      const uint32_t thr = B + __hip_atomic_load(state + t * 4, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(state + t * 4, thr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       // next encode's candidate bound: beta x this exact threshold, beta steered so the
       // candidates stay between ~2k and 3/4 of the list
-      // written by this block's select just now (agent-scope load: not a stale L1 line)
-      const uint32_t thr = __hip_atomic_load(state + t * 4, __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT);
       const uint32_t M = pst[t * 8 + 2], fast = pst[t * 8 + 3], had = pst[t * 8 + 4];
       float beta = __uint_as_float(pst[t * 8 + 1]);
       if (!(beta > 0.0f)) beta = PK_BETA0;

@@ -532,6 +532,9 @@ class Trainer:
         try:  # the counters come back on the failure path too (eager fallback stays in step)
             if self.graph_mode == "full":
                 g = torch.cuda.CUDAGraph()
+                dump = os.environ.get("EWDML_GRAPH_DUMP")  # DOT file of the captured step
+                if dump:
+                    g.enable_debug_mode()
                 with torch.cuda.graph(g, stream=self.gstream, capture_error_mode=mode):
                     try:
                         if self._in_graph_batch:
@@ -541,6 +544,8 @@ class Trainer:
                     except BaseException:
                         self._rejoin_side()
                         raise
+                if dump:
+                    g.debug_dump(dump)
                 self._graphs = (g,)
             elif self.graph_mode == "segmented":
                 seg = SegmentedCapture(self.gstream, ex.comm_stream, mode="relaxed",
