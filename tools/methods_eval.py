@@ -183,9 +183,10 @@ def main(argv=None):
             "## Communication vs computation time (per worker, measured with `--phase-timing`)",
             "",
             "Mean over the workers of the summed phase times of the run (exposed communication = "
-            "the collective phases: gather / broadcast / all-gather and the waits for them; "
-            "computation = forward, backward, encode, the server-side aggregate seen as wait by "
-            "the workers excluded, decode + update).  The report charts the same split for VGG-11 "
+            "the collective phases: gather / broadcast / all-gather and the waits for them -- "
+            "in the parameter-server methods that wait includes the server's decode / average / "
+            "re-encode of the pull, as the reference's fetch time did; computation = forward, "
+            "backward, encode, decode + update).  The report charts the same split for VGG-11 "
             "trained to convergence on CPUs (minutes); its communication share is the comparable "
             "figure.",
             "",
