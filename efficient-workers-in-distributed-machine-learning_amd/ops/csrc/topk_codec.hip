@@ -25,6 +25,8 @@
 // share by a decoupled look-back over the tensor's earlier chunks instead of a count pass.
 // The global state lives in one scratch block: zero-initialised once, histograms re-cleared by
 // k_topk_write after use, everything else fully rewritten per encode (no per-step memset).
+#include <cstdlib>
+
 #include "common.h"
 #include "ewdml_ops.h"
 
@@ -970,7 +972,9 @@ __device__ __forceinline__ void pk_append(bool pred, uint32_t key, int* counter,
   uint32_t base = 0;
   if (lane == leader) base = (uint32_t)atomicAdd(counter, __popcll(m));
   base = __shfl(base, leader, 64);
-  if (pred) dst[base + __popcll(m & ((1ull << lane) - 1ull))] = key;
+  if (pred)  // agent scope: read by other blocks of the fused select kernel
+    __hip_atomic_store(dst + base + __popcll(m & ((1ull << lane) - 1ull)), key, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Radix select over a tensor's keys in *relative* digits: rel = key - B, digit 0 = rel >> s0
@@ -989,8 +993,14 @@ __device__ __forceinline__ void pk_select(const uint32_t* __restrict__ hist,
                                           uint32_t shift) {
   constexpr int PER = NB / EW_BLOCK;
   __shared__ uint32_t ws[EW_WAVES];
-  const uint32_t k_rem = FIRST ? (uint32_t)tensors[t].k : state[t * 4 + 1];
-  const uint32_t prefix = FIRST ? 0u : state[t * 4 + 0];
+  // state is handed between the blocks of the fused select kernel (other XCDs): agent-scope
+  // (L2-coherent) loads and stores
+  const uint32_t k_rem = FIRST ? (uint32_t)tensors[t].k
+                               : __hip_atomic_load(state + t * 4 + 1, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t prefix = FIRST ? 0u
+                                : __hip_atomic_load(state + t * 4, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
   uint32_t cnt[PER];
   uint32_t tsum = 0;
 #pragma unroll
@@ -1005,7 +1015,7 @@ __device__ __forceinline__ void pk_select(const uint32_t* __restrict__ hist,
   if (FIRST && threadIdx.x == 0) {
     uint32_t m = 0;
     for (int r = 0; r < NREP; ++r) m = max(m, kmaxr[r * T + t]);
-    state[t * 4 + 2] = m;
+    __hip_atomic_store(state + t * 4 + 2, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   uint32_t total;
   const uint32_t excl = ew_block_excl_scan(tsum, ws, total);
@@ -1015,13 +1025,44 @@ __device__ __forceinline__ void pk_select(const uint32_t* __restrict__ hist,
     for (int j = 0; j < PER; ++j) {
       if (run + cnt[j] >= k_rem) {
         const uint32_t bin = NB - 1 - (threadIdx.x * PER + j);
-        state[t * 4 + 0] = prefix | (bin << shift);
-        state[t * 4 + 1] = k_rem - run;
+        __hip_atomic_store(state + t * 4, prefix | (bin << shift), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(state + t * 4 + 1, k_rem - run, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
       run += cnt[j];
     }
   }
+}
+
+// Tensor t's pass-2 tail (one thread): the exact threshold as an absolute key, the reset of the
+// pass-1 key count, and the next encode's candidate bound: beta x this threshold, beta steered so
+// the candidates stay between ~2k and 3/4 of the list.
+__device__ __forceinline__ void pk_predict(const TensorRow& tr, int t, uint32_t B,
+                                           uint32_t* __restrict__ state, uint32_t* __restrict__ pst,
+                                           int* __restrict__ cand_n) {
+  cand_n[TICK_STRIDE * t] = 0;  // every block read n before it arrived
+  // written by this block's select just now (agent-scope load: not a stale L1 line)
+  const uint32_t thr = B + __hip_atomic_load(state + t * 4, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(state + t * 4, thr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // next encode's candidate bound: beta x this exact threshold, beta steered so the
+  // candidates stay between ~2k and 3/4 of the list
+  const uint32_t M = pst[t * 8 + 2], fast = pst[t * 8 + 3], had = pst[t * 8 + 4];
+  float beta = __uint_as_float(pst[t * 8 + 1]);
+  if (!(beta > 0.0f)) beta = PK_BETA0;
+  const uint32_t k = (uint32_t)tr.k, cap = (uint32_t)tr.cap;
+  if (had) {
+    if (!fast && M > cap) beta = beta + (1.0f - beta) * 0.5f;  // too many: tighter
+    else if (!fast) beta = beta * 0.8f;                        // too few: the bound was above
+    else if (M > cap - cap / 4) beta = beta + (1.0f - beta) * 0.25f;
+    else if (M < 2u * k) beta = beta * 0.95f;
+  }
+  beta = fminf(fmaxf(beta, 0.25f), 0.99f);
+  pst[t * 8 + 1] = __float_as_uint(beta);
+  pst[t * 8 + 0] = ew_key(__uint_as_float(thr) * beta);
+  pst[t * 8 + 4] = 1u;
 }
 
 // Radix pass 0 over the candidates (fast) or the tensor (full).
@@ -1167,28 +1208,221 @@ __global__ __launch_bounds__(EW_BLOCK) void k_pk_pass2(
     pk_select<NB2, false>(hist, tensors, state, kmaxr, T, t, 0u);
     __syncthreads();
     if (threadIdx.x == 0) {
-      cand_n[TICK_STRIDE * t] = 0;  // every block read n before it arrived
-      // written by this block's select just now (agent-scope load: not a stale L1 line)
-      const uint32_t thr = B + __hip_atomic_load(state + t * 4, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(state + t * 4, thr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      // next encode's candidate bound: beta x this exact threshold, beta steered so the
-      // candidates stay between ~2k and 3/4 of the list
-      const uint32_t M = pst[t * 8 + 2], fast = pst[t * 8 + 3], had = pst[t * 8 + 4];
-      float beta = __uint_as_float(pst[t * 8 + 1]);
-      if (!(beta > 0.0f)) beta = PK_BETA0;
-      const uint32_t k = (uint32_t)tr.k, cap = (uint32_t)tr.cap;
-      if (had) {
-        if (!fast && M > cap) beta = beta + (1.0f - beta) * 0.5f;  // too many: tighter
-        else if (!fast) beta = beta * 0.8f;                        // too few: the bound was above
-        else if (M > cap - cap / 4) beta = beta + (1.0f - beta) * 0.25f;
-        else if (M < 2u * k) beta = beta * 0.95f;
-      }
-      beta = fminf(fmaxf(beta, 0.25f), 0.99f);
-      pst[t * 8 + 1] = __float_as_uint(beta);
-      pst[t * 8 + 0] = ew_key(__uint_as_float(thr) * beta);
-      pst[t * 8 + 4] = 1u;
+      pk_predict(tr, t, B, state, pst, cand_n);
     }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// The three radix passes as ONE launch: a tensor's candidate-pass blocks (<= 24 for VGG-11's
+// largest) meet at a per-tensor barrier between passes instead of at kernel boundaries -- each
+// pass kernel cost ~8-15 us of which little was work (a chain of dependent round trips: block
+// row, tensor row, data, histogram flush, ticket, select).  Valid only when every block of the
+// grid is resident at once (the host launches it when the grid is at most one block per CU;
+// otherwise the three kernels above).  The barrier: the pass's last arriver runs the select and
+// then publishes a per-tensor generation word the others wait on (bounded poll; a timeout bumps
+// the look-back error counter, which the health check turns into a failure).
+// ---------------------------------------------------------------------------------------------
+constexpr uint32_t PK_MAX_POLLS = 1u << 20;
+
+// Everything handed across the barrier is written with device-coherent operations (histogram
+// atomics, agent-scope stores of the select state and the pass-1 keys) and every wave drains its
+// memory operations (vmcnt) before the block arrives, so no release fence (a write-back of the
+// XCD's L2) is needed; a block that proceeds past a barrier takes an agent acquire (cdna
+// guideline 16, as topk_tensor_last).
+// block-uniform: true in the pass's last-arriving block of tensor t
+__device__ __forceinline__ bool pk_arrive(int* arrive, int ncb, int* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's flushes and appends landed
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int prev = __hip_atomic_fetch_add(arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = prev == ncb - 1;
+    if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    *flag = last;
+  }
+  __syncthreads();
+  return *flag != 0;
+}
+
+// the last arriver, after its select: reset the arrive count, publish generation `g`
+__device__ __forceinline__ void pk_publish(int* arrive, uint32_t* gen, uint32_t g) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's select stores landed
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(arrive, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(gen, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// everyone else: wait for generation g, block-uniform
+__device__ __forceinline__ void pk_wait(const uint32_t* gen, uint32_t g, int* err) {
+  if (threadIdx.x == 0) {
+    uint32_t polls = 0;
+    while ((int)(__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - g) < 0) {
+      if (++polls > PK_MAX_POLLS) {
+        atomicAdd(err, 1);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(8);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(EW_BLOCK) void k_pk_select(
+    GradPtrs gp, const float* __restrict__ flat, const ChunkRow* __restrict__ chunks,
+    const CBlockRow* __restrict__ cblocks, const TensorRow* __restrict__ tensors,
+    uint32_t* __restrict__ pst, const uint2* __restrict__ pcand, uint32_t* __restrict__ hist0,
+    uint32_t* __restrict__ hist1, uint32_t* __restrict__ hist2, const uint32_t* __restrict__ kmaxr,
+    uint32_t* __restrict__ state, int T, int* __restrict__ arrive, uint32_t* __restrict__ gen,
+    uint32_t* __restrict__ cand, int* __restrict__ cand_n, int* __restrict__ err) {
+  constexpr int HSUB = 4;
+  constexpr int R = EW_CHUNK / EW_BLOCK;
+  __shared__ uint32_t hs[NB0 * HSUB];
+  __shared__ uint32_t ws[EW_WAVES];
+  __shared__ uint32_t s_base;
+  __shared__ int s_flag;
+  const CBlockRow cb = cblocks[blockIdx.x];
+  const int t = cb.tensor;
+  const TensorRow tr = tensors[t];
+  int* arr = arrive + TICK_STRIDE * t;
+  uint32_t* gn = gen + TICK_STRIDE * t;
+  // every block reads the generation before its first arrival; it moves only after all arrived
+  const uint32_t g0 = __hip_atomic_load(gn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const bool fast = pst[t * 8 + 3] != 0;
+  const uint32_t M = pst[t * 8 + 2];
+  const uint32_t B = pst[t * 8 + 5], s0 = pst[t * 8 + 6], s1 = pst[t * 8 + 7];
+  // this block's candidates (fast path), loaded once for passes 0 and 1
+  const uint32_t i0 = (uint32_t)cb.j * EW_CHUNK + threadIdx.x;
+  const uint32_t i1 = min(M, (uint32_t)cb.j * EW_CHUNK + EW_CHUNK);
+  uint32_t kv[R];
+  if (fast) {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(pcand + tr.cap0);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const uint32_t i = i0 + r * EW_BLOCK;
+      kv[r] = i < i1 ? (src[2 * i] & 0x7fffffffu) : 0u;
+    }
+  }
+  // ---- pass 0: digit (key - B) >> s0 ----
+  for (int i = threadIdx.x; i < NB0 * HSUB; i += EW_BLOCK) hs[i] = 0;
+  __syncthreads();
+  {
+    uint32_t* h = hs + (threadIdx.x & (HSUB - 1));
+    if (fast) {
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        if (i0 + r * EW_BLOCK < i1) atomicAdd(&h[((kv[r] - B) >> s0) * HSUB], 1u);
+    } else {
+      pk_visit(gp, flat, chunks, tr, cb.j, false, 0u, pcand,
+               [&](uint32_t k) { atomicAdd(&h[((k - B) >> s0) * HSUB], 1u); });
+    }
+  }
+  __syncthreads();
+  {
+    uint32_t* dst = hist0 + (size_t)t * NB0;
+    for (int i = threadIdx.x; i < NB0; i += EW_BLOCK) {
+      uint32_t x = 0;
+#pragma unroll
+      for (int q = 0; q < HSUB; ++q) x += hs[i * HSUB + q];
+      if (x) atomicAdd(&dst[i], x);
+    }
+  }
+  if (pk_arrive(arr, tr.ncb, &s_flag)) {
+    pk_select<NB0, true>(hist0, tensors, state, kmaxr, T, t, s0);
+    pk_publish(arr, gn, g0 + 1u);
+  } else {
+    pk_wait(gn, g0 + 1u, err);
+  }
+  // ---- pass 1: next s0 - s1 bits of the keys in the selected digit 0; those keys -> cand ----
+  {
+    const uint32_t want = __hip_atomic_load(state + t * 4, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT) >> s0;
+    const uint32_t dmask = (1u << (s0 - s1)) - 1u;
+    int* cn = cand_n + TICK_STRIDE * t;
+    uint32_t* cdst = cand + tr.off;
+    uint32_t* h = hs;
+    for (int i = threadIdx.x; i < NB1; i += EW_BLOCK) h[i] = 0;
+    __syncthreads();
+    if (fast) {
+      uint32_t nm = 0, mbits = 0;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const uint32_t rel = kv[r] - B;
+        if (i0 + r * EW_BLOCK < i1 && (rel >> s0) == want) {
+          atomicAdd(&h[(rel >> s1) & dmask], 1u);
+          ++nm;
+          mbits |= 1u << r;
+        }
+      }
+      uint32_t tot;
+      const uint32_t ex = ew_block_excl_scan(nm, ws, tot);
+      if (threadIdx.x == 0) s_base = tot ? (uint32_t)atomicAdd(cn, (int)tot) : 0u;
+      __syncthreads();
+      if (nm) {
+        uint32_t pos = s_base + ex;
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+          if ((mbits >> r) & 1u)
+            __hip_atomic_store(cdst + pos++, kv[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    } else {
+      pk_visit(gp, flat, chunks, tr, cb.j, false, 0u, pcand, [&](uint32_t k) {
+        const uint32_t rel = k - B;
+        const bool m = (rel >> s0) == want;
+        if (m) atomicAdd(&h[(rel >> s1) & dmask], 1u);
+        pk_append(m, k, cn, cdst);
+      });
+    }
+    __syncthreads();
+    uint32_t* dst = hist1 + (size_t)t * NB1;
+    for (int i = threadIdx.x; i < NB1; i += EW_BLOCK)
+      if (h[i]) atomicAdd(&dst[i], h[i]);
+  }
+  if (pk_arrive(arr, tr.ncb, &s_flag)) {
+    pk_select<NB1, false>(hist1, tensors, state, kmaxr, T, t, s1);
+    pk_publish(arr, gn, g0 + 2u);
+  } else {
+    pk_wait(gn, g0 + 2u, err);
+  }
+  // ---- pass 2: the last s1 bits over the pass-1 keys ----
+  {
+    const uint32_t n = (uint32_t)__hip_atomic_load(cand_n + TICK_STRIDE * t, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t want = __hip_atomic_load(state + t * 4, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT) >> s1;
+    const uint32_t dmask = (1u << s1) - 1u;
+    const uint32_t* src = cand + tr.off;
+    const uint32_t stride = (uint32_t)tr.ncb * EW_CHUNK;
+    uint32_t* h = hs;
+    for (int i = threadIdx.x; i < NB2; i += EW_BLOCK) h[i] = 0;
+    __syncthreads();
+    for (uint32_t b0 = (uint32_t)cb.j * EW_CHUNK; b0 < n; b0 += stride) {
+      const uint32_t j0 = b0 + threadIdx.x, j1 = min(n, b0 + EW_CHUNK);
+      uint32_t kk[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const uint32_t i = j0 + r * EW_BLOCK;
+        kk[r] = i < j1 ? __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                       : 0u;
+      }
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const uint32_t rel = kk[r] - B;
+        if (j0 + r * EW_BLOCK < j1 && (rel >> s1) == want) atomicAdd(&h[rel & dmask], 1u);
+      }
+    }
+    __syncthreads();
+    uint32_t* dst = hist2 + (size_t)t * NB2;
+    for (int i = threadIdx.x; i < NB2; i += EW_BLOCK)
+      if (h[i]) atomicAdd(&dst[i], h[i]);
+  }
+  if (pk_arrive(arr, tr.ncb, &s_flag)) {
+    pk_select<NB2, false>(hist2, tensors, state, kmaxr, T, t, 0u);
+    __syncthreads();
+    if (threadIdx.x == 0) pk_predict(tr, t, B, state, pst, cand_n);
+    pk_publish(arr, gn, g0 + 3u);
   }
 }
 
@@ -1338,6 +1572,21 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_decode_apply(
 #define EW_LAUNCH(kern, grid, stream, ...) \
   hipLaunchKernelGGL(kern, dim3(grid), dim3(EW_BLOCK), 0, (hipStream_t)(stream), __VA_ARGS__)
 
+// Largest candidate-pass grid launched as the fused select kernel: one block per CU, so every
+// block is resident at once whatever else shares the GPU (its barriers wait for peers of the
+// same launch).  EWDML_TOPK_FUSED_SELECT=0: always the three pass kernels.
+static int ew_pk_fused_max_blocks() {
+  static int n = -1;
+  if (n < 0) {
+    const char* e = std::getenv("EWDML_TOPK_FUSED_SELECT");
+    int dev = 0, cus = 0;
+    EW_CHECK(hipGetDevice(&dev));
+    EW_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    n = (e && e[0] == '0') ? 0 : cus;
+  }
+  return n;
+}
+
 void ew_topk_encode(const TopkEncodeArgs& a) {
   auto* chunks = reinterpret_cast<const ChunkRow*>(a.chunks);
   auto* tensors = reinterpret_cast<const TensorRow*>(a.tensors);
@@ -1406,12 +1655,19 @@ void ew_topk_encode(const TopkEncodeArgs& a) {
     else if (resid) EW_PKH(EF_PLAIN);
     else EW_PKH(EF_NONE);
 #undef EW_PKH
-    EW_LAUNCH(k_pk_pass0, G, s, g, src_flat, chunks, cbl, tensors, pst, pcand, hist0, kmaxr, state,
-              T, tick + TICK_STRIDE * T);
-    EW_LAUNCH(k_pk_pass1, G, s, g, src_flat, chunks, cbl, tensors, pst, pcand, hist1, kmaxr, state,
-              T, tick + 2 * TICK_STRIDE * T, cand, cand_n);
-    EW_LAUNCH(k_pk_pass2, G, s, cbl, tensors, pst, hist2, kmaxr, state, T,
-              tick + 3 * TICK_STRIDE * T, cand, cand_n);
+    if (G <= ew_pk_fused_max_blocks()) {
+      // one launch for the three passes (per-tensor barriers; every block resident at once)
+      EW_LAUNCH(k_pk_select, G, s, g, src_flat, chunks, cbl, tensors, pst, pcand, hist0, hist1,
+                hist2, kmaxr, state, T, tick + TICK_STRIDE * T,
+                reinterpret_cast<uint32_t*>(tick + 2 * TICK_STRIDE * T), cand, cand_n, lb_err);
+    } else {
+      EW_LAUNCH(k_pk_pass0, G, s, g, src_flat, chunks, cbl, tensors, pst, pcand, hist0, kmaxr,
+                state, T, tick + TICK_STRIDE * T);
+      EW_LAUNCH(k_pk_pass1, G, s, g, src_flat, chunks, cbl, tensors, pst, pcand, hist1, kmaxr,
+                state, T, tick + 2 * TICK_STRIDE * T, cand, cand_n);
+      EW_LAUNCH(k_pk_pass2, G, s, cbl, tensors, pst, hist2, kmaxr, state, T,
+                tick + 3 * TICK_STRIDE * T, cand, cand_n);
+    }
 #define EW_PKW(VK, EFV)                                                                          \
   EW_LAUNCH((k_topk_write<VK, EFV, true, true>), C, s, g, resid, chunks, tensors, state, chunk_off, \
             chunk_ties, inv, pay, a.scales_off, a.idx_off, a.codes_off, a.bitmap_off, a.levels,   \

@@ -274,3 +274,31 @@ def test_ef21_estimate_tracks_the_gradient():
         errs.append(float((g[:4000] - G[:4000]).norm()))
     assert torch.equal(G, h)  # world of one: the global estimate is the local one
     assert errs[-1] < 0.3 * errs[0] and all(b <= a + 1e-6 for a, b in zip(errs, errs[1:]))
+
+
+def test_plan_candidate_capacity_and_blocks():
+    """Predictive top-k encode tables (compress/plan.py): a tensor keeps at most 8 k + 4096
+    candidates (capped at numel), its candidate list starts after the previous tensor's, and its
+    candidate passes get one block per 8192 entries of capacity."""
+    import torch
+
+    from ewdml.compress.plan import CAND_K_MULT, CAND_SLACK, CHUNK, BucketPlan
+
+    numels = [20, 500, 2359296, 100003]
+    offs, o = [], 0
+    for n in numels:
+        offs.append(o)
+        o += (n + 63) // 64 * 64
+    plan = BucketPlan(numels, offs, 0.01, 0, o)
+    for n, k, cap in zip(plan.numels, plan.ks, plan.tensor_cap):
+        assert cap == min(n, CAND_K_MULT * k + CAND_SLACK)
+    assert plan.tensor_cap0 == [0, 20, 520, 520 + plan.tensor_cap[2]]
+    assert plan.total_cap == sum(plan.tensor_cap)
+    assert plan.tensor_cblocks == [max(1, -(-c // CHUNK)) for c in plan.tensor_cap]
+    tt = plan.tensor_table("cpu")
+    assert tt[:, 9].tolist() == plan.tensor_cap0 and tt[:, 10].tolist() == plan.tensor_cap
+    cb = plan.cblock_table("cpu")
+    assert cb.shape == (plan.num_cblocks, 2)
+    for t, nb in enumerate(plan.tensor_cblocks):
+        rows = cb[cb[:, 0] == t]
+        assert rows[:, 1].tolist() == list(range(nb))
