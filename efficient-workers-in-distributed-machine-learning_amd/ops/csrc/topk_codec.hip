@@ -636,13 +636,21 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_write(
     float* __restrict__ vel, unsigned long long* __restrict__ lb, int counts_off,
     int* __restrict__ lb_err, const uint32_t* __restrict__ pst,
     const uint32_t* __restrict__ cbase, const uint32_t* __restrict__ ccnt,
-    const uint2* __restrict__ pcand, int lb_fault) {
+    const uint2* __restrict__ pcand, int lb_fault, uint32_t* __restrict__ rz1, uint32_t rz1_words,
+    uint32_t* __restrict__ rz2, uint32_t rz2_words) {
   __shared__ uint32_t ws[EW_WAVES];
   __shared__ uint32_t s_lb[2 * EW_WAVES];
   // the histograms / max-key replicas are dead once the thresholds are selected: clear them here
-  // for the next encode of this bucket (replaces a per-step memset node; first use: zero-alloc)
+  // for the next encode of this bucket (replaces a per-step memset node; first use: zero-alloc).
+  // The predictive path uses one histogram copy per pass: three short ranges (rz1, rz2 too).
   for (uint32_t i = blockIdx.x * EW_BLOCK + threadIdx.x; i < rezero_words; i += gridDim.x * EW_BLOCK)
     rezero[i] = 0u;
+  if (PK) {
+    for (uint32_t i = blockIdx.x * EW_BLOCK + threadIdx.x; i < rz1_words; i += gridDim.x * EW_BLOCK)
+      rz1[i] = 0u;
+    for (uint32_t i = blockIdx.x * EW_BLOCK + threadIdx.x; i < rz2_words; i += gridDim.x * EW_BLOCK)
+      rz2[i] = 0u;
+  }
   const uint32_t key = keyp ? *keyp : key_arg;  // device key: fresh per replay of a captured graph
   const ChunkRow c = chunks[blockIdx.x];
   const TensorRow tr = tensors[c.tensor];
@@ -1483,10 +1491,21 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_decode_apply(
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   for (int i = threadIdx.x; i < (c.len + 3) / 4; i += EW_BLOCK) acc4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   // entry offset of this chunk inside each rank's payload: entry0 + sum of earlier chunk counts
+  // (a wave per rank; each lane's loads of up to 8 counts are all in flight before the sum: the
+  // tensor's last chunks sum a few hundred counts, a dependent round trip per 64 otherwise)
   for (int r = w; r < nranks; r += EW_WAVES) {
     const uint16_t* cnts = reinterpret_cast<const uint16_t*>(recv + r * stride + counts_off) + tr.chunk0;
     uint32_t s = 0;
-    for (int j = lane; j < c.local; j += 64) s += cnts[j];
+    for (int j0 = 0; j0 < c.local; j0 += 8 * 64) {
+      uint32_t v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int j = j0 + u * 64 + lane;
+        v[u] = j < c.local ? (uint32_t)cnts[j] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
     s = ew_wave_sum_u(s);
     if (lane == 0) s_off[r] = (uint32_t)tr.entry0 + s;
   }
@@ -1645,7 +1664,10 @@ void ew_topk_encode(const TopkEncodeArgs& a) {
   auto* pay = reinterpret_cast<uint8_t*>(a.payload);
   const bool pk = a.predict && !a.norm_l2 && a.cblocks && a.num_cblocks > 0;
   if (pk) {
-    // predictive path: hist0 (+ candidates) -> 3 radix passes over the candidates -> write
+    // predictive path: hist0 (+ candidates) -> 3 radix passes over the candidates -> write.
+    // Its passes use histogram copy 0 only: kmaxr + hist0's copy 0 are one range, hist1's and
+    // hist2's copies 0 two more (0.6 MB for VGG-11 instead of 5 MB of zeroing per encode)
+    const uint32_t pk_rz0 = (uint32_t)(NREP * T + T * NB0);
     auto* cbl = reinterpret_cast<const CBlockRow*>(a.cblocks);
     const int G = a.num_cblocks;
 #define EW_PKH(EFM)                                                                              \
@@ -1672,8 +1694,8 @@ void ew_topk_encode(const TopkEncodeArgs& a) {
   EW_LAUNCH((k_topk_write<VK, EFV, true, true>), C, s, g, resid, chunks, tensors, state, chunk_off, \
             chunk_ties, inv, pay, a.scales_off, a.idx_off, a.codes_off, a.bitmap_off, a.levels,   \
             a.inv_levels, a.key, reinterpret_cast<const uint32_t*>(a.key_ptr), a.bucket_offset,   \
-            kmaxr, rezero_words, dg.mask ? dg.vel : nullptr, lb, a.counts_off, lb_err, pst, cbase, \
-            ccnt, pcand, a.lb_fault)
+            kmaxr, pk_rz0, dg.mask ? dg.vel : nullptr, lb, a.counts_off, lb_err, pst, cbase,      \
+            ccnt, pcand, a.lb_fault, hist1, (uint32_t)(T * NB1), hist2, (uint32_t)(T * NB2))
     if (a.value_kind == VK_Q8) {
       if (resid) EW_PKW(VK_Q8, true); else EW_PKW(VK_Q8, false);
     } else if (a.value_kind == VK_Q4) {
@@ -1710,7 +1732,7 @@ void ew_topk_encode(const TopkEncodeArgs& a) {
             chunk_ties, inv, pay, a.scales_off, a.idx_off, a.codes_off, a.bitmap_off, a.levels,     \
             a.inv_levels, a.key, reinterpret_cast<const uint32_t*>(a.key_ptr), a.bucket_offset,     \
             kmaxr, rezero_words, dg.mask ? dg.vel : nullptr, lb, a.counts_off, lb_err, nullptr,     \
-            nullptr, nullptr, nullptr, a.lb_fault)
+            nullptr, nullptr, nullptr, a.lb_fault, nullptr, 0u, nullptr, 0u)
 #define EW_WRITE2(VK, EFV) \
   do { if (lbk) EW_WRITE(VK, EFV, true); else EW_WRITE(VK, EFV, false); } while (0)
   if (a.value_kind == VK_Q8) {
