@@ -1510,16 +1510,61 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_decode_apply(
     if (lane == 0) s_off[r] = (uint32_t)tr.entry0 + s;
   }
   __syncthreads();
+  // Index-list tensors: every rank's first entry of this thread (e = thread index: all of a chunk's
+  // entries at <= 2.5 % density) is loaded for the first PR ranks before any is summed -- one
+  // round trip for all ranks instead of one per rank -- then the rank-ordered LDS sum below
+  // consumes them (same order, same bits).  Loads are clamped into the tensor's entry range and
+  // masked, not branched around (a branch makes the compiler wait for every load at its merge).
+  constexpr int PR = 8;
+  const uint32_t eend = (uint32_t)(tr.entry0 + tr.k);  // never read past the tensor's entries
+  float pre_v[PR];
+  int pre_i[PR];
+  const bool list = tr.bm0 < 0;
+  if (list) {
+#pragma unroll
+    for (int r = 0; r < PR; ++r) {
+      pre_i[r] = -1;
+      pre_v[r] = 0.0f;
+      if (r < nranks) {
+        const uint8_t* pay = recv + r * stride;
+        const uint32_t off = s_off[r];
+        uint32_t cnt = reinterpret_cast<const uint16_t*>(pay + counts_off)[blockIdx.x];
+        cnt = off >= eend ? 0u : min(cnt, eend - off);
+        const float step = VK != VK_F32
+            ? reinterpret_cast<const float*>(pay + scales_off)[c.tensor] * inv_levels : 1.0f;
+        const uint32_t e = threadIdx.x;
+        const uint32_t pe = min(off + min(e, cnt ? cnt - 1u : 0u), eend - 1u);
+        const float prod = ew_topk_code<VK>(pay, codes_off, pe) * step;
+        const int i = reinterpret_cast<const uint16_t*>(pay + idx_off)[tr.idx0 + (pe - (uint32_t)tr.entry0)];
+        if (e < cnt) {
+          pre_v[r] = prod;
+          pre_i[r] = i;
+        }
+      }
+    }
+  }
   for (int r = 0; r < nranks; ++r) {
     const uint8_t* pay = recv + r * stride;
     const uint32_t off = s_off[r];
     // clamp to the tensor's entry range: a corrupted payload must not read out of bounds
-    const uint32_t eend = (uint32_t)(tr.entry0 + tr.k);
     uint32_t cnt = reinterpret_cast<const uint16_t*>(pay + counts_off)[blockIdx.x];
     cnt = off >= eend ? 0u : min(cnt, eend - off);
     float step = 1.0f;
     if (VK != VK_F32) step = reinterpret_cast<const float*>(pay + scales_off)[c.tensor] * inv_levels;
-    if (tr.bm0 >= 0) {
+    if (list && r < PR) {  // the prefetched first entry, then any beyond the block's width
+#pragma unroll
+      for (int q = 0; q < PR; ++q)
+        if (q == r && pre_i[q] >= 0 && pre_i[q] < c.len) acc[pre_i[q]] = acc[pre_i[q]] + pre_v[q];
+      if (cnt > (uint32_t)EW_BLOCK) {
+        const uint16_t* idx = reinterpret_cast<const uint16_t*>(pay + idx_off) + tr.idx0 +
+                              (off - (uint32_t)tr.entry0);
+        for (uint32_t e = threadIdx.x + EW_BLOCK; e < cnt; e += EW_BLOCK) {
+          const float prod = ew_topk_code<VK>(pay, codes_off, off + e) * step;
+          const int i = idx[e];
+          if (i < c.len) acc[i] = acc[i] + prod;
+        }
+      }
+    } else if (tr.bm0 >= 0) {
       // bitmap-indexed tensor: thread t owns word t of the chunk (256 words = 8192 elements);
       // a block scan of the popcounts gives each word's first entry
       const uint32_t* bw = reinterpret_cast<const uint32_t*>(pay + bitmap_off) + tr.bm0 +

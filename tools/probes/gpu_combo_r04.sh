@@ -4,3 +4,5 @@ bash tools/gpurun_suite.sh prof pk_vgg "--no-extras --steps 20" > gpurun_out/com
 grep -E "k_pk|k_topk" gpurun_out/prof_pk_vgg.txt | head -12
 bash tools/gpurun_suite.sh bench "" || exit 1
 EXTRA="" bash tools/probes/gpu_graph_shape.sh || exit 1
+timeout -k 10 300 python tools/probes/decode_probe.py > gpurun_out/decode_probe.txt 2>&1 || { tail gpurun_out/decode_probe.txt; exit 1; }
+cat gpurun_out/decode_probe.txt
