@@ -133,6 +133,20 @@ def topk_stats(dp) -> dict:
     return {"lookback_errors": e, "fast": fast, "full": full}
 
 
+_GRAPH_NODE_TYPES = ["kernel", "memcpy", "memset", "host", "graph", "empty", "wait_event",
+                     "event_record", "ext_semas_signal", "ext_semas_wait", "mem_alloc", "mem_free",
+                     "memcpy_from_symbol", "memcpy_to_symbol", "batch_mem_op", "t15"]
+
+
+def graph_info(graph, dot_path: str = "") -> dict:
+    """Node / edge counts of a captured graph kept with ``torch.cuda.CUDAGraph(keep_graph=True)``
+    (``raw_cuda_graph()``): a straight line has no forks or joins and one root."""
+    v = require().graph_info(int(graph), dot_path)
+    types = {_GRAPH_NODE_TYPES[i]: int(c) for i, c in enumerate(v[5:]) if c}
+    return {"nodes": v[0], "edges": v[1], "forks": v[2], "joins": v[3], "roots": v[4],
+            "linear": v[2] == 0 and v[3] == 0 and v[4] <= 1, "types": types}
+
+
 def topk_lookback_errors(dp) -> int:
     """Times a top-k write block gave up waiting on a predecessor's look-back word (bounded spin;
     0 unless something is badly wrong).  Synchronises."""

@@ -21,6 +21,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("topk_scratch_bytes", &ew_topk_scratch_bytes);
   m.def("topk_lookback_errors", &ew_topk_lookback_errors);
   m.def("topk_stats", &ew_topk_stats);
+  m.def("graph_info", &ew_graph_info);
   m.def("qsgd_scratch_bytes", &ew_qsgd_scratch_bytes);
 
   m.def("topk_encode",

@@ -99,6 +99,7 @@ struct AdamFlatArgs {
 size_t ew_topk_scratch_bytes(int num_tensors, int num_chunks, long long bucket_len,
                              long long total_cap);
 std::vector<int> ew_topk_stats(uintptr_t scratch, int num_tensors, int num_chunks);
+std::vector<long long> ew_graph_info(uintptr_t graph, const std::string& dot_path);
 int ew_topk_lookback_errors(uintptr_t scratch, int num_tensors, int num_chunks);
 void ew_topk_encode(const TopkEncodeArgs& a);
 void ew_topk_decode_apply(const TopkDecodeArgs& a);

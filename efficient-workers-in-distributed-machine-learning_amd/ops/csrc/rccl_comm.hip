@@ -366,3 +366,38 @@ void ew_test_spin(uintptr_t flag, double max_s, uintptr_t stream) {
                      reinterpret_cast<const int*>(flag), (unsigned long long)(max_s * 1e8));
   EW_CHECK_LAUNCH();
 }
+
+// ---------------------------------------------------------------------------------------------
+// Shape of a captured HIP graph (node count per type, edges, forks / joins): whether a step graph
+// is a straight line, which ROCm replays with one batched submission, or a DAG, which it walks
+// node by node from the host.  `dot_path`: also hipGraphDebugDotPrint.
+// ---------------------------------------------------------------------------------------------
+std::vector<long long> ew_graph_info(uintptr_t graph, const std::string& dot_path) {
+  hipGraph_t g = reinterpret_cast<hipGraph_t>(graph);
+  if (!g) throw std::runtime_error("ewdml graph_info: null graph");
+  size_t n = 0, ne = 0;
+  EW_CHECK(hipGraphGetNodes(g, nullptr, &n));
+  std::vector<hipGraphNode_t> nodes(n);
+  if (n) EW_CHECK(hipGraphGetNodes(g, nodes.data(), &n));
+  EW_CHECK(hipGraphGetEdges(g, nullptr, nullptr, &ne));
+  std::vector<hipGraphNode_t> from(ne), to(ne);
+  if (ne) EW_CHECK(hipGraphGetEdges(g, from.data(), to.data(), &ne));
+  // out: [nodes, edges, forks (out-degree > 1), joins (in-degree > 1), roots, then count per
+  // hipGraphNodeType 0..15]
+  std::vector<long long> out(5 + 16, 0);
+  out[0] = (long long)n;
+  out[1] = (long long)ne;
+  for (size_t i = 0; i < n; ++i) {
+    hipGraphNodeType t;
+    EW_CHECK(hipGraphNodeGetType(nodes[i], &t));
+    if ((int)t >= 0 && (int)t < 16) out[5 + (int)t] += 1;
+    size_t od = 0, id = 0;
+    EW_CHECK(hipGraphNodeGetDependentNodes(nodes[i], nullptr, &od));
+    EW_CHECK(hipGraphNodeGetDependencies(nodes[i], nullptr, &id));
+    out[2] += od > 1;
+    out[3] += id > 1;
+    out[4] += id == 0;
+  }
+  if (!dot_path.empty()) EW_CHECK(hipGraphDebugDotPrint(g, dot_path.c_str(), 0));
+  return out;
+}

@@ -531,10 +531,10 @@ class Trainer:
         torch.cuda.synchronize()
         try:  # the counters come back on the failure path too (eager fallback stays in step)
             if self.graph_mode == "full":
-                g = torch.cuda.CUDAGraph()
-                dump = os.environ.get("EWDML_GRAPH_DUMP")  # DOT file of the captured step
-                if dump:
-                    g.enable_debug_mode()
+                # EWDML_GRAPH_DUMP=<path>: the captured step's shape (node / edge counts, forks,
+                # joins, node types) as JSON at <path> and the DOT file at <path>.dot
+                dump = os.environ.get("EWDML_GRAPH_DUMP")
+                g = torch.cuda.CUDAGraph(keep_graph=True) if dump else torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, stream=self.gstream, capture_error_mode=mode):
                     try:
                         if self._in_graph_batch:
@@ -545,7 +545,15 @@ class Trainer:
                         self._rejoin_side()
                         raise
                 if dump:
-                    g.debug_dump(dump)
+                    import json
+
+                    from .. import ops
+
+                    info = ops.graph_info(g.raw_cuda_graph(), dump + ".dot")
+                    info["comm"] = self.comm.kind
+                    with open(dump, "w") as f:
+                        json.dump(info, f)
+                    g.instantiate()
                 self._graphs = (g,)
             elif self.graph_mode == "segmented":
                 seg = SegmentedCapture(self.gstream, ex.comm_stream, mode="relaxed",

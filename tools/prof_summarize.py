@@ -46,17 +46,25 @@ def summarize(rows, frac=0.5, gap_ns=150_000_000, steps=None):
     if not rows:
         return "no kernels\n"
     t0, t1 = rows[0][0], max(r[1] for r in rows)
-    cut = None
+    gaps = []  # (idle start, idle end)
     end = rows[0][1]
     for s, e, _ in rows[1:]:
         if s - end >= gap_ns:
-            cut = s
+            gaps.append((end, s))
         end = max(end, e)
-    how = "after last idle gap"
-    if cut is None:
+    # bench.py (EWDML_PROF_GAP=1) idles before and after the timed loop: the window between the
+    # last two gaps; a trace with one gap: everything after it
+    stop = None
+    if len(gaps) >= 2:
+        cut, stop = gaps[-2][1], gaps[-1][0]
+        how = "between the last two idle gaps"
+    elif gaps:
+        cut = gaps[-1][1]
+        how = "after last idle gap"
+    else:
         cut = t0 + (t1 - t0) * (1 - frac)
         how = f"last {frac:.0%} of trace"
-    win = [r for r in rows if r[0] >= cut]
+    win = [r for r in rows if r[0] >= cut and (stop is None or r[0] < stop)]
     span = max(r[1] for r in win) - win[0][0]
     busy = 0
     cur_s, cur_e = win[0][0], win[0][1]
