@@ -998,7 +998,7 @@ __device__ __forceinline__ void pk_select(const uint32_t* __restrict__ hist,
                                           const TensorRow* __restrict__ tensors,
                                           uint32_t* __restrict__ state,
                                           const uint32_t* __restrict__ kmaxr, int T, int t,
-                                          uint32_t shift) {
+                                          uint32_t shift, size_t hstride = NB) {
   constexpr int PER = NB / EW_BLOCK;
   __shared__ uint32_t ws[EW_WAVES];
   // state is handed between the blocks of the fused select kernel (other XCDs): agent-scope
@@ -1014,7 +1014,7 @@ __device__ __forceinline__ void pk_select(const uint32_t* __restrict__ hist,
 #pragma unroll
   for (int j = 0; j < PER; ++j) cnt[j] = 0;
   {  // the candidate passes use one histogram copy (<= ncb blocks per tensor add to it)
-    const uint32_t* ht = hist + (size_t)t * NB;
+    const uint32_t* ht = hist + (size_t)t * hstride;  // hstride 0: this block's LDS histogram
 #pragma unroll
     for (int j = 0; j < PER; ++j) cnt[j] = ht[NB - 1 - (threadIdx.x * PER + j)];
   }
@@ -1231,7 +1231,8 @@ __global__ __launch_bounds__(EW_BLOCK) void k_pk_pass2(
 // then publishes a per-tensor generation word the others wait on (bounded poll; a timeout bumps
 // the look-back error counter, which the health check turns into a failure).
 // ---------------------------------------------------------------------------------------------
-constexpr uint32_t PK_MAX_POLLS = 1u << 20;
+constexpr uint32_t PK_MAX_POLLS = 1u << 22;  // ~2 s of polls: only a broken launch gets there
+constexpr uint32_t PK_LOCAL_MAX = 4 * EW_CHUNK;  // pass-1 keys one block takes pass 2 over
 
 // Everything handed across the barrier is written with device-coherent operations (histogram
 // atomics, agent-scope stores of the select state and the pass-1 keys) and every wave drains its
@@ -1262,20 +1263,23 @@ __device__ __forceinline__ void pk_publish(int* arrive, uint32_t* gen, uint32_t 
   }
 }
 
-// everyone else: wait for generation g, block-uniform
-__device__ __forceinline__ void pk_wait(const uint32_t* gen, uint32_t g, int* err) {
+// everyone else: wait for generation g, block-uniform; returns the generation seen
+__device__ __forceinline__ uint32_t pk_wait(const uint32_t* gen, uint32_t g, int* err,
+                                            uint32_t* s_gen) {
   if (threadIdx.x == 0) {
-    uint32_t polls = 0;
-    while ((int)(__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - g) < 0) {
+    uint32_t polls = 0, v;
+    while ((int)((v = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) - g) < 0) {
       if (++polls > PK_MAX_POLLS) {
         atomicAdd(err, 1);
         break;
       }
-      __builtin_amdgcn_s_sleep(8);
+      __builtin_amdgcn_s_sleep(2);
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    *s_gen = v;
   }
   __syncthreads();
+  return *s_gen;
 }
 
 __global__ __launch_bounds__(EW_BLOCK) void k_pk_select(
@@ -1289,7 +1293,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_pk_select(
   constexpr int R = EW_CHUNK / EW_BLOCK;
   __shared__ uint32_t hs[NB0 * HSUB];
   __shared__ uint32_t ws[EW_WAVES];
-  __shared__ uint32_t s_base;
+  __shared__ uint32_t s_base, s_gen;
   __shared__ int s_flag;
   const CBlockRow cb = cblocks[blockIdx.x];
   const int t = cb.tensor;
@@ -1341,7 +1345,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_pk_select(
     pk_select<NB0, true>(hist0, tensors, state, kmaxr, T, t, s0);
     pk_publish(arr, gn, g0 + 1u);
   } else {
-    pk_wait(gn, g0 + 1u, err);
+    pk_wait(gn, g0 + 1u, err, &s_gen);
   }
   // ---- pass 1: next s0 - s1 bits of the keys in the selected digit 0; those keys -> cand ----
   {
@@ -1390,9 +1394,44 @@ __global__ __launch_bounds__(EW_BLOCK) void k_pk_select(
   }
   if (pk_arrive(arr, tr.ncb, &s_flag)) {
     pk_select<NB1, false>(hist1, tensors, state, kmaxr, T, t, s1);
+    // few pass-1 keys (the usual case): this block runs pass 2 over them alone, in LDS, and the
+    // tensor is done without a third barrier (generation g0 + 3 tells the waiting blocks)
+    const uint32_t n = (uint32_t)__hip_atomic_load(cand_n + TICK_STRIDE * t, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+    if (n <= PK_LOCAL_MAX) {
+      __syncthreads();  // the select's state stores issued; hs free
+      const uint32_t want = __hip_atomic_load(state + t * 4, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT) >> s1;
+      const uint32_t dmask = (1u << s1) - 1u;
+      const uint32_t* src = cand + tr.off;
+      uint32_t* h = hs;
+      for (int i = threadIdx.x; i < NB2; i += EW_BLOCK) h[i] = 0;
+      __syncthreads();
+      for (uint32_t b0 = 0; b0 < n; b0 += EW_CHUNK) {
+        const uint32_t j0 = b0 + threadIdx.x, j1 = min(n, b0 + EW_CHUNK);
+        uint32_t kk[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const uint32_t i = j0 + r * EW_BLOCK;
+          kk[r] = i < j1 ? __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                         : 0u;
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const uint32_t rel = kk[r] - B;
+          if (j0 + r * EW_BLOCK < j1 && (rel >> s1) == want) atomicAdd(&h[rel & dmask], 1u);
+        }
+      }
+      __syncthreads();
+      pk_select<NB2, false>(h, tensors, state, kmaxr, T, t, 0u, 0);
+      __syncthreads();
+      if (threadIdx.x == 0) pk_predict(tr, t, B, state, pst, cand_n);
+      pk_publish(arr, gn, g0 + 3u);
+      return;
+    }
     pk_publish(arr, gn, g0 + 2u);
-  } else {
-    pk_wait(gn, g0 + 2u, err);
+  } else if (pk_wait(gn, g0 + 2u, err, &s_gen) == g0 + 3u) {
+    return;  // pass 2 ran in the last block of pass 1
   }
   // ---- pass 2: the last s1 bits over the pass-1 keys ----
   {
