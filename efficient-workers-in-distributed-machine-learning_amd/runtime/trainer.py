@@ -144,8 +144,11 @@ class Trainer:
         self.graph_plan = None
         if (cfg.hip_graph == "auto" and self.cuda and not cfg.sync_debug
                 and cfg.topology == "allgather" and cfg.sync_every == 1 and not cfg.select_best):
+            # EWDML_PLAN_AS_WORLD (test hook): plan as if the job had that many ranks, so the
+            # N > 1 decision runs end to end on a one-GPU box (world of one, real communicator)
+            plan_world = int(os.environ.get("EWDML_PLAN_AS_WORLD", self.world))
             self.graph_plan = plan_graph_mode(
-                self.world, self.comm.kind, cfg.compress,
+                plan_world, self.comm.kind, cfg.compress,
                 sum(p.numel() for p in model.parameters() if p.requires_grad),
                 bits=cfg.qsgd_bits, overlap=cfg.overlap, bucket_bytes=bucket_bytes)
             bucket_bytes = self.graph_plan["bucket_bytes"]

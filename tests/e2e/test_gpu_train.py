@@ -290,6 +290,21 @@ def test_comm_probe_passes_and_failure_falls_back_to_process_group():
     assert bad["payload_bytes_per_rank"] == ok["payload_bytes_per_rank"]
 
 
+def test_auto_plan_at_n8_runs_segmented_through_rccl():
+    """--hip-graph auto as planned for 8 ranks (EWDML_PLAN_AS_WORLD=8) on the real RCCL
+    communicator (world of one): the dense fp32 exchange becomes the segmented step -- comm
+    graphs with the all-reduce on their own stream beside backward -- and the replicas check and
+    the JSON fields hold; the top-k headline stays one graph."""
+    dense = _bench_pg("none", "rccl", extra=("--error-feedback", "off"),
+                      env_extra={"EWDML_PLAN_AS_WORLD": "8"})
+    assert dense["graph_plan"]["mode"] == "segmented" and dense["graph_plan"]["splits"] == 2
+    assert dense["config"]["hip_graph"] == "segmented" and dense["overlap_comm_graphs"] >= 1
+    assert dense["config"]["buckets"] >= 3 and dense["replicas_identical"] is True
+    assert dense["final_loss"] == dense["final_loss"]
+    topk = _bench_pg("topk_qsgd", "rccl", env_extra={"EWDML_PLAN_AS_WORLD": "8"})
+    assert topk["graph_plan"]["mode"] == "full" and topk["config"]["hip_graph"] == "full"
+
+
 @pytest.mark.parametrize("codec", ["topk_qsgd", "none"])
 def test_bench_through_rccl_process_group(codec):
     """bench.py under torch.distributed.run with a real RCCL communicator (world of one,
