@@ -134,73 +134,6 @@ __device__ __forceinline__ void ew_ld_chunk(const GradPtrs& gp, const float* fla
     }
   }
 }
-// slabs [U0, U0 + NU) of a chunk of a flat fp32 buffer (src / dst = chunk start), tail handled
-template <int NU, int U0>
-__device__ __forceinline__ void ew_ld_slabs(const float* src, int len, float4 (&v)[NU]) {
-  if (len == EW_CHUNK) {
-#pragma unroll
-    for (int u = 0; u < NU; ++u) v[u] = *reinterpret_cast<const float4*>(src + ew_chunk_idx(U0 + u));
-  } else {
-#pragma unroll
-    for (int u = 0; u < NU; ++u) {
-      const int i = ew_chunk_idx(U0 + u);
-      float xs[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-      if (i + 3 < len) {
-        const float4 t = *reinterpret_cast<const float4*>(src + i);
-        xs[0] = t.x; xs[1] = t.y; xs[2] = t.z; xs[3] = t.w;
-      } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (i + j < len) xs[j] = src[i + j];
-      }
-      v[u] = make_float4(xs[0], xs[1], xs[2], xs[3]);
-    }
-  }
-}
-template <int NU, int U0>
-__device__ __forceinline__ void ew_st_slabs(float* dst, int len, const float4 (&v)[NU]) {
-#pragma unroll
-  for (int u = 0; u < NU; ++u) {
-    const int i = ew_chunk_idx(U0 + u);
-    if (i + 3 < len) {
-      *reinterpret_cast<float4*>(dst + i) = v[u];
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (i + j < len) dst[i + j] = (j == 0 ? v[u].x : j == 1 ? v[u].y : j == 2 ? v[u].z : v[u].w);
-    }
-  }
-}
-
-// slabs [U0, U0 + NU) of a chunk (ew_ld_chunk for part of the chunk)
-template <int NU, int U0>
-__device__ __forceinline__ void ew_ld_chunk_part(const GradPtrs& gp, const float* flat,
-                                                 const ChunkRow& c, float4* v) {
-  const size_t off = (size_t)c.local * EW_CHUNK;
-  const bool bf = !flat && ((gp.bf16[c.tensor >> 5] >> (c.tensor & 31)) & 1u);
-  const float* src = flat ? flat + c.start : reinterpret_cast<const float*>(gp.p[c.tensor]) + off;
-  if (c.len == EW_CHUNK && !bf) {
-#pragma unroll
-    for (int u = 0; u < NU; ++u) v[u] = *reinterpret_cast<const float4*>(src + ew_chunk_idx(U0 + u));
-  } else if (c.len == EW_CHUNK) {
-    const uint16_t* s16 = reinterpret_cast<const uint16_t*>(gp.p[c.tensor]) + off;
-    uint2 r[NU];
-#pragma unroll
-    for (int u = 0; u < NU; ++u) r[u] = *reinterpret_cast<const uint2*>(s16 + ew_chunk_idx(U0 + u));
-#pragma unroll
-    for (int u = 0; u < NU; ++u)
-      v[u] = make_float4(ew_bf16f(r[u].x), ew_bf16f(r[u].x >> 16), ew_bf16f(r[u].y),
-                         ew_bf16f(r[u].y >> 16));
-  } else {
-#pragma unroll
-    for (int u = 0; u < NU; ++u) {
-      float xs[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-      if (ew_chunk_idx(U0 + u) < c.len) ew_ld4t(gp, flat, c, ew_chunk_idx(U0 + u), xs);
-      v[u] = make_float4(xs[0], xs[1], xs[2], xs[3]);
-    }
-  }
-}
-
 __device__ __forceinline__ float ew_f4(const float4& v, int j) {
   return j == 0 ? v.x : j == 1 ? v.y : j == 2 ? v.z : v.w;
 }

@@ -86,49 +86,6 @@ struct DgcArgs {
 // error-feedback mode of the encode: none, plain (e = g + r), momentum-corrected (DGC)
 enum EfMode { EF_NONE = 0, EF_PLAIN = 1, EF_DGC = 2 };
 
-// One half (slabs [U0, U0 + EW_CU / 2)) of the DGC staging of a chunk held in registers.
-template <int U0, bool LOAD_G = false>
-__device__ __forceinline__ void dgc_half(const GradPtrs& gp, const DgcArgs& dg,
-                                         float* __restrict__ resid, const ChunkRow& c,
-                                         float4 (&v)[EW_CU], float lr) {
-  constexpr int H = EW_CU / 2;
-  float4 r[H], uv[H], pv[H];
-  if (LOAD_G) ew_ld_chunk_part<H, U0>(gp, nullptr, c, v + U0);  // this half of the gradient
-  ew_ld_slabs<H, U0>(resid + c.start, c.len, r);
-  ew_ld_slabs<H, U0>(dg.vel + c.start, c.len, uv);
-  if (dg.wd != 0.0f) ew_ld_slabs<H, U0>(dg.param + c.start, c.len, pv);  // uniform branch
-#pragma unroll
-  for (int u = 0; u < H; ++u) {
-    const float4 gv = v[U0 + u];
-    float g4[4] = {gv.x, gv.y, gv.z, gv.w};
-    float u4[4] = {uv[u].x, uv[u].y, uv[u].z, uv[u].w};
-    const float r4[4] = {r[u].x, r[u].y, r[u].z, r[u].w};
-    float e4[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float g = g4[j];
-      if (dg.wd != 0.0f) g = g + ew_f4(pv[u], j) * dg.wd;
-      const float a = u4[j] * dg.momentum;
-      const float b = g * dg.damp1;
-      u4[j] = a + b;
-      float d = u4[j];
-      if (dg.nesterov) {
-        const float mu = u4[j] * dg.momentum;
-        d = g + mu;
-      }
-      if (dg.lr_ptr) d = d * lr;
-      e4[j] = r4[j] + d;
-    }
-    uv[u] = make_float4(u4[0], u4[1], u4[2], u4[3]);
-    v[U0 + u] = make_float4(e4[0], e4[1], e4[2], e4[3]);
-  }
-  ew_st_slabs<H, U0>(dg.vel + c.start, c.len, uv);
-  float4 ev[H];
-#pragma unroll
-  for (int u = 0; u < H; ++u) ev[u] = v[U0 + u];
-  ew_st_slabs<H, U0>(resid + c.start, c.len, ev);
-}
-
 // Error-feedback staging of one chunk held in registers (v = the gradient on entry, the vector to
 // compress on exit): plain e = g + r, or DGC's momentum correction; e (and DGC's velocity) are
 // written back, so later passes read e from the residual.
@@ -146,12 +103,37 @@ __device__ __forceinline__ void topk_ef_stage(const GradPtrs& gp, const DgcArgs&
   } else if (EFM == EF_DGC) {
     // momentum correction (oracle.dgc_accumulate, every product / sum rounded on its own):
     // g' = g + wd p ; u = m u + (1 - d) g' ; d = g' + m u (Nesterov) | u ; e = r + d
-    // In two halves of EW_CU / 2 slabs: the residual, velocity (and parameters) of one half are
-    // live at a time (147 -> fewer VGPRs: more blocks per CU, so a bucket's ~1200 chunk blocks
-    // run in fewer rounds)
+    float4 r[EW_CU], uv[EW_CU], pv[EW_CU];
     const float lr = dg.lr_ptr ? *dg.lr_ptr : 1.0f;
-    dgc_half<0>(gp, dg, resid, c, v, lr);
-    dgc_half<EW_CU / 2>(gp, dg, resid, c, v, lr);
+    ew_ld_chunk(gp, resid, c, r);
+    ew_ld_chunk(gp, dg.vel, c, uv);
+    if (dg.wd != 0.0f) ew_ld_chunk(gp, dg.param, c, pv);  // uniform branch
+#pragma unroll
+    for (int u = 0; u < EW_CU; ++u) {
+      float g4[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+      float u4[4] = {uv[u].x, uv[u].y, uv[u].z, uv[u].w};
+      const float r4[4] = {r[u].x, r[u].y, r[u].z, r[u].w};
+      float e4[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float g = g4[j];
+        if (dg.wd != 0.0f) g = g + ew_f4(pv[u], j) * dg.wd;
+        const float a = u4[j] * dg.momentum;
+        const float b = g * dg.damp1;
+        u4[j] = a + b;
+        float d = u4[j];
+        if (dg.nesterov) {
+          const float mu = u4[j] * dg.momentum;
+          d = g + mu;
+        }
+        if (dg.lr_ptr) d = d * lr;
+        e4[j] = r4[j] + d;
+      }
+      uv[u] = make_float4(u4[0], u4[1], u4[2], u4[3]);
+      v[u] = make_float4(e4[0], e4[1], e4[2], e4[3]);
+    }
+    ew_st_chunk(dg.vel + c.start, c.len, uv);
+    ew_st_chunk(resid + c.start, c.len, v);
   }
 }
 
@@ -862,17 +844,10 @@ __global__ __launch_bounds__(EW_BLOCK) void k_pk_hist0(
   const TensorRow tr = tensors[c.tensor];
   if (threadIdx.x == 0) lb[blockIdx.x] = 0ull;  // the write pass's look-back word
   float4 v[EW_CU];
-  if (EFM == EF_DGC) {  // gradient, residual and velocity half by half (register footprint)
-    const float lr = dg.lr_ptr ? *dg.lr_ptr : 1.0f;
-    dgc_half<0, true>(gp, dg, resid, c, v, lr);
-    dgc_half<EW_CU / 2, true>(gp, dg, resid, c, v, lr);
-  } else {
-    ew_ld_chunk(gp, nullptr, c, v);
-    topk_ef_stage<EFM>(gp, dg, resid, c, v);
-  }
+  ew_ld_chunk(gp, nullptr, c, v);
+  topk_ef_stage<EFM>(gp, dg, resid, c, v);
   const uint32_t P = pst[c.tensor * 8];
   uint32_t kmax = 0;
-  uint32_t cmask = 0;  // bit 4 u + j: element (u, j) of this thread is a candidate
   unsigned long long pa = 0, pb = 0;  // candidates per slab, 16-bit fields (slabs 0-3, 4-7)
 #pragma unroll
   for (int u = 0; u < EW_CU; ++u) {
@@ -882,23 +857,25 @@ __global__ __launch_bounds__(EW_BLOCK) void k_pk_hist0(
       if (ew_chunk_idx(u) + j < c.len) {
         const uint32_t k = ew_key(ew_f4(v[u], j));
         kmax = max(kmax, k);
-        const bool cnd = k >= P;
-        n += cnd;
-        cmask |= (uint32_t)cnd << (4 * u + j);
+        n += k >= P;
       }
     }
     if (u < 4) pa |= (unsigned long long)n << (16 * u);
     else pb |= (unsigned long long)n << (16 * (u - 4));
   }
-  // the values are dead from here: the (few) candidates are re-read from the staged e (L2-hot)
-  // or the gradient when they are written, which keeps the register footprint of the scan down
   kmax = ew_wave_max_u(kmax);
   if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = kmax;
   unsigned long long ta, tb;
   pk_scan2(pa, pb, ws2, ta, tb);  // contains __syncthreads: wmax visible
-  uint32_t tot = 0;
+  // slab starts within the chunk's candidate segment (index order: slab, then thread, then j)
+  uint32_t start[EW_CU];
+  uint32_t run = 0;
 #pragma unroll
-  for (int u = 0; u < EW_CU; ++u) tot += (uint32_t)(((u < 4 ? ta : tb) >> (16 * (u & 3))) & 0xffffull);
+  for (int u = 0; u < EW_CU; ++u) {
+    start[u] = run;
+    run += (uint32_t)(((u < 4 ? ta : tb) >> (16 * (u & 3))) & 0xffffull);
+  }
+  const uint32_t tot = run;
   if (threadIdx.x == 0) {
     uint32_t m = wmax[0];
     for (int w = 1; w < EW_WAVES; ++w) m = max(m, wmax[w]);
@@ -909,20 +886,18 @@ __global__ __launch_bounds__(EW_BLOCK) void k_pk_hist0(
     ccnt[blockIdx.x] = tot;
   }
   __syncthreads();
-  if (cmask) {
+  if (tot) {
     uint2* dst = pcand + tr.cap0;
-    const uint32_t cap = (uint32_t)tr.cap;
-    // slab starts within the chunk's candidate segment (index order: slab, then thread, then j)
-    uint32_t start = s_base;
+    const uint32_t cap = (uint32_t)tr.cap, base = s_base;
 #pragma unroll
     for (int u = 0; u < EW_CU; ++u) {
-      uint32_t pos = start + (uint32_t)(((u < 4 ? pa : pb) >> (16 * (u & 3))) & 0xffffull);
-      start += (uint32_t)(((u < 4 ? ta : tb) >> (16 * (u & 3))) & 0xffffull);
+      uint32_t pos = base + start[u] +
+                     (uint32_t)(((u < 4 ? pa : pb) >> (16 * (u & 3))) & 0xffffull);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        if ((cmask >> (4 * u + j)) & 1u) {
-          const int i = ew_chunk_idx(u) + j;
-          const float x = EFM != EF_NONE ? resid[c.start + i] : ew_ld1(gp, nullptr, c, i);
+        const int i = ew_chunk_idx(u) + j;
+        const float x = ew_f4(v[u], j);
+        if (i < c.len && ew_key(x) >= P) {
           if (pos < cap) dst[pos] = make_uint2(__float_as_uint(x), (uint32_t)(c.local * EW_CHUNK + i));
           ++pos;
         }
