@@ -1667,6 +1667,158 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_decode_apply(
   }
 }
 
+// The SPARSE step of k_topk_decode_apply (no momentum buffer, no weight decay, no averaged
+// gradient out: only touched float4s change) in its own kernel sized for one round of blocks: no
+// parameter / momentum prefetch registers, and the LDS accumulator holds half a chunk -- the
+// chunk's two halves are summed and applied one after the other from the same entry loads (the
+// index-list entries are prefetched once and filtered per half).  16 KB of LDS and no prefetch:
+// >= 5 blocks per CU instead of 4, so a VGG-11 bucket's ~1200 chunk blocks run in one round.
+// Sums are per element in rank order from +0, as in k_topk_decode_apply: the same bits.
+template <int VK>
+__global__ __launch_bounds__(EW_BLOCK) void k_topk_decode_sparse(
+    const uint8_t* __restrict__ recv, int nranks, long long stride,
+    const ChunkRow* __restrict__ chunks, const TensorRow* __restrict__ tensors, int scales_off,
+    int counts_off, int idx_off, int codes_off, int bitmap_off, float inv_levels,
+    float* __restrict__ param, uint16_t* __restrict__ shadow, SgdArgs sa) {
+  constexpr int HALF = EW_CHUNK / 2;
+  __shared__ float4 acc4[HALF / 4];
+  __shared__ uint32_t s_off[EW_MAX_RANKS];
+  __shared__ uint32_t ws[EW_WAVES];
+  float* acc = reinterpret_cast<float*>(acc4);
+  ew_sgd_resolve(sa);
+  ew_key_advance(sa);
+  const ChunkRow c = chunks[blockIdx.x];
+  const TensorRow tr = tensors[c.tensor];
+  float* p = param + c.start;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int r = w; r < nranks; r += EW_WAVES) {
+    const uint16_t* cnts = reinterpret_cast<const uint16_t*>(recv + r * stride + counts_off) + tr.chunk0;
+    uint32_t s = 0;
+    for (int j0 = 0; j0 < c.local; j0 += 8 * 64) {
+      uint32_t v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int j = j0 + u * 64 + lane;
+        v[u] = j < c.local ? (uint32_t)cnts[j] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    s = ew_wave_sum_u(s);
+    if (lane == 0) s_off[r] = (uint32_t)tr.entry0 + s;
+  }
+  __syncthreads();
+  constexpr int PR = 8;
+  const uint32_t eend = (uint32_t)(tr.entry0 + tr.k);
+  float pre_v[PR];
+  int pre_i[PR];
+  const bool list = tr.bm0 < 0;
+  if (list) {
+#pragma unroll
+    for (int r = 0; r < PR; ++r) {
+      pre_i[r] = -1;
+      pre_v[r] = 0.0f;
+      if (r < nranks) {
+        const uint8_t* pay = recv + r * stride;
+        const uint32_t off = s_off[r];
+        uint32_t cnt = reinterpret_cast<const uint16_t*>(pay + counts_off)[blockIdx.x];
+        cnt = off >= eend ? 0u : min(cnt, eend - off);
+        const float step = VK != VK_F32
+            ? reinterpret_cast<const float*>(pay + scales_off)[c.tensor] * inv_levels : 1.0f;
+        const uint32_t e = threadIdx.x;
+        const uint32_t pe = min(off + min(e, cnt ? cnt - 1u : 0u), eend - 1u);
+        const float prod = ew_topk_code<VK>(pay, codes_off, pe) * step;
+        const int i = reinterpret_cast<const uint16_t*>(pay + idx_off)[tr.idx0 + (pe - (uint32_t)tr.entry0)];
+        if (e < cnt) {
+          pre_v[r] = prod;
+          pre_i[r] = i;
+        }
+      }
+    }
+  }
+  for (int lo = 0; lo < c.len; lo += HALF) {  // block-uniform
+    const int hl = min(c.len - lo, HALF);
+    if (lo) __syncthreads();  // the previous half's apply has read the accumulator
+    for (int i = threadIdx.x; i < (hl + 3) / 4; i += EW_BLOCK) acc4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    __syncthreads();
+    for (int r = 0; r < nranks; ++r) {
+      const uint8_t* pay = recv + r * stride;
+      const uint32_t off = s_off[r];
+      uint32_t cnt = reinterpret_cast<const uint16_t*>(pay + counts_off)[blockIdx.x];
+      cnt = off >= eend ? 0u : min(cnt, eend - off);
+      float step = 1.0f;
+      if (VK != VK_F32) step = reinterpret_cast<const float*>(pay + scales_off)[c.tensor] * inv_levels;
+      if (list && r < PR) {
+#pragma unroll
+        for (int q = 0; q < PR; ++q) {
+          const int i = pre_i[q] - lo;
+          if (q == r && pre_i[q] >= 0 && i >= 0 && i < hl) acc[i] = acc[i] + pre_v[q];
+        }
+        if (cnt > (uint32_t)EW_BLOCK) {
+          const uint16_t* idx = reinterpret_cast<const uint16_t*>(pay + idx_off) + tr.idx0 +
+                                (off - (uint32_t)tr.entry0);
+          for (uint32_t e = threadIdx.x + EW_BLOCK; e < cnt; e += EW_BLOCK) {
+            const int i = (int)idx[e] - lo;
+            if (i >= 0 && i < hl) acc[i] = acc[i] + ew_topk_code<VK>(pay, codes_off, off + e) * step;
+          }
+        }
+      } else if (!list) {
+        // bitmap: thread t owns word t (elements 32t..32t+31); the scan runs over the whole chunk
+        // (it gives each word's first entry), the adds only for the words of this half
+        const uint32_t* bw = reinterpret_cast<const uint32_t*>(pay + bitmap_off) + tr.bm0 +
+                             c.local * EW_BM_WORDS;
+        uint32_t word = (int)threadIdx.x * 32 < c.len ? bw[threadIdx.x] : 0u;
+        uint32_t tot;
+        uint32_t e = ew_block_excl_scan((uint32_t)__popc(word), ws, tot);
+        if ((int)threadIdx.x * 32 < lo || (int)threadIdx.x * 32 >= lo + hl) word = 0u;
+        while (word) {
+          const int b = __ffs(word) - 1;
+          word &= word - 1u;
+          const int i = (int)threadIdx.x * 32 + b - lo;
+          if (e < cnt && i < hl) acc[i] = acc[i] + ew_topk_code<VK>(pay, codes_off, off + e) * step;
+          ++e;
+        }
+      } else {
+        const uint16_t* idx = reinterpret_cast<const uint16_t*>(pay + idx_off) + tr.idx0 +
+                              (off - (uint32_t)tr.entry0);
+        for (uint32_t e = threadIdx.x; e < cnt; e += EW_BLOCK) {
+          const int i = (int)idx[e] - lo;
+          if (i >= 0 && i < hl) acc[i] = acc[i] + ew_topk_code<VK>(pay, codes_off, off + e) * step;
+        }
+      }
+      __syncthreads();
+    }
+    const float inv_n = sa.grad_scale;
+    float* ph = p + lo;
+    const int n4 = hl >> 2;
+    for (int i = threadIdx.x; i < n4; i += EW_BLOCK) {
+      const float4 a = acc4[i];
+      if (a.x == 0.0f && a.y == 0.0f && a.z == 0.0f && a.w == 0.0f) continue;
+      float4 pu = reinterpret_cast<const float4*>(ph)[i];
+      float bz = 0.0f;
+      ew_sgd(pu.x, bz, a.x * inv_n, sa);
+      bz = 0.0f;
+      ew_sgd(pu.y, bz, a.y * inv_n, sa);
+      bz = 0.0f;
+      ew_sgd(pu.z, bz, a.z * inv_n, sa);
+      bz = 0.0f;
+      ew_sgd(pu.w, bz, a.w * inv_n, sa);
+      reinterpret_cast<float4*>(ph)[i] = pu;
+      if (shadow) {
+        const float v4[4] = {pu.x, pu.y, pu.z, pu.w};
+        ew_st4_bf16(shadow + c.start + lo + 4 * i, 4, v4);
+      }
+    }
+    for (int i = (n4 << 2) + threadIdx.x; i < hl; i += EW_BLOCK) {
+      if (acc[i] == 0.0f) continue;
+      float pv = ph[i], bz = 0.0f;
+      ew_sgd(pv, bz, acc[i] * inv_n, sa);
+      ph[i] = pv;
+      if (shadow) shadow[c.start + lo + i] = ew_f2bf(pv);
+    }
+  }
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------------------------
@@ -1885,8 +2037,15 @@ void ew_topk_decode_apply(const TopkDecodeArgs& a) {
   auto* go = reinterpret_cast<float*>(a.grad_out);
   auto* sh = reinterpret_cast<uint16_t*>(a.shadow);
   const int C = a.num_chunks;
+  // neither momentum nor weight decay nor an averaged-gradient output: the sparse kernel
+  const bool sparse = a.apply && !m && a.momentum == 0.0f && a.weight_decay == 0.0f && !go;
 #define EW_DEC(VK)                                                                                   \
-  EW_LAUNCH(k_topk_decode_apply<VK>, C, a.stream, recv, a.nranks, a.stride, chunks, tensors,         \
+  if (sparse)                                                                                       \
+    EW_LAUNCH(k_topk_decode_sparse<VK>, C, a.stream, recv, a.nranks, a.stride, chunks, tensors,      \
+              a.scales_off, a.counts_off, a.idx_off, a.codes_off, a.bitmap_off, a.inv_levels, p, sh, \
+              sa);                                                                                   \
+  else                                                                                              \
+    EW_LAUNCH(k_topk_decode_apply<VK>, C, a.stream, recv, a.nranks, a.stride, chunks, tensors,         \
             a.scales_off, a.counts_off, a.idx_off, a.codes_off, a.bitmap_off, a.inv_levels, p, m, go, \
             sh, sa,                                                                                  \
             a.apply)

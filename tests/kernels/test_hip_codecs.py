@@ -410,25 +410,29 @@ def test_pack_grads_mixed_dtypes():
             assert torch.equal(dst[o:o + n], (t.float() * 0.5).to(dt))
 
 
-def test_topk_decode_sparse_update_bitwise():
-    """Without momentum buffer and weight decay the decode reads and writes only the float4s
-    whose averaged gradient is non-zero: bitwise the dense update (p - lr * (+0) is p, -0.0
-    parameters included), shadow copy too."""
+@pytest.mark.parametrize("kind,bits", [("topk_qsgd", 8), ("topk_qsgd", 4), ("topk", 8)])
+@pytest.mark.parametrize("ratio,N", [(0.01, 2), (0.06, 5), (0.03, 11), (0.4, 3)])
+def test_topk_decode_sparse_update_bitwise(kind, bits, ratio, N):
+    """Without momentum buffer and weight decay the decode (its own kernel: half a chunk of LDS
+    at a time) reads and writes only the float4s whose averaged gradient is non-zero: bitwise the
+    dense update (p - lr * (+0) is p, -0.0 parameters included), shadow copy too.  Index lists
+    (0.06: more entries per chunk than threads), bitmaps (0.4), ranks past the prefetched ones
+    (N = 11), entries in both halves of a chunk and a partial last chunk (33333)."""
     ops.require()
-    plan = _plan([9000, 64, 33333], 0.01)
-    lay = Layout.build("topk_qsgd", plan, 8)
-    N = 2
-    recv = torch.stack([oracle.encode_topk(_grad(plan, seed=r), plan, lay, 127, "max",
+    plan = _plan([9000, 64, 33333], ratio)
+    lay = Layout.build(kind, plan, bits)
+    lv = 127 if bits == 8 else 7
+    recv = torch.stack([oracle.encode_topk(_grad(plan, seed=r), plan, lay, lv, "max",
                                            stream_key(0, 0, r)) for r in range(N)]).to(DEV)
     p0 = torch.randn(plan.length, device=DEV)
     p0[::7] = -0.0
     dp = ops.DevicePlan(plan, DEV)
     sparse, sh_s = p0.clone(), torch.zeros(plan.length, dtype=torch.bfloat16, device=DEV)
-    ops.topk_decode_apply(dp, recv, lay, 127, param=sparse, mom=None, lr=0.05,
+    ops.topk_decode_apply(dp, recv, lay, lv, param=sparse, mom=None, lr=0.05,
                           grad_scale=1.0 / N, shadow=sh_s)
     dense, sh_d = p0.clone(), torch.zeros(plan.length, dtype=torch.bfloat16, device=DEV)
     mom = torch.zeros(plan.length, device=DEV)  # a momentum buffer forces the dense pass
-    ops.topk_decode_apply(dp, recv, lay, 127, param=dense, mom=mom, lr=0.05, momentum=0.0,
+    ops.topk_decode_apply(dp, recv, lay, lv, param=dense, mom=mom, lr=0.05, momentum=0.0,
                           grad_scale=1.0 / N, shadow=sh_d)
     torch.cuda.synchronize()
     assert torch.equal(sparse.view(torch.int32), dense.view(torch.int32))

@@ -17,10 +17,16 @@ run() {  # name env... -- args
   rm -f $out/$name.graph.json.dot  # large; the JSON summary is kept
   python3 -c "import json; d=json.loads([l for l in open('$out/$name.json') if l.startswith('{')][-1]); g=json.load(open('$out/$name.graph.json')); print('$name', d['value'], d['ms_per_step'], 'enq', d['host_enqueue_ms_per_step'], d['config']['comm'], d['config']['hip_graph'], g)"
 }
-for codec in "--compress none --no-error-feedback" ""; do
+for codec in "--compress none" ""; do
   ARGS="$codec"
   tag=$([ -n "$codec" ] && echo dense || echo topk)
   run ${tag}_local EWDML_X=0 || exit 1
   run ${tag}_rccl EWDML_FORCE_PG=1 || exit 1
   run ${tag}_rccl_nomix EWDML_FORCE_PG=1 NCCL_GRAPH_MIXING_SUPPORT=0 || exit 1
+done
+# segmented (the comm graphs beside the compute segments), dense and top-k, real communicator
+for codec in "--compress none" ""; do
+  ARGS="$codec --hip-graph segmented"
+  tag=$([ -n "$codec" ] && echo dense || echo topk)
+  run ${tag}_rccl_seg EWDML_FORCE_PG=1 || exit 1
 done
