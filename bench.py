@@ -239,8 +239,9 @@ def main(argv=None):
         "host_enqueue_ms_per_step": round(enq * 1e3 / a.steps, 4),
         # multi-GPU self-validation: replicas bitwise identical after the timed steps, the
         # data-plane communicator and its first-contact probe (parallel/probe.py)
-        "replicas_identical": rep["identical"],
-        "replica_fingerprint": rep["fingerprints"][0],
+        # (None under local SGD between syncs: the replicas agree only right after a sync step)
+        "replicas_identical": rep["identical"] if rep is not None else None,
+        "replica_fingerprint": rep["fingerprints"][0] if rep is not None else None,
         "comm": tr.comm_kind,
         "rccl_world": world if tr.comm_kind == "rccl-stream" else 0,
         "comm_probe": tr.comm_probe,

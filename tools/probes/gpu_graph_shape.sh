@@ -15,7 +15,7 @@ run() {  # name env... -- args
     bench.py --gpus 1 --preset resnet50_cifar --steps 6 --warmup 4 --no-extras $ARGS \
     > $out/$name.json 2> $out/$name.err || { tail -20 $out/$name.err; return 1; }
   rm -f $out/$name.graph.json.dot  # large; the JSON summary is kept
-  python3 -c "import json; d=json.loads([l for l in open('$out/$name.json') if l.startswith('{')][-1]); g=json.load(open('$out/$name.graph.json')); print('$name', d['value'], d['ms_per_step'], 'enq', d['host_enqueue_ms_per_step'], d['config']['comm'], d['config']['hip_graph'], g)"
+  python3 -c "import json; d=json.loads([l for l in open('$out/$name.json') if l.startswith('{')][-1]); import os; g=json.load(open('$out/$name.graph.json')) if os.path.exists('$out/$name.graph.json') else 'no dump (segmented)'; print('$name', d['value'], d['ms_per_step'], 'enq', d['host_enqueue_ms_per_step'], d['config']['comm'], d['config']['hip_graph'], g)"
 }
 for codec in "--compress none" ""; do
   ARGS="$codec"
