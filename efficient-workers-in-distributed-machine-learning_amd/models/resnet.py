@@ -185,6 +185,16 @@ class ResNet(nn.Module):
             else:
                 out = F.max_pool2d(out, 3, 2, 1)
         out = self.layer4(self.layer3(self.layer2(self.layer1(out))))
+        if fused.active(out):
+            # NHWC pool kernels + the MFMA head linear (ops/head.py): no torch reduce / copy /
+            # hipBLASLt launches in the step
+            from ..ops import head as head_ops
+            from ..ops.nn import global_avg_pool
+
+            out = global_avg_pool(out)
+            if head_ops.linear_supported(self.linear, out):
+                return head_ops.head_linear(out, self.linear)
+            return self.linear(out)
         out = F.adaptive_avg_pool2d(out, 1).flatten(1)
         return self.linear(out)
 

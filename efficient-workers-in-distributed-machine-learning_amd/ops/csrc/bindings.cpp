@@ -353,6 +353,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("wino_f32_bwd_data_bn", &ew_wino_f32_bwd_data_bn);
   m.def("maxpool2_nhwc", &ew_maxpool2_nhwc);
   m.def("maxpool3s2_nhwc", &ew_maxpool3s2_nhwc);
+  m.def("gap_nhwc", &ew_gap_nhwc);
   m.def("maxpool2_fwd", &ew_maxpool2_fwd);
   m.def("maxpool2_bwd", &ew_maxpool2_bwd);
   m.def("ticket_ints", [] { return EW_TICKET_INTS; });

@@ -149,6 +149,10 @@ struct BnBwdArgs {
   int pre_nblk;  // > 0: `part` already holds [2][pre_nblk][C] sums (sum dz, sum dz*(h-mean))
   int phase;     // 0: statistics + apply, 1: statistics only (coef, dgamma, dbeta), 2: apply
 };
+// NHWC global average pool: forward x [N, HW, C] -> y [N, C]; backward x = dy [N, C] -> y = dx
+// [N, HW, C] (C % 8 == 0)
+void ew_gap_nhwc(uintptr_t x, uintptr_t y, long long N, int HW, int C, int is_bf16, int backward,
+                 uintptr_t stream);
 int ew_bn_part_floats();
 void ew_bn_relu_fwd(const BnFwdArgs& a);
 void ew_bn_relu_bwd(const BnBwdArgs& a);

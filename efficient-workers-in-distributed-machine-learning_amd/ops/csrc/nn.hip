@@ -1006,6 +1006,87 @@ void ew_maxpool3s2_nhwc(uintptr_t x, uintptr_t y, uintptr_t code, long long N, i
   EW_CHECK_LAUNCH();
 }
 
+// ---- global average pool over H x W (NHWC [N, HW, C] -> [N, C]; the ResNet head) ----
+// Forward: one thread per (n, 8 channels), the HW rows summed in order in fp32, times 1 / HW.
+// Backward: dx[n, hw, c] = dy[n, c] / HW, a vector store per (row, 8 channels).
+template <typename T>
+__global__ __launch_bounds__(EW_BLOCK) void k_gap_nhwc_fwd(const T* __restrict__ x,
+                                                           T* __restrict__ y, int N, int HW, int C,
+                                                           float inv) {
+  const uint32_t tpr = C >> 3;
+  const uint32_t v = blockIdx.x * EW_BLOCK + threadIdx.x;
+  if (v >= (uint32_t)N * tpr) return;
+  const uint32_t n = v / tpr;
+  const int c0 = (int)(v - n * tpr) * 8;
+  const T* src = x + (long long)n * HW * C + c0;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int r = 0;
+  for (; r + 4 <= HW; r += 4) {  // 4 rows' loads in flight, added in row order
+    float a[4][8];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) V8<T>::ld(src + (long long)(r + u) * C, a[u]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += a[u][j];
+  }
+  for (; r < HW; ++r) {
+    float a[8];
+    V8<T>::ld(src + (long long)r * C, a);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += a[j];
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] *= inv;
+  V8<T>::st(y + (long long)n * C + c0, acc);
+}
+
+template <typename T>
+__global__ __launch_bounds__(EW_BLOCK) void k_gap_nhwc_bwd(const T* __restrict__ dy,
+                                                           T* __restrict__ dx, long long rows,
+                                                           int HW, int C, float inv) {
+  const uint32_t tpr = C >> 3;
+  const uint32_t nvec = (uint32_t)rows * tpr;
+  for (uint32_t v = blockIdx.x * EW_BLOCK + threadIdx.x; v < nvec; v += gridDim.x * EW_BLOCK) {
+    const uint32_t row = v / tpr;
+    const int c0 = (int)(v - row * tpr) * 8;
+    float d[8];
+    V8<T>::ld(dy + (long long)(row / HW) * C + c0, d);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) d[j] *= inv;
+    V8<T>::st(dx + (long long)row * C + c0, d);
+  }
+}
+
+void ew_gap_nhwc(uintptr_t x, uintptr_t y, long long N, int HW, int C, int is_bf16, int backward,
+                 uintptr_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const float inv = 1.0f / (float)HW;
+  if (!backward) {
+    const int grid = (int)((N * (C / 8) + EW_BLOCK - 1) / EW_BLOCK);
+    if (is_bf16)
+      hipLaunchKernelGGL(k_gap_nhwc_fwd<uint16_t>, dim3(grid), dim3(EW_BLOCK), 0, s,
+                         reinterpret_cast<const uint16_t*>(x), reinterpret_cast<uint16_t*>(y),
+                         (int)N, HW, C, inv);
+    else
+      hipLaunchKernelGGL(k_gap_nhwc_fwd<float>, dim3(grid), dim3(EW_BLOCK), 0, s,
+                         reinterpret_cast<const float*>(x), reinterpret_cast<float*>(y), (int)N,
+                         HW, C, inv);
+  } else {  // x = dy [N, C], y = dx [N, HW, C]
+    const long long rows = N * HW;
+    const int grid = ew_grid_vec(rows * (C / 8));
+    if (is_bf16)
+      hipLaunchKernelGGL(k_gap_nhwc_bwd<uint16_t>, dim3(grid), dim3(EW_BLOCK), 0, s,
+                         reinterpret_cast<const uint16_t*>(x), reinterpret_cast<uint16_t*>(y), rows,
+                         HW, C, inv);
+    else
+      hipLaunchKernelGGL(k_gap_nhwc_bwd<float>, dim3(grid), dim3(EW_BLOCK), 0, s,
+                         reinterpret_cast<const float*>(x), reinterpret_cast<float*>(y), rows, HW,
+                         C, inv);
+  }
+  EW_CHECK_LAUNCH();
+}
+
 // ================================================================================================
 // Cross-entropy loss (mean over the batch) of [B, K] logits (bf16 or fp32) and int64 labels, as
 // F.cross_entropy(logits.float(), y): forward = one block (one wave per row, fixed-order

@@ -144,6 +144,14 @@ def _lin_ok(lin, x_width, dtype):
             and x_width % 32 == 0 and w.data_ptr() % 16 == 0)
 
 
+def linear_supported(lin, x) -> bool:
+    """Whether ``lin(x)`` (one ``nn.Linear`` on a device [B, K] activation) runs the head kernels."""
+    return (_ENABLED and isinstance(lin, nn.Linear) and x.is_cuda and x.dim() == 2
+            and x.dtype in (torch.bfloat16, torch.float32) and _lin_ok(lin, x.shape[1], x.dtype)
+            and x.is_contiguous() and x.data_ptr() % 16 == 0 and 0 < x.shape[0]
+            and x.shape[0] * max(x.shape[1], lin.out_features) < 2 ** 31)
+
+
 def supported(cls, x) -> bool:
     mods = _head_layout(cls)
     if not _ENABLED or mods is None or not (x.is_cuda and x.dim() == 2

@@ -366,6 +366,45 @@ def maxpool3x3s2(x):
     return _MaxPool3s2.apply(x)
 
 
+class _GlobalAvgPool(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        C_ = require()
+        N, C, H, W = x.shape
+        y = torch.empty((N, C), dtype=x.dtype, device=x.device)
+        C_.gap_nhwc(_ptr(x), _ptr(y), N, H * W, C, int(x.dtype == torch.bfloat16), 0, _stream())
+        ctx.shape = x.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        C_ = require()
+        N, C, H, W = ctx.shape
+        dy = dy.contiguous()
+        if dy.data_ptr() % 16:
+            dy = dy.clone()
+        dx = torch.empty((N, C, H, W), dtype=dy.dtype, device=dy.device,
+                         memory_format=torch.channels_last)
+        C_.gap_nhwc(_ptr(dy), _ptr(dx), N, H * W, C, int(dy.dtype == torch.bfloat16), 1,
+                    _stream())
+        return dx
+
+
+def global_avg_pool(x):
+    """``F.adaptive_avg_pool2d(x, 1).flatten(1)`` (the ResNet head's pool): HIP kernels for device
+    bf16/fp32 channels_last tensors with C % 8 == 0 (fp32 sums in row order), torch otherwise."""
+    import torch.nn.functional as F
+
+    x = materialize(x)
+    ok = (x.is_cuda and x.dim() == 4 and x.dtype in (torch.bfloat16, torch.float32)
+          and x.numel() > 0 and x.numel() < 2 ** 31 and x.shape[1] % 8 == 0
+          and x.is_contiguous(memory_format=torch.channels_last) and x.data_ptr() % 16 == 0
+          and available())
+    if not ok:
+        return F.adaptive_avg_pool2d(x, 1).flatten(1)
+    return _GlobalAvgPool.apply(x)
+
+
 _UNIT_GRAD = [None]  # (weakref to the trainer's persistent d(loss)/d(loss) = 1 seed, version)
 
 

@@ -531,3 +531,24 @@ def test_head_linear_fp32_dropout_edges(rows, C, p):
     assert torch.allclose(lin.bias.grad.double(), dyr.sum(0), rtol=1e-5, atol=1e-5)
     assert _rel64(x.grad, dyr @ lin.weight.detach().double()) < 1e-5
     assert _rel64(lin.weight.grad, dyr.t() @ x.detach().double()) < 1e-5
+
+
+@pytest.mark.parametrize("shape", [(128, 2048, 4, 4), (6, 64, 7, 5), (3, 512, 1, 1)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_global_avg_pool_matches_torch(shape, dtype):
+    """ResNet head pool (NHWC HIP kernels) against the fp32 torch reference, both directions."""
+    fnn = _ops()
+    torch.manual_seed(4)
+    x = torch.randn(shape, device="cuda").to(dtype).contiguous(memory_format=torch.channels_last)
+    xx = x.clone().requires_grad_(True)
+    y = fnn.global_avg_pool(xx)
+    xr = x.float().clone().requires_grad_(True)
+    yr = F.adaptive_avg_pool2d(xr, 1).flatten(1)
+    tol = 1e-6 if dtype == torch.float32 else 1e-2
+    assert y.shape == yr.shape and y.dtype == dtype
+    assert _rel(y, yr) < tol
+    dy = torch.randn(yr.shape, device="cuda")
+    y.backward(dy.to(dtype))
+    yr.backward(dy)
+    assert xx.grad.is_contiguous(memory_format=torch.channels_last)
+    assert _rel(xx.grad, xr.grad) < tol

@@ -52,12 +52,17 @@ def summarize(rows, frac=0.5, gap_ns=150_000_000, steps=None):
         if s - end >= gap_ns:
             gaps.append((end, s))
         end = max(end, e)
-    # bench.py (EWDML_PROF_GAP=1) idles before and after the timed loop: the window between the
-    # last two gaps; a trace with one gap: everything after it
+    # bench.py (EWDML_PROF_GAP=1) idles before and after the timed loop: of the windows between
+    # two consecutive gaps, the one with the most kernels (teardown after the loop can add idle
+    # gaps of its own); a trace with one gap: everything after it
     stop = None
     if len(gaps) >= 2:
-        cut, stop = gaps[-2][1], gaps[-1][0]
-        how = "between the last two idle gaps"
+        def count(a, b):
+            return sum(1 for r in rows if a <= r[0] < b)
+
+        i = max(range(len(gaps) - 1), key=lambda j: (count(gaps[j][1], gaps[j + 1][0]), j))
+        cut, stop = gaps[i][1], gaps[i + 1][0]
+        how = "between two idle gaps (the busiest window)"
     elif gaps:
         cut = gaps[-1][1]
         how = "after last idle gap"
