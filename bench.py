@@ -217,7 +217,8 @@ def main(argv=None):
                    "bf16_params": tr.flat.shadow is not None,
                    "grad_mode": "views" if tr.flat.attach_grads else "pointers",
                    "layout": "nhwc" if tr.channels_last else "nchw",
-                   "fused_nn": a.fused_nn, "comm": tr.comm_kind},
+                   "fused_nn": a.fused_nn, "comm": tr.comm_kind,
+                   "wgrad_stream": bool(getattr(tr, "wgrad_stream", False))},
         # overlap that actually happens: a collective to hide (world > 1) issued while backward
         # still runs -- a segmented graph with at least one comm-stream graph, or eager steps
         # with the side stream and more than one bucket

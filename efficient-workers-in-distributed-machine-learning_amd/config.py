@@ -139,6 +139,12 @@ class Config:
     # segment) from HIP events on the step's stream, in the JSONL and summary.json; serialises the
     # eager step (no side stream) and makes --hip-graph auto split the graph at the collectives
     phase_timing: bool = False
+    # weight gradients of the MFMA convs on a second stream, beside the backward-data chain
+    # (auto = on for deep conv nets, >= 30 convolutions, with pointer-mode gradients).  Measured
+    # +1.7 % on ResNet-50 CIFAR and -6 % on VGG-11, but the fork / join per conv makes the
+    # captured graph a DAG whose replay costs ~5 ms of host time per ResNet-50 step (0.12 ms
+    # linear): off by default (profiles/ab/README.md)
+    wgrad_stream: str = "off"
     summary_file: Optional[str] = None  # rank 0's run summary (default <train_dir>/summary.json)
     inject_fault: Optional[str] = None  # "rank:step" -> that rank raises at that step (tests)
     comm_timeout: float = 600.0
@@ -290,6 +296,7 @@ def build_parser(prog="distributed_nn.py") -> argparse.ArgumentParser:
     a("--profile", type=int, default=0)
     a("--roctx", action="store_true", default=False)
     a("--phase-timing", action="store_true", default=False)
+    a("--wgrad-stream", choices=["auto", "on", "off"], default=d.wgrad_stream)
     a("--summary-file", type=str, default=None)
     a("--inject-fault", type=str, default=None)
     a("--comm-timeout", type=float, default=d.comm_timeout)

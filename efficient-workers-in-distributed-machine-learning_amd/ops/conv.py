@@ -81,6 +81,17 @@ _WINO_WG_SPLITS = int(os.environ.get("EWDML_WINO_WG_SPLITS", "4"))
 # exchange engine before it encodes a bucket, so a bucket's gradients are complete when its
 # encode starts.
 _DEFER_WOUT = os.environ.get("EWDML_WINO_DEFER_WOUT", "1") != "0"
+# weight gradients on a second stream: a conv's wgrad runs beside the backward-data chain of the
+# layers before it (the chain is the backward's critical path).  Joined before any consumer reads
+# a gradient (join_wgrad: flush_pending, the end of the backward).
+_WGRAD_SIDE = False
+# weight-gradient launches collected before one fork to the side stream: each fork is a
+# cross-stream edge of the captured graph, which costs replay time of its own
+_WGRAD_BATCH = int(os.environ.get("EWDML_WGRAD_BATCH", "1"))
+_SIDE = {}
+_SIDE_PENDING = set()
+_SIDE_QUEUE = []  # (device index, launch closure, tensors it reads / writes)
+SIDE_LAUNCHES = 0  # weight gradients issued on the side stream (tests)
 # fp32 stride-2 3x3 / 1x1 convs (ResNet down-sampling) on the MFMA kernels: opt-in
 # (EWDML_CONV_S2=1).  Measured slower than MIOpen's tuned (find-mode) solvers on every ResNet-50
 # shape, 2078 vs 1740 us per step for the six layers, ResNet-50 CIFAR 8.38K vs 8.53K img/s
@@ -109,10 +120,77 @@ def _job_fixup(job):
     return dst, (g, dw)
 
 
+def _dw_may_lag(ctx):
+    """Whether this conv's dw may be written after the backward returns it (deferred transform,
+    side-stream launch): its parameter's gradient is installed, not accumulated (grad None, no
+    tied use), and nothing but the exchange engine's hooks (which join / flush before reading)
+    looks at it during the backward."""
+    p = getattr(ctx, "w_param", None)
+    if p is None or p.grad is not None or torch.is_grad_enabled():
+        return False
+    if getattr(p, "_backward_hooks", None) or getattr(p, "_ew_tied", False):
+        return False
+    eng = getattr(p, "_ew_engine_hooks", 0)
+    post = getattr(p, "_post_accumulate_grad_hooks", None)
+    return not post or len(post) <= eng
+
+
+def _wgrad_side(device):
+    """The weight-gradient stream of ``device`` when side-stream weight gradients are on
+    (set_wgrad_stream; the trainer's --wgrad-stream), else None."""
+    if not _WGRAD_SIDE:
+        return None
+    s = _SIDE.get(device.index)
+    if s is None:
+        s = _SIDE[device.index] = torch.cuda.Stream(device)
+    return s
+
+
+def set_wgrad_stream(on: bool):
+    """Side-stream weight gradients on / off.  The trainer switches them on around its own
+    backward passes only and joins (join_wgrad) right after: every other caller of backward()
+    keeps single-stream convs."""
+    global _WGRAD_SIDE
+    _WGRAD_SIDE = bool(on)
+
+
+def _issue_side():
+    """Issue the collected weight-gradient launches on the side stream, after everything the
+    current stream has issued (their inputs)."""
+    if not _SIDE_QUEUE:
+        return
+    jobs = list(_SIDE_QUEUE)
+    _SIDE_QUEUE.clear()
+    cur = torch.cuda.current_stream()
+    for idx in sorted({j[0] for j in jobs}):
+        _SIDE[idx].wait_stream(cur)
+        _SIDE_PENDING.add(idx)
+    global SIDE_LAUNCHES
+    SIDE_LAUNCHES += len(jobs)
+    for idx, fn, keep in jobs:
+        side = _SIDE[idx]
+        for t in keep:
+            if t is not None:
+                t.record_stream(side)
+        with torch.cuda.stream(side):
+            fn()
+
+
+def join_wgrad():
+    """The current stream waits for the weight gradients issued on the side stream."""
+    _issue_side()
+    if _SIDE_PENDING:
+        cur = torch.cuda.current_stream()
+        for idx in list(_SIDE_PENDING):
+            cur.wait_stream(_SIDE[idx])
+        _SIDE_PENDING.clear()
+
+
 def flush_pending(final=False):
     """Run a deferred weight-gradient output transform now (``final`` is accepted for the end-of-
     backward callback; every flush runs the job).  Returns True."""
     global _PENDING
+    join_wgrad()  # every caller is about to read (or transform) a weight gradient
     job = _PENDING
     if job is None:
         return True
@@ -485,29 +563,44 @@ class _Conv(torch.autograd.Function):
                 sink.grad, sink.taken = None, True
         if ctx.needs_input_grad[1]:
             dw = torch.empty_like(w, memory_format=torch.channels_last)
-            if m:
-                # dw = G^T (sum over tiles of (A dy A^T) V) G: a^2 GEMMs of K = N*H*W/m^2
-                V = ctx.wino[1]
-                dU = torch.empty(aa * Nc * C, dtype=torch.float32, device=x.device)
-                slabs = torch.empty(_WINO_WG_SPLITS * aa * Nc * C + 64, dtype=torch.float32,
-                                    device=x.device)
-                # one pending job at a time: an earlier one is flushed first (if it cannot be
-                # yet, this layer's transform runs now)
-                if _POISON_DW:
-                    dw.fill_(float("nan"))
-                defer = _can_defer(ctx) and flush_pending()
-                split = C_.wino_f32_wgrad(_ptr(dy), _ptr(V), _ptr(dw), _ptr(D), d_ready,
-                                          _ptr(dU), _ptr(slabs), slabs.numel(), N, H, W, C, Nc,
-                                          m, int(defer), _stream())
-                if defer:
-                    global _PENDING
-                    _PENDING = (slabs if split > 1 else dU, split, ctx.w_param, Nc, C, m,
-                                (dU, slabs), dw.untyped_storage(), tuple(dw.shape), dw.stride())
-                    torch.autograd.Variable._execution_engine.queue_callback(_flush_final)
+            side = _wgrad_side(x.device) if _dw_may_lag(ctx) else None
+            V = ctx.wino[1] if m else None
+
+            def launch_wgrad():
+                if m:
+                    # dw = G^T (sum over tiles of (A dy A^T) V) G: a^2 GEMMs of K = N*H*W/m^2
+                    dU = torch.empty(aa * Nc * C, dtype=torch.float32, device=x.device)
+                    slabs = torch.empty(_WINO_WG_SPLITS * aa * Nc * C + 64,
+                                        dtype=torch.float32, device=x.device)
+                    # one pending job at a time: an earlier one is flushed first (if it cannot
+                    # be yet, this layer's transform runs now)
+                    if _POISON_DW:
+                        dw.fill_(float("nan"))
+                    defer = side is None and _can_defer(ctx) and flush_pending()
+                    split = C_.wino_f32_wgrad(_ptr(dy), _ptr(V), _ptr(dw), _ptr(D), d_ready,
+                                              _ptr(dU), _ptr(slabs), slabs.numel(), N, H, W, C,
+                                              Nc, m, int(defer), _stream())
+                    if defer:
+                        global _PENDING
+                        _PENDING = (slabs if split > 1 else dU, split, ctx.w_param, Nc, C, m,
+                                    (dU, slabs), dw.untyped_storage(), tuple(dw.shape),
+                                    dw.stride())
+                        torch.autograd.Variable._execution_engine.queue_callback(_flush_final)
+                else:
+                    wgrad = C_.conv_f32_wgrad if f32 else C_.conv_wgrad
+                    wsw = _ws(x.device)  # the current stream's slabs (the side stream's own)
+                    wgrad(_ptr(dy), _ptr(x), _ptr(dw), _ptr(wsw), wsw.numel(), N, H, W, C, Nc, k,
+                          _stream())
+
+            if side is None:
+                launch_wgrad()
             else:
-                wgrad = C_.conv_f32_wgrad if f32 else C_.conv_wgrad
-                wgrad(_ptr(dy), _ptr(x), _ptr(dw), _ptr(ws), ws.numel(), N, H, W, C, Nc, k,
-                      _stream())
+                # queued (holding its tensors, so their memory is not reused), issued on the side
+                # stream with the next _WGRAD_BATCH - 1 ones or at the first gradient read
+                _SIDE_QUEUE.append((x.device.index, launch_wgrad,
+                                    (dy, x, dw, V, D)))
+                if len(_SIDE_QUEUE) >= _WGRAD_BATCH:
+                    _issue_side()
         ctx.wino = None
         return dx, dw, None, None
 

@@ -137,6 +137,12 @@ class Trainer:
         ptr_grads = (self.cuda and cfg.topology == "allgather"
                      and os.environ.get("EWDML_GRAD_VIEWS") != "1")
         bf16_params = ptr_grads and cfg.amp == "bf16" and cfg.param_dtype == "auto"
+        # weight gradients beside the backward-data chain (ops/conv.py), switched on around this
+        # trainer's backward passes only: deep conv nets
+        n_conv = sum(isinstance(m, torch.nn.Conv2d) for m in model.modules())
+        self.wgrad_stream = bool(self.cuda and cfg.fused_nn == "on" and (
+            cfg.wgrad_stream == "on"
+            or (cfg.wgrad_stream == "auto" and ptr_grads and n_conv >= 30)))
         bucket_bytes = int(cfg.bucket_mb * (1 << 20))
         # --hip-graph auto for the all-to-all exchange: overlap large dense collectives with
         # backward at N > 1 (segmented graphs), one graph otherwise (plan_graph_mode); decided
@@ -307,7 +313,17 @@ class Trainer:
                     from ..ops.nn import set_unit_grad
 
                     set_unit_grad(seed)
-            loss.backward(seed)
+            if self.cuda:
+                from ..ops.conv import join_wgrad, set_wgrad_stream
+
+                set_wgrad_stream(self.wgrad_stream)
+                try:
+                    loss.backward(seed)
+                finally:
+                    set_wgrad_stream(False)
+                    join_wgrad()  # weight gradients issued on the side stream
+            else:
+                loss.backward(seed)
         if self.clock is not None:
             self.clock.mark("backward")
         return loss, out

@@ -460,3 +460,46 @@ def test_method6_device_best_worker_two_ranks(tmp_path):
     for a, b in zip(res[0]["bn"], res[1]["bn"]):
         torch.testing.assert_close(a, b, rtol=0, atol=0)
     assert res[0]["best"] == res[1]["best"] and len(res[0]["best"]) == 2
+
+
+RESNET = ["--network", "ResNet50", "--dataset", "Cifar10", "--batch-size", "32",
+          "--synthetic-size", "256", "--momentum", "0.9", "--lr", "0.02", "--eval-freq", "0",
+          "--quiet", "--device", "cuda", "--amp", "none", "--graph-warmup", "2"]
+
+
+@pytest.mark.parametrize("graph", ["off", "full", "segmented"])
+@pytest.mark.parametrize("codec", ["topk_qsgd", "none"])
+def test_wgrad_side_stream_is_bitwise_single_stream(graph, codec):
+    """--wgrad-stream (ResNet-50: weight gradients of the MFMA convs on a second stream beside
+    the backward-data chain, joined before any gradient is read) trains bit for bit as the
+    single-stream step: eager, one captured graph (fork / join inside it) and segmented graphs
+    (the exchange's bucket hooks join before they encode)."""
+    ops.require()
+    from ewdml.ops import conv as cv
+
+    # deterministic runs to compare: MIOpen's stride-2 backward solvers accumulate with atomics
+    # (run-to-run bits differ), so the six stride-2 convs take the MFMA kernels here
+    cv.set_stride2(True)
+    flags = RESNET + ["--compress", codec, "--hip-graph", graph]
+    try:
+        ref, l_ref = _run(flags + ["--wgrad-stream", "off"], 4)
+        ref2, l_ref2 = _run(flags + ["--wgrad-stream", "off"], 4)
+        assert l_ref2 == l_ref, "single-stream runs differ: nothing to compare against"
+        _check_side_run(flags, ref, l_ref)
+    finally:
+        cv.set_stride2(False)
+    ref.close()
+    ref2.close()
+
+
+def _check_side_run(flags, ref, l_ref):
+    from ewdml.ops import conv as cv
+
+    assert not ref.wgrad_stream
+    before = cv.SIDE_LAUNCHES
+    tr, l = _run(flags + ["--wgrad-stream", "auto"], 4)
+    assert tr.wgrad_stream and cv.SIDE_LAUNCHES > before  # auto: on for ResNet-50
+    assert l == l_ref
+    assert torch.equal(tr.flat.data.view(torch.int32), ref.flat.data.view(torch.int32))
+    assert not cv._WGRAD_SIDE and not cv._SIDE_QUEUE and not cv._SIDE_PENDING
+    tr.close()
