@@ -1483,6 +1483,72 @@ __device__ __forceinline__ float ew_topk_code(const uint8_t* pay, int codes_off,
   return (float)(q >= 8 ? q - 16 : q);
 }
 
+// Every rank's first list entry of this thread (e = thread index: all of a chunk's entries at
+// <= 2.5 % density) for the first PR ranks, loaded before any is summed -- one round trip for all
+// of them instead of one per rank -- plus each of those ranks' count and scale (any tensor kind),
+// kept in registers for the rank-ordered sum.  Loads are clamped into the tensor's entry range and
+// masked, not branched around (a branch makes the compiler wait for every load at its merge).
+template <int VK, int PR>
+__device__ __forceinline__ void topk_decode_prefetch(
+    const uint8_t* __restrict__ recv, int nranks, long long stride, const ChunkRow& c,
+    const TensorRow& tr, int scales_off, int counts_off, int idx_off, int codes_off,
+    float inv_levels, const uint32_t* s_off, uint32_t eend, bool list, float (&pre_v)[PR],
+    int (&pre_i)[PR], uint32_t (&pre_c)[PR], float (&pre_s)[PR]) {
+#pragma unroll
+  for (int r = 0; r < PR; ++r) {
+    pre_i[r] = -1;
+    pre_v[r] = 0.0f;
+    pre_c[r] = 0u;
+    pre_s[r] = 1.0f;
+    if (r < nranks) {
+      const uint8_t* pay = recv + r * stride;
+      const uint32_t off = s_off[r];
+      uint32_t cnt = reinterpret_cast<const uint16_t*>(pay + counts_off)[blockIdx.x];
+      cnt = off >= eend ? 0u : min(cnt, eend - off);
+      const float step = VK != VK_F32
+          ? reinterpret_cast<const float*>(pay + scales_off)[c.tensor] * inv_levels : 1.0f;
+      pre_c[r] = cnt;
+      pre_s[r] = step;
+      if (list) {
+        const uint32_t e = threadIdx.x;
+        const uint32_t pe = min(off + min(e, cnt ? cnt - 1u : 0u), eend - 1u);
+        const float prod = ew_topk_code<VK>(pay, codes_off, pe) * step;
+        const int i = reinterpret_cast<const uint16_t*>(pay + idx_off)[tr.idx0 + (pe - (uint32_t)tr.entry0)];
+        if (e < cnt) {
+          pre_v[r] = prod;
+          pre_i[r] = i;
+        }
+      }
+    }
+  }
+}
+
+// Rank r's entry count in this chunk (clamped) and value step: from the prefetch registers for
+// the first PR ranks, loaded otherwise.
+template <int VK, int PR>
+__device__ __forceinline__ void topk_decode_rank_cs(const uint8_t* pay, int r, const ChunkRow& c,
+                                                    int counts_off, int scales_off,
+                                                    float inv_levels, uint32_t off, uint32_t eend,
+                                                    const uint32_t (&pre_c)[PR],
+                                                    const float (&pre_s)[PR], uint32_t& cnt,
+                                                    float& step) {
+  if (r < PR) {
+    cnt = 0u;
+    step = 1.0f;
+#pragma unroll
+    for (int q = 0; q < PR; ++q)
+      if (q == r) {
+        cnt = pre_c[q];
+        step = pre_s[q];
+      }
+    return;
+  }
+  cnt = reinterpret_cast<const uint16_t*>(pay + counts_off)[blockIdx.x];
+  cnt = off >= eend ? 0u : min(cnt, eend - off);
+  step = VK != VK_F32
+      ? reinterpret_cast<const float*>(pay + scales_off)[c.tensor] * inv_levels : 1.0f;
+}
+
 // Receive side: one block per chunk.  Sum the N ranks' entries for this chunk in rank order in an
 // LDS accumulator (indices are unique within a rank, so no atomics), scale by 1/N, then either
 // write the averaged gradient and/or apply the SGD update to the chunk's parameters.
@@ -1556,40 +1622,22 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_decode_apply(
   // masked, not branched around (a branch makes the compiler wait for every load at its merge).
   constexpr int PR = 8;
   const uint32_t eend = (uint32_t)(tr.entry0 + tr.k);  // never read past the tensor's entries
-  float pre_v[PR];
+  float pre_v[PR], pre_s[PR];
   int pre_i[PR];
+  uint32_t pre_c[PR];
   const bool list = tr.bm0 < 0;
-  if (list) {
-#pragma unroll
-    for (int r = 0; r < PR; ++r) {
-      pre_i[r] = -1;
-      pre_v[r] = 0.0f;
-      if (r < nranks) {
-        const uint8_t* pay = recv + r * stride;
-        const uint32_t off = s_off[r];
-        uint32_t cnt = reinterpret_cast<const uint16_t*>(pay + counts_off)[blockIdx.x];
-        cnt = off >= eend ? 0u : min(cnt, eend - off);
-        const float step = VK != VK_F32
-            ? reinterpret_cast<const float*>(pay + scales_off)[c.tensor] * inv_levels : 1.0f;
-        const uint32_t e = threadIdx.x;
-        const uint32_t pe = min(off + min(e, cnt ? cnt - 1u : 0u), eend - 1u);
-        const float prod = ew_topk_code<VK>(pay, codes_off, pe) * step;
-        const int i = reinterpret_cast<const uint16_t*>(pay + idx_off)[tr.idx0 + (pe - (uint32_t)tr.entry0)];
-        if (e < cnt) {
-          pre_v[r] = prod;
-          pre_i[r] = i;
-        }
-      }
-    }
-  }
+  topk_decode_prefetch<VK, PR>(recv, nranks, stride, c, tr, scales_off, counts_off, idx_off,
+                               codes_off, inv_levels, s_off, eend, list, pre_v, pre_i, pre_c,
+                               pre_s);
   for (int r = 0; r < nranks; ++r) {
     const uint8_t* pay = recv + r * stride;
     const uint32_t off = s_off[r];
-    // clamp to the tensor's entry range: a corrupted payload must not read out of bounds
-    uint32_t cnt = reinterpret_cast<const uint16_t*>(pay + counts_off)[blockIdx.x];
-    cnt = off >= eend ? 0u : min(cnt, eend - off);
-    float step = 1.0f;
-    if (VK != VK_F32) step = reinterpret_cast<const float*>(pay + scales_off)[c.tensor] * inv_levels;
+    // clamped to the tensor's entry range (a corrupted payload must not read out of bounds);
+    // the first PR ranks' count and scale were loaded with the prefetch
+    uint32_t cnt;
+    float step;
+    topk_decode_rank_cs<VK, PR>(pay, r, c, counts_off, scales_off, inv_levels, off, eend, pre_c,
+                                pre_s, cnt, step);
     if (list && r < PR) {  // the prefetched first entry, then any beyond the block's width
 #pragma unroll
       for (int q = 0; q < PR; ++q)
@@ -1709,33 +1757,14 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_decode_sparse(
   }
   __syncthreads();
   constexpr int PR = 8;
-  const uint32_t eend = (uint32_t)(tr.entry0 + tr.k);
-  float pre_v[PR];
+  const uint32_t eend = (uint32_t)(tr.entry0 + tr.k);  // never read past the tensor's entries
+  float pre_v[PR], pre_s[PR];
   int pre_i[PR];
+  uint32_t pre_c[PR];
   const bool list = tr.bm0 < 0;
-  if (list) {
-#pragma unroll
-    for (int r = 0; r < PR; ++r) {
-      pre_i[r] = -1;
-      pre_v[r] = 0.0f;
-      if (r < nranks) {
-        const uint8_t* pay = recv + r * stride;
-        const uint32_t off = s_off[r];
-        uint32_t cnt = reinterpret_cast<const uint16_t*>(pay + counts_off)[blockIdx.x];
-        cnt = off >= eend ? 0u : min(cnt, eend - off);
-        const float step = VK != VK_F32
-            ? reinterpret_cast<const float*>(pay + scales_off)[c.tensor] * inv_levels : 1.0f;
-        const uint32_t e = threadIdx.x;
-        const uint32_t pe = min(off + min(e, cnt ? cnt - 1u : 0u), eend - 1u);
-        const float prod = ew_topk_code<VK>(pay, codes_off, pe) * step;
-        const int i = reinterpret_cast<const uint16_t*>(pay + idx_off)[tr.idx0 + (pe - (uint32_t)tr.entry0)];
-        if (e < cnt) {
-          pre_v[r] = prod;
-          pre_i[r] = i;
-        }
-      }
-    }
-  }
+  topk_decode_prefetch<VK, PR>(recv, nranks, stride, c, tr, scales_off, counts_off, idx_off,
+                               codes_off, inv_levels, s_off, eend, list, pre_v, pre_i, pre_c,
+                               pre_s);
   for (int lo = 0; lo < c.len; lo += HALF) {  // block-uniform
     const int hl = min(c.len - lo, HALF);
     if (lo) __syncthreads();  // the previous half's apply has read the accumulator
@@ -1744,10 +1773,10 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_decode_sparse(
     for (int r = 0; r < nranks; ++r) {
       const uint8_t* pay = recv + r * stride;
       const uint32_t off = s_off[r];
-      uint32_t cnt = reinterpret_cast<const uint16_t*>(pay + counts_off)[blockIdx.x];
-      cnt = off >= eend ? 0u : min(cnt, eend - off);
-      float step = 1.0f;
-      if (VK != VK_F32) step = reinterpret_cast<const float*>(pay + scales_off)[c.tensor] * inv_levels;
+      uint32_t cnt;
+      float step;
+      topk_decode_rank_cs<VK, PR>(pay, r, c, counts_off, scales_off, inv_levels, off, eend, pre_c,
+                                  pre_s, cnt, step);
       if (list && r < PR) {
 #pragma unroll
         for (int q = 0; q < PR; ++q) {
