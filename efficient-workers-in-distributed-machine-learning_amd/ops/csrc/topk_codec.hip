@@ -553,7 +553,10 @@ __device__ __forceinline__ void topk_write_cands(
     int* __restrict__ lb_err, uint32_t n, const uint2* __restrict__ cs, uint32_t* ws,
     uint32_t* s_lb, int lb_fault) {
   __shared__ uint32_t bm[EW_BM_WORDS];
+  // the tensor's selection state, loaded together before the look-back's barriers
   const uint32_t thr = state[c.tensor * 4];
+  const uint32_t need = state[c.tensor * 4 + 1];
+  const float scale = __uint_as_float(state[c.tensor * 4 + 2]);
   const uint32_t eend = (uint32_t)(tr.entry0 + tr.k);
   const bool bitmap = tr.bm0 >= 0;
   if (bitmap)
@@ -565,14 +568,12 @@ __device__ __forceinline__ void topk_write_cands(
     eq += k == thr;
   }
   topk_lookback(gt, eq, c, tr, lb, lb_err, s_lb, lb_fault);  // ends with __syncthreads
-  const uint32_t need = state[c.tensor * 4 + 1];
   const uint32_t gb = s_lb[0], eb = s_lb[1], gtc = s_lb[2], eqc = s_lb[3];
   const uint32_t left_ties = need > eb ? need - eb : 0u;
   const uint32_t ties = left_ties < eqc ? left_ties : eqc;
   const uint32_t ebase = (uint32_t)tr.entry0 + gb + (need < eb ? need : eb);
   if (threadIdx.x == 0)
     reinterpret_cast<uint16_t*>(payload + counts_off)[blockIdx.x] = (uint16_t)(gtc + ties);
-  const float scale = __uint_as_float(state[c.tensor * 4 + 2]);
   const float inv = scale > 0.0f ? levels / scale : 0.0f;
   const float step = VK != VK_F32 ? scale * inv_levels : 0.0f;
   if (threadIdx.x == 0 && c.local == 0) reinterpret_cast<float*>(payload + scales_off)[c.tensor] = scale;
@@ -640,6 +641,10 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_write(
     uint32_t* __restrict__ rz2, uint32_t rz2_words) {
   __shared__ uint32_t ws[EW_WAVES];
   __shared__ uint32_t s_lb[2 * EW_WAVES];
+  // loads that depend on the block index alone first: the chunk row and (predictive encode) this
+  // chunk's candidate segment, in flight together; then the tensor's rows
+  const ChunkRow c = chunks[blockIdx.x];
+  const uint32_t pk_n = PK ? ccnt[blockIdx.x] : 0u, pk_b = PK ? cbase[blockIdx.x] : 0u;
   // the histograms / max-key replicas are dead once the thresholds are selected: clear them here
   // for the next encode of this bucket (replaces a per-step memset node; first use: zero-alloc).
   // The predictive path uses one histogram copy per pass: three short ranges (rz1, rz2 too).
@@ -652,13 +657,11 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_write(
       rz2[i] = 0u;
   }
   const uint32_t key = keyp ? *keyp : key_arg;  // device key: fresh per replay of a captured graph
-  const ChunkRow c = chunks[blockIdx.x];
   const TensorRow tr = tensors[c.tensor];
   if (PK && pst[c.tensor * 8 + 3]) {  // predictive fast path: the chunk's candidates only
     topk_write_cands<VK, EF>(c, tr, resid, vel, state, payload, scales_off, idx_off, codes_off,
                              bitmap_off, counts_off, levels, inv_levels, key, bucket_offset, lb,
-                             lb_err, ccnt[blockIdx.x], pcand + tr.cap0 + cbase[blockIdx.x], ws,
-                             s_lb, lb_fault);
+                             lb_err, pk_n, pcand + tr.cap0 + pk_b, ws, s_lb, lb_fault);
     return;
   }
   const float* flat = EF ? resid : nullptr;  // EF: hist0 staged e = g + r in the residual
