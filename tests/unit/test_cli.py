@@ -112,3 +112,22 @@ def test_ef21_rejected_at_parse_time_on_the_gpu(monkeypatch):
     monkeypatch.setenv("EWDML_ORACLE", "1")
     monkeypatch.setenv("EWDML_GRAD_VIEWS", "1")
     assert ewdml.parse_args(["--ef-mode", "ef21", "--device", "cuda"]).ef_mode == "ef21"
+
+
+def test_wgrad_stream_flag():
+    """--wgrad-stream: off by default (the DAG graph's replay cost, profiles/ab/README.md), on /
+    auto accepted, anything else rejected."""
+    assert ewdml.parse_args([]).wgrad_stream == "off"
+    for v in ("on", "auto", "off"):
+        assert ewdml.parse_args(["--wgrad-stream", v]).wgrad_stream == v
+    with pytest.raises(SystemExit):
+        ewdml.parse_args(["--wgrad-stream", "maybe"])
+
+
+def test_wgrad_stream_is_scoped_to_the_trainer_backward():
+    """The side-stream switch is off outside a trainer's backward (so a user's own backward()
+    never runs weight gradients on a second stream) and nothing is queued at import."""
+    from ewdml.ops import conv as cv
+
+    assert cv._WGRAD_SIDE is False and not cv._SIDE_QUEUE and not cv._SIDE_PENDING
+    cv.join_wgrad()  # no-op without side work (no device needed)
