@@ -1187,6 +1187,11 @@ CfPlan cf_plan(int M, int Ncol, int ksteps, long long ws_floats, int batch) {
       return CfPlan{bm, bn, (ksteps + kps - 1) / kps, kps};
     }
   }
+  // the reduction launch's fixed cost (us); EWDML_CF_RED_US overrides (A/B)
+  static const double red_us = [] {
+    const char* e = getenv("EWDML_CF_RED_US");
+    return e ? atof(e) : 2.0;
+  }();
   static const int shapes[4][2] = {{128, 128}, {128, 64}, {64, 128}, {64, 64}};
   static const double derate[4] = {1.0, 0.9, 0.9, 0.75};
   CfPlan best{64, 64, 1, ksteps};
@@ -1205,7 +1210,7 @@ CfPlan cf_plan(int M, int Ncol, int ksteps, long long ws_floats, int batch) {
       // operand traffic: every block streams (bm + bn) x K floats, ~6 TB/s from HBM / MALL
       // (small tiles over a long K -- the Winograd weight-gradient GEMMs -- are bound by it)
       t = std::max(t, (double)tiles * (bm + bn) * ksteps * CF_BK * 4 / 6e6);
-      if (sp > 1) t += 8.0 * sp * slab1 / 4e6 + 2.0;
+      if (sp > 1) t += 8.0 * sp * slab1 / 4e6 + red_us;
       if (t < best_t * 0.999) {
         best_t = t;
         best = CfPlan{bm, bn, sp, kps};
