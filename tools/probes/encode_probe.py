@@ -22,6 +22,7 @@ def main():
     a = argparse.ArgumentParser()
     a.add_argument("--ratio", type=float, default=0.01)
     a.add_argument("--reps", type=int, default=50)
+    a.add_argument("--modes", default="plain,ef,dgc")
     args = a.parse_args()
     ops.require()
     dev = torch.device("cuda")
@@ -42,7 +43,10 @@ def main():
     param = torch.randn(plan.length, device=dev)
     dgc = dict(velocity=vel, momentum=0.9, dampening=0.0, nesterov=False, weight_decay=0.0,
                param=param, mask=True)
-    for name, kw in (("plain", {}), ("ef", dict(resid=resid)), ("dgc", dict(resid=resid, dgc=dgc))):
+    modes = (("plain", {}), ("ef", dict(resid=resid)), ("dgc", dict(resid=resid, dgc=dgc)))
+    for name, kw in modes:
+        if name not in args.modes.split(","):
+            continue
         for _ in range(3):
             ops.topk_encode(dp, grad, pay, lay, 127, "max", 7, **kw)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
