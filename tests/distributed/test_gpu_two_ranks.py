@@ -69,3 +69,21 @@ def test_four_ranks_on_one_gpu_identical(tmp_path, flags, graph):
         assert all(r["graph"] == graph for r in res)
     else:  # parameter server: the workers split-graph, the server captures nothing
         assert all(r["graph"] == "split" for r in res[1:])
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("ef", [False, True])
+def test_eight_ranks_on_one_gpu_identical(tmp_path, ef):
+    """Eight ranks on the box's one GPU (Gloo between them, the size of the 8-GPU node): the HIP
+    encode, the all-gather of 8 payload slots and the rank-ordered decode of all 8 (past the 8
+    ranks whose first entries the decode prefetches) keep the replicas bitwise identical, with
+    and without momentum-corrected error feedback (the headline codec)."""
+    flags = ["--compress", "topk_qsgd", "--hip-graph", "auto", "--graph-warmup", "1"]
+    if ef:
+        flags += ["--error-feedback"]
+    res = run_world(_train, 8, tmp_path, args=(flags, 3))
+    assert torch.isfinite(res[0]["params"]).all()
+    for r in res[1:]:
+        assert torch.equal(res[0]["params"], r["params"])
+        assert r["bytes"] == res[0]["bytes"] > 0
+    assert all(r["graph"] == "split" for r in res)
