@@ -1486,6 +1486,44 @@ __device__ __forceinline__ float ew_topk_code(const uint8_t* pay, int codes_off,
   return (float)(q >= 8 ? q - 16 : q);
 }
 
+// Entry offset of this chunk inside each rank's payload: entry0 + the sum of the tensor's earlier
+// chunk counts (a few hundred for the last chunks of a large tensor).  A wave takes ranks w and
+// w + EW_WAVES together, every count load of both in flight before any is summed: one round trip
+// for up to 2 * EW_WAVES = 8 ranks instead of one per group of 4.
+__device__ __forceinline__ void topk_chunk_offsets(const uint8_t* __restrict__ recv, int nranks,
+                                                   long long stride, int counts_off,
+                                                   const ChunkRow& c, const TensorRow& tr,
+                                                   uint32_t* s_off, int lane, int w) {
+  for (int r = w; r < nranks; r += 2 * EW_WAVES) {
+    const int r2 = r + EW_WAVES;
+    const bool two = r2 < nranks;  // wave-uniform
+    const uint16_t* cn1 = reinterpret_cast<const uint16_t*>(recv + r * stride + counts_off) + tr.chunk0;
+    const uint16_t* cn2 = reinterpret_cast<const uint16_t*>(recv + (two ? r2 : r) * stride +
+                                                            counts_off) + tr.chunk0;
+    uint32_t s1 = 0, s2 = 0;
+    for (int j0 = 0; j0 < c.local; j0 += 8 * 64) {
+      uint32_t v1[8], v2[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int j = j0 + u * 64 + lane;
+        v1[u] = j < c.local ? (uint32_t)cn1[j] : 0u;
+        v2[u] = j < c.local ? (uint32_t)cn2[j] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        s1 += v1[u];
+        s2 += v2[u];
+      }
+    }
+    s1 = ew_wave_sum_u(s1);
+    s2 = ew_wave_sum_u(s2);
+    if (lane == 0) {
+      s_off[r] = (uint32_t)tr.entry0 + s1;
+      if (two) s_off[r2] = (uint32_t)tr.entry0 + s2;
+    }
+  }
+}
+
 // Every rank's first list entry of this thread (e = thread index: all of a chunk's entries at
 // <= 2.5 % density) for the first PR ranks, loaded before any is summed -- one round trip for all
 // of them instead of one per rank -- plus each of those ranks' count and scale (any tensor kind),
@@ -1601,22 +1639,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_decode_apply(
   // entry offset of this chunk inside each rank's payload: entry0 + sum of earlier chunk counts
   // (a wave per rank; each lane's loads of up to 8 counts are all in flight before the sum: the
   // tensor's last chunks sum a few hundred counts, a dependent round trip per 64 otherwise)
-  for (int r = w; r < nranks; r += EW_WAVES) {
-    const uint16_t* cnts = reinterpret_cast<const uint16_t*>(recv + r * stride + counts_off) + tr.chunk0;
-    uint32_t s = 0;
-    for (int j0 = 0; j0 < c.local; j0 += 8 * 64) {
-      uint32_t v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int j = j0 + u * 64 + lane;
-        v[u] = j < c.local ? (uint32_t)cnts[j] : 0u;
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) s += v[u];
-    }
-    s = ew_wave_sum_u(s);
-    if (lane == 0) s_off[r] = (uint32_t)tr.entry0 + s;
-  }
+  topk_chunk_offsets(recv, nranks, stride, counts_off, c, tr, s_off, lane, w);
   __syncthreads();
   // Index-list tensors: every rank's first entry of this thread (e = thread index: all of a chunk's
   // entries at <= 2.5 % density) is loaded for the first PR ranks before any is summed -- one
@@ -1742,22 +1765,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_decode_sparse(
   const TensorRow tr = tensors[c.tensor];
   float* p = param + c.start;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  for (int r = w; r < nranks; r += EW_WAVES) {
-    const uint16_t* cnts = reinterpret_cast<const uint16_t*>(recv + r * stride + counts_off) + tr.chunk0;
-    uint32_t s = 0;
-    for (int j0 = 0; j0 < c.local; j0 += 8 * 64) {
-      uint32_t v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int j = j0 + u * 64 + lane;
-        v[u] = j < c.local ? (uint32_t)cnts[j] : 0u;
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) s += v[u];
-    }
-    s = ew_wave_sum_u(s);
-    if (lane == 0) s_off[r] = (uint32_t)tr.entry0 + s;
-  }
+  topk_chunk_offsets(recv, nranks, stride, counts_off, c, tr, s_off, lane, w);
   __syncthreads();
   constexpr int PR = 8;
   const uint32_t eend = (uint32_t)(tr.entry0 + tr.k);  // never read past the tensor's entries
