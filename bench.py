@@ -267,7 +267,11 @@ def main(argv=None):
         for key, amp, e, xf in extras:
             if cuda:
                 torch.cuda.empty_cache()
-            el, tr2, fl, _, _, rep2 = measure(a, world, amp, e, xf)
+            try:
+                el, tr2, fl, _, _, rep2 = measure(a, world, amp, e, xf)
+            except Exception as exc:  # an extra never costs the headline line (same on every rank)
+                rec[f"error_{key}"] = repr(exc)[:300]
+                continue
             if rep2 is not None:
                 rec[f"replicas_identical_{key}"] = rep2["identical"]
             rec[f"value_{key}"] = round(world * a.batch_size * a.steps / el, 2)
