@@ -64,6 +64,21 @@ def _residual_block(x, main, bn_last, sc):
     return bn_act(h, bn_last, "add_relu", res=_shortcut(sc, x))
 
 
+def _lazy_into(conv, h) -> bool:
+    """Whether BN-ReLU output (of input ``h``) may stay unwritten because ``conv`` -- its only
+    consumer -- runs the fp32 Winograd path, whose input transform applies the BN layer on the
+    fly (as models/fused.py does for VGG; EWDML_LAZY_BN=0: always materialise)."""
+    if not fused._LAZY:
+        return False
+    if not (conv.stride in (1, (1, 1)) and conv.padding in (1, (1, 1))
+            and conv.dilation in (1, (1, 1)) and conv.groups == 1):
+        return False
+    from ..ops import conv as conv_hip
+
+    return conv_hip.enabled() and conv_hip.wino_tile_for(tuple(h.shape), h.dtype,
+                                                          conv.weight) > 0
+
+
 def _shortcut(sc, x):
     """Identity or projection (1x1 conv + BN, through the fused BN kernel)."""
     if len(sc) == 0:
@@ -96,7 +111,7 @@ class BasicBlock(nn.Module):
 
         first = sink is not None and module_supported(self.conv1, x)
         h = conv2d_module(self.conv1, x, sink if first else None)
-        out = bn_act(h, self.bn1, "relu")
+        out = bn_act(h, self.bn1, "relu", lazy=_lazy_into(self.conv2, h))
         return _conv(self.conv2, out), first
 
     def forward(self, x):
@@ -132,7 +147,7 @@ class Bottleneck(nn.Module):
 
         first = sink is not None and module_supported(self.conv1, x)
         h = conv2d_module(self.conv1, x, sink if first else None)
-        out = bn_act(h, self.bn1, "relu")
+        out = bn_act(h, self.bn1, "relu", lazy=_lazy_into(self.conv2, h))
         out = bn_act(_conv(self.conv2, out), self.bn2, "relu")
         return _conv(self.conv3, out), first
 

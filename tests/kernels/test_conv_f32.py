@@ -481,6 +481,9 @@ def test_fp32_resnet18_step_convs_in_situ():
 
         materialize(dy)  # a lazily formed BN input gradient (ops/nn.py): record its values
         x, w = ctx.saved_tensors
+        # a lazily applied BN output (the Winograd conv's forward transformed it on the fly, its
+        # backward never reads it): write it for the float64 reference
+        materialize(x)
         had_sink = ctx.sink is not None and getattr(ctx.sink, "grad", None) is not None
         dx, dw, a, b = orig(ctx, dy)
         recs.append((x.detach().clone(), w.detach().clone(), dy.detach().clone(),
