@@ -61,3 +61,40 @@ def test_resnet50_error_feedback_tracks_dense():
     assert max(ef) < 1.5 * chance, f"EF loss peaked at {max(ef):.2f}"
     assert tail(ef) < tail(dense) + 0.1, (tail(ef), tail(dense))
     assert tail(ef) < 0.5 * tail(noef), (tail(ef), tail(noef))
+
+
+VGG = ["--network", "VGG11", "--dataset", "Cifar10", "--batch-size", "128",
+       "--synthetic-size", "16384", "--momentum", "0.9", "--lr", "0.01", "--eval-freq", "0",
+       "--quiet", "--device", "cuda", "--amp", "none", "--hip-graph", "full", "--graph-warmup",
+       "2", "--max-steps", str(STEPS)]
+
+
+@pytest.mark.timeout(600)
+def test_vgg11_headline_codec_tracks_dense():
+    """The headline configuration (VGG-11-BN fp32, top-1 % + QSGD-8, DGC error feedback with its
+    warm-up recipe -- what bench.py times) trains like the dense fp32 all-reduce (Method 3) on
+    the same synthetic CIFAR-shaped data: no divergence, and the loss over the last 60 of 400
+    steps within 0.1 nats of dense."""
+    ops.require()
+    from ewdml.runtime import Trainer
+
+    def curve(flags):
+        torch.manual_seed(0)
+        tr = Trainer(ewdml.parse_args(VGG + flags))
+        out = [tr.train_step()[0].detach() for _ in range(STEPS)]
+        torch.cuda.synchronize()
+        tr.close()
+        return tr, [float(v) for v in out]
+
+    tr, ef = curve(["--compress", "topk_qsgd", "--topk-ratio", "0.01"])
+    assert tr.exchange.ef_mode == "dgc" and tr.exchange.codec.ratio == 0.01
+    _, dense = curve(["--compress", "none"] + LR_WARMUP)
+
+    def tail(c):
+        return sum(c[-60:]) / 60
+
+    print(f"VGG-11 loss, last 60 of {STEPS} steps: top-1 % + QSGD-8 + DGC {tail(ef):.4f}, "
+          f"dense fp32 {tail(dense):.4f}; first step {ef[0]:.3f}, max {max(ef):.3f}")
+    assert all(math.isfinite(v) for v in ef)
+    assert max(ef) < 1.5 * math.log(10), f"loss peaked at {max(ef):.2f}"
+    assert tail(ef) < tail(dense) + 0.1, (tail(ef), tail(dense))
