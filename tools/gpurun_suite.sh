@@ -44,6 +44,9 @@ run_prof() {
   name=$1; args=$2
   steps=$(echo "$args" | sed -n 's/.*--steps \([0-9]*\).*/\1/p'); steps=${steps:-20}
   case "$args" in *--steps*) ;; *) args="$args --steps $steps --warmup 6";; esac
+  # the headline configuration only: each extra measurement has a timed window of its own, and
+  # the summariser's busiest window could be one of theirs (PROF_EXTRAS=1 keeps them)
+  [ "${PROF_EXTRAS:-0}" = 1 ] || case "$args" in *--no-extras*) ;; *) args="$args --no-extras";; esac
   rm -rf /tmp/p_$name
   EWDML_PROF_GAP=1 timeout -k 10 600 rocprofv3 --kernel-trace --output-format csv -d /tmp/p_$name \
       -o run -- python3 bench.py $args > gpurun_out/prof_$name.log 2>&1 \
