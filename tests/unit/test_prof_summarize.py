@@ -1,6 +1,7 @@
-"""tools/prof_summarize.py: the timed window of a bench trace is the busiest window between two
-idle gaps (bench.py EWDML_PROF_GAP=1 sleeps before and after the timed loop; teardown after it can
-add idle gaps of its own), and the report's per-step numbers come from that window only."""
+"""tools/prof_summarize.py: the timed window of a bench trace is the first window between two idle
+gaps that the GPU kept busy (bench.py EWDML_PROF_GAP=1 sleeps before and after each timed loop; the
+extra measurements and teardown after it add windows of their own), else the busiest, and the
+report's per-step numbers come from that window only."""
 import os
 import sys
 
@@ -26,9 +27,31 @@ def test_busiest_window_between_gaps():
     late, _ = _kernels(t + 300 * MS, 2, 5, "k_late")
     txt = summarize(warm + timed + tail + late, steps=4)
     first = txt.splitlines()[0]
-    assert "busiest" in first and "40 kernels" in first
+    assert "90 % busy" in first and "40 kernels" in first
     assert "k_step" in txt and "k_warm" not in txt and "copyBuffer" not in txt
     assert "last step, 10 kernels" in txt
+
+
+def test_headline_window_before_the_extra_measurements():
+    warm, t = _kernels(0, 30, 10, "k_warm")
+    head, t = _kernels(t + 250 * MS, 40, 20, "k_head_step")
+    # an extra measurement: an eager setup window (more kernels, mostly idle), then its own
+    # timed window (more kernels than the headline's)
+    setup, t = _kernels(t + 250 * MS, 90, 5, "k_setup", gap_us=60)
+    extra, t = _kernels(t + 250 * MS, 60, 20, "k_extra_step")
+    end, _ = _kernels(t + 250 * MS, 2, 5, "k_end")
+    txt = summarize(warm + head + setup + extra + end, steps=4)
+    assert "40 kernels" in txt.splitlines()[0]
+    assert "k_head_step" in txt and "k_extra_step" not in txt and "k_setup" not in txt
+
+
+def test_busiest_window_when_none_is_dense():
+    a, t = _kernels(0, 5, 10, "a")
+    b, t = _kernels(t + 200 * MS, 30, 5, "b", gap_us=20)
+    c, t = _kernels(t + 200 * MS, 12, 5, "c", gap_us=20)
+    d, _ = _kernels(t + 200 * MS, 2, 5, "d")
+    first = summarize(a + b + c + d).splitlines()[0]
+    assert "busiest" in first and "30 kernels" in first
 
 
 def test_single_gap_and_no_gap():

@@ -41,8 +41,9 @@ def short(name):
 
 
 def summarize(rows, frac=0.5, gap_ns=150_000_000, steps=None):
-    """Window = kernels after the last idle gap >= gap_ns (bench.py EWDML_PROF_GAP=1 sleeps before
-    the timed loop); falls back to the last ``frac`` of the trace."""
+    """Window = the timed loop between two idle gaps >= gap_ns (bench.py EWDML_PROF_GAP=1 sleeps
+    before and after it), or everything after a single gap; falls back to the last ``frac`` of the
+    trace."""
     if not rows:
         return "no kernels\n"
     t0, t1 = rows[0][0], max(r[1] for r in rows)
@@ -52,17 +53,36 @@ def summarize(rows, frac=0.5, gap_ns=150_000_000, steps=None):
         if s - end >= gap_ns:
             gaps.append((end, s))
         end = max(end, e)
-    # bench.py (EWDML_PROF_GAP=1) idles before and after the timed loop: of the windows between
-    # two consecutive gaps, the one with the most kernels (teardown after the loop can add idle
-    # gaps of its own); a trace with one gap: everything after it
+    # bench.py (EWDML_PROF_GAP=1) idles before and after each timed loop: of the windows between
+    # two consecutive gaps, the first one the GPU kept >= 90 % busy (the headline's timed steps;
+    # the extra measurements that follow each add a setup window and a timed window of their own),
+    # else the one with the most kernels (teardown after the loop can add idle gaps of its own); a
+    # trace with one gap: everything after it
     stop = None
     if len(gaps) >= 2:
-        def count(a, b):
-            return sum(1 for r in rows if a <= r[0] < b)
+        def stats(a, b):
+            w = [r for r in rows if a <= r[0] < b]
+            if not w:
+                return 0, 0.0
+            busy, cs, ce = 0, w[0][0], w[0][1]
+            for s, e, _ in w[1:]:
+                if s > ce:
+                    busy += ce - cs
+                    cs, ce = s, e
+                else:
+                    ce = max(ce, e)
+            busy += ce - cs
+            return len(w), busy / max(1, max(r[1] for r in w) - w[0][0])
 
-        i = max(range(len(gaps) - 1), key=lambda j: (count(gaps[j][1], gaps[j + 1][0]), j))
+        st = [stats(gaps[j][1], gaps[j + 1][0]) for j in range(len(gaps) - 1)]
+        dense = [j for j, (n, f) in enumerate(st) if n >= 10 and f >= 0.9]
+        if dense:
+            i = dense[0]
+            how = "between two idle gaps (the first >= 90 % busy window)"
+        else:
+            i = max(range(len(st)), key=lambda j: (st[j][0], j))
+            how = "between two idle gaps (the busiest window)"
         cut, stop = gaps[i][1], gaps[i + 1][0]
-        how = "between two idle gaps (the busiest window)"
     elif gaps:
         cut = gaps[-1][1]
         how = "after last idle gap"
