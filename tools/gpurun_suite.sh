@@ -1,7 +1,7 @@
 #!/bin/bash
 # One parameterised GPU runner for everything this repo measures on an MI355X box.
 # Run through gpurun from the repo root, e.g.
-#   gpurun --timeout 900 -- bash tools/gpurun_suite.sh tests
+#   gpurun --timeout 900 -- bash tools/gpurun_suite.sh tests     # TESTS_K="stem or lazy": a -k filter
 #   gpurun --timeout 900 -- bash tools/gpurun_suite.sh bench "--amp none" "--amp bf16"
 #   gpurun --timeout 900 -- bash tools/gpurun_suite.sh prof NAME "--amp none --steps 20"
 #   gpurun --timeout 900 -- bash tools/gpurun_suite.sh pmc NAME "SQ_WAVES SQ_BUSY_CYCLES" "--amp none"
@@ -18,7 +18,8 @@ task=${1:-validate}; shift
 
 run_tests() {
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
-      ${TESTS_ARGS:-} > gpurun_out/gpu_tests.log 2>&1 || { tail -60 gpurun_out/gpu_tests.log; exit 1; }
+      ${TESTS_ARGS:-} ${TESTS_K:+-k "$TESTS_K"} > gpurun_out/gpu_tests.log 2>&1 \
+      || { tail -60 gpurun_out/gpu_tests.log; exit 1; }
   tail -1 gpurun_out/gpu_tests.log
 }
 
