@@ -888,7 +888,7 @@ constexpr int CS_WMAX = 256;
 template <int PIX>
 constexpr int cs_patch_floats() { return (PIX + 2 * CS_WMAX + 2) * 3 + 8; }
 
-template <int PIX>
+template <int PIX, int NT = EW_BLOCK>
 __device__ __forceinline__ int cs_patch(const float* __restrict__ x, int m0, int W, int M,
                                         float* patch, int t) {
   int lo = (m0 - W - 1) * 3;
@@ -896,7 +896,7 @@ __device__ __forceinline__ int cs_patch(const float* __restrict__ x, int m0, int
   int hi = ((m0 + PIX + W + 1) * 3 + 3) & ~3;
   hi = hi > 3 * M ? 3 * M : hi;
   const int nch = (hi - lo) >> 2;
-  for (int c = t; c < nch; c += EW_BLOCK)
+  for (int c = t; c < nch; c += NT)
     *reinterpret_cast<f32x4*>(patch + 4 * c) = *reinterpret_cast<const f32x4*>(x + lo + 4 * c);
   return lo;
 }
@@ -1005,9 +1005,10 @@ __global__ __launch_bounds__(EW_BLOCK) void k_cf_stem_fwd(const float* __restric
   }
 }
 
-// Stem weight gradient dw[n][k] = sum_m dy[m][n] x~[m][k]: block = 256 pixels x 64 channels.
+// Stem weight gradient dw[n][k] = sum_m dy[m][n] x~[m][k]: block = 256 pixels x 64 channels, 512
+// threads (the ~116 KB of LDS allow one block per CU: 8 waves, not 4, keep its loads in flight).
 // dy rows ([256 m][64 n], RC) and the im2col rows ([256 m][28 k], RC) go to LDS; wave v computes
-// n0 + [16 v, 16 v + 16) x k 0..31 (2 tiles) over all 256 m (64 MFMA k-steps), fp32 partial
+// the 16 x 16 tile n0 + 16 (v & 3) x k 16 (v >> 2) over all 256 m (64 MFMA k-steps), fp32 partial
 // [64][27] per block into the slab, summed by k_cf_stem_reduce.
 // LAZY: dy is not materialised -- it is the BatchNorm(+ReLU)(+2x2 pool) backward of the stem's
 // output, formed here from that layer's input h (= the stem output), the gradient of its
@@ -1021,23 +1022,25 @@ struct CsLazy {
   const float* coef;
   int pool;
 };
+constexpr int CS_WG_THREADS = 512;
 
 template <bool LAZY>
-__global__ __launch_bounds__(EW_BLOCK) void k_cf_stem_wgrad(const float* __restrict__ dy,
-                                                            const float* __restrict__ x,
-                                                            float* __restrict__ slab, int H,
-                                                            int W, int Nc, int M, CsLazy lz) {
+__global__ __launch_bounds__(CS_WG_THREADS) void k_cf_stem_wgrad(const float* __restrict__ dy,
+                                                                 const float* __restrict__ x,
+                                                                 float* __restrict__ slab, int H,
+                                                                 int W, int Nc, int M, CsLazy lz) {
+  constexpr int NT = CS_WG_THREADS, NU = 256 * 16 / NT;  // f32x4 quads of dy per thread
   constexpr int DP = 64 + 4, XP = 32 + 4;  // pitches (floats): k and k + 4 16 banks apart
   __shared__ __attribute__((aligned(16))) float dsm[256 * DP];
   __shared__ __attribute__((aligned(16))) float xsm[256 * XP];
   __shared__ __attribute__((aligned(16))) float patch[cs_patch_floats<256>()];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6, li = lane & 15, g = lane >> 4;
   const int m0 = blockIdx.x * 256, n0 = blockIdx.y * 64, HW = H * W;
-  f32x4 d[16];
+  f32x4 d[NU];
   if constexpr (!LAZY) {
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {  // 256 rows x 16 quads
-      const int e = t + EW_BLOCK * u, r = e >> 4, ch = e & 15;
+    for (int u = 0; u < NU; ++u) {  // 256 rows x 16 quads
+      const int e = t + NT * u, r = e >> 4, ch = e & 15;
       d[u] = *reinterpret_cast<const f32x4*>(dy + (long long)(m0 + r) * Nc + n0 + ch * 4);
     }
   } else {
@@ -1049,80 +1052,73 @@ __global__ __launch_bounds__(EW_BLOCK) void k_cf_stem_wgrad(const float* __restr
     const f32x4 ce = *reinterpret_cast<const f32x4*>(lz.coef + c0);
     const f32x4 cf = *reinterpret_cast<const f32x4*>(lz.coef + Nc + c0);
     const int Ho = H >> 1, Wo = W >> 1;
+    f32x4 hv[NU], dn[NU];
+    uint32_t kw[NU], qq[NU];
 #pragma unroll
-    for (int h8 = 0; h8 < 2; ++h8) {  // two halves of 8 rows: the loads of a half in flight
-      f32x4 hv[8], dn[8];
-      uint32_t kw[8], qq[8];
-#pragma unroll
-      for (int u8 = 0; u8 < 8; ++u8) {
-        const int u = 8 * h8 + u8, r = (t + EW_BLOCK * u) >> 4, m = m0 + r;
-        hv[u8] = *reinterpret_cast<const f32x4*>(lz.h + (long long)m * Nc + c0);
-        if (lz.pool) {
-          const int n = m / HW, p = m - n * HW, hh = p / W, ww = p - hh * W;
-          const long long pr = ((long long)n * Ho + (hh >> 1)) * Wo + (ww >> 1);
-          dn[u8] = *reinterpret_cast<const f32x4*>(lz.dnext + pr * Nc + c0);
-          kw[u8] = *reinterpret_cast<const uint32_t*>(lz.code + pr * Nc + c0);
-          qq[u8] = (uint32_t)((hh & 1) * 2 + (ww & 1));
-        } else {
-          dn[u8] = *reinterpret_cast<const f32x4*>(lz.dnext + (long long)m * Nc + c0);
-          kw[u8] = 0u;
-          qq[u8] = 0u;
-        }
-      }
-#pragma unroll
-      for (int u8 = 0; u8 < 8; ++u8) {
-        f32x4 o;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float xv = hv[u8][j];
-          const bool route = !lz.pool || ((kw[u8] >> (8 * j)) & 0xffu) == qq[u8];
-          const float z = xv * sc[j] + sh[j];  // k_bn_bwd_apply's expressions: the same bits
-          const float dz = (route && !(z <= 0.0f)) ? dn[u8][j] : 0.0f;
-          o[j] = sc[j] * dz + ce[j] * (xv - mn[j]) + cf[j];
-        }
-        d[8 * h8 + u8] = o;
+    for (int u = 0; u < NU; ++u) {  // every load of the thread in flight at once
+      const int r = (t + NT * u) >> 4, m = m0 + r;
+      hv[u] = *reinterpret_cast<const f32x4*>(lz.h + (long long)m * Nc + c0);
+      if (lz.pool) {
+        const int n = m / HW, p = m - n * HW, hh = p / W, ww = p - hh * W;
+        const long long pr = ((long long)n * Ho + (hh >> 1)) * Wo + (ww >> 1);
+        dn[u] = *reinterpret_cast<const f32x4*>(lz.dnext + pr * Nc + c0);
+        kw[u] = *reinterpret_cast<const uint32_t*>(lz.code + pr * Nc + c0);
+        qq[u] = (uint32_t)((hh & 1) * 2 + (ww & 1));
+      } else {
+        dn[u] = *reinterpret_cast<const f32x4*>(lz.dnext + (long long)m * Nc + c0);
+        kw[u] = 0u;
+        qq[u] = 0u;
       }
     }
-  }
-  const int lo = cs_patch<256>(x, m0, W, M, patch, t);
 #pragma unroll
-  for (int u = 0; u < 16; ++u) {
-    const int e = t + EW_BLOCK * u, r = e >> 4, ch = e & 15;
+    for (int u = 0; u < NU; ++u) {
+      f32x4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float xv = hv[u][j];
+        const bool route = !lz.pool || ((kw[u] >> (8 * j)) & 0xffu) == qq[u];
+        const float z = xv * sc[j] + sh[j];  // k_bn_bwd_apply's expressions: the same bits
+        const float dz = (route && !(z <= 0.0f)) ? dn[u][j] : 0.0f;
+        o[j] = sc[j] * dz + ce[j] * (xv - mn[j]) + cf[j];
+      }
+      d[u] = o;
+    }
+  }
+  const int lo = cs_patch<256, NT>(x, m0, W, M, patch, t);
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    const int e = t + NT * u, r = e >> 4, ch = e & 15;
     *reinterpret_cast<f32x4*>(dsm + r * DP + ch * 4) = d[u];
   }
   __syncthreads();
   {
-    // im2col row r = t: k 0..31 (k >= 27 zero)
-    const int m = m0 + t, p = m % HW, h = p / W, ww = p - h * W;
+    // im2col row r = t & 255: k 16 (t >> 8) .. + 15 (k >= 27 zero)
+    const int r = t & 255, kh = t >> 8;
+    const int m = m0 + r, p = m % HW, h = p / W, ww = p - h * W;
 #pragma unroll
-    for (int k4 = 0; k4 < 8; ++k4) {
+    for (int k4 = 0; k4 < 4; ++k4) {
       f32x4 v;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = cs_x(patch, lo, m, h, ww, H, W, 4 * k4 + e);
-      *reinterpret_cast<f32x4*>(xsm + t * XP + 4 * k4) = v;
+      for (int e = 0; e < 4; ++e) v[e] = cs_x(patch, lo, m, h, ww, H, W, 16 * kh + 4 * k4 + e);
+      *reinterpret_cast<f32x4*>(xsm + r * XP + 16 * kh + 4 * k4) = v;
     }
   }
   __syncthreads();
-  f32x4 acc[2];
-  acc[0] = acc[1] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  const int nt = wv & 3, j = wv >> 2;
+  f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll 8
   for (int s = 0; s < 64; ++s) {
     // reduction row of MFMA step s for lane group g: the four groups read rows 4 apart (the +4
     // pitch pads put them 16 banks apart)
     const int mr = (s >> 2) * 16 + 4 * g + (s & 3);
-    const float a = dsm[mr * DP + 16 * wv + li];
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-      acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, xsm[mr * XP + 16 * j + li], acc[j], 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(dsm[mr * DP + 16 * nt + li],
+                                               xsm[mr * XP + 16 * j + li], acc, 0, 0, 0);
   }
   float* sp = slab + (long long)blockIdx.x * Nc * CS_K;
+  const int k = 16 * j + li;
+  if (k < CS_K) {
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int k = 16 * j + li;
-    if (k < CS_K) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) sp[(long long)(n0 + 16 * wv + 4 * g + q) * CS_K + k] = acc[j][q];
-    }
+    for (int q = 0; q < 4; ++q) sp[(long long)(n0 + 16 * nt + 4 * g + q) * CS_K + k] = acc[q];
   }
 }
 
@@ -1516,11 +1512,11 @@ static void cf_stem_wgrad(const float* dy, const CsLazy* lz, uintptr_t x, uintpt
   float* slab = reinterpret_cast<float*>(ws);
   const CsLazy none{nullptr, nullptr, nullptr, nullptr, nullptr, 0};
   if (lz)
-    hipLaunchKernelGGL(k_cf_stem_wgrad<true>, dim3((int)nb, Nc / 64), dim3(EW_BLOCK), 0, s,
+    hipLaunchKernelGGL(k_cf_stem_wgrad<true>, dim3((int)nb, Nc / 64), dim3(CS_WG_THREADS), 0, s,
                        nullptr, reinterpret_cast<const float*>(x), slab, H, W, Nc, (int)M, *lz);
   else
-    hipLaunchKernelGGL(k_cf_stem_wgrad<false>, dim3((int)nb, Nc / 64), dim3(EW_BLOCK), 0, s, dy,
-                       reinterpret_cast<const float*>(x), slab, H, W, Nc, (int)M, none);
+    hipLaunchKernelGGL(k_cf_stem_wgrad<false>, dim3((int)nb, Nc / 64), dim3(CS_WG_THREADS), 0, s,
+                       dy, reinterpret_cast<const float*>(x), slab, H, W, Nc, (int)M, none);
   EW_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_cf_stem_reduce, dim3((int)((n + 7) / 8)), dim3(EW_BLOCK), 0, s, slab,
                      (int)nb, (int)n, reinterpret_cast<float*>(dw));
