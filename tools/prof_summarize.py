@@ -40,16 +40,15 @@ def short(name):
     return n[:cut][:110] or name[:110]
 
 
-def summarize(rows, frac=0.5, gap_ns=150_000_000, steps=None):
-    """Window = the timed loop between two idle gaps >= gap_ns (bench.py EWDML_PROF_GAP=1 sleeps
-    before and after it), or everything after a single gap; falls back to the last ``frac`` of the
-    trace."""
-    if not rows:
-        return "no kernels\n"
+def timed_window(rows, frac=0.5, gap_ns=150_000_000):
+    """Rows (start, end, name, ...) of the timed loop: the window between two idle gaps >= gap_ns
+    (bench.py EWDML_PROF_GAP=1 sleeps before and after it), or everything after a single gap;
+    falls back to the last ``frac`` of the trace.  Returns (rows, description)."""
     t0, t1 = rows[0][0], max(r[1] for r in rows)
     gaps = []  # (idle start, idle end)
     end = rows[0][1]
-    for s, e, _ in rows[1:]:
+    for r in rows[1:]:
+        s, e = r[0], r[1]
         if s - end >= gap_ns:
             gaps.append((end, s))
         end = max(end, e)
@@ -65,7 +64,7 @@ def summarize(rows, frac=0.5, gap_ns=150_000_000, steps=None):
             if not w:
                 return 0, 0.0
             busy, cs, ce = 0, w[0][0], w[0][1]
-            for s, e, _ in w[1:]:
+            for s, e, *_ in w[1:]:
                 if s > ce:
                     busy += ce - cs
                     cs, ce = s, e
@@ -89,7 +88,14 @@ def summarize(rows, frac=0.5, gap_ns=150_000_000, steps=None):
     else:
         cut = t0 + (t1 - t0) * (1 - frac)
         how = f"last {frac:.0%} of trace"
-    win = [r for r in rows if r[0] >= cut and (stop is None or r[0] < stop)]
+    return [r for r in rows if r[0] >= cut and (stop is None or r[0] < stop)], how
+
+
+def summarize(rows, frac=0.5, gap_ns=150_000_000, steps=None):
+    """Per-kernel report of the timed window (``timed_window``)."""
+    if not rows:
+        return "no kernels\n"
+    win, how = timed_window(rows, frac, gap_ns)
     span = max(r[1] for r in win) - win[0][0]
     busy = 0
     cur_s, cur_e = win[0][0], win[0][1]
