@@ -14,7 +14,9 @@ The reference has no counterpart (its Gloo/MPI collectives are trusted as-is:
 of a data plane that cannot be exercised at N > 1 before the scaling run.
 
 Test hook: ``EWDML_PROBE_CORRUPT=<rank>[,<rank>...]`` flips one byte of the listed ranks' probe
-results (``<rank>:graph`` only in the captured replays).
+results (``<rank>:graph`` only in the captured replays); ``<rank>:capture`` makes that rank's graph
+capture raise (every rank must then skip the replays: a replay holds collectives that would wait
+forever for the rank that has no graph).
 """
 import os
 
@@ -82,29 +84,39 @@ def _wait(work):
         work.wait()
 
 
-def _graphed(comm, device, corrupt: bool) -> bool:
+def _graph_capture(comm, device, fail: bool = False):
     """The three collectives captured in one HIP graph on a side stream (as the step graph
-    captures them), replayed twice with new inputs copied into the static buffers between
-    replays: each replay must read the current inputs and produce their closed forms."""
+    captures them).  Returns the replay state; raises if the capture fails (``fail``: test
+    hook).  Nothing here waits on a peer: capture only records the collectives."""
     rank, world = comm.rank, comm.world
+    if fail:
+        raise RuntimeError(f"probe capture failure injected on rank {rank}")
     out = torch.zeros(world * _AG_N, dtype=torch.uint8, device=device)
     slot = out[rank * _AG_N:(rank + 1) * _AG_N]
     ar = torch.zeros(_AR_N, dtype=torch.float32, device=device)
     bc = torch.zeros(_BC_N, dtype=torch.float32, device=device)
-    src_ag = torch.zeros(_AG_N, dtype=torch.uint8, device=device)
-    src_ar = torch.zeros_like(ar)
-    src_bc = torch.zeros_like(bc)
+    src = (torch.zeros(_AG_N, dtype=torch.uint8, device=device), torch.zeros_like(ar),
+           torch.zeros_like(bc))
     (_, _), (_, _), (_, _, root) = _inputs(rank, world, 0, device)
     s = torch.cuda.Stream(device=device)
     s.wait_stream(torch.cuda.current_stream(device))
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
-        slot.copy_(src_ag)
-        ar.copy_(src_ar)
-        bc.copy_(src_bc)
+        slot.copy_(src[0])
+        ar.copy_(src[1])
+        bc.copy_(src[2])
         comm.all_gather(out, slot)
         comm.all_reduce(ar)
         comm.broadcast(bc, src=root)
+    return g, out, ar, bc, src
+
+
+def _graph_replay(comm, device, state, corrupt: bool) -> bool:
+    """Replay the captured probe twice with new inputs copied into the static buffers between
+    replays: each replay must read the current inputs and produce their closed forms.  Every rank
+    calls it (the replays hold collectives), only after all ranks captured."""
+    rank, world = comm.rank, comm.world
+    g, out, ar, bc, (src_ag, src_ar, src_bc) = state
     ok = True
     for salt in (1, 2):
         (ag_in, ag_exp), (ar_in, ar_exp), (bc_in, bc_exp, _) = _inputs(rank, world, salt, device)
@@ -118,25 +130,48 @@ def _graphed(comm, device, corrupt: bool) -> bool:
         if corrupt:
             ar[1] += 1.0
         ok = ok and _check(out, ag_exp) and _check(ar, ar_exp) and _check(bc, bc_exp)
-    del g
     return ok
+
+
+def _graph_supported(device) -> bool:
+    return device.type == "cuda"
 
 
 def probe_collectives(comm, device, graph: bool = True) -> dict:
     """Run the probe on every rank and agree on the outcome (collective: every rank calls it with
-    the same ``graph``).  Returns ``{"ok", "eager", "graph", "local_ok"}``; ``ok`` is the
-    all-rank verdict.  A rank whose probe raised counts as failed (its peers still reach the
-    agreement all-reduce, so nobody hangs on a half-run probe)."""
+    the same ``graph``).  Returns ``{"ok", "eager", "graph", "local_ok", "error"}``; ``ok`` is the
+    all-rank verdict.  A rank whose probe raised counts as failed.  The ranks agree (process-group
+    all-reduce, the control plane) after the eager phase and again after capturing the graph, so
+    the captured collectives are replayed only when every rank holds its graph: a rank whose
+    capture raised never leaves its peers waiting inside a replay."""
     device = torch.device(device)
     phase = _corrupt_phase(comm.rank)
     res = {"eager": None, "graph": None}
     err = None
     try:
         res["eager"] = _eager(comm, device, corrupt=phase == "all")
-        if graph and device.type == "cuda":
-            res["graph"] = _graphed(comm, device, corrupt=phase in ("all", "graph"))
     except Exception as e:  # noqa: BLE001 - a raising probe is a failed probe
         err = repr(e)
+    if graph and _graph_supported(device):
+        eager_bad = comm.all_reduce_scalars([0.0 if err is None else 1.0], op="max")[0]
+        state = None
+        if eager_bad == 0.0:
+            try:
+                state = _graph_capture(comm, device, fail=phase == "capture")
+            except Exception as e:  # noqa: BLE001
+                err = repr(e)
+            cap_bad = comm.all_reduce_scalars([0.0 if state is not None else 1.0], op="max")[0]
+            if cap_bad == 0.0:
+                try:
+                    res["graph"] = _graph_replay(comm, device, state,
+                                                 corrupt=phase in ("all", "graph"))
+                except Exception as e:  # noqa: BLE001
+                    err = repr(e)
+            else:
+                res["graph"] = False  # some rank has no graph: nobody replays
+            del state
+        else:
+            res["graph"] = False
     local_ok = err is None and res["eager"] is not False and res["graph"] is not False
     bad = comm.all_reduce_scalars([0.0 if local_ok else 1.0], op="max")[0]
     res.update(ok=bad == 0.0, local_ok=local_ok, error=err)
