@@ -124,6 +124,27 @@ def measure(a, world, amp, ef, extra=()):
 
     flags, gw = _flags(a, world, amp, ef)
     tr = Trainer(ewdml.parse_args(flags + list(extra), prog="bench.py"))
+    try:
+        return _measure(a, tr, gw)
+    finally:
+        tr.close()  # watchdog and own RCCL communicator (the next measure() builds its own)
+
+
+def _any_rank(flag: bool) -> bool:
+    """Whether ``flag`` holds on any rank (process-group all-reduce; every rank must call it)."""
+    import torch
+    import torch.distributed as dist
+
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return bool(flag)
+    dev = "cuda" if torch.cuda.is_available() and dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([1.0 if flag else 0.0], device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return bool(t.item() > 0)
+
+
+def _measure(a, tr, gw):
+    import torch
 
     def sync():
         if tr.cuda:
@@ -157,17 +178,25 @@ def measure(a, world, amp, ef, extra=()):
     from ewdml.parallel.engine import check_replicas
 
     ge = getattr(tr.exchange, "inner", tr.exchange)
-    # top-k encode counters; raises if a write block gave up on its look-back (corrupt payload)
-    tr.codec_health = ge.codec_health() if hasattr(ge, "codec_health") else {}
+    # top-k encode counters; raises if a write block gave up on its look-back (corrupt payload).
+    # The counters are per rank: the verdict is agreed after the replica check (which every rank
+    # must reach), so all ranks raise together and stay in step for the next measurement.
+    health_err = None
+    try:
+        tr.codec_health = ge.codec_health() if hasattr(ge, "codec_health") else {}
+    except Exception as exc:  # noqa: BLE001
+        health_err = repr(exc)
+        tr.codec_health = {"error": health_err[:300]}
 
     rep = None if every > 1 else check_replicas(tr.comm, tr.flat.data)
+    if _any_rank(health_err is not None):
+        raise RuntimeError(f"codec health check failed on some rank: {health_err}")
     final_loss = float(loss.detach()) if loss is not None else float("nan")
     tr.comm_kind = tr.comm.kind
     tr.comm_probe = None if tr.comm.probe is None else {
         k: tr.comm.probe[k] for k in ("ok", "eager", "graph")}
     g = getattr(tr, "_graphs", None)
     tr.overlap_comm_graphs = len(g[1].comms) if (g and g[0] == "segmented") else 0
-    tr.close()  # watchdog and own RCCL communicator (the next measure() builds its own)
     return elapsed_max, tr, final_loss, t_enq - t0, (elapsed_min, elapsed_max), rep
 
 
@@ -267,10 +296,15 @@ def main(argv=None):
         for key, amp, e, xf in extras:
             if cuda:
                 torch.cuda.empty_cache()
+            err = None
             try:
                 el, tr2, fl, _, _, rep2 = measure(a, world, amp, e, xf)
-            except Exception as exc:  # an extra never costs the headline line (same on every rank)
-                rec[f"error_{key}"] = repr(exc)[:300]
+            except Exception as exc:  # noqa: BLE001 - an extra never costs the headline line
+                err = repr(exc)[:300]
+            # agreed by every rank before the next measurement's collectives (a failure on one
+            # rank skips this extra everywhere)
+            if _any_rank(err is not None):
+                rec[f"error_{key}"] = err or "failed on another rank"
                 continue
             if rep2 is not None:
                 rec[f"replicas_identical_{key}"] = rep2["identical"]

@@ -176,7 +176,11 @@ class Config:
         if c.compress_grad.lower() == "none":
             c.compress = "none"
         if c.error_feedback is None:
-            c.error_feedback = c.compress in ("topk", "topk_qsgd")
+            # only the all-gather exchange keeps a residual (parallel/engine.py
+            # GradientExchange); the parameter-server / sharded exchanges have none, so their
+            # top-k runs keep the reference's schedule (no EF warm-up) and record no EF
+            c.error_feedback = (c.compress in ("topk", "topk_qsgd")
+                                and c.topology == "allgather")
         if c.ef_mode == "ef21" and c.error_feedback and c.device != "cpu" and not c.no_cuda:
             import os
 

@@ -75,8 +75,11 @@ def _lazy_into(conv, h) -> bool:
         return False
     from ..ops import conv as conv_hip
 
-    return conv_hip.enabled() and conv_hip.wino_tile_for(tuple(h.shape), h.dtype,
-                                                          conv.weight) > 0
+    # the conv must also take the MFMA path at all (channels_last weight, 16-B pointers, C % 64:
+    # conv2d_module's own test, on h as the stand-in of the same-shaped BN output), else it would
+    # fall back to a kernel that reads the never-written activation
+    return (conv_hip.enabled() and conv_hip.module_supported(conv, h)
+            and conv_hip.lazy_input_ok(tuple(h.shape), h.dtype, conv.weight))
 
 
 def _shortcut(sc, x):

@@ -101,6 +101,19 @@ def test_error_feedback_is_the_default_for_topk_codecs():
     assert not ewdml.parse_args(["--method", "3"]).error_feedback
 
 
+def test_error_feedback_default_only_where_a_residual_is_kept():
+    """only the all-gather exchange keeps an error-feedback residual; parameter-server
+    and sharded top-k runs default to none and keep the reference's schedule (no EF warm-up)."""
+    import ewdml
+
+    for topo in ("ps", "sharded"):
+        c = ewdml.parse_args(["--compress", "topk_qsgd", "--topology", topo])
+        assert not c.error_feedback
+        assert c.topk_warmup == "" and c.lr_warmup_epochs == 0
+    c = ewdml.parse_args(["--compress", "topk_qsgd", "--topology", "allgather"])
+    assert c.error_feedback and c.topk_warmup
+
+
 def test_ef21_rejected_at_parse_time_on_the_gpu(monkeypatch):
     """EF21 has only the torch-oracle encode: a GPU run is refused when the configuration is
     parsed, not after the model, buffers and communicator are set up."""
