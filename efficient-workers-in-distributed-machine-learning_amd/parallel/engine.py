@@ -588,46 +588,63 @@ OVERLAP_MAX_SPLITS = 3
 
 
 def plan_graph_mode(world: int, comm_kind: str, codec_kind: str, grad_numel: int,
-                    bits: int = 8, overlap: bool = True, bucket_bytes: int = 16 << 20) -> dict:
+                    bits: int = 8, overlap: bool = True, bucket_bytes: int = 16 << 20,
+                    model: str = None, topk_ratio: float = 0.01) -> dict:
     """``--hip-graph auto`` for the all-to-all exchange (``GradientExchange``).
 
     * N = 1, or collectives on the process group (not capturable), or ``--no-overlap``: the
       one-graph step (``full``; the trainer demotes it to ``split`` for process-group
       collectives).  At N = 1 there is nothing to hide: the segmented step only adds graph
       boundaries (+11 % on dense VGG-11, profiles/ab/segmented_overlap.txt).
-    * Top-k codecs: ``full`` at every N.  Their all-gather is a few hundred KiB per rank (tens of
-      microseconds over 7 xGMI links) while their encode, which has to run on the comm stream in a
-      segmented step, slows the concurrent backward GEMMs by more than it hides (+20 % at N = 1).
-    * Dense codecs (fp32 / half all-reduce, dense QSGD all-gather) at N > 1 whose per-rank wire
-      bytes reach ``OVERLAP_MIN_WIRE_BYTES``: ``segmented`` -- per-bucket collectives on their
-      own stream overlap the rest of backward, as Horovod's background all-reduce does
-      (``horvod_pytorch.py:197-201``) and the reference's ``LeNetSplit`` prototyped
-      (``src/model_ops/lenet.py:111-186``).  One split per 32 MiB of payload (at most 3), and
-      buckets small enough that every split point has buckets on both sides.
+    * A configuration with a measured N = 1 profile (``parallel/step_model.py``): the mode the
+      step model predicts faster at this N -- ``full`` (backward, then the collective) or
+      ``segmented`` (per-bucket collectives on their own stream beside the rest of backward, as
+      Horovod's background all-reduce does, ``horvod_pytorch.py:197-201``, and the reference's
+      ``LeNetSplit`` prototyped, ``src/model_ops/lenet.py:111-186``).  The prediction of both is
+      returned (``predicted_ms``) so a scaling run can be checked against it.
+    * Otherwise the codec-kind rule: ``full`` for top-k payloads (a few hundred KiB per rank;
+      their encode, which a segmented step runs on the comm stream, slows the concurrent backward
+      GEMMs by more than it hides: +20 % at N = 1), ``segmented`` for dense collectives whose
+      per-rank wire bytes reach ``OVERLAP_MIN_WIRE_BYTES``.
+    * Segmented steps get one split per 32 MiB of payload (at most 3) and buckets small enough
+      that every split point has buckets on both sides.
 
-    Returns ``{"mode", "splits", "bucket_bytes", "wire_bytes", "reason"}``."""
+    Returns ``{"mode", "splits", "bucket_bytes", "wire_bytes", "reason"}`` (+ ``predicted_ms``)."""
+    from .step_model import overlap_splits, predict, profile_for
+
     per_elem = {"none": 4.0, "fp16": 2.0, "bf16": 2.0, "qsgd": bits / 8.0}.get(codec_kind)
     payload = grad_numel * (per_elem or 0.0)
+    # top-k payload per rank (estimate): k entries of one code byte (4-bit: half) + a 2-byte index
+    pb = payload if per_elem is not None else grad_numel * topk_ratio * (2.0 + max(bits, 4) / 8.0)
     if codec_kind in ("none", "fp16", "bf16"):
         wire = 2.0 * (world - 1) / max(world, 1) * payload  # ring all-reduce
     else:
-        wire = (world - 1) * payload  # all-gather
+        wire = (world - 1) * pb  # all-gather
     out = {"mode": "full", "splits": 1, "bucket_bytes": int(bucket_bytes), "wire_bytes": int(wire)}
+    splits = overlap_splits(payload, OVERLAP_MAX_SPLITS, OVERLAP_BYTES_PER_SPLIT)
+    prof = profile_for(model, codec_kind)
+    pred = None
+    if prof is not None:
+        pred = predict(prof, world, codec_kind, pb, 4.0 * grad_numel, splits)
+        out["predicted_ms"] = pred
     if world <= 1:
         return dict(out, reason="one rank: nothing to overlap")
     if comm_kind != "rccl-stream":
         return dict(out, reason="process-group collectives are not captured")
     if not overlap:
         return dict(out, reason="--no-overlap")
+    want = (4 * grad_numel) // (2 * (splits + 1))
+    seg = {"mode": "segmented", "splits": splits,
+           "bucket_bytes": int(min(bucket_bytes, max(1 << 20, want)))}
+    if pred is not None:
+        if pred["segmented"] < pred["full"]:
+            return dict(out, **seg, reason="step model: overlap hides more than it costs")
+        return dict(out, reason="step model: the one-graph step is faster")
     if per_elem is None:
         return dict(out, reason="top-k payloads are small; the encode would slow backward")
     if wire < OVERLAP_MIN_WIRE_BYTES:
         return dict(out, reason="collective below the overlap threshold")
-    splits = int(min(OVERLAP_MAX_SPLITS, max(1, math.ceil(payload / OVERLAP_BYTES_PER_SPLIT))))
-    want = (4 * grad_numel) // (2 * (splits + 1))
-    bb = int(min(bucket_bytes, max(1 << 20, want)))
-    return {"mode": "segmented", "splits": splits, "bucket_bytes": bb, "wire_bytes": int(wire),
-            "reason": "dense collective overlapped with backward"}
+    return dict(out, **seg, reason="dense collective overlapped with backward")
 
 
 def replica_fingerprint(t: torch.Tensor) -> dict:

@@ -156,7 +156,8 @@ class Trainer:
             self.graph_plan = plan_graph_mode(
                 plan_world, self.comm.kind, cfg.compress,
                 sum(p.numel() for p in model.parameters() if p.requires_grad),
-                bits=cfg.qsgd_bits, overlap=cfg.overlap, bucket_bytes=bucket_bytes)
+                bits=cfg.qsgd_bits, overlap=cfg.overlap, bucket_bytes=bucket_bytes,
+                model=cfg.network, topk_ratio=cfg.topk_ratio)
             bucket_bytes = self.graph_plan["bucket_bytes"]
         self.flat = FlatModel(model, bucket_bytes=bucket_bytes,
                               attach_grads=not ptr_grads, bf16_params=bf16_params)
