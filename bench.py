@@ -276,6 +276,10 @@ def main(argv=None):
         "rccl_world": world if tr.comm_kind == "rccl-stream" else 0,
         "comm_probe": tr.comm_probe,
         "graph_plan": tr.graph_plan,
+        # the N > 1 step model's prediction for the mode that ran (parallel/step_model.py: N = 1
+        # measurements + an xGMI collective model), to check a scaling run against
+        "predicted_ms_per_step": ((tr.graph_plan or {}).get("predicted_ms") or {}).get(
+            "segmented" if tr.graph_mode == "segmented" else "full"),
         "codec_health": tr.codec_health,
         "step_ms_min": round(span[0] * 1e3 / a.steps, 4),
         "step_ms_max": round(span[1] * 1e3 / a.steps, 4),

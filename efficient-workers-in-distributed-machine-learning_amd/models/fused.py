@@ -80,7 +80,8 @@ class FusedFeatures(nn.Sequential):
     @staticmethod
     def _lazy_into(plan, gi, h, pool) -> bool:
         """Whether group gi's BN-ReLU(-pool) output feeds only the next group's conv and that
-        conv runs Winograd on it: then the conv's input transform applies the BN layer
+        conv forms its input on the fly (Winograd input transform, 2x2-map GEMM operand load): then
+        that conv applies the BN layer
         (ops/nn.py bn_relu(lazy=True)) and the activation is never written."""
         # pooled layers stay materialised: recomputing the 2x2 max for every patch element
         # (16 reads of h per element) costs more than the apply kernel it would save
@@ -96,7 +97,7 @@ class FusedFeatures(nn.Sequential):
             return False
         N, C, H, W = h.shape
         shape = (N, C, H // 2, W // 2) if pool else (N, C, H, W)
-        return conv_hip.enabled() and conv_hip.wino_tile_for(shape, h.dtype, nxt.weight) > 0
+        return conv_hip.enabled() and conv_hip.lazy_input_ok(shape, h.dtype, nxt.weight)
 
     def forward(self, x):
         if not (_ENABLED and x.is_cuda):

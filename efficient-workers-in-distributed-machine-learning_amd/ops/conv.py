@@ -97,6 +97,11 @@ SIDE_LAUNCHES = 0  # weight gradients issued on the side stream (tests)
 # shape, 2078 vs 1740 us per step for the six layers, ResNet-50 CIFAR 8.38K vs 8.53K img/s
 # (profiles/ab/conv_stride2_vs_miopen.txt), so MIOpen keeps them by default
 _S2 = os.environ.get("EWDML_CONV_S2", "0") == "1"
+# fp32 3x3 layers over 2x2 maps (VGG-11's conv7 / conv8) as dense position GEMMs
+# (ops/csrc/smallmap_f32.hip): one forward launch and one backward launch (data + weight gradient)
+# instead of Winograd's input / GEMM / output transform per pass.  EWDML_SMALLMAP=0: Winograd
+_SMALLMAP = os.environ.get("EWDML_SMALLMAP", "1") != "0"
+_SM_WS = {}
 
 
 def set_stride2(on: bool):
@@ -303,6 +308,46 @@ def wino_ok(x, w) -> bool:
     return wino_tile(x, w) > 0
 
 
+def set_smallmap(on: bool):
+    """Dense position GEMMs for fp32 3x3 layers over 2x2 maps on / off (off: Winograd)."""
+    global _SMALLMAP
+    _SMALLMAP = bool(on)
+
+
+def smallmap_for(shape, dtype, w) -> bool:
+    """Whether the fp32 conv of an input of ``shape`` by ``w`` runs as the 2x2-map dense position
+    GEMM (``ops/csrc/smallmap_f32.hip``): 3x3 weight, H = W = 2, N, C_in and C_out multiples of
+    64."""
+    if not _SMALLMAP or dtype != torch.float32 or w.dtype != dtype or tuple(w.shape[-2:]) != (3, 3):
+        return False
+    N, C, H, W = shape
+    Nc = w.shape[0]
+    return (H == 2 and W == 2 and w.shape[1] == C and N % 64 == 0 and C % 64 == 0
+            and Nc % 64 == 0 and N * 4 * max(C, Nc) < 2 ** 31)
+
+
+def lazy_input_ok(shape, dtype, w) -> bool:
+    """Whether the conv of an input of ``shape`` forms a lazily applied BatchNorm(+ReLU) input on
+    the fly (Winograd input transform or the 2x2-map GEMM's operand load)."""
+    return wino_tile_for(shape, dtype, w) > 0 or smallmap_for(shape, dtype, w)
+
+
+def _sm_ws(device, N, C, Nc):
+    """(slab, tickets) of the 2x2-map GEMMs' in-launch split-K reduction, per (device, stream); the
+    tickets are zeroed once and left zero by every launch."""
+    C_ = require()
+    key = (device.index, _stream())
+    need = (C_.sm_f32_ws_floats(N, C, Nc), C_.sm_f32_counters(N, C, Nc))
+    ws = _SM_WS.get(key)
+    if ws is None or ws[0].numel() < need[0] or ws[1].numel() < need[1]:
+        slab = torch.empty(max(need[0], ws[0].numel() if ws else 0), dtype=torch.float32,
+                           device=device)
+        cnt = torch.zeros(max(need[1], ws[1].numel() if ws else 0), dtype=torch.int32,
+                          device=device)
+        ws = _SM_WS[key] = (slab, cnt)
+    return ws
+
+
 def epilogue_fusion_ok(x) -> bool:
     """Whether a conv on input ``x`` takes the epilogue fusions (BN backward sums, addend)."""
     return x.numel() <= (_EPI_MAX_F32 if x.dtype == torch.float32 else _EPI_MAX)
@@ -434,16 +479,30 @@ class _Conv(torch.autograd.Function):
         # the following fused BN (ops/nn.py bn_act) skips its statistics pass when present
         part = torch.empty(_part_floats(N * H * W, Nc), dtype=torch.float32, device=x.device)
         ctx.wino = None
-        m = wino_tile(x, w)
+        ctx.sm = None
+        sm = sink is None and smallmap_for(tuple(x.shape), x.dtype, w)
+        m = 0 if sm else wino_tile(x, w)
         # x may be the lazily applied output of a fused BN layer (ops/nn.py bn_relu(lazy=True)):
-        # the Winograd input transform applies that layer on the fly; anything else needs it
+        # the Winograd input transform (or the 2x2-map GEMM's operand load, unpooled) applies
+        # that layer on the fly; anything else needs it
         lazy = getattr(x, "_ew_lazy_fwd", None)
-        if lazy is not None and not m:
+        if lazy is not None and (not (m or sm) or (sm and lazy[4])):
             from .nn import materialize
 
             materialize(x)
             lazy = None
-        if m:
+        if sm:
+            slab, cnt = _sm_ws(x.device, N, C, Nc)
+            bh, bstats, _bcode, bnbt, _bpool = lazy if lazy is not None else (None,) * 5
+            rows = C_.sm_f32_fwd(_ptr(x) if lazy is None else 0, _ptr(bh), _ptr(bstats),
+                                 _ptr(bnbt), _ptr(w), _ptr(y), _ptr(slab), slab.numel(),
+                                 _ptr(cnt), cnt.numel(), N, C, Nc, _ptr(part), part.numel(),
+                                 _stream())
+            if lazy is not None:  # a later materialisation must not count the batch twice
+                x._ew_materialize = getattr(x, "_ew_materialize_no_nbt", None)
+            # the BN source of x (None: x itself), formed again by the weight gradient
+            ctx.sm = ((bh, bstats) if lazy is not None else None,)
+        elif m:
             aa = (m + 2) ** 2
             # transformed weight U[a^2][Nc][C] (m = 2: kept for the backward-data GEMMs, read
             # flipped) and input V (kept for the weight-gradient GEMMs)
@@ -482,6 +541,8 @@ class _Conv(torch.autograd.Function):
         x, w = ctx.saved_tensors
         N, C, H, W = x.shape
         Nc, k = w.shape[0], w.shape[-1]
+        if ctx.sm is not None:
+            return _Conv._backward_sm(ctx, dy, x, w)
         # dy may be the lazily formed input gradient of the BN layer this conv feeds (ops/nn.py):
         # the Winograd backward-data input transform forms it on the fly, anything else needs it
         lazy = getattr(dy, "_ew_lazy_bwd", None)
@@ -602,6 +663,53 @@ class _Conv(torch.autograd.Function):
                 if len(_SIDE_QUEUE) >= _WGRAD_BATCH:
                     _issue_side()
         ctx.wino = None
+        return dx, dw, None, None
+
+
+    @staticmethod
+    def _backward_sm(ctx, dy, x, w):
+        """Backward of a 2x2-map conv: input and weight gradient in one launch, dy formed from the
+        BN layer this conv feeds when it is lazy, x from the BN layer in front when it was."""
+        C_ = require()
+        flush_pending()  # a deferred Winograd weight-gradient transform, while its data is warm
+        N, C, H, W = x.shape
+        Nc = w.shape[0]
+        xsrc, = ctx.sm
+        ctx.sm = None
+        lazy = getattr(dy, "_ew_lazy_bwd", None)
+        if lazy is not None and dy.dtype != x.dtype:
+            from .nn import materialize
+
+            materialize(dy)
+            lazy = None
+        if lazy is None:
+            dy = dy.contiguous(memory_format=torch.channels_last)
+            if dy.dtype != x.dtype:
+                dy = dy.to(x.dtype)
+            if dy.data_ptr() % 16:
+                dy = dy.clone(memory_format=torch.channels_last)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x, memory_format=torch.channels_last)
+        if ctx.needs_input_grad[1]:
+            dw = torch.empty_like(w, memory_format=torch.channels_last)
+        node, ctx.bn_node = ctx.bn_node, None
+        ctx.sink = None
+        link = _bn_bwd_link(node, x) if dx is not None else None
+        ph, pres, pcode, pstats, prelu = link if link is not None else (None,) * 5
+        part = (torch.empty(_part_floats(N * H * W, C), dtype=torch.float32, device=x.device)
+                if link is not None else None)
+        oh, odn, ocode, ostats, ocoef, opool = lazy if lazy is not None else (None,) * 6
+        bh, bstats = xsrc if xsrc is not None else (None, None)
+        slab, cnt = _sm_ws(x.device, N, C, Nc)
+        rows = C_.sm_f32_bwd(_ptr(x) if xsrc is None else 0, _ptr(bh), _ptr(bstats),
+                             _ptr(dy) if lazy is None else 0, _ptr(oh), _ptr(odn), _ptr(ocode),
+                             _ptr(ostats), _ptr(ocoef), int(bool(opool)), _ptr(w), _ptr(dx),
+                             _ptr(dw), _ptr(slab), slab.numel(), _ptr(cnt), cnt.numel(), N, C,
+                             Nc, _ptr(ph), _ptr(pres), _ptr(pcode), _ptr(pstats), int(prelu or 0),
+                             _ptr(part), part.numel() if part is not None else 0, _stream())
+        if rows > 0:
+            node._ew_pre_bwd = (part, rows, dx, dx._version)
         return dx, dw, None, None
 
 
@@ -794,7 +902,8 @@ def _apply(x, w, sink=None):
     part = getattr(node, "bn_part", None) if node is not None else None
     if part is not None:
         y._ew_bn_part = part
-    if node is not None and getattr(node, "wino", None) is not None:
+    if node is not None and (getattr(node, "wino", None) is not None
+                             or getattr(node, "sm", None) is not None):
         y._ew_wino_out = True  # the BN layer it feeds may leave its backward apply to us
     return y
 
@@ -831,4 +940,6 @@ def conv2d_module(m, x, sink=None):
     if (_S2 and m.bias is None and m.padding_mode == "zeros" and x.is_cuda
             and s2_supported(x, m.weight, m.stride, m.padding, m.dilation, m.groups)):
         return conv_s2(x, m.weight)
-    return m(x)
+    from .nn import materialize
+
+    return m(materialize(x))  # a lazily applied BN output is written before a foreign kernel

@@ -351,6 +351,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("wino_f32_wgrad_out", &ew_wino_f32_wgrad_out);
   m.def("wino_f32_fwd_bn", &ew_wino_f32_fwd_bn);
   m.def("wino_f32_bwd_data_bn", &ew_wino_f32_bwd_data_bn);
+  m.def("sm_f32_ws_floats", &ew_sm_f32_ws_floats);
+  m.def("sm_f32_counters", &ew_sm_f32_counters);
+  m.def("sm_f32_fwd", &ew_sm_f32_fwd);
+  m.def("sm_set_fence", &ew_sm_set_fence);
+  m.def("topk_fused_select_max_blocks", &ew_topk_fused_select_max_blocks);
+  m.def("sm_f32_bwd", &ew_sm_f32_bwd);
   m.def("maxpool2_nhwc", &ew_maxpool2_nhwc);
   m.def("maxpool3s2_nhwc", &ew_maxpool3s2_nhwc);
   m.def("gap_nhwc", &ew_gap_nhwc);

@@ -100,6 +100,8 @@ size_t ew_topk_scratch_bytes(int num_tensors, int num_chunks, long long bucket_l
                              long long total_cap);
 std::vector<int> ew_topk_stats(uintptr_t scratch, int num_tensors, int num_chunks);
 std::vector<long long> ew_graph_info(uintptr_t graph, const std::string& dot_path);
+// largest candidate-block count the fused select kernel takes (0: always three kernels)
+int ew_topk_fused_select_max_blocks();
 int ew_topk_lookback_errors(uintptr_t scratch, int num_tensors, int num_chunks);
 void ew_topk_encode(const TopkEncodeArgs& a);
 void ew_topk_decode_apply(const TopkDecodeArgs& a);
@@ -289,6 +291,23 @@ int ew_wino_f32_wgrad(uintptr_t dy, uintptr_t V, uintptr_t dw, uintptr_t D, int 
                       int W, int C, int Nc, int m, int defer_out, uintptr_t stream);
 void ew_wino_f32_wgrad_out(uintptr_t src, int split, uintptr_t dw, int Nc, int C, int m,
                            uintptr_t stream);
+
+// ---- fp32 3x3 convolutions over 2x2 maps as dense position GEMMs (smallmap_f32.hip): slab
+// workspace floats and ticket ints (zeroed once; the kernels leave them zero) for N, C, Nc
+long long ew_sm_f32_ws_floats(long long N, int C, int Nc);
+int ew_sm_set_fence(int on);  // split-K hand-off with fences (1) or write-through (0); returns the previous
+long long ew_sm_f32_counters(long long N, int C, int Nc);
+int ew_sm_f32_fwd(uintptr_t x, uintptr_t bn_h, uintptr_t bn_stats, uintptr_t nbt, uintptr_t w,
+                  uintptr_t y, uintptr_t slab, long long slab_floats, uintptr_t cnt,
+                  long long cnt_ints, long long N, int C, int Nc, uintptr_t bnpart,
+                  long long bnpart_floats, uintptr_t stream);
+int ew_sm_f32_bwd(uintptr_t x, uintptr_t bn_h, uintptr_t bn_stats, uintptr_t dy,
+                  uintptr_t out_h, uintptr_t out_dnext, uintptr_t out_code, uintptr_t out_stats,
+                  uintptr_t out_coef, int out_pool, uintptr_t w, uintptr_t dx, uintptr_t dw,
+                  uintptr_t slab, long long slab_floats, uintptr_t cnt, long long cnt_ints,
+                  long long N, int C, int Nc, uintptr_t pb_h, uintptr_t pb_res, uintptr_t pb_code,
+                  uintptr_t pb_stats, int pb_relu, uintptr_t bnpart, long long bnpart_floats,
+                  uintptr_t stream);
 
 // ---- RCCL communicator issuing collectives on the caller's stream (rccl_comm.hip) ----
 // dtype codes: 0 f32, 1 bf16, 2 f16, 3 u8, 4 i32, 5 f64, 6 i64; op: 0 sum, 1 max, 2 min, 3 avg

@@ -544,6 +544,16 @@ __device__ __forceinline__ void topk_lookback(uint32_t gt, uint32_t eq, const Ch
 // one) were compacted by k_pk_hist0 in index order, so this block reads only them -- ~3 % of the
 // chunk -- instead of the chunk.  Same selection, positions, codes, bitmap words and residual /
 // velocity updates as the full pass below, bit for bit.
+// The tensor scale a payload publishes: NaN once any encode of this bucket counted a failure
+// (a look-back or a fused-select barrier that gave up: its offsets / thresholds are stale), so a
+// corrupted exchange poisons every rank's decoded update at once -- a non-finite loss at the next
+// step -- instead of training on silently until the next health check (codec_health raises too).
+__device__ __forceinline__ float topk_pub_scale(float scale, const int* lb_err) {
+  return (lb_err && __hip_atomic_load(lb_err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
+             ? __uint_as_float(0x7fc00000u)
+             : scale;
+}
+
 template <int VK, bool EF>
 __device__ __forceinline__ void topk_write_cands(
     const ChunkRow& c, const TensorRow& tr, float* __restrict__ resid, float* __restrict__ vel,
@@ -576,7 +586,8 @@ __device__ __forceinline__ void topk_write_cands(
     reinterpret_cast<uint16_t*>(payload + counts_off)[blockIdx.x] = (uint16_t)(gtc + ties);
   const float inv = scale > 0.0f ? levels / scale : 0.0f;
   const float step = VK != VK_F32 ? scale * inv_levels : 0.0f;
-  if (threadIdx.x == 0 && c.local == 0) reinterpret_cast<float*>(payload + scales_off)[c.tensor] = scale;
+  if (threadIdx.x == 0 && c.local == 0)
+    reinterpret_cast<float*>(payload + scales_off)[c.tensor] = topk_pub_scale(scale, lb_err);
   uint16_t* idx_out = reinterpret_cast<uint16_t*>(payload + idx_off) + (bitmap ? 0 : tr.idx0) -
                       tr.entry0;
   const uint32_t gbase = bucket_offset + (uint32_t)c.start;
@@ -699,7 +710,8 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_write(
     const float scale = __uint_as_float(state[c.tensor * 4 + 2]);
     inv = scale > 0.0f ? levels / scale : 0.0f;
     if (VK != VK_F32) step = scale * inv_levels;
-    if (threadIdx.x == 0 && c.local == 0) reinterpret_cast<float*>(payload + scales_off)[c.tensor] = scale;
+    if (threadIdx.x == 0 && c.local == 0)
+      reinterpret_cast<float*>(payload + scales_off)[c.tensor] = topk_pub_scale(scale, lb_err);
   } else {
     ties = chunk_ties[blockIdx.x];
     ebase = (uint32_t)tr.entry0 + chunk_off[blockIdx.x];
@@ -846,6 +858,11 @@ __global__ __launch_bounds__(EW_BLOCK) void k_pk_hist0(
   const ChunkRow c = chunks[blockIdx.x];
   const TensorRow tr = tensors[c.tensor];
   if (threadIdx.x == 0) lb[blockIdx.x] = 0ull;  // the write pass's look-back word
+  // the candidate passes' per-tensor arrival counts start from zero every encode: a fused select
+  // whose barrier gave up (pk_wait's poll bound) can leave one behind, which would desynchronise
+  // every later encode's barriers (the generation words are read relative to their value)
+  if (blockIdx.x == 0)
+    for (int t = threadIdx.x; t < T; t += EW_BLOCK) tick[TICK_STRIDE * (T + t)] = 0;
   float4 v[EW_CU];
   ew_ld_chunk(gp, nullptr, c, v);
   topk_ef_stage<EFM>(gp, dg, resid, c, v);
@@ -1867,20 +1884,32 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_decode_sparse(
 #define EW_LAUNCH(kern, grid, stream, ...) \
   hipLaunchKernelGGL(kern, dim3(grid), dim3(EW_BLOCK), 0, (hipStream_t)(stream), __VA_ARGS__)
 
-// Largest candidate-pass grid launched as the fused select kernel: one block per CU, so every
-// block is resident at once whatever else shares the GPU (its barriers wait for peers of the
-// same launch).  EWDML_TOPK_FUSED_SELECT=0: always the three pass kernels.
+// Largest candidate-pass grid launched as the fused select kernel (its per-tensor barriers wait
+// for peers of the same launch, so every block must become resident).  One block per CU, and only
+// when the occupancy API reports room for at least two per CU: the API can read one block per CU
+// high for some SGPR counts (MI355X_MICROARCH.md, correctness boundaries), so two leave the one
+// we use even then.  Kernels sharing the GPU (a concurrent graph branch) delay blocks, they cannot
+// strand them: they do not wait on this launch, so they drain and free their CUs
+// (tests/kernels/test_hip_codecs.py::test_fused_select_beside_a_long_gemm); a barrier that still
+// gives up counts a failure, which codec_health raises and the next payload's NaN scale makes
+// visible on every rank (topk_pub_scale).  No cooperative launch: the step graph captures this
+// kernel, and the graph path does not enforce co-residency either.  EWDML_TOPK_FUSED_SELECT=0:
+// always the three pass kernels.
 static int ew_pk_fused_max_blocks() {
   static int n = -1;
   if (n < 0) {
     const char* e = std::getenv("EWDML_TOPK_FUSED_SELECT");
-    int dev = 0, cus = 0;
+    int dev = 0, cus = 0, occ = 0;
     EW_CHECK(hipGetDevice(&dev));
     EW_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    n = (e && e[0] == '0') ? 0 : cus;
+    EW_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &occ, reinterpret_cast<const void*>(&k_pk_select), EW_BLOCK, 0));
+    n = ((e && e[0] == '0') || occ < 2) ? 0 : cus;
   }
   return n;
 }
+
+int ew_topk_fused_select_max_blocks() { return ew_pk_fused_max_blocks(); }
 
 void ew_topk_encode(const TopkEncodeArgs& a) {
   auto* chunks = reinterpret_cast<const ChunkRow*>(a.chunks);

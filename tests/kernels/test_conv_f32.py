@@ -18,15 +18,17 @@ pytestmark = pytest.mark.gpu
 TOL = 1e-5
 
 
-def _conv(wino=False, min_c=64, tile="auto"):
+def _conv(wino=False, min_c=64, tile="auto", sm=False):
     """The conv module with the Winograd path off (direct implicit GEMM for every shape) or on
-    for every layer with at least ``min_c`` channels, tile m = 2, 4 or auto."""
+    for every layer with at least ``min_c`` channels, tile m = 2, 4 or auto; ``sm``: the 2x2-map
+    dense position GEMMs (ops/csrc/smallmap_f32.hip) for the layers they take."""
     from ewdml import ops
     from ewdml.ops import conv
 
     ops.require()
     conv.set_enabled(True)
     conv.set_winograd(wino, min_c, tile)
+    conv.set_smallmap(sm)
     return conv
 
 
@@ -35,10 +37,11 @@ def _restore_winograd():
     from ewdml.ops import conv
 
     saved = (conv._WINO, conv._WINO_MIN_C, conv._WINO_TILE)
-    s2 = conv._S2
+    s2, sm = conv._S2, conv._SMALLMAP
     yield
     conv.set_winograd(*saved)
     conv.set_stride2(s2)
+    conv.set_smallmap(sm)
 
 
 def _rel(a, b):
@@ -429,14 +432,15 @@ def test_fp32_vgg11_step_vs_fp64():
     exact gradient is 0 (BN removes them), so any fp32 value is pure rounding noise."""
     from ewdml.models import build_model
 
-    conv = _conv(wino=True, min_c=128, tile=2)  # the production choice
+    conv = _conv(wino=True, min_c=128, tile=2, sm=True)  # the production choice
     torch.manual_seed(0)
     m0 = build_model("vgg11", 10).to(memory_format=torch.channels_last)
     for mod in m0.modules():
         if isinstance(mod, torch.nn.Dropout):
             mod.p = 0.0
-    x = torch.randn(32, 3, 32, 32).contiguous(memory_format=torch.channels_last)
-    y = torch.randint(0, 10, (32,))
+    # batch 64: the 2x2-map layers take the small-map GEMMs (N % 64 == 0)
+    x = torch.randn(64, 3, 32, 32).contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (64,))
     m64 = copy.deepcopy(m0).double()
     out64 = m64(x.double())
     F.cross_entropy(out64, y).backward()
@@ -456,9 +460,10 @@ def test_fp32_vgg11_step_vs_fp64():
                                                                  torch.nn.BatchNorm2d)}
         big = [(p.grad, r, n) for (n, p), r in zip(m.named_parameters(), g64)
                if float(r.norm()) > 1e-6 and n not in zero]
-        res.append((_rel(out, out64), max(_rel(a, b) for a, b, _ in big)))
-    (o_h, e_h), (o_m, e_m) = res
-    assert o_h < 1e-5 and e_h < 1e-4, (o_h, e_h)
+        worst = max(big, key=lambda t: _rel(t[0], t[1]))
+        res.append((_rel(out, out64), _rel(worst[0], worst[1]), worst[2]))
+    (o_h, e_h, n_h), (o_m, e_m, n_m) = res
+    assert o_h < 1e-5 and e_h < 1e-4, (o_h, e_h, n_h, e_m, n_m)
     assert o_h <= 2 * o_m + 1e-6 and e_h <= 2 * e_m + 1e-5, (o_h, o_m, e_h, e_m)
 
 
@@ -519,7 +524,7 @@ def test_lazy_bn_through_winograd_matches_materialised(steps):
     from ewdml.models import fused
     from ewdml.ops import nn as onn
 
-    _conv(wino=True, min_c=128, tile=2)
+    _conv(wino=True, min_c=128, tile=2, sm=True)  # the production choice
     torch.manual_seed(0)
     m0 = build_model("vgg11", 10).to(memory_format=torch.channels_last).cuda()
     for mod in m0.modules():
@@ -773,3 +778,146 @@ def test_projection_shortcut_gradient_sink_matches_autograd_sum(s2):
         assert _rel(o_a, o_b) < 1e-4, _rel(o_a, o_b)
         assert e <= 3 * e_n + 1e-5 and max(errs) <= 3 * max(noise) + 1e-5, (e, e_n, max(errs),
                                                                              max(noise))
+
+
+# ---- 2x2-map dense position GEMMs (ops/csrc/smallmap_f32.hip) ----
+SM_SHAPES = [  # (N, C, Nc) on 2x2 maps
+    (128, 512, 512),   # VGG-11 conv7 / conv8: tile counts multiples of 8 (XCD-grouped splits)
+    (64, 256, 128),
+    (64, 64, 192),     # 12 forward / 4 backward tiles: plain split mapping
+    (192, 128, 64),
+]
+
+
+@pytest.mark.parametrize("N,C,Nc", SM_SHAPES)
+def test_conv_f32_smallmap_forward_backward(N, C, Nc):
+    """Forward, input and weight gradient of the 2x2-map GEMMs against float64; bitwise
+    repeatable (in-launch split-K reduced in split order); close to the direct kernels."""
+    conv = _conv(sm=True)
+    x, w = _data(N, C, Nc, 2, 2, seed=51)
+    assert conv.smallmap_for(tuple(x.shape), x.dtype, w)
+    g = torch.Generator(device="cuda").manual_seed(52)
+    dy = torch.randn(N, Nc, 2, 2, device="cuda", generator=g).contiguous(
+        memory_format=torch.channels_last)
+    xa, wa = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
+    y = conv.conv(xa, wa)
+    assert getattr(y.grad_fn, "sm", None) is not None  # the small-map path ran
+    y.backward(dy)
+    ref, gx, gw = _ref64(x, w, 3, dy)
+    assert _rel(y, ref) < TOL, _rel(y, ref)
+    assert _rel(xa.grad, gx) < TOL, _rel(xa.grad, gx)
+    assert _rel(wa.grad, gw) < TOL, _rel(wa.grad, gw)
+    xb, wb = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
+    y2 = conv.conv(xb, wb)
+    y2.backward(dy)
+    assert torch.equal(y, y2) and torch.equal(xa.grad, xb.grad) and torch.equal(wa.grad, wb.grad)
+    d = _conv(sm=False)
+    assert _rel(d.conv(x, w), y) < 2 * TOL
+    # only one of the gradients requested
+    xc = x.clone().requires_grad_(True)
+    _conv(sm=True).conv(xc, w).backward(dy)
+    assert torch.equal(xc.grad, xa.grad)
+    wc = w.clone().requires_grad_(True)
+    _conv(sm=True).conv(x, wc).backward(dy)
+    assert torch.equal(wc.grad, wa.grad)
+
+
+def test_conv_f32_smallmap_bn_statistics():
+    """The split-K reducer's BatchNorm partial sums (8 rows) give the BN kernels' own statistics."""
+    from ewdml.ops import nn as fnn
+
+    conv = _conv(sm=True)
+    x, w = _data(128, 512, 512, 2, 2, seed=53)
+    bn0 = torch.nn.BatchNorm2d(512).cuda()
+    bn1 = copy.deepcopy(bn0)
+    h = conv.conv(x, w.clone().requires_grad_(True))
+    part, rows = h._ew_bn_part
+    assert rows == 8
+    y0 = fnn.bn_act(h, bn0, "relu")
+    y1 = fnn.bn_act(h.detach().clone(), bn1, "relu")
+    assert _rel(y0, y1) < 1e-5
+    assert torch.allclose(bn0.running_mean, bn1.running_mean, rtol=1e-5, atol=1e-7)
+    assert torch.allclose(bn0.running_var, bn1.running_var, rtol=1e-5, atol=1e-7)
+
+
+@pytest.mark.parametrize("front_pool", [False, True])
+@pytest.mark.parametrize("pool", [True, False])
+def test_conv_f32_smallmap_lazy_bn_matches_materialised(pool, front_pool):
+    """conv -> BN-ReLU -> 2x2-map conv -> BN-ReLU(-pool to 1x1): with the BN layers applied inside
+    the small-map GEMM's operand loads (forward x, backward dy; ops/nn.py lazy BN) every output,
+    gradient, running statistic and batch counter equals the materialised path bit for bit; the
+    producing BN layer's backward sums come from the reducer (pooled: routed by the 4x4 -> 2x2
+    window codes).  The 2x2-map conv's output is also checked against float64."""
+    from ewdml.ops import nn as fnn
+
+    conv = _conv(wino=True, min_c=64, tile=2, sm=True)
+    N, C = 64, 128
+    HW0 = 4 if front_pool else 2
+    x0, w0 = _data(N, C, C, HW0, HW0, seed=61)
+    _, w1 = _data(N, C, C, 2, 2, seed=62)
+    bns = [torch.nn.BatchNorm2d(C).cuda() for _ in range(2)]
+    with torch.no_grad():
+        for bn in bns:
+            bn.weight.uniform_(0.5, 1.5)
+            bn.bias.uniform_(-0.3, 0.3)
+    gshape = (N, C, 1, 1) if pool else (N, C, 2, 2)
+    g = torch.randn(gshape, device="cuda").contiguous(memory_format=torch.channels_last)
+    lazy_bwd = fnn._LAZY_BWD
+    runs = []
+    try:
+        for lazy in (True, False):
+            fnn._LAZY_BWD = lazy
+            b0, b1 = copy.deepcopy(bns[0]), copy.deepcopy(bns[1])
+            xa, wa, wb = (t.clone().requires_grad_(True) for t in (x0, w0, w1))
+            h = conv.conv(xa, wa)
+            y = fnn.bn_relu(h, None, b0, pool=front_pool, lazy=lazy and not front_pool)
+            z = conv.conv(y, wb)
+            assert getattr(z.grad_fn, "sm", None) is not None
+            if not lazy:
+                zref = _ref64(fnn.materialize(y).detach(), w1, 3)
+                assert _rel(z, zref) < TOL, _rel(z, zref)
+            out = fnn.bn_act(z, b1, "relu", pool=pool)
+            out.backward(g)
+            runs.append([out, xa.grad, wa.grad, wb.grad] +
+                        [t for b in (b0, b1) for t in (b.weight.grad, b.bias.grad,
+                                                      b.running_mean, b.running_var,
+                                                      b.num_batches_tracked)])
+    finally:
+        fnn._LAZY_BWD = lazy_bwd
+    for i, (a, b) in enumerate(zip(*runs)):
+        assert torch.equal(a, b), i
+
+
+@pytest.mark.parametrize("mode,pool", [("relu", True), ("relu", False), ("none", False)])
+def test_conv_f32_smallmap_bn_backward_sums(mode, pool):
+    """The 2x2-map backward-data reducer's BN backward sums (the producing BN layer's sum dz and
+    sum dz * (h - mean), routed through its 4x4 -> 2x2 pool codes) give the gradients of the BN
+    layer's own statistics pass."""
+    from ewdml.ops import nn as fnn
+
+    conv = _conv(wino=True, min_c=64, tile=2, sm=True)
+    N, C = 64, 128
+    HW = 4 if pool else 2
+    x0, w0 = _data(N, C, C, HW, HW, seed=71)
+    _, w1 = _data(N, C, C, 2, 2, seed=72)
+    bn0 = torch.nn.BatchNorm2d(C).cuda()
+    with torch.no_grad():
+        bn0.weight.uniform_(0.5, 1.5)
+        bn0.bias.uniform_(-0.3, 0.3)
+    g = torch.randn(N, C, 2, 2, device="cuda").contiguous(memory_format=torch.channels_last)
+    grads = []
+    for fused in (True, False):
+        conv.set_bn_bwd_fusion(fused)
+        used = fnn.PRE_BWD_USED
+        bn = copy.deepcopy(bn0)
+        xa, wa, wb = (t.clone().requires_grad_(True) for t in (x0, w0, w1))
+        h = conv.conv(xa, wa)
+        y = fnn.bn_act(h, bn, mode, pool=pool)
+        z = conv.conv(y, wb)
+        assert getattr(z.grad_fn, "sm", None) is not None
+        z.backward(g)
+        assert (fnn.PRE_BWD_USED > used) == fused
+        grads.append([xa.grad, wa.grad, wb.grad, bn.weight.grad, bn.bias.grad])
+    conv.set_bn_bwd_fusion(True)
+    for i, (a, b) in enumerate(zip(*grads)):
+        assert _rel(a, b) < 1e-5, (i, _rel(a, b))

@@ -566,3 +566,45 @@ def test_lookback_failure_is_reported(monkeypatch, predict):
 
     with pytest.raises(RuntimeError, match="look-back"):
         GradientExchange.codec_health(_Ex)
+    # and the next payload publishes NaN scales: every rank's decoded update goes non-finite at
+    # once, so a corrupted exchange cannot train on silently until the next health check
+    ops.topk_encode(dp, g, pay, lay, 127, "max", 3)
+    torch.cuda.synchronize()
+    T = plan.num_tensors
+    assert torch.isnan(pay[:4 * T].view(torch.float32)).all()
+
+
+def test_fused_select_beside_a_long_gemm():
+    """the fused select's per-tensor barriers with a concurrent kernel on
+    another stream holding CUs (a segmented graph runs encodes beside backward GEMMs).  The GEMM
+    does not wait on the encode, so it drains and the select's blocks all become resident: no
+    barrier gives up, and every payload is bitwise the oracle's."""
+    ops.require()
+    C_ = ops.require()
+    assert C_.topk_fused_select_max_blocks() > 0  # the fused kernel is in use on this GPU
+    plan = _plan([1728, 64, 2359296, 512, 262144, 5120], 0.01, bucket_offset=64)
+    lay = Layout.build("topk_qsgd", plan, 8)
+    dp = ops.DevicePlan(plan, DEV)
+    pay = torch.zeros(lay.nbytes, dtype=torch.uint8, device=DEV)
+    r_ref, v_ref = torch.zeros(plan.length), torch.zeros(plan.length)
+    r_dev, v_dev = r_ref.to(DEV), v_ref.to(DEV)
+    hp = dict(momentum=0.9, dampening=0.0, nesterov=False, weight_decay=0.0)
+    a = torch.randn(6144, 6144, device=DEV)
+    side = torch.cuda.Stream()
+    for it in range(10):
+        g = _grad(plan, seed=80 + it)
+        key = stream_key(1, it, 0)
+        ref = oracle.encode_topk(g.clone(), plan, lay, 127, "max", key, residual=r_ref,
+                                 dgc=dict(velocity=v_ref, param=None, **hp))
+        gd = g.to(DEV)
+        torch.cuda.synchronize()
+        busy = [a @ a for _ in range(3)]  # ~10 ms of GEMMs on the default stream
+        with torch.cuda.stream(side):
+            ops.topk_encode(dp, gd, pay, lay, 127, "max", key, resid=r_dev,
+                            dgc=dict(velocity=v_dev, param=None, **hp))
+        torch.cuda.synchronize()
+        del busy
+        assert torch.equal(pay.cpu(), ref), f"step {it}: payload"
+    st = ops.topk_stats(dp)
+    assert st["lookback_errors"] == 0, st
+    assert st["fast"] > 0  # the candidate (fused select) path ran
