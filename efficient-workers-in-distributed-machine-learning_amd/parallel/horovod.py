@@ -15,8 +15,9 @@ none/fp16/bf16, packed all-gather for qsgd/topk/topk_qsgd -- the fusion buffer o
 levels* across ranks and decodes with the local norm), every rank's payload
 is decoded with its own scale before averaging.
 
-``Adasum`` (``--use-adasum``, ``horvod_pytorch.py:35-36``): the dense gradients are all-gathered and
-combined with the Adasum rule in a fixed binary tree over ranks, identical on every rank.
+``Adasum`` (``--use-adasum``, ``horvod_pytorch.py:35-36``): the dense gradients are combined with the
+Adasum rule in a fixed binary tree over ranks by pairwise exchanges between the tree's groups
+(``adasum_tree``: D log2 N bytes per rank), identical on every rank.
 """
 import os
 
@@ -172,22 +173,64 @@ class _OptAdapter:
         self.steps += 1
 
 
+def adasum_pair(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """The Adasum rule for two gradients (a: the lower-rank group's, b: the higher one's), in
+    float64: ``(1 - a.b / 2|a|^2) a + (1 - a.b / 2|b|^2) b`` (a zero vector keeps weight 1)."""
+    a, b = a.double(), b.double()
+    dot = torch.dot(a, b)
+    na, nb = torch.dot(a, a), torch.dot(b, b)
+    one = torch.ones((), dtype=a.dtype, device=a.device)
+    ca = torch.where(na > 0, 1 - dot / (2 * torch.where(na > 0, na, one)), one)
+    cb = torch.where(nb > 0, 1 - dot / (2 * torch.where(nb > 0, nb, one)), one)
+    return (ca * a + cb * b).float()
+
+
 def adasum_combine(grads: torch.Tensor) -> torch.Tensor:
-    """Adasum of ``grads`` [N, D] over a fixed binary tree (rank order)."""
+    """Adasum of ``grads`` [N, D] over a fixed binary tree (rank order): at level l the groups of
+    2^l consecutive ranks combine pairwise, a trailing unpaired group passes through."""
     vs = list(grads.unbind(0))
     while len(vs) > 1:
-        nxt = []
-        for i in range(0, len(vs) - 1, 2):
-            a, b = vs[i].double(), vs[i + 1].double()
-            dot = torch.dot(a, b)
-            na, nb = torch.dot(a, a), torch.dot(b, b)
-            ca = 1 - dot / (2 * na) if na > 0 else torch.ones((), dtype=a.dtype, device=a.device)
-            cb = 1 - dot / (2 * nb) if nb > 0 else torch.ones((), dtype=a.dtype, device=a.device)
-            nxt.append((ca * a + cb * b).float())
+        nxt = [adasum_pair(vs[i], vs[i + 1]) for i in range(0, len(vs) - 1, 2)]
         if len(vs) % 2:
             nxt.append(vs[-1])
         vs = nxt
     return vs[0]
+
+
+def adasum_tree(comm, g: torch.Tensor) -> torch.Tensor:
+    """The same tree as :func:`adasum_combine`, run distributed by point-to-point exchanges:
+    at level l every rank holds its group's combined vector; it swaps it with one rank of the
+    partner group (group index xor 1) and both combine (lower group first), so after
+    ceil(log2 N) levels every rank holds the root.  O(D) memory and D * log2 N bytes per rank on
+    the wire, instead of all-gathering N vectors (N * D), and bitwise the same result on every
+    rank (the same operands in the same order).  A trailing partner group smaller than the
+    group serves several ranks: each of its members sends to the ranks that map to it."""
+    rank, n = comm.rank, comm.world
+    v = g.detach().clone()
+    level = 0
+    while (1 << level) < n:
+        size = 1 << level
+        grp = rank // size
+        pg = grp ^ 1
+        lo, hi = pg * size, min(n, (pg + 1) * size)  # partner group's ranks
+        if lo >= n:  # no partner group: pass through
+            level += 1
+            continue
+
+        def src_of(r):  # the partner-group rank that serves rank r
+            q = (r // size ^ 1) * size + r % size
+            return min(q, min(n, ((r // size ^ 1) + 1) * size) - 1)
+
+        other = torch.empty_like(v)
+        reqs = [comm.irecv(other, src_of(rank), tag=100 + level)]
+        for r in range(lo, hi):  # the partner ranks that take their vector from me
+            if src_of(r) == rank:
+                reqs.append(comm.isend(v, r, tag=100 + level))
+        for q in reqs:
+            q.wait()
+        v = adasum_pair(v, other) if grp < pg else adasum_pair(other, v)
+        level += 1
+    return v
 
 
 class _DistributedOptimizer:
@@ -225,9 +268,7 @@ class _DistributedOptimizer:
             return
         if self.op == Adasum and self.comm.world > 1:
             g = self.flat.grad
-            allg = torch.zeros((self.comm.world, g.numel()), dtype=g.dtype, device=g.device)
-            self.comm.all_gather(allg.view(-1), g)
-            g.copy_(adasum_combine(allg))
+            g.copy_(adasum_tree(self.comm, g))  # pairwise tree exchange (horvod_pytorch.py:35-36)
             self.exchange._active = False
         else:
             self.exchange.finish(apply=False)

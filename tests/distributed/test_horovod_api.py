@@ -123,8 +123,11 @@ def _adasum_ref(vs):
     return vs[0]
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 3, 4])
 def test_adasum_closed_form(tmp_path, world):
+    """The pairwise-tree exchange (horovod.adasum_tree: point-to-point swaps between the tree's
+    groups, a trailing smaller group serving several ranks at world 3) gives every rank the
+    closed-form tree of rank-ordered Adasum pairs."""
     from ewdml.parallel import horovod as hvd
 
     res = run_world(_step, world, tmp_path, args=("none", hvd.Adasum))
