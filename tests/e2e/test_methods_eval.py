@@ -36,3 +36,24 @@ def test_methods_eval_bytes_match_layouts(method):
         expect = static[4] / 20
     assert r["MiB_per_iter"] == pytest.approx(expect, rel=1e-9)
     assert 0 < r["top1"] <= 100
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("method", [3, 5, 6])
+def test_methods_eval_on_the_gpu_bytes_and_time_to_accuracy(method):
+    """The MI355X path of the harness (three Gloo ranks sharing one GPU, HIP codecs and graphs):
+    the same byte column as the layouts predict, and a time-to-accuracy record."""
+    from ewdml.models import build_model
+    from ewdml.parallel.flat import FlatModel
+    from tools.methods_eval import MiB, run_method
+    from tools.methods_table import table
+
+    steps = 40
+    r = run_method(method, 0.4, steps, every=20, target=99.0, device="cuda", targets=(10.0,))
+    static = table("LeNet", 0.4)
+    flat = FlatModel(build_model("LeNet"))
+    pad = 4 * (flat.numel - flat.param_numel) / MiB
+    expect = static[method - 1] + {3: 4}.get(method, 0) * pad if method <= 5 else static[4] / 20
+    assert r["MiB_per_iter"] == pytest.approx(expect, rel=1e-9)
+    assert r["device"] == "cuda" and r["train_s"] > 0
+    assert "10.0" in r["hit"] and r["hit"]["10.0"][0] in (20, 40)

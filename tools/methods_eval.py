@@ -17,6 +17,12 @@ Measured per method (from the exchanges' byte counters, not from layouts):
     next to the report's "Communication and Computation Time" chart (VGG-11, minutes).
 
     python tools/methods_eval.py [--steps 1500] [--ratio 0.4] [--out RESULTS_methods.md]
+    python tools/methods_eval.py --device cuda --targets 97,98 --out-gpu gpu.md   # MI355X
+
+``--device cuda``: the same three Gloo ranks share one MI355X (as
+``tests/distributed/test_gpu_two_ranks.py`` does), through the HIP codecs, fused update kernels
+and HIP graphs; the table adds wall-clock seconds of training (evaluations excluded) to each
+``--targets`` accuracy, next to the report's end-to-end training time and epochs per method.
 """
 import argparse
 import json
@@ -37,6 +43,10 @@ PUBLISHED_TOP1 = [98, 97, 97, 98, 96.5, 97]  # LeNet, Top1 Accuracy.png
 # Computation Time .png); the report publishes no LeNet split
 PUBLISHED_VGG_COMM_MIN = [20, 17, 20, 16, 10, 5]
 PUBLISHED_VGG_COMP_MIN = [380, 382, 380, 383, 385, 381]
+# LeNet end-to-end training time (minutes) and epochs to converge per method (Report.zip: End to
+# end training time.png, Total Epochs.png; 2 Colab CPU workers + 1 server, 60K MNIST images)
+PUBLISHED_E2E_MIN = [20, 19, 20, 16, 15, 10]
+PUBLISHED_EPOCHS = [20, 21, 20, 20, 23, 21]
 
 
 def _free_port():
@@ -45,10 +55,10 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _flags(method, ratio, steps):
+def _flags(method, ratio, steps, device="cpu"):
     f = ["--network", "LeNet", "--dataset", "MNIST", "--data-dir", MNIST,
          "--holdout-from-test", "1000", "--batch-size", "64", "--lr", "0.01", "--momentum", "0.9",
-         "--eval-freq", "0", "--quiet", "--device", "cpu", "--amp", "none", "--method",
+         "--eval-freq", "0", "--quiet", "--device", device, "--amp", "none", "--method",
          str(method), "--topk-ratio", str(ratio), "--qsgd-norm", "l2", "--test-batch-size",
          "1000", "--max-steps", str(steps), "--log-interval", "1000000", "--phase-timing",
          "--no-error-feedback"]
@@ -57,21 +67,30 @@ def _flags(method, ratio, steps):
     return f
 
 
-def _worker(rank, world, port, method, ratio, steps, every, target, out):
+def _worker(rank, world, port, method, ratio, steps, every, target, out, device="cpu",
+            targets=()):
+    cuda = device == "cuda"
+    # on the GPU every rank shares the box's one device
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
-                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+                      WORLD_SIZE=str(world), LOCAL_RANK="0" if cuda else str(rank))
     import torch
 
     torch.set_num_threads(2)
     import torch.distributed as dist
 
+    if cuda:
+        torch.cuda.set_device(0)  # every rank on the one GPU
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         import ewdml
         from ewdml.runtime import Trainer
 
         torch.manual_seed(0)
-        tr = Trainer(ewdml.parse_args(_flags(method, ratio, steps)))
+        # phase timing partitions the eager step (no graphs): off for the wall-clock runs
+        flags = _flags(method, ratio, steps, device)
+        if cuda:
+            flags.remove("--phase-timing")
+        tr = Trainer(ewdml.parse_args(flags))
         worker = not getattr(tr, "is_server", False)
         from ewdml.parallel.engine import Stopwatch
 
@@ -79,41 +98,53 @@ def _worker(rank, world, port, method, ratio, steps, every, target, out):
         comm_ms = comp_ms = 0.0
         phases = {}
         curve, reached = [], None
+        hit = {}  # target -> (step, training seconds)
+        train_s, t_last = 0.0, time.perf_counter()
         for s in range(1, steps + 1):
             tr.train_step()
             st = tr.exchange.last
             sent += st.wire_bytes_sent
             recv += st.wire_bytes_recv
-            ph = tr.clock.phases()
-            for k, v in ph.items():
-                phases[k] = phases.get(k, 0.0) + v
-            c, p = Stopwatch.split(ph)
-            comm_ms += c
-            comp_ms += p
+            if not cuda:
+                ph = tr.clock.phases()
+                for k, v in ph.items():
+                    phases[k] = phases.get(k, 0.0) + v
+                c, p = Stopwatch.split(ph)
+                comm_ms += c
+                comp_ms += p
             if s % every == 0 or s == steps:
+                if cuda:
+                    torch.cuda.synchronize()
+                train_s += time.perf_counter() - t_last
                 # every rank evaluates its replica (the server holds the model in PS methods)
                 top1 = tr.evaluate()["top1"]
                 curve.append((s, top1))
                 if reached is None and top1 >= target:
                     reached = s
+                for tg in targets:
+                    if tg not in hit and top1 >= tg:
+                        hit[tg] = (s, round(train_s, 3))
+                t_last = time.perf_counter()
         res = {"rank": rank, "worker": worker, "sent": sent, "recv": recv, "steps": steps,
                "curve": curve, "reached": reached, "top1": curve[-1][1],
                "comm_s": comm_ms / 1e3, "compute_s": comp_ms / 1e3,
-               "phase_ms_per_step": {k: v / steps for k, v in phases.items()}}
+               "phase_ms_per_step": {k: v / steps for k, v in phases.items()},
+               "train_s": round(train_s, 3), "hit": {str(k): v for k, v in hit.items()},
+               "graph": getattr(tr, "graph_mode", None)}
         with open(os.path.join(out, f"r{rank}.json"), "w") as f:
             json.dump(res, f)
     finally:
         dist.destroy_process_group()
 
 
-def run_method(method, ratio, steps, every, target):
+def run_method(method, ratio, steps, every, target, device="cpu", targets=()):
     import torch.multiprocessing as mp
 
     world = 3 if method <= 5 else 2
     with tempfile.TemporaryDirectory() as out:
         ctx = mp.start_processes(_worker, nprocs=world, join=False, start_method="spawn",
                                  args=(world, _free_port(), method, ratio, steps, every, target,
-                                       out))
+                                       out, device, tuple(targets)))
         while not ctx.join(timeout=600):
             pass
         res = [json.load(open(os.path.join(out, f"r{r}.json"))) for r in range(world)]
@@ -127,7 +158,40 @@ def run_method(method, ratio, steps, every, target):
             "bytes_per_iter": per_iter, "MiB_per_iter": per_iter / MiB,
             "top1": model["top1"], "reached": model["reached"], "curve": model["curve"],
             "comm_s": comm, "compute_s": comp, "comm_frac": comm / max(comm + comp, 1e-12),
-            "worker_phase_ms": workers[0]["phase_ms_per_step"]}
+            "worker_phase_ms": workers[0]["phase_ms_per_step"], "device": device,
+            "train_s": max(r["train_s"] for r in res), "hit": model["hit"],
+            "graph": workers[0]["graph"]}
+
+
+def gpu_table(rows, steps, ratio, targets, batches_per_epoch=9000 / 64):
+    """Markdown section: time / steps to each target on the GPU against the report."""
+    tg = [f"{t:g}" for t in targets]
+    lines = [
+        "## MI355X: time to accuracy per method",
+        "",
+        f"`python tools/methods_eval.py --device cuda --steps {steps} --ratio {ratio} --targets "
+        f"{','.join(tg)}`: the same runs (1 server + 2 workers; Method 6 two ranks), the three "
+        "Gloo ranks sharing one MI355X, through the HIP codecs, fused update kernels and HIP "
+        "graphs.  Seconds are training wall-clock up to the first held-out evaluation at the "
+        "target (evaluations excluded; the evaluation interval bounds the resolution); epochs = "
+        f"steps / {batches_per_epoch:.1f} batches of this 9K-image set.  The report's times are "
+        "minutes to convergence on Colab CPUs with 60K images, for scale.",
+        "",
+        "| Method | MiB/iter | final top-1 % | " +
+        " | ".join(f"steps / epochs / s to {t} %" for t in tg) +
+        " | train s total | graph | report end-to-end min | report epochs |",
+        "|---|---|---|" + "---|" * len(tg) + "---|---|---|---|",
+    ]
+    for r in rows:
+        m = r["method"]
+        cells = []
+        for t in targets:
+            h = r["hit"].get(str(float(t))) or r["hit"].get(str(t))
+            cells.append(f"{h[0]} / {h[0] / batches_per_epoch:.1f} / {h[1]:.2f}" if h else "-")
+        lines.append(f"| {m} | {r['MiB_per_iter']:.4f} | {r['top1']:.1f} | " + " | ".join(cells) +
+                     f" | {r['train_s']:.1f} | {r['graph']} | {PUBLISHED_E2E_MIN[m - 1]} | "
+                     f"{PUBLISHED_EPOCHS[m - 1]} |")
+    return lines
 
 
 def main(argv=None):
@@ -139,17 +203,24 @@ def main(argv=None):
     ap.add_argument("--methods", default="1,2,3,4,5,6")
     ap.add_argument("--out", default=None, help="write a markdown table here")
     ap.add_argument("--json", default=None)
+    ap.add_argument("--device", default="cpu", choices=["cpu", "cuda"])
+    ap.add_argument("--targets", default="", help="top-1 targets for time-to-accuracy, e.g. 97,98")
+    ap.add_argument("--out-gpu", default=None, help="write the time-to-accuracy section here")
     a = ap.parse_args(argv)
+    targets = [float(v) for v in a.targets.split(",") if v]
     rows = []
     for m in [int(v) for v in a.methods.split(",")]:
         t0 = time.time()
-        r = run_method(m, a.ratio, a.steps, a.every, a.target)
+        r = run_method(m, a.ratio, a.steps, a.every, a.target, a.device, targets)
         r["wall_s"] = round(time.time() - t0, 1)
         rows.append(r)
         print(json.dumps({k: v for k, v in r.items() if k != "curve"}), flush=True)
     if a.json:
         with open(a.json, "w") as f:
             json.dump(rows, f, indent=1)
+    if a.out_gpu:
+        with open(a.out_gpu, "w") as f:
+            f.write("\n".join(gpu_table(rows, a.steps, a.ratio, targets)) + "\n")
     if a.out:
         from tools.methods_table import table
 
