@@ -51,21 +51,25 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int SM_T = 512;  // threads per block (8 waves, two per SIMD)
-constexpr int SM_BM = 64, SM_BN = 64, SM_BK = 32;
+constexpr int SM_BM = 64, SM_BN = 64, SM_BK = 64;
 constexpr int SM_RC_PITCH = SM_BN + 4;                 // RC image row pitch (floats)
-constexpr int SM_KC_BYTES = SM_BM * SM_BK * 4;         // 8 KB
-constexpr int SM_RC_BYTES = SM_BK * SM_RC_PITCH * 4;   // 8.5 KB
+constexpr int SM_KC_BYTES = SM_BM * SM_BK * 4;         // 16 KB
+constexpr int SM_RC_BYTES = SM_BK * SM_RC_PITCH * 4;   // 17 KB
 constexpr int SM_STAGE = 2 * SM_RC_BYTES;              // A + B image, any layouts
 // the A image's size (B follows it): an RC image is larger than a KC one
 template <int AL>
 constexpr int sm_abytes() { return AL == 0 ? SM_KC_BYTES : SM_RC_BYTES; }
 constexpr int SM_TILE = SM_BM * SM_BN;                 // slab floats per (tile, split)
+struct F2 {  // two plain operand vectors
+  f32x4 v[2];
+};
 
 enum { SM_KC = 0, SM_RC = 1 };
 
-// KC image: [64 rows][32 k], 128-B rows, 16-B chunk c of row r at c ^ ((r >> 1) & 7) (the swizzle
-// of conv_f32.hip: a ds_read_b128 lane group reading 16 rows at one chunk hits 16 bank slots)
-__device__ __forceinline__ int sm_kc(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
+// KC image: [64 rows][64 k], 256-B rows (one full pass over the 64 banks), 16-B chunk c of row r at
+// c ^ (r & 15): a ds_read_b128 lane group reading 16 rows at one chunk hits 16 distinct 4-bank
+// slots, and the 16 lanes writing one row's chunks fill the row
+__device__ __forceinline__ int sm_kc(int r, int c) { return r * 256 + ((c ^ (r & 15)) << 4); }
 
 // tap joining input position ip and output position op of a 2x2 map (positions p = h * 2 + w)
 __device__ __forceinline__ int sm_tap(int ip, int op) {
@@ -136,16 +140,19 @@ __device__ __forceinline__ void sm_dy_coef(const SmDy& s, int Nc, int o, SmDyCoe
 // Operand staging is split in two: the k-loop issues a step's raw loads two steps ahead (RawX /
 // RawDy, no arithmetic on them) and forms the operand only when it writes the step to LDS one step
 // later, so a lazily formed operand (KIND 1 / 2) never makes the loop wait for its loads.
-struct RawX {  // x: the value (KIND 0) or the BN input and its scale / shift (KIND 1)
-  f32x4 v, sc, sh;
+// A thread stages two vectors of each operand per step: rows (or k-rows) r and r + 32, the same
+// four channels.
+struct RawX {  // x: the values (KIND 0) or the BN inputs and their scale / shift (KIND 1)
+  f32x4 v[2], sc, sh;
 };
+// rows at off and off + rs
 template <int XK>
-__device__ __forceinline__ void sm_raw_x(const SmX& s, long long off, const float* stats_c,
-                                         int C, RawX& r) {
-  if constexpr (XK == 0) {
-    r.v = *reinterpret_cast<const f32x4*>(s.x + off);
-  } else {
-    r.v = *reinterpret_cast<const f32x4*>(s.h + off);
+__device__ __forceinline__ void sm_raw_x(const SmX& s, long long off, long long rs,
+                                         const float* stats_c, int C, RawX& r) {
+  const float* src = XK == 0 ? s.x : s.h;
+  r.v[0] = *reinterpret_cast<const f32x4*>(src + off);
+  r.v[1] = *reinterpret_cast<const f32x4*>(src + off + rs);
+  if constexpr (XK == 1) {
     if (stats_c) {  // per-step channels (else hoisted by the caller)
       r.sc = *reinterpret_cast<const f32x4*>(stats_c + 2 * C);
       r.sh = *reinterpret_cast<const f32x4*>(stats_c + 3 * C);
@@ -153,14 +160,14 @@ __device__ __forceinline__ void sm_raw_x(const SmX& s, long long off, const floa
   }
 }
 template <int XK>
-__device__ __forceinline__ f32x4 sm_make_x(const RawX& r) {
+__device__ __forceinline__ f32x4 sm_make_x(const RawX& r, int i) {
   if constexpr (XK == 0) {
-    return r.v;
+    return r.v[i];
   } else {
     f32x4 v;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const float z = r.v[q] * r.sc[q] + r.sh[q];  // as k_bn_fwd_apply writes it
+      const float z = r.v[i][q] * r.sc[q] + r.sh[q];  // as k_bn_fwd_apply writes it
       v[q] = (z > 0.0f || z != z) ? z : 0.0f;
     }
     return v;
@@ -168,45 +175,51 @@ __device__ __forceinline__ f32x4 sm_make_x(const RawX& r) {
 }
 
 struct RawDy {  // dy (KIND 0) or this conv's output h, the BN layer's output gradient, its codes
-  f32x4 v, dn;
-  uint32_t code;
+  f32x4 v[2], dn[2];
+  uint32_t code[2];
   SmDyCoef k;
 };
-// dy at image n, output position op, channels o..o+3; coef: load the channels' coefficients
-// (per-step channels) or leave them to the caller (hoisted)
+// dy at images n and n + 32, output position op, channels o..o+3; coef: load the channels'
+// coefficients (per-step channels) or leave them to the caller (hoisted)
 template <int DK>
 __device__ __forceinline__ void sm_raw_dy(const SmDy& s, int Nc, int n, int op, int o, bool coef,
                                           RawDy& r) {
-  const long long off = ((long long)n * 4 + op) * Nc + o;
-  if constexpr (DK == 0) {
-    r.v = *reinterpret_cast<const f32x4*>(s.dy + off);
-  } else {
-    r.v = *reinterpret_cast<const f32x4*>(s.h + off);
-    if constexpr (DK == 3) {  // 2x2 -> 1x1 pool: the window is the whole map, op's code is op
-      r.dn = *reinterpret_cast<const f32x4*>(s.dnext + (long long)n * Nc + o);
-      r.code = *reinterpret_cast<const uint32_t*>(s.code + (long long)n * Nc + o);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const long long m = n + 32 * i;
+    const long long off = (m * 4 + op) * Nc + o;
+    if constexpr (DK == 0) {
+      r.v[i] = *reinterpret_cast<const f32x4*>(s.dy + off);
     } else {
-      r.dn = *reinterpret_cast<const f32x4*>(s.dnext + off);
-      r.code = 0u;
+      r.v[i] = *reinterpret_cast<const f32x4*>(s.h + off);
+      if constexpr (DK == 3) {  // 2x2 -> 1x1 pool: the window is the whole map, op's code is op
+        r.dn[i] = *reinterpret_cast<const f32x4*>(s.dnext + m * Nc + o);
+        r.code[i] = *reinterpret_cast<const uint32_t*>(s.code + m * Nc + o);
+      } else {
+        r.dn[i] = *reinterpret_cast<const f32x4*>(s.dnext + off);
+        r.code[i] = 0u;
+      }
     }
+  }
+  if constexpr (DK != 0) {
     if (coef) sm_dy_coef(s, Nc, o, r.k);
   }
 }
 template <int DK>
 __device__ __forceinline__ f32x4 sm_make_dy(const SmDy& s, int op, const RawDy& r,
-                                            const SmDyCoef& k) {
+                                            const SmDyCoef& k, int i) {
   if constexpr (DK == 0) {
-    return r.v;
+    return r.v[i];
   } else {
     f32x4 v;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const float dp =
-          (DK != 3 || ((r.code >> (8 * q)) & 0xffu) == (uint32_t)op) ? r.dn[q] : 0.0f;
+          (DK != 3 || ((r.code[i] >> (8 * q)) & 0xffu) == (uint32_t)op) ? r.dn[i][q] : 0.0f;
       // the expressions of k_bn_bwd_apply: the same contraction, the same bits
-      const float z = r.v[q] * k.sc[q] + k.sh[q];
+      const float z = r.v[i][q] * k.sc[q] + k.sh[q];
       const float dz = !(z <= 0.0f) ? dp : 0.0f;
-      v[q] = k.sc[q] * dz + k.e[q] * (r.v[q] - k.mean[q]) + k.f[q];
+      v[q] = k.sc[q] * dz + k.e[q] * (r.v[i][q] - k.mean[q]) + k.f[q];
     }
     return v;
   }
@@ -214,8 +227,8 @@ __device__ __forceinline__ f32x4 sm_make_dy(const SmDy& s, int op, const RawDy& 
 
 // ---- the GEMM core: 8 waves (two per SIMD) as 4 x 2 tiles of 16 rows x 32 columns over a
 // 64 x 64 tile, v_mfma_f32_16x16x4_f32 (A lane l = A[l & 15][k], B lane l = B[k][l & 15], D lane
-// l reg e = D[4 (l >> 4) + e][l & 15]), a 32-deep k-step per iteration through two LDS stages.
-// Lane group g = lane >> 4 takes k = 4 (4 r + g) + jj for MFMA (r, jj), r < 2, in both operands.
+// l reg e = D[4 (l >> 4) + e][l & 15]), a 64-deep k-step per iteration through two LDS stages.
+// Lane group g = lane >> 4 takes k = 4 (4 r + g) + jj for MFMA (r, jj), r < 4, in both operands.
 constexpr int SM_WM = 4, SM_WN = 2;        // wave grid
 constexpr int SM_NJ = SM_BN / SM_WN / 16;  // 16-column accumulators per wave (2)
 
@@ -236,9 +249,10 @@ __device__ __forceinline__ void sm_mma_step(const char* __restrict__ st, int wm,
   const char* As = st;
   const char* Bs = st + sm_abytes<AL>();
   const int g = lane >> 4, li = lane & 15;
-  f32x4 fa[2], fb[2][SM_NJ];
+  constexpr int R = SM_BK / 16;
+  f32x4 fa[R], fb[R][SM_NJ];
 #pragma unroll
-  for (int r = 0; r < 2; ++r) {
+  for (int r = 0; r < R; ++r) {
     const int ch = r * 4 + g;
     if constexpr (AL == SM_KC) {
       fa[r] = *reinterpret_cast<const f32x4*>(As + sm_kc(wm * 16 + li, ch));
@@ -260,7 +274,7 @@ __device__ __forceinline__ void sm_mma_step(const char* __restrict__ st, int wm,
     }
   }
 #pragma unroll
-  for (int r = 0; r < 2; ++r)
+  for (int r = 0; r < R; ++r)
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj)
 #pragma unroll
@@ -268,22 +282,23 @@ __device__ __forceinline__ void sm_mma_step(const char* __restrict__ st, int wm,
         acc.a[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[r][jj], fb[r][j][jj], acc.a[j], 0, 0, 0);
 }
 
-// one operand vector -> LDS stage.  KC ([64 rows][32 k]): thread t's chunk t & 7 of row t >> 3;
-// RC ([32 k][64 cols]): chunk t & 15 of k-row t >> 4
+// operand vector i of thread t -> LDS stage: chunk t & 15 of row (KC, [64 rows][64 k]) or k-row
+// (RC, [64 k][64 cols]) (t >> 4) + 32 i
 template <int L>
-__device__ __forceinline__ void sm_put(char* img, int t, const f32x4& v) {
+__device__ __forceinline__ void sm_put(char* img, int t, int i, const f32x4& v) {
+  const int r = (t >> 4) + 32 * i;
   if constexpr (L == SM_KC)
-    *reinterpret_cast<f32x4*>(img + sm_kc(t >> 3, t & 7)) = v;
+    *reinterpret_cast<f32x4*>(img + sm_kc(r, t & 15)) = v;
   else
-    *reinterpret_cast<f32x4*>(img + ((t >> 4) * SM_RC_PITCH + (t & 15) * 4) * 4) = v;
+    *reinterpret_cast<f32x4*>(img + (r * SM_RC_PITCH + (t & 15) * 4) * 4) = v;
 }
 
 // The pipelined k-loop over ksteps steps, SM_NS register stages deep: step s + SM_NS is loaded
 // while s computes and s + 1 is written to the other LDS stage (the loads have SM_NS - 1 steps to
 // land: a 64x64 step is only ~1k SIMD cycles of MFMA, shorter than a miss to HBM under load, so two
 // stages -- conv_f32.hip's depth for its 4x longer steps -- left the loop waiting on memory).
-// LA(s, RA&) / LB(s, RB&) issue step s's raw loads, MA(const RA&) / MB(const RB&) form the operand
-// vectors at LDS-write time.  Loads past the last step are clamped re-loads of it.
+// LA(s, RA&) / LB(s, RB&) issue step s's raw loads, MA(const RA&, i) / MB(const RB&, i) form the
+// thread's operand vector i (i < 2) at LDS-write time.  Loads past the last step are clamped re-loads of it.
 constexpr int SM_NS = 2;
 template <int AL, int BL, typename RA, typename RB, typename LA, typename LB, typename MA,
           typename MB>
@@ -302,8 +317,11 @@ __device__ __forceinline__ void sm_gemm(char* smem, int ksteps, LA&& la, LB&& lb
     la(min(i, last), ra[i]);
     lb(min(i, last), rb[i]);
   }
-  sm_put<AL>(smem, t, ma(ra[0]));
-  sm_put<BL>(smem + sm_abytes<AL>(), t, mb(rb[0]));
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    sm_put<AL>(smem, t, i, ma(ra[0], i));
+    sm_put<BL>(smem + sm_abytes<AL>(), t, i, mb(rb[0], i));
+  }
   __syncthreads();
   // iteration s: compute LDS stage s % 2, reload register slot s % SM_NS with step s + SM_NS,
   // write step s + 1 (slot (s + 1) % SM_NS) to the other stage
@@ -313,8 +331,11 @@ __device__ __forceinline__ void sm_gemm(char* smem, int ksteps, LA&& la, LB&& lb
     lb(min(s + SM_NS, last), rb[u]);
     sm_mma_step<AL, BL>(smem + (u & 1) * SM_STAGE, wm, wn, lane, acc);
     char* ns = smem + ((u + 1) & 1) * SM_STAGE;
-    sm_put<AL>(ns, t, ma(ra[(u + 1) % SM_NS]));
-    sm_put<BL>(ns + sm_abytes<AL>(), t, mb(rb[(u + 1) % SM_NS]));
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      sm_put<AL>(ns, t, i, ma(ra[(u + 1) % SM_NS], i));
+      sm_put<BL>(ns + sm_abytes<AL>(), t, i, mb(rb[(u + 1) % SM_NS], i));
+    }
     __syncthreads();
   };
   static_assert(SM_NS == 2 || SM_NS == 4, "register stages");
@@ -461,17 +482,22 @@ __global__ __launch_bounds__(SM_T) void k_sm_fwd(SmX xs, const float* __restrict
   const int ot = tile % ots, op = (tile / ots) & 3, mt = tile / (ots * 4);
   const int ip = split, tap = sm_tap(ip, op);
   const int n0 = mt * SM_BM, o0 = ot * SM_BN;
-  const int q = t & 7, r0 = t >> 3;  // KC: chunk q of row r0
+  const int q = t & 15, r0 = t >> 4;  // KC: chunk q of rows r0, r0 + 32
   const long long arow = ((long long)(n0 + r0) * 4 + ip) * C + q * 4;
   const float* wr = w + ((long long)(o0 + r0) * 9 + tap) * C + q * 4;
   SmAcc acc;
-  sm_gemm<SM_KC, SM_KC, RawX, f32x4>(
+  sm_gemm<SM_KC, SM_KC, RawX, F2>(
       smem, C / SM_BK,
       [&](int s, RawX& r) {
-        sm_raw_x<XK>(xs, arow + s * SM_BK, XK == 1 ? xs.stats + s * SM_BK + q * 4 : nullptr, C, r);
+        sm_raw_x<XK>(xs, arow + s * SM_BK, 32LL * 4 * C,
+                     XK == 1 ? xs.stats + s * SM_BK + q * 4 : nullptr, C, r);
       },
-      [&](int s, f32x4& r) { r = *reinterpret_cast<const f32x4*>(wr + s * SM_BK); },
-      [&](const RawX& r) { return sm_make_x<XK>(r); }, [&](const f32x4& r) { return r; }, acc);
+      [&](int s, F2& r) {
+        r.v[0] = *reinterpret_cast<const f32x4*>(wr + s * SM_BK);
+        r.v[1] = *reinterpret_cast<const f32x4*>(wr + 32LL * 9 * C + s * SM_BK);
+      },
+      [&](const RawX& r, int i) { return sm_make_x<XK>(r, i); },
+      [&](const F2& r, int i) { return r.v[i]; }, acc);
   __syncthreads();
   if (!sm_reduce(acc, slab, cnt, tile, split, &flag, fence)) return;
   const int lane = t & 63, wq = t >> 6, wm = wq / SM_WN, wn = wq % SM_WN;
@@ -510,18 +536,20 @@ __global__ __launch_bounds__(SM_T) void k_sm_bwd(SmX xs, SmDy ds, const float* _
     const int ct = tile % cts, ip = (tile / cts) & 3, mt = tile / (cts * 4);
     const int op = split, tap = sm_tap(ip, op);
     const int n0 = mt * SM_BM, c0 = ct * SM_BN;
-    const int q = t & 7, r0 = t >> 3;            // A (KC): row n0 + r0, channels 4 q..
-    const int kr = t >> 4, cq = (t & 15) * 4;    // B (RC): k-row o = kr, columns c0 + cq
+    const int q = t & 15, r0 = t >> 4;           // A (KC): rows n0 + r0 (+ 32), channels 4 q..
+    const int kr = t >> 4, cq = (t & 15) * 4;    // B (RC): k-rows o = kr (+ 32), columns c0 + cq
     const float* wb = w + ((long long)kr * 9 + tap) * C + c0 + cq;
     SmAcc acc;
-    sm_gemm<SM_KC, SM_RC, RawDy, f32x4>(
+    sm_gemm<SM_KC, SM_RC, RawDy, F2>(
         smem, Nc / SM_BK,
         [&](int s, RawDy& r) { sm_raw_dy<DK>(ds, Nc, n0 + r0, op, s * SM_BK + q * 4, true, r); },
-        [&](int s, f32x4& r) {
-          r = *reinterpret_cast<const f32x4*>(wb + (long long)s * SM_BK * 9 * C);
+        [&](int s, F2& r) {
+          const float* p = wb + (long long)s * SM_BK * 9 * C;
+          r.v[0] = *reinterpret_cast<const f32x4*>(p);
+          r.v[1] = *reinterpret_cast<const f32x4*>(p + 32LL * 9 * C);
         },
-        [&](const RawDy& r) { return sm_make_dy<DK>(ds, op, r, r.k); },
-        [&](const f32x4& r) { return r; }, acc);
+        [&](const RawDy& r, int i) { return sm_make_dy<DK>(ds, op, r, r.k, i); },
+        [&](const F2& r, int i) { return r.v[i]; }, acc);
     __syncthreads();
     if (!sm_reduce(acc, slab, cnt, tile, split, &flag, fence)) return;
     float s1[SM_NJ][4], s2[SM_NJ][4];
@@ -580,7 +608,7 @@ __global__ __launch_bounds__(SM_T) void k_sm_bwd(SmX xs, SmDy ds, const float* _
   const int ot = rem / cts, ct = rem % cts;
   const int o0 = ot * SM_BN, c0 = ct * SM_BN;
   const int np = sm_npairs(tap);
-  const int kr = t >> 4, cq = (t & 15) * 4;  // both RC: k-row n = kr, columns +cq
+  const int kr = t >> 4, cq = (t & 15) * 4;  // both RC: k-rows n = kr (+ 32), columns +cq
   SmDyCoef k;
   if constexpr (DK >= 2) sm_dy_coef(ds, Nc, o0 + cq, k);
   RawX xc;  // hoisted BN scale / shift of the thread's 4 x channels
@@ -607,14 +635,14 @@ __global__ __launch_bounds__(SM_T) void k_sm_bwd(SmX xs, SmDy ds, const float* _
         const int p = s / spp, n = (s - p * spp) * SM_BK + kr;
         int ip, op;
         sm_pair(tap, p, ip, op);
-        sm_raw_x<XK>(xs, ((long long)n * 4 + ip) * C + c0 + cq, nullptr, C, r);
+        sm_raw_x<XK>(xs, ((long long)n * 4 + ip) * C + c0 + cq, 32LL * 4 * C, nullptr, C, r);
         if constexpr (XK == 1) {
           r.sc = xc.sc;
           r.sh = xc.sh;
         }
       },
-      [&](const RawDyOp& r) { return sm_make_dy<DK>(ds, r.op, r.r, k); },
-      [&](const RawX& r) { return sm_make_x<XK>(r); }, acc);
+      [&](const RawDyOp& r, int i) { return sm_make_dy<DK>(ds, r.op, r.r, k, i); },
+      [&](const RawX& r, int i) { return sm_make_x<XK>(r, i); }, acc);
 #pragma unroll
   for (int j = 0; j < SM_NJ; ++j)
 #pragma unroll
