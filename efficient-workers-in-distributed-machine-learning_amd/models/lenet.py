@@ -30,6 +30,13 @@ class LeNet(nn.Module):
             x = F.relu(x)
         return self.fc2(x)
 
+    def fused_loss(self, x, y):
+        """(mean cross-entropy, logits) through the fused HIP step (``ops/lenet.py``: four
+        launches), or None where it does not apply (the caller then runs ``forward``)."""
+        from ..ops.lenet import lenet_loss
+
+        return lenet_loss(self, x, y)
+
     def name(self):
         return "lenet"
 

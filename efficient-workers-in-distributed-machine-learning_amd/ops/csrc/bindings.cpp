@@ -357,6 +357,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("sm_set_fence", &ew_sm_set_fence);
   m.def("topk_fused_select_max_blocks", &ew_topk_fused_select_max_blocks);
   m.def("sm_f32_bwd", &ew_sm_f32_bwd);
+  m.def("lenet_ws_floats", &ew_lenet_ws_floats);
+  m.def("lenet_counters", &ew_lenet_counters);
+  m.def("lenet_set_prof", &ew_lenet_set_prof);
+  m.def("lenet_fwd", &ew_lenet_fwd);
+  m.def("lenet_bwd", &ew_lenet_bwd);
   m.def("maxpool2_nhwc", &ew_maxpool2_nhwc);
   m.def("maxpool3s2_nhwc", &ew_maxpool3s2_nhwc);
   m.def("gap_nhwc", &ew_gap_nhwc);

@@ -309,6 +309,24 @@ int ew_sm_f32_bwd(uintptr_t x, uintptr_t bn_h, uintptr_t bn_stats, uintptr_t dy,
                   uintptr_t pb_stats, int pb_relu, uintptr_t bnpart, long long bnpart_floats,
                   uintptr_t stream);
 
+// ---- LeNet's fp32 training step in four launches (lenet_f32.hip): persistent workspace floats
+// and ticket ints (zeroed once; the kernels leave them zero) for batch B
+long long ew_lenet_ws_floats(int B);
+int ew_lenet_counters(int B);
+void ew_lenet_set_prof(uintptr_t buf);  // probes: phase stamps of the conv backward (0: off)
+void ew_lenet_fwd(uintptr_t x, uintptr_t w1, uintptr_t b1, uintptr_t w2, uintptr_t b2,
+                  uintptr_t wf1, uintptr_t bf1, uintptr_t wf2, uintptr_t bf2, uintptr_t y, int B,
+                  int K, uintptr_t a1, uintptr_t code1, uintptr_t a2, uintptr_t code2,
+                  uintptr_t h1, uintptr_t logits, uintptr_t dlogits, uintptr_t dh1,
+                  uintptr_t lossrow, uintptr_t loss, uintptr_t ws, long long ws_floats,
+                  uintptr_t cnt, int cnt_ints, uintptr_t stream);
+void ew_lenet_bwd(uintptr_t x, uintptr_t w2, uintptr_t wf1, uintptr_t a1, uintptr_t code1,
+                  uintptr_t a2, uintptr_t code2, uintptr_t h1, uintptr_t dlogits, uintptr_t dh1,
+                  uintptr_t gscale, int B, int K, uintptr_t dp2, uintptr_t dw1, uintptr_t db1,
+                  uintptr_t dw2, uintptr_t db2, uintptr_t dwf1, uintptr_t dbf1, uintptr_t dwf2,
+                  uintptr_t dbf2, uintptr_t ws, long long ws_floats, uintptr_t cnt, int cnt_ints,
+                  uintptr_t stream);
+
 // ---- RCCL communicator issuing collectives on the caller's stream (rccl_comm.hip) ----
 // dtype codes: 0 f32, 1 bf16, 2 f16, 3 u8, 4 i32, 5 f64, 6 i64; op: 0 sum, 1 max, 2 min, 3 avg
 std::string ew_rccl_unique_id();

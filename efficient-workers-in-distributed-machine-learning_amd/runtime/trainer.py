@@ -295,16 +295,28 @@ class Trainer:
     def forward_backward(self, x, y):
         self.flat.zero_grad()
         self.exchange.begin()
-        with self._range("forward"), self.autocast():
-            out = self.model(x)
-        if self.clock is not None:
-            self.clock.mark("forward")
-        if self.cuda and self.cfg.fused_nn == "on":
-            from ..ops.nn import cross_entropy  # one HIP kernel per direction
-
-            loss = cross_entropy(out, y)
+        fused = None
+        # a model with a fused training step of its own (LeNet: ops/lenet.py) returns the loss
+        # and logits from it, or None where it does not apply
+        fl = getattr(self.model, "fused_loss", None)
+        if fl is not None and self.cuda and self.cfg.fused_nn == "on" and self.amp_dtype is None:
+            with self._range("forward"):
+                fused = fl(x, y)
+        if fused is not None:
+            loss, out = fused
+            if self.clock is not None:
+                self.clock.mark("forward")
         else:
-            loss = F.cross_entropy(out.float(), y)
+            with self._range("forward"), self.autocast():
+                out = self.model(x)
+            if self.clock is not None:
+                self.clock.mark("forward")
+            if self.cuda and self.cfg.fused_nn == "on":
+                from ..ops.nn import cross_entropy  # one HIP kernel per direction
+
+                loss = cross_entropy(out, y)
+            else:
+                loss = F.cross_entropy(out.float(), y)
         with self._range("backward+encode"):
             # a persistent d(loss)/d(loss) = 1: backward() would fill a fresh one every step
             seed = getattr(self, "_loss_seed", None)
