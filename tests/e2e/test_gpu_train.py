@@ -243,11 +243,14 @@ def _bench_pg(codec, comm, extra=(), env_extra=None):
 
     root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     env = dict(os.environ, EWDML_FORCE_PG="1", EWDML_COMM=comm, **(env_extra or {}))
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py",
-           "--gpus", "1", "--steps", "4", "--warmup", "4", "--batch-size", "64",
-           "--compress", codec, "--no-extras", *extra]
-    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=300)
+    for _ in range(2):  # a rendezvous port taken between _free_port and the launcher: a new port
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node",
+               "1", "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py",
+               "--gpus", "1", "--steps", "4", "--warmup", "4", "--batch-size", "64",
+               "--compress", codec, "--no-extras", *extra]
+        r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=300)
+        if not (r.returncode != 0 and "EADDRINUSE" in r.stderr and "failed to listen" in r.stderr):
+            break
     if r.returncode != 0:
         errs = [ln for ln in r.stderr.splitlines()
                 if ("rror" in ln or "what()" in ln or "Watchdog" in ln) and "frame #" not in ln]
@@ -292,17 +295,22 @@ def test_comm_probe_passes_and_failure_falls_back_to_process_group():
 
 def test_auto_plan_at_n8_runs_segmented_through_rccl():
     """--hip-graph auto as planned for 8 ranks (EWDML_PLAN_AS_WORLD=8) on the real RCCL
-    communicator (world of one): the dense fp32 exchange becomes the segmented step -- comm
-    graphs with the all-reduce on their own stream beside backward -- and the replicas check and
-    the JSON fields hold; the top-k headline stays one graph."""
-    dense = _bench_pg("none", "rccl", extra=("--error-feedback", "off"),
+    communicator (world of one) takes the mode the step model predicts faster
+    (parallel/step_model.py), for the dense and the top-k exchange; and the segmented step --
+    comm graphs with the all-reduce on their own stream beside backward -- runs through RCCL with
+    the replicas check and the JSON fields holding."""
+    for codec, extra in (("none", ("--error-feedback", "off")), ("topk_qsgd", ())):
+        rec = _bench_pg(codec, "rccl", extra=extra, env_extra={"EWDML_PLAN_AS_WORLD": "8"})
+        plan = rec["graph_plan"]
+        pred = plan["predicted_ms"]
+        want = "segmented" if pred["segmented"] < pred["full"] else "full"
+        assert plan["mode"] == want and rec["config"]["hip_graph"] == want, (codec, plan)
+        assert rec["predicted_ms_per_step"] == pred[want]
+    dense = _bench_pg("none", "rccl", extra=("--error-feedback", "off", "--hip-graph", "segmented"),
                       env_extra={"EWDML_PLAN_AS_WORLD": "8"})
-    assert dense["graph_plan"]["mode"] == "segmented" and dense["graph_plan"]["splits"] == 2
     assert dense["config"]["hip_graph"] == "segmented" and dense["overlap_comm_graphs"] >= 1
-    assert dense["config"]["buckets"] >= 3 and dense["replicas_identical"] is True
+    assert dense["replicas_identical"] is True
     assert dense["final_loss"] == dense["final_loss"]
-    topk = _bench_pg("topk_qsgd", "rccl", env_extra={"EWDML_PLAN_AS_WORLD": "8"})
-    assert topk["graph_plan"]["mode"] == "full" and topk["config"]["hip_graph"] == "full"
 
 
 @pytest.mark.parametrize("codec", ["topk_qsgd", "none"])
