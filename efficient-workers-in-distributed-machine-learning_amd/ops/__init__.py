@@ -249,7 +249,8 @@ def topk_encode(dp: DevicePlan, grad, payload, layout, levels: int, norm: str, k
                   1 if norm == "l2" else 0, float(levels), float(1.0 / levels), key & 0xFFFFFFFF,
                   dp.plan.bucket_offset & 0xFFFFFFFF, _keyp(key_tensor), _stream(), _ptr(vel),
                   _ptr(par), mom, damp1, wd, nest, layout.bitmap, dmask, _lrp(lrt), dp.plan.length,
-                  _ptr(dp.cblocks), dp.plan.num_cblocks, int(_TOPK_PREDICT), int(_LB_FAULT[0]))
+                  _ptr(dp.cblocks), dp.plan.num_cblocks, int(_TOPK_PREDICT), int(_LB_FAULT[0]),
+                  int(max(dp.plan.ks)) if dp.plan.ks else 0)
 
 
 def _lrp(lr_tensor):

@@ -33,9 +33,10 @@ PYBIND11_MODULE(_C, m) {
            uintptr_t param, float dgc_momentum, float dgc_damp1, float dgc_wd,
            int dgc_nesterov, int bitmap_off, int dgc_mask, uintptr_t dgc_lr_ptr,
            long long bucket_len, uintptr_t cblocks, int num_cblocks, int predict,
-           int lb_fault) {
+           int lb_fault, int max_k) {
           TopkEncodeArgs a{};
           a.lb_fault = lb_fault;
+          a.max_k = max_k;
           a.bucket_len = bucket_len;
           a.cblocks = cblocks;
           a.num_cblocks = num_cblocks;

@@ -33,6 +33,7 @@ struct TopkEncodeArgs {
   int num_cblocks;
   int predict;
   int lb_fault;  // test hook: tensors' first chunks skip their look-back word (lb_err path)
+  int max_k;     // largest per-tensor k of the bucket (0: unknown)
 };
 
 struct TopkDecodeArgs {

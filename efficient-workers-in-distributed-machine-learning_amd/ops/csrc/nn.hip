@@ -308,6 +308,21 @@ __global__ __launch_bounds__(EW_BLOCK) void k_bn_fwd_finalize(
     float* __restrict__ rmean, float* __restrict__ rvar, const long long* __restrict__ nbt,
     float momentum, float eps, float* __restrict__ stats) {
   const int c = blockIdx.x * EW_FIN_CH + (threadIdx.x % EW_FIN_CH);
+  // the per-channel operands of the tail, loaded before the partial rows (their round trips
+  // overlap the sums' instead of following them: a finalize is a short chain of L2 round trips)
+  const int cc = c < C ? c : C - 1;
+  const float g = gamma ? gamma[cc] : 1.0f;
+  const float bb = beta ? beta[cc] : 0.0f;
+  float rm0 = 0.0f, rv0 = 0.0f, cb = 0.0f;
+  long long nb0 = 0;
+  if (rmean) {
+    rm0 = rmean[cc];
+    rv0 = rvar[cc];
+    if (momentum < 0.0f) nb0 = *nbt;
+    if (cbias)
+      cb = cb_bf16 ? ew_bf16f(reinterpret_cast<const uint16_t*>(cbias)[cc])
+                   : reinterpret_cast<const float*>(cbias)[cc];
+  }
   double sums[2];
   if (!ew_sum_parts<2>(part, nblk, C, c, sums)) return;
   const double mean = sums[0] / (double)M;
@@ -315,8 +330,6 @@ __global__ __launch_bounds__(EW_BLOCK) void k_bn_fwd_finalize(
   if (var < 0.0) var = 0.0;
   const float invstd = (float)(1.0 / sqrt(var + (double)eps));
   const float mf = (float)mean;
-  const float g = gamma ? gamma[c] : 1.0f;
-  const float bb = beta ? beta[c] : 0.0f;
   const float scale = g * invstd;
   stats[c] = mf;
   stats[C + c] = invstd;
@@ -325,15 +338,11 @@ __global__ __launch_bounds__(EW_BLOCK) void k_bn_fwd_finalize(
   if (rmean) {
     // momentum < 0: cumulative moving average (nn.BatchNorm2d(momentum=None)) over the batches
     // seen including this one; num_batches_tracked itself is incremented by the apply kernel
-    const float f = momentum >= 0.0f ? momentum : 1.0f / (float)(*nbt + 1);
+    const float f = momentum >= 0.0f ? momentum : 1.0f / (float)(nb0 + 1);
     const double unb = M > 1 ? var * (double)M / (double)(M - 1) : var;
-    float cb = 0.0f;
-    if (cbias)
-      cb = cb_bf16 ? ew_bf16f(reinterpret_cast<const uint16_t*>(cbias)[c])
-                   : reinterpret_cast<const float*>(cbias)[c];
     const float bm = mf + cb;
-    rmean[c] = (1.0f - f) * rmean[c] + f * bm;
-    rvar[c] = (1.0f - f) * rvar[c] + f * (float)unb;
+    rmean[c] = (1.0f - f) * rm0 + f * bm;
+    rvar[c] = (1.0f - f) * rv0 + f * (float)unb;
   }
 }
 
@@ -531,10 +540,11 @@ __global__ __launch_bounds__(EW_BLOCK) void k_bn_bwd_finalize(
     float* __restrict__ coef, float* __restrict__ dgamma, float* __restrict__ dbeta,
     void* __restrict__ dcbias, int cb_bf16) {
   const int c = blockIdx.x * EW_FIN_CH + (threadIdx.x % EW_FIN_CH);
+  const int cc = c < C ? c : C - 1;
+  const double invstd = stats[C + cc], scale = stats[2 * C + cc];  // ahead of the sums' loads
   double sums[3];
   if (!ew_sum_parts<NS>(part, nblk, C, c, sums)) return;
   if (NS == 2) sums[2] = 0.0;
-  const double invstd = stats[C + c], scale = stats[2 * C + c];
   const double db = sums[0];             // sum dz
   const double dg = sums[1] * invstd;    // sum dz * xhat
   const double e = -scale * invstd * dg / (double)M;

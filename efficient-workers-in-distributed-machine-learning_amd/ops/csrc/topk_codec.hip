@@ -845,114 +845,6 @@ __device__ __forceinline__ void pk_scan2(unsigned long long& a, unsigned long lo
   b = bb + ib - b;
 }
 
-template <int EFM>
-__global__ __launch_bounds__(EW_BLOCK) void k_pk_hist0(
-    GradPtrs gp, DgcArgs dg, unsigned long long* __restrict__ lb, float* __restrict__ resid,
-    const ChunkRow* __restrict__ chunks, uint32_t* __restrict__ kmaxr, int T,
-    const TensorRow* __restrict__ tensors, uint32_t* __restrict__ pst, int* __restrict__ tick,
-    int* __restrict__ ccount, uint32_t* __restrict__ cbase, uint32_t* __restrict__ ccnt,
-    uint2* __restrict__ pcand, int* __restrict__ stats) {
-  __shared__ unsigned long long ws2[2 * EW_WAVES];
-  __shared__ uint32_t wmax[EW_WAVES];
-  __shared__ uint32_t s_base;
-  const ChunkRow c = chunks[blockIdx.x];
-  const TensorRow tr = tensors[c.tensor];
-  if (threadIdx.x == 0) lb[blockIdx.x] = 0ull;  // the write pass's look-back word
-  // the candidate passes' per-tensor arrival counts start from zero every encode: a fused select
-  // whose barrier gave up (pk_wait's poll bound) can leave one behind, which would desynchronise
-  // every later encode's barriers (the generation words are read relative to their value)
-  if (blockIdx.x == 0)
-    for (int t = threadIdx.x; t < T; t += EW_BLOCK) tick[TICK_STRIDE * (T + t)] = 0;
-  float4 v[EW_CU];
-  ew_ld_chunk(gp, nullptr, c, v);
-  topk_ef_stage<EFM>(gp, dg, resid, c, v);
-  const uint32_t P = pst[c.tensor * 8];
-  uint32_t kmax = 0;
-  unsigned long long pa = 0, pb = 0;  // candidates per slab, 16-bit fields (slabs 0-3, 4-7)
-#pragma unroll
-  for (int u = 0; u < EW_CU; ++u) {
-    uint32_t n = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if (ew_chunk_idx(u) + j < c.len) {
-        const uint32_t k = ew_key(ew_f4(v[u], j));
-        kmax = max(kmax, k);
-        n += k >= P;
-      }
-    }
-    if (u < 4) pa |= (unsigned long long)n << (16 * u);
-    else pb |= (unsigned long long)n << (16 * (u - 4));
-  }
-  kmax = ew_wave_max_u(kmax);
-  if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = kmax;
-  unsigned long long ta, tb;
-  pk_scan2(pa, pb, ws2, ta, tb);  // contains __syncthreads: wmax visible
-  // slab starts within the chunk's candidate segment (index order: slab, then thread, then j)
-  uint32_t start[EW_CU];
-  uint32_t run = 0;
-#pragma unroll
-  for (int u = 0; u < EW_CU; ++u) {
-    start[u] = run;
-    run += (uint32_t)(((u < 4 ? ta : tb) >> (16 * (u & 3))) & 0xffffull);
-  }
-  const uint32_t tot = run;
-  if (threadIdx.x == 0) {
-    uint32_t m = wmax[0];
-    for (int w = 1; w < EW_WAVES; ++w) m = max(m, wmax[w]);
-    atomicMax(&kmaxr[(blockIdx.x & (NREP - 1)) * T + c.tensor], m);
-    const uint32_t base = tot ? (uint32_t)atomicAdd(ccount + TICK_STRIDE * c.tensor, (int)tot) : 0u;
-    s_base = base;
-    cbase[blockIdx.x] = base;
-    ccnt[blockIdx.x] = tot;
-  }
-  __syncthreads();
-  if (tot) {
-    uint2* dst = pcand + tr.cap0;
-    const uint32_t cap = (uint32_t)tr.cap, base = s_base;
-#pragma unroll
-    for (int u = 0; u < EW_CU; ++u) {
-      uint32_t pos = base + start[u] +
-                     (uint32_t)(((u < 4 ? pa : pb) >> (16 * (u & 3))) & 0xffffull);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int i = ew_chunk_idx(u) + j;
-        const float x = ew_f4(v[u], j);
-        if (i < c.len && ew_key(x) >= P) {
-          if (pos < cap) dst[pos] = make_uint2(__float_as_uint(x), (uint32_t)(c.local * EW_CHUNK + i));
-          ++pos;
-        }
-      }
-    }
-  }
-  if (topk_tensor_last(tick + TICK_STRIDE * c.tensor, tr.nchunks, reinterpret_cast<int*>(wmax)) &&
-      threadIdx.x == 0) {
-    int* cc = ccount + TICK_STRIDE * c.tensor;
-    const uint32_t M = (uint32_t)__hip_atomic_load(cc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(cc, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t fast = M >= (uint32_t)tr.k && M <= (uint32_t)tr.cap;
-    pst[c.tensor * 8 + 2] = M;
-    pst[c.tensor * 8 + 3] = fast;
-    // digit geometry of the radix passes (pk_select): relative to P over the candidates, the
-    // key's own bits on the full passes
-    uint32_t B = 0u, s0 = 20u, s1 = 10u;
-    if (fast) {
-      uint32_t kmax = 0;
-      for (int r = 0; r < NREP; ++r)
-        kmax = max(kmax, __hip_atomic_load(kmaxr + r * T + c.tensor, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT));
-      B = P;
-      const uint32_t span = kmax - P;  // >= 0: M >= k >= 1 candidates are >= P
-      const int bl = span ? 32 - __clz(span) : 0;
-      s0 = bl > 11 ? (uint32_t)(bl - 11) : 0u;
-      s1 = s0 > 10 ? s0 - 10 : 0u;
-    }
-    pst[c.tensor * 8 + 5] = B;
-    pst[c.tensor * 8 + 6] = s0;
-    pst[c.tensor * 8 + 7] = s1;
-    atomicAdd(stats + (fast ? 0 : 1), 1);
-  }
-}
-
 // Calls f(key) (f(key, value) not needed) for this candidate-pass block's share of tensor t: its
 // candidates [8192 j, 8192 (j + 1)) on the fast path, else every ncb-th chunk from j of the tensor
 // (the full pass, read from the staged e or the gradients).
@@ -1093,6 +985,195 @@ __device__ __forceinline__ void pk_predict(const TensorRow& tr, int t, uint32_t 
   pst[t * 8 + 4] = 1u;
 }
 
+// Tensor t's three radix passes over its M <= PK_INLINE_MAX candidates in one block (LDS
+// histograms), run by k_pk_hist0's tensor-last block: the same digits and selects as the
+// candidate-pass kernels, so the same threshold and tie count, without their per-tensor barriers
+// (each a chain of L2 round trips).  The candidates were written by other blocks of this launch
+// with sc1 stores; read here with sc1 loads (cdna_hip_programming.md Guideline 16).
+constexpr uint32_t PK_INLINE_MAX = 16384;  // EWDML_TOPK_INLINE: another bound, 0 = off
+
+__device__ __forceinline__ void pk_inline_select(const uint2* __restrict__ cands, uint32_t M,
+                                                 uint32_t B, uint32_t s0, uint32_t s1,
+                                                 const TensorRow* __restrict__ tensors,
+                                                 uint32_t* __restrict__ state,
+                                                 const uint32_t* __restrict__ kmaxr, int T, int t) {
+  __shared__ uint32_t h[NB0];
+  constexpr int R = 16;
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(cands);
+  // pass p: histogram of the digit of the keys whose higher digits match `want`
+  auto pass = [&](int p, uint32_t want) {
+    const int nb = p == 0 ? NB0 : NB1;
+    for (int i = threadIdx.x; i < nb; i += EW_BLOCK) h[i] = 0;
+    __syncthreads();
+    for (uint32_t b0 = 0; b0 < M; b0 += EW_BLOCK * R) {
+      uint32_t kv[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const uint32_t i = min(b0 + r * EW_BLOCK + threadIdx.x, M - 1);
+        kv[r] = __hip_atomic_load(src + 2 * i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if (b0 + r * EW_BLOCK + threadIdx.x >= M) continue;
+        const uint32_t rel = (kv[r] & 0x7fffffffu) - B;
+        if (p == 0) atomicAdd(&h[rel >> s0], 1u);
+        else if (p == 1) {
+          if ((rel >> s0) == want) atomicAdd(&h[(rel >> s1) & ((1u << (s0 - s1)) - 1u)], 1u);
+        } else if ((rel >> s1) == want) {
+          atomicAdd(&h[rel & ((1u << s1) - 1u)], 1u);
+        }
+      }
+    }
+    __syncthreads();
+  };
+  // the select's state stores (one thread) drained before the block reads them back
+  auto sync_state = [&]() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    return __hip_atomic_load(state + t * 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  pass(0, 0u);
+  pk_select<NB0, true>(h, tensors, state, kmaxr, T, t, s0, 0);
+  uint32_t pre = sync_state();
+  pass(1, pre >> s0);
+  pk_select<NB1, false>(h, tensors, state, kmaxr, T, t, s1, 0);
+  pre = sync_state();
+  pass(2, pre >> s1);
+  pk_select<NB2, false>(h, tensors, state, kmaxr, T, t, 0u, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+}
+
+template <int EFM>
+__global__ __launch_bounds__(EW_BLOCK) void k_pk_hist0(
+    GradPtrs gp, DgcArgs dg, unsigned long long* __restrict__ lb, float* __restrict__ resid,
+    const ChunkRow* __restrict__ chunks, uint32_t* __restrict__ kmaxr, int T,
+    const TensorRow* __restrict__ tensors, uint32_t* __restrict__ pst, int* __restrict__ tick,
+    int* __restrict__ ccount, uint32_t* __restrict__ cbase, uint32_t* __restrict__ ccnt,
+    uint2* __restrict__ pcand, int* __restrict__ stats, uint32_t* __restrict__ state,
+    int* __restrict__ cand_n, uint32_t inline_max) {
+  __shared__ unsigned long long ws2[2 * EW_WAVES];
+  __shared__ uint32_t wmax[EW_WAVES];
+  __shared__ uint32_t s_base;
+  __shared__ uint32_t s_sel[4];  // tensor-last block: inline flag, B, s0, s1
+  const ChunkRow c = chunks[blockIdx.x];
+  const TensorRow tr = tensors[c.tensor];
+  if (threadIdx.x == 0) lb[blockIdx.x] = 0ull;  // the write pass's look-back word
+  // the candidate passes' per-tensor arrival counts start from zero every encode: a fused select
+  // whose barrier gave up (pk_wait's poll bound) can leave one behind, which would desynchronise
+  // every later encode's barriers (the generation words are read relative to their value)
+  if (blockIdx.x == 0)
+    for (int t = threadIdx.x; t < T; t += EW_BLOCK) tick[TICK_STRIDE * (T + t)] = 0;
+  float4 v[EW_CU];
+  ew_ld_chunk(gp, nullptr, c, v);
+  topk_ef_stage<EFM>(gp, dg, resid, c, v);
+  const uint32_t P = pst[c.tensor * 8];
+  uint32_t kmax = 0;
+  unsigned long long pa = 0, pb = 0;  // candidates per slab, 16-bit fields (slabs 0-3, 4-7)
+#pragma unroll
+  for (int u = 0; u < EW_CU; ++u) {
+    uint32_t n = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (ew_chunk_idx(u) + j < c.len) {
+        const uint32_t k = ew_key(ew_f4(v[u], j));
+        kmax = max(kmax, k);
+        n += k >= P;
+      }
+    }
+    if (u < 4) pa |= (unsigned long long)n << (16 * u);
+    else pb |= (unsigned long long)n << (16 * (u - 4));
+  }
+  kmax = ew_wave_max_u(kmax);
+  if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = kmax;
+  unsigned long long ta, tb;
+  pk_scan2(pa, pb, ws2, ta, tb);  // contains __syncthreads: wmax visible
+  // slab starts within the chunk's candidate segment (index order: slab, then thread, then j)
+  uint32_t start[EW_CU];
+  uint32_t run = 0;
+#pragma unroll
+  for (int u = 0; u < EW_CU; ++u) {
+    start[u] = run;
+    run += (uint32_t)(((u < 4 ? ta : tb) >> (16 * (u & 3))) & 0xffffull);
+  }
+  const uint32_t tot = run;
+  if (threadIdx.x == 0) {
+    uint32_t m = wmax[0];
+    for (int w = 1; w < EW_WAVES; ++w) m = max(m, wmax[w]);
+    atomicMax(&kmaxr[(blockIdx.x & (NREP - 1)) * T + c.tensor], m);
+    const uint32_t base = tot ? (uint32_t)atomicAdd(ccount + TICK_STRIDE * c.tensor, (int)tot) : 0u;
+    s_base = base;
+    cbase[blockIdx.x] = base;
+    ccnt[blockIdx.x] = tot;
+  }
+  __syncthreads();
+  if (tot) {
+    uint2* dst = pcand + tr.cap0;
+    const uint32_t cap = (uint32_t)tr.cap, base = s_base;
+#pragma unroll
+    for (int u = 0; u < EW_CU; ++u) {
+      uint32_t pos = base + start[u] +
+                     (uint32_t)(((u < 4 ? pa : pb) >> (16 * (u & 3))) & 0xffffull);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int i = ew_chunk_idx(u) + j;
+        const float x = ew_f4(v[u], j);
+        if (i < c.len && ew_key(x) >= P) {
+          // write-through (sc1): the tensor's last block may select over the list in this launch
+          if (pos < cap)
+            __hip_atomic_store(reinterpret_cast<unsigned long long*>(dst + pos),
+                               (unsigned long long)__float_as_uint(x) |
+                                   ((unsigned long long)(c.local * EW_CHUNK + i) << 32),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ++pos;
+        }
+      }
+    }
+  }
+  if (!topk_tensor_last(tick + TICK_STRIDE * c.tensor, tr.nchunks, reinterpret_cast<int*>(wmax)))
+    return;
+  if (threadIdx.x == 0) {
+    int* cc = ccount + TICK_STRIDE * c.tensor;
+    const uint32_t M = (uint32_t)__hip_atomic_load(cc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(cc, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t fast = M >= (uint32_t)tr.k && M <= (uint32_t)tr.cap;
+    pst[c.tensor * 8 + 2] = M;
+    pst[c.tensor * 8 + 3] = fast;
+    // digit geometry of the radix passes (pk_select): relative to P over the candidates, the
+    // key's own bits on the full passes
+    uint32_t B = 0u, s0 = 20u, s1 = 10u;
+    if (fast) {
+      uint32_t kmax = 0;
+      for (int r = 0; r < NREP; ++r)
+        kmax = max(kmax, __hip_atomic_load(kmaxr + r * T + c.tensor, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT));
+      B = P;
+      const uint32_t span = kmax - P;  // >= 0: M >= k >= 1 candidates are >= P
+      const int bl = span ? 32 - __clz(span) : 0;
+      s0 = bl > 11 ? (uint32_t)(bl - 11) : 0u;
+      s1 = s0 > 10 ? s0 - 10 : 0u;
+    }
+    pst[c.tensor * 8 + 5] = B;
+    pst[c.tensor * 8 + 6] = s0;
+    pst[c.tensor * 8 + 7] = s1;
+    atomicAdd(stats + (fast ? 0 : 1), 1);
+    s_sel[0] = fast && M <= inline_max;
+    s_sel[1] = B;
+    s_sel[2] = s0;
+    s_sel[3] = s1;
+  }
+  __syncthreads();
+  if (!s_sel[0]) return;
+  // few candidates: this block runs the three radix passes over them itself (the select launch's
+  // blocks of this tensor then exit at once: pst fast flag 2)
+  pk_inline_select(pcand + tr.cap0, pst[c.tensor * 8 + 2], s_sel[1], s_sel[2], s_sel[3], tensors,
+                   state, kmaxr, T, c.tensor);
+  if (threadIdx.x == 0) {
+    pk_predict(tr, c.tensor, s_sel[1], state, pst, cand_n);
+    pst[c.tensor * 8 + 3] = 2u;
+  }
+}
+
 // Radix pass 0 over the candidates (fast) or the tensor (full).
 __global__ __launch_bounds__(EW_BLOCK) void k_pk_pass0(
     GradPtrs gp, const float* __restrict__ flat, const ChunkRow* __restrict__ chunks,
@@ -1106,6 +1187,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_pk_pass0(
   uint32_t* h = hs + (threadIdx.x & (HSUB - 1));
   const CBlockRow cb = cblocks[blockIdx.x];
   const int t = cb.tensor;
+  if (pst[t * 8 + 3] == 2u) return;  // selected inline by k_pk_hist0
   const TensorRow tr = tensors[t];
   const uint32_t B = pst[t * 8 + 5], s0 = pst[t * 8 + 6];
   pk_visit(gp, flat, chunks, tr, cb.j, pst[t * 8 + 3] != 0, pst[t * 8 + 2], pcand,
@@ -1138,6 +1220,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_pk_pass1(
   __syncthreads();
   const CBlockRow cb = cblocks[blockIdx.x];
   const int t = cb.tensor;
+  if (pst[t * 8 + 3] == 2u) return;  // selected inline by k_pk_hist0
   const TensorRow tr = tensors[t];
   const uint32_t B = pst[t * 8 + 5], s0 = pst[t * 8 + 6], s1 = pst[t * 8 + 7];
   const uint32_t want = state[t * 4] >> s0;
@@ -1205,6 +1288,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_pk_pass2(
   __syncthreads();
   const CBlockRow cb = cblocks[blockIdx.x];
   const int t = cb.tensor;
+  if (pst[t * 8 + 3] == 2u) return;  // selected inline by k_pk_hist0
   const TensorRow tr = tensors[t];
   const uint32_t n = (uint32_t)__hip_atomic_load(cand_n + TICK_STRIDE * t, __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_AGENT);
@@ -1317,6 +1401,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_pk_select(
   __shared__ int s_flag;
   const CBlockRow cb = cblocks[blockIdx.x];
   const int t = cb.tensor;
+  if (pst[t * 8 + 3] == 2u) return;  // selected inline by k_pk_hist0: no barrier to join
   const TensorRow tr = tensors[t];
   int* arr = arrive + TICK_STRIDE * t;
   uint32_t* gn = gen + TICK_STRIDE * t;
@@ -1911,6 +1996,17 @@ static int ew_pk_fused_max_blocks() {
 
 int ew_topk_fused_select_max_blocks() { return ew_pk_fused_max_blocks(); }
 
+// Most candidates a tensor may have for k_pk_hist0's tensor-last block to select over them itself
+static uint32_t ew_pk_inline_max() {
+  static long long n = -1;
+  if (n < 0) {
+    const char* e = std::getenv("EWDML_TOPK_INLINE");
+    n = e ? std::atoll(e) : (long long)PK_INLINE_MAX;
+    if (n < 0) n = 0;
+  }
+  return (uint32_t)n;
+}
+
 void ew_topk_encode(const TopkEncodeArgs& a) {
   auto* chunks = reinterpret_cast<const ChunkRow*>(a.chunks);
   auto* tensors = reinterpret_cast<const TensorRow*>(a.tensors);
@@ -1973,11 +2069,16 @@ void ew_topk_encode(const TopkEncodeArgs& a) {
     // Its passes use histogram copy 0 only: kmaxr + hist0's copy 0 are one range, hist1's and
     // hist2's copies 0 two more (0.6 MB for VGG-11 instead of 5 MB of zeroing per encode)
     const uint32_t pk_rz0 = (uint32_t)(NREP * T + T * NB0);
+    // in-hist0 selects only when every tensor's candidates can fit one block (the encode steers
+    // them to ~2-3 k): then the select launch's blocks all exit at once.  With any larger tensor
+    // the select launch keeps its barriers anyway, and inline selects would only lengthen hist0.
+    const uint32_t inline_max =
+        (a.max_k > 0 && 4LL * a.max_k <= (long long)ew_pk_inline_max()) ? ew_pk_inline_max() : 0u;
     auto* cbl = reinterpret_cast<const CBlockRow*>(a.cblocks);
     const int G = a.num_cblocks;
 #define EW_PKH(EFM)                                                                              \
   EW_LAUNCH(k_pk_hist0<EFM>, C, s, g, dg, lb, resid, chunks, kmaxr, T, tensors, pst, tick, ccount, \
-            cbase, ccnt, pcand, pk_stats)
+            cbase, ccnt, pcand, pk_stats, state, cand_n, inline_max)
     if (dg.vel) EW_PKH(EF_DGC);
     else if (resid) EW_PKH(EF_PLAIN);
     else EW_PKH(EF_NONE);
