@@ -101,6 +101,12 @@ _S2 = os.environ.get("EWDML_CONV_S2", "0") == "1"
 # (ops/csrc/smallmap_f32.hip): one forward launch and one backward launch (data + weight gradient)
 # instead of Winograd's input / GEMM / output transform per pass.  EWDML_SMALLMAP=0: Winograd
 _SMALLMAP = os.environ.get("EWDML_SMALLMAP", "1") != "0"
+# the BN backward that follows a 2x2-map conv left to that conv's backward launch (KIND 2 dy formed
+# on load, EWDML_SM_LAZY_BWD=1) or written by the BN backward apply and read plain (default): the
+# lazy dy cost the two backward launches +14 / +18 us (every one of the conv's GEMM tiles re-forms
+# it), more than the two apply launches it saves; 3 interleaved rounds 1.197 / 1.193 / 1.201 vs
+# 1.217 / 1.212 / 1.214 ms per step (profiles/ab/README.md)
+_SM_LAZY_BWD = os.environ.get("EWDML_SM_LAZY_BWD", "0") == "1"
 _SM_WS = {}
 
 
@@ -903,7 +909,7 @@ def _apply(x, w, sink=None):
     if part is not None:
         y._ew_bn_part = part
     if node is not None and (getattr(node, "wino", None) is not None
-                             or getattr(node, "sm", None) is not None):
+                             or (_SM_LAZY_BWD and getattr(node, "sm", None) is not None)):
         y._ew_wino_out = True  # the BN layer it feeds may leave its backward apply to us
     return y
 

@@ -908,11 +908,12 @@ def test_conv_f32_smallmap_lazy_bn_matches_materialised(pool, front_pool):
             bn.bias.uniform_(-0.3, 0.3)
     gshape = (N, C, 1, 1) if pool else (N, C, 2, 2)
     g = torch.randn(gshape, device="cuda").contiguous(memory_format=torch.channels_last)
-    lazy_bwd = fnn._LAZY_BWD
+    lazy_bwd, sm_lazy = fnn._LAZY_BWD, conv._SM_LAZY_BWD
     runs = []
     try:
         for lazy in (True, False):
             fnn._LAZY_BWD = lazy
+            conv._SM_LAZY_BWD = lazy  # the lazy dy path of the small-map backward (opt-in)
             b0, b1 = copy.deepcopy(bns[0]), copy.deepcopy(bns[1])
             xa, wa, wb = (t.clone().requires_grad_(True) for t in (x0, w0, w1))
             h = conv.conv(xa, wa)
@@ -929,7 +930,7 @@ def test_conv_f32_smallmap_lazy_bn_matches_materialised(pool, front_pool):
                                                       b.running_mean, b.running_var,
                                                       b.num_batches_tracked)])
     finally:
-        fnn._LAZY_BWD = lazy_bwd
+        fnn._LAZY_BWD, conv._SM_LAZY_BWD = lazy_bwd, sm_lazy
     for i, (a, b) in enumerate(zip(*runs)):
         assert torch.equal(a, b), i
 
