@@ -10,6 +10,7 @@ it).
 """
 import math
 
+import torch
 import torch.nn as nn
 
 from . import fused
@@ -67,6 +68,26 @@ class VGG(nn.Module):
 
             return vgg_head(self.classifier, f)
         return self.classifier(f)
+
+    def fused_loss(self, x, y):
+        """(mean cross-entropy, logits) with the classifier tail and the loss in one HIP launch
+        each way (``ops/head.py`` ``vgg_loss``), or None where that path does not apply (the
+        caller then runs ``forward`` and its own loss)."""
+        if not (x.is_cuda and x.dtype == torch.float32 and fused.active(x)):
+            return None
+        from ..ops import head as head_ops
+
+        probe = torch.empty((x.shape[0], self.classifier[1].in_features), dtype=x.dtype,
+                            device=x.device)
+        if not head_ops.tail_supported(self.classifier, probe, y):
+            return None
+        f = self.features(x).flatten(1)
+        if not head_ops.tail_supported(self.classifier, f, y):  # not expected: same checks
+            from ..ops.nn import cross_entropy
+
+            out = head_ops.vgg_head(self.classifier, f) if fused.active(f) else self.classifier(f)
+            return cross_entropy(out, y), out.detach()
+        return head_ops.vgg_loss(self.classifier, f, y)
 
 
 def _make(cfg_key, bn, num_classes=10):

@@ -107,6 +107,8 @@ _SMALLMAP = os.environ.get("EWDML_SMALLMAP", "1") != "0"
 # it), more than the two apply launches it saves; 3 interleaved rounds 1.197 / 1.193 / 1.201 vs
 # 1.217 / 1.212 / 1.214 ms per step (profiles/ab/README.md)
 _SM_LAZY_BWD = os.environ.get("EWDML_SM_LAZY_BWD", "0") == "1"
+# the same for the Winograd convs (their backward input transforms form the KIND 2 dy)
+_WINO_LAZY_BWD = os.environ.get("EWDML_WINO_LAZY_BWD", "1") != "0"
 _SM_WS = {}
 
 
@@ -908,7 +910,7 @@ def _apply(x, w, sink=None):
     part = getattr(node, "bn_part", None) if node is not None else None
     if part is not None:
         y._ew_bn_part = part
-    if node is not None and (getattr(node, "wino", None) is not None
+    if node is not None and ((_WINO_LAZY_BWD and getattr(node, "wino", None) is not None)
                              or (_SM_LAZY_BWD and getattr(node, "sm", None) is not None)):
         y._ew_wino_out = True  # the BN layer it feeds may leave its backward apply to us
     return y

@@ -362,6 +362,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("lenet_counters", &ew_lenet_counters);
   m.def("lenet_set_prof", &ew_lenet_set_prof);
   m.def("lenet_fwd", &ew_lenet_fwd);
+  m.def("tail_ws_floats", &ew_tail_ws_floats);
+  m.def("tail_counters", &ew_tail_counters);
+  m.def("tail_fwd", &ew_tail_fwd);
+  m.def("tail_bwd", &ew_tail_bwd);
   m.def("lenet_bwd", &ew_lenet_bwd);
   m.def("maxpool2_nhwc", &ew_maxpool2_nhwc);
   m.def("maxpool3s2_nhwc", &ew_maxpool3s2_nhwc);

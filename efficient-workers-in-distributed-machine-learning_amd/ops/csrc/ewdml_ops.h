@@ -328,6 +328,17 @@ void ew_lenet_bwd(uintptr_t x, uintptr_t w2, uintptr_t wf1, uintptr_t a1, uintpt
                   uintptr_t dbf2, uintptr_t ws, long long ws_floats, uintptr_t cnt, int cnt_ints,
                   uintptr_t stream);
 
+// ---- VGG classifier tail (fc2 + ReLU + fc3 + cross-entropy) and its backward (head_tail.hip)
+long long ew_tail_ws_floats(int B, int N2);
+int ew_tail_counters(int B);
+void ew_tail_fwd(uintptr_t h1, uintptr_t w2, uintptr_t b2, uintptr_t w3, uintptr_t b3, uintptr_t y,
+                 int B, int K1, int N2, int K, uintptr_t h2, uintptr_t logits, uintptr_t dlogits,
+                 uintptr_t dh2, uintptr_t lossrow, uintptr_t loss, uintptr_t ws,
+                 long long ws_floats, uintptr_t cnt, int cnt_ints, uintptr_t stream);
+void ew_tail_bwd(uintptr_t h1, uintptr_t h2, uintptr_t dh2, uintptr_t dlogits, uintptr_t w2,
+                 uintptr_t gscale, int B, int K1, int N2, int K, uintptr_t dh1, uintptr_t dw2,
+                 uintptr_t db2, uintptr_t dw3, uintptr_t db3, uintptr_t stream);
+
 // ---- RCCL communicator issuing collectives on the caller's stream (rccl_comm.hip) ----
 // dtype codes: 0 f32, 1 bf16, 2 f16, 3 u8, 4 i32, 5 f64, 6 i64; op: 0 sum, 1 max, 2 min, 3 avg
 std::string ew_rccl_unique_id();

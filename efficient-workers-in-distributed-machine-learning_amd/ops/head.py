@@ -174,6 +174,84 @@ def _spec(d, device, layer):
     return (_ctr(d, device), (_SALT ^ (0x9E3779B9 * (layer + 1))) & 0xFFFFFFFF, p)
 
 
+# VGG classifier tail (fc2 + fc3 + cross-entropy, one launch each way) instead of head.hip's
+# per-Linear kernels + the cross-entropy kernel: opt-in (EWDML_HEAD_TAIL=1).  Three launches fewer,
+# but its forward's chain (tile GEMM, ticket, logit shares, loss, dh2, ticket) took 23.7 us
+# against 17.7 for the three launches it replaces: 1.200 vs 1.193 ms per VGG-11 step
+# (profiles/ab/README.md)
+_TAIL = os.environ.get("EWDML_HEAD_TAIL", "0") == "1"
+_TAIL_WS = {}  # (device index, B, N2) -> (workspace, tickets): zeroed once, kept zero
+
+
+class _HeadTail(torch.autograd.Function):
+    """(mean cross-entropy, logits) of ``relu(h1 W2^T + b2) W3^T + b3`` against ``y`` -- VGG's
+    classifier after its first Linear -- in one launch each way (ops/csrc/head_tail.hip)."""
+
+    @staticmethod
+    def forward(ctx, h1, y, w2, b2, w3, b3):
+        C_ = require()
+        B, K1 = h1.shape
+        N2, K = w2.shape[0], w3.shape[0]
+        dev = h1.device
+        f32 = dict(dtype=torch.float32, device=dev)
+        h2 = torch.empty(B, N2, **f32)
+        dh2 = torch.empty(B, N2, **f32)
+        logits = torch.empty(B, K, **f32)
+        dlogits = torch.empty(B, K, **f32)
+        lossrow = torch.empty(B, **f32)
+        loss = torch.empty((), **f32)
+        key = (dev.index, B, N2)
+        ws = _TAIL_WS.get(key)
+        if ws is None:
+            ws = _TAIL_WS[key] = (torch.zeros(C_.tail_ws_floats(B, N2), **f32),
+                                  torch.zeros(C_.tail_counters(B), dtype=torch.int32, device=dev))
+        C_.tail_fwd(_ptr(h1), _ptr(w2), _ptr(b2), _ptr(w3), _ptr(b3), _ptr(y), B, K1, N2, K,
+                    _ptr(h2), _ptr(logits), _ptr(dlogits), _ptr(dh2), _ptr(lossrow), _ptr(loss),
+                    _ptr(ws[0]), ws[0].numel(), _ptr(ws[1]), ws[1].numel(), _stream())
+        ctx.save_for_backward(h1, h2, dh2, dlogits, w2)
+        ctx.shapes = (w3.shape, b2.shape, b3.shape)
+        ctx.mark_non_differentiable(logits)
+        ctx.set_materialize_grads(False)
+        return loss, logits
+
+    @staticmethod
+    def backward(ctx, gloss, _glogits):
+        C_ = require()
+        h1, h2, dh2, dlogits, w2 = ctx.saved_tensors
+        B, K1 = h1.shape
+        N2, K = w2.shape[0], dlogits.shape[1]
+        g = gloss.detach().to(torch.float32).contiguous()
+        dh1 = torch.empty_like(h1)
+        dw2, db2 = torch.empty_like(w2), torch.empty(N2, dtype=torch.float32, device=h1.device)
+        dw3 = torch.empty(K, N2, dtype=torch.float32, device=h1.device)
+        db3 = torch.empty(K, dtype=torch.float32, device=h1.device)
+        C_.tail_bwd(_ptr(h1), _ptr(h2), _ptr(dh2), _ptr(dlogits), _ptr(w2), _ptr(g), B, K1, N2, K,
+                    _ptr(dh1), _ptr(dw2), _ptr(db2), _ptr(dw3), _ptr(db3), _stream())
+        return dh1, None, dw2, db2, dw3, db3
+
+
+def tail_supported(cls, x, y) -> bool:
+    """The fused classifier tail applies: fp32 VGG head layout, <= 16 classes, widths % 16, int64
+    labels, no autocast."""
+    if not (_TAIL and supported(cls, x) and x.dtype == torch.float32 and y is not None
+            and y.dtype == torch.int64 and y.dim() == 1 and y.shape[0] == x.shape[0]
+            and y.is_contiguous() and not torch.is_autocast_enabled("cuda")):
+        return False
+    l2, l3 = cls[4], cls[6]
+    return (0 < l3.out_features <= 16 and l2.in_features % 16 == 0 and l2.out_features % 16 == 0
+            and l3.weight.is_contiguous() and l3.bias.is_contiguous()
+            and l2.weight.data_ptr() % 16 == 0)
+
+
+def vgg_loss(cls, x, y):
+    """(mean cross-entropy, logits) of VGG's classifier on ``x`` against ``y``: the first Linear
+    (with both dropouts) on head.hip's kernels, the rest on the fused tail."""
+    d0, l1, _, d1, l2, _, l3 = list(cls)
+    dev = x.device
+    h1 = head_linear(x, l1, relu=True, din=_spec(d0, dev, 0), dout=_spec(d1, dev, 1))
+    return _HeadTail.apply(h1, y, l2.weight, l2.bias, l3.weight, l3.bias)
+
+
 def vgg_head(cls, x):
     """``cls(x)`` for VGG's classifier ``nn.Sequential`` through the fused kernels."""
     if not supported(cls, x):
