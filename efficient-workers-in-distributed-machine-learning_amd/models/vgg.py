@@ -77,6 +77,9 @@ class VGG(nn.Module):
             return None
         from ..ops import head as head_ops
 
+        if not head_ops._TAIL:
+            return None
+
         probe = torch.empty((x.shape[0], self.classifier[1].in_features), dtype=x.dtype,
                             device=x.device)
         if not head_ops.tail_supported(self.classifier, probe, y):
