@@ -927,11 +927,21 @@ __global__ __launch_bounds__(EW_BLOCK) void k_cf_stem_fwd(const float* __restric
   constexpr int WP = CS_KP + 8;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6, li = lane & 15, g = lane >> 4;
   const int m0 = blockIdx.x * 128, n0 = blockIdx.y * 64;
-  for (int e = t; e < 64 * CS_KP; e += EW_BLOCK) {
-    const int nn = e / CS_KP, k = e - nn * CS_KP;
-    wsm[nn * WP + k] = k < CS_K ? w[(long long)(n0 + nn) * CS_K + k] : 0.0f;
+  // the block's 64 x 27 weights: every load of the thread issued before its first LDS write (a
+  // copy loop waited for each load in turn: 7 round trips at the head of every block)
+  constexpr int WR = (64 * CS_KP + EW_BLOCK - 1) / EW_BLOCK;
+  float wr[WR];
+#pragma unroll
+  for (int r = 0; r < WR; ++r) {
+    const int e = min(t + r * EW_BLOCK, 64 * CS_KP - 1), nn = e / CS_KP, k = e - nn * CS_KP;
+    wr[r] = w[(long long)(n0 + nn) * CS_K + min(k, CS_K - 1)];
   }
   const int lo = cs_patch<128>(x, m0, W, M, patch, t);
+#pragma unroll
+  for (int r = 0; r < WR; ++r) {
+    const int e = t + r * EW_BLOCK, nn = e / CS_KP, k = e - nn * CS_KP;
+    if (e < 64 * CS_KP) wsm[nn * WP + k] = k < CS_K ? wr[r] : 0.0f;
+  }
   __syncthreads();
   const int HW = H * W;
   float a[2][7];
