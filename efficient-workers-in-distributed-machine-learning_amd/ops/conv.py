@@ -109,6 +109,12 @@ _SMALLMAP = os.environ.get("EWDML_SMALLMAP", "1") != "0"
 _SM_LAZY_BWD = os.environ.get("EWDML_SM_LAZY_BWD", "0") == "1"
 # the same for the Winograd convs (their backward input transforms form the KIND 2 dy)
 _WINO_LAZY_BWD = os.environ.get("EWDML_WINO_LAZY_BWD", "1") != "0"
+# the backward finalisation of the BN layer whose input gradient a conv's backward-data launch
+# produced (its partial sums come from that launch's epilogue) riding in the same conv's fp32
+# weight-gradient GEMM launch as extra blocks (ops/csrc/bn_fin.h) instead of its own launch after
+# it; EWDML_BN_FIN_RIDE=0: the BN backward launches it
+_FIN_RIDE = os.environ.get("EWDML_BN_FIN_RIDE", "1") != "0"
+FIN_RIDES = 0  # finalisations that rode in a weight-gradient launch (tests / diagnostics)
 _SM_WS = {}
 
 
@@ -474,6 +480,37 @@ def _bn_bwd_link(node, x):
     return h, res, code, stats, int(node.mode != "none")
 
 
+def _arm_fin(job):
+    """Arm the BN backward finalisation of ``job`` (see ``_FIN_RIDE``) for the next fp32
+    weight-gradient GEMM launch; returns its outputs (coef, dgamma, dbeta, dcbias)."""
+    if job is None:
+        return None
+    node, part, rows, h, stats = job
+    need = node.needs_input_grad
+    Cb = h.shape[1]
+    dev = h.device
+    coef = torch.empty(2 * Cb, dtype=torch.float32, device=dev)
+    cb_dtype = getattr(node, "cb_dtype", None)
+    dcb = torch.empty(Cb, dtype=cb_dtype, device=dev) if need[2] and cb_dtype else None
+    dg = torch.empty(Cb, dtype=torch.float32, device=dev) if need[3] else None
+    db = torch.empty(Cb, dtype=torch.float32, device=dev) if need[4] else None
+    M = h.shape[0] * h.shape[2] * h.shape[3]
+    require().cf_arm_bn_fin(_ptr(part), int(rows), Cb, M, _ptr(stats), _ptr(coef), _ptr(dg),
+                            _ptr(db), _ptr(dcb), int(cb_dtype == torch.bfloat16))
+    return coef, dg, db, dcb
+
+
+def _fin_done(node, fin):
+    """After the weight-gradient launch: the finalisation ran in it (or runs now on its own); the
+    BN backward of ``node`` takes its outputs instead of launching it."""
+    global FIN_RIDES
+    if require().cf_flush_bn_fin(_stream()) == 0:
+        FIN_RIDES += 1
+    pre = getattr(node, "_ew_pre_bwd", None)
+    if pre is not None:
+        node._ew_pre_bwd = pre[:4] + (fin,)
+
+
 class _Conv(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, bn_node=None, sink=None):
@@ -569,6 +606,7 @@ class _Conv(torch.autograd.Function):
         f32 = x.dtype == torch.float32
         bwd_data = C_.conv_f32_bwd_data if f32 else C_.conv_bwd_data
         dx = dw = None
+        fin_job = None  # (BN node, partials, rows, h, stats): its finalisation may ride in the wgrad
         D = None  # Winograd: the weight gradient's dy transform, made by the bwd-data pass
         m = ctx.wino[2] if ctx.wino is not None else 0
         aa = (m + 2) ** 2
@@ -628,12 +666,15 @@ class _Conv(torch.autograd.Function):
                                 _ptr(part), part.numel(), _ptr(add), _stream())
                 if rows > 0:
                     node._ew_pre_bwd = (part, rows, dx, dx._version)
+                    if _FIN_RIDE and f32 and ctx.needs_input_grad[1]:
+                        fin_job = (node, part, rows, h, stats)
             if sink is not None:
                 sink.grad, sink.taken = None, True
         if ctx.needs_input_grad[1]:
             dw = torch.empty_like(w, memory_format=torch.channels_last)
             side = _wgrad_side(x.device) if _dw_may_lag(ctx) else None
             V = ctx.wino[1] if m else None
+            fin = _arm_fin(fin_job) if side is None else None
 
             def launch_wgrad():
                 if m:
@@ -663,6 +704,8 @@ class _Conv(torch.autograd.Function):
 
             if side is None:
                 launch_wgrad()
+                if fin is not None:
+                    _fin_done(fin_job[0], fin)
             else:
                 # queued (holding its tensors, so their memory is not reused), issued on the side
                 # stream with the next _WGRAD_BATCH - 1 ones or at the first gradient read

@@ -31,6 +31,7 @@
 #include <cstdio>
 #include <cstdlib>
 
+#include "bn_fin.h"
 #include "common.h"
 #include "conv_f32.h"
 #include "ewdml_ops.h"
@@ -584,13 +585,29 @@ __global__ __launch_bounds__(64 * WM * WN, WPE) void k_cf_gemm(const float* __re
                                                    float* __restrict__ out,
                                                    float* __restrict__ slab, CfGeom geo,
                                                    float* __restrict__ bnpart, CfBnBwd bb,
-                                                   const float* __restrict__ addend) {
+                                                   const float* __restrict__ addend, EwBnFin fin) {
   using L = CfLayout<MODE, BM, BN>;
   using acc_t = typename CfMfma<SH>::acc_t;
   constexpr int NT = 64 * WM * WN;
   constexpr int MI = BM / WM / SH, NJ = BN / WN / SH;
   static_assert(MI >= 1 && NJ >= 1 && MI * SH * WM == BM && NJ * SH * WN == BN, "wave tiling");
+  static_assert(NT >= EW_BLOCK && 2 * L::STAGE >= 3 * EW_WAVES * EW_FIN_CH * 8, "finalize rider");
   __shared__ __attribute__((aligned(16))) char smem[2 * L::STAGE];
+  int gz = gridDim.z;
+  if constexpr (MODE == CF_WGRAD) {
+    // a BatchNorm backward finalisation riding along (cf_gemm: extra z slices after the GEMM's,
+    // dispatched last, one channel group per block; bn_fin.h)
+    if (fin.ngrp) {
+      const int gxy = gridDim.x * gridDim.y;
+      gz -= (fin.ngrp + gxy - 1) / gxy;
+      if ((int)blockIdx.z >= gz) {
+        const int g = ((int)blockIdx.z - gz) * gxy + blockIdx.y * gridDim.x + blockIdx.x;
+        // 8 rows in flight: no more registers than the GEMM's own (16 raised the 64x64 tile's)
+        if (g < fin.ngrp) ew_bn_bwd_fin_group<2, 8>(fin, g, reinterpret_cast<double*>(smem));
+        return;
+      }
+    }
+  }
   const int t = threadIdx.x, lane = t & 63, wq = t >> 6;
   const int wm = wq / WN, wn = wq % WN;
   const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
@@ -599,7 +616,7 @@ __global__ __launch_bounds__(64 * WM * WN, WPE) void k_cf_gemm(const float* __re
   b_src += (geo.b_flip ? cf_flip4(zb) : zb) * geo.b_bs;
   out += zb * geo.o_bs;
   // slabs [split][batch][M][Ncol]: the reduction sums the splits of a contiguous batch run
-  if (slab) slab += (long long)(zs * (gridDim.z / geo.nsplit) + zb) * geo.M * geo.Ncol;
+  if (slab) slab += (long long)(zs * (gz / geo.nsplit) + zb) * geo.M * geo.Ncol;
   // stride-2 backward data: z = dx phase, heaviest first (3x3: z 0 = phase (1, 1) with 4 taps
   // ... z 3 = phase (0, 0) with 1; blocks dispatch in z order, so the light phases backfill)
   constexpr bool S2B = STR == 2 && MODE == CF_BWD;
@@ -1170,6 +1187,15 @@ bool cf_glds_on() {
   return g_cf_glds == 1;
 }
 
+// The BatchNorm backward finalisation armed for the next weight-gradient GEMM launch (host thread
+// that enqueues a conv's backward; ew_cf_arm_bn_fin / ew_cf_flush_bn_fin)
+thread_local EwBnFin g_cf_fin{};
+
+__global__ __launch_bounds__(EW_BLOCK) void k_cf_bn_fin(EwBnFin f) {
+  __shared__ double red[2 * EW_WAVES * EW_FIN_CH];
+  ew_bn_bwd_fin_group<2>(f, blockIdx.x, red);
+}
+
 // Launch plan: tile shape and split of the reduction, from a small cost model (us): every block
 // k-step costs its MFMA time (bm*bn*32*2 FLOP at 614 GFLOP/s per CU, derated for the narrower
 // tiles' lower operand reuse), each block pays ~3 k-steps of prologue / epilogue, a CU runs
@@ -1228,7 +1254,7 @@ CfPlan cf_plan(int M, int Ncol, int ksteps, long long ws_floats, int batch) {
 
 #define CF_LAUNCH_W(MODE_, BM_, BN_, WM_, WN_, SH_, WPE_)                                   \
   hipLaunchKernelGGL((k_cf_gemm<MODE_, BM_, BN_, WM_, WN_, SH_, STR, WPE_>), grid,                \
-                     dim3(64 * WM_ * WN_), 0, s, a, b, out, slab, geo, bnp, bbv, addend)
+                     dim3(64 * WM_ * WN_), 0, s, a, b, out, slab, geo, bnp, bbv, addend, fin)
 #define CF_LAUNCH(MODE_, BM_, BN_, WM_, WN_, SH_) CF_LAUNCH_W(MODE_, BM_, BN_, WM_, WN_, SH_, 0)
 #define CF_LAUNCH_GL(BM_, BN_, WM_, WN_, SH_, WPE_)                                           \
   hipLaunchKernelGGL((k_cf_gemm_gl<BM_, BN_, WM_, WN_, SH_, WPE_>), grid, dim3(64 * WM_ * WN_), 0, \
@@ -1263,6 +1289,13 @@ int cf_gemm(const float* a, const float* b, float* out, float* ws, long long ws_
   geo.kps = p.kps;
   geo.nsplit = p.split;
   dim3 grid(geo.M / p.bm, geo.Ncol / p.bn, p.split * batch);
+  // an armed BatchNorm backward finalisation (ew_cf_arm_bn_fin) rides in a weight-gradient GEMM
+  EwBnFin fin{};
+  if (MODE == CF_WGRAD && g_cf_fin.ngrp) {
+    fin = g_cf_fin;
+    g_cf_fin = EwBnFin{};
+    grid.z += (fin.ngrp + grid.x * grid.y - 1) / (grid.x * grid.y);
+  }
   float* slab = p.split > 1 ? ws : nullptr;
   const long long prow = geo.M / p.bm;
   float* bnp = (bnpart && !slab && prow <= 1024 && 2 * prow * geo.Ncol <= bnpart_floats) ? bnpart
@@ -1356,6 +1389,29 @@ int cf_taps(int ksize) {
 
 // ------------------------------------------------------------------------------------------------
 // host side (shapes validated here: the kernels assume them)
+
+// Arm a BatchNorm backward finalisation (the partials of a backward-data epilogue, NS = 2; see
+// bn_fin.h) for the next weight-gradient GEMM launched from this thread; ew_cf_flush_bn_fin
+// launches it on its own if none took it (returns 1 then).
+void ew_cf_arm_bn_fin(uintptr_t part, int nblk, int C, long long M, uintptr_t stats, uintptr_t coef,
+                      uintptr_t dgamma, uintptr_t dbeta, uintptr_t dcbias, int cb_bf16) {
+  if (!part || !stats || !coef || nblk <= 0 || C <= 0 || M <= 0)
+    throw std::runtime_error("ewdml conv f32: bad BatchNorm finalisation job");
+  if (g_cf_fin.ngrp) throw std::runtime_error("ewdml conv f32: a finalisation is already armed");
+  g_cf_fin = EwBnFin{reinterpret_cast<const float*>(part), reinterpret_cast<const float*>(stats),
+                     reinterpret_cast<float*>(coef), reinterpret_cast<float*>(dgamma),
+                     reinterpret_cast<float*>(dbeta), reinterpret_cast<void*>(dcbias), M, nblk, C,
+                     cb_bf16, (C + EW_FIN_CH - 1) / EW_FIN_CH};
+}
+
+int ew_cf_flush_bn_fin(uintptr_t stream) {
+  if (!g_cf_fin.ngrp) return 0;
+  const EwBnFin f = g_cf_fin;
+  g_cf_fin = EwBnFin{};
+  hipLaunchKernelGGL(k_cf_bn_fin, dim3(f.ngrp), dim3(EW_BLOCK), 0, (hipStream_t)stream, f);
+  EW_CHECK_LAUNCH();
+  return 1;
+}
 
 int ew_cf_set_glds(int on) {
   const int prev = cf_glds_on() ? 1 : 0;

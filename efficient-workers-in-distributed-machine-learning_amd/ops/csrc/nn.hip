@@ -7,6 +7,7 @@
 // two 2-element row pairs (4 B each in bf16) and writes the max + its code; backward writes the
 // 2x2 window from dy and the code.  Tie / NaN semantics match PyTorch (first max in row-major
 // window order; a NaN wins).
+#include "bn_fin.h"
 #include "common.h"
 #include "ewdml_ops.h"
 
@@ -247,61 +248,6 @@ __device__ __forceinline__ double ew_wave_sum_d(double v) {
   return v;
 }
 
-// Sum the nblk partial rows of NS quantities per channel in a fixed order.  Block = 16 channels
-// (t & 15) x 16 row slices (t >> 4): a wave's load covers 4 rows x 16 consecutive channels (64-B
-// segments; 4 channels x 64 slices -- 16-B segments, 16 lines per load -- was slower, 5.7 -> 7.2
-// us), each thread issues the loads of 16 of its rows for every quantity before adding any (was 4:
-// ~8 dependent round trips for VGG's 512-row partials).  Slices combine by a fixed shuffle tree
-// within each wave (lanes with the same channel: xor 16, 32) and then over the 4 waves in order
-// through LDS.  Returns true (for lanes 0-15 of wave 0, c < C) with out[] holding the sums.
-constexpr int EW_FIN_CH = 16;
-template <int NS>
-__device__ __forceinline__ bool ew_sum_parts(const float* __restrict__ part, int nblk, int C,
-                                             int c, double out[NS]) {
-  __shared__ double red[NS][EW_WAVES][EW_FIN_CH];
-  const int t = threadIdx.x, rs = t / EW_FIN_CH, lane = t & 63, w = t >> 6;
-  constexpr int RS = EW_BLOCK / EW_FIN_CH;  // row slices
-  constexpr int U = 16;                     // rows in flight per thread
-  double acc[NS];
-#pragma unroll
-  for (int s = 0; s < NS; ++s) acc[s] = 0.0;
-  if (c < C) {
-    for (int b0 = rs; b0 < nblk; b0 += U * RS) {
-      // unconditional loads of a clamped row, masked when added: a guarded load is a branch,
-      // and hipcc waits for every load at each branch merge (one round trip per row)
-      float v[NS][U];
-#pragma unroll
-      for (int s = 0; s < NS; ++s)
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int b = min(b0 + u * RS, nblk - 1);
-          v[s][u] = part[((long long)s * nblk + b) * C + c];
-        }
-#pragma unroll
-      for (int s = 0; s < NS; ++s)
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-          if (b0 + u * RS < nblk) acc[s] += (double)v[s][u];
-    }
-  }
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-#pragma unroll
-    for (int o = EW_FIN_CH; o < 64; o <<= 1) acc[s] += __shfl_xor(acc[s], o, 64);
-    if (lane < EW_FIN_CH) red[s][w][lane] = acc[s];
-  }
-  __syncthreads();
-  if (t >= EW_FIN_CH || c >= C) return false;
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    double a = red[s][0][t];
-#pragma unroll
-    for (int r = 1; r < EW_WAVES; ++r) a += red[s][r][t];
-    out[s] = a;
-  }
-  return true;
-}
-
 __global__ __launch_bounds__(EW_BLOCK) void k_bn_fwd_finalize(
     const float* __restrict__ part, int nblk, int C, long long M, const float* __restrict__ gamma,
     const float* __restrict__ beta, const void* __restrict__ cbias, int cb_bf16,
@@ -323,8 +269,9 @@ __global__ __launch_bounds__(EW_BLOCK) void k_bn_fwd_finalize(
       cb = cb_bf16 ? ew_bf16f(reinterpret_cast<const uint16_t*>(cbias)[cc])
                    : reinterpret_cast<const float*>(cbias)[cc];
   }
+  __shared__ double red[2 * EW_WAVES * EW_FIN_CH];
   double sums[2];
-  if (!ew_sum_parts<2>(part, nblk, C, c, sums)) return;
+  if (!ew_sum_parts<2>(part, nblk, C, c, sums, red)) return;
   const double mean = sums[0] / (double)M;
   double var = sums[1] / (double)M - mean * mean;
   if (var < 0.0) var = 0.0;
@@ -532,31 +479,11 @@ __global__ __launch_bounds__(EW_BLOCK) void k_bn_bwd_stats(
   }
 }
 
-// NS = 3: partials of k_bn_bwd_stats; NS = 2: of a backward-data conv epilogue (ops/csrc/conv.hip
-// CvBnBwd), whose sum(h - mean) -- 0 up to rounding -- is taken as 0
+// NS = 3: partials of k_bn_bwd_stats; NS = 2: of a backward-data conv epilogue (bn_fin.h)
 template <int NS>
-__global__ __launch_bounds__(EW_BLOCK) void k_bn_bwd_finalize(
-    const float* __restrict__ part, int nblk, int C, long long M, const float* __restrict__ stats,
-    float* __restrict__ coef, float* __restrict__ dgamma, float* __restrict__ dbeta,
-    void* __restrict__ dcbias, int cb_bf16) {
-  const int c = blockIdx.x * EW_FIN_CH + (threadIdx.x % EW_FIN_CH);
-  const int cc = c < C ? c : C - 1;
-  const double invstd = stats[C + cc], scale = stats[2 * C + cc];  // ahead of the sums' loads
-  double sums[3];
-  if (!ew_sum_parts<NS>(part, nblk, C, c, sums)) return;
-  if (NS == 2) sums[2] = 0.0;
-  const double db = sums[0];             // sum dz
-  const double dg = sums[1] * invstd;    // sum dz * xhat
-  const double e = -scale * invstd * dg / (double)M;
-  coef[c] = (float)e;
-  coef[C + c] = (float)(-scale * db / (double)M);
-  if (dgamma) dgamma[c] = (float)dg;
-  if (dbeta) dbeta[c] = (float)db;
-  if (dcbias) {  // sum over rows of dx = e * sum(h - mean)
-    const float v = (float)(e * sums[2]);
-    if (cb_bf16) reinterpret_cast<uint16_t*>(dcbias)[c] = ew_f2bf(v);
-    else reinterpret_cast<float*>(dcbias)[c] = v;
-  }
+__global__ __launch_bounds__(EW_BLOCK) void k_bn_bwd_finalize(EwBnFin f) {
+  __shared__ double red[NS * EW_WAVES * EW_FIN_CH];
+  ew_bn_bwd_fin_group<NS>(f, blockIdx.x, red);
 }
 
 template <typename T, int MODE>
@@ -917,21 +844,24 @@ static void ew_bn_bwd_impl(const BnBwdArgs& a) {
   const uint8_t* code = reinterpret_cast<const uint8_t*>(a.code);
   const float* st = reinterpret_cast<const float*>(a.stats);
   float* coef = reinterpret_cast<float*>(a.coef);
+  EwBnFin fin{};
+  fin.dgamma = reinterpret_cast<float*>(a.dgamma);
+  fin.dbeta = reinterpret_cast<float*>(a.dbeta);
+  fin.dcbias = reinterpret_cast<void*>(a.dcbias);
+  fin.ngrp = (C + EW_FIN_CH - 1) / EW_FIN_CH;
   if (a.phase == 2) {
     // apply only (a lazy backward materialised after all): coef from the earlier phase-1 call
   } else if (pre) {
-    hipLaunchKernelGGL(k_bn_bwd_finalize<2>, dim3((C + EW_FIN_CH - 1) / EW_FIN_CH), dim3(EW_BLOCK),
-                       0, s, part, a.pre_nblk, C, M, st, coef, reinterpret_cast<float*>(a.dgamma),
-                       reinterpret_cast<float*>(a.dbeta), reinterpret_cast<void*>(a.dcbias),
-                       a.cb_bf16);
+    hipLaunchKernelGGL(k_bn_bwd_finalize<2>, dim3(fin.ngrp), dim3(EW_BLOCK), 0, s,
+                       EwBnFin{part, st, coef, fin.dgamma, fin.dbeta, fin.dcbias, M, (int)a.pre_nblk,
+                               C, a.cb_bf16, fin.ngrp});
   } else {
     hipLaunchKernelGGL((k_bn_bwd_stats<T, MODE>), dim3(nblk), dim3(EW_BLOCK), 0, s, h, res, dy,
                        code, st, rows, C, Ho, Wo, rpb, part);
     EW_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_bn_bwd_finalize<3>, dim3((C + EW_FIN_CH - 1) / EW_FIN_CH), dim3(EW_BLOCK),
-                       0, s, part, nblk, C, M, st, coef, reinterpret_cast<float*>(a.dgamma),
-                       reinterpret_cast<float*>(a.dbeta), reinterpret_cast<void*>(a.dcbias),
-                       a.cb_bf16);
+    hipLaunchKernelGGL(k_bn_bwd_finalize<3>, dim3(fin.ngrp), dim3(EW_BLOCK), 0, s,
+                       EwBnFin{part, st, coef, fin.dgamma, fin.dbeta, fin.dcbias, M, nblk, C,
+                               a.cb_bf16, fin.ngrp});
   }
   EW_CHECK_LAUNCH();
   if (a.phase == 1) return;  // lazy: the producing conv's input transform forms dx (KIND 2)

@@ -138,16 +138,23 @@ class _BNAct(torch.autograd.Function):
         pre = getattr(ctx, "_ew_pre_bwd", None)
         ctx._ew_pre_bwd = None
         part, pre_rows = _part(dev), 0
+        done = False  # coef / dgamma / dbeta already made by the conv's weight-gradient launch
         if pre is not None and pre[2] is dy_in and dy_in._version == pre[3]:
             part, pre_rows = pre[0], pre[1]
             global PRE_BWD_USED
             PRE_BWD_USED += 1
+            if len(pre) > 4:  # ops/conv.py _arm_fin: the same outputs the finalize would write
+                coef, dg, db, dcb = pre[4]
+                done = True
         args = (_ptr(h), _ptr(res), _ptr(dy), _ptr(code), _ptr(stats), _ptr(coef), _ptr(part),
                 _ptr(dx), _ptr(dres), _ptr(dg), _ptr(db), _ptr(dcb), N, H, W, C,
                 int(h.dtype == torch.bfloat16), int(ctx.pool), _MODES[ctx.mode],
                 int(ctx.cb_dtype == torch.bfloat16), _stream(), int(pre_rows))
         lazy = ctx.lazy_bwd and sink is None
-        C_.bn_relu_bwd(*args, 1 if lazy else 0)
+        if not done:
+            C_.bn_relu_bwd(*args, 1 if lazy else 0)
+        elif not lazy:
+            C_.bn_relu_bwd(*args, 2)  # the apply alone
         if lazy:
             # statistics only (coef, dgamma, dbeta): the Winograd conv that produced h forms dx
             # in its backward input transform (ops/conv.py); dx is written only if materialised

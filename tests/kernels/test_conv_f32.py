@@ -425,6 +425,47 @@ def test_conv_f32_winograd_bn_backward_sums(mode, pool, m):
         assert _rel(a, b) < 1e-5, _rel(a, b)
 
 
+@pytest.mark.parametrize("wino,m,k,C", [(True, 2, 3, 128), (True, 4, 3, 128), (False, 2, 3, 64),
+                                        (False, 2, 1, 512)])
+@pytest.mark.parametrize("mode,pool", [("relu", True), ("relu", False)])
+def test_bn_finalize_rides_in_wgrad_launch(wino, m, k, C, mode, pool):
+    """The BN backward finalisation riding in the next conv's weight-gradient GEMM launch (extra
+    blocks, ops/csrc/bn_fin.h) gives bitwise the gradients of its own launch, Winograd and direct
+    convs, with the lazy BN backward (coef read by the first conv's input transform) and without."""
+    from ewdml.ops import conv as cmod
+    from ewdml.ops import nn as fnn
+
+    _conv(wino=wino, tile=m)
+    N, HW = 32, 16
+    x0, w0 = _data(N, C, C, HW, HW, seed=51, k=k)
+    _, w1 = _data(8, C, C, 8, 8, seed=52, k=k)
+    bn0 = torch.nn.BatchNorm2d(C).cuda()
+    with torch.no_grad():
+        bn0.weight.uniform_(0.5, 1.5)
+        bn0.bias.uniform_(-0.3, 0.3)
+    g = None
+    grads = []
+    saved = cmod._FIN_RIDE
+    try:
+        for ride in (True, False):
+            cmod._FIN_RIDE = ride
+            rides = cmod.FIN_RIDES
+            bn = copy.deepcopy(bn0)
+            xa, wa, wb = (t.clone().requires_grad_(True) for t in (x0, w0, w1))
+            y = fnn.bn_act(cmod.conv(xa, wa), bn, mode, pool=pool)
+            z = cmod.conv(y, wb)
+            if g is None:
+                g = torch.randn(z.shape, device="cuda").contiguous(
+                    memory_format=torch.channels_last)
+            z.backward(g)
+            assert (cmod.FIN_RIDES > rides) == ride
+            grads.append([xa.grad, wa.grad, wb.grad, bn.weight.grad, bn.bias.grad])
+    finally:
+        cmod._FIN_RIDE = saved
+    for a, b in zip(*grads):
+        assert torch.equal(a, b), _rel(a, b)
+
+
 def test_fp32_vgg11_step_vs_fp64():
     """One fp32 VGG-11-BN training step (fused NHWC path, fp32 MFMA convs, lazy BN through the
     Winograd convs) against the same step in float64 on the CPU, and no worse than the step
