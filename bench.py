@@ -71,6 +71,9 @@ def parse(argv=None):
     # with backward (segmented graphs) for large dense collectives at N > 1 (plan_graph_mode)
     p.add_argument("--hip-graph", default="auto",
                    choices=["auto", "off", "split", "full", "segmented"])
+    # steps per graph launch in the timed loop (Trainer.train_steps): the same steps, one launch
+    # boundary (~7.7 us, tools/probes/launch_floor.py) per U steps; 1 = one graph per step
+    p.add_argument("--graph-unroll", type=int, default=8)
     p.add_argument("--param-dtype", default="auto", choices=["auto", "fp32"])
     p.add_argument("--json-out", default=None, help="also write the JSON line to this file")
     p.add_argument("--extra", default="", help="extra distributed_nn.py flags")
@@ -157,6 +160,11 @@ def _measure(a, tr, gw):
         warm = max(warm, every + gw)
     for _ in range(warm):
         tr.train_step()
+    # --graph-unroll U: the U-step graph captured and replayed once before the clock starts
+    unroll = a.graph_unroll if tr.prepare_unrolled(a.graph_unroll) else 1
+    if unroll > 1:
+        tr.train_steps(unroll, unroll)
+    tr.graph_unroll_used = unroll
     sync()
     tr.comm.barrier()
     sync()
@@ -164,8 +172,7 @@ def _measure(a, tr, gw):
         time.sleep(0.25)
     t0 = time.perf_counter()
     loss = None
-    for _ in range(a.steps):
-        loss, _ = tr.train_step()
+    loss, _ = tr.train_steps(a.steps, unroll)
     t_enq = time.perf_counter()  # host done enqueuing (the GPU may still be running)
     sync()
     t1 = time.perf_counter()
@@ -267,6 +274,7 @@ def main(argv=None):
         "final_loss_note": f"{a.warmup + a.steps} steps from random init, steady-state codec "
                            "without the EF warm-up (see profiles/validation/ef_stability_r03.md)",
         "host_enqueue_ms_per_step": round(enq * 1e3 / a.steps, 4),
+        "graph_unroll": getattr(tr, "graph_unroll_used", 1),
         # multi-GPU self-validation: replicas bitwise identical after the timed steps, the
         # data-plane communicator and its first-contact probe (parallel/probe.py)
         # (None under local SGD between syncs: the replicas agree only right after a sync step)

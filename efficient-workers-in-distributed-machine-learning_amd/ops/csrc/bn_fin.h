@@ -16,13 +16,15 @@
 // are bitwise those of an EW_BLOCK launch.  Returns true (for threads 0-15, c < C) with out[]
 // holding the sums.
 constexpr int EW_FIN_CH = 16;
-// U: rows in flight per thread (the sums' order does not depend on it)
-template <int NS, int U = 16>
+// U: rows in flight per thread (the sums' order does not depend on it); TH: the threads that sum
+// (TH / 16 row slices, TH / 64 waves; the order does depend on it)
+template <int NS, int U = 16, int TH = EW_BLOCK>
 __device__ __forceinline__ bool ew_sum_parts(const float* __restrict__ part, int nblk, int C,
                                              int c, double out[NS], double* red) {
+  constexpr int NW = TH / 64;
   const int t = threadIdx.x, rs = t / EW_FIN_CH, lane = t & 63, w = t >> 6;
-  const bool act = t < EW_BLOCK;
-  constexpr int RS = EW_BLOCK / EW_FIN_CH;  // row slices
+  const bool act = t < TH;
+  constexpr int RS = TH / EW_FIN_CH;  // row slices
   double acc[NS];
 #pragma unroll
   for (int s = 0; s < NS; ++s) acc[s] = 0.0;
@@ -49,15 +51,15 @@ __device__ __forceinline__ bool ew_sum_parts(const float* __restrict__ part, int
   for (int s = 0; s < NS; ++s) {
 #pragma unroll
     for (int o = EW_FIN_CH; o < 64; o <<= 1) acc[s] += __shfl_xor(acc[s], o, 64);
-    if (act && lane < EW_FIN_CH) red[(s * EW_WAVES + w) * EW_FIN_CH + lane] = acc[s];
+    if (act && lane < EW_FIN_CH) red[(s * NW + w) * EW_FIN_CH + lane] = acc[s];
   }
   __syncthreads();
   if (t >= EW_FIN_CH || c >= C) return false;
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
-    double a = red[s * EW_WAVES * EW_FIN_CH + t];
+    double a = red[s * NW * EW_FIN_CH + t];
 #pragma unroll
-    for (int r = 1; r < EW_WAVES; ++r) a += red[(s * EW_WAVES + r) * EW_FIN_CH + t];
+    for (int r = 1; r < NW; ++r) a += red[(s * NW + r) * EW_FIN_CH + t];
     out[s] = a;
   }
   return true;

@@ -248,7 +248,10 @@ __device__ __forceinline__ double ew_wave_sum_d(double v) {
   return v;
 }
 
-__global__ __launch_bounds__(EW_BLOCK) void k_bn_fwd_finalize(
+// TH threads: 1024 (64 row slices) for the long partial lists of the large maps (1024 rows at
+// VGG's 32x32 layers: one batch of loads per thread instead of four)
+template <int TH>
+__global__ __launch_bounds__(TH) void k_bn_fwd_finalize(
     const float* __restrict__ part, int nblk, int C, long long M, const float* __restrict__ gamma,
     const float* __restrict__ beta, const void* __restrict__ cbias, int cb_bf16,
     float* __restrict__ rmean, float* __restrict__ rvar, const long long* __restrict__ nbt,
@@ -269,9 +272,9 @@ __global__ __launch_bounds__(EW_BLOCK) void k_bn_fwd_finalize(
       cb = cb_bf16 ? ew_bf16f(reinterpret_cast<const uint16_t*>(cbias)[cc])
                    : reinterpret_cast<const float*>(cbias)[cc];
   }
-  __shared__ double red[2 * EW_WAVES * EW_FIN_CH];
+  __shared__ double red[2 * (TH / 64) * EW_FIN_CH];
   double sums[2];
-  if (!ew_sum_parts<2>(part, nblk, C, c, sums, red)) return;
+  if (!ew_sum_parts<2, 16, TH>(part, nblk, C, c, sums, red)) return;
   const double mean = sums[0] / (double)M;
   double var = sums[1] / (double)M - mean * mean;
   if (var < 0.0) var = 0.0;
@@ -770,6 +773,15 @@ static int ew_grid_vec(long long nvec) {
 }
 
 
+// EWDML_BN_FIN_WIDE=0: every forward finalize at EW_BLOCK threads (A/B)
+static bool ew_fin_wide() {
+  static const bool on = [] {
+    const char* e = getenv("EWDML_BN_FIN_WIDE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 void ew_bn_relu_fwd(const BnFwdArgs& a) {
   hipStream_t s = (hipStream_t)a.stream;
   const long long M = a.N * (long long)a.H * a.W;
@@ -788,13 +800,17 @@ void ew_bn_relu_fwd(const BnFwdArgs& a) {
       hipLaunchKernelGGL(k_bn_fwd_stats<float>, dim3(nblk), dim3(EW_BLOCK), 0, s,
                          reinterpret_cast<const float*>(a.h), M, C, rpb, part);
     EW_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_bn_fwd_finalize, dim3((C + EW_FIN_CH - 1) / EW_FIN_CH), dim3(EW_BLOCK), 0,
-                       s, part, nblk, C, M, reinterpret_cast<const float*>(a.gamma),
-                       reinterpret_cast<const float*>(a.beta),
-                       reinterpret_cast<const void*>(a.cbias), a.cb_bf16,
-                       reinterpret_cast<float*>(a.rmean), reinterpret_cast<float*>(a.rvar),
-                       reinterpret_cast<const long long*>(a.nbt), a.momentum, a.eps,
-                       reinterpret_cast<float*>(a.stats));
+#define EW_FF(TH)                                                                               \
+  hipLaunchKernelGGL(k_bn_fwd_finalize<TH>, dim3((C + EW_FIN_CH - 1) / EW_FIN_CH), dim3(TH), 0, s, \
+                     part, nblk, C, M, reinterpret_cast<const float*>(a.gamma),                    \
+                     reinterpret_cast<const float*>(a.beta),                                       \
+                     reinterpret_cast<const void*>(a.cbias), a.cb_bf16,                            \
+                     reinterpret_cast<float*>(a.rmean), reinterpret_cast<float*>(a.rvar),          \
+                     reinterpret_cast<const long long*>(a.nbt), a.momentum, a.eps,                 \
+                     reinterpret_cast<float*>(a.stats))
+    if (nblk > 256 && ew_fin_wide()) EW_FF(1024);
+    else EW_FF(EW_BLOCK);
+#undef EW_FF
     EW_CHECK_LAUNCH();
   }
   if (a.phase == 1) return;  // lazy: the consumer applies (winograd_f32.hip WgSrc KIND 1)

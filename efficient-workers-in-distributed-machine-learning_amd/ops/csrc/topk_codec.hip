@@ -89,7 +89,39 @@ enum EfMode { EF_NONE = 0, EF_PLAIN = 1, EF_DGC = 2 };
 // Error-feedback staging of one chunk held in registers (v = the gradient on entry, the vector to
 // compress on exit): plain e = g + r, or DGC's momentum correction; e (and DGC's velocity) are
 // written back, so later passes read e from the residual.
-template <int EFM>
+// slabs [u0, u0 + N) of a chunk of a flat fp32 buffer (src / dst = the chunk's start), as
+// ew_ld_chunk / ew_st_chunk hold them
+template <int N>
+__device__ __forceinline__ void ew_ld_slabs(const float* src, int len, int u0, float4 (&v)[N]) {
+#pragma unroll
+  for (int q = 0; q < N; ++q) {
+    const int i = ew_chunk_idx(u0 + q);
+    if (len == EW_CHUNK) {
+      v[q] = *reinterpret_cast<const float4*>(src + i);
+    } else {
+      float xs[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) xs[j] = i + j < len ? src[i + j] : 0.0f;
+      v[q] = make_float4(xs[0], xs[1], xs[2], xs[3]);
+    }
+  }
+}
+template <int N>
+__device__ __forceinline__ void ew_st_slabs(float* dst, int len, int u0, const float4* v) {
+#pragma unroll
+  for (int q = 0; q < N; ++q) {
+    const int i = ew_chunk_idx(u0 + q);
+    if (i + 3 < len) {
+      *reinterpret_cast<float4*>(dst + i) = v[q];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (i + j < len) dst[i + j] = ew_f4(v[q], j);
+    }
+  }
+}
+
+template <int EFM, bool HALVES = false>
 __device__ __forceinline__ void topk_ef_stage(const GradPtrs& gp, const DgcArgs& dg,
                                               float* __restrict__ resid, const ChunkRow& c,
                                               float4 (&v)[EW_CU]) {
@@ -100,6 +132,46 @@ __device__ __forceinline__ void topk_ef_stage(const GradPtrs& gp, const DgcArgs&
     for (int u = 0; u < EW_CU; ++u)
       v[u] = make_float4(v[u].x + r[u].x, v[u].y + r[u].y, v[u].z + r[u].z, v[u].w + r[u].w);
     ew_st_chunk(resid + c.start, c.len, v);
+  } else if (EFM == EF_DGC && HALVES) {
+    // the same in two halves of the chunk: the residual / velocity / parameter registers of one
+    // half at a time (k_pk_hist0: 150 -> fewer VGPRs, more chunks resident at once)
+    const float lr = dg.lr_ptr ? *dg.lr_ptr : 1.0f;
+    constexpr int H = EW_CU / 2;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      float4 r[H], uv[H], pv[H];
+      ew_ld_slabs<H>(resid + c.start, c.len, hh * H, r);
+      ew_ld_slabs<H>(dg.vel + c.start, c.len, hh * H, uv);
+      if (dg.wd != 0.0f) ew_ld_slabs<H>(dg.param + c.start, c.len, hh * H, pv);
+#pragma unroll
+      for (int q = 0; q < H; ++q) {
+        const int u = hh * H + q;
+        float g4[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+        float u4[4] = {uv[q].x, uv[q].y, uv[q].z, uv[q].w};
+        const float r4[4] = {r[q].x, r[q].y, r[q].z, r[q].w};
+        float e4[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float g = g4[j];
+          if (dg.wd != 0.0f) g = g + ew_f4(pv[q], j) * dg.wd;
+          const float a = u4[j] * dg.momentum;
+          const float b = g * dg.damp1;
+          u4[j] = a + b;
+          float d = u4[j];
+          if (dg.nesterov) {
+            const float mu = u4[j] * dg.momentum;
+            d = g + mu;
+          }
+          if (dg.lr_ptr) d = d * lr;
+          e4[j] = r4[j] + d;
+        }
+        uv[q] = make_float4(u4[0], u4[1], u4[2], u4[3]);
+        v[u] = make_float4(e4[0], e4[1], e4[2], e4[3]);
+      }
+      ew_st_slabs<H>(dg.vel + c.start, c.len, hh * H, uv);
+      ew_st_slabs<H>(resid + c.start, c.len, hh * H, v + hh * H);
+      __builtin_amdgcn_sched_barrier(0);  // the second half's loads after the first half's stores
+    }
   } else if (EFM == EF_DGC) {
     // momentum correction (oracle.dgc_accumulate, every product / sum rounded on its own):
     // g' = g + wd p ; u = m u + (1 - d) g' ; d = g' + m u (Nesterov) | u ; e = r + d
@@ -1044,8 +1116,10 @@ __device__ __forceinline__ void pk_inline_select(const uint2* __restrict__ cands
   __syncthreads();
 }
 
-template <int EFM>
-__global__ __launch_bounds__(EW_BLOCK) void k_pk_hist0(
+// WPE: waves per SIMD the register allocation must allow (0: the compiler's choice, 150 VGPRs with
+// DGC staging = 3 blocks per CU, so VGG-11's 1190 chunks ran in two rounds)
+template <int EFM, int WPE = 0>
+__global__ __launch_bounds__(EW_BLOCK, WPE) void k_pk_hist0(
     GradPtrs gp, DgcArgs dg, unsigned long long* __restrict__ lb, float* __restrict__ resid,
     const ChunkRow* __restrict__ chunks, uint32_t* __restrict__ kmaxr, int T,
     const TensorRow* __restrict__ tensors, uint32_t* __restrict__ pst, int* __restrict__ tick,
@@ -1066,7 +1140,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_pk_hist0(
     for (int t = threadIdx.x; t < T; t += EW_BLOCK) tick[TICK_STRIDE * (T + t)] = 0;
   float4 v[EW_CU];
   ew_ld_chunk(gp, nullptr, c, v);
-  topk_ef_stage<EFM>(gp, dg, resid, c, v);
+  topk_ef_stage<EFM, (WPE > 0)>(gp, dg, resid, c, v);
   const uint32_t P = pst[c.tensor * 8];
   uint32_t kmax = 0;
   unsigned long long pa = 0, pb = 0;  // candidates per slab, 16-bit fields (slabs 0-3, 4-7)
@@ -2079,10 +2153,20 @@ void ew_topk_encode(const TopkEncodeArgs& a) {
 #define EW_PKH(EFM)                                                                              \
   EW_LAUNCH(k_pk_hist0<EFM>, C, s, g, dg, lb, resid, chunks, kmaxr, T, tensors, pst, tick, ccount, \
             cbase, ccnt, pcand, pk_stats, state, cand_n, inline_max)
-    if (dg.vel) EW_PKH(EF_DGC);
+#define EW_PKH_W(EFM, WPE)                                                                       \
+  EW_LAUNCH((k_pk_hist0<EFM, WPE>), C, s, g, dg, lb, resid, chunks, kmaxr, T, tensors, pst, tick,  \
+            ccount, cbase, ccnt, pcand, pk_stats, state, cand_n, inline_max)
+    static const int h0_wpe = [] {  // EWDML_PK_H0_WPE=4|5: DGC hist0 held to that occupancy (A/B)
+      const char* e = getenv("EWDML_PK_H0_WPE");
+      return e ? atoi(e) : 0;
+    }();
+    if (dg.vel && h0_wpe == 5) EW_PKH_W(EF_DGC, 5);
+    else if (dg.vel && h0_wpe == 4) EW_PKH_W(EF_DGC, 4);
+    else if (dg.vel) EW_PKH(EF_DGC);
     else if (resid) EW_PKH(EF_PLAIN);
     else EW_PKH(EF_NONE);
 #undef EW_PKH
+#undef EW_PKH_W
     if (G <= ew_pk_fused_max_blocks()) {
       // one launch for the three passes (per-tensor barriers; every block resident at once)
       EW_LAUNCH(k_pk_select, G, s, g, src_flat, chunks, cbl, tensors, pst, pcand, hist0, hist1,

@@ -255,6 +255,9 @@ class Trainer:
         if self.graph_mode == "segmented":  # collectives on their own stream, beside backward
             self.exchange.comm_stream = torch.cuda.Stream(device=self.device)
         self._graphs = None
+        # (U, graph, loss, out): U consecutive steps captured as one graph (train_steps)
+        self._ugraph = None
+        self._unroll_bad = False
         # local SGD keeps two captured steps, "local" and (model mode, own communicator) "sync";
         # the idle one waits here with its static inputs and outputs
         self._gkind, self._gslots = "local", {}
@@ -351,6 +354,7 @@ class Trainer:
         """Forget every captured step (the next graphed step re-captures)."""
         self._graphs = None
         self._gslots = {}
+        self._ugraph = None
 
     def _graph_kind(self):
         """Local SGD: make the captured graph of this step's kind current."""
@@ -402,6 +406,111 @@ class Trainer:
         if self.clock is not None:
             self.clock.mark("other")  # anything after the last phase mark (host bookkeeping)
         return out
+
+    def train_steps(self, n: int, unroll: int = 1):
+        """``n`` synchronous steps; returns the last one's (loss, out).  With ``unroll`` U > 1 and
+        a captured single-graph step (``--hip-graph full``, fused loader, constant schedules),
+        runs of U steps replay one graph holding U copies of the step: the same kernels and
+        collectives, one graph launch boundary (~7.7 us on MI355X,
+        ``tools/probes/launch_floor.py``) per U steps instead of per step.  Steps that do not fit a
+        run of U (the remainder, an epoch boundary) replay the one-step graph."""
+        out = None
+        while n > 0:
+            if unroll > 1 and n >= unroll and self._unroll_ok(unroll) and \
+                    (self._ugraph is not None and self._ugraph[0] == unroll
+                     or self.prepare_unrolled(unroll)):
+                out = self._unrolled_step()
+                n -= unroll
+            else:
+                out = self.train_step()
+                n -= 1
+        return out
+
+    def prepare_unrolled(self, unroll: int) -> bool:
+        """Capture the U-step graph now (outside a timed region) if :meth:`train_steps` would use
+        it; True when it is ready."""
+        if unroll > 1 and not self._unroll_bad and self._unroll_ok(unroll, pos=False):
+            if self._ugraph is None or self._ugraph[0] != unroll:
+                err = None
+                try:
+                    self._capture_unrolled(unroll)
+                except Exception as e:  # noqa: BLE001 - the one-step graph keeps running
+                    err = e
+                # every rank or none (the graph holds the step's collectives)
+                if self.comm.all_reduce_scalars([0.0 if err is None else 1.0], op="max")[0]:
+                    self._ugraph = None
+                    self._unroll_bad = True
+                    if err is not None:  # a failed capture can leave its stream capturing
+                        self.gstream = torch.cuda.Stream(device=self.device)
+                        ge = getattr(self.exchange, "inner", self.exchange)
+                        if getattr(ge, "side", None) is not None:
+                            ge.side = torch.cuda.Stream(device=self.device)
+                    torch.cuda.synchronize()
+                    self.log.info(f"unrolled graph capture failed ({err!r} on this rank); "
+                                  "one graph per step")
+                    return False
+            return True
+        return False
+
+    def _unroll_ok(self, unroll: int, pos: bool = True) -> bool:
+        cfg = self.cfg
+        ok = (self.graph_mode == "full" and self._graphs is not None and len(self._graphs) == 1
+              and self._in_graph_batch and self.loader is not None and self.loader.fused
+              and self.clock is None and not self.local_sgd and not self.is_server
+              and not self.ps_graph and self.fault is None and self.gstream is not None
+              and not (cfg.lr_warmup_epochs > 0 or cfg.lr_decay_epochs)
+              and not [v for v in cfg.topk_warmup.split(",") if v.strip()])
+        if ok and pos:  # no epoch roll-over inside the run (the permutation is host-driven)
+            self.loader.begin_step()
+            ok = self.loader._pos + unroll <= self.loader.batches_per_epoch
+        return ok
+
+    def _capture_unrolled(self, unroll: int):
+        ex = self.exchange
+        saved = (ex.step_idx, self.opt.steps)
+        mode = os.environ.get("EWDML_GRAPH_CAPTURE_MODE", "thread_local")
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        try:
+            # the one-step graph's pool: the two never run at once (same stream, in order)
+            with torch.cuda.graph(g, pool=self._graphs[0].pool(), stream=self.gstream,
+                                  capture_error_mode=mode):
+                try:
+                    for _ in range(unroll):
+                        self._gx, self._gy = self.loader.emit()
+                        loss, out = self.forward_backward(self._gx, self._gy)
+                        ex.finish()
+                except BaseException:
+                    self._rejoin_side()
+                    raise
+        finally:
+            ex.step_idx, self.opt.steps = saved
+        self._ugraph = (unroll, g, loss, out)
+
+    def _unrolled_step(self):
+        unroll, g, loss, out = self._ugraph
+        ex = self.exchange
+        for _ in range(unroll):
+            self.loader.advance()
+        if not self._key_synced:
+            ex.set_device_key()
+            self._key_synced = True
+        if _SAME_STREAM_REPLAY:  # as the one-step graph (train_step)
+            with self._range("graph_steps"):
+                g.replay()
+        else:
+            gs = self.gstream
+            gs.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(gs):
+                with self._range("graph_steps"):
+                    g.replay()
+            torch.cuda.current_stream().wait_stream(gs)
+        self.comm.watch()
+        ex.step_idx += unroll
+        self.opt.steps += unroll
+        ex.last = self._gbytes
+        self.step += unroll
+        return loss, (out, self._gy)
 
     def close(self):
         """Release the exchange hooks, the watchdog and the own RCCL communicator (collective:

@@ -44,6 +44,33 @@ def test_graph_modes_match_eager(codec):
         assert abs(l[-1] - l_ref[-1]) < 1e-2
 
 
+@pytest.mark.parametrize("extra", [["--compress", "topk_qsgd"],
+                                   ["--compress", "topk_qsgd", "--error-feedback", "--ef-warmup",
+                                    "none"],
+                                   ["--compress", "none", "--optimizer", "adam", "--lr", "0.001"]])
+def test_unrolled_graph_steps_bitwise_single_graph_steps(extra):
+    """Trainer.train_steps(n, U): runs of U steps replayed as one graph (bench --graph-unroll)
+    leave bitwise the parameters and loss of n one-step replays, across an epoch boundary (32
+    batches per epoch: the runs stop before it and single steps cross it)."""
+    from ewdml.runtime import Trainer
+
+    ops.require()
+    flags = LENET + extra + ["--hip-graph", "full"]
+    res = []
+    for unroll in (1, 4):
+        torch.manual_seed(0)
+        tr = Trainer(ewdml.parse_args(flags + ["--max-steps", "60"]))
+        for _ in range(3):
+            tr.train_step()
+        loss, _ = tr.train_steps(38, unroll)
+        torch.cuda.synchronize()
+        assert tr.step == 41 and tr.opt.steps == 41
+        assert (tr._ugraph is not None) == (unroll > 1)
+        res.append((tr.flat.data.clone(), float(loss)))
+    assert torch.equal(res[0][0], res[1][0])
+    assert res[0][1] == res[1][1]
+
+
 @pytest.mark.parametrize("opt", ["adam", "amsgrad"])
 def test_adam_graph_matches_eager(opt):
     """Adam's bias correction follows the step count inside a replayed HIP graph (a device step
