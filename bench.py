@@ -158,13 +158,21 @@ def _measure(a, tr, gw):
     if a.hip_graph != "off" and every > 1:
         # local SGD captures two steps (local, sync): both before the clock starts
         warm = max(warm, every + gw)
-    for _ in range(warm):
+    # --graph-unroll U (when the timed run holds at least one run of U steps): the U-step graph is
+    # captured and replayed once as the last U warmup steps (at least gw + 1 one-step warmup steps
+    # before it: the eager steps and the one-step capture)
+    unroll = a.graph_unroll if 1 < a.graph_unroll <= a.steps else 1
+    single = warm if unroll == 1 else max(gw + 1, warm - unroll)
+    for _ in range(single):
         tr.train_step()
-    # --graph-unroll U: the U-step graph captured and replayed once before the clock starts
-    unroll = a.graph_unroll if tr.prepare_unrolled(a.graph_unroll) else 1
-    if unroll > 1:
+    if unroll > 1 and tr.prepare_unrolled(unroll):
         tr.train_steps(unroll, unroll)
+    else:
+        for _ in range(warm - single):
+            tr.train_step()
+        unroll = 1
     tr.graph_unroll_used = unroll
+    tr.warmup_run = single + (unroll if unroll > 1 else warm - single)
     sync()
     tr.comm.barrier()
     sync()
@@ -235,6 +243,9 @@ def main(argv=None):
         "n_gpus": world,
         "steps": a.steps,
         "warmup": a.warmup,
+        # untimed steps actually run (>= warmup: the eager steps before the graph capture and, with
+        # --graph-unroll, one replay of the U-step graph)
+        "warmup_steps_run": getattr(tr, "warmup_run", a.warmup),
         "ms_per_step": round(ms, 4),
         "higher_is_better": True,
         "scaling": "weak",

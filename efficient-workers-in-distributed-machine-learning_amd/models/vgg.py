@@ -70,15 +70,26 @@ class VGG(nn.Module):
         return self.classifier(f)
 
     def fused_loss(self, x, y):
-        """(mean cross-entropy, logits) with the classifier tail and the loss in one HIP launch
-        each way (``ops/head.py`` ``vgg_loss``), or None where that path does not apply (the
-        caller then runs ``forward`` and its own loss)."""
+        """(mean cross-entropy, logits) with the loss riding in the last Linear's forward launch
+        (``ops/head.py`` ``vgg_head_loss``; opt-in ``EWDML_HEAD_TAIL=1``: the classifier tail and
+        the loss in one launch each way, ``vgg_loss``), or None where neither applies (the caller
+        then runs ``forward`` and its own loss)."""
         if not (x.is_cuda and x.dtype == torch.float32 and fused.active(x)):
             return None
         from ..ops import head as head_ops
 
         if not head_ops._TAIL:
-            return None
+            if not head_ops._HEAD_CE:
+                return None
+            # the loss riding in the last Linear's launch (ops/head.py vgg_head_loss)
+            f = self.features(x).flatten(1)
+            if not head_ops.head_ce_supported(self.classifier, f, y):
+                from ..ops.nn import cross_entropy
+
+                out = head_ops.vgg_head(self.classifier, f) if fused.active(f) else \
+                    self.classifier(f)
+                return cross_entropy(out, y), out.detach()
+            return head_ops.vgg_head_loss(self.classifier, f, y)
 
         probe = torch.empty((x.shape[0], self.classifier[1].in_features), dtype=x.dtype,
                             device=x.device)

@@ -315,6 +315,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_wgrad", &ew_conv_wgrad);
   m.def("conv_stem_fwd", &ew_conv_stem_fwd);
   m.def("head_fwd", &ew_head_fwd);
+  m.def("head_fwd_ce", &ew_head_fwd_ce);
   m.def("head_bwd", &ew_head_bwd);
   m.def("conv_stem_wgrad", &ew_conv_stem_wgrad);
   m.def("rccl_unique_id", [] { return pybind11::bytes(ew_rccl_unique_id()); });

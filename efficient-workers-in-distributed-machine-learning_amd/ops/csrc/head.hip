@@ -99,6 +99,76 @@ __device__ __forceinline__ void hd_wave_reduce(hd_f32x4& acc, float* red, int wv
   }
 }
 
+// Cross-entropy riding in the last Linear's forward (N <= 16 classes: a block's tile holds whole
+// rows): per row log-sum-exp, loss and d(loss)/d(logits) for an upstream 1 (k_ce_fwd's expressions,
+// bit for bit), the per-row losses summed by the grid's last block in k_ce_fwd's order.
+template <typename T>
+struct HdCe {
+  const long long* y;  // labels; null: no cross-entropy
+  float* lossrow;      // [B] scratch
+  float* loss;         // mean loss
+  float* lse;          // [B]
+  T* dlog;             // [B][N] (nullable)
+  int* tick;           // zeroed grid ticket (left zeroed)
+};
+
+// wave 0 of a forward block (16 rows x N <= 16 logits in zq, lane = column li of row group
+// lane >> 4); the grid's last block (a wave-level ticket: the other waves have exited) sums
+// the row losses.
+template <typename T>
+__device__ __forceinline__ void hd_ce_tail(const HdCe<T>& ce, const float (&zq)[4], int B, int N,
+                                           int lane, int n) {
+  const float g1 = 1.0f / (float)B;
+  const int base = lane & ~15;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int rr = blockIdx.x * 16 + 4 * (lane >> 4) + q;
+    const bool valid = rr < B;
+    const float xv = zq[q];
+    float m = -INFINITY;
+    for (int k = 0; k < N; ++k) m = fmaxf(m, __shfl(xv, base + k, 64));
+    float sum = 0.0f;
+    for (int k = 0; k < N; ++k) sum += expf(__shfl(xv, base + k, 64) - m);
+    const float l = m + logf(sum);
+    const long long t = valid ? ce.y[rr] : -1;
+    const bool tin = t >= 0 && t < N;
+    const float xt = __shfl(xv, base + (tin ? (int)t : 0), 64);
+    if (!valid) continue;
+    if (n < N && ce.dlog) {
+      float v = expf(xv - l);
+      if ((long long)n == t) v -= 1.0f;
+      v *= g1;
+      ce.dlog[(long long)rr * N + n] = HdT<T>::st(v);
+    }
+    if ((lane & 15) == 0) {
+      ce.lse[rr] = l;
+      // write-through: the grid's last block reads the row losses in this launch
+      __hip_atomic_store(ce.lossrow + rr, l - (tin ? xt : 0.0f), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  int last = 0;
+  if (lane == 0) {
+    const int G = (int)(gridDim.x * gridDim.y);
+    last = __hip_atomic_fetch_add(ce.tick, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == G - 1;
+    if (last) __hip_atomic_store(ce.tick, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (!__shfl(last, 0, 64)) return;
+  // k_ce_fwd's sum: its wave w (of 16) lane l held rows w * 64 + l + 1024 j; butterfly per wave,
+  // then the 16 wave sums in order
+  float tot = 0.0f;
+  for (int w = 0; w < 16; ++w) {
+    float a = 0.0f;
+    for (int r = w * 64 + lane; r < B; r += 1024)
+      a += __hip_atomic_load(ce.lossrow + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o, 64);
+    tot += __shfl(a, 0, 64);
+  }
+  if (lane == 0) *ce.loss = tot / (float)B;
+}
+
 // ---- forward: z[B][N] = drop_out(act(drop_in(x) w^T + b)), y = pre-activation (optional) ----
 // Block: one 16 x 16 output tile; wave v takes the k-steps v, v + 4, ... (all its loads issued
 // before the first MFMA), the 4 partial tiles are summed through LDS.
@@ -107,7 +177,8 @@ __global__ __launch_bounds__(EW_BLOCK) void k_head_fwd(const T* __restrict__ x,
                                                        const T* __restrict__ w,
                                                        const T* __restrict__ b,
                                                        T* __restrict__ z, T* __restrict__ y, int B,
-                                                       int N, int K, HdDrop din, HdDrop dout) {
+                                                       int N, int K, HdDrop din, HdDrop dout,
+                                                       HdCe<T> ce) {
   using H = HdT<T>;
   typedef typename H::v8 v8;
   __shared__ float red[16 * 64];
@@ -148,21 +219,26 @@ __global__ __launch_bounds__(EW_BLOCK) void k_head_fwd(const T* __restrict__ x,
   }
   hd_wave_reduce(acc, red, wv, lane);
   // C/D layout: column li (output feature), rows 4 (lane >> 4) + q (batch rows)
-  if (wv != 0 || !nok) return;
-  const float bias = b ? H::f(b[n]) : 0.0f;
+  if (wv != 0) return;
+  const float bias = (b && nok) ? H::f(b[n]) : 0.0f;
   const uint32_t kout = hd_key(dout);
   const float sout = hd_scale(dout);
+  float zq[4];  // the stored outputs (the cross-entropy reads them as k_ce_fwd reads the logits)
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int rr = blockIdx.x * 16 + 4 * (lane >> 4) + q;
-    if (rr >= B) continue;
     const long long o = (long long)rr * N + n;
     const T yb = H::st(acc[q] + bias);  // the GEMM's output (bias in fp32)
-    if (y) y[o] = yb;
     float v = H::f(yb);
     if (RELU) v = hd_relu(v);
     if (dout.p > 0.0f) v = v * hd_mask((uint32_t)o, kout, dout.p, sout);
+    zq[q] = H::f(H::st(v));
+    if (rr >= B || !nok) continue;
+    if (y) y[o] = yb;
     z[o] = H::st(v);
+  }
+  if constexpr (!RELU) {
+    if (ce.y) hd_ce_tail<T>(ce, zq, B, N, lane, n);
   }
 }
 
@@ -342,7 +418,7 @@ void ew_head_fwd(uintptr_t x, uintptr_t w, uintptr_t b, uintptr_t z, uintptr_t y
   hipLaunchKernelGGL((k_head_fwd<T, R>), grid, dim3(EW_BLOCK), 0, (hipStream_t)stream,         \
                      reinterpret_cast<const T*>(x), reinterpret_cast<const T*>(w),               \
                      reinterpret_cast<const T*>(b), reinterpret_cast<T*>(z),                     \
-                     reinterpret_cast<T*>(y), B, N, K, din, dout)
+                     reinterpret_cast<T*>(y), B, N, K, din, dout, HdCe<T>{})
   if (is_f32) {
     if (relu) HD_FWD(float, true);
     else HD_FWD(float, false);
@@ -351,6 +427,31 @@ void ew_head_fwd(uintptr_t x, uintptr_t w, uintptr_t b, uintptr_t z, uintptr_t y
     else HD_FWD(uint16_t, false);
   }
 #undef HD_FWD
+  EW_CHECK_LAUNCH();
+}
+
+// The last Linear (no activation, no dropout) with the cross-entropy against labels yl riding in
+// it (HdCe): z = logits, loss, lse [B], dlog [B][N] (nullable), lossrow [B] scratch, tick one
+// zeroed int (left zeroed).  N <= 16.
+void ew_head_fwd_ce(uintptr_t x, uintptr_t w, uintptr_t b, uintptr_t z, int B, int N, int K,
+                    uintptr_t yl, uintptr_t lossrow, uintptr_t loss, uintptr_t lse, uintptr_t dlog,
+                    uintptr_t tick, uintptr_t stream, int is_f32) {
+  if (B <= 0 || N <= 0 || N > 16 || K % 32 || !yl || !lossrow || !loss || !lse || !tick)
+    throw std::runtime_error("ewdml head: the cross-entropy head needs 0 < N <= 16, K % 32 == 0");
+  const HdDrop none{nullptr, 0u, 0.0f};
+  const dim3 grid((B + 15) / 16, 1);
+#define HD_FWD_CE(T)                                                                            \
+  hipLaunchKernelGGL((k_head_fwd<T, false>), grid, dim3(EW_BLOCK), 0, (hipStream_t)stream,      \
+                     reinterpret_cast<const T*>(x), reinterpret_cast<const T*>(w),               \
+                     reinterpret_cast<const T*>(b), reinterpret_cast<T*>(z), nullptr, B, N, K,   \
+                     none, none,                                                                 \
+                     HdCe<T>{reinterpret_cast<const long long*>(yl),                             \
+                             reinterpret_cast<float*>(lossrow), reinterpret_cast<float*>(loss),  \
+                             reinterpret_cast<float*>(lse), reinterpret_cast<T*>(dlog),          \
+                             reinterpret_cast<int*>(tick)})
+  if (is_f32) HD_FWD_CE(float);
+  else HD_FWD_CE(uint16_t);
+#undef HD_FWD_CE
   EW_CHECK_LAUNCH();
 }
 

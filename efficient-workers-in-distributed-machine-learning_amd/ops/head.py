@@ -120,6 +120,65 @@ class _HeadLinear(torch.autograd.Function):
         return dx, (dw if need[1] else None), (db if need[2] else None), None, None, None, None
 
 
+class _HeadLinearCE(torch.autograd.Function):
+    """(mean cross-entropy, logits) of ``x W^T + b`` against ``y``: the cross-entropy rides in the
+    Linear's forward launch (ops/csrc/head.hip HdCe, <= 16 classes), d(loss)/d(logits) for the
+    trainer's unit seed written there too (as ``ops.nn.cross_entropy``), so the backward is the
+    Linear's one launch."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, y):
+        from .nn import _unit_seed
+
+        C_ = require()
+        B, K = x.shape
+        N = w.shape[0]
+        dev = x.device
+        z = torch.empty((B, N), dtype=x.dtype, device=dev)
+        f32 = dict(dtype=torch.float32, device=dev)
+        loss = torch.empty((), **f32)
+        lse = torch.empty(B, **f32)
+        lossrow = torch.empty(B, **f32)
+        want = torch.is_grad_enabled() and _unit_seed() is not None
+        dlog = torch.empty_like(z) if want else None
+        tick = _ctr(_HeadLinearCE, dev)[2:3]  # word 2: free in the counter layout (_CTR_INTS)
+        C_.head_fwd_ce(_ptr(x), _ptr(w), _ptr(b), _ptr(z), B, N, K, _ptr(y), _ptr(lossrow),
+                       _ptr(loss), _ptr(lse), _ptr(dlog), _ptr(tick), _stream(),
+                       int(x.dtype == torch.float32))
+        ctx.save_for_backward(x, w, z, y, lse)
+        ctx.dlog = dlog
+        ctx.mark_non_differentiable(z)
+        ctx.set_materialize_grads(False)
+        return loss, z
+
+    @staticmethod
+    def backward(ctx, gloss, _gz):
+        from .nn import _unit_seed
+
+        C_ = require()
+        x, w, z, y, lse = ctx.saved_tensors
+        dlog, ctx.dlog = ctx.dlog, None
+        B, K = x.shape
+        N = w.shape[0]
+        need = ctx.needs_input_grad
+        if gloss is None:
+            return None, None, None, None
+        seed = _unit_seed()
+        if not (dlog is not None and seed is not None and gloss.numel() == 1
+                and gloss.dtype == torch.float32 and gloss.data_ptr() == seed.data_ptr()):
+            dlog = torch.empty_like(z)
+            g = gloss.detach().float().contiguous()
+            C_.cross_entropy_bwd(_ptr(z), _ptr(y), _ptr(lse), _ptr(g), B, N,
+                                 int(z.dtype == torch.bfloat16), _ptr(dlog), _stream())
+        dx = torch.empty_like(x) if need[0] else None
+        dw = torch.empty_like(w)
+        db = torch.empty(N, dtype=w.dtype, device=w.device)
+        C_.head_bwd(_ptr(dlog), 0, _ptr(x), _ptr(w), _ptr(dx), _ptr(dw), _ptr(db),
+                    int(db.dtype == torch.bfloat16), B, N, K, 0, 0, 0, 0.0, 0, 0, 0.0, 1,
+                    _stream(), int(x.dtype == torch.float32))
+        return dx, (dw if need[1] else None), (db if need[2] else None), None
+
+
 def head_linear(x, lin, relu=False, din=None, dout=None, advance=True):
     """``drop_out(act(lin(drop_in(x))))`` through the head kernels; ``din`` / ``dout``: dropout
     specs ``(counter, salt, p)`` (see :func:`_ctr`) or None."""
@@ -250,6 +309,31 @@ def vgg_loss(cls, x, y):
     dev = x.device
     h1 = head_linear(x, l1, relu=True, din=_spec(d0, dev, 0), dout=_spec(d1, dev, 1))
     return _HeadTail.apply(h1, y, l2.weight, l2.bias, l3.weight, l3.bias)
+
+
+# the cross-entropy riding in the last Linear's forward launch (_HeadLinearCE), opt-in
+# (EWDML_HEAD_CE=1): one launch fewer, but the step is unchanged (VGG-11 1.1691 / 1.1714 vs
+# 1.1684 / 1.1667 ms, profiles/ab/README.md): the row losses' ticket chain takes about what the
+# separate cross-entropy launch took
+_HEAD_CE = os.environ.get("EWDML_HEAD_CE", "0") == "1"
+
+
+def head_ce_supported(cls, x, y) -> bool:
+    """VGG's classifier with the loss riding in its last Linear applies: head layout, <= 16
+    classes, int64 labels, no autocast."""
+    return (_HEAD_CE and supported(cls, x) and y is not None and y.dtype == torch.int64
+            and y.dim() == 1 and y.shape[0] == x.shape[0] and y.is_contiguous()
+            and 0 < cls[6].out_features <= 16 and not torch.is_autocast_enabled("cuda"))
+
+
+def vgg_head_loss(cls, x, y):
+    """(mean cross-entropy, logits) of VGG's classifier on ``x``: head.hip's kernels, the loss in
+    the last Linear's launch."""
+    d0, l1, _, d1, l2, _, l3 = list(cls)
+    dev = x.device
+    h = head_linear(x, l1, relu=True, din=_spec(d0, dev, 0), dout=_spec(d1, dev, 1))
+    h = head_linear(h, l2, relu=True)
+    return _HeadLinearCE.apply(h, l3.weight, l3.bias, y)
 
 
 def vgg_head(cls, x):
