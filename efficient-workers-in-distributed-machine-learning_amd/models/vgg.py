@@ -62,11 +62,13 @@ class VGG(nn.Module):
                 m.bias.data.zero_()
 
     def forward(self, x):
-        f = self.features(x).flatten(1)
+        feat = self.features(x)
+        f = feat.flatten(1)
         if fused.active(f):  # hipBLASLt GEMMs + fused activation/dropout kernels (ops/head.py)
             from ..ops.head import vgg_head
 
-            return vgg_head(self.classifier, f)
+            # the last BN layer's backward may ride in the first Linear's (ops/head.py)
+            return vgg_head(self.classifier, f, getattr(feat, "_ew_bn_node", None))
         return self.classifier(f)
 
     def fused_loss(self, x, y):
@@ -82,14 +84,16 @@ class VGG(nn.Module):
             if not head_ops._HEAD_CE:
                 return None
             # the loss riding in the last Linear's launch (ops/head.py vgg_head_loss)
-            f = self.features(x).flatten(1)
+            feat = self.features(x)
+            f = feat.flatten(1)
+            node = getattr(feat, "_ew_bn_node", None)
             if not head_ops.head_ce_supported(self.classifier, f, y):
                 from ..ops.nn import cross_entropy
 
-                out = head_ops.vgg_head(self.classifier, f) if fused.active(f) else \
+                out = head_ops.vgg_head(self.classifier, f, node) if fused.active(f) else \
                     self.classifier(f)
                 return cross_entropy(out, y), out.detach()
-            return head_ops.vgg_head_loss(self.classifier, f, y)
+            return head_ops.vgg_head_loss(self.classifier, f, y, node)
 
         probe = torch.empty((x.shape[0], self.classifier[1].in_features), dtype=x.dtype,
                             device=x.device)

@@ -485,15 +485,12 @@ def _arm_fin(job):
     weight-gradient GEMM launch; returns its outputs (coef, dgamma, dbeta, dcbias)."""
     if job is None:
         return None
+    from .nn import bn_fin_outputs
+
     node, part, rows, h, stats = job
-    need = node.needs_input_grad
     Cb = h.shape[1]
-    dev = h.device
-    coef = torch.empty(2 * Cb, dtype=torch.float32, device=dev)
+    coef, dg, db, dcb = bn_fin_outputs(node, Cb, h.device)
     cb_dtype = getattr(node, "cb_dtype", None)
-    dcb = torch.empty(Cb, dtype=cb_dtype, device=dev) if need[2] and cb_dtype else None
-    dg = torch.empty(Cb, dtype=torch.float32, device=dev) if need[3] else None
-    db = torch.empty(Cb, dtype=torch.float32, device=dev) if need[4] else None
     M = h.shape[0] * h.shape[2] * h.shape[3]
     require().cf_arm_bn_fin(_ptr(part), int(rows), Cb, M, _ptr(stats), _ptr(coef), _ptr(dg),
                             _ptr(db), _ptr(dcb), int(cb_dtype == torch.bfloat16))

@@ -317,6 +317,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("head_fwd", &ew_head_fwd);
   m.def("head_fwd_ce", &ew_head_fwd_ce);
   m.def("head_bwd", &ew_head_bwd);
+  m.def("head_bwd_bn", &ew_head_bwd_bn);
   m.def("conv_stem_wgrad", &ew_conv_stem_wgrad);
   m.def("rccl_unique_id", [] { return pybind11::bytes(ew_rccl_unique_id()); });
   m.def("rccl_version", &ew_rccl_version);

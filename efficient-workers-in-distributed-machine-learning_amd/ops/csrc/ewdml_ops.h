@@ -221,6 +221,13 @@ void ew_head_fwd(uintptr_t x, uintptr_t w, uintptr_t b, uintptr_t z, uintptr_t y
 void ew_head_fwd_ce(uintptr_t x, uintptr_t w, uintptr_t b, uintptr_t z, int B, int N, int K,
                     uintptr_t yl, uintptr_t lossrow, uintptr_t loss, uintptr_t lse, uintptr_t dlog,
                     uintptr_t tick, uintptr_t stream, int is_f32);
+void ew_head_bwd_bn(uintptr_t dz, uintptr_t y, uintptr_t x, uintptr_t w, uintptr_t dx,
+                    uintptr_t dw, uintptr_t db, int B, int N, int K, int relu, uintptr_t ctr_out,
+                    uint32_t salt_out, float p_out, uintptr_t ctr_in, uint32_t salt_in,
+                    float p_in, int advance, uintptr_t bn_h, uintptr_t bn_code,
+                    uintptr_t bn_stats, uintptr_t bn_coef, uintptr_t bn_dgamma,
+                    uintptr_t bn_dbeta, uintptr_t bn_dcbias, int bn_cb_bf16, uintptr_t bn_tick,
+                    uintptr_t stream);
 void ew_head_bwd(uintptr_t dz, uintptr_t y, uintptr_t x, uintptr_t w, uintptr_t dx, uintptr_t dw,
                  uintptr_t db, int db_bf16, int B, int N, int K, int relu, uintptr_t ctr_out,
                  uint32_t salt_out, float p_out, uintptr_t ctr_in, uint32_t salt_in, float p_in,

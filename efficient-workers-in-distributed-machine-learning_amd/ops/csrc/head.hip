@@ -252,6 +252,86 @@ __device__ __forceinline__ float hd_dyv(T dzv, T yv, uint32_t o, uint32_t kout,
   return HdT<T>::rnd(v);
 }
 
+// The backward statistics and finalisation of the BatchNorm + ReLU + 2x2 max pool layer (2x2 maps
+// pooled to 1x1: VGG's last conv block) whose flattened output is this Linear's input, riding in
+// the input-gradient blocks: each channel tile's last row tile (a ticket per tile) sums, for its
+// 16 channels over all rows, dz = dx at the pool's argmax where its ReLU passed, dz * (h - mean)
+// and h - mean (the three sums of nn.hip k_bn_bwd_stats), then forms k_bn_bwd_finalize's outputs.
+// fp32 only.
+struct HdBnB {
+  const float* h;        // [B][2][2][K] BN input (null: none)
+  const uint8_t* code;   // [B][K] pool window codes
+  const float* stats;    // [4][K] mean, invstd, scale, shift
+  float* coef;           // [2][K]
+  float* dgamma;         // nullable
+  float* dbeta;          // nullable
+  void* dcbias;          // nullable
+  int cb_bf16;
+  int* tick;             // [K / 16] zeroed tickets (left zeroed)
+};
+
+__device__ __forceinline__ void hd_bn_tile(const HdBnB& bn, const float* dx, int B, int K, int tk,
+                                           double* red) {
+  const int t = threadIdx.x, li = t & 15, sl = t >> 4, lane = t & 63, wv = t >> 6;
+  const int c = tk * 16 + li;
+  const bool cok = c < K;
+  const int cc = cok ? c : K - 1;
+  const float mean = bn.stats[cc], sc = bn.stats[2 * K + cc], sh = bn.stats[3 * K + cc];
+  float s1 = 0.0f, s2 = 0.0f, s3 = 0.0f;
+  for (int r0 = sl; r0 < B; r0 += 16 * 4) {  // 4 rows in flight per thread
+    float d[4], x[4][4];
+    uint8_t k[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int r = min(r0 + 16 * u, B - 1);
+      d[u] = __hip_atomic_load(const_cast<float*>(dx) + (long long)r * K + cc, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+      k[u] = bn.code[(long long)r * K + cc];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) x[u][q] = bn.h[((long long)r * 4 + q) * K + cc];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (r0 + 16 * u >= B) continue;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float dz = (k[u] == q && hd_relu_pass(x[u][q] * sc + sh)) ? d[u] : 0.0f;
+        const float xc = x[u][q] - mean;
+        s1 += dz;
+        s2 += dz * xc;
+        s3 += xc;
+      }
+    }
+  }
+  double a[3] = {s1, s2, s3};
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    a[i] += __shfl_xor(a[i], 16, 64);
+    a[i] += __shfl_xor(a[i], 32, 64);
+    if (lane < 16) red[(i * 4 + wv) * 16 + lane] = a[i];
+  }
+  __syncthreads();
+  if (t >= 16 || !cok) return;
+  double sum[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+    sum[i] = (red[(i * 4) * 16 + t] + red[(i * 4 + 1) * 16 + t]) +
+             (red[(i * 4 + 2) * 16 + t] + red[(i * 4 + 3) * 16 + t]);
+  const double M = 4.0 * B;
+  const double invstd = bn.stats[K + c], scale = sc;
+  const double db = sum[0], dg = sum[1] * invstd;
+  const double e = -scale * invstd * dg / M;
+  bn.coef[c] = (float)e;
+  bn.coef[K + c] = (float)(-scale * db / M);
+  if (bn.dgamma) bn.dgamma[c] = (float)dg;
+  if (bn.dbeta) bn.dbeta[c] = (float)db;
+  if (bn.dcbias) {
+    const float v = (float)(e * sum[2]);
+    if (bn.cb_bf16) reinterpret_cast<uint16_t*>(bn.dcbias)[c] = ew_f2bf(v);
+    else reinterpret_cast<float*>(bn.dcbias)[c] = v;
+  }
+}
+
 // ---- backward: blocks [0, nbw) 16 x 16 weight-gradient tiles (+ bias gradient), the rest
 // 16 x 16 input-gradient tiles; in both, wave v takes a quarter of the reduction ----
 template <typename T, bool RELU>
@@ -259,7 +339,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_head_bwd(
     const T* __restrict__ dz, const T* __restrict__ y, const T* __restrict__ x,
     const T* __restrict__ w, T* __restrict__ dx, T* __restrict__ dw, void* __restrict__ db,
     int db_bf16, int B, int N, int K, HdDrop dout, HdDrop din, int nbw, int* __restrict__ adv0,
-    int* __restrict__ adv1) {
+    int* __restrict__ adv1, HdBnB bn) {
   using H = HdT<T>;
   typedef typename H::v8 v8;
   __shared__ float red[16 * 64];
@@ -381,7 +461,30 @@ __global__ __launch_bounds__(EW_BLOCK) void k_head_bwd(
         const long long o = (long long)rr * K + k;
         float v = acc[q];
         if (din.p > 0.0f) v = v * hd_mask((uint32_t)o, kin, din.p, sin);
+        if constexpr (sizeof(T) == 4) {
+          if (bn.h) {  // write-through: the tile's last row block reads it in this launch
+            __hip_atomic_store(reinterpret_cast<float*>(dx) + o, v, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            continue;
+          }
+        }
         dx[o] = H::st(v);
+      }
+    }
+    if constexpr (sizeof(T) == 4) {
+      if (bn.h) {
+        __shared__ int last;
+        __shared__ double bred[3 * 4 * 16];
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+          const int prev =
+              __hip_atomic_fetch_add(bn.tick + tk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          last = prev == b16 - 1;
+          if (last) __hip_atomic_store(bn.tick + tk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
+        if (last) hd_bn_tile(bn, reinterpret_cast<const float*>(dx), B, K, tk, bred);
       }
     }
   }
@@ -455,10 +558,10 @@ void ew_head_fwd_ce(uintptr_t x, uintptr_t w, uintptr_t b, uintptr_t z, int B, i
   EW_CHECK_LAUNCH();
 }
 
-void ew_head_bwd(uintptr_t dz, uintptr_t y, uintptr_t x, uintptr_t w, uintptr_t dx, uintptr_t dw,
-                 uintptr_t db, int db_bf16, int B, int N, int K, int relu, uintptr_t ctr_out,
-                 uint32_t salt_out, float p_out, uintptr_t ctr_in, uint32_t salt_in, float p_in,
-                 int advance, uintptr_t stream, int is_f32) {
+static void hd_bwd(uintptr_t dz, uintptr_t y, uintptr_t x, uintptr_t w, uintptr_t dx, uintptr_t dw,
+                   uintptr_t db, int db_bf16, int B, int N, int K, int relu, uintptr_t ctr_out,
+                   uint32_t salt_out, float p_out, uintptr_t ctr_in, uint32_t salt_in, float p_in,
+                   int advance, uintptr_t stream, int is_f32, const HdBnB& bn) {
   if (B <= 0 || N <= 0 || K % 32)
     throw std::runtime_error("ewdml head: needs B, N > 0 and K % 32 == 0");
   if (relu && !y) throw std::runtime_error("ewdml head: ReLU backward needs the pre-activation");
@@ -479,7 +582,7 @@ void ew_head_bwd(uintptr_t dz, uintptr_t y, uintptr_t x, uintptr_t w, uintptr_t 
                      reinterpret_cast<const T*>(dz), reinterpret_cast<const T*>(y),              \
                      reinterpret_cast<const T*>(x), reinterpret_cast<const T*>(w),               \
                      reinterpret_cast<T*>(dx), reinterpret_cast<T*>(dw),                         \
-                     reinterpret_cast<void*>(db), db_bf16, B, N, K, dout, din, nbw, a0, a1)
+                     reinterpret_cast<void*>(db), db_bf16, B, N, K, dout, din, nbw, a0, a1, bn)
   if (is_f32) {
     if (relu) HD_BWD(float, true);
     else HD_BWD(float, false);
@@ -489,4 +592,33 @@ void ew_head_bwd(uintptr_t dz, uintptr_t y, uintptr_t x, uintptr_t w, uintptr_t 
   }
 #undef HD_BWD
   EW_CHECK_LAUNCH();
+}
+
+void ew_head_bwd(uintptr_t dz, uintptr_t y, uintptr_t x, uintptr_t w, uintptr_t dx, uintptr_t dw,
+                 uintptr_t db, int db_bf16, int B, int N, int K, int relu, uintptr_t ctr_out,
+                 uint32_t salt_out, float p_out, uintptr_t ctr_in, uint32_t salt_in, float p_in,
+                 int advance, uintptr_t stream, int is_f32) {
+  hd_bwd(dz, y, x, w, dx, dw, db, db_bf16, B, N, K, relu, ctr_out, salt_out, p_out, ctr_in, salt_in,
+         p_in, advance, stream, is_f32, HdBnB{});
+}
+
+// ew_head_bwd (fp32) whose input x is the flattened output of a BatchNorm + ReLU + 2x2 max pool
+// layer over 2x2 maps (bn_h [B][2][2][K], bn_code [B][K], bn_stats [4][K]): that layer's backward
+// statistics and finalisation (coef [2][K], dgamma, dbeta, dcbias: k_bn_bwd_finalize's outputs)
+// ride in the input-gradient blocks (HdBnB); bn_tick: K / 16 zeroed ints (left zeroed).
+void ew_head_bwd_bn(uintptr_t dz, uintptr_t y, uintptr_t x, uintptr_t w, uintptr_t dx,
+                    uintptr_t dw, uintptr_t db, int B, int N, int K, int relu, uintptr_t ctr_out,
+                    uint32_t salt_out, float p_out, uintptr_t ctr_in, uint32_t salt_in,
+                    float p_in, int advance, uintptr_t bn_h, uintptr_t bn_code,
+                    uintptr_t bn_stats, uintptr_t bn_coef, uintptr_t bn_dgamma,
+                    uintptr_t bn_dbeta, uintptr_t bn_dcbias, int bn_cb_bf16, uintptr_t bn_tick,
+                    uintptr_t stream) {
+  if (!dx || !bn_h || !bn_code || !bn_stats || !bn_coef || !bn_tick || K % 16)
+    throw std::runtime_error("ewdml head: the BN backward rider needs dx, h, code, stats, coef");
+  const HdBnB bn{reinterpret_cast<const float*>(bn_h), reinterpret_cast<const uint8_t*>(bn_code),
+                 reinterpret_cast<const float*>(bn_stats), reinterpret_cast<float*>(bn_coef),
+                 reinterpret_cast<float*>(bn_dgamma), reinterpret_cast<float*>(bn_dbeta),
+                 reinterpret_cast<void*>(bn_dcbias), bn_cb_bf16, reinterpret_cast<int*>(bn_tick)};
+  hd_bwd(dz, y, x, w, dx, dw, db, 0, B, N, K, relu, ctr_out, salt_out, p_out, ctr_in, salt_in, p_in,
+         advance, stream, 1, bn);
 }

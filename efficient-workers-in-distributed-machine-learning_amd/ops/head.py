@@ -88,7 +88,7 @@ class _HeadLinear(torch.autograd.Function):
     ``advance``."""
 
     @staticmethod
-    def forward(ctx, x, w, b, relu, din, dout, advance):
+    def forward(ctx, x, w, b, relu, din, dout, advance, bn_node=None):
         C_ = require()
         B, K = x.shape
         N = w.shape[0]
@@ -97,6 +97,7 @@ class _HeadLinear(torch.autograd.Function):
         C_.head_fwd(_ptr(x), _ptr(w), _ptr(b), _ptr(z), _ptr(y), B, N, K, int(relu),
                     *_drop_args(din), *_drop_args(dout), _stream(), int(x.dtype == torch.float32))
         ctx.relu, ctx.din, ctx.dout, ctx.advance = relu, din, dout, advance
+        ctx.bn_node = bn_node
         ctx.save_for_backward(x, w, y)
         return z
 
@@ -113,11 +114,32 @@ class _HeadLinear(torch.autograd.Function):
         dx = torch.empty_like(x) if need[0] else None
         dw = torch.empty_like(w)
         db = torch.empty(N, dtype=w.dtype, device=w.device)
-        C_.head_bwd(_ptr(dz), _ptr(y), _ptr(x), _ptr(w), _ptr(dx), _ptr(dw), _ptr(db),
-                    int(db.dtype == torch.bfloat16), B, N, K, int(ctx.relu),
-                    *_drop_args(ctx.dout), *_drop_args(ctx.din), int(ctx.advance), _stream(),
-                    int(x.dtype == torch.float32))
-        return dx, (dw if need[1] else None), (db if need[2] else None), None, None, None, None
+        node, ctx.bn_node = ctx.bn_node, None
+        link = _head_bn_link(node, x) if (dx is not None and db.dtype == torch.float32) else None
+        if link is None:
+            C_.head_bwd(_ptr(dz), _ptr(y), _ptr(x), _ptr(w), _ptr(dx), _ptr(dw), _ptr(db),
+                        int(db.dtype == torch.bfloat16), B, N, K, int(ctx.relu),
+                        *_drop_args(ctx.dout), *_drop_args(ctx.din), int(ctx.advance), _stream(),
+                        int(x.dtype == torch.float32))
+        else:
+            # the backward statistics + finalisation of the BN layer x comes from ride in the
+            # input-gradient blocks; its backward then only applies (ops/nn.py _BNAct)
+            from .nn import bn_fin_outputs
+
+            h, code, stats = link
+            fin = bn_fin_outputs(node, K, x.device)
+            coef, dgm, dbt, dcb = fin
+            cb_dtype = getattr(node, "cb_dtype", None)
+            C_.head_bwd_bn(_ptr(dz), _ptr(y), _ptr(x), _ptr(w), _ptr(dx), _ptr(dw), _ptr(db), B, N,
+                           K, int(ctx.relu), *_drop_args(ctx.dout), *_drop_args(ctx.din),
+                           int(ctx.advance), _ptr(h), _ptr(code), _ptr(stats), _ptr(coef),
+                           _ptr(dgm), _ptr(dbt), _ptr(dcb), int(cb_dtype == torch.bfloat16),
+                           _ptr(_bn_ticks(x.device, K)), _stream())
+            node._ew_pre_bwd = (None, 0, dx, dx._version, fin)
+            global BN_RIDES
+            BN_RIDES += 1
+        return (dx, (dw if need[1] else None), (db if need[2] else None), None, None, None, None,
+                None)
 
 
 class _HeadLinearCE(torch.autograd.Function):
@@ -179,10 +201,45 @@ class _HeadLinearCE(torch.autograd.Function):
         return dx, (dw if need[1] else None), (db if need[2] else None), None
 
 
-def head_linear(x, lin, relu=False, din=None, dout=None, advance=True):
+# the backward of the BN + ReLU + 2x2-pool layer feeding the head (VGG's last conv block) riding in
+# the first Linear's input-gradient launch (ops/csrc/head.hip HdBnB); EWDML_HEAD_BN=0: its own
+# statistics + finalize launches
+_HEAD_BN = os.environ.get("EWDML_HEAD_BN", "1") != "0"
+BN_RIDES = 0  # head backward launches that formed the BN layer's finalisation (tests)
+_BN_TICKS = {}
+
+
+def _bn_ticks(device, K):
+    t = _BN_TICKS.get((device.index, K))
+    if t is None:
+        t = _BN_TICKS[(device.index, K)] = torch.zeros(max(1, K // 16), dtype=torch.int32,
+                                                       device=device)
+    return t
+
+
+def _head_bn_link(node, x):
+    """(h, code, stats) of the fused BN layer ``node`` (``ops.nn.bn_act`` ctx) whose pooled 1x1
+    output, flattened, is ``x`` -- a BN + ReLU + 2x2 max pool over 2x2 maps, fp32 -- or None."""
+    if node is None or not _HEAD_BN or x.dtype != torch.float32:
+        return None
+    try:
+        h, res, code, stats = node.saved_tensors
+    except RuntimeError:  # already freed
+        return None
+    B, K = x.shape
+    if not (node.pool and node.mode == "relu" and res is None and code is not None
+            and h.dtype == torch.float32 and tuple(h.shape) == (B, K, 2, 2)
+            and h.is_contiguous(memory_format=torch.channels_last) and K % 16 == 0):
+        return None
+    return h, code, stats
+
+
+def head_linear(x, lin, relu=False, din=None, dout=None, advance=True, bn_node=None):
     """``drop_out(act(lin(drop_in(x))))`` through the head kernels; ``din`` / ``dout``: dropout
-    specs ``(counter, salt, p)`` (see :func:`_ctr`) or None."""
-    return _HeadLinear.apply(x, lin.weight, lin.bias, bool(relu), din, dout, bool(advance))
+    specs ``(counter, salt, p)`` (see :func:`_ctr`) or None; ``bn_node``: the ``_BNAct`` node of
+    the BN layer ``x`` is the flattened output of (its backward may ride in this one's)."""
+    return _HeadLinear.apply(x, lin.weight, lin.bias, bool(relu), din, dout, bool(advance),
+                             bn_node)
 
 
 def _head_layout(cls):
@@ -326,22 +383,25 @@ def head_ce_supported(cls, x, y) -> bool:
             and 0 < cls[6].out_features <= 16 and not torch.is_autocast_enabled("cuda"))
 
 
-def vgg_head_loss(cls, x, y):
+def vgg_head_loss(cls, x, y, bn_node=None):
     """(mean cross-entropy, logits) of VGG's classifier on ``x``: head.hip's kernels, the loss in
     the last Linear's launch."""
     d0, l1, _, d1, l2, _, l3 = list(cls)
     dev = x.device
-    h = head_linear(x, l1, relu=True, din=_spec(d0, dev, 0), dout=_spec(d1, dev, 1))
+    h = head_linear(x, l1, relu=True, din=_spec(d0, dev, 0), dout=_spec(d1, dev, 1),
+                    bn_node=bn_node)
     h = head_linear(h, l2, relu=True)
     return _HeadLinearCE.apply(h, l3.weight, l3.bias, y)
 
 
-def vgg_head(cls, x):
-    """``cls(x)`` for VGG's classifier ``nn.Sequential`` through the fused kernels."""
+def vgg_head(cls, x, bn_node=None):
+    """``cls(x)`` for VGG's classifier ``nn.Sequential`` through the fused kernels; ``bn_node``:
+    see :func:`head_linear`."""
     if not supported(cls, x):
         return cls(x)
     d0, l1, _, d1, l2, _, l3 = list(cls)
     dev = x.device
-    h = head_linear(x, l1, relu=True, din=_spec(d0, dev, 0), dout=_spec(d1, dev, 1))
+    h = head_linear(x, l1, relu=True, din=_spec(d0, dev, 0), dout=_spec(d1, dev, 1),
+                    bn_node=bn_node)
     h = head_linear(h, l2, relu=True)
     return head_linear(h, l3)

@@ -139,7 +139,10 @@ class _BNAct(torch.autograd.Function):
         ctx._ew_pre_bwd = None
         part, pre_rows = _part(dev), 0
         done = False  # coef / dgamma / dbeta already made by the conv's weight-gradient launch
-        if pre is not None and pre[2] is dy_in and dy_in._version == pre[3]:
+        # (the same storage and version: a flatten between the producer and this layer makes
+        # dy a view of the tensor the producer wrote)
+        if (pre is not None and dy_in.data_ptr() == pre[2].data_ptr()
+                and dy_in.numel() == pre[2].numel() and dy_in._version == pre[3]):
             part, pre_rows = pre[0], pre[1]
             global PRE_BWD_USED
             PRE_BWD_USED += 1
@@ -163,6 +166,19 @@ class _BNAct(torch.autograd.Function):
         if sink is not None and not sink.taken:  # to the block's first conv (ops/conv)
             sink.grad, dres = dres, None
         return dx, dres, dcb, dg, db, None, None, None, None, None, None, None, None, None, None
+
+
+def bn_fin_outputs(node, C, device):
+    """(coef, dgamma, dbeta, dcbias) buffers of the BN layer whose backward autograd node (the
+    ``_BNAct`` ctx) is ``node``, for a producer that forms its backward finalisation (ops/conv.py
+    _arm_fin, ops/head.py): allocated as that backward would, for the gradients it needs."""
+    need = node.needs_input_grad
+    coef = torch.empty(2 * C, dtype=torch.float32, device=device)
+    cb_dtype = getattr(node, "cb_dtype", None)
+    dcb = torch.empty(C, dtype=cb_dtype, device=device) if need[2] and cb_dtype else None
+    dg = torch.empty(C, dtype=torch.float32, device=device) if need[3] else None
+    db = torch.empty(C, dtype=torch.float32, device=device) if need[4] else None
+    return coef, dg, db, dcb
 
 
 def _apply_eval(h, stats, pool, mode="relu", res=None):

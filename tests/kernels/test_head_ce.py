@@ -80,3 +80,45 @@ def test_vgg_trainer_step_runs_head_ce():
         head._HEAD_CE = saved
     assert len(calls) == 3
     assert all(v == v for v in losses)
+
+
+@pytest.mark.parametrize("B", [128, 64])
+@pytest.mark.parametrize("cbias", [False, True])
+def test_bn_backward_rides_in_head_input_gradient(B, cbias):
+    """The backward statistics + finalisation of the BN + ReLU + 2x2 pool layer feeding VGG's
+    classifier, formed in the first Linear's input-gradient blocks (ops/csrc/head.hip HdBnB),
+    against its own statistics + finalize launches (EWDML_HEAD_BN=0): the same gradients up to
+    the order of the fp32 sums."""
+    from ewdml.ops import head
+    from ewdml.ops import nn as fnn
+
+    cls0 = _cls(torch.float32, seed=7)
+    cls0.train()
+    bn0 = torch.nn.BatchNorm2d(512).cuda()
+    with torch.no_grad():
+        bn0.weight.uniform_(0.5, 1.5)
+        bn0.bias.uniform_(-0.3, 0.3)
+    h0 = torch.randn(B, 512, 2, 2, device="cuda").contiguous(memory_format=torch.channels_last)
+    cb0 = torch.randn(512, device="cuda") * 0.1
+    g = torch.randn(B, 10, device="cuda")
+    res = []
+    saved = head._HEAD_BN
+    try:
+        for on in (True, False):
+            head._HEAD_BN = on
+            rides, used = head.BN_RIDES, fnn.PRE_BWD_USED
+            cls, bn = copy.deepcopy(cls0), copy.deepcopy(bn0)
+            h = h0.clone().requires_grad_(True)
+            cb = cb0.clone().requires_grad_(True) if cbias else None
+            feat = fnn.bn_act(h, bn, "relu", pool=True, cbias=cb)
+            out = head.vgg_head(cls, feat.flatten(1), getattr(feat, "_ew_bn_node", None))
+            out.backward(g)
+            assert (head.BN_RIDES > rides) == on and (fnn.PRE_BWD_USED > used) == on
+            # (a conv bias feeding BN has an exact gradient of 0: its fp32 value is rounding
+            # noise, no comparison)
+            res.append([h.grad, bn.weight.grad, bn.bias.grad] + [p.grad for p in cls.parameters()])
+    finally:
+        head._HEAD_BN = saved
+    for a, b in zip(*res):
+        a, b = a.double(), b.double()
+        assert float((a - b).norm() / (b.norm() + 1e-30)) < 1e-5
