@@ -750,14 +750,30 @@ class _Conv(torch.autograd.Function):
         oh, odn, ocode, ostats, ocoef, opool = lazy if lazy is not None else (None,) * 6
         bh, bstats = xsrc if xsrc is not None else (None, None)
         slab, cnt = _sm_ws(x.device, N, C, Nc)
+        # the BN layer's backward finalisation by each channel tile's last row tile of this launch
+        # (the weight-gradient tiles run beside it; ops/csrc/smallmap_f32.hip k_sm_bwd)
+        fin = None
+        if link is not None and _FIN_RIDE:
+            from .nn import bn_fin_outputs
+
+            fin = bn_fin_outputs(node, C, x.device)
+        coef, fdg, fdb, fdcb = fin if fin is not None else (None,) * 4
+        cb_dtype = getattr(node, "cb_dtype", None) if node is not None else None
         rows = C_.sm_f32_bwd(_ptr(x) if xsrc is None else 0, _ptr(bh), _ptr(bstats),
                              _ptr(dy) if lazy is None else 0, _ptr(oh), _ptr(odn), _ptr(ocode),
                              _ptr(ostats), _ptr(ocoef), int(bool(opool)), _ptr(w), _ptr(dx),
                              _ptr(dw), _ptr(slab), slab.numel(), _ptr(cnt), cnt.numel(), N, C,
                              Nc, _ptr(ph), _ptr(pres), _ptr(pcode), _ptr(pstats), int(prelu or 0),
-                             _ptr(part), part.numel() if part is not None else 0, _stream())
+                             _ptr(part), part.numel() if part is not None else 0, _ptr(coef),
+                             _ptr(fdg), _ptr(fdb), _ptr(fdcb), int(cb_dtype == torch.bfloat16),
+                             ph.shape[0] * ph.shape[2] * ph.shape[3] if ph is not None else 0,
+                             _stream())
         if rows > 0:
             node._ew_pre_bwd = (part, rows, dx, dx._version)
+            if fin is not None:
+                global FIN_RIDES
+                FIN_RIDES += 1
+                node._ew_pre_bwd += (fin,)
         return dx, dw, None, None
 
 

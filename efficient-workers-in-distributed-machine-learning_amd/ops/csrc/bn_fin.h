@@ -105,3 +105,67 @@ __device__ __forceinline__ void ew_bn_bwd_fin_group(const EwBnFin& f, int grp, d
     else reinterpret_cast<float*>(f.dcbias)[c] = v;
   }
 }
+
+// ew_bn_bwd_fin_group's sums for one channel c in one thread, in exactly the group's order (the
+// 16 row slices' sums in row order, the xor-16 / xor-32 pairs of each wave, then the 4 waves in
+// order): bitwise the same outputs, for a producer whose last block finalises a few channels
+// itself.  SC1: the partials were written in this launch by other blocks (write-through), read
+// with agent-scope loads.
+template <bool SC1>
+__device__ __forceinline__ float ew_fin_ld(const float* p) {
+  return SC1 ? __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+             : *p;
+}
+
+template <int NS, bool SC1>
+__device__ __forceinline__ void ew_bn_bwd_fin_chan(const EwBnFin& f, int c) {
+  const int C = f.C;
+  double sums[3] = {0.0, 0.0, 0.0};
+  // up to 16 partial rows (one per row slice): every load issued before the first add
+  float r16[NS][16];
+  if (f.nblk <= 16) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+      for (int b = 0; b < 16; ++b)
+        r16[s][b] = ew_fin_ld<SC1>(f.part + ((long long)s * f.nblk + min(b, f.nblk - 1)) * C + c);
+  }
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    double w4[4];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      double x[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        double a = 0.0;
+        if (f.nblk <= 16) {
+          if (4 * w + i < f.nblk) a += (double)r16[s][4 * w + i];
+        } else {
+          for (int b = 4 * w + i; b < f.nblk; b += 16)
+            a += (double)ew_fin_ld<SC1>(f.part + ((long long)s * f.nblk + b) * C + c);
+        }
+        x[i] = a;
+      }
+      w4[w] = (x[0] + x[1]) + (x[2] + x[3]);
+    }
+    double a = w4[0];
+#pragma unroll
+    for (int w = 1; w < 4; ++w) a += w4[w];
+    sums[s] = a;
+  }
+  const double invstd = f.stats[C + c], scale = f.stats[2 * C + c];
+  if (NS == 2) sums[2] = 0.0;
+  const double db = sums[0];
+  const double dg = sums[1] * invstd;
+  const double e = -scale * invstd * dg / (double)f.M;
+  f.coef[c] = (float)e;
+  f.coef[C + c] = (float)(-scale * db / (double)f.M);
+  if (f.dgamma) f.dgamma[c] = (float)dg;
+  if (f.dbeta) f.dbeta[c] = (float)db;
+  if (f.dcbias) {
+    const float v = (float)(e * sums[2]);
+    if (f.cb_bf16) reinterpret_cast<uint16_t*>(f.dcbias)[c] = ew_f2bf(v);
+    else reinterpret_cast<float*>(f.dcbias)[c] = v;
+  }
+}

@@ -321,7 +321,8 @@ int ew_sm_f32_bwd(uintptr_t x, uintptr_t bn_h, uintptr_t bn_stats, uintptr_t dy,
                   uintptr_t slab, long long slab_floats, uintptr_t cnt, long long cnt_ints,
                   long long N, int C, int Nc, uintptr_t pb_h, uintptr_t pb_res, uintptr_t pb_code,
                   uintptr_t pb_stats, int pb_relu, uintptr_t bnpart, long long bnpart_floats,
-                  uintptr_t stream);
+                  uintptr_t fin_coef, uintptr_t fin_dgamma, uintptr_t fin_dbeta,
+                  uintptr_t fin_dcbias, int fin_cb_bf16, long long fin_M, uintptr_t stream);
 
 // ---- LeNet's fp32 training step in four launches (lenet_f32.hip): persistent workspace floats
 // and ticket ints (zeroed once; the kernels leave them zero) for batch B

@@ -41,6 +41,7 @@
 #include <type_traits>
 #include <string>
 
+#include "bn_fin.h"
 #include "common.h"
 #include "conv_f32.h"
 #include "ewdml_ops.h"
@@ -429,9 +430,10 @@ __device__ __forceinline__ bool sm_reduce(SmAcc& acc, float* __restrict__ slab, 
 // Column sums of the tile (two quantities) over its 64 rows: a lane's 4 rows, the 4 lanes of a
 // column (xor 16, 32), then the 4 row waves through LDS in a fixed order -> bnpart[2][nrows][ld]
 // at row prow, columns col0..+63
+// wt: write-through stores (a BN finalisation riding in this launch reads them)
 __device__ __forceinline__ void sm_colsums(const float (&s1)[SM_NJ][4],
                                            const float (&s2)[SM_NJ][4], char* smem, float* bnpart,
-                                           int nrows, int prow, int ld, int col0) {
+                                           int nrows, int prow, int ld, int col0, bool wt = false) {
   const int t = threadIdx.x, lane = t & 63, wq = t >> 6;
   const int wm = wq / SM_WN, wn = wq % SM_WN;
   float* red = reinterpret_cast<float*>(smem);  // [SM_WM][2][64]
@@ -461,8 +463,15 @@ __device__ __forceinline__ void sm_colsums(const float (&s1)[SM_NJ][4],
       sa += red[(r * 2 + 0) * 64 + t];
       sq += red[(r * 2 + 1) * 64 + t];
     }
-    bnpart[(long long)prow * ld + col0 + t] = sa;
-    bnpart[(long long)(nrows + prow) * ld + col0 + t] = sq;
+    float* pa = bnpart + (long long)prow * ld + col0 + t;
+    float* pq = bnpart + (long long)(nrows + prow) * ld + col0 + t;
+    if (wt) {
+      __hip_atomic_store(pa, sa, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(pq, sq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      *pa = sa;
+      *pq = sq;
+    }
   }
 }
 
@@ -524,7 +533,8 @@ __global__ __launch_bounds__(SM_T) void k_sm_bwd(SmX xs, SmDy ds, const float* _
                                                  float* __restrict__ dx, float* __restrict__ dw,
                                                  float* __restrict__ slab, int* __restrict__ cnt,
                                                  int N, int C, int Nc, int nbd, CfBnBwd bb,
-                                                 float* __restrict__ bnpart, int fence) {
+                                                 float* __restrict__ bnpart, int fence,
+                                                 EwBnFin fin, int* __restrict__ fcnt) {
   __shared__ __attribute__((aligned(16))) char smem[2 * SM_STAGE + 16];
   int& flag = *reinterpret_cast<int*>(smem + 2 * SM_STAGE);
   const int t = threadIdx.x;
@@ -596,7 +606,25 @@ __global__ __launch_bounds__(SM_T) void k_sm_bwd(SmX xs, SmDy ds, const float* _
         }
       }
     }
-    if (bb.h && bnpart) sm_colsums(s1, s2, smem, bnpart, (N / SM_BM) * 4, mt * 4 + ip, C, c0);
+    if (bb.h && bnpart) {
+      const int nrows = (N / SM_BM) * 4;
+      sm_colsums(s1, s2, smem, bnpart, nrows, mt * 4 + ip, C, c0, fin.ngrp != 0);
+      if (fin.ngrp) {
+        // the BN backward finalisation of this channel tile, by its last row tile (the weight-
+        // gradient blocks of the launch keep running beside it)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (t == 0) {
+          const int prev = __hip_atomic_fetch_add(fcnt + ct, 1, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+          const int last = prev == nrows - 1;
+          if (last) __hip_atomic_store(fcnt + ct, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          flag = last;
+        }
+        __syncthreads();
+        if (flag && t < SM_BN) ew_bn_bwd_fin_chan<2, true>(fin, c0 + t);
+      }
+    }
     return;
   }
   // weight gradient: dw[o][tap][c] = sum over the tap's pairs and the batch
@@ -677,7 +705,8 @@ long long ew_sm_f32_ws_floats(long long N, int C, int Nc) {
   return 4LL * N * 4 * std::max(C, Nc);
 }
 long long ew_sm_f32_counters(long long N, int C, int Nc) {
-  return (N / SM_BM) * 4 * (std::max(C, Nc) / SM_BN);
+  // the tile tickets, then one finalisation ticket per 64-channel tile (k_sm_bwd)
+  return (N / SM_BM) * 4 * (std::max(C, Nc) / SM_BN) + std::max(C, Nc) / SM_BN;
 }
 
 // y [N][2][2][Nc] = conv(x) with x materialised (bn_h == 0) or relu(bn_h * scale + shift) of the
@@ -722,7 +751,8 @@ int ew_sm_f32_bwd(uintptr_t x, uintptr_t bn_h, uintptr_t bn_stats, uintptr_t dy,
                   uintptr_t slab, long long slab_floats, uintptr_t cnt, long long cnt_ints,
                   long long N, int C, int Nc, uintptr_t pb_h, uintptr_t pb_res, uintptr_t pb_code,
                   uintptr_t pb_stats, int pb_relu, uintptr_t bnpart, long long bnpart_floats,
-                  uintptr_t stream) {
+                  uintptr_t fin_coef, uintptr_t fin_dgamma, uintptr_t fin_dbeta,
+                  uintptr_t fin_dcbias, int fin_cb_bf16, long long fin_M, uintptr_t stream) {
   sm_check(N, C, Nc);
   if (!dy && !(out_h && out_dnext && out_stats && out_coef))
     throw std::runtime_error("ewdml small-map conv: backward needs dy or its BN source");
@@ -751,12 +781,24 @@ int ew_sm_f32_bwd(uintptr_t x, uintptr_t bn_h, uintptr_t bn_stats, uintptr_t dy,
   const dim3 grid((unsigned)(nbd + nbw));
   auto* sp = reinterpret_cast<float*>(slab);
   auto* cp = reinterpret_cast<int*>(cnt);
+  // fin_coef: that layer's backward finalisation rides here (coef [2][C], dgamma, dbeta, dcbias
+  // as k_bn_bwd_finalize<2> forms them from bnpart, bitwise), one ticket per 64-channel tile in
+  // cnt[tiles ..)
+  EwBnFin fin{};
+  if (fin_coef && bp) {
+    if (cnt_ints < tiles + C / SM_BN || fin_M <= 0)
+      throw std::runtime_error("ewdml small-map conv: finalisation tickets / rows missing");
+    fin = EwBnFin{bp, reinterpret_cast<const float*>(pb_stats), reinterpret_cast<float*>(fin_coef),
+                  reinterpret_cast<float*>(fin_dgamma), reinterpret_cast<float*>(fin_dbeta),
+                  reinterpret_cast<void*>(fin_dcbias), fin_M, rows, C, fin_cb_bf16,
+                  (C + EW_FIN_CH - 1) / EW_FIN_CH};
+  }
   const float* wp = reinterpret_cast<const float*>(w);
   float* dxp = reinterpret_cast<float*>(dx);
   float* dwp = reinterpret_cast<float*>(dw);
 #define SM_BWD(XK_, DK_)                                                                         \
   hipLaunchKernelGGL((k_sm_bwd<XK_, DK_>), grid, dim3(SM_T), 0, (hipStream_t)stream, xs, ds, wp, \
-                     dxp, dwp, sp, cp, (int)N, C, Nc, nbd, bb, bp, sm_fence())
+                     dxp, dwp, sp, cp, (int)N, C, Nc, nbd, bb, bp, sm_fence(), fin, cp + tiles)
   // DK: dy materialised (0), formed from the BN layer it feeds (2), that layer pooled 2x2 -> 1x1 (3)
   const int dk = dy ? 0 : out_pool ? 3 : 2;
   if (bn_h) {

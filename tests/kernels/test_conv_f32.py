@@ -976,6 +976,43 @@ def test_conv_f32_smallmap_lazy_bn_matches_materialised(pool, front_pool):
         assert torch.equal(a, b), i
 
 
+@pytest.mark.parametrize("N,C", [(64, 128), (128, 512)])
+@pytest.mark.parametrize("pool", [True, False])
+def test_bn_finalize_rides_in_smallmap_backward(N, C, pool):
+    """The BN backward finalisation formed by each channel tile's last row tile of the 2x2-map
+    backward launch (ops/csrc/smallmap_f32.hip, bn_fin.h ew_bn_bwd_fin_chan) gives bitwise the
+    gradients of the finalize launch."""
+    from ewdml.ops import conv as cmod
+    from ewdml.ops import nn as fnn
+
+    _conv(wino=True, min_c=64, tile=2, sm=True)
+    HW = 4 if pool else 2
+    x0, w0 = _data(N, C, C, HW, HW, seed=81)
+    _, w1 = _data(N, C, C, 2, 2, seed=82)
+    bn0 = torch.nn.BatchNorm2d(C).cuda()
+    with torch.no_grad():
+        bn0.weight.uniform_(0.5, 1.5)
+        bn0.bias.uniform_(-0.3, 0.3)
+    g = torch.randn(N, C, 2, 2, device="cuda").contiguous(memory_format=torch.channels_last)
+    grads = []
+    saved = cmod._FIN_RIDE
+    try:
+        for ride in (True, False):
+            cmod._FIN_RIDE = ride
+            rides = cmod.FIN_RIDES
+            bn = copy.deepcopy(bn0)
+            xa, wa, wb = (t.clone().requires_grad_(True) for t in (x0, w0, w1))
+            z = cmod.conv(fnn.bn_act(cmod.conv(xa, wa), bn, "relu", pool=pool), wb)
+            assert getattr(z.grad_fn, "sm", None) is not None
+            z.backward(g)
+            assert (cmod.FIN_RIDES > rides) == ride
+            grads.append([xa.grad, wa.grad, wb.grad, bn.weight.grad, bn.bias.grad])
+    finally:
+        cmod._FIN_RIDE = saved
+    for a, b in zip(*grads):
+        assert torch.equal(a, b), _rel(a, b)
+
+
 @pytest.mark.parametrize("mode,pool", [("relu", True), ("relu", False), ("none", False)])
 def test_conv_f32_smallmap_bn_backward_sums(mode, pool):
     """The 2x2-map backward-data reducer's BN backward sums (the producing BN layer's sum dz and
