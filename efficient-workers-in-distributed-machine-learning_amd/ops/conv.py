@@ -115,6 +115,9 @@ _WINO_LAZY_BWD = os.environ.get("EWDML_WINO_LAZY_BWD", "1") != "0"
 # it; EWDML_BN_FIN_RIDE=0: the BN backward launches it
 _FIN_RIDE = os.environ.get("EWDML_BN_FIN_RIDE", "1") != "0"
 FIN_RIDES = 0  # finalisations that rode in a weight-gradient launch (tests / diagnostics)
+# deferred Winograd weight-gradient output transforms that rode in a direct conv's backward-data
+# GEMM (same switch, EWDML_BN_FIN_RIDE)
+WO_RIDES = 0
 _SM_WS = {}
 
 
@@ -597,10 +600,18 @@ class _Conv(torch.autograd.Function):
         dy = dy.contiguous(memory_format=torch.channels_last)
         if dy.dtype != x.dtype:
             dy = dy.to(x.dtype)
-        if ctx.wino is None:  # nothing here carries a deferred transform: run it while warm
-            flush_pending()
-        ws = _ws(x.device)
         f32 = x.dtype == torch.float32
+        wo_job = None  # a deferred Winograd transform riding in this direct conv's bwd-data GEMM
+        if ctx.wino is None:  # nothing here carries a deferred transform: run it while warm
+            if (_FIN_RIDE and f32 and ctx.needs_input_grad[0] and _PENDING is not None
+                    and _PENDING[5] == 2):
+                join_wgrad()  # its source may come from the side stream
+                wo, wo_job = _take_pending(2)
+                if wo_job is not None:
+                    require().cf_arm_wgout(*wo)
+            else:
+                flush_pending()
+        ws = _ws(x.device)
         bwd_data = C_.conv_f32_bwd_data if f32 else C_.conv_bwd_data
         dx = dw = None
         fin_job = None  # (BN node, partials, rows, h, stats): its finalisation may ride in the wgrad
@@ -667,6 +678,12 @@ class _Conv(torch.autograd.Function):
                         fin_job = (node, part, rows, h, stats)
             if sink is not None:
                 sink.grad, sink.taken = None, True
+        if wo_job is not None:
+            # taken by the bwd-data GEMM (a 128-row tile) or run now on its own
+            if require().cf_flush_wgout(_stream()) == 0:
+                global WO_RIDES
+                WO_RIDES += 1
+            del wo_job  # enqueued: the stream orders any reuse of its buffers after it
         if ctx.needs_input_grad[1]:
             dw = torch.empty_like(w, memory_format=torch.channels_last)
             side = _wgrad_side(x.device) if _dw_may_lag(ctx) else None

@@ -274,6 +274,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("cf_set_glds", &ew_cf_set_glds);
   m.def("cf_arm_bn_fin", &ew_cf_arm_bn_fin);
   m.def("cf_flush_bn_fin", &ew_cf_flush_bn_fin);
+  m.def("cf_arm_wgout", &ew_cf_arm_wgout);
+  m.def("cf_flush_wgout", &ew_cf_flush_wgout);
   m.def("bn_part_floats", &ew_bn_part_floats);
   m.def("bn_relu_fwd",
         [](uintptr_t h, uintptr_t res, uintptr_t y, uintptr_t code, uintptr_t stats,

@@ -35,6 +35,7 @@
 #include "common.h"
 #include "conv_f32.h"
 #include "ewdml_ops.h"
+#include "wg_common.h"
 
 namespace {
 
@@ -585,7 +586,8 @@ __global__ __launch_bounds__(64 * WM * WN, WPE) void k_cf_gemm(const float* __re
                                                    float* __restrict__ out,
                                                    float* __restrict__ slab, CfGeom geo,
                                                    float* __restrict__ bnpart, CfBnBwd bb,
-                                                   const float* __restrict__ addend, EwBnFin fin) {
+                                                   const float* __restrict__ addend, EwBnFin fin,
+                                                   WgOut wo) {
   using L = CfLayout<MODE, BM, BN>;
   using acc_t = typename CfMfma<SH>::acc_t;
   constexpr int NT = 64 * WM * WN;
@@ -594,16 +596,34 @@ __global__ __launch_bounds__(64 * WM * WN, WPE) void k_cf_gemm(const float* __re
   static_assert(NT >= EW_BLOCK && 2 * L::STAGE >= 3 * EW_WAVES * EW_FIN_CH * 8, "finalize rider");
   __shared__ __attribute__((aligned(16))) char smem[2 * L::STAGE];
   int gz = gridDim.z;
-  if constexpr (MODE == CF_WGRAD) {
-    // a BatchNorm backward finalisation riding along (cf_gemm: extra z slices after the GEMM's,
-    // dispatched last, one channel group per block; bn_fin.h)
-    if (fin.ngrp) {
+  if constexpr (MODE != CF_FWD) {
+    // riders (cf_gemm: extra z slices after the GEMM's, dispatched last): a BatchNorm backward
+    // finalisation (weight-gradient launches; one channel group per block, bn_fin.h) and a
+    // deferred Winograd weight-gradient output transform (backward-data launches; NT element
+    // groups per block, wg_common.h)
+    // (each kind compiled only into the mode it rides in: the other's registers stay out)
+    if constexpr (MODE != CF_WGRAD) fin.ngrp = 0;
+    // (the transform rides only in 128-row stride-1 tiles: in the 64x64 one it doubled the VGPRs)
+    if constexpr (MODE != CF_BWD || BM != 128 || STR != 1) wo.src = nullptr;
+    if (fin.ngrp || wo.src) {
       const int gxy = gridDim.x * gridDim.y;
-      gz -= (fin.ngrp + gxy - 1) / gxy;
+      const int nwb = wo.src ? (wo.Nc * (wo.C / WG2_VW) + NT - 1) / NT : 0;
+      const int zf = (fin.ngrp + gxy - 1) / gxy, zw = (nwb + gxy - 1) / gxy;
+      gz -= zf + zw;
       if ((int)blockIdx.z >= gz) {
-        const int g = ((int)blockIdx.z - gz) * gxy + blockIdx.y * gridDim.x + blockIdx.x;
-        // 8 rows in flight: no more registers than the GEMM's own (16 raised the 64x64 tile's)
-        if (g < fin.ngrp) ew_bn_bwd_fin_group<2, 8>(fin, g, reinterpret_cast<double*>(smem));
+        const int rz = (int)blockIdx.z - gz, bxy = blockIdx.y * gridDim.x + blockIdx.x;
+        if (rz < zf) {
+          const int g = rz * gxy + bxy;
+          // 8 rows in flight: no more registers than the GEMM's own (16 raised the 64x64 tile's)
+          if constexpr (MODE == CF_WGRAD)
+            if (g < fin.ngrp) ew_bn_bwd_fin_group<2, 8>(fin, g, reinterpret_cast<double*>(smem));
+        } else {
+          const int g = (rz - zf) * gxy + bxy;
+          if constexpr (MODE == CF_BWD && BM == 128 && STR == 1)
+            if (g < nwb)
+              wg_wgrad_out<2>(wo.src, wo.nsplit, wo.dw, wo.Nc, wo.C,
+                              (long long)g * NT + threadIdx.x);
+        }
         return;
       }
     }
@@ -1190,6 +1210,14 @@ bool cf_glds_on() {
 // The BatchNorm backward finalisation armed for the next weight-gradient GEMM launch (host thread
 // that enqueues a conv's backward; ew_cf_arm_bn_fin / ew_cf_flush_bn_fin)
 thread_local EwBnFin g_cf_fin{};
+// the deferred Winograd (m = 2) weight-gradient output transform armed for the next backward-data
+// GEMM launch (ew_cf_arm_wgout / ew_cf_flush_wgout)
+thread_local WgOut g_cf_wo{nullptr, nullptr, 1, 0, 0};
+
+__global__ __launch_bounds__(EW_BLOCK) void k_cf_wgout(WgOut wo) {
+  wg_wgrad_out<2>(wo.src, wo.nsplit, wo.dw, wo.Nc, wo.C,
+                  (long long)blockIdx.x * EW_BLOCK + threadIdx.x);
+}
 
 __global__ __launch_bounds__(EW_BLOCK) void k_cf_bn_fin(EwBnFin f) {
   __shared__ double red[2 * EW_WAVES * EW_FIN_CH];
@@ -1254,7 +1282,7 @@ CfPlan cf_plan(int M, int Ncol, int ksteps, long long ws_floats, int batch) {
 
 #define CF_LAUNCH_W(MODE_, BM_, BN_, WM_, WN_, SH_, WPE_)                                   \
   hipLaunchKernelGGL((k_cf_gemm<MODE_, BM_, BN_, WM_, WN_, SH_, STR, WPE_>), grid,                \
-                     dim3(64 * WM_ * WN_), 0, s, a, b, out, slab, geo, bnp, bbv, addend, fin)
+                     dim3(64 * WM_ * WN_), 0, s, a, b, out, slab, geo, bnp, bbv, addend, fin, wo)
 #define CF_LAUNCH(MODE_, BM_, BN_, WM_, WN_, SH_) CF_LAUNCH_W(MODE_, BM_, BN_, WM_, WN_, SH_, 0)
 #define CF_LAUNCH_GL(BM_, BN_, WM_, WN_, SH_, WPE_)                                           \
   hipLaunchKernelGGL((k_cf_gemm_gl<BM_, BN_, WM_, WN_, SH_, WPE_>), grid, dim3(64 * WM_ * WN_), 0, \
@@ -1296,6 +1324,20 @@ int cf_gemm(const float* a, const float* b, float* out, float* ws, long long ws_
     g_cf_fin = EwBnFin{};
     grid.z += (fin.ngrp + grid.x * grid.y - 1) / (grid.x * grid.y);
   }
+  static const int w4 = [] {  // EWDML_CF_WAVES=4: 4-wave 128x128 blocks (64x64 wave tiles)
+    const char* e = getenv("EWDML_CF_WAVES");
+    return e && e[0] == '4';
+  }();
+  // an armed deferred Winograd weight-gradient output transform rides in a backward-data GEMM
+  WgOut wo{nullptr, nullptr, 1, 0, 0};
+  if (MODE == CF_BWD && STR == 1 && p.bm == 128 && g_cf_wo.src) {
+    wo = g_cf_wo;
+    g_cf_wo = WgOut{nullptr, nullptr, 1, 0, 0};
+    // the launched variant's threads (k_cf_gemm's NT): 8 waves but the 4-wave 128x128 option
+    const int NTL = (p.bm == 128 && p.bn == 128 && w4) ? 256 : 512;
+    const int nwb = (wo.Nc * (wo.C / WG2_VW) + NTL - 1) / NTL;
+    grid.z += (nwb + grid.x * grid.y - 1) / (grid.x * grid.y);
+  }
   float* slab = p.split > 1 ? ws : nullptr;
   const long long prow = geo.M / p.bm;
   float* bnp = (bnpart && !slab && prow <= 1024 && 2 * prow * geo.Ncol <= bnpart_floats) ? bnpart
@@ -1304,10 +1346,6 @@ int cf_gemm(const float* a, const float* b, float* out, float* ws, long long ws_
   const CfBnBwd bbv = (bnp && bnb) ? *bnb : none;
   // wave grids: 128x128 -> 2x4 waves of 64x32; 128x64 -> 4x2 of 32x32; 64x128 -> 2x4 of 32x32;
   // 64x64 -> 4x2 of 16x32
-  static const int w4 = [] {  // EWDML_CF_WAVES=4: 4-wave 128x128 blocks (64x64 wave tiles)
-    const char* e = getenv("EWDML_CF_WAVES");
-    return e && e[0] == '4';
-  }();
   // The 8-wave 128x64 / 64x128 kernels held to 128 VGPRs (4 waves per SIMD: two blocks per CU)
   // instead of the compiler's 130 (one block per CU), for grids of more than one block per CU:
   // ResNet-50 CIFAR +1.1 %, VGG-11 (one block per CU at these tiles) unchanged either way
@@ -1316,6 +1354,9 @@ int cf_gemm(const float* a, const float* b, float* out, float* ws, long long ws_
     const char* e = getenv("EWDML_CF_OCC");
     return e ? e[0] - '0' : 1;
   }();
+  // (rider slices count: with them a one-block-per-CU grid of 256 GEMM blocks leaves the riders
+  // waiting for a CU -- VGG-11 conv2's backward data + transform 60 us held to one block per CU,
+  // 54 us at two, profiles/ab/README.md)
   const bool occ2 = occ_env == 2 || (occ_env == 1 && (long long)grid.x * grid.y * grid.z > 256);
   bool launched = false;
   if constexpr (MODE == CF_FWD && STR == 1) {
@@ -1402,6 +1443,24 @@ void ew_cf_arm_bn_fin(uintptr_t part, int nblk, int C, long long M, uintptr_t st
                      reinterpret_cast<float*>(coef), reinterpret_cast<float*>(dgamma),
                      reinterpret_cast<float*>(dbeta), reinterpret_cast<void*>(dcbias), M, nblk, C,
                      cb_bf16, (C + EW_FIN_CH - 1) / EW_FIN_CH};
+}
+
+void ew_cf_arm_wgout(uintptr_t src, int split, uintptr_t dw, int Nc, int C) {
+  if (!src || !dw || split < 1 || Nc <= 0 || C % WG2_VW)
+    throw std::runtime_error("ewdml conv f32: bad weight-gradient output transform job");
+  if (g_cf_wo.src) throw std::runtime_error("ewdml conv f32: a transform is already armed");
+  g_cf_wo = WgOut{reinterpret_cast<const float*>(src), reinterpret_cast<float*>(dw), split, Nc, C};
+}
+
+int ew_cf_flush_wgout(uintptr_t stream) {
+  if (!g_cf_wo.src) return 0;
+  const WgOut wo = g_cf_wo;
+  g_cf_wo = WgOut{nullptr, nullptr, 1, 0, 0};
+  const long long n = (long long)wo.Nc * (wo.C / WG2_VW);
+  hipLaunchKernelGGL(k_cf_wgout, dim3((unsigned)((n + EW_BLOCK - 1) / EW_BLOCK)), dim3(EW_BLOCK),
+                     0, (hipStream_t)stream, wo);
+  EW_CHECK_LAUNCH();
+  return 1;
 }
 
 int ew_cf_flush_bn_fin(uintptr_t stream) {

@@ -119,6 +119,8 @@ int ew_cf_set_glds(int on);
 void ew_cf_arm_bn_fin(uintptr_t part, int nblk, int C, long long M, uintptr_t stats, uintptr_t coef,
                       uintptr_t dgamma, uintptr_t dbeta, uintptr_t dcbias, int cb_bf16);
 int ew_cf_flush_bn_fin(uintptr_t stream);
+void ew_cf_arm_wgout(uintptr_t src, int split, uintptr_t dw, int Nc, int C);
+int ew_cf_flush_wgout(uintptr_t stream);
 // SGD of one bucket from its per-tensor gradients (pointer table; a.grad / a.n / a.grad_dtype
 // unused): param / mom / shadow are the bucket's flat views, chunk rows address them
 void ew_sgd_ptrs(const uintptr_t* grad_ptrs, int n_ptrs, const uint32_t* bf16_mask, int n_mask,

@@ -713,6 +713,52 @@ def test_winograd_deferred_wgrad_output_transform(m):
         _opt_out(ws, handles)
 
 
+@pytest.mark.parametrize("k0", [3, 1])
+def test_winograd_deferred_transform_rides_in_direct_bwd_data(k0):
+    """The deferred weight-gradient output transform of a Winograd layer rides in the direct
+    (non-Winograd) conv's backward-data GEMM launch behind it (ops/csrc/conv_f32.hip WgOut rider):
+    bitwise the immediate transform."""
+    conv = _conv(True, 128, "2")
+    torch.manual_seed(1)
+    N, H = 128, 16  # VGG-11's conv2 -> conv3 (the bwd-data GEMM takes 128-row tiles)
+    w0 = torch.nn.Parameter((torch.randn(128, 64, k0, k0, device="cuda") / (k0 * 8.0))
+                            .contiguous(memory_format=torch.channels_last))
+    w1 = torch.nn.Parameter((torch.randn(128, 128, 3, 3, device="cuda") / 34.0)
+                            .contiguous(memory_format=torch.channels_last))
+    ws = [w0, w1]
+    x = torch.randn(N, 64, H, H, device="cuda").contiguous(memory_format=torch.channels_last)
+    x.requires_grad_(True)
+    dy = torch.randn(N, 128, H, H, device="cuda").contiguous(memory_format=torch.channels_last)
+    handles = _opt_in(ws)
+
+    def run(defer):
+        conv._DEFER_WOUT = defer
+        conv._POISON_DW = True
+        conv.new_pass()  # the exchange engine's begin: not a second (tied) use of the weights
+        for w in ws:
+            w.grad = None
+            w._ew_tied = False
+        x.grad = None
+        rides = conv.WO_RIDES
+        h = conv.conv(x, w0)
+        assert conv.wino_tile(x, w0) == 0 and conv.wino_tile(h, w1) == 2
+        conv.conv(h, w1).backward(dy)
+        torch.cuda.synchronize()
+        return [w.grad.clone() for w in ws] + [x.grad.clone()], conv.WO_RIDES - rides
+
+    try:
+        ref, r0 = run(False)
+        got, r1 = run(True)
+        assert r0 == 0 and r1 == 1
+        for a, b in zip(got, ref):
+            assert not torch.isnan(a).any()
+            assert torch.equal(a, b)
+    finally:
+        conv._DEFER_WOUT = True
+        conv._POISON_DW = False
+        _opt_out(ws, handles)
+
+
 def _opt_in(ws):
     """Mark parameters the way parallel/engine.py does (a post-accumulate hook it owns, counted
     in _ew_engine_hooks): only those defer their weight-gradient output transform."""
