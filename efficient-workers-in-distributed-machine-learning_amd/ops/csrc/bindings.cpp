@@ -272,6 +272,7 @@ PYBIND11_MODULE(_C, m) {
         });
 
   m.def("cf_set_glds", &ew_cf_set_glds);
+  m.def("cf_set_inred", &ew_cf_set_inred);
   m.def("cf_arm_bn_fin", &ew_cf_arm_bn_fin);
   m.def("cf_flush_bn_fin", &ew_cf_flush_bn_fin);
   m.def("cf_arm_wgout", &ew_cf_arm_wgout);

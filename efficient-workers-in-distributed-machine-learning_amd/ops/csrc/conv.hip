@@ -1173,6 +1173,7 @@ static int ew_conv_nt(const uint16_t* x, const uint16_t* w, uint16_t* out, float
   // the last 64 floats of the workspace are a zero page (never part of a slab)
   ws_floats -= 64;
   const uint16_t* zero = reinterpret_cast<const uint16_t*>(ws + ws_floats);
+  ws_floats -= 4096;  // conv_f32.hip's in-launch split-K tickets (CF_RED_TICKETS) precede the zero page
   const CvPlan p = cv_plan(tiles, ksteps, dma ? 1 : (big ? 2 : 4), (long long)M * Nc, ws_floats);
   dim3 grid(M / BM, Nc / BM, p.split);
   float* slab = p.split > 1 ? ws : nullptr;

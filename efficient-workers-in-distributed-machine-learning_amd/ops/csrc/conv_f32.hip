@@ -437,13 +437,23 @@ struct CfStager {
 // (BM/WM) x (BN/WN) tiles of MI x NJ SH x SH MFMA blocks.
 // RMAP (stride-2 backward data): GEMM row r = dy pixel (n, i, j) of an rHo x rWo map is written
 // to dx pixel (n, 2 i + rph, 2 j + rpw) (out and addend; no slab, no BN sums on this path)
+// 16-B load through to L2 (agent scope): data another block of this launch wrote write-through
+__device__ __forceinline__ f32x4 cf_ld4_sc1(const float* p) {
+  f32x4 v;
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    v[k] = __hip_atomic_load(const_cast<float*>(p) + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return v;
+}
+
 template <int BM, int BN, int WM, int WN, int SH, int MI, int NJ, bool RMAP = false>
 __device__ __forceinline__ void cf_epilogue(typename CfMfma<SH>::acc_t (&acc)[MI][NJ], char* smem,
                                             int wm, int wn, int lane, int m0, int n0, int M,
                                             int Nc, float* __restrict__ out,
                                             float* __restrict__ slab, float* __restrict__ bnpart,
                                             const CfBnBwd& bb, const float* __restrict__ addend,
-                                            int rHo = 0, int rWo = 0, int rph = 0, int rpw = 0) {
+                                            int rHo = 0, int rWo = 0, int rph = 0, int rpw = 0,
+                                            int* redtk = nullptr, int nsplit = 1, int zs = 0) {
   using F = CfMfma<SH>;
   constexpr int E = F::E;
   const int row0 = m0 + wm * (BM / WM), col0 = n0 + wn * (BN / WN);
@@ -461,6 +471,62 @@ __device__ __forceinline__ void cf_epilogue(typename CfMfma<SH>::acc_t (&acc)[MI
   };
   if (slab) {
     float* sp = slab;  // this block's split slab (k_cf_gemm offsets it)
+    if (!RMAP && redtk) {
+      // in-launch split-K reduction (no reduction launch): the slab is stored write-through, the
+      // tile's last split (ticket red[tile]) sums the splits in k_cf_slab_reduce's order, reading
+      // the others with agent-scope loads (cdna_hip_programming.md Guideline 16)
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int e = 0; e < E; ++e)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j)
+            __hip_atomic_store(sp + (long long)row_of(i, e) * Nc + col_of(j), acc[i][j][e],
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      int* flag = reinterpret_cast<int*>(smem);
+      if (threadIdx.x == 0) {
+        int* tk = redtk + blockIdx.x + gridDim.x * blockIdx.y;
+        const int last =
+            __hip_atomic_fetch_add(tk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nsplit - 1;
+        if (last) __hip_atomic_store(tk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *flag = last;
+      }
+      __syncthreads();
+      if (!*flag) return;
+      const long long zstride = (long long)M * Nc;
+      const float* base = slab - (long long)zs * zstride;
+      // the tile's BM x BN block of every split (the own one re-read: the same bits) summed in
+      // split order as float4 rows, k_cf_slab_reduce's expression per element
+      constexpr int NTH = 64 * WM * WN, Q = BN / 4, CH = BM * Q / NTH;
+      static_assert(BM * Q % NTH == 0, "tile chunks");
+      f32x4 a[CH];
+#pragma unroll
+      for (int u = 0; u < CH; ++u) {
+        const int c = (int)threadIdx.x + u * NTH, r = c / Q, q = c - r * Q;
+        a[u] = cf_ld4_sc1(base + (long long)(m0 + r) * Nc + n0 + 4 * q);
+      }
+      for (int z = 1; z < nsplit; ++z) {
+        f32x4 v[CH];
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+          const int c = (int)threadIdx.x + u * NTH, r = c / Q, q = c - r * Q;
+          v[u] = cf_ld4_sc1(base + z * zstride + (long long)(m0 + r) * Nc + n0 + 4 * q);
+        }
+#pragma unroll
+        for (int u = 0; u < CH; ++u) a[u] += v[u];
+      }
+#pragma unroll
+      for (int u = 0; u < CH; ++u) {
+        const int c = (int)threadIdx.x + u * NTH, r = c / Q, q = c - r * Q;
+        const long long o = (long long)(m0 + r) * Nc + n0 + 4 * q;
+        f32x4 w = a[u];
+        if (addend) w += *reinterpret_cast<const f32x4*>(addend + o);
+        *reinterpret_cast<f32x4*>(out + o) = w;
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -587,7 +653,7 @@ __global__ __launch_bounds__(64 * WM * WN, WPE) void k_cf_gemm(const float* __re
                                                    float* __restrict__ slab, CfGeom geo,
                                                    float* __restrict__ bnpart, CfBnBwd bb,
                                                    const float* __restrict__ addend, EwBnFin fin,
-                                                   WgOut wo) {
+                                                   WgOut wo, int* __restrict__ red) {
   using L = CfLayout<MODE, BM, BN>;
   using acc_t = typename CfMfma<SH>::acc_t;
   constexpr int NT = 64 * WM * WN;
@@ -691,7 +757,7 @@ __global__ __launch_bounds__(64 * WM * WN, WPE) void k_cf_gemm(const float* __re
   __syncthreads();  // the epilogue reuses smem
   cf_epilogue<BM, BN, WM, WN, SH, MI, NJ, S2B>(acc, smem, wm, wn, lane, m0, n0, geo.M, geo.Ncol,
                                                out, slab, bnpart, bb, addend, geo.H, geo.W,
-                                               phase >> 1, phase & 1);
+                                               phase >> 1, phase & 1, red, geo.nsplit, zs);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1280,9 +1346,35 @@ CfPlan cf_plan(int M, int Ncol, int ksteps, long long ws_floats, int batch) {
   return best;
 }
 
+// tickets of the in-launch split-K reduction (k_cf_gemm's epilogue) per workspace; conv.hip keeps
+// its slabs clear of them
+constexpr int CF_RED_TICKETS = 4096;
+// EWDML_CF_INRED=1: the in-launch reduction instead of the k_cf_slab_reduce launch (opt-in,
+// ew_cf_set_inred at run time).  Measured slower: VGG-11 1.153 -> 1.195 ms, ResNet-50 CIFAR 13.16
+// -> 14.13 ms -- the write-through slabs and the reducing blocks' sc1 loads cost more than the
+// launch they save (profiles/ab/README.md)
+int g_cf_inred = -1;
+bool cf_inred_on() {
+  if (g_cf_inred < 0) {
+    const char* e = getenv("EWDML_CF_INRED");
+    g_cf_inred = (e && e[0] == '1') ? 1 : 0;
+  }
+  return g_cf_inred == 1;
+}
+// whether the split reduction would write BN partial rows (k_cf_slab_reduce_bn's condition)
+bool Nc_bn_ok(const CfGeom& geo, long long bnpart_floats) {
+  const int M = geo.M, Nc = geo.Ncol;
+  const int tpr = Nc / 4, rpi = tpr <= EW_BLOCK ? EW_BLOCK / tpr : 0;
+  if (rpi <= 0 || EW_BLOCK % tpr) return false;
+  int rpb = rpi;
+  while ((M + rpb - 1) / rpb > 1024) rpb += rpi;
+  return 2LL * ((M + rpb - 1) / rpb) * Nc <= bnpart_floats;
+}
+
 #define CF_LAUNCH_W(MODE_, BM_, BN_, WM_, WN_, SH_, WPE_)                                   \
   hipLaunchKernelGGL((k_cf_gemm<MODE_, BM_, BN_, WM_, WN_, SH_, STR, WPE_>), grid,                \
-                     dim3(64 * WM_ * WN_), 0, s, a, b, out, slab, geo, bnp, bbv, addend, fin, wo)
+                     dim3(64 * WM_ * WN_), 0, s, a, b, out, slab, geo, bnp, bbv, addend, fin, wo, \
+                     red)
 #define CF_LAUNCH(MODE_, BM_, BN_, WM_, WN_, SH_) CF_LAUNCH_W(MODE_, BM_, BN_, WM_, WN_, SH_, 0)
 #define CF_LAUNCH_GL(BM_, BN_, WM_, WN_, SH_, WPE_)                                           \
   hipLaunchKernelGGL((k_cf_gemm_gl<BM_, BN_, WM_, WN_, SH_, WPE_>), grid, dim3(64 * WM_ * WN_), 0, \
@@ -1293,6 +1385,13 @@ int cf_gemm(const float* a, const float* b, float* out, float* ws, long long ws_
             CfGeom geo, hipStream_t s, float* bnpart, long long bnpart_floats,
             const CfBnBwd* bnb, const float* addend, int* split_out = nullptr) {
   ws_floats -= 64;  // the workspace's last 64 floats are conv.hip's zero page (never a slab)
+  // the shared per-stream workspace (not a caller's own slabs): the in-launch split-K tickets sit
+  // before the zero page (zeroed with it, left zeroed)
+  int* tick = nullptr;
+  if (!split_out) {
+    ws_floats -= CF_RED_TICKETS;
+    tick = reinterpret_cast<int*>(ws + ws_floats);
+  }
   const int batch = geo.nsplit;  // callers pass the batch count here (1: no batching)
   {
     // the buffer-load operands (per batch) must fit 32-bit byte offsets (CfStager)
@@ -1340,6 +1439,13 @@ int cf_gemm(const float* a, const float* b, float* out, float* ws, long long ws_
   }
   float* slab = p.split > 1 ? ws : nullptr;
   const long long prow = geo.M / p.bm;
+  // split-K reduced in-launch by each tile's last split (no k_cf_slab_reduce launch) when no BN
+  // sums are due from the reduction (their partial rows come from k_cf_slab_reduce_bn)
+  int* red = nullptr;
+  if (slab && tick && batch == 1 && cf_inred_on() &&
+      (long long)grid.x * grid.y <= CF_RED_TICKETS && !(bnpart && Nc_bn_ok(geo, bnpart_floats)) &&
+      !(MODE == CF_FWD && STR == 1 && cf_glds_on() && !w4))  // (the LDS-DMA kernel: no tickets)
+    red = tick;
   float* bnp = (bnpart && !slab && prow <= 1024 && 2 * prow * geo.Ncol <= bnpart_floats) ? bnpart
                                                                                       : nullptr;
   const CfBnBwd none{nullptr, nullptr, nullptr, nullptr, 0, 0, 0};
@@ -1392,6 +1498,7 @@ int cf_gemm(const float* a, const float* b, float* out, float* ws, long long ws_
   }
   if (p.split > 1 && batch > 1)
     throw std::runtime_error("ewdml conv f32: a batched split GEMM needs the caller's reduction");
+  if (p.split > 1 && red) return 0;  // reduced in the launch (no BN partial rows)
   if (p.split > 1) {
     const int M = geo.M, Nc = geo.Ncol;
     const long long n = (long long)M * Nc;
@@ -1470,6 +1577,12 @@ int ew_cf_flush_bn_fin(uintptr_t stream) {
   hipLaunchKernelGGL(k_cf_bn_fin, dim3(f.ngrp), dim3(EW_BLOCK), 0, (hipStream_t)stream, f);
   EW_CHECK_LAUNCH();
   return 1;
+}
+
+int ew_cf_set_inred(int on) {
+  const int prev = cf_inred_on() ? 1 : 0;
+  if (on >= 0) g_cf_inred = on ? 1 : 0;
+  return prev;
 }
 
 int ew_cf_set_glds(int on) {

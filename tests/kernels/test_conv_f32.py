@@ -135,6 +135,35 @@ def test_conv_f32_backward(N, C, Nc, H, W, k):
     assert _rel(wa.grad, gw) < TOL, _rel(wa.grad, gw)
 
 
+@pytest.mark.parametrize("N,C,Nc,H,W,k", [(128, 64, 128, 16, 16, 3), (32, 256, 64, 32, 32, 1),
+                                          (64, 256, 512, 4, 4, 3), (128, 512, 512, 2, 2, 3)])
+def test_conv_f32_inlaunch_split_reduction_bitwise(N, C, Nc, H, W, k):
+    """Split-K GEMMs reduced by each tile's last split inside the launch (k_cf_gemm epilogue,
+    write-through slabs + ticket) give bitwise what the separate k_cf_slab_reduce launch gives:
+    forward, backward data and weight gradient."""
+    from ewdml import ops
+
+    conv = _conv()
+    C_ = ops.require()
+    x, w = _data(N, C, Nc, H, W, seed=9, k=k)
+    dy = torch.randn(N, Nc, H, W, device="cuda").contiguous(memory_format=torch.channels_last)
+    res = []
+    prev = C_.cf_set_inred(1)
+    try:
+        for on in (1, 0):
+            C_.cf_set_inred(on)
+            xa, wa = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
+            y = conv.conv(xa, wa)
+            y.backward(dy)
+            torch.cuda.synchronize()
+            res.append((y.detach(), xa.grad, wa.grad))
+    finally:
+        C_.cf_set_inred(prev)
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+    assert _rel(res[0][2], _ref64(x, w, k, dy)[2]) < TOL
+
+
 def test_conv_f32_deterministic():
     conv = _conv()
     x, w = _data(128, 512, 512, 2, 2, seed=3)
