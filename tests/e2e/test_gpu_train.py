@@ -301,6 +301,23 @@ def test_own_rccl_communicator_matches_process_group(codec):
     assert own["payload_bytes_per_rank"] == pg["payload_bytes_per_rank"]
 
 
+def test_unrolled_bench_through_own_rccl_communicator():
+    """bench.py's timed loop with 8 steps per graph launch through the own RCCL communicator
+    (world 1, EWDML_FORCE_PG=1: the collectives are captured in the graph, eight sets of them in
+    the unrolled one): the same final loss, bytes and healthy codec as one graph per step."""
+    extra = ("--steps", "16", "--warmup", "12", "--graph-unroll")
+    u8 = _bench_pg("topk_qsgd", "rccl", extra=extra + ("8",))
+    u1 = _bench_pg("topk_qsgd", "rccl", extra=extra + ("1",))
+    assert u8["config"]["comm"] == "rccl-stream" and u8["config"]["hip_graph"] == "full"
+    assert u8["graph_unroll"] == 8 and u1["graph_unroll"] == 1
+    # the same 28 steps (4 + one 8-step replay of warmup, then 16 timed) on both
+    assert u8["warmup_steps_run"] == u1["warmup_steps_run"] == 12
+    assert u8["final_loss"] == u1["final_loss"]
+    assert u8["replicas_identical"] is not False
+    assert "error" not in (u8["codec_health"] or {})
+    assert u8["payload_bytes_per_rank"] == u1["payload_bytes_per_rank"]
+
+
 def test_comm_probe_passes_and_failure_falls_back_to_process_group():
     """The first-contact probe of the own RCCL communicator (parallel/probe.py: rank-coded
     all-gather / all-reduce / broadcast, eager and captured in a HIP graph replayed twice) passes
