@@ -50,7 +50,7 @@ def parse(argv=None):
     p.add_argument("--preset", default="vgg11", choices=sorted(PRESETS),
                    help="BASELINE.json config (explicit flags override it)")
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=30)
+    p.add_argument("--steps", type=int, default=32)  # a multiple of --graph-unroll
     p.add_argument("--warmup", type=int, default=8)
     p.add_argument("--network", default=None)
     p.add_argument("--dataset", default=None)
