@@ -118,6 +118,10 @@ FIN_RIDES = 0  # finalisations that rode in a weight-gradient launch (tests / di
 # deferred Winograd weight-gradient output transforms that rode in a direct conv's backward-data
 # GEMM (same switch, EWDML_BN_FIN_RIDE)
 WO_RIDES = 0
+# whether a direct conv's split-K weight-gradient reduction was left pending for the stem's
+# reduction launch (ops/csrc/conv_f32.hip ew_cf_defer_reduce: the conv fed by the stem's BN layer,
+# whose backward runs next); flush_pending runs it before any gradient is read
+_STEM_RED = [False]
 _SM_WS = {}
 
 
@@ -208,11 +212,15 @@ def join_wgrad():
         _SIDE_PENDING.clear()
 
 
-def flush_pending(final=False):
+def flush_pending(final=False, keep_stem_red=False):
     """Run a deferred weight-gradient output transform now (``final`` is accepted for the end-of-
-    backward callback; every flush runs the job).  Returns True."""
+    backward callback; every flush runs the job) and a split-K reduction left for the stem's
+    launch (unless ``keep_stem_red``: the stem's own backward, which takes it).  Returns True."""
     global _PENDING
     join_wgrad()  # every caller is about to read (or transform) a weight gradient
+    if _STEM_RED[0] and not keep_stem_red:  # left for the stem's reduction launch (C++ side)
+        _STEM_RED[0] = False
+        require().cf_flush_reduce()
     job = _PENDING
     if job is None:
         return True
@@ -615,6 +623,7 @@ class _Conv(torch.autograd.Function):
         bwd_data = C_.conv_f32_bwd_data if f32 else C_.conv_bwd_data
         dx = dw = None
         fin_job = None  # (BN node, partials, rows, h, stats): its finalisation may ride in the wgrad
+        stem_next = False
         D = None  # Winograd: the weight gradient's dy transform, made by the bwd-data pass
         m = ctx.wino[2] if ctx.wino is not None else 0
         aa = (m + 2) ** 2
@@ -676,6 +685,8 @@ class _Conv(torch.autograd.Function):
                     node._ew_pre_bwd = (part, rows, dx, dx._version)
                     if _FIN_RIDE and f32 and ctx.needs_input_grad[1]:
                         fin_job = (node, part, rows, h, stats)
+                # the stem's backward runs next: its reduction launch may take this conv's
+                stem_next = f32 and getattr(node, "stem_in", False)
             if sink is not None:
                 sink.grad, sink.taken = None, True
         if wo_job is not None:
@@ -713,6 +724,13 @@ class _Conv(torch.autograd.Function):
                 else:
                     wgrad = C_.conv_f32_wgrad if f32 else C_.conv_wgrad
                     wsw = _ws(x.device)  # the current stream's slabs (the side stream's own)
+                    # (like the deferred Winograd transforms, dw is then written after this
+                    # backward returns: off with _DEFER_WOUT)
+                    if stem_next and side is None and _FIN_RIDE and _DEFER_WOUT:
+                        C_.cf_defer_reduce()  # its split-K reduction: in the stem's launch
+                        if not _STEM_RED[0]:  # run at the latest when the backward pass ends
+                            torch.autograd.Variable._execution_engine.queue_callback(_flush_final)
+                        _STEM_RED[0] = True
                     wgrad(_ptr(dy), _ptr(x), _ptr(dw), _ptr(wsw), wsw.numel(), N, H, W, C, Nc, k,
                           _stream())
 
@@ -816,7 +834,7 @@ class _ConvStem(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         C_ = require()
-        flush_pending()  # a deferred Winograd weight-gradient transform, while its data is warm
+        flush_pending(keep_stem_red=True)  # a deferred Winograd transform, while its data is warm
         x, w = ctx.saved_tensors
         N, C, H, W = x.shape
         Nc = w.shape[0]

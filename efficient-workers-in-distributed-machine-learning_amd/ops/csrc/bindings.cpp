@@ -273,6 +273,8 @@ PYBIND11_MODULE(_C, m) {
 
   m.def("cf_set_glds", &ew_cf_set_glds);
   m.def("cf_set_inred", &ew_cf_set_inred);
+  m.def("cf_defer_reduce", &ew_cf_defer_reduce);
+  m.def("cf_flush_reduce", &ew_cf_flush_reduce);
   m.def("cf_arm_bn_fin", &ew_cf_arm_bn_fin);
   m.def("cf_flush_bn_fin", &ew_cf_flush_bn_fin);
   m.def("cf_arm_wgout", &ew_cf_arm_wgout);

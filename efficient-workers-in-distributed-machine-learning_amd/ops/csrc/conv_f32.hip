@@ -1262,6 +1262,74 @@ __global__ __launch_bounds__(EW_BLOCK) void k_cf_stem_reduce(const float* __rest
   if (ck == 0 && o < n) dw[o] = red[0][t & 7];
 }
 
+// A split-K reduction left pending (ew_cf_defer_reduce) for the stem's reduction launch to run
+// beside its own (k_cf_reduce2): its slabs stay in the workspace until then, and any GEMM launch
+// that may write slabs, or a flush before a gradient is read, runs it on its own first.
+struct CfPendRed {
+  const float* slab;
+  float* out;
+  long long n;  // floats (multiple of 4)
+  int split;
+  hipStream_t s;
+};
+thread_local CfPendRed g_cf_pred{nullptr, nullptr, 0, 0, nullptr};
+thread_local int g_cf_defer_red = 0;
+
+// blocks [0, nb1): k_cf_stem_reduce's work; the rest k_cf_slab_reduce's (no addend), each
+// element in its own kernel's order
+__global__ __launch_bounds__(EW_BLOCK) void k_cf_reduce2(const float* __restrict__ sslab, int snb,
+                                                         int sn, float* __restrict__ sdw, int nb1,
+                                                         const float* __restrict__ slab,
+                                                         int nsplit, long long n,
+                                                         float* __restrict__ out) {
+  if ((int)blockIdx.x < nb1) {
+    __shared__ float red[32][8];
+    const int t = threadIdx.x, o = blockIdx.x * 8 + (t & 7), ck = t >> 3;
+    float sv = 0.0f;
+    if (o < sn) {
+      const int per = (snb + 31) / 32, b0 = ck * per, b1 = min(b0 + per, snb);
+      int b = b0;
+      for (; b + 3 < b1; b += 4) {
+        const float v0 = sslab[(long long)b * sn + o], v1 = sslab[(long long)(b + 1) * sn + o];
+        const float v2 = sslab[(long long)(b + 2) * sn + o], v3 = sslab[(long long)(b + 3) * sn + o];
+        sv += (v0 + v1) + (v2 + v3);
+      }
+      for (; b < b1; ++b) sv += sslab[(long long)b * sn + o];
+    }
+    red[ck][t & 7] = sv;
+    __syncthreads();
+#pragma unroll
+    for (int h = 16; h > 0; h >>= 1) {
+      if (ck < h) red[ck][t & 7] += red[ck + h][t & 7];
+      __syncthreads();
+    }
+    if (ck == 0 && o < sn) sdw[o] = red[0][t & 7];
+    return;
+  }
+  const long long nv = n / 4;
+  for (long long v = (blockIdx.x - nb1) * (long long)EW_BLOCK + threadIdx.x; v < nv;
+       v += (long long)(gridDim.x - nb1) * EW_BLOCK) {
+    const f32x4* p = reinterpret_cast<const f32x4*>(slab) + v;
+    f32x4 a = p[0];
+    for (int z = 1; z < nsplit; ++z) a += p[(long long)z * (n / 4)];  // fixed order
+    reinterpret_cast<f32x4*>(out)[v] = a;
+  }
+}
+
+long long cf_reduce_grid(long long n) {
+  long long gr = (n / 4 + EW_BLOCK - 1) / EW_BLOCK;
+  return gr > 2048 ? 2048 : gr;
+}
+
+void cf_flush_pred() {
+  if (!g_cf_pred.slab) return;
+  const CfPendRed j = g_cf_pred;
+  g_cf_pred = CfPendRed{nullptr, nullptr, 0, 0, nullptr};
+  hipLaunchKernelGGL(k_cf_slab_reduce, dim3((int)cf_reduce_grid(j.n)), dim3(EW_BLOCK), 0, j.s,
+                     j.slab, j.split, j.n, j.out, nullptr);
+  EW_CHECK_LAUNCH();
+}
+
 // Forward GEMMs through the LDS-DMA kernel (k_cf_gemm_gl): EWDML_CF_GLDS=1/0 at load, or
 // ew_cf_set_glds at run time (tests compare both paths in one process)
 int g_cf_glds = -1;
@@ -1384,6 +1452,9 @@ template <int MODE, int STR = 1>
 int cf_gemm(const float* a, const float* b, float* out, float* ws, long long ws_floats,
             CfGeom geo, hipStream_t s, float* bnpart, long long bnpart_floats,
             const CfBnBwd* bnb, const float* addend, int* split_out = nullptr) {
+  cf_flush_pred();  // this launch may write slabs over a pending reduction's
+  const int defer_red = g_cf_defer_red;  // armed for this launch only
+  g_cf_defer_red = 0;
   ws_floats -= 64;  // the workspace's last 64 floats are conv.hip's zero page (never a slab)
   // the shared per-stream workspace (not a caller's own slabs): the in-launch split-K tickets sit
   // before the zero page (zeroed with it, left zeroed)
@@ -1516,10 +1587,12 @@ int cf_gemm(const float* a, const float* b, float* out, float* ws, long long ws_
       EW_CHECK_LAUNCH();
       return nblk;
     }
-    long long gr = (n / 4 + EW_BLOCK - 1) / EW_BLOCK;
-    if (gr > 2048) gr = 2048;
-    hipLaunchKernelGGL(k_cf_slab_reduce, dim3((int)gr), dim3(EW_BLOCK), 0, s, ws, p.split, n, out,
-                       addend);
+    if (defer_red && !addend && n % 4 == 0) {  // left to the stem's reduction launch
+      g_cf_pred = CfPendRed{ws, out, n, p.split, s};
+      return 0;
+    }
+    hipLaunchKernelGGL(k_cf_slab_reduce, dim3((int)cf_reduce_grid(n)), dim3(EW_BLOCK), 0, s, ws,
+                       p.split, n, out, addend);
     EW_CHECK_LAUNCH();
   }
   return bnp ? (int)prow : 0;
@@ -1577,6 +1650,15 @@ int ew_cf_flush_bn_fin(uintptr_t stream) {
   hipLaunchKernelGGL(k_cf_bn_fin, dim3(f.ngrp), dim3(EW_BLOCK), 0, (hipStream_t)stream, f);
   EW_CHECK_LAUNCH();
   return 1;
+}
+
+// Leave the next plain split-K reduction of an fp32 GEMM pending for the stem's reduction launch
+// (ops/conv.py: the conv whose input comes from the stem's BN layer); ew_cf_flush_reduce runs a
+// pending one (before any gradient is read).
+void ew_cf_defer_reduce() { g_cf_defer_red = 1; }
+void ew_cf_flush_reduce() {
+  g_cf_defer_red = 0;
+  cf_flush_pred();
 }
 
 int ew_cf_set_inred(int on) {
@@ -1748,6 +1830,19 @@ static void cf_stem_wgrad(const float* dy, const CsLazy* lz, uintptr_t x, uintpt
     throw std::runtime_error("ewdml conv f32 stem: a pooled BN backward needs even maps, codes");
   hipStream_t s = (hipStream_t)stream;
   float* slab = reinterpret_cast<float*>(ws);
+  // a pending split-K reduction (its slabs at the workspace's start) runs in this reduction
+  // launch: the stem's partials go behind them when they fit, else it runs now on its own
+  CfPendRed pend = g_cf_pred;
+  if (pend.slab) {
+    const long long used = (long long)pend.split * pend.n;
+    if (pend.slab == slab && pend.s == s && used + nb * n <= ws_floats - 64 - CF_RED_TICKETS) {
+      slab += (used + 63) / 64 * 64;
+      g_cf_pred = CfPendRed{nullptr, nullptr, 0, 0, nullptr};
+    } else {
+      cf_flush_pred();
+      pend.slab = nullptr;
+    }
+  }
   const CsLazy none{nullptr, nullptr, nullptr, nullptr, nullptr, 0};
   if (lz)
     hipLaunchKernelGGL(k_cf_stem_wgrad<true>, dim3((int)nb, Nc / 64), dim3(CS_WG_THREADS), 0, s,
@@ -1756,8 +1851,15 @@ static void cf_stem_wgrad(const float* dy, const CsLazy* lz, uintptr_t x, uintpt
     hipLaunchKernelGGL(k_cf_stem_wgrad<false>, dim3((int)nb, Nc / 64), dim3(CS_WG_THREADS), 0, s,
                        dy, reinterpret_cast<const float*>(x), slab, H, W, Nc, (int)M, none);
   EW_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_cf_stem_reduce, dim3((int)((n + 7) / 8)), dim3(EW_BLOCK), 0, s, slab,
-                     (int)nb, (int)n, reinterpret_cast<float*>(dw));
+  if (pend.slab) {
+    const int nb1 = (int)((n + 7) / 8);
+    hipLaunchKernelGGL(k_cf_reduce2, dim3(nb1 + (int)cf_reduce_grid(pend.n)), dim3(EW_BLOCK), 0,
+                       s, slab, (int)nb, (int)n, reinterpret_cast<float*>(dw), nb1, pend.slab,
+                       pend.split, pend.n, pend.out);
+  } else {
+    hipLaunchKernelGGL(k_cf_stem_reduce, dim3((int)((n + 7) / 8)), dim3(EW_BLOCK), 0, s, slab,
+                       (int)nb, (int)n, reinterpret_cast<float*>(dw));
+  }
   EW_CHECK_LAUNCH();
 }
 

@@ -117,6 +117,8 @@ void ew_adam_flat(const AdamFlatArgs& a);
 // returns the previous setting
 int ew_cf_set_glds(int on);
 int ew_cf_set_inred(int on);
+void ew_cf_defer_reduce();
+void ew_cf_flush_reduce();
 void ew_cf_arm_bn_fin(uintptr_t part, int nblk, int C, long long M, uintptr_t stats, uintptr_t coef,
                       uintptr_t dgamma, uintptr_t dbeta, uintptr_t dcbias, int cb_bf16);
 int ew_cf_flush_bn_fin(uintptr_t stream);

@@ -108,6 +108,8 @@ class _BNAct(torch.autograd.Function):
                                        or getattr(h, "_ew_stem_out", False))
                         and mode == "relu" and res is None and h.dtype == torch.float32)
         ctx.pool, ctx.mode = pool, mode
+        # h is the fp32 stem's output: the stem's backward follows this layer's (ops/conv.py)
+        ctx.stem_in = bool(getattr(h, "_ew_stem_out", False))
         ctx.res_sink = res_sink
         ctx.cb_dtype = None if cb is None else cb.dtype
         ctx.save_for_backward(h, res, code, stats)

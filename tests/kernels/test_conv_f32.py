@@ -541,6 +541,45 @@ def test_fp32_vgg11_step_vs_fp64():
     assert o_h <= 2 * o_m + 1e-6 and e_h <= 2 * e_m + 1e-5, (o_h, o_m, e_h, e_m)
 
 
+def test_vgg11_step_with_deferred_reduction_bitwise():
+    """Two fp32 VGG-11 training steps (production path) with conv2's split-K weight-gradient
+    reduction left to the stem's reduction launch (ops/csrc/conv_f32.hip k_cf_reduce2) and with
+    its own launch (EWDML_BN_FIN_RIDE off for it): bitwise the same weights and losses."""
+    from ewdml.models import build_model
+    from ewdml.ops import conv as cmod
+
+    _conv(wino=True, min_c=128, tile=2, sm=True)
+    torch.manual_seed(0)
+    m0 = build_model("vgg11", 10).to(memory_format=torch.channels_last).cuda()
+    for mod in m0.modules():
+        if isinstance(mod, torch.nn.Dropout):
+            mod.p = 0.0
+    x = torch.randn(128, 3, 32, 32, device="cuda").contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (128,), device="cuda")
+    runs = []
+    saved = cmod._FIN_RIDE
+    try:
+        for ride in (True, False):
+            cmod._FIN_RIDE = ride
+            m = copy.deepcopy(m0)
+            opt = torch.optim.SGD(m.parameters(), lr=0.05, momentum=0.9)
+            losses = []
+            for _ in range(2):
+                opt.zero_grad()
+                loss = F.cross_entropy(m(x), y)
+                loss.backward()  # (a pending reduction is run by the end-of-backward callback)
+                assert not cmod._STEM_RED[0]
+                opt.step()
+                losses.append(float(loss.detach()))
+            runs.append((m, losses))
+    finally:
+        cmod._FIN_RIDE = saved
+    (ma, la), (mb, lb) = runs
+    assert la == lb
+    for (k, a), b in zip(ma.state_dict().items(), mb.state_dict().values()):
+        assert torch.equal(a, b), k
+
+
 def test_fp32_vgg11_convs_in_situ():
     """Every MFMA conv backward of one fp32 VGG-11 step at batch 64 (the production path: lazy BN,
     Winograd conv3-6, small-map GEMMs for the 2x2 conv7 / conv8) against float64 on the tensors it
