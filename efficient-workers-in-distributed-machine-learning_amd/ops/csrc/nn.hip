@@ -310,7 +310,7 @@ __device__ __forceinline__ bool ew_act_pass(float v) {
   else return ew_relu_pass(v);
 }
 
-template <typename T, int MODE>
+template <typename T, int MODE, bool REGS = false>
 __global__ __launch_bounds__(EW_BLOCK) void k_bn_fwd_apply(const T* __restrict__ h,
                                                            const T* __restrict__ res,
                                                            T* __restrict__ y,
@@ -322,19 +322,41 @@ __global__ __launch_bounds__(EW_BLOCK) void k_bn_fwd_apply(const T* __restrict__
   float* lsc = ew_dyn_lds;
   float* lsh = ew_dyn_lds + C;
   if (nbt && blockIdx.x == 0 && threadIdx.x == 0) *nbt += 1;  // after the finalize read it
-  for (int c = threadIdx.x; c < C; c += EW_BLOCK) {
-    lsc[c] = stats[2 * C + c];
-    lsh[c] = stats[3 * C + c];
-  }
-  __syncthreads();
   const uint32_t tpr = C >> 3, HoWo = (uint32_t)Ho * Wo;
   const uint32_t nvec = (uint32_t)rows * tpr;
+  // C / 8 dividing the block (every power-of-two C <= 2048): the grid stride is a multiple of
+  // C / 8, so a thread keeps one 8-channel group -- its coefficients in registers, loaded once
+  // (the LDS copy read per vector had 2-way bank conflicts on every read)
+  const bool fixed = REGS && EW_BLOCK % tpr == 0;
+  float rsc[8], rsh[8];
+  if (fixed) {
+    const int c0 = (int)(threadIdx.x % tpr) * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      rsc[j] = stats[2 * C + c0 + j];
+      rsh[j] = stats[3 * C + c0 + j];
+    }
+  } else {
+    for (int c = threadIdx.x; c < C; c += EW_BLOCK) {
+      lsc[c] = stats[2 * C + c];
+      lsh[c] = stats[3 * C + c];
+    }
+    __syncthreads();
+  }
   for (uint32_t v = blockIdx.x * EW_BLOCK + threadIdx.x; v < nvec; v += gridDim.x * EW_BLOCK) {
     const uint32_t row = v / tpr;
     const int c0 = (int)(v - row * tpr) * 8;
     float sc[8], sh[8];
-    ew_lds8(lsc + c0, sc);
-    ew_lds8(lsh + c0, sh);
+    if (fixed) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        sc[j] = rsc[j];
+        sh[j] = rsh[j];
+      }
+    } else {
+      ew_lds8(lsc + c0, sc);
+      ew_lds8(lsh + c0, sh);
+    }
     if constexpr (MODE != EW_BN_RELU_POOL) {
       float x[8];
       V8<T>::ld(h + (long long)row * C + c0, x);
@@ -489,7 +511,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_bn_bwd_finalize(EwBnFin f) {
   ew_bn_bwd_fin_group<NS>(f, blockIdx.x, red);
 }
 
-template <typename T, int MODE>
+template <typename T, int MODE, bool REGS = false>
 __global__ __launch_bounds__(EW_BLOCK) void k_bn_bwd_apply(
     const T* __restrict__ h, const T* __restrict__ res, const T* __restrict__ dy,
     const uint8_t* __restrict__ code, const float* __restrict__ stats,
@@ -501,27 +523,54 @@ __global__ __launch_bounds__(EW_BLOCK) void k_bn_bwd_apply(
   float* lsh = lsc + C;
   float* le = lsh + C;
   float* lf = le + C;
-  for (int c = threadIdx.x; c < C; c += EW_BLOCK) {
-    lm[c] = stats[c];
-    lsc[c] = stats[2 * C + c];
-    lsh[c] = stats[3 * C + c];
-    le[c] = coef[c];
-    lf[c] = coef[C + c];
-  }
-  __syncthreads();
   const uint32_t tpr = C >> 3, HoWo = (uint32_t)Ho * Wo;
   const uint32_t nvec = (uint32_t)rows * tpr;
+  // a thread keeps one 8-channel group when C / 8 divides the block (k_bn_fwd_apply): its five
+  // coefficient vectors in registers instead of ten conflicting LDS reads per vector
+  const bool fixed = REGS && EW_BLOCK % tpr == 0;
+  float rmn[8], rsc[8], rsh[8], rce[8], rcf[8];
+  if (fixed) {
+    const int c0 = (int)(threadIdx.x % tpr) * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      rmn[j] = stats[c0 + j];
+      rsc[j] = stats[2 * C + c0 + j];
+      rsh[j] = stats[3 * C + c0 + j];
+      rce[j] = coef[c0 + j];
+      rcf[j] = coef[C + c0 + j];
+    }
+  } else {
+    for (int c = threadIdx.x; c < C; c += EW_BLOCK) {
+      lm[c] = stats[c];
+      lsc[c] = stats[2 * C + c];
+      lsh[c] = stats[3 * C + c];
+      le[c] = coef[c];
+      lf[c] = coef[C + c];
+    }
+    __syncthreads();
+  }
   for (uint32_t v = blockIdx.x * EW_BLOCK + threadIdx.x; v < nvec; v += gridDim.x * EW_BLOCK) {
     const uint32_t row = v / tpr;
     const int c0 = (int)(v - row * tpr) * 8;
     float d[8];
     V8<T>::ld(dy + (long long)row * C + c0, d);
     float mn[8], sc[8], sh[8], ce[8], cf[8];
-    ew_lds8(lm + c0, mn);
-    ew_lds8(lsc + c0, sc);
-    ew_lds8(lsh + c0, sh);
-    ew_lds8(le + c0, ce);
-    ew_lds8(lf + c0, cf);
+    if (fixed) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        mn[j] = rmn[j];
+        sc[j] = rsc[j];
+        sh[j] = rsh[j];
+        ce[j] = rce[j];
+        cf[j] = rcf[j];
+      }
+    } else {
+      ew_lds8(lm + c0, mn);
+      ew_lds8(lsc + c0, sc);
+      ew_lds8(lsh + c0, sh);
+      ew_lds8(le + c0, ce);
+      ew_lds8(lf + c0, cf);
+    }
     if constexpr (MODE != EW_BN_RELU_POOL) {
       float x[8], o[8], rr[8], dzs[8];
       V8<T>::ld(h + (long long)row * C + c0, x);
@@ -773,6 +822,18 @@ static int ew_grid_vec(long long nvec) {
 }
 
 
+// The apply kernels keep each thread's channel coefficients in registers (k_bn_fwd_apply /
+// k_bn_bwd_apply REGS) instead of reading the block's LDS copy (2-way bank conflicts) per vector:
+// VGG-11 1.1454 -> 1.1410 ms, ResNet-50 CIFAR 13.16 -> 13.13 ms despite the lower occupancy
+// (profiles/ab/README.md).  EWDML_BN_REGS=0: the LDS copy.
+static bool ew_bn_regs() {
+  static const bool on = [] {
+    const char* e = getenv("EWDML_BN_REGS");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // EWDML_BN_FIN_WIDE=0: every forward finalize at EW_BLOCK threads (A/B)
 static bool ew_fin_wide() {
   static const bool on = [] {
@@ -822,9 +883,14 @@ void ew_bn_relu_fwd(const BnFwdArgs& a) {
   const long long rows = a.pool ? a.N * (long long)Ho * Wo : M;
   const int grid = ew_grid_vec(rows * (C / 8));
 #define EW_FA(T, MODE)                                                                          \
-  hipLaunchKernelGGL((k_bn_fwd_apply<T, MODE>), dim3(grid), dim3(EW_BLOCK), lds, s,             \
-                     reinterpret_cast<const T*>(a.h), reinterpret_cast<const T*>(a.res),         \
-                     reinterpret_cast<T*>(a.y), code, st, rows, C, Ho, Wo, nbt)
+  if (ew_bn_regs())                                                                             \
+    hipLaunchKernelGGL((k_bn_fwd_apply<T, MODE, true>), dim3(grid), dim3(EW_BLOCK), lds, s,     \
+                       reinterpret_cast<const T*>(a.h), reinterpret_cast<const T*>(a.res),       \
+                       reinterpret_cast<T*>(a.y), code, st, rows, C, Ho, Wo, nbt);              \
+  else                                                                                          \
+    hipLaunchKernelGGL((k_bn_fwd_apply<T, MODE>), dim3(grid), dim3(EW_BLOCK), lds, s,           \
+                       reinterpret_cast<const T*>(a.h), reinterpret_cast<const T*>(a.res),       \
+                       reinterpret_cast<T*>(a.y), code, st, rows, C, Ho, Wo, nbt)
 #define EW_FA_MODES(T)                                                                          \
   switch (mode) {                                                                               \
     case EW_BN_RELU: EW_FA(T, EW_BN_RELU); break;                                               \
@@ -881,9 +947,14 @@ static void ew_bn_bwd_impl(const BnBwdArgs& a) {
   }
   EW_CHECK_LAUNCH();
   if (a.phase == 1) return;  // lazy: the producing conv's input transform forms dx (KIND 2)
-  hipLaunchKernelGGL((k_bn_bwd_apply<T, MODE>), dim3(ew_grid_vec(rows * (C / 8))),
-                     dim3(EW_BLOCK), 5 * sizeof(float) * C, s, h, res, dy, code, st, coef,
-                     reinterpret_cast<T*>(a.dx), reinterpret_cast<T*>(a.dres), rows, C, Ho, Wo);
+  if (ew_bn_regs())
+    hipLaunchKernelGGL((k_bn_bwd_apply<T, MODE, true>), dim3(ew_grid_vec(rows * (C / 8))),
+                       dim3(EW_BLOCK), 5 * sizeof(float) * C, s, h, res, dy, code, st, coef,
+                       reinterpret_cast<T*>(a.dx), reinterpret_cast<T*>(a.dres), rows, C, Ho, Wo);
+  else
+    hipLaunchKernelGGL((k_bn_bwd_apply<T, MODE>), dim3(ew_grid_vec(rows * (C / 8))),
+                       dim3(EW_BLOCK), 5 * sizeof(float) * C, s, h, res, dy, code, st, coef,
+                       reinterpret_cast<T*>(a.dx), reinterpret_cast<T*>(a.dres), rows, C, Ho, Wo);
   EW_CHECK_LAUNCH();
 }
 
