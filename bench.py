@@ -50,7 +50,7 @@ def parse(argv=None):
     p.add_argument("--preset", default="vgg11", choices=sorted(PRESETS),
                    help="BASELINE.json config (explicit flags override it)")
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=32)  # a multiple of --graph-unroll
+    p.add_argument("--steps", type=int, default=32)
     p.add_argument("--warmup", type=int, default=8)
     p.add_argument("--network", default=None)
     p.add_argument("--dataset", default=None)
@@ -71,9 +71,11 @@ def parse(argv=None):
     # with backward (segmented graphs) for large dense collectives at N > 1 (plan_graph_mode)
     p.add_argument("--hip-graph", default="auto",
                    choices=["auto", "off", "split", "full", "segmented"])
-    # steps per graph launch in the timed loop (Trainer.train_steps): the same steps, one launch
-    # boundary (~7.7 us, tools/probes/launch_floor.py) per U steps; 1 = one graph per step
-    p.add_argument("--graph-unroll", type=int, default=8)
+    # most steps per graph launch in the timed loop (Trainer.train_steps; the U <= this that needs
+    # the fewest launches for --steps): the same steps, one launch boundary (~7.7 us,
+    # tools/probes/launch_floor.py) per U steps; 1 = one graph per step.  16 vs 8: VGG-11 1.1401 /
+    # 1.1408 vs 1.1454 / 1.1470 ms (profiles/ab/README.md)
+    p.add_argument("--graph-unroll", type=int, default=16)
     p.add_argument("--param-dtype", default="auto", choices=["auto", "fp32"])
     p.add_argument("--json-out", default=None, help="also write the JSON line to this file")
     p.add_argument("--extra", default="", help="extra distributed_nn.py flags")
@@ -146,6 +148,18 @@ def _any_rank(flag: bool) -> bool:
     return bool(t.item() > 0)
 
 
+def _pick_unroll(steps: int, umax: int) -> int:
+    """Steps per graph launch for ``steps`` timed steps: the U <= umax that needs the fewest
+    launches (K // U replays of the U-step graph + K % U one-step replays), the larger U on a tie;
+    1 = one graph per step."""
+    best = (steps, 1)
+    for u in range(2, min(umax, steps) + 1):
+        n = steps // u + steps % u
+        if n < best[0] or (n == best[0] and u > best[1]):
+            best = (n, u)
+    return best[1]
+
+
 def _measure(a, tr, gw):
     import torch
 
@@ -161,7 +175,7 @@ def _measure(a, tr, gw):
     # --graph-unroll U (when the timed run holds at least one run of U steps): the U-step graph is
     # captured and replayed once as the last U warmup steps (at least gw + 1 one-step warmup steps
     # before it: the eager steps and the one-step capture)
-    unroll = a.graph_unroll if 1 < a.graph_unroll <= a.steps else 1
+    unroll = _pick_unroll(a.steps, a.graph_unroll)
     single = warm if unroll == 1 else max(gw + 1, warm - unroll)
     for _ in range(single):
         tr.train_step()

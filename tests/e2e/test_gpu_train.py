@@ -274,7 +274,7 @@ def _bench_pg(codec, comm, extra=(), env_extra=None):
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node",
                "1", "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py",
                "--gpus", "1", "--steps", "4", "--warmup", "4", "--batch-size", "64",
-               "--compress", codec, "--no-extras", *extra]
+               "--compress", codec, "--no-extras", "--graph-unroll", "1", *extra]
         r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=300)
         if not (r.returncode != 0 and "EADDRINUSE" in r.stderr and "failed to listen" in r.stderr):
             break
