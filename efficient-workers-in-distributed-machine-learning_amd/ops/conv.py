@@ -122,6 +122,7 @@ WO_RIDES = 0
 # reduction launch (ops/csrc/conv_f32.hip ew_cf_defer_reduce: the conv fed by the stem's BN layer,
 # whose backward runs next); flush_pending runs it before any gradient is read
 _STEM_RED = [False]
+STEM_RED_DEFERS = 0  # reductions left for the stem's launch (tests / diagnostics)
 _SM_WS = {}
 
 
@@ -726,8 +727,13 @@ class _Conv(torch.autograd.Function):
                     wsw = _ws(x.device)  # the current stream's slabs (the side stream's own)
                     # (like the deferred Winograd transforms, dw is then written after this
                     # backward returns: off with _DEFER_WOUT)
-                    if stem_next and side is None and _FIN_RIDE and _DEFER_WOUT:
+                    # only when dw is installed (not accumulated) and nothing but the engine's
+                    # hooks reads it before the flush: a flat-view .grad (PS / sharded
+                    # topologies), foreign hooks or autograd.grad callers need dw now
+                    if stem_next and side is None and _FIN_RIDE and _can_defer(ctx):
                         C_.cf_defer_reduce()  # its split-K reduction: in the stem's launch
+                        global STEM_RED_DEFERS
+                        STEM_RED_DEFERS += 1
                         if not _STEM_RED[0]:  # run at the latest when the backward pass ends
                             torch.autograd.Variable._execution_engine.queue_callback(_flush_final)
                         _STEM_RED[0] = True

@@ -253,6 +253,15 @@ class Comm:
     def irecv(self, t: torch.Tensor, src: int, tag: int = 0):
         return dist.irecv(t, src=src, group=self.group, tag=tag)
 
+    def batch_p2p(self, sends=(), recvs=()):
+        """Post point-to-point sends ``[(tensor, dst)]`` and receives ``[(tensor, src)]`` as ONE
+        group (``dist.batch_isend_irecv``) and return the Works.  With RCCL, p2p ops of one rank
+        pair share a communicator and stream: ungrouped, a recv posted before the matching send
+        on both sides waits for a send queued behind it (deadlock); grouped, RCCL pairs them."""
+        ops = [dist.P2POp(dist.irecv, t, src, group=self.group) for t, src in recvs]
+        ops += [dist.P2POp(dist.isend, t, dst, group=self.group) for t, dst in sends]
+        return dist.batch_isend_irecv(ops) if ops else []
+
     def recv_any(self, t: torch.Tensor, tag: int = 0) -> int:
         """Blocking receive from whichever rank sends first (Gloo); returns the sender."""
         return dist.recv(t, src=None, group=self.group, tag=tag)

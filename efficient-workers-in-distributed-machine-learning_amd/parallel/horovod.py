@@ -222,11 +222,10 @@ def adasum_tree(comm, g: torch.Tensor) -> torch.Tensor:
             return min(q, min(n, ((r // size ^ 1) + 1) * size) - 1)
 
         other = torch.empty_like(v)
-        reqs = [comm.irecv(other, src_of(rank), tag=100 + level)]
-        for r in range(lo, hi):  # the partner ranks that take their vector from me
-            if src_of(r) == rank:
-                reqs.append(comm.isend(v, r, tag=100 + level))
-        for q in reqs:
+        # the partner ranks that take their vector from me; the level's sends and receive are
+        # posted as one group (separate isend / irecv to one peer deadlock on RCCL)
+        sends = [(v, r) for r in range(lo, hi) if src_of(r) == rank]
+        for q in comm.batch_p2p(sends=sends, recvs=[(other, src_of(rank))]):
             q.wait()
         v = adasum_pair(v, other) if grp < pg else adasum_pair(other, v)
         level += 1

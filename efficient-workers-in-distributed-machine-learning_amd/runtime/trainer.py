@@ -471,6 +471,11 @@ class Trainer:
         mode = os.environ.get("EWDML_GRAPH_CAPTURE_MODE", "thread_local")
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
+        # the returned loss / logits live outside the shared pool: one-step replays interleaved
+        # with this graph's may reuse the blocks of its temporaries (PyTorch guarantees pool
+        # sharing only for replays in capture order), and a caller may still hold the values
+        keep = tuple(None if t is None else torch.empty_like(t)
+                     for t in (self._gloss, self._gout))
         try:
             # the one-step graph's pool: the two never run at once (same stream, in order)
             with torch.cuda.graph(g, pool=self._graphs[0].pool(), stream=self.gstream,
@@ -480,6 +485,8 @@ class Trainer:
                         self._gx, self._gy = self.loader.emit()
                         loss, out = self.forward_backward(self._gx, self._gy)
                         ex.finish()
+                    loss, out = (t if k is None else k.copy_(t)
+                                 for k, t in zip(keep, (loss, out)))
                 except BaseException:
                     self._rejoin_side()
                     raise

@@ -562,15 +562,20 @@ def test_vgg11_step_with_deferred_reduction_bitwise():
         for ride in (True, False):
             cmod._FIN_RIDE = ride
             m = copy.deepcopy(m0)
+            hs = _opt_in(list(m.parameters()))  # the engine's hooks: deferral allowed
             opt = torch.optim.SGD(m.parameters(), lr=0.05, momentum=0.9)
             losses = []
+            defers = cmod.STEM_RED_DEFERS
             for _ in range(2):
                 opt.zero_grad()
+                cmod.new_pass()
                 loss = F.cross_entropy(m(x), y)
                 loss.backward()  # (a pending reduction is run by the end-of-backward callback)
                 assert not cmod._STEM_RED[0]
                 opt.step()
                 losses.append(float(loss.detach()))
+            assert (cmod.STEM_RED_DEFERS > defers) == ride
+            _opt_out(list(m.parameters()), hs)
             runs.append((m, losses))
     finally:
         cmod._FIN_RIDE = saved
@@ -578,6 +583,48 @@ def test_vgg11_step_with_deferred_reduction_bitwise():
     assert la == lb
     for (k, a), b in zip(ma.state_dict().items(), mb.state_dict().values()):
         assert torch.equal(a, b), k
+
+
+def test_vgg11_flat_view_grads_never_defer_reduction():
+    """With the gradients pre-attached as views of one flat buffer (FlatModel(attach_grads=True),
+    the PS / sharded topologies) AccumulateGrad adds dw into .grad as soon as the conv's backward
+    returns it, so conv2's split-K reduction must not be left for the stem's launch: the
+    gradients (NaN-poisoned dw) are bitwise those of the run without any rider."""
+    from ewdml.models import build_model
+    from ewdml.ops import conv as cmod
+    from ewdml.parallel.flat import FlatModel
+
+    _conv(wino=True, min_c=128, tile=2, sm=True)
+    torch.manual_seed(0)
+    m0 = build_model("vgg11", 10).to(memory_format=torch.channels_last).cuda()
+    for mod in m0.modules():
+        if isinstance(mod, torch.nn.Dropout):
+            mod.p = 0.0
+    x = torch.randn(128, 3, 32, 32, device="cuda").contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (128,), device="cuda")
+    grads = []
+    saved = cmod._FIN_RIDE
+    try:
+        for ride in (True, False):
+            cmod._FIN_RIDE = ride
+            cmod._POISON_DW = True
+            m = copy.deepcopy(m0)
+            params = list(m.parameters())
+            flat = FlatModel(params, attach_grads=True)
+            hs = _opt_in(params)
+            flat.zero_grad()
+            cmod.new_pass()
+            defers = cmod.STEM_RED_DEFERS
+            F.cross_entropy(m(x), y).backward()
+            torch.cuda.synchronize()
+            assert cmod.STEM_RED_DEFERS == defers  # .grad was not None: no deferral
+            _opt_out(params, hs)
+            grads.append(flat.grad.clone())
+    finally:
+        cmod._FIN_RIDE = saved
+        cmod._POISON_DW = False
+    assert not torch.isnan(grads[0]).any()
+    assert torch.equal(grads[0], grads[1])
 
 
 def test_fp32_vgg11_convs_in_situ():
