@@ -125,9 +125,11 @@ class Codec:
     # -- encode / decode ----------------------------------------------------------------------
     def encode(self, b: int, grad: torch.Tensor, payload: torch.Tensor, step: int, rank: int,
                resid: torch.Tensor = None, key_tensor: torch.Tensor = None, dgc: dict = None,
-               ef21: bool = False):
+               ef21: bool = False, apply: dict = None):
         """Compress bucket ``b`` of the flat gradient (``grad`` = that bucket's view).  ``dgc``:
-        error feedback with momentum correction (top-k codecs; ``oracle.dgc_accumulate``)."""
+        error feedback with momentum correction (top-k codecs; ``oracle.dgc_accumulate``).
+        ``apply`` (GPU top-k, a world of one): the encode also applies the decoded update
+        (``ops.topk_encode``), so no decode launch follows."""
         if dgc is not None and (resid is None or self.kind not in ("topk", "topk_qsgd")):
             raise ValueError("momentum correction needs a top-k codec and a residual")
         plan, lay = self.plans[b], self.layouts[b]
@@ -143,8 +145,10 @@ class Codec:
                                 resid, key_tensor)
             else:
                 ops.topk_encode(self.dplans[b], grad, payload, lay, self.levels, self.norm, key,
-                                resid, key_tensor, dgc=dgc)
+                                resid, key_tensor, dgc=dgc, apply=apply)
             return
+        if apply is not None:
+            raise ValueError("the encode-side apply runs on the GPU codec only")
         if isinstance(grad, (list, tuple)):
             raise TypeError("CPU encode takes the bucket's flat gradient view")
         if self.kind == "qsgd":

@@ -206,9 +206,15 @@ def _keyp(key_tensor):
 
 
 def topk_encode(dp: DevicePlan, grad, payload, layout, levels: int, norm: str, key: int,
-                resid=None, key_tensor=None, dgc=None):
+                resid=None, key_tensor=None, dgc=None, apply=None):
     """``dgc``: momentum-corrected error feedback, ``{velocity, momentum, dampening, nesterov,
-    weight_decay, param}`` (bucket views; compress/oracle.py dgc_accumulate)."""
+    weight_decay, param}`` (bucket views; compress/oracle.py dgc_accumulate).
+
+    ``apply`` (a world of one, where the all-gathered payload is this rank's own): the write pass
+    also applies the update ``topk_decode_apply`` would with no momentum buffer --
+    ``{param, lr, lr_tensor, grad_scale, shadow, key_state, key_seed, key_rank}``: at each sent
+    coordinate p -= lr * grad_scale * sent (and the bf16 shadow), then the RNG key state moves to
+    the next step; bitwise the decode's result (tests/kernels/test_hip_codecs.py)."""
     C = require()
     ptrs, mask = grad_pointers(dp, grad)
     _check(payload, torch.uint8, "payload")
@@ -250,7 +256,23 @@ def topk_encode(dp: DevicePlan, grad, payload, layout, levels: int, norm: str, k
                   dp.plan.bucket_offset & 0xFFFFFFFF, _keyp(key_tensor), _stream(), _ptr(vel),
                   _ptr(par), mom, damp1, wd, nest, layout.bitmap, dmask, _lrp(lrt), dp.plan.length,
                   _ptr(dp.cblocks), dp.plan.num_cblocks, int(_TOPK_PREDICT), int(_LB_FAULT[0]),
-                  int(max(dp.plan.ks)) if dp.plan.ks else 0)
+                  int(max(dp.plan.ks)) if dp.plan.ks else 0, *_apply_args(dp, apply, norm))
+
+
+def _apply_args(dp, apply, norm):
+    if apply is None:
+        return (0, 0, 0.0, 0, 1.0, 0, 0, 0)
+    if not _TOPK_PREDICT or norm != "max":
+        raise ValueError("the write-pass apply needs the predictive (max-norm) encode")
+    param = apply["param"]
+    _check_bucket(dp, param, "param")
+    _check_shadow(dp, apply.get("shadow"))
+    ks = apply.get("key_state")
+    if ks is not None:
+        _check(ks, torch.int32, "key_state", align=4)
+    return (_ptr(param), _ptr(apply.get("shadow")), float(apply["lr"]),
+            _lrp(apply.get("lr_tensor")), float(apply.get("grad_scale", 1.0)), _ptr(ks),
+            int(apply.get("key_seed", 0)) & 0xFFFFFFFF, int(apply.get("key_rank", 0)) & 0xFFFFFFFF)
 
 
 def _lrp(lr_tensor):

@@ -33,8 +33,18 @@ PYBIND11_MODULE(_C, m) {
            uintptr_t param, float dgc_momentum, float dgc_damp1, float dgc_wd,
            int dgc_nesterov, int bitmap_off, int dgc_mask, uintptr_t dgc_lr_ptr,
            long long bucket_len, uintptr_t cblocks, int num_cblocks, int predict,
-           int lb_fault, int max_k) {
+           int lb_fault, int max_k, uintptr_t apply_param, uintptr_t apply_shadow,
+           float apply_lr, uintptr_t apply_lr_ptr, float apply_scale,
+           uintptr_t apply_key_state, uint32_t apply_key_seed, uint32_t apply_key_rank) {
           TopkEncodeArgs a{};
+          a.apply_param = apply_param;
+          a.apply_shadow = apply_shadow;
+          a.apply_lr = apply_lr;
+          a.apply_lr_ptr = apply_lr_ptr;
+          a.apply_scale = apply_scale;
+          a.apply_key_state = apply_key_state;
+          a.apply_key_seed = apply_key_seed;
+          a.apply_key_rank = apply_key_rank;
           a.lb_fault = lb_fault;
           a.max_k = max_k;
           a.bucket_len = bucket_len;
@@ -366,6 +376,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("sm_f32_fwd", &ew_sm_f32_fwd);
   m.def("sm_set_fence", &ew_sm_set_fence);
   m.def("topk_fused_select_max_blocks", &ew_topk_fused_select_max_blocks);
+  m.def("topk_one_max_blocks", &ew_topk_one_max_blocks);
+  m.def("topk_one_stamps", &ew_topk_one_stamps);
   m.def("sm_f32_bwd", &ew_sm_f32_bwd);
   m.def("lenet_ws_floats", &ew_lenet_ws_floats);
   m.def("lenet_counters", &ew_lenet_counters);

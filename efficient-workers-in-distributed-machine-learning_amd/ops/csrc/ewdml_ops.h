@@ -34,6 +34,13 @@ struct TopkEncodeArgs {
   int predict;
   int lb_fault;  // test hook: tensors' first chunks skip their look-back word (lb_err path)
   int max_k;     // largest per-tensor k of the bucket (0: unknown)
+  // world of one (the all-gather is this rank's payload): the write pass also applies the update
+  // the decode would, p -= lr * scale * sent at each sent coordinate (momentum-corrected error
+  // feedback: no receiver momentum); apply_param 0 = off.  apply_key_state: advance the RNG key
+  // state {step, key} after every block read the key (the last bucket's decode did it)
+  uintptr_t apply_param, apply_shadow, apply_lr_ptr, apply_key_state;
+  float apply_lr, apply_scale;
+  uint32_t apply_key_seed, apply_key_rank;
 };
 
 struct TopkDecodeArgs {
@@ -103,6 +110,8 @@ std::vector<int> ew_topk_stats(uintptr_t scratch, int num_tensors, int num_chunk
 std::vector<long long> ew_graph_info(uintptr_t graph, const std::string& dot_path);
 // largest candidate-block count the fused select kernel takes (0: always three kernels)
 int ew_topk_fused_select_max_blocks();
+int ew_topk_one_max_blocks();
+std::vector<unsigned long long> ew_topk_one_stamps();
 int ew_topk_lookback_errors(uintptr_t scratch, int num_tensors, int num_chunks);
 void ew_topk_encode(const TopkEncodeArgs& a);
 void ew_topk_decode_apply(const TopkDecodeArgs& a);

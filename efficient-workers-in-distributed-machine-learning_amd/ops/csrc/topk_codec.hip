@@ -26,6 +26,7 @@
 // The global state lives in one scratch block: zero-initialised once, histograms re-cleared by
 // k_topk_write after use, everything else fully rewritten per encode (no per-step memset).
 #include <cstdlib>
+#include <vector>
 
 #include "common.h"
 #include "ewdml_ops.h"
@@ -611,6 +612,33 @@ __device__ __forceinline__ void topk_lookback(uint32_t gt, uint32_t eq, const Ch
   __syncthreads();
 }
 
+// World of one: the update the decode of this rank's own payload would apply, done by the write
+// pass at each sent coordinate (k_topk_decode_sparse's arithmetic for one rank: acc = 0 + sent,
+// skipped where it is 0, p = p - lr * (acc * scale)); param null = off.
+struct TkApply {
+  float* param;
+  uint16_t* shadow;
+  SgdArgs sa;  // lr / lr_ptr (resolved on entry), grad_scale; momentum, decay 0
+  int* ticket;  // grid arrival ticket of the key advance (sa.key_state)
+};
+__device__ __forceinline__ void tk_apply_one(const TkApply& ap, size_t i, float sent) {
+  if (sent == 0.0f) return;  // the decode's zero accumulator: p - lr * 0 is p, bit for bit
+  float pv = ap.param[i], bz = 0.0f;
+  ew_sgd(pv, bz, sent * ap.sa.grad_scale, ap.sa);
+  ap.param[i] = pv;
+  if (ap.shadow) ap.shadow[i] = ew_f2bf(pv);
+}
+// after the block's last read of the key: the last block of the launch advances the key state
+__device__ __forceinline__ void tk_apply_done(const TkApply& ap) {
+  if (!ap.param || !ap.sa.key_state) return;
+  __syncthreads();
+  if (threadIdx.x == 0 && ew_grid_last(ap.ticket)) {
+    const uint32_t st = ap.sa.key_state[0] + 1u;
+    ap.sa.key_state[0] = st;
+    ap.sa.key_state[1] = ew_stream_key(ap.sa.key_seed, st, ap.sa.key_rank);
+  }
+}
+
 // Predictive encode, write pass of a tensor on the fast path: the chunk's candidates (every
 // element at or above the predicted threshold, which the fast path guarantees is <= the exact
 // one) were compacted by k_pk_hist0 in index order, so this block reads only them -- ~3 % of the
@@ -633,12 +661,8 @@ __device__ __forceinline__ void topk_write_cands(
     int idx_off, int codes_off, int bitmap_off, int counts_off, float levels, float inv_levels,
     uint32_t key, uint32_t bucket_offset, unsigned long long* __restrict__ lb,
     int* __restrict__ lb_err, uint32_t n, const uint2* __restrict__ cs, uint32_t* ws,
-    uint32_t* s_lb, int lb_fault) {
+    uint32_t* s_lb, int lb_fault, uint32_t thr, uint32_t need, float scale, const TkApply& ap) {
   __shared__ uint32_t bm[EW_BM_WORDS];
-  // the tensor's selection state, loaded together before the look-back's barriers
-  const uint32_t thr = state[c.tensor * 4];
-  const uint32_t need = state[c.tensor * 4 + 1];
-  const float scale = __uint_as_float(state[c.tensor * 4 + 2]);
   const uint32_t eend = (uint32_t)(tr.entry0 + tr.k);
   const bool bitmap = tr.bm0 >= 0;
   if (bitmap)
@@ -696,6 +720,7 @@ __device__ __forceinline__ void topk_write_cands(
       }
       if (vel) vel[c.start + li] = 0.0f;
       if (EF) resid[c.start + li] = x - sent;
+      if (ap.param) tk_apply_one(ap, (size_t)c.start + li, sent);
     }
     carry_gt += tot & 0xffffu;
     carry_eq += tot >> 16;
@@ -708,88 +733,16 @@ __device__ __forceinline__ void topk_write_cands(
   }
 }
 
-template <int VK, bool EF, bool LB, bool PK>
-__global__ __launch_bounds__(EW_BLOCK) void k_topk_write(
-    GradPtrs gp, float* __restrict__ resid, const ChunkRow* __restrict__ chunks,
-    const TensorRow* __restrict__ tensors, const uint32_t* __restrict__ state,
-    const uint32_t* __restrict__ chunk_off, const uint32_t* __restrict__ chunk_ties,
-    const float* __restrict__ inv_arr, uint8_t* __restrict__ payload, int scales_off, int idx_off,
-    int codes_off, int bitmap_off, float levels, float inv_levels, uint32_t key_arg,
-    const uint32_t* __restrict__ keyp,
-    uint32_t bucket_offset, uint32_t* __restrict__ rezero, uint32_t rezero_words,
-    float* __restrict__ vel, unsigned long long* __restrict__ lb, int counts_off,
-    int* __restrict__ lb_err, const uint32_t* __restrict__ pst,
-    const uint32_t* __restrict__ cbase, const uint32_t* __restrict__ ccnt,
-    const uint2* __restrict__ pcand, int lb_fault, uint32_t* __restrict__ rz1, uint32_t rz1_words,
-    uint32_t* __restrict__ rz2, uint32_t rz2_words) {
-  __shared__ uint32_t ws[EW_WAVES];
-  __shared__ uint32_t s_lb[2 * EW_WAVES];
-  // loads that depend on the block index alone first: the chunk row and (predictive encode) this
-  // chunk's candidate segment, in flight together; then the tensor's rows
-  const ChunkRow c = chunks[blockIdx.x];
-  const uint32_t pk_n = PK ? ccnt[blockIdx.x] : 0u, pk_b = PK ? cbase[blockIdx.x] : 0u;
-  // the histograms / max-key replicas are dead once the thresholds are selected: clear them here
-  // for the next encode of this bucket (replaces a per-step memset node; first use: zero-alloc).
-  // The predictive path uses one histogram copy per pass: three short ranges (rz1, rz2 too).
-  for (uint32_t i = blockIdx.x * EW_BLOCK + threadIdx.x; i < rezero_words; i += gridDim.x * EW_BLOCK)
-    rezero[i] = 0u;
-  if (PK) {
-    for (uint32_t i = blockIdx.x * EW_BLOCK + threadIdx.x; i < rz1_words; i += gridDim.x * EW_BLOCK)
-      rz1[i] = 0u;
-    for (uint32_t i = blockIdx.x * EW_BLOCK + threadIdx.x; i < rz2_words; i += gridDim.x * EW_BLOCK)
-      rz2[i] = 0u;
-  }
-  const uint32_t key = keyp ? *keyp : key_arg;  // device key: fresh per replay of a captured graph
-  const TensorRow tr = tensors[c.tensor];
-  if (PK && pst[c.tensor * 8 + 3]) {  // predictive fast path: the chunk's candidates only
-    topk_write_cands<VK, EF>(c, tr, resid, vel, state, payload, scales_off, idx_off, codes_off,
-                             bitmap_off, counts_off, levels, inv_levels, key, bucket_offset, lb,
-                             lb_err, pk_n, pcand + tr.cap0 + pk_b, ws, s_lb, lb_fault);
-    return;
-  }
-  const float* flat = EF ? resid : nullptr;  // EF: hist0 staged e = g + r in the residual
-  const uint32_t thr = state[c.tensor * 4];
-  const uint32_t eend = (uint32_t)(tr.entry0 + tr.k);  // never write past this tensor's entries
-  float4 v[EW_CU];
-  ew_ld_chunk(gp, flat, c, v);
-  uint32_t ties, ebase;
-  float inv, step = 0.0f;
-  if (LB) {
-    // this chunk's #(key > thr) and #(key == thr), then the exclusive prefix over the tensor's
-    // earlier chunks by decoupled look-back: the entry offset and the chunk's share of the
-    // threshold ties (lowest index first) without a counting pass
-    uint32_t gt = 0, eq = 0;
-#pragma unroll
-    for (int u = 0; u < EW_CU; ++u) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t k = ew_key(ew_f4(v[u], j));
-        const bool ok = ew_chunk_idx(u) + j < c.len;
-        gt += ok && k > thr;
-        eq += ok && k == thr;
-      }
-    }
-    topk_lookback(gt, eq, c, tr, lb, lb_err, s_lb, lb_fault);
-    // ties go to the lowest-index chunks: this chunk keeps what the earlier ones left of `need`
-    const uint32_t need = state[c.tensor * 4 + 1];
-    const uint32_t gb = s_lb[0], eb = s_lb[1], gtc = s_lb[2], eqc = s_lb[3];
-    const uint32_t left_ties = need > eb ? need - eb : 0u;
-    ties = left_ties < eqc ? left_ties : eqc;
-    ebase = (uint32_t)tr.entry0 + gb + (need < eb ? need : eb);
-    if (threadIdx.x == 0)
-      reinterpret_cast<uint16_t*>(payload + counts_off)[blockIdx.x] = (uint16_t)(gtc + ties);
-    // max-norm scale: the largest selected |e| is the tensor's max key (hist0)
-    const float scale = __uint_as_float(state[c.tensor * 4 + 2]);
-    inv = scale > 0.0f ? levels / scale : 0.0f;
-    if (VK != VK_F32) step = scale * inv_levels;
-    if (threadIdx.x == 0 && c.local == 0)
-      reinterpret_cast<float*>(payload + scales_off)[c.tensor] = topk_pub_scale(scale, lb_err);
-  } else {
-    ties = chunk_ties[blockIdx.x];
-    ebase = (uint32_t)tr.entry0 + chunk_off[blockIdx.x];
-    inv = inv_arr[c.tensor];
-    if (VK != VK_F32) step = reinterpret_cast<const float*>(payload + scales_off)[c.tensor] * inv_levels;
-  }
+// The ordered write of one chunk held in registers (v: the vector to compress, e under error
+// feedback), given its tensor's threshold key, this chunk's share of the threshold ties, its first
+// entry and the quantiser's scale factors: indices or bitmap words, codes, residual and velocity.
+template <int VK, bool EF>
+__device__ __forceinline__ void topk_write_chunk(
+    const ChunkRow& c, const TensorRow& tr, const float4 (&v)[EW_CU], float* __restrict__ resid,
+    float* __restrict__ vel, uint8_t* __restrict__ payload, int idx_off, int codes_off,
+    int bitmap_off, float levels, uint32_t key, uint32_t bucket_offset, uint32_t thr,
+    uint32_t ties, uint32_t ebase, uint32_t eend, float inv, float step, uint32_t* ws,
+    const TkApply& ap) {
   // entries' indices: the tensor's u16 list (chunk-local offsets), or its bitmap (one bit per
   // element; a wave's 256 elements of a slab are 8 whole words)
   const bool bitmap = tr.bm0 >= 0;
@@ -849,6 +802,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_write(
         // is e bit for bit, so only the sent coordinates are rewritten (a sparse store instead
         // of rewriting the whole bucket)
         if (EF) resid[c.start + i0 + j] = xs[j] - sent;
+        if (ap.param) tk_apply_one(ap, (size_t)c.start + i0 + j, sent);
         ++pos;
       }
     }
@@ -863,6 +817,118 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_write(
     carry_gt += tot & 0xffffu;
     carry_eq += tot >> 16;
   }
+}
+
+// The look-back write of one chunk held in registers (max-norm scale): this chunk's #(key > thr)
+// and #(key == thr), then the exclusive prefix over the tensor's earlier chunks by decoupled
+// look-back -- the entry offset and the chunk's share of the threshold ties (lowest index first)
+// without a counting pass -- then the ordered write.  need: the tensor's ties to keep; scale: its
+// max |e|.
+template <int VK, bool EF>
+__device__ __forceinline__ void topk_write_lb(
+    const ChunkRow& c, const TensorRow& tr, const float4 (&v)[EW_CU], float* __restrict__ resid,
+    float* __restrict__ vel, uint8_t* __restrict__ payload, int scales_off, int idx_off,
+    int codes_off, int bitmap_off, int counts_off, float levels, float inv_levels, uint32_t key,
+    uint32_t bucket_offset, unsigned long long* __restrict__ lb, int* __restrict__ lb_err,
+    uint32_t* s_lb, uint32_t* ws, int lb_fault, uint32_t thr, uint32_t need, float scale,
+    const TkApply& ap) {
+  const uint32_t eend = (uint32_t)(tr.entry0 + tr.k);  // never write past this tensor's entries
+  uint32_t gt = 0, eq = 0;
+#pragma unroll
+  for (int u = 0; u < EW_CU; ++u) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t k = ew_key(ew_f4(v[u], j));
+      const bool ok = ew_chunk_idx(u) + j < c.len;
+      gt += ok && k > thr;
+      eq += ok && k == thr;
+    }
+  }
+  topk_lookback(gt, eq, c, tr, lb, lb_err, s_lb, lb_fault);
+  // ties go to the lowest-index chunks: this chunk keeps what the earlier ones left of `need`
+  const uint32_t gb = s_lb[0], eb = s_lb[1], gtc = s_lb[2], eqc = s_lb[3];
+  const uint32_t left_ties = need > eb ? need - eb : 0u;
+  const uint32_t ties = left_ties < eqc ? left_ties : eqc;
+  const uint32_t ebase = (uint32_t)tr.entry0 + gb + (need < eb ? need : eb);
+  if (threadIdx.x == 0)
+    reinterpret_cast<uint16_t*>(payload + counts_off)[blockIdx.x] = (uint16_t)(gtc + ties);
+  // max-norm scale: the largest selected |e| is the tensor's max key (hist0)
+  const float inv = scale > 0.0f ? levels / scale : 0.0f;
+  const float step = VK != VK_F32 ? scale * inv_levels : 0.0f;
+  if (threadIdx.x == 0 && c.local == 0)
+    reinterpret_cast<float*>(payload + scales_off)[c.tensor] = topk_pub_scale(scale, lb_err);
+  topk_write_chunk<VK, EF>(c, tr, v, resid, vel, payload, idx_off, codes_off, bitmap_off, levels,
+                           key, bucket_offset, thr, ties, ebase, eend, inv, step, ws, ap);
+}
+
+template <int VK, bool EF, bool LB, bool PK>
+__global__ __launch_bounds__(EW_BLOCK) void k_topk_write(
+    GradPtrs gp, float* __restrict__ resid, const ChunkRow* __restrict__ chunks,
+    const TensorRow* __restrict__ tensors, const uint32_t* __restrict__ state,
+    const uint32_t* __restrict__ chunk_off, const uint32_t* __restrict__ chunk_ties,
+    const float* __restrict__ inv_arr, uint8_t* __restrict__ payload, int scales_off, int idx_off,
+    int codes_off, int bitmap_off, float levels, float inv_levels, uint32_t key_arg,
+    const uint32_t* __restrict__ keyp,
+    uint32_t bucket_offset, uint32_t* __restrict__ rezero, uint32_t rezero_words,
+    float* __restrict__ vel, unsigned long long* __restrict__ lb, int counts_off,
+    int* __restrict__ lb_err, const uint32_t* __restrict__ pst,
+    const uint32_t* __restrict__ cbase, const uint32_t* __restrict__ ccnt,
+    const uint2* __restrict__ pcand, int lb_fault, uint32_t* __restrict__ rz1, uint32_t rz1_words,
+    uint32_t* __restrict__ rz2, uint32_t rz2_words, TkApply ap) {
+  __shared__ uint32_t ws[EW_WAVES];
+  ew_sgd_resolve(ap.sa);
+  __shared__ uint32_t s_lb[2 * EW_WAVES];
+  // loads that depend on the block index alone first: the chunk row and (predictive encode) this
+  // chunk's candidate segment, in flight together; then the tensor's rows
+  const ChunkRow c = chunks[blockIdx.x];
+  const uint32_t pk_n = PK ? ccnt[blockIdx.x] : 0u, pk_b = PK ? cbase[blockIdx.x] : 0u;
+  // the histograms / max-key replicas are dead once the thresholds are selected: clear them here
+  // for the next encode of this bucket (replaces a per-step memset node; first use: zero-alloc).
+  // The predictive path uses one histogram copy per pass: three short ranges (rz1, rz2 too).
+  for (uint32_t i = blockIdx.x * EW_BLOCK + threadIdx.x; i < rezero_words; i += gridDim.x * EW_BLOCK)
+    rezero[i] = 0u;
+  if (PK) {
+    for (uint32_t i = blockIdx.x * EW_BLOCK + threadIdx.x; i < rz1_words; i += gridDim.x * EW_BLOCK)
+      rz1[i] = 0u;
+    for (uint32_t i = blockIdx.x * EW_BLOCK + threadIdx.x; i < rz2_words; i += gridDim.x * EW_BLOCK)
+      rz2[i] = 0u;
+  }
+  const uint32_t key = keyp ? *keyp : key_arg;  // device key: fresh per replay of a captured graph
+  const TensorRow tr = tensors[c.tensor];
+  if (PK && pst[c.tensor * 8 + 3]) {  // predictive fast path: the chunk's candidates only
+    // the tensor's selection state, loaded together before the look-back's barriers
+    topk_write_cands<VK, EF>(c, tr, resid, vel, state, payload, scales_off, idx_off, codes_off,
+                             bitmap_off, counts_off, levels, inv_levels, key, bucket_offset, lb,
+                             lb_err, pk_n, pcand + tr.cap0 + pk_b, ws, s_lb, lb_fault,
+                             state[c.tensor * 4], state[c.tensor * 4 + 1],
+                             __uint_as_float(state[c.tensor * 4 + 2]), ap);
+    tk_apply_done(ap);
+    return;
+  }
+  const float* flat = EF ? resid : nullptr;  // EF: hist0 staged e = g + r in the residual
+  const uint32_t thr = state[c.tensor * 4];
+  const uint32_t eend = (uint32_t)(tr.entry0 + tr.k);  // never write past this tensor's entries
+  float4 v[EW_CU];
+  ew_ld_chunk(gp, flat, c, v);
+  if (LB) {
+    topk_write_lb<VK, EF>(c, tr, v, resid, vel, payload, scales_off, idx_off, codes_off,
+                          bitmap_off, counts_off, levels, inv_levels, key, bucket_offset, lb,
+                          lb_err, s_lb, ws, lb_fault, thr, state[c.tensor * 4 + 1],
+                          __uint_as_float(state[c.tensor * 4 + 2]), ap);
+    tk_apply_done(ap);
+    return;
+  }
+  uint32_t ties, ebase;
+  float inv, step = 0.0f;
+  {
+    ties = chunk_ties[blockIdx.x];
+    ebase = (uint32_t)tr.entry0 + chunk_off[blockIdx.x];
+    inv = inv_arr[c.tensor];
+    if (VK != VK_F32) step = reinterpret_cast<const float*>(payload + scales_off)[c.tensor] * inv_levels;
+  }
+  topk_write_chunk<VK, EF>(c, tr, v, resid, vel, payload, idx_off, codes_off, bitmap_off, levels,
+                           key, bucket_offset, thr, ties, ebase, eend, inv, step, ws, ap);
+  tk_apply_done(ap);
 }
 
 // =============================================================================================
@@ -1031,30 +1097,53 @@ __device__ __forceinline__ void pk_select(const uint32_t* __restrict__ hist,
 // Tensor t's pass-2 tail (one thread): the exact threshold as an absolute key, the reset of the
 // pass-1 key count, and the next encode's candidate bound: beta x this threshold, beta steered so
 // the candidates stay between ~2k and 3/4 of the list.
-__device__ __forceinline__ void pk_predict(const TensorRow& tr, int t, uint32_t B,
-                                           uint32_t* __restrict__ state, uint32_t* __restrict__ pst,
-                                           int* __restrict__ cand_n) {
+// (beta_bits, had: pst[8 t + 1], pst[8 t + 4] as this encode found them, loaded by the caller)
+__device__ __forceinline__ void pk_predict_thr(const TensorRow& tr, int t, uint32_t thr,
+                                               uint32_t* __restrict__ pst,
+                                               int* __restrict__ cand_n, uint32_t M,
+                                               uint32_t fast, uint32_t beta_bits, uint32_t had,
+                                               uint32_t hi = 0xffffffffu) {
   cand_n[TICK_STRIDE * t] = 0;  // every block read n before it arrived
-  // written by this block's select just now (agent-scope load: not a stale L1 line)
-  const uint32_t thr = B + __hip_atomic_load(state + t * 4, __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(state + t * 4, thr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   // next encode's candidate bound: beta x this exact threshold, beta steered so the
   // candidates stay between ~2k and 3/4 of the list
-  const uint32_t M = pst[t * 8 + 2], fast = pst[t * 8 + 3], had = pst[t * 8 + 4];
-  float beta = __uint_as_float(pst[t * 8 + 1]);
+  float beta = __uint_as_float(beta_bits);
   if (!(beta > 0.0f)) beta = PK_BETA0;
   const uint32_t k = (uint32_t)tr.k, cap = (uint32_t)tr.cap;
   if (had) {
     if (!fast && M > cap) beta = beta + (1.0f - beta) * 0.5f;  // too many: tighter
     else if (!fast) beta = beta * 0.8f;                        // too few: the bound was above
-    else if (M > cap - cap / 4) beta = beta + (1.0f - beta) * 0.25f;
+    else if (M > min(cap - cap / 4, hi)) beta = beta + (1.0f - beta) * 0.25f;
     else if (M < 2u * k) beta = beta * 0.95f;
   }
   beta = fminf(fmaxf(beta, 0.25f), 0.99f);
   pst[t * 8 + 1] = __float_as_uint(beta);
-  pst[t * 8 + 0] = ew_key(__uint_as_float(thr) * beta);
+  // a tensor whose every element fits the candidate list (biases, small layers) takes them all:
+  // bound 0, always the fast path -- without error feedback such tensors' thresholds jump from
+  // step to step and a predicted bound above the k-th key sent the whole select launch through
+  // the full passes (LeNet no-EF: 1 tensor-encode in 11)
+  pst[t * 8 + 0] = cap >= (uint32_t)tr.numel ? 0u : ew_key(__uint_as_float(thr) * beta);
   pst[t * 8 + 4] = 1u;
+}
+
+// the same after a select whose state holds the threshold relative to B (made absolute here)
+__device__ __forceinline__ void pk_predict_mf(const TensorRow& tr, int t, uint32_t B,
+                                              uint32_t* __restrict__ state,
+                                              uint32_t* __restrict__ pst,
+                                              int* __restrict__ cand_n, uint32_t M,
+                                              uint32_t fast) {
+  // written by this block's select just now (agent-scope load: not a stale L1 line)
+  const uint32_t thr = B + __hip_atomic_load(state + t * 4, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(state + t * 4, thr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  pk_predict_thr(tr, t, thr, pst, cand_n, M, fast, pst[t * 8 + 1], pst[t * 8 + 4]);
+}
+
+// the same, M and the fast flag from pst (set by k_pk_hist0's tensor-last block: an earlier launch,
+// or this block)
+__device__ __forceinline__ void pk_predict(const TensorRow& tr, int t, uint32_t B,
+                                           uint32_t* __restrict__ state, uint32_t* __restrict__ pst,
+                                           int* __restrict__ cand_n) {
+  pk_predict_mf(tr, t, B, state, pst, cand_n, pst[t * 8 + 2], pst[t * 8 + 3]);
 }
 
 // Tensor t's three radix passes over its M <= PK_INLINE_MAX candidates in one block (LDS
@@ -1652,6 +1741,427 @@ __global__ __launch_bounds__(EW_BLOCK) void k_pk_select(
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Small buckets (every chunk block resident at once): the whole predictive encode as ONE launch.
+// The bucket's three launches (k_pk_hist0 -> k_pk_select -> k_topk_write) were each a chain of
+// dependent round trips over a few dozen blocks (LeNet: 53 chunks; ~40 us of encode for 1.7 MB):
+//   1. stage + compact candidates (k_pk_hist0's body; the staged chunk stays in registers);
+//   2. the tensor's last-arriving block selects the exact threshold over the candidates, staged
+//      in LDS (fast path), and publishes the tensor's generation word; when the prediction missed
+//      (the first encode, a jump), every block of the tensor joins three histogram passes over
+//      its own registers with a per-tensor barrier between them (k_pk_select's full path);
+//   3. each block writes its chunk (k_topk_write: candidates or registers, decoupled look-back
+//      over its tensor's earlier chunks, all resident).
+// Same selection, codes, ties, residual and velocity as the three launches, bit for bit.
+// Hand-offs (cdna_hip_programming.md Guideline 16; MI355X_MICROARCH.md's table, row 1): every
+// word another block reads -- candidates, select state, mode and generation words, look-back
+// words, histogram rows -- is written by agent-scope atomics or sc1 stores after the writer's
+// vmcnt drain and read by agent-scope (sc1) loads after the poll, plus an agent acquire.
+// ---------------------------------------------------------------------------------------------
+constexpr int PK1_LDS_KEYS = 10240;  // candidate keys the selecting block stages in LDS (40 KB):
+                                     // with the histograms ~73 KB, two blocks per CU
+constexpr int PK1_HSUB = 4;  // pass-0 sub-histograms (lanes t % 4): the candidates crowd the low
+                             // bins (just above the predicted bound), a same-address LDS atomic hot
+                             // spot
+
+// One digit select over an LDS histogram of NB bins, scanned from the top, state in LDS: the bin
+// holding the k_rem-th largest key (st[0] |= bin << shift; st[1] = what is left of k_rem).  The
+// same arithmetic as pk_select without its global state round trips.
+template <int NB>
+__device__ __forceinline__ void pk1_digit(const uint32_t* h, uint32_t* st, uint32_t shift,
+                                          uint32_t* ws) {
+  constexpr int PER = NB / EW_BLOCK;
+  const uint32_t k_rem = st[1], prefix = st[0];
+  uint32_t cnt[PER], tsum = 0;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    cnt[j] = h[NB - 1 - (threadIdx.x * PER + j)];
+    tsum += cnt[j];
+  }
+  uint32_t total;
+  const uint32_t excl = ew_block_excl_scan(tsum, ws, total);  // (its barriers: k_rem read by all)
+  if (excl < k_rem && k_rem <= excl + tsum) {
+    uint32_t run = excl;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      if (run + cnt[j] >= k_rem) {
+        st[0] = prefix | ((uint32_t)(NB - 1 - (threadIdx.x * PER + j)) << shift);
+        st[1] = k_rem - run;
+        break;
+      }
+      run += cnt[j];
+    }
+  }
+  __syncthreads();
+}
+
+// Tensor t's three radix passes over its M candidates (keys in .x of pcand) in one block: keys
+// [0, nl) from LDS (staged there first), the rest from the list (sc1 loads); histograms and the
+// select state in LDS; the same digits and selects as pk_inline_select / the candidate-pass
+// kernels.  Leaves the absolute threshold key in st[0] and the ties to keep in st[1], and stores
+// the tensor's select state {threshold, ties, max key} once.
+__device__ __forceinline__ void pk1_select_cands(const uint2* __restrict__ cands, uint32_t M,
+                                                 uint32_t B, uint32_t s0, uint32_t s1,
+                                                 uint32_t kmax, uint32_t k, uint32_t* keys,
+                                                 uint32_t nl, uint32_t* h, uint32_t* st,
+                                                 uint32_t* ws, uint32_t* __restrict__ state,
+                                                 int t) {
+  constexpr int R = 16;  // loads in flight per thread (each an L2 round trip)
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(cands);
+  for (uint32_t b0 = 0; b0 < nl; b0 += EW_BLOCK * R) {
+    uint32_t kv[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const uint32_t i = min(b0 + r * EW_BLOCK + threadIdx.x, nl - 1);
+      kv[r] = __hip_atomic_load(src + 2 * i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const uint32_t i = b0 + r * EW_BLOCK + threadIdx.x;
+      if (i < nl) keys[i] = kv[r] & 0x7fffffffu;
+    }
+  }
+  uint32_t* h0 = h + (threadIdx.x & (PK1_HSUB - 1));
+  auto add = [&](int p, uint32_t want, uint32_t key) {
+    const uint32_t rel = key - B;
+    if (p == 0) atomicAdd(&h0[(rel >> s0) * PK1_HSUB], 1u);
+    else if (p == 1) {
+      if ((rel >> s0) == want) atomicAdd(&h[(rel >> s1) & ((1u << (s0 - s1)) - 1u)], 1u);
+    } else if ((rel >> s1) == want) {
+      atomicAdd(&h[rel & ((1u << s1) - 1u)], 1u);
+    }
+  };
+  auto pass = [&](int p, uint32_t want) {
+    const int nb = p == 0 ? NB0 * PK1_HSUB : NB1;
+    for (int i = threadIdx.x; i < nb; i += EW_BLOCK) h[i] = 0;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nl; i += EW_BLOCK) add(p, want, keys[i]);
+    for (uint32_t b0 = nl; b0 < M; b0 += EW_BLOCK * R) {  // beyond the LDS copy: batched loads
+      uint32_t kv[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const uint32_t i = min(b0 + r * EW_BLOCK + threadIdx.x, M - 1);
+        kv[r] = __hip_atomic_load(src + 2 * i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        if (b0 + r * EW_BLOCK + threadIdx.x < M) add(p, want, kv[r] & 0x7fffffffu);
+    }
+    __syncthreads();
+  };
+  if (threadIdx.x == 0) {
+    st[0] = 0u;
+    st[1] = k;
+  }
+  pass(0, 0u);  // (its barriers order st's initialisation before the digit select)
+  {  // fold the sub-histograms into bins 0..NB0-1 (all read before any is overwritten)
+    constexpr int PER = NB0 / EW_BLOCK;
+    uint32_t x[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int i = threadIdx.x + j * EW_BLOCK;
+      x[j] = 0;
+#pragma unroll
+      for (int q = 0; q < PK1_HSUB; ++q) x[j] += h[i * PK1_HSUB + q];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < PER; ++j) h[threadIdx.x + j * EW_BLOCK] = x[j];
+    __syncthreads();
+  }
+  pk1_digit<NB0>(h, st, s0, ws);
+  pass(1, st[0] >> s0);
+  pk1_digit<NB1>(h, st, s1, ws);
+  pass(2, st[0] >> s1);
+  pk1_digit<NB2>(h, st, 0u, ws);
+  if (threadIdx.x == 0) {
+    st[0] += B;  // absolute threshold key
+    __hip_atomic_store(state + t * 4, st[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(state + t * 4 + 1, st[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(state + t * 4 + 2, kmax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// the tensor's generation word moved to >= g (block-uniform; bounded poll, then an acquire)
+__device__ __forceinline__ void pk1_wait(const uint32_t* gen, uint32_t g, int* err, uint32_t* s_gen) {
+  pk_wait(gen, g, err, s_gen);
+}
+
+template <int EFM, int VK, bool EF>
+__global__ __launch_bounds__(EW_BLOCK) void k_pk_one(
+    GradPtrs gp, DgcArgs dg, unsigned long long* __restrict__ lb, float* __restrict__ resid,
+    const ChunkRow* __restrict__ chunks, uint32_t* __restrict__ kmaxr, int T,
+    const TensorRow* __restrict__ tensors, uint32_t* __restrict__ pst, int* __restrict__ tick,
+    int* __restrict__ ccount, uint2* __restrict__ pcand, int* __restrict__ stats,
+    uint32_t* __restrict__ state, int* __restrict__ cand_n, uint32_t* __restrict__ gen,
+    uint32_t* __restrict__ mode, uint32_t* __restrict__ hist0, uint32_t* __restrict__ hist1,
+    uint32_t* __restrict__ hist2, int* __restrict__ lb_err, uint8_t* __restrict__ payload,
+    int scales_off, int idx_off, int codes_off, int bitmap_off, int counts_off, float levels,
+    float inv_levels, uint32_t key_arg, const uint32_t* __restrict__ keyp, uint32_t bucket_offset,
+    int lb_fault, uint32_t lds_keys, unsigned long long* __restrict__ stamps, TkApply ap) {
+  extern __shared__ uint32_t s_dyn[];  // select: histogram + staged keys; full passes: histograms
+  // stamps (probes, EWDML_PK1_STAMPS=1): thread 0 stamps wall_clock64() at the phase boundaries
+#define PK1_STAMP(i) \
+  if (stamps && threadIdx.x == 0) stamps[(size_t)blockIdx.x * 8 + (i)] = wall_clock64()
+  PK1_STAMP(0);
+  __shared__ unsigned long long ws2[2 * EW_WAVES];
+  __shared__ uint32_t wmax[EW_WAVES];
+  __shared__ uint32_t ws[EW_WAVES];
+  __shared__ uint32_t s_lb[2 * EW_WAVES];
+  __shared__ uint32_t s_u[7];  // base of this chunk's candidates; tensor-last: fast, B, s0, s1, M,
+                              // max key
+  __shared__ uint32_t s_st[2];  // the select's {prefix, k_rem}
+  __shared__ int s_flag;
+  __shared__ uint32_t s_gen;
+  const ChunkRow c = chunks[blockIdx.x];
+  const int t = c.tensor;
+  const TensorRow tr = tensors[t];
+  uint32_t* gn = gen + TICK_STRIDE * t;
+  int* arr = tick + TICK_STRIDE * (T + t);  // the full passes' arrival count
+  // the generation moves only after every block of the tensor arrived: read before arriving
+  const uint32_t g0 = __hip_atomic_load(gn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // this chunk's look-back word starts unpublished; its successors read it after the tensor's
+  // select (they wait for the generation, which moves after this block arrived)
+  if (threadIdx.x == 0)
+    __hip_atomic_store(lb + blockIdx.x, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t key = keyp ? *keyp : key_arg;
+  ew_sgd_resolve(ap.sa);
+  // ---- 1. stage (error feedback) and compact the candidates (k_pk_hist0) ----
+  float4 v[EW_CU];
+  ew_ld_chunk(gp, nullptr, c, v);
+  topk_ef_stage<EFM>(gp, dg, resid, c, v);
+  // the previous launch's prediction (and its steering state, for the tensor-last block)
+  const uint32_t P = pst[t * 8], pbeta = pst[t * 8 + 1], phad = pst[t * 8 + 4];
+  PK1_STAMP(1);
+  uint32_t kmax = 0;
+  unsigned long long pa = 0, pb = 0;
+#pragma unroll
+  for (int u = 0; u < EW_CU; ++u) {
+    uint32_t n = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (ew_chunk_idx(u) + j < c.len) {
+        const uint32_t k = ew_key(ew_f4(v[u], j));
+        kmax = max(kmax, k);
+        n += k >= P;
+      }
+    }
+    if (u < 4) pa |= (unsigned long long)n << (16 * u);
+    else pb |= (unsigned long long)n << (16 * (u - 4));
+  }
+  kmax = ew_wave_max_u(kmax);
+  if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = kmax;
+  unsigned long long ta, tb;
+  pk_scan2(pa, pb, ws2, ta, tb);
+  uint32_t start[EW_CU];
+  uint32_t run = 0;
+#pragma unroll
+  for (int u = 0; u < EW_CU; ++u) {
+    start[u] = run;
+    run += (uint32_t)(((u < 4 ? ta : tb) >> (16 * (u & 3))) & 0xffffull);
+  }
+  const uint32_t tot = run;
+  if (threadIdx.x == 0) {
+    uint32_t m = wmax[0];
+    for (int w = 1; w < EW_WAVES; ++w) m = max(m, wmax[w]);
+    atomicMax(&kmaxr[(blockIdx.x & (NREP - 1)) * T + t], m);
+    s_u[0] = tot ? (uint32_t)atomicAdd(ccount + TICK_STRIDE * t, (int)tot) : 0u;
+  }
+  __syncthreads();
+  const uint32_t cbase0 = s_u[0];
+  if (tot) {
+    uint2* dst = pcand + tr.cap0;
+    const uint32_t cap = (uint32_t)tr.cap;
+#pragma unroll
+    for (int u = 0; u < EW_CU; ++u) {
+      uint32_t pos = cbase0 + start[u] +
+                     (uint32_t)(((u < 4 ? pa : pb) >> (16 * (u & 3))) & 0xffffull);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int i = ew_chunk_idx(u) + j;
+        const float x = ew_f4(v[u], j);
+        if (i < c.len && ew_key(x) >= P) {
+          if (pos < cap)
+            __hip_atomic_store(reinterpret_cast<unsigned long long*>(dst + pos),
+                               (unsigned long long)__float_as_uint(x) |
+                                   ((unsigned long long)(c.local * EW_CHUNK + i) << 32),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ++pos;
+        }
+      }
+    }
+  }
+  // ---- 2. the tensor's select ----
+  PK1_STAMP(2);
+  if (topk_tensor_last(tick + TICK_STRIDE * t, tr.nchunks, reinterpret_cast<int*>(wmax))) {
+    PK1_STAMP(6);
+    if (threadIdx.x == 0) {
+      int* cc = ccount + TICK_STRIDE * t;
+      // the candidate count and the max-key replicas: all loads in flight together
+      uint32_t kr[NREP];
+#pragma unroll
+      for (int r = 0; r < NREP; ++r)
+        kr[r] = __hip_atomic_load(kmaxr + r * T + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t M = (uint32_t)__hip_atomic_load(cc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(cc, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t fast = M >= (uint32_t)tr.k && M <= (uint32_t)tr.cap;
+      uint32_t B = 0u, s0 = 20u, s1 = 10u;
+      if (fast) {
+        uint32_t km = 0;
+#pragma unroll
+        for (int r = 0; r < NREP; ++r) km = max(km, kr[r]);
+        s_u[6] = km;
+        B = P;
+        const uint32_t span = km - P;
+        const int bl = span ? 32 - __clz(span) : 0;
+        s0 = bl > 11 ? (uint32_t)(bl - 11) : 0u;
+        s1 = s0 > 10 ? s0 - 10 : 0u;
+      }
+      // M is read back by the full passes' last block (maybe another block): agent-scope
+      __hip_atomic_store(pst + t * 8 + 2, M, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      pst[t * 8 + 3] = fast;
+      pst[t * 8 + 5] = B;
+      pst[t * 8 + 6] = s0;
+      pst[t * 8 + 7] = s1;
+      atomicAdd(stats + (fast ? 0 : 1), 1);
+      s_u[1] = fast;
+      s_u[2] = B;
+      s_u[3] = s0;
+      s_u[4] = s1;
+      s_u[5] = M;
+    }
+    __syncthreads();
+    const uint32_t fast = s_u[1], M = s_u[5];
+    if (fast) {
+      pk1_select_cands(pcand + tr.cap0, M, s_u[2], s_u[3], s_u[4], s_u[6], (uint32_t)tr.k,
+                       s_dyn + NB0 * PK1_HSUB, min(M, lds_keys), s_dyn, s_st, ws, state, t);
+      if (threadIdx.x == 0) {
+        // candidates steered to fit the LDS copy (7/8 of it), not only 3/4 of the list
+        pk_predict_thr(tr, t, s_st[0], pst, cand_n, M, 1u, pbeta, phad, lds_keys - lds_keys / 8);
+        for (int r = 0; r < NREP; ++r)  // dead once the max is in the select state
+          __hip_atomic_store(kmaxr + r * T + t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    if (threadIdx.x == 0)
+      __hip_atomic_store(mode + TICK_STRIDE * t, fast, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    PK1_STAMP(7);
+    pk_publish(arr, gn, g0 + 1u);  // (arr: zero already; rewritten to zero)
+  } else {
+    pk1_wait(gn, g0 + 1u, lb_err, &s_gen);
+  }
+  __syncthreads();
+  const bool fast = __hip_atomic_load(mode + TICK_STRIDE * t, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT) != 0u;
+  if (!fast) {
+    // ---- 2'. the prediction missed: three radix passes over the tensor, every block over its
+    // own registers (k_pk_select's full path: key bits [30:20], [19:10], [9:0]) ----
+    constexpr int HSUB = 4;
+    uint32_t* hs = s_dyn;
+    auto flush = [&](uint32_t* dstrow, int nb, int sub) {
+      __syncthreads();
+      for (int i = threadIdx.x; i < nb; i += EW_BLOCK) {
+        uint32_t x = 0;
+        for (int q = 0; q < sub; ++q) x += hs[i * sub + q];
+        if (x) atomicAdd(&dstrow[i], x);
+      }
+    };
+    // pass 0
+    for (int i = threadIdx.x; i < NB0 * HSUB; i += EW_BLOCK) hs[i] = 0;
+    __syncthreads();
+    {
+      uint32_t* h = hs + (threadIdx.x & (HSUB - 1));
+#pragma unroll
+      for (int u = 0; u < EW_CU; ++u)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (ew_chunk_idx(u) + j < c.len) atomicAdd(&h[(ew_key(ew_f4(v[u], j)) >> 20) * HSUB], 1u);
+    }
+    flush(hist0 + (size_t)t * NB0, NB0, HSUB);
+    if (pk_arrive(arr, tr.nchunks, &s_flag)) {
+      pk_select<NB0, true>(hist0, tensors, state, kmaxr, T, t, 20u);
+      __syncthreads();
+      for (int i = threadIdx.x; i < NB0; i += EW_BLOCK) hist0[(size_t)t * NB0 + i] = 0u;
+      if (threadIdx.x < NREP)
+        __hip_atomic_store(kmaxr + threadIdx.x * T + t, 0u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      pk_publish(arr, gn, g0 + 2u);
+    } else {
+      pk1_wait(gn, g0 + 2u, lb_err, &s_gen);
+    }
+    // pass 1
+    __syncthreads();
+    uint32_t want = __hip_atomic_load(state + t * 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 20;
+    for (int i = threadIdx.x; i < NB1; i += EW_BLOCK) hs[i] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < EW_CU; ++u)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t k = ew_key(ew_f4(v[u], j));
+        if (ew_chunk_idx(u) + j < c.len && (k >> 20) == want) atomicAdd(&hs[(k >> 10) & 1023u], 1u);
+      }
+    flush(hist1 + (size_t)t * NB1, NB1, 1);
+    if (pk_arrive(arr, tr.nchunks, &s_flag)) {
+      pk_select<NB1, false>(hist1, tensors, state, kmaxr, T, t, 10u);
+      __syncthreads();
+      for (int i = threadIdx.x; i < NB1; i += EW_BLOCK) hist1[(size_t)t * NB1 + i] = 0u;
+      pk_publish(arr, gn, g0 + 3u);
+    } else {
+      pk1_wait(gn, g0 + 3u, lb_err, &s_gen);
+    }
+    // pass 2
+    __syncthreads();
+    want = __hip_atomic_load(state + t * 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 10;
+    for (int i = threadIdx.x; i < NB2; i += EW_BLOCK) hs[i] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < EW_CU; ++u)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t k = ew_key(ew_f4(v[u], j));
+        if (ew_chunk_idx(u) + j < c.len && (k >> 10) == want) atomicAdd(&hs[k & 1023u], 1u);
+      }
+    flush(hist2 + (size_t)t * NB2, NB2, 1);
+    if (pk_arrive(arr, tr.nchunks, &s_flag)) {
+      pk_select<NB2, false>(hist2, tensors, state, kmaxr, T, t, 0u);
+      __syncthreads();
+      for (int i = threadIdx.x; i < NB2; i += EW_BLOCK) hist2[(size_t)t * NB2 + i] = 0u;
+      if (threadIdx.x == 0) {
+        const uint32_t M = __hip_atomic_load(pst + t * 8 + 2, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t thr = __hip_atomic_load(state + t * 4, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);  // (B = 0: absolute)
+        pk_predict_thr(tr, t, thr, pst, cand_n, M, 0u, pbeta, phad);
+      }
+      pk_publish(arr, gn, g0 + 4u);
+    } else {
+      pk1_wait(gn, g0 + 4u, lb_err, &s_gen);
+    }
+    __syncthreads();
+  }
+  PK1_STAMP(3);
+  // ---- 3. the ordered write of this chunk ----
+  const uint32_t thr = __hip_atomic_load(state + t * 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t need = __hip_atomic_load(state + t * 4 + 1, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+  const float scale = __uint_as_float(__hip_atomic_load(state + t * 4 + 2, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT));
+  float* velm = dg.mask ? dg.vel : nullptr;
+  if (fast) {
+    topk_write_cands<VK, EF>(c, tr, resid, velm, state, payload, scales_off, idx_off, codes_off,
+                             bitmap_off, counts_off, levels, inv_levels, key, bucket_offset, lb,
+                             lb_err, tot, pcand + tr.cap0 + cbase0, ws, s_lb, lb_fault, thr, need,
+                             scale, ap);
+  } else {
+    topk_write_lb<VK, EF>(c, tr, v, resid, velm, payload, scales_off, idx_off, codes_off,
+                          bitmap_off, counts_off, levels, inv_levels, key, bucket_offset, lb,
+                          lb_err, s_lb, ws, lb_fault, thr, need, scale, ap);
+  }
+  tk_apply_done(ap);
+  PK1_STAMP(4);
+#undef PK1_STAMP
+}
+
 // Value of payload entry `pe` (fp32 value, or the int8 / int4 QSGD code as a float).
 template <int VK>
 __device__ __forceinline__ float ew_topk_code(const uint8_t* pay, int codes_off, uint32_t pe) {
@@ -2070,6 +2580,58 @@ static int ew_pk_fused_max_blocks() {
 
 int ew_topk_fused_select_max_blocks() { return ew_pk_fused_max_blocks(); }
 
+// dynamic LDS of k_pk_one: the select's histogram + staged keys, or the full passes' histograms
+constexpr size_t PK1_DYN_BYTES = 4 * (size_t)(NB0 * PK1_HSUB + PK1_LDS_KEYS);
+
+// Largest bucket (in chunks) encoded by the one-launch kernel k_pk_one: its per-tensor waits and
+// look-backs wait for peers of the same launch, so every block must be resident -- one block per
+// CU, and only when the occupancy API reports room for two (as ew_pk_fused_max_blocks).
+// EWDML_TOPK_ONE=0: never (the three launches).
+static int ew_pk_one_max_blocks() {
+  static int n = -1;
+  if (n < 0) {
+    const char* e = std::getenv("EWDML_TOPK_ONE");
+    int dev = 0, cus = 0, occ = 0;
+    EW_CHECK(hipGetDevice(&dev));
+    EW_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    EW_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &occ, reinterpret_cast<const void*>(&k_pk_one<EF_DGC, VK_Q8, true>), EW_BLOCK,
+        PK1_DYN_BYTES));
+    n = ((e && e[0] == '0') || occ < 2) ? 0 : cus;
+  }
+  return n;
+}
+
+int ew_topk_one_max_blocks() { return ew_pk_one_max_blocks(); }
+
+// EWDML_PK1_STAMPS=1 (probes): k_pk_one's per-block phase stamps, 8 u64 per block, of the last
+// launch (tools/probes/encode_probe.py reads them with topk_one_stamps)
+static unsigned long long* g_pk1_stamps = nullptr;
+static int g_pk1_stamp_blocks = 0;
+static unsigned long long* ew_pk1_stamps(int C) {
+  static const bool on = [] {
+    const char* e = std::getenv("EWDML_PK1_STAMPS");
+    return e && e[0] == '1';
+  }();
+  if (!on) return nullptr;
+  if (C > g_pk1_stamp_blocks) {
+    if (g_pk1_stamps) EW_CHECK(hipFree(g_pk1_stamps));
+    EW_CHECK(hipMalloc(&g_pk1_stamps, (size_t)C * 8 * sizeof(unsigned long long)));
+    EW_CHECK(hipMemset(g_pk1_stamps, 0, (size_t)C * 8 * sizeof(unsigned long long)));
+    g_pk1_stamp_blocks = C;
+  }
+  return g_pk1_stamps;
+}
+
+std::vector<unsigned long long> ew_topk_one_stamps() {
+  std::vector<unsigned long long> out((size_t)g_pk1_stamp_blocks * 8);
+  if (g_pk1_stamps) {
+    EW_CHECK(hipDeviceSynchronize());
+    EW_CHECK(hipMemcpy(out.data(), g_pk1_stamps, out.size() * 8, hipMemcpyDeviceToHost));
+  }
+  return out;
+}
+
 // Most candidates a tensor may have for k_pk_hist0's tensor-last block to select over them itself
 static uint32_t ew_pk_inline_max() {
   static long long n = -1;
@@ -2108,7 +2670,9 @@ void ew_topk_encode(const TopkEncodeArgs& a) {
   int* cand_n = tick + 4 * TICK_STRIDE * T;
   int* lb_err = cand_n + TICK_STRIDE * T;
   int* pk_stats = lb_err + 2;  // predictive encode: tensor-encodes on the fast / full path
-  auto* lb = reinterpret_cast<unsigned long long*>(lb_err + TICK_STRIDE);
+  // the write-pass apply's grid arrival ticket (ew_grid_last: 9 lines, left zeroed)
+  int* apply_ticket = lb_err + TICK_STRIDE;
+  auto* lb = reinterpret_cast<unsigned long long*>(apply_ticket + 9 * TICK_STRIDE);
   uint32_t* cand = reinterpret_cast<uint32_t*>(lb + C);
   if (a.bucket_len <= 0) throw std::runtime_error("ewdml topk: bucket length missing");
   // predictive encode state after the candidate keys: pstate u32[8 T] | chunk candidate base and
@@ -2138,6 +2702,19 @@ void ew_topk_encode(const TopkEncodeArgs& a) {
     throw std::runtime_error("ewdml topk: weight decay in the momentum correction needs params");
   auto* pay = reinterpret_cast<uint8_t*>(a.payload);
   const bool pk = a.predict && !a.norm_l2 && a.cblocks && a.num_cblocks > 0;
+  TkApply ap{};
+  if (a.apply_param) {
+    if (!pk) throw std::runtime_error("ewdml topk: the write-pass apply needs the predictive encode");
+    ap.param = reinterpret_cast<float*>(a.apply_param);
+    ap.shadow = reinterpret_cast<uint16_t*>(a.apply_shadow);
+    ap.sa.lr = a.apply_lr;
+    ap.sa.lr_ptr = reinterpret_cast<const float*>(a.apply_lr_ptr);
+    ap.sa.grad_scale = a.apply_scale;
+    ap.sa.key_state = reinterpret_cast<uint32_t*>(a.apply_key_state);
+    ap.sa.key_seed = a.apply_key_seed;
+    ap.sa.key_rank = a.apply_key_rank;
+    ap.ticket = apply_ticket;
+  }
   if (pk) {
     // predictive path: hist0 (+ candidates) -> 3 radix passes over the candidates -> write.
     // Its passes use histogram copy 0 only: kmaxr + hist0's copy 0 are one range, hist1's and
@@ -2150,6 +2727,29 @@ void ew_topk_encode(const TopkEncodeArgs& a) {
         (a.max_k > 0 && 4LL * a.max_k <= (long long)ew_pk_inline_max()) ? ew_pk_inline_max() : 0u;
     auto* cbl = reinterpret_cast<const CBlockRow*>(a.cblocks);
     const int G = a.num_cblocks;
+    if (C <= ew_pk_one_max_blocks()) {
+      // small bucket: stage, select and write in ONE launch (k_pk_one)
+      uint32_t* gen1 = reinterpret_cast<uint32_t*>(tick + 2 * TICK_STRIDE * T);
+      uint32_t* mode1 = reinterpret_cast<uint32_t*>(tick + 3 * TICK_STRIDE * T);
+#define EW_PK1(EFM, VK, EFV)                                                                     \
+  hipLaunchKernelGGL((k_pk_one<EFM, VK, EFV>), dim3(C), dim3(EW_BLOCK), PK1_DYN_BYTES, s, g, dg,  \
+                     lb, resid, chunks, kmaxr, T, tensors, pst, tick, ccount, pcand, pk_stats,    \
+                     state, cand_n, gen1, mode1, hist0, hist1, hist2, lb_err, pay, a.scales_off,   \
+                     a.idx_off, a.codes_off, a.bitmap_off, a.counts_off, a.levels, a.inv_levels,  \
+                     a.key, reinterpret_cast<const uint32_t*>(a.key_ptr), a.bucket_offset,         \
+                     a.lb_fault, (uint32_t)PK1_LDS_KEYS, ew_pk1_stamps(C), ap)
+#define EW_PK1_VK(EFM, EFV)                                                                      \
+  if (a.value_kind == VK_Q8) EW_PK1(EFM, VK_Q8, EFV);                                            \
+  else if (a.value_kind == VK_Q4) EW_PK1(EFM, VK_Q4, EFV);                                       \
+  else EW_PK1(EFM, VK_F32, EFV)
+      if (dg.vel) { EW_PK1_VK(EF_DGC, true); }
+      else if (resid) { EW_PK1_VK(EF_PLAIN, true); }
+      else { EW_PK1_VK(EF_NONE, false); }
+#undef EW_PK1_VK
+#undef EW_PK1
+      EW_CHECK_LAUNCH();
+      return;
+    }
 #define EW_PKH(EFM)                                                                              \
   EW_LAUNCH(k_pk_hist0<EFM>, C, s, g, dg, lb, resid, chunks, kmaxr, T, tensors, pst, tick, ccount, \
             cbase, ccnt, pcand, pk_stats, state, cand_n, inline_max)
@@ -2185,7 +2785,7 @@ void ew_topk_encode(const TopkEncodeArgs& a) {
             chunk_ties, inv, pay, a.scales_off, a.idx_off, a.codes_off, a.bitmap_off, a.levels,   \
             a.inv_levels, a.key, reinterpret_cast<const uint32_t*>(a.key_ptr), a.bucket_offset,   \
             kmaxr, pk_rz0, dg.mask ? dg.vel : nullptr, lb, a.counts_off, lb_err, pst, cbase,      \
-            ccnt, pcand, a.lb_fault, hist1, (uint32_t)(T * NB1), hist2, (uint32_t)(T * NB2))
+            ccnt, pcand, a.lb_fault, hist1, (uint32_t)(T * NB1), hist2, (uint32_t)(T * NB2), ap)
     if (a.value_kind == VK_Q8) {
       if (resid) EW_PKW(VK_Q8, true); else EW_PKW(VK_Q8, false);
     } else if (a.value_kind == VK_Q4) {
@@ -2222,7 +2822,7 @@ void ew_topk_encode(const TopkEncodeArgs& a) {
             chunk_ties, inv, pay, a.scales_off, a.idx_off, a.codes_off, a.bitmap_off, a.levels,     \
             a.inv_levels, a.key, reinterpret_cast<const uint32_t*>(a.key_ptr), a.bucket_offset,     \
             kmaxr, rezero_words, dg.mask ? dg.vel : nullptr, lb, a.counts_off, lb_err, nullptr,     \
-            nullptr, nullptr, nullptr, a.lb_fault, nullptr, 0u, nullptr, 0u)
+            nullptr, nullptr, nullptr, a.lb_fault, nullptr, 0u, nullptr, 0u, TkApply{})
 #define EW_WRITE2(VK, EFV) \
   do { if (lbk) EW_WRITE(VK, EFV, true); else EW_WRITE(VK, EFV, false); } while (0)
   if (a.value_kind == VK_Q8) {
@@ -2242,7 +2842,7 @@ size_t ew_topk_scratch_bytes(int T, int C, long long L, long long total_cap) {
   // candidate keys; predictive state, chunk candidate tables, counters, candidate list
   return sizeof(uint32_t) *
              ((size_t)4 * T + (size_t)NREP * T * (1 + NB0 + NB1 + NB2) + 5 * (size_t)C + T +
-              (5 * (size_t)T + 2) * TICK_STRIDE + (size_t)L) +
+              (5 * (size_t)T + 2 + 9) * TICK_STRIDE + (size_t)L) +
          sizeof(unsigned long long) * (size_t)C + 128 +
          sizeof(uint32_t) * (8 * (size_t)T + 2 * (size_t)C + (size_t)TICK_STRIDE * T) + 16 +
          sizeof(uint2) * (size_t)total_cap;

@@ -88,6 +88,7 @@ class GradientExchange:
             ef_mode if (self.dgc or self.ef21) else "plain")
         self.vel = torch.zeros_like(flat.grad) if self.dgc else None
         self.gest = torch.zeros_like(flat.grad) if self.ef21 else None  # EF21's global G
+        self.local_apply = False  # enable_local_apply
         if not flat.attach_grads and not self.cuda:
             raise ValueError("pointer-mode gradients need the HIP kernels (device tensors)")
         self._pack_plans = [ops.DevicePlan(b.plan, self.device) for b in flat.buckets] \
@@ -126,6 +127,29 @@ class GradientExchange:
                 # ours flush deferred weight-gradient transforms before reading (ops/conv.py)
                 p._ew_engine_hooks = getattr(p, "_ew_engine_hooks", 0) + 1
         self.last = StepStats()
+
+    def enable_local_apply(self) -> bool:
+        """A world of one: the all-gather of one payload is that payload, so the top-k encode's
+        write pass applies the decoded update itself (``ops.topk_encode(apply=...)``, bitwise the
+        decode's) and :meth:`apply` launches no decode.  Only where the decode is the sparse one
+        (momentum-corrected error feedback under momentum SGD: no receiver momentum) and the step
+        always applies (the trainer's all-to-all step; not ``finish(apply=False)`` callers).
+        Returns whether it is on."""
+        codec = self.codec
+        self.local_apply = bool(
+            self.cuda and self.N == 1 and self.dgc and not self.ef21 and not codec.allreduce
+            and codec.kind in ("topk", "topk_qsgd") and getattr(codec, "norm", "max") == "max"
+            and getattr(self.opt, "fusable", False) and ops._TOPK_PREDICT and not self.src_flat)
+        return self.local_apply
+
+    def _apply_hp(self, bi: int) -> dict:
+        """The sparse decode's SGD arguments of bucket ``bi`` (momentum-corrected EF: momentum and
+        weight decay ran on the sender; without masking the lr is inside the residual)."""
+        o = self.opt
+        hp = dict(o.hparams(), momentum=0.0, dampening=0.0, weight_decay=0.0, nesterov=False)
+        if not self.dgc_mask:
+            hp.update(lr=1.0, lr_t=None)
+        return hp
 
     def _alloc_payloads(self):
         for b in self.flat.buckets:
@@ -274,10 +298,19 @@ class GradientExchange:
                        param=self.flat.data_view(b), mask=self.dgc_mask,
                        lr=None if self.dgc_mask else o.lr,
                        lr_t=None if self.dgc_mask else getattr(o, "lr_t", None))
+        apply = None
+        if self.local_apply:  # world of one: the write pass applies the update (no decode)
+            hp = self._apply_hp(bi)
+            adv = self.dev_key_advance and self.use_dev_key and bi == self.nb - 1
+            apply = dict(param=self.flat.data_view(b), shadow=self.flat.shadow_view(b),
+                         lr=hp["lr"], lr_tensor=hp.get("lr_t"),
+                         grad_scale=self.predivide / self.N,
+                         key_state=self.key_state if adv else None, key_seed=self.codec.seed,
+                         key_rank=self.comm.rank)
         self.codec.encode(bi, g, self.payload[bi], self.step_idx + self.seed_offset,
                           self.comm.rank, resid,
                           key_tensor=self.key_dev if self.use_dev_key else None, dgc=dgc,
-                          ef21=self.ef21)
+                          ef21=self.ef21, apply=apply)
 
     def _collective(self, bi: int):
         if self.codec.allreduce:
@@ -371,6 +404,8 @@ class GradientExchange:
                     G = self.gest[b.start:b.start + b.length]
                     G.add_(gv)
                     opt.step_range(b.start, b.length, G, 1.0)
+                elif self.local_apply:
+                    continue  # applied by the encode's write pass (enable_local_apply)
                 elif getattr(opt, "fusable", False):
                     adv = self.dev_key_advance and self.use_dev_key and b.index == self.nb - 1
                     hp, mom = opt.hparams(), opt.mom[b.start:b.start + b.length]

@@ -204,6 +204,10 @@ class Trainer:
             if cfg.sync_every > 1 or cfg.select_best:
                 self.exchange = LocalSGDExchange(self.exchange, cfg.sync_every, cfg.sync_mode,
                                                  cfg.select_best, score_fn=self._holdout_score)
+            elif self.world == 1 and os.environ.get("EWDML_LOCAL_APPLY", "1") != "0":
+                # a world of one: the top-k write pass applies the update (the all-gather of one
+                # payload is that payload: no decode launch).  EWDML_LOCAL_APPLY=0: decode
+                self.exchange.enable_local_apply()
         self.amp_dtype = {"bf16": torch.bfloat16, "fp16": torch.float16}.get(cfg.amp)
         self.graph_mode = cfg.hip_graph if (self.cuda and not cfg.sync_debug) else "off"
         self.local_sgd = isinstance(self.exchange, LocalSGDExchange)

@@ -555,3 +555,31 @@ def _check_side_run(flags, ref, l_ref):
     assert torch.equal(tr.flat.data.view(torch.int32), ref.flat.data.view(torch.int32))
     assert not cv._WGRAD_SIDE and not cv._SIDE_QUEUE and not cv._SIDE_PENDING
     tr.close()
+
+
+@pytest.mark.parametrize("graph", ["off", "full"])
+def test_world_of_one_encode_apply_bitwise_decode(monkeypatch, graph):
+    """A world of one: the top-k write pass applies the update (GradientExchange.
+    enable_local_apply, no decode launch) -- the trajectory is bitwise the one with the decode of
+    the one-rank all-gather (EWDML_LOCAL_APPLY=0), eager and through the captured (unrolled)
+    graphs, whose device RNG key the write pass now advances."""
+    from ewdml.runtime import Trainer
+
+    ops.require()
+    flags = LENET + ["--compress", "topk_qsgd", "--error-feedback", "--ef-warmup", "none",
+                     "--hip-graph", graph, "--max-steps", "40"]
+    res = []
+    for on in ("0", "1"):
+        monkeypatch.setenv("EWDML_LOCAL_APPLY", on)
+        torch.manual_seed(0)
+        tr = Trainer(ewdml.parse_args(flags))
+        assert tr.exchange.local_apply == (on == "1")
+        for _ in range(4):
+            tr.train_step()
+        loss, _ = tr.train_steps(12, 4 if graph == "full" else 1)
+        torch.cuda.synchronize()
+        res.append((tr.flat.data.clone(), float(loss), tr.exchange.key_state.clone()))
+        tr.close()
+    assert torch.equal(res[0][0], res[1][0])
+    assert res[0][1] == res[1][1]
+    assert torch.equal(res[0][2], res[1][2])

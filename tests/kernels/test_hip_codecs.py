@@ -485,9 +485,10 @@ def test_topk_predictive_encode_fast_and_full_paths(kind, bits, ratio):
     seq = [g0, g0 * 1.02 + noise, g0 * 1e-3, g0, g0 * 1.01 - noise]
     big = [n > c for n, c in zip(plan.numels, plan.tensor_cap)]
     T, nbig = plan.num_tensors, sum(big)
-    # full passes: the first encode (no prediction yet) and the growth (too many candidates) for
-    # the tensors larger than their candidate list; the 1000x shrink (too few candidates) for all
-    expect_full = 2 * nbig + T
+    # full passes, only for the tensors larger than their candidate list (the others take every
+    # element as a candidate: bound 0, always the fast path): the first encode (no prediction
+    # yet), the 1000x shrink (too few candidates) and the growth (too many)
+    expect_full = 3 * nbig
     for it, g in enumerate(seq):
         key = stream_key(4, it, 2)
         ref = oracle.encode_topk(g.clone(), plan, lay, levels, "max", key)
@@ -608,3 +609,93 @@ def test_fused_select_beside_a_long_gemm():
     st = ops.topk_stats(dp)
     assert st["lookback_errors"] == 0, st
     assert st["fast"] > 0  # the candidate (fused select) path ran
+
+
+SMALL = [20 * 25, 20, 50 * 500, 50, 800 * 500, 500, 5000, 10]  # LeNet's 8 tensors
+
+
+@pytest.mark.parametrize("ef", ["none", "plain", "dgc"])
+@pytest.mark.parametrize("kind,bits", [("topk_qsgd", 8), ("topk_qsgd", 4), ("topk", 8)])
+def test_topk_one_launch_encode_matches_oracle(ef, kind, bits):
+    """Small buckets (every chunk block resident: LeNet's 431,080 elements in 53 chunks) encode in
+    ONE launch (ops/csrc/topk_codec.hip k_pk_one: stage + candidates, the tensor's select in its
+    last block, the ordered write), on the candidate path and on the full passes it falls back
+    to (the first encode, a 1000x shrink, the growth back; ties at the threshold): payload,
+    residual and velocity bitwise the oracle's at every step."""
+    C_ = ops.require()
+    plan = _plan(SMALL, 0.01, bucket_offset=128)
+    assert plan.num_chunks <= C_.topk_one_max_blocks(), "the one-launch encode is not in use"
+    lay = Layout.build(kind, plan, bits)
+    levels = 127 if bits == 8 else 7
+    dp = ops.DevicePlan(plan, DEV)
+    pay = torch.zeros(lay.nbytes, dtype=torch.uint8, device=DEV)
+    g0 = _grad(plan, seed=31)
+    seq = [g0, g0 * 1.01, g0 * 1e-3, g0, _grad(plan, seed=32, ties=True)] + [
+        _grad(plan, seed=40 + i) * (1.0 + 0.01 * i) for i in range(6)]
+    r_ref = torch.zeros(plan.length) if ef != "none" else None
+    v_ref = torch.zeros(plan.length) if ef == "dgc" else None
+    r_dev = r_ref.to(DEV) if r_ref is not None else None
+    v_dev = v_ref.to(DEV) if v_ref is not None else None
+    hp = dict(momentum=0.9, dampening=0.0, nesterov=False, weight_decay=0.0)
+    for it, g in enumerate(seq):
+        key = stream_key(7, it, 1)
+        dgc_ref = dict(velocity=v_ref, param=None, **hp) if ef == "dgc" else None
+        dgc_dev = dict(velocity=v_dev, param=None, **hp) if ef == "dgc" else None
+        ref = oracle.encode_topk(g.clone(), plan, lay, levels, "max", key, residual=r_ref,
+                                 dgc=dgc_ref)
+        ops.topk_encode(dp, g.to(DEV), pay, lay, levels, "max", key, resid=r_dev, dgc=dgc_dev)
+        assert torch.equal(pay.cpu(), ref), f"step {it}: payload"
+        if r_ref is not None:
+            assert torch.equal(r_dev.cpu(), r_ref), f"step {it}: resid"
+        if v_ref is not None:
+            assert torch.equal(v_dev.cpu(), v_ref), f"step {it}: vel"
+    st = ops.topk_stats(dp)
+    assert st["lookback_errors"] == 0, st
+    assert st["fast"] > 0 and st["full"] > 0, st  # both paths ran
+
+
+@pytest.mark.parametrize("numels", [SMALL, [1728, 64, 2359296, 512, 262144, 5120]])
+@pytest.mark.parametrize("kind,bits", [("topk_qsgd", 8), ("topk_qsgd", 4), ("topk", 8)])
+def test_topk_encode_apply_matches_decode(numels, kind, bits):
+    """A world of one: the encode's write pass applies the update itself (ops.topk_encode
+    apply=..., on the one-launch and the three-launch encodes) -- parameters, bf16 shadow and the
+    advanced RNG key state bitwise those of the encode followed by the sparse decode of the
+    one-rank all-gather (k_topk_decode_sparse), step after step under DGC error feedback."""
+    ops.require()
+    plan = _plan(numels, 0.01, bucket_offset=64)
+    lay = Layout.build(kind, plan, bits)
+    levels = 127 if bits == 8 else 7
+    hp = dict(momentum=0.9, dampening=0.0, nesterov=False, weight_decay=0.0)
+    gen = torch.Generator().manual_seed(5)
+    p0 = torch.randn(plan.length, generator=gen).to(DEV)
+    runs = []
+    for fused in (False, True):
+        dp = ops.DevicePlan(plan, DEV)
+        pay = torch.zeros(lay.nbytes, dtype=torch.uint8, device=DEV)
+        r = torch.zeros(plan.length, device=DEV)
+        v = torch.zeros(plan.length, device=DEV)
+        p = p0.clone()
+        sh = p0.to(torch.bfloat16)  # the invariant the trainer keeps: shadow = bf16(param)
+        k3 = int(stream_key(9, 3, 0))
+        ks = torch.tensor([3, k3 - (1 << 32) if k3 >= 1 << 31 else k3], dtype=torch.int32,
+                          device=DEV)
+        for it in range(8):
+            g = _grad(plan, seed=70 + it).to(DEV)
+            dgc = dict(velocity=v, param=None, **hp)
+            kd = ks[1:2]
+            if fused:
+                ops.topk_encode(dp, g, pay, lay, levels, "max", 0, resid=r, key_tensor=kd,
+                                dgc=dgc, apply=dict(param=p, shadow=sh, lr=0.05, grad_scale=1.0,
+                                                    key_state=ks, key_seed=9, key_rank=0))
+            else:
+                ops.topk_encode(dp, g, pay, lay, levels, "max", 0, resid=r, key_tensor=kd,
+                                dgc=dgc)
+                ops.topk_decode_apply(dp, pay.view(1, -1), lay, levels, param=p, mom=None,
+                                      lr=0.05, grad_scale=1.0, shadow=sh, key_state=ks,
+                                      key_seed=9, key_rank=0)
+        torch.cuda.synchronize()
+        runs.append((p, sh, ks, r, v, pay))
+    for name, a, b in zip(("param", "shadow", "key_state", "resid", "vel", "payload"), *runs):
+        assert torch.equal(a.view(torch.uint8) if a.dtype != torch.uint8 else a,
+                           b.view(torch.uint8) if b.dtype != torch.uint8 else b), name
+    assert not torch.equal(runs[0][0], p0)

@@ -17,8 +17,8 @@ mkdir -p gpurun_out
 task=${1:-validate}; shift
 
 run_tests() {
-  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
-      ${TESTS_ARGS:-} ${TESTS_K:+-k "$TESTS_K"} > gpurun_out/gpu_tests.log 2>&1 \
+  timeout -k 10 900 python -u -m pytest ${TESTS_ARGS:-tests} -m gpu -x -q --timeout 120 --timeout-method thread \
+      ${TESTS_K:+-k "$TESTS_K"} > gpurun_out/gpu_tests.log 2>&1 \
       || { tail -60 gpurun_out/gpu_tests.log; exit 1; }
   tail -1 gpurun_out/gpu_tests.log
 }
