@@ -492,6 +492,27 @@ def make_batch(src, labels, perm, state, done, out, out_y, mean, inv_std, pad=4,
                   int(rank) & 0xFFFFFFFF, [float(v) for v in mean], [float(v) for v in inv_std],
                   _stream())
 
+def flag_signal(flags, i: int):
+    """Stream hand-off (``csrc/stream_flag.hip``): bump counter ``i`` of the int32 ``flags`` (one
+    128-B line per counter) on the current stream."""
+    _check(flags, torch.int32, "flags", align=128)
+    if not 0 <= i < flags.numel() // 32:
+        raise ValueError("flag index out of range")
+    require().flag_signal(flags.data_ptr() + 128 * i, _stream())
+
+
+def flag_wait(flags, i: int, seen: int, need: int, err: int):
+    """Wait on the current stream until counter ``i`` of ``flags`` has moved ``need`` more times
+    than this wait's private ``seen`` counter (also a line of ``flags``) recorded; ``err``: the
+    line counting a poll bound reached."""
+    _check(flags, torch.int32, "flags", align=128)
+    n = flags.numel() // 32
+    if not all(0 <= j < n for j in (i, seen, err)) or need < 1:
+        raise ValueError("flag index out of range")
+    b = flags.data_ptr()
+    require().flag_wait(b + 128 * i, b + 128 * seen, int(need), b + 128 * err, _stream())
+
+
 def build(force: bool = False) -> str:
     from .build import build as _b
     return _b(force=force)

@@ -377,6 +377,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("sm_set_fence", &ew_sm_set_fence);
   m.def("topk_fused_select_max_blocks", &ew_topk_fused_select_max_blocks);
   m.def("topk_one_max_blocks", &ew_topk_one_max_blocks);
+  m.def("flag_signal", &ew_flag_signal);
+  m.def("flag_wait", &ew_flag_wait);
   m.def("topk_one_stamps", &ew_topk_one_stamps);
   m.def("sm_f32_bwd", &ew_sm_f32_bwd);
   m.def("lenet_ws_floats", &ew_lenet_ws_floats);

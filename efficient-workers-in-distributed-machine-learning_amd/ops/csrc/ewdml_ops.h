@@ -111,6 +111,8 @@ std::vector<long long> ew_graph_info(uintptr_t graph, const std::string& dot_pat
 // largest candidate-block count the fused select kernel takes (0: always three kernels)
 int ew_topk_fused_select_max_blocks();
 int ew_topk_one_max_blocks();
+void ew_flag_signal(uintptr_t flag, uintptr_t stream);
+void ew_flag_wait(uintptr_t flag, uintptr_t seen, int need, uintptr_t err, uintptr_t stream);
 std::vector<unsigned long long> ew_topk_one_stamps();
 int ew_topk_lookback_errors(uintptr_t scratch, int num_tensors, int num_chunks);
 void ew_topk_encode(const TopkEncodeArgs& a);

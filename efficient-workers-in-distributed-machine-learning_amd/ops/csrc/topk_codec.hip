@@ -1102,7 +1102,7 @@ __device__ __forceinline__ void pk_predict_thr(const TensorRow& tr, int t, uint3
                                                uint32_t* __restrict__ pst,
                                                int* __restrict__ cand_n, uint32_t M,
                                                uint32_t fast, uint32_t beta_bits, uint32_t had,
-                                               uint32_t hi = 0xffffffffu) {
+                                               uint32_t hi = 0xffffffffu, uint32_t lo = 0u) {
   cand_n[TICK_STRIDE * t] = 0;  // every block read n before it arrived
   // next encode's candidate bound: beta x this exact threshold, beta steered so the
   // candidates stay between ~2k and 3/4 of the list
@@ -1113,7 +1113,7 @@ __device__ __forceinline__ void pk_predict_thr(const TensorRow& tr, int t, uint3
     if (!fast && M > cap) beta = beta + (1.0f - beta) * 0.5f;  // too many: tighter
     else if (!fast) beta = beta * 0.8f;                        // too few: the bound was above
     else if (M > min(cap - cap / 4, hi)) beta = beta + (1.0f - beta) * 0.25f;
-    else if (M < 2u * k) beta = beta * 0.95f;
+    else if (M < (lo ? lo : 2u * k)) beta = beta * 0.95f;
   }
   beta = fminf(fmaxf(beta, 0.25f), 0.99f);
   pst[t * 8 + 1] = __float_as_uint(beta);
@@ -2036,8 +2036,11 @@ __global__ __launch_bounds__(EW_BLOCK) void k_pk_one(
       pk1_select_cands(pcand + tr.cap0, M, s_u[2], s_u[3], s_u[4], s_u[6], (uint32_t)tr.k,
                        s_dyn + NB0 * PK1_HSUB, min(M, lds_keys), s_dyn, s_st, ws, state, t);
       if (threadIdx.x == 0) {
-        // candidates steered to fit the LDS copy (7/8 of it), not only 3/4 of the list
-        pk_predict_thr(tr, t, s_st[0], pst, cand_n, M, 1u, pbeta, phad, lds_keys - lds_keys / 8);
+        // candidates steered to 1.5 k .. min(2.5 k, 7/8 of the LDS copy): the select's time
+        // grows with them, and its single block is this launch's critical path
+        const uint32_t kk = (uint32_t)tr.k;
+        pk_predict_thr(tr, t, s_st[0], pst, cand_n, M, 1u, pbeta, phad,
+                       min(lds_keys - lds_keys / 8, kk * 2u + kk / 2u), kk + kk / 2u);
         for (int r = 0; r < NREP; ++r)  // dead once the max is in the select state
           __hip_atomic_store(kmaxr + r * T + t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }

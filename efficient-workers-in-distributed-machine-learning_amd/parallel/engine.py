@@ -134,10 +134,12 @@ class GradientExchange:
         decode's) and :meth:`apply` launches no decode.  Only where the decode is the sparse one
         (momentum-corrected error feedback under momentum SGD: no receiver momentum) and the step
         always applies (the trainer's all-to-all step; not ``finish(apply=False)`` callers).
-        Returns whether it is on."""
+        The caller guarantees that the encode runs after backward produced every gradient (one
+        bucket, no segmented step): the apply moves parameters.  Returns whether it is on."""
         codec = self.codec
         self.local_apply = bool(
-            self.cuda and self.N == 1 and self.dgc and not self.ef21 and not codec.allreduce
+            self.cuda and self.N == 1 and self.nb == 1 and self.dgc and not self.ef21
+            and not codec.allreduce
             and codec.kind in ("topk", "topk_qsgd") and getattr(codec, "norm", "max") == "max"
             and getattr(self.opt, "fusable", False) and ops._TOPK_PREDICT and not self.src_flat)
         return self.local_apply
@@ -505,8 +507,19 @@ class SegmentedCapture:
     begun on another thread (autograd's device thread runs the hooks)."""
 
     def __init__(self, gstream, cstream, mode: str = "relaxed", total_bytes: int = 0,
-                 splits: int = 1):
+                 splits: int = 1, device_handoff: bool = False):
         self.gs, self.cs, self.mode = gstream, cstream, mode
+        # device hand-offs (ops/csrc/stream_flag.hip): each compute segment ends with a signal
+        # kernel, each comm graph starts with a wait kernel on it and ends with a signal, and the
+        # apply is captured into the last segment behind a wait on the comm graphs -- no event
+        # record / stream wait between the replays (a cross-queue event hop measured ~20 us of
+        # GPU time each) and one graph fewer per step.  Off: events and an apply graph (needed
+        # by --phase-timing's per-phase marks).
+        self.device = bool(device_handoff)
+        # int32 counter lines (128 B each): 0 error count, 1 comm-graphs-done, 2 its wait's seen
+        # count, then per split a (fork signal, fork seen) pair
+        self.flags = torch.zeros(32 * (3 + 2 * max(1, splits)), dtype=torch.int32,
+                                 device=torch.cuda.current_device()) if self.device else None
         # split points: the first time the ready gradient bytes reach k / (splits + 1) of the
         # step's total; each split costs a graph boundary and a stream hop, so a few large
         # comm graphs beat one per bucket
@@ -553,17 +566,36 @@ class SegmentedCapture:
         self.cur = None
 
     def split(self, issue):
+        i = len(self.comms)
+        if self.device:  # the segment's last kernel: its gradients are complete
+            with torch.cuda.stream(self.gs):
+                ops.flag_signal(self.flags, 3 + 2 * i)
         self._end_segment()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.stream(self.cs):
             g.capture_begin(pool=self.cpool, capture_error_mode=self.mode)
             try:
+                if self.device:
+                    ops.flag_wait(self.flags, 3 + 2 * i, 4 + 2 * i, 1, 0)
                 issue()
+                if self.device:
+                    ops.flag_signal(self.flags, 1)
             finally:
                 g.capture_end()
         self.comms.append(g)
         self._evs.append(torch.cuda.Event())
         self.begin()
+
+    def join_comms(self):
+        """Device hand-offs: the current (last) segment waits for every comm graph before the
+        apply captured after this call."""
+        if self.device and self.comms:
+            with torch.cuda.stream(self.gs):
+                ops.flag_wait(self.flags, 1, 2, len(self.comms), 0)
+
+    def handoff_errors(self) -> int:
+        """Wait kernels that gave up on their poll bound (synchronises; 0 when healthy)."""
+        return int(self.flags[0].item()) if self.device else 0
 
     def end(self):
         self._end_segment()
@@ -589,6 +621,16 @@ class SegmentedCapture:
         part of the collectives), the apply as ``decode_update``, and each comm graph's own span
         on the comm stream as the overlapped side interval ``comm_graph``."""
         cur = torch.cuda.current_stream()
+        if self.device:  # the kernels hand off on the device: launch back to back
+            for i, seg in enumerate(self.segments):
+                if seg is not None:
+                    seg.replay()
+                if i < len(self.comms):
+                    with torch.cuda.stream(self.cs):
+                        self.comms[i].replay()
+            if clock is not None:
+                clock.mark("compute")
+            return
         for i, seg in enumerate(self.segments):
             if seg is not None:
                 seg.replay()

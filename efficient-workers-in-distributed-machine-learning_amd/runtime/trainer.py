@@ -204,10 +204,7 @@ class Trainer:
             if cfg.sync_every > 1 or cfg.select_best:
                 self.exchange = LocalSGDExchange(self.exchange, cfg.sync_every, cfg.sync_mode,
                                                  cfg.select_best, score_fn=self._holdout_score)
-            elif self.world == 1 and os.environ.get("EWDML_LOCAL_APPLY", "1") != "0":
-                # a world of one: the top-k write pass applies the update (the all-gather of one
-                # payload is that payload: no decode launch).  EWDML_LOCAL_APPLY=0: decode
-                self.exchange.enable_local_apply()
+
         self.amp_dtype = {"bf16": torch.bfloat16, "fp16": torch.float16}.get(cfg.amp)
         self.graph_mode = cfg.hip_graph if (self.cuda and not cfg.sync_debug) else "off"
         self.local_sgd = isinstance(self.exchange, LocalSGDExchange)
@@ -231,6 +228,14 @@ class Trainer:
                 self.graph_mode = "full"
             else:
                 self.graph_mode = "split" if ps_split else "off"
+        if (self.world == 1 and type(self.exchange) is GradientExchange
+                and len(self.flat.buckets) == 1 and self.graph_mode != "segmented"
+                and os.environ.get("EWDML_LOCAL_APPLY", "1") != "0"):
+            # a world of one: the top-k write pass applies the update (the all-gather of one
+            # payload is that payload: no decode launch).  One bucket, encoded once backward has
+            # produced every gradient (an earlier bucket's encode would move parameters that the
+            # rest of backward still reads); EWDML_LOCAL_APPLY=0: decode
+            self.exchange.enable_local_apply()
         if self.graph_mode != "off" and not (isinstance(self.exchange, GradientExchange) or
                                              (self.local_sgd and self.graph_mode == "full") or
                                              (ps_split and self.graph_mode == "split")):
@@ -708,9 +713,13 @@ class Trainer:
                     g.instantiate()
                 self._graphs = (g,)
             elif self.graph_mode == "segmented":
+                # device hand-offs unless --phase-timing marks the phases between the graphs
+                # (EWDML_SEG_HANDOFF=event: cross-stream events and an apply graph)
+                dev = (self.clock is None
+                       and os.environ.get("EWDML_SEG_HANDOFF", "device") != "event")
                 seg = SegmentedCapture(self.gstream, ex.comm_stream, mode="relaxed",
                                        total_bytes=4 * self.flat.numel,
-                                       splits=self.overlap_splits)
+                                       splits=self.overlap_splits, device_handoff=dev)
                 ex.seg = seg
                 try:
                     seg.begin()
@@ -718,6 +727,12 @@ class Trainer:
                         self._gx, self._gy = self.loader.emit()
                     loss, out = self.forward_backward(self._gx, self._gy)
                     ex.launch_pending()
+                    if dev:  # the apply in the last segment, behind the comm graphs
+                        ex.seg = None
+                        seg.join_comms()
+                        ex._active = False
+                        with torch.cuda.stream(self.gstream):
+                            ex.apply()
                     seg.end()
                 except BaseException:
                     seg.abort()
@@ -725,12 +740,13 @@ class Trainer:
                 finally:
                     ex.seg = None
                 ex._active = False
-                # the apply waits for every comm graph (replay joins the comm stream first)
-                ga = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(ga, pool=seg.pool, stream=self.gstream,
-                                      capture_error_mode=mode):
-                    ex.apply()
-                seg.apply = ga
+                if not dev:
+                    # the apply waits for every comm graph (replay joins the comm stream first)
+                    ga = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(ga, pool=seg.pool, stream=self.gstream,
+                                          capture_error_mode=mode):
+                        ex.apply()
+                    seg.apply = ga
                 self._graphs = ("segmented", seg)
             else:
                 ex.defer_comm = True

@@ -102,9 +102,32 @@ def test_segmented_graph_matches_full_graph(codec, splits):
     assert seg.graph_mode == "segmented" and seg._graphs[0] == "segmented"
     sc = seg._graphs[1]
     assert len(seg.flat.buckets) >= 3 and 1 <= len(sc.comms) <= splits
-    assert len(sc.segments) == len(sc.comms) + 1 and sc.apply is not None
+    assert len(sc.segments) == len(sc.comms) + 1
+    # device hand-offs (the default): the apply rides in the last segment, no apply graph
+    assert sc.device and sc.apply is None and sc.handoff_errors() == 0
     assert lf == ls
     assert torch.equal(full.flat.data, seg.flat.data)
+
+
+def test_segmented_event_handoff_matches_device_handoff(monkeypatch):
+    """The two segmented-step hand-offs (cross-stream events + an apply graph, or the device
+    flag kernels of ops/csrc/stream_flag.hip with the apply in the last segment) run the same
+    kernels on the same data: bitwise the same trajectory."""
+    ops.require()
+    flags = ["--network", "VGG11", "--dataset", "Cifar10", "--batch-size", "32",
+             "--synthetic-size", "512", "--momentum", "0.9", "--eval-freq", "0", "--quiet",
+             "--device", "cuda", "--graph-warmup", "2", "--amp", "none", "--bucket-mb", "6",
+             "--compress", "none", "--hip-graph", "segmented", "--overlap-splits", "2"]
+    res = []
+    for mode in ("event", "device"):
+        monkeypatch.setenv("EWDML_SEG_HANDOFF", mode)
+        tr, l = _run(flags, 9)
+        sc = tr._graphs[1]
+        assert sc.device == (mode == "device") and len(sc.comms) >= 1
+        assert sc.handoff_errors() == 0
+        res.append((tr.flat.data.clone(), l))
+    assert res[0][1] == res[1][1]
+    assert torch.equal(res[0][0], res[1][0])
 
 
 @pytest.mark.parametrize("opt", ["sgd", "adam"])
