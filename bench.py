@@ -279,6 +279,8 @@ def main(argv=None):
                    "grad_mode": "views" if tr.flat.attach_grads else "pointers",
                    "layout": "nhwc" if tr.channels_last else "nchw",
                    "fused_nn": a.fused_nn, "comm": tr.comm_kind,
+                   "local_apply": bool(getattr(getattr(tr.exchange, "inner", tr.exchange),
+                                               "local_apply", False)),
                    "wgrad_stream": bool(getattr(tr, "wgrad_stream", False))},
         # overlap that actually happens: a collective to hide (world > 1) issued while backward
         # still runs -- a segmented graph with at least one comm-stream graph, or eager steps
@@ -313,11 +315,16 @@ def main(argv=None):
         # measurements + an xGMI collective model), to check a scaling run against
         "predicted_ms_per_step": ((tr.graph_plan or {}).get("predicted_ms") or {}).get(
             "segmented" if tr.graph_mode == "segmented" else "full"),
+        # the step model against this run at N = 1, where it has no collective term to blame
+        # (|error| <= 3 % on the committed preset lines: tests/unit/test_graph_plan.py)
+        "model_error_n1": None,
         "codec_health": tr.codec_health,
         "step_ms_min": round(span[0] * 1e3 / a.steps, 4),
         "step_ms_max": round(span[1] * 1e3 / a.steps, 4),
         "hip_ext": ewdml.ops.library_path() if cuda else None,
     }
+    if world == 1 and rec["predicted_ms_per_step"]:
+        rec["model_error_n1"] = round(rec["predicted_ms_per_step"] / rec["ms_per_step"] - 1, 4)
     del tr
     if not a.no_extras:
         extras = []

@@ -666,7 +666,7 @@ OVERLAP_MAX_SPLITS = 3
 
 def plan_graph_mode(world: int, comm_kind: str, codec_kind: str, grad_numel: int,
                     bits: int = 8, overlap: bool = True, bucket_bytes: int = 16 << 20,
-                    model: str = None, topk_ratio: float = 0.01) -> dict:
+                    model: str = None, topk_ratio: float = 0.01, dtype: str = "fp32") -> dict:
     """``--hip-graph auto`` for the all-to-all exchange (``GradientExchange``).
 
     * N = 1, or collectives on the process group (not capturable), or ``--no-overlap``: the
@@ -699,10 +699,12 @@ def plan_graph_mode(world: int, comm_kind: str, codec_kind: str, grad_numel: int
         wire = (world - 1) * pb  # all-gather
     out = {"mode": "full", "splits": 1, "bucket_bytes": int(bucket_bytes), "wire_bytes": int(wire)}
     splits = overlap_splits(payload, OVERLAP_MAX_SPLITS, OVERLAP_BYTES_PER_SPLIT)
-    prof = profile_for(model, codec_kind)
+    prof = profile_for(model, codec_kind, dtype)
     pred = None
     if prof is not None:
-        pred = predict(prof, world, codec_kind, pb, 4.0 * grad_numel, splits)
+        # the all-reduce moves the wire dtype's bytes (fp16 / bf16 codecs: 2 per element)
+        pred = predict(prof, world, codec_kind, pb, payload if per_elem is not None and
+                       codec_kind in ("none", "fp16", "bf16") else 4.0 * grad_numel, splits)
         out["predicted_ms"] = pred
     if world <= 1:
         return dict(out, reason="one rank: nothing to overlap")

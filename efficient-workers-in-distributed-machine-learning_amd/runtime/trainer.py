@@ -157,7 +157,8 @@ class Trainer:
                 plan_world, self.comm.kind, cfg.compress,
                 sum(p.numel() for p in model.parameters() if p.requires_grad),
                 bits=cfg.qsgd_bits, overlap=cfg.overlap, bucket_bytes=bucket_bytes,
-                model=cfg.network, topk_ratio=cfg.topk_ratio)
+                model=cfg.network, topk_ratio=cfg.topk_ratio,
+                dtype={"bf16": "bf16", "fp16": "fp16"}.get(cfg.amp, "fp32"))
             bucket_bytes = self.graph_plan["bucket_bytes"]
         self.flat = FlatModel(model, bucket_bytes=bucket_bytes,
                               attach_grads=not ptr_grads, bf16_params=bf16_params)
