@@ -266,7 +266,10 @@ def main(argv=None):
         "vs_baseline": round(img_s / BASELINE_IMG_S, 2) if a.preset == "vgg11" else None,
         "baseline_note": "reference publishes no img/s; BASELINE.md derives ~104 img/s (VGG-11, "
                          "2 Colab CPU workers)",
-        "dtype": a.amp if a.amp != "none" else "fp32",
+        # the compute dtype actually used (--amp bf16 on a model whose fused fp32 step is faster
+        # -- LeNet -- trains in fp32: Trainer.amp_kept_fp32)
+        "dtype": getattr(tr, "compute_dtype", a.amp if a.amp != "none" else "fp32"),
+        "amp_requested": a.amp,
         "data": f"synthetic ({a.dataset} shape {'x'.join(map(str, tr.info['shape']))}, "
                 f"{tr.info['classes']} classes, random-init weights)",
         "config": {"model": "vgg11_bn" if a.network.lower() in ("vgg11", "vgg11_bn") else
@@ -353,6 +356,7 @@ def main(argv=None):
             if rep2 is not None:
                 rec[f"replicas_identical_{key}"] = rep2["identical"]
             rec[f"value_{key}"] = round(world * a.batch_size * a.steps / el, 2)
+            rec[f"dtype_{key}"] = getattr(tr2, "compute_dtype", amp)
             rec[f"ms_per_step_{key}"] = round(el * 1e3 / a.steps, 4)
             rec[f"final_loss_{key}"] = fl
             if key == "method6":

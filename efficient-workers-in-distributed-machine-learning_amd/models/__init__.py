@@ -52,6 +52,16 @@ def input_shape(name: str):
     return _REGISTRY[canonical_name(name)][1]
 
 
+def fused_fp32_beats_amp(name: str) -> bool:
+    """Whether the named model's fused fp32 training step is faster than its bf16 autocast path
+    (a class attribute, ``LeNet.fused_fp32_beats_amp``): the trainer keeps that step under
+    ``--amp bf16``."""
+    entry = _REGISTRY.get(canonical_name(name))
+    cls = {"lenet": LeNet}.get(canonical_name(name))
+    return bool(entry is not None and cls is not None and getattr(cls, "fused_fp32_beats_amp",
+                                                                  False))
+
+
 def build_model(name: str, num_classes: int = 10, **kw):
     return _REGISTRY[canonical_name(name)][0](num_classes, **kw)
 

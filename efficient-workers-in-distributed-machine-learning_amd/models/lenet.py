@@ -30,6 +30,10 @@ class LeNet(nn.Module):
             x = F.relu(x)
         return self.fc2(x)
 
+    # its fused fp32 step (four launches, latency-bound at batch 64) beats the bf16 autocast path
+    # (cuBLAS-class GEMMs and MIOpen convs per layer): the trainer keeps it under --amp bf16
+    fused_fp32_beats_amp = True
+
     def fused_loss(self, x, y):
         """(mean cross-entropy, logits) through the fused HIP step (``ops/lenet.py``: four
         launches), or None where it does not apply (the caller then runs ``forward``)."""

@@ -362,6 +362,23 @@ __device__ __forceinline__ void sm_gemm(char* smem, int ksteps, LA&& la, LB&& lb
 // before the block's barrier and one lane draws the ticket; the reducer reads the other slabs
 // with agent-scope (sc1) loads only, so neither a release (an L2 write-back of the XCD) nor an
 // acquire (an L1 invalidate) is needed, wherever the four splits ran.
+//
+// The contract, cell by cell against MI355X_MICROARCH.md's table of measured hand-offs (row 1):
+//   who signals   -- ONE lane per storing workgroup (t == 0), an agent-scope atomic add (the
+//                    ticket), after EVERY storing wave's `s_waitcnt vmcnt(0)` and a workgroup
+//                    barrier (so the add comes after all four waves' slab stores landed);
+//   how learned   -- the workgroup whose add came last, told by the value its add returned;
+//   before loads  -- the reducer's waves load only after the block barrier that publishes the
+//                    flag the ticket-drawing lane set;
+//   memory        -- hipMalloc'd slabs (the torch caching allocator), one block per CU or more;
+//   stores/loads  -- every slab byte stored by a 4-B sc1 store, read by a 4-B sc1 load.
+// That table records hardware behaviour measured on gfx950 / ROCm 7.2, not a guarantee of the
+// HIP memory model: with relaxed atomics and no release / acquire pair the language does not
+// order the slab stores before the ticket.  The fenced form (fence = 1: plain stores, lane 0's
+// agent release fence + vmcnt before the ticket, the last arriver's agent acquire) is the memory
+// model's own release/acquire pairing; tests/kernels/test_conv_f32.py::
+// test_conv_f32_smallmap_fenced_handoff_bitwise keeps it bitwise equal to the default, so a
+// compiler or firmware change that broke the measured form can be answered by EWDML_SM_FENCE=1.
 int g_sm_fence = -1;  // EWDML_SM_FENCE=1: plain stores + release / acquire fences (A/B, tests)
 
 __device__ __forceinline__ bool sm_reduce(SmAcc& acc, float* __restrict__ slab, int* cnt, int tile,

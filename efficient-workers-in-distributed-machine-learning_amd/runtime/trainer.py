@@ -106,6 +106,16 @@ class Trainer:
         self.info = info
         n_workers = self.world - 1 if cfg.topology == "ps" else self.world
         w_rank = self.rank - 1 if cfg.topology == "ps" else self.rank
+        # a model whose fused fp32 training step is faster than its bf16 autocast path (LeNet:
+        # 0.10 vs 0.28 ms per step, latency-bound, ops/lenet.py) keeps that step under
+        # --amp bf16: bf16 is a request for speed, and the fp32 step is also the more precise
+        # one.  The compute dtype actually used is self.compute_dtype (bench.py reports it);
+        # EWDML_AMP_FUSED_FP32=0: bf16 autocast anyway
+        from ..models import fused_fp32_beats_amp
+
+        self.amp_kept_fp32 = bool(self.cuda and cfg.amp == "bf16" and cfg.fused_nn == "on"
+                                  and fused_fp32_beats_amp(net)
+                                  and os.environ.get("EWDML_AMP_FUSED_FP32", "1") != "0")
         self.loader = None
         if not self.is_server:
             self.loader = DeviceLoader(x, y, info, cfg.batch_size, rank=w_rank,
@@ -114,8 +124,9 @@ class Trainer:
                                        seed=cfg.seed, device=self.device,
                                        channels_last=self.channels_last,
                                        fused=self.cuda and cfg.fused_data == "on",
-                                       out_dtype=torch.bfloat16 if (self.cuda and cfg.amp == "bf16")
-                                       else torch.float32)
+                                       out_dtype=torch.bfloat16 if (
+                                           self.cuda and cfg.amp == "bf16"
+                                           and not self.amp_kept_fp32) else torch.float32)
         if hold <= 0:
             tx, ty, _ = load_dataset(cfg.dataset, cfg.data_dir, train=False,
                                      synthetic_size=(cfg.synthetic_size // 5)
@@ -136,7 +147,8 @@ class Trainer:
         # parameter server keeps flat gradient views
         ptr_grads = (self.cuda and cfg.topology == "allgather"
                      and os.environ.get("EWDML_GRAD_VIEWS") != "1")
-        bf16_params = ptr_grads and cfg.amp == "bf16" and cfg.param_dtype == "auto"
+        bf16_params = (ptr_grads and cfg.amp == "bf16" and cfg.param_dtype == "auto"
+                       and not self.amp_kept_fp32)
         # weight gradients beside the backward-data chain (ops/conv.py), switched on around this
         # trainer's backward passes only: deep conv nets
         n_conv = sum(isinstance(m, torch.nn.Conv2d) for m in model.modules())
@@ -158,7 +170,8 @@ class Trainer:
                 sum(p.numel() for p in model.parameters() if p.requires_grad),
                 bits=cfg.qsgd_bits, overlap=cfg.overlap, bucket_bytes=bucket_bytes,
                 model=cfg.network, topk_ratio=cfg.topk_ratio,
-                dtype={"bf16": "bf16", "fp16": "fp16"}.get(cfg.amp, "fp32"))
+                dtype="fp32" if self.amp_kept_fp32 else
+                {"bf16": "bf16", "fp16": "fp16"}.get(cfg.amp, "fp32"))
             bucket_bytes = self.graph_plan["bucket_bytes"]
         self.flat = FlatModel(model, bucket_bytes=bucket_bytes,
                               attach_grads=not ptr_grads, bf16_params=bf16_params)
@@ -207,6 +220,12 @@ class Trainer:
                                                  cfg.select_best, score_fn=self._holdout_score)
 
         self.amp_dtype = {"bf16": torch.bfloat16, "fp16": torch.float16}.get(cfg.amp)
+        if self.amp_kept_fp32:
+            self.amp_dtype = None
+            self.log.info("--amp bf16: the model's fused fp32 step is faster than its bf16 "
+                          "path; training in fp32")
+        self.compute_dtype = {torch.bfloat16: "bf16", torch.float16: "fp16"}.get(
+            self.amp_dtype, "fp32")
         self.graph_mode = cfg.hip_graph if (self.cuda and not cfg.sync_debug) else "off"
         self.local_sgd = isinstance(self.exchange, LocalSGDExchange)
         if self.local_sgd and cfg.select_best:

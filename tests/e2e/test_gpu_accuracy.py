@@ -43,17 +43,22 @@ LENET = ["--network", "LeNet", "--dataset", "MNIST", "--data-dir", MNIST,
          "--graph-warmup", "2", "--test-batch-size", "1000"]
 
 
-@pytest.mark.parametrize("amp", ["none", "bf16"])
+@pytest.mark.parametrize("amp", ["none", "bf16", "bf16_autocast"])
 @pytest.mark.parametrize("codec", ["dense", "topk1_qsgd_ef", "method5"])
-def test_lenet_real_mnist_gpu(codec, amp):
+def test_lenet_real_mnist_gpu(codec, amp, monkeypatch):
+    """``bf16``: --amp bf16 keeps LeNet's fused fp32 step (faster and more precise: the trainer's
+    amp_kept_fp32); ``bf16_autocast`` (EWDML_AMP_FUSED_FP32=0): the bf16 autocast path itself."""
     ops.require()
+    if amp == "bf16_autocast":
+        monkeypatch.setenv("EWDML_AMP_FUSED_FP32", "0")
     extra = {"dense": ["--compress", "none"],
              "topk1_qsgd_ef": ["--compress", "topk_qsgd", "--topk-ratio", "0.01",
                                "--error-feedback"],
              "method5": ["--compress", "topk_qsgd", "--topk-ratio", "0.4", "--qsgd-norm", "l2",
                          "--no-error-feedback"]}
-    tr, losses = _train(LENET + ["--amp", amp] + extra[codec], 1500)
+    tr, losses = _train(LENET + ["--amp", amp.split("_")[0]] + extra[codec], 1500)
     assert tr.graph_mode == "full" and tr._graphs is not None
+    assert tr.compute_dtype == ("bf16" if amp == "bf16_autocast" else "fp32")
     ev = tr.evaluate()
     assert ev["samples"] == 1000
     assert ev["top1"] >= 96.5, f"{codec}/{amp}: holdout top-1 {ev['top1']:.1f}% < 96.5%"

@@ -1070,6 +1070,37 @@ def test_conv_f32_smallmap_forward_backward(N, C, Nc):
     assert torch.equal(wc.grad, wa.grad)
 
 
+@pytest.mark.parametrize("N,C,Nc", SM_SHAPES[:2])
+def test_conv_f32_smallmap_fenced_handoff_bitwise(N, C, Nc):
+    """The small-map split-K hand-off has two forms (ops/csrc/smallmap_f32.hip sm_reduce): the
+    default write-through one (sc1 stores and loads, no fences: MI355X_MICROARCH.md's hand-off
+    table, row 1) and the fenced one (plain stores, agent release before the ticket, acquire
+    after it: the HIP memory model's own form, EWDML_SM_FENCE=1).  Both give the same bits, so
+    the fenced path stays a drop-in should the write-through form ever stop holding."""
+    from ewdml import ops
+
+    conv = _conv(sm=True)
+    C_ = ops.require()
+    x, w = _data(N, C, Nc, 2, 2, seed=57)
+    g = torch.Generator(device="cuda").manual_seed(58)
+    dy = torch.randn(N, Nc, 2, 2, device="cuda", generator=g).contiguous(
+        memory_format=torch.channels_last)
+    outs = []
+    prev = C_.sm_set_fence(0)
+    try:
+        for fence in (0, 1):
+            C_.sm_set_fence(fence)
+            xa, wa = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
+            y = conv.conv(xa, wa)
+            y.backward(dy)
+            torch.cuda.synchronize()
+            outs.append((y.detach(), xa.grad, wa.grad))
+    finally:
+        C_.sm_set_fence(prev)
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
 def test_conv_f32_smallmap_bn_statistics():
     """The split-K reducer's BatchNorm partial sums (8 rows) give the BN kernels' own statistics."""
     from ewdml.ops import nn as fnn
