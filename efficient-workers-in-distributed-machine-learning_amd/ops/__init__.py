@@ -259,9 +259,15 @@ def topk_encode(dp: DevicePlan, grad, payload, layout, levels: int, norm: str, k
                   int(max(dp.plan.ks)) if dp.plan.ks else 0, *_apply_args(dp, apply, norm))
 
 
+def topk_one_launch(dp) -> bool:
+    """Whether this bucket's top-k encode runs as the one-launch kernel (k_pk_one: every chunk
+    block resident)."""
+    return _TOPK_PREDICT and dp.plan.num_chunks <= require().topk_one_max_blocks()
+
+
 def _apply_args(dp, apply, norm):
     if apply is None:
-        return (0, 0, 0.0, 0, 1.0, 0, 0, 0)
+        return (0, 0, 0.0, 0, 1.0, 0, 0, 0, 0, 0, 0.0, 0.0, 0.0, 0, 0)
     if not _TOPK_PREDICT or norm != "max":
         raise ValueError("the write-pass apply needs the predictive (max-norm) encode")
     param = apply["param"]
@@ -270,9 +276,19 @@ def _apply_args(dp, apply, norm):
     ks = apply.get("key_state")
     if ks is not None:
         _check(ks, torch.int32, "key_state", align=4)
+    dense = "mom" in apply  # receiver-side momentum SGD over every element (one-launch only)
+    mom = apply.get("mom")
+    if dense:
+        if mom is None or not topk_one_launch(dp):
+            raise ValueError("the dense write-pass apply needs the momentum buffer and the "
+                             "one-launch encode")
+        _check_bucket(dp, mom, "mom")
     return (_ptr(param), _ptr(apply.get("shadow")), float(apply["lr"]),
             _lrp(apply.get("lr_tensor")), float(apply.get("grad_scale", 1.0)), _ptr(ks),
-            int(apply.get("key_seed", 0)) & 0xFFFFFFFF, int(apply.get("key_rank", 0)) & 0xFFFFFFFF)
+            int(apply.get("key_seed", 0)) & 0xFFFFFFFF, int(apply.get("key_rank", 0)) & 0xFFFFFFFF,
+            int(dense), _ptr(mom), float(apply.get("momentum", 0.0)),
+            float(apply.get("dampening", 0.0)), float(apply.get("weight_decay", 0.0)),
+            int(bool(apply.get("nesterov", False))), int(bool(apply.get("first", False))))
 
 
 def _lrp(lr_tensor):

@@ -35,8 +35,17 @@ PYBIND11_MODULE(_C, m) {
            long long bucket_len, uintptr_t cblocks, int num_cblocks, int predict,
            int lb_fault, int max_k, uintptr_t apply_param, uintptr_t apply_shadow,
            float apply_lr, uintptr_t apply_lr_ptr, float apply_scale,
-           uintptr_t apply_key_state, uint32_t apply_key_seed, uint32_t apply_key_rank) {
+           uintptr_t apply_key_state, uint32_t apply_key_seed, uint32_t apply_key_rank,
+           int apply_mom_set, uintptr_t apply_mom, float apply_momentum, float apply_dampening,
+           float apply_wd, int apply_nesterov, int apply_first) {
           TopkEncodeArgs a{};
+          a.apply_mom_set = apply_mom_set;
+          a.apply_mom = apply_mom;
+          a.apply_momentum = apply_momentum;
+          a.apply_dampening = apply_dampening;
+          a.apply_wd = apply_wd;
+          a.apply_nesterov = apply_nesterov;
+          a.apply_first = apply_first;
           a.apply_param = apply_param;
           a.apply_shadow = apply_shadow;
           a.apply_lr = apply_lr;

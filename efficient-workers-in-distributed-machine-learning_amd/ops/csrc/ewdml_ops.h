@@ -41,6 +41,11 @@ struct TopkEncodeArgs {
   uintptr_t apply_param, apply_shadow, apply_lr_ptr, apply_key_state;
   float apply_lr, apply_scale;
   uint32_t apply_key_seed, apply_key_rank;
+  // dense variant (receiver-side momentum SGD over every element; one-launch encodes only)
+  int apply_mom_set;
+  uintptr_t apply_mom;
+  float apply_momentum, apply_dampening, apply_wd;
+  int apply_nesterov, apply_first;
 };
 
 struct TopkDecodeArgs {

@@ -25,6 +25,7 @@
 // share by a decoupled look-back over the tensor's earlier chunks instead of a count pass.
 // The global state lives in one scratch block: zero-initialised once, histograms re-cleared by
 // k_topk_write after use, everything else fully rewritten per encode (no per-step memset).
+#include <cstdio>
 #include <cstdlib>
 #include <vector>
 
@@ -618,10 +619,19 @@ __device__ __forceinline__ void topk_lookback(uint32_t gt, uint32_t eq, const Ch
 struct TkApply {
   float* param;
   uint16_t* shadow;
-  SgdArgs sa;  // lr / lr_ptr (resolved on entry), grad_scale; momentum, decay 0
+  SgdArgs sa;  // lr / lr_ptr (resolved on entry), grad_scale; momentum, decay 0 (sparse)
   int* ticket;  // grid arrival ticket of the key advance (sa.key_state)
+  // dense (receiver-side momentum: no-EF / plain-EF top-k, k_pk_one only): the momentum buffer
+  // and the chunk's LDS accumulator the write fills; the step then runs over the whole chunk
+  // (k_topk_decode_apply's dense pass for one rank)
+  float* mom;
+  float* acc;
 };
 __device__ __forceinline__ void tk_apply_one(const TkApply& ap, size_t i, float sent) {
+  if (ap.acc) {  // dense: the decode's one-rank accumulator, 0 + sent
+    ap.acc[i - 0] = 0.0f + sent;
+    return;
+  }
   if (sent == 0.0f) return;  // the decode's zero accumulator: p - lr * 0 is p, bit for bit
   float pv = ap.param[i], bz = 0.0f;
   ew_sgd(pv, bz, sent * ap.sa.grad_scale, ap.sa);
@@ -720,7 +730,7 @@ __device__ __forceinline__ void topk_write_cands(
       }
       if (vel) vel[c.start + li] = 0.0f;
       if (EF) resid[c.start + li] = x - sent;
-      if (ap.param) tk_apply_one(ap, (size_t)c.start + li, sent);
+      if (ap.param) tk_apply_one(ap, ap.acc ? (size_t)li : (size_t)c.start + li, sent);
     }
     carry_gt += tot & 0xffffu;
     carry_eq += tot >> 16;
@@ -802,7 +812,7 @@ __device__ __forceinline__ void topk_write_chunk(
         // is e bit for bit, so only the sent coordinates are rewritten (a sparse store instead
         // of rewriting the whole bucket)
         if (EF) resid[c.start + i0 + j] = xs[j] - sent;
-        if (ap.param) tk_apply_one(ap, (size_t)c.start + i0 + j, sent);
+        if (ap.param) tk_apply_one(ap, ap.acc ? (size_t)(i0 + j) : (size_t)c.start + i0 + j, sent);
         ++pos;
       }
     }
@@ -1125,6 +1135,10 @@ __device__ __forceinline__ void pk_predict_thr(const TensorRow& tr, int t, uint3
   pst[t * 8 + 4] = 1u;
 }
 
+// The candidate band of the three-launch encode in quarters of k ({lo, hi}; hi 0: 3/4 of the
+// list): EWDML_PK_BAND="lo,hi" (ew_topk_encode sets it once)
+__device__ uint32_t g_pk_band_q[2] = {8u, 0u};
+
 // the same after a select whose state holds the threshold relative to B (made absolute here)
 __device__ __forceinline__ void pk_predict_mf(const TensorRow& tr, int t, uint32_t B,
                                               uint32_t* __restrict__ state,
@@ -1135,7 +1149,10 @@ __device__ __forceinline__ void pk_predict_mf(const TensorRow& tr, int t, uint32
   const uint32_t thr = B + __hip_atomic_load(state + t * 4, __ATOMIC_RELAXED,
                                              __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_store(state + t * 4, thr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  pk_predict_thr(tr, t, thr, pst, cand_n, M, fast, pst[t * 8 + 1], pst[t * 8 + 4]);
+  const uint32_t k = (uint32_t)tr.k, lq = g_pk_band_q[0], hq = g_pk_band_q[1];
+  pk_predict_thr(tr, t, thr, pst, cand_n, M, fast, pst[t * 8 + 1], pst[t * 8 + 4],
+                 hq ? (uint32_t)(((unsigned long long)k * hq) / 4u) : 0xffffffffu,
+                 (uint32_t)(((unsigned long long)k * lq) / 4u));
 }
 
 // the same, M and the fast flag from pst (set by k_pk_hist0's tensor-last block: an earlier launch,
@@ -2143,6 +2160,11 @@ __global__ __launch_bounds__(EW_BLOCK) void k_pk_one(
     __syncthreads();
   }
   PK1_STAMP(3);
+  if (ap.param && ap.mom) {  // dense apply: the chunk's accumulator in the (free) dynamic LDS
+    ap.acc = reinterpret_cast<float*>(s_dyn);
+    for (int i = threadIdx.x; i < EW_CHUNK; i += EW_BLOCK) ap.acc[i] = 0.0f;
+    __syncthreads();
+  }
   // ---- 3. the ordered write of this chunk ----
   const uint32_t thr = __hip_atomic_load(state + t * 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint32_t need = __hip_atomic_load(state + t * 4 + 1, __ATOMIC_RELAXED,
@@ -2159,6 +2181,49 @@ __global__ __launch_bounds__(EW_BLOCK) void k_pk_one(
     topk_write_lb<VK, EF>(c, tr, v, resid, velm, payload, scales_off, idx_off, codes_off,
                           bitmap_off, counts_off, levels, inv_levels, key, bucket_offset, lb,
                           lb_err, s_lb, ws, lb_fault, thr, need, scale, ap);
+  }
+  if (ap.acc) {  // dense apply over the chunk (its accumulator holds the sent values)
+    __syncthreads();
+    const float inv_n = ap.sa.grad_scale;
+    float* p = ap.param + c.start;
+    float* b = ap.mom + c.start;
+    const int n4 = c.len >> 2;
+    const float4* acc4 = reinterpret_cast<const float4*>(ap.acc);
+    // every load of the thread's vectors in flight before the first step (k_topk_decode_apply's
+    // dense pass: the same per-element arithmetic)
+    float4 pv[EW_CU], bv[EW_CU];
+#pragma unroll
+    for (int u = 0; u < EW_CU; ++u) {
+      const int i = threadIdx.x + u * EW_BLOCK;
+      if (i < n4) {
+        pv[u] = reinterpret_cast<const float4*>(p)[i];
+        bv[u] = reinterpret_cast<const float4*>(b)[i];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < EW_CU; ++u) {
+      const int i = threadIdx.x + u * EW_BLOCK;
+      if (i >= n4) break;
+      const float4 a = acc4[i];
+      float4 pu = pv[u], bu = bv[u];
+      ew_sgd(pu.x, bu.x, a.x * inv_n, ap.sa);
+      ew_sgd(pu.y, bu.y, a.y * inv_n, ap.sa);
+      ew_sgd(pu.z, bu.z, a.z * inv_n, ap.sa);
+      ew_sgd(pu.w, bu.w, a.w * inv_n, ap.sa);
+      reinterpret_cast<float4*>(p)[i] = pu;
+      reinterpret_cast<float4*>(b)[i] = bu;
+      if (ap.shadow) {
+        const float v4[4] = {pu.x, pu.y, pu.z, pu.w};
+        ew_st4_bf16(ap.shadow + c.start + 4 * i, 4, v4);
+      }
+    }
+    for (int i = (n4 << 2) + threadIdx.x; i < c.len; i += EW_BLOCK) {
+      float pq = p[i], bq = b[i];
+      ew_sgd(pq, bq, ap.acc[i] * inv_n, ap.sa);
+      p[i] = pq;
+      b[i] = bq;
+      if (ap.shadow) ap.shadow[c.start + i] = ew_f2bf(pq);
+    }
   }
   tk_apply_done(ap);
   PK1_STAMP(4);
@@ -2646,7 +2711,19 @@ static uint32_t ew_pk_inline_max() {
   return (uint32_t)n;
 }
 
+static void ew_pk_band_init() {
+  static bool done = false;
+  if (done) return;
+  done = true;
+  const char* e = std::getenv("EWDML_PK_BAND");
+  if (!e) return;
+  uint32_t q[2] = {8u, 0u};
+  if (std::sscanf(e, "%u,%u", &q[0], &q[1]) < 1) return;
+  EW_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_pk_band_q), q, sizeof(q)));
+}
+
 void ew_topk_encode(const TopkEncodeArgs& a) {
+  ew_pk_band_init();
   auto* chunks = reinterpret_cast<const ChunkRow*>(a.chunks);
   auto* tensors = reinterpret_cast<const TensorRow*>(a.tensors);
   auto* scratch = reinterpret_cast<uint8_t*>(a.scratch);
@@ -2717,6 +2794,17 @@ void ew_topk_encode(const TopkEncodeArgs& a) {
     ap.sa.key_seed = a.apply_key_seed;
     ap.sa.key_rank = a.apply_key_rank;
     ap.ticket = apply_ticket;
+    if (a.apply_mom_set) {  // receiver-side momentum SGD: the dense pass (k_pk_one only)
+      ap.mom = reinterpret_cast<float*>(a.apply_mom);
+      ap.sa.momentum = a.apply_momentum;
+      ap.sa.dampening = a.apply_dampening;
+      ap.sa.weight_decay = a.apply_wd;
+      ap.sa.nesterov = a.apply_nesterov;
+      ap.sa.first = a.apply_first;
+      if (!ap.mom) throw std::runtime_error("ewdml topk: dense apply needs the momentum buffer");
+      if (!(pk && C <= ew_pk_one_max_blocks()))
+        throw std::runtime_error("ewdml topk: the dense write-pass apply runs in k_pk_one only");
+    }
   }
   if (pk) {
     // predictive path: hist0 (+ candidates) -> 3 radix passes over the candidates -> write.

@@ -329,7 +329,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_wg_output(const float* __restrict_
                                                         const float* __restrict__ addend) {
   typedef float T __attribute__((ext_vector_type(VW)));
   constexpr int A = Wg<M>::A;
-  __shared__ float red[2][EW_BLOCK * 4];
+  __shared__ __attribute__((aligned(16))) float red[2][EW_BLOCK * 4];
   const int tpr = Nc / VW, rpi = EW_BLOCK / tpr;
   const int t = threadIdx.x, rg = t / tpr, c0 = (t - rg * tpr) * VW;
   const long long t0 = (long long)blockIdx.x * tpb;
@@ -420,10 +420,18 @@ __global__ __launch_bounds__(EW_BLOCK) void k_wg_output(const float* __restrict_
       }
   }
   if (!bnpart) return;
+  // one VW-wide store per thread and array (lanes' vectors contiguous): scalar stores of
+  // stride-VW addresses were VW-way bank conflicts (2.0 conflicts per LDS instruction, round-5
+  // PMC table)
+  {
+    T a, b;
 #pragma unroll
-  for (int q = 0; q < VW; ++q) {
-    red[0][rg * Nc + c0 + q] = s1[q];
-    red[1][rg * Nc + c0 + q] = s2[q];
+    for (int q = 0; q < VW; ++q) {
+      a[q] = s1[q];
+      b[q] = s2[q];
+    }
+    *reinterpret_cast<T*>(&red[0][rg * Nc + c0]) = a;
+    *reinterpret_cast<T*>(&red[1][rg * Nc + c0]) = b;
   }
   __syncthreads();
   const int nb = gridDim.x;

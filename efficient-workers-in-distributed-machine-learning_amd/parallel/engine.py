@@ -89,6 +89,7 @@ class GradientExchange:
         self.vel = torch.zeros_like(flat.grad) if self.dgc else None
         self.gest = torch.zeros_like(flat.grad) if self.ef21 else None  # EF21's global G
         self.local_apply = False  # enable_local_apply
+        self.local_apply_dense = False
         if not flat.attach_grads and not self.cuda:
             raise ValueError("pointer-mode gradients need the HIP kernels (device tensors)")
         self._pack_plans = [ops.DevicePlan(b.plan, self.device) for b in flat.buckets] \
@@ -137,11 +138,18 @@ class GradientExchange:
         The caller guarantees that the encode runs after backward produced every gradient (one
         bucket, no segmented step): the apply moves parameters.  Returns whether it is on."""
         codec = self.codec
-        self.local_apply = bool(
-            self.cuda and self.N == 1 and self.nb == 1 and self.dgc and not self.ef21
-            and not codec.allreduce
-            and codec.kind in ("topk", "topk_qsgd") and getattr(codec, "norm", "max") == "max"
-            and getattr(self.opt, "fusable", False) and ops._TOPK_PREDICT and not self.src_flat)
+        ok = bool(self.cuda and self.N == 1 and self.nb == 1 and not self.ef21
+                  and not codec.allreduce and codec.kind in ("topk", "topk_qsgd")
+                  and getattr(codec, "norm", "max") == "max"
+                  and getattr(self.opt, "fusable", False) and ops._TOPK_PREDICT
+                  and not self.src_flat)
+        # momentum-corrected EF: the sparse step at the sent coordinates; otherwise (no EF or
+        # plain EF: the momentum runs on the receiver) the dense step over the whole bucket,
+        # which the one-launch encode (k_pk_one) runs chunk by chunk after its write
+        self.local_apply_dense = ok and not self.dgc
+        if self.local_apply_dense:
+            ok = all(ops.topk_one_launch(dp) for dp in codec.dplans)
+        self.local_apply = ok
         return self.local_apply
 
     def _apply_hp(self, bi: int) -> dict:
@@ -302,13 +310,18 @@ class GradientExchange:
                        lr_t=None if self.dgc_mask else getattr(o, "lr_t", None))
         apply = None
         if self.local_apply:  # world of one: the write pass applies the update (no decode)
-            hp = self._apply_hp(bi)
             adv = self.dev_key_advance and self.use_dev_key and bi == self.nb - 1
+            o = self.opt
+            hp = o.hparams() if self.local_apply_dense else self._apply_hp(bi)
             apply = dict(param=self.flat.data_view(b), shadow=self.flat.shadow_view(b),
                          lr=hp["lr"], lr_tensor=hp.get("lr_t"),
                          grad_scale=self.predivide / self.N,
                          key_state=self.key_state if adv else None, key_seed=self.codec.seed,
                          key_rank=self.comm.rank)
+            if self.local_apply_dense:  # the receiver's momentum SGD over every element
+                apply.update(mom=o.mom[b.start:b.start + b.length], momentum=hp["momentum"],
+                             dampening=hp["dampening"], weight_decay=hp["weight_decay"],
+                             nesterov=hp["nesterov"], first=o.first)
         self.codec.encode(bi, g, self.payload[bi], self.step_idx + self.seed_offset,
                           self.comm.rank, resid,
                           key_tensor=self.key_dev if self.use_dev_key else None, dgc=dgc,

@@ -580,8 +580,9 @@ def _check_side_run(flags, ref, l_ref):
     tr.close()
 
 
+@pytest.mark.parametrize("ef", [True, False])
 @pytest.mark.parametrize("graph", ["off", "full"])
-def test_world_of_one_encode_apply_bitwise_decode(monkeypatch, graph):
+def test_world_of_one_encode_apply_bitwise_decode(monkeypatch, graph, ef):
     """A world of one: the top-k write pass applies the update (GradientExchange.
     enable_local_apply, no decode launch) -- the trajectory is bitwise the one with the decode of
     the one-rank all-gather (EWDML_LOCAL_APPLY=0), eager and through the captured (unrolled)
@@ -589,8 +590,8 @@ def test_world_of_one_encode_apply_bitwise_decode(monkeypatch, graph):
     from ewdml.runtime import Trainer
 
     ops.require()
-    flags = LENET + ["--compress", "topk_qsgd", "--error-feedback", "--ef-warmup", "none",
-                     "--hip-graph", graph, "--max-steps", "40"]
+    flags = LENET + ["--compress", "topk_qsgd", "--hip-graph", graph, "--max-steps", "40"] + (
+        ["--error-feedback", "--ef-warmup", "none"] if ef else [])  # (LENET: no EF otherwise)
     res = []
     for on in ("0", "1"):
         monkeypatch.setenv("EWDML_LOCAL_APPLY", on)

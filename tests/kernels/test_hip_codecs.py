@@ -699,3 +699,49 @@ def test_topk_encode_apply_matches_decode(numels, kind, bits):
         assert torch.equal(a.view(torch.uint8) if a.dtype != torch.uint8 else a,
                            b.view(torch.uint8) if b.dtype != torch.uint8 else b), name
     assert not torch.equal(runs[0][0], p0)
+
+
+@pytest.mark.parametrize("ef", ["none", "plain"])
+@pytest.mark.parametrize("kind,bits", [("topk_qsgd", 8), ("topk", 8)])
+def test_topk_encode_dense_apply_matches_decode(ef, kind, bits):
+    """A world of one without momentum correction (the reference's Method 5: the momentum runs
+    on the receiver): the one-launch encode applies the dense momentum step over its chunk after
+    the write -- parameters, momentum, bf16 shadow and key state bitwise the encode followed by
+    the decode's dense pass (k_topk_decode_apply with a momentum buffer), step after step."""
+    ops.require()
+    plan = _plan(SMALL, 0.01, bucket_offset=64)
+    lay = Layout.build(kind, plan, bits)
+    levels = 127 if bits == 8 else 7
+    gen = torch.Generator().manual_seed(6)
+    p0 = torch.randn(plan.length, generator=gen).to(DEV)
+    m0 = torch.randn(plan.length, generator=gen).to(DEV) * 0.1
+    hp = dict(lr=0.05, momentum=0.9, dampening=0.0, weight_decay=1e-4, nesterov=True)
+    runs = []
+    for fused in (False, True):
+        dp = ops.DevicePlan(plan, DEV)
+        assert ops.topk_one_launch(dp)
+        pay = torch.zeros(lay.nbytes, dtype=torch.uint8, device=DEV)
+        r = torch.zeros(plan.length, device=DEV) if ef == "plain" else None
+        p, m = p0.clone(), m0.clone()
+        sh = p0.to(torch.bfloat16)
+        k3 = int(stream_key(9, 3, 0))
+        ks = torch.tensor([3, k3 - (1 << 32) if k3 >= 1 << 31 else k3], dtype=torch.int32,
+                          device=DEV)
+        for it in range(6):
+            g = _grad(plan, seed=90 + it).to(DEV)
+            first = it == 0
+            if fused:
+                ops.topk_encode(dp, g, pay, lay, levels, "max", 0, resid=r, key_tensor=ks[1:2],
+                                apply=dict(param=p, mom=m, shadow=sh, grad_scale=1.0,
+                                           key_state=ks, key_seed=9, key_rank=0, first=first,
+                                           **hp))
+            else:
+                ops.topk_encode(dp, g, pay, lay, levels, "max", 0, resid=r, key_tensor=ks[1:2])
+                ops.topk_decode_apply(dp, pay.view(1, -1), lay, levels, param=p, mom=m,
+                                      grad_scale=1.0, shadow=sh, key_state=ks, key_seed=9,
+                                      key_rank=0, first=first, **hp)
+        torch.cuda.synchronize()
+        runs.append((p, m, sh, ks, pay))
+    for name, a, b in zip(("param", "mom", "shadow", "key_state", "payload"), *runs):
+        assert torch.equal(a.view(torch.uint8) if a.dtype != torch.uint8 else a,
+                           b.view(torch.uint8) if b.dtype != torch.uint8 else b), name
