@@ -64,13 +64,25 @@ def build(verbose: bool = False, force: bool = False) -> str:
                    "-I", pybind11.get_include(), "-I", sysconfig.get_paths()["include"],
                    "-fvisibility=hidden", "-o", obj, src]
         jobs.append(cmd)
+    import time
+
+    def timed(cmd):
+        t0 = time.time()
+        r = _run(cmd)
+        return cmd, r, time.time() - t0
+
     with ThreadPoolExecutor(max_workers=min(8, max(1, len(jobs)))) as ex:
-        for r in ex.map(_run, jobs):
-            if verbose and (r.stdout or r.stderr):
-                print(r.stdout, r.stderr)
+        for cmd, r, dt in ex.map(timed, jobs):
+            if verbose:  # one line per compiled file: the command and its wall time
+                print(f"[{dt:6.1f} s] {' '.join(cmd)}", flush=True)
+                if r.stdout or r.stderr:
+                    print(r.stdout, r.stderr)
     out = ext_path()
     if force or jobs or not os.path.exists(out):
-        _run([HIPCC, "-shared", f"--offload-arch={ARCH}", "-fPIC", "-o", out, *objs])
+        link = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-fPIC", "-o", out, *objs]
+        _run(link)
+        if verbose:
+            print(" ".join(link), flush=True)
     return out
 
 

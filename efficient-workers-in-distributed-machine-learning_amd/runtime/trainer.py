@@ -248,14 +248,6 @@ class Trainer:
                 self.graph_mode = "full"
             else:
                 self.graph_mode = "split" if ps_split else "off"
-        if (self.world == 1 and type(self.exchange) is GradientExchange
-                and len(self.flat.buckets) == 1 and self.graph_mode != "segmented"
-                and os.environ.get("EWDML_LOCAL_APPLY", "1") != "0"):
-            # a world of one: the top-k write pass applies the update (the all-gather of one
-            # payload is that payload: no decode launch).  One bucket, encoded once backward has
-            # produced every gradient (an earlier bucket's encode would move parameters that the
-            # rest of backward still reads); EWDML_LOCAL_APPLY=0: decode
-            self.exchange.enable_local_apply()
         if self.graph_mode != "off" and not (isinstance(self.exchange, GradientExchange) or
                                              (self.local_sgd and self.graph_mode == "full") or
                                              (ps_split and self.graph_mode == "split")):
@@ -273,6 +265,14 @@ class Trainer:
             # one graph has no inside to time: cut it at the collectives (graph A -> eager
             # collectives -> graph B) so the communication / computation split is measured
             self.graph_mode = "split"
+        if (self.world == 1 and type(self.exchange) is GradientExchange
+                and len(self.flat.buckets) == 1 and self.graph_mode in ("full", "off")
+                and os.environ.get("EWDML_LOCAL_APPLY", "1") != "0"):
+            # a world of one: the top-k write pass applies the update (the all-gather of one
+            # payload is that payload: no decode launch).  One bucket, encoded once backward has
+            # produced every gradient (an earlier bucket's encode would move parameters that the
+            # rest of backward still reads); EWDML_LOCAL_APPLY=0: decode
+            self.exchange.enable_local_apply()
         # --phase-timing: the step's phase clock, shared with the exchange (engine.Stopwatch)
         self.clock = Stopwatch(self.cuda) if cfg.phase_timing else None
         for e in (self.exchange, getattr(self.exchange, "inner", None)):
