@@ -256,7 +256,20 @@ def topk_encode(dp: DevicePlan, grad, payload, layout, levels: int, norm: str, k
                   dp.plan.bucket_offset & 0xFFFFFFFF, _keyp(key_tensor), _stream(), _ptr(vel),
                   _ptr(par), mom, damp1, wd, nest, layout.bitmap, dmask, _lrp(lrt), dp.plan.length,
                   _ptr(dp.cblocks), dp.plan.num_cblocks, int(_TOPK_PREDICT), int(_LB_FAULT[0]),
-                  int(max(dp.plan.ks)) if dp.plan.ks else 0, *_apply_args(dp, apply, norm))
+                  int(max(dp.plan.ks)) if dp.plan.ks else 0, *_apply_args(dp, apply, norm),
+                  _stamps_ptr(dp, dgc))
+
+
+def _stamps_ptr(dp, dgc):
+    """The producer-staging stamp words of a momentum-corrected encode (``dgc["stamps"]``:
+    int32 [T] device tensor, 1 = that tensor's producer already staged it this step)."""
+    st = None if dgc is None else dgc.get("stamps")
+    if st is None:
+        return 0
+    _check(st, torch.int32, "stamps", align=4)
+    if st.numel() < dp.plan.num_tensors:
+        raise ValueError("one stamp word per tensor of the bucket")
+    return st.data_ptr()
 
 
 def topk_one_launch(dp) -> bool:

@@ -266,6 +266,40 @@ def new_pass():
     _USE_EPOCH[0] += 1
 
 
+# the momentum-corrected error-feedback staging of a weight gradient done by the kernel that
+# forms it (the small-map backward; ops/csrc/dgc_stage.h): the exchange engine arms a parameter
+# with ``_ew_dgc_stage`` (velocity / residual / parameter pointers at its slot, the momentum
+# hyper-parameters, its stamp word) and the encode reads e instead of the gradient.
+# Opt-in (EWDML_PRODUCER_STAGE=1): measured a wash on VGG-11 -- the encode's first pass gets
+# ~10 us shorter and the two small-map backward launches ~4 us longer each
+# (profiles/ab/README.md "Round 6"); off, the encode stages every tensor itself
+_PRODUCER_STAGE = os.environ.get("EWDML_PRODUCER_STAGE", "0") == "1"
+STAGE_RIDES = 0  # weight gradients staged by their producer (tests / diagnostics)
+_NO_STAGE = (0, 0, 0, 0.0, 1.0, 0.0, 0, 0, 0)
+
+
+def _stage_args(ctx):
+    """The staging arguments of this conv's weight gradient, or None: armed by the exchange,
+    and (as for a deferred transform) dw installed, not accumulated, and read by nothing but
+    the engine's encode -- the gradient itself is never written."""
+    p = getattr(ctx, "w_param", None)
+    st = getattr(p, "_ew_dgc_stage", None) if p is not None else None
+    if st is None or not _PRODUCER_STAGE or not _can_defer_any(p):
+        return None
+    return st
+
+
+def _can_defer_any(p):
+    if not (p.grad is None and p.dtype == torch.float32 and p.requires_grad
+            and not torch.is_grad_enabled()):
+        return False
+    if getattr(p, "_backward_hooks", None) or getattr(p, "_ew_tied", False):
+        return False
+    eng = getattr(p, "_ew_engine_hooks", 0)
+    post = getattr(p, "_post_accumulate_grad_hooks", None)
+    return eng > 0 and (not post or len(post) <= eng)
+
+
 def _can_defer(ctx):
     # opt-in: only parameters whose sole post-accumulate hooks are the exchange engine's (which
     # flushes before it reads); no tensor hooks on the weight (they would see dw unwritten)
@@ -800,6 +834,12 @@ class _Conv(torch.autograd.Function):
             fin = bn_fin_outputs(node, C, x.device)
         coef, fdg, fdb, fdcb = fin if fin is not None else (None,) * 4
         cb_dtype = getattr(node, "cb_dtype", None) if node is not None else None
+        # the exchange's momentum-corrected error-feedback staging of this weight's gradient, done
+        # by the weight-gradient tiles of this launch (dgc_stage.h): dw is then never stored
+        stage = _stage_args(ctx) if dw is not None else None
+        if stage is not None:
+            global STAGE_RIDES
+            STAGE_RIDES += 1
         rows = C_.sm_f32_bwd(_ptr(x) if xsrc is None else 0, _ptr(bh), _ptr(bstats),
                              _ptr(dy) if lazy is None else 0, _ptr(oh), _ptr(odn), _ptr(ocode),
                              _ptr(ostats), _ptr(ocoef), int(bool(opool)), _ptr(w), _ptr(dx),
@@ -808,7 +848,7 @@ class _Conv(torch.autograd.Function):
                              _ptr(part), part.numel() if part is not None else 0, _ptr(coef),
                              _ptr(fdg), _ptr(fdb), _ptr(fdcb), int(cb_dtype == torch.bfloat16),
                              ph.shape[0] * ph.shape[2] * ph.shape[3] if ph is not None else 0,
-                             _stream())
+                             _stream(), *(stage or _NO_STAGE))
         if rows > 0:
             node._ew_pre_bwd = (part, rows, dx, dx._version)
             if fin is not None:

@@ -37,8 +37,9 @@ PYBIND11_MODULE(_C, m) {
            float apply_lr, uintptr_t apply_lr_ptr, float apply_scale,
            uintptr_t apply_key_state, uint32_t apply_key_seed, uint32_t apply_key_rank,
            int apply_mom_set, uintptr_t apply_mom, float apply_momentum, float apply_dampening,
-           float apply_wd, int apply_nesterov, int apply_first) {
+           float apply_wd, int apply_nesterov, int apply_first, uintptr_t dgc_stamps) {
           TopkEncodeArgs a{};
+          a.dgc_stamps = dgc_stamps;
           a.apply_mom_set = apply_mom_set;
           a.apply_mom = apply_mom;
           a.apply_momentum = apply_momentum;

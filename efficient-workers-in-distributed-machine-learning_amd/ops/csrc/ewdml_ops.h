@@ -42,6 +42,7 @@ struct TopkEncodeArgs {
   float apply_lr, apply_scale;
   uint32_t apply_key_seed, apply_key_rank;
   // dense variant (receiver-side momentum SGD over every element; one-launch encodes only)
+  uintptr_t dgc_stamps;  // nullable u32[T]: producer-staged tensors (dgc_stage.h)
   int apply_mom_set;
   uintptr_t apply_mom;
   float apply_momentum, apply_dampening, apply_wd;
@@ -343,7 +344,10 @@ int ew_sm_f32_bwd(uintptr_t x, uintptr_t bn_h, uintptr_t bn_stats, uintptr_t dy,
                   long long N, int C, int Nc, uintptr_t pb_h, uintptr_t pb_res, uintptr_t pb_code,
                   uintptr_t pb_stats, int pb_relu, uintptr_t bnpart, long long bnpart_floats,
                   uintptr_t fin_coef, uintptr_t fin_dgamma, uintptr_t fin_dbeta,
-                  uintptr_t fin_dcbias, int fin_cb_bf16, long long fin_M, uintptr_t stream);
+                  uintptr_t fin_dcbias, int fin_cb_bf16, long long fin_M, uintptr_t stream,
+                  uintptr_t st_vel = 0, uintptr_t st_resid = 0, uintptr_t st_param = 0,
+                  float st_momentum = 0.0f, float st_damp1 = 1.0f, float st_wd = 0.0f,
+                  int st_nesterov = 0, uintptr_t st_lr = 0, uintptr_t st_stamp = 0);
 
 // ---- LeNet's fp32 training step in four launches (lenet_f32.hip): persistent workspace floats
 // and ticket ints (zeroed once; the kernels leave them zero) for batch B

@@ -43,6 +43,7 @@
 
 #include "bn_fin.h"
 #include "common.h"
+#include "dgc_stage.h"
 #include "conv_f32.h"
 #include "ewdml_ops.h"
 
@@ -551,7 +552,8 @@ __global__ __launch_bounds__(SM_T) void k_sm_bwd(SmX xs, SmDy ds, const float* _
                                                  float* __restrict__ slab, int* __restrict__ cnt,
                                                  int N, int C, int Nc, int nbd, CfBnBwd bb,
                                                  float* __restrict__ bnpart, int fence,
-                                                 EwBnFin fin, int* __restrict__ fcnt) {
+                                                 EwBnFin fin, int* __restrict__ fcnt,
+                                                 DgcStage st) {
   __shared__ __attribute__((aligned(16))) char smem[2 * SM_STAGE + 16];
   int& flag = *reinterpret_cast<int*>(smem + 2 * SM_STAGE);
   const int t = threadIdx.x;
@@ -666,6 +668,21 @@ __global__ __launch_bounds__(SM_T) void k_sm_bwd(SmX xs, SmDy ds, const float* _
     RawDy r;
     int op;
   };
+  // producer staging (dgc_stage.h): the tile's velocity / residual (/ parameter) loads issued
+  // here, ahead of the k-loop, so they are in registers by the epilogue
+  float su[SM_NJ][4], sr[SM_NJ][4], sp[SM_NJ][4];
+  if (st.vel) {
+#pragma unroll
+    for (int j = 0; j < SM_NJ; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const long long i =
+            ((long long)(o0 + sm_row(wm, lane, e)) * 9 + tap) * C + c0 + sm_col(wn, lane, j);
+        su[j][e] = st.vel[i];
+        sr[j][e] = st.resid[i];
+        sp[j][e] = st.wd != 0.0f ? st.param[i] : 0.0f;
+      }
+  }
   SmAcc acc;
   sm_gemm<SM_RC, SM_RC, RawDyOp, RawX>(
       smem, np * spp,
@@ -688,6 +705,19 @@ __global__ __launch_bounds__(SM_T) void k_sm_bwd(SmX xs, SmDy ds, const float* _
       },
       [&](const RawDyOp& r, int i) { return sm_make_dy<DK>(ds, r.op, r.r, k, i); },
       [&](const RawX& r, int i) { return sm_make_x<XK>(r, i); }, acc);
+  if (st.vel) {  // the encode's error-feedback staging here (dgc_stage.h): dw is never stored
+    const float lr = st.lr_ptr ? *st.lr_ptr : 1.0f;
+#pragma unroll
+    for (int j = 0; j < SM_NJ; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        dgc_stage_loaded(st, lr,
+                         ((long long)(o0 + sm_row(wm, lane, e)) * 9 + tap) * C + c0 +
+                             sm_col(wn, lane, j),
+                         acc.a[j][e], su[j][e], sr[j][e], sp[j][e]);
+    if (b == 0 && t == 0) *st.stamp = 1u;  // read by the encode, a later kernel
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < SM_NJ; ++j)
 #pragma unroll
@@ -769,8 +799,17 @@ int ew_sm_f32_bwd(uintptr_t x, uintptr_t bn_h, uintptr_t bn_stats, uintptr_t dy,
                   long long N, int C, int Nc, uintptr_t pb_h, uintptr_t pb_res, uintptr_t pb_code,
                   uintptr_t pb_stats, int pb_relu, uintptr_t bnpart, long long bnpart_floats,
                   uintptr_t fin_coef, uintptr_t fin_dgamma, uintptr_t fin_dbeta,
-                  uintptr_t fin_dcbias, int fin_cb_bf16, long long fin_M, uintptr_t stream) {
+                  uintptr_t fin_dcbias, int fin_cb_bf16, long long fin_M, uintptr_t stream,
+                  uintptr_t st_vel, uintptr_t st_resid, uintptr_t st_param, float st_momentum,
+                  float st_damp1, float st_wd, int st_nesterov, uintptr_t st_lr,
+                  uintptr_t st_stamp) {
   sm_check(N, C, Nc);
+  const DgcStage st{reinterpret_cast<float*>(st_vel), reinterpret_cast<float*>(st_resid),
+                    reinterpret_cast<const float*>(st_param), st_momentum, st_damp1, st_wd,
+                    st_nesterov, reinterpret_cast<const float*>(st_lr),
+                    reinterpret_cast<uint32_t*>(st_stamp)};
+  if (st.vel && !(dw && st.resid && st.stamp && (st.wd == 0.0f || st.param)))
+    throw std::runtime_error("ewdml small-map conv: error-feedback staging arguments missing");
   if (!dy && !(out_h && out_dnext && out_stats && out_coef))
     throw std::runtime_error("ewdml small-map conv: backward needs dy or its BN source");
   if (out_h && out_pool && !out_code)
@@ -815,7 +854,8 @@ int ew_sm_f32_bwd(uintptr_t x, uintptr_t bn_h, uintptr_t bn_stats, uintptr_t dy,
   float* dwp = reinterpret_cast<float*>(dw);
 #define SM_BWD(XK_, DK_)                                                                         \
   hipLaunchKernelGGL((k_sm_bwd<XK_, DK_>), grid, dim3(SM_T), 0, (hipStream_t)stream, xs, ds, wp, \
-                     dxp, dwp, sp, cp, (int)N, C, Nc, nbd, bb, bp, sm_fence(), fin, cp + tiles)
+                     dxp, dwp, sp, cp, (int)N, C, Nc, nbd, bb, bp, sm_fence(), fin, cp + tiles, \
+                     st)
   // DK: dy materialised (0), formed from the BN layer it feeds (2), that layer pooled 2x2 -> 1x1 (3)
   const int dk = dy ? 0 : out_pool ? 3 : 2;
   if (bn_h) {

@@ -83,6 +83,10 @@ struct DgcArgs {
   int nesterov;
   int mask;              // momentum factor masking (DGC) | keep the velocity (--ef-mode local)
   const float* lr_ptr;   // nullable: accumulate lr-scaled updates (--ef-mode local)
+  // nullable, one word per tensor: 1 = the gradient's producer already staged this tensor
+  // (dgc_stage.h: e in the residual, the velocity updated, the gradient never stored); the encode
+  // reads e and clears the word (its write pass)
+  uint32_t* stamps;
 };
 
 // error-feedback mode of the encode: none, plain (e = g + r), momentum-corrected (DGC)
@@ -211,6 +215,21 @@ __device__ __forceinline__ void topk_ef_stage(const GradPtrs& gp, const DgcArgs&
   }
 }
 
+// The chunk to compress into registers: the gradient, staged (topk_ef_stage) -- or, for a tensor
+// its producer already staged this step (DgcArgs.stamps, dgc_stage.h), e straight from the
+// residual: neither the gradient nor the velocity is read, nothing is written.
+template <int EFM, bool HALVES = false>
+__device__ __forceinline__ void topk_load_stage(const GradPtrs& gp, const DgcArgs& dg,
+                                                float* __restrict__ resid, const ChunkRow& c,
+                                                float4 (&v)[EW_CU]) {
+  if (EFM == EF_DGC && dg.stamps && dg.stamps[c.tensor]) {
+    ew_ld_chunk(gp, resid, c, v);
+    return;
+  }
+  ew_ld_chunk(gp, nullptr, c, v);
+  topk_ef_stage<EFM, HALVES>(gp, dg, resid, c, v);
+}
+
 // state[t] = {prefix, k_rem, max_key, pad}
 template <int EFM>
 __global__ __launch_bounds__(EW_BLOCK) void k_topk_hist0(GradPtrs gp, DgcArgs dg,
@@ -234,8 +253,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_hist0(GradPtrs gp, DgcArgs dg
   // the write pass's look-back word of this chunk, from the previous encode (stream-ordered)
   if (threadIdx.x == 0) lb[blockIdx.x] = 0ull;
   float4 v[EW_CU];
-  ew_ld_chunk(gp, nullptr, c, v);
-  topk_ef_stage<EFM>(gp, dg, resid, c, v);
+  topk_load_stage<EFM>(gp, dg, resid, c, v);
   uint32_t kmax = 0;
 #pragma unroll
   for (int u = 0; u < EW_CU; ++u) {
@@ -884,7 +902,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_write(
     int* __restrict__ lb_err, const uint32_t* __restrict__ pst,
     const uint32_t* __restrict__ cbase, const uint32_t* __restrict__ ccnt,
     const uint2* __restrict__ pcand, int lb_fault, uint32_t* __restrict__ rz1, uint32_t rz1_words,
-    uint32_t* __restrict__ rz2, uint32_t rz2_words, TkApply ap) {
+    uint32_t* __restrict__ rz2, uint32_t rz2_words, TkApply ap, uint32_t* __restrict__ stamps) {
   __shared__ uint32_t ws[EW_WAVES];
   ew_sgd_resolve(ap.sa);
   __shared__ uint32_t s_lb[2 * EW_WAVES];
@@ -905,6 +923,8 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_write(
   }
   const uint32_t key = keyp ? *keyp : key_arg;  // device key: fresh per replay of a captured graph
   const TensorRow tr = tensors[c.tensor];
+  // the producer-staging stamps were read by the staging pass (an earlier launch): re-arm
+  if (stamps && c.local == 0 && threadIdx.x == 0) stamps[c.tensor] = 0u;
   if (PK && pst[c.tensor * 8 + 3]) {  // predictive fast path: the chunk's candidates only
     // the tensor's selection state, loaded together before the look-back's barriers
     topk_write_cands<VK, EF>(c, tr, resid, vel, state, payload, scales_off, idx_off, codes_off,
@@ -1245,8 +1265,7 @@ __global__ __launch_bounds__(EW_BLOCK, WPE) void k_pk_hist0(
   if (blockIdx.x == 0)
     for (int t = threadIdx.x; t < T; t += EW_BLOCK) tick[TICK_STRIDE * (T + t)] = 0;
   float4 v[EW_CU];
-  ew_ld_chunk(gp, nullptr, c, v);
-  topk_ef_stage<EFM, (WPE > 0)>(gp, dg, resid, c, v);
+  topk_load_stage<EFM, (WPE > 0)>(gp, dg, resid, c, v);
   const uint32_t P = pst[c.tensor * 8];
   uint32_t kmax = 0;
   unsigned long long pa = 0, pb = 0;  // candidates per slab, 16-bit fields (slabs 0-3, 4-7)
@@ -1945,8 +1964,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_pk_one(
   ew_sgd_resolve(ap.sa);
   // ---- 1. stage (error feedback) and compact the candidates (k_pk_hist0) ----
   float4 v[EW_CU];
-  ew_ld_chunk(gp, nullptr, c, v);
-  topk_ef_stage<EFM>(gp, dg, resid, c, v);
+  topk_load_stage<EFM>(gp, dg, resid, c, v);
   // the previous launch's prediction (and its steering state, for the tensor-last block)
   const uint32_t P = pst[t * 8], pbeta = pst[t * 8 + 1], phad = pst[t * 8 + 4];
   PK1_STAMP(1);
@@ -2012,6 +2030,8 @@ __global__ __launch_bounds__(EW_BLOCK) void k_pk_one(
   PK1_STAMP(2);
   if (topk_tensor_last(tick + TICK_STRIDE * t, tr.nchunks, reinterpret_cast<int*>(wmax))) {
     PK1_STAMP(6);
+    // every block of the tensor read its producer-staging stamp before arriving: re-arm it
+    if (dg.stamps && threadIdx.x == 0) dg.stamps[t] = 0u;
     if (threadIdx.x == 0) {
       int* cc = ccount + TICK_STRIDE * t;
       // the candidate count and the max-key replicas: all loads in flight together
@@ -2776,7 +2796,10 @@ void ew_topk_encode(const TopkEncodeArgs& a) {
   // each pass's per-tensor step (select / scan) runs in the tensor's last-arriving chunk block
   DgcArgs dg{reinterpret_cast<float*>(a.vel), reinterpret_cast<const float*>(a.param),
              a.dgc_momentum, a.dgc_damp1, a.dgc_wd, a.dgc_nesterov, a.dgc_mask,
-             reinterpret_cast<const float*>(a.dgc_lr_ptr)};
+             reinterpret_cast<const float*>(a.dgc_lr_ptr),
+             reinterpret_cast<uint32_t*>(a.dgc_stamps)};
+  if (dg.stamps && !dg.vel)
+    throw std::runtime_error("ewdml topk: producer-staging stamps need momentum correction");
   if (dg.vel && !resid) throw std::runtime_error("ewdml topk: momentum correction needs a residual");
   if (dg.vel && dg.wd != 0.0f && !dg.param)
     throw std::runtime_error("ewdml topk: weight decay in the momentum correction needs params");
@@ -2876,7 +2899,8 @@ void ew_topk_encode(const TopkEncodeArgs& a) {
             chunk_ties, inv, pay, a.scales_off, a.idx_off, a.codes_off, a.bitmap_off, a.levels,   \
             a.inv_levels, a.key, reinterpret_cast<const uint32_t*>(a.key_ptr), a.bucket_offset,   \
             kmaxr, pk_rz0, dg.mask ? dg.vel : nullptr, lb, a.counts_off, lb_err, pst, cbase,      \
-            ccnt, pcand, a.lb_fault, hist1, (uint32_t)(T * NB1), hist2, (uint32_t)(T * NB2), ap)
+            ccnt, pcand, a.lb_fault, hist1, (uint32_t)(T * NB1), hist2, (uint32_t)(T * NB2), ap, \
+            dg.stamps)
     if (a.value_kind == VK_Q8) {
       if (resid) EW_PKW(VK_Q8, true); else EW_PKW(VK_Q8, false);
     } else if (a.value_kind == VK_Q4) {
@@ -2913,7 +2937,7 @@ void ew_topk_encode(const TopkEncodeArgs& a) {
             chunk_ties, inv, pay, a.scales_off, a.idx_off, a.codes_off, a.bitmap_off, a.levels,     \
             a.inv_levels, a.key, reinterpret_cast<const uint32_t*>(a.key_ptr), a.bucket_offset,     \
             kmaxr, rezero_words, dg.mask ? dg.vel : nullptr, lb, a.counts_off, lb_err, nullptr,     \
-            nullptr, nullptr, nullptr, a.lb_fault, nullptr, 0u, nullptr, 0u, TkApply{})
+            nullptr, nullptr, nullptr, a.lb_fault, nullptr, 0u, nullptr, 0u, TkApply{}, dg.stamps)
 #define EW_WRITE2(VK, EFV) \
   do { if (lbk) EW_WRITE(VK, EFV, true); else EW_WRITE(VK, EFV, false); } while (0)
   if (a.value_kind == VK_Q8) {

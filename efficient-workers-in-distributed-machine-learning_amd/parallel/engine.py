@@ -90,6 +90,25 @@ class GradientExchange:
         self.gest = torch.zeros_like(flat.grad) if self.ef21 else None  # EF21's global G
         self.local_apply = False  # enable_local_apply
         self.local_apply_dense = False
+        # producer staging (ops/csrc/dgc_stage.h): the kernel forming a weight gradient (the
+        # small-map backward) runs this exchange's momentum-corrected error-feedback staging
+        # itself -- velocity and e written, the gradient never stored -- and sets the tensor's
+        # stamp word, so the encode's first pass reads e alone for it.  Every parameter is armed
+        # with its slots (ops/conv.py _stage_args decides per launch whether it may apply)
+        self.stamps = None
+        if self.dgc and self.cuda and not flat.attach_grads:
+            self.stamps = [torch.zeros(len(b.params), dtype=torch.int32, device=self.device)
+                           for b in flat.buckets]
+            o = optimizer
+            vp, rp, pp = self.vel.data_ptr(), self.resid.data_ptr(), flat.data.data_ptr()
+            lrt = getattr(o, "lr_t", None)
+            lrp = lrt.data_ptr() if (not self.dgc_mask and lrt is not None) else 0
+            for b, st in zip(flat.buckets, self.stamps):
+                for ti, (p, off) in enumerate(zip(b.params, b.plan.offsets)):
+                    base = 4 * (b.start + off)
+                    p._ew_dgc_stage = (vp + base, rp + base, pp + base, float(o.momentum),
+                                       float(1.0 - o.dampening), float(o.weight_decay),
+                                       int(bool(o.nesterov)), lrp, st.data_ptr() + 4 * ti)
         if not flat.attach_grads and not self.cuda:
             raise ValueError("pointer-mode gradients need the HIP kernels (device tensors)")
         self._pack_plans = [ops.DevicePlan(b.plan, self.device) for b in flat.buckets] \
@@ -307,7 +326,8 @@ class GradientExchange:
                        dampening=o.dampening, nesterov=o.nesterov, weight_decay=o.weight_decay,
                        param=self.flat.data_view(b), mask=self.dgc_mask,
                        lr=None if self.dgc_mask else o.lr,
-                       lr_t=None if self.dgc_mask else getattr(o, "lr_t", None))
+                       lr_t=None if self.dgc_mask else getattr(o, "lr_t", None),
+                       stamps=self.stamps[bi] if self.stamps is not None else None)
         apply = None
         if self.local_apply:  # world of one: the write pass applies the update (no decode)
             adv = self.dev_key_advance and self.use_dev_key and bi == self.nb - 1
@@ -490,6 +510,11 @@ class GradientExchange:
         return {"topk_encode_fast": tot["fast"], "topk_encode_full": tot["full"]}
 
     def close(self):
+        if self.stamps is not None:
+            for p in self.flat.params:
+                if hasattr(p, "_ew_dgc_stage"):
+                    del p._ew_dgc_stage
+            self.stamps = None
         if self._hooks:
             for p in self.flat.params:
                 p._ew_engine_hooks = max(0, getattr(p, "_ew_engine_hooks", 1) - 1)

@@ -607,3 +607,42 @@ def test_world_of_one_encode_apply_bitwise_decode(monkeypatch, graph, ef):
     assert torch.equal(res[0][0], res[1][0])
     assert res[0][1] == res[1][1]
     assert torch.equal(res[0][2], res[1][2])
+
+
+@pytest.mark.parametrize("graph", ["off", "full"])
+def test_producer_staging_bitwise_encode_staging(graph):
+    """The small-map backward runs the exchange's momentum-corrected error-feedback staging for
+    VGG-11's conv7 / conv8 weights itself (ops/csrc/dgc_stage.h: velocity and e written, the
+    gradient never stored, the tensor stamped) and the encode reads e for those tensors: the
+    trajectory -- parameters, residual, velocity -- is bitwise the one where the encode stages
+    every tensor, eager and in the captured graph."""
+    from ewdml.ops import conv as cmod
+    from ewdml.runtime import Trainer
+
+    ops.require()
+    flags = ["--network", "VGG11", "--dataset", "Cifar10", "--batch-size", "64",
+             "--synthetic-size", "1024", "--momentum", "0.9", "--lr", "0.02", "--eval-freq", "0",
+             "--quiet", "--device", "cuda", "--amp", "none", "--graph-warmup", "2",
+             "--compress", "topk_qsgd", "--error-feedback", "--ef-warmup", "none",
+             "--hip-graph", graph, "--max-steps", "20"]
+    res = []
+    saved = cmod._PRODUCER_STAGE
+    try:
+        for on in (False, True):
+            cmod._PRODUCER_STAGE = on
+            rides = cmod.STAGE_RIDES
+            torch.manual_seed(0)
+            tr = Trainer(ewdml.parse_args(flags))
+            for _ in range(8):
+                tr.train_step()
+            torch.cuda.synchronize()
+            ex = tr.exchange
+            assert (cmod.STAGE_RIDES > rides) == on
+            res.append((tr.flat.data.clone(), ex.resid.clone(), ex.vel.clone()))
+            if on:
+                assert all(int(s.abs().sum()) == 0 for s in ex.stamps)  # re-armed by the encode
+            tr.close()
+    finally:
+        cmod._PRODUCER_STAGE = saved
+    for name, a, b in zip(("params", "resid", "vel"), *res):
+        assert torch.equal(a, b), name
