@@ -67,10 +67,12 @@ def _residual_block(x, main, bn_last, sc):
 def _lazy_into(conv, h) -> bool:
     """Whether BN-ReLU output (of input ``h``) may stay unwritten because ``conv`` -- its only
     consumer -- runs the fp32 Winograd path, whose input transform applies the BN layer on the
-    fly (as models/fused.py does for VGG; EWDML_LAZY_BN=0: always materialise)."""
+    fly (as models/fused.py does for VGG), or is a 1x1 conv whose GEMM forms it in its operand
+    staging (forward and weight gradient; EWDML_LAZY_BN=0: always materialise)."""
     if not fused._LAZY:
         return False
-    if not (conv.stride in (1, (1, 1)) and conv.padding in (1, (1, 1))
+    pad = 0 if tuple(conv.kernel_size) == (1, 1) else 1
+    if not (conv.stride in (1, (1, 1)) and conv.padding in (pad, (pad, pad))
             and conv.dilation in (1, (1, 1)) and conv.groups == 1):
         return False
     from ..ops import conv as conv_hip
@@ -151,7 +153,8 @@ class Bottleneck(nn.Module):
         first = sink is not None and module_supported(self.conv1, x)
         h = conv2d_module(self.conv1, x, sink if first else None)
         out = bn_act(h, self.bn1, "relu", lazy=_lazy_into(self.conv2, h))
-        out = bn_act(_conv(self.conv2, out), self.bn2, "relu")
+        h2 = _conv(self.conv2, out)
+        out = bn_act(h2, self.bn2, "relu", lazy=_lazy_into(self.conv3, h2))
         return _conv(self.conv3, out), first
 
     def forward(self, x):

@@ -107,6 +107,11 @@ _SMALLMAP = os.environ.get("EWDML_SMALLMAP", "1") != "0"
 # it), more than the two apply launches it saves; 3 interleaved rounds 1.197 / 1.193 / 1.201 vs
 # 1.217 / 1.212 / 1.214 ms per step (profiles/ab/README.md)
 _SM_LAZY_BWD = os.environ.get("EWDML_SM_LAZY_BWD", "0") == "1"
+# fp32 1x1 convs of a lazily applied BN + ReLU input (ResNet bottleneck conv3 of relu(bn2(h))):
+# the GEMM's operand staging forms the input from h in the forward and the weight gradient
+# (conv_f32.hip CfLz), so the BN apply never writes it.  EWDML_LAZY_1X1=0: materialised
+_LAZY_1X1 = os.environ.get("EWDML_LAZY_1X1", "1") != "0"
+LAZY_1X1_USES = 0  # forward passes that took it (tests / diagnostics)
 # the same for the Winograd convs (their backward input transforms form the KIND 2 dy)
 _WINO_LAZY_BWD = os.environ.get("EWDML_WINO_LAZY_BWD", "1") != "0"
 # the backward finalisation of the BN layer whose input gradient a conv's backward-data launch
@@ -386,9 +391,23 @@ def smallmap_for(shape, dtype, w) -> bool:
             and Nc % 64 == 0 and N * 4 * max(C, Nc) < 2 ** 31)
 
 
+def lazy_1x1_ok(shape, dtype, w) -> bool:
+    """Whether the fp32 1x1 conv of an input of ``shape`` forms a lazily applied (unpooled)
+    BatchNorm + ReLU input in its GEMM operand staging (forward and weight gradient)."""
+    if not _LAZY_1X1 or dtype != torch.float32 or w.dtype != dtype or tuple(w.shape[-2:]) != (1, 1):
+        return False
+    N, C, H, W = shape
+    Nc = w.shape[0]
+    return (w.shape[1] == C and C % 64 == 0 and Nc % 64 == 0 and (N * H * W) % 64 == 0
+            and N * H * W * max(C, Nc) < 2 ** 31)
+
+
 def lazy_input_ok(shape, dtype, w) -> bool:
     """Whether the conv of an input of ``shape`` forms a lazily applied BatchNorm(+ReLU) input on
-    the fly (Winograd input transform or the 2x2-map GEMM's operand load)."""
+    the fly (Winograd input transform, the 2x2-map GEMM's operand load, or a 1x1 GEMM's operand
+    staging)."""
+    if tuple(w.shape[-2:]) == (1, 1):
+        return lazy_1x1_ok(shape, dtype, w)
     return wino_tile_for(shape, dtype, w) > 0 or smallmap_for(shape, dtype, w)
 
 
@@ -568,13 +587,16 @@ class _Conv(torch.autograd.Function):
         part = torch.empty(_part_floats(N * H * W, Nc), dtype=torch.float32, device=x.device)
         ctx.wino = None
         ctx.sm = None
+        ctx.lz = None
         sm = sink is None and smallmap_for(tuple(x.shape), x.dtype, w)
         m = 0 if sm else wino_tile(x, w)
         # x may be the lazily applied output of a fused BN layer (ops/nn.py bn_relu(lazy=True)):
-        # the Winograd input transform (or the 2x2-map GEMM's operand load, unpooled) applies
-        # that layer on the fly; anything else needs it
+        # the Winograd input transform (or the 2x2-map GEMM's operand load, unpooled, or a 1x1
+        # GEMM's operand staging, unpooled) applies that layer on the fly; anything else needs it
         lazy = getattr(x, "_ew_lazy_fwd", None)
-        if lazy is not None and (not (m or sm) or (sm and lazy[4])):
+        lz1 = (lazy is not None and not (m or sm) and k == 1 and not lazy[4]
+               and lazy_1x1_ok(tuple(x.shape), x.dtype, w))
+        if lazy is not None and ((not (m or sm) and not lz1) or (sm and lazy[4])):
             from .nn import materialize
 
             materialize(x)
@@ -610,6 +632,17 @@ class _Conv(torch.autograd.Function):
                 rows = C_.wino_f32_fwd(_ptr(x), _ptr(w), _ptr(U), _ptr(y), _ptr(V), _ptr(Mo), N,
                                        H, W, C, Nc, m, _ptr(part), part.numel(), _stream())
             ctx.wino = (U if m == 2 else None, V, m)
+        elif lz1:
+            bh, bstats, _bcode, bnbt, _bpool = lazy
+            rows = C_.conv_f32_fwd_lz(_ptr(bh), _ptr(bstats), _ptr(bnbt), _ptr(w), _ptr(y),
+                                      _ptr(ws), ws.numel(), N, H, W, C, Nc, _ptr(part),
+                                      part.numel(), _stream())
+            # a later materialisation must not count the batch twice
+            x._ew_materialize = getattr(x, "_ew_materialize_no_nbt", None)
+            # x itself stays unwritten: the weight gradient forms it from the same source
+            ctx.lz = (bh, bstats)
+            global LAZY_1X1_USES
+            LAZY_1X1_USES += 1
         else:
             fwd = C_.conv_f32_fwd if x.dtype == torch.float32 else C_.conv_fwd
             rows = fwd(_ptr(x), _ptr(w), _ptr(y), _ptr(ws), ws.numel(), N, H, W, C, Nc, k,
@@ -730,6 +763,8 @@ class _Conv(torch.autograd.Function):
                 global WO_RIDES
                 WO_RIDES += 1
             del wo_job  # enqueued: the stream orders any reuse of its buffers after it
+        # (formed from the BN source even if x was materialised since: the same values)
+        lz, ctx.lz = ctx.lz, None
         if ctx.needs_input_grad[1]:
             dw = torch.empty_like(w, memory_format=torch.channels_last)
             side = _wgrad_side(x.device) if _dw_may_lag(ctx) else None
@@ -771,8 +806,12 @@ class _Conv(torch.autograd.Function):
                         if not _STEM_RED[0]:  # run at the latest when the backward pass ends
                             torch.autograd.Variable._execution_engine.queue_callback(_flush_final)
                         _STEM_RED[0] = True
-                    wgrad(_ptr(dy), _ptr(x), _ptr(dw), _ptr(wsw), wsw.numel(), N, H, W, C, Nc, k,
-                          _stream())
+                    if lz is not None:  # x = relu(bn(h)) formed in the GEMM's operand staging
+                        C_.conv_f32_wgrad_lz(_ptr(dy), _ptr(lz[0]), _ptr(lz[1]), _ptr(dw),
+                                             _ptr(wsw), wsw.numel(), N, H, W, C, Nc, _stream())
+                    else:
+                        wgrad(_ptr(dy), _ptr(x), _ptr(dw), _ptr(wsw), wsw.numel(), N, H, W, C,
+                              Nc, k, _stream())
 
             if side is None:
                 launch_wgrad()
@@ -782,7 +821,7 @@ class _Conv(torch.autograd.Function):
                 # queued (holding its tensors, so their memory is not reused), issued on the side
                 # stream with the next _WGRAD_BATCH - 1 ones or at the first gradient read
                 _SIDE_QUEUE.append((x.device.index, launch_wgrad,
-                                    (dy, x, dw, V, D)))
+                                    (dy, x, dw, V, D, lz)))
                 if len(_SIDE_QUEUE) >= _WGRAD_BATCH:
                     _issue_side()
         ctx.wino = None

@@ -368,6 +368,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_f32_fwd", &ew_conv_f32_fwd);
   m.def("conv_f32_bwd_data", &ew_conv_f32_bwd_data);
   m.def("conv_f32_wgrad", &ew_conv_f32_wgrad);
+  m.def("conv_f32_fwd_lz", &ew_conv_f32_fwd_lz);
+  m.def("conv_f32_wgrad_lz", &ew_conv_f32_wgrad_lz);
   m.def("conv_f32_fwd_s2", &ew_conv_f32_fwd_s2);
   m.def("conv_f32_bwd_data_s2", &ew_conv_f32_bwd_data_s2);
   m.def("conv_f32_wgrad_s2", &ew_conv_f32_wgrad_s2);

@@ -199,10 +199,33 @@ __device__ __forceinline__ void cf_mma(const CfFrag<SH, MI, NJ>& f,
   if (CF_PRIO) __builtin_amdgcn_s_setprio(0);
 }
 
-// Staging registers of one operand: R 16-B vectors per thread (named members: no scratch)
+// Staging registers of one operand: R 16-B vectors per thread (named members: no scratch); sc /
+// sh: the k-step's BatchNorm scale / shift of a lazily applied forward A operand (CfLz)
 struct CfRegs {
   f32x4 v0, v1, v2, v3;
+  f32x4 sc, sh;
 };
+
+// A lazily applied BatchNorm + ReLU operand (k_cf_gemm<..., LZ = true>; 1x1 stride-1 convs only:
+// no padding taps, whose zeros the transform would not keep).  The conv's input relu(bn(h)) --
+// ResNet bottleneck conv3's, models/resnet.py -- is never written: the forward's A rows and the
+// weight gradient's x rows are read from h, and relu(h * scale + shift) is formed in the staging
+// registers on their way to LDS, exactly as k_bn_fwd_apply writes it (bitwise the materialised
+// operand).  stats [4][C]: mean, invstd, scale, shift; nbt: the BN layer's num_batches_tracked
+// (the forward counts the batch, once) or null.
+struct CfLz {
+  const float* stats;
+  long long* nbt;
+};
+__device__ __forceinline__ f32x4 cf_bn_relu4(const f32x4& v, const f32x4& sc, const f32x4& sh) {
+  f32x4 r;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float z = v[q] * sc[q] + sh[q];  // as k_bn_fwd_apply writes it
+    r[q] = (z > 0.0f || z != z) ? z : 0.0f;
+  }
+  return r;
+}
 #define CF_FOR(R_, ...)                                                                         \
   do {                                                                                          \
     { constexpr int i = 0; auto& v = RG.v0; __VA_ARGS__; }                                     \
@@ -227,7 +250,7 @@ __device__ __forceinline__ f32x4 cf_bload(__amdgpu_buffer_rsrc_t r, unsigned vof
   return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, soff, 0));
 }
 
-template <int MODE, int BM, int BN, int NT, int STR = 1>
+template <int MODE, int BM, int BN, int NT, int STR = 1, bool LZ = false>
 struct CfStager {
   using L = CfLayout<MODE, BM, BN>;
   static constexpr int RA = 8 * BM / NT, RB = 8 * BN / NT;    // 16-B vectors per thread
@@ -248,6 +271,20 @@ struct CfStager {
   // (fwd / bwd A: an add, the padding test and a select per load; B and wgrad A: soffset only).
   __amdgpu_buffer_rsrc_t rsa, rsb;
   unsigned aoff[RA], boff[RB];
+  // LZ: the forward's scale / shift rows (read per k-step into CfRegs); the weight gradient's
+  // fixed 4 columns' scale / shift
+  const float* lzs;
+  f32x4 wsc, wsh;
+
+  __device__ __forceinline__ void lz_init(const CfGeom& g, const CfLz& lz) {
+    static_assert(STR == 1 && (MODE == CF_FWD || MODE == CF_WGRAD), "lazy BN operand");
+    if constexpr (MODE == CF_FWD) {
+      lzs = lz.stats;
+    } else {
+      wsc = *reinterpret_cast<const f32x4*>(lz.stats + 2 * g.C + bc);
+      wsh = *reinterpret_cast<const f32x4*>(lz.stats + 3 * g.C + bc);
+    }
+  }
 
   __device__ __forceinline__ void init(const CfGeom& g, const float* a_src, const float* b_src,
                                        int t_, int m0_, int n0_, int zb = 0) {
@@ -355,6 +392,12 @@ struct CfStager {
           v = cf_bload(rsa, ok ? aoff[i] + sa : CF_OOB, 0);
         });
       }
+      if constexpr (LZ && MODE == CF_FWD) {
+        // this step's channels cb*32 + chunk*4 .. + 3 (1x1: tap 0)
+        const int c = cb * CF_BK + (t & 7) * 4;
+        ra.sc = *reinterpret_cast<const f32x4*>(lzs + 2 * g.C + c);
+        ra.sh = *reinterpret_cast<const f32x4*>(lzs + 3 * g.C + c);
+      }
       if constexpr (MODE == CF_FWD) {
         // B: w[n][taps*C], k index s*32 + chunk*4
         CfRegs& RG = rb;
@@ -411,7 +454,14 @@ struct CfStager {
     {
       const CfRegs& RG = ra;
       if constexpr (L::A_KC) {
-        CF_FOR(RA, { *reinterpret_cast<f32x4*>(As + cf_off((t >> 3) + (NT / 8) * i, t & 7)) = v; });
+        if constexpr (LZ && MODE == CF_FWD) {
+          CF_FOR(RA, {
+            *reinterpret_cast<f32x4*>(As + cf_off((t >> 3) + (NT / 8) * i, t & 7)) =
+                cf_bn_relu4(v, RG.sc, RG.sh);
+          });
+        } else {
+          CF_FOR(RA, { *reinterpret_cast<f32x4*>(As + cf_off((t >> 3) + (NT / 8) * i, t & 7)) = v; });
+        }
       } else {
         CF_FOR(RA, {
           *reinterpret_cast<f32x4*>(As + ((t / RCA + RPA * i) * L::PA + (t % RCA) * 4) * 4) = v;
@@ -422,6 +472,11 @@ struct CfStager {
       const CfRegs& RG = rb;
       if constexpr (L::B_KC) {
         CF_FOR(RB, { *reinterpret_cast<f32x4*>(Bs + cf_off((t >> 3) + (NT / 8) * i, t & 7)) = v; });
+      } else if constexpr (LZ && MODE == CF_WGRAD) {
+        CF_FOR(RB, {
+          *reinterpret_cast<f32x4*>(Bs + ((t / RCB + RPB * i) * L::PB + (t % RCB) * 4) * 4) =
+              cf_bn_relu4(v, wsc, wsh);
+        });
       } else {
         CF_FOR(RB, {
           *reinterpret_cast<f32x4*>(Bs + ((t / RCB + RPB * i) * L::PB + (t % RCB) * 4) * 4) = v;
@@ -646,14 +701,16 @@ __device__ __forceinline__ void cf_epilogue(typename CfMfma<SH>::acc_t (&acc)[MI
 // loaded while s computes and s+1 is written), split z covers k-steps
 // [z*kps, min((z+1)*kps, ksteps)).
 // WPE: waves per SIMD the register allocation must allow (0: the compiler's choice)
-template <int MODE, int BM, int BN, int WM, int WN, int SH, int STR = 1, int WPE = 0>
+// LZ: a lazily applied BatchNorm + ReLU operand (CfLz): forward A / weight-gradient B
+template <int MODE, int BM, int BN, int WM, int WN, int SH, int STR = 1, int WPE = 0,
+          bool LZ = false>
 __global__ __launch_bounds__(64 * WM * WN, WPE) void k_cf_gemm(const float* __restrict__ a_src,
                                                    const float* __restrict__ b_src,
                                                    float* __restrict__ out,
                                                    float* __restrict__ slab, CfGeom geo,
                                                    float* __restrict__ bnpart, CfBnBwd bb,
                                                    const float* __restrict__ addend, EwBnFin fin,
-                                                   WgOut wo, int* __restrict__ red) {
+                                                   WgOut wo, int* __restrict__ red, CfLz lz) {
   using L = CfLayout<MODE, BM, BN>;
   using acc_t = typename CfMfma<SH>::acc_t;
   constexpr int NT = 64 * WM * WN;
@@ -711,8 +768,13 @@ __global__ __launch_bounds__(64 * WM * WN, WPE) void k_cf_gemm(const float* __re
   const int ksteps =
       S2B ? cf_s2_ntaps(geo.taps, phase >> 1, phase & 1) * (geo.Nc / CF_BK) : geo.ksteps;
   const int kend = min(kbeg + geo.kps, ksteps);
-  CfStager<MODE, BM, BN, NT, STR> st;
+  CfStager<MODE, BM, BN, NT, STR, LZ> st;
   st.init(geo, a_src, b_src, t, m0, n0, phase);
+  if constexpr (LZ) {
+    st.lz_init(geo, lz);
+    if constexpr (MODE == CF_FWD)
+      if (lz.nbt && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && t == 0) *lz.nbt += 1;
+  }
 
   acc_t acc[MI][NJ];
 #pragma unroll
@@ -1440,18 +1502,40 @@ bool Nc_bn_ok(const CfGeom& geo, long long bnpart_floats) {
 }
 
 #define CF_LAUNCH_W(MODE_, BM_, BN_, WM_, WN_, SH_, WPE_)                                   \
-  hipLaunchKernelGGL((k_cf_gemm<MODE_, BM_, BN_, WM_, WN_, SH_, STR, WPE_>), grid,                \
+  hipLaunchKernelGGL((k_cf_gemm<MODE_, BM_, BN_, WM_, WN_, SH_, STR, WPE_, LZ>), grid,            \
                      dim3(64 * WM_ * WN_), 0, s, a, b, out, slab, geo, bnp, bbv, addend, fin, wo, \
-                     red)
+                     red, lz)
 #define CF_LAUNCH(MODE_, BM_, BN_, WM_, WN_, SH_) CF_LAUNCH_W(MODE_, BM_, BN_, WM_, WN_, SH_, 0)
 #define CF_LAUNCH_GL(BM_, BN_, WM_, WN_, SH_, WPE_)                                           \
   hipLaunchKernelGGL((k_cf_gemm_gl<BM_, BN_, WM_, WN_, SH_, WPE_>), grid, dim3(64 * WM_ * WN_), 0, \
                      s, a, b, out, slab, geo, bnp, bbv, addend)
 
+// the register-staged GEMM variant of a plan (LZ: with the lazy BatchNorm operand)
+template <int MODE, int STR, bool LZ>
+void cf_launch_staged(const CfPlan& p, bool w4, bool occ2, dim3 grid, hipStream_t s,
+                      const float* a, const float* b, float* out, float* slab, const CfGeom& geo,
+                      float* bnp, const CfBnBwd& bbv, const float* addend, const EwBnFin& fin,
+                      const WgOut& wo, int* red, const CfLz& lz) {
+  if (p.bm == 128 && p.bn == 128) {
+    if (w4) CF_LAUNCH(MODE, 128, 128, 2, 2, 32);
+    else CF_LAUNCH(MODE, 128, 128, 2, 4, 32);
+  } else if (p.bm == 128) {
+    if (occ2) CF_LAUNCH_W(MODE, 128, 64, 4, 2, 32, 4);
+    else CF_LAUNCH(MODE, 128, 64, 4, 2, 32);
+  } else if (p.bn == 128) {
+    if (occ2) CF_LAUNCH_W(MODE, 64, 128, 2, 4, 32, 4);
+    else CF_LAUNCH(MODE, 64, 128, 2, 4, 32);
+  } else {
+    CF_LAUNCH(MODE, 64, 64, 4, 2, 16);
+  }
+}
+
+// lz (forward / weight gradient, stride 1): the lazily applied BatchNorm operand (CfLz)
 template <int MODE, int STR = 1>
 int cf_gemm(const float* a, const float* b, float* out, float* ws, long long ws_floats,
             CfGeom geo, hipStream_t s, float* bnpart, long long bnpart_floats,
-            const CfBnBwd* bnb, const float* addend, int* split_out = nullptr) {
+            const CfBnBwd* bnb, const float* addend, int* split_out = nullptr,
+            CfLz lz = CfLz{nullptr, nullptr}) {
   cf_flush_pred();  // this launch may write slabs over a pending reduction's
   const int defer_red = g_cf_defer_red;  // armed for this launch only
   g_cf_defer_red = 0;
@@ -1536,8 +1620,15 @@ int cf_gemm(const float* a, const float* b, float* out, float* ws, long long ws_
   // 54 us at two, profiles/ab/README.md)
   const bool occ2 = occ_env == 2 || (occ_env == 1 && (long long)grid.x * grid.y * grid.z > 256);
   bool launched = false;
+  if constexpr ((MODE == CF_FWD || MODE == CF_WGRAD) && STR == 1) {
+    if (lz.stats) {
+      cf_launch_staged<MODE, STR, true>(p, w4, occ2, grid, s, a, b, out, slab, geo, bnp, bbv,
+                                        addend, fin, wo, red, lz);
+      launched = true;
+    }
+  }
   if constexpr (MODE == CF_FWD && STR == 1) {
-    if (cf_glds_on() && !w4) {
+    if (!launched && cf_glds_on() && !w4) {
       if (p.bm == 128 && p.bn == 128)
         CF_LAUNCH_GL(128, 128, 2, 4, 32, 0);
       else if (p.bm == 128)  // held to 128 VGPRs: two blocks per CU (72 KB of LDS each)
@@ -1549,19 +1640,9 @@ int cf_gemm(const float* a, const float* b, float* out, float* ws, long long ws_
       launched = true;
     }
   }
-  if (launched) {
-  } else if (p.bm == 128 && p.bn == 128) {
-    if (w4) CF_LAUNCH(MODE, 128, 128, 2, 2, 32);
-    else CF_LAUNCH(MODE, 128, 128, 2, 4, 32);
-  } else if (p.bm == 128) {
-    if (occ2) CF_LAUNCH_W(MODE, 128, 64, 4, 2, 32, 4);
-    else CF_LAUNCH(MODE, 128, 64, 4, 2, 32);
-  } else if (p.bn == 128) {
-    if (occ2) CF_LAUNCH_W(MODE, 64, 128, 2, 4, 32, 4);
-    else CF_LAUNCH(MODE, 64, 128, 2, 4, 32);
-  } else {
-    CF_LAUNCH(MODE, 64, 64, 4, 2, 16);
-  }
+  if (!launched)
+    cf_launch_staged<MODE, STR, false>(p, w4, occ2, grid, s, a, b, out, slab, geo, bnp, bbv,
+                                       addend, fin, wo, red, lz);
   EW_CHECK_LAUNCH();
   if (split_out) {  // the caller reduces the slabs (ws[split][batch][M][Ncol]) itself
     *split_out = p.split;
@@ -1752,6 +1833,38 @@ void ew_conv_f32_wgrad(uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws, lo
   cf_gemm<CF_WGRAD>(reinterpret_cast<const float*>(dy), reinterpret_cast<const float*>(x),
                     reinterpret_cast<float*>(dw), reinterpret_cast<float*>(ws), ws_floats, g,
                     (hipStream_t)stream, nullptr, 0, nullptr, nullptr);
+}
+
+// 1x1 convolutions of a lazily applied BatchNorm + ReLU input (CfLz): x = relu(h * scale + shift)
+// is formed in the GEMM's operand staging from h [N][H][W][C] and the BN layer's stats [4][C];
+// the forward counts the layer's batch in nbt (0: none)
+int ew_conv_f32_fwd_lz(uintptr_t h, uintptr_t stats, uintptr_t nbt, uintptr_t w, uintptr_t y,
+                       uintptr_t ws, long long ws_floats, long long N, int H, int W, int C, int Nc,
+                       uintptr_t bnpart, long long bnpart_floats, uintptr_t stream) {
+  const long long P = N * H * W;
+  if (!h || !stats || (stats & 15) || C % 64 || Nc % 64 || P % 64 ||
+      P * (long long)std::max(C, Nc) >= (1LL << 31))
+    throw std::runtime_error("ewdml conv f32 lazy-BN 1x1: needs C, Nc, N*H*W % 64 == 0");
+  CfGeom g{(int)P, Nc, (int)P, H, W, C, Nc, 1, C / CF_BK, 0, 1, 0, 0, 0};
+  return cf_gemm<CF_FWD>(reinterpret_cast<const float*>(h), reinterpret_cast<const float*>(w),
+                         reinterpret_cast<float*>(y), reinterpret_cast<float*>(ws), ws_floats, g,
+                         (hipStream_t)stream, reinterpret_cast<float*>(bnpart), bnpart_floats,
+                         nullptr, nullptr, nullptr,
+                         CfLz{reinterpret_cast<const float*>(stats), reinterpret_cast<long long*>(nbt)});
+}
+
+void ew_conv_f32_wgrad_lz(uintptr_t dy, uintptr_t h, uintptr_t stats, uintptr_t dw, uintptr_t ws,
+                          long long ws_floats, long long N, int H, int W, int C, int Nc,
+                          uintptr_t stream) {
+  const long long P = N * H * W;
+  if (!h || !stats || (stats & 15) || C % 64 || Nc % 64 || P % CF_BK ||
+      P * (long long)std::max(C, Nc) >= (1LL << 31))
+    throw std::runtime_error("ewdml conv f32 lazy-BN 1x1 wgrad: needs C, Nc % 64 == 0");
+  CfGeom g{Nc, C, (int)P, H, W, C, Nc, 1, (int)(P / CF_BK), 0, 1, 0, 0, 0};
+  cf_gemm<CF_WGRAD>(reinterpret_cast<const float*>(dy), reinterpret_cast<const float*>(h),
+                    reinterpret_cast<float*>(dw), reinterpret_cast<float*>(ws), ws_floats, g,
+                    (hipStream_t)stream, nullptr, 0, nullptr, nullptr, nullptr,
+                    CfLz{reinterpret_cast<const float*>(stats), nullptr});
 }
 
 // ---- stride-2 3x3 / pad 1 and 1x1 / pad 0 convolutions (the ResNet down-sampling convs):

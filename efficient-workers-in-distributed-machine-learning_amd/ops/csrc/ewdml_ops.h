@@ -273,6 +273,12 @@ int ew_conv_f32_bwd_data(uintptr_t dy, uintptr_t w, uintptr_t dx, uintptr_t ws,
                          uintptr_t stream);
 void ew_conv_f32_wgrad(uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws, long long ws_floats,
                        long long N, int H, int W, int C, int Nc, int ksize, uintptr_t stream);
+int ew_conv_f32_fwd_lz(uintptr_t h, uintptr_t stats, uintptr_t nbt, uintptr_t w, uintptr_t y,
+                       uintptr_t ws, long long ws_floats, long long N, int H, int W, int C, int Nc,
+                       uintptr_t bnpart, long long bnpart_floats, uintptr_t stream);
+void ew_conv_f32_wgrad_lz(uintptr_t dy, uintptr_t h, uintptr_t stats, uintptr_t dw, uintptr_t ws,
+                          long long ws_floats, long long N, int H, int W, int C, int Nc,
+                          uintptr_t stream);
 // stride-2 3x3 / pad 1 and 1x1 / pad 0 (H, W = the input map, even; y / dy are H/2 x W/2)
 int ew_conv_f32_fwd_s2(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t ws, long long ws_floats,
                        long long N, int H, int W, int C, int Nc, int ksize, uintptr_t bnpart,

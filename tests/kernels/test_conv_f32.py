@@ -1238,3 +1238,77 @@ def test_conv_f32_smallmap_bn_backward_sums(mode, pool):
     conv.set_bn_bwd_fusion(True)
     for i, (a, b) in enumerate(zip(*grads)):
         assert _rel(a, b) < 1e-5, (i, _rel(a, b))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,C,Nc,HW", [(64, 64, 256, 8), (32, 128, 512, 4), (16, 512, 2048, 4)])
+def test_conv_f32_1x1_lazy_bn_matches_materialised(N, C, Nc, HW):
+    """ResNet bottleneck tail: 1x1 conv -> BN-ReLU -> 1x1 conv -> BN.  With the middle BN layer
+    applied in the second conv's GEMM operand staging (forward A rows and weight-gradient x rows
+    formed from h, conv_f32.hip CfLz; ops/nn.py lazy BN) every output, gradient, running
+    statistic and batch counter equals the materialised path bit for bit, and the lazy conv's
+    output matches float64."""
+    from ewdml.ops import nn as fnn
+
+    conv = _conv()
+    x0, w0 = _data(N, C, C, HW, HW, seed=71, k=1)
+    _, w1 = _data(N, C, Nc, HW, HW, seed=72, k=1)
+    bns = [torch.nn.BatchNorm2d(C).cuda(), torch.nn.BatchNorm2d(Nc).cuda()]
+    with torch.no_grad():
+        for bn in bns:
+            bn.weight.uniform_(0.5, 1.5)
+            bn.bias.uniform_(-0.3, 0.3)
+    g = torch.randn(N, Nc, HW, HW, device="cuda").contiguous(memory_format=torch.channels_last)
+    runs = []
+    uses = conv.LAZY_1X1_USES
+    for lazy in (True, False):
+        b0, b1 = copy.deepcopy(bns[0]), copy.deepcopy(bns[1])
+        xa, wa, wb = (t.clone().requires_grad_(True) for t in (x0, w0, w1))
+        h = conv.conv(xa, wa)
+        y = fnn.bn_act(h, b0, "relu", lazy=lazy)
+        assert conv.lazy_input_ok(tuple(y.shape), y.dtype, wb)
+        z = conv.conv(y, wb)
+        if lazy:
+            assert conv.LAZY_1X1_USES == uses + 1
+            # materialised only now, after the conv consumed it lazily (no second batch count)
+            zref = _ref64(fnn.materialize(y).detach(), w1, 1)
+            assert _rel(z, zref) < TOL, _rel(z, zref)
+        out = fnn.bn_act(z, b1, "none")
+        out.backward(g)
+        runs.append([out, xa.grad, wa.grad, wb.grad] +
+                    [t for b in (b0, b1) for t in (b.weight.grad, b.bias.grad, b.running_mean,
+                                                  b.running_var, b.num_batches_tracked)])
+    for i, (a, b) in enumerate(zip(*runs)):
+        assert torch.equal(a, b), i
+
+
+@pytest.mark.gpu
+def test_resnet50_lazy_bn_into_conv3_bitwise():
+    """ResNet-50 (CIFAR stem, our stride-2 kernels: deterministic): every bottleneck's conv3 reads
+    relu(bn2(h)) through its GEMM operand staging instead of a written activation; one training
+    step's output, parameter gradients and BN buffers equal the materialised step bit for bit."""
+    from ewdml.models import build_model
+    from ewdml.ops import conv as cmod
+
+    _conv(wino=True, min_c=128, tile="size")
+    cmod.set_stride2(True)
+    torch.manual_seed(0)
+    m0 = build_model("resnet50", 10).cuda().to(memory_format=torch.channels_last)
+    x = torch.randn(8, 3, 32, 32, device="cuda").contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (8,), device="cuda")
+    saved = cmod._LAZY_1X1
+    res = []
+    try:
+        for on in (True, False):
+            cmod._LAZY_1X1 = on
+            m = copy.deepcopy(m0)
+            uses = cmod.LAZY_1X1_USES
+            out = m(x)
+            F.cross_entropy(out, y).backward()
+            assert cmod.LAZY_1X1_USES - uses == (16 if on else 0)
+            res.append([out.detach()] + [p.grad.detach().clone() for p in m.parameters()]
+                       + [b.clone() for b in m.buffers()])
+    finally:
+        cmod._LAZY_1X1 = saved
+    for i, (a, b) in enumerate(zip(*res)):
+        assert torch.equal(a, b), i
