@@ -821,7 +821,7 @@ class _Conv(torch.autograd.Function):
                 # queued (holding its tensors, so their memory is not reused), issued on the side
                 # stream with the next _WGRAD_BATCH - 1 ones or at the first gradient read
                 _SIDE_QUEUE.append((x.device.index, launch_wgrad,
-                                    (dy, x, dw, V, D, lz)))
+                                    (dy, x, dw, V, D) + (lz or ())))
                 if len(_SIDE_QUEUE) >= _WGRAD_BATCH:
                     _issue_side()
         ctx.wino = None

@@ -1117,6 +1117,9 @@ __device__ __forceinline__ void pk_select(const uint32_t* __restrict__ hist,
                            __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(state + t * 4 + 1, k_rem - run, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
+        // the digit-0 bin's key count: few keys are ranked directly (k_pk_select pass 1)
+        if (FIRST)
+          __hip_atomic_store(state + t * 4 + 3, cnt[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
       run += cnt[j];
@@ -1536,6 +1539,9 @@ __global__ __launch_bounds__(EW_BLOCK) void k_pk_pass2(
 // ---------------------------------------------------------------------------------------------
 constexpr uint32_t PK_MAX_POLLS = 1u << 22;  // ~2 s of polls: only a broken launch gets there
 constexpr uint32_t PK_LOCAL_MAX = 4 * EW_CHUNK;  // pass-1 keys one block takes pass 2 over
+constexpr uint32_t PK_RANK_MAX = EW_BLOCK;  // digit-0 keys the pass-1 last block ranks directly
+// ... as set for this process (EWDML_PK_RANK=0: never, the digit-1 / digit-2 histograms; A/B)
+__device__ uint32_t g_pk_rank_max = PK_RANK_MAX;
 
 // Everything handed across the barrier is written with device-coherent operations (histogram
 // atomics, agent-scope stores of the select state and the pass-1 keys) and every wave drains its
@@ -1652,6 +1658,10 @@ __global__ __launch_bounds__(EW_BLOCK) void k_pk_select(
     pk_wait(gn, g0 + 1u, err, &s_gen);
   }
   // ---- pass 1: next s0 - s1 bits of the keys in the selected digit 0; those keys -> cand ----
+  // (fast path with at most PK_RANK_MAX keys in that digit: no digit-1 histogram -- the last
+  // block ranks the compacted keys directly)
+  const bool ranked = fast && __hip_atomic_load(state + t * 4 + 3, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT) <= g_pk_rank_max;
   {
     const uint32_t want = __hip_atomic_load(state + t * 4, __ATOMIC_RELAXED,
                                             __HIP_MEMORY_SCOPE_AGENT) >> s0;
@@ -1659,15 +1669,17 @@ __global__ __launch_bounds__(EW_BLOCK) void k_pk_select(
     int* cn = cand_n + TICK_STRIDE * t;
     uint32_t* cdst = cand + tr.off;
     uint32_t* h = hs;
-    for (int i = threadIdx.x; i < NB1; i += EW_BLOCK) h[i] = 0;
-    __syncthreads();
+    if (!ranked) {
+      for (int i = threadIdx.x; i < NB1; i += EW_BLOCK) h[i] = 0;
+      __syncthreads();
+    }
     if (fast) {
       uint32_t nm = 0, mbits = 0;
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         const uint32_t rel = kv[r] - B;
         if (i0 + r * EW_BLOCK < i1 && (rel >> s0) == want) {
-          atomicAdd(&h[(rel >> s1) & dmask], 1u);
+          if (!ranked) atomicAdd(&h[(rel >> s1) & dmask], 1u);
           ++nm;
           mbits |= 1u << r;
         }
@@ -1691,12 +1703,48 @@ __global__ __launch_bounds__(EW_BLOCK) void k_pk_select(
         pk_append(m, k, cn, cdst);
       });
     }
-    __syncthreads();
-    uint32_t* dst = hist1 + (size_t)t * NB1;
-    for (int i = threadIdx.x; i < NB1; i += EW_BLOCK)
-      if (h[i]) atomicAdd(&dst[i], h[i]);
+    if (!ranked) {
+      __syncthreads();
+      uint32_t* dst = hist1 + (size_t)t * NB1;
+      for (int i = threadIdx.x; i < NB1; i += EW_BLOCK)
+        if (h[i]) atomicAdd(&dst[i], h[i]);
+    }
   }
   if (pk_arrive(arr, tr.ncb, &s_flag)) {
+    if (ranked) {
+      // the n compacted keys (absolute), one per thread: the k_rem-th largest is the threshold,
+      // k_rem minus the keys above it the ties to keep (what digits 1 and 2 give)
+      const uint32_t n = (uint32_t)__hip_atomic_load(cand_n + TICK_STRIDE * t, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t k_rem = __hip_atomic_load(state + t * 4 + 1, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t* src = cand + tr.off;
+      // n is the digit-0 bin's count (<= PK_RANK_MAX): the same keys, the same predicate
+      if (threadIdx.x == 0 && n > (uint32_t)EW_BLOCK) atomicAdd(err, 1);
+      if (threadIdx.x < n)
+        hs[threadIdx.x] = __hip_atomic_load(src + threadIdx.x, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      if (threadIdx.x < n) {
+        const uint32_t mine = hs[threadIdx.x];
+        uint32_t gt = 0, eq = 0;
+        for (uint32_t j = 0; j < n; ++j) {
+          const uint32_t x = hs[j];
+          gt += x > mine;
+          eq += x == mine;
+        }
+        if (gt < k_rem && k_rem <= gt + eq) {  // (equal keys: the same two words)
+          __hip_atomic_store(state + t * 4, mine - B, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(state + t * 4 + 1, k_rem - gt, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the state stores before pk_predict's loads
+      __syncthreads();
+      if (threadIdx.x == 0) pk_predict(tr, t, B, state, pst, cand_n);
+      pk_publish(arr, gn, g0 + 3u);
+      return;
+    }
     pk_select<NB1, false>(hist1, tensors, state, kmaxr, T, t, s1);
     // few pass-1 keys (the usual case): this block runs pass 2 over them alone, in LDS, and the
     // tensor is done without a third barrier (generation g0 + 3 tells the waiting blocks)
@@ -1794,6 +1842,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_pk_select(
 // words, histogram rows -- is written by agent-scope atomics or sc1 stores after the writer's
 // vmcnt drain and read by agent-scope (sc1) loads after the poll, plus an agent acquire.
 // ---------------------------------------------------------------------------------------------
+constexpr int PK1_NSTAMP = 16;  // probe stamps per block (EWDML_PK1_STAMPS)
 constexpr int PK1_LDS_KEYS = 10240;  // candidate keys the selecting block stages in LDS (40 KB):
                                      // with the histograms ~73 KB, two blocks per CU
 constexpr int PK1_HSUB = 4;  // pass-0 sub-histograms (lanes t % 4): the candidates crowd the low
@@ -1841,22 +1890,13 @@ __device__ __forceinline__ void pk1_select_cands(const uint2* __restrict__ cands
                                                  uint32_t kmax, uint32_t k, uint32_t* keys,
                                                  uint32_t nl, uint32_t* h, uint32_t* st,
                                                  uint32_t* ws, uint32_t* __restrict__ state,
-                                                 int t) {
+                                                 int t, unsigned long long* stamp = nullptr) {
+  // probe stamps (k_pk_one's row, slots 8..12): pass 0 (keys staged), fold, digit 0, the
+  // selected bin's keys ranked (or passes 1 and 2)
+#define PK1_SSTAMP(i) \
+  if (stamp && threadIdx.x == 0) stamp[i] = wall_clock64()
   constexpr int R = 16;  // loads in flight per thread (each an L2 round trip)
   const uint32_t* src = reinterpret_cast<const uint32_t*>(cands);
-  for (uint32_t b0 = 0; b0 < nl; b0 += EW_BLOCK * R) {
-    uint32_t kv[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const uint32_t i = min(b0 + r * EW_BLOCK + threadIdx.x, nl - 1);
-      kv[r] = __hip_atomic_load(src + 2 * i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const uint32_t i = b0 + r * EW_BLOCK + threadIdx.x;
-      if (i < nl) keys[i] = kv[r] & 0x7fffffffu;
-    }
-  }
   uint32_t* h0 = h + (threadIdx.x & (PK1_HSUB - 1));
   auto add = [&](int p, uint32_t want, uint32_t key) {
     const uint32_t rel = key - B;
@@ -1867,12 +1907,9 @@ __device__ __forceinline__ void pk1_select_cands(const uint2* __restrict__ cands
       atomicAdd(&h[rel & ((1u << s1) - 1u)], 1u);
     }
   };
-  auto pass = [&](int p, uint32_t want) {
-    const int nb = p == 0 ? NB0 * PK1_HSUB : NB1;
-    for (int i = threadIdx.x; i < nb; i += EW_BLOCK) h[i] = 0;
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < nl; i += EW_BLOCK) add(p, want, keys[i]);
-    for (uint32_t b0 = nl; b0 < M; b0 += EW_BLOCK * R) {  // beyond the LDS copy: batched loads
+  // the keys beyond the LDS copy: batched sc1 loads from the list
+  auto beyond = [&](auto&& f) {
+    for (uint32_t b0 = nl; b0 < M; b0 += EW_BLOCK * R) {
       uint32_t kv[R];
 #pragma unroll
       for (int r = 0; r < R; ++r) {
@@ -1881,15 +1918,44 @@ __device__ __forceinline__ void pk1_select_cands(const uint2* __restrict__ cands
       }
 #pragma unroll
       for (int r = 0; r < R; ++r)
-        if (b0 + r * EW_BLOCK + threadIdx.x < M) add(p, want, kv[r] & 0x7fffffffu);
+        if (b0 + r * EW_BLOCK + threadIdx.x < M) f(kv[r] & 0x7fffffffu);
     }
+  };
+  auto pass = [&](int p, uint32_t want) {
+    const int nb = p == 0 ? NB0 * PK1_HSUB : NB1;
+    for (int i = threadIdx.x; i < nb; i += EW_BLOCK) h[i] = 0;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nl; i += EW_BLOCK) add(p, want, keys[i]);
+    beyond([&](uint32_t key) { add(p, want, key); });
     __syncthreads();
   };
   if (threadIdx.x == 0) {
     st[0] = 0u;
     st[1] = k;
   }
-  pass(0, 0u);  // (its barriers order st's initialisation before the digit select)
+  // pass 0 while the keys are staged into LDS: each key counted as it arrives
+  for (int i = threadIdx.x; i < NB0 * PK1_HSUB; i += EW_BLOCK) h[i] = 0;
+  __syncthreads();  // (also orders st's initialisation before the digit select)
+  for (uint32_t b0 = 0; b0 < nl; b0 += EW_BLOCK * R) {
+    uint32_t kv[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const uint32_t i = min(b0 + r * EW_BLOCK + threadIdx.x, nl - 1);
+      kv[r] = __hip_atomic_load(src + 2 * i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const uint32_t i = b0 + r * EW_BLOCK + threadIdx.x;
+      if (i < nl) {
+        const uint32_t key = kv[r] & 0x7fffffffu;
+        keys[i] = key;
+        add(0, 0u, key);
+      }
+    }
+  }
+  beyond([&](uint32_t key) { add(0, 0u, key); });
+  __syncthreads();
+  PK1_SSTAMP(8);
   {  // fold the sub-histograms into bins 0..NB0-1 (all read before any is overwritten)
     constexpr int PER = NB0 / EW_BLOCK;
     uint32_t x[PER];
@@ -1905,11 +1971,56 @@ __device__ __forceinline__ void pk1_select_cands(const uint2* __restrict__ cands
     for (int j = 0; j < PER; ++j) h[threadIdx.x + j * EW_BLOCK] = x[j];
     __syncthreads();
   }
-  pk1_digit<NB0>(h, st, s0, ws);
-  pass(1, st[0] >> s0);
-  pk1_digit<NB1>(h, st, s1, ws);
-  pass(2, st[0] >> s1);
-  pk1_digit<NB2>(h, st, 0u, ws);
+  PK1_SSTAMP(9);
+  pk1_digit<NB0>(h, st, s0, ws);  // (ends with a barrier: h is free)
+  PK1_SSTAMP(10);
+  // the keys of the selected digit-0 bin (a small share of the candidates) compacted into LDS
+  // (h[0] their count, h[1..] the keys relative to B) and ranked directly: the k_rem-th largest
+  // of them is the threshold, k_rem minus the keys above it the ties to keep -- the threshold
+  // and tie count digits 1 and 2 would give, without two more passes over every candidate
+  const uint32_t rank_max = min((uint32_t)EW_BLOCK, g_pk_rank_max);
+  if (rank_max) {
+    if (threadIdx.x == 0) h[0] = 0u;
+    __syncthreads();
+    const uint32_t want = st[0] >> s0;
+    constexpr uint32_t CAP = NB0 * PK1_HSUB - 1;
+    auto put = [&](uint32_t key) {
+      const uint32_t rel = key - B;
+      if ((rel >> s0) == want) {
+        const uint32_t pos = atomicAdd(&h[0], 1u);
+        if (pos < CAP) h[1 + pos] = rel;
+      }
+    };
+    for (uint32_t i = threadIdx.x; i < nl; i += EW_BLOCK) put(keys[i]);
+    beyond(put);
+    __syncthreads();
+  }
+  const uint32_t nbin = rank_max ? h[0] : 0xffffffffu, k_rem = st[1];
+  __syncthreads();  // every thread holds them before st or h is rewritten
+  if (nbin <= rank_max) {
+    if (threadIdx.x < nbin) {
+      const uint32_t mine = h[1 + threadIdx.x];
+      uint32_t gt = 0, eq = 0;
+      for (uint32_t j = 0; j < nbin; ++j) {
+        const uint32_t x = h[1 + j];
+        gt += x > mine;
+        eq += x == mine;
+      }
+      // (threads holding an equal key write the same two words)
+      if (gt < k_rem && k_rem <= gt + eq) {
+        st[0] = mine;
+        st[1] = k_rem - gt;
+      }
+    }
+    __syncthreads();
+  } else {  // a crowded bin: the two remaining radix digits
+    pass(1, st[0] >> s0);
+    pk1_digit<NB1>(h, st, s1, ws);
+    pass(2, st[0] >> s1);
+    pk1_digit<NB2>(h, st, 0u, ws);
+  }
+  PK1_SSTAMP(11);
+#undef PK1_SSTAMP
   if (threadIdx.x == 0) {
     st[0] += B;  // absolute threshold key
     __hip_atomic_store(state + t * 4, st[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1938,7 +2049,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_pk_one(
   extern __shared__ uint32_t s_dyn[];  // select: histogram + staged keys; full passes: histograms
   // stamps (probes, EWDML_PK1_STAMPS=1): thread 0 stamps wall_clock64() at the phase boundaries
 #define PK1_STAMP(i) \
-  if (stamps && threadIdx.x == 0) stamps[(size_t)blockIdx.x * 8 + (i)] = wall_clock64()
+  if (stamps && threadIdx.x == 0) stamps[(size_t)blockIdx.x * PK1_NSTAMP + (i)] = wall_clock64()
   PK1_STAMP(0);
   __shared__ unsigned long long ws2[2 * EW_WAVES];
   __shared__ uint32_t wmax[EW_WAVES];
@@ -2071,7 +2182,8 @@ __global__ __launch_bounds__(EW_BLOCK) void k_pk_one(
     const uint32_t fast = s_u[1], M = s_u[5];
     if (fast) {
       pk1_select_cands(pcand + tr.cap0, M, s_u[2], s_u[3], s_u[4], s_u[6], (uint32_t)tr.k,
-                       s_dyn + NB0 * PK1_HSUB, min(M, lds_keys), s_dyn, s_st, ws, state, t);
+                       s_dyn + NB0 * PK1_HSUB, min(M, lds_keys), s_dyn, s_st, ws, state, t,
+                       stamps ? stamps + (size_t)blockIdx.x * PK1_NSTAMP : nullptr);
       if (threadIdx.x == 0) {
         // candidates steered to 1.5 k .. min(2.5 k, 7/8 of the LDS copy): the select's time
         // grows with them, and its single block is this launch's critical path
@@ -2081,6 +2193,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_pk_one(
         for (int r = 0; r < NREP; ++r)  // dead once the max is in the select state
           __hip_atomic_store(kmaxr + r * T + t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
+      PK1_STAMP(13);
     }
     if (threadIdx.x == 0)
       __hip_atomic_store(mode + TICK_STRIDE * t, fast, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2692,7 +2805,7 @@ static int ew_pk_one_max_blocks() {
 
 int ew_topk_one_max_blocks() { return ew_pk_one_max_blocks(); }
 
-// EWDML_PK1_STAMPS=1 (probes): k_pk_one's per-block phase stamps, 8 u64 per block, of the last
+// EWDML_PK1_STAMPS=1 (probes): k_pk_one's per-block phase stamps, 16 u64 per block, of the last
 // launch (tools/probes/encode_probe.py reads them with topk_one_stamps)
 static unsigned long long* g_pk1_stamps = nullptr;
 static int g_pk1_stamp_blocks = 0;
@@ -2704,15 +2817,15 @@ static unsigned long long* ew_pk1_stamps(int C) {
   if (!on) return nullptr;
   if (C > g_pk1_stamp_blocks) {
     if (g_pk1_stamps) EW_CHECK(hipFree(g_pk1_stamps));
-    EW_CHECK(hipMalloc(&g_pk1_stamps, (size_t)C * 8 * sizeof(unsigned long long)));
-    EW_CHECK(hipMemset(g_pk1_stamps, 0, (size_t)C * 8 * sizeof(unsigned long long)));
+    EW_CHECK(hipMalloc(&g_pk1_stamps, (size_t)C * PK1_NSTAMP * sizeof(unsigned long long)));
+    EW_CHECK(hipMemset(g_pk1_stamps, 0, (size_t)C * PK1_NSTAMP * sizeof(unsigned long long)));
     g_pk1_stamp_blocks = C;
   }
   return g_pk1_stamps;
 }
 
 std::vector<unsigned long long> ew_topk_one_stamps() {
-  std::vector<unsigned long long> out((size_t)g_pk1_stamp_blocks * 8);
+  std::vector<unsigned long long> out((size_t)g_pk1_stamp_blocks * PK1_NSTAMP);
   if (g_pk1_stamps) {
     EW_CHECK(hipDeviceSynchronize());
     EW_CHECK(hipMemcpy(out.data(), g_pk1_stamps, out.size() * 8, hipMemcpyDeviceToHost));
@@ -2742,8 +2855,19 @@ static void ew_pk_band_init() {
   EW_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_pk_band_q), q, sizeof(q)));
 }
 
+static void ew_pk_rank_init() {
+  static bool done = false;
+  if (done) return;
+  done = true;
+  const char* e = std::getenv("EWDML_PK_RANK");
+  if (!e || e[0] != '0') return;
+  const uint32_t z = 0u;
+  EW_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_pk_rank_max), &z, sizeof(z)));
+}
+
 void ew_topk_encode(const TopkEncodeArgs& a) {
   ew_pk_band_init();
+  ew_pk_rank_init();
   auto* chunks = reinterpret_cast<const ChunkRow*>(a.chunks);
   auto* tensors = reinterpret_cast<const TensorRow*>(a.tensors);
   auto* scratch = reinterpret_cast<uint8_t*>(a.scratch);
