@@ -1979,30 +1979,71 @@ __device__ __forceinline__ void pk1_select_cands(const uint2* __restrict__ cands
   // of them is the threshold, k_rem minus the keys above it the ties to keep -- the threshold
   // and tie count digits 1 and 2 would give, without two more passes over every candidate
   const uint32_t rank_max = min((uint32_t)EW_BLOCK, g_pk_rank_max);
+  uint32_t* lst = h + 4;  // (16-B aligned: read four keys at a time when ranking)
+  uint32_t nbin = 0xffffffffu;
+  const uint32_t k_rem = st[1];
   if (rank_max) {
-    if (threadIdx.x == 0) h[0] = 0u;
-    __syncthreads();
+    // count, scan, place: no atomics (a per-match atomic made each step a dependent round trip)
     const uint32_t want = st[0] >> s0;
-    constexpr uint32_t CAP = NB0 * PK1_HSUB - 1;
-    auto put = [&](uint32_t key) {
-      const uint32_t rel = key - B;
-      if ((rel >> s0) == want) {
-        const uint32_t pos = atomicAdd(&h[0], 1u);
-        if (pos < CAP) h[1 + pos] = rel;
-      }
+    constexpr uint32_t CAP = NB0 * PK1_HSUB - 4;
+    const uint4* k4 = reinterpret_cast<const uint4*>(keys);
+    const uint32_t nq = (nl + 3u) >> 2;
+    auto hit = [&](uint32_t key, uint32_t idx) -> uint32_t {
+      return (idx < nl && ((key - B) >> s0) == want) ? 1u : 0u;
     };
-    for (uint32_t i = threadIdx.x; i < nl; i += EW_BLOCK) put(keys[i]);
-    beyond(put);
-    __syncthreads();
+    uint32_t cnt = 0;
+    for (uint32_t q = threadIdx.x; q < nq; q += EW_BLOCK) {
+      const uint4 x = k4[q];
+      cnt += hit(x.x, 4 * q) + hit(x.y, 4 * q + 1) + hit(x.z, 4 * q + 2) + hit(x.w, 4 * q + 3);
+    }
+    uint32_t total;
+    uint32_t pos = ew_block_excl_scan(cnt, ws, total);  // (its barriers: st read by all first)
+    if (cnt) {
+      for (uint32_t q = threadIdx.x; q < nq; q += EW_BLOCK) {
+        const uint4 x = k4[q];
+        const uint32_t kk[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (hit(kk[e], 4 * q + e)) {
+            if (pos < CAP) lst[pos] = kk[e] - B;
+            ++pos;
+          }
+      }
+    }
+    nbin = total;
+    if (M > nl) {  // (rare: the band keeps the candidates within the LDS copy)
+      if (threadIdx.x == 0) h[0] = total;
+      __syncthreads();
+      beyond([&](uint32_t key) {
+        const uint32_t rel = key - B;
+        if ((rel >> s0) == want) {
+          const uint32_t p = atomicAdd(&h[0], 1u);
+          if (p < CAP) lst[p] = rel;
+        }
+      });
+      __syncthreads();
+      nbin = h[0];
+    }
   }
-  const uint32_t nbin = rank_max ? h[0] : 0xffffffffu, k_rem = st[1];
-  __syncthreads();  // every thread holds them before st or h is rewritten
+  __syncthreads();  // the list complete; every thread holds k_rem before st is rewritten
+  PK1_SSTAMP(12);
+  if (stamp && threadIdx.x == 0) {  // (probe: the candidate count and the ranked bin's)
+    stamp[14] = M;
+    stamp[15] = nbin;
+  }
   if (nbin <= rank_max) {
     if (threadIdx.x < nbin) {
-      const uint32_t mine = h[1 + threadIdx.x];
-      uint32_t gt = 0, eq = 0;
-      for (uint32_t j = 0; j < nbin; ++j) {
-        const uint32_t x = h[1 + j];
+      const uint32_t mine = lst[threadIdx.x];
+      uint32_t gt = 0, eq = 0, j = 0;
+      for (; j + 4 <= nbin; j += 4) {
+        const uint4 x = *reinterpret_cast<const uint4*>(lst + j);
+        gt += (uint32_t)(x.x > mine) + (uint32_t)(x.y > mine) + (uint32_t)(x.z > mine) +
+              (uint32_t)(x.w > mine);
+        eq += (uint32_t)(x.x == mine) + (uint32_t)(x.y == mine) + (uint32_t)(x.z == mine) +
+              (uint32_t)(x.w == mine);
+      }
+      for (; j < nbin; ++j) {
+        const uint32_t x = lst[j];
         gt += x > mine;
         eq += x == mine;
       }

@@ -6,7 +6,7 @@ LeNet's bucket, steady-state DGC error feedback.  Run with EWDML_PK1_STAMPS=1:
 Prints, per tensor, the spread of each phase over its blocks in us from the launch's first
 stamp: 0 start, 1 staged, 2 candidates appended (ticket), 6/7 select begin/end (tensor-last
 block), 3 selected (generation seen), 4 written; inside the tensor-last block's select: 8 pass 0
-(keys staged), 9 fold, 10 digit 0, 11 the selected bin's keys ranked (or digits 1 and 2), 13 the
+(keys staged), 9 fold, 10 digit 0, 12 the selected bin's keys compacted, 11 ranked (or digits 1 and 2), 13 the
 prediction stored."""
 import os
 import sys
@@ -48,10 +48,12 @@ def main():
     chunk_t = [int(x) for x in plan.chunk_table("cpu")[:, 0].tolist()]
     for t in range(plan.num_tensors):
         bs = [b for b in range(C) if chunk_t[b] == t]
-        ph = {i: [us(rows[b][i]) for b in bs if rows[b][i]] for i in (0, 1, 2, 6, 8, 9, 10, 11, 13, 7, 3, 4)}
+        ph = {i: [us(rows[b][i]) for b in bs if rows[b][i]] for i in (0, 1, 2, 6, 8, 9, 10, 12, 11, 13, 7, 3, 4)}
         desc = "  ".join(f"{i}:{min(x):6.2f}-{max(x):6.2f}" if x else f"{i}:-"
                          for i, x in ph.items())
-        print(f"tensor {t} ({plan.numels[t]} el, {len(bs)} blocks, k={plan.ks[t]})  {desc}")
+        last = [b for b in bs if rows[b][14]]
+        mn = f"  M={rows[last[0]][14]} bin={rows[last[0]][15]}" if last else ""
+        print(f"tensor {t} ({plan.numels[t]} el, {len(bs)} blocks, k={plan.ks[t]})  {desc}{mn}")
     print("launch span us", max(us(rw[4]) for rw in rows))
 
 
