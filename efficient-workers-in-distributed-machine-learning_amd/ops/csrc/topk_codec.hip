@@ -1852,7 +1852,8 @@ constexpr int PK1_HSUB = 4;  // pass-0 sub-histograms (lanes t % 4): the candida
 // One digit select over an LDS histogram of NB bins, scanned from the top, state in LDS: the bin
 // holding the k_rem-th largest key (st[0] |= bin << shift; st[1] = what is left of k_rem).  The
 // same arithmetic as pk_select without its global state round trips.
-template <int NB>
+// SUB: bin b's count is the sum of h[b * SUB .. b * SUB + SUB - 1] (pass 0's sub-histograms)
+template <int NB, int SUB = 1>
 __device__ __forceinline__ void pk1_digit(const uint32_t* h, uint32_t* st, uint32_t shift,
                                           uint32_t* ws) {
   constexpr int PER = NB / EW_BLOCK;
@@ -1860,7 +1861,15 @@ __device__ __forceinline__ void pk1_digit(const uint32_t* h, uint32_t* st, uint3
   uint32_t cnt[PER], tsum = 0;
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
-    cnt[j] = h[NB - 1 - (threadIdx.x * PER + j)];
+    const int b = NB - 1 - (threadIdx.x * PER + j);
+    if constexpr (SUB == 4) {
+      const uint4 q = *reinterpret_cast<const uint4*>(h + b * 4);
+      cnt[j] = q.x + q.y + q.z + q.w;
+    } else {
+      cnt[j] = 0;
+#pragma unroll
+      for (int q = 0; q < SUB; ++q) cnt[j] += h[b * SUB + q];
+    }
     tsum += cnt[j];
   }
   uint32_t total;
@@ -1933,9 +1942,8 @@ __device__ __forceinline__ void pk1_select_cands(const uint2* __restrict__ cands
     st[0] = 0u;
     st[1] = k;
   }
-  // pass 0 while the keys are staged into LDS: each key counted as it arrives
-  for (int i = threadIdx.x; i < NB0 * PK1_HSUB; i += EW_BLOCK) h[i] = 0;
-  __syncthreads();  // (also orders st's initialisation before the digit select)
+  // pass 0 while the keys are staged into LDS: each key counted as it arrives (h: its
+  // NB0 x PK1_HSUB sub-histograms, zeroed by every block at the kernel's start)
   for (uint32_t b0 = 0; b0 < nl; b0 += EW_BLOCK * R) {
     uint32_t kv[R];
 #pragma unroll
@@ -1956,23 +1964,8 @@ __device__ __forceinline__ void pk1_select_cands(const uint2* __restrict__ cands
   beyond([&](uint32_t key) { add(0, 0u, key); });
   __syncthreads();
   PK1_SSTAMP(8);
-  {  // fold the sub-histograms into bins 0..NB0-1 (all read before any is overwritten)
-    constexpr int PER = NB0 / EW_BLOCK;
-    uint32_t x[PER];
-#pragma unroll
-    for (int j = 0; j < PER; ++j) {
-      const int i = threadIdx.x + j * EW_BLOCK;
-      x[j] = 0;
-#pragma unroll
-      for (int q = 0; q < PK1_HSUB; ++q) x[j] += h[i * PK1_HSUB + q];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < PER; ++j) h[threadIdx.x + j * EW_BLOCK] = x[j];
-    __syncthreads();
-  }
   PK1_SSTAMP(9);
-  pk1_digit<NB0>(h, st, s0, ws);  // (ends with a barrier: h is free)
+  pk1_digit<NB0, PK1_HSUB>(h, st, s0, ws);  // (ends with a barrier: h is free)
   PK1_SSTAMP(10);
   // the keys of the selected digit-0 bin (a small share of the candidates) compacted into LDS
   // (h[0] their count, h[1..] the keys relative to B) and ranked directly: the k_rem-th largest
@@ -2087,7 +2080,8 @@ __global__ __launch_bounds__(EW_BLOCK) void k_pk_one(
     int scales_off, int idx_off, int codes_off, int bitmap_off, int counts_off, float levels,
     float inv_levels, uint32_t key_arg, const uint32_t* __restrict__ keyp, uint32_t bucket_offset,
     int lb_fault, uint32_t lds_keys, unsigned long long* __restrict__ stamps, TkApply ap) {
-  extern __shared__ uint32_t s_dyn[];  // select: histogram + staged keys; full passes: histograms
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];  // select: histogram + staged
+  // keys; full passes: histograms
   // stamps (probes, EWDML_PK1_STAMPS=1): thread 0 stamps wall_clock64() at the phase boundaries
 #define PK1_STAMP(i) \
   if (stamps && threadIdx.x == 0) stamps[(size_t)blockIdx.x * PK1_NSTAMP + (i)] = wall_clock64()
@@ -2114,6 +2108,10 @@ __global__ __launch_bounds__(EW_BLOCK) void k_pk_one(
     __hip_atomic_store(lb + blockIdx.x, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint32_t key = keyp ? *keyp : key_arg;
   ew_sgd_resolve(ap.sa);
+  // the select's pass-0 sub-histograms zeroed while this block's staging loads are in flight
+  // (any block may turn out to be its tensor's last; the barriers before the select order it)
+  for (int i = threadIdx.x; i < NB0 * PK1_HSUB / 4; i += EW_BLOCK)
+    reinterpret_cast<uint4*>(s_dyn)[i] = uint4{0u, 0u, 0u, 0u};
   // ---- 1. stage (error feedback) and compact the candidates (k_pk_hist0) ----
   float4 v[EW_CU];
   topk_load_stage<EFM>(gp, dg, resid, c, v);
@@ -2225,21 +2223,24 @@ __global__ __launch_bounds__(EW_BLOCK) void k_pk_one(
       pk1_select_cands(pcand + tr.cap0, M, s_u[2], s_u[3], s_u[4], s_u[6], (uint32_t)tr.k,
                        s_dyn + NB0 * PK1_HSUB, min(M, lds_keys), s_dyn, s_st, ws, state, t,
                        stamps ? stamps + (size_t)blockIdx.x * PK1_NSTAMP : nullptr);
-      if (threadIdx.x == 0) {
-        // candidates steered to 1.5 k .. min(2.5 k, 7/8 of the LDS copy): the select's time
-        // grows with them, and its single block is this launch's critical path
-        const uint32_t kk = (uint32_t)tr.k;
-        pk_predict_thr(tr, t, s_st[0], pst, cand_n, M, 1u, pbeta, phad,
-                       min(lds_keys - lds_keys / 8, kk * 2u + kk / 2u), kk + kk / 2u);
-        for (int r = 0; r < NREP; ++r)  // dead once the max is in the select state
-          __hip_atomic_store(kmaxr + r * T + t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      PK1_STAMP(13);
     }
     if (threadIdx.x == 0)
       __hip_atomic_store(mode + TICK_STRIDE * t, fast, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     PK1_STAMP(7);
     pk_publish(arr, gn, g0 + 1u);  // (arr: zero already; rewritten to zero)
+    if (fast && threadIdx.x == 0) {
+      // the next launch's prediction, after the publish: no block of this launch reads these
+      // words again (P, beta and had were read before the tensor's ticket; n before arriving;
+      // the write takes the scale from the select state).  Candidates steered to 1.5 k ..
+      // min(2.5 k, 7/8 of the LDS copy): the select's time grows with them, and its single
+      // block is this launch's critical path
+      const uint32_t kk = (uint32_t)tr.k;
+      pk_predict_thr(tr, t, s_st[0], pst, cand_n, M, 1u, pbeta, phad,
+                     min(lds_keys - lds_keys / 8, kk * 2u + kk / 2u), kk + kk / 2u);
+      for (int r = 0; r < NREP; ++r)  // dead once the max is in the select state
+        __hip_atomic_store(kmaxr + r * T + t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      PK1_STAMP(13);
+    }
   } else {
     pk1_wait(gn, g0 + 1u, lb_err, &s_gen);
   }
