@@ -26,6 +26,8 @@ exchange is a fixed-size all-gather with no size handshake):
 from dataclasses import dataclass, field
 from typing import List
 
+import os
+
 import torch
 
 CHUNK = 8192
@@ -35,6 +37,14 @@ BM_WORDS = CHUNK // 32  # bitmap words per chunk
 # numel; more (or fewer than k) and that tensor takes the exact full-pass path for the step
 CAND_K_MULT = 8
 CAND_SLACK = 4096
+# ... but a tensor of at most this many elements keeps all of them (bound 0, never a miss;
+# EWDML_CAND_ALL_MAX, default 0 = off: measured slower, profiles/ab/README.md "Round 6")
+CAND_ALL_MAX = int(os.environ.get("EWDML_CAND_ALL_MAX", "0"))
+
+
+def cand_cap(n: int, k: int) -> int:
+    """Candidate-list capacity of a tensor of n elements keeping k."""
+    return n if n <= CAND_ALL_MAX else min(n, CAND_K_MULT * k + CAND_SLACK)
 
 
 def _align(n: int, a: int = 16) -> int:
@@ -105,7 +115,7 @@ class BucketPlan:
         self.total_bm_words = bw
         cap0 = 0
         for n, k in zip(self.numels, self.ks):
-            cap = min(n, CAND_K_MULT * k + CAND_SLACK)
+            cap = cand_cap(n, k)
             self.tensor_cap.append(cap)
             self.tensor_cap0.append(cap0)
             cap0 += cap

@@ -889,6 +889,12 @@ __device__ __forceinline__ void topk_write_lb(
                            key, bucket_offset, thr, ties, ebase, eend, inv, step, ws, ap);
 }
 
+// A chunk with more candidates than this writes from its staged values instead of its candidate
+// list (the same entries, bit for bit: the candidates are every element at or above the bound,
+// which the threshold is not below, in index order): the list's write runs one round of L2 loads
+// and a block scan per 256 candidates, the register write a fixed EW_CU scans
+constexpr uint32_t PK_WRITE_CANDS_MAX = 2048;
+
 template <int VK, bool EF, bool LB, bool PK>
 __global__ __launch_bounds__(EW_BLOCK) void k_topk_write(
     GradPtrs gp, float* __restrict__ resid, const ChunkRow* __restrict__ chunks,
@@ -925,7 +931,8 @@ __global__ __launch_bounds__(EW_BLOCK) void k_topk_write(
   const TensorRow tr = tensors[c.tensor];
   // the producer-staging stamps were read by the staging pass (an earlier launch): re-arm
   if (stamps && c.local == 0 && threadIdx.x == 0) stamps[c.tensor] = 0u;
-  if (PK && pst[c.tensor * 8 + 3]) {  // predictive fast path: the chunk's candidates only
+  if (PK && pst[c.tensor * 8 + 3] && pk_n <= PK_WRITE_CANDS_MAX) {
+    // predictive fast path: the chunk's candidates only
     // the tensor's selection state, loaded together before the look-back's barriers
     topk_write_cands<VK, EF>(c, tr, resid, vel, state, payload, scales_off, idx_off, codes_off,
                              bitmap_off, counts_off, levels, inv_levels, key, bucket_offset, lb,
@@ -2347,7 +2354,7 @@ __global__ __launch_bounds__(EW_BLOCK) void k_pk_one(
   const float scale = __uint_as_float(__hip_atomic_load(state + t * 4 + 2, __ATOMIC_RELAXED,
                                                         __HIP_MEMORY_SCOPE_AGENT));
   float* velm = dg.mask ? dg.vel : nullptr;
-  if (fast) {
+  if (fast && tot <= PK_WRITE_CANDS_MAX) {
     topk_write_cands<VK, EF>(c, tr, resid, velm, state, payload, scales_off, idx_off, codes_off,
                              bitmap_off, counts_off, levels, inv_levels, key, bucket_offset, lb,
                              lb_err, tot, pcand + tr.cap0 + cbase0, ws, s_lb, lb_fault, thr, need,
