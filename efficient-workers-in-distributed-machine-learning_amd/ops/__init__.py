@@ -127,10 +127,12 @@ def topk_stats(dp) -> dict:
     """Counters of a bucket's top-k encodes (synchronises): ``lookback_errors`` (write blocks that
     gave up waiting on a predecessor's look-back word: their payload offsets are wrong -- must be
     0), and the tensor-encodes of the predictive encode on the ``fast`` (candidates only) and the
-    ``full`` path."""
-    e, fast, full = require().topk_stats(_ptr(dp.scratch), dp.plan.num_tensors,
-                                         dp.plan.num_chunks)
-    return {"lookback_errors": e, "fast": fast, "full": full}
+    ``full`` path (``full_by_tensor``: the first 28 tensors' share of the latter, as [too few
+    candidates, too many] pairs)."""
+    v = require().topk_stats(_ptr(dp.scratch), dp.plan.num_tensors, dp.plan.num_chunks)
+    e, fast, full = v[:3]
+    return {"lookback_errors": e, "fast": fast, "full": full,
+            "full_by_tensor": [[x & 0xFFFF, x >> 16] for x in v[3:3 + dp.plan.num_tensors]]}
 
 
 _GRAPH_NODE_TYPES = ["kernel", "memcpy", "memset", "host", "graph", "empty", "wait_event",

@@ -42,6 +42,9 @@ constexpr int NB2 = 1024;  // pass-2 digit: key bits [9:0]
 // bins), and one copy serialised ~300 global atomics per bin; the select kernel sums the copies.
 constexpr int NREP = 8;
 constexpr int TICK_STRIDE = 32;  // ints per ticket (one 128-B line)
+// the first PK_MISS_T tensors' full-path (missed prediction) counts, after the fast / full totals
+// on the look-back error counter's line
+constexpr int PK_MISS_T = TICK_STRIDE - 4;
 
 // Per-tensor hand-off from the chunk blocks of a pass to the tensor's last-arriving block, which
 // then runs the pass's per-tensor step itself (select / scan) instead of a one-block-per-tensor
@@ -1366,6 +1369,8 @@ __global__ __launch_bounds__(EW_BLOCK, WPE) void k_pk_hist0(
     pst[c.tensor * 8 + 6] = s0;
     pst[c.tensor * 8 + 7] = s1;
     atomicAdd(stats + (fast ? 0 : 1), 1);
+    if (!fast && c.tensor < PK_MISS_T)  // per-tensor misses: too few candidates (1) / too many (2^16)
+      atomicAdd(stats + 2 + c.tensor, M < (uint32_t)tr.k ? 1 : 65536);
     s_sel[0] = fast && M <= inline_max;
     s_sel[1] = B;
     s_sel[2] = s0;
@@ -1850,6 +1855,11 @@ __global__ __launch_bounds__(EW_BLOCK) void k_pk_select(
 // vmcnt drain and read by agent-scope (sc1) loads after the poll, plus an agent acquire.
 // ---------------------------------------------------------------------------------------------
 constexpr int PK1_NSTAMP = 16;  // probe stamps per block (EWDML_PK1_STAMPS)
+// the candidate band's floor for few-k tensors (k_pk_one's prediction; EWDML_PK1_LO at build)
+#ifndef EWDML_PK1_LO
+#define EWDML_PK1_LO 2048
+#endif
+constexpr uint32_t PK1_LO_KEYS = EWDML_PK1_LO;
 constexpr int PK1_LDS_KEYS = 10240;  // candidate keys the selecting block stages in LDS (40 KB):
                                      // with the histograms ~73 KB, two blocks per CU
 constexpr int PK1_HSUB = 4;  // pass-0 sub-histograms (lanes t % 4): the candidates crowd the low
@@ -2218,6 +2228,8 @@ __global__ __launch_bounds__(EW_BLOCK) void k_pk_one(
       pst[t * 8 + 6] = s0;
       pst[t * 8 + 7] = s1;
       atomicAdd(stats + (fast ? 0 : 1), 1);
+      if (!fast && t < PK_MISS_T)  // per-tensor misses: too few candidates (1) / too many (2^16)
+        atomicAdd(stats + 2 + t, M < (uint32_t)tr.k ? 1 : 65536);
       s_u[1] = fast;
       s_u[2] = B;
       s_u[3] = s0;
@@ -2240,10 +2252,13 @@ __global__ __launch_bounds__(EW_BLOCK) void k_pk_one(
       // words again (P, beta and had were read before the tensor's ticket; n before arriving;
       // the write takes the scale from the select state).  Candidates steered to 1.5 k ..
       // min(2.5 k, 7/8 of the LDS copy): the select's time grows with them, and its single
-      // block is this launch's critical path
+      // block is this launch's critical path.  Few-k tensors keep at least PK1_LO_KEYS (their
+      // thresholds jump the most -- without error feedback LeNet's conv2 and fc2 missed ~1 step
+      // in 4 -- and a few thousand keys cost their select next to nothing)
       const uint32_t kk = (uint32_t)tr.k;
-      pk_predict_thr(tr, t, s_st[0], pst, cand_n, M, 1u, pbeta, phad,
-                     min(lds_keys - lds_keys / 8, kk * 2u + kk / 2u), kk + kk / 2u);
+      const uint32_t hi = min(lds_keys - lds_keys / 8, max(kk * 2u + kk / 2u, 2u * PK1_LO_KEYS));
+      pk_predict_thr(tr, t, s_st[0], pst, cand_n, M, 1u, pbeta, phad, hi,
+                     max(kk + kk / 2u, min(PK1_LO_KEYS, hi / 2u)));
       for (int r = 0; r < NREP; ++r)  // dead once the max is in the select state
         __hip_atomic_store(kmaxr + r * T + t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       PK1_STAMP(13);
@@ -3145,9 +3160,11 @@ std::vector<int> ew_topk_stats(uintptr_t scratch, int T, int C) {
   int* tick = reinterpret_cast<int*>(
       (reinterpret_cast<uintptr_t>(inv + T) + TICK_STRIDE * 4 - 1) & ~(uintptr_t)(TICK_STRIDE * 4 - 1));
   int* lb_err = tick + 5 * TICK_STRIDE * T;
-  std::vector<int> v(3, 0);
+  // {look-back errors, fast, full, full per tensor (the first PK_MISS_T tensors)}
+  std::vector<int> v(3 + PK_MISS_T, 0);
   EW_CHECK(hipMemcpy(v.data(), lb_err, sizeof(int), hipMemcpyDeviceToHost));
-  EW_CHECK(hipMemcpy(v.data() + 1, lb_err + 2, 2 * sizeof(int), hipMemcpyDeviceToHost));
+  EW_CHECK(hipMemcpy(v.data() + 1, lb_err + 2, (2 + PK_MISS_T) * sizeof(int),
+                     hipMemcpyDeviceToHost));
   return v;
 }
 

@@ -496,18 +496,22 @@ class GradientExchange:
         if not self.cuda or codec.kind not in ("topk", "topk_qsgd") or codec.allreduce:
             return {}
         tot = {"lookback_errors": 0, "fast": 0, "full": 0}
+        misses = []  # per bucket: its tensors' full-path counts
         seen = set()
         for _, _, dplans in getattr(codec, "_bound", {}).values():
             for dp in dplans:
                 if id(dp) in seen:
                     continue
                 seen.add(id(dp))
-                for k, v in ops.topk_stats(dp).items():
+                st = ops.topk_stats(dp)
+                misses.append(st.pop("full_by_tensor", []))
+                for k, v in st.items():
                     tot[k] += v
         if tot["lookback_errors"]:
             raise RuntimeError(f"top-k encode: {tot['lookback_errors']} write block(s) gave up on "
                                "the decoupled look-back; the payload offsets are corrupt")
-        return {"topk_encode_fast": tot["fast"], "topk_encode_full": tot["full"]}
+        return {"topk_encode_fast": tot["fast"], "topk_encode_full": tot["full"],
+                "topk_encode_full_by_tensor": misses}
 
     def close(self):
         if self.stamps is not None:
