@@ -1855,11 +1855,9 @@ __global__ __launch_bounds__(EW_BLOCK) void k_pk_select(
 // vmcnt drain and read by agent-scope (sc1) loads after the poll, plus an agent acquire.
 // ---------------------------------------------------------------------------------------------
 constexpr int PK1_NSTAMP = 16;  // probe stamps per block (EWDML_PK1_STAMPS)
-// the candidate band's floor for few-k tensors (k_pk_one's prediction; EWDML_PK1_LO at build)
-#ifndef EWDML_PK1_LO
-#define EWDML_PK1_LO 2048
-#endif
-constexpr uint32_t PK1_LO_KEYS = EWDML_PK1_LO;
+// the candidate band's floor for few-k tensors without error feedback (k_pk_one's prediction;
+// EWDML_PK1_LO: another, 0 = none; A/B)
+__device__ uint32_t g_pk1_lo_keys = 2048u;
 constexpr int PK1_LDS_KEYS = 10240;  // candidate keys the selecting block stages in LDS (40 KB):
                                      // with the histograms ~73 KB, two blocks per CU
 constexpr int PK1_HSUB = 4;  // pass-0 sub-histograms (lanes t % 4): the candidates crowd the low
@@ -2252,13 +2250,15 @@ __global__ __launch_bounds__(EW_BLOCK) void k_pk_one(
       // words again (P, beta and had were read before the tensor's ticket; n before arriving;
       // the write takes the scale from the select state).  Candidates steered to 1.5 k ..
       // min(2.5 k, 7/8 of the LDS copy): the select's time grows with them, and its single
-      // block is this launch's critical path.  Few-k tensors keep at least PK1_LO_KEYS (their
+      // block is this launch's critical path.  Few-k tensors keep at least g_pk1_lo_keys (their
       // thresholds jump the most -- without error feedback LeNet's conv2 and fc2 missed ~1 step
       // in 4 -- and a few thousand keys cost their select next to nothing)
-      const uint32_t kk = (uint32_t)tr.k;
-      const uint32_t hi = min(lds_keys - lds_keys / 8, max(kk * 2u + kk / 2u, 2u * PK1_LO_KEYS));
+      // (without error feedback only: under EF the thresholds move smoothly, and the floor's
+      // extra candidates cost the write ~2 us, profiles/ab/README.md)
+      const uint32_t kk = (uint32_t)tr.k, lo_keys = EF ? 0u : g_pk1_lo_keys;
+      const uint32_t hi = min(lds_keys - lds_keys / 8, max(kk * 2u + kk / 2u, 2u * lo_keys));
       pk_predict_thr(tr, t, s_st[0], pst, cand_n, M, 1u, pbeta, phad, hi,
-                     max(kk + kk / 2u, min(PK1_LO_KEYS, hi / 2u)));
+                     max(kk + kk / 2u, min(lo_keys, hi / 2u)));
       for (int r = 0; r < NREP; ++r)  // dead once the max is in the select state
         __hip_atomic_store(kmaxr + r * T + t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       PK1_STAMP(13);
@@ -2919,6 +2919,16 @@ static void ew_pk_band_init() {
   EW_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_pk_band_q), q, sizeof(q)));
 }
 
+static void ew_pk1_lo_init() {
+  static bool done = false;
+  if (done) return;
+  done = true;
+  const char* e = std::getenv("EWDML_PK1_LO");
+  if (!e) return;
+  const uint32_t v = (uint32_t)std::atol(e);
+  EW_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_pk1_lo_keys), &v, sizeof(v)));
+}
+
 static void ew_pk_rank_init() {
   static bool done = false;
   if (done) return;
@@ -2932,6 +2942,7 @@ static void ew_pk_rank_init() {
 void ew_topk_encode(const TopkEncodeArgs& a) {
   ew_pk_band_init();
   ew_pk_rank_init();
+  ew_pk1_lo_init();
   auto* chunks = reinterpret_cast<const ChunkRow*>(a.chunks);
   auto* tensors = reinterpret_cast<const TensorRow*>(a.tensors);
   auto* scratch = reinterpret_cast<uint8_t*>(a.scratch);
