@@ -692,15 +692,19 @@ __device__ __forceinline__ void topk_write_cands(
     int idx_off, int codes_off, int bitmap_off, int counts_off, float levels, float inv_levels,
     uint32_t key, uint32_t bucket_offset, unsigned long long* __restrict__ lb,
     int* __restrict__ lb_err, uint32_t n, const uint2* __restrict__ cs, uint32_t* ws,
-    uint32_t* s_lb, int lb_fault, uint32_t thr, uint32_t need, float scale, const TkApply& ap) {
+    uint32_t* s_lb, int lb_fault, uint32_t thr, uint32_t need, float scale, const TkApply& ap,
+    bool have0 = false, uint2 e0 = uint2{0u, 0u}) {
+  // have0: the thread's first candidate (index threadIdx.x < n) already loaded as e0 (ahead of
+  // the wait for the select); otherwise it is loaded once here for both loops
   __shared__ uint32_t bm[EW_BM_WORDS];
   const uint32_t eend = (uint32_t)(tr.entry0 + tr.k);
   const bool bitmap = tr.bm0 >= 0;
   if (bitmap)
     for (int i = threadIdx.x; i < EW_BM_WORDS; i += EW_BLOCK) bm[i] = 0u;
+  if (!have0 && threadIdx.x < n) e0 = cs[threadIdx.x];
   uint32_t gt = 0, eq = 0;
   for (uint32_t i = threadIdx.x; i < n; i += EW_BLOCK) {
-    const uint32_t k = cs[i].x & 0x7fffffffu;
+    const uint32_t k = (i == threadIdx.x ? e0 : cs[i]).x & 0x7fffffffu;
     gt += k > thr;
     eq += k == thr;
   }
@@ -723,7 +727,7 @@ __device__ __forceinline__ void topk_write_cands(
   for (uint32_t r0 = 0; r0 < n; r0 += EW_BLOCK) {  // uniform: n is the block's
     const uint32_t i = r0 + threadIdx.x;
     const bool valid = i < n;
-    const uint2 e = valid ? cs[i] : make_uint2(0u, 0u);
+    const uint2 e = valid ? (r0 == 0 ? e0 : cs[i]) : make_uint2(0u, 0u);
     const float x = __uint_as_float(e.x);
     const uint32_t k = e.x & 0x7fffffffu;
     const bool isgt = valid && k > thr, iseq = valid && k == thr;
@@ -2193,6 +2197,8 @@ __global__ __launch_bounds__(EW_BLOCK) void k_pk_one(
   }
   // ---- 2. the tensor's select ----
   PK1_STAMP(2);
+  unsigned long long pre0 = 0ull;  // (non-last blocks: the first candidate, loaded before the wait)
+  bool have_pre = false;
   if (topk_tensor_last(tick + TICK_STRIDE * t, tr.nchunks, reinterpret_cast<int*>(wmax))) {
     PK1_STAMP(6);
     // every block of the tensor read its producer-staging stamp before arriving: re-arm it
@@ -2264,6 +2270,12 @@ __global__ __launch_bounds__(EW_BLOCK) void k_pk_one(
       PK1_STAMP(13);
     }
   } else {
+    // this block's first candidates (written by it before the ticket), in flight during the wait
+    have_pre = tot <= PK_WRITE_CANDS_MAX;  // (block-uniform)
+    if (threadIdx.x < tot && have_pre)
+      pre0 = __hip_atomic_load(reinterpret_cast<const unsigned long long*>(
+                                   pcand + tr.cap0 + cbase0 + threadIdx.x),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     pk1_wait(gn, g0 + 1u, lb_err, &s_gen);
   }
   __syncthreads();
@@ -2373,7 +2385,8 @@ __global__ __launch_bounds__(EW_BLOCK) void k_pk_one(
     topk_write_cands<VK, EF>(c, tr, resid, velm, state, payload, scales_off, idx_off, codes_off,
                              bitmap_off, counts_off, levels, inv_levels, key, bucket_offset, lb,
                              lb_err, tot, pcand + tr.cap0 + cbase0, ws, s_lb, lb_fault, thr, need,
-                             scale, ap);
+                             scale, ap, have_pre,
+                             make_uint2((uint32_t)pre0, (uint32_t)(pre0 >> 32)));
   } else {
     topk_write_lb<VK, EF>(c, tr, v, resid, velm, payload, scales_off, idx_off, codes_off,
                           bitmap_off, counts_off, levels, inv_levels, key, bucket_offset, lb,
