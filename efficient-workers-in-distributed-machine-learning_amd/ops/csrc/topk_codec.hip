@@ -2272,7 +2272,9 @@ __global__ __launch_bounds__(EW_BLOCK) void k_pk_one(
   } else {
     // this block's first candidates (written by it before the ticket), in flight during the wait
     have_pre = tot <= PK_WRITE_CANDS_MAX;  // (block-uniform)
-    if (threadIdx.x < tot && have_pre)
+    // (only entries inside the tensor's list: past its capacity -- a prediction that let too many
+    // in -- nothing was stored, and the address may lie past the scratch)
+    if (threadIdx.x < tot && have_pre && cbase0 + threadIdx.x < (uint32_t)tr.cap)
       pre0 = __hip_atomic_load(reinterpret_cast<const unsigned long long*>(
                                    pcand + tr.cap0 + cbase0 + threadIdx.x),
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
