@@ -117,15 +117,52 @@ class DeviceLoader:
         if self._pos >= self.batches_per_epoch:
             self._start_epoch(self.epoch + 1)
 
-    def emit(self):
+    def emit(self, defer=False):
         """(fused) Launch the batch kernel for the device-side position and return the static
-        (x, y) buffers; graph-capturable.  The caller advances the host position (:meth:`advance`)."""
+        (x, y) buffers; graph-capturable.  The caller advances the host position (:meth:`advance`).
+
+        ``defer``: no launch -- the buffers carry ``_ew_batch`` (this loader) and the consumer
+        either forms the batch in its own first launch (ops/lenet.py: the LeNet conv launch,
+        :meth:`batch_args`) or calls :meth:`flush` before reading them."""
+        if defer and self.batch_fusable():
+            self._deferred = True
+            self.bx._ew_batch = self
+            return self.bx, self.by
+        # (a deferral left over from an aborted capture never ran: dropped, not launched)
+        self._deferred = False
+        self.bx._ew_batch = None
+        self._launch()
+        return self.bx, self.by
+
+    def _launch(self):
         from .. import ops
 
         ops.make_batch(self.x, self.y, self._perm, self._state, self._done, self.bx, self.by,
                        self._mean_l, self._istd_l, pad=4, augment=self.augment,
                        seed=self.seed * 7919 + 17, rank=self.rank)
-        return self.bx, self.by
+
+    def batch_fusable(self) -> bool:
+        """A consumer may form this loader's batch itself: fp32 NCHW, one channel, no
+        augmentation (the LeNet conv launch's gather)."""
+        return (self.fused and not self.augment and self.x.shape[1] == 1
+                and self.bx.dtype == torch.float32 and self.bx.is_contiguous())
+
+    def take_deferred(self):
+        """(consumer) The pending batch's kernel arguments, or None; the batch is then the
+        consumer's to form."""
+        if not getattr(self, "_deferred", False):
+            return None
+        self._deferred = False
+        self.bx._ew_batch = None
+        return (self.x, self.y, self._perm, self._state, self._done, self._mean_l[0],
+                self._istd_l[0])
+
+    def flush(self):
+        """Launch a deferred batch kernel (a consumer that cannot form the batch)."""
+        if getattr(self, "_deferred", False):
+            self._deferred = False
+            self.bx._ew_batch = None
+            self._launch()
 
     def advance(self):
         self._pos += 1

@@ -365,7 +365,10 @@ void ew_lenet_fwd(uintptr_t x, uintptr_t w1, uintptr_t b1, uintptr_t w2, uintptr
                   int K, uintptr_t a1, uintptr_t code1, uintptr_t a2, uintptr_t code2,
                   uintptr_t h1, uintptr_t logits, uintptr_t dlogits, uintptr_t dh1,
                   uintptr_t lossrow, uintptr_t loss, uintptr_t ws, long long ws_floats,
-                  uintptr_t cnt, int cnt_ints, uintptr_t stream);
+                  uintptr_t cnt, int cnt_ints, uintptr_t stream, uintptr_t bsrc = 0,
+                  uintptr_t blabels = 0, uintptr_t bperm = 0, long long bperm_len = 0,
+                  uintptr_t bstate = 0, uintptr_t bdone = 0, float bmean = 0.0f,
+                  float binv_std = 1.0f);
 void ew_lenet_bwd(uintptr_t x, uintptr_t w2, uintptr_t wf1, uintptr_t a1, uintptr_t code1,
                   uintptr_t a2, uintptr_t code2, uintptr_t h1, uintptr_t dlogits, uintptr_t dh1,
                   uintptr_t gscale, int B, int K, uintptr_t dp2, uintptr_t dw1, uintptr_t db1,

@@ -118,6 +118,22 @@ __device__ __forceinline__ void ln_stage(float* dst, const float* src, int n4, i
 // ---- forward convolutions: block (q, n), q = conv2's pooled output row ----
 constexpr int LN_CT = 256;  // conv forward block (4 waves)
 
+// The batch formed in the conv launch instead of its own (data/loader.py DeviceLoader, the
+// k_make_batch arithmetic of data.hip without augmentation, 1 channel): every block normalises
+// image n from the uint8 source at its slot of the permutation, the q = 0 blocks write it (for
+// the backward) and its label, and the launch's last block advances the batch position -- as
+// k_make_batch does, bit for bit.  src == nullptr: x is an ordinary input.
+struct LnBatch {
+  const uint8_t* src;
+  const long long* labels;
+  const long long* perm;
+  long long* state;  // {position, epoch}
+  int* done;         // arrival ticket (zeroed, left zeroed)
+  long long perm_len;
+  float mean, inv_std;
+  long long* y_out;
+};
+
 __global__ __launch_bounds__(LN_CT) void k_ln_conv_fwd(const float* __restrict__ x,
                                                        const float* __restrict__ w1,
                                                        const float* __restrict__ b1,
@@ -126,7 +142,8 @@ __global__ __launch_bounds__(LN_CT) void k_ln_conv_fwd(const float* __restrict__
                                                        float* __restrict__ a1,
                                                        uint8_t* __restrict__ code1,
                                                        float* __restrict__ a2,
-                                                       uint8_t* __restrict__ code2) {
+                                                       uint8_t* __restrict__ code2,
+                                                       LnBatch bt) {
   __shared__ __attribute__((aligned(16))) float s_x[IN * IN];
   __shared__ __attribute__((aligned(16))) float s_w1[W1N];
   __shared__ float s_b1[C1];
@@ -135,9 +152,28 @@ __global__ __launch_bounds__(LN_CT) void k_ln_conv_fwd(const float* __restrict__
   const int t = threadIdx.x, q = blockIdx.x, n = blockIdx.y;
   const int w = t >> 6, l = t & 63, g = l >> 4, li = l & 15;
   const int r0 = 2 * q;
+  long long bpos = 0;
   {
-    const f32x4* xs = reinterpret_cast<const f32x4*>(x + (long long)n * IN * IN);
-    const f32x4 xv = xs[min(t, IN * IN / 4 - 1)];
+    f32x4 xv;
+    if (bt.src) {
+      bpos = bt.state[0];
+      long long slot = bpos * gridDim.y + n;
+      if (slot >= bt.perm_len) slot %= bt.perm_len;  // never read past the permutation
+      const long long sample = bt.perm[slot];
+      const uint32_t px = reinterpret_cast<const uint32_t*>(
+          bt.src + sample * (IN * IN))[min(t, IN * IN / 4 - 1)];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        xv[k] = ((float)((px >> (8 * k)) & 0xffu) * (1.0f / 255.0f) - bt.mean) * bt.inv_std;
+      if (q == 0) {
+        if (t < IN * IN / 4)
+          reinterpret_cast<f32x4*>(const_cast<float*>(x) + (long long)n * IN * IN)[t] = xv;
+        if (t == 0) bt.y_out[n] = bt.labels[sample];
+      }
+    } else {
+      const f32x4* xs = reinterpret_cast<const f32x4*>(x + (long long)n * IN * IN);
+      xv = xs[min(t, IN * IN / 4 - 1)];
+    }
     const f32x4 wv = reinterpret_cast<const f32x4*>(w1)[min(t, W1N / 4 - 1)];
     const float bv = b1[min(t, C1 - 1)];
     if (t < IN * IN / 4) reinterpret_cast<f32x4*>(s_x)[t] = xv;
@@ -233,6 +269,12 @@ __global__ __launch_bounds__(LN_CT) void k_ln_conv_fwd(const float* __restrict__
         code2[i] = (uint8_t)code;
       }
     }
+  }
+  if (bt.src) {
+    // the launch's last block advances the batch position (k_make_batch's rule: every block read
+    // it before its barrier, hence before its arrival)
+    __syncthreads();
+    if (t == 0 && ew_grid_last(bt.done)) bt.state[0] = bpos + 1;
   }
 }
 
@@ -828,10 +870,20 @@ void ew_lenet_fwd(uintptr_t x, uintptr_t w1, uintptr_t b1, uintptr_t w2, uintptr
                   int K, uintptr_t a1, uintptr_t code1, uintptr_t a2, uintptr_t code2,
                   uintptr_t h1, uintptr_t logits, uintptr_t dlogits, uintptr_t dh1,
                   uintptr_t lossrow, uintptr_t loss, uintptr_t ws, long long ws_floats,
-                  uintptr_t cnt, int cnt_ints, uintptr_t stream) {
+                  uintptr_t cnt, int cnt_ints, uintptr_t stream, uintptr_t bsrc,
+                  uintptr_t blabels, uintptr_t bperm, long long bperm_len, uintptr_t bstate,
+                  uintptr_t bdone, float bmean, float binv_std) {
   ln_check(B, K);
   if (ws_floats < ew_lenet_ws_floats(B) || cnt_ints < ew_lenet_counters(B))
     throw std::runtime_error("ewdml lenet: workspace too small");
+  // bsrc: form the batch in the conv launch (LnBatch) into x and y
+  if (bsrc && (!blabels || !bperm || !bstate || !bdone || bperm_len < B || (bsrc & 3)))
+    throw std::runtime_error("ewdml lenet: bad batch source");
+  const LnBatch bt{reinterpret_cast<const uint8_t*>(bsrc),
+                   reinterpret_cast<const long long*>(blabels),
+                   reinterpret_cast<const long long*>(bperm), reinterpret_cast<long long*>(bstate),
+                   reinterpret_cast<int*>(bdone), bperm_len, bmean, binv_std,
+                   reinterpret_cast<long long*>(y)};
   ln_aligned(x, "x");
   ln_aligned(w1, "conv1 weight");
   ln_aligned(w2, "conv2 weight");
@@ -843,7 +895,7 @@ void ew_lenet_fwd(uintptr_t x, uintptr_t w1, uintptr_t b1, uintptr_t w2, uintptr
                      reinterpret_cast<const float*>(b1), reinterpret_cast<const float*>(w2),
                      reinterpret_cast<const float*>(b2), reinterpret_cast<float*>(a1),
                      reinterpret_cast<uint8_t*>(code1), reinterpret_cast<float*>(a2),
-                     reinterpret_cast<uint8_t*>(code2));
+                     reinterpret_cast<uint8_t*>(code2), bt);
   EW_CHECK_LAUNCH();
   const int nrt = (B + FT - 1) / FT;
   hipLaunchKernelGGL(k_ln_fc_fwd, dim3(F1T, nrt), dim3(LN_FT), 0, s,

@@ -62,7 +62,7 @@ def supported(model, x, y) -> bool:
 
 class _LeNetStep(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, y, w1, b1, w2, b2, wf1, bf1, wf2, bf2):
+    def forward(ctx, x, y, w1, b1, w2, b2, wf1, bf1, wf2, bf2, batch=None):
         C_ = require()
         B, K = x.shape[0], wf2.shape[0]
         dev = x.device
@@ -82,7 +82,7 @@ class _LeNetStep(torch.autograd.Function):
                      _ptr(wf2), _ptr(bf2), _ptr(y), B, K, _ptr(a1), _ptr(code1), _ptr(a2),
                      _ptr(code2), _ptr(h1), _ptr(logits), _ptr(dlogits), _ptr(dh1),
                      _ptr(lossrow), _ptr(loss), _ptr(ws), ws.numel(), _ptr(cnt), cnt.numel(),
-                     _stream())
+                     _stream(), *_batch_ptrs(batch))
         ctx.save_for_backward(x, w2, wf1, a1, code1, a2, code2, h1, dlogits, dh1)
         ctx.params = (w1, b1, w2, b2, wf1, bf1, wf2, bf2)
         ctx.mark_non_differentiable(logits)
@@ -103,12 +103,26 @@ class _LeNetStep(torch.autograd.Function):
                      _ptr(h1), _ptr(dlogits), _ptr(dh1), _ptr(g), B, K, _ptr(dp2),
                      *[_ptr(t) for t in grads], _ptr(ws), ws.numel(), _ptr(cnt), cnt.numel(),
                      _stream())
-        return (None, None, *grads)
+        return (None, None, *grads, None)
+
+
+def _batch_ptrs(batch):
+    """lenet_fwd's batch-source arguments (data/loader.py take_deferred), zeros for none."""
+    if batch is None:
+        return (0, 0, 0, 0, 0, 0, 0.0, 1.0)
+    src, labels, perm, state, done, mean, inv_std = batch
+    return (_ptr(src), _ptr(labels), _ptr(perm), perm.numel(), _ptr(state), _ptr(done),
+            float(mean), float(inv_std))
 
 
 def lenet_loss(model, x, y):
     """(mean cross-entropy, logits) of ``model`` (a ``models.LeNet``) through the fused kernels,
-    or None where they do not apply."""
+    or None where they do not apply.  ``x`` may be a fused loader's deferred batch buffer
+    (``_ew_batch``): the conv launch then forms the batch (and its labels in ``y``) itself."""
     if not supported(model, x, y):
         return None
-    return _LeNetStep.apply(x, y, *_params(model))
+    ldr = getattr(x, "_ew_batch", None)
+    batch = None
+    if ldr is not None and ldr.bx is x and ldr.by is y:
+        batch = ldr.take_deferred()
+    return _LeNetStep.apply(x, y, *_params(model), batch)

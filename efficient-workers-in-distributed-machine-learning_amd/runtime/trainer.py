@@ -324,6 +324,13 @@ class Trainer:
             return contextlib.nullcontext()
         return torch.cuda.nvtx.range(name)
 
+    def _defer_batch(self) -> bool:
+        """The fused loader's batch may be formed by the model's fused step (LeNet: its conv
+        launch, ops/lenet.py) instead of its own launch (EWDML_BATCH_IN_MODEL=0: never)."""
+        return (os.environ.get("EWDML_BATCH_IN_MODEL", "1") != "0"
+                and getattr(self.model, "fused_loss", None) is not None and self.cuda
+                and self.cfg.fused_nn == "on" and self.amp_dtype is None)
+
     def forward_backward(self, x, y):
         self.flat.zero_grad()
         self.exchange.begin()
@@ -339,6 +346,9 @@ class Trainer:
             if self.clock is not None:
                 self.clock.mark("forward")
         else:
+            ldr = getattr(x, "_ew_batch", None)
+            if ldr is not None:  # a deferred batch nobody formed: its kernel now
+                ldr.flush()
             with self._range("forward"), self.autocast():
                 out = self.model(x)
             if self.clock is not None:
@@ -511,7 +521,7 @@ class Trainer:
                                   capture_error_mode=mode):
                 try:
                     for _ in range(unroll):
-                        self._gx, self._gy = self.loader.emit()
+                        self._gx, self._gy = self.loader.emit(defer=self._defer_batch())
                         loss, out = self.forward_backward(self._gx, self._gy)
                         ex.finish()
                     loss, out = (t if k is None else k.copy_(t)
@@ -715,7 +725,7 @@ class Trainer:
                 with torch.cuda.graph(g, stream=self.gstream, capture_error_mode=mode):
                     try:
                         if self._in_graph_batch:
-                            self._gx, self._gy = self.loader.emit()
+                            self._gx, self._gy = self.loader.emit(defer=self._defer_batch())
                         loss, out = self.forward_backward(self._gx, self._gy)
                         ex.finish()
                     except BaseException:
@@ -744,7 +754,7 @@ class Trainer:
                 try:
                     seg.begin()
                     if self._in_graph_batch:
-                        self._gx, self._gy = self.loader.emit()
+                        self._gx, self._gy = self.loader.emit(defer=self._defer_batch())
                     loss, out = self.forward_backward(self._gx, self._gy)
                     ex.launch_pending()
                     if dev:  # the apply in the last segment, behind the comm graphs
@@ -774,7 +784,7 @@ class Trainer:
                 with torch.cuda.graph(ga, stream=self.gstream, capture_error_mode=mode):
                     try:
                         if self._in_graph_batch:
-                            self._gx, self._gy = self.loader.emit()
+                            self._gx, self._gy = self.loader.emit(defer=self._defer_batch())
                         loss, out = self.forward_backward(self._gx, self._gy)
                         ex.launch_pending()
                     except BaseException:
